@@ -1,0 +1,91 @@
+// Shared helpers for the hlhgat HIP library (gfx950 / CDNA4 only).
+//
+// Every exported entry point (include/hlhgat.h) validates its arguments on the
+// host, launches on the caller's stream and returns 0 on success or a nonzero
+// code with a thread-local message readable through hlhgat_last_error().
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdarg>
+#include <string>
+
+#include "../../include/hlhgat.h"
+
+namespace hlhgat {
+
+void set_error(const char* fmt, ...);
+
+#define HLH_CHECK_ARG(cond, ...)                     \
+  do {                                               \
+    if (!(cond)) {                                   \
+      ::hlhgat::set_error(__VA_ARGS__);              \
+      return HLHGAT_EINVAL;                          \
+    }                                                \
+  } while (0)
+
+#define HLH_CHECK_HIP(expr)                                              \
+  do {                                                                   \
+    hipError_t _e = (expr);                                              \
+    if (_e != hipSuccess) {                                              \
+      ::hlhgat::set_error("%s failed: %s (%s:%d)", #expr,                \
+                          hipGetErrorString(_e), __FILE__, __LINE__);    \
+      return HLHGAT_EHIP;                                                \
+    }                                                                    \
+  } while (0)
+
+#define HLH_CHECK_LAUNCH() HLH_CHECK_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool aligned16(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+inline bool aligned8(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 7u) == 0;
+}
+
+inline int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------
+// Live kernel timing (hlhgat_prof_*): when enabled, launches of the kernel
+// class being profiled are bracketed by hipEvents recorded on the SAME stream
+// the kernel runs on, and the algorithmic bytes of each launch are recorded.
+// ---------------------------------------------------------------------------
+struct ProfScope {
+  int slot = -1;
+  ProfScope(int kernel_class, hipStream_t s, double bytes, double flops);
+  ~ProfScope();
+  hipStream_t stream = nullptr;
+};
+
+}  // namespace hlhgat
+
+// Vector helpers ------------------------------------------------------------
+template <int V> struct VecT;
+template <> struct VecT<1> { using type = float; };
+template <> struct VecT<2> { using type = float2; };
+template <> struct VecT<4> { using type = float4; };
+
+__device__ __forceinline__ float vzero1() { return 0.f; }
+
+template <int V>
+__device__ __forceinline__ typename VecT<V>::type vload(const float* p) {
+  return *reinterpret_cast<const typename VecT<V>::type*>(p);
+}
+template <int V>
+__device__ __forceinline__ void vstore(float* p, typename VecT<V>::type v) {
+  *reinterpret_cast<typename VecT<V>::type*>(p) = v;
+}
+
+// Element access on the vector types so kernels can loop over components.
+__device__ __forceinline__ float& vget(float& v, int) { return v; }
+__device__ __forceinline__ float& vget(float2& v, int i) { return (&v.x)[i]; }
+__device__ __forceinline__ float& vget(float4& v, int i) { return (&v.x)[i]; }

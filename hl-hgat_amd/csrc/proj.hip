@@ -1,0 +1,641 @@
+// Dense per-simplex projections on the fp32 matrix cores of gfx950.
+//
+// HodgeLaguerreConv computes out = sum_k lins[k](T_k) + bias
+// (lib/Hodge_Cheb_Conv.py:487,497,509,512-513) and NodeEdgeInt computes
+// Linear(cat[a, b]) (lib/Hodge_Cheb_Conv.py:307-308).  Both are one GEMM whose
+// reduction axis is split over several operand blocks A_b (the basis terms
+// T_k, or the two halves of the concatenation), so neither the K separate
+// GEMMs + adds nor the torch.cat are materialised.
+//
+// MFMA: v_mfma_f32_16x16x4_f32 (exact f32 fma chain; 32-cycle issue).  Lane
+// l = 16*q + i supplies A[i][k=q] and B[k=q][i]; the four MFMAs of a 16-wide
+// k chunk use k = k0 + 4q + j (j = 0..3), which lets every lane fetch its four
+// k values of a row with ONE 16-byte load (A and W are both k-contiguous).
+// Accumulator register r of lane l holds C[4q + r][i].
+//
+// Shapes here are skinny (N = d_out <= 256, M = simplices up to millions), so
+// the kernels stream A straight into registers (each row read once, W served
+// from L1/L2), 4 waves per workgroup stacked along M.
+#include "common.h"
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+using namespace hlhgat;
+
+namespace {
+
+constexpr int MAXB = HLHGAT_MAX_BLOCKS;
+
+__device__ __forceinline__ floatx4 mfma16(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <bool VEC>
+__device__ __forceinline__ void load_k4(const float* __restrict__ p, int kk,
+                                        int kb, bool valid, float (&o)[4]) {
+  if (VEC) {
+    if (valid && kk < kb) {
+      float4 v = *reinterpret_cast<const float4*>(p + kk);
+      o[0] = v.x;
+      o[1] = v.y;
+      o[2] = v.z;
+      o[3] = v.w;
+    } else {
+      o[0] = o[1] = o[2] = o[3] = 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = (valid && kk + t < kb) ? p[kk + t] : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward: C = sum_b A_b W_b^T + bias
+// ---------------------------------------------------------------------------
+struct FwdArgs {
+  int nb;
+  int N;
+  int64_t M;
+  const float* A[MAXB];
+  const float* W[MAXB];
+  int64_t lda[MAXB];
+  int64_t ldw[MAXB];
+  int kb[MAXB];
+  const float* bias;
+  float* C;
+  int64_t ldc;
+  int accumulate;
+};
+
+template <int TM, int TN, bool VEC>
+__global__ __launch_bounds__(256) void k_proj_fwd(FwdArgs a) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  const int64_t m_base = ((int64_t)blockIdx.x * 4 + wave) * (TM * 16);
+  const int n_base = blockIdx.y * (TN * 16);
+  if (m_base >= a.M) return;
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int b = 0; b < a.nb; ++b) {
+    const int kb = a.kb[b];
+    const float* arow[TM];
+    bool aval[TM];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int64_t row = m_base + tm * 16 + i;
+      aval[tm] = row < a.M;
+      arow[tm] = a.A[b] + (aval[tm] ? row : 0) * a.lda[b];
+    }
+    const float* wrow[TN];
+    bool wval[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int col = n_base + tn * 16 + i;
+      wval[tn] = col < a.N;
+      wrow[tn] = a.W[b] + (int64_t)(wval[tn] ? col : 0) * a.ldw[b];
+    }
+    float af[TM][4], bf[TN][4];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) load_k4<VEC>(arow[tm], 4 * q, kb, aval[tm], af[tm]);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) load_k4<VEC>(wrow[tn], 4 * q, kb, wval[tn], bf[tn]);
+    for (int k0 = 0; k0 < kb; k0 += 16) {
+      // prefetch the next 16-wide chunk while this one feeds the MFMAs
+      float an[TM][4], bn[TN][4];
+      const int kn = k0 + 16 + 4 * q;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) load_k4<VEC>(arow[tm], kn, kb, aval[tm], an[tm]);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) load_k4<VEC>(wrow[tn], kn, kb, wval[tn], bn[tn]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[tm][tn] = mfma16(af[tm][j], bf[tn][j], acc[tm][tn]);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) af[tm][t] = an[tm][t];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bf[tn][t] = bn[tn][t];
+    }
+  }
+
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = n_base + tn * 16 + i;
+    if (col >= a.N) continue;
+    const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m_base + tm * 16 + 4 * q + r;
+        if (row >= a.M) continue;
+        float v = acc[tm][tn][r];
+        if (a.bias) v = v + bv;
+        float* dst = a.C + row * a.ldc + col;
+        *dst = a.accumulate ? *dst + v : v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// data gradient: dA_b = dC W_b   (reduction over N)
+// ---------------------------------------------------------------------------
+struct BwdDataArgs {
+  int nb;
+  int N;
+  int64_t M;
+  const float* G;
+  int64_t ldg;
+  const float* W[MAXB];
+  float* O[MAXB];
+  int64_t ldw[MAXB];
+  int64_t ldo[MAXB];
+  int kb[MAXB];
+  int tile_start[MAXB + 1];
+  int accumulate;
+};
+
+template <int TM, int TN, bool VEC>
+__global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  const int64_t m_base = ((int64_t)blockIdx.x * 4 + wave) * (TM * 16);
+  if (m_base >= a.M) return;
+  int b = 0;
+  while (b + 1 < a.nb && (int)blockIdx.y >= a.tile_start[b + 1]) ++b;
+  const int kb = a.kb[b];
+  const int c_base = ((int)blockIdx.y - a.tile_start[b]) * (TN * 16);
+  const float* __restrict__ W = a.W[b];
+  const int64_t ldw = a.ldw[b];
+
+  floatx4 acc[TM][TN];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const float* grow[TM];
+  bool gval[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int64_t row = m_base + tm * 16 + i;
+    gval[tm] = row < a.M;
+    grow[tm] = a.G + (gval[tm] ? row : 0) * a.ldg;
+  }
+  int cols[TN];
+  bool cval[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    cols[tn] = c_base + tn * 16 + i;
+    cval[tn] = cols[tn] < kb;
+  }
+  for (int r0 = 0; r0 < a.N; r0 += 16) {
+    const int kk = r0 + 4 * q;
+    float af[TM][4], bf[TN][4];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) load_k4<VEC>(grow[tm], kk, a.N, gval[tm], af[tm]);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[tn][j] = (cval[tn] && kk + j < a.N) ? W[(int64_t)(kk + j) * ldw + cols[tn]] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = mfma16(af[tm][j], bf[tn][j], acc[tm][tn]);
+  }
+  float* __restrict__ O = a.O[b];
+  const int64_t ldo = a.ldo[b];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    if (!cval[tn]) continue;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m_base + tm * 16 + 4 * q + r;
+        if (row >= a.M) continue;
+        float* dst = O + row * ldo + cols[tn];
+        const float v = acc[tm][tn][r];
+        *dst = a.accumulate ? *dst + v : v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient: dW_b = dC^T A_b  (reduction over M, split over workgroups)
+// Each workgroup owns one (64 n x 64 k) output tile of one block and one slice
+// of M; its 4 waves take interleaved 16-row chunks of the slice and are summed
+// through LDS in wave order; slices are summed in order by k_reduce_splits.
+// The bias gradient (column sums of dC) rides along in the k_base == 0 tiles
+// of block 0.
+// ---------------------------------------------------------------------------
+constexpr int WT_TM = 4;  // 64 rows of n per tile
+constexpr int WT_TN = 4;  // 64 cols of k per tile
+constexpr int WT_ROWS = WT_TM * 16;
+constexpr int WT_COLS = WT_TN * 16;
+
+struct BwdWeightArgs {
+  int nb;
+  int N;
+  int64_t M;
+  const float* G;
+  int64_t ldg;
+  const float* A[MAXB];
+  int64_t lda[MAXB];
+  int kb[MAXB];
+  int tile_start[MAXB + 1];
+  int64_t part_off[MAXB];
+  int64_t bias_off;  // -1: no bias gradient
+  int64_t part_stride;
+  float* part;
+  int64_t rows_per_split;
+  int tiles_n;
+};
+
+__global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
+  __shared__ float red[4][WT_TM * WT_TN * 4][64];
+  __shared__ float bred[4][WT_TM][64];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  int b = 0;
+  while (b + 1 < a.nb && (int)blockIdx.y >= a.tile_start[b + 1]) ++b;
+  const int t = (int)blockIdx.y - a.tile_start[b];
+  const int n_base = (t % a.tiles_n) * WT_ROWS;
+  const int k_base = (t / a.tiles_n) * WT_COLS;
+  const int kb = a.kb[b];
+  const float* __restrict__ A = a.A[b];
+  const int64_t lda = a.lda[b];
+  const bool do_bias = a.bias_off >= 0 && b == 0 && k_base == 0;
+
+  const int64_t m_lo = (int64_t)blockIdx.z * a.rows_per_split;
+  int64_t m_hi = m_lo + a.rows_per_split;
+  if (m_hi > a.M) m_hi = a.M;
+
+  floatx4 acc[WT_TM][WT_TN];
+#pragma unroll
+  for (int tm = 0; tm < WT_TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < WT_TN; ++tn) acc[tm][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bsum[WT_TM];
+#pragma unroll
+  for (int tm = 0; tm < WT_TM; ++tm) bsum[tm] = 0.f;
+
+  int ncol[WT_TM];
+  bool nval[WT_TM];
+#pragma unroll
+  for (int tm = 0; tm < WT_TM; ++tm) {
+    ncol[tm] = n_base + tm * 16 + i;
+    nval[tm] = ncol[tm] < a.N;
+  }
+  int kcol[WT_TN];
+  bool kval[WT_TN];
+#pragma unroll
+  for (int tn = 0; tn < WT_TN; ++tn) {
+    kcol[tn] = k_base + tn * 16 + i;
+    kval[tn] = kcol[tn] < kb;
+  }
+
+  for (int64_t m0 = m_lo + wave * 16; m0 < m_hi; m0 += 64) {
+    float af[WT_TM][4], bf[WT_TN][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = m0 + 4 * q + j;
+      const bool mv = m < m_hi;
+      const float* grow = a.G + (mv ? m : 0) * a.ldg;
+      const float* arow = A + (mv ? m : 0) * lda;
+#pragma unroll
+      for (int tm = 0; tm < WT_TM; ++tm) af[tm][j] = (mv && nval[tm]) ? grow[ncol[tm]] : 0.f;
+#pragma unroll
+      for (int tn = 0; tn < WT_TN; ++tn) bf[tn][j] = (mv && kval[tn]) ? arow[kcol[tn]] : 0.f;
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int tm = 0; tm < WT_TM; ++tm)
+        bsum[tm] = bsum[tm] + ((af[tm][0] + af[tm][1]) + (af[tm][2] + af[tm][3]));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int tm = 0; tm < WT_TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < WT_TN; ++tn)
+          acc[tm][tn] = mfma16(af[tm][j], bf[tn][j], acc[tm][tn]);
+  }
+
+  // cross-wave reduction (fixed order: wave 0 + 1 + 2 + 3)
+#pragma unroll
+  for (int tm = 0; tm < WT_TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < WT_TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][(tm * WT_TN + tn) * 4 + r][lane] = acc[tm][tn][r];
+  if (do_bias) {
+#pragma unroll
+    for (int tm = 0; tm < WT_TM; ++tm) bred[wave][tm][lane] = bsum[tm];
+  }
+  __syncthreads();
+  float* slab = a.part + (int64_t)blockIdx.z * a.part_stride;
+  // every thread finalises 16 of the 4096 tile entries
+  for (int idx = threadIdx.x; idx < WT_TM * WT_TN * 4 * 64; idx += 256) {
+    const int ln = idx & 63;
+    const int reg = idx >> 6;  // (tm*WT_TN + tn)*4 + r
+    const int r = reg & 3;
+    const int tn = (reg >> 2) % WT_TN;
+    const int tm = (reg >> 2) / WT_TN;
+    const float v = ((red[0][reg][ln] + red[1][reg][ln]) + red[2][reg][ln]) + red[3][reg][ln];
+    const int n = n_base + tm * 16 + 4 * (ln >> 4) + r;
+    const int k = k_base + tn * 16 + (ln & 15);
+    if (n < a.N && k < kb) slab[a.part_off[b] + (int64_t)n * kb + k] = v;
+  }
+  if (do_bias && threadIdx.x < WT_ROWS) {
+    const int tm = threadIdx.x >> 4;
+    const int ii = threadIdx.x & 15;
+    // lanes ii, ii+16, ii+32, ii+48 of each wave hold partial sums of column
+    // n_base + tm*16 + ii
+    float v = 0.f;
+    for (int w = 0; w < 4; ++w)
+      for (int qq = 0; qq < 4; ++qq) v = v + bred[w][tm][qq * 16 + ii];
+    const int n = n_base + tm * 16 + ii;
+    if (n < a.N) slab[a.bias_off + n] = v;
+  }
+}
+
+struct ReduceArgs {
+  int nb;
+  int N;
+  int splits;
+  const float* part;
+  int64_t part_stride;
+  int64_t part_off[MAXB];
+  int kb[MAXB];
+  float* dW[MAXB];
+  int64_t lddw[MAXB];
+  int64_t elem_start[MAXB + 1];
+  int64_t bias_off;
+  float* dbias;
+  int accumulate;
+};
+
+__global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = a.elem_start[a.nb] + (a.bias_off >= 0 ? a.N : 0);
+  if (e >= total) return;
+  int64_t src;
+  float* dst;
+  if (e >= a.elem_start[a.nb]) {
+    const int64_t n = e - a.elem_start[a.nb];
+    src = a.bias_off + n;
+    dst = a.dbias + n;
+  } else {
+    int b = 0;
+    while (b + 1 < a.nb && e >= a.elem_start[b + 1]) ++b;
+    const int64_t loc = e - a.elem_start[b];
+    const int64_t n = loc / a.kb[b];
+    const int64_t k = loc % a.kb[b];
+    src = a.part_off[b] + loc;
+    dst = a.dW[b] + n * a.lddw[b] + k;
+  }
+  float s = 0.f;
+  for (int sp = 0; sp < a.splits; ++sp) s = s + a.part[(int64_t)sp * a.part_stride + src];
+  *dst = a.accumulate ? *dst + s : s;
+}
+
+// --- planning ------------------------------------------------------------------
+struct WeightPlan {
+  int tiles_n;
+  int tiles_total;
+  int splits;
+  int64_t rows_per_split;
+  int64_t part_stride;
+  int64_t part_off[MAXB];
+  int64_t bias_off;
+  int tile_start[MAXB + 1];
+};
+
+WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
+                       bool with_bias) {
+  WeightPlan p{};
+  p.tiles_n = (int)ceil_div(N, WT_ROWS);
+  int64_t off = 0;
+  p.tile_start[0] = 0;
+  for (int b = 0; b < nb; ++b) {
+    p.part_off[b] = off;
+    off += N * kb[b];
+    p.tile_start[b + 1] = p.tile_start[b] + p.tiles_n * (int)ceil_div(kb[b], WT_COLS);
+  }
+  p.bias_off = with_bias ? off : -1;
+  if (with_bias) off += N;
+  p.part_stride = off;
+  p.tiles_total = p.tile_start[nb];
+  // aim for ~2048 workgroups, each slice >= 256 rows
+  int64_t splits = ceil_div(2048, p.tiles_total > 0 ? p.tiles_total : 1);
+  int64_t max_splits = ceil_div(M, 256);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int64_t rps = ceil_div(M, splits);
+  rps = ceil_div(rps, 64) * 64;
+  if (rps < 64) rps = 64;
+  p.rows_per_split = rps;
+  p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
+  return p;
+}
+
+bool vec_ok(const float* p, int64_t ld, int64_t kb) {
+  return aligned16(p) && (ld % 4) == 0 && (kb % 4) == 0;
+}
+
+}  // namespace
+
+using namespace hlhgat;
+
+extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
+                               const int64_t* lda, const float* const* W,
+                               const int64_t* ldw, const int64_t* kb, int64_t M,
+                               int64_t N, const float* bias, float* C,
+                               int64_t ldc, int accumulate, void* stream) {
+  HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_fwd: nblocks=%d", nblocks);
+  HLH_CHECK_ARG(M >= 0 && N > 0 && N < (1 << 30) && ldc >= N,
+                "proj_fwd: bad M/N/ldc");
+  HLH_CHECK_ARG(C, "proj_fwd: C is NULL");
+  FwdArgs a{};
+  a.nb = nblocks;
+  a.M = M;
+  a.N = (int)N;
+  a.bias = bias;
+  a.C = C;
+  a.ldc = ldc;
+  a.accumulate = accumulate;
+  bool vec = true;
+  double flops = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    HLH_CHECK_ARG(A[b] && W[b] && kb[b] > 0 && lda[b] >= kb[b] && ldw[b] >= kb[b],
+                  "proj_fwd: bad block %d", b);
+    a.A[b] = A[b];
+    a.W[b] = W[b];
+    a.lda[b] = lda[b];
+    a.ldw[b] = ldw[b];
+    a.kb[b] = (int)kb[b];
+    vec = vec && vec_ok(A[b], lda[b], kb[b]) && vec_ok(W[b], ldw[b], kb[b]);
+    flops += 2.0 * (double)M * (double)N * (double)kb[b];
+  }
+  if (M == 0) return HLHGAT_OK;
+  hipStream_t s = as_stream(stream);
+  const int tn = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
+  const int tm = M >= 262144 ? 2 : 1;
+  dim3 grid((unsigned)ceil_div(M, 4 * tm * 16), (unsigned)ceil_div(N, tn * 16));
+  double bytes = 4.0 * (double)M * N;
+  for (int b = 0; b < nblocks; ++b) bytes += 4.0 * (double)M * kb[b] + 4.0 * N * kb[b];
+  ProfScope prof(HLHGAT_PROF_PROJ, s, bytes, flops);
+#define HLH_FWD(TM_, TN_)                                                       \
+  if (vec)                                                                      \
+    k_proj_fwd<TM_, TN_, true><<<grid, 256, 0, s>>>(a);                         \
+  else                                                                          \
+    k_proj_fwd<TM_, TN_, false><<<grid, 256, 0, s>>>(a);
+  if (tm == 1 && tn == 1) { HLH_FWD(1, 1) }
+  else if (tm == 1 && tn == 2) { HLH_FWD(1, 2) }
+  else if (tm == 1) { HLH_FWD(1, 4) }
+  else if (tn == 1) { HLH_FWD(2, 1) }
+  else if (tn == 2) { HLH_FWD(2, 2) }
+  else { HLH_FWD(2, 4) }
+#undef HLH_FWD
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
+                                    const float* const* W, const int64_t* ldw,
+                                    const int64_t* kb, int64_t M, int64_t N,
+                                    float* const* dA, const int64_t* ldda,
+                                    int accumulate, void* stream) {
+  HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_bwd_data: nblocks=%d",
+                nblocks);
+  HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd_data: bad dC");
+  BwdDataArgs a{};
+  a.nb = nblocks;
+  a.M = M;
+  a.N = (int)N;
+  a.G = dC;
+  a.ldg = lddc;
+  a.accumulate = accumulate;
+  const int TN = 4;
+  a.tile_start[0] = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    HLH_CHECK_ARG(W[b] && dA[b] && kb[b] > 0 && ldw[b] >= kb[b] && ldda[b] >= kb[b],
+                  "proj_bwd_data: bad block %d", b);
+    a.W[b] = W[b];
+    a.O[b] = dA[b];
+    a.ldw[b] = ldw[b];
+    a.ldo[b] = ldda[b];
+    a.kb[b] = (int)kb[b];
+    a.tile_start[b + 1] = a.tile_start[b] + (int)ceil_div(kb[b], TN * 16);
+  }
+  if (M == 0) return HLHGAT_OK;
+  const bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
+  hipStream_t s = as_stream(stream);
+  dim3 grid((unsigned)ceil_div(M, 4 * 16), (unsigned)a.tile_start[nblocks]);
+  if (vec)
+    k_proj_bwd_data<1, TN, true><<<grid, 256, 0, s>>>(a);
+  else
+    k_proj_bwd_data<1, TN, false><<<grid, 256, 0, s>>>(a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int64_t hlhgat_proj_bwd_weight_workspace_floats(int nblocks,
+                                                           const int64_t* kb,
+                                                           int64_t M, int64_t N,
+                                                           int with_bias) {
+  if (nblocks < 1 || nblocks > MAXB || N <= 0 || M < 0) return 0;
+  WeightPlan p = plan_weight(nblocks, kb, M, N, with_bias != 0);
+  return (int64_t)p.splits * p.part_stride;
+}
+
+extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
+                                      const float* const* A, const int64_t* lda,
+                                      const int64_t* kb, int64_t M, int64_t N,
+                                      float* const* dW, const int64_t* lddw,
+                                      float* dbias, int accumulate,
+                                      float* workspace, int64_t workspace_floats,
+                                      void* stream) {
+  HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_bwd_weight: nblocks=%d",
+                nblocks);
+  HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd_weight: bad dC");
+  WeightPlan p = plan_weight(nblocks, kb, M, N, dbias != nullptr);
+  HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
+                "proj_bwd_weight: workspace too small");
+  BwdWeightArgs a{};
+  a.nb = nblocks;
+  a.M = M;
+  a.N = (int)N;
+  a.G = dC;
+  a.ldg = lddc;
+  ReduceArgs r{};
+  r.nb = nblocks;
+  r.N = (int)N;
+  r.elem_start[0] = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    HLH_CHECK_ARG(A[b] && dW[b] && kb[b] > 0 && lda[b] >= kb[b] && lddw[b] >= kb[b],
+                  "proj_bwd_weight: bad block %d", b);
+    a.A[b] = A[b];
+    a.lda[b] = lda[b];
+    a.kb[b] = (int)kb[b];
+    a.tile_start[b] = p.tile_start[b];
+    a.part_off[b] = p.part_off[b];
+    r.part_off[b] = p.part_off[b];
+    r.kb[b] = (int)kb[b];
+    r.dW[b] = dW[b];
+    r.lddw[b] = lddw[b];
+    r.elem_start[b + 1] = r.elem_start[b] + N * kb[b];
+  }
+  a.tile_start[nblocks] = p.tile_start[nblocks];
+  a.bias_off = p.bias_off;
+  a.part_stride = p.part_stride;
+  a.part = workspace;
+  a.rows_per_split = p.rows_per_split;
+  a.tiles_n = p.tiles_n;
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    // no rows: gradient contribution is zero
+    if (!accumulate) {
+      for (int b = 0; b < nblocks; ++b)
+        for (int64_t n = 0; n < N; ++n)
+          HLH_CHECK_HIP(hipMemsetAsync(dW[b] + n * lddw[b], 0, sizeof(float) * kb[b], s));
+      if (dbias) HLH_CHECK_HIP(hipMemsetAsync(dbias, 0, sizeof(float) * N, s));
+    }
+    return HLHGAT_OK;
+  }
+  dim3 grid(1, (unsigned)p.tiles_total, (unsigned)p.splits);
+  k_proj_bwd_weight<<<grid, 256, 0, s>>>(a);
+  HLH_CHECK_LAUNCH();
+  r.splits = p.splits;
+  r.part = workspace;
+  r.part_stride = p.part_stride;
+  r.bias_off = p.bias_off;
+  r.dbias = dbias;
+  r.accumulate = accumulate;
+  const int64_t total = r.elem_start[nblocks] + (dbias ? N : 0);
+  k_reduce_splits<<<(unsigned)ceil_div(total, 256), 256, 0, s>>>(r);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}

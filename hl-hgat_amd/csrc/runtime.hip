@@ -1,0 +1,117 @@
+// Library-level state: error messages, version, live kernel timing.
+#include "common.h"
+
+#include <mutex>
+#include <vector>
+
+namespace hlhgat {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+// --- live timing -----------------------------------------------------------
+// A fixed pool of hipEvent pairs per kernel class.  Records are appended in
+// launch order; hlhgat_prof_read() synchronises them and sums elapsed time.
+namespace {
+constexpr int kPoolSize = 1 << 14;
+struct ProfClass {
+  bool enabled = false;
+  std::vector<hipEvent_t> start, stop;
+  std::vector<double> bytes, flops;
+  int used = 0;
+  int64_t dropped = 0;
+};
+std::mutex g_prof_mu;
+ProfClass g_prof[HLHGAT_PROF_NCLASS];
+int g_active_class = -1;  // class of the currently open scope (no nesting)
+}  // namespace
+
+ProfScope::ProfScope(int kernel_class, hipStream_t s, double b, double f) {
+  if (kernel_class < 0 || kernel_class >= HLHGAT_PROF_NCLASS) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  ProfClass& pc = g_prof[kernel_class];
+  if (!pc.enabled) return;
+  if (pc.used >= (int)pc.start.size()) {
+    pc.dropped++;
+    return;
+  }
+  slot = pc.used++;
+  pc.bytes[slot] = b;
+  pc.flops[slot] = f;
+  stream = s;
+  g_active_class = kernel_class;
+  (void)hipEventRecord(pc.start[slot], s);
+}
+
+ProfScope::~ProfScope() {
+  if (slot < 0) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  (void)hipEventRecord(g_prof[g_active_class].stop[slot], stream);
+}
+
+}  // namespace hlhgat
+
+using namespace hlhgat;
+
+extern "C" int hlhgat_version(void) { return 100; }
+
+extern "C" const char* hlhgat_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int hlhgat_prof_enable(int kernel_class, int enable) {
+  HLH_CHECK_ARG(kernel_class >= 0 && kernel_class < HLHGAT_PROF_NCLASS,
+                "prof_enable: bad kernel class %d", kernel_class);
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  ProfClass& pc = g_prof[kernel_class];
+  if (enable && pc.start.empty()) {
+    pc.start.resize(kPoolSize);
+    pc.stop.resize(kPoolSize);
+    pc.bytes.resize(kPoolSize);
+    pc.flops.resize(kPoolSize);
+    for (int i = 0; i < kPoolSize; ++i) {
+      HLH_CHECK_HIP(hipEventCreate(&pc.start[i]));
+      HLH_CHECK_HIP(hipEventCreate(&pc.stop[i]));
+    }
+  }
+  pc.enabled = enable != 0;
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_prof_reset(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& pc : g_prof) {
+    pc.used = 0;
+    pc.dropped = 0;
+  }
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_prof_read(int kernel_class, int64_t* launches,
+                                double* total_ms, double* total_bytes,
+                                double* total_flops) {
+  HLH_CHECK_ARG(kernel_class >= 0 && kernel_class < HLHGAT_PROF_NCLASS,
+                "prof_read: bad kernel class %d", kernel_class);
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  ProfClass& pc = g_prof[kernel_class];
+  double ms = 0, b = 0, f = 0;
+  for (int i = 0; i < pc.used; ++i) {
+    HLH_CHECK_HIP(hipEventSynchronize(pc.stop[i]));
+    float t = 0.f;
+    HLH_CHECK_HIP(hipEventElapsedTime(&t, pc.start[i], pc.stop[i]));
+    ms += t;
+    b += pc.bytes[i];
+    f += pc.flops[i];
+  }
+  if (launches) *launches = pc.used;
+  if (total_ms) *total_ms = ms;
+  if (total_bytes) *total_bytes = b;
+  if (total_flops) *total_flops = f;
+  return HLHGAT_OK;
+}

@@ -1,0 +1,18 @@
+"""hlhgat — MI355X-native (gfx950) Hodge-Laplacian message passing for HL-HGAT.
+
+Drop-in for the hot path of deepika090/HL-HGAT (lib/Hodge_Cheb_Conv.py):
+HodgeLaguerreConv / HodgeChebConv / NodeEdgeInt / MSI / HL_filter / SAPool
+keep the reference's constructors, forward signatures and state_dict keys; the
+arithmetic runs in hand-written HIP kernels behind the C-ABI of
+include/hlhgat.h (libhlhgat.so).  There is no CPU fallback: importing this
+package loads the HIP library or raises.
+"""
+from . import ops  # noqa: F401  (loads libhlhgat.so; raises if missing)
+from .hodge_cheb_conv import (HL_filter, HodgeChebConv, HodgeLaguerreConv,  # noqa: F401
+                              HodgeLaguerreFastConv, MSI, NodeEdgeInt, SAPool)
+from .hodge_dataset import (Batch, BoundaryOperator, PairData, adj2par1, collate,  # noqa: F401
+                            degree)
+from .hodge_st_model import HL_HGCNN_zinc_dense_int3_pyr  # noqa: F401
+from .nn import BatchNorm, Linear, Sequential, global_mean_pool  # noqa: F401
+
+__version__ = "0.1.0"

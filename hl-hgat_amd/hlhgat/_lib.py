@@ -1,0 +1,99 @@
+"""ctypes binding of the C-ABI in include/hlhgat.h (libhlhgat.so).
+
+The product path has no fallback: if the HIP library is missing or fails to
+load, importing :mod:`hlhgat.ops` raises.  ``torch`` is imported first so the
+library binds to the HIP runtime torch already loaded (same SONAME
+libamdhip64.so.7), which makes torch's device pointers and streams valid
+arguments.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the library load, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HLHGAT_LIB", os.path.join(_HERE, "libhlhgat.so"))
+
+c_i32, c_i64, c_f32, c_f64, c_vp, c_sz = (C.c_int32, C.c_int64, C.c_float,
+                                           C.c_double, C.c_void_p, C.c_size_t)
+P_i64 = C.POINTER(c_i64)
+P_f64 = C.POINTER(c_f64)
+P_vp = C.POINTER(c_vp)
+
+# name -> (restype, argtypes); mirrors include/hlhgat.h exactly
+SIGNATURES = {
+    "hlhgat_version": (c_i32, []),
+    "hlhgat_last_error": (C.c_char_p, []),
+    "hlhgat_csr_workspace_bytes": (c_sz, [c_i64]),
+    "hlhgat_csr_from_coo": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp,
+                                    c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "hlhgat_csr_from_sorted_coo": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
+                                           c_vp, c_vp]),
+    "hlhgat_coo_check_sorted": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "hlhgat_incidence_csr": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "hlhgat_spmm": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp,
+                            c_i64, c_vp]),
+    "hlhgat_poly_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                 c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_f32,
+                                 c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
+    "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                      c_i64, c_i32, c_vp, c_vp]),
+    "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32,
+                                      c_vp, c_vp]),
+    "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
+                                c_vp, c_i64, c_i32, c_vp]),
+    "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
+                                     P_vp, P_i64, c_i32, c_vp]),
+    "hlhgat_proj_bwd_weight_workspace_floats": (c_i64, [c_i32, P_i64, c_i64, c_i64, c_i32]),
+    "hlhgat_proj_bwd_weight": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
+                                       P_vp, P_i64, c_vp, c_i32, c_vp, c_i64, c_vp]),
+    "hlhgat_edge_gather2": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_f32,
+                                    c_f32, c_vp, c_i64, c_i32, c_vp]),
+    "hlhgat_att_score_fwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                     c_f32, c_f32, c_f32, c_i32, c_vp, c_vp]),
+    "hlhgat_att_score_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                     c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_i64, c_vp]),
+    "hlhgat_segment_mean_fwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                        c_vp]),
+    "hlhgat_segment_mean_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                        c_vp]),
+    "hlhgat_prof_enable": (c_i32, [c_i32, c_i32]),
+    "hlhgat_prof_reset": (c_i32, []),
+    "hlhgat_prof_read": (c_i32, [c_i32, P_i64, P_f64, P_f64, P_f64]),
+}
+
+# constants from include/hlhgat.h
+POLY_LAGUERRE, POLY_CHEB = 0, 1
+SIGMA_SIGMOID, SIGMA_RELU = 0, 1
+PROF_POLY, PROF_PROJ = 0, 1
+MAX_BLOCKS = 16
+
+
+class HlhgatError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"hlhgat: HIP library not found at {path}. Build it with "
+            f"`python -c 'import __graft_entry__ as g; g.build()'` or "
+            f"`make -C hl-hgat_amd/csrc` (hipcc --offload-arch=gfx950).")
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if a declared symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = load()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = LIB.hlhgat_last_error().decode(errors="replace")
+        raise HlhgatError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,281 @@
+"""The HL-HGAT hot-path layers, MI355X-native, with the reference's interface.
+
+Same class names, constructor arguments, attributes, forward signatures and
+state_dict keys as lib/Hodge_Cheb_Conv.py of deepika090/HL-HGAT; the
+arithmetic runs in the HIP kernels of libhlhgat.so (see ops.py):
+
+  HodgeLaguerreConv  (:452-523)  fused basis + one MFMA projection, adjoint bwd
+  HodgeChebConv      (:366-448)  same kernels, Chebyshev recurrence
+  NodeEdgeInt / MSI  (:255-309 / :61-115)  incidence gathers, split-K Linear,
+                                           fused attention score
+  HL_filter          (:117-188)  block composition
+  SAPool             (:36-59)    attention-scaled cluster pooling
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch import Tensor
+from torch.nn import Dropout, Parameter
+
+from . import ops
+from .hodge_dataset import BoundaryOperator, adj2par1, boundary_from_sparse, degree
+from .nn import BatchNorm, Linear, Sequential
+
+__all__ = ["HodgeLaguerreConv", "HodgeChebConv", "NodeEdgeInt", "MSI", "HL_filter", "SAPool",
+           "HodgeLaguerreFastConv"]
+
+
+class _HodgePolyConv(nn.Module):
+    _kind = ops.POLY_LAGUERRE
+
+    def __init__(self, in_channels: int, out_channels: int, K: int, bias: bool = True,
+                 **kwargs):
+        super().__init__()
+        aggr = kwargs.pop("aggr", "add")
+        if aggr != "add":
+            raise ValueError("HodgeConv: only aggr='add' is supported (as in the reference)")
+        assert K > 0
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.lins = nn.ModuleList([
+            Linear(in_channels, out_channels, bias=False, weight_initializer="glorot")
+            for _ in range(K)
+        ])
+        if bias:
+            self.bias = Parameter(torch.empty(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        for lin in self.lins:
+            lin.reset_parameters()
+        if self.bias is not None:
+            with torch.no_grad():
+                self.bias.zero_()
+
+    def forward(self, x: Tensor, edge_index: Tensor, edge_weight: Optional[Tensor] = None,
+                batch: Optional[Tensor] = None) -> Tensor:
+        op = ops.hodge_operator(edge_index, edge_weight, x.size(0))
+        return ops.hodge_poly_conv(x, op, [lin.weight for lin in self.lins], self.bias,
+                                   self._kind)
+
+    def __repr__(self) -> str:
+        return (f"{self.__class__.__name__}({self.in_channels}, "
+                f"{self.out_channels}, K={len(self.lins)})")
+
+
+class HodgeLaguerreConv(_HodgePolyConv):
+    """Laguerre-polynomial Hodge filter (lib/Hodge_Cheb_Conv.py:452-523):
+    T_0 = x, T_1 = x - L x, T_{k+1} = (-L T_k + (2k+1) T_k - k T_{k-1})/(k+1),
+    out = sum_k lins[k](T_k) + bias."""
+    _kind = ops.POLY_LAGUERRE
+
+
+class HodgeChebConv(_HodgePolyConv):
+    """Chebyshev-polynomial Hodge filter (lib/Hodge_Cheb_Conv.py:366-448):
+    T_1 = L x, T_{k+1} = 2 L T_k - T_{k-1}."""
+    _kind = ops.POLY_CHEB
+
+
+class HodgeLaguerreFastConv(HodgeLaguerreConv):
+    """DEMO fork's torch_sparse variant (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:519-582),
+    forward(x, adj_t) with adj_t given as (edge_index, edge_weight).  The
+    DEMO's k>=2 term uses x instead of Tx_1 (:561); that bug is NOT reproduced
+    here — this is the corrected recurrence."""
+
+    def forward(self, x: Tensor, adj_t, *args, **kwargs) -> Tensor:  # type: ignore[override]
+        edge_index, edge_weight = adj_t
+        return super().forward(x, edge_index, edge_weight)
+
+
+def _sigma_code(sigma: nn.Module) -> int:
+    if isinstance(sigma, nn.Sigmoid):
+        return ops.SIGMA_SIGMOID
+    if isinstance(sigma, nn.ReLU):
+        return ops.SIGMA_RELU
+    raise NotImplementedError(f"NodeEdgeInt: sigma {type(sigma).__name__} has no HIP kernel "
+                              f"(supported: nn.Sigmoid, nn.ReLU)")
+
+
+def _as_boundary(par, n_nodes: int, n_edges: int) -> BoundaryOperator:
+    if isinstance(par, BoundaryOperator):
+        return par
+    if torch.is_tensor(par) and par.is_sparse:
+        return boundary_from_sparse(par)
+    raise TypeError("NodeEdgeInt: par must come from adj2par1")
+
+
+def _run_mlp(seq: nn.Sequential, blocks) -> Tensor:
+    """WV_* = Linear(2d,dl)->BN->ReLU->Linear(dl,dv)->BN->ReLU with the first
+    Linear consuming the concatenation as separate blocks."""
+    h = None
+    for i, m in enumerate(seq):
+        if isinstance(m, nn.Linear):
+            h = ops.linear_blocks(blocks if h is None else [h], m.weight, m.bias)
+        else:
+            h = m(h)
+    return h
+
+
+class NodeEdgeInt(nn.Module):
+    """Node<->edge interaction through the boundary operator
+    (lib/Hodge_Cheb_Conv.py:255-309)."""
+
+    def __init__(self, d=64, dk=32, dv=64, dl=64, only_att=False, sigma=nn.Sigmoid(), l=0.9):
+        super().__init__()
+        dl = dv
+        self.sigma = sigma
+        self.dk = dk
+        self.only_att = only_att
+        if only_att:
+            self.WQ_Node = nn.Linear(d, dk)
+            self.WK_Node = nn.Linear(d, dk)
+            self.WQ_Edge = nn.Linear(d, dk)
+            self.WK_Edge = nn.Linear(d, dk)
+        else:
+            self.WV_Node = nn.Sequential(
+                nn.Linear(d * 2, dl), nn.BatchNorm1d(dl), nn.ReLU(),
+                nn.Linear(dl, dv), nn.BatchNorm1d(dv), nn.ReLU())
+            self.WV_Edge = nn.Sequential(
+                nn.Linear(d * 2, dl), nn.BatchNorm1d(dl), nn.ReLU(),
+                nn.Linear(dl, dv), nn.BatchNorm1d(dv), nn.ReLU())
+        self.lambda_Node = l
+        self.lambda_Edge = l
+
+    def interact(self, x_t: Tensor, x_s: Tensor, par, D: Tensor):
+        """x_s2t = (1/D)·|B1| x_s and x_t2s = |B1|^T x_t / 2 (:294-295)."""
+        bop = _as_boundary(par, x_t.size(0), x_s.size(0))
+        inc = bop.incidence()
+        rD = (1 / D).view(-1)
+        x_s2t = ops.node_from_edges(x_s, inc, rD)
+        x_t2s = ops.edge_from_nodes(x_t, inc)
+        return x_s2t, x_t2s
+
+    def forward(self, x_t: Tensor, x_s: Tensor, par, D: Tensor):
+        x_s2t, x_t2s = self.interact(x_t, x_s, par, D)
+        if self.only_att:
+            code = _sigma_code(self.sigma)
+            dk = self.dk
+            sq = float(np.sqrt(dk))
+            # node side: K = WK_Node(x_t), Q_self = WQ_Node(x_t) in one GEMM
+            w_t = torch.cat([self.WK_Node.weight, self.WQ_Node.weight], 0)
+            b_t = torch.cat([self.WK_Node.bias, self.WQ_Node.bias], 0)
+            kq_t = ops.linear_blocks([x_t], w_t, b_t)
+            qc_t = ops.linear_blocks([x_s2t], self.WQ_Edge.weight, self.WQ_Edge.bias)
+            a_t = ops.att_score(qc_t, kq_t[:, dk:], kq_t[:, :dk], 1 - self.lambda_Node,
+                                self.lambda_Node, sq, code)
+            w_s = torch.cat([self.WK_Edge.weight, self.WQ_Edge.weight], 0)
+            b_s = torch.cat([self.WK_Edge.bias, self.WQ_Edge.bias], 0)
+            kq_s = ops.linear_blocks([x_s], w_s, b_s)
+            qc_s = ops.linear_blocks([x_t2s], self.WQ_Node.weight, self.WQ_Node.bias)
+            a_s = ops.att_score(qc_s, kq_s[:, dk:], kq_s[:, :dk], 1 - self.lambda_Edge,
+                                self.lambda_Edge, sq, code)
+            return a_t, a_s
+        x_t1 = _run_mlp(self.WV_Node, [x_s2t, x_t])
+        x_s1 = _run_mlp(self.WV_Edge, [x_t2s, x_s])
+        return x_t1, x_s1
+
+
+class MSI(NodeEdgeInt):
+    """Identical twin of NodeEdgeInt (lib/Hodge_Cheb_Conv.py:61-115)."""
+
+
+class HL_filter(nn.Module):
+    """Stack of HL-filtering blocks (lib/Hodge_Cheb_Conv.py:117-188)."""
+
+    def __init__(self, channels=2, filters=32, K=4, node_dim=64, edge_dim=64,
+                 dropout_ratio=0.0, leaky_slope=0.1, if_dense=True):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.node_dim = node_dim
+        self.edge_dim = edge_dim
+        self.if_dense = if_dense
+        gcn_outsize = self.filters
+        t_insize = self.node_dim
+        s_insize = self.edge_dim
+        for j in range(self.channels):
+            if self.if_dense:
+                setattr(self, "MSI{}".format(j), MSI(d=t_insize, dv=gcn_outsize))
+                cin_t = cin_s = gcn_outsize
+            else:
+                cin_t, cin_s = t_insize, s_insize
+            layers = [(HodgeLaguerreConv(cin_t, gcn_outsize, K=K),
+                       "x_t, edge_index_t, edge_weight_t -> x_t"),
+                      (BatchNorm(gcn_outsize), "x_t -> x_t"),
+                      (nn.LeakyReLU(negative_slope=leaky_slope), "x_t -> x_t"),
+                      (Dropout(p=dropout_ratio), "x_t -> x_t"),
+                      (HodgeLaguerreConv(cin_s, gcn_outsize, K=K),
+                       "x_s, edge_index_s, edge_weight_s -> x_s"),
+                      (BatchNorm(gcn_outsize), "x_s -> x_s"),
+                      (nn.LeakyReLU(negative_slope=leaky_slope), "x_s -> x_s"),
+                      (Dropout(p=dropout_ratio), "x_s -> x_s"),
+                      (lambda x1, x2: [x1, x2], "x_t, x_s -> x")]
+            setattr(self, "NEConv{}".format(j),
+                    Sequential("x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, "
+                               "edge_weight_s", layers))
+            if self.if_dense:
+                t_insize = t_insize + gcn_outsize
+                s_insize = s_insize + gcn_outsize
+            else:
+                t_insize = gcn_outsize
+                s_insize = gcn_outsize
+
+    def forward(self, x_t0, edge_index_t, edge_weight_t, x_s0, edge_index_s, edge_weight_s,
+                par_1=None, D=None):
+        for j in range(self.channels):
+            if self.if_dense:
+                x_t, x_s = getattr(self, "MSI{}".format(j))(x_t0, x_s0, par_1, D)
+                x_t, x_s = getattr(self, "NEConv{}".format(j))(
+                    x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, edge_weight_s)
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            else:
+                x_t0, x_s0 = getattr(self, "NEConv{}".format(j))(
+                    x_t0, edge_index_t, edge_weight_t, x_s0, edge_index_s, edge_weight_s)
+        return x_t0, x_s0
+
+
+def cluster_mean(x: Tensor, assign: Tensor) -> Tensor:
+    """torch_scatter.scatter_mean(x, assign, dim=0) on the HIP segment-mean
+    kernel; members are grouped per cluster (stable) by the CSR builder."""
+    n = x.size(0)
+    idx = assign.view(-1).to(torch.long)
+    n_seg = int(idx.max().item()) + 1 if n else 0
+    ar = torch.arange(n, device=x.device)
+    csr = ops._csr_general(idx, ar, None, n_seg, max(n, 1))
+    return ops.segment_mean(x, csr.rowptr, n_seg, csr.col)
+
+
+class SAPool(nn.Module):
+    """Attention-scaled structural pooling (lib/Hodge_Cheb_Conv.py:36-59)."""
+
+    def __init__(self, d=64, dk=32):
+        super().__init__()
+        self.NEAtt = MSI(d=d, dk=dk, only_att=True, sigma=nn.Sigmoid())
+
+    def forward(self, x_t0, x_s0, par_1, D, datas, pos_ts, pos_ss, k, device="cuda:0"):
+        att_t, att_s = self.NEAtt(x_t0, x_s0, par_1, D)
+        x_t0 = x_t0 * att_t
+        x_s0 = x_s0 * att_s
+        pos_t, pos_s = pos_ts[k], pos_ss[k]
+        x_t0 = cluster_mean(x_t0, pos_t)
+        keep = ~torch.isinf(pos_s).view(-1)
+        x_s0 = x_s0[keep]
+        pos_s = pos_s[keep]
+        x_s0 = cluster_mean(x_s0, pos_s)
+        edge_index_s = datas[k + 1].edge_index_s.to(device)
+        edge_weight_s = datas[k + 1].edge_weight_s.to(device)
+        edge_index_t = datas[k + 1].edge_index_t.to(device)
+        edge_weight_t = datas[k + 1].edge_weight_t.to(device)
+        k += 1
+        par_1 = adj2par1(datas[k].edge_index.to(device), x_t0.shape[0], x_s0.shape[0])
+        D = degree(datas[k].edge_index.view(-1).to(device), num_nodes=x_t0.shape[0]) + 1e-6
+        return (x_t0, x_s0, par_1, D, k, edge_index_t, edge_weight_t, edge_index_s,
+                edge_weight_s, att_t, att_s)

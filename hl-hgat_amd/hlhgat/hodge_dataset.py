@@ -1,0 +1,255 @@
+"""Simplex-graph layout (PairData), PyG-free batching and the boundary operator.
+
+Mirrors lib/Hodge_Dataset.py of the reference:
+  * PairData and its batching offsets (:27-48): x_t [N_t, F_t], x_s [N_s, F_s],
+    edge_index_t / edge_weight_t = COO of L0, edge_index_s / edge_weight_s = COO
+    of L1 (diagonal included, row-major sorted), edge_index = B1 columns (i<j),
+    num_node1 / num_edge1 / num_nodes, y.  On collation edge_index_s is
+    shifted by N_s, edge_index_t and edge_index by N_t.
+  * adj2par1 (:169-191) -> BoundaryOperator (|B1| as a lazily built incidence
+    CSR instead of an uncoalesced torch sparse COO).
+  * the Hodge builder of the ZINC process() (:447-470): L0 = 2 B1 B1^T / lmax,
+    L1 = 2 B1^T B1 / lmax, dense_to_sparse row-major COO.
+Host-side code (numpy / torch CPU), run once per graph outside the hot loop.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+__all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
+           "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric"]
+
+_INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index")
+_HODGE_KEYS = ("edge_index_s", "edge_index_t")
+
+
+class PairData:
+    """One simplex graph (lib/Hodge_Dataset.py:27-38)."""
+
+    def __init__(self, edge_index_s=None, x_s=None, edge_index_t=None, x_t=None,
+                 edge_weight_s=None, edge_weight_t=None, edge_index=None, y=None, **kw):
+        self.edge_index_s = edge_index_s
+        self.x_s = x_s
+        self.edge_index_t = edge_index_t
+        self.x_t = x_t
+        self.edge_weight_s = edge_weight_s
+        self.edge_weight_t = edge_weight_t
+        self.edge_index = edge_index
+        self.y = y
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+    def __inc__(self, key: str, value=None) -> int:
+        """Batching offset per key (lib/Hodge_Dataset.py:40-48)."""
+        if key == "edge_index_s":
+            return self.x_s.size(0)
+        if key in ("edge_index", "edge_index_t"):
+            return self.x_t.size(0)
+        return 0
+
+    def keys(self) -> List[str]:
+        return [k for k, v in self.__dict__.items() if v is not None and not k.startswith("_")]
+
+    def to(self, device):
+        for k in self.keys():
+            v = getattr(self, k)
+            if torch.is_tensor(v):
+                setattr(self, k, v.to(device))
+        return self
+
+    def __repr__(self) -> str:
+        parts = []
+        for k in self.keys():
+            v = getattr(self, k)
+            parts.append(f"{k}={list(v.shape)}" if torch.is_tensor(v) else f"{k}={v}")
+        return f"PairData({', '.join(parts)})"
+
+
+class Batch(PairData):
+    """A collated mini-batch of PairData graphs.
+
+    Per-graph scalars (num_node1, num_edge1) become int64 tensors [B] as PyG
+    collation does; ``hodge_sorted`` records which Laplacian COO blocks are
+    row-major sorted and symmetric so the device path can build CSR without a
+    sort (ops.mark_hodge)."""
+
+    num_graphs: int
+    hodge_sorted: Dict[str, bool]
+
+    def to(self, device, non_blocking: bool = False):
+        for k in self.keys():
+            v = getattr(self, k)
+            if torch.is_tensor(v):
+                setattr(self, k, v.to(device, non_blocking=non_blocking))
+        self._mark()
+        return self
+
+    def _mark(self) -> None:
+        if getattr(self, "hodge_sorted", None) is None:
+            return
+        for k, ok in self.hodge_sorted.items():
+            t = getattr(self, k, None)
+            if ok and torch.is_tensor(t) and t.is_cuda:
+                from .ops import mark_hodge
+                mark_hodge(t)
+
+    @property
+    def batch_t(self) -> torch.Tensor:
+        return torch.repeat_interleave(torch.arange(self.num_graphs, device=self.x_t.device),
+                                       self.num_node1.to(self.x_t.device))
+
+    @property
+    def batch_s(self) -> torch.Tensor:
+        return torch.repeat_interleave(torch.arange(self.num_graphs, device=self.x_s.device),
+                                       self.num_edge1.to(self.x_s.device))
+
+
+def is_sorted_symmetric(ei: np.ndarray, w: Optional[np.ndarray]) -> bool:
+    """True if COO (ei, w) is sorted by (row, col) and equals its transpose."""
+    if ei.shape[1] == 0:
+        return True
+    r, c = ei[0], ei[1]
+    if np.any((r[1:] < r[:-1]) | ((r[1:] == r[:-1]) & (c[1:] < c[:-1]))):
+        return False
+    order = np.lexsort((r, c))  # sort the transpose by (col, row)
+    if not (np.array_equal(c[order], r) and np.array_equal(r[order], c)):
+        return False
+    if w is not None and not np.array_equal(w[order], w):
+        return False
+    return True
+
+
+def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
+    """PyG-free equivalent of DataLoader collation for PairData
+    (offsets from PairData.__inc__, lib/Hodge_Dataset.py:40-48)."""
+    b = Batch()
+    B = len(graphs)
+    b.num_graphs = B
+    first = graphs[0]
+    keys = first.keys()
+    for k in keys:
+        vals = [getattr(g, k) for g in graphs]
+        v0 = vals[0]
+        if k in _INC_KEYS:
+            incs = np.array([g.__inc__(k) for g in graphs], dtype=np.int64)
+            off = np.concatenate([[0], np.cumsum(incs)[:-1]])
+            cat = np.concatenate([np.asarray(v) + o for v, o in zip(vals, off)], axis=1)
+            setattr(b, k, torch.from_numpy(np.ascontiguousarray(cat)))
+        elif torch.is_tensor(v0):
+            if v0.dim() == 0:
+                setattr(b, k, torch.stack(vals))
+            else:
+                setattr(b, k, torch.cat(vals, dim=0))
+        elif isinstance(v0, (int, np.integer, float)):
+            setattr(b, k, torch.tensor(vals))
+        else:
+            setattr(b, k, vals)
+    b.num_nodes = int(sum(g.x_t.size(0) for g in graphs))
+    hs = {}
+    for k, wk in (("edge_index_s", "edge_weight_s"), ("edge_index_t", "edge_weight_t")):
+        if getattr(b, k, None) is None:
+            continue
+        if check_hodge:
+            ok = all(is_sorted_symmetric(np.asarray(getattr(g, k)),
+                                         None if getattr(g, wk, None) is None
+                                         else np.asarray(getattr(g, wk)))
+                     for g in graphs)
+        else:
+            ok = all(getattr(g, "_hodge_sorted", False) for g in graphs)
+        hs[k] = ok
+    b.hodge_sorted = hs
+    return b
+
+
+class BoundaryOperator:
+    """|B1| / B1 of adj2par1 for the undirected edge list edge_index [2, E]
+    (column e: -1 at edge_index[0][e], +1 at edge_index[1][e]).
+
+    The product path consumes it as an incidence CSR (ops.incidence) built
+    once and shared by every NodeEdgeInt of a block group.  ``to_sparse_coo``
+    returns the reference's exact torch sparse tensor for interop."""
+
+    def __init__(self, edge_index: torch.Tensor, num_node: int, num_edge: int):
+        self.edge_index = edge_index
+        self.num_node = int(num_node)
+        self.num_edge = int(num_edge)
+        if edge_index.size(1) != self.num_edge:
+            raise ValueError(f"adj2par1: edge_index has {edge_index.size(1)} edges, "
+                             f"num_edge={num_edge}")
+        self._inc = None
+
+    @property
+    def shape(self):
+        return torch.Size([self.num_node, self.num_edge])
+
+    def incidence(self):
+        if self._inc is None:
+            from .ops import incidence
+            self._inc = incidence(self.edge_index, self.num_node)
+        return self._inc
+
+    def to_sparse_coo(self) -> torch.Tensor:
+        ei = self.edge_index
+        E = ei.shape[1]
+        col_idx = torch.cat([torch.arange(E), torch.arange(E)]).to(ei.device)
+        row_idx = torch.cat([ei[0], ei[1]])
+        val = torch.cat([ei[0].new_full(ei[0].shape, -1), ei[0].new_full(ei[0].shape, 1)]).float()
+        return torch.sparse_coo_tensor(torch.stack([row_idx, col_idx]), val,
+                                       (self.num_node, self.num_edge))
+
+    def to_dense(self) -> torch.Tensor:
+        return self.to_sparse_coo().to_dense()
+
+
+def adj2par1(edge_index: torch.Tensor, num_node: int, num_edge: int) -> BoundaryOperator:
+    """First boundary operator of the undirected adjacency
+    (lib/Hodge_Dataset.py:169-191)."""
+    return BoundaryOperator(edge_index, num_node, num_edge)
+
+
+def boundary_from_sparse(par: torch.Tensor) -> BoundaryOperator:
+    """Recover the edge list from a reference-built torch sparse B1."""
+    par = par.coalesce()
+    idx, val = par.indices(), par.values()
+    E = par.shape[1]
+    ei = torch.empty(2, E, dtype=torch.int64, device=idx.device)
+    neg = val < 0
+    ei[0, idx[1][neg]] = idx[0][neg]
+    ei[1, idx[1][~neg]] = idx[0][~neg]
+    return BoundaryOperator(ei, par.shape[0], E)
+
+
+def degree(index: torch.Tensor, num_nodes: Optional[int] = None,
+           dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """torch_geometric.utils.degree: occurrences of each index (float)."""
+    n = num_nodes if num_nodes is not None else (int(index.max()) + 1 if index.numel() else 0)
+    out = torch.zeros(n, dtype=dtype or torch.get_default_dtype(), device=index.device)
+    return out.scatter_add_(0, index, torch.ones_like(index, dtype=out.dtype))
+
+
+def dense_to_sparse(a: torch.Tensor):
+    """torch_geometric.utils.dense_to_sparse for one 2-D matrix: row-major
+    indices of the nonzero entries and their values."""
+    idx = a.nonzero().t().contiguous()
+    return idx, a[idx[0], idx[1]]
+
+
+def hodge_laplacians(edge_index: np.ndarray, n: int):
+    """(L0, L1, maxeig, B1) of an undirected simple graph (edges i<j), computed
+    exactly as the ZINC process() does in float32 torch
+    (lib/Hodge_Dataset.py:451-456)."""
+    ei = torch.as_tensor(np.asarray(edge_index), dtype=torch.int64)
+    E = ei.shape[1]
+    par1 = torch.zeros(n, E)
+    ar = torch.arange(E)
+    par1[ei[0], ar] = -1.0
+    par1[ei[1], ar] = 1.0
+    L0 = torch.matmul(par1, par1.T)
+    lam = torch.linalg.eigh(L0)[0]
+    maxeig = lam.max()
+    L0 = 2 * torch.matmul(par1, par1.T) / maxeig
+    L1 = 2 * torch.matmul(par1.T, par1) / maxeig
+    return L0, L1, maxeig, par1

@@ -1,0 +1,101 @@
+"""HL-HGAT task heads (callers of the hot path), reference names and keys.
+
+Mirrors lib/Hodge_ST_Model.py; the per-step host work of the reference
+(Python loops building batch vectors, :611-615) is replaced by device-side
+segment pointers built from num_node1 / num_edge1.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+from torch.nn import Dropout, Linear
+
+from . import ops
+from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt
+from .hodge_dataset import adj2par1, degree
+from .nn import BatchNorm, Sequential
+
+__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "segment_ptr", "mean_pool_sorted"]
+
+
+def segment_ptr(counts: torch.Tensor, device) -> torch.Tensor:
+    """int32 [B+1] offsets of graph-contiguous rows (PairData batching)."""
+    counts = counts.to(device)
+    ptr = torch.zeros(counts.numel() + 1, dtype=torch.int32, device=device)
+    ptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return ptr
+
+
+def mean_pool_sorted(x: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+    """global_mean_pool(x, batch) for a graph-contiguous batch vector
+    (lib/Hodge_ST_Model.py:636) on the HIP segment-mean kernel."""
+    return ops.segment_mean(x, segment_ptr(counts, x.device), counts.numel())
+
+
+def _hl_block(cin_t, cin_s, cout, K, dropout_ratio, act=nn.ReLU):
+    layers = [(HodgeLaguerreConv(cin_t, cout, K=K), "x_t, edge_index_t, edge_weight_t -> x_t"),
+              (BatchNorm(cout), "x_t -> x_t"),
+              (act(), "x_t -> x_t"),
+              (Dropout(p=dropout_ratio), "x_t -> x_t"),
+              (HodgeLaguerreConv(cin_s, cout, K=K), "x_s, edge_index_s, edge_weight_s -> x_s"),
+              (BatchNorm(cout), "x_s -> x_s"),
+              (act(), "x_s -> x_s"),
+              (Dropout(p=dropout_ratio), "x_s -> x_s"),
+              (lambda x1, x2: [x1, x2], "x_t, x_s -> x")]
+    return Sequential("x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, edge_weight_s", layers)
+
+
+class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
+    """ZINC regression head (lib/Hodge_ST_Model.py:544-646): HL_init_conv,
+    then per block NEInt{i}{j} (NodeEdgeInt on the dense concatenation) and
+    NEConv{i}{j} (Laguerre on L0 and L1), mean readout, MLP."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=21, edge_dim=3, num_classes=1, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, keig=7):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.mlp_channels = mlp_channels
+        self.node_dim = node_dim + keig
+        self.edge_dim = edge_dim + keig
+        self.initial_channel = self.filters[0]
+        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, K,
+                                      dropout_ratio)
+        gcn_insize = self.initial_channel
+        for i, gcn_outsize in enumerate(self.filters):
+            for j in range(self.channels[i]):
+                setattr(self, "NEInt{}{}".format(i, j), NodeEdgeInt(d=gcn_insize, dv=gcn_outsize))
+                setattr(self, "NEConv{}{}".format(i, j),
+                        _hl_block(gcn_outsize, gcn_outsize, gcn_outsize, K, dropout_ratio))
+                gcn_insize = gcn_outsize + gcn_insize
+        mlp_insize = self.filters[-1] * 2
+        for i, mlp_outsize in enumerate(mlp_channels):
+            setattr(self, "mlp%d" % i, nn.Sequential(
+                Linear(mlp_insize, mlp_outsize), nn.BatchNorm1d(mlp_outsize), nn.ReLU(),
+                nn.Dropout(dropout_ratio_mlp)))
+            mlp_insize = mlp_outsize
+        self.out = Linear(mlp_insize, num_classes)
+
+    def forward(self, data, device="cuda:0", if_final_layer=False):
+        x_s, edge_index_s, edge_weight_s = data.x_s, data.edge_index_s, data.edge_weight_s
+        x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
+        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                     edge_weight_s)
+        x_s0, x_t0 = x_s, x_t
+        for i, _ in enumerate(self.channels):
+            par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
+            D = degree(data.edge_index.view(-1))
+            for j in range(self.channels[i]):
+                x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
+                x_t, x_s = getattr(self, "NEConv{}{}".format(i, j))(
+                    x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, edge_weight_s)
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+        x = torch.cat((mean_pool_sorted(x_s, data.num_edge1),
+                       mean_pool_sorted(x_t, data.num_node1)), -1)
+        for i, _ in enumerate(self.mlp_channels):
+            x = getattr(self, "mlp%d" % i)(x)
+        if if_final_layer:
+            return x, self.out(x)
+        return self.out(x)

@@ -1,0 +1,156 @@
+"""PyG-free building blocks with the reference's module names and semantics.
+
+The reference composes its layers with torch_geometric ``Sequential``,
+``BatchNorm`` and ``Linear`` (e.g. lib/Hodge_ST_Model.py:556-567,
+lib/Hodge_Cheb_Conv.py:462-465); its checkpoints therefore carry keys such as
+``HL_init_conv.module_0.lins.0.weight`` and ``.module_1.module.running_mean``
+(verified against HL-HGAT-DEMO/weights/HL_HGAT_Brain.pt).  These classes
+reproduce those names so reference state_dicts load unchanged.
+"""
+from __future__ import annotations
+
+import math
+import re
+from typing import Callable, List, Sequence, Tuple, Union
+
+import torch
+import torch.nn as tnn
+
+__all__ = ["Sequential", "BatchNorm", "Linear", "glorot", "global_mean_pool"]
+
+
+def glorot(t: torch.Tensor) -> None:
+    """torch_geometric.nn.inits.glorot: U(-a, a), a = sqrt(6/(fan_in+fan_out))."""
+    if t is not None:
+        a = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+        with torch.no_grad():
+            t.uniform_(-a, a)
+
+
+class Linear(tnn.Module):
+    """torch_geometric.nn.dense.linear.Linear (weight [out, in]); the convs only
+    use ``.weight`` (bias=False, weight_initializer='glorot',
+    lib/Hodge_Cheb_Conv.py:462-465)."""
+
+    def __init__(self, in_channels: int, out_channels: int, bias: bool = True,
+                 weight_initializer: str = "glorot", bias_initializer=None):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.weight_initializer = weight_initializer
+        self.weight = tnn.Parameter(torch.empty(out_channels, in_channels))
+        if bias:
+            self.bias = tnn.Parameter(torch.empty(out_channels))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        if self.weight_initializer == "glorot":
+            glorot(self.weight)
+        else:
+            tnn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            with torch.no_grad():
+                self.bias.zero_()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from .ops import linear_blocks
+        shp = x.shape
+        y = linear_blocks([x.reshape(-1, shp[-1])], self.weight, self.bias)
+        return y.view(*shp[:-1], self.out_channels)
+
+    def __repr__(self) -> str:
+        return (f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, "
+                f"bias={self.bias is not None})")
+
+
+class BatchNorm(tnn.Module):
+    """torch_geometric.nn.BatchNorm: BatchNorm1d held as ``.module``."""
+
+    def __init__(self, in_channels: int, eps: float = 1e-5, momentum: float = 0.1,
+                 affine: bool = True, track_running_stats: bool = True):
+        super().__init__()
+        self.in_channels = in_channels
+        self.module = tnn.BatchNorm1d(in_channels, eps, momentum, affine, track_running_stats)
+
+    def reset_parameters(self) -> None:
+        self.module.reset_parameters()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.module(x)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.in_channels})"
+
+
+_ARROW = re.compile(r"\s*->\s*")
+
+
+def _names(s: str) -> List[str]:
+    return [t.strip() for t in s.split(",") if t.strip()]
+
+
+class Sequential(tnn.Module):
+    """torch_geometric.nn.Sequential(input_args, [(callable, 'a, b -> c'), ...]).
+
+    Entry i is registered as ``module_{i}`` (modules and plain callables
+    alike), arguments are routed by name, and the value of the last entry is
+    returned — e.g. the ``lambda x1, x2: [x1, x2]`` tail of every HL block
+    (lib/Hodge_ST_Model.py:566)."""
+
+    def __init__(self, input_args: str,
+                 modules: Sequence[Union[Tuple[Callable, str], Callable]]):
+        super().__init__()
+        self.input_args = _names(input_args)
+        self._routes: List[Tuple[List[str], List[str]]] = []
+        prev_out = list(self.input_args)
+        for i, entry in enumerate(modules):
+            if isinstance(entry, (tuple, list)):
+                fn, desc = entry
+                parts = _ARROW.split(desc)
+                ins = _names(parts[0])
+                outs = _names(parts[1]) if len(parts) > 1 else list(ins)
+            else:
+                fn, ins, outs = entry, list(prev_out), list(prev_out[:1])
+            if isinstance(fn, tnn.Module):
+                self.add_module(f"module_{i}", fn)
+            else:
+                object.__setattr__(self, f"module_{i}", fn)
+            self._routes.append((ins, outs))
+            prev_out = outs
+        self._n = len(modules)
+
+    def forward(self, *args):
+        if len(args) != len(self.input_args):
+            raise TypeError(f"Sequential expects {len(self.input_args)} inputs "
+                            f"({', '.join(self.input_args)}), got {len(args)}")
+        env = dict(zip(self.input_args, args))
+        out = None
+        for i, (ins, outs) in enumerate(self._routes):
+            fn = getattr(self, f"module_{i}")
+            out = fn(*[env[n] for n in ins])
+            if len(outs) == 1:
+                env[outs[0]] = out
+            else:
+                for n, v in zip(outs, out):
+                    env[n] = v
+        return out
+
+    def __len__(self) -> int:
+        return self._n
+
+    def __getitem__(self, i: int):
+        return getattr(self, f"module_{i}")
+
+
+def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int = None) -> torch.Tensor:
+    """torch_geometric.nn.global_mean_pool over a sorted batch vector
+    (PairData batches are graph-contiguous), on the HIP segment-mean kernel."""
+    from .ops import segment_mean
+    if size is None:
+        size = int(batch.max().item()) + 1 if batch.numel() else 0
+    counts = torch.bincount(batch, minlength=size)
+    ptr = torch.zeros(size + 1, dtype=torch.int32, device=x.device)
+    ptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return segment_mean(x, ptr, size)

@@ -1,0 +1,114 @@
+"""Synthetic simplex graphs of the BASELINE.json shapes (no datasets offline).
+
+ZINC-like molecules: n ~ clip(round(N(23.2, 4.5)), 9, 38) atoms,
+a random tree with max degree 4 plus ring closures (E ≈ n + 1.7 on average),
+atom / bond one-hots (21 / 3 classes) concatenated with keig Laplacian
+eigenvector PEs, Hodge Laplacians exactly as the reference ZINC process()
+builds them (lib/Hodge_Dataset.py:447-477) and the get()-time PE padding /
+sign flips (:425-440).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import numpy as np
+import torch
+
+from .hodge_dataset import PairData, collate, dense_to_sparse, hodge_laplacians
+
+__all__ = ["zinc_like_graph", "zinc_like_batch", "molecule_edges"]
+
+
+def molecule_edges(rng: np.random.Generator, n: int, extra_mean: float = 2.7) -> np.ndarray:
+    """Undirected edge list (i<j, sorted) of a random tree with max degree 4
+    plus ring closures between atoms 4-5 bonds apart."""
+    deg = np.zeros(n, dtype=np.int64)
+    edges = set()
+    adj = [[] for _ in range(n)]
+    for v in range(1, n):
+        cand = [u for u in range(v) if deg[u] < 4]
+        u = int(rng.choice(cand))
+        edges.add((u, v))
+        adj[u].append(v)
+        adj[v].append(u)
+        deg[u] += 1
+        deg[v] += 1
+    n_extra = int(rng.poisson(extra_mean))
+    tries = 0
+    while n_extra > 0 and tries < 50:
+        tries += 1
+        a = int(rng.integers(n))
+        if deg[a] >= 4:
+            continue
+        # BFS distances from a
+        dist = -np.ones(n, dtype=np.int64)
+        dist[a] = 0
+        frontier = [a]
+        while frontier:
+            nxt = []
+            for x in frontier:
+                for y in adj[x]:
+                    if dist[y] < 0:
+                        dist[y] = dist[x] + 1
+                        nxt.append(y)
+            frontier = nxt
+        cand = [b for b in range(n) if dist[b] in (4, 5) and deg[b] < 4]
+        if not cand:
+            continue
+        b = int(rng.choice(cand))
+        e = (min(a, b), max(a, b))
+        if e in edges:
+            continue
+        edges.add(e)
+        adj[a].append(b)
+        adj[b].append(a)
+        deg[a] += 1
+        deg[b] += 1
+        n_extra -= 1
+    return np.array(sorted(edges), dtype=np.int64).T.reshape(2, -1)
+
+
+def _eig_pe(L: torch.Tensor, k: int) -> torch.Tensor:
+    """eig_pe (lib/Hodge_Dataset.py:97-112): eigenvectors 1..k-1 by ascending
+    eigenvalue."""
+    vals, vecs = np.linalg.eigh(L.numpy().astype(np.float64))
+    vecs = vecs[:, vals.argsort()]
+    return torch.from_numpy(vecs[:, 1:k].astype(np.float32))
+
+
+def _pad_sign(x: torch.Tensor, width: int, n_fixed: int, rng: np.random.Generator):
+    if x.shape[1] < width:
+        return torch.cat([x, torch.zeros(x.shape[0], width - x.shape[1])], dim=-1)
+    sign = torch.cat([torch.ones(n_fixed),
+                      torch.from_numpy(rng.integers(0, 2, width - n_fixed) * 2.0 - 1.0).float()])
+    return x[:, :width] * sign
+
+
+def zinc_like_graph(seed: int, keig: int = 15) -> PairData:
+    rng = np.random.default_rng(seed)
+    n = int(np.clip(round(rng.normal(23.2, 4.5)), 9, 38))
+    ei = molecule_edges(rng, n)
+    E = ei.shape[1]
+    L0, L1, maxeig, _ = hodge_laplacians(ei, n)
+    atom = torch.from_numpy(rng.integers(0, 21, n))
+    bond = torch.from_numpy(rng.integers(0, 3, E))
+    x_t = torch.cat([torch.nn.functional.one_hot(atom, 21).float(), _eig_pe(L0, keig + 1)], -1)
+    x_s = torch.cat([torch.nn.functional.one_hot(bond, 3).float(), _eig_pe(L1, keig + 1)], -1)
+    x_t = _pad_sign(x_t, 21 + keig, 21, rng)
+    x_s = _pad_sign(x_s, 3 + keig, 3, rng)
+    eit, ewt = dense_to_sparse(L0)
+    eis, ews = dense_to_sparse(L1)
+    g = PairData(x_s=x_s, edge_index_s=eis, edge_weight_s=ews, x_t=x_t, edge_index_t=eit,
+                 edge_weight_t=ewt, y=torch.tensor([float(rng.normal())]))
+    g.edge_index = torch.from_numpy(ei)
+    g.num_node1 = n
+    g.num_edge1 = E
+    g.num_nodes = n
+    g._hodge_sorted = True  # dense_to_sparse of symmetric L: row-major, symmetric
+    return g
+
+
+def zinc_like_batch(n_graphs: int, seed: int = 0, keig: int = 15,
+                    check_hodge: bool = False):
+    graphs: List[PairData] = [zinc_like_graph(seed * 1_000_003 + i, keig) for i in range(n_graphs)]
+    return collate(graphs, check_hodge=check_hodge)

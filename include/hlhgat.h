@@ -1,0 +1,236 @@
+/*
+ * hlhgat.h — C-ABI of the MI355X-native (gfx950) Hodge-Laplacian
+ * message-passing hot path of HL-HGAT.
+ *
+ * Every entry point takes plain device pointers, sizes and a HIP stream
+ * (passed as void*), launches asynchronously on that stream and returns
+ * HLHGAT_OK (0) or an error code; hlhgat_last_error() returns a
+ * thread-local message for the last failure.  No entry point allocates
+ * device memory or synchronises the stream (graph-capture safe); scratch
+ * space is supplied by the caller (see the *_workspace_bytes queries).
+ *
+ * Layout conventions (DESIGN.md "Data layout in HBM"):
+ *  - features are fp32, row-major [rows][ld] with ld >= width;
+ *  - a sparse operator A (L0, L1, |B1|) is CSR with int32 rowptr[n+1],
+ *    int32 col[nnz], fp32 val[nnz] (val == NULL means all ones);
+ *  - a polynomial basis slab is k-major: block k is [n][F] contiguous.
+ *
+ * Reference interfaces replaced (paths relative to deepika090/HL-HGAT):
+ *  - PyG MessagePassing.propagate + message(x_j, norm) = norm*x_j, aggr='add'
+ *      lib/Hodge_Cheb_Conv.py:412,416,424,430,494,502,442-443,518-519
+ *      -> hlhgat_csr_*, hlhgat_spmm, hlhgat_poly_step
+ *  - HodgeLaguerreConv.forward recurrence   lib/Hodge_Cheb_Conv.py:480-515
+ *  - HodgeChebConv.forward recurrence       lib/Hodge_Cheb_Conv.py:394-439
+ *      -> hlhgat_poly_basis_fwd / hlhgat_poly_basis_bwd
+ *  - torch_geometric Linear / nn.Linear projections (lins[k], WV_*, WQ/WK)
+ *      lib/Hodge_Cheb_Conv.py:462-465,497,509,270-289,276-289
+ *      -> hlhgat_proj_fwd / hlhgat_proj_bwd_data / hlhgat_proj_bwd_weight
+ *  - adj2par1 + torch.sparse.mm(|B1|, .) and (|B1|^T, .)
+ *      lib/Hodge_Dataset.py:169-191, lib/Hodge_Cheb_Conv.py:294-295,100-101
+ *      -> hlhgat_incidence_csr, hlhgat_edge_gather2 (+ hlhgat_poly_step as
+ *         the node-side segment mean)
+ *  - NodeEdgeInt/MSI only_att score     lib/Hodge_Cheb_Conv.py:297-305,103-111
+ *      -> hlhgat_att_score_fwd / hlhgat_att_score_bwd
+ *  - torch_scatter.scatter_mean / global_mean_pool (cluster pooling, readout)
+ *      lib/Hodge_Cheb_Conv.py:50-53, lib/Hodge_ST_Model.py:636
+ *      -> hlhgat_segment_mean_fwd / hlhgat_segment_mean_bwd
+ */
+#ifndef HLHGAT_H_
+#define HLHGAT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HLHGAT_OK 0
+#define HLHGAT_EINVAL 1 /* bad argument (shape, alignment, null pointer) */
+#define HLHGAT_EHIP 2   /* HIP runtime error */
+
+#define HLHGAT_POLY_LAGUERRE 0 /* HodgeLaguerreConv recurrence */
+#define HLHGAT_POLY_CHEB 1     /* HodgeChebConv recurrence */
+
+#define HLHGAT_SIGMA_SIGMOID 0 /* nn.Sigmoid (NodeEdgeInt default) */
+#define HLHGAT_SIGMA_RELU 1    /* nn.ReLU (attpool heads) */
+
+/* ---- library ---------------------------------------------------------- */
+int hlhgat_version(void);
+const char* hlhgat_last_error(void);
+
+/* ---- CSR construction ------------------------------------------------- */
+/* Scratch bytes needed by hlhgat_csr_from_coo for nnz entries. */
+size_t hlhgat_csr_workspace_bytes(int64_t nnz);
+
+/* COO (row[e], col[e], w[e]) -> CSR keyed by row.  Entries are ordered by
+ * (row, col) exactly as torch.sparse coalesce orders them, duplicates kept
+ * (propagate sums duplicates, so does the SpMM).  w may be NULL (val NULL).
+ * Rows/cols are int64 (PyG edge_index); both must lie in [0,n_rows) and
+ * [0,n_cols).  `perm` (optional, int32[nnz]) receives the source entry of
+ * each CSR slot.  Replaces the gather/scatter set-up of PyG propagate
+ * (lib/Hodge_Cheb_Conv.py:494,502) and the coalesce inside torch.sparse.mm
+ * (lib/Hodge_Cheb_Conv.py:294-295). */
+int hlhgat_csr_from_coo(const int64_t* row, const int64_t* col, const float* w,
+                        int64_t nnz, int64_t n_rows, int64_t n_cols,
+                        int32_t* rowptr, int32_t* col_out, float* val_out,
+                        int32_t* perm, void* workspace, size_t workspace_bytes,
+                        void* stream);
+
+/* Fast path for COO already sorted by (row, col) — e.g. dense_to_sparse output
+ * of the Hodge builder (lib/Hodge_Dataset.py:467-468) shifted by PairData
+ * batching (lib/Hodge_Dataset.py:40-48).  Caller guarantees sortedness;
+ * hlhgat_coo_check_sorted can verify it on device. */
+int hlhgat_csr_from_sorted_coo(const int64_t* row, const int64_t* col,
+                               const float* w, int64_t nnz, int64_t n_rows,
+                               int32_t* rowptr, int32_t* col_out,
+                               float* val_out, void* stream);
+
+/* Writes 1 to *flag_dev if (row,col) is non-decreasing lexicographically and
+ * every index is in range, else 0. */
+int hlhgat_coo_check_sorted(const int64_t* row, const int64_t* col, int64_t nnz,
+                            int64_t n_rows, int64_t n_cols, int32_t* flag_dev,
+                            void* stream);
+
+/* Incidence CSR of |B1| (adj2par1, lib/Hodge_Dataset.py:169-191): for each
+ * node v, the edges e with edge_index[0][e]==v or edge_index[1][e]==v, in
+ * increasing e.  edge_index is int64 [2][n_edges] (row 0 = i, row 1 = j).
+ * Needs hlhgat_csr_workspace_bytes(2*n_edges) of scratch. */
+int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
+                         int64_t n_nodes, int32_t* rowptr, int32_t* edge_ids,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- SpMM and fused polynomial step ----------------------------------- */
+/* Y = A·X (PyG propagate with aggr='add', source_to_target, when A is the
+ * CSR keyed by edge_index[1]).  X,Y [n][d] with row strides ldx, ldy. */
+int hlhgat_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
+                int64_t n_rows, int64_t nnz, const float* X, int64_t ldx,
+                int64_t d, float* Y, int64_t ldy, void* stream);
+
+/* Generic fused step (one launch):
+ *   Y = (alpha * rs[r] * (A·X)[r] + beta*X[r] + gamma*Z[r]) / div
+ *       + p*P[r] + q*Q[r]
+ * Z, P, Q, rs (row scale) may be NULL (term dropped).  Y may alias P (each
+ * row is read then written by the same lanes).  A is n_rows x n_rows when
+ * beta != 0; otherwise X may have any row count >= max(col)+1. */
+int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
+                     const float* val, const float* rs, int64_t n_rows,
+                     int64_t nnz, const float* X, int64_t ldx, int64_t d,
+                     const float* Z, int64_t ldz, const float* P, int64_t ldp,
+                     const float* Q, int64_t ldq, float alpha, float beta,
+                     float gamma, float div, float p, float q, float* Y,
+                     int64_t ldy, void* stream);
+
+/* Polynomial basis T_1..T_{K-1} of X over A (K >= 1; K==1 is a no-op).
+ * kind = HLHGAT_POLY_LAGUERRE: T_1 = X - A X,
+ *        T_{k+1} = (-A T_k + (2k+1) T_k - k T_{k-1}) / (k+1)
+ *        (lib/Hodge_Cheb_Conv.py:494,507)
+ * kind = HLHGAT_POLY_CHEB:     T_1 = A X, T_{k+1} = 2 A T_k - T_{k-1}
+ *        (lib/Hodge_Cheb_Conv.py:416,430-432)
+ * X: [n][F] row stride ldx.  T: (K-1) contiguous blocks of [n][F]. */
+int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
+                          const float* val, int64_t n, int64_t nnz,
+                          const float* X, int64_t ldx, int64_t F, int K,
+                          float* T, void* stream);
+
+/* Adjoint of hlhgat_poly_basis_fwd.  On entry G holds K contiguous blocks
+ * [n][F]: G_k = dLoss/dT_k from the consumers of each T_k (block 0 = the
+ * direct gradient of X).  On exit block 0 holds dLoss/dX.  Blocks 1..K-1 are
+ * used as scratch.  The CSR passed must be A^T (== A for the symmetric Hodge
+ * Laplacians). */
+int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
+                          const int32_t* col_t, const float* val_t, int64_t n,
+                          int64_t nnz, int64_t F, int K, float* G,
+                          void* stream);
+
+/* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
+#define HLHGAT_MAX_BLOCKS 16
+
+/* Forward:  C[m][n] = beta_acc*C[m][n] + sum_b sum_k A_b[m][k]*W_b[n][k]
+ *                     + bias[n]
+ * A_b: [M][kb[b]] row stride lda[b]; W_b: [N][kb[b]] row stride ldw[b]
+ * (nn.Linear weight layout).  accumulate != 0 adds into C.  bias may be NULL.
+ * Replaces out = sum_k lins[k](T_k) + bias (lib/Hodge_Cheb_Conv.py:487,497,
+ * 509,512-513) and Linear(cat[a,b]) (lib/Hodge_Cheb_Conv.py:307-308). */
+int hlhgat_proj_fwd(int nblocks, const float* const* A, const int64_t* lda,
+                    const float* const* W, const int64_t* ldw,
+                    const int64_t* kb, int64_t M, int64_t N, const float* bias,
+                    float* C, int64_t ldc, int accumulate, void* stream);
+
+/* Data gradient:  dA_b[m][k] (+)= sum_n dC[m][n] * W_b[n][k]. */
+int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
+                         const float* const* W, const int64_t* ldw,
+                         const int64_t* kb, int64_t M, int64_t N,
+                         float* const* dA, const int64_t* ldda,
+                         int accumulate, void* stream);
+
+/* Scratch floats needed by hlhgat_proj_bwd_weight. */
+int64_t hlhgat_proj_bwd_weight_workspace_floats(int nblocks, const int64_t* kb,
+                                                int64_t M, int64_t N,
+                                                int with_bias);
+
+/* Weight / bias gradient (deterministic split-M reduction, no atomics):
+ *   dW_b[n][k] (+)= sum_m dC[m][n] * A_b[m][k];   dbias[n] (+)= sum_m dC[m][n]
+ * dbias may be NULL. */
+int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
+                           const float* const* A, const int64_t* lda,
+                           const int64_t* kb, int64_t M, int64_t N,
+                           float* const* dW, const int64_t* lddw, float* dbias,
+                           int accumulate, float* workspace,
+                           int64_t workspace_floats, void* stream);
+
+/* ---- boundary-operator interaction ------------------------------------ */
+/* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] with (i,j) = edge_index[:,e]
+ * (sa/sb per-node scale vectors, may be NULL).  With ca=cb=0.5 and no
+ * scales this is x_t2s = (|B1|^T x_t)/2 (lib/Hodge_Cheb_Conv.py:295). */
+int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
+                        const float* x, int64_t ldx, int64_t d, const float* sa,
+                        const float* sb, float ca, float cb, float* out,
+                        int64_t ldo, int accumulate, void* stream);
+
+/* ---- attention score (NodeEdgeInt only_att) ---------------------------- */
+/* a[r] = sigma((w_cross*<Qc[r],Kr[r]> + w_self*<Qs[r],Kr[r]>) / sqrt_dk)
+ * with w_cross = (1-lambda), w_self = lambda (lib/Hodge_Cheb_Conv.py:299-304).
+ * Qc, Qs, Kr: [n][dk] with row strides. */
+int hlhgat_att_score_fwd(int64_t n, int64_t dk, const float* Qc, int64_t ldqc,
+                         const float* Qs, int64_t ldqs, const float* Kr,
+                         int64_t ldk, float w_cross, float w_self,
+                         float sqrt_dk, int sigma, float* a, void* stream);
+
+/* Backward of hlhgat_att_score_fwd given a (the forward output) and da. */
+int hlhgat_att_score_bwd(int64_t n, int64_t dk, const float* Qc, int64_t ldqc,
+                         const float* Qs, int64_t ldqs, const float* Kr,
+                         int64_t ldk, float w_cross, float w_self,
+                         float sqrt_dk, int sigma, const float* a,
+                         const float* da, float* dQc, float* dQs, float* dK,
+                         int64_t ldg, void* stream);
+
+/* ---- segment mean (scatter_mean / global_mean_pool) -------------------- */
+/* out[s] = mean over rows r of CSR segment s of x[r] (rows listed in
+ * seg_rows, or contiguous when seg_rows == NULL); empty segments give 0. */
+int hlhgat_segment_mean_fwd(const int32_t* seg_ptr, const int32_t* seg_rows,
+                            int64_t n_seg, const float* x, int64_t ldx,
+                            int64_t d, float* out, int64_t ldo, void* stream);
+/* dx[r] = dout[seg(r)] / |seg| for every row r listed in a segment; rows in
+ * no segment are left untouched (caller zero-fills). */
+int hlhgat_segment_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
+                            int64_t n_seg, const float* dout, int64_t ldo,
+                            int64_t d, float* dx, int64_t ldx, void* stream);
+
+/* ---- live kernel timing ------------------------------------------------ */
+#define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */
+#define HLHGAT_PROF_PROJ 1 /* MFMA projection forward */
+#define HLHGAT_PROF_NCLASS 2
+/* Enable (1) / disable (0) event timing of the given kernel class. */
+int hlhgat_prof_enable(int kernel_class, int enable);
+int hlhgat_prof_reset(void);
+/* Synchronises the recorded events and returns launch count, summed kernel
+ * milliseconds, summed algorithmic bytes and flops for the class. */
+int hlhgat_prof_read(int kernel_class, int64_t* launches, double* total_ms,
+                     double* total_bytes, double* total_flops);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HLHGAT_H_ */

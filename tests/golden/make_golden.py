@@ -1,0 +1,159 @@
+"""Generate the golden fixtures in tests/golden/*.npz from the REFERENCE itself.
+
+Run in the build container only (the reference is not on the GPU box):
+
+    python tests/golden/make_golden.py [/root/reference]
+
+It imports the reference's own lib/Hodge_Cheb_Conv.py, lib/Hodge_Dataset.py and
+lib/Hodge_ST_Model.py (behind pyg_standin.py, since PyG / torch_scatter are not
+installed), runs their forward and autograd backward on CPU for seeded inputs,
+and stores inputs, parameters, outputs and gradients as plain .npz arrays
+(no pickles).  Nothing from the reference source is copied.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "hl-hgat_amd"))
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _save(name, **arrays):
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print("wrote", path, sum(np.asarray(v).nbytes for v in arrays.values()), "bytes")
+
+
+def small_batch(n_graphs, seed):
+    # host-side data layer only (synthetic molecules + collation); no HIP
+    from hlhgat.synthetic import zinc_like_graph
+    from hlhgat.hodge_dataset import collate
+    return collate([zinc_like_graph(seed * 1000 + i, keig=15) for i in range(n_graphs)],
+                   check_hodge=True)
+
+
+def conv_cases(ref, b):
+    gen = torch.Generator().manual_seed(1234)
+    cases = []
+    for kind, Ks in (("laguerre", (1, 2, 3, 6)), ("cheb", (2, 4))):
+        for K in Ks:
+            for side in ("t", "s"):
+                cases.append((kind, K, side, 2))
+    cases.append(("laguerre", 3, "t", 3))  # 3-D input [N, T, C]
+    for kind, K, side, ndim in cases:
+        ei = getattr(b, "edge_index_" + side)
+        ew = getattr(b, "edge_weight_" + side)
+        n = getattr(b, "x_" + side).shape[0]
+        cin, cout = 12, 16
+        torch.manual_seed(K * 7 + (side == "s"))
+        cls = ref.HodgeLaguerreConv if kind == "laguerre" else ref.HodgeChebConv
+        conv = cls(cin, cout, K=K)
+        with torch.no_grad():
+            conv.bias.uniform_(-0.5, 0.5)  # reference zero-inits; exercise the bias path
+        shape = (n, cin) if ndim == 2 else (n, 3, cin)
+        x = torch.randn(*shape, generator=gen).requires_grad_(True)
+        out = conv(x, ei, ew)
+        R = torch.randn(out.shape, generator=gen)
+        (out * R).sum().backward()
+        arrays = dict(x=_np(x), edge_index=_np(ei), edge_weight=_np(ew), out=_np(out), R=_np(R),
+                      grad_x=_np(x.grad), bias=_np(conv.bias), grad_bias=_np(conv.bias.grad))
+        for k, lin in enumerate(conv.lins):
+            arrays[f"w{k}"] = _np(lin.weight)
+            arrays[f"grad_w{k}"] = _np(lin.weight.grad)
+        _save(f"conv_{kind}_K{K}_{side}_{ndim}d", K=np.int64(K), **arrays)
+
+
+def nei_cases(ref, b):
+    gen = torch.Generator().manual_seed(99)
+    N_t, N_s = b.x_t.shape[0], b.x_s.shape[0]
+    ei = b.edge_index
+    par = ref_ds.adj2par1(ei, N_t, N_s)
+    D = ref_utils.degree(ei.view(-1), num_nodes=N_t)
+    for name, kw, eps in (("value", dict(d=24, dv=16), 0.0),
+                          ("att_sigmoid", dict(d=24, dk=8, only_att=True,
+                                               sigma=torch.nn.Sigmoid(), l=0.9), 1e-6),
+                          ("att_relu", dict(d=24, dk=8, only_att=True,
+                                            sigma=torch.nn.ReLU(), l=0.5), 1e-6)):
+        torch.manual_seed(5)
+        m = ref.NodeEdgeInt(**kw)
+        m.train()
+        x_t = torch.randn(N_t, kw["d"], generator=gen).requires_grad_(True)
+        x_s = torch.randn(N_s, kw["d"], generator=gen).requires_grad_(True)
+        Dv = D + eps
+        a, c = m(x_t, x_s, par, Dv)
+        Ra = torch.randn(a.shape, generator=gen)
+        Rc = torch.randn(c.shape, generator=gen)
+        ((a * Ra).sum() + (c * Rc).sum()).backward()
+        arrays = dict(x_t=_np(x_t), x_s=_np(x_s), edge_index=_np(ei), D=_np(Dv), out_t=_np(a),
+                      out_s=_np(c), R_t=_np(Ra), R_s=_np(Rc), grad_x_t=_np(x_t.grad),
+                      grad_x_s=_np(x_s.grad))
+        for k, v in m.state_dict().items():
+            arrays["sd/" + k] = _np(v)
+        for k, p in m.named_parameters():
+            arrays["grad/" + k] = _np(p.grad)
+        _save(f"nei_{name}", **arrays)
+
+
+class _RefData:
+    pass
+
+
+def zinc_case(ref_model, b):
+    torch.manual_seed(3)
+    m = ref_model.HL_HGCNN_zinc_dense_int3_pyr(channels=[1, 1], filters=[16, 16],
+                                               mlp_channels=[32], K=3, keig=15)
+    m.train()
+    d = _RefData()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index"):
+        setattr(d, k, getattr(b, k))
+    d.num_node1 = [int(v) for v in b.num_node1]
+    d.num_edge1 = [int(v) for v in b.num_edge1]
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    out = m(d, device="cpu")
+    gen = torch.Generator().manual_seed(7)
+    R = torch.randn(out.shape, generator=gen)
+    (out * R).sum().backward()
+    arrays = dict(x_t=_np(b.x_t), x_s=_np(b.x_s), edge_index_t=_np(b.edge_index_t),
+                  edge_weight_t=_np(b.edge_weight_t), edge_index_s=_np(b.edge_index_s),
+                  edge_weight_s=_np(b.edge_weight_s), edge_index=_np(b.edge_index),
+                  num_node1=_np(b.num_node1), num_edge1=_np(b.num_edge1), out=_np(out), R=_np(R))
+    for k, v in sd0.items():
+        arrays["sd/" + k] = _np(v)
+    for k, p in m.named_parameters():
+        arrays["grad/" + k] = _np(p.grad)
+    _save("zinc_model_small", **arrays)
+
+
+def structure_case(b):
+    """adj2par1 of the reference, densified, for a 2-graph batch."""
+    par = ref_ds.adj2par1(b.edge_index, b.x_t.shape[0], b.x_s.shape[0])
+    _save("adj2par1_small", edge_index=_np(b.edge_index), dense=_np(par.to_dense()),
+          n_nodes=np.int64(b.x_t.shape[0]))
+
+
+if __name__ == "__main__":
+    ref_root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    import pyg_standin
+    pyg_standin.install()
+    sys.path.insert(0, ref_root)
+    import lib.Hodge_Cheb_Conv as ref           # noqa: E402  (reference code)
+    import lib.Hodge_Dataset as ref_ds          # noqa: E402
+    import lib.Hodge_ST_Model as ref_model      # noqa: E402
+    import torch_geometric.utils as ref_utils   # noqa: E402  (stand-in)
+    torch.set_num_threads(1)  # deterministic CPU reduction order
+    b = small_batch(6, seed=11)
+    conv_cases(ref, b)
+    nei_cases(ref, b)
+    zinc_case(ref_model, small_batch(8, seed=12))
+    structure_case(small_batch(2, seed=13))

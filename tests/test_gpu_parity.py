@@ -1,0 +1,340 @@
+"""HIP path vs the oracle / the reference's golden vectors (MI355X only).
+
+Tolerances, written per assertion:
+  * SpMM, Laguerre/Chebyshev basis, incidence gathers: BIT-EXACT vs the oracle
+    (same operation order, -ffp-contract=off);
+  * outputs through the MFMA projection: max|d| <= 1e-5 * max(1, max|ref|);
+  * gradients: 1e-4 relative;  whole model after BN: 1e-4 relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import close, golden_names, load_golden
+from oracle import hodge_ref as R
+
+pytestmark = pytest.mark.gpu
+
+T = torch.from_numpy
+
+
+def dev(a, d="cuda:0"):
+    return (T(a) if isinstance(a, np.ndarray) else a).to(d)
+
+
+def rand_graph(n, nnz, seed, sym=False, sort=True):
+    g = torch.Generator().manual_seed(seed)
+    r = torch.randint(0, max(n, 1), (nnz,), generator=g)
+    c = torch.randint(0, max(n, 1), (nnz,), generator=g)
+    w = torch.randn(nnz, generator=g)
+    if sym:
+        r, c = torch.cat([r, c]), torch.cat([c, r])
+        w = torch.cat([w, w])
+    ei = torch.stack([r, c])
+    if sort:
+        key = ei[0] * max(n, 1) + ei[1]
+        o = torch.argsort(key, stable=True)
+        ei, w = ei[:, o], w[o]
+    return ei.contiguous(), w.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# SpMM / propagate
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("d", [1, 2, 3, 18, 36, 64, 128, 300])
+@pytest.mark.parametrize("mode", ["general", "general_unsorted"])
+def test_spmm_bitexact_vs_propagate(cuda, d, mode):
+    from hlhgat import ops
+    n = 517
+    ei, w = rand_graph(n, 3000, seed=d, sort=(mode == "general"))
+    x = torch.randn(n, d, generator=torch.Generator().manual_seed(1))
+    ref = R.propagate(x, ei, w)
+    op = ops.hodge_operator(dev(ei), dev(w), n)
+    y = ops.spmm(op.fwd, dev(x)).cpu()
+    # CSR keeps COO order within a row only for sorted input; unsorted input is
+    # reordered by (row, col) like torch coalesce -> compare with tolerance
+    if mode == "general":
+        assert torch.equal(y, ref), (y - ref).abs().max()
+    else:
+        close(y, ref, 1e-5, "spmm unsorted")
+
+
+def test_spmm_hodge_fast_path_bitexact(cuda):
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(40, seed=3)
+    for side in ("t", "s"):
+        ei = getattr(b, "edge_index_" + side)
+        w = getattr(b, "edge_weight_" + side)
+        n = getattr(b, "x_" + side).shape[0]
+        x = torch.randn(n, 64, generator=torch.Generator().manual_seed(2))
+        ref = R.propagate(x, ei, w)
+        ei_d = ops.mark_hodge(dev(ei))
+        op = ops.hodge_operator(ei_d, dev(w), n)
+        assert op.fwd is op.bwd  # symmetric fast path: one CSR
+        y = ops.spmm(op.fwd, dev(x)).cpu()
+        assert torch.equal(y, ref)
+
+
+def test_spmm_empty_rows_and_empty_matrix(cuda):
+    from hlhgat import ops
+    n = 50
+    ei = torch.tensor([[3, 3, 7], [1, 9, 7]])  # rows 0..2, 4..6, 8.. are empty
+    w = torch.tensor([1.5, -2.0, 0.25])
+    x = torch.randn(n, 64)
+    op = ops.hodge_operator(dev(ei), dev(w), n)
+    assert torch.equal(ops.spmm(op.fwd, dev(x)).cpu(), R.propagate(x, ei, w))
+    op0 = ops.hodge_operator(dev(torch.zeros(2, 0, dtype=torch.long)),
+                             dev(torch.zeros(0)), n)
+    assert torch.equal(ops.spmm(op0.fwd, dev(x)).cpu(), torch.zeros(n, 64))
+
+
+def test_spmm_skewed_rows(cuda):
+    """A hub row with thousands of entries next to rows with one (L1-style skew)."""
+    from hlhgat import ops
+    n = 3000
+    hub = torch.stack([torch.zeros(n, dtype=torch.long), torch.arange(n)])
+    diag = torch.stack([torch.arange(n), torch.arange(n)])
+    ei = torch.cat([hub, diag], 1)
+    key = ei[0] * n + ei[1]
+    o = torch.argsort(key, stable=True)
+    ei = ei[:, o].contiguous()
+    w = torch.randn(ei.size(1))
+    x = torch.randn(n, 64)
+    op = ops.hodge_operator(dev(ei), dev(w), n)
+    close(ops.spmm(op.fwd, dev(x)).cpu(), R.propagate(x, ei, w), 1e-6, "skew")
+
+
+# ---------------------------------------------------------------------------
+# polynomial basis (bit-exact) and full conv vs golden
+# ---------------------------------------------------------------------------
+def _ref_basis(x, ei, w, K, kind):
+    Ts = [x]
+    if K > 1:
+        p = R.propagate(x, ei, w)
+        Ts.append(x - p if kind == "laguerre" else p)
+    for k in range(1, K - 1):
+        p = R.propagate(Ts[k], ei, w)
+        if kind == "laguerre":
+            Ts.append((-p + (2 * k + 1) * Ts[k] - k * Ts[k - 1]) / (k + 1))
+        else:
+            Ts.append(2. * p - Ts[k - 1])
+    return Ts[1:]
+
+
+@pytest.mark.parametrize("kind", ["laguerre", "cheb"])
+@pytest.mark.parametrize("K", [2, 3, 4, 6])
+def test_poly_basis_bitexact(cuda, kind, K):
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(20, seed=K)
+    ei, w, n = b.edge_index_s, b.edge_weight_s, b.x_s.shape[0]
+    x = torch.randn(n, 64, generator=torch.Generator().manual_seed(K))
+    op = ops.hodge_operator(ops.mark_hodge(dev(ei)), dev(w), n)
+    code = ops.POLY_LAGUERRE if kind == "laguerre" else ops.POLY_CHEB
+    Tdev = ops.poly_basis(op, dev(x), K, code).cpu()
+    for k, Tr in enumerate(_ref_basis(x, ei, w, K, kind)):
+        assert torch.equal(Tdev[k], Tr), (kind, K, k, (Tdev[k] - Tr).abs().max())
+
+
+@pytest.mark.parametrize("name", golden_names("conv_"))
+def test_conv_vs_reference_golden(cuda, name):
+    import hlhgat
+    g = load_golden(name)
+    K = int(g["K"])
+    cls = hlhgat.HodgeChebConv if "cheb" in name else hlhgat.HodgeLaguerreConv
+    conv = cls(g["w0"].shape[1], g["w0"].shape[0], K=K).to(cuda)
+    sd = {"bias": T(g["bias"])}
+    sd.update({f"lins.{k}.weight": T(g[f"w{k}"]) for k in range(K)})
+    conv.load_state_dict(sd)
+    x = dev(g["x"]).requires_grad_(True)
+    out = conv(x, dev(g["edge_index"]), dev(g["edge_weight"]))
+    close(out.detach().cpu(), g["out"], 1e-5, "out")
+    (out * dev(g["R"])).sum().backward()
+    close(x.grad.cpu(), g["grad_x"], 1e-4, "grad_x")
+    close(conv.bias.grad.cpu(), g["grad_bias"], 1e-4, "grad_bias")
+    for k in range(K):
+        close(conv.lins[k].weight.grad.cpu(), g[f"grad_w{k}"], 1e-4, f"grad_w{k}")
+
+
+def test_conv_unsorted_nonsymmetric_operator(cuda):
+    """General (sorting) CSR path incl. the transposed adjoint for a
+    non-symmetric operator: gradient w.r.t. x must use L^T."""
+    import hlhgat
+    n, cin, cout, K = 300, 24, 32, 4
+    ei, w = rand_graph(n, 2000, seed=5, sort=False)
+    torch.manual_seed(0)
+    conv = hlhgat.HodgeLaguerreConv(cin, cout, K=K).to(cuda)
+    ref = R.RefHodgeConv(cin, cout, K)
+    ref.load_state_dict({k: v.cpu() for k, v in conv.state_dict().items()})
+    x = torch.randn(n, cin)
+    xd = dev(x).requires_grad_(True)
+    xr = x.clone().requires_grad_(True)
+    out = conv(xd, dev(ei), dev(w))
+    outr = ref(xr, ei, w)
+    close(out.detach().cpu(), outr.detach(), 1e-5, "out")
+    Rg = torch.randn(out.shape)
+    (out * dev(Rg)).sum().backward()
+    (outr * Rg).sum().backward()
+    close(xd.grad.cpu(), xr.grad, 1e-4, "grad_x")
+
+
+def test_conv_K1_is_linear(cuda):
+    import hlhgat
+    conv = hlhgat.HodgeLaguerreConv(8, 5, K=1).to(cuda)
+    x = torch.randn(10, 8, device=cuda)
+    ei = torch.zeros(2, 0, dtype=torch.long, device=cuda)
+    out = conv(x, ei, torch.zeros(0, device=cuda))
+    close(out.cpu(), (x @ conv.lins[0].weight.t() + conv.bias).cpu(), 1e-5, "K=1")
+
+
+# ---------------------------------------------------------------------------
+# MFMA projection GEMMs vs a plain fp32 torch reference
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("M,N,kbs", [(1, 1, [1]), (17, 16, [4]), (1000, 64, [64, 64, 64]),
+                                     (5000, 64, [384, 384]), (333, 33, [18, 7]),
+                                     (4097, 130, [36]), (2048, 256, [128, 128]),
+                                     (70000, 64, [64])])
+def test_linear_blocks_fwd_bwd(cuda, M, N, kbs):
+    from hlhgat import ops
+    g = torch.Generator().manual_seed(M + N)
+    As = [torch.randn(M, k, generator=g) for k in kbs]
+    W = torch.randn(N, sum(kbs), generator=g) * 0.1
+    b = torch.randn(N, generator=g)
+    Ad = [dev(a).requires_grad_(True) for a in As]
+    Wd = dev(W).requires_grad_(True)
+    bd = dev(b).requires_grad_(True)
+    out = ops.linear_blocks(Ad, Wd, bd)
+    Ar = [a.clone().double().requires_grad_(True) for a in As]
+    Wr = W.clone().double().requires_grad_(True)
+    br = b.clone().double().requires_grad_(True)
+    outr = torch.cat(Ar, 1) @ Wr.t() + br
+    close(out.detach().cpu(), outr.detach(), 1e-5, "fwd")
+    Rg = torch.randn(M, N, generator=g)
+    (out * dev(Rg)).sum().backward()
+    (outr * Rg.double()).sum().backward()
+    for i in range(len(kbs)):
+        close(Ad[i].grad.cpu(), Ar[i].grad, 1e-5, f"dA{i}")
+    close(Wd.grad.cpu(), Wr.grad, 1e-4, "dW")
+    close(bd.grad.cpu(), br.grad, 1e-4, "db")
+
+
+def test_linear_blocks_strided_views(cuda):
+    """Operands that are column slices of wider tensors (ld > width)."""
+    from hlhgat import ops
+    A = torch.randn(500, 96, device=cuda)
+    W = torch.randn(40, 64, device=cuda)
+    out = ops.linear_blocks([A[:, 8:40], A[:, 64:96]], W, None)
+    exp = torch.cat([A[:, 8:40], A[:, 64:96]], 1) @ W.t()
+    close(out.cpu(), exp.cpu(), 1e-5, "strided")
+
+
+# ---------------------------------------------------------------------------
+# boundary operator, attention, pooling
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["nei_value", "nei_att_sigmoid", "nei_att_relu"])
+def test_node_edge_int_vs_reference_golden(cuda, name):
+    import hlhgat
+    g = load_golden(name)
+    sd = {k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")}
+    if name == "nei_value":
+        m = hlhgat.NodeEdgeInt(d=sd["WV_Node.0.weight"].shape[1] // 2,
+                               dv=sd["WV_Node.3.weight"].shape[0])
+    else:
+        sig = torch.nn.Sigmoid() if "sigmoid" in name else torch.nn.ReLU()
+        m = hlhgat.NodeEdgeInt(d=sd["WQ_Node.weight"].shape[1], dk=sd["WQ_Node.weight"].shape[0],
+                               only_att=True, sigma=sig, l=0.9 if "sigmoid" in name else 0.5)
+    m.load_state_dict(sd)
+    m = m.to(cuda).train()
+    x_t = dev(g["x_t"]).requires_grad_(True)
+    x_s = dev(g["x_s"]).requires_grad_(True)
+    par = hlhgat.adj2par1(dev(g["edge_index"]), x_t.shape[0], x_s.shape[0])
+    a, c = m(x_t, x_s, par, dev(g["D"]))
+    close(a.detach().cpu(), g["out_t"], 1e-5, "out_t")
+    close(c.detach().cpu(), g["out_s"], 1e-5, "out_s")
+    ((a * dev(g["R_t"])).sum() + (c * dev(g["R_s"])).sum()).backward()
+    close(x_t.grad.cpu(), g["grad_x_t"], 1e-4, "grad_x_t")
+    close(x_s.grad.cpu(), g["grad_x_s"], 1e-4, "grad_x_s")
+    for k, p in m.named_parameters():
+        close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
+
+
+def test_incidence_gathers_bitexact(cuda):
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(30, seed=8)
+    ei = b.edge_index
+    N_t, N_s = b.x_t.shape[0], b.x_s.shape[0]
+    D = R.degree(ei.reshape(-1), N_t) + 1e-6
+    x_t, x_s = torch.randn(N_t, 40), torch.randn(N_s, 40)
+    par = R.adj2par1(ei, N_t, N_s)
+    s2t, t2s = R.boundary_mix(x_t, x_s, par, D)
+    inc = ops.incidence(dev(ei), N_t)
+    s2t_d = ops.node_from_edges(dev(x_s), inc, dev(1 / D)).cpu()
+    t2s_d = ops.edge_from_nodes(dev(x_t), inc).cpu()
+    assert torch.equal(t2s_d, t2s)
+    assert torch.equal(s2t_d, s2t)
+
+
+def test_segment_and_cluster_mean(cuda):
+    from hlhgat import ops
+    from hlhgat.hodge_cheb_conv import cluster_mean
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(1000, 48, generator=g)
+    assign = torch.randint(0, 77, (1000,), generator=g)
+    xd = dev(x).requires_grad_(True)
+    out = cluster_mean(xd, dev(assign))
+    xr = x.clone().requires_grad_(True)
+    outr = R.scatter_mean(xr, assign)
+    close(out.detach().cpu(), outr.detach(), 1e-6, "scatter_mean")
+    Rg = torch.randn(outr.shape, generator=g)
+    (out * dev(Rg)).sum().backward()
+    (outr * Rg).sum().backward()
+    close(xd.grad.cpu(), xr.grad, 1e-6, "scatter_mean grad")
+
+
+# ---------------------------------------------------------------------------
+# whole model (lib/Hodge_ST_Model.py:544-646)
+# ---------------------------------------------------------------------------
+def test_zinc_model_vs_reference_golden(cuda):
+    import hlhgat
+    from hlhgat.hodge_dataset import Batch
+    g = load_golden("zinc_model_small")
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[1, 1], filters=[16, 16],
+                                            mlp_channels=[32], K=3, keig=15)
+    m.load_state_dict({k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")})
+    m = m.to(cuda).train()
+    b = Batch()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index", "num_node1", "num_edge1"):
+        setattr(b, k, dev(g[k]))
+    out = m(b)
+    close(out.detach().cpu(), g["out"], 1e-4, "out")
+    (out * dev(g["R"])).sum().backward()
+    for k, p in m.named_parameters():
+        close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
+
+
+def test_zinc_model_cfg2_vs_oracle(cuda):
+    """BASELINE config 2 model at a 200-graph batch: HIP product vs oracle."""
+    import hlhgat
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(200, seed=21)
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2, 2], filters=[64, 64, 64],
+                                            mlp_channels=[256, 256], K=3, keig=15)
+    ref = R.RefZincModel(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256],
+                         K=3, keig=15)
+    ref.load_state_dict(m.state_dict())
+    m = m.to(cuda).train()
+    ref.train()
+    out_r = ref(b)
+    bd = zinc_like_batch(200, seed=21).to(cuda)
+    out = m(bd)
+    close(out.detach().cpu(), out_r.detach(), 1e-4, "out")
+    Rg = torch.randn(out_r.shape)
+    (out * dev(Rg)).sum().backward()
+    (out_r * Rg).sum().backward()
+    rp = dict(ref.named_parameters())
+    for k, p in m.named_parameters():
+        close(p.grad.cpu(), rp[k].grad, 1e-3, "grad " + k)

@@ -1,0 +1,116 @@
+"""Host-side logic: PairData batching, layouts, module names (CPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+
+def test_collate_offsets_follow_pairdata_inc():
+    """lib/Hodge_Dataset.py:40-48: edge_index_s += N_s, edge_index_t and
+    edge_index += N_t per preceding graph."""
+    from hlhgat.synthetic import zinc_like_graph
+    from hlhgat.hodge_dataset import collate
+    gs = [zinc_like_graph(i) for i in range(3)]
+    b = collate(gs)
+    nt = [g.x_t.shape[0] for g in gs]
+    ns = [g.x_s.shape[0] for g in gs]
+    assert b.x_t.shape[0] == sum(nt) and b.x_s.shape[0] == sum(ns)
+    e0 = gs[0].edge_index_s.shape[1]
+    assert torch.equal(b.edge_index_s[:, e0:e0 + gs[1].edge_index_s.shape[1]],
+                       gs[1].edge_index_s + ns[0])
+    c0 = gs[0].edge_index.shape[1]
+    assert torch.equal(b.edge_index[:, c0:c0 + gs[1].edge_index.shape[1]],
+                       gs[1].edge_index + nt[0])
+    t0 = gs[0].edge_index_t.shape[1]
+    assert torch.equal(b.edge_index_t[:, t0:t0 + gs[1].edge_index_t.shape[1]],
+                       gs[1].edge_index_t + nt[0])
+    assert b.num_node1.tolist() == nt and b.num_edge1.tolist() == ns
+    assert b.hodge_sorted == {"edge_index_s": True, "edge_index_t": True}
+
+
+def test_hodge_laplacian_structure():
+    """L0 = 2 B1 B1^T / lmax, L1 = 2 B1^T B1 / lmax (lib/Hodge_Dataset.py:451-456):
+    nnz(L0) = N + 2E for a graph without isolated nodes, nnz(L1) = E + sum d(d-1),
+    spectrum of both in [0, 2]."""
+    from hlhgat.synthetic import zinc_like_graph
+    g = zinc_like_graph(5)
+    n, E = g.x_t.shape[0], g.x_s.shape[0]
+    assert g.edge_index_t.shape[1] == n + 2 * E
+    deg = np.bincount(g.edge_index.numpy().reshape(-1), minlength=n)
+    assert g.edge_index_s.shape[1] == E + int((deg * (deg - 1)).sum())
+    L1 = torch.zeros(E, E)
+    L1[g.edge_index_s[0], g.edge_index_s[1]] = g.edge_weight_s
+    ev = torch.linalg.eigvalsh(L1.double())
+    assert ev.min() > -1e-5 and ev.max() < 2 + 1e-5
+
+
+def test_is_sorted_symmetric():
+    from hlhgat.hodge_dataset import is_sorted_symmetric
+    ei = np.array([[0, 0, 1, 1], [0, 1, 0, 1]])
+    w = np.array([1.0, 2.0, 2.0, 3.0])
+    assert is_sorted_symmetric(ei, w)
+    assert not is_sorted_symmetric(ei, np.array([1.0, 2.0, 2.5, 3.0]))
+    assert not is_sorted_symmetric(ei[:, ::-1].copy(), w[::-1].copy())
+
+
+def test_adj2par1_dense_matches_reference_golden():
+    from hlhgat.hodge_dataset import adj2par1
+    g = load_golden("adj2par1_small")
+    par = adj2par1(torch.from_numpy(g["edge_index"]), int(g["n_nodes"]),
+                   g["edge_index"].shape[1])
+    assert np.array_equal(par.to_dense().numpy(), g["dense"])
+
+
+def test_boundary_from_sparse_roundtrip():
+    from hlhgat.hodge_dataset import adj2par1, boundary_from_sparse
+    ei = torch.tensor([[0, 0, 1, 2], [1, 2, 2, 3]])
+    par = adj2par1(ei, 4, 4).to_sparse_coo()
+    assert torch.equal(boundary_from_sparse(par).edge_index, ei)
+
+
+def test_state_dict_keys_match_reference_checkpoint_names():
+    """Product and oracle modules share the reference's state_dict keys; the
+    gnn.Sequential module_{i} / gnn.BatchNorm .module naming follows
+    HL-HGAT-DEMO/weights/HL_HGAT_Brain.pt."""
+    import hlhgat
+    from oracle.hodge_ref import RefZincModel
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2, 2], filters=[64, 64, 64],
+                                            mlp_channels=[256, 256], K=3, keig=15)
+    r = RefZincModel(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256],
+                     K=3, keig=15)
+    assert list(m.state_dict().keys()) == list(r.state_dict().keys())
+    keys = set(m.state_dict().keys())
+    for k in ("HL_init_conv.module_0.lins.0.weight", "HL_init_conv.module_1.module.running_mean",
+              "HL_init_conv.module_4.bias", "NEInt00.WV_Node.0.weight", "NEInt21.WV_Edge.4.bias",
+              "NEConv21.module_5.module.weight", "mlp1.0.weight", "out.bias"):
+        assert k in keys, k
+    assert sum(p.numel() for p in m.parameters()) == 658433  # 0.66M
+
+
+def test_reference_golden_state_dict_loads_into_product():
+    import hlhgat
+    g = load_golden("zinc_model_small")
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[1, 1], filters=[16, 16],
+                                            mlp_channels=[32], K=3, keig=15)
+    missing, unexpected = m.load_state_dict(
+        {k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("sd/")}, strict=True)
+    assert not missing and not unexpected
+
+
+def test_sequential_routing_and_names():
+    from hlhgat.nn import Sequential
+    seq = Sequential("a, b", [(torch.nn.Identity(), "a -> a"), (lambda x, y: x + y, "a, b -> c"),
+                              (torch.nn.ReLU(), "c -> c")])
+    out = seq(torch.tensor([-1.0, 2.0]), torch.tensor([0.5, 0.5]))
+    assert torch.equal(out, torch.tensor([0.0, 2.5]))
+    assert "module_0" in dict(seq.named_children()) and callable(seq.module_1)
+
+
+def test_synthetic_zinc_statistics():
+    """Synthetic ZINC-like batch matches the survey's shape statistics."""
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(300, seed=1)
+    assert 21.5 < b.num_node1.float().mean() < 25.0
+    assert 23.0 < b.num_edge1.float().mean() < 27.0
+    assert b.x_t.shape[1] == 36 and b.x_s.shape[1] == 18

@@ -1,0 +1,96 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tests/golden/make_golden.py imports deepika090/HL-HGAT's lib/*.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import close, golden_names, load_golden
+from oracle import hodge_ref as R
+
+T = torch.from_numpy
+
+
+@pytest.mark.parametrize("name", golden_names("conv_"))
+def test_conv_oracle_matches_reference(name):
+    g = load_golden(name)
+    K = int(g["K"])
+    kind = "cheb" if "cheb" in name else "laguerre"
+    x = T(g["x"]).requires_grad_(True)
+    ws = [T(g[f"w{k}"]).requires_grad_(True) for k in range(K)]
+    b = T(g["bias"]).requires_grad_(True)
+    fn = R.cheb_conv if kind == "cheb" else R.laguerre_conv
+    out = fn(x, T(g["edge_index"]), T(g["edge_weight"]), ws, b)
+    close(out.detach(), g["out"], 1e-6, "out")
+    (out * T(g["R"])).sum().backward()
+    close(x.grad, g["grad_x"], 1e-6, "grad_x")
+    close(b.grad, g["grad_bias"], 1e-6, "grad_bias")
+    for k in range(K):
+        close(ws[k].grad, g[f"grad_w{k}"], 1e-6, f"grad_w{k}")
+
+
+def _sd(g):
+    return {k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")}
+
+
+@pytest.mark.parametrize("name", ["nei_value", "nei_att_sigmoid", "nei_att_relu"])
+def test_node_edge_int_oracle(name):
+    g = load_golden(name)
+    sd = _sd(g)
+    if name == "nei_value":
+        d = sd["WV_Node.0.weight"].shape[1] // 2
+        m = R.RefNodeEdgeInt(d=d, dv=sd["WV_Node.3.weight"].shape[0])
+    else:
+        d = sd["WQ_Node.weight"].shape[1]
+        sig = torch.nn.Sigmoid() if "sigmoid" in name else torch.nn.ReLU()
+        lam = 0.9 if "sigmoid" in name else 0.5
+        m = R.RefNodeEdgeInt(d=d, dk=sd["WQ_Node.weight"].shape[0], only_att=True, sigma=sig,
+                             l=lam)
+    m.load_state_dict(sd)
+    m.train()
+    x_t = T(g["x_t"]).requires_grad_(True)
+    x_s = T(g["x_s"]).requires_grad_(True)
+    par = R.adj2par1(T(g["edge_index"]), x_t.shape[0], x_s.shape[0])
+    a, c = m(x_t, x_s, par, T(g["D"]))
+    close(a.detach(), g["out_t"], 1e-6, "out_t")
+    close(c.detach(), g["out_s"], 1e-6, "out_s")
+    ((a * T(g["R_t"])).sum() + (c * T(g["R_s"])).sum()).backward()
+    close(x_t.grad, g["grad_x_t"], 1e-5, "grad_x_t")
+    close(x_s.grad, g["grad_x_s"], 1e-5, "grad_x_s")
+    for k, p in m.named_parameters():
+        close(p.grad, g["grad/" + k], 1e-4, "grad " + k)
+
+
+class _D:
+    pass
+
+
+def test_zinc_model_oracle():
+    g = load_golden("zinc_model_small")
+    m = R.RefZincModel(channels=[1, 1], filters=[16, 16], mlp_channels=[32], K=3, keig=15)
+    m.load_state_dict(_sd(g))
+    m.train()
+    d = _D()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index", "num_node1", "num_edge1"):
+        setattr(d, k, T(g[k]))
+    out = m(d)
+    close(out.detach(), g["out"], 1e-5, "out")
+    (out * T(g["R"])).sum().backward()
+    for k, p in m.named_parameters():
+        close(p.grad, g["grad/" + k], 1e-4, "grad " + k)
+
+
+def test_adj2par1_oracle():
+    g = load_golden("adj2par1_small")
+    par = R.adj2par1(T(g["edge_index"]), int(g["n_nodes"]), g["edge_index"].shape[1])
+    assert np.array_equal(par.to_dense().numpy(), g["dense"])
+
+
+def test_oracle_propagate_is_sequential_scatter():
+    """propagate = gather * norm then scatter-add in edge order (PyG aggr='add')."""
+    ei = torch.tensor([[0, 1, 2, 2], [1, 0, 0, 2]])
+    w = torch.tensor([0.5, 2.0, -1.0, 3.0])
+    x = torch.tensor([[1.0, 2.0], [3.0, 4.0], [5.0, 6.0]])
+    out = R.propagate(x, ei, w)
+    exp = torch.tensor([[6.0 - 5.0, 8.0 - 6.0], [0.5, 1.0], [15.0, 18.0]])
+    assert torch.equal(out, exp)
