@@ -185,7 +185,7 @@ def test_conv_K1_is_linear(cuda):
     x = torch.randn(10, 8, device=cuda)
     ei = torch.zeros(2, 0, dtype=torch.long, device=cuda)
     out = conv(x, ei, torch.zeros(0, device=cuda))
-    close(out.cpu(), (x @ conv.lins[0].weight.t() + conv.bias).cpu(), 1e-5, "K=1")
+    close(out.detach().cpu(), (x @ conv.lins[0].weight.t() + conv.bias).detach().cpu(), 1e-5, "K=1")
 
 
 # ---------------------------------------------------------------------------
