@@ -1,0 +1,499 @@
+// Training-mode BatchNorm1d (+ optional fused ReLU) for the HL blocks.
+//
+// Every HL block is HodgeLaguerreConv -> gnn.BatchNorm -> ReLU -> Dropout
+// (lib/Hodge_ST_Model.py:556-566) and every NodeEdgeInt value MLP is
+// Linear -> BatchNorm1d -> ReLU twice (lib/Hodge_Cheb_Conv.py:276-289), so
+// each conv output passes through a batch-statistics reduction over all
+// simplices.  Two launches per direction:
+//   fwd: k_bn_stats  — per-workgroup column partials (fp64 sum, sum of squares)
+//                      and, in the LAST workgroup to arrive, the final mean /
+//                      invstd and the running-stat update (deterministic: the
+//                      last arriver sums the partials in workgroup order);
+//        k_bn_apply  — y = relu?(x * s + t).
+//   bwd: k_bn_bwd_reduce — partials of sum(g) and sum(g*(x-mean)), g = dy *
+//                      [y > 0]; the last arriver forms dweight, dbias and the
+//                      per-channel coefficients of dx;
+//        k_bn_bwd_apply  — dx = a*g + b*x + c.
+// Inter-workgroup hand-off follows MI355X_MICROARCH.md / cdna_hip_programming.md
+// Guideline 16: plain stores, every wave's vmcnt(0), barrier, lane-0 agent
+// release fence, relaxed agent atomic ticket; the last arriver issues an
+// agent acquire fence before reading the partials.
+#include "common.h"
+
+using namespace hlhgat;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct BnLayout {
+  int v;       // floats per thread (4 or 1)
+  int tpr;     // threads per row within a column tile
+  int rp;      // rows per pass (kThreads / tpr)
+  int tile_c;  // columns per tile (tpr * v)
+  int tiles;   // column tiles
+  int parts;   // row partitions (grid.x)
+  int64_t rows_per_part;
+};
+
+BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
+  BnLayout L;
+  L.v = vec ? 4 : 1;
+  int lanes = (int)ceil_div(C, L.v);
+  L.tpr = next_pow2(lanes);
+  if (L.tpr > kThreads) L.tpr = kThreads;
+  L.rp = kThreads / L.tpr;
+  L.tile_c = L.tpr * L.v;
+  L.tiles = (int)ceil_div(C, L.tile_c);
+  // ~512 workgroups in all, each partition at least 4 passes of rows
+  int64_t parts = ceil_div(512, L.tiles);
+  int64_t max_parts = ceil_div(n, (int64_t)L.rp * 4);
+  if (parts > max_parts) parts = max_parts;
+  if (parts < 1) parts = 1;
+  if (parts > 1024) parts = 1024;
+  L.rows_per_part = ceil_div(n, parts);
+  L.parts = (int)ceil_div(n > 0 ? n : 1, L.rows_per_part);
+  return L;
+}
+
+struct BnWs {
+  double* part;      // [parts][C][2]
+  unsigned* count;   // [tiles] (zero between launches)
+  float* coef;       // [3][C] (bwd: a, b, c)
+};
+
+size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
+
+size_t bn_ws_bytes(int64_t n, int64_t C) {
+  BnLayout L = bn_layout(n, C, false);  // scalar layout has the most parts
+  BnLayout L4 = bn_layout(n, C, true);
+  int64_t parts = L.parts > L4.parts ? L.parts : L4.parts;
+  int64_t tiles = L.tiles > L4.tiles ? L.tiles : L4.tiles;
+  return align_up(sizeof(double) * 2 * parts * C) + align_up(sizeof(unsigned) * tiles) +
+         align_up(sizeof(float) * 3 * C);
+}
+
+BnWs carve(void* ws, int64_t n, int64_t C) {
+  BnLayout L = bn_layout(n, C, false);
+  BnLayout L4 = bn_layout(n, C, true);
+  int64_t parts = L.parts > L4.parts ? L.parts : L4.parts;
+  int64_t tiles = L.tiles > L4.tiles ? L.tiles : L4.tiles;
+  char* p = (char*)ws;
+  BnWs w;
+  w.part = (double*)p;
+  p += align_up(sizeof(double) * 2 * parts * C);
+  w.count = (unsigned*)p;
+  p += align_up(sizeof(unsigned) * tiles);
+  w.coef = (float*)p;
+  return w;
+}
+
+struct StatsArgs {
+  const float* x;
+  int64_t ldx;
+  const float* y;   // bwd: forward output for the ReLU mask (or NULL)
+  int64_t ldy;
+  const float* dy;  // bwd only
+  int64_t lddy;
+  int64_t n;
+  int C;
+  int tpr, rp, tiles, parts;
+  int64_t rows_per_part;
+  double* part;
+  unsigned* count;
+  // forward finalisation
+  const float* weight;
+  const float* bias;
+  float* running_mean;
+  float* running_var;
+  int64_t* nbt;
+  float momentum, eps;
+  float* save_mean;
+  float* save_invstd;
+  // backward finalisation
+  float* coef;
+  float* dweight;
+  float* dbias;
+};
+
+// Signal arrival; returns true in the last workgroup of this column tile.
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == total - 1) ? 1u : 0u;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *counter = 0u;  // ready for the next launch (stream-ordered)
+    }
+  }
+  __syncthreads();
+  return s_last != 0u;
+}
+
+// Block-level column partials: threads (row group rg, column lane cl) hold V
+// columns each; reduce over the rp row groups through LDS in fixed order.
+template <int V>
+__device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
+                                               const StatsArgs& a, int c0) {
+  __shared__ double red[2][kThreads * 4];
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    red[0][rg * a.tpr * V + cl * V + v] = s0[v];
+    red[1][rg * a.tpr * V + cl * V + v] = s1[v];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < a.tpr * V; t += kThreads) {
+    double u0 = 0.0, u1 = 0.0;
+    for (int g = 0; g < a.rp; ++g) {
+      u0 += red[0][g * a.tpr * V + t];
+      u1 += red[1][g * a.tpr * V + t];
+    }
+    const int c = c0 + t;
+    if (c < a.C) {
+      double* dst = a.part + ((int64_t)blockIdx.x * a.C + c) * 2;
+      dst[0] = u0;
+      dst[1] = u1;
+    }
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c0 = blockIdx.y * a.tpr * V;
+  const int c = c0 + cl * V;
+  const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
+  int64_t r_hi = r_lo + a.rows_per_part;
+  if (r_hi > a.n) r_hi = a.n;
+  double s0[V], s1[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
+  if (c < a.C) {
+    for (int64_t r = r_lo + rg; r < r_hi; r += a.rp) {
+      vt xv = vload<V>(a.x + r * a.ldx + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const double xd = (double)vget(xv, v);
+        s0[v] += xd;
+        s1[v] += xd * xd;
+      }
+    }
+  }
+  write_partials<V>(s0, s1, a, c0);
+  if (!arrive_last(a.count + blockIdx.y, (unsigned)a.parts)) return;
+  // last arriver of this column tile: finalise its columns
+  for (int t = threadIdx.x; t < a.tpr * V; t += kThreads) {
+    const int cc = c0 + t;
+    if (cc >= a.C) continue;
+    double u0 = 0.0, u1 = 0.0;
+    for (int p = 0; p < a.parts; ++p) {
+      const double* src = a.part + ((int64_t)p * a.C + cc) * 2;
+      u0 += src[0];
+      u1 += src[1];
+    }
+    const double nn = (double)a.n;
+    const double mean = u0 / nn;
+    double var = u1 / nn - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+    a.save_mean[cc] = (float)mean;
+    a.save_invstd[cc] = invstd;
+    if (a.running_mean) {
+      const double unb = a.n > 1 ? var * nn / (nn - 1.0) : var;
+      a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
+      a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
+    }
+  }
+  if (a.nbt && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+}
+
+struct ApplyArgs {
+  const float* x;
+  int64_t ldx;
+  float* y;
+  int64_t ldy;
+  int64_t n;
+  int C;
+  const float* mean;
+  const float* invstd;
+  const float* weight;
+  const float* bias;
+  int relu;
+  int tpr, rp;
+};
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c = blockIdx.y * a.tpr * V + cl * V;
+  if (c >= a.C) return;
+  float s[V], t[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const float w = a.weight ? a.weight[c + v] : 1.f;
+    const float b = a.bias ? a.bias[c + v] : 0.f;
+    s[v] = w * a.invstd[c + v];
+    t[v] = b - a.mean[c + v] * s[v];
+  }
+  for (int64_t r = (int64_t)blockIdx.x * a.rp + rg; r < a.n; r += (int64_t)gridDim.x * a.rp) {
+    vt xv = vload<V>(a.x + r * a.ldx + c);
+    vt o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float z = vget(xv, v) * s[v] + t[v];
+      vget(o, v) = (a.relu && z < 0.f) ? 0.f : z;
+    }
+    vstore<V>(a.y + r * a.ldy + c, o);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c0 = blockIdx.y * a.tpr * V;
+  const int c = c0 + cl * V;
+  const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
+  int64_t r_hi = r_lo + a.rows_per_part;
+  if (r_hi > a.n) r_hi = a.n;
+  double s0[V], s1[V];
+  float mu[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    s0[v] = s1[v] = 0.0;
+    mu[v] = (c + v < a.C) ? a.save_mean[c + v] : 0.f;
+  }
+  if (c < a.C) {
+    for (int64_t r = r_lo + rg; r < r_hi; r += a.rp) {
+      vt xv = vload<V>(a.x + r * a.ldx + c);
+      vt gv = vload<V>(a.dy + r * a.lddy + c);
+      vt yv;
+      if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float g = vget(gv, v);
+        if (a.y && !(vget(yv, v) > 0.f)) g = 0.f;
+        s0[v] += (double)g;
+        s1[v] += (double)g * (double)(vget(xv, v) - mu[v]);
+      }
+    }
+  }
+  write_partials<V>(s0, s1, a, c0);
+  if (!arrive_last(a.count + blockIdx.y, (unsigned)a.parts)) return;
+  for (int t = threadIdx.x; t < a.tpr * V; t += kThreads) {
+    const int cc = c0 + t;
+    if (cc >= a.C) continue;
+    double sg = 0.0, sgx = 0.0;
+    for (int p = 0; p < a.parts; ++p) {
+      const double* src = a.part + ((int64_t)p * a.C + cc) * 2;
+      sg += src[0];
+      sgx += src[1];
+    }
+    const double is = (double)a.save_invstd[cc];
+    const double w = a.weight ? (double)a.weight[cc] : 1.0;
+    const double nn = (double)a.n;
+    if (a.dweight) a.dweight[cc] = (float)(sgx * is);
+    if (a.dbias) a.dbias[cc] = (float)sg;
+    // dx = w*is*(g - sg/n - (x-mean)*is^2*sgx/n) = A*g + B*x + Cc
+    const double A = w * is;
+    const double B = -w * is * is * is * sgx / nn;
+    const double Cc = -w * is * sg / nn - B * (double)a.save_mean[cc];
+    a.coef[cc] = (float)A;
+    a.coef[a.C + cc] = (float)B;
+    a.coef[2 * a.C + cc] = (float)Cc;
+  }
+}
+
+struct BwdApplyArgs {
+  const float* x;
+  int64_t ldx;
+  const float* y;
+  int64_t ldy;
+  const float* dy;
+  int64_t lddy;
+  float* dx;
+  int64_t lddx;
+  int64_t n;
+  int C;
+  const float* coef;
+  int tpr, rp;
+};
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c = blockIdx.y * a.tpr * V + cl * V;
+  if (c >= a.C) return;
+  float A[V], B[V], Cc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    A[v] = a.coef[c + v];
+    B[v] = a.coef[a.C + c + v];
+    Cc[v] = a.coef[2 * a.C + c + v];
+  }
+  for (int64_t r = (int64_t)blockIdx.x * a.rp + rg; r < a.n; r += (int64_t)gridDim.x * a.rp) {
+    vt xv = vload<V>(a.x + r * a.ldx + c);
+    vt gv = vload<V>(a.dy + r * a.lddy + c);
+    vt yv;
+    if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+    vt o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float g = vget(gv, v);
+      if (a.y && !(vget(yv, v) > 0.f)) g = 0.f;
+      vget(o, v) = A[v] * g + (B[v] * vget(xv, v) + Cc[v]);
+    }
+    vstore<V>(a.dx + r * a.lddx + c, o);
+  }
+}
+
+bool bn_vec_ok(int64_t C, std::initializer_list<int64_t> lds,
+               std::initializer_list<const void*> ptrs) {
+  if (C % 4) return false;
+  for (int64_t ld : lds)
+    if (ld % 4) return false;
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return false;
+  return true;
+}
+
+unsigned apply_grid_x(int64_t n, int rp) {
+  int64_t g = ceil_div(n, rp * 8);  // ~8 rows per thread
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
+  if (n < 0 || C <= 0) return 0;
+  return (int64_t)bn_ws_bytes(n, C);
+}
+
+extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64_t C,
+                                   const float* weight, const float* bias,
+                                   float* running_mean, float* running_var,
+                                   int64_t* num_batches_tracked, float momentum,
+                                   float eps, int relu, float* y, int64_t ldy,
+                                   float* save_mean, float* save_invstd,
+                                   void* workspace, int64_t workspace_bytes,
+                                   void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 24) && ldx >= C && ldy >= C,
+                "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
+  HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                "bn_fwd_train: running_mean/var must both be given or both NULL");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_fwd_train: workspace too small");
+  const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
+  BnLayout L = bn_layout(n, C, vec);
+  BnWs w = carve(workspace, n, C);
+  StatsArgs s{};
+  s.x = x;
+  s.ldx = ldx;
+  s.n = n;
+  s.C = (int)C;
+  s.tpr = L.tpr;
+  s.rp = L.rp;
+  s.tiles = L.tiles;
+  s.parts = L.parts;
+  s.rows_per_part = L.rows_per_part;
+  s.part = w.part;
+  s.count = w.count;
+  s.weight = weight;
+  s.bias = bias;
+  s.running_mean = running_mean;
+  s.running_var = running_var;
+  s.nbt = num_batches_tracked;
+  s.momentum = momentum;
+  s.eps = eps;
+  s.save_mean = save_mean;
+  s.save_invstd = save_invstd;
+  hipStream_t st = as_stream(stream);
+  dim3 g1(L.parts, L.tiles);
+  if (vec)
+    k_bn_stats<4><<<g1, kThreads, 0, st>>>(s);
+  else
+    k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
+  HLH_CHECK_LAUNCH();
+  ApplyArgs p{x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
+              L.tpr, L.rp};
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  if (vec)
+    k_bn_apply<4><<<g2, kThreads, 0, st>>>(p);
+  else
+    k_bn_apply<1><<<g2, kThreads, 0, st>>>(p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
+                                   int64_t ldy, const float* dy, int64_t lddy,
+                                   int64_t n, int64_t C, const float* weight,
+                                   const float* save_mean, const float* save_invstd,
+                                   float* dx, int64_t lddx, float* dweight,
+                                   float* dbias, void* workspace,
+                                   int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && lddx >= C && (!y || ldy >= C),
+                "bn_bwd_train: bad sizes");
+  HLH_CHECK_ARG(x && dy && dx && save_mean && save_invstd, "bn_bwd_train: NULL pointer");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_bwd_train: workspace too small");
+  const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
+  BnLayout L = bn_layout(n, C, vec);
+  BnWs w = carve(workspace, n, C);
+  StatsArgs s{};
+  s.x = x;
+  s.ldx = ldx;
+  s.y = y;
+  s.ldy = ldy;
+  s.dy = dy;
+  s.lddy = lddy;
+  s.n = n;
+  s.C = (int)C;
+  s.tpr = L.tpr;
+  s.rp = L.rp;
+  s.tiles = L.tiles;
+  s.parts = L.parts;
+  s.rows_per_part = L.rows_per_part;
+  s.part = w.part;
+  s.count = w.count;
+  s.weight = weight;
+  s.save_mean = const_cast<float*>(save_mean);
+  s.save_invstd = const_cast<float*>(save_invstd);
+  s.coef = w.coef;
+  s.dweight = dweight;
+  s.dbias = dbias;
+  hipStream_t st = as_stream(stream);
+  dim3 g1(L.parts, L.tiles);
+  if (vec)
+    k_bn_bwd_reduce<4><<<g1, kThreads, 0, st>>>(s);
+  else
+    k_bn_bwd_reduce<1><<<g1, kThreads, 0, st>>>(s);
+  HLH_CHECK_LAUNCH();
+  BwdApplyArgs p{x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, L.tpr, L.rp};
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  if (vec)
+    k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);
+  else
+    k_bn_bwd_apply<1><<<g2, kThreads, 0, st>>>(p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}

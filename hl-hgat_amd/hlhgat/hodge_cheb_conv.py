@@ -24,7 +24,7 @@ from torch.nn import Dropout, Parameter
 
 from . import ops
 from .hodge_dataset import BoundaryOperator, adj2par1, boundary_from_sparse, degree
-from .nn import BatchNorm, Linear, Sequential
+from .nn import BatchNorm, Linear, Sequential, run_sequential
 
 __all__ = ["HodgeLaguerreConv", "HodgeChebConv", "NodeEdgeInt", "MSI", "HL_filter", "SAPool",
            "HodgeLaguerreFastConv"]
@@ -111,18 +111,6 @@ def _as_boundary(par, n_nodes: int, n_edges: int) -> BoundaryOperator:
     raise TypeError("NodeEdgeInt: par must come from adj2par1")
 
 
-def _run_mlp(seq: nn.Sequential, blocks) -> Tensor:
-    """WV_* = Linear(2d,dl)->BN->ReLU->Linear(dl,dv)->BN->ReLU with the first
-    Linear consuming the concatenation as separate blocks."""
-    h = None
-    for i, m in enumerate(seq):
-        if isinstance(m, nn.Linear):
-            h = ops.linear_blocks(blocks if h is None else [h], m.weight, m.bias)
-        else:
-            h = m(h)
-    return h
-
-
 class NodeEdgeInt(nn.Module):
     """Node<->edge interaction through the boundary operator
     (lib/Hodge_Cheb_Conv.py:255-309)."""
@@ -177,8 +165,8 @@ class NodeEdgeInt(nn.Module):
             a_s = ops.att_score(qc_s, kq_s[:, dk:], kq_s[:, :dk], 1 - self.lambda_Edge,
                                 self.lambda_Edge, sq, code)
             return a_t, a_s
-        x_t1 = _run_mlp(self.WV_Node, [x_s2t, x_t])
-        x_s1 = _run_mlp(self.WV_Edge, [x_t2s, x_s])
+        x_t1 = run_sequential(self.WV_Node, [x_s2t, x_t])
+        x_s1 = run_sequential(self.WV_Edge, [x_t2s, x_s])
         return x_t1, x_s1
 
 

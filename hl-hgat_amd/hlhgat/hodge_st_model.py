@@ -13,7 +13,7 @@ from torch.nn import Dropout, Linear
 from . import ops
 from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt
 from .hodge_dataset import adj2par1, degree
-from .nn import BatchNorm, Sequential
+from .nn import BatchNorm, Sequential, run_sequential
 
 __all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "segment_ptr", "mean_pool_sorted"]
 
@@ -95,7 +95,8 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         x = torch.cat((mean_pool_sorted(x_s, data.num_edge1),
                        mean_pool_sorted(x_t, data.num_node1)), -1)
         for i, _ in enumerate(self.mlp_channels):
-            x = getattr(self, "mlp%d" % i)(x)
+            x = run_sequential(getattr(self, "mlp%d" % i), [x])
+        y = ops.linear_blocks([x], self.out.weight, self.out.bias)
         if if_final_layer:
-            return x, self.out(x)
-        return self.out(x)
+            return x, y
+        return y

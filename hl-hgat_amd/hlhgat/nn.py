@@ -78,7 +78,8 @@ class BatchNorm(tnn.Module):
         self.module.reset_parameters()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.module(x)
+        from .ops import batch_norm_act
+        return batch_norm_act(x, self.module, relu=False)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels})"
@@ -120,6 +121,15 @@ class Sequential(tnn.Module):
             self._routes.append((ins, outs))
             prev_out = outs
         self._n = len(modules)
+        # BatchNorm immediately followed by ReLU on the same variable runs as
+        # one fused HIP BN+ReLU op (same result as the two modules in turn)
+        self._fuse_relu = [False] * self._n
+        for i in range(self._n - 1):
+            a, b = getattr(self, f"module_{i}"), getattr(self, f"module_{i + 1}")
+            ra, rb = self._routes[i], self._routes[i + 1]
+            if (isinstance(a, BatchNorm) and isinstance(b, tnn.ReLU) and len(ra[1]) == 1
+                    and rb[0] == ra[1] and rb[1] == ra[1]):
+                self._fuse_relu[i] = True
 
     def forward(self, *args):
         if len(args) != len(self.input_args):
@@ -127,9 +137,18 @@ class Sequential(tnn.Module):
                             f"({', '.join(self.input_args)}), got {len(args)}")
         env = dict(zip(self.input_args, args))
         out = None
+        skip = False
         for i, (ins, outs) in enumerate(self._routes):
+            if skip:
+                skip = False
+                continue
             fn = getattr(self, f"module_{i}")
-            out = fn(*[env[n] for n in ins])
+            if self._fuse_relu[i]:
+                from .ops import batch_norm_act
+                out = batch_norm_act(env[ins[0]], fn.module, relu=True)
+                skip = True
+            else:
+                out = fn(*[env[n] for n in ins])
             if len(outs) == 1:
                 env[outs[0]] = out
             else:
@@ -142,6 +161,32 @@ class Sequential(tnn.Module):
 
     def __getitem__(self, i: int):
         return getattr(self, f"module_{i}")
+
+
+def run_sequential(seq: tnn.Sequential, blocks) -> torch.Tensor:
+    """Run an nn.Sequential of Linear / BatchNorm1d / ReLU / Dropout modules on
+    the HIP ops: the first Linear consumes ``blocks`` (a list of tensors whose
+    concatenation is its input, e.g. cat[x_s2t, x_t] of NodeEdgeInt,
+    lib/Hodge_Cheb_Conv.py:307-308) without materialising the cat, and each
+    BatchNorm1d followed by ReLU runs as one fused op."""
+    from .ops import batch_norm_act, linear_blocks
+    mods = list(seq)
+    h = None
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, tnn.Linear):
+            h = linear_blocks(blocks if h is None else [h], m.weight, m.bias)
+        elif isinstance(m, tnn.BatchNorm1d):
+            relu = i + 1 < len(mods) and isinstance(mods[i + 1], tnn.ReLU)
+            h = batch_norm_act(h, m, relu=relu)
+            i += relu
+        elif isinstance(m, tnn.Dropout) and (m.p == 0.0 or not m.training):
+            pass
+        else:
+            h = m(h if h is not None else torch.cat(list(blocks), -1))
+        i += 1
+    return h
 
 
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int = None) -> torch.Tensor:

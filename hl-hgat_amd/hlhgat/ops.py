@@ -621,6 +621,87 @@ def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,
 
 
 # ----------------------------------------------------------------------------
+# BatchNorm1d (training statistics) + optional fused ReLU
+# ----------------------------------------------------------------------------
+_BN_WS = {}
+
+
+def _bn_workspace(device: torch.device, n: int, C: int) -> torch.Tensor:
+    """Persistent zero-initialised scratch per device (the kernels leave their
+    arrival counters at zero, so it is reused by every BN launch on the
+    stream)."""
+    need = int(LIB.hlhgat_bn_workspace_bytes(n, C))
+    key = (device.type, device.index)
+    ws = _BN_WS.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(max(need, 1 << 20), dtype=torch.uint8, device=device)
+        _BN_WS[key] = ws
+    return ws
+
+
+class _BatchNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
+        n, C = x.shape
+        y = torch.empty(n, C, device=x.device, dtype=x.dtype)
+        mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        invstd = torch.empty(C, device=x.device, dtype=torch.float32)
+        ws = _bn_workspace(x.device, n, C)
+        check(LIB.hlhgat_bn_fwd_train(x.data_ptr(), _ld(x), n, C, _ptr(weight), _ptr(bias),
+                                      _ptr(running_mean), _ptr(running_var), _ptr(nbt),
+                                      momentum, eps, int(relu), y.data_ptr(), _ld(y),
+                                      mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), _stream(x)), "bn_fwd_train")
+        ctx.relu = relu
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        dy = _rows2d(dy, "grad")
+        n, C = x.shape
+        dx = torch.empty(n, C, device=x.device, dtype=x.dtype)
+        need_w = weight is not None and ctx.needs_input_grad[1]
+        need_b = ctx.needs_input_grad[2]
+        dw = torch.empty(C, device=x.device, dtype=x.dtype) if need_w else None
+        db = torch.empty(C, device=x.device, dtype=x.dtype) if need_b else None
+        ws = _bn_workspace(x.device, n, C)
+        check(LIB.hlhgat_bn_bwd_train(x.data_ptr(), _ld(x), _ptr(y), _ld(y) if y is not None else 0,
+                                      dy.data_ptr(), _ld(dy), n, C, _ptr(weight), mean.data_ptr(),
+                                      invstd.data_ptr(), dx.data_ptr(), _ld(dx), _ptr(dw),
+                                      _ptr(db), ws.data_ptr(), ws.numel(), _stream(x)),
+              "bn_bwd_train")
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False) -> torch.Tensor:
+    """bn(x) followed by ReLU when ``relu``; training mode (or no running
+    stats) uses the HIP batch-statistics kernels, eval mode the running
+    statistics (ATen's fused eval kernel)."""
+    _req_dev(x, "x")
+    if x.dim() != 2:
+        raise RuntimeError("hlhgat: batch_norm_act expects [N, C] input")
+    use_batch = bn.training or not bn.track_running_stats
+    if not use_batch:
+        y = torch.nn.functional.batch_norm(x, bn.running_mean, bn.running_var, bn.weight,
+                                           bn.bias, False, 0.0, bn.eps)
+        return torch.relu(y) if relu else y
+    if x.size(0) < 2 and bn.training:
+        raise ValueError(f"Expected more than 1 value per channel when training, got input "
+                         f"size {tuple(x.shape)}")
+    track = bn.training and bn.track_running_stats and bn.running_mean is not None
+    if track and bn.momentum is None:
+        momentum = 1.0 / float(bn.num_batches_tracked.item() + 1)
+    else:
+        momentum = float(bn.momentum) if bn.momentum is not None else 0.0
+    return _BatchNormActFn.apply(
+        _rows2d(x, "x"), bn.weight, bn.bias, bn.running_mean if track else None,
+        bn.running_var if track else None, bn.num_batches_tracked if track else None,
+        momentum, float(bn.eps), bool(relu))
+
+
+# ----------------------------------------------------------------------------
 # live kernel timing (bench.py)
 # ----------------------------------------------------------------------------
 def prof_enable(kernel_class: int, enable: bool = True) -> None:

@@ -217,6 +217,32 @@ int hlhgat_segment_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
                             int64_t n_seg, const float* dout, int64_t ldo,
                             int64_t d, float* dx, int64_t ldx, void* stream);
 
+/* ---- BatchNorm1d (training) + optional fused ReLU ---------------------- */
+/* gnn.BatchNorm / nn.BatchNorm1d in training mode over x [n][C] (batch
+ * statistics, biased variance for normalisation, unbiased for the running
+ * update, momentum as torch), followed by ReLU when relu != 0 — the
+ * conv -> BatchNorm -> ReLU tail of every HL block (lib/Hodge_ST_Model.py:
+ * 556-566) and of NodeEdgeInt's WV_* MLPs (lib/Hodge_Cheb_Conv.py:276-289).
+ * weight/bias may be NULL (affine=False); running stats may be NULL.
+ * The workspace must be zero-filled before its first use and must not be
+ * shared by launches that run concurrently; the kernels leave it reusable. */
+int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C);
+int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64_t C,
+                        const float* weight, const float* bias,
+                        float* running_mean, float* running_var,
+                        int64_t* num_batches_tracked, float momentum, float eps,
+                        int relu, float* y, int64_t ldy, float* save_mean,
+                        float* save_invstd, void* workspace,
+                        int64_t workspace_bytes, void* stream);
+/* Backward; y (the forward output) supplies the ReLU mask, NULL if no ReLU.
+ * dweight/dbias may be NULL. */
+int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                        const float* dy, int64_t lddy, int64_t n, int64_t C,
+                        const float* weight, const float* save_mean,
+                        const float* save_invstd, float* dx, int64_t lddx,
+                        float* dweight, float* dbias, void* workspace,
+                        int64_t workspace_bytes, void* stream);
+
 /* ---- live kernel timing ------------------------------------------------ */
 #define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */
 #define HLHGAT_PROF_PROJ 1 /* MFMA projection forward */

@@ -338,3 +338,43 @@ def test_zinc_model_cfg2_vs_oracle(cuda):
     rp = dict(ref.named_parameters())
     for k, p in m.named_parameters():
         close(p.grad.cpu(), rp[k].grad, 1e-3, "grad " + k)
+
+
+# ---------------------------------------------------------------------------
+# fused BatchNorm1d (+ReLU), training statistics
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("n,C,relu", [(2, 1, False), (23000, 64, True), (1000, 256, True),
+                                      (4097, 18, False), (777, 130, True), (50, 384, False)])
+def test_batch_norm_act_vs_torch(cuda, n, C, relu):
+    from hlhgat import ops
+    g = torch.Generator().manual_seed(n + C)
+    x = torch.randn(n, C, generator=g) * 3 + 1.5
+    bn_ref = torch.nn.BatchNorm1d(C)
+    with torch.no_grad():
+        bn_ref.weight.uniform_(0.5, 1.5)
+        bn_ref.bias.uniform_(-0.5, 0.5)
+        bn_ref.running_mean.uniform_(-1, 1)
+        bn_ref.running_var.uniform_(0.5, 2)
+    bn = torch.nn.BatchNorm1d(C).to(cuda)
+    bn.load_state_dict(bn_ref.state_dict())
+    bn.train()
+    bn_ref.train()
+    xr = x.clone().requires_grad_(True)
+    yr = bn_ref(xr)
+    if relu:
+        yr = torch.relu(yr)
+    xd = dev(x).requires_grad_(True)
+    y = ops.batch_norm_act(xd, bn, relu=relu)
+    close(y.detach().cpu(), yr.detach(), 1e-5, "y")
+    Rg = torch.randn(n, C, generator=g)
+    (yr * Rg).sum().backward()
+    (y * dev(Rg)).sum().backward()
+    close(xd.grad.cpu(), xr.grad, 1e-4, "dx")
+    close(bn.weight.grad.cpu(), bn_ref.weight.grad, 1e-4, "dw")
+    close(bn.bias.grad.cpu(), bn_ref.bias.grad, 1e-4, "db")
+    close(bn.running_mean.cpu(), bn_ref.running_mean, 1e-5, "running_mean")
+    close(bn.running_var.cpu(), bn_ref.running_var, 1e-5, "running_var")
+    assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
+    # a second call reuses the (self-resetting) workspace counters
+    y2 = ops.batch_norm_act(xd.detach(), bn, relu=relu)
+    close(y2.cpu(), y.detach().cpu(), 1e-6, "repeat")
