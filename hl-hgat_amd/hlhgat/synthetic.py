@@ -108,6 +108,54 @@ def zinc_like_graph(seed: int, keig: int = 15) -> PairData:
     return g
 
 
+def tsp_like_graph(seed: int, n: int = 10000, k: int = 9) -> PairData:
+    """TSP-like simplex graph (BASELINE config 5): n uniform points in [0,1]^2,
+    symmetric k-NN edges (i<j), L0 = 2 B1 B1^T / lmax and L1 = 2 B1^T B1 / lmax
+    built SPARSE (a dense E x E L1 would be ~10 GB at n = 10k), lmax of L0 by
+    Lanczos; COO row-major sorted like dense_to_sparse.  Features: node
+    coordinates (2), edge length + mask (2) as in main_TSP (:99-176)."""
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import eigsh
+    from scipy.spatial import cKDTree
+    rng = np.random.default_rng(seed)
+    pts = rng.random((n, 2))
+    _, nbr = cKDTree(pts).query(pts, k=k + 1)
+    a = np.repeat(np.arange(n), k)
+    b = nbr[:, 1:].reshape(-1)
+    i, j = np.minimum(a, b), np.maximum(a, b)
+    key = np.unique(i.astype(np.int64) * n + j)
+    ei = np.stack([key // n, key % n])
+    E = ei.shape[1]
+    B = sp.csr_matrix((np.concatenate([-np.ones(E), np.ones(E)]).astype(np.float32),
+                       (np.concatenate([ei[0], ei[1]]), np.concatenate([np.arange(E)] * 2))),
+                      shape=(n, E))
+    L0 = (B @ B.T).tocsr()
+    lmax = float(eigsh(L0.astype(np.float64), k=1, which="LA", return_eigenvectors=False)[0])
+    L0 = (2.0 * L0 / lmax).astype(np.float32).tocoo()
+    L1 = (2.0 * (B.T @ B) / lmax).astype(np.float32).tocoo()
+
+    def coo(M):
+        M.sum_duplicates()
+        o = np.lexsort((M.col, M.row))
+        keep = M.data[o] != 0
+        r, c, v = M.row[o][keep], M.col[o][keep], M.data[o][keep]
+        return torch.from_numpy(np.stack([r, c]).astype(np.int64)), torch.from_numpy(v)
+
+    eit, ewt = coo(L0)
+    eis, ews = coo(L1)
+    length = np.linalg.norm(pts[ei[0]] - pts[ei[1]], axis=1).astype(np.float32)
+    x_s = torch.from_numpy(np.stack([length, np.ones(E, np.float32)], 1))
+    g = PairData(x_s=x_s, edge_index_s=eis, edge_weight_s=ews,
+                 x_t=torch.from_numpy(pts.astype(np.float32)), edge_index_t=eit,
+                 edge_weight_t=ewt, y=torch.zeros(E))
+    g.edge_index = torch.from_numpy(ei)
+    g.num_node1 = n
+    g.num_edge1 = E
+    g.num_nodes = n
+    g._hodge_sorted = True
+    return g
+
+
 def zinc_like_batch(n_graphs: int, seed: int = 0, keig: int = 15,
                     check_hodge: bool = False):
     graphs: List[PairData] = [zinc_like_graph(seed * 1_000_003 + i, keig) for i in range(n_graphs)]
