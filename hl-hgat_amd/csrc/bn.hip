@@ -25,6 +25,8 @@ using namespace hlhgat;
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kMaxParts = 256;
+constexpr int kMaxTiles = 1024;
 
 struct BnLayout {
   int v;       // floats per thread (4 or 1)
@@ -41,49 +43,46 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   L.v = vec ? 4 : 1;
   int lanes = (int)ceil_div(C, L.v);
   L.tpr = next_pow2(lanes);
-  if (L.tpr > kThreads) L.tpr = kThreads;
+  if (L.tpr > kThreads / L.v) L.tpr = kThreads / L.v;  // tile_c <= kThreads
   L.rp = kThreads / L.tpr;
   L.tile_c = L.tpr * L.v;
   L.tiles = (int)ceil_div(C, L.tile_c);
-  // ~512 workgroups in all, each partition at least 4 passes of rows
-  int64_t parts = ceil_div(512, L.tiles);
-  int64_t max_parts = ceil_div(n, (int64_t)L.rp * 4);
+  // ~256 workgroups in all; each partition at least 2 passes of rows; the
+  // last arriver then reduces <= kMaxParts partials with all 256 threads
+  int64_t parts = ceil_div(256, L.tiles);
+  int64_t max_parts = ceil_div(n, (int64_t)L.rp * 2);
   if (parts > max_parts) parts = max_parts;
   if (parts < 1) parts = 1;
-  if (parts > 1024) parts = 1024;
+  if (parts > kMaxParts) parts = kMaxParts;
   L.rows_per_part = ceil_div(n, parts);
   L.parts = (int)ceil_div(n > 0 ? n : 1, L.rows_per_part);
   return L;
 }
 
 struct BnWs {
+  unsigned* count;   // [kMaxTiles] at offset 0 (zero between launches)
   double* part;      // [parts][C][2]
-  unsigned* count;   // [tiles] (zero between launches)
   float* coef;       // [3][C] (bwd: a, b, c)
 };
 
 size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 
+// Counters live at a FIXED offset so a launch with a different (n, C) never
+// reads another launch's partials as a counter.
 size_t bn_ws_bytes(int64_t n, int64_t C) {
-  BnLayout L = bn_layout(n, C, false);  // scalar layout has the most parts
-  BnLayout L4 = bn_layout(n, C, true);
-  int64_t parts = L.parts > L4.parts ? L.parts : L4.parts;
-  int64_t tiles = L.tiles > L4.tiles ? L.tiles : L4.tiles;
-  return align_up(sizeof(double) * 2 * parts * C) + align_up(sizeof(unsigned) * tiles) +
+  (void)n;
+  return align_up(sizeof(unsigned) * kMaxTiles) + align_up(sizeof(double) * 2 * kMaxParts * C) +
          align_up(sizeof(float) * 3 * C);
 }
 
 BnWs carve(void* ws, int64_t n, int64_t C) {
-  BnLayout L = bn_layout(n, C, false);
-  BnLayout L4 = bn_layout(n, C, true);
-  int64_t parts = L.parts > L4.parts ? L.parts : L4.parts;
-  int64_t tiles = L.tiles > L4.tiles ? L.tiles : L4.tiles;
+  (void)n;
   char* p = (char*)ws;
   BnWs w;
-  w.part = (double*)p;
-  p += align_up(sizeof(double) * 2 * parts * C);
   w.count = (unsigned*)p;
-  p += align_up(sizeof(unsigned) * tiles);
+  p += align_up(sizeof(unsigned) * kMaxTiles);
+  w.part = (double*)p;
+  p += align_up(sizeof(double) * 2 * kMaxParts * C);
   w.coef = (float*)p;
   return w;
 }
@@ -166,6 +165,40 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
   }
 }
 
+// Final reduction in the last-arriving workgroup: all 256 threads take part
+// (column t % tile_c, partial group t / tile_c, 4 independent accumulators),
+// groups combined in fixed order through LDS -> deterministic.
+__device__ __forceinline__ void reduce_parts(const StatsArgs& a, int c0, int tile_c,
+                                             double* out0, double* out1) {
+  __shared__ double fin[2][kThreads];
+  const int groups = kThreads / tile_c > 0 ? kThreads / tile_c : 1;
+  const int t = threadIdx.x % tile_c;
+  const int grp = threadIdx.x / tile_c;
+  const int c = c0 + t;
+  double u0[4] = {0.0, 0.0, 0.0, 0.0}, u1[4] = {0.0, 0.0, 0.0, 0.0};
+  if (grp < groups && c < a.C) {
+    int i = 0;
+    for (int p = grp; p < a.parts; p += groups, ++i) {
+      const double* src = a.part + ((int64_t)p * a.C + c) * 2;
+      u0[i & 3] += src[0];
+      u1[i & 3] += src[1];
+    }
+  }
+  fin[0][threadIdx.x] = (u0[0] + u0[1]) + (u0[2] + u0[3]);
+  fin[1][threadIdx.x] = (u1[0] + u1[1]) + (u1[2] + u1[3]);
+  __syncthreads();
+  if (threadIdx.x < tile_c) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int g = 0; g < groups; ++g) {
+      s0 += fin[0][g * tile_c + threadIdx.x];
+      s1 += fin[1][g * tile_c + threadIdx.x];
+    }
+    out0[threadIdx.x] = s0;
+    out1[threadIdx.x] = s1;
+  }
+  __syncthreads();
+}
+
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   using vt = typename VecT<V>::type;
@@ -193,15 +226,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   write_partials<V>(s0, s1, a, c0);
   if (!arrive_last(a.count + blockIdx.y, (unsigned)a.parts)) return;
   // last arriver of this column tile: finalise its columns
-  for (int t = threadIdx.x; t < a.tpr * V; t += kThreads) {
+  __shared__ double sum0[kThreads], sum1[kThreads];
+  const int tile_c = a.tpr * V;
+  reduce_parts(a, c0, tile_c, sum0, sum1);
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
-    double u0 = 0.0, u1 = 0.0;
-    for (int p = 0; p < a.parts; ++p) {
-      const double* src = a.part + ((int64_t)p * a.C + cc) * 2;
-      u0 += src[0];
-      u1 += src[1];
-    }
+    const double u0 = sum0[t], u1 = sum1[t];
     const double nn = (double)a.n;
     const double mean = u0 / nn;
     double var = u1 / nn - mean * mean;
@@ -294,15 +325,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
   }
   write_partials<V>(s0, s1, a, c0);
   if (!arrive_last(a.count + blockIdx.y, (unsigned)a.parts)) return;
-  for (int t = threadIdx.x; t < a.tpr * V; t += kThreads) {
+  __shared__ double sum0[kThreads], sum1[kThreads];
+  const int tile_c = a.tpr * V;
+  reduce_parts(a, c0, tile_c, sum0, sum1);
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
-    double sg = 0.0, sgx = 0.0;
-    for (int p = 0; p < a.parts; ++p) {
-      const double* src = a.part + ((int64_t)p * a.C + cc) * 2;
-      sg += src[0];
-      sgx += src[1];
-    }
+    const double sg = sum0[t], sgx = sum1[t];
     const double is = (double)a.save_invstd[cc];
     const double w = a.weight ? (double)a.weight[cc] : 1.0;
     const double nn = (double)a.n;
@@ -395,7 +424,7 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64
                                    float* save_mean, float* save_invstd,
                                    void* workspace, int64_t workspace_bytes,
                                    void* stream) {
-  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 24) && ldx >= C && ldy >= C,
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
                 "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
   HLH_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
   HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),

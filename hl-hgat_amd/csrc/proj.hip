@@ -152,6 +152,142 @@ __global__ __launch_bounds__(256) void k_proj_fwd(FwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// forward, LDS-staged weights (vector path: every kb % 4 == 0, 16-B aligned)
+//
+// Workgroup = 4 waves x 16 rows = 64 rows, TN*16 output columns.  The weight
+// chunk W_b[n_tile][k0:k0+64] is loaded ONCE per workgroup into LDS (double
+// buffered, rows padded to 68 floats so the 16 rows a ds_read_b128 lane group
+// touches fall in 16 distinct 16-B bank slots) and shared by the 4 waves;
+// each lane streams its A row chunk straight into registers one chunk ahead.
+// ---------------------------------------------------------------------------
+constexpr int KC = 64;
+constexpr int KCP = KC + 4;
+
+template <int TN>
+struct WStage {
+  float4 v[TN];
+};
+
+// cooperative load of W rows [n_base, n_base+TN*16) x k [k0, k0+64) of block b
+template <int TN>
+__device__ __forceinline__ void load_w_chunk(const FwdArgs& a, int b, int k0, int n_base,
+                                             WStage<TN>& st) {
+  const float* W = a.W[b];
+  const int kb = a.kb[b];
+  const int64_t ldw = a.ldw[b];
+#pragma unroll
+  for (int u = 0; u < TN; ++u) {
+    const int idx = threadIdx.x + 256 * u;  // TN*16 rows x 16 float4
+    const int r = idx >> 4, c4 = idx & 15;
+    const int n = n_base + r, k = k0 + 4 * c4;
+    if (n < a.N && k < kb)
+      st.v[u] = *reinterpret_cast<const float4*>(W + (int64_t)n * ldw + k);
+    else
+      st.v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int TN>
+__device__ __forceinline__ void store_w_chunk(float (*lds)[KCP], const WStage<TN>& st) {
+#pragma unroll
+  for (int u = 0; u < TN; ++u) {
+    const int idx = threadIdx.x + 256 * u;
+    const int r = idx >> 4, c4 = idx & 15;
+    *reinterpret_cast<float4*>(&lds[r][4 * c4]) = st.v[u];
+  }
+}
+
+__device__ __forceinline__ void load_a_chunk(const float* arow, bool valid, int k0, int kb,
+                                             int q, float4 (&o)[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = k0 + 16 * s + 4 * q;
+    if (valid && k < kb)
+      o[s] = *reinterpret_cast<const float4*>(arow + k);
+    else
+      o[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int TN>
+__global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
+  __shared__ float wl[2][TN * 16][KCP];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  const int64_t m_base = ((int64_t)blockIdx.x * 4 + wave) * 16;
+  const int n_base = blockIdx.y * (TN * 16);
+  const int64_t row = m_base + i;
+  const bool aval = row < a.M;
+
+  floatx4 acc[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  int b = 0, k0 = 0;
+  WStage<TN> wst;
+  float4 ac[4];
+  load_w_chunk<TN>(a, b, k0, n_base, wst);
+  load_a_chunk(a.A[b] + (aval ? row : 0) * a.lda[b], aval, k0, a.kb[b], q, ac);
+  store_w_chunk<TN>(wl[0], wst);
+  __syncthreads();
+  int buf = 0;
+  while (b < a.nb) {
+    int nbk = b, nk = k0 + KC;
+    if (nk >= a.kb[b]) {
+      nbk = b + 1;
+      nk = 0;
+    }
+    const bool has_next = nbk < a.nb;
+    float4 an[4];
+    if (has_next) {
+      load_w_chunk<TN>(a, nbk, nk, n_base, wst);
+      load_a_chunk(a.A[nbk] + (aval ? row : 0) * a.lda[nbk], aval, nk, a.kb[nbk], q, an);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float4 bf[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][16 * s + 4 * q]);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        acc[tn] = mfma16(ac[s].x, bf[tn].x, acc[tn]);
+        acc[tn] = mfma16(ac[s].y, bf[tn].y, acc[tn]);
+        acc[tn] = mfma16(ac[s].z, bf[tn].z, acc[tn]);
+        acc[tn] = mfma16(ac[s].w, bf[tn].w, acc[tn]);
+      }
+    }
+    if (has_next) {
+      store_w_chunk<TN>(wl[buf ^ 1], wst);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) ac[s] = an[s];
+    }
+    __syncthreads();
+    buf ^= 1;
+    b = nbk;
+    k0 = nk;
+  }
+
+  if (m_base >= a.M) return;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = n_base + tn * 16 + i;
+    if (col >= a.N) continue;
+    const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t rr = m_base + 4 * q + r;
+      if (rr >= a.M) continue;
+      float v = acc[tn][r];
+      if (a.bias) v = v + bv;
+      float* dst = a.C + rr * a.ldc + col;
+      *dst = a.accumulate ? *dst + v : v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // data gradient: dA_b = dC W_b   (reduction over N)
 // ---------------------------------------------------------------------------
 struct BwdDataArgs {
@@ -241,6 +377,109 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
   }
 }
 
+// Vector path of the data gradient: W_b[n0:n0+64][c_tile] is staged in LDS
+// TRANSPOSED (wl[c][n], rows padded) so each lane's B fragment (4 consecutive
+// n of one column) is one ds_read_b128; dC rows stream into registers one
+// 64-wide n chunk ahead.
+template <int TN>
+__global__ __launch_bounds__(256) void k_proj_bwd_data_lds(BwdDataArgs a) {
+  __shared__ float wl[2][TN * 16][KCP];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  const int64_t m_base = ((int64_t)blockIdx.x * 4 + wave) * 16;
+  int b = 0;
+  while (b + 1 < a.nb && (int)blockIdx.y >= a.tile_start[b + 1]) ++b;
+  const int kb = a.kb[b];
+  const int c_base = ((int)blockIdx.y - a.tile_start[b]) * (TN * 16);
+  const float* __restrict__ W = a.W[b];
+  const int64_t ldw = a.ldw[b];
+  const int64_t row = m_base + i;
+  const bool gval = row < a.M;
+  const float* grow = a.G + (gval ? row : 0) * a.ldg;
+
+  // staging: TN*16 columns x 64 n = TN*256 float4 over 256 threads; thread
+  // loads W[n][c4*4 .. +3] (16 float4 per n row) and scatters 4 floats.
+  auto load_w = [&](int n0, float4 (&st)[TN]) {
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int nl = idx / (TN * 4), c4 = idx % (TN * 4);
+      const int n = n0 + nl, c = c_base + 4 * c4;
+      if (n < a.N && c < kb)
+        st[u] = *reinterpret_cast<const float4*>(W + (int64_t)n * ldw + c);
+      else
+        st[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_w = [&](float (*lds)[KCP], const float4 (&st)[TN]) {
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int nl = idx / (TN * 4), c4 = idx % (TN * 4);
+      lds[4 * c4 + 0][nl] = st[u].x;
+      lds[4 * c4 + 1][nl] = st[u].y;
+      lds[4 * c4 + 2][nl] = st[u].z;
+      lds[4 * c4 + 3][nl] = st[u].w;
+    }
+  };
+
+  floatx4 acc[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float4 wst[TN], gc[4];
+  load_w(0, wst);
+  load_a_chunk(grow, gval, 0, a.N, q, gc);
+  store_w(wl[0], wst);
+  __syncthreads();
+  int buf = 0;
+  for (int n0 = 0; n0 < a.N; n0 += KC) {
+    const bool has_next = n0 + KC < a.N;
+    float4 gn[4];
+    if (has_next) {
+      load_w(n0 + KC, wst);
+      load_a_chunk(grow, gval, n0 + KC, a.N, q, gn);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float4 bf[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][16 * s + 4 * q]);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        acc[tn] = mfma16(gc[s].x, bf[tn].x, acc[tn]);
+        acc[tn] = mfma16(gc[s].y, bf[tn].y, acc[tn]);
+        acc[tn] = mfma16(gc[s].z, bf[tn].z, acc[tn]);
+        acc[tn] = mfma16(gc[s].w, bf[tn].w, acc[tn]);
+      }
+    }
+    if (has_next) {
+      store_w(wl[buf ^ 1], wst);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) gc[s] = gn[s];
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (m_base >= a.M) return;
+  float* __restrict__ O = a.O[b];
+  const int64_t ldo = a.ldo[b];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = c_base + tn * 16 + i;
+    if (col >= kb) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t rr = m_base + 4 * q + r;
+      if (rr >= a.M) continue;
+      float* dst = O + rr * ldo + col;
+      const float v = acc[tn][r];
+      *dst = a.accumulate ? *dst + v : v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // weight gradient: dW_b = dC^T A_b  (reduction over M, split over workgroups)
 // Each workgroup owns one (64 n x 64 k) output tile of one block and one slice
@@ -316,8 +555,8 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
     kval[tn] = kcol[tn] < kb;
   }
 
-  for (int64_t m0 = m_lo + wave * 16; m0 < m_hi; m0 += 64) {
-    float af[WT_TM][4], bf[WT_TN][4];
+  // operands of one 16-row chunk: lane (q, i) holds rows m0 + 4q + j (j=0..3)
+  auto load_chunk = [&](int64_t m0, float (&af)[WT_TM][4], float (&bf)[WT_TN][4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t m = m0 + 4 * q + j;
@@ -329,6 +568,14 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
 #pragma unroll
       for (int tn = 0; tn < WT_TN; ++tn) bf[tn][j] = (mv && kval[tn]) ? arow[kcol[tn]] : 0.f;
     }
+  };
+  float af[WT_TM][4], bf[WT_TN][4];
+  int64_t m0 = m_lo + wave * 16;
+  if (m0 < m_hi) load_chunk(m0, af, bf);
+  for (; m0 < m_hi; m0 += 64) {
+    float an[WT_TM][4], bn[WT_TN][4];
+    const bool has_next = m0 + 64 < m_hi;
+    if (has_next) load_chunk(m0 + 64, an, bn);  // prefetch the next chunk
     if (do_bias) {
 #pragma unroll
       for (int tm = 0; tm < WT_TM; ++tm)
@@ -341,6 +588,16 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
 #pragma unroll
         for (int tn = 0; tn < WT_TN; ++tn)
           acc[tm][tn] = mfma16(af[tm][j], bf[tn][j], acc[tm][tn]);
+    if (has_next) {
+#pragma unroll
+      for (int tm = 0; tm < WT_TM; ++tm)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) af[tm][j] = an[tm][j];
+#pragma unroll
+      for (int tn = 0; tn < WT_TN; ++tn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[tn][j] = bn[tn][j];
+    }
   }
 
   // cross-wave reduction (fixed order: wave 0 + 1 + 2 + 3)
@@ -397,28 +654,43 @@ struct ReduceArgs {
   int accumulate;
 };
 
+// 64 consecutive output elements per workgroup; the 4 waves sum interleaved
+// subsets of the splits (coalesced 256-B reads per split), then combine in
+// fixed order through LDS -> deterministic and fully parallel.
 __global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
   const int64_t total = a.elem_start[a.nb] + (a.bias_off >= 0 ? a.N : 0);
-  if (e >= total) return;
-  int64_t src;
-  float* dst;
-  if (e >= a.elem_start[a.nb]) {
-    const int64_t n = e - a.elem_start[a.nb];
-    src = a.bias_off + n;
-    dst = a.dbias + n;
-  } else {
-    int b = 0;
-    while (b + 1 < a.nb && e >= a.elem_start[b + 1]) ++b;
-    const int64_t loc = e - a.elem_start[b];
-    const int64_t n = loc / a.kb[b];
-    const int64_t k = loc % a.kb[b];
-    src = a.part_off[b] + loc;
-    dst = a.dW[b] + n * a.lddw[b] + k;
+  int64_t src = -1;
+  float* dst = nullptr;
+  if (e < total) {
+    if (e >= a.elem_start[a.nb]) {
+      const int64_t n = e - a.elem_start[a.nb];
+      src = a.bias_off + n;
+      dst = a.dbias + n;
+    } else {
+      int b = 0;
+      while (b + 1 < a.nb && e >= a.elem_start[b + 1]) ++b;
+      const int64_t loc = e - a.elem_start[b];
+      const int64_t n = loc / a.kb[b];
+      const int64_t k = loc % a.kb[b];
+      src = a.part_off[b] + loc;
+      dst = a.dW[b] + n * a.lddw[b] + k;
+    }
   }
-  float s = 0.f;
-  for (int sp = 0; sp < a.splits; ++sp) s = s + a.part[(int64_t)sp * a.part_stride + src];
-  *dst = a.accumulate ? *dst + s : s;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (src >= 0) {
+    int it = 0;
+    for (int sp = grp; sp < a.splits; sp += 4, ++it)
+      s[it & 3] = s[it & 3] + a.part[(int64_t)sp * a.part_stride + src];
+  }
+  red[grp][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (grp == 0 && dst) {
+    const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    *dst = a.accumulate ? *dst + v : v;
+  }
 }
 
 // --- planning ------------------------------------------------------------------
@@ -448,8 +720,8 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   if (with_bias) off += N;
   p.part_stride = off;
   p.tiles_total = p.tile_start[nb];
-  // aim for ~2048 workgroups, each slice >= 256 rows
-  int64_t splits = ceil_div(2048, p.tiles_total > 0 ? p.tiles_total : 1);
+  // aim for ~768 workgroups (3 per CU), each slice >= 256 rows
+  int64_t splits = ceil_div(768, p.tiles_total > 0 ? p.tiles_total : 1);
   int64_t max_splits = ceil_div(M, 256);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -507,18 +779,27 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   double bytes = 4.0 * (double)M * N;
   for (int b = 0; b < nblocks; ++b) bytes += 4.0 * (double)M * kb[b] + 4.0 * N * kb[b];
   ProfScope prof(HLHGAT_PROF_PROJ, s, bytes, flops);
-#define HLH_FWD(TM_, TN_)                                                       \
-  if (vec)                                                                      \
-    k_proj_fwd<TM_, TN_, true><<<grid, 256, 0, s>>>(a);                         \
-  else                                                                          \
-    k_proj_fwd<TM_, TN_, false><<<grid, 256, 0, s>>>(a);
-  if (tm == 1 && tn == 1) { HLH_FWD(1, 1) }
-  else if (tm == 1 && tn == 2) { HLH_FWD(1, 2) }
-  else if (tm == 1) { HLH_FWD(1, 4) }
-  else if (tn == 1) { HLH_FWD(2, 1) }
-  else if (tn == 2) { HLH_FWD(2, 2) }
-  else { HLH_FWD(2, 4) }
-#undef HLH_FWD
+  if (vec) {
+    dim3 g((unsigned)ceil_div(M, 64), (unsigned)ceil_div(N, tn * 16));
+    if (tn == 1)
+      k_proj_fwd_lds<1><<<g, 256, 0, s>>>(a);
+    else if (tn == 2)
+      k_proj_fwd_lds<2><<<g, 256, 0, s>>>(a);
+    else
+      k_proj_fwd_lds<4><<<g, 256, 0, s>>>(a);
+  } else if (tm == 1 && tn == 1) {
+    k_proj_fwd<1, 1, false><<<grid, 256, 0, s>>>(a);
+  } else if (tm == 1 && tn == 2) {
+    k_proj_fwd<1, 2, false><<<grid, 256, 0, s>>>(a);
+  } else if (tm == 1) {
+    k_proj_fwd<1, 4, false><<<grid, 256, 0, s>>>(a);
+  } else if (tn == 1) {
+    k_proj_fwd<2, 1, false><<<grid, 256, 0, s>>>(a);
+  } else if (tn == 2) {
+    k_proj_fwd<2, 2, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    k_proj_fwd<2, 4, false><<<grid, 256, 0, s>>>(a);
+  }
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -551,11 +832,13 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
     a.tile_start[b + 1] = a.tile_start[b] + (int)ceil_div(kb[b], TN * 16);
   }
   if (M == 0) return HLHGAT_OK;
-  const bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
+  bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
+  for (int b = 0; b < nblocks; ++b)
+    vec = vec && aligned16(W[b]) && (ldw[b] % 4) == 0 && (kb[b] % 4) == 0;
   hipStream_t s = as_stream(stream);
   dim3 grid((unsigned)ceil_div(M, 4 * 16), (unsigned)a.tile_start[nblocks]);
   if (vec)
-    k_proj_bwd_data<1, TN, true><<<grid, 256, 0, s>>>(a);
+    k_proj_bwd_data_lds<TN><<<grid, 256, 0, s>>>(a);
   else
     k_proj_bwd_data<1, TN, false><<<grid, 256, 0, s>>>(a);
   HLH_CHECK_LAUNCH();
@@ -635,7 +918,7 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   r.dbias = dbias;
   r.accumulate = accumulate;
   const int64_t total = r.elem_start[nblocks] + (dbias ? N : 0);
-  k_reduce_splits<<<(unsigned)ceil_div(total, 256), 256, 0, s>>>(r);
+  k_reduce_splits<<<(unsigned)ceil_div(total, 64), 256, 0, s>>>(r);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
