@@ -25,7 +25,7 @@ using namespace hlhgat;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxParts = 256;
+constexpr int kMaxParts = 128;
 constexpr int kMaxTiles = 1024;
 
 struct BnLayout {
@@ -47,9 +47,9 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   L.rp = kThreads / L.tpr;
   L.tile_c = L.tpr * L.v;
   L.tiles = (int)ceil_div(C, L.tile_c);
-  // ~256 workgroups in all; each partition at least 2 passes of rows; the
-  // last arriver then reduces <= kMaxParts partials with all 256 threads
-  int64_t parts = ceil_div(256, L.tiles);
+  // <= kMaxParts row partitions per column tile (fat partitions keep the
+  // last arriver's reduction to one batch of loads per thread)
+  int64_t parts = kMaxParts;
   int64_t max_parts = ceil_div(n, (int64_t)L.rp * 2);
   if (parts > max_parts) parts = max_parts;
   if (parts < 1) parts = 1;
@@ -175,17 +175,30 @@ __device__ __forceinline__ void reduce_parts(const StatsArgs& a, int c0, int til
   const int t = threadIdx.x % tile_c;
   const int grp = threadIdx.x / tile_c;
   const int c = c0 + t;
-  double u0[4] = {0.0, 0.0, 0.0, 0.0}, u1[4] = {0.0, 0.0, 0.0, 0.0};
+  const int per = (a.parts + groups - 1) / groups;
+  const int p0 = grp * per;
+  double u0 = 0.0, u1 = 0.0;
   if (grp < groups && c < a.C) {
-    int i = 0;
-    for (int p = grp; p < a.parts; p += groups, ++i) {
-      const double* src = a.part + ((int64_t)p * a.C + c) * 2;
-      u0[i & 3] += src[0];
-      u1[i & 3] += src[1];
+    // batches of 16 independent loads in flight per thread
+    for (int pb = 0; pb < per; pb += 16) {
+      double v0[16], v1[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int p = p0 + pb + u;
+        const bool ok = pb + u < per && p < a.parts;
+        const double* src = a.part + ((int64_t)(ok ? p : 0) * a.C + c) * 2;
+        v0[u] = ok ? src[0] : 0.0;
+        v1[u] = ok ? src[1] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        u0 += v0[u];
+        u1 += v1[u];
+      }
     }
   }
-  fin[0][threadIdx.x] = (u0[0] + u0[1]) + (u0[2] + u0[3]);
-  fin[1][threadIdx.x] = (u1[0] + u1[1]) + (u1[2] + u1[3]);
+  fin[0][threadIdx.x] = u0;
+  fin[1][threadIdx.x] = u1;
   __syncthreads();
   if (threadIdx.x < tile_c) {
     double s0 = 0.0, s1 = 0.0;
@@ -213,7 +226,21 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
 #pragma unroll
   for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
   if (c < a.C) {
-    for (int64_t r = r_lo + rg; r < r_hi; r += a.rp) {
+    int64_t r = r_lo + rg;
+    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows in flight
+      vt x4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x4[u] = vload<V>(a.x + (r + u * a.rp) * a.ldx + c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const double xd = (double)vget(x4[u], v);
+          s0[v] += xd;
+          s1[v] += xd * xd;
+        }
+    }
+    for (; r < r_hi; r += a.rp) {
       vt xv = vload<V>(a.x + r * a.ldx + c);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
@@ -279,6 +306,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
     s[v] = w * a.invstd[c + v];
     t[v] = b - a.mean[c + v] * s[v];
   }
+#pragma unroll 4
   for (int64_t r = (int64_t)blockIdx.x * a.rp + rg; r < a.n; r += (int64_t)gridDim.x * a.rp) {
     vt xv = vload<V>(a.x + r * a.ldx + c);
     vt o;
@@ -309,6 +337,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
     mu[v] = (c + v < a.C) ? a.save_mean[c + v] : 0.f;
   }
   if (c < a.C) {
+#pragma unroll 4
     for (int64_t r = r_lo + rg; r < r_hi; r += a.rp) {
       vt xv = vload<V>(a.x + r * a.ldx + c);
       vt gv = vload<V>(a.dy + r * a.lddy + c);
@@ -376,6 +405,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     B[v] = a.coef[a.C + c + v];
     Cc[v] = a.coef[2 * a.C + c + v];
   }
+#pragma unroll 4
   for (int64_t r = (int64_t)blockIdx.x * a.rp + rg; r < a.n; r += (int64_t)gridDim.x * a.rp) {
     vt xv = vload<V>(a.x + r * a.ldx + c);
     vt gv = vload<V>(a.dy + r * a.lddy + c);

@@ -106,6 +106,7 @@ def degree(index, num_nodes=None):
 
 def boundary_mix(x_t, x_s, par, D):
     """x_s2t, x_t2s of lib/Hodge_Cheb_Conv.py:294-295."""
+    par = par if par.dtype == x_s.dtype else par.to(x_s.dtype)  # (fp64 noise studies)
     x_s2t = (1 / D).view(-1, 1) * torch.sparse.mm(par.abs(), x_s)
     x_t2s = torch.sparse.mm(par.abs().transpose(0, 1), x_t) / 2
     return x_s2t, x_t2s

@@ -316,28 +316,52 @@ def test_zinc_model_vs_reference_golden(cuda):
 
 
 def test_zinc_model_cfg2_vs_oracle(cuda):
-    """BASELINE config 2 model at a 200-graph batch: HIP product vs oracle."""
+    """BASELINE config 2 model at a 200-graph batch: HIP product vs oracle.
+
+    Tolerance: forward output 1e-4 relative.  Gradients pass through 6 blocks of
+    batch-statistics BN, where fp32 rounding noise is amplified: the fp32 oracle
+    itself deviates from an fp64 evaluation by up to ~3e-2 (relative, max-norm)
+    on deep-layer weight gradients.  So each parameter gradient of the HIP path
+    must be as close to the fp64 oracle as the fp32 oracle is (<= 3x its error,
+    floor 1e-4 relative)."""
     import hlhgat
     from hlhgat.synthetic import zinc_like_batch
     b = zinc_like_batch(200, seed=21)
+    kw = dict(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256], K=3, keig=15)
     torch.manual_seed(0)
-    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2, 2], filters=[64, 64, 64],
-                                            mlp_channels=[256, 256], K=3, keig=15)
-    ref = R.RefZincModel(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256],
-                         K=3, keig=15)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**kw)
+    ref = R.RefZincModel(**kw)
     ref.load_state_dict(m.state_dict())
-    m = m.to(cuda).train()
-    ref.train()
+    ref64 = R.RefZincModel(**kw).double()
+    ref64.load_state_dict({k: v.double() if v.is_floating_point() else v
+                           for k, v in m.state_dict().items()})
+    m, ref, ref64 = m.to(cuda).train(), ref.train(), ref64.train()
+
+    class _D:
+        pass
+
+    b64 = _D()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index", "num_node1", "num_edge1"):
+        v = getattr(b, k)
+        setattr(b64, k, v.double() if v.is_floating_point() else v)
     out_r = ref(b)
+    out_64 = ref64(b64)
     bd = zinc_like_batch(200, seed=21).to(cuda)
     out = m(bd)
     close(out.detach().cpu(), out_r.detach(), 1e-4, "out")
     Rg = torch.randn(out_r.shape)
     (out * dev(Rg)).sum().backward()
     (out_r * Rg).sum().backward()
+    (out_64 * Rg.double()).sum().backward()
     rp = dict(ref.named_parameters())
+    r64 = dict(ref64.named_parameters())
     for k, p in m.named_parameters():
-        close(p.grad.cpu(), rp[k].grad, 1e-3, "grad " + k)
+        e = r64[k].grad
+        scale = max(1.0, e.abs().max().item())
+        err_ref = (rp[k].grad.double() - e).abs().max().item() / scale
+        err_hip = (p.grad.cpu().double() - e).abs().max().item() / scale
+        assert err_hip <= max(3 * err_ref, 1e-4), (k, err_hip, err_ref)
 
 
 # ---------------------------------------------------------------------------
