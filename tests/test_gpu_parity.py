@@ -400,5 +400,6 @@ def test_batch_norm_act_vs_torch(cuda, n, C, relu):
     close(bn.running_var.cpu(), bn_ref.running_var, 1e-5, "running_var")
     assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
     # a second call reuses the (self-resetting) workspace counters
-    y2 = ops.batch_norm_act(xd.detach(), bn, relu=relu)
+    with torch.no_grad():
+        y2 = ops.batch_norm_act(xd.detach(), bn, relu=relu)
     close(y2.cpu(), y.detach().cpu(), 1e-6, "repeat")
