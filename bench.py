@@ -105,7 +105,7 @@ def main():
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(
             model, device_ids=[local], bucket_cap_mb=32, gradient_as_bucket_view=True)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-3)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-3, fused=True)
     crit = torch.nn.L1Loss()
 
     def step(i):

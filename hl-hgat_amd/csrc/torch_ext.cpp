@@ -1,0 +1,636 @@
+// Host-side torch binding of the hot path: C++ autograd nodes over the C-ABI
+// of include/hlhgat.h.
+//
+// Python autograd Functions + ctypes cost 20-70 us of host time per op, which
+// made the ZINC-scale training step host-bound.  Here each
+// composite layer is ONE C++ autograd node whose forward / backward issue the
+// whole launch sequence from C++:
+//   conv_bn     HodgeLaguerreConv / HodgeChebConv (+ BatchNorm (+ ReLU))
+//               lib/Hodge_Cheb_Conv.py:480-515 / :394-439, lib/Hodge_ST_Model.py:556-566
+//   bn_act      gnn.BatchNorm / BatchNorm1d (+ ReLU), training statistics
+//   linear      Linear over a split reduction axis (Linear(cat[a, b]))
+//   mlp2        NodeEdgeInt WV_*: Linear->BN->ReLU->Linear->BN->ReLU
+//               lib/Hodge_Cheb_Conv.py:276-289,307-308
+//   node_from_edges / edge_from_nodes   (1/D)|B1| x_s and |B1|^T x_t / 2
+//               lib/Hodge_Cheb_Conv.py:294-295
+// Every kernel runs on torch's current HIP stream; no CPU fallback exists.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <algorithm>
+#include <optional>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/hlhgat.h"
+
+namespace {
+
+using torch::Tensor;
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+using OptT = std::optional<Tensor>;
+
+inline void* stream_of(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.get_device()).stream();
+}
+inline void chk(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "hlhgat: ", what, " failed: ", hlhgat_last_error());
+}
+inline int64_t ld_of(const Tensor& t) {
+  return std::max<int64_t>({t.stride(0), t.size(1), (int64_t)1});
+}
+inline bool has(const OptT& t) { return t.has_value() && t->defined(); }
+inline const float* fptr(const OptT& t) { return has(t) ? t->data_ptr<float>() : nullptr; }
+inline float* mfptr(const OptT& t) { return has(t) ? t->data_ptr<float>() : nullptr; }
+inline Tensor rows2d(const Tensor& t) {
+  if (t.stride(1) != 1 || t.stride(0) < t.size(1)) return t.contiguous();
+  return t;
+}
+inline void req(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "hlhgat: ", name, " must be on a ROCm device (no CPU fallback)");
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "hlhgat: ", name, " must be float32");
+}
+
+// ---------------------------------------------------------------------------
+// raw launches
+// ---------------------------------------------------------------------------
+struct Csr {
+  Tensor rowptr, col;
+  OptT val;
+  int64_t nnz;
+};
+
+Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
+  static auto* cache = new std::unordered_map<int, Tensor>();  // leaked: outlives HIP teardown
+  const int dev = like.get_device();
+  const int64_t need = hlhgat_bn_workspace_bytes(n, C);
+  auto it = cache->find(dev);
+  if (it == cache->end() || it->second.numel() < need) {
+    (*cache)[dev] = at::zeros({std::max<int64_t>(need, 1 << 20)}, like.options().dtype(at::kByte));
+  }
+  return (*cache)[dev];
+}
+
+// out[M, N] = sum_b A_b W_b^T + bias
+void proj_fwd(const std::vector<const float*>& A, const std::vector<int64_t>& lda,
+              const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
+              const std::vector<int64_t>& kb, int64_t M, int64_t N, const float* bias,
+              Tensor& out, void* s) {
+  chk(hlhgat_proj_fwd((int)A.size(), A.data(), lda.data(), W.data(), ldw.data(), kb.data(), M, N,
+                      bias, out.data_ptr<float>(), ld_of(out), 0, s),
+      "proj_fwd");
+}
+
+void proj_bwd_weight(const Tensor& G, const std::vector<const float*>& A,
+                     const std::vector<int64_t>& lda, const std::vector<int64_t>& kb,
+                     std::vector<float*>& dW, const std::vector<int64_t>& lddw, float* db,
+                     void* s) {
+  const int nb = (int)A.size();
+  const int64_t M = G.size(0), N = G.size(1);
+  const int64_t wsf =
+      hlhgat_proj_bwd_weight_workspace_floats(nb, kb.data(), M, N, db != nullptr);
+  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, G.options());
+  chk(hlhgat_proj_bwd_weight(nb, G.data_ptr<float>(), ld_of(G), A.data(), lda.data(), kb.data(),
+                             M, N, dW.data(), lddw.data(), db, 0, ws.data_ptr<float>(), wsf, s),
+      "proj_bwd_weight");
+}
+
+void proj_bwd_data(const Tensor& G, const std::vector<const float*>& W,
+                   const std::vector<int64_t>& ldw, const std::vector<int64_t>& kb,
+                   std::vector<float*>& dA, const std::vector<int64_t>& ldda, void* s) {
+  chk(hlhgat_proj_bwd_data((int)W.size(), G.data_ptr<float>(), ld_of(G), W.data(), ldw.data(),
+                           kb.data(), G.size(0), G.size(1), dA.data(), ldda.data(), 0, s),
+      "proj_bwd_data");
+}
+
+struct BnState {
+  OptT w, b, rm, rv, nbt;
+  double momentum = 0.1, eps = 1e-5;
+};
+
+Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd) {
+  const int64_t n = x.size(0), C = x.size(1);
+  Tensor y = at::empty({n, C}, x.options());
+  mean = at::empty({C}, x.options());
+  invstd = at::empty({C}, x.options());
+  Tensor ws = bn_workspace(x, n, C);
+  int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
+  chk(hlhgat_bn_fwd_train(x.data_ptr<float>(), ld_of(x), n, C, fptr(st.w), fptr(st.b),
+                          mfptr(st.rm), mfptr(st.rv), nbt, (float)st.momentum, (float)st.eps,
+                          relu ? 1 : 0, y.data_ptr<float>(), C, mean.data_ptr<float>(),
+                          invstd.data_ptr<float>(), ws.data_ptr(), ws.numel(), stream_of(x)),
+      "bn_fwd_train");
+  return y;
+}
+
+// returns dx; fills dw/db when requested
+Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
+                   const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
+                   Tensor& dw, Tensor& db) {
+  const int64_t n = x.size(0), C = x.size(1);
+  Tensor dyc = rows2d(dy);
+  Tensor dx = at::empty({n, C}, x.options());
+  dw = (need_w && has(w)) ? at::empty({C}, x.options()) : Tensor();
+  db = need_b ? at::empty({C}, x.options()) : Tensor();
+  Tensor ws = bn_workspace(x, n, C);
+  chk(hlhgat_bn_bwd_train(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
+                          dyc.data_ptr<float>(), ld_of(dyc), n, C, fptr(w),
+                          mean.data_ptr<float>(), invstd.data_ptr<float>(), dx.data_ptr<float>(),
+                          C, dw.defined() ? dw.data_ptr<float>() : nullptr,
+                          db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
+                          ws.numel(), stream_of(x)),
+      "bn_bwd_train");
+  return dx;
+}
+
+// ---------------------------------------------------------------------------
+// conv (+ BN (+ ReLU))
+// ---------------------------------------------------------------------------
+class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
+ public:
+  // x: [N, C] or [N, T, C]; A/At: CSR of L and L^T; W: K weights [dout, C]
+  static Tensor forward(AutogradContext* ctx, Tensor x, Tensor a_rowptr, Tensor a_col,
+                        OptT a_val, Tensor t_rowptr, Tensor t_col, OptT t_val, int64_t nnz,
+                        int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
+                        OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
+                        int64_t bn_mode) {
+    req(x, "x");
+    const int64_t N = x.size(0);
+    const int64_t Cin = x.size(-1);
+    const int64_t K = (int64_t)W.size();
+    Tensor x2 = x.dim() == 2 ? rows2d(x) : x.contiguous().view({N, -1});
+    const int64_t F = x2.size(1);
+    const int64_t M = N * (F / Cin);
+    const int64_t dout = W[0].size(0);
+    void* s = stream_of(x);
+    Tensor T = at::empty({std::max<int64_t>(K - 1, 0), N, F}, x.options());
+    if (K > 1 && N > 0) {
+      chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
+                                nnz ? a_col.data_ptr<int>() : nullptr,
+                                nnz ? fptr(a_val) : nullptr, N, nnz, x2.data_ptr<float>(),
+                                ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
+          "poly_basis_fwd");
+    }
+    std::vector<const float*> Ap(K), Wp(K);
+    std::vector<int64_t> lda(K), ldw(K), kb(K, Cin);
+    Ap[0] = x2.data_ptr<float>();
+    lda[0] = x.dim() == 2 ? ld_of(x2) : Cin;
+    for (int64_t k = 1; k < K; ++k) {
+      Ap[k] = T.data_ptr<float>() + (k - 1) * N * F;
+      lda[k] = Cin;
+    }
+    for (int64_t k = 0; k < K; ++k) {
+      req(W[k], "lins[k].weight");
+      TORCH_CHECK(W[k].stride(1) == 1, "hlhgat: weights need unit inner stride");
+      Wp[k] = W[k].data_ptr<float>();
+      ldw[k] = W[k].stride(0);
+    }
+    Tensor pre = at::empty({M, dout}, x.options());
+    if (M > 0) {
+      proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, s);
+    } else if (has(bias)) {
+      pre.copy_(bias->expand_as(pre));
+    }
+    Tensor out = pre, mean, invstd;
+    if (bn_mode > 0) {
+      BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps};
+      out = bn_forward(pre, st, bn_mode == 2, mean, invstd);
+    }
+    ctx->saved_data["dims"] = std::vector<int64_t>{N, Cin, F, M, dout, K, kind, nnz, bn_mode,
+                                                   has(bias) ? 1 : 0};
+    ctx->saved_data["xshape"] = x.sizes().vec();
+    std::vector<Tensor> save = {x2,
+                                T,
+                                t_rowptr,
+                                t_col,
+                                has(t_val) ? *t_val : Tensor(),
+                                bn_mode > 0 ? pre : Tensor(),
+                                bn_mode == 2 ? out : Tensor(),
+                                mean,
+                                invstd,
+                                has(bn_w) ? *bn_w : Tensor()};
+    for (const auto& w : W) save.push_back(w);
+    ctx->save_for_backward(save);
+    std::vector<int64_t> oshape = x.sizes().vec();
+    oshape.back() = dout;
+    return out.view(oshape);
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto d = ctx->saved_data["dims"].toIntVector();
+    const int64_t N = d[0], Cin = d[1], F = d[2], M = d[3], dout = d[4], K = d[5], kind = d[6],
+                  nnz = d[7], bn_mode = d[8];
+    const bool has_bias = d[9] != 0;
+    auto xshape = ctx->saved_data["xshape"].toIntVector();
+    auto sv = ctx->get_saved_variables();
+    Tensor x2 = sv[0], T = sv[1], t_rowptr = sv[2], t_col = sv[3], t_val = sv[4], pre = sv[5],
+           yout = sv[6], mean = sv[7], invstd = sv[8], bn_w = sv[9];
+    std::vector<Tensor> W(sv.begin() + 10, sv.end());
+    void* s = stream_of(x2);
+    Tensor G = grads[0].reshape({M, dout});
+    G = rows2d(G).contiguous();
+    // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
+    //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
+    const int64_t n_pos = 18 + K;
+    variable_list out(n_pos);
+    const bool need_x = ctx->needs_input_grad(0);
+    Tensor dbn_w, dbn_b;
+    if (bn_mode > 0) {
+      OptT y = bn_mode == 2 ? OptT(yout) : OptT();
+      OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
+      G = bn_backward(pre, y, G, w, mean, invstd, ctx->needs_input_grad(10 + K),
+                      ctx->needs_input_grad(11 + K), dbn_w, dbn_b);
+      out[10 + K] = dbn_w;
+      out[11 + K] = dbn_b;
+    }
+    std::vector<const float*> Ap(K);
+    std::vector<int64_t> lda(K), kb(K, Cin);
+    Ap[0] = x2.data_ptr<float>();
+    lda[0] = (int64_t)xshape.size() == 2 ? ld_of(x2) : Cin;
+    for (int64_t k = 1; k < K; ++k) {
+      Ap[k] = T.data_ptr<float>() + (k - 1) * N * F;
+      lda[k] = Cin;
+    }
+    bool need_w = false;
+    for (int64_t k = 0; k < K; ++k) need_w = need_w || ctx->needs_input_grad(9 + k);
+    const bool need_b = has_bias && ctx->needs_input_grad(9 + K);
+    if (need_w || need_b) {
+      std::vector<Tensor> dW(K);
+      std::vector<float*> dWp(K);
+      std::vector<int64_t> lddw(K);
+      for (int64_t k = 0; k < K; ++k) {
+        dW[k] = at::empty({dout, Cin}, x2.options());
+        dWp[k] = dW[k].data_ptr<float>();
+        lddw[k] = Cin;
+      }
+      Tensor db = need_b ? at::empty({dout}, x2.options()) : Tensor();
+      if (M > 0) {
+        proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, s);
+      } else {
+        for (auto& t : dW) t.zero_();
+        if (need_b) db.zero_();
+      }
+      for (int64_t k = 0; k < K; ++k)
+        if (ctx->needs_input_grad(9 + k)) out[9 + k] = dW[k];
+      if (need_b) out[9 + K] = db;
+    }
+    if (need_x) {
+      Tensor Gs = at::empty({K, N, F}, x2.options());
+      if (M > 0) {
+        std::vector<const float*> Wp(K);
+        std::vector<int64_t> ldw(K), ldda(K, Cin);
+        std::vector<float*> dA(K);
+        for (int64_t k = 0; k < K; ++k) {
+          Wp[k] = W[k].data_ptr<float>();
+          ldw[k] = W[k].stride(0);
+          dA[k] = Gs.data_ptr<float>() + k * N * F;
+        }
+        proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
+        if (K > 1) {
+          chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
+                                    nnz ? t_col.data_ptr<int>() : nullptr,
+                                    (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
+                                    N, nnz, F, (int)K, Gs.data_ptr<float>(), s),
+              "poly_basis_bwd");
+        }
+      } else {
+        Gs.zero_();
+      }
+      out[0] = Gs[0].view(xshape);
+    }
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// BatchNorm (+ ReLU)
+// ---------------------------------------------------------------------------
+class BNActFn : public torch::autograd::Function<BNActFn> {
+ public:
+  static Tensor forward(AutogradContext* ctx, Tensor x, OptT w, OptT b, OptT rm, OptT rv,
+                        OptT nbt, double momentum, double eps, bool relu) {
+    req(x, "x");
+    Tensor xc = rows2d(x);
+    Tensor mean, invstd;
+    BnState st{w, b, rm, rv, nbt, momentum, eps};
+    Tensor y = bn_forward(xc, st, relu, mean, invstd);
+    ctx->saved_data["relu"] = relu;
+    ctx->save_for_backward({xc, relu ? y : Tensor(), has(w) ? *w : Tensor(), mean, invstd});
+    return y;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    Tensor dw, db;
+    OptT y = sv[1].defined() ? OptT(sv[1]) : OptT();
+    OptT w = sv[2].defined() ? OptT(sv[2]) : OptT();
+    Tensor dx = bn_backward(sv[0], y, grads[0], w, sv[3], sv[4], ctx->needs_input_grad(1),
+                           ctx->needs_input_grad(2), dw, db);
+    return {dx, dw, db, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Linear over blocks: out = cat(As, -1) @ W^T + b, W column-split per block
+// ---------------------------------------------------------------------------
+Tensor linear_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT& b) {
+  const int64_t M = As[0].size(0), N = W.size(0);
+  const int nb = (int)As.size();
+  std::vector<const float*> Ap(nb), Wp(nb);
+  std::vector<int64_t> lda(nb), ldw(nb), kb(nb);
+  int64_t off = 0;
+  for (int i = 0; i < nb; ++i) {
+    Ap[i] = As[i].data_ptr<float>();
+    lda[i] = ld_of(As[i]);
+    kb[i] = As[i].size(1);
+    Wp[i] = W.data_ptr<float>() + off;
+    ldw[i] = W.stride(0);
+    off += kb[i];
+  }
+  TORCH_CHECK(off == W.size(1), "hlhgat: Linear expects ", W.size(1), " input features, got ",
+              off);
+  Tensor out = at::empty({M, N}, W.options());
+  if (M > 0) proj_fwd(Ap, lda, Wp, ldw, kb, M, N, fptr(b), out, stream_of(W));
+  return out;
+}
+
+// grads of linear_forward; dAs[i] only where need_a[i]
+void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Tensor& W,
+                     bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
+                     Tensor& db, std::vector<Tensor>& dAs) {
+  Tensor G = rows2d(Gin);
+  const int64_t M = G.size(0), N = G.size(1);
+  const int nb = (int)As.size();
+  void* s = stream_of(W);
+  std::vector<int64_t> kb(nb), offs(nb);
+  int64_t off = 0;
+  for (int i = 0; i < nb; ++i) {
+    kb[i] = As[i].size(1);
+    offs[i] = off;
+    off += kb[i];
+  }
+  dW = Tensor();
+  db = Tensor();
+  if (need_w || need_b) {
+    Tensor gw = at::empty_like(W, at::MemoryFormat::Contiguous);
+    Tensor gb = need_b ? at::empty({N}, W.options()) : Tensor();
+    if (M > 0) {
+      std::vector<const float*> Ap(nb);
+      std::vector<int64_t> lda(nb), lddw(nb, W.size(1));
+      std::vector<float*> dWp(nb);
+      for (int i = 0; i < nb; ++i) {
+        Ap[i] = As[i].data_ptr<float>();
+        lda[i] = ld_of(As[i]);
+        dWp[i] = gw.data_ptr<float>() + offs[i];
+      }
+      proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, s);
+    } else {
+      gw.zero_();
+      if (need_b) gb.zero_();
+    }
+    if (need_w) dW = gw;
+    if (need_b) db = gb;
+  }
+  dAs.assign(nb, Tensor());
+  std::vector<int> idx;
+  for (int i = 0; i < nb; ++i)
+    if (need_a[i]) idx.push_back(i);
+  if (!idx.empty()) {
+    std::vector<const float*> Wp;
+    std::vector<int64_t> ldw, kbs, ldda;
+    std::vector<float*> dA;
+    for (int i : idx) {
+      dAs[i] = at::empty({M, kb[i]}, W.options());
+      Wp.push_back(W.data_ptr<float>() + offs[i]);
+      ldw.push_back(W.stride(0));
+      kbs.push_back(kb[i]);
+      dA.push_back(dAs[i].data_ptr<float>());
+      ldda.push_back(kb[i]);
+    }
+    if (M > 0) proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s);
+  }
+}
+
+class LinearFn : public torch::autograd::Function<LinearFn> {
+ public:
+  static Tensor forward(AutogradContext* ctx, Tensor W, OptT b, at::TensorList As_in) {
+    req(W, "weight");
+    std::vector<Tensor> As;
+    for (const auto& a : As_in) {
+      req(a, "input");
+      As.push_back(rows2d(a));
+    }
+    Tensor Wc = W.stride(1) == 1 ? W : W.contiguous();
+    Tensor out = linear_forward(As, Wc, b);
+    ctx->saved_data["has_b"] = has(b);
+    std::vector<Tensor> save = {Wc};
+    save.insert(save.end(), As.begin(), As.end());
+    ctx->save_for_backward(save);
+    return out;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    Tensor W = sv[0];
+    std::vector<Tensor> As(sv.begin() + 1, sv.end());
+    std::vector<bool> need_a(As.size());
+    for (size_t i = 0; i < As.size(); ++i) need_a[i] = ctx->needs_input_grad(2 + i);
+    Tensor dW, db;
+    std::vector<Tensor> dAs;
+    linear_backward(grads[0], As, W, ctx->needs_input_grad(0),
+                    ctx->saved_data["has_b"].toBool() && ctx->needs_input_grad(1), need_a, dW, db,
+                    dAs);
+    variable_list out = {dW, db};
+    out.insert(out.end(), dAs.begin(), dAs.end());
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// NodeEdgeInt WV_* : Linear(blocks) -> BN -> ReLU -> Linear -> BN -> ReLU
+// ---------------------------------------------------------------------------
+class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
+ public:
+  static Tensor forward(AutogradContext* ctx, at::TensorList blocks_in, Tensor W0, OptT b0,
+                        OptT g1, OptT be1, OptT rm1, OptT rv1, OptT nbt1, Tensor W3, OptT b3,
+                        OptT g4, OptT be4, OptT rm4, OptT rv4, OptT nbt4, double mom1, double eps1,
+                        double mom4, double eps4) {
+    std::vector<Tensor> blocks;
+    for (const auto& a : blocks_in) {
+      req(a, "input");
+      blocks.push_back(rows2d(a));
+    }
+    Tensor W0c = W0.stride(1) == 1 ? W0 : W0.contiguous();
+    Tensor W3c = W3.stride(1) == 1 ? W3 : W3.contiguous();
+    Tensor h1 = linear_forward(blocks, W0c, b0);
+    Tensor m1, i1, m4, i4;
+    Tensor a1 = bn_forward(h1, BnState{g1, be1, rm1, rv1, nbt1, mom1, eps1}, true, m1, i1);
+    Tensor h2 = linear_forward({a1}, W3c, b3);
+    Tensor y = bn_forward(h2, BnState{g4, be4, rm4, rv4, nbt4, mom4, eps4}, true, m4, i4);
+    ctx->saved_data["nb"] = (int64_t)blocks.size();
+    ctx->saved_data["has_b0"] = has(b0);
+    ctx->saved_data["has_b3"] = has(b3);
+    std::vector<Tensor> save = {W0c, h1, a1, m1, i1, has(g1) ? *g1 : Tensor(), W3c, h2, y, m4, i4,
+                                has(g4) ? *g4 : Tensor()};
+    save.insert(save.end(), blocks.begin(), blocks.end());
+    ctx->save_for_backward(save);
+    return y;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    const int64_t nb = ctx->saved_data["nb"].toInt();
+    Tensor W0 = sv[0], h1 = sv[1], a1 = sv[2], m1 = sv[3], i1 = sv[4], g1 = sv[5], W3 = sv[6],
+           h2 = sv[7], y = sv[8], m4 = sv[9], i4 = sv[10], g4 = sv[11];
+    std::vector<Tensor> blocks(sv.begin() + 12, sv.end());
+    // positions: blocks[0..nb), W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4, rm4, rv4,
+    //            nbt4, mom1, eps1, mom4, eps4
+    const int64_t P = nb;
+    variable_list out(nb + 18);
+    Tensor dg4, dbe4, dg1, dbe1;
+    Tensor dh2 = bn_backward(h2, OptT(y), grads[0], g4.defined() ? OptT(g4) : OptT(), m4, i4,
+                             ctx->needs_input_grad(P + 9), ctx->needs_input_grad(P + 10), dg4,
+                             dbe4);
+    out[P + 9] = dg4;
+    out[P + 10] = dbe4;
+    Tensor dW3, db3, dW0, db0;
+    std::vector<Tensor> da1;
+    linear_backward(dh2, {a1}, W3, ctx->needs_input_grad(P + 7),
+                    ctx->saved_data["has_b3"].toBool() && ctx->needs_input_grad(P + 8), {true},
+                    dW3, db3, da1);
+    out[P + 7] = dW3;
+    out[P + 8] = db3;
+    Tensor dh1 = bn_backward(h1, OptT(a1), da1[0], g1.defined() ? OptT(g1) : OptT(), m1, i1,
+                             ctx->needs_input_grad(P + 2), ctx->needs_input_grad(P + 3), dg1,
+                             dbe1);
+    out[P + 2] = dg1;
+    out[P + 3] = dbe1;
+    std::vector<bool> need_a(nb);
+    for (int64_t i = 0; i < nb; ++i) need_a[i] = ctx->needs_input_grad(i);
+    std::vector<Tensor> dblocks;
+    linear_backward(dh1, blocks, W0, ctx->needs_input_grad(P),
+                    ctx->saved_data["has_b0"].toBool() && ctx->needs_input_grad(P + 1), need_a,
+                    dW0, db0, dblocks);
+    out[P] = dW0;
+    out[P + 1] = db0;
+    for (int64_t i = 0; i < nb; ++i) out[i] = dblocks[i];
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// boundary operator gathers
+// ---------------------------------------------------------------------------
+Tensor node_segment(const Tensor& rowptr, const Tensor& eids, int64_t n_nodes, int64_t n_edges,
+                    const Tensor& x, const float* rs, float alpha) {
+  Tensor out = at::empty({n_nodes, x.size(1)}, x.options());
+  if (n_nodes > 0) {
+    chk(hlhgat_poly_step(rowptr.data_ptr<int>(), n_edges ? eids.data_ptr<int>() : nullptr,
+                         nullptr, rs, n_nodes, 2 * n_edges, x.data_ptr<float>(), ld_of(x),
+                         x.size(1), nullptr, 0, nullptr, 0, nullptr, 0, alpha, 0.f, 0.f, 1.f,
+                         0.f, 0.f, out.data_ptr<float>(), ld_of(out), stream_of(x)),
+        "poly_step(incidence)");
+  }
+  return out;
+}
+
+Tensor edge_gather(const Tensor& ei, int64_t n_edges, const Tensor& x, const float* sa,
+                   const float* sb, float ca, float cb) {
+  Tensor out = at::empty({n_edges, x.size(1)}, x.options());
+  if (n_edges > 0) {
+    chk(hlhgat_edge_gather2(ei.data_ptr<int64_t>(), n_edges, x.data_ptr<float>(), ld_of(x),
+                            x.size(1), sa, sb, ca, cb, out.data_ptr<float>(), ld_of(out), 0,
+                            stream_of(x)),
+        "edge_gather2");
+  }
+  return out;
+}
+
+class NodeFromEdgesFn : public torch::autograd::Function<NodeFromEdgesFn> {
+ public:
+  // (1/D) |B1| x_s
+  static Tensor forward(AutogradContext* ctx, Tensor x_s, Tensor rowptr, Tensor eids, Tensor ei,
+                        Tensor rD, int64_t n_nodes) {
+    req(x_s, "x_s");
+    Tensor xs = rows2d(x_s);
+    const int64_t E = ei.size(1);
+    TORCH_CHECK(xs.size(0) == E, "hlhgat: x_s rows != |B1| edges");
+    ctx->saved_data["n"] = n_nodes;
+    ctx->save_for_backward({ei, rD});
+    return node_segment(rowptr, eids, n_nodes, E, xs, rD.data_ptr<float>(), 1.f);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    Tensor g = rows2d(grads[0]);
+    const float* rD = sv[1].data_ptr<float>();
+    Tensor gx = edge_gather(sv[0], sv[0].size(1), g, rD, rD, 1.f, 1.f);
+    return {gx, Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+class EdgeFromNodesFn : public torch::autograd::Function<EdgeFromNodesFn> {
+ public:
+  // |B1|^T x_t / 2
+  static Tensor forward(AutogradContext* ctx, Tensor x_t, Tensor rowptr, Tensor eids, Tensor ei) {
+    req(x_t, "x_t");
+    Tensor xt = rows2d(x_t);
+    ctx->saved_data["n"] = xt.size(0);
+    ctx->save_for_backward({rowptr, eids, ei});
+    return edge_gather(ei, ei.size(1), xt, nullptr, nullptr, 0.5f, 0.5f);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    Tensor g = rows2d(grads[0]);
+    const int64_t n = ctx->saved_data["n"].toInt();
+    Tensor gx = node_segment(sv[0], sv[1], n, sv[2].size(1), g, nullptr, 0.5f);
+    return {gx, Tensor(), Tensor(), Tensor()};
+  }
+};
+
+// ---------------------------------------------------------------------------
+// python entry points
+// ---------------------------------------------------------------------------
+Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_rowptr, Tensor t_col,
+               OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
+               OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
+               int64_t bn_mode) {
+  return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
+                         at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
+                         bn_mode);
+}
+
+Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,
+              bool relu) {
+  return BNActFn::apply(x, w, b, rm, rv, nbt, momentum, eps, relu);
+}
+
+Tensor linear(std::vector<Tensor> As, Tensor W, OptT b) {
+  return LinearFn::apply(W, b, at::TensorList(As));
+}
+
+Tensor mlp2(std::vector<Tensor> blocks, Tensor W0, OptT b0, OptT g1, OptT be1, OptT rm1, OptT rv1,
+            OptT nbt1, Tensor W3, OptT b3, OptT g4, OptT be4, OptT rm4, OptT rv4, OptT nbt4,
+            double mom1, double eps1, double mom4, double eps4) {
+  return MLP2Fn::apply(at::TensorList(blocks), W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4,
+                       rm4, rv4, nbt4, mom1, eps1, mom4, eps4);
+}
+
+Tensor node_from_edges(Tensor x_s, Tensor rowptr, Tensor eids, Tensor ei, Tensor rD,
+                       int64_t n_nodes) {
+  return NodeFromEdgesFn::apply(x_s, rowptr, eids, ei, rD, n_nodes);
+}
+
+Tensor edge_from_nodes(Tensor x_t, Tensor rowptr, Tensor eids, Tensor ei) {
+  return EdgeFromNodesFn::apply(x_t, rowptr, eids, ei);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
+  m.def("conv_bn", &conv_bn);
+  m.def("bn_act", &bn_act);
+  m.def("linear", &linear);
+  m.def("mlp2", &mlp2);
+  m.def("node_from_edges", &node_from_edges);
+  m.def("edge_from_nodes", &edge_from_nodes);
+  m.def("version", []() { return hlhgat_version(); });
+}

@@ -65,6 +65,15 @@ class _HodgePolyConv(nn.Module):
         return ops.hodge_poly_conv(x, op, [lin.weight for lin in self.lins], self.bias,
                                    self._kind)
 
+    def forward_bn(self, x: Tensor, edge_index: Tensor, edge_weight: Optional[Tensor],
+                   bn: nn.BatchNorm1d, relu: bool) -> Tensor:
+        """forward -> bn -> (ReLU) as one fused C++ autograd node (the tail of
+        every HL block, lib/Hodge_ST_Model.py:556-566); same result as the
+        three modules applied in turn."""
+        op = ops.hodge_operator(edge_index, edge_weight, x.size(0))
+        return ops.hodge_poly_conv(x, op, [lin.weight for lin in self.lins], self.bias,
+                                   self._kind, bn=bn, relu=relu)
+
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "
                 f"{self.out_channels}, K={len(self.lins)})")
@@ -109,6 +118,19 @@ def _as_boundary(par, n_nodes: int, n_edges: int) -> BoundaryOperator:
     if torch.is_tensor(par) and par.is_sparse:
         return boundary_from_sparse(par)
     raise TypeError("NodeEdgeInt: par must come from adj2par1")
+
+
+def _value_mlp(seq: nn.Sequential, blocks) -> Tensor:
+    """WV_* on cat(blocks): one fused C++ node for the reference structure
+    Linear->BN->ReLU->Linear->BN->ReLU in training mode, module-by-module on
+    the HIP ops otherwise."""
+    m = list(seq)
+    if (len(m) == 6 and isinstance(m[0], nn.Linear) and isinstance(m[1], nn.BatchNorm1d)
+            and isinstance(m[2], nn.ReLU) and isinstance(m[3], nn.Linear)
+            and isinstance(m[4], nn.BatchNorm1d) and isinstance(m[5], nn.ReLU)
+            and all(b.training or not b.track_running_stats for b in (m[1], m[4]))):
+        return ops.mlp2(blocks, seq)
+    return run_sequential(seq, blocks)
 
 
 class NodeEdgeInt(nn.Module):
@@ -165,8 +187,8 @@ class NodeEdgeInt(nn.Module):
             a_s = ops.att_score(qc_s, kq_s[:, dk:], kq_s[:, :dk], 1 - self.lambda_Edge,
                                 self.lambda_Edge, sq, code)
             return a_t, a_s
-        x_t1 = run_sequential(self.WV_Node, [x_s2t, x_t])
-        x_s1 = run_sequential(self.WV_Edge, [x_t2s, x_s])
+        x_t1 = _value_mlp(self.WV_Node, [x_s2t, x_t])
+        x_s1 = _value_mlp(self.WV_Edge, [x_t2s, x_s])
         return x_t1, x_s1
 
 

@@ -121,15 +121,27 @@ class Sequential(tnn.Module):
             self._routes.append((ins, outs))
             prev_out = outs
         self._n = len(modules)
-        # BatchNorm immediately followed by ReLU on the same variable runs as
-        # one fused HIP BN+ReLU op (same result as the two modules in turn)
-        self._fuse_relu = [False] * self._n
-        for i in range(self._n - 1):
-            a, b = getattr(self, f"module_{i}"), getattr(self, f"module_{i + 1}")
-            ra, rb = self._routes[i], self._routes[i + 1]
-            if (isinstance(a, BatchNorm) and isinstance(b, tnn.ReLU) and len(ra[1]) == 1
-                    and rb[0] == ra[1] and rb[1] == ra[1]):
-                self._fuse_relu[i] = True
+        # Fusions (same result as the modules in turn):
+        #  HodgeConv -> BatchNorm [-> ReLU] on one variable: one C++ node
+        #  BatchNorm -> ReLU: one fused HIP BN+ReLU op
+        self._fuse = [None] * self._n  # (kind, n_entries_consumed)
+        i = 0
+        while i < self._n:
+            m0 = getattr(self, f"module_{i}")
+            r0 = self._routes[i]
+
+            def same_var(j):
+                return (j < self._n and len(r0[1]) == 1
+                        and self._routes[j][0] == r0[1] and self._routes[j][1] == r0[1])
+
+            if hasattr(m0, "forward_bn") and same_var(i + 1) and isinstance(
+                    getattr(self, f"module_{i + 1}"), BatchNorm):
+                relu = same_var(i + 2) and isinstance(getattr(self, f"module_{i + 2}"), tnn.ReLU)
+                self._fuse[i] = ("conv_bn_relu" if relu else "conv_bn", 3 if relu else 2)
+            elif isinstance(m0, BatchNorm) and same_var(i + 1) and isinstance(
+                    getattr(self, f"module_{i + 1}"), tnn.ReLU):
+                self._fuse[i] = ("bn_relu", 2)
+            i += self._fuse[i][1] if self._fuse[i] else 1
 
     def forward(self, *args):
         if len(args) != len(self.input_args):
@@ -137,18 +149,23 @@ class Sequential(tnn.Module):
                             f"({', '.join(self.input_args)}), got {len(args)}")
         env = dict(zip(self.input_args, args))
         out = None
-        skip = False
-        for i, (ins, outs) in enumerate(self._routes):
-            if skip:
-                skip = False
-                continue
+        i = 0
+        while i < self._n:
+            ins, outs = self._routes[i]
             fn = getattr(self, f"module_{i}")
-            if self._fuse_relu[i]:
+            fuse = self._fuse[i]
+            if fuse is None:
+                out = fn(*[env[n] for n in ins])
+                i += 1
+            elif fuse[0] == "bn_relu":
                 from .ops import batch_norm_act
                 out = batch_norm_act(env[ins[0]], fn.module, relu=True)
-                skip = True
+                i += 2
             else:
-                out = fn(*[env[n] for n in ins])
+                bn = getattr(self, f"module_{i + 1}").module
+                out = fn.forward_bn(*[env[n] for n in ins], bn=bn,
+                                    relu=fuse[0] == "conv_bn_relu")
+                i += fuse[1]
             if len(outs) == 1:
                 env[outs[0]] = out
             else:

@@ -18,9 +18,16 @@ import torch
 from . import _lib
 from ._lib import LIB, check
 
+try:  # C++ autograd nodes over the same C-ABI (hl-hgat_amd/csrc/torch_ext.cpp)
+    from . import _hlhgat_ext as _ext
+except ImportError as e:  # pragma: no cover - the build always produces it
+    raise ImportError(f"hlhgat: torch extension _hlhgat_ext missing ({e}); run the build "
+                      f"(make -C hl-hgat_amd/csrc)") from e
+
 __all__ = [
     "SparseCSR", "HodgeOperator", "Incidence", "hodge_operator", "incidence",
-    "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks",
+    "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks", "mlp2",
+    "batch_norm_act",
     "node_from_edges", "edge_from_nodes", "att_score", "segment_mean",
     "POLY_LAGUERRE", "POLY_CHEB", "SIGMA_SIGMOID", "SIGMA_RELU",
 ]
@@ -33,7 +40,7 @@ SIGMA_SIGMOID, SIGMA_RELU = _lib.SIGMA_SIGMOID, _lib.SIGMA_RELU
 # helpers
 # ----------------------------------------------------------------------------
 def _stream(t: torch.Tensor) -> int:
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return torch._C._cuda_getCurrentRawStream(t.device.index)
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -305,152 +312,55 @@ def _proj_bwd_weight(G: torch.Tensor, As: List[torch.Tensor], dWs: List[torch.Te
 # ----------------------------------------------------------------------------
 # HodgeLaguerreConv / HodgeChebConv fused forward + hand-written backward
 # ----------------------------------------------------------------------------
-class _HodgePolyConvFn(torch.autograd.Function):
-    """out = sum_k T_k W_k^T + bias with T_k the Laguerre / Chebyshev basis of
-    x over L (lib/Hodge_Cheb_Conv.py:480-515 / :394-439).  x may be [N, C] or
-    [N, T, C] (3-D inputs propagate over [N, T*C] rows, :493-505)."""
+def _bn_args(bn: Optional[torch.nn.BatchNorm1d]):
+    """(weight, bias, running_mean, running_var, num_batches_tracked, momentum,
+    eps) for a training-mode BatchNorm1d, torch semantics."""
+    track = bn.training and bn.track_running_stats and bn.running_mean is not None
+    if track and bn.momentum is None:
+        momentum = 1.0 / float(bn.num_batches_tracked.item() + 1)
+    else:
+        momentum = float(bn.momentum) if bn.momentum is not None else 0.0
+    return (bn.weight, bn.bias, bn.running_mean if track else None,
+            bn.running_var if track else None, bn.num_batches_tracked if track else None,
+            momentum, float(bn.eps))
 
-    @staticmethod
-    def forward(ctx, x, op, kind, bias, *weights):
-        K = len(weights)
-        N = x.size(0)
-        C_in = x.size(-1)
-        xf = x.reshape(N, -1)
-        if xf.stride(-1) != 1:
-            xf = xf.contiguous()
-        F = xf.size(1)
-        T = poly_basis(op, xf, K, kind)  # [K-1, N, F]
-        M = xf.numel() // C_in if N else 0
-        dout = weights[0].size(0)
-        out = torch.empty(M, dout, device=x.device, dtype=x.dtype)
-        As = [xf.reshape(M, C_in)] + [T[k].view(M, C_in) for k in range(K - 1)]
-        if M > 0:
-            _proj_fwd(As, list(weights), M, dout, bias, out)
-        elif bias is not None:
-            out.copy_(bias.expand_as(out))
-        ctx.op, ctx.kind, ctx.K = op, kind, K
-        ctx.shape = (x.shape, N, F, M, C_in, dout)
-        ctx.has_bias = bias is not None
-        ctx.save_for_backward(xf, T, *weights)
-        return out.view(*x.shape[:-1], dout)
 
-    @staticmethod
-    def backward(ctx, gout):
-        xf, T, *weights = ctx.saved_tensors
-        xshape, N, F, M, C_in, dout = ctx.shape
-        K = ctx.K
-        G = gout.reshape(M, dout)
-        if G.stride(-1) != 1 or G.stride(0) != dout:
-            G = G.contiguous()
-        need_x = ctx.needs_input_grad[0]
-        need_b = ctx.has_bias and ctx.needs_input_grad[3]
-        need_w = any(ctx.needs_input_grad[4:])
-        gx = gb = None
-        gws = [None] * K
-        As = [xf.reshape(M, C_in)] + [T[k].view(M, C_in) for k in range(K - 1)]
-        if (need_w or need_b) and M > 0:
-            dWs = [torch.empty_like(w) for w in weights]
-            gb = torch.empty(dout, device=G.device, dtype=G.dtype) if need_b else None
-            _proj_bwd_weight(G, As, dWs, gb)
-            gws = dWs if need_w else gws
-        elif need_w or need_b:
-            gws = [torch.zeros_like(w) for w in weights]
-            gb = torch.zeros(dout, device=G.device, dtype=G.dtype) if need_b else None
-        if need_x:
-            Gs = torch.empty(K, N, F, device=G.device, dtype=G.dtype)
-            if M > 0:
-                _proj_bwd_data(G, list(weights), [C_in] * K,
-                               [Gs[k].view(M, C_in) for k in range(K)])
-                if K > 1:
-                    B = ctx.op.bwd
-                    check(LIB.hlhgat_poly_basis_bwd(
-                        ctx.kind, B.rowptr.data_ptr(), B.col.data_ptr() if B.nnz else None,
-                        _ptr(B.val) if B.nnz else None, N, B.nnz, F, K, Gs.data_ptr(),
-                        _stream(G)), "poly_basis_bwd")
-            else:
-                Gs.zero_()
-            gx = Gs[0].view(xshape)
-        return (gx, None, None, gb, *gws)
+def _bn_uses_batch_stats(bn) -> bool:
+    return bn.training or not bn.track_running_stats
 
 
 def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.Tensor],
-                    bias: Optional[torch.Tensor], kind: int = POLY_LAGUERRE) -> torch.Tensor:
+                    bias: Optional[torch.Tensor], kind: int = POLY_LAGUERRE,
+                    bn: Optional[torch.nn.BatchNorm1d] = None, relu: bool = False
+                    ) -> torch.Tensor:
+    """out = sum_k T_k W_k^T + bias with T_k the Laguerre / Chebyshev basis of
+    x over L (lib/Hodge_Cheb_Conv.py:480-515 / :394-439); x may be [N, C] or
+    [N, T, C] (3-D inputs propagate over [N, T*C] rows, :493-505).  With
+    ``bn`` the following BatchNorm (and ReLU) of the HL block runs inside the
+    same C++ autograd node (lib/Hodge_ST_Model.py:556-566)."""
     _req_dev(x, "x")
-    for w in weights:
-        _req_dev(w, "lins[k].weight")
-        if w.stride(-1) != 1:
-            raise RuntimeError("hlhgat: weights must have unit inner stride")
-    if bias is not None:
-        _req_dev(bias, "bias")
     if x.size(0) != op.fwd.n_rows:
         raise RuntimeError(f"hlhgat: x has {x.size(0)} rows but the operator has "
                            f"{op.fwd.n_rows}")
-    return _HodgePolyConvFn.apply(x, op, kind, bias, *weights)
+    A, At = op.fwd, op.bwd
+    ws = list(weights)
+    if bn is not None and x.dim() == 2 and _bn_uses_batch_stats(bn):
+        if x.size(0) < 2 and bn.training:
+            raise ValueError("Expected more than 1 value per channel when training")
+        return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
+                            ws, bias, *_bn_args(bn), 2 if relu else 1)
+    out = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
+                       bias, None, None, None, None, None, 0.0, 0.0, 0)
+    if bn is not None:
+        out = batch_norm_act(out, bn, relu)
+    elif relu:
+        out = torch.relu(out)
+    return out
 
 
 # ----------------------------------------------------------------------------
 # Linear over a split reduction axis (Linear(cat[a, b]) without the cat)
 # ----------------------------------------------------------------------------
-class _LinearBlocksFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, weight, bias, *As):
-        M = As[0].size(0)
-        N = weight.size(0)
-        offs, Ws = [], []
-        o = 0
-        for a in As:
-            offs.append(o)
-            Ws.append(weight[:, o:o + a.size(1)])
-            o += a.size(1)
-        if o != weight.size(1):
-            raise RuntimeError(f"hlhgat: Linear expects {weight.size(1)} input features, "
-                               f"got {o}")
-        out = torch.empty(M, N, device=weight.device, dtype=weight.dtype)
-        if M > 0:
-            _proj_fwd(list(As), Ws, M, N, bias, out)
-        ctx.has_bias = bias is not None
-        ctx.save_for_backward(weight, *As)
-        return out
-
-    @staticmethod
-    def backward(ctx, gout):
-        weight, *As = ctx.saved_tensors
-        G = gout if (gout.stride(-1) == 1 and gout.stride(0) == gout.size(1)) else gout.contiguous()
-        M, N = G.size(0), G.size(1)
-        kbs = [a.size(1) for a in As]
-        Ws, o = [], 0
-        for k in kbs:
-            Ws.append(weight[:, o:o + k])
-            o += k
-        gw = gb = None
-        need_b = ctx.has_bias and ctx.needs_input_grad[1]
-        if ctx.needs_input_grad[0] or need_b:
-            if M > 0:
-                gw = torch.empty_like(weight)
-                dWs, o = [], 0
-                for k in kbs:
-                    dWs.append(gw[:, o:o + k])
-                    o += k
-                gb = torch.empty(N, device=G.device, dtype=G.dtype) if need_b else None
-                _proj_bwd_weight(G, list(As), dWs, gb)
-            else:
-                gw = torch.zeros_like(weight)
-                gb = torch.zeros(N, device=G.device, dtype=G.dtype) if need_b else None
-            if not ctx.needs_input_grad[0]:
-                gw = None
-        gAs = [None] * len(As)
-        need_a = [ctx.needs_input_grad[2 + i] for i in range(len(As))]
-        if any(need_a) and M > 0:
-            idx = [i for i in range(len(As)) if need_a[i]]
-            outs = [torch.empty(M, kbs[i], device=G.device, dtype=G.dtype) for i in idx]
-            _proj_bwd_data(G, [Ws[i] for i in idx], [kbs[i] for i in idx], outs)
-            for i, t in zip(idx, outs):
-                gAs[i] = t
-        elif any(need_a):
-            gAs = [torch.zeros_like(a) if n else None for a, n in zip(As, need_a)]
-        return (gw, gb, *gAs)
-
-
 def linear_blocks(As: Sequence[torch.Tensor], weight: torch.Tensor,
                   bias: Optional[torch.Tensor]) -> torch.Tensor:
     """F.linear(cat(As, -1), weight, bias) with the concatenation folded into
@@ -458,71 +368,21 @@ def linear_blocks(As: Sequence[torch.Tensor], weight: torch.Tensor,
     if len(As) > _lib.MAX_BLOCKS:
         raise RuntimeError(f"hlhgat: at most {_lib.MAX_BLOCKS} operand blocks")
     _req_dev(weight, "weight")
-    if weight.stride(-1) != 1:
-        weight = weight.contiguous()
-    fixed = []
-    for a in As:
-        _req_dev(a, "input")
-        fixed.append(_rows2d(a, "input"))
-    return _LinearBlocksFn.apply(weight, bias, *fixed)
+    return _ext.linear(list(As), weight, bias)
+
+
+def mlp2(blocks: Sequence[torch.Tensor], seq: torch.nn.Sequential) -> torch.Tensor:
+    """NodeEdgeInt WV_* (Linear(2d, dl) -> BN -> ReLU -> Linear(dl, dv) -> BN ->
+    ReLU, lib/Hodge_Cheb_Conv.py:276-289) on cat(blocks) as one C++ node."""
+    lin0, bn1, _, lin3, bn4, _ = list(seq)
+    return _ext.mlp2(list(blocks), lin0.weight, lin0.bias, *_bn_args(bn1)[:5], lin3.weight,
+                     lin3.bias, *_bn_args(bn4)[:5], _bn_args(bn1)[5], float(bn1.eps),
+                     _bn_args(bn4)[5], float(bn4.eps))
 
 
 # ----------------------------------------------------------------------------
 # boundary operator: x_s2t = (1/D) |B1| x_s ; x_t2s = |B1|^T x_t / 2
 # ----------------------------------------------------------------------------
-class _NodeFromEdgesFn(torch.autograd.Function):
-    """x_s2t = (1/D).view(-1,1) * (|B1| @ x_s)   (lib/Hodge_Cheb_Conv.py:294)."""
-
-    @staticmethod
-    def forward(ctx, x_s, inc, rD):
-        out = torch.empty(inc.n_nodes, x_s.size(1), device=x_s.device, dtype=x_s.dtype)
-        A = SparseCSR(inc.rowptr, inc.edge_ids, None, inc.n_nodes, inc.n_edges, 2 * inc.n_edges)
-        if inc.n_nodes:
-            _poly_step(A, x_s, out, rs=rD)
-        ctx.inc = inc
-        ctx.save_for_backward(rD)
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        (rD,) = ctx.saved_tensors
-        inc = ctx.inc
-        g = _rows2d(g, "grad")
-        gx = torch.empty(inc.n_edges, g.size(1), device=g.device, dtype=g.dtype)
-        if inc.n_edges:
-            # d x_s[e] = rD[i] g[i] + rD[j] g[j]
-            check(LIB.hlhgat_edge_gather2(inc.edge_index.data_ptr(), inc.n_edges, g.data_ptr(),
-                                          _ld(g), g.size(1), rD.data_ptr(), rD.data_ptr(),
-                                          1.0, 1.0, gx.data_ptr(), _ld(gx), 0, _stream(g)),
-                  "edge_gather2")
-        return gx, None, None
-
-
-class _EdgeFromNodesFn(torch.autograd.Function):
-    """x_t2s = (|B1|^T @ x_t) / 2   (lib/Hodge_Cheb_Conv.py:295)."""
-
-    @staticmethod
-    def forward(ctx, x_t, inc):
-        out = torch.empty(inc.n_edges, x_t.size(1), device=x_t.device, dtype=x_t.dtype)
-        if inc.n_edges:
-            check(LIB.hlhgat_edge_gather2(inc.edge_index.data_ptr(), inc.n_edges, x_t.data_ptr(),
-                                          _ld(x_t), x_t.size(1), None, None, 0.5, 0.5,
-                                          out.data_ptr(), _ld(out), 0, _stream(x_t)),
-                  "edge_gather2")
-        ctx.inc = inc
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        inc = ctx.inc
-        g = _rows2d(g, "grad")
-        gx = torch.empty(inc.n_nodes, g.size(1), device=g.device, dtype=g.dtype)
-        A = SparseCSR(inc.rowptr, inc.edge_ids, None, inc.n_nodes, inc.n_edges, 2 * inc.n_edges)
-        if inc.n_nodes:
-            _poly_step(A, g, gx, alpha=0.5)
-        return gx, None
-
-
 def node_from_edges(x_s: torch.Tensor, inc: Incidence, rD: torch.Tensor) -> torch.Tensor:
     _req_dev(x_s, "x_s")
     _req_dev(rD, "1/D")
@@ -530,14 +390,15 @@ def node_from_edges(x_s: torch.Tensor, inc: Incidence, rD: torch.Tensor) -> torc
         raise RuntimeError(f"hlhgat: x_s has {x_s.size(0)} rows, |B1| has {inc.n_edges} edges")
     if rD.numel() != inc.n_nodes:
         raise RuntimeError(f"hlhgat: D has {rD.numel()} entries, |B1| has {inc.n_nodes} nodes")
-    return _NodeFromEdgesFn.apply(_rows2d(x_s, "x_s"), inc, rD.contiguous().view(-1))
+    return _ext.node_from_edges(x_s, inc.rowptr, inc.edge_ids, inc.edge_index,
+                                rD.contiguous().view(-1), inc.n_nodes)
 
 
 def edge_from_nodes(x_t: torch.Tensor, inc: Incidence) -> torch.Tensor:
     _req_dev(x_t, "x_t")
     if x_t.size(0) != inc.n_nodes:
         raise RuntimeError(f"hlhgat: x_t has {x_t.size(0)} rows, |B1| has {inc.n_nodes} nodes")
-    return _EdgeFromNodesFn.apply(_rows2d(x_t, "x_t"), inc)
+    return _ext.edge_from_nodes(x_t, inc.rowptr, inc.edge_ids, inc.edge_index)
 
 
 # ----------------------------------------------------------------------------
@@ -623,58 +484,6 @@ def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,
 # ----------------------------------------------------------------------------
 # BatchNorm1d (training statistics) + optional fused ReLU
 # ----------------------------------------------------------------------------
-_BN_WS = {}
-
-
-def _bn_workspace(device: torch.device, n: int, C: int) -> torch.Tensor:
-    """Persistent zero-initialised scratch per device (the kernels leave their
-    arrival counters at zero, so it is reused by every BN launch on the
-    stream)."""
-    need = int(LIB.hlhgat_bn_workspace_bytes(n, C))
-    key = (device.type, device.index)
-    ws = _BN_WS.get(key)
-    if ws is None or ws.numel() < need:
-        ws = torch.zeros(max(need, 1 << 20), dtype=torch.uint8, device=device)
-        _BN_WS[key] = ws
-    return ws
-
-
-class _BatchNormActFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum, eps, relu):
-        n, C = x.shape
-        y = torch.empty(n, C, device=x.device, dtype=x.dtype)
-        mean = torch.empty(C, device=x.device, dtype=torch.float32)
-        invstd = torch.empty(C, device=x.device, dtype=torch.float32)
-        ws = _bn_workspace(x.device, n, C)
-        check(LIB.hlhgat_bn_fwd_train(x.data_ptr(), _ld(x), n, C, _ptr(weight), _ptr(bias),
-                                      _ptr(running_mean), _ptr(running_var), _ptr(nbt),
-                                      momentum, eps, int(relu), y.data_ptr(), _ld(y),
-                                      mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(),
-                                      ws.numel(), _stream(x)), "bn_fwd_train")
-        ctx.relu = relu
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
-        dy = _rows2d(dy, "grad")
-        n, C = x.shape
-        dx = torch.empty(n, C, device=x.device, dtype=x.dtype)
-        need_w = weight is not None and ctx.needs_input_grad[1]
-        need_b = ctx.needs_input_grad[2]
-        dw = torch.empty(C, device=x.device, dtype=x.dtype) if need_w else None
-        db = torch.empty(C, device=x.device, dtype=x.dtype) if need_b else None
-        ws = _bn_workspace(x.device, n, C)
-        check(LIB.hlhgat_bn_bwd_train(x.data_ptr(), _ld(x), _ptr(y), _ld(y) if y is not None else 0,
-                                      dy.data_ptr(), _ld(dy), n, C, _ptr(weight), mean.data_ptr(),
-                                      invstd.data_ptr(), dx.data_ptr(), _ld(dx), _ptr(dw),
-                                      _ptr(db), ws.data_ptr(), ws.numel(), _stream(x)),
-              "bn_bwd_train")
-        return dx, dw, db, None, None, None, None, None, None
-
-
 def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False) -> torch.Tensor:
     """bn(x) followed by ReLU when ``relu``; training mode (or no running
     stats) uses the HIP batch-statistics kernels, eval mode the running
@@ -690,15 +499,7 @@ def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False
     if x.size(0) < 2 and bn.training:
         raise ValueError(f"Expected more than 1 value per channel when training, got input "
                          f"size {tuple(x.shape)}")
-    track = bn.training and bn.track_running_stats and bn.running_mean is not None
-    if track and bn.momentum is None:
-        momentum = 1.0 / float(bn.num_batches_tracked.item() + 1)
-    else:
-        momentum = float(bn.momentum) if bn.momentum is not None else 0.0
-    return _BatchNormActFn.apply(
-        _rows2d(x, "x"), bn.weight, bn.bias, bn.running_mean if track else None,
-        bn.running_var if track else None, bn.num_batches_tracked if track else None,
-        momentum, float(bn.eps), bool(relu))
+    return _ext.bn_act(x, *_bn_args(bn), bool(relu))
 
 
 # ----------------------------------------------------------------------------

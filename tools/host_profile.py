@@ -19,7 +19,7 @@ def main():
     batches = bench.make_batches(2, 0, dev)
     torch.manual_seed(0)
     model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**bench.MODEL_KW).to(dev).train()
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-3)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-3, fused=True)
     crit = torch.nn.L1Loss()
 
     def step(i):
