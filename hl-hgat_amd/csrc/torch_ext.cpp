@@ -52,6 +52,25 @@ inline void req(const Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kFloat, "hlhgat: ", name, " must be float32");
 }
 
+// Argument position -> autograd edge index.  In C++ custom functions
+// needs_input_grad() indexes EDGES: a Tensor argument is always an edge, an
+// optional<Tensor> only when defined, each TensorList element is one, and any
+// other argument none.  Backward still returns one gradient per position.
+struct EdgeMap {
+  std::vector<int64_t> e;
+  int64_t n = 0;
+  void tensor() { e.push_back(n++); }
+  void opt(const OptT& t) { e.push_back(has(t) ? n++ : -1); }
+  void list(at::TensorList l) {
+    for (size_t i = 0; i < l.size(); ++i) e.push_back(n++);
+  }
+  void other() { e.push_back(-1); }
+};
+inline bool need(AutogradContext* ctx, int64_t pos) {
+  const auto em = ctx->saved_data["edges"].toIntVector();
+  return pos < (int64_t)em.size() && em[pos] >= 0 && ctx->needs_input_grad(em[pos]);
+}
+
 // ---------------------------------------------------------------------------
 // raw launches
 // ---------------------------------------------------------------------------
@@ -199,6 +218,29 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, Cin, F, M, dout, K, kind, nnz, bn_mode,
                                                    has(bias) ? 1 : 0};
+    {
+      EdgeMap em;
+      em.tensor();  // x
+      em.tensor();
+      em.tensor();
+      em.opt(a_val);
+      em.tensor();
+      em.tensor();
+      em.opt(t_val);
+      em.other();
+      em.other();
+      em.list(W);
+      em.opt(bias);
+      em.opt(bn_w);
+      em.opt(bn_b);
+      em.opt(bn_rm);
+      em.opt(bn_rv);
+      em.opt(bn_nbt);
+      em.other();
+      em.other();
+      em.other();
+      ctx->saved_data["edges"] = em.e;
+    }
     ctx->saved_data["xshape"] = x.sizes().vec();
     std::vector<Tensor> save = {x2,
                                 T,
@@ -234,13 +276,13 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
     const int64_t n_pos = 18 + K;
     variable_list out(n_pos);
-    const bool need_x = ctx->needs_input_grad(0);
+    const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
     if (bn_mode > 0) {
       OptT y = bn_mode == 2 ? OptT(yout) : OptT();
       OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-      G = bn_backward(pre, y, G, w, mean, invstd, ctx->needs_input_grad(10 + K),
-                      ctx->needs_input_grad(11 + K), dbn_w, dbn_b);
+      G = bn_backward(pre, y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K), dbn_w,
+                      dbn_b);
       out[10 + K] = dbn_w;
       out[11 + K] = dbn_b;
     }
@@ -253,8 +295,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       lda[k] = Cin;
     }
     bool need_w = false;
-    for (int64_t k = 0; k < K; ++k) need_w = need_w || ctx->needs_input_grad(9 + k);
-    const bool need_b = has_bias && ctx->needs_input_grad(9 + K);
+    for (int64_t k = 0; k < K; ++k) need_w = need_w || need(ctx, 9 + k);
+    const bool need_b = has_bias && need(ctx, 9 + K);
     if (need_w || need_b) {
       std::vector<Tensor> dW(K);
       std::vector<float*> dWp(K);
@@ -272,7 +314,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
         if (need_b) db.zero_();
       }
       for (int64_t k = 0; k < K; ++k)
-        if (ctx->needs_input_grad(9 + k)) out[9 + k] = dW[k];
+        if (need(ctx, 9 + k)) out[9 + k] = dW[k];
       if (need_b) out[9 + K] = db;
     }
     if (need_x) {
@@ -316,6 +358,14 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
     BnState st{w, b, rm, rv, nbt, momentum, eps};
     Tensor y = bn_forward(xc, st, relu, mean, invstd);
     ctx->saved_data["relu"] = relu;
+    EdgeMap em;
+    em.tensor();
+    em.opt(w);
+    em.opt(b);
+    em.opt(rm);
+    em.opt(rv);
+    em.opt(nbt);
+    ctx->saved_data["edges"] = em.e;
     ctx->save_for_backward({xc, relu ? y : Tensor(), has(w) ? *w : Tensor(), mean, invstd});
     return y;
   }
@@ -324,8 +374,8 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
     Tensor dw, db;
     OptT y = sv[1].defined() ? OptT(sv[1]) : OptT();
     OptT w = sv[2].defined() ? OptT(sv[2]) : OptT();
-    Tensor dx = bn_backward(sv[0], y, grads[0], w, sv[3], sv[4], ctx->needs_input_grad(1),
-                           ctx->needs_input_grad(2), dw, db);
+    Tensor dx = bn_backward(sv[0], y, grads[0], w, sv[3], sv[4], need(ctx, 1), need(ctx, 2), dw,
+                           db);
     return {dx, dw, db, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
 };
@@ -423,6 +473,11 @@ class LinearFn : public torch::autograd::Function<LinearFn> {
     Tensor Wc = W.stride(1) == 1 ? W : W.contiguous();
     Tensor out = linear_forward(As, Wc, b);
     ctx->saved_data["has_b"] = has(b);
+    EdgeMap em;
+    em.tensor();
+    em.opt(b);
+    em.list(As_in);
+    ctx->saved_data["edges"] = em.e;
     std::vector<Tensor> save = {Wc};
     save.insert(save.end(), As.begin(), As.end());
     ctx->save_for_backward(save);
@@ -433,12 +488,10 @@ class LinearFn : public torch::autograd::Function<LinearFn> {
     Tensor W = sv[0];
     std::vector<Tensor> As(sv.begin() + 1, sv.end());
     std::vector<bool> need_a(As.size());
-    for (size_t i = 0; i < As.size(); ++i) need_a[i] = ctx->needs_input_grad(2 + i);
+    for (size_t i = 0; i < As.size(); ++i) need_a[i] = need(ctx, 2 + (int64_t)i);
     Tensor dW, db;
     std::vector<Tensor> dAs;
-    linear_backward(grads[0], As, W, ctx->needs_input_grad(0),
-                    ctx->saved_data["has_b"].toBool() && ctx->needs_input_grad(1), need_a, dW, db,
-                    dAs);
+    linear_backward(grads[0], As, W, need(ctx, 0), need(ctx, 1), need_a, dW, db, dAs);
     variable_list out = {dW, db};
     out.insert(out.end(), dAs.begin(), dAs.end());
     return out;
@@ -467,6 +520,26 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     Tensor h2 = linear_forward({a1}, W3c, b3);
     Tensor y = bn_forward(h2, BnState{g4, be4, rm4, rv4, nbt4, mom4, eps4}, true, m4, i4);
     ctx->saved_data["nb"] = (int64_t)blocks.size();
+    {
+      EdgeMap em;
+      em.list(blocks_in);
+      em.tensor();  // W0
+      em.opt(b0);
+      em.opt(g1);
+      em.opt(be1);
+      em.opt(rm1);
+      em.opt(rv1);
+      em.opt(nbt1);
+      em.tensor();  // W3
+      em.opt(b3);
+      em.opt(g4);
+      em.opt(be4);
+      em.opt(rm4);
+      em.opt(rv4);
+      em.opt(nbt4);
+      for (int i = 0; i < 4; ++i) em.other();
+      ctx->saved_data["edges"] = em.e;
+    }
     ctx->saved_data["has_b0"] = has(b0);
     ctx->saved_data["has_b3"] = has(b3);
     std::vector<Tensor> save = {W0c, h1, a1, m1, i1, has(g1) ? *g1 : Tensor(), W3c, h2, y, m4, i4,
@@ -487,27 +560,25 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     variable_list out(nb + 18);
     Tensor dg4, dbe4, dg1, dbe1;
     Tensor dh2 = bn_backward(h2, OptT(y), grads[0], g4.defined() ? OptT(g4) : OptT(), m4, i4,
-                             ctx->needs_input_grad(P + 9), ctx->needs_input_grad(P + 10), dg4,
+                             need(ctx, P + 9), need(ctx, P + 10), dg4,
                              dbe4);
     out[P + 9] = dg4;
     out[P + 10] = dbe4;
     Tensor dW3, db3, dW0, db0;
     std::vector<Tensor> da1;
-    linear_backward(dh2, {a1}, W3, ctx->needs_input_grad(P + 7),
-                    ctx->saved_data["has_b3"].toBool() && ctx->needs_input_grad(P + 8), {true},
+    linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true},
                     dW3, db3, da1);
     out[P + 7] = dW3;
     out[P + 8] = db3;
     Tensor dh1 = bn_backward(h1, OptT(a1), da1[0], g1.defined() ? OptT(g1) : OptT(), m1, i1,
-                             ctx->needs_input_grad(P + 2), ctx->needs_input_grad(P + 3), dg1,
+                             need(ctx, P + 2), need(ctx, P + 3), dg1,
                              dbe1);
     out[P + 2] = dg1;
     out[P + 3] = dbe1;
     std::vector<bool> need_a(nb);
-    for (int64_t i = 0; i < nb; ++i) need_a[i] = ctx->needs_input_grad(i);
+    for (int64_t i = 0; i < nb; ++i) need_a[i] = need(ctx, i);
     std::vector<Tensor> dblocks;
-    linear_backward(dh1, blocks, W0, ctx->needs_input_grad(P),
-                    ctx->saved_data["has_b0"].toBool() && ctx->needs_input_grad(P + 1), need_a,
+    linear_backward(dh1, blocks, W0, need(ctx, P), need(ctx, P + 1), need_a,
                     dW0, db0, dblocks);
     out[P] = dW0;
     out[P + 1] = db0;
