@@ -638,6 +638,100 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
   }
 }
 
+// Weight gradient, vector path (all operands 16-B aligned, widths % 4 == 0):
+// a workgroup owns a 64(n) x 64(k) tile and one M-slice; 32-row chunks of dC
+// and A_b are staged in LDS with coalesced float4 loads (double buffered) and
+// each wave accumulates one 32x32 quadrant with v_mfma_f32_32x32x2_f32:
+// lane l supplies dC[m0 + (l>>5)][n = 32wn + (l&31)] and
+// A_b[m0 + (l>>5)][k = 32wk + (l&31)] — row-contiguous ds_read_b32, no bank
+// conflicts, and no cross-wave reduction.  Partials go to the split slab.
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int WR = 32;  // rows per staged chunk
+
+__global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
+  __shared__ float gl[2][WR][64];
+  __shared__ float al[2][WR][64];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wn = wave >> 1, wk = wave & 1;
+  int b = 0;
+  while (b + 1 < a.nb && (int)blockIdx.y >= a.tile_start[b + 1]) ++b;
+  const int t = (int)blockIdx.y - a.tile_start[b];
+  const int n_base = (t % a.tiles_n) * 64;
+  const int k_base = (t / a.tiles_n) * 64;
+  const int kb = a.kb[b];
+  const float* __restrict__ A = a.A[b];
+  const int64_t lda = a.lda[b];
+  const bool do_bias = a.bias_off >= 0 && b == 0 && k_base == 0;
+  const int64_t m_lo = (int64_t)blockIdx.z * a.rows_per_split;
+  int64_t m_hi = m_lo + a.rows_per_split;
+  if (m_hi > a.M) m_hi = a.M;
+
+  // staging: each tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
+  const int sr = threadIdx.x >> 4, sc = (threadIdx.x & 15) * 4;
+  auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t m = m0 + sr + 16 * u;
+      const bool mv = m < m_hi;
+      const int n = n_base + sc, k = k_base + sc;
+      g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[u] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int buf, const float4 (&g)[2], const float4 (&x)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      *reinterpret_cast<float4*>(&gl[buf][sr + 16 * u][sc]) = g[u];
+      *reinterpret_cast<float4*>(&al[buf][sr + 16 * u][sc]) = x[u];
+    }
+  };
+
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bsum = 0.f;
+  const int rl = lane >> 5, cl = lane & 31;
+  float4 g[2], x[2];
+  int buf = 0;
+  if (m_lo < m_hi) {
+    load(m_lo, g, x);
+    store(0, g, x);
+  }
+  __syncthreads();
+  for (int64_t m0 = m_lo; m0 < m_hi; m0 += WR) {
+    const bool has_next = m0 + WR < m_hi;
+    if (has_next) load(m0 + WR, g, x);
+#pragma unroll
+    for (int kk = 0; kk < WR / 2; ++kk) {
+      const float av = gl[buf][2 * kk + rl][32 * wn + cl];
+      const float bv = al[buf][2 * kk + rl][32 * wk + cl];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      bsum = bsum + av;
+    }
+    if (has_next) store(buf ^ 1, g, x);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  float* slab = a.part + (int64_t)blockIdx.z * a.part_stride + a.part_off[b];
+  const int k = k_base + 32 * wk + cl;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n_base + 32 * wn + (r & 3) + 8 * (r >> 2) + 4 * rl;
+    if (n < a.N && k < kb) slab[(int64_t)n * kb + k] = acc[r];
+  }
+  if (do_bias && wk == 0) {
+    // lanes l and l+32 hold partial column sums of n = n_base + 32wn + (l&31)
+    const float tot = bsum + __shfl_xor(bsum, 32, 64);
+    const int n = n_base + 32 * wn + cl;
+    if (rl == 0 && n < a.N)
+      a.part[(int64_t)blockIdx.z * a.part_stride + a.bias_off + n] = tot;
+  }
+}
+
 struct ReduceArgs {
   int nb;
   int N;
@@ -720,9 +814,10 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   if (with_bias) off += N;
   p.part_stride = off;
   p.tiles_total = p.tile_start[nb];
-  // aim for ~768 workgroups (3 per CU), each slice >= 256 rows
-  int64_t splits = ceil_div(768, p.tiles_total > 0 ? p.tiles_total : 1);
-  int64_t max_splits = ceil_div(M, 256);
+  // aim for ~384 workgroups (1.5 per CU), each slice >= 128 rows: balances
+  // MFMA parallelism against the split-slab traffic the reduce re-reads
+  int64_t splits = ceil_div(384, p.tiles_total > 0 ? p.tiles_total : 1);
+  int64_t max_splits = ceil_div(M, 128);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int64_t rps = ceil_div(M, splits);
@@ -909,7 +1004,13 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
     return HLHGAT_OK;
   }
   dim3 grid(1, (unsigned)p.tiles_total, (unsigned)p.splits);
-  k_proj_bwd_weight<<<grid, 256, 0, s>>>(a);
+  bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
+  for (int b = 0; b < nblocks; ++b)
+    vec = vec && aligned16(A[b]) && (lda[b] % 4) == 0 && (kb[b] % 4) == 0;
+  if (vec)
+    k_proj_bwd_weight32<<<grid, 256, 0, s>>>(a);
+  else
+    k_proj_bwd_weight<<<grid, 256, 0, s>>>(a);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
