@@ -87,24 +87,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+    from hlhgat.distributed import init_distributed, max_over_ranks, wrap_ddp
+    rank, world, device = init_distributed("nccl")  # RCCL over xGMI; one process per GPU
 
     import hlhgat
     from hlhgat import ops
 
     log(f"[rank {rank}] generating {args.batches} x {GRAPHS_PER_GPU} synthetic graphs")
-    batches = make_batches(args.batches, rank, device)
+    batches = make_batches(args.batches, rank, device)  # each rank: its own graphs
     torch.manual_seed(0)
     model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**MODEL_KW).to(device).train()
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(
-            model, device_ids=[local], bucket_cap_mb=32, gradient_as_bucket_view=True)
+    model = wrap_ddp(model, device)  # gradient all-reduce = the only exchange step
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-3, fused=True)
     crit = torch.nn.L1Loss()
 
@@ -138,10 +131,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ops.prof_enable(hlhgat._lib.PROF_POLY, False)
     ops.prof_enable(hlhgat._lib.PROF_PROJ, False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = max_over_ranks(elapsed, device)
 
     poly = ops.prof_read(hlhgat._lib.PROF_POLY)
     proj = ops.prof_read(hlhgat._lib.PROF_PROJ)

@@ -1,0 +1,89 @@
+"""Data parallelism for HL-HGAT: shard batches BY GRAPH, all-reduce gradients.
+
+The reference is single-device ('cuda:0' hard-coded).
+Simplex graphs are independent units (block-diagonal L0 / L1 / B1,
+lib/Hodge_Dataset.py:40-48), so each rank owns whole graphs and the only
+exchange step is the per-step gradient all-reduce (torch DDP over RCCL /
+xGMI; backend "nccl" is RCCL on ROCm).  One graph never spans GPUs.
+
+BatchNorm statistics stay per rank by default (like the reference's per-batch
+statistics, computed on each rank's shard); SURVEY.md §8e notes the exact-
+parity caveats.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["world_info", "shard_range", "shard_graphs", "shard_by_weight", "init_distributed",
+           "wrap_ddp", "max_over_ranks"]
+
+
+def world_info() -> Tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, balanced [lo, hi) share of n items (sizes differ by <= 1)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def shard_graphs(graphs: Sequence, rank: int, world: int) -> List:
+    lo, hi = shard_range(len(graphs), rank, world)
+    return list(graphs[lo:hi])
+
+
+def shard_by_weight(weights: Sequence[float], world: int) -> List[List[int]]:
+    """Greedy longest-processing-time assignment of items (e.g. graphs by
+    nnz(L1), for the TSP config where graph sizes differ) to ranks."""
+    order = sorted(range(len(weights)), key=lambda i: -weights[i])
+    loads = [0.0] * world
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda j: (loads[j], j))
+        out[r].append(i)
+        loads[r] += weights[i]
+    return [sorted(o) for o in out]
+
+
+def init_distributed(backend: str = None) -> Tuple[int, int, torch.device]:
+    """Initialise the process group (RCCL on GPU, gloo on CPU); one process
+    per GPU.  Returns (rank, world, device)."""
+    rank, world, local = world_info()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        kw = {"device_id": device} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return rank, world, device
+
+
+def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 32):
+    """DistributedDataParallel with one gradient bucket per ~32 MB: the whole
+    0.6-16 MB gradient of the SURVEY configs fits in one or two ring
+    all-reduces over the 7 xGMI links."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return model
+    ids = [device.index] if device.type == "cuda" else None
+    return torch.nn.parallel.DistributedDataParallel(
+        model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+
+
+def max_over_ranks(value: float, device: torch.device = torch.device("cpu")) -> float:
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
