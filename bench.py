@@ -1,14 +1,18 @@
 """HL-HGAT training throughput on MI355X (BASELINE.json metric, config 2).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--eager]
     (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
 
 A step = one training step of HL_HGCNN_zinc_dense_int3_pyr(channels=[2,2,2],
 filters=[64,64,64], mlp=[256,256], K=3, keig=15) on a 1000-graph batch of
-synthetic ZINC-like simplex graphs per GPU (weak scaling): CSR / incidence
-construction for the batch, forward, L1 loss, backward, Adam step.  Inputs
-are resident in HBM before the timed region (several distinct batches,
-rotated).  Rank 0 prints one JSON line.
+synthetic ZINC-like simplex graphs per GPU (weak scaling): the batch is
+copied into the step's static buffers, CSR / incidence construction for the
+batch, forward, L1 loss, backward, gradient all-reduce (N > 1) and Adam.
+Inputs are resident in HBM before the timed region (several distinct
+batches, rotated).  The step runs as a replayed hipGraph per batch shape
+(hlhgat.train.TrainStep; --eager runs it op by op).  After the timed region
+a short eager pass with hipExtLaunchKernel event stamps on the SpMM and the
+projection kernels gives the roofline figures.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -82,56 +86,59 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--batches", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph replay")
+    ap.add_argument("--prof-steps", type=int, default=3,
+                    help="eager steps with kernel event stamps for the roofline")
     args = ap.parse_args()
 
-    from hlhgat.distributed import init_distributed, max_over_ranks, wrap_ddp
+    from hlhgat.distributed import init_distributed, max_over_ranks
     rank, world, device = init_distributed("nccl")  # RCCL over xGMI; one process per GPU
 
     import hlhgat
     from hlhgat import ops
+    from hlhgat.train import TrainStep
 
     log(f"[rank {rank}] generating {args.batches} x {GRAPHS_PER_GPU} synthetic graphs")
     batches = make_batches(args.batches, rank, device)  # each rank: its own graphs
     torch.manual_seed(0)
     model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**MODEL_KW).to(device).train()
-    model = wrap_ddp(model, device)  # gradient all-reduce = the only exchange step
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-3, fused=True)
     crit = torch.nn.L1Loss()
 
-    def step(i):
-        b = batches[i % len(batches)]
-        ops.clear_caches()  # CSR / incidence built per step, as for a fresh batch
-        out = model(b)
-        loss = crit(out.view(-1, 1), b.y.view(-1, 1))
-        loss.backward()
-        opt.step()
-        opt.zero_grad(set_to_none=True)
-        return loss
+    def loss_fn(out, b):
+        return crit(out.view(-1, 1), b.y.view(-1, 1))
+
+    # flat params + one-bucket gradient all-reduce (the only exchange step)
+    step = TrainStep(model, loss_fn, lr=1e-3, weight_decay=1e-3, graphs=not args.eager)
 
     for i in range(args.warmup):
-        step(i)
+        step(batches[i % len(batches)])
     torch.cuda.synchronize()
-    log(f"[rank {rank}] warmup done")
+    log(f"[rank {rank}] warmup done {step.stats}")
 
-    ops.prof_reset()
-    ops.prof_enable(hlhgat._lib.PROF_POLY, True)
-    ops.prof_enable(hlhgat._lib.PROF_PROJ, True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(batches[i % len(batches)])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, device)
+
+    # roofline pass: eager steps, SpMM / projection launches event-stamped
+    ops.prof_reset()
+    ops.prof_enable(hlhgat._lib.PROF_POLY, True)
+    ops.prof_enable(hlhgat._lib.PROF_PROJ, True)
+    for i in range(args.prof_steps):
+        step._eager(batches[i % len(batches)])
+    torch.cuda.synchronize()
     ops.prof_enable(hlhgat._lib.PROF_POLY, False)
     ops.prof_enable(hlhgat._lib.PROF_PROJ, False)
-    elapsed = max_over_ranks(elapsed, device)
 
     poly = ops.prof_read(hlhgat._lib.PROF_POLY)
     proj = ops.prof_read(hlhgat._lib.PROF_PROJ)
@@ -144,6 +151,8 @@ def main():
     poly_gbs = gbs(poly)
     roofline = {
         "kernel": "k_poly_step (CSR SpMM / fused Laguerre step, fwd + adjoint)",
+        "measured": f"hipExtLaunchKernel start/stop stamps, {args.prof_steps} eager steps after "
+                    f"the timed region",
         "bound": "hbm", "achieved": round(poly_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(poly_gbs / HBM_PEAK_GBS, 4), "traffic": None,
         "launches": poly["launches"],
@@ -159,7 +168,10 @@ def main():
         "data": "synthetic ZINC-like simplex graphs (random-init weights; no dataset offline)",
         "config": {"workload": "BASELINE configs[1]: ZINC-12k-scale, HL_HGCNN_zinc_dense_int3_pyr "
                                "channels=[2,2,2] filters=[64,64,64] K=3 mlp=[256,256] keig=15; "
-                               "step = CSR build + fwd + L1 + bwd + Adam",
+                               "step = batch copy-in + CSR build + fwd + L1 + bwd "
+                               "(+ grad all-reduce) + Adam",
+                   "execution": "eager" if args.eager else "hipGraph replay per batch shape "
+                                "(captured during warmup), node/edge chains on 2 streams",
                    "graphs_per_gpu": GRAPHS_PER_GPU, "global_batch": world * GRAPHS_PER_GPU,
                    "parallelism": f"dp{world}"},
         "roofline": roofline,

@@ -232,33 +232,33 @@ int pick_lpr(int64_t d, int v) {
   return l > 64 ? 64 : l;
 }
 
-#define HLH_DISPATCH_VL(V, L, KERNEL, GRID_ROWS, STREAM, ARGS)                 \
+#define HLH_DISPATCH_VL(V, L, KERNEL, GRID_ROWS, STREAM, ARGS, PROF)           \
   do {                                                                         \
     const int64_t _rows_per_block = 256 / (L);                                 \
     const unsigned _grid = (unsigned)ceil_div((GRID_ROWS), _rows_per_block);   \
     if (_grid == 0) break;                                                     \
     switch ((V) * 100 + (L)) {                                                 \
-      case 101: KERNEL<1, 1><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 102: KERNEL<1, 2><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 104: KERNEL<1, 4><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 108: KERNEL<1, 8><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 116: KERNEL<1, 16><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 132: KERNEL<1, 32><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 164: KERNEL<1, 64><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 201: KERNEL<2, 1><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 202: KERNEL<2, 2><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 204: KERNEL<2, 4><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 208: KERNEL<2, 8><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 216: KERNEL<2, 16><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 232: KERNEL<2, 32><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 264: KERNEL<2, 64><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 401: KERNEL<4, 1><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 402: KERNEL<4, 2><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 404: KERNEL<4, 4><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 408: KERNEL<4, 8><<<_grid, 256, 0, STREAM>>>(ARGS); break;          \
-      case 416: KERNEL<4, 16><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 432: KERNEL<4, 32><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
-      case 464: KERNEL<4, 64><<<_grid, 256, 0, STREAM>>>(ARGS); break;         \
+      case 101: launch(KERNEL<1, 1>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 102: launch(KERNEL<1, 2>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 104: launch(KERNEL<1, 4>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 108: launch(KERNEL<1, 8>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 116: launch(KERNEL<1, 16>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 132: launch(KERNEL<1, 32>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 164: launch(KERNEL<1, 64>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 201: launch(KERNEL<2, 1>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 202: launch(KERNEL<2, 2>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 204: launch(KERNEL<2, 4>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 208: launch(KERNEL<2, 8>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 216: launch(KERNEL<2, 16>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 232: launch(KERNEL<2, 32>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 264: launch(KERNEL<2, 64>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 401: launch(KERNEL<4, 1>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 402: launch(KERNEL<4, 2>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 404: launch(KERNEL<4, 4>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 408: launch(KERNEL<4, 8>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 416: launch(KERNEL<4, 16>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 432: launch(KERNEL<4, 32>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
+      case 464: launch(KERNEL<4, 64>, _grid, 256, 0, STREAM, PROF, ARGS); break; \
       default: break;                                                          \
     }                                                                          \
   } while (0)
@@ -295,7 +295,7 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
   const int l = pick_lpr(a.d, v);
   ProfScope prof(HLHGAT_PROF_POLY, s, poly_bytes(a, nnz),
                  2.0 * (double)nnz * a.d);
-  HLH_DISPATCH_VL(v, l, k_poly_step, a.n_rows, s, a);
+  HLH_DISPATCH_VL(v, l, k_poly_step, a.n_rows, s, a, &prof);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -458,7 +458,7 @@ extern "C" int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
   const int v = pick_vec(d, {ldx, ldo}, {x, out});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
-  HLH_DISPATCH_VL(v, l, k_edge_gather2, n_edges, s, a);
+  HLH_DISPATCH_VL(v, l, k_edge_gather2, n_edges, s, a, nullptr);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -475,7 +475,7 @@ extern "C" int hlhgat_segment_mean_fwd(const int32_t* seg_ptr,
   const int v = pick_vec(d, {ldx, ldo}, {x, out});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
-  HLH_DISPATCH_VL(v, l, k_segment_mean_fwd, n_seg, s, a);
+  HLH_DISPATCH_VL(v, l, k_segment_mean_fwd, n_seg, s, a, nullptr);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -492,7 +492,7 @@ extern "C" int hlhgat_segment_mean_bwd(const int32_t* seg_ptr,
   const int v = pick_vec(d, {ldx, ldo}, {dout, dx});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
-  HLH_DISPATCH_VL(v, l, k_segment_mean_bwd, n_seg, s, a);
+  HLH_DISPATCH_VL(v, l, k_segment_mean_bwd, n_seg, s, a, nullptr);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -877,23 +877,23 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   if (vec) {
     dim3 g((unsigned)ceil_div(M, 64), (unsigned)ceil_div(N, tn * 16));
     if (tn == 1)
-      k_proj_fwd_lds<1><<<g, 256, 0, s>>>(a);
+      launch(k_proj_fwd_lds<1>, g, 256, 0, s, &prof, a);
     else if (tn == 2)
-      k_proj_fwd_lds<2><<<g, 256, 0, s>>>(a);
+      launch(k_proj_fwd_lds<2>, g, 256, 0, s, &prof, a);
     else
-      k_proj_fwd_lds<4><<<g, 256, 0, s>>>(a);
+      launch(k_proj_fwd_lds<4>, g, 256, 0, s, &prof, a);
   } else if (tm == 1 && tn == 1) {
-    k_proj_fwd<1, 1, false><<<grid, 256, 0, s>>>(a);
+    launch(k_proj_fwd<1, 1, false>, grid, 256, 0, s, &prof, a);
   } else if (tm == 1 && tn == 2) {
-    k_proj_fwd<1, 2, false><<<grid, 256, 0, s>>>(a);
+    launch(k_proj_fwd<1, 2, false>, grid, 256, 0, s, &prof, a);
   } else if (tm == 1) {
-    k_proj_fwd<1, 4, false><<<grid, 256, 0, s>>>(a);
+    launch(k_proj_fwd<1, 4, false>, grid, 256, 0, s, &prof, a);
   } else if (tn == 1) {
-    k_proj_fwd<2, 1, false><<<grid, 256, 0, s>>>(a);
+    launch(k_proj_fwd<2, 1, false>, grid, 256, 0, s, &prof, a);
   } else if (tn == 2) {
-    k_proj_fwd<2, 2, false><<<grid, 256, 0, s>>>(a);
+    launch(k_proj_fwd<2, 2, false>, grid, 256, 0, s, &prof, a);
   } else {
-    k_proj_fwd<2, 4, false><<<grid, 256, 0, s>>>(a);
+    launch(k_proj_fwd<2, 4, false>, grid, 256, 0, s, &prof, a);
   }
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;

@@ -18,8 +18,10 @@ void set_error(const char* fmt, ...) {
 }
 
 // --- live timing -----------------------------------------------------------
-// A fixed pool of hipEvent pairs per kernel class.  Records are appended in
-// launch order; hlhgat_prof_read() synchronises them and sums elapsed time.
+// A fixed pool of hipEvent pairs per kernel class, stamped by
+// hipExtLaunchKernel at kernel start / end (common.h: launch()).  Records are
+// appended in launch order; hlhgat_prof_read() synchronises them and sums the
+// kernel durations.
 namespace {
 constexpr int kPoolSize = 1 << 14;
 struct ProfClass {
@@ -31,10 +33,10 @@ struct ProfClass {
 };
 std::mutex g_prof_mu;
 ProfClass g_prof[HLHGAT_PROF_NCLASS];
-int g_active_class = -1;  // class of the currently open scope (no nesting)
 }  // namespace
 
 ProfScope::ProfScope(int kernel_class, hipStream_t s, double b, double f) {
+  (void)s;
   if (kernel_class < 0 || kernel_class >= HLHGAT_PROF_NCLASS) return;
   std::lock_guard<std::mutex> lk(g_prof_mu);
   ProfClass& pc = g_prof[kernel_class];
@@ -46,15 +48,8 @@ ProfScope::ProfScope(int kernel_class, hipStream_t s, double b, double f) {
   slot = pc.used++;
   pc.bytes[slot] = b;
   pc.flops[slot] = f;
-  stream = s;
-  g_active_class = kernel_class;
-  (void)hipEventRecord(pc.start[slot], s);
-}
-
-ProfScope::~ProfScope() {
-  if (slot < 0) return;
-  std::lock_guard<std::mutex> lk(g_prof_mu);
-  (void)hipEventRecord(g_prof[g_active_class].stop[slot], stream);
+  start_ev = pc.start[slot];
+  stop_ev = pc.stop[slot];
 }
 
 }  // namespace hlhgat
@@ -113,5 +108,26 @@ extern "C" int hlhgat_prof_read(int kernel_class, int64_t* launches,
   if (total_ms) *total_ms = ms;
   if (total_bytes) *total_bytes = b;
   if (total_flops) *total_flops = f;
+  return HLHGAT_OK;
+}
+
+// --- workspace initialisation ------------------------------------------------
+namespace {
+__global__ void k_zero_words(uint32_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0u;
+}
+}  // namespace
+
+extern "C" int hlhgat_zero_fill(void* p, size_t bytes, void* stream) {
+  HLH_CHECK_ARG(bytes % 4 == 0 && (bytes == 0 || p) && (reinterpret_cast<uintptr_t>(p) & 3) == 0,
+                "zero_fill: pointer / size must be 4-byte aligned");
+  const int64_t n = (int64_t)(bytes / 4);
+  if (n == 0) return HLHGAT_OK;
+  int64_t g = ceil_div(n, 256);
+  if (g > 1024) g = 1024;
+  k_zero_words<<<(unsigned)g, 256, 0, as_stream(stream)>>>(static_cast<uint32_t*>(p), n);
+  HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

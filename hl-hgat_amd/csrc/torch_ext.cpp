@@ -80,15 +80,20 @@ struct Csr {
   int64_t nnz;
 };
 
+// One BN workspace per (device, stream): its arrival counters must not be
+// shared by launches that can run concurrently (node / edge chains run on two
+// streams, see hlhgat.ops.fork).  Stream-ordered reuse on one stream is safe.
 Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
-  static auto* cache = new std::unordered_map<int, Tensor>();  // leaked: outlives HIP teardown
-  const int dev = like.get_device();
+  static auto* cache = new std::unordered_map<uintptr_t, Tensor>();  // leaked: outlives HIP teardown
+  const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
   const int64_t need = hlhgat_bn_workspace_bytes(n, C);
-  auto it = cache->find(dev);
+  auto it = cache->find(key);
   if (it == cache->end() || it->second.numel() < need) {
-    (*cache)[dev] = at::zeros({std::max<int64_t>(need, 1 << 20)}, like.options().dtype(at::kByte));
+    Tensor ws = at::empty({std::max<int64_t>(need, 1 << 20)}, like.options().dtype(at::kByte));
+    chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream_of(like)), "zero_fill");
+    (*cache)[key] = ws;
   }
-  return (*cache)[dev];
+  return (*cache)[key];
 }
 
 // out[M, N] = sum_b A_b W_b^T + bias

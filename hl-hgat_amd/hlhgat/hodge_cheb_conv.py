@@ -187,9 +187,10 @@ class NodeEdgeInt(nn.Module):
             a_s = ops.att_score(qc_s, kq_s[:, dk:], kq_s[:, :dk], 1 - self.lambda_Edge,
                                 self.lambda_Edge, sq, code)
             return a_t, a_s
-        x_t1 = _value_mlp(self.WV_Node, [x_s2t, x_t])
-        x_s1 = _value_mlp(self.WV_Edge, [x_t2s, x_s])
-        return x_t1, x_s1
+        # node and edge MLPs are independent: edge side on the side stream
+        return ops.fork(lambda: _value_mlp(self.WV_Node, [x_s2t, x_t]),
+                        lambda: _value_mlp(self.WV_Edge, [x_t2s, x_s]),
+                        side_inputs=(x_t2s, x_s), device=x_t.device)
 
 
 class MSI(NodeEdgeInt):

@@ -142,20 +142,37 @@ class Sequential(tnn.Module):
                     getattr(self, f"module_{i + 1}"), tnn.ReLU):
                 self._fuse[i] = ("bn_relu", 2)
             i += self._fuse[i][1] if self._fuse[i] else 1
+        self._split = self._two_chains()
 
-    def forward(self, *args):
-        if len(args) != len(self.input_args):
-            raise TypeError(f"Sequential expects {len(self.input_args)} inputs "
-                            f"({', '.join(self.input_args)}), got {len(args)}")
-        env = dict(zip(self.input_args, args))
+    def _two_chains(self):
+        """Index s such that entries [0, s) and [s, n-1) touch disjoint
+        variables and entry n-1 joins them (the node / edge chains of every
+        HL block, lib/Hodge_ST_Model.py:556-566), else None."""
+        if self._n < 3:
+            return None
+        for s in range(1, self._n - 1):
+            if any(self._fuse[j] and j + self._fuse[j][1] > s for j in range(s)):
+                continue
+            a = set().union(*[set(r[0]) | set(r[1]) for r in self._routes[:s]])
+            b = set().union(*[set(r[0]) | set(r[1]) for r in self._routes[s:self._n - 1]])
+            if not (a & b):
+                last_in = set(self._routes[-1][0])
+                if last_in & a and last_in & b:
+                    return s
+        return None
+
+    def _run(self, env, lo, hi):
         out = None
-        i = 0
-        while i < self._n:
+        i = lo
+        while i < hi:
             ins, outs = self._routes[i]
             fn = getattr(self, f"module_{i}")
             fuse = self._fuse[i]
             if fuse is None:
-                out = fn(*[env[n] for n in ins])
+                if isinstance(fn, tnn.Dropout) and (fn.p == 0.0 or not fn.training):
+                    out = env[ins[0]]  # identity: no copy kernel
+                else:
+                    out = fn(*[env[n] for n in ins])
                 i += 1
             elif fuse[0] == "bn_relu":
                 from .ops import batch_norm_act
@@ -172,6 +189,27 @@ class Sequential(tnn.Module):
                 for n, v in zip(outs, out):
                     env[n] = v
         return out
+
+    def forward(self, *args):
+        if len(args) != len(self.input_args):
+            raise TypeError(f"Sequential expects {len(self.input_args)} inputs "
+                            f"({', '.join(self.input_args)}), got {len(args)}")
+        env = dict(zip(self.input_args, args))
+        s = self._split
+        dev = next((a.device for a in args if torch.is_tensor(a)), None)
+        if s is None or dev is None:
+            return self._run(env, 0, self._n)
+        # node chain on the current stream, edge chain on the side stream
+        from .ops import fork
+        side_env = dict(env)
+        side_in = [env[n] for r in self._routes[s:self._n - 1] for n in r[0]
+                   if n in env and torch.is_tensor(env[n])]
+        fork(lambda: self._run(env, 0, s), lambda: self._run(side_env, s, self._n - 1),
+             side_inputs=side_in, device=dev)
+        for r in self._routes[s:self._n - 1]:
+            for k in r[1]:
+                env[k] = side_env[k]
+        return self._run(env, self._n - 1, self._n)
 
     def __len__(self) -> int:
         return self._n

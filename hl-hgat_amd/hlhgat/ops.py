@@ -73,6 +73,65 @@ def _arr(ctype, vals):
 
 
 # ----------------------------------------------------------------------------
+# node / edge chain concurrency
+# ----------------------------------------------------------------------------
+# Every HL block runs two independent chains — the node side on L0 and the edge
+# side on L1 (lib/Hodge_ST_Model.py:556-566, lib/Hodge_Cheb_Conv.py:307-308).
+# At ZINC scale each launch is latency-bound and fills a fraction of the 256
+# CUs, so the edge chain is issued on a second HIP stream and the two overlap.
+# Autograd replays each node's backward on the stream its forward used, so the
+# backward chains overlap too; captured into a hipGraph the fork/join becomes
+# two graph branches.
+_SIDE_STREAMS = {}
+_FORK_ENABLED = True
+
+
+def set_stream_fork(enabled: bool) -> None:
+    """Enable / disable issuing the edge chain on a second stream."""
+    global _FORK_ENABLED
+    _FORK_ENABLED = bool(enabled)
+
+
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _SIDE_STREAMS[idx] = s
+    return s
+
+
+def _tensors(x):
+    if torch.is_tensor(x):
+        yield x
+    elif isinstance(x, (list, tuple)):
+        for v in x:
+            yield from _tensors(v)
+
+
+def fork(fn_main, fn_side, side_inputs=(), device=None):
+    """Run fn_main() on the current stream and fn_side() on the side stream
+    concurrently; returns (fn_main(), fn_side()) with the side results ordered
+    before anything issued next on the current stream.  Tensors in
+    side_inputs (produced on the current stream) are kept alive for the side
+    stream's use."""
+    if not _FORK_ENABLED or device is None or device.type != "cuda":
+        return fn_main(), fn_side()
+    main = torch.cuda.current_stream(device)
+    side = side_stream(device)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        for t in _tensors(side_inputs):
+            t.record_stream(side)
+        out_side = fn_side()
+    out_main = fn_main()
+    main.wait_stream(side)
+    for t in _tensors(out_side):
+        t.record_stream(main)
+    return out_main, out_side
+
+
+# ----------------------------------------------------------------------------
 # sparse operators (CSR) and their per-batch cache
 # ----------------------------------------------------------------------------
 @dataclass

@@ -243,6 +243,11 @@ int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy
                         float* dweight, float* dbias, void* workspace,
                         int64_t workspace_bytes, void* stream);
 
+/* ---- workspaces --------------------------------------------------------- */
+/* Zero `bytes` (a multiple of 4) at p with a kernel on `stream` (graph-capture
+ * safe; used to initialise the BatchNorm workspace counters). */
+int hlhgat_zero_fill(void* p, size_t bytes, void* stream);
+
 /* ---- live kernel timing ------------------------------------------------ */
 #define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */
 #define HLHGAT_PROF_PROJ 1 /* MFMA projection forward */

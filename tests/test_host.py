@@ -114,3 +114,24 @@ def test_synthetic_zinc_statistics():
     assert 21.5 < b.num_node1.float().mean() < 25.0
     assert 23.0 < b.num_edge1.float().mean() < 27.0
     assert b.x_t.shape[1] == 36 and b.x_s.shape[1] == 18
+
+
+def test_sequential_two_chain_split_cpu():
+    """The node / edge chains of an HL block are detected as independent
+    (they run on two HIP streams on the GPU); on CPU the result is the
+    modules applied in turn."""
+    import torch
+    from hlhgat.nn import Sequential
+    torch.manual_seed(0)
+    lt, ls = torch.nn.Linear(4, 3), torch.nn.Linear(5, 3)
+    seq = Sequential("x_t, w_t, x_s, w_s", [
+        (lt, "x_t -> x_t"), (torch.nn.ReLU(), "x_t -> x_t"), (torch.nn.Dropout(0.0), "x_t -> x_t"),
+        (ls, "x_s -> x_s"), (torch.nn.Tanh(), "x_s -> x_s"),
+        (lambda a, b: [a, b], "x_t, x_s -> x")])
+    assert seq._split == 3
+    xt, xs = torch.randn(6, 4), torch.randn(7, 5)
+    a, b = seq(xt, None, xs, None)
+    assert torch.equal(a, torch.relu(lt(xt)))
+    assert torch.equal(b, torch.tanh(ls(xs)))
+    chain = Sequential("x", [(lt, "x -> y"), (torch.nn.ReLU(), "y -> y")])
+    assert chain._split is None

@@ -1,0 +1,164 @@
+"""hlhgat.train.TrainStep: flat parameters + fused Adam + one-bucket gradient
+all-reduce, replayed as hipGraphs per batch shape.
+
+CPU (gloo, not gpu): the eager step on a plain torch model equals the
+reference training loop (torch.optim.Adam, DDP-style mean of gradients).
+GPU: the hipGraph-replayed HL-HGAT step equals the eager step bit for bit,
+and the two-stream node/edge fork changes no bit of the result."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+
+class _Tiny(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(5, 7)
+        self.b = torch.nn.Linear(7, 1)
+
+    def forward(self, batch):
+        return self.b(torch.relu(self.a(batch.x)))
+
+
+class _B:
+    def __init__(self, x, y):
+        self.x, self.y = x, y
+
+
+def _loss(out, b):
+    return torch.nn.functional.l1_loss(out.view(-1), b.y.view(-1))
+
+
+def _data(seed, n=16):
+    g = torch.Generator().manual_seed(seed)
+    return _B(torch.randn(n, 5, generator=g), torch.randn(n, generator=g))
+
+
+def test_eager_step_matches_adam_loop():
+    from hlhgat.train import TrainStep
+    torch.manual_seed(0)
+    m1 = _Tiny()
+    m2 = _Tiny()
+    m2.load_state_dict(m1.state_dict())
+    step = TrainStep(m1, _loss, lr=1e-2, weight_decay=1e-3, graphs=False)
+    opt = torch.optim.Adam(m2.parameters(), lr=1e-2, weight_decay=1e-3)
+    for i in range(4):
+        b = _data(i)
+        l1 = step(b)
+        opt.zero_grad()
+        l2 = _loss(m2(b), b)
+        l2.backward()
+        opt.step()
+        assert torch.allclose(l1, l2.detach(), rtol=1e-6, atol=1e-7)
+    for (k, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.allclose(p1, p2, rtol=1e-6, atol=1e-7), k
+    # parameters are views of the flat buffer
+    assert m1.a.weight.data_ptr() == step.flat.data_ptr()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "hl-hgat_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from hlhgat.distributed import init_distributed
+    from hlhgat.train import TrainStep
+    init_distributed("gloo")
+    torch.manual_seed(0)
+    m = _Tiny()
+    step = TrainStep(m, _loss, lr=1e-2, graphs=False)
+    for i in range(3):
+        step(_data(10 * i + rank))
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_matches_mean_gradient():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    # single-process reference: Adam on the mean of the two shards' gradients
+    torch.manual_seed(0)
+    m = _Tiny()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    for i in range(3):
+        opt.zero_grad()
+        for r in range(world):
+            b = _data(10 * i + r)
+            (_loss(m(b), b) / world).backward()
+        opt.step()
+    for k, v in m.state_dict().items():
+        for r in range(world):
+            assert torch.allclose(torch.from_numpy(res[r][k]), v, rtol=1e-5, atol=1e-6), (k, r)
+
+
+# ---------------------------------------------------------------------------
+# GPU: graph replay == eager, fork == no fork
+# ---------------------------------------------------------------------------
+KW = dict(channels=[1, 1], filters=[32, 32], mlp_channels=[64], K=3, keig=15)
+
+
+def _run(graphs, fork, batches, order):
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.train import TrainStep
+    ops.set_stream_fork(fork)
+    try:
+        torch.manual_seed(0)
+        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to("cuda:0").train()
+        crit = torch.nn.L1Loss()
+        step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                         weight_decay=1e-3, graphs=graphs)
+        losses = [float(step(batches[i])) for i in order]
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        return losses, sd, dict(step.stats)
+    finally:
+        ops.set_stream_fork(True)
+
+
+@pytest.mark.gpu
+def test_graph_replay_equals_eager(cuda):
+    from hlhgat.synthetic import zinc_like_batch
+    batches = [zinc_like_batch(40, seed=3).to(cuda), zinc_like_batch(33, seed=4).to(cuda),
+               zinc_like_batch(40, seed=3).to(cuda)]  # [2] = same shape as [0], other tensors
+    order = [0, 1, 0, 1, 2, 0]
+    l_e, sd_e, _ = _run(False, True, batches, order)
+    l_g, sd_g, st = _run(True, True, batches, order)
+    assert st["captures"] == 2 and st["replay"] == 4, st
+    assert l_e == l_g
+    for k in sd_e:
+        assert torch.equal(sd_e[k], sd_g[k]), k
+
+
+@pytest.mark.gpu
+def test_stream_fork_is_bitwise_neutral(cuda):
+    from hlhgat.synthetic import zinc_like_batch
+    batches = [zinc_like_batch(40, seed=7).to(cuda)]
+    l0, sd0, _ = _run(False, False, batches, [0, 0])
+    l1, sd1, _ = _run(False, True, batches, [0, 0])
+    assert l0 == l1
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k

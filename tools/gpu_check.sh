@@ -20,10 +20,10 @@ if [[ $MODE == all || $MODE == test ]]; then
   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
-  run bench 600 python bench.py --steps 20 --warmup 5
+  run bench 600 python bench.py --steps 20 --warmup 6
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
   export TMPDIR=/tmp
-  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 6 --no-cpu-baseline
 fi
 echo "=== done"
