@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
   }
 }
 
-// out[e] = ca*(sa[i]*x[i]) + cb*(sb[j]*x[j]) (+ out[e])
+// out[e] = ca*(sa[i]*x[i]) + cb*(sb[j]*x[j]) (+ z[e]) (+ out[e])
 struct Gather2Args {
   const int64_t* ei;
   int64_t n_edges;
@@ -121,6 +121,8 @@ struct Gather2Args {
   const float* sa;
   const float* sb;
   float ca, cb;
+  const float* z;  // optional per-edge addend [n_edges][ldz]
+  int64_t ldz;
   float* out;
   int64_t ldo;
   int accumulate;
@@ -143,6 +145,11 @@ __global__ __launch_bounds__(256) void k_edge_gather2(Gather2Args a) {
 #pragma unroll
     for (int c = 0; c < V; ++c)
       vget(o, c) = a.ca * (si * vget(xi, c)) + a.cb * (sj * vget(xj, c));
+    if (a.z) {
+      vt zv = vload<V>(a.z + e * a.ldz + f);
+#pragma unroll
+      for (int c = 0; c < V; ++c) vget(o, c) = vget(zv, c) + vget(o, c);
+    }
     if (a.accumulate) {
       vt prev = vload<V>(a.out + e * a.ldo + f);
 #pragma unroll
@@ -447,15 +454,16 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
 extern "C" int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
                                    const float* x, int64_t ldx, int64_t d,
                                    const float* sa, const float* sb, float ca,
-                                   float cb, float* out, int64_t ldo,
-                                   int accumulate, void* stream) {
-  HLH_CHECK_ARG(n_edges >= 0 && d > 0 && ldx >= d && ldo >= d,
+                                   float cb, const float* z, int64_t ldz,
+                                   float* out, int64_t ldo, int accumulate,
+                                   void* stream) {
+  HLH_CHECK_ARG(n_edges >= 0 && d > 0 && ldx >= d && ldo >= d && (!z || ldz >= d),
                 "edge_gather2: bad sizes");
   if (n_edges == 0) return HLHGAT_OK;
   HLH_CHECK_ARG(edge_index && x && out, "edge_gather2: NULL pointer");
-  Gather2Args a{edge_index, n_edges, x, ldx, (int)d, sa, sb, ca, cb, out, ldo,
+  Gather2Args a{edge_index, n_edges, x, ldx, (int)d, sa, sb, ca, cb, z, ldz, out, ldo,
                 accumulate};
-  const int v = pick_vec(d, {ldx, ldo}, {x, out});
+  const int v = pick_vec(d, {ldx, ldo, z ? ldz : 4}, {x, out, z});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
   HLH_DISPATCH_VL(v, l, k_edge_gather2, n_edges, s, a, nullptr);

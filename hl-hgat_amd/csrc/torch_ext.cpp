@@ -16,6 +16,8 @@
 // Every kernel runs on torch's current HIP stream; no CPU fallback exists.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <algorithm>
 #include <optional>
@@ -96,6 +98,52 @@ Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
   return (*cache)[key];
 }
 
+// ---------------------------------------------------------------------------
+// Gradient bucket (hlhgat.train.TrainStep): parameters are views of one flat
+// buffer and their gradients go to the same offsets of one flat gradient
+// buffer.  A node computing a parameter gradient writes it straight into a
+// FRESH view of that bucket region and returns the view; autograd's
+// AccumulateGrad then adopts it as .grad without a copy or an add kernel (it
+// steals a gradient whose only reference it holds).  A region is handed out
+// once per backward; a second request (a parameter used twice) gets a plain
+// tensor so AccumulateGrad's sum stays correct.
+// ---------------------------------------------------------------------------
+struct BucketEntry {
+  Tensor flat;
+  int64_t offset;
+  int64_t numel;
+  bool claimed;
+};
+std::unordered_map<const void*, BucketEntry>& bucket() {
+  static auto* m = new std::unordered_map<const void*, BucketEntry>();
+  return *m;
+}
+
+Tensor grad_like(const Tensor& p) {
+  if (!p.defined()) return Tensor();
+  auto& m = bucket();
+  auto it = m.find(p.data_ptr());
+  if (it != m.end() && !it->second.claimed && it->second.numel == p.numel() &&
+      it->second.flat.device() == p.device()) {
+    it->second.claimed = true;
+    return it->second.flat.narrow(0, it->second.offset, p.numel()).view(p.sizes());
+  }
+  return at::empty(p.sizes(), p.options());
+}
+Tensor grad_like(const OptT& p) { return has(p) ? grad_like(*p) : Tensor(); }
+
+void grad_bucket_set(std::vector<Tensor> params, Tensor flat_grad, std::vector<int64_t> offsets) {
+  TORCH_CHECK(params.size() == offsets.size(), "hlhgat: grad bucket: params / offsets differ");
+  auto& m = bucket();
+  m.clear();
+  for (size_t i = 0; i < params.size(); ++i)
+    m[params[i].data_ptr()] = BucketEntry{flat_grad, offsets[i], params[i].numel(), false};
+}
+void grad_bucket_begin() {
+  for (auto& kv : bucket()) kv.second.claimed = false;
+}
+void grad_bucket_clear() { bucket().clear(); }
+
 // out[M, N] = sum_b A_b W_b^T + bias
 void proj_fwd(const std::vector<const float*>& A, const std::vector<int64_t>& lda,
               const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
@@ -149,19 +197,24 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
 }
 
 // returns dx; fills dw/db when requested
+// dx_into: optional [n, C] row-strided destination (e.g. a column slice)
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
                    const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
-                   Tensor& dw, Tensor& db) {
+                   Tensor& dw, Tensor& db, const Tensor* dx_into = nullptr,
+                   const Tensor* b_param = nullptr) {
   const int64_t n = x.size(0), C = x.size(1);
   Tensor dyc = rows2d(dy);
-  Tensor dx = at::empty({n, C}, x.options());
-  dw = (need_w && has(w)) ? at::empty({C}, x.options()) : Tensor();
-  db = need_b ? at::empty({C}, x.options()) : Tensor();
+  Tensor dx = dx_into ? *dx_into : at::empty({n, C}, x.options());
+  TORCH_CHECK(dx.size(0) == n && dx.size(1) == C && dx.stride(1) == 1, "hlhgat: bad dx view");
+  dw = (need_w && has(w)) ? grad_like(w) : Tensor();
+  db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
+                                                 : at::empty({C}, x.options()))
+              : Tensor();
   Tensor ws = bn_workspace(x, n, C);
   chk(hlhgat_bn_bwd_train(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
                           dyc.data_ptr<float>(), ld_of(dyc), n, C, fptr(w),
                           mean.data_ptr<float>(), invstd.data_ptr<float>(), dx.data_ptr<float>(),
-                          C, dw.defined() ? dw.data_ptr<float>() : nullptr,
+                          ld_of(dx), dw.defined() ? dw.data_ptr<float>() : nullptr,
                           db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
                           ws.numel(), stream_of(x)),
       "bn_bwd_train");
@@ -256,7 +309,9 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                 bn_mode == 2 ? out : Tensor(),
                                 mean,
                                 invstd,
-                                has(bn_w) ? *bn_w : Tensor()};
+                                has(bn_w) ? *bn_w : Tensor(),
+                                has(bias) ? *bias : Tensor(),
+                                has(bn_b) ? *bn_b : Tensor()};
     for (const auto& w : W) save.push_back(w);
     ctx->save_for_backward(save);
     std::vector<int64_t> oshape = x.sizes().vec();
@@ -272,8 +327,9 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     auto xshape = ctx->saved_data["xshape"].toIntVector();
     auto sv = ctx->get_saved_variables();
     Tensor x2 = sv[0], T = sv[1], t_rowptr = sv[2], t_col = sv[3], t_val = sv[4], pre = sv[5],
-           yout = sv[6], mean = sv[7], invstd = sv[8], bn_w = sv[9];
-    std::vector<Tensor> W(sv.begin() + 10, sv.end());
+           yout = sv[6], mean = sv[7], invstd = sv[8], bn_w = sv[9], bias_p = sv[10],
+           bn_b = sv[11];
+    std::vector<Tensor> W(sv.begin() + 12, sv.end());
     void* s = stream_of(x2);
     Tensor G = grads[0].reshape({M, dout});
     G = rows2d(G).contiguous();
@@ -287,7 +343,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       OptT y = bn_mode == 2 ? OptT(yout) : OptT();
       OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
       G = bn_backward(pre, y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K), dbn_w,
-                      dbn_b);
+                      dbn_b, nullptr, &bn_b);
       out[10 + K] = dbn_w;
       out[11 + K] = dbn_b;
     }
@@ -307,11 +363,11 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       std::vector<float*> dWp(K);
       std::vector<int64_t> lddw(K);
       for (int64_t k = 0; k < K; ++k) {
-        dW[k] = at::empty({dout, Cin}, x2.options());
+        dW[k] = need(ctx, 9 + k) ? grad_like(W[k]) : at::empty({dout, Cin}, x2.options());
         dWp[k] = dW[k].data_ptr<float>();
         lddw[k] = Cin;
       }
-      Tensor db = need_b ? at::empty({dout}, x2.options()) : Tensor();
+      Tensor db = need_b ? grad_like(bias_p) : Tensor();
       if (M > 0) {
         proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, s);
       } else {
@@ -371,7 +427,8 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
     em.opt(rv);
     em.opt(nbt);
     ctx->saved_data["edges"] = em.e;
-    ctx->save_for_backward({xc, relu ? y : Tensor(), has(w) ? *w : Tensor(), mean, invstd});
+    ctx->save_for_backward(
+        {xc, relu ? y : Tensor(), has(w) ? *w : Tensor(), mean, invstd, has(b) ? *b : Tensor()});
     return y;
   }
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
@@ -380,7 +437,7 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
     OptT y = sv[1].defined() ? OptT(sv[1]) : OptT();
     OptT w = sv[2].defined() ? OptT(sv[2]) : OptT();
     Tensor dx = bn_backward(sv[0], y, grads[0], w, sv[3], sv[4], need(ctx, 1), need(ctx, 2), dw,
-                           db);
+                           db, nullptr, &sv[5]);
     return {dx, dw, db, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
 };
@@ -412,7 +469,7 @@ Tensor linear_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT
 // grads of linear_forward; dAs[i] only where need_a[i]
 void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Tensor& W,
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
-                     Tensor& db, std::vector<Tensor>& dAs) {
+                     Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr) {
   Tensor G = rows2d(Gin);
   const int64_t M = G.size(0), N = G.size(1);
   const int nb = (int)As.size();
@@ -427,8 +484,10 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
   dW = Tensor();
   db = Tensor();
   if (need_w || need_b) {
-    Tensor gw = at::empty_like(W, at::MemoryFormat::Contiguous);
-    Tensor gb = need_b ? at::empty({N}, W.options()) : Tensor();
+    Tensor gw = need_w ? grad_like(W) : at::empty_like(W, at::MemoryFormat::Contiguous);
+    Tensor gb = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
+                                                          : at::empty({N}, W.options()))
+                       : Tensor();
     if (M > 0) {
       std::vector<const float*> Ap(nb);
       std::vector<int64_t> lda(nb), lddw(nb, W.size(1));
@@ -483,20 +542,20 @@ class LinearFn : public torch::autograd::Function<LinearFn> {
     em.opt(b);
     em.list(As_in);
     ctx->saved_data["edges"] = em.e;
-    std::vector<Tensor> save = {Wc};
+    std::vector<Tensor> save = {Wc, has(b) ? *b : Tensor()};
     save.insert(save.end(), As.begin(), As.end());
     ctx->save_for_backward(save);
     return out;
   }
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     auto sv = ctx->get_saved_variables();
-    Tensor W = sv[0];
-    std::vector<Tensor> As(sv.begin() + 1, sv.end());
+    Tensor W = sv[0], b = sv[1];
+    std::vector<Tensor> As(sv.begin() + 2, sv.end());
     std::vector<bool> need_a(As.size());
     for (size_t i = 0; i < As.size(); ++i) need_a[i] = need(ctx, 2 + (int64_t)i);
     Tensor dW, db;
     std::vector<Tensor> dAs;
-    linear_backward(grads[0], As, W, need(ctx, 0), need(ctx, 1), need_a, dW, db, dAs);
+    linear_backward(grads[0], As, W, need(ctx, 0), need(ctx, 1), need_a, dW, db, dAs, &b);
     variable_list out = {dW, db};
     out.insert(out.end(), dAs.begin(), dAs.end());
     return out;
@@ -548,7 +607,9 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     ctx->saved_data["has_b0"] = has(b0);
     ctx->saved_data["has_b3"] = has(b3);
     std::vector<Tensor> save = {W0c, h1, a1, m1, i1, has(g1) ? *g1 : Tensor(), W3c, h2, y, m4, i4,
-                                has(g4) ? *g4 : Tensor()};
+                                has(g4) ? *g4 : Tensor(), has(b0) ? *b0 : Tensor(),
+                                has(be1) ? *be1 : Tensor(), has(b3) ? *b3 : Tensor(),
+                                has(be4) ? *be4 : Tensor()};
     save.insert(save.end(), blocks.begin(), blocks.end());
     ctx->save_for_backward(save);
     return y;
@@ -558,7 +619,8 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     const int64_t nb = ctx->saved_data["nb"].toInt();
     Tensor W0 = sv[0], h1 = sv[1], a1 = sv[2], m1 = sv[3], i1 = sv[4], g1 = sv[5], W3 = sv[6],
            h2 = sv[7], y = sv[8], m4 = sv[9], i4 = sv[10], g4 = sv[11];
-    std::vector<Tensor> blocks(sv.begin() + 12, sv.end());
+    Tensor b0 = sv[12], be1 = sv[13], b3 = sv[14], be4 = sv[15];
+    std::vector<Tensor> blocks(sv.begin() + 16, sv.end());
     // positions: blocks[0..nb), W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4, rm4, rv4,
     //            nbt4, mom1, eps1, mom4, eps4
     const int64_t P = nb;
@@ -566,25 +628,25 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     Tensor dg4, dbe4, dg1, dbe1;
     Tensor dh2 = bn_backward(h2, OptT(y), grads[0], g4.defined() ? OptT(g4) : OptT(), m4, i4,
                              need(ctx, P + 9), need(ctx, P + 10), dg4,
-                             dbe4);
+                             dbe4, nullptr, &be4);
     out[P + 9] = dg4;
     out[P + 10] = dbe4;
     Tensor dW3, db3, dW0, db0;
     std::vector<Tensor> da1;
     linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true},
-                    dW3, db3, da1);
+                    dW3, db3, da1, &b3);
     out[P + 7] = dW3;
     out[P + 8] = db3;
     Tensor dh1 = bn_backward(h1, OptT(a1), da1[0], g1.defined() ? OptT(g1) : OptT(), m1, i1,
                              need(ctx, P + 2), need(ctx, P + 3), dg1,
-                             dbe1);
+                             dbe1, nullptr, &be1);
     out[P + 2] = dg1;
     out[P + 3] = dbe1;
     std::vector<bool> need_a(nb);
     for (int64_t i = 0; i < nb; ++i) need_a[i] = need(ctx, i);
     std::vector<Tensor> dblocks;
     linear_backward(dh1, blocks, W0, need(ctx, P), need(ctx, P + 1), need_a,
-                    dW0, db0, dblocks);
+                    dW0, db0, dblocks, &b0);
     out[P] = dW0;
     out[P + 1] = db0;
     for (int64_t i = 0; i < nb; ++i) out[i] = dblocks[i];
@@ -613,8 +675,8 @@ Tensor edge_gather(const Tensor& ei, int64_t n_edges, const Tensor& x, const flo
   Tensor out = at::empty({n_edges, x.size(1)}, x.options());
   if (n_edges > 0) {
     chk(hlhgat_edge_gather2(ei.data_ptr<int64_t>(), n_edges, x.data_ptr<float>(), ld_of(x),
-                            x.size(1), sa, sb, ca, cb, out.data_ptr<float>(), ld_of(out), 0,
-                            stream_of(x)),
+                            x.size(1), sa, sb, ca, cb, nullptr, 0, out.data_ptr<float>(),
+                            ld_of(out), 0, stream_of(x)),
         "edge_gather2");
   }
   return out;
@@ -662,6 +724,251 @@ class EdgeFromNodesFn : public torch::autograd::Function<EdgeFromNodesFn> {
 };
 
 // ---------------------------------------------------------------------------
+// NodeEdgeInt value path, both sides in one node, projected BEFORE the
+// boundary-operator gathers (lib/Hodge_Cheb_Conv.py:293-295,307-308):
+//
+//   WV_Node(cat[(1/D)|B1| x_s, x_t]) first Linear
+//     = x_t Wn_b^T + b_n + (1/D) |B1| (x_s Wn_a^T)
+//   WV_Edge(cat[|B1|^T x_t / 2, x_s]) first Linear
+//     = x_s We_b^T + b_e + |B1|^T (x_t We_a^T) / 2
+//
+// (W = [W_a | W_b] split at column d).  The gathers then run at the latent
+// width dl = 64 instead of the growing input width d (64..384 in cfg2), the
+// d-wide x_s2t / x_t2s are never materialised, and the two first-layer GEMMs
+// become ONE per input with N = 2*dl:
+//   Yt = x_t [Wn_b; We_a]^T  ->  [Qt | P2]      Ys = x_s [We_b; Wn_a]^T -> [Qs | P1]
+//   h1_t = Qt + rD * |B1| P1                    h1_s = Qs + (P2[i] + P2[j]) / 2
+// then BN -> ReLU -> Linear -> BN -> ReLU per side as in the reference.
+// Same fp32 arithmetic up to summation order (1e-5 relative, tests).
+// ---------------------------------------------------------------------------
+// Two-stream fork inside one autograd node: the node (current) stream and a
+// persistent side stream per device, ordered by hipEvents (captured into a
+// hipGraph as branch dependencies).  Tensors allocated while the side stream
+// is current and then used on the node stream are record_stream()-ed.
+// (PyTorch-ROCm exposes HIP streams to torch as "cuda" streams: the
+// MasqueradingAsCUDA wrappers are the ones its allocator and guards accept.)
+using TStream = c10::hip::HIPStreamMasqueradingAsCUDA;
+using TStreamGuard = c10::hip::HIPStreamGuardMasqueradingAsCUDA;
+struct Fork {
+  TStream main, side;
+  explicit Fork(int dev)
+      : main(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)dev)),
+        side(side_of(dev)) {}
+  static TStream side_of(int dev) {
+    static auto* streams = new std::unordered_map<int, TStream>();
+    auto it = streams->find(dev);
+    if (it == streams->end())
+      it = streams->emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
+                                     false, (c10::DeviceIndex)dev)).first;
+    return it->second;
+  }
+  static hipEvent_t next_event() {
+    static thread_local std::vector<hipEvent_t> pool;
+    static thread_local size_t k = 0;
+    if (pool.empty()) {
+      pool.resize(64);
+      for (auto& e : pool) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == 0);
+    }
+    return pool[k++ % pool.size()];
+  }
+  static void order(const TStream& from, const TStream& to) {
+    hipEvent_t e = next_event();
+    TORCH_CHECK(hipEventRecord(e, from.stream()) == hipSuccess, "hlhgat: hipEventRecord");
+    TORCH_CHECK(hipStreamWaitEvent(to.stream(), e, 0) == hipSuccess, "hlhgat: hipStreamWaitEvent");
+  }
+  void side_waits_main() { order(main, side); }
+  void main_waits_side() { order(side, main); }
+  void escape(std::initializer_list<Tensor> ts) {
+    for (const auto& t : ts)
+      if (t.defined()) t.record_stream(main);
+  }
+};
+
+struct SideMlp {  // [W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4, rm4, rv4, nbt4]
+  Tensor h1, a1, m1, i1, h2, y, m4, i4;
+};
+
+class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
+ public:
+  static variable_list forward(AutogradContext* ctx, Tensor x_t, Tensor x_s, Tensor rowptr,
+                               Tensor eids, Tensor ei, Tensor rD, at::TensorList pn,
+                               at::TensorList pe, double mom1n, double eps1n, double mom4n,
+                               double eps4n, double mom1e, double eps1e, double mom4e,
+                               double eps4e) {
+    req(x_t, "x_t");
+    req(x_s, "x_s");
+    TORCH_CHECK(pn.size() == 14 && pe.size() == 14, "hlhgat: nei_value expects 14+14 params");
+    Tensor xt = rows2d(x_t), xs = rows2d(x_s);
+    const int64_t N = xt.size(0), E = xs.size(0), d = xt.size(1);
+    TORCH_CHECK(xs.size(1) == d, "hlhgat: NodeEdgeInt x_t / x_s widths differ");
+    TORCH_CHECK(ei.size(1) == E, "hlhgat: x_s rows != |B1| edges");
+    TORCH_CHECK(rD.numel() == N, "hlhgat: D has ", rD.numel(), " entries, x_t has ", N, " rows");
+    const Tensor &W0n = pn[0], &W0e = pe[0];
+    TORCH_CHECK(W0n.size(1) == 2 * d && W0e.size(1) == 2 * d, "hlhgat: WV first Linear expects ",
+                2 * d, " input features");
+    const int64_t dn = W0n.size(0), de = W0e.size(0);
+    Tensor Wt = at::cat({W0n.narrow(1, d, d), W0e.narrow(1, 0, d)}, 0).contiguous();
+    Tensor Ws = at::cat({W0e.narrow(1, d, d), W0n.narrow(1, 0, d)}, 0).contiguous();
+    Tensor bt = at::cat({pn[1], at::zeros({de}, pn[1].options())});
+    Tensor bs = at::cat({pe[1], at::zeros({dn}, pe[1].options())});
+    Tensor Yt = at::empty({N, dn + de}, xt.options());  // [Qt | P2]
+    Tensor Ys = at::empty({E, de + dn}, xt.options());  // [Qs | P1]
+    Tensor h1t = at::empty({N, dn}, xt.options());
+    Tensor h1s = at::empty({E, de}, xt.options());
+    auto side = [&](const at::TensorList& p, const Tensor& h1, double m1, double e1, double m4,
+                    double e4, SideMlp& o) {
+      o.h1 = h1;
+      o.a1 = bn_forward(h1, BnState{p[2], p[3], p[4], p[5], p[6], m1, e1}, true, o.m1, o.i1);
+      Tensor W3 = p[7].stride(1) == 1 ? p[7] : p[7].contiguous();
+      o.h2 = linear_forward({o.a1}, W3, p[8]);
+      o.y = bn_forward(o.h2, BnState{p[9], p[10], p[11], p[12], p[13], m4, e4}, true, o.m4, o.i4);
+    };
+    auto lin_into = [](const Tensor& A, const Tensor& W, const Tensor& b, Tensor& out) {
+      if (A.size(0) > 0)
+        proj_fwd({A.data_ptr<float>()}, {ld_of(A)}, {W.data_ptr<float>()}, {W.stride(0)},
+                 {A.size(1)}, A.size(0), W.size(0), b.data_ptr<float>(), out, stream_of(A));
+    };
+    SideMlp tn, te;
+    Fork fk(xt.get_device());
+    fk.side_waits_main();
+    {  // edge side: first-layer GEMM on the side stream
+      TStreamGuard g(fk.side);
+      lin_into(xs, Ws, bs, Ys);
+    }
+    lin_into(xt, Wt, bt, Yt);
+    fk.side_waits_main();  // side needs Yt
+    fk.main_waits_side();  // main needs Ys
+    {  // edge side: h1_s = Qs + (P2[i] + P2[j]) / 2, then its MLP
+      TStreamGuard g(fk.side);
+      if (E > 0) {
+        chk(hlhgat_edge_gather2(ei.data_ptr<int64_t>(), E, Yt.data_ptr<float>() + dn, dn + de, de,
+                                nullptr, nullptr, 0.5f, 0.5f, Ys.data_ptr<float>(), de + dn,
+                                h1s.data_ptr<float>(), de, 0, fk.side.stream()),
+            "edge_gather2(nei edge)");
+      }
+      side(pe, h1s, mom1e, eps1e, mom4e, eps4e, te);
+    }
+    if (N > 0) {  // node side: h1_t = Qt + rD * |B1| P1, then its MLP
+      chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
+                           rD.data_ptr<float>(), N, 2 * E, Ys.data_ptr<float>() + de, de + dn, dn,
+                           Yt.data_ptr<float>(), dn + de, nullptr, 0, nullptr, 0, 1.f, 0.f, 1.f,
+                           1.f, 0.f, 0.f, h1t.data_ptr<float>(), dn, fk.main.stream()),
+          "poly_step(nei node)");
+    }
+    side(pn, h1t, mom1n, eps1n, mom4n, eps4n, tn);
+    fk.main_waits_side();
+    fk.escape({te.a1, te.m1, te.i1, te.h2, te.y, te.m4, te.i4});
+    {
+      EdgeMap em;
+      for (int i = 0; i < 6; ++i) em.tensor();
+      em.list(pn);
+      em.list(pe);
+      for (int i = 0; i < 8; ++i) em.other();
+      ctx->saved_data["edges"] = em.e;
+    }
+    ctx->saved_data["dims"] = std::vector<int64_t>{N, E, d, dn, de};
+    ctx->save_for_backward({xt, xs, rowptr, eids, ei, rD, Wt, Ws, pn[2], pn[7], pn[9], pe[2],
+                            pe[7], pe[9], tn.h1, tn.a1, tn.m1, tn.i1, tn.h2, tn.y, tn.m4, tn.i4,
+                            te.h1, te.a1, te.m1, te.i1, te.h2, te.y, te.m4, te.i4,
+                            // 30..: W0, b0, be1, b3, be4 per side (gradient bucket targets)
+                            pn[0], pn[1], pn[3], pn[8], pn[10], pe[0], pe[1], pe[3], pe[8],
+                            pe[10]});
+    return {tn.y, te.y};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    const auto dims = ctx->saved_data["dims"].toIntVector();
+    const int64_t N = dims[0], E = dims[1], d = dims[2], dn = dims[3], de = dims[4];
+    Tensor xt = sv[0], xs = sv[1], rowptr = sv[2], eids = sv[3], ei = sv[4], rD = sv[5],
+           Wt = sv[6], Ws = sv[7];
+    // positions: x_t 0, x_s 1, rowptr 2, eids 3, ei 4, rD 5, pn 6..19, pe 20..33, hyper 34..41
+    variable_list out(42);
+    const int64_t PN = 6, PE = 20;
+    Tensor dYt = at::empty({N, dn + de}, xt.options());
+    Tensor dYs = at::empty({E, de + dn}, xt.options());
+    auto side_bwd = [&](const Tensor& gy, int64_t P, const Tensor& g1, const Tensor& W3,
+                        const Tensor& g4, int o0, Tensor dest, int q0) {
+      const Tensor &be1 = sv[q0 + 2], &b3 = sv[q0 + 3], &be4 = sv[q0 + 4];
+      Tensor h1 = sv[o0], a1 = sv[o0 + 1], m1 = sv[o0 + 2], i1 = sv[o0 + 3], h2 = sv[o0 + 4],
+             y = sv[o0 + 5], m4 = sv[o0 + 6], i4 = sv[o0 + 7];
+      Tensor dg4, dbe4, dg1, dbe1, dW3, db3;
+      Tensor gyc = gy.defined() ? gy : at::zeros_like(y);
+      Tensor dh2 = bn_backward(h2, OptT(y), gyc, OptT(g4), m4, i4, need(ctx, P + 9),
+                               need(ctx, P + 10), dg4, dbe4, nullptr, &be4);
+      std::vector<Tensor> da1;
+      linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true}, dW3, db3, da1,
+                      &b3);
+      bn_backward(h1, OptT(a1), da1[0], OptT(g1), m1, i1, need(ctx, P + 2), need(ctx, P + 3), dg1,
+                  dbe1, &dest, &be1);
+      out[P + 2] = dg1;
+      out[P + 3] = dbe1;
+      out[P + 7] = dW3;
+      out[P + 8] = db3;
+      out[P + 9] = dg4;
+      out[P + 10] = dbe4;
+    };
+    Fork fk(xt.get_device());
+    fk.side_waits_main();
+    {  // edge side MLP backward on the side stream -> dYs[:, :de]
+      TStreamGuard g(fk.side);
+      side_bwd(grads[1], PE, sv[11], sv[12], sv[13], 22, dYs.narrow(1, 0, de), 35);
+    }
+    side_bwd(grads[0], PN, sv[8], sv[9], sv[10], 14, dYt.narrow(1, 0, dn), 30);
+    fk.side_waits_main();  // side needs dh1_t
+    fk.main_waits_side();  // main needs dh1_s
+    {  // dP1[e] = rD[i] dh1_t[i] + rD[j] dh1_t[j] -> dYs[:, de:], then the edge GEMM grads
+      TStreamGuard g(fk.side);
+      if (E > 0) {
+        const float* r = rD.data_ptr<float>();
+        chk(hlhgat_edge_gather2(ei.data_ptr<int64_t>(), E, dYt.data_ptr<float>(), dn + de, dn, r,
+                                r, 1.f, 1.f, nullptr, 0, dYs.data_ptr<float>() + de, de + dn, 0,
+                                fk.side.stream()),
+            "edge_gather2(nei edge bwd)");
+      }
+    }
+    // dP2[v] = 1/2 sum_{e ni v} dh1_s[e]  -> dYt[:, dn:]
+    if (N > 0) {
+      chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
+                           nullptr, N, 2 * E, dYs.data_ptr<float>(), de + dn, de, nullptr, 0,
+                           nullptr, 0, nullptr, 0, 0.5f, 0.f, 0.f, 1.f, 0.f, 0.f,
+                           dYt.data_ptr<float>() + dn, dn + de, fk.main.stream()),
+          "poly_step(nei node bwd)");
+    }
+    const bool nW = need(ctx, PN) || need(ctx, PE), nB = need(ctx, PN + 1) || need(ctx, PE + 1);
+    Tensor dWt, dbt, dWs, dbs;
+    std::vector<Tensor> dxt, dxs;
+    {
+      TStreamGuard g(fk.side);
+      linear_backward(dYs, {xs}, Ws, nW, nB, {need(ctx, 1)}, dWs, dbs, dxs);
+    }
+    linear_backward(dYt, {xt}, Wt, nW, nB, {need(ctx, 0)}, dWt, dbt, dxt);
+    fk.main_waits_side();
+    fk.escape({dWs, dbs, dxs[0], out[PE + 2], out[PE + 3], out[PE + 7], out[PE + 8], out[PE + 9],
+               out[PE + 10]});
+    out[0] = dxt[0];
+    out[1] = dxs[0];
+    if (nW) {
+      // Wt = [Wn_b; We_a], Ws = [We_b; Wn_a]  (W0 = [W_a | W_b])
+      if (need(ctx, PN)) {
+        out[PN] = grad_like(sv[30]);
+        at::cat_out(out[PN], {dWs.narrow(0, de, dn), dWt.narrow(0, 0, dn)}, 1);
+      }
+      if (need(ctx, PE)) {
+        out[PE] = grad_like(sv[35]);
+        at::cat_out(out[PE], {dWt.narrow(0, dn, de), dWs.narrow(0, 0, de)}, 1);
+      }
+    }
+    if (nB) {
+      if (need(ctx, PN + 1)) out[PN + 1] = grad_like(sv[31]).copy_(dbt.narrow(0, 0, dn));
+      if (need(ctx, PE + 1)) out[PE + 1] = grad_like(sv[36]).copy_(dbs.narrow(0, 0, de));
+    }
+    (void)d;
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
 // python entry points
 // ---------------------------------------------------------------------------
 Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_rowptr, Tensor t_col,
@@ -698,6 +1005,16 @@ Tensor edge_from_nodes(Tensor x_t, Tensor rowptr, Tensor eids, Tensor ei) {
   return EdgeFromNodesFn::apply(x_t, rowptr, eids, ei);
 }
 
+std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids, Tensor ei,
+                              Tensor rD, std::vector<Tensor> pn, std::vector<Tensor> pe,
+                              double mom1n, double eps1n, double mom4n, double eps4n,
+                              double mom1e, double eps1e, double mom4e, double eps4e) {
+  auto r = NEIntValueFn::apply(x_t, x_s, rowptr, eids, ei, rD, at::TensorList(pn),
+                               at::TensorList(pe), mom1n, eps1n, mom4n, eps4n, mom1e, eps1e,
+                               mom4e, eps4e);
+  return {r[0], r[1]};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -706,6 +1023,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);
+  m.def("nei_value", &nei_value);
+  m.def("grad_bucket_set", &grad_bucket_set);
+  m.def("grad_bucket_begin", &grad_bucket_begin);
+  m.def("grad_bucket_clear", &grad_bucket_clear);
   m.def("node_from_edges", &node_from_edges);
   m.def("edge_from_nodes", &edge_from_nodes);
   m.def("version", []() { return hlhgat_version(); });

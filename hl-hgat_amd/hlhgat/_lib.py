@@ -50,7 +50,7 @@ SIGNATURES = {
     "hlhgat_proj_bwd_weight": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
                                        P_vp, P_i64, c_vp, c_i32, c_vp, c_i64, c_vp]),
     "hlhgat_edge_gather2": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_f32,
-                                    c_f32, c_vp, c_i64, c_i32, c_vp]),
+                                    c_f32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_att_score_fwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,
                                      c_f32, c_f32, c_f32, c_i32, c_vp, c_vp]),
     "hlhgat_att_score_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,

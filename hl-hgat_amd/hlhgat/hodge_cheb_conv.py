@@ -168,6 +168,12 @@ class NodeEdgeInt(nn.Module):
         return x_s2t, x_t2s
 
     def forward(self, x_t: Tensor, x_s: Tensor, par, D: Tensor):
+        if not self.only_att and x_t.is_cuda and x_t.dim() == 2:
+            bop = _as_boundary(par, x_t.size(0), x_s.size(0))
+            r = ops.nei_value(x_t, x_s, bop.incidence(), (1 / D).view(-1), self.WV_Node,
+                              self.WV_Edge)
+            if r is not None:
+                return r
         x_s2t, x_t2s = self.interact(x_t, x_s, par, D)
         if self.only_att:
             code = _sigma_code(self.sigma)

@@ -26,7 +26,7 @@ except ImportError as e:  # pragma: no cover - the build always produces it
 
 __all__ = [
     "SparseCSR", "HodgeOperator", "Incidence", "hodge_operator", "incidence",
-    "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks", "mlp2",
+    "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks", "mlp2", "nei_value",
     "batch_norm_act",
     "node_from_edges", "edge_from_nodes", "att_score", "segment_mean",
     "POLY_LAGUERRE", "POLY_CHEB", "SIGMA_SIGMOID", "SIGMA_RELU",
@@ -437,6 +437,50 @@ def mlp2(blocks: Sequence[torch.Tensor], seq: torch.nn.Sequential) -> torch.Tens
     return _ext.mlp2(list(blocks), lin0.weight, lin0.bias, *_bn_args(bn1)[:5], lin3.weight,
                      lin3.bias, *_bn_args(bn4)[:5], _bn_args(bn1)[5], float(bn1.eps),
                      _bn_args(bn4)[5], float(bn4.eps))
+
+
+def _mlp2_params(seq: torch.nn.Sequential):
+    """The 14 tensors of a reference WV_* MLP (Linear, BN, ReLU, Linear, BN,
+    ReLU) in training mode with affine, tracked BN and biased Linears, or
+    None when the module differs from that structure."""
+    m = list(seq)
+    if not (len(m) == 6 and isinstance(m[0], torch.nn.Linear)
+            and isinstance(m[1], torch.nn.BatchNorm1d) and isinstance(m[2], torch.nn.ReLU)
+            and isinstance(m[3], torch.nn.Linear) and isinstance(m[4], torch.nn.BatchNorm1d)
+            and isinstance(m[5], torch.nn.ReLU)):
+        return None
+    l0, b1, _, l3, b4, _ = m
+    for b in (b1, b4):
+        if not (b.training and b.affine and b.track_running_stats and b.momentum is not None
+                and b.running_mean is not None):
+            return None
+    if l0.bias is None or l3.bias is None:
+        return None
+    return ([l0.weight, l0.bias, b1.weight, b1.bias, b1.running_mean, b1.running_var,
+             b1.num_batches_tracked, l3.weight, l3.bias, b4.weight, b4.bias, b4.running_mean,
+             b4.running_var, b4.num_batches_tracked],
+            [float(b1.momentum), float(b1.eps), float(b4.momentum), float(b4.eps)])
+
+
+def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.Tensor,
+              wv_node: torch.nn.Sequential, wv_edge: torch.nn.Sequential):
+    """NodeEdgeInt value path (lib/Hodge_Cheb_Conv.py:293-295,307-308) as one
+    C++ node, first Linear projected before the |B1| gathers (torch_ext.cpp,
+    NEIntValueFn); returns (x_t1, x_s1), or None when the WV_* modules are not
+    the reference training-mode structure (caller falls back)."""
+    pn, pe = _mlp2_params(wv_node), _mlp2_params(wv_edge)
+    if pn is None or pe is None:
+        return None
+    _req_dev(x_t, "x_t")
+    _req_dev(x_s, "x_s")
+    if x_s.size(0) != inc.n_edges or x_t.size(0) != inc.n_nodes:
+        raise RuntimeError(f"hlhgat: x_t/x_s rows ({x_t.size(0)}, {x_s.size(0)}) do not match "
+                           f"|B1| ({inc.n_nodes}, {inc.n_edges})")
+    if rD.numel() != inc.n_nodes:
+        raise RuntimeError(f"hlhgat: D has {rD.numel()} entries, |B1| has {inc.n_nodes} nodes")
+    r = _ext.nei_value(x_t, x_s, inc.rowptr, inc.edge_ids, inc.edge_index,
+                       rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1])
+    return r[0], r[1]
 
 
 # ----------------------------------------------------------------------------

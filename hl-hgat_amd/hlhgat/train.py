@@ -86,6 +86,7 @@ class TrainStep:
         self.flat = torch.empty(n, device=dev, dtype=torch.float32)
         self.flat_grad = torch.zeros(n, device=dev, dtype=torch.float32)
         off = 0
+        self._offsets = []
         with torch.no_grad():
             for p in params:
                 if p.dtype != torch.float32:
@@ -94,8 +95,15 @@ class TrainStep:
                 self.flat[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = self.flat[off:off + k].view_as(p)
                 p.grad = self.flat_grad[off:off + k].view_as(p)
+                self._offsets.append(off)
                 off += k
         self.params = params
+        # HIP autograd nodes write parameter gradients straight into flat_grad
+        # (torch_ext.cpp, "Gradient bucket"): no per-parameter add / copy
+        self._ext = None
+        if dev.type == "cuda":
+            self._ext = ops._ext
+            self._ext.grad_bucket_set(params, self.flat_grad, self._offsets)
         self.master = torch.nn.Parameter(self.flat)  # shares storage with the model
         self.master.grad = self.flat_grad
         kw = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
@@ -112,10 +120,29 @@ class TrainStep:
     # -- the step ---------------------------------------------------------
     def _fwd_bwd(self, batch) -> torch.Tensor:
         self.flat_grad.zero_()
+        if self._ext is not None:
+            for p in self.params:
+                p.grad = None
+            self._ext.grad_bucket_begin()
         out = self.model(batch)
         loss = self.loss_fn(out, batch)
         loss.backward()
+        if self._ext is not None:
+            self._adopt_grads()
         return loss.detach()
+
+    def _adopt_grads(self) -> None:
+        """Every p.grad must be its flat_grad view: gradients produced outside
+        the bucket (torch ops) are copied in; missing ones stay zero."""
+        base = self.flat_grad.data_ptr()
+        for p, off in zip(self.params, self._offsets):
+            g = p.grad
+            view = self.flat_grad[off:off + p.numel()].view_as(p)
+            if g is None:
+                p.grad = view
+            elif g.data_ptr() != base + 4 * off:
+                view.copy_(g)
+                p.grad = view
 
     def _exchange_and_update(self) -> None:
         if self.world > 1:

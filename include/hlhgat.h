@@ -180,13 +180,15 @@ int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
                            int64_t workspace_floats, void* stream);
 
 /* ---- boundary-operator interaction ------------------------------------ */
-/* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] with (i,j) = edge_index[:,e]
- * (sa/sb per-node scale vectors, may be NULL).  With ca=cb=0.5 and no
- * scales this is x_t2s = (|B1|^T x_t)/2 (lib/Hodge_Cheb_Conv.py:295). */
+/* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
+ * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge
+ * addend [n_edges][ldz]; each may be NULL).  With ca=cb=0.5 and no scales
+ * this is x_t2s = (|B1|^T x_t)/2 (lib/Hodge_Cheb_Conv.py:295). */
 int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
                         const float* x, int64_t ldx, int64_t d, const float* sa,
-                        const float* sb, float ca, float cb, float* out,
-                        int64_t ldo, int accumulate, void* stream);
+                        const float* sb, float ca, float cb, const float* z,
+                        int64_t ldz, float* out, int64_t ldo, int accumulate,
+                        void* stream);
 
 /* ---- attention score (NodeEdgeInt only_att) ---------------------------- */
 /* a[r] = sigma((w_cross*<Qc[r],Kr[r]> + w_self*<Qs[r],Kr[r]>) / sqrt_dk)

@@ -403,3 +403,43 @@ def test_batch_norm_act_vs_torch(cuda, n, C, relu):
     with torch.no_grad():
         y2 = ops.batch_norm_act(xd.detach(), bn, relu=relu)
     close(y2.cpu(), y.detach().cpu(), 1e-6, "repeat")
+
+
+@pytest.mark.parametrize("d,dv", [(64, 64), (96, 64), (40, 24)])
+def test_nei_value_projected_first_matches_gather_first(cuda, d, dv, monkeypatch):
+    """NEIntValueFn (first Linear projected before the |B1| gathers) against
+    the gather-then-Linear path of the reference's operation order: outputs
+    1e-5, gradients 1e-4 relative, BN running statistics 1e-5."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(60, seed=21)
+    N_t, N_s = b.x_t.shape[0], b.x_s.shape[0]
+    g = torch.Generator().manual_seed(d)
+    xt0, xs0 = torch.randn(N_t, d, generator=g), torch.randn(N_s, d, generator=g)
+    Rt, Rs = torch.randn(N_t, dv, generator=g), torch.randn(N_s, dv, generator=g)
+    D = R.degree(b.edge_index.reshape(-1), N_t)
+    torch.manual_seed(3)
+    m0 = hlhgat.NodeEdgeInt(d=d, dv=dv)
+    sd0 = {k: v.clone() for k, v in m0.state_dict().items()}
+
+    def run(fused):
+        m = hlhgat.NodeEdgeInt(d=d, dv=dv)
+        m.load_state_dict(sd0)
+        m = m.to(cuda).train()
+        if not fused:
+            monkeypatch.setattr(ops, "nei_value", lambda *a, **k: None)
+        x_t = dev(xt0).requires_grad_(True)
+        x_s = dev(xs0).requires_grad_(True)
+        par = hlhgat.adj2par1(dev(b.edge_index), N_t, N_s)
+        a, c = m(x_t, x_s, par, dev(D))
+        ((a * dev(Rt)).sum() + (c * dev(Rs)).sum()).backward()
+        monkeypatch.undo()
+        res = {"out_t": a, "out_s": c, "gx_t": x_t.grad, "gx_s": x_s.grad}
+        res.update({"grad/" + k: p.grad for k, p in m.named_parameters()})
+        res.update({"buf/" + k: v for k, v in m.state_dict().items() if "running" in k})
+        return {k: v.detach().cpu() for k, v in res.items()}
+
+    ref, new = run(False), run(True)
+    for k in ref:
+        close(new[k], ref[k], 1e-4 if k.startswith(("g", "grad")) else 1e-5, k)
