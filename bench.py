@@ -82,6 +82,26 @@ def cpu_baseline(batch_cpu, budget_s=15.0):
                       f"{GRAPHS_PER_GPU}-graph synthetic ZINC batch, median step {med*1e3:.1f} ms"}
 
 
+def pmc_traffic(kernel="k_poly_step"):
+    """HBM traffic per launch of `kernel` at this workload, from the newest
+    committed rocprofv3 PMC summary (profiles/*_pmc_traffic.json, written by
+    tools/pmc_traffic.py from two --pmc passes of this bench: FETCH_SIZE x2
+    (gfx950 wide-load correction) + WRITE_SIZE, MI355X_MICROARCH.md §HBM).
+    Counters cannot be read from inside the timed process, so the figure is
+    the committed measurement of the same command; None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["traffic_bytes"], os.path.relpath(path, REPO)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,12 +169,14 @@ def main():
         return p["bytes"] / (p["ms"] * 1e-3) / 1e9 if p["ms"] > 0 else 0.0
 
     poly_gbs = gbs(poly)
+    traffic, traffic_src = pmc_traffic("k_poly_step")
     roofline = {
         "kernel": "k_poly_step (CSR SpMM / fused Laguerre step, fwd + adjoint)",
         "measured": f"hipExtLaunchKernel start/stop stamps, {args.prof_steps} eager steps after "
                     f"the timed region",
         "bound": "hbm", "achieved": round(poly_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(poly_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+        "frac": round(poly_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+        "traffic_source": traffic_src,
         "launches": poly["launches"],
         "avg_launch_us": round(poly["ms"] * 1e3 / max(poly["launches"], 1), 2),
         "algorithmic_bytes_per_launch": round(poly["bytes"] / max(poly["launches"], 1)),

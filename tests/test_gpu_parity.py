@@ -194,7 +194,9 @@ def test_conv_K1_is_linear(cuda):
 @pytest.mark.parametrize("M,N,kbs", [(1, 1, [1]), (17, 16, [4]), (1000, 64, [64, 64, 64]),
                                      (5000, 64, [384, 384]), (333, 33, [18, 7]),
                                      (4097, 130, [36]), (2048, 256, [128, 128]),
-                                     (70000, 64, [64])])
+                                     (70000, 64, [64]), (23001, 64, [36, 36, 36]),
+                                     (999, 32, [20, 12, 4]), (513, 16, [8, 40]),
+                                     (3000, 64, [384, 384, 128])])
 def test_linear_blocks_fwd_bwd(cuda, M, N, kbs):
     from hlhgat import ops
     g = torch.Generator().manual_seed(M + N)
