@@ -131,3 +131,61 @@ extern "C" int hlhgat_zero_fill(void* p, size_t bytes, void* stream) {
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
+
+// --- batched 2-D strided copies (parameter packing) -------------------------
+// Up to HLHGAT_MAX_COPY_BLOCKS rectangles dst[r][c] = src ? src[r][c] : 0 in
+// ONE launch: the NodeEdgeInt value path repacks its first-Linear weights and
+// biases (and unpacks their gradients) every step; one launch replaces the
+// cat / zeros / narrow-copy kernels that would otherwise sit on the critical
+// stream.
+namespace {
+struct CopyArgs {
+  int n;
+  const float* src[HLHGAT_MAX_COPY_BLOCKS];
+  float* dst[HLHGAT_MAX_COPY_BLOCKS];
+  int64_t lds[HLHGAT_MAX_COPY_BLOCKS];
+  int64_t ldd[HLHGAT_MAX_COPY_BLOCKS];
+  int64_t cols[HLHGAT_MAX_COPY_BLOCKS];
+  int64_t start[HLHGAT_MAX_COPY_BLOCKS + 1];  // element offsets of the blocks
+};
+
+__global__ __launch_bounds__(256) void k_copy2d_batched(CopyArgs a) {
+  const int64_t total = a.start[a.n];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    int b = 0;
+    while (b + 1 < a.n && e >= a.start[b + 1]) ++b;
+    const int64_t loc = e - a.start[b];
+    const int64_t r = loc / a.cols[b], c = loc % a.cols[b];
+    a.dst[b][r * a.ldd[b] + c] = a.src[b] ? a.src[b][r * a.lds[b] + c] : 0.f;
+  }
+}
+}  // namespace
+
+extern "C" int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
+                                     float* const* dst, const int64_t* ldd,
+                                     const int64_t* rows, const int64_t* cols, void* stream) {
+  HLH_CHECK_ARG(n >= 0 && n <= HLHGAT_MAX_COPY_BLOCKS, "copy2d_batched: n=%d", n);
+  CopyArgs a{};
+  a.n = n;
+  a.start[0] = 0;
+  for (int b = 0; b < n; ++b) {
+    HLH_CHECK_ARG(rows[b] >= 0 && cols[b] >= 0, "copy2d_batched: block %d: negative size", b);
+    HLH_CHECK_ARG(rows[b] * cols[b] == 0 || dst[b], "copy2d_batched: block %d: NULL dst", b);
+    HLH_CHECK_ARG(!src[b] || lds[b] >= cols[b], "copy2d_batched: block %d: lds < cols", b);
+    HLH_CHECK_ARG(rows[b] <= 1 || ldd[b] >= cols[b], "copy2d_batched: block %d: ldd < cols", b);
+    a.src[b] = src[b];
+    a.dst[b] = dst[b];
+    a.lds[b] = lds[b];
+    a.ldd[b] = ldd[b];
+    a.cols[b] = cols[b] > 0 ? cols[b] : 1;
+    a.start[b + 1] = a.start[b] + rows[b] * cols[b];
+  }
+  const int64_t total = a.start[n];
+  if (total == 0) return HLHGAT_OK;
+  int64_t g = ceil_div(total, 256);
+  if (g > 2048) g = 2048;
+  k_copy2d_batched<<<(unsigned)g, 256, 0, as_stream(stream)>>>(a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}

@@ -784,6 +784,28 @@ struct Fork {
   }
 };
 
+// One launch for a set of strided rectangles (hlhgat_copy2d_batched);
+// src == nullptr zero-fills.
+struct CopyBlocks {
+  std::vector<const float*> src;
+  std::vector<float*> dst;
+  std::vector<int64_t> lds, ldd, rows, cols;
+  void add(const float* s, int64_t ls, float* d, int64_t ld, int64_t r, int64_t c) {
+    src.push_back(s);
+    lds.push_back(ls);
+    dst.push_back(d);
+    ldd.push_back(ld);
+    rows.push_back(r);
+    cols.push_back(c);
+  }
+  void run(void* stream) {
+    if (src.empty()) return;
+    chk(hlhgat_copy2d_batched((int)src.size(), src.data(), lds.data(), dst.data(), ldd.data(),
+                              rows.data(), cols.data(), stream),
+        "copy2d_batched");
+  }
+};
+
 struct SideMlp {  // [W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4, rm4, rv4, nbt4]
   Tensor h1, a1, m1, i1, h2, y, m4, i4;
 };
@@ -807,10 +829,27 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     TORCH_CHECK(W0n.size(1) == 2 * d && W0e.size(1) == 2 * d, "hlhgat: WV first Linear expects ",
                 2 * d, " input features");
     const int64_t dn = W0n.size(0), de = W0e.size(0);
-    Tensor Wt = at::cat({W0n.narrow(1, d, d), W0e.narrow(1, 0, d)}, 0).contiguous();
-    Tensor Ws = at::cat({W0e.narrow(1, d, d), W0n.narrow(1, 0, d)}, 0).contiguous();
-    Tensor bt = at::cat({pn[1], at::zeros({de}, pn[1].options())});
-    Tensor bs = at::cat({pe[1], at::zeros({dn}, pe[1].options())});
+    // Wt = [Wn_b; We_a], Ws = [We_b; Wn_a], bt = [b_n; 0], bs = [b_e; 0]: one launch
+    Tensor Wn = W0n.stride(1) == 1 ? W0n : W0n.contiguous();
+    Tensor We = W0e.stride(1) == 1 ? W0e : W0e.contiguous();
+    Tensor bn0 = pn[1].contiguous(), be0 = pe[1].contiguous();
+    Tensor Wt = at::empty({dn + de, d}, xt.options());
+    Tensor Ws = at::empty({de + dn, d}, xt.options());
+    Tensor bt = at::empty({dn + de}, xt.options());
+    Tensor bs = at::empty({de + dn}, xt.options());
+    {
+      CopyBlocks cb;
+      const float *pwn = Wn.data_ptr<float>(), *pwe = We.data_ptr<float>();
+      cb.add(pwn + d, Wn.stride(0), Wt.data_ptr<float>(), d, dn, d);
+      cb.add(pwe, We.stride(0), Wt.data_ptr<float>() + dn * d, d, de, d);
+      cb.add(pwe + d, We.stride(0), Ws.data_ptr<float>(), d, de, d);
+      cb.add(pwn, Wn.stride(0), Ws.data_ptr<float>() + de * d, d, dn, d);
+      cb.add(bn0.data_ptr<float>(), dn, bt.data_ptr<float>(), dn, 1, dn);
+      cb.add(nullptr, 0, bt.data_ptr<float>() + dn, de, 1, de);
+      cb.add(be0.data_ptr<float>(), de, bs.data_ptr<float>(), de, 1, de);
+      cb.add(nullptr, 0, bs.data_ptr<float>() + de, dn, 1, dn);
+      cb.run(stream_of(xt));
+    }
     Tensor Yt = at::empty({N, dn + de}, xt.options());  // [Qt | P2]
     Tensor Ys = at::empty({E, de + dn}, xt.options());  // [Qs | P1]
     Tensor h1t = at::empty({N, dn}, xt.options());
@@ -948,20 +987,35 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                out[PE + 10]});
     out[0] = dxt[0];
     out[1] = dxs[0];
-    if (nW) {
-      // Wt = [Wn_b; We_a], Ws = [We_b; Wn_a]  (W0 = [W_a | W_b])
-      if (need(ctx, PN)) {
+    {
+      // Wt = [Wn_b; We_a], Ws = [We_b; Wn_a]  (W0 = [W_a | W_b]): unpack the
+      // gradients (into the flat bucket when one is set) in one launch
+      CopyBlocks cb;
+      auto rows_into = [&](Tensor& g, const Tensor& src, int64_t r0, int64_t rows, int64_t c0) {
+        cb.add(src.data_ptr<float>() + r0 * src.stride(0), src.stride(0),
+               g.data_ptr<float>() + c0, g.stride(0), rows, d);
+      };
+      if (nW && need(ctx, PN)) {
         out[PN] = grad_like(sv[30]);
-        at::cat_out(out[PN], {dWs.narrow(0, de, dn), dWt.narrow(0, 0, dn)}, 1);
+        TORCH_CHECK(out[PN].stride(1) == 1, "hlhgat: gradient of WV_Node[0] not row-major");
+        rows_into(out[PN], dWs, de, dn, 0);
+        rows_into(out[PN], dWt, 0, dn, d);
       }
-      if (need(ctx, PE)) {
+      if (nW && need(ctx, PE)) {
         out[PE] = grad_like(sv[35]);
-        at::cat_out(out[PE], {dWt.narrow(0, dn, de), dWs.narrow(0, 0, de)}, 1);
+        TORCH_CHECK(out[PE].stride(1) == 1, "hlhgat: gradient of WV_Edge[0] not row-major");
+        rows_into(out[PE], dWt, dn, de, 0);
+        rows_into(out[PE], dWs, 0, de, d);
       }
-    }
-    if (nB) {
-      if (need(ctx, PN + 1)) out[PN + 1] = grad_like(sv[31]).copy_(dbt.narrow(0, 0, dn));
-      if (need(ctx, PE + 1)) out[PE + 1] = grad_like(sv[36]).copy_(dbs.narrow(0, 0, de));
+      if (nB && need(ctx, PN + 1)) {
+        out[PN + 1] = grad_like(sv[31]);
+        cb.add(dbt.data_ptr<float>(), dn, out[PN + 1].data_ptr<float>(), dn, 1, dn);
+      }
+      if (nB && need(ctx, PE + 1)) {
+        out[PE + 1] = grad_like(sv[36]);
+        cb.add(dbs.data_ptr<float>(), de, out[PE + 1].data_ptr<float>(), de, 1, de);
+      }
+      cb.run(stream_of(xt));
     }
     (void)d;
     return out;

@@ -67,6 +67,7 @@ SIGNATURES = {
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_vp,
                                     c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_zero_fill": (c_i32, [c_vp, c_sz, c_vp]),
+    "hlhgat_copy2d_batched": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlhgat_prof_enable": (c_i32, [c_i32, c_i32]),
     "hlhgat_prof_reset": (c_i32, []),
     "hlhgat_prof_read": (c_i32, [c_i32, P_i64, P_f64, P_f64, P_f64]),

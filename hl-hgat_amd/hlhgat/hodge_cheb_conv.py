@@ -162,7 +162,7 @@ class NodeEdgeInt(nn.Module):
         """x_s2t = (1/D)·|B1| x_s and x_t2s = |B1|^T x_t / 2 (:294-295)."""
         bop = _as_boundary(par, x_t.size(0), x_s.size(0))
         inc = bop.incidence()
-        rD = (1 / D).view(-1)
+        rD = ops.reciprocal(D)
         x_s2t = ops.node_from_edges(x_s, inc, rD)
         x_t2s = ops.edge_from_nodes(x_t, inc)
         return x_s2t, x_t2s
@@ -170,7 +170,7 @@ class NodeEdgeInt(nn.Module):
     def forward(self, x_t: Tensor, x_s: Tensor, par, D: Tensor):
         if not self.only_att and x_t.is_cuda and x_t.dim() == 2:
             bop = _as_boundary(par, x_t.size(0), x_s.size(0))
-            r = ops.nei_value(x_t, x_s, bop.incidence(), (1 / D).view(-1), self.WV_Node,
+            r = ops.nei_value(x_t, x_s, bop.incidence(), ops.reciprocal(D), self.WV_Node,
                               self.WV_Edge)
             if r is not None:
                 return r

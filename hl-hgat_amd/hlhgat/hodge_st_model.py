@@ -83,12 +83,14 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
                                      edge_weight_s)
         x_s0, x_t0 = x_s, x_t
+        # the reference rebuilds par_1 and D for every block group (:623-624) from
+        # the same edge_index, so the values are identical: build them once.
+        # reference: degree(edge_index.view(-1)) sized max(index)+1 (:624); that
+        # equals N_t whenever it does not crash (1/D broadcast over x_t rows),
+        # so size it by N_t and skip the host sync of max()
+        par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
+        D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0])
         for i, _ in enumerate(self.channels):
-            par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
-            # reference: degree(edge_index.view(-1)) sized max(index)+1 (:624); that
-            # equals N_t whenever it does not crash (1/D broadcast over x_t rows),
-            # so size it by N_t and skip the host sync of max()
-            D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0])
             for j in range(self.channels[i]):
                 x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
                 x_t, x_s = getattr(self, "NEConv{}{}".format(i, j))(

@@ -193,11 +193,25 @@ class _IdCache:
 
 _HODGE_CACHE = _IdCache()
 _INC_CACHE = _IdCache()
+_RCP_CACHE = _IdCache()
 
 
 def clear_caches() -> None:
     _HODGE_CACHE.clear()
     _INC_CACHE.clear()
+    _RCP_CACHE.clear()
+
+
+def reciprocal(D: torch.Tensor) -> torch.Tensor:
+    """(1 / D).view(-1) (lib/Hodge_Cheb_Conv.py:294), computed once per D
+    tensor: every NodeEdgeInt of a block group divides by the same degrees.
+    Gradients do not flow into D (the reference's D is an integer count)."""
+    if D.requires_grad:
+        return (1 / D).view(-1)
+    hit = _RCP_CACHE.get([D], None)
+    if hit is not None:
+        return hit
+    return _RCP_CACHE.put([D], None, (1 / D).view(-1))
 
 
 def mark_hodge(edge_index: torch.Tensor) -> torch.Tensor:

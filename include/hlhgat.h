@@ -250,6 +250,15 @@ int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy
  * safe; used to initialise the BatchNorm workspace counters). */
 int hlhgat_zero_fill(void* p, size_t bytes, void* stream);
 
+/* n <= HLHGAT_MAX_COPY_BLOCKS strided fp32 rectangles in ONE launch:
+ * dst[b][r*ldd[b] + c] = src[b] ? src[b][r*lds[b] + c] : 0, r < rows[b],
+ * c < cols[b].  Packs the NodeEdgeInt first-Linear weights (replaces the
+ * torch.cat of lib/Hodge_Cheb_Conv.py:307-308's split weight blocks). */
+#define HLHGAT_MAX_COPY_BLOCKS 8
+int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
+                          float* const* dst, const int64_t* ldd, const int64_t* rows,
+                          const int64_t* cols, void* stream);
+
 /* ---- live kernel timing ------------------------------------------------ */
 #define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */
 #define HLHGAT_PROF_PROJ 1 /* MFMA projection forward */
