@@ -181,16 +181,18 @@ struct BnState {
   double momentum = 0.1, eps = 1e-5;
 };
 
-Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd) {
+Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
+                  const Tensor* y_into = nullptr) {
   const int64_t n = x.size(0), C = x.size(1);
-  Tensor y = at::empty({n, C}, x.options());
+  Tensor y = y_into ? *y_into : at::empty({n, C}, x.options());
+  TORCH_CHECK(y.size(0) == n && y.size(1) == C && y.stride(1) == 1, "hlhgat: bad BN output view");
   mean = at::empty({C}, x.options());
   invstd = at::empty({C}, x.options());
   Tensor ws = bn_workspace(x, n, C);
   int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
   chk(hlhgat_bn_fwd_train(x.data_ptr<float>(), ld_of(x), n, C, fptr(st.w), fptr(st.b),
                           mfptr(st.rm), mfptr(st.rv), nbt, (float)st.momentum, (float)st.eps,
-                          relu ? 1 : 0, y.data_ptr<float>(), C, mean.data_ptr<float>(),
+                          relu ? 1 : 0, y.data_ptr<float>(), ld_of(y), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), ws.data_ptr(), ws.numel(), stream_of(x)),
       "bn_fwd_train");
   return y;
@@ -231,7 +233,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         OptT a_val, Tensor t_rowptr, Tensor t_col, OptT t_val, int64_t nnz,
                         int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-                        int64_t bn_mode) {
+                        int64_t bn_mode, OptT out_buf) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -263,7 +265,14 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       Wp[k] = W[k].data_ptr<float>();
       ldw[k] = W[k].stride(0);
     }
-    Tensor pre = at::empty({M, dout}, x.options());
+    // out_buf: caller-owned [M, dout] destination (a column block of the dense
+    // concatenation slab, hlhgat.ops.DenseConcat); the final output lands there
+    const bool sink = has(out_buf);
+    if (sink)
+      TORCH_CHECK(out_buf->size(0) == M && out_buf->size(1) == dout && out_buf->stride(1) == 1 &&
+                      out_buf->device() == x.device(),
+                  "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
+    Tensor pre = (sink && bn_mode == 0) ? *out_buf : at::empty({M, dout}, x.options());
     if (M > 0) {
       proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, s);
     } else if (has(bias)) {
@@ -272,7 +281,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     Tensor out = pre, mean, invstd;
     if (bn_mode > 0) {
       BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps};
-      out = bn_forward(pre, st, bn_mode == 2, mean, invstd);
+      out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, Cin, F, M, dout, K, kind, nnz, bn_mode,
                                                    has(bias) ? 1 : 0};
@@ -297,6 +306,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.other();
       em.other();
       em.other();
+      em.opt(out_buf);
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["xshape"] = x.sizes().vec();
@@ -332,10 +342,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     std::vector<Tensor> W(sv.begin() + 12, sv.end());
     void* s = stream_of(x2);
     Tensor G = grads[0].reshape({M, dout});
-    G = rows2d(G).contiguous();
+    G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 18 + K;
+    const int64_t n_pos = 19 + K;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -1028,10 +1038,10 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
 Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_rowptr, Tensor t_col,
                OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-               int64_t bn_mode) {
+               int64_t bn_mode, OptT out_buf) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
-                         bn_mode);
+                         bn_mode, out_buf);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

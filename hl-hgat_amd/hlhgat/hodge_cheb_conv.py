@@ -62,8 +62,9 @@ class _HodgePolyConv(nn.Module):
     def forward(self, x: Tensor, edge_index: Tensor, edge_weight: Optional[Tensor] = None,
                 batch: Optional[Tensor] = None) -> Tensor:
         op = ops.hodge_operator(edge_index, edge_weight, x.size(0))
+        out, self._hlhgat_out = getattr(self, "_hlhgat_out", None), None
         return ops.hodge_poly_conv(x, op, [lin.weight for lin in self.lins], self.bias,
-                                   self._kind)
+                                   self._kind, out=out)
 
     def forward_bn(self, x: Tensor, edge_index: Tensor, edge_weight: Optional[Tensor],
                    bn: nn.BatchNorm1d, relu: bool) -> Tensor:
@@ -71,8 +72,10 @@ class _HodgePolyConv(nn.Module):
         every HL block, lib/Hodge_ST_Model.py:556-566); same result as the
         three modules applied in turn."""
         op = ops.hodge_operator(edge_index, edge_weight, x.size(0))
+        # one-shot output destination set by the caller (a DenseConcat sink)
+        out, self._hlhgat_out = getattr(self, "_hlhgat_out", None), None
         return ops.hodge_poly_conv(x, op, [lin.weight for lin in self.lins], self.bias,
-                                   self._kind, bn=bn, relu=relu)
+                                   self._kind, bn=bn, relu=relu, out=out)
 
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "

@@ -45,6 +45,13 @@ def _hl_block(cin_t, cin_s, cout, K, dropout_ratio, act=nn.ReLU):
     return Sequential("x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, edge_weight_s", layers)
 
 
+def _sink(block, dt, ds, width):
+    """Point the node / edge convs of an HL block (module_0 on L0, module_4 on
+    L1, see _hl_block) at the next column blocks of the dense slabs."""
+    block.module_0._hlhgat_out = dt.sink(width)
+    block.module_4._hlhgat_out = ds.sink(width)
+
+
 class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
     """ZINC regression head (lib/Hodge_ST_Model.py:544-646): HL_init_conv,
     then per block NEInt{i}{j} (NodeEdgeInt on the dense concatenation) and
@@ -80,8 +87,19 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
     def forward(self, data, device="cuda:0", if_final_layer=False):
         x_s, edge_index_s, edge_weight_s = data.x_s, data.edge_index_s, data.edge_weight_s
         x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
+        # the dense concatenations x_t0 / x_s0 (:631-632) live in one slab per
+        # side; every block's conv writes its output into its column block
+        width = self.initial_channel + sum(c * f for c, f in zip(self.channels, self.filters))
+        dense = x_t.is_cuda and x_t.dim() == 2 and ops.DENSE_SLAB
+        if dense:
+            dt = ops.DenseConcat(x_t.size(0), width, x_t)
+            ds = ops.DenseConcat(x_s.size(0), width, x_s)
+            _sink(self.HL_init_conv, dt, ds, self.initial_channel)
         x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
                                      edge_weight_s)
+        if dense:
+            dt.append(x_t)
+            ds.append(x_s)
         x_s0, x_t0 = x_s, x_t
         # the reference rebuilds par_1 and D for every block group (:623-624) from
         # the same edge_index, so the values are identical: build them once.
@@ -92,11 +110,20 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0])
         for i, _ in enumerate(self.channels):
             for j in range(self.channels[i]):
+                if dense:
+                    x_t0, x_s0 = dt.view(), ds.view()
                 x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
-                x_t, x_s = getattr(self, "NEConv{}{}".format(i, j))(
-                    x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, edge_weight_s)
-                x_t0 = torch.cat([x_t0, x_t], dim=-1)
-                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+                conv = getattr(self, "NEConv{}{}".format(i, j))
+                if dense:
+                    _sink(conv, dt, ds, self.filters[i])
+                x_t, x_s = conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                edge_weight_s)
+                if dense:
+                    dt.append(x_t)
+                    ds.append(x_s)
+                else:
+                    x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                    x_s0 = torch.cat([x_s0, x_s], dim=-1)
         x = torch.cat((mean_pool_sorted(x_s, data.num_edge1),
                        mean_pool_sorted(x_t, data.num_node1)), -1)
         for i, _ in enumerate(self.mlp_channels):

@@ -9,9 +9,10 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 import weakref
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import Tuple, List, Optional, Sequence
 
 import torch
 
@@ -404,13 +405,15 @@ def _bn_uses_batch_stats(bn) -> bool:
 
 def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.Tensor],
                     bias: Optional[torch.Tensor], kind: int = POLY_LAGUERRE,
-                    bn: Optional[torch.nn.BatchNorm1d] = None, relu: bool = False
-                    ) -> torch.Tensor:
+                    bn: Optional[torch.nn.BatchNorm1d] = None, relu: bool = False,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = sum_k T_k W_k^T + bias with T_k the Laguerre / Chebyshev basis of
     x over L (lib/Hodge_Cheb_Conv.py:480-515 / :394-439); x may be [N, C] or
     [N, T, C] (3-D inputs propagate over [N, T*C] rows, :493-505).  With
     ``bn`` the following BatchNorm (and ReLU) of the HL block runs inside the
-    same C++ autograd node (lib/Hodge_ST_Model.py:556-566)."""
+    same C++ autograd node (lib/Hodge_ST_Model.py:556-566).  ``out`` (a
+    DenseConcat sink) receives the final output when the conv, BN and ReLU run
+    as one node; otherwise it is ignored and the caller copies."""
     _req_dev(x, "x")
     if x.size(0) != op.fwd.n_rows:
         raise RuntimeError(f"hlhgat: x has {x.size(0)} rows but the operator has "
@@ -421,14 +424,107 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
         if x.size(0) < 2 and bn.training:
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
-                            ws, bias, *_bn_args(bn), 2 if relu else 1)
-    out = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
-                       bias, None, None, None, None, None, 0.0, 0.0, 0)
+                            ws, bias, *_bn_args(bn), 2 if relu else 1, out)
+    sink = out if (bn is None and not relu and x.dim() == 2) else None
+    y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
+                     bias, None, None, None, None, None, 0.0, 0.0, 0, sink)
     if bn is not None:
-        out = batch_norm_act(out, bn, relu)
+        y = batch_norm_act(y, bn, relu)
     elif relu:
-        out = torch.relu(out)
-    return out
+        y = torch.relu(y)
+    return y
+
+
+# ----------------------------------------------------------------------------
+# Dense concatenation of the HL blocks in one slab
+# ----------------------------------------------------------------------------
+DENSE_SLAB = os.environ.get("HLHGAT_DENSE_SLAB", "1") != "0"
+
+
+class DenseConcat:
+    """The running concatenation x0 = cat[y_0, y_1, ...] of the dense HL
+    blocks (lib/Hodge_ST_Model.py:631-632: x_t0 = torch.cat([x_t0, x_t], -1))
+    held in ONE preallocated [rows, width] slab.
+
+    Each block output is written straight into its column block (``sink``
+    hands the conv a destination; ``append`` copies only when the producer
+    could not write there), and ``view()`` returns x0 as a column prefix of the
+    slab: no O(depth^2) re-copies in the forward.  In the backward, every
+    view's gradient is accumulated into one gradient slab and each block's
+    output gradient is handed out as a column block of it, so the per-block
+    slice / add / copy kernels of torch.cat's backward disappear too.  Forward
+    values are identical to the torch.cat formulation; gradients are the same
+    fp32 sums, accumulated in view order (tests: tolerance of the model)."""
+
+    def __init__(self, rows: int, width: int, like: torch.Tensor):
+        self.S = torch.empty(rows, width, dtype=torch.float32, device=like.device)
+        self.width = width
+        # backward-side state shared by the views; it holds no reference to the
+        # parts, so the autograd graph and this object do not form a cycle
+        self._state = _DenseGrad(self.S)
+        self.parts: List[torch.Tensor] = []
+        self.cols: List[Tuple[int, int]] = []
+        self.owned: List[bool] = []  # part's gradient already handed to a view
+
+    @property
+    def used(self) -> int:
+        return self.cols[-1][1] if self.cols else 0
+
+    def sink(self, w: int) -> torch.Tensor:
+        c0 = self.used
+        if c0 + w > self.width:
+            raise RuntimeError(f"hlhgat: DenseConcat overflow ({c0}+{w} > {self.width})")
+        return self.S[:, c0:c0 + w]
+
+    def append(self, y: torch.Tensor) -> None:
+        if y.dim() != 2 or y.size(0) != self.S.size(0):
+            raise RuntimeError(f"hlhgat: DenseConcat rows {self.S.size(0)}, got {tuple(y.shape)}")
+        c0 = self.used
+        c1 = c0 + y.size(1)
+        if c1 > self.width:
+            raise RuntimeError(f"hlhgat: DenseConcat overflow ({c1} > {self.width})")
+        if y.data_ptr() != self.S.data_ptr() + 4 * c0 or y.stride(0) != self.S.stride(0):
+            with torch.no_grad():
+                self.S[:, c0:c1].copy_(y)
+        self.parts.append(y)
+        self.cols.append((c0, c1))
+        self.owned.append(False)
+
+    def view(self) -> torch.Tensor:
+        w = self.used
+        if not torch.is_grad_enabled() or not any(p.requires_grad for p in self.parts):
+            return self.S[:, :w]
+        # the first view created after a part was appended is the last of the
+        # views to run backward that covers it: it hands out that part's gradient
+        ranges = [(c0, c1, not o) for (c0, c1), o in zip(self.cols, self.owned)]
+        self.owned = [True] * len(self.owned)
+        return _DenseViewFn.apply(self._state, ranges, w, *self.parts)
+
+
+class _DenseGrad:
+    def __init__(self, S: torch.Tensor):
+        self.S = S
+        self.G: Optional[torch.Tensor] = None
+
+
+class _DenseViewFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, state, ranges, w, *parts):
+        ctx.state, ctx.ranges, ctx.w = state, ranges, w
+        return state.S[:, :w]
+
+    @staticmethod
+    def backward(ctx, g):
+        st, w = ctx.state, ctx.w
+        if st.G is None:
+            # first view to run backward = the widest (created last): it
+            # initialises every column the narrower views accumulate into
+            st.G = torch.empty_like(st.S)
+            st.G[:, :w].copy_(g)
+        else:
+            st.G[:, :w].add_(g)
+        grads = [st.G[:, c0:c1] if own else None for c0, c1, own in ctx.ranges]
+        return (None, None, None, *grads)
 
 
 # ----------------------------------------------------------------------------

@@ -135,3 +135,35 @@ def test_sequential_two_chain_split_cpu():
     assert torch.equal(b, torch.tanh(ls(xs)))
     chain = Sequential("x", [(lt, "x -> y"), (torch.nn.ReLU(), "y -> y")])
     assert chain._split is None
+
+
+def test_dense_concat_matches_torch_cat():
+    """ops.DenseConcat (one slab for the dense HL concatenation,
+    lib/Hodge_ST_Model.py:631-632) gives torch.cat's values and gradients."""
+    from hlhgat import ops
+    torch.manual_seed(0)
+    N = 7
+    x = torch.randn(N, 3, requires_grad=True)
+    ws = [torch.randn(3, 4)] + [torch.randn(4 * k, 4) for k in range(1, 4)]
+
+    def run(dense):
+        y0 = torch.tanh(x @ ws[0])
+        d = ops.DenseConcat(N, 16, x) if dense else None
+        x0 = y0
+        if dense:
+            d.append(y0)
+        for k in range(1, 4):
+            xin = d.view() if dense else x0
+            y = torch.sin(xin @ ws[k])
+            if dense:
+                d.append(y)
+            else:
+                x0 = torch.cat([x0, y], -1)
+        return (y ** 2).sum() + (d.view() if dense else x0).sum()
+
+    l1 = run(False)
+    g1, = torch.autograd.grad(l1, x)
+    l2 = run(True)
+    g2, = torch.autograd.grad(l2, x)
+    assert torch.equal(l1.detach(), l2.detach())
+    assert torch.allclose(g1, g2, rtol=0, atol=1e-6)
