@@ -20,6 +20,8 @@
 // agent acquire fence before reading the partials.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace hlhgat;
 
 namespace {
@@ -27,6 +29,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxParts = 128;
 constexpr int kMaxTiles = 1024;
+constexpr int APPLY_RPT = 2;  // rows per thread in the elementwise apply kernels
 
 struct BnLayout {
   int v;       // floats per thread (4 or 1)
@@ -37,6 +40,19 @@ struct BnLayout {
   int parts;   // row partitions (grid.x)
   int64_t rows_per_part;
 };
+
+// Row partitions of the statistics pass: each partition is one workgroup
+// whose loads are all in flight within a couple of round trips, and the
+// last-arriving workgroup sums `parts` partials, so fewer, fatter partitions
+// shorten that serial tail.  HLHGAT_BN_PARTS overrides (A/B measurements).
+int64_t bn_parts() {
+  static int64_t v = [] {
+    const char* e = getenv("HLHGAT_BN_PARTS");
+    int64_t p = e ? atoll(e) : 64;
+    return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
+  }();
+  return v;
+}
 
 BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   BnLayout L;
@@ -49,7 +65,7 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   L.tiles = (int)ceil_div(C, L.tile_c);
   // <= kMaxParts row partitions per column tile (fat partitions keep the
   // last arriver's reduction to one batch of loads per thread)
-  int64_t parts = kMaxParts;
+  int64_t parts = bn_parts();
   int64_t max_parts = ceil_div(n, (int64_t)L.rp * 2);
   if (parts > max_parts) parts = max_parts;
   if (parts < 1) parts = 1;
@@ -227,12 +243,12 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
   if (c < a.C) {
     int64_t r = r_lo + rg;
-    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows in flight
-      vt x4[4];
+    for (; r + 7 * a.rp < r_hi; r += 8 * a.rp) {  // 8 rows in flight
+      vt x4[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x4[u] = vload<V>(a.x + (r + u * a.rp) * a.ldx + c);
+      for (int u = 0; u < 8; ++u) x4[u] = vload<V>(a.x + (r + u * a.rp) * a.ldx + c);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           const double xd = (double)vget(x4[u], v);
@@ -306,13 +322,22 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
     s[v] = w * a.invstd[c + v];
     t[v] = b - a.mean[c + v] * s[v];
   }
-#pragma unroll 4
-  for (int64_t r = (int64_t)blockIdx.x * a.rp + rg; r < a.n; r += (int64_t)gridDim.x * a.rp) {
-    vt xv = vload<V>(a.x + r * a.ldx + c);
+  // APPLY_RPT rows per thread, all loads issued before any store
+  const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
+  vt xv[APPLY_RPT];
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r < a.n) xv[u] = vload<V>(a.x + r * a.ldx + c);
+  }
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r >= a.n) break;
     vt o;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      float z = vget(xv, v) * s[v] + t[v];
+      float z = vget(xv[u], v) * s[v] + t[v];
       vget(o, v) = (a.relu && z < 0.f) ? 0.f : z;
     }
     vstore<V>(a.y + r * a.ldy + c, o);
@@ -337,12 +362,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
     mu[v] = (c + v < a.C) ? a.save_mean[c + v] : 0.f;
   }
   if (c < a.C) {
-#pragma unroll 4
-    for (int64_t r = r_lo + rg; r < r_hi; r += a.rp) {
-      vt xv = vload<V>(a.x + r * a.ldx + c);
-      vt gv = vload<V>(a.dy + r * a.lddy + c);
-      vt yv;
-      if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+    auto acc = [&](vt xv, vt gv, vt yv) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         float g = vget(gv, v);
@@ -350,6 +370,26 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
         s0[v] += (double)g;
         s1[v] += (double)g * (double)(vget(xv, v) - mu[v]);
       }
+    };
+    int64_t r = r_lo + rg;
+    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows (12 loads) in flight
+      vt xv[4], gv[4], yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t rr = r + u * a.rp;
+        xv[u] = vload<V>(a.x + rr * a.ldx + c);
+        gv[u] = vload<V>(a.dy + rr * a.lddy + c);
+        if (a.y) yv[u] = vload<V>(a.y + rr * a.ldy + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc(xv[u], gv[u], yv[u]);
+    }
+    for (; r < r_hi; r += a.rp) {
+      vt xv = vload<V>(a.x + r * a.ldx + c);
+      vt gv = vload<V>(a.dy + r * a.lddy + c);
+      vt yv;
+      if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+      acc(xv, gv, yv);
     }
   }
   write_partials<V>(s0, s1, a, c0);
@@ -405,18 +445,27 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     B[v] = a.coef[a.C + c + v];
     Cc[v] = a.coef[2 * a.C + c + v];
   }
-#pragma unroll 4
-  for (int64_t r = (int64_t)blockIdx.x * a.rp + rg; r < a.n; r += (int64_t)gridDim.x * a.rp) {
-    vt xv = vload<V>(a.x + r * a.ldx + c);
-    vt gv = vload<V>(a.dy + r * a.lddy + c);
-    vt yv;
-    if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+  const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
+  vt xv[APPLY_RPT], gv[APPLY_RPT], yv[APPLY_RPT];
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r < a.n) {
+      xv[u] = vload<V>(a.x + r * a.ldx + c);
+      gv[u] = vload<V>(a.dy + r * a.lddy + c);
+      if (a.y) yv[u] = vload<V>(a.y + r * a.ldy + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r >= a.n) break;
     vt o;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      float g = vget(gv, v);
-      if (a.y && !(vget(yv, v) > 0.f)) g = 0.f;
-      vget(o, v) = A[v] * g + (B[v] * vget(xv, v) + Cc[v]);
+      float g = vget(gv[u], v);
+      if (a.y && !(vget(yv[u], v) > 0.f)) g = 0.f;
+      vget(o, v) = A[v] * g + (B[v] * vget(xv[u], v) + Cc[v]);
     }
     vstore<V>(a.dx + r * a.lddx + c, o);
   }
@@ -433,8 +482,7 @@ bool bn_vec_ok(int64_t C, std::initializer_list<int64_t> lds,
 }
 
 unsigned apply_grid_x(int64_t n, int rp) {
-  int64_t g = ceil_div(n, rp * 8);  // ~8 rows per thread
-  if (g > 2048) g = 2048;
+  int64_t g = ceil_div(n, (int64_t)rp * APPLY_RPT);  // every row owned by one thread
   if (g < 1) g = 1;
   return (unsigned)g;
 }

@@ -18,6 +18,8 @@
 // from L1/L2), 4 waves per workgroup stacked along M.
 #include "common.h"
 
+#include <cstdlib>
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 using namespace hlhgat;
@@ -209,6 +211,64 @@ __device__ __forceinline__ void load_a_chunk(const float* arow, bool valid, int 
   }
 }
 
+// Epilogue through LDS: a wave's 16 x (TN*16) accumulator tile (lane (q,i)
+// holds rows 4q..4q+3 of column i) is transposed in a per-wave LDS scratch
+// (pitch TN*16+4: the 64 lanes' writes hit 64 distinct banks) and written
+// back as whole-row float4 stores (each store instruction covers 4 full
+// 64-column rows) instead of 4-byte column-strided stores.
+template <int TN>
+__device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[TN], float* scratch,
+                                                int64_t row0, int64_t M, float* dst0,
+                                                int64_t ld, int ncols, const float* bias,
+                                                int accumulate, bool vec_ok) {
+  constexpr int CT = TN * 16, P = CT + 4;
+  const int lane = threadIdx.x & 63, q = lane >> 4, i = lane & 15;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int col = tn * 16 + i;
+    const float bv = (bias && col < ncols) ? bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = acc[tn][r];
+      if (bias) v = v + bv;
+      scratch[(4 * q + r) * P + col] = v;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (vec_ok) {
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int idx = lane + 64 * u;
+      const int r = idx / (CT / 4), c4 = idx % (CT / 4);
+      const int64_t row = row0 + r;
+      if (row < M && 4 * c4 < ncols) {
+        float4 v = *reinterpret_cast<const float4*>(&scratch[r * P + 4 * c4]);
+        float4* d = reinterpret_cast<float4*>(dst0 + row * ld + 4 * c4);
+        if (accumulate) {
+          const float4 o = *d;
+          v.x = o.x + v.x;
+          v.y = o.y + v.y;
+          v.z = o.z + v.z;
+          v.w = o.w + v.w;
+        }
+        *d = v;
+      }
+    }
+  } else {
+    for (int idx = lane; idx < 16 * CT; idx += 64) {
+      const int r = idx / CT, c = idx % CT;
+      const int64_t row = row0 + r;
+      if (row < M && c < ncols) {
+        float* d = dst0 + row * ld + c;
+        const float v = scratch[r * P + c];
+        *d = accumulate ? *d + v : v;
+      }
+    }
+  }
+}
+
 template <int TN>
 __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
   __shared__ float wl[2][TN * 16][KCP];
@@ -269,22 +329,13 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
     k0 = nk;
   }
 
-  if (m_base >= a.M) return;
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int col = n_base + tn * 16 + i;
-    if (col >= a.N) continue;
-    const float bv = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t rr = m_base + 4 * q + r;
-      if (rr >= a.M) continue;
-      float v = acc[tn][r];
-      if (a.bias) v = v + bv;
-      float* dst = a.C + rr * a.ldc + col;
-      *dst = a.accumulate ? *dst + v : v;
-    }
-  }
+  // every wave is past the loop's last barrier: wl is free for the epilogue
+  float* scratch = &wl[0][0][0] + wave * 16 * (TN * 16 + 4);
+  const int ncols = a.N - n_base < TN * 16 ? a.N - n_base : TN * 16;
+  const bool vec_ok = (a.N % 4) == 0 && (a.ldc % 4) == 0 &&
+                      (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
+  store_tile_rows<TN>(acc, scratch, m_base, a.M, a.C + n_base, a.ldc, ncols,
+                      a.bias ? a.bias + n_base : nullptr, a.accumulate, vec_ok);
 }
 
 // ---------------------------------------------------------------------------
@@ -462,22 +513,11 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data_lds(BwdDataArgs a) {
     __syncthreads();
     buf ^= 1;
   }
-  if (m_base >= a.M) return;
-  float* __restrict__ O = a.O[b];
-  const int64_t ldo = a.ldo[b];
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int col = c_base + tn * 16 + i;
-    if (col >= kb) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t rr = m_base + 4 * q + r;
-      if (rr >= a.M) continue;
-      float* dst = O + rr * ldo + col;
-      const float v = acc[tn][r];
-      *dst = a.accumulate ? *dst + v : v;
-    }
-  }
+  float* scratch = &wl[0][0][0] + wave * 16 * (TN * 16 + 4);
+  const int ncols = kb - c_base < TN * 16 ? kb - c_base : TN * 16;
+  const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
+  store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
+                      a.accumulate, vec_ok);
 }
 
 // ---------------------------------------------------------------------------
@@ -694,16 +734,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float bsum = 0.f;
   const int rl = lane >> 5, cl = lane & 31;
-  float4 g[2], x[2];
-  int buf = 0;
-  if (m_lo < m_hi) {
-    load(m_lo, g, x);
-    store(0, g, x);
-  }
-  __syncthreads();
-  for (int64_t m0 = m_lo; m0 < m_hi; m0 += WR) {
-    const bool has_next = m0 + WR < m_hi;
-    if (has_next) load(m0 + WR, g, x);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < WR / 2; ++kk) {
       const float av = gl[buf][2 * kk + rl][32 * wn + cl];
@@ -711,9 +742,26 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
       bsum = bsum + av;
     }
-    if (has_next) store(buf ^ 1, g, x);
+  };
+  // two chunks in flight in registers while one is consumed from LDS
+  float4 g0[2], x0[2], g1[2], x1[2];
+  const int64_t nchunk = m_hi > m_lo ? (m_hi - m_lo + WR - 1) / WR : 0;
+  if (nchunk > 0) load(m_lo, g0, x0);
+  if (nchunk > 1) load(m_lo + WR, g1, x1);
+  if (nchunk > 0) store(0, g0, x0);
+  __syncthreads();
+  for (int64_t c = 0; c < nchunk; c += 2) {
+    // chunk c in LDS[0], chunk c+1 in (g1, x1)
+    if (c + 2 < nchunk) load(m_lo + (c + 2) * WR, g0, x0);
+    compute(0);
+    if (c + 1 < nchunk) store(1, g1, x1);
     __syncthreads();
-    buf ^= 1;
+    if (c + 1 >= nchunk) break;
+    // chunk c+1 in LDS[1], chunk c+2 in (g0, x0)
+    if (c + 3 < nchunk) load(m_lo + (c + 3) * WR, g1, x1);
+    compute(1);
+    if (c + 2 < nchunk) store(0, g0, x0);
+    __syncthreads();
   }
 
   float* slab = a.part + (int64_t)blockIdx.z * a.part_stride + a.part_off[b];
@@ -775,9 +823,17 @@ __global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
   }
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   if (src >= 0) {
-    int it = 0;
-    for (int sp = grp; sp < a.splits; sp += 4, ++it)
-      s[it & 3] = s[it & 3] + a.part[(int64_t)sp * a.part_stride + src];
+    // splits grp, grp+4, ... in batches of 8 independent loads
+    for (int sp0 = grp; sp0 < a.splits; sp0 += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int sp = sp0 + 4 * u;
+        v[u] = sp < a.splits ? a.part[(int64_t)sp * a.part_stride + src] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u & 3] = s[u & 3] + v[u];
+    }
   }
   red[grp][lane] = (s[0] + s[1]) + (s[2] + s[3]);
   __syncthreads();
@@ -798,6 +854,15 @@ struct WeightPlan {
   int64_t bias_off;
   int tile_start[MAXB + 1];
 };
+
+// HLHGAT_WSPLIT_ROWS: rows per weight-gradient split (A/B; 0 = plan below)
+int64_t wsplit_rows() {
+  static int64_t v = [] {
+    const char* e = getenv("HLHGAT_WSPLIT_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  return v;
+}
 
 WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
                        bool with_bias) {
@@ -822,10 +887,21 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   if (splits < 1) splits = 1;
   int64_t rps = ceil_div(M, splits);
   rps = ceil_div(rps, 64) * 64;
+  if (wsplit_rows() > 0) rps = ceil_div(wsplit_rows(), 64) * 64;
   if (rps < 64) rps = 64;
   p.rows_per_split = rps;
   p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
   return p;
+}
+
+// HLHGAT_PROJ_TN caps the 16-column tiles per wave (A/B of the wave count
+// against the SIMD count; 0 = default)
+int proj_tn() {
+  static int v = [] {
+    const char* e = getenv("HLHGAT_PROJ_TN");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 bool vec_ok(const float* p, int64_t ld, int64_t kb) {
@@ -868,7 +944,18 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   }
   if (M == 0) return HLHGAT_OK;
   hipStream_t s = as_stream(stream);
-  const int tn = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
+  // 16-column tiles per wave: enough waves to cover the 1024 SIMDs several
+  // times over (measured at the HL-HGAT shapes, tools/kbench.py): small M ->
+  // 1, K <= 256 -> 2 (re-reading A from L2 is cheap), long K -> 4
+  int64_t ktot = 0;
+  for (int b = 0; b < nblocks; ++b) ktot += kb[b];
+  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
+  if (N <= 16) tn = 1;
+  else if (N <= 32 && tn > 2) tn = 2;
+  if (proj_tn()) {
+    const int cap = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
+    tn = proj_tn() < cap ? proj_tn() : cap;
+  }
   const int tm = M >= 262144 ? 2 : 1;
   dim3 grid((unsigned)ceil_div(M, 4 * tm * 16), (unsigned)ceil_div(N, tn * 16));
   double bytes = 4.0 * (double)M * N;
@@ -915,6 +1002,10 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   a.ldg = lddc;
   a.accumulate = accumulate;
   const int TN = 4;
+  int64_t ktot = 0;
+  for (int b = 0; b < nblocks; ++b) ktot += kb[b];
+  int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // see proj_fwd
+  if (proj_tn()) tnd = proj_tn();
   a.tile_start[0] = 0;
   for (int b = 0; b < nblocks; ++b) {
     HLH_CHECK_ARG(W[b] && dA[b] && kb[b] > 0 && ldw[b] >= kb[b] && ldda[b] >= kb[b],
@@ -924,7 +1015,7 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
     a.ldw[b] = ldw[b];
     a.ldo[b] = ldda[b];
     a.kb[b] = (int)kb[b];
-    a.tile_start[b + 1] = a.tile_start[b] + (int)ceil_div(kb[b], TN * 16);
+    a.tile_start[b + 1] = a.tile_start[b] + (int)ceil_div(kb[b], tnd * 16);
   }
   if (M == 0) return HLHGAT_OK;
   bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
@@ -933,9 +1024,23 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   hipStream_t s = as_stream(stream);
   dim3 grid((unsigned)ceil_div(M, 4 * 16), (unsigned)a.tile_start[nblocks]);
   if (vec)
-    k_proj_bwd_data_lds<TN><<<grid, 256, 0, s>>>(a);
+  {
+    if (tnd == 1)
+      k_proj_bwd_data_lds<1><<<grid, 256, 0, s>>>(a);
+    else if (tnd == 2)
+      k_proj_bwd_data_lds<2><<<grid, 256, 0, s>>>(a);
+    else
+      k_proj_bwd_data_lds<TN><<<grid, 256, 0, s>>>(a);
+  }
   else
-    k_proj_bwd_data<1, TN, false><<<grid, 256, 0, s>>>(a);
+  {
+    if (tnd == 1)
+      k_proj_bwd_data<1, 1, false><<<grid, 256, 0, s>>>(a);
+    else if (tnd == 2)
+      k_proj_bwd_data<1, 2, false><<<grid, 256, 0, s>>>(a);
+    else
+      k_proj_bwd_data<1, TN, false><<<grid, 256, 0, s>>>(a);
+  }
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
