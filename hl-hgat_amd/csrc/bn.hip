@@ -387,7 +387,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
     for (; r < r_hi; r += a.rp) {
       vt xv = vload<V>(a.x + r * a.ldx + c);
       vt gv = vload<V>(a.dy + r * a.lddy + c);
-      vt yv;
+      vt yv = gv;
       if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
       acc(xv, gv, yv);
     }

@@ -18,6 +18,7 @@ using namespace hlhgat;
 namespace {
 
 struct PolyArgs {
+  const int32_t* order;  // optional row schedule: slot -> row (a permutation)
   const int32_t* rowptr;
   const int32_t* col;
   const float* val;
@@ -33,53 +34,78 @@ struct PolyArgs {
   float alpha, beta, gamma, div, p, q;
 };
 
+// Row r's CSR entries are staged LPR at a time: lane `sub` of the row group
+// loads entry eb+sub's column and weight with ONE coalesced load, and the
+// group broadcasts them with __shfl (ds_bpermute) while it walks the entries
+// in CSR order.  The per-entry index / weight traffic thus leaves the vector
+// memory pipe, which then carries only the gathered feature rows (the cost
+// that bounds this kernel at TSP scale: ~20 gathered 512-B rows per output
+// row).  Summation order is unchanged: acc += w_e * X[c_e] for e ascending.
+__device__ __forceinline__ unsigned xcd_slot(unsigned b, unsigned nb) {
+  const unsigned x = b & 7u, k = b >> 3, per = nb >> 3, extra = nb & 7u;
+  return x * per + (x < extra ? x : extra) + k;
+}
+
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
   using vt = typename VecT<V>::type;
-  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  // XCD-aware slots: blocks are dealt round-robin over the 8 XCDs, so block b
+  // takes slot range xcd_slot(b): each XCD walks ONE contiguous range of the
+  // (optionally locality-ordered) row schedule and its L2 sees the neighbours
+  // of the rows it is working on.
+  const int64_t slot = ((int64_t)xcd_slot(blockIdx.x, gridDim.x) * 256 + threadIdx.x) / LPR;
   const int sub = threadIdx.x % LPR;
-  if (row >= a.n_rows) return;
-  const int e0 = a.rowptr[row];
-  const int e1 = a.rowptr[row + 1];
-  const float rsv = a.rs ? a.rs[row] : 1.f;
+  const bool live = slot < a.n_rows;
+  const int64_t row = live ? (a.order ? (int64_t)a.order[slot] : slot) : 0;
+  const int64_t rr = row;
+  const int e0 = live ? a.rowptr[rr] : 0;
+  const int e1 = live ? a.rowptr[rr + 1] : 0;
+  const float rsv = (live && a.rs) ? a.rs[rr] : 1.f;
   const float* __restrict__ X = a.X;
-  for (int f = sub * V; f < a.d; f += LPR * V) {
+  for (int f0 = 0; f0 < a.d; f0 += LPR * V) {
+    const int f = f0 + sub * V;
+    const bool fok = live && f < a.d;
     vt acc;
 #pragma unroll
     for (int i = 0; i < V; ++i) vget(acc, i) = 0.f;
-    int e = e0;
-    // four gathers in flight per lane before the (sequential) accumulation
-    for (; e + 3 < e1; e += 4) {
-      const int c0 = a.col[e], c1 = a.col[e + 1], c2 = a.col[e + 2],
-                c3 = a.col[e + 3];
-      float w0 = 1.f, w1 = 1.f, w2 = 1.f, w3 = 1.f;
-      if (a.val) {
-        w0 = a.val[e];
-        w1 = a.val[e + 1];
-        w2 = a.val[e + 2];
-        w3 = a.val[e + 3];
-      }
-      vt x0 = vload<V>(X + (int64_t)c0 * a.ldx + f);
-      vt x1 = vload<V>(X + (int64_t)c1 * a.ldx + f);
-      vt x2 = vload<V>(X + (int64_t)c2 * a.ldx + f);
-      vt x3 = vload<V>(X + (int64_t)c3 * a.ldx + f);
+    for (int eb = e0; eb < e1; eb += LPR) {
+      const int me = eb + sub;
+      const int cm = me < e1 ? a.col[me] : 0;
+      const float wm = me < e1 ? (a.val ? a.val[me] : 1.f) : 0.f;
+      const int cnt = e1 - eb < LPR ? e1 - eb : LPR;
+      int j = 0;
+      for (; j + 3 < cnt; j += 4) {  // four gathers in flight per lane
+        const int c0 = __shfl(cm, j, LPR), c1 = __shfl(cm, j + 1, LPR),
+                  c2 = __shfl(cm, j + 2, LPR), c3 = __shfl(cm, j + 3, LPR);
+        const float w0 = __shfl(wm, j, LPR), w1 = __shfl(wm, j + 1, LPR),
+                    w2 = __shfl(wm, j + 2, LPR), w3 = __shfl(wm, j + 3, LPR);
+        if (fok) {
+          vt x0 = vload<V>(X + (int64_t)c0 * a.ldx + f);
+          vt x1 = vload<V>(X + (int64_t)c1 * a.ldx + f);
+          vt x2 = vload<V>(X + (int64_t)c2 * a.ldx + f);
+          vt x3 = vload<V>(X + (int64_t)c3 * a.ldx + f);
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
-        float s = vget(acc, i);
-        s = s + w0 * vget(x0, i);
-        s = s + w1 * vget(x1, i);
-        s = s + w2 * vget(x2, i);
-        s = s + w3 * vget(x3, i);
-        vget(acc, i) = s;
+          for (int i = 0; i < V; ++i) {
+            float s = vget(acc, i);
+            s = s + w0 * vget(x0, i);
+            s = s + w1 * vget(x1, i);
+            s = s + w2 * vget(x2, i);
+            s = s + w3 * vget(x3, i);
+            vget(acc, i) = s;
+          }
+        }
+      }
+      for (; j < cnt; ++j) {
+        const int c = __shfl(cm, j, LPR);
+        const float w = __shfl(wm, j, LPR);
+        if (fok) {
+          vt x = vload<V>(X + (int64_t)c * a.ldx + f);
+#pragma unroll
+          for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
+        }
       }
     }
-    for (; e < e1; ++e) {
-      const int c = a.col[e];
-      const float w = a.val ? a.val[e] : 1.f;
-      vt x = vload<V>(X + (int64_t)c * a.ldx + f);
-#pragma unroll
-      for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
-    }
+    if (!fok) continue;
     vt out;
 #pragma unroll
     for (int i = 0; i < V; ++i) vget(out, i) = a.alpha * (rsv * vget(acc, i));
@@ -309,8 +335,9 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
 
 PolyArgs make_args(const int32_t* rowptr, const int32_t* col, const float* val,
                    int64_t n, const float* X, int64_t ldx, int64_t d, float* Y,
-                   int64_t ldy) {
+                   int64_t ldy, const int32_t* order = nullptr) {
   PolyArgs a{};
+  a.order = order;
   a.rowptr = rowptr;
   a.col = col;
   a.val = val;
@@ -336,21 +363,22 @@ using namespace hlhgat;
 
 extern "C" int hlhgat_spmm(const int32_t* rowptr, const int32_t* col,
                            const float* val, int64_t n_rows, int64_t nnz,
-                           const float* X, int64_t ldx, int64_t d, float* Y,
-                           int64_t ldy, void* stream) {
-  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy);
+                           const int32_t* row_order, const float* X, int64_t ldx,
+                           int64_t d, float* Y, int64_t ldy, void* stream) {
+  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy, row_order);
   return launch_poly(a, nnz, as_stream(stream));
 }
 
 extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
                                 const float* val, const float* rs,
-                                int64_t n_rows, int64_t nnz, const float* X,
+                                int64_t n_rows, int64_t nnz,
+                                const int32_t* row_order, const float* X,
                                 int64_t ldx, int64_t d, const float* Z,
                                 int64_t ldz, const float* P, int64_t ldp,
                                 const float* Q, int64_t ldq, float alpha,
                                 float beta, float gamma, float div, float p,
                                 float q, float* Y, int64_t ldy, void* stream) {
-  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy);
+  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy, row_order);
   a.rs = rs;
   a.Z = Z;
   a.ldz = ldz;
@@ -369,7 +397,8 @@ extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
 
 extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
                                      const int32_t* col, const float* val,
-                                     int64_t n, int64_t nnz, const float* X,
+                                     int64_t n, int64_t nnz,
+                                     const int32_t* row_order, const float* X,
                                      int64_t ldx, int64_t F, int K, float* T,
                                      void* stream) {
   HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
@@ -382,7 +411,7 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
   auto Tk = [&](int k) -> float* { return T + (int64_t)(k - 1) * blk; };
   // T_1
   {
-    PolyArgs a = make_args(rowptr, col, val, n, X, ldx, F, Tk(1), F);
+    PolyArgs a = make_args(rowptr, col, val, n, X, ldx, F, Tk(1), F, row_order);
     if (kind == HLHGAT_POLY_LAGUERRE) {  // Tx_1 = x - L x   (:494)
       a.alpha = -1.f;
       a.beta = 1.f;
@@ -393,7 +422,7 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
   for (int k = 1; k + 1 < K; ++k) {
     const float* prev = (k == 1) ? X : Tk(k - 1);
     const int64_t ldprev = (k == 1) ? ldx : F;
-    PolyArgs a = make_args(rowptr, col, val, n, Tk(k), F, F, Tk(k + 1), F);
+    PolyArgs a = make_args(rowptr, col, val, n, Tk(k), F, F, Tk(k + 1), F, row_order);
     a.Z = prev;
     a.ldz = ldprev;
     if (kind == HLHGAT_POLY_LAGUERRE) {
@@ -415,7 +444,8 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
 
 extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                                      const int32_t* col_t, const float* val_t,
-                                     int64_t n, int64_t nnz, int64_t F, int K,
+                                     int64_t n, int64_t nnz,
+                                     const int32_t* row_order, int64_t F, int K,
                                      float* G, void* stream) {
   HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
                 "poly_basis_bwd: bad kind %d", kind);
@@ -426,7 +456,7 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
   const int64_t blk = n * F;
   auto Gk = [&](int k) -> float* { return G + (int64_t)k * blk; };
   for (int k = K - 1; k >= 1; --k) {
-    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F);
+    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F, row_order);
     a.P = Gk(k - 1);
     a.ldp = F;
     a.p = 1.f;

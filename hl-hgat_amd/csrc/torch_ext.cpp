@@ -36,6 +36,9 @@ using OptT = std::optional<Tensor>;
 inline void* stream_of(const Tensor& t) {
   return c10::hip::getCurrentHIPStream(t.get_device()).stream();
 }
+inline const int32_t* iptr(const std::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr<int32_t>() : nullptr;
+}
 inline void chk(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "hlhgat: ", what, " failed: ", hlhgat_last_error());
 }
@@ -233,7 +236,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         OptT a_val, Tensor t_rowptr, Tensor t_col, OptT t_val, int64_t nnz,
                         int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-                        int64_t bn_mode, OptT out_buf) {
+                        int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -247,7 +250,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     if (K > 1 && N > 0) {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
-                                nnz ? fptr(a_val) : nullptr, N, nnz, x2.data_ptr<float>(),
+                                nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
+                                x2.data_ptr<float>(),
                                 ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
           "poly_basis_fwd");
     }
@@ -307,11 +311,14 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.other();
       em.other();
       em.opt(out_buf);
+      em.opt(a_order);
+      em.opt(t_order);
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["xshape"] = x.sizes().vec();
     std::vector<Tensor> save = {x2,
                                 T,
+                                has(t_order) ? *t_order : Tensor(),
                                 t_rowptr,
                                 t_col,
                                 has(t_val) ? *t_val : Tensor(),
@@ -336,16 +343,16 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     const bool has_bias = d[9] != 0;
     auto xshape = ctx->saved_data["xshape"].toIntVector();
     auto sv = ctx->get_saved_variables();
-    Tensor x2 = sv[0], T = sv[1], t_rowptr = sv[2], t_col = sv[3], t_val = sv[4], pre = sv[5],
-           yout = sv[6], mean = sv[7], invstd = sv[8], bn_w = sv[9], bias_p = sv[10],
-           bn_b = sv[11];
-    std::vector<Tensor> W(sv.begin() + 12, sv.end());
+    Tensor x2 = sv[0], T = sv[1], t_order = sv[2], t_rowptr = sv[3], t_col = sv[4],
+           t_val = sv[5], pre = sv[6], yout = sv[7], mean = sv[8], invstd = sv[9], bn_w = sv[10],
+           bias_p = sv[11], bn_b = sv[12];
+    std::vector<Tensor> W(sv.begin() + 13, sv.end());
     void* s = stream_of(x2);
     Tensor G = grads[0].reshape({M, dout});
     G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 19 + K;
+    const int64_t n_pos = 21 + K;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -404,7 +411,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
           chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
                                     nnz ? t_col.data_ptr<int>() : nullptr,
                                     (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
-                                    N, nnz, F, (int)K, Gs.data_ptr<float>(), s),
+                                    N, nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
+                                    F, (int)K, Gs.data_ptr<float>(), s),
               "poly_basis_bwd");
         }
       } else {
@@ -672,7 +680,7 @@ Tensor node_segment(const Tensor& rowptr, const Tensor& eids, int64_t n_nodes, i
   Tensor out = at::empty({n_nodes, x.size(1)}, x.options());
   if (n_nodes > 0) {
     chk(hlhgat_poly_step(rowptr.data_ptr<int>(), n_edges ? eids.data_ptr<int>() : nullptr,
-                         nullptr, rs, n_nodes, 2 * n_edges, x.data_ptr<float>(), ld_of(x),
+                         nullptr, rs, n_nodes, 2 * n_edges, nullptr, x.data_ptr<float>(), ld_of(x),
                          x.size(1), nullptr, 0, nullptr, 0, nullptr, 0, alpha, 0.f, 0.f, 1.f,
                          0.f, 0.f, out.data_ptr<float>(), ld_of(out), stream_of(x)),
         "poly_step(incidence)");
@@ -899,7 +907,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     }
     if (N > 0) {  // node side: h1_t = Qt + rD * |B1| P1, then its MLP
       chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
-                           rD.data_ptr<float>(), N, 2 * E, Ys.data_ptr<float>() + de, de + dn, dn,
+                           rD.data_ptr<float>(), N, 2 * E, nullptr, Ys.data_ptr<float>() + de,
+                           de + dn, dn,
                            Yt.data_ptr<float>(), dn + de, nullptr, 0, nullptr, 0, 1.f, 0.f, 1.f,
                            1.f, 0.f, 0.f, h1t.data_ptr<float>(), dn, fk.main.stream()),
           "poly_step(nei node)");
@@ -979,7 +988,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     // dP2[v] = 1/2 sum_{e ni v} dh1_s[e]  -> dYt[:, dn:]
     if (N > 0) {
       chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
-                           nullptr, N, 2 * E, dYs.data_ptr<float>(), de + dn, de, nullptr, 0,
+                           nullptr, N, 2 * E, nullptr, dYs.data_ptr<float>(), de + dn, de,
+                           nullptr, 0,
                            nullptr, 0, nullptr, 0, 0.5f, 0.f, 0.f, 1.f, 0.f, 0.f,
                            dYt.data_ptr<float>() + dn, dn + de, fk.main.stream()),
           "poly_step(nei node bwd)");
@@ -1038,10 +1048,10 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
 Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_rowptr, Tensor t_col,
                OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-               int64_t bn_mode, OptT out_buf) {
+               int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
-                         bn_mode, out_buf);
+                         bn_mode, out_buf, a_order, t_order);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

@@ -20,9 +20,9 @@ import numpy as np
 import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
-           "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric"]
+           "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order"]
 
-_INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index")
+_INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
 _HODGE_KEYS = ("edge_index_s", "edge_index_t")
 
 
@@ -44,9 +44,9 @@ class PairData:
 
     def __inc__(self, key: str, value=None) -> int:
         """Batching offset per key (lib/Hodge_Dataset.py:40-48)."""
-        if key == "edge_index_s":
+        if key in ("edge_index_s", "row_order_s"):
             return self.x_s.size(0)
-        if key in ("edge_index", "edge_index_t"):
+        if key in ("edge_index", "edge_index_t", "row_order_t"):
             return self.x_t.size(0)
         return 0
 
@@ -88,13 +88,15 @@ class Batch(PairData):
         return self
 
     def _mark(self) -> None:
-        if getattr(self, "hodge_sorted", None) is None:
-            return
-        for k, ok in self.hodge_sorted.items():
+        from .ops import mark_hodge, set_row_order
+        for k, ok in (getattr(self, "hodge_sorted", None) or {}).items():
             t = getattr(self, k, None)
             if ok and torch.is_tensor(t) and t.is_cuda:
-                from .ops import mark_hodge
                 mark_hodge(t)
+        for k, ko in (("edge_index_s", "row_order_s"), ("edge_index_t", "row_order_t")):
+            t, o = getattr(self, k, None), getattr(self, ko, None)
+            if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(o):
+                set_row_order(t, o)
 
     @property
     def batch_t(self) -> torch.Tensor:
@@ -105,6 +107,24 @@ class Batch(PairData):
     def batch_s(self) -> torch.Tensor:
         return torch.repeat_interleave(torch.arange(self.num_graphs, device=self.x_s.device),
                                        self.num_edge1.to(self.x_s.device))
+
+
+def locality_order(edge_index, n: int) -> torch.Tensor:
+    """Row schedule for the SpMM of a large Laplacian: reverse Cuthill-McKee
+    order of its sparsity pattern (int64 permutation of range(n)).
+
+    Rows visited in this order share most of their neighbours with the rows
+    visited just before them, so each XCD's L2 (the kernel walks one
+    contiguous range of the schedule per XCD) serves the gathers that a
+    natural order would send to the Infinity Cache.  A schedule only: results
+    are bitwise those of the natural order (hlhgat_spmm, row_order).  Built
+    once per graph with the Hodge Laplacians (host side, like
+    lib/Hodge_Dataset.py:451-468)."""
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    ei = np.asarray(edge_index)
+    A = sp.csr_matrix((np.ones(ei.shape[1], dtype=np.int8), (ei[0], ei[1])), shape=(n, n))
+    return torch.from_numpy(reverse_cuthill_mckee(A, symmetric_mode=True).astype(np.int64))
 
 
 def is_sorted_symmetric(ei: np.ndarray, w: Optional[np.ndarray]) -> bool:
@@ -136,7 +156,7 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
         if k in _INC_KEYS:
             incs = np.array([g.__inc__(k) for g in graphs], dtype=np.int64)
             off = np.concatenate([[0], np.cumsum(incs)[:-1]])
-            cat = np.concatenate([np.asarray(v) + o for v, o in zip(vals, off)], axis=1)
+            cat = np.concatenate([np.asarray(v) + o for v, o in zip(vals, off)], axis=-1)
             setattr(b, k, torch.from_numpy(np.ascontiguousarray(cat)))
         elif torch.is_tensor(v0):
             if v0.dim() == 0:

@@ -102,10 +102,15 @@ int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
 
 /* ---- SpMM and fused polynomial step ----------------------------------- */
 /* Y = A·X (PyG propagate with aggr='add', source_to_target, when A is the
- * CSR keyed by edge_index[1]).  X,Y [n][d] with row strides ldx, ldy. */
+ * CSR keyed by edge_index[1]).  X,Y [n][d] with row strides ldx, ldy.
+ * row_order (optional, int32[n_rows], a permutation) is the order in which
+ * rows are SCHEDULED (e.g. hlhgat_locality_order): results are identical for
+ * any order (each row's entries are still summed in CSR order); only which
+ * rows share an XCD's L2 at a time changes.  NULL = natural order. */
 int hlhgat_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
-                int64_t n_rows, int64_t nnz, const float* X, int64_t ldx,
-                int64_t d, float* Y, int64_t ldy, void* stream);
+                int64_t n_rows, int64_t nnz, const int32_t* row_order,
+                const float* X, int64_t ldx, int64_t d, float* Y, int64_t ldy,
+                void* stream);
 
 /* Generic fused step (one launch):
  *   Y = (alpha * rs[r] * (A·X)[r] + beta*X[r] + gamma*Z[r]) / div
@@ -115,7 +120,8 @@ int hlhgat_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
  * beta != 0; otherwise X may have any row count >= max(col)+1. */
 int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
                      const float* val, const float* rs, int64_t n_rows,
-                     int64_t nnz, const float* X, int64_t ldx, int64_t d,
+                     int64_t nnz, const int32_t* row_order, const float* X,
+                     int64_t ldx, int64_t d,
                      const float* Z, int64_t ldz, const float* P, int64_t ldp,
                      const float* Q, int64_t ldq, float alpha, float beta,
                      float gamma, float div, float p, float q, float* Y,
@@ -130,8 +136,8 @@ int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
  * X: [n][F] row stride ldx.  T: (K-1) contiguous blocks of [n][F]. */
 int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
                           const float* val, int64_t n, int64_t nnz,
-                          const float* X, int64_t ldx, int64_t F, int K,
-                          float* T, void* stream);
+                          const int32_t* row_order, const float* X, int64_t ldx,
+                          int64_t F, int K, float* T, void* stream);
 
 /* Adjoint of hlhgat_poly_basis_fwd.  On entry G holds K contiguous blocks
  * [n][F]: G_k = dLoss/dT_k from the consumers of each T_k (block 0 = the
@@ -140,8 +146,8 @@ int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
  * Laplacians). */
 int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                           const int32_t* col_t, const float* val_t, int64_t n,
-                          int64_t nnz, int64_t F, int K, float* G,
-                          void* stream);
+                          int64_t nnz, const int32_t* row_order, int64_t F,
+                          int K, float* G, void* stream);
 
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
 #define HLHGAT_MAX_BLOCKS 16

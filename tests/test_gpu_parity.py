@@ -445,3 +445,54 @@ def test_nei_value_projected_first_matches_gather_first(cuda, d, dv, monkeypatch
     ref, new = run(False), run(True)
     for k in ref:
         close(new[k], ref[k], 1e-4 if k.startswith(("g", "grad")) else 1e-5, k)
+
+
+# ---------------------------------------------------------------------------
+# row schedules (locality_order) and XCD-aware slots never change results
+# ---------------------------------------------------------------------------
+def test_row_schedule_is_bitwise_neutral(cuda):
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import locality_order
+    from hlhgat.synthetic import tsp_like_graph
+    g = tsp_like_graph(1, n=2000, k=6)
+    ei, w, n = g.edge_index_s, g.edge_weight_s, g.x_s.shape[0]
+    x = torch.randn(n, 64, generator=torch.Generator().manual_seed(0))
+    ref = R.propagate(x, ei, w)
+    ei_d = ops.mark_hodge(dev(ei))
+    op = ops.hodge_operator(ei_d, dev(w), n)
+    y0 = ops.spmm(op.fwd, dev(x))
+    for order in (locality_order(ei.numpy(), n), torch.randperm(n)):
+        ei_o = ops.set_row_order(ops.mark_hodge(dev(ei)), order)
+        op_o = ops.hodge_operator(ei_o, dev(w), n)
+        assert op_o.fwd.order is not None
+        y = ops.spmm(op_o.fwd, dev(x))
+        assert torch.equal(y, y0)
+        assert torch.equal(y.cpu(), ref)
+        T0 = ops.poly_basis(op, dev(x), 4, ops.POLY_LAGUERRE)
+        T1 = ops.poly_basis(op_o, dev(x), 4, ops.POLY_LAGUERRE)
+        assert torch.equal(T0, T1)
+
+
+def test_conv_with_row_schedule_matches(cuda):
+    """HodgeLaguerreConv forward + backward with a scheduled operator equal
+    the natural-order results bitwise (TSP-like graph, config 5 shape)."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import tsp_like_graph
+    g = tsp_like_graph(2, n=1500, k=6)
+    n = g.x_s.shape[0]
+    torch.manual_seed(0)
+    conv = hlhgat.HodgeLaguerreConv(32, 32, K=4).to(cuda)
+    x = torch.randn(n, 32, device=cuda)
+    outs = []
+    for sched in (False, True):
+        ei = ops.mark_hodge(dev(g.edge_index_s))
+        if sched:
+            ops.set_row_order(ei, g.row_order_s)
+        xx = x.clone().requires_grad_(True)
+        y = conv(xx, ei, dev(g.edge_weight_s))
+        (y * y).sum().backward()
+        outs.append((y.detach(), xx.grad.clone(), conv.lins[2].weight.grad.clone()))
+        conv.zero_grad()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

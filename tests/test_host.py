@@ -167,3 +167,25 @@ def test_dense_concat_matches_torch_cat():
     g2, = torch.autograd.grad(l2, x)
     assert torch.equal(l1.detach(), l2.detach())
     assert torch.allclose(g1, g2, rtol=0, atol=1e-6)
+
+
+def test_row_order_collate_offsets_and_permutation():
+    """locality_order is a permutation; collate offsets it like edge_index."""
+    from hlhgat.hodge_dataset import collate, locality_order
+    from hlhgat.synthetic import tsp_like_graph
+    gs = [tsp_like_graph(s, n=300, k=5) for s in range(2)]
+    for g in gs:
+        for k, n in (("row_order_s", g.x_s.shape[0]), ("row_order_t", g.x_t.shape[0])):
+            o = getattr(g, k)
+            assert torch.equal(torch.sort(o).values, torch.arange(n))
+    b = collate(gs, check_hodge=False)
+    ns = [g.x_s.shape[0] for g in gs]
+    assert torch.equal(b.row_order_s[:ns[0]], gs[0].row_order_s)
+    assert torch.equal(b.row_order_s[ns[0]:], gs[1].row_order_s + ns[0])
+    assert torch.equal(torch.sort(b.row_order_s).values, torch.arange(sum(ns)))
+    # RCM shrinks the bandwidth of L1 substantially
+    ei = gs[0].edge_index_s.numpy()
+    o = locality_order(ei, ns[0]).numpy()
+    inv = np.empty_like(o)
+    inv[o] = np.arange(len(o))
+    assert np.abs(inv[ei[0]] - inv[ei[1]]).max() < np.abs(ei[0] - ei[1]).max()
