@@ -236,7 +236,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         OptT a_val, Tensor t_rowptr, Tensor t_col, OptT t_val, int64_t nnz,
                         int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-                        int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order) {
+                        int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order,
+                        OptT tiles, int64_t tile_rows, int64_t tile_nnz) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -251,7 +252,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
                                 nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
-                                x2.data_ptr<float>(),
+                                iptr(tiles), has(tiles) ? tiles->numel() - 1 : 0, tile_rows,
+                                tile_nnz, x2.data_ptr<float>(),
                                 ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
           "poly_basis_fwd");
     }
@@ -313,12 +315,18 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.opt(out_buf);
       em.opt(a_order);
       em.opt(t_order);
+      em.opt(tiles);
+      em.other();
+      em.other();
       ctx->saved_data["edges"] = em.e;
+      ctx->saved_data["tile_rows"] = tile_rows;
+      ctx->saved_data["tile_nnz"] = tile_nnz;
     }
     ctx->saved_data["xshape"] = x.sizes().vec();
     std::vector<Tensor> save = {x2,
                                 T,
                                 has(t_order) ? *t_order : Tensor(),
+                                has(tiles) ? *tiles : Tensor(),
                                 t_rowptr,
                                 t_col,
                                 has(t_val) ? *t_val : Tensor(),
@@ -343,16 +351,18 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     const bool has_bias = d[9] != 0;
     auto xshape = ctx->saved_data["xshape"].toIntVector();
     auto sv = ctx->get_saved_variables();
-    Tensor x2 = sv[0], T = sv[1], t_order = sv[2], t_rowptr = sv[3], t_col = sv[4],
-           t_val = sv[5], pre = sv[6], yout = sv[7], mean = sv[8], invstd = sv[9], bn_w = sv[10],
-           bias_p = sv[11], bn_b = sv[12];
-    std::vector<Tensor> W(sv.begin() + 13, sv.end());
+    Tensor x2 = sv[0], T = sv[1], t_order = sv[2], tiles = sv[3], t_rowptr = sv[4],
+           t_col = sv[5], t_val = sv[6], pre = sv[7], yout = sv[8], mean = sv[9], invstd = sv[10],
+           bn_w = sv[11], bias_p = sv[12], bn_b = sv[13];
+    std::vector<Tensor> W(sv.begin() + 14, sv.end());
+    const int64_t tile_rows = ctx->saved_data["tile_rows"].toInt();
+    const int64_t tile_nnz = ctx->saved_data["tile_nnz"].toInt();
     void* s = stream_of(x2);
     Tensor G = grads[0].reshape({M, dout});
     G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 21 + K;
+    const int64_t n_pos = 24 + K;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -412,7 +422,9 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                     nnz ? t_col.data_ptr<int>() : nullptr,
                                     (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
                                     N, nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
-                                    F, (int)K, Gs.data_ptr<float>(), s),
+                                    tiles.defined() ? tiles.data_ptr<int>() : nullptr,
+                                    tiles.defined() ? tiles.numel() - 1 : 0, tile_rows,
+                                    tile_nnz, F, (int)K, Gs.data_ptr<float>(), s),
               "poly_basis_bwd");
         }
       } else {
@@ -1048,10 +1060,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
 Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_rowptr, Tensor t_col,
                OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-               int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order) {
+               int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT tiles,
+               int64_t tile_rows, int64_t tile_nnz) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
-                         bn_mode, out_buf, a_order, t_order);
+                         bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

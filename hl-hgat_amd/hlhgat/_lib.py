@@ -39,9 +39,10 @@ SIGNATURES = {
                                  c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_f32,
                                  c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                      c_i64, c_i64, c_i32, c_vp, c_vp]),
-    "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                      c_i32, c_vp, c_vp]),
+                                      c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp,
+                                      c_vp]),
+    "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
+                                      c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,

@@ -20,7 +20,8 @@ import numpy as np
 import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
-           "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order"]
+           "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
+           "graph_tiles"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
 _HODGE_KEYS = ("edge_index_s", "edge_index_t")
@@ -88,15 +89,18 @@ class Batch(PairData):
         return self
 
     def _mark(self) -> None:
-        from .ops import mark_hodge, set_row_order
+        from .ops import mark_hodge, set_row_order, set_tiles
         for k, ok in (getattr(self, "hodge_sorted", None) or {}).items():
             t = getattr(self, k, None)
             if ok and torch.is_tensor(t) and t.is_cuda:
                 mark_hodge(t)
-        for k, ko in (("edge_index_s", "row_order_s"), ("edge_index_t", "row_order_t")):
-            t, o = getattr(self, k, None), getattr(self, ko, None)
+        for k, ko, kt in (("edge_index_s", "row_order_s", "tile_ptr_s"),
+                          ("edge_index_t", "row_order_t", "tile_ptr_t")):
+            t, o, tp = getattr(self, k, None), getattr(self, ko, None), getattr(self, kt, None)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(o):
                 set_row_order(t, o)
+            if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(tp):
+                set_tiles(t, tp, TILE_ROWS, TILE_NNZ)
 
     @property
     def batch_t(self) -> torch.Tensor:
@@ -107,6 +111,34 @@ class Batch(PairData):
     def batch_s(self) -> torch.Tensor:
         return torch.repeat_interleave(torch.arange(self.num_graphs, device=self.x_s.device),
                                        self.num_edge1.to(self.x_s.device))
+
+
+TILE_ROWS = 64   # row bound of a graph tile
+TILE_NNZ = 512   # CSR-entry bound of a graph tile (LDS: 2 x 64 x 68 floats + entries = 39 KB)
+
+
+def graph_tiles(counts, nnz, max_rows: int = TILE_ROWS,
+                max_nnz: int = TILE_NNZ) -> Optional[torch.Tensor]:
+    """Row tiles of a block-diagonal batch: consecutive WHOLE graphs packed
+    greedily into runs of <= max_rows rows and <= max_nnz Laplacian entries
+    (int32 [n_tiles+1] row offsets), or None if one graph alone exceeds a
+    bound.  Every Laplacian entry of a tile's rows stays inside the tile
+    (PairData batching offsets, lib/Hodge_Dataset.py:40-48), which is what the
+    graph-local basis kernels rely on."""
+    c = np.asarray(counts, dtype=np.int64).reshape(-1)
+    z = np.asarray(nnz, dtype=np.int64).reshape(-1)
+    if c.size == 0 or c.max() > max_rows or z.max() > max_nnz:
+        return None
+    ptr = [0]
+    acc = accz = 0
+    for k, kz in zip(c, z):
+        if (acc + k > max_rows or accz + kz > max_nnz) and acc > 0:
+            ptr.append(ptr[-1] + acc)
+            acc = accz = 0
+        acc += int(k)
+        accz += int(kz)
+    ptr.append(ptr[-1] + acc)
+    return torch.tensor(ptr, dtype=torch.int32)
 
 
 def locality_order(edge_index, n: int) -> torch.Tensor:
@@ -181,6 +213,15 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
             ok = all(getattr(g, "_hodge_sorted", False) for g in graphs)
         hs[k] = ok
     b.hodge_sorted = hs
+    # whole-graph row tiles for the graph-local polynomial basis
+    for key, xk, ek in (("tile_ptr_t", "x_t", "edge_index_t"), ("tile_ptr_s", "x_s", "edge_index_s")):
+        if getattr(first, ek, None) is None:
+            continue
+        counts = [getattr(g, xk).size(0) for g in graphs]
+        nnz = [np.asarray(getattr(g, ek)).shape[1] for g in graphs]
+        tp = graph_tiles(counts, nnz)
+        if tp is not None:
+            setattr(b, key, tp)
     return b
 
 

@@ -144,6 +144,9 @@ class SparseCSR:
     n_cols: int
     nnz: int
     order: Optional[torch.Tensor] = None  # int32 [n_rows] row schedule (locality_order)
+    tiles: Optional[torch.Tensor] = None  # int32 [n_tiles+1] whole-graph row tiles (graph_tiles)
+    tile_rows: int = 0                    # bound on the rows of any tile
+    tile_nnz: int = 0                     # bound on the CSR entries of any tile
 
 
 @dataclass
@@ -236,6 +239,18 @@ def set_row_order(edge_index: torch.Tensor, order: torch.Tensor) -> torch.Tensor
     return edge_index
 
 
+def set_tiles(edge_index: torch.Tensor, tile_ptr: torch.Tensor, tile_rows: int,
+              tile_nnz: int) -> torch.Tensor:
+    """Declare that the operator built from edge_index is block-diagonal over
+    the row tiles tile_ptr (runs of whole graphs, each <= tile_rows rows and
+    <= tile_nnz CSR entries, hodge_dataset.graph_tiles): its polynomial bases
+    then run graph-local, one launch per basis."""
+    edge_index._hlhgat_tiles = (tile_ptr.to(device=edge_index.device,  # type: ignore
+                                            dtype=torch.int32).contiguous(), int(tile_rows),
+                                int(tile_nnz))
+    return edge_index
+
+
 def _csr_sorted(row: torch.Tensor, col: torch.Tensor, w: Optional[torch.Tensor],
                 n_rows: int, n_cols: int) -> SparseCSR:
     nnz = row.numel()
@@ -292,14 +307,16 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
     order = getattr(edge_index, "_hlhgat_row_order", None)
     if order is not None and order.numel() != n:
         raise RuntimeError(f"hlhgat: row schedule has {order.numel()} entries, operator {n} rows")
+    tiles, tile_rows, tile_nnz = getattr(edge_index, "_hlhgat_tiles", (None, 0, 0))
     if getattr(edge_index, "_hlhgat_sorted_symmetric", False):
         a = _csr_sorted(ei[0], ei[1], w, n, n)
-        a.order = order
+        a.order, a.tiles, a.tile_rows, a.tile_nnz = order, tiles, tile_rows, tile_nnz
         op = HodgeOperator(a, a)
     else:
         fwd = _csr_general(ei[1], ei[0], w, n, n)
         bwd = _csr_general(ei[0], ei[1], w, n, n)
-        fwd.order = bwd.order = order
+        for c in (fwd, bwd):  # the transpose of a block-diagonal operator has the same tiles
+            c.order, c.tiles, c.tile_rows, c.tile_nnz = order, tiles, tile_rows, tile_nnz
         op = HodgeOperator(fwd, bwd)
     return _HODGE_CACHE.put(keys, n, op)
 
@@ -361,7 +378,9 @@ def poly_basis(op: HodgeOperator, X: torch.Tensor, K: int, kind: int) -> torch.T
         check(LIB.hlhgat_poly_basis_fwd(kind, A.rowptr.data_ptr(),
                                         A.col.data_ptr() if A.nnz else None,
                                         _ptr(A.val) if A.nnz else None, n, A.nnz,
-                                        _ptr(A.order), X.data_ptr(), _ld(X), F, K,
+                                        _ptr(A.order), _ptr(A.tiles),
+                                        A.tiles.numel() - 1 if A.tiles is not None else 0,
+                                        A.tile_rows, A.tile_nnz, X.data_ptr(), _ld(X), F, K,
                                         T.data_ptr(),
                                         _stream(X)), "poly_basis_fwd")
     return T
@@ -442,10 +461,12 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
         if x.size(0) < 2 and bn.training:
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
-                            ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order)
+                            ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order,
+                            A.tiles, A.tile_rows, A.tile_nnz)
     sink = out if (bn is None and not relu and x.dim() == 2) else None
     y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
-                     bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order)
+                     bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order,
+                     A.tiles, A.tile_rows, A.tile_nnz)
     if bn is not None:
         y = batch_norm_act(y, bn, relu)
     elif relu:

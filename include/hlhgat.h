@@ -134,10 +134,19 @@ int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
  * kind = HLHGAT_POLY_CHEB:     T_1 = A X, T_{k+1} = 2 A T_k - T_{k-1}
  *        (lib/Hodge_Cheb_Conv.py:416,430-432)
  * X: [n][F] row stride ldx.  T: (K-1) contiguous blocks of [n][F]. */
+/* tile_ptr (optional, int32[n_tiles+1], with max_tile_rows >= every tile's
+ * row count): row ranges of runs of WHOLE graphs of a block-diagonal batch
+ * (hodge_dataset.graph_tiles); max_tile_nnz bounds a tile's CSR entries (a
+ * larger tile is still correct, its entries are read from global memory).
+ * When given and a tile fits in LDS, the whole basis is one graph-local
+ * launch (bitwise the same values); otherwise (or NULL) the K-1 steps run as
+ * separate launches. */
 int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
                           const float* val, int64_t n, int64_t nnz,
-                          const int32_t* row_order, const float* X, int64_t ldx,
-                          int64_t F, int K, float* T, void* stream);
+                          const int32_t* row_order, const int32_t* tile_ptr,
+                          int64_t n_tiles, int64_t max_tile_rows, int64_t max_tile_nnz,
+                          const float* X, int64_t ldx, int64_t F, int K, float* T,
+                          void* stream);
 
 /* Adjoint of hlhgat_poly_basis_fwd.  On entry G holds K contiguous blocks
  * [n][F]: G_k = dLoss/dT_k from the consumers of each T_k (block 0 = the
@@ -146,7 +155,9 @@ int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
  * Laplacians). */
 int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                           const int32_t* col_t, const float* val_t, int64_t n,
-                          int64_t nnz, const int32_t* row_order, int64_t F,
+                          int64_t nnz, const int32_t* row_order,
+                          const int32_t* tile_ptr, int64_t n_tiles,
+                          int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F,
                           int K, float* G, void* stream);
 
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */

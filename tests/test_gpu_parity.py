@@ -496,3 +496,41 @@ def test_conv_with_row_schedule_matches(cuda):
         conv.zero_grad()
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("kind,K", [("lag", 3), ("lag", 6), ("cheb", 4), ("lag", 2)])
+@pytest.mark.parametrize("side", ["t", "s"])
+@pytest.mark.parametrize("nnz_bound", ["packed", "tiny"])
+def test_graph_local_basis_bitwise_equals_steps(cuda, kind, K, side, nnz_bound):
+    """One-launch graph-local basis (whole-graph tiles) == K-1 step launches,
+    forward and adjoint, bitwise (ZINC-like batch, tiles from collate)."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(64, seed=11)
+    assert getattr(b, "tile_ptr_" + side) is not None
+    ei = getattr(b, "edge_index_" + side)
+    w = getattr(b, "edge_weight_" + side)
+    n = getattr(b, "x_" + side).shape[0]
+    k = ops.POLY_LAGUERRE if kind == "lag" else ops.POLY_CHEB
+    x = torch.randn(n, 64, generator=torch.Generator().manual_seed(K)).to(cuda)
+    conv_cls = hlhgat.HodgeLaguerreConv if kind == "lag" else hlhgat.HodgeChebConv
+    torch.manual_seed(0)
+    conv = conv_cls(64, 32, K=K).to(cuda)
+    res = []
+    for tiled in (False, True):
+        e = ops.mark_hodge(dev(ei))
+        if tiled:
+            # "tiny": every tile exceeds the entry bound -> global-memory entries path
+            ops.set_tiles(e, getattr(b, "tile_ptr_" + side), hlhgat.hodge_dataset.TILE_ROWS,
+                          hlhgat.hodge_dataset.TILE_NNZ if nnz_bound == "packed" else 8)
+        op = ops.hodge_operator(e, dev(w), n)
+        assert (op.fwd.tiles is not None) == tiled
+        T = ops.poly_basis(op, x, K, k)
+        xx = x.clone().requires_grad_(True)
+        y = conv(xx, e, dev(w))
+        (y * y).sum().backward()
+        res.append((T, y.detach(), xx.grad.clone(), conv.lins[-1].weight.grad.clone()))
+        conv.zero_grad()
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
