@@ -8,9 +8,10 @@ filters=[64,64,64], mlp=[256,256], K=3, keig=15) on a 1000-graph batch of
 synthetic ZINC-like simplex graphs per GPU (weak scaling): the batch is
 copied into the step's static buffers, CSR / incidence construction for the
 batch, forward, L1 loss, backward, gradient all-reduce (N > 1) and Adam.
-Inputs are resident in HBM before the timed region (several distinct
-batches, rotated).  The step runs as a replayed hipGraph per batch shape
-(hlhgat.train.TrainStep; --eager runs it op by op).  After the timed region
+Inputs are resident in HBM before the timed region (8 distinct batches,
+rotated, padded to one capacity bucket).  The step runs as ONE replayed
+hipGraph for every batch of the bucket (hlhgat.train.TrainStep +
+hodge_dataset.pad_batch; --eager runs it op by op).  After the timed region
 a short eager pass with hipExtLaunchKernel event stamps on the SpMM and the
 projection kernels gives the roofline figures.  Rank 0 prints one JSON line.
 """
@@ -41,13 +42,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_batches(n_batches, rank, device):
+def make_batches(n_batches, rank, device, quantum=512):
+    """n_batches distinct synthetic 1000-graph batches, padded to ONE capacity
+    bucket (the max of their static_caps) so that a single captured hipGraph
+    replays every one of them -- as a training loop pads its DataLoader
+    batches to the dataset's bucket (hodge_dataset.pad_batch)."""
+    from hlhgat.hodge_dataset import pad_batch, static_caps
     from hlhgat.synthetic import zinc_like_batch
-    out = []
-    for i in range(n_batches):
-        b = zinc_like_batch(GRAPHS_PER_GPU, seed=1 + rank * 101 + i)
-        out.append(b.to(device))
-    return out
+    raw = [zinc_like_batch(GRAPHS_PER_GPU, seed=1 + rank * 101 + i) for i in range(n_batches)]
+    cs = [static_caps(b, quantum) for b in raw]
+    caps = {k: max(c[k] for c in cs) for k in cs[0]}
+    real = sum(b.x_t.size(0) + b.x_s.size(0) for b in raw) / n_batches
+    return [pad_batch(b, caps).to(device) for b in raw], caps, real
 
 
 def cpu_baseline(batch_cpu, budget_s=15.0):
@@ -107,7 +113,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--batches", type=int, default=3)
+    ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph replay")
     ap.add_argument("--prof-steps", type=int, default=3,
@@ -122,7 +128,7 @@ def main():
     from hlhgat.train import TrainStep
 
     log(f"[rank {rank}] generating {args.batches} x {GRAPHS_PER_GPU} synthetic graphs")
-    batches = make_batches(args.batches, rank, device)  # each rank: its own graphs
+    batches, caps, real_rows = make_batches(args.batches, rank, device)  # each rank: its own
     torch.manual_seed(0)
     model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**MODEL_KW).to(device).train()
     crit = torch.nn.L1Loss()
@@ -193,8 +199,12 @@ def main():
                                "channels=[2,2,2] filters=[64,64,64] K=3 mlp=[256,256] keig=15; "
                                "step = batch copy-in + CSR build + fwd + L1 + bwd "
                                "(+ grad all-reduce) + Adam",
-                   "execution": "eager" if args.eager else "hipGraph replay per batch shape "
-                                "(captured during warmup), node/edge chains on 2 streams",
+                   "execution": "eager" if args.eager else
+                   f"one hipGraph for the capacity bucket (captured in warmup, "
+                   f"{step.stats['captures']} capture(s)), replayed for {args.batches} distinct "
+                   f"batches padded to it; node/edge chains on 2 streams",
+                   "static_caps": caps,
+                   "padding_overhead": round((caps["rows_t"] + caps["rows_s"]) / real_rows - 1, 4),
                    "graphs_per_gpu": GRAPHS_PER_GPU, "global_batch": world * GRAPHS_PER_GPU,
                    "parallelism": f"dp{world}"},
         "roofline": roofline,

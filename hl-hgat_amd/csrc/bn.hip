@@ -103,7 +103,18 @@ BnWs carve(void* ws, int64_t n, int64_t C) {
   return w;
 }
 
+// n_valid (optional, device int32): only rows [0, min(n, *n_valid)) are
+// simplices of the batch; the rest are capacity padding (hlhgat.train static
+// shapes).  Statistics use the valid rows only, outputs / gradients of padded
+// rows are written as 0.
+__device__ __forceinline__ int64_t eff_rows(int64_t n, const int32_t* nvalid) {
+  if (!nvalid) return n;
+  const int64_t v = (int64_t)*nvalid;
+  return v < n ? (v < 0 ? 0 : v) : n;
+}
+
 struct StatsArgs {
+  const int32_t* nvalid;
   const float* x;
   int64_t ldx;
   const float* y;   // bwd: forward output for the ReLU mask (or NULL)
@@ -237,7 +248,8 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   const int c = c0 + cl * V;
   const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
   int64_t r_hi = r_lo + a.rows_per_part;
-  if (r_hi > a.n) r_hi = a.n;
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
+  if (r_hi > n_eff) r_hi = n_eff;
   double s0[V], s1[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
@@ -276,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
     const double u0 = sum0[t], u1 = sum1[t];
-    const double nn = (double)a.n;
+    const double nn = (double)(n_eff > 0 ? n_eff : 1);
     const double mean = u0 / nn;
     double var = u1 / nn - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -284,7 +296,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
     a.save_mean[cc] = (float)mean;
     a.save_invstd[cc] = invstd;
     if (a.running_mean) {
-      const double unb = a.n > 1 ? var * nn / (nn - 1.0) : var;
+      const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
       a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
       a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
     }
@@ -293,6 +305,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
 }
 
 struct ApplyArgs {
+  const int32_t* nvalid;
   const float* x;
   int64_t ldx;
   float* y;
@@ -323,12 +336,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
     t[v] = b - a.mean[c + v] * s[v];
   }
   // APPLY_RPT rows per thread, all loads issued before any store
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
   const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
   vt xv[APPLY_RPT];
 #pragma unroll
   for (int u = 0; u < APPLY_RPT; ++u) {
     const int64_t r = r0 + u * a.rp;
-    if (r < a.n) xv[u] = vload<V>(a.x + r * a.ldx + c);
+    if (r < n_eff) xv[u] = vload<V>(a.x + r * a.ldx + c);
   }
 #pragma unroll
   for (int u = 0; u < APPLY_RPT; ++u) {
@@ -338,7 +352,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float z = vget(xv[u], v) * s[v] + t[v];
-      vget(o, v) = (a.relu && z < 0.f) ? 0.f : z;
+      vget(o, v) = r >= n_eff ? 0.f : ((a.relu && z < 0.f) ? 0.f : z);
     }
     vstore<V>(a.y + r * a.ldy + c, o);
   }
@@ -353,7 +367,8 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
   const int c = c0 + cl * V;
   const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
   int64_t r_hi = r_lo + a.rows_per_part;
-  if (r_hi > a.n) r_hi = a.n;
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
+  if (r_hi > n_eff) r_hi = n_eff;
   double s0[V], s1[V];
   float mu[V];
 #pragma unroll
@@ -403,7 +418,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
     const double sg = sum0[t], sgx = sum1[t];
     const double is = (double)a.save_invstd[cc];
     const double w = a.weight ? (double)a.weight[cc] : 1.0;
-    const double nn = (double)a.n;
+    const double nn = (double)(n_eff > 0 ? n_eff : 1);
     if (a.dweight) a.dweight[cc] = (float)(sgx * is);
     if (a.dbias) a.dbias[cc] = (float)sg;
     // dx = w*is*(g - sg/n - (x-mean)*is^2*sgx/n) = A*g + B*x + Cc
@@ -417,6 +432,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
 }
 
 struct BwdApplyArgs {
+  const int32_t* nvalid;
   const float* x;
   int64_t ldx;
   const float* y;
@@ -445,12 +461,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     B[v] = a.coef[a.C + c + v];
     Cc[v] = a.coef[2 * a.C + c + v];
   }
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
   const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
   vt xv[APPLY_RPT], gv[APPLY_RPT], yv[APPLY_RPT];
 #pragma unroll
   for (int u = 0; u < APPLY_RPT; ++u) {
     const int64_t r = r0 + u * a.rp;
-    if (r < a.n) {
+    if (r < n_eff) {
       xv[u] = vload<V>(a.x + r * a.ldx + c);
       gv[u] = vload<V>(a.dy + r * a.lddy + c);
       if (a.y) yv[u] = vload<V>(a.y + r * a.ldy + c);
@@ -465,7 +482,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     for (int v = 0; v < V; ++v) {
       float g = vget(gv[u], v);
       if (a.y && !(vget(yv[u], v) > 0.f)) g = 0.f;
-      vget(o, v) = A[v] * g + (B[v] * vget(xv[u], v) + Cc[v]);
+      vget(o, v) = r >= n_eff ? 0.f : A[v] * g + (B[v] * vget(xv[u], v) + Cc[v]);
     }
     vstore<V>(a.dx + r * a.lddx + c, o);
   }
@@ -494,7 +511,8 @@ extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
   return (int64_t)bn_ws_bytes(n, C);
 }
 
-extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64_t C,
+extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
+                                   const int32_t* n_valid, int64_t C,
                                    const float* weight, const float* bias,
                                    float* running_mean, float* running_var,
                                    int64_t* num_batches_tracked, float momentum,
@@ -513,6 +531,7 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64
   BnLayout L = bn_layout(n, C, vec);
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
+  s.nvalid = n_valid;
   s.x = x;
   s.ldx = ldx;
   s.n = n;
@@ -540,7 +559,7 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64
   else
     k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
-  ApplyArgs p{x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
+  ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
               L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
@@ -553,7 +572,8 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64
 
 extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
                                    int64_t ldy, const float* dy, int64_t lddy,
-                                   int64_t n, int64_t C, const float* weight,
+                                   int64_t n, const int32_t* n_valid, int64_t C,
+                                   const float* weight,
                                    const float* save_mean, const float* save_invstd,
                                    float* dx, int64_t lddx, float* dweight,
                                    float* dbias, void* workspace,
@@ -567,6 +587,7 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   BnLayout L = bn_layout(n, C, vec);
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
+  s.nvalid = n_valid;
   s.x = x;
   s.ldx = ldx;
   s.y = y;
@@ -595,7 +616,7 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   else
     k_bn_bwd_reduce<1><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
-  BwdApplyArgs p{x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, L.tpr, L.rp};
+  BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
     k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);

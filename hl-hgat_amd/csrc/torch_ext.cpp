@@ -182,6 +182,7 @@ void proj_bwd_data(const Tensor& G, const std::vector<const float*>& W,
 struct BnState {
   OptT w, b, rm, rv, nbt;
   double momentum = 0.1, eps = 1e-5;
+  OptT valid;  // device int32 [1]: rows >= *valid are static-shape padding
 };
 
 Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
@@ -193,7 +194,8 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
   invstd = at::empty({C}, x.options());
   Tensor ws = bn_workspace(x, n, C);
   int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
-  chk(hlhgat_bn_fwd_train(x.data_ptr<float>(), ld_of(x), n, C, fptr(st.w), fptr(st.b),
+  chk(hlhgat_bn_fwd_train(x.data_ptr<float>(), ld_of(x), n, iptr(st.valid), C, fptr(st.w),
+                          fptr(st.b),
                           mfptr(st.rm), mfptr(st.rv), nbt, (float)st.momentum, (float)st.eps,
                           relu ? 1 : 0, y.data_ptr<float>(), ld_of(y), mean.data_ptr<float>(),
                           invstd.data_ptr<float>(), ws.data_ptr(), ws.numel(), stream_of(x)),
@@ -206,7 +208,7 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
                    const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
                    Tensor& dw, Tensor& db, const Tensor* dx_into = nullptr,
-                   const Tensor* b_param = nullptr) {
+                   const Tensor* b_param = nullptr, const Tensor& valid = Tensor()) {
   const int64_t n = x.size(0), C = x.size(1);
   Tensor dyc = rows2d(dy);
   Tensor dx = dx_into ? *dx_into : at::empty({n, C}, x.options());
@@ -217,7 +219,8 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
               : Tensor();
   Tensor ws = bn_workspace(x, n, C);
   chk(hlhgat_bn_bwd_train(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
-                          dyc.data_ptr<float>(), ld_of(dyc), n, C, fptr(w),
+                          dyc.data_ptr<float>(), ld_of(dyc), n,
+                          valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
                           mean.data_ptr<float>(), invstd.data_ptr<float>(), dx.data_ptr<float>(),
                           ld_of(dx), dw.defined() ? dw.data_ptr<float>() : nullptr,
                           db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
@@ -237,7 +240,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
                         int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order,
-                        OptT tiles, int64_t tile_rows, int64_t tile_nnz) {
+                        OptT tiles, int64_t tile_rows, int64_t tile_nnz, OptT valid) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -286,7 +289,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     }
     Tensor out = pre, mean, invstd;
     if (bn_mode > 0) {
-      BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps};
+      BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
       out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, Cin, F, M, dout, K, kind, nnz, bn_mode,
@@ -318,6 +321,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.opt(tiles);
       em.other();
       em.other();
+      em.opt(valid);
       ctx->saved_data["edges"] = em.e;
       ctx->saved_data["tile_rows"] = tile_rows;
       ctx->saved_data["tile_nnz"] = tile_nnz;
@@ -327,6 +331,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                 T,
                                 has(t_order) ? *t_order : Tensor(),
                                 has(tiles) ? *tiles : Tensor(),
+                                has(valid) ? *valid : Tensor(),
                                 t_rowptr,
                                 t_col,
                                 has(t_val) ? *t_val : Tensor(),
@@ -351,10 +356,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     const bool has_bias = d[9] != 0;
     auto xshape = ctx->saved_data["xshape"].toIntVector();
     auto sv = ctx->get_saved_variables();
-    Tensor x2 = sv[0], T = sv[1], t_order = sv[2], tiles = sv[3], t_rowptr = sv[4],
-           t_col = sv[5], t_val = sv[6], pre = sv[7], yout = sv[8], mean = sv[9], invstd = sv[10],
-           bn_w = sv[11], bias_p = sv[12], bn_b = sv[13];
-    std::vector<Tensor> W(sv.begin() + 14, sv.end());
+    Tensor x2 = sv[0], T = sv[1], t_order = sv[2], tiles = sv[3], valid = sv[4],
+           t_rowptr = sv[5], t_col = sv[6], t_val = sv[7], pre = sv[8], yout = sv[9],
+           mean = sv[10], invstd = sv[11], bn_w = sv[12], bias_p = sv[13], bn_b = sv[14];
+    std::vector<Tensor> W(sv.begin() + 15, sv.end());
     const int64_t tile_rows = ctx->saved_data["tile_rows"].toInt();
     const int64_t tile_nnz = ctx->saved_data["tile_nnz"].toInt();
     void* s = stream_of(x2);
@@ -362,7 +367,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 24 + K;
+    const int64_t n_pos = 25 + K;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -370,7 +375,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       OptT y = bn_mode == 2 ? OptT(yout) : OptT();
       OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
       G = bn_backward(pre, y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K), dbn_w,
-                      dbn_b, nullptr, &bn_b);
+                      dbn_b, nullptr, &bn_b, valid);
       out[10 + K] = dbn_w;
       out[11 + K] = dbn_b;
     }
@@ -442,11 +447,11 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
 class BNActFn : public torch::autograd::Function<BNActFn> {
  public:
   static Tensor forward(AutogradContext* ctx, Tensor x, OptT w, OptT b, OptT rm, OptT rv,
-                        OptT nbt, double momentum, double eps, bool relu) {
+                        OptT nbt, double momentum, double eps, bool relu, OptT valid) {
     req(x, "x");
     Tensor xc = rows2d(x);
     Tensor mean, invstd;
-    BnState st{w, b, rm, rv, nbt, momentum, eps};
+    BnState st{w, b, rm, rv, nbt, momentum, eps, valid};
     Tensor y = bn_forward(xc, st, relu, mean, invstd);
     ctx->saved_data["relu"] = relu;
     EdgeMap em;
@@ -457,8 +462,8 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
     em.opt(rv);
     em.opt(nbt);
     ctx->saved_data["edges"] = em.e;
-    ctx->save_for_backward(
-        {xc, relu ? y : Tensor(), has(w) ? *w : Tensor(), mean, invstd, has(b) ? *b : Tensor()});
+    ctx->save_for_backward({xc, relu ? y : Tensor(), has(w) ? *w : Tensor(), mean, invstd,
+                            has(b) ? *b : Tensor(), has(valid) ? *valid : Tensor()});
     return y;
   }
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
@@ -467,8 +472,8 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
     OptT y = sv[1].defined() ? OptT(sv[1]) : OptT();
     OptT w = sv[2].defined() ? OptT(sv[2]) : OptT();
     Tensor dx = bn_backward(sv[0], y, grads[0], w, sv[3], sv[4], need(ctx, 1), need(ctx, 2), dw,
-                           db, nullptr, &sv[5]);
-    return {dx, dw, db, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+                           db, nullptr, &sv[5], sv[6]);
+    return {dx, dw, db, Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
   }
 };
 
@@ -846,7 +851,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                                Tensor eids, Tensor ei, Tensor rD, at::TensorList pn,
                                at::TensorList pe, double mom1n, double eps1n, double mom4n,
                                double eps4n, double mom1e, double eps1e, double mom4e,
-                               double eps4e) {
+                               double eps4e, OptT valid_t, OptT valid_s) {
     req(x_t, "x_t");
     req(x_s, "x_s");
     TORCH_CHECK(pn.size() == 14 && pe.size() == 14, "hlhgat: nei_value expects 14+14 params");
@@ -885,12 +890,14 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     Tensor h1t = at::empty({N, dn}, xt.options());
     Tensor h1s = at::empty({E, de}, xt.options());
     auto side = [&](const at::TensorList& p, const Tensor& h1, double m1, double e1, double m4,
-                    double e4, SideMlp& o) {
+                    double e4, const OptT& valid, SideMlp& o) {
       o.h1 = h1;
-      o.a1 = bn_forward(h1, BnState{p[2], p[3], p[4], p[5], p[6], m1, e1}, true, o.m1, o.i1);
+      o.a1 = bn_forward(h1, BnState{p[2], p[3], p[4], p[5], p[6], m1, e1, valid}, true, o.m1,
+                        o.i1);
       Tensor W3 = p[7].stride(1) == 1 ? p[7] : p[7].contiguous();
       o.h2 = linear_forward({o.a1}, W3, p[8]);
-      o.y = bn_forward(o.h2, BnState{p[9], p[10], p[11], p[12], p[13], m4, e4}, true, o.m4, o.i4);
+      o.y = bn_forward(o.h2, BnState{p[9], p[10], p[11], p[12], p[13], m4, e4, valid}, true,
+                       o.m4, o.i4);
     };
     auto lin_into = [](const Tensor& A, const Tensor& W, const Tensor& b, Tensor& out) {
       if (A.size(0) > 0)
@@ -915,7 +922,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                                 h1s.data_ptr<float>(), de, 0, fk.side.stream()),
             "edge_gather2(nei edge)");
       }
-      side(pe, h1s, mom1e, eps1e, mom4e, eps4e, te);
+      side(pe, h1s, mom1e, eps1e, mom4e, eps4e, valid_s, te);
     }
     if (N > 0) {  // node side: h1_t = Qt + rD * |B1| P1, then its MLP
       chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
@@ -925,7 +932,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                            1.f, 0.f, 0.f, h1t.data_ptr<float>(), dn, fk.main.stream()),
           "poly_step(nei node)");
     }
-    side(pn, h1t, mom1n, eps1n, mom4n, eps4n, tn);
+    side(pn, h1t, mom1n, eps1n, mom4n, eps4n, valid_t, tn);
     fk.main_waits_side();
     fk.escape({te.a1, te.m1, te.i1, te.h2, te.y, te.m4, te.i4});
     {
@@ -934,6 +941,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       em.list(pn);
       em.list(pe);
       for (int i = 0; i < 8; ++i) em.other();
+      em.opt(valid_t);
+      em.opt(valid_s);
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, E, d, dn, de};
@@ -942,7 +951,9 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                             te.h1, te.a1, te.m1, te.i1, te.h2, te.y, te.m4, te.i4,
                             // 30..: W0, b0, be1, b3, be4 per side (gradient bucket targets)
                             pn[0], pn[1], pn[3], pn[8], pn[10], pe[0], pe[1], pe[3], pe[8],
-                            pe[10]});
+                            pe[10],
+                            // 40, 41: valid-row counts of the node / edge sides
+                            has(valid_t) ? *valid_t : Tensor(), has(valid_s) ? *valid_s : Tensor()});
     return {tn.y, te.y};
   }
 
@@ -952,25 +963,26 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     const int64_t N = dims[0], E = dims[1], d = dims[2], dn = dims[3], de = dims[4];
     Tensor xt = sv[0], xs = sv[1], rowptr = sv[2], eids = sv[3], ei = sv[4], rD = sv[5],
            Wt = sv[6], Ws = sv[7];
-    // positions: x_t 0, x_s 1, rowptr 2, eids 3, ei 4, rD 5, pn 6..19, pe 20..33, hyper 34..41
-    variable_list out(42);
+    // positions: x_t 0, x_s 1, rowptr 2, eids 3, ei 4, rD 5, pn 6..19, pe 20..33, hyper 34..41,
+    //            valid_t 42, valid_s 43
+    variable_list out(44);
     const int64_t PN = 6, PE = 20;
     Tensor dYt = at::empty({N, dn + de}, xt.options());
     Tensor dYs = at::empty({E, de + dn}, xt.options());
     auto side_bwd = [&](const Tensor& gy, int64_t P, const Tensor& g1, const Tensor& W3,
-                        const Tensor& g4, int o0, Tensor dest, int q0) {
+                        const Tensor& g4, int o0, Tensor dest, int q0, const Tensor& valid) {
       const Tensor &be1 = sv[q0 + 2], &b3 = sv[q0 + 3], &be4 = sv[q0 + 4];
       Tensor h1 = sv[o0], a1 = sv[o0 + 1], m1 = sv[o0 + 2], i1 = sv[o0 + 3], h2 = sv[o0 + 4],
              y = sv[o0 + 5], m4 = sv[o0 + 6], i4 = sv[o0 + 7];
       Tensor dg4, dbe4, dg1, dbe1, dW3, db3;
       Tensor gyc = gy.defined() ? gy : at::zeros_like(y);
       Tensor dh2 = bn_backward(h2, OptT(y), gyc, OptT(g4), m4, i4, need(ctx, P + 9),
-                               need(ctx, P + 10), dg4, dbe4, nullptr, &be4);
+                               need(ctx, P + 10), dg4, dbe4, nullptr, &be4, valid);
       std::vector<Tensor> da1;
       linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true}, dW3, db3, da1,
                       &b3);
       bn_backward(h1, OptT(a1), da1[0], OptT(g1), m1, i1, need(ctx, P + 2), need(ctx, P + 3), dg1,
-                  dbe1, &dest, &be1);
+                  dbe1, &dest, &be1, valid);
       out[P + 2] = dg1;
       out[P + 3] = dbe1;
       out[P + 7] = dW3;
@@ -982,9 +994,9 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     fk.side_waits_main();
     {  // edge side MLP backward on the side stream -> dYs[:, :de]
       TStreamGuard g(fk.side);
-      side_bwd(grads[1], PE, sv[11], sv[12], sv[13], 22, dYs.narrow(1, 0, de), 35);
+      side_bwd(grads[1], PE, sv[11], sv[12], sv[13], 22, dYs.narrow(1, 0, de), 35, sv[41]);
     }
-    side_bwd(grads[0], PN, sv[8], sv[9], sv[10], 14, dYt.narrow(1, 0, dn), 30);
+    side_bwd(grads[0], PN, sv[8], sv[9], sv[10], 14, dYt.narrow(1, 0, dn), 30, sv[40]);
     fk.side_waits_main();  // side needs dh1_t
     fk.main_waits_side();  // main needs dh1_s
     {  // dP1[e] = rD[i] dh1_t[i] + rD[j] dh1_t[j] -> dYs[:, de:], then the edge GEMM grads
@@ -1061,15 +1073,16 @@ Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_row
                OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
                int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT tiles,
-               int64_t tile_rows, int64_t tile_nnz) {
+               int64_t tile_rows, int64_t tile_nnz, OptT valid) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
-                         bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz);
+                         bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz,
+                         valid);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,
-              bool relu) {
-  return BNActFn::apply(x, w, b, rm, rv, nbt, momentum, eps, relu);
+              bool relu, OptT valid) {
+  return BNActFn::apply(x, w, b, rm, rv, nbt, momentum, eps, relu, valid);
 }
 
 Tensor linear(std::vector<Tensor> As, Tensor W, OptT b) {
@@ -1095,10 +1108,11 @@ Tensor edge_from_nodes(Tensor x_t, Tensor rowptr, Tensor eids, Tensor ei) {
 std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids, Tensor ei,
                               Tensor rD, std::vector<Tensor> pn, std::vector<Tensor> pe,
                               double mom1n, double eps1n, double mom4n, double eps4n,
-                              double mom1e, double eps1e, double mom4e, double eps4e) {
+                              double mom1e, double eps1e, double mom4e, double eps4e,
+                              OptT valid_t, OptT valid_s) {
   auto r = NEIntValueFn::apply(x_t, x_s, rowptr, eids, ei, rD, at::TensorList(pn),
                                at::TensorList(pe), mom1n, eps1n, mom4n, eps4n, mom1e, eps1e,
-                               mom4e, eps4e);
+                               mom4e, eps4e, valid_t, valid_s);
   return {r[0], r[1]};
 }
 

@@ -174,9 +174,12 @@ class NodeEdgeInt(nn.Module):
         if not self.only_att and x_t.is_cuda and x_t.dim() == 2:
             bop = _as_boundary(par, x_t.size(0), x_s.size(0))
             r = ops.nei_value(x_t, x_s, bop.incidence(), ops.reciprocal(D), self.WV_Node,
-                              self.WV_Edge)
+                              self.WV_Edge, bop.valid_t, bop.valid_s)
             if r is not None:
                 return r
+        if getattr(par, "valid_t", None) is not None:
+            raise RuntimeError("hlhgat: static-shape (padded) batches need the fused "
+                               "NodeEdgeInt value path (training-mode WV_* MLPs)")
         x_s2t, x_t2s = self.interact(x_t, x_s, par, D)
         if self.only_att:
             code = _sigma_code(self.sigma)

@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "graph_tiles"]
+           "graph_tiles", "static_caps", "pad_batch"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
 _HODGE_KEYS = ("edge_index_s", "edge_index_t")
@@ -89,18 +89,27 @@ class Batch(PairData):
         return self
 
     def _mark(self) -> None:
-        from .ops import mark_hodge, set_row_order, set_tiles
+        from .ops import mark_hodge, set_row_order, set_tiles, set_valid
         for k, ok in (getattr(self, "hodge_sorted", None) or {}).items():
             t = getattr(self, k, None)
             if ok and torch.is_tensor(t) and t.is_cuda:
                 mark_hodge(t)
-        for k, ko, kt in (("edge_index_s", "row_order_s", "tile_ptr_s"),
-                          ("edge_index_t", "row_order_t", "tile_ptr_t")):
+        for k, ko, kt, kv in (("edge_index_s", "row_order_s", "tile_ptr_s", "n_valid_s"),
+                              ("edge_index_t", "row_order_t", "tile_ptr_t", "n_valid_t")):
             t, o, tp = getattr(self, k, None), getattr(self, ko, None), getattr(self, kt, None)
+            nv = getattr(self, kv, None)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(o):
                 set_row_order(t, o)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(tp):
                 set_tiles(t, tp, TILE_ROWS, TILE_NNZ)
+            if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(nv):
+                set_valid(t, nv)
+        ei = getattr(self, "edge_index", None)
+        if torch.is_tensor(ei) and ei.is_cuda:
+            for kv in ("n_valid_t", "n_valid_s"):
+                nv = getattr(self, kv, None)
+                if torch.is_tensor(nv):
+                    set_valid(ei, nv, "_hlhgat_valid_" + kv[-1])
 
     @property
     def batch_t(self) -> torch.Tensor:
@@ -225,6 +234,102 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     return b
 
 
+PAD_MIN_ROWS = 64  # padding rows share the padding entries: keep every padding row short
+
+
+def _spread(n_items: int, n_bins: int) -> np.ndarray:
+    """Items per bin for n_items spread evenly over n_bins (first bins +1)."""
+    base, extra = divmod(int(n_items), int(n_bins))
+    return np.full(n_bins, base, dtype=np.int64) + (np.arange(n_bins) < extra)
+
+
+def _roundup(v: int, q: int) -> int:
+    return (int(v) + q - 1) // q * q
+
+
+def static_caps(b: "Batch", quantum: int = 512) -> Dict[str, int]:
+    """Capacity bucket of a collated batch for hipGraph replay: node / edge
+    rows rounded up to `quantum` (at least one padding row), Laplacian entries
+    to 4*quantum, tile counts to a bound that holds for any batch of these
+    capacities.  Batches with equal caps share one captured training step."""
+    rows_t = _roundup(b.x_t.size(0) + PAD_MIN_ROWS, quantum)
+    rows_s = _roundup(b.x_s.size(0) + PAD_MIN_ROWS, quantum)
+    caps = {"rows_t": rows_t, "rows_s": rows_s,
+            "nnz_t": _roundup(b.edge_index_t.size(1) + 1, 4 * quantum),
+            "nnz_s": _roundup(b.edge_index_s.size(1) + 1, 4 * quantum)}
+    for side in ("t", "s"):
+        r, z = caps["rows_" + side], caps["nnz_" + side]
+        # greedy packing: two consecutive tiles always exceed a bound
+        caps["tiles_" + side] = 2 * max(-(-r // TILE_ROWS), -(-z // TILE_NNZ)) + 4
+    return caps
+
+
+def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
+    """Static-shape copy of a collated host batch (hlhgat.train replays one
+    hipGraph for every batch of the same caps).
+
+    Padding rows are isolated simplices that belong to no graph:
+      * x_t / x_s get zero rows; num_node1 / num_edge1 are unchanged, so the
+        per-graph readouts never see them;
+      * each Laplacian gets zero-weight self-loops spread evenly over its
+        padding rows (COO stays row-sorted and symmetric; real rows keep
+        their entries; no padding row is long);
+      * the B1 edge list gets self-edges spread over the padding nodes;
+      * n_valid_t / n_valid_s (int32 [1]) and valid_mask_t tell the BatchNorm
+        kernels and the degree normalisation which rows are real;
+      * graph tiles cover the padding rows and are padded with empty tiles.
+    The real rows' values, gradients and statistics are those of the
+    unpadded batch (tests/test_train_step.py)."""
+    nt, ns = b.x_t.size(0), b.x_s.size(0)
+    Rt, Rs = caps["rows_t"], caps["rows_s"]
+    if Rt <= nt or Rs <= ns:
+        raise ValueError(f"pad_batch: caps ({Rt}, {Rs}) must exceed the rows ({nt}, {ns})")
+    out = Batch()
+    for k, v in vars(b).items():
+        setattr(out, k, v)
+
+    def pad_rows(x, R):
+        return torch.cat([x, x.new_zeros((R - x.size(0),) + tuple(x.shape[1:]))], 0)
+
+    def pad_coo(ei, w, n, R, Z):
+        extra = Z - ei.size(1)
+        if extra < 0:
+            raise ValueError(f"pad_batch: {ei.size(1)} Laplacian entries exceed the cap {Z}")
+        per_row = _spread(extra, R - n)
+        rows = torch.from_numpy(np.repeat(np.arange(n, R), per_row)).to(ei.dtype)
+        return (torch.cat([ei, torch.stack([rows, rows])], 1),
+                torch.cat([w, w.new_zeros(extra)]), per_row)
+
+    out.x_t, out.x_s = pad_rows(b.x_t, Rt), pad_rows(b.x_s, Rs)
+    out.edge_index_t, out.edge_weight_t, pr_t = pad_coo(b.edge_index_t, b.edge_weight_t, nt, Rt,
+                                                        caps["nnz_t"])
+    out.edge_index_s, out.edge_weight_s, pr_s = pad_coo(b.edge_index_s, b.edge_weight_s, ns, Rs,
+                                                        caps["nnz_s"])
+    if getattr(b, "edge_index", None) is not None:
+        nodes = torch.from_numpy(nt + np.arange(Rs - ns) % (Rt - nt)).to(b.edge_index.dtype)
+        out.edge_index = torch.cat([b.edge_index, torch.stack([nodes, nodes])], 1)
+    for side, n, R, per_row in (("t", nt, Rt, pr_t), ("s", ns, Rs, pr_s)):
+        o = getattr(b, "row_order_" + side, None)
+        if o is not None:
+            setattr(out, "row_order_" + side, torch.cat([o, torch.arange(n, R, dtype=o.dtype)]))
+        tp = getattr(b, "tile_ptr_" + side, None)
+        if tp is not None:
+            # padding rows are isolated: pack them under the same row / entry bounds
+            pads = graph_tiles(np.ones(R - n, dtype=np.int64), per_row)
+            if pads is None:
+                raise ValueError("pad_batch: a padding row exceeds the tile entry bound")
+            tp = torch.cat([tp, pads[1:] + n])
+            cap = caps["tiles_" + side]
+            if tp.numel() - 1 > cap:
+                raise ValueError(f"pad_batch: {tp.numel() - 1} tiles exceed the cap {cap}")
+            tp = torch.cat([tp, tp[-1:].expand(cap + 1 - tp.numel())])
+            setattr(out, "tile_ptr_" + side, tp.contiguous())
+        setattr(out, "n_valid_" + side, torch.tensor([n], dtype=torch.int32))
+    out.valid_mask_t = torch.arange(Rt) < nt
+    out.num_nodes = Rt
+    return out
+
+
 class BoundaryOperator:
     """|B1| / B1 of adj2par1 for the undirected edge list edge_index [2, E]
     (column e: -1 at edge_index[0][e], +1 at edge_index[1][e]).
@@ -241,6 +346,9 @@ class BoundaryOperator:
             raise ValueError(f"adj2par1: edge_index has {edge_index.size(1)} edges, "
                              f"num_edge={num_edge}")
         self._inc = None
+        # static-shape batches: valid node / edge row counts (pad_batch)
+        self.valid_t = getattr(edge_index, "_hlhgat_valid_t", None)
+        self.valid_s = getattr(edge_index, "_hlhgat_valid_s", None)
 
     @property
     def shape(self):

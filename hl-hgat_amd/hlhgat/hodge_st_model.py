@@ -108,6 +108,9 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         # so size it by N_t and skip the host sync of max()
         par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
         D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0])
+        valid_t = getattr(data, "valid_mask_t", None)
+        if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
+            D = D.masked_fill(~valid_t, 1.0)
         for i, _ in enumerate(self.channels):
             for j in range(self.channels[i]):
                 if dense:

@@ -147,6 +147,7 @@ class SparseCSR:
     tiles: Optional[torch.Tensor] = None  # int32 [n_tiles+1] whole-graph row tiles (graph_tiles)
     tile_rows: int = 0                    # bound on the rows of any tile
     tile_nnz: int = 0                     # bound on the CSR entries of any tile
+    valid: Optional[torch.Tensor] = None  # int32 [1]: rows >= valid are static-shape padding
 
 
 @dataclass
@@ -251,6 +252,15 @@ def set_tiles(edge_index: torch.Tensor, tile_ptr: torch.Tensor, tile_rows: int,
     return edge_index
 
 
+def set_valid(edge_index: torch.Tensor, n_valid: torch.Tensor, attr: str = "_hlhgat_valid"
+              ) -> torch.Tensor:
+    """Declare the rows >= n_valid (device int32 [1]) of the operator built
+    from edge_index as static-shape padding (hodge_dataset.pad_batch): the
+    BatchNorm statistics of its layers use the valid rows only."""
+    setattr(edge_index, attr, n_valid.to(device=edge_index.device, dtype=torch.int32).view(1))
+    return edge_index
+
+
 def _csr_sorted(row: torch.Tensor, col: torch.Tensor, w: Optional[torch.Tensor],
                 n_rows: int, n_cols: int) -> SparseCSR:
     nnz = row.numel()
@@ -308,15 +318,18 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
     if order is not None and order.numel() != n:
         raise RuntimeError(f"hlhgat: row schedule has {order.numel()} entries, operator {n} rows")
     tiles, tile_rows, tile_nnz = getattr(edge_index, "_hlhgat_tiles", (None, 0, 0))
+    valid = getattr(edge_index, "_hlhgat_valid", None)
     if getattr(edge_index, "_hlhgat_sorted_symmetric", False):
         a = _csr_sorted(ei[0], ei[1], w, n, n)
         a.order, a.tiles, a.tile_rows, a.tile_nnz = order, tiles, tile_rows, tile_nnz
+        a.valid = valid
         op = HodgeOperator(a, a)
     else:
         fwd = _csr_general(ei[1], ei[0], w, n, n)
         bwd = _csr_general(ei[0], ei[1], w, n, n)
         for c in (fwd, bwd):  # the transpose of a block-diagonal operator has the same tiles
             c.order, c.tiles, c.tile_rows, c.tile_nnz = order, tiles, tile_rows, tile_nnz
+            c.valid = valid
         op = HodgeOperator(fwd, bwd)
     return _HODGE_CACHE.put(keys, n, op)
 
@@ -462,13 +475,13 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
                             ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order,
-                            A.tiles, A.tile_rows, A.tile_nnz)
+                            A.tiles, A.tile_rows, A.tile_nnz, A.valid)
     sink = out if (bn is None and not relu and x.dim() == 2) else None
     y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
                      bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order,
-                     A.tiles, A.tile_rows, A.tile_nnz)
+                     A.tiles, A.tile_rows, A.tile_nnz, A.valid)
     if bn is not None:
-        y = batch_norm_act(y, bn, relu)
+        y = batch_norm_act(y, bn, relu, valid=A.valid)
     elif relu:
         y = torch.relu(y)
     return y
@@ -612,7 +625,8 @@ def _mlp2_params(seq: torch.nn.Sequential):
 
 
 def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.Tensor,
-              wv_node: torch.nn.Sequential, wv_edge: torch.nn.Sequential):
+              wv_node: torch.nn.Sequential, wv_edge: torch.nn.Sequential,
+              valid_t: Optional[torch.Tensor] = None, valid_s: Optional[torch.Tensor] = None):
     """NodeEdgeInt value path (lib/Hodge_Cheb_Conv.py:293-295,307-308) as one
     C++ node, first Linear projected before the |B1| gathers (torch_ext.cpp,
     NEIntValueFn); returns (x_t1, x_s1), or None when the WV_* modules are not
@@ -628,7 +642,7 @@ def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.
     if rD.numel() != inc.n_nodes:
         raise RuntimeError(f"hlhgat: D has {rD.numel()} entries, |B1| has {inc.n_nodes} nodes")
     r = _ext.nei_value(x_t, x_s, inc.rowptr, inc.edge_ids, inc.edge_index,
-                       rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1])
+                       rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1], valid_t, valid_s)
     return r[0], r[1]
 
 
@@ -736,7 +750,8 @@ def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,
 # ----------------------------------------------------------------------------
 # BatchNorm1d (training statistics) + optional fused ReLU
 # ----------------------------------------------------------------------------
-def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False) -> torch.Tensor:
+def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False,
+                   valid: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bn(x) followed by ReLU when ``relu``; training mode (or no running
     stats) uses the HIP batch-statistics kernels, eval mode the running
     statistics (ATen's fused eval kernel)."""
@@ -751,7 +766,7 @@ def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False
     if x.size(0) < 2 and bn.training:
         raise ValueError(f"Expected more than 1 value per channel when training, got input "
                          f"size {tuple(x.shape)}")
-    return _ext.bn_act(x, *_bn_args(bn), bool(relu))
+    return _ext.bn_act(x, *_bn_args(bn), bool(relu), valid)
 
 
 # ----------------------------------------------------------------------------

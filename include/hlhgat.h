@@ -246,7 +246,11 @@ int hlhgat_segment_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
  * The workspace must be zero-filled before its first use and must not be
  * shared by launches that run concurrently; the kernels leave it reusable. */
 int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C);
-int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64_t C,
+/* n_valid (optional, device int32 scalar): rows >= *n_valid are capacity
+ * padding of a static-shape batch: excluded from the statistics, their
+ * outputs (and, backward, input gradients) written as 0.  NULL = all n. */
+int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
+                        const int32_t* n_valid, int64_t C,
                         const float* weight, const float* bias,
                         float* running_mean, float* running_var,
                         int64_t* num_batches_tracked, float momentum, float eps,
@@ -256,7 +260,8 @@ int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n, int64_t C,
 /* Backward; y (the forward output) supplies the ReLU mask, NULL if no ReLU.
  * dweight/dbias may be NULL. */
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                        const float* dy, int64_t lddy, int64_t n, int64_t C,
+                        const float* dy, int64_t lddy, int64_t n,
+                        const int32_t* n_valid, int64_t C,
                         const float* weight, const float* save_mean,
                         const float* save_invstd, float* dx, int64_t lddx,
                         float* dweight, float* dbias, void* workspace,

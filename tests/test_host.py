@@ -189,3 +189,25 @@ def test_row_order_collate_offsets_and_permutation():
     inv = np.empty_like(o)
     inv[o] = np.arange(len(o))
     assert np.abs(inv[ei[0]] - inv[ei[1]]).max() < np.abs(ei[0] - ei[1]).max()
+
+
+def test_pad_batch_structure():
+    from hlhgat.hodge_dataset import is_sorted_symmetric, pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(30, seed=2)
+    caps = static_caps(b, 128)
+    p = pad_batch(b, caps)
+    assert p.x_t.shape[0] == caps["rows_t"] and p.x_s.shape[0] == caps["rows_s"]
+    assert p.edge_index_t.shape[1] == caps["nnz_t"] and p.edge_index_s.shape[1] == caps["nnz_s"]
+    assert p.edge_index.shape[1] == caps["rows_s"]
+    for side in ("t", "s"):
+        ei, w = getattr(p, "edge_index_" + side), getattr(p, "edge_weight_" + side)
+        assert is_sorted_symmetric(ei.numpy(), w.numpy())
+        tp = getattr(p, "tile_ptr_" + side)
+        assert tp.numel() == caps["tiles_" + side] + 1
+        assert int(tp[-1]) == caps["rows_" + side] and bool((tp[1:] >= tp[:-1]).all())
+        n = getattr(b, "x_" + side).shape[0]
+        assert int(getattr(p, "n_valid_" + side)) == n
+        assert float(getattr(p, "x_" + side)[n:].abs().sum()) == 0.0
+    assert int(p.valid_mask_t.sum()) == b.x_t.shape[0]
+    assert torch.equal(p.num_node1, b.num_node1) and torch.equal(p.num_edge1, b.num_edge1)

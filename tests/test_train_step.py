@@ -162,3 +162,62 @@ def test_stream_fork_is_bitwise_neutral(cuda):
     assert l0 == l1
     for k in sd0:
         assert torch.equal(sd0[k], sd1[k]), k
+
+
+# ---------------------------------------------------------------------------
+# GPU: static-shape (padded) batches
+# ---------------------------------------------------------------------------
+def _caps_for(batches, quantum=256):
+    from hlhgat.hodge_dataset import static_caps
+    cs = [static_caps(b, quantum) for b in batches]
+    return {k: max(c[k] for c in cs) for k in cs[0]}
+
+
+@pytest.mark.gpu
+def test_padded_batch_matches_unpadded(cuda):
+    """Capacity padding (hodge_dataset.pad_batch) leaves the real rows' forward
+    values and every parameter gradient unchanged (BN statistics over the
+    valid rows only, padding rows isolated)."""
+    import hlhgat
+    from hlhgat.hodge_dataset import pad_batch
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(37, seed=21)
+    pb = pad_batch(b, _caps_for([b]))
+    assert pb.x_t.shape[0] > b.x_t.shape[0] and pb.x_s.shape[0] > b.x_s.shape[0]
+    res = []
+    for batch in (b, pb):
+        torch.manual_seed(0)
+        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
+        d = batch.to(cuda)
+        out = m(d)
+        loss = torch.nn.functional.l1_loss(out.view(-1), d.y.view(-1))
+        loss.backward()
+        res.append((out.detach().cpu(), {k: p.grad.detach().cpu().clone()
+                                         for k, p in m.named_parameters()},
+                    {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+    (o0, g0, s0), (o1, g1, s1) = res
+    assert torch.allclose(o0, o1, rtol=1e-5, atol=1e-6), (o0 - o1).abs().max()
+    for k in g0:
+        scale = g0[k].abs().max().clamp_min(1e-6)
+        assert ((g0[k] - g1[k]).abs().max() / scale) < 1e-4, k
+    for k in s0:  # running statistics of every BatchNorm
+        if s0[k].dtype.is_floating_point:
+            assert torch.allclose(s0[k], s1[k], rtol=1e-5, atol=1e-6), k
+
+
+@pytest.mark.gpu
+def test_padded_batches_share_one_graph(cuda):
+    """Batches of different sizes padded to one capacity bucket replay ONE
+    captured step; the replay equals the eager step on the same batches."""
+    from hlhgat.hodge_dataset import pad_batch
+    from hlhgat.synthetic import zinc_like_batch
+    raw = [zinc_like_batch(40, seed=s) for s in (3, 4, 5)]
+    caps = _caps_for(raw)
+    batches = [pad_batch(b, caps).to(cuda) for b in raw]
+    order = [0, 1, 2, 1, 0]
+    l_e, sd_e, _ = _run(False, True, batches, order)
+    l_g, sd_g, st = _run(True, True, batches, order)
+    assert st["captures"] == 1 and st["replay"] == len(order) - 1, st
+    assert l_e == l_g
+    for k in sd_e:
+        assert torch.equal(sd_e[k], sd_g[k]), k
