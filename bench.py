@@ -177,8 +177,8 @@ def main():
     poly_gbs = gbs(poly)
     traffic, traffic_src = pmc_traffic("k_poly_step")
     roofline = {
-        "kernel": "k_basis_local + k_poly_step (Laguerre basis over L0/L1 as graph-local "
-                  "one-launch kernels fwd + adjoint, CSR SpMM steps of the NodeEdgeInt gathers)",
+        "kernel": "k_poly_step (CSR SpMM / fused Laguerre step over L0 and L1, fwd + adjoint, "
+                  "and the NodeEdgeInt |B1| gathers)",
         "measured": f"hipExtLaunchKernel start/stop stamps, {args.prof_steps} eager steps after "
                     f"the timed region",
         "bound": "hbm", "achieved": round(poly_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -240,6 +240,13 @@ def set_row_order(edge_index: torch.Tensor, order: torch.Tensor) -> torch.Tensor
     return edge_index
 
 
+# Graph-local bases for collated batches (Batch._mark attaches the whole-graph
+# tiles).  Off by default: at the ZINC shape one graph-local launch costs what
+# its K-1 step launches cost (tools/kbench.py "basis" cases, profiles/), so the
+# simpler step path runs; HLHGAT_GRAPH_LOCAL=1 turns it on.
+GRAPH_LOCAL = os.environ.get("HLHGAT_GRAPH_LOCAL", "0") == "1"
+
+
 def set_tiles(edge_index: torch.Tensor, tile_ptr: torch.Tensor, tile_rows: int,
               tile_nnz: int) -> torch.Tensor:
     """Declare that the operator built from edge_index is block-diagonal over
