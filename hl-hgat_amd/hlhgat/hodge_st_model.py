@@ -15,7 +15,8 @@ from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt
 from .hodge_dataset import adj2par1, degree
 from .nn import BatchNorm, Sequential, run_sequential
 
-__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "segment_ptr", "mean_pool_sorted"]
+__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr", "segment_ptr",
+           "mean_pool_sorted"]
 
 
 def segment_ptr(counts: torch.Tensor, device) -> torch.Tensor:
@@ -135,3 +136,87 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         if if_final_layer:
             return x, y
         return y
+
+
+class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
+    """TSP edge-classification head (lib/Hodge_ST_Model.py:756-855, BASELINE
+    config 5): HL_init_conv on node coordinates and edge lengths, dense HL
+    blocks, readout per edge = [x_s, |B1^T x_t| / 2] -> K=1 HL conv MLP ->
+    K=1 HL conv, masked by the edge mask column of x_s.  Returns
+    (logits * mask, s_batch) like the reference."""
+
+    def __init__(self, channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[], K=2,
+                 node_dim=2, edge_dim=1, num_classes=1, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, keig=20):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.mlp_channels = mlp_channels
+        self.node_dim = node_dim
+        self.edge_dim = edge_dim
+        self.initial_channel = self.filters[0]
+        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, K,
+                                      dropout_ratio)
+        gcn_insize = self.initial_channel
+        for i, gcn_outsize in enumerate(self.filters):
+            for j in range(self.channels[i]):
+                setattr(self, "NEInt{}{}".format(i, j), NodeEdgeInt(d=gcn_insize, dv=gcn_outsize))
+                setattr(self, "NEConv{}{}".format(i, j),
+                        _hl_block(gcn_outsize, gcn_outsize, gcn_outsize, K, dropout_ratio))
+                gcn_insize = gcn_outsize + gcn_insize
+        mlp_insize = self.filters[-1] * 2
+        if len(self.mlp_channels) == 1:
+            self.mlp = Sequential("x_t, edge_index_t, edge_weight_t", [
+                (HodgeLaguerreConv(mlp_insize, self.mlp_channels[0], K=1),
+                 "x_t, edge_index_t, edge_weight_t -> x_t"),
+                (BatchNorm(self.mlp_channels[0]), "x_t -> x_t"),
+                (nn.ReLU(), "x_t -> x_t"),
+                (Dropout(p=dropout_ratio), "x_t -> x_t")])
+            mlp_insize = self.mlp_channels[0]
+        self.out = Sequential("x_t, edge_index_t, edge_weight_t", [
+            (HodgeLaguerreConv(mlp_insize, num_classes, K=1),
+             "x_t, edge_index_t, edge_weight_t -> x_t")])
+
+    def forward(self, data, device="cuda:0"):
+        dev = data.x_s.device
+        s_batch = torch.repeat_interleave(torch.arange(data.num_edge1.numel(), device=dev),
+                                          data.num_edge1.to(dev))
+        x_s, edge_index_s, edge_weight_s = data.x_s[:, :1], data.edge_index_s, data.edge_weight_s
+        edge_mask = data.x_s[:, 1:]
+        x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
+        width = self.initial_channel + sum(c * f for c, f in zip(self.channels, self.filters))
+        dense = x_t.is_cuda and x_t.dim() == 2 and ops.DENSE_SLAB
+        if dense:
+            dt = ops.DenseConcat(x_t.size(0), width, x_t)
+            ds = ops.DenseConcat(x_s.size(0), width, x_s)
+            _sink(self.HL_init_conv, dt, ds, self.initial_channel)
+        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                     edge_weight_s)
+        if dense:
+            dt.append(x_t)
+            ds.append(x_s)
+        x_s0, x_t0 = x_s, x_t
+        par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
+        D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0]) + 1e-6  # (:823)
+        for i, _ in enumerate(self.channels):
+            for j in range(self.channels[i]):
+                if dense:
+                    x_t0, x_s0 = dt.view(), ds.view()
+                x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
+                conv = getattr(self, "NEConv{}{}".format(i, j))
+                if dense:
+                    _sink(conv, dt, ds, self.filters[i])
+                x_t, x_s = conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                edge_weight_s)
+                if dense:
+                    dt.append(x_t)
+                    ds.append(x_s)
+                else:
+                    x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                    x_s0 = torch.cat([x_s0, x_s], dim=-1)
+        # readout (:846-851): x_t2s = |B1^T x_t| / 2 per edge
+        x_t2s = ops.boundary_t(x_t, par_1.incidence()).abs() / 2
+        x_s = torch.cat([x_s, x_t2s], dim=-1)
+        if len(self.mlp_channels) == 1:
+            x_s = self.mlp(x_s, edge_index_s, edge_weight_s)
+        return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch

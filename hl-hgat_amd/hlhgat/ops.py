@@ -667,6 +667,59 @@ def node_from_edges(x_s: torch.Tensor, inc: Incidence, rD: torch.Tensor) -> torc
                                 rD.contiguous().view(-1), inc.n_nodes)
 
 
+def _incidence_signs(inc: Incidence) -> torch.Tensor:
+    """Signed B1 values in incidence-CSR order: for node v's slot of edge e,
+    -1 if v = edge_index[0][e] (tail), +1 if v = edge_index[1][e] (head)
+    (adj2par1, lib/Hodge_Dataset.py:169-191).  Cached on the Incidence."""
+    s = getattr(inc, "_signs", None)
+    if s is None:
+        dev = inc.rowptr.device
+        counts = (inc.rowptr[1:] - inc.rowptr[:-1]).long()
+        node = torch.repeat_interleave(torch.arange(inc.n_nodes, device=dev), counts,
+                                       output_size=2 * inc.n_edges)
+        head = inc.edge_index[1][inc.edge_ids.long()]
+        s = torch.where(head == node, 1.0, -1.0).to(torch.float32).contiguous()
+        inc._signs = s  # type: ignore[attr-defined]
+    return s
+
+
+class _BoundaryTFn(torch.autograd.Function):
+    """y = B1^T x_t (y[e] = x_t[j] - x_t[i]); backward dx = B1 dy."""
+
+    @staticmethod
+    def forward(ctx, x_t, inc):
+        ctx.inc = inc
+        E, d = inc.n_edges, x_t.size(1)
+        y = torch.empty(E, d, device=x_t.device, dtype=x_t.dtype)
+        if E:
+            check(LIB.hlhgat_edge_gather2(inc.edge_index.data_ptr(), E, x_t.data_ptr(), _ld(x_t),
+                                          d, None, None, -1.0, 1.0, None, 0, y.data_ptr(),
+                                          _ld(y), 0, _stream(x_t)), "edge_gather2(B1^T)")
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        inc = ctx.inc
+        g = _rows2d(g.contiguous(), "grad")
+        A = SparseCSR(inc.rowptr, inc.edge_ids, _incidence_signs(inc), inc.n_nodes,
+                      inc.n_edges, 2 * inc.n_edges)
+        dx = torch.empty(inc.n_nodes, g.size(1), device=g.device, dtype=g.dtype)
+        if inc.n_nodes:
+            _poly_step(A, g, dx)
+        return dx, None
+
+
+def boundary_t(x_t: torch.Tensor, inc: Incidence) -> torch.Tensor:
+    """torch.sparse.mm(par_1.transpose(0, 1), x_t) for par_1 = adj2par1(...)
+    (lib/Hodge_ST_Model.py:846): per edge (i, j), x_t[j] - x_t[i], summed in
+    the coalesced order of the sparse product (tail entry first)."""
+    _req_dev(x_t, "x_t")
+    x_t = _rows2d(x_t, "x_t")
+    if x_t.size(0) != inc.n_nodes:
+        raise RuntimeError(f"hlhgat: x_t has {x_t.size(0)} rows, |B1| has {inc.n_nodes} nodes")
+    return _BoundaryTFn.apply(x_t, inc)
+
+
 def edge_from_nodes(x_t: torch.Tensor, inc: Incidence) -> torch.Tensor:
     _req_dev(x_t, "x_t")
     if x_t.size(0) != inc.n_nodes:

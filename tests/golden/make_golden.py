@@ -135,6 +135,40 @@ def zinc_case(ref_model, b):
     _save("zinc_model_small", **arrays)
 
 
+def tsp_case(ref_model):
+    """Whole HL_HGCNN_TSP_dense_int3_pyr (lib/Hodge_ST_Model.py:756-855) on two
+    small TSP-like graphs (k-NN on random points, sparse Hodge Laplacians)."""
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph
+    b = collate([tsp_like_graph(40 + s, n=48, k=4, row_order=False) for s in range(2)],
+                check_hodge=True)
+    torch.manual_seed(4)
+    m = ref_model.HL_HGCNN_TSP_dense_int3_pyr(channels=[1, 1], filters=[16, 16],
+                                              mlp_channels=[32], K=3)
+    m.train()
+    d = _RefData()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index"):
+        setattr(d, k, getattr(b, k))
+    d.num_node1 = [int(v) for v in b.num_node1]
+    d.num_edge1 = [int(v) for v in b.num_edge1]
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    out, s_batch = m(d, device="cpu")
+    gen = torch.Generator().manual_seed(8)
+    R = torch.randn(out.shape, generator=gen)
+    (out * R).sum().backward()
+    arrays = dict(x_t=_np(b.x_t), x_s=_np(b.x_s), edge_index_t=_np(b.edge_index_t),
+                  edge_weight_t=_np(b.edge_weight_t), edge_index_s=_np(b.edge_index_s),
+                  edge_weight_s=_np(b.edge_weight_s), edge_index=_np(b.edge_index),
+                  num_node1=_np(b.num_node1), num_edge1=_np(b.num_edge1), out=_np(out),
+                  s_batch=_np(s_batch), R=_np(R))
+    for k, v in sd0.items():
+        arrays["sd/" + k] = _np(v)
+    for k, p in m.named_parameters():
+        arrays["grad/" + k] = _np(p.grad)
+    _save("tsp_model_small", **arrays)
+
+
 def structure_case(b):
     """adj2par1 of the reference, densified, for a 2-graph batch."""
     par = ref_ds.adj2par1(b.edge_index, b.x_t.shape[0], b.x_s.shape[0])
@@ -157,3 +191,4 @@ if __name__ == "__main__":
     nei_cases(ref, b)
     zinc_case(ref_model, small_batch(8, seed=12))
     structure_case(small_batch(2, seed=13))
+    tsp_case(ref_model)

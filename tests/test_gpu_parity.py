@@ -317,6 +317,58 @@ def test_zinc_model_vs_reference_golden(cuda):
         close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
 
 
+def test_tsp_model_vs_reference_golden(cuda):
+    """HL_HGCNN_TSP_dense_int3_pyr (lib/Hodge_ST_Model.py:756-855, config 5
+    head) against the reference's own forward / backward on two small
+    TSP-like graphs (tests/golden/make_golden.py tsp_case): reference state
+    dict loaded unchanged, masked edge logits and every parameter gradient
+    within 1e-4 relative."""
+    import hlhgat
+    from hlhgat.hodge_dataset import Batch
+    g = load_golden("tsp_model_small")
+    m = hlhgat.HL_HGCNN_TSP_dense_int3_pyr(channels=[1, 1], filters=[16, 16],
+                                           mlp_channels=[32], K=3)
+    m.load_state_dict({k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")})
+    m = m.to(cuda).train()
+    b = Batch()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index", "num_node1", "num_edge1"):
+        setattr(b, k, dev(g[k]))
+    out, s_batch = m(b)
+    assert torch.equal(s_batch.cpu(), T(g["s_batch"]))
+    close(out.detach().cpu(), g["out"], 1e-4, "out")
+    (out * dev(g["R"])).sum().backward()
+    import re
+    for k, p in m.named_parameters():
+        if re.search(r"module_[04]\.bias$", k) and not k.startswith("out."):
+            # bias of a conv/linear that feeds a training-mode BatchNorm: its gradient
+            # is analytically 0 (BN removes any per-channel shift); both sides
+            # hold only fp32 rounding noise, compared as such
+            assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
+            continue
+        close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
+
+
+def test_boundary_transpose_matches_sparse_mm(cuda):
+    """ops.boundary_t == torch.sparse.mm(adj2par1(...).T, x) bitwise, and its
+    adjoint == B1 @ g (reference readout, lib/Hodge_ST_Model.py:846)."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import adj2par1
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(20, seed=4)
+    par = adj2par1(b.edge_index, b.x_t.shape[0], b.x_s.shape[0])
+    B1 = par.to_sparse_coo()
+    x = torch.randn(b.x_t.shape[0], 24, generator=torch.Generator().manual_seed(1))
+    ref = torch.sparse.mm(B1.t().coalesce(), x)
+    pard = adj2par1(dev(b.edge_index), b.x_t.shape[0], b.x_s.shape[0])
+    xd = dev(x).requires_grad_(True)
+    y = ops.boundary_t(xd, pard.incidence())
+    assert torch.equal(y.detach().cpu(), ref)
+    gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(2))
+    y.backward(dev(gy))
+    assert torch.equal(xd.grad.cpu(), torch.sparse.mm(B1.coalesce(), gy))
+
+
 def test_zinc_model_cfg2_vs_oracle(cuda):
     """BASELINE config 2 model at a 200-graph batch: HIP product vs oracle.
 
