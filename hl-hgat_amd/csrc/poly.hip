@@ -24,11 +24,12 @@ struct PolyArgs {
   const float* val;
   const float* rs;
   const float* X;
+  const float* B;  // operand of the beta term (NULL: X itself)
   const float* Z;
   const float* P;
   const float* Q;
   float* Y;
-  int64_t ldx, ldz, ldp, ldq, ldy;
+  int64_t ldx, ldb, ldz, ldp, ldq, ldy;
   int64_t n_rows;
   int d;
   float alpha, beta, gamma, div, p, q;
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
 #pragma unroll
     for (int i = 0; i < V; ++i) vget(out, i) = a.alpha * (rsv * vget(acc, i));
     if (a.beta != 0.f) {
-      vt xr = vload<V>(X + row * a.ldx + f);
+      vt xr = a.B ? vload<V>(a.B + row * a.ldb + f) : vload<V>(X + row * a.ldx + f);
 #pragma unroll
       for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.beta * vget(xr, i);
     }
@@ -570,6 +571,7 @@ int launch_local(bool fwd, int kind, const int32_t* rowptr, const int32_t* col,
                  int64_t max_rows, int64_t max_nnz, const float* X, int64_t ldx, int64_t F,
                  int K, float* out, hipStream_t s) {
   if (!tile_ptr || n_tiles <= 0 || max_rows <= 0 || max_nnz <= 0 || K > LOC_MAXK) return 0;
+  if (kind == HLHGAT_POLY_LAGUERRE_DEMO) return 0;  // step path only
   const int v = pick_vec(F, {fwd ? ldx : F, F}, {fwd ? X : out, out});
   const int l = pick_lpr(F, v);
   if ((int64_t)l * v < F) return 0;  // one lane group must span the features
@@ -646,10 +648,40 @@ int launch_local(bool fwd, int kind, const int32_t* rowptr, const int32_t* col,
 // Algorithmic bytes of one poly-step launch: CSR streamed once
 // (int32 col + fp32 val per nnz, int32 rowptr), the gathered operand counted
 // once per row (X read once), every dense row operand read once, Y written.
+// Reverse sweep of the DEMO recurrence (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py
+// :552-568) for one element:  T_1 = x - S,  T_{k+1} = (-S + (2k+1) T_k -
+// k T_{k-1})/(k+1) with S = L x.  In: G_k = dLoss/dT_k (G_0 = direct dX).
+// Out: block 0 = direct dX, block 1 = dS.
+struct DemoArgs {
+  float* G;
+  int64_t blk;
+  int K;
+};
+
+__global__ __launch_bounds__(256) void k_demo_adjoint_fold(DemoArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.blk) return;
+  float g[LOC_MAXK];
+#pragma unroll
+  for (int k = 0; k < LOC_MAXK; ++k) g[k] = k < a.K ? a.G[k * a.blk + i] : 0.f;
+  float ds = 0.f;
+#pragma unroll
+  for (int k = LOC_MAXK - 1; k >= 2; --k) {  // T_k from T_{k-1}, T_{k-2}, S
+    if (k >= a.K) continue;
+    const float gk = g[k] / (float)k;
+    g[k - 1] = g[k - 1] + (float)(2 * k - 1) * gk;
+    g[k - 2] = g[k - 2] - (float)(k - 1) * gk;
+    ds = ds - gk;
+  }
+  a.G[i] = g[0] + g[1];       // T_1 = x - S
+  a.G[a.blk + i] = ds - g[1];
+}
+
 double poly_bytes(const PolyArgs& a, int64_t nnz) {
   double b = (double)nnz * (a.val ? 8.0 : 4.0) + 4.0 * (double)(a.n_rows + 1);
   double row_bytes = 4.0 * (double)a.n_rows * a.d;
   int dense = 2;  // gathered X (read once) + Y written
+  if (a.B) dense++;
   if (a.Z) dense++;
   if (a.P) dense++;
   if (a.Q) dense++;
@@ -664,14 +696,15 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
   HLH_CHECK_ARG(a.rowptr && (nnz == 0 || a.col) && a.X && a.Y,
                 "poly_step: NULL pointer");
   HLH_CHECK_ARG(a.ldx >= a.d && a.ldy >= a.d, "poly_step: ld < d");
+  HLH_CHECK_ARG(!a.B || a.ldb >= a.d, "poly_step: ldb < d");
   HLH_CHECK_ARG(!a.Z || a.ldz >= a.d, "poly_step: ldz < d");
   HLH_CHECK_ARG(!a.P || a.ldp >= a.d, "poly_step: ldp < d");
   HLH_CHECK_ARG(!a.Q || a.ldq >= a.d, "poly_step: ldq < d");
   HLH_CHECK_ARG(a.div != 0.f, "poly_step: div == 0");
   if (a.n_rows == 0) return HLHGAT_OK;
   const int v = pick_vec(a.d, {a.ldx, a.ldy, a.Z ? a.ldz : 4, a.P ? a.ldp : 4,
-                               a.Q ? a.ldq : 4},
-                         {a.X, a.Y, a.Z, a.P, a.Q});
+                               a.Q ? a.ldq : 4, a.B ? a.ldb : 4},
+                         {a.X, a.Y, a.Z, a.P, a.Q, a.B});
   const int l = pick_lpr(a.d, v);
   ProfScope prof(HLHGAT_PROF_POLY, s, poly_bytes(a, nnz),
                  2.0 * (double)nnz * a.d);
@@ -750,7 +783,8 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
                                      int64_t max_tile_nnz, const float* X,
                                      int64_t ldx, int64_t F, int K, float* T,
                                      void* stream) {
-  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
+  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB ||
+                    kind == HLHGAT_POLY_LAGUERRE_DEMO,
                 "poly_basis_fwd: bad kind %d", kind);
   HLH_CHECK_ARG(K >= 1, "poly_basis_fwd: K must be > 0 (assert K > 0)");
   if (K == 1 || n == 0) return HLHGAT_OK;
@@ -766,7 +800,7 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
   // T_1
   {
     PolyArgs a = make_args(rowptr, col, val, n, X, ldx, F, Tk(1), F, row_order);
-    if (kind == HLHGAT_POLY_LAGUERRE) {  // Tx_1 = x - L x   (:494)
+    if (kind != HLHGAT_POLY_CHEB) {  // Tx_1 = x - L x   (:494; DEMO :554)
       a.alpha = -1.f;
       a.beta = 1.f;
     }  // Cheb: Tx_1 = L x   (:416)
@@ -779,7 +813,19 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
     PolyArgs a = make_args(rowptr, col, val, n, Tk(k), F, F, Tk(k + 1), F, row_order);
     a.Z = prev;
     a.ldz = ldprev;
-    if (kind == HLHGAT_POLY_LAGUERRE) {
+    if (kind == HLHGAT_POLY_LAGUERRE_DEMO) {
+      // DEMO fork: Tx_2 = (-L x + (2k+1) Tx_1 - k Tx_0) / (k+1) -- the SpMM
+      // operand is the layer INPUT x at every k
+      // (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:561,566)
+      a.X = X;
+      a.ldx = ldx;
+      a.B = Tk(k);
+      a.ldb = F;
+      a.alpha = -1.f;
+      a.beta = (float)(2 * k + 1);
+      a.gamma = -(float)k;
+      a.div = (float)(k + 1);
+    } else if (kind == HLHGAT_POLY_LAGUERRE) {
       // Tx_2 = (-L Tx_1 + (2k+1) Tx_1 - k Tx_0) / (k+1)   (:502,507)
       a.alpha = -1.f;
       a.beta = (float)(2 * k + 1);
@@ -803,7 +849,8 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                                      int64_t n_tiles, int64_t max_tile_rows,
                                      int64_t max_tile_nnz, int64_t F, int K,
                                      float* G, void* stream) {
-  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
+  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB ||
+                    kind == HLHGAT_POLY_LAGUERRE_DEMO,
                 "poly_basis_bwd: bad kind %d", kind);
   HLH_CHECK_ARG(K >= 1, "poly_basis_bwd: K must be > 0");
   if (K == 1 || n == 0) return HLHGAT_OK;
@@ -817,6 +864,21 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
   }
   const int64_t blk = n * F;
   auto Gk = [&](int k) -> float* { return G + (int64_t)k * blk; };
+  if (kind == HLHGAT_POLY_LAGUERRE_DEMO) {
+    // Every T_k (k >= 1) depends on x through S = L x and the recurrence:
+    // one elementwise reverse sweep folds G_K-1..G_1 into dS (block 1) and
+    // the direct part of dX (block 0), then dX += L^T dS.
+    HLH_CHECK_ARG(K <= LOC_MAXK, "poly_basis_bwd: DEMO recurrence needs K <= %d", LOC_MAXK);
+    DemoArgs d{G, n * F, K};
+    hipLaunchKernelGGL(k_demo_adjoint_fold, dim3((unsigned)ceil_div(n * F, (int64_t)256)),
+                       dim3(256), 0, s, d);
+    HLH_CHECK_LAUNCH();
+    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(1), F, F, Gk(0), F, row_order);
+    a.P = Gk(0);
+    a.ldp = F;
+    a.p = 1.f;
+    return launch_poly(a, nnz, s);
+  }
   for (int k = K - 1; k >= 1; --k) {
     PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F, row_order);
     a.P = Gk(k - 1);

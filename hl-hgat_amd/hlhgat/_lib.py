@@ -76,7 +76,7 @@ SIGNATURES = {
 }
 
 # constants from include/hlhgat.h
-POLY_LAGUERRE, POLY_CHEB = 0, 1
+POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
 PROF_POLY, PROF_PROJ = 0, 1
 MAX_BLOCKS = 16

@@ -97,12 +97,46 @@ class HodgeChebConv(_HodgePolyConv):
 
 class HodgeLaguerreFastConv(HodgeLaguerreConv):
     """DEMO fork's torch_sparse variant (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:519-582),
-    forward(x, adj_t) with adj_t given as (edge_index, edge_weight).  The
-    DEMO's k>=2 term uses x instead of Tx_1 (:561); that bug is NOT reproduced
-    here — this is the corrected recurrence."""
+    ``forward(x, adj_t)``.
+
+    As published, its k >= 2 terms propagate the layer INPUT x instead of
+    Tx_1 (:561):  T_{k+1} = (-L x + (2k+1) T_k - k T_{k-1}) / (k+1).  That is
+    what models trained with the DEMO (HL-HGAT-DEMO/weights/HL_HGAT_Brain.pt)
+    compute, so it is the default here (``demo_recurrence=True``, HIP kind
+    HLHGAT_POLY_LAGUERRE_DEMO); ``demo_recurrence=False`` gives the corrected
+    Laguerre recurrence of lib/Hodge_Cheb_Conv.py:502-507.  K = 1, 2 agree.
+
+    ``adj_t`` is any of: a torch_sparse-style object with ``.coo() -> (row,
+    col, value)`` (the DEMO's ``SparseTensor(row=ei[0], col=ei[1],
+    value=w).t()``, :179-180), a torch sparse COO/CSR tensor holding that
+    transpose (``adj_t[j, i] = w_ij``), or an ``(edge_index, edge_weight)``
+    pair in the ``propagate`` convention."""
+
+    def __init__(self, in_channels: int, out_channels: int, K: int, bias: bool = True,
+                 demo_recurrence: bool = True, **kwargs):
+        super().__init__(in_channels, out_channels, K, bias=bias, **kwargs)
+        self.demo_recurrence = demo_recurrence
+        self._kind = ops.POLY_LAGUERRE_DEMO if demo_recurrence else ops.POLY_LAGUERRE
+
+    @staticmethod
+    def adj_to_edge_index(adj_t):
+        """(edge_index, edge_weight) in the propagate convention (messages
+        flow edge_index[0] -> edge_index[1]) for adj_t = A^T."""
+        if isinstance(adj_t, (tuple, list)):
+            return adj_t[0], (adj_t[1] if len(adj_t) > 1 else None)
+        if hasattr(adj_t, "coo"):  # torch_sparse.SparseTensor
+            row, col, val = adj_t.coo()
+        elif torch.is_tensor(adj_t) and adj_t.layout in (torch.sparse_coo, torch.sparse_csr):
+            coo = adj_t.to_sparse_coo().coalesce()
+            (row, col), val = coo.indices(), coo.values()
+        else:
+            raise TypeError("HodgeLaguerreFastConv: adj_t must be a SparseTensor, a torch "
+                            "sparse tensor or (edge_index, edge_weight)")
+        # adj_t[r, c] = w  <=>  message c -> r; row-major order = target-sorted
+        return torch.stack([col, row]), val
 
     def forward(self, x: Tensor, adj_t, *args, **kwargs) -> Tensor:  # type: ignore[override]
-        edge_index, edge_weight = adj_t
+        edge_index, edge_weight = self.adj_to_edge_index(adj_t)
         return super().forward(x, edge_index, edge_weight)
 
 

@@ -30,10 +30,11 @@ __all__ = [
     "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks", "mlp2", "nei_value",
     "batch_norm_act",
     "node_from_edges", "edge_from_nodes", "att_score", "segment_mean",
-    "POLY_LAGUERRE", "POLY_CHEB", "SIGMA_SIGMOID", "SIGMA_RELU",
+    "POLY_LAGUERRE", "POLY_CHEB", "POLY_LAGUERRE_DEMO", "SIGMA_SIGMOID", "SIGMA_RELU",
 ]
 
 POLY_LAGUERRE, POLY_CHEB = _lib.POLY_LAGUERRE, _lib.POLY_CHEB
+POLY_LAGUERRE_DEMO = _lib.POLY_LAGUERRE_DEMO
 SIGMA_SIGMOID, SIGMA_RELU = _lib.SIGMA_SIGMOID, _lib.SIGMA_RELU
 
 

@@ -51,6 +51,11 @@ extern "C" {
 
 #define HLHGAT_POLY_LAGUERRE 0 /* HodgeLaguerreConv recurrence */
 #define HLHGAT_POLY_CHEB 1     /* HodgeChebConv recurrence */
+/* HL-HGAT-DEMO HodgeLaguerreFastConv as published: its k >= 2 terms
+ * propagate the layer input x instead of Tx_1
+ * (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:561); needed to reproduce outputs of
+ * models trained with it (HL-HGAT-DEMO/weights/HL_HGAT_Brain.pt). */
+#define HLHGAT_POLY_LAGUERRE_DEMO 2
 
 #define HLHGAT_SIGMA_SIGMOID 0 /* nn.Sigmoid (NodeEdgeInt default) */
 #define HLHGAT_SIGMA_RELU 1    /* nn.ReLU (attpool heads) */
@@ -133,6 +138,9 @@ int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
  *        (lib/Hodge_Cheb_Conv.py:494,507)
  * kind = HLHGAT_POLY_CHEB:     T_1 = A X, T_{k+1} = 2 A T_k - T_{k-1}
  *        (lib/Hodge_Cheb_Conv.py:416,430-432)
+ * kind = HLHGAT_POLY_LAGUERRE_DEMO: T_1 = X - A X,
+ *        T_{k+1} = (-A X + (2k+1) T_k - k T_{k-1}) / (k+1)
+ *        (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:554,561,566; K <= 16)
  * X: [n][F] row stride ldx.  T: (K-1) contiguous blocks of [n][F]. */
 /* tile_ptr (optional, int32[n_tiles+1], with max_tile_rows >= every tile's
  * row count): row ranges of runs of WHOLE graphs of a block-diagonal batch

@@ -6,6 +6,7 @@ PyTorch-CPU restatement of the HL-HGAT hot path, following the reference
   propagate            PyG MessagePassing, message = norm*x_j, aggr='add'
                        (lib/Hodge_Cheb_Conv.py:442-443, 518-519, 455)
   laguerre_conv        lib/Hodge_Cheb_Conv.py:480-515
+  laguerre_fast_conv_demo  HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:542-574 (bug kept)
   cheb_conv            lib/Hodge_Cheb_Conv.py:394-439
   adj2par1             lib/Hodge_Dataset.py:169-191
   node_edge_int        lib/Hodge_Cheb_Conv.py:293-309
@@ -65,6 +66,41 @@ def laguerre_conv(x, edge_index, edge_weight, weights, bias):
         Tx_0, Tx_1 = Tx_1, Tx_2
     if bias is not None:
         out = out + bias                                                  # :512-513
+    return out
+
+
+def laguerre_fast_conv_demo(x, edge_index, edge_weight, weights, bias):
+    """HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:542-574 (HodgeLaguerreFastConv) AS
+    PUBLISHED: the k >= 2 terms propagate the layer input x, not Tx_1 (:561).
+    torch_sparse.matmul(adj_t, x, reduce='add') with adj_t = A^T of
+    SparseTensor(row=ei[0], col=ei[1], value=w) (:179-180, :577-578) is the
+    same sum as propagate."""
+    K = len(weights)
+    Tx_0 = x
+    Tx_1 = x
+    out = F.linear(Tx_0, weights[0])
+    xshape = x.shape
+    k = 1
+    xv = x
+    if K > 1:
+        xv = x.reshape(xshape[0], -1)
+        Tx_1 = xv - propagate(xv, edge_index, edge_weight)                # :554
+        if len(xshape) >= 3:
+            Tx_1 = Tx_1.view(xshape[0], xshape[1], -1)
+        out = out + F.linear(Tx_1, weights[1])
+    for w in weights[2:]:
+        inshape = Tx_1.shape
+        Tx_1 = Tx_1.reshape(inshape[0], -1)
+        Tx_2 = propagate(xv, edge_index, edge_weight)                     # :561 (x, not Tx_1)
+        if len(xshape) >= 3:
+            Tx_2 = Tx_2.view(inshape[0], inshape[1], -1)
+            Tx_1 = Tx_1.view(xshape[0], xshape[1], -1)
+        Tx_2 = (-Tx_2 + (2 * k + 1) * Tx_1 - k * Tx_0) / (k + 1)          # :566
+        k += 1
+        out = out + F.linear(Tx_2, w)
+        Tx_0, Tx_1 = Tx_1, Tx_2
+    if bias is not None:
+        out = out + bias
     return out
 
 

@@ -12,6 +12,9 @@ It restates the documented semantics of the few symbols the hot path touches:
   * torch_geometric.nn.Sequential (entries registered as module_{i})
   * torch_geometric.utils.degree / dense_to_sparse, global_mean_pool,
     torch_scatter.scatter_mean
+  * torch_sparse.SparseTensor(row, col, value) with .t() / .coo(), and
+    torch_sparse.matmul(A, x, reduce='add'): out[r] = sum over A's row-r
+    entries in column order of value * x[col] (the DEMO fork only)
 Everything else is an inert placeholder.  It is not PyG.
 """
 from __future__ import annotations
@@ -141,6 +144,32 @@ def global_mean_pool(x, batch, size=None):
     return scatter_mean(x, batch, 0, size)
 
 
+class SparseTensor:
+    def __init__(self, row=None, col=None, value=None, sparse_sizes=None, **kw):
+        n = sparse_sizes or (int(row.max()) + 1, int(col.max()) + 1)
+        key = row * max(int(n[1]), 1) + col  # row-major (CSR) order
+        perm = torch.argsort(key, stable=True)
+        self.row, self.col = row[perm], col[perm]
+        self.value = value[perm] if value is not None else None
+        self.sizes = (int(n[0]), int(n[1]))
+
+    def t(self):
+        return SparseTensor(row=self.col, col=self.row, value=self.value,
+                            sparse_sizes=(self.sizes[1], self.sizes[0]))
+
+    def coo(self):
+        return self.row, self.col, self.value
+
+
+def sparse_matmul(src, other, reduce="sum"):
+    assert reduce in ("sum", "add")
+    msg = other.index_select(0, src.col)
+    if src.value is not None:
+        msg = src.value.view(-1, *([1] * (other.dim() - 1))) * msg
+    out = torch.zeros((src.sizes[0],) + tuple(other.shape[1:]), dtype=msg.dtype)
+    return out.index_add_(0, src.row, msg)
+
+
 def install():
     tg = _mod("torch_geometric")
     tg.__path__ = []
@@ -163,6 +192,10 @@ def install():
     nnm.global_max_pool = _Placeholder
     typing_ = _mod("torch_geometric.typing")
     typing_.OptTensor = object
+    typing_.SparseTensor = SparseTensor
+    tsp = _mod("torch_sparse")
+    tsp.SparseTensor = SparseTensor
+    tsp.matmul = sparse_matmul
     data = _mod("torch_geometric.data")
 
     class Data:
@@ -184,7 +217,8 @@ def install():
     utils = _mod("torch_geometric.utils")
     utils.__path__ = []
     for name in ("add_self_loops", "to_undirected", "coalesce", "to_scipy_sparse_matrix",
-                 "subgraph", "unbatch_edge_index", "softmax", "unbatch"):
+                 "subgraph", "unbatch_edge_index", "softmax", "unbatch",
+                 "remove_isolated_nodes"):
         setattr(utils, name, _Placeholder)
     utils.degree = degree
     utils.dense_to_sparse = dense_to_sparse

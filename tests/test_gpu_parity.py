@@ -157,6 +157,48 @@ def test_conv_vs_reference_golden(cuda, name):
         close(conv.lins[k].weight.grad.cpu(), g[f"grad_w{k}"], 1e-4, f"grad_w{k}")
 
 
+@pytest.mark.parametrize("name", golden_names("demo_fastconv_"))
+def test_demo_fastconv_vs_reference_golden(cuda, name):
+    """HL-HGAT-DEMO HodgeLaguerreFastConv (published :561 recurrence) on the
+    HIP kind HLHGAT_POLY_LAGUERRE_DEMO, adj_t in the DEMO's transpose form."""
+    import hlhgat
+    g = load_golden(name)
+    K = int(g["K"])
+    conv = hlhgat.HodgeLaguerreFastConv(g["w0"].shape[1], g["w0"].shape[0], K=K).to(cuda)
+    sd = {"bias": T(g["bias"])}
+    sd.update({f"lins.{k}.weight": T(g[f"w{k}"]) for k in range(K)})
+    conv.load_state_dict(sd)
+    ei, w = T(g["edge_index"]), T(g["edge_weight"])
+    n = g["x"].shape[0]
+    adj_t = torch.sparse_coo_tensor(torch.stack([ei[1], ei[0]]), w, (n, n)).to(cuda)
+    x = dev(g["x"]).requires_grad_(True)
+    out = conv(x, adj_t)
+    close(out.detach().cpu(), g["out"], 1e-5, "out")
+    (out * dev(g["R"])).sum().backward()
+    close(x.grad.cpu(), g["grad_x"], 1e-4, "grad_x")
+    close(conv.bias.grad.cpu(), g["grad_bias"], 1e-4, "grad_bias")
+    for k in range(K):
+        close(conv.lins[k].weight.grad.cpu(), g[f"grad_w{k}"], 1e-4, f"grad_w{k}")
+
+
+@pytest.mark.parametrize("K", [3, 5])
+def test_demo_basis_bitexact(cuda, K):
+    """Forward DEMO basis equals the oracle's operation order bit for bit."""
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(20, seed=K + 40)
+    ei, w, n = b.edge_index_t, b.edge_weight_t, b.x_t.shape[0]
+    x = torch.randn(n, 32, generator=torch.Generator().manual_seed(K))
+    op = ops.hodge_operator(ops.mark_hodge(dev(ei)), dev(w), n)
+    Tdev = ops.poly_basis(op, dev(x), K, ops.POLY_LAGUERRE_DEMO).cpu()
+    p = R.propagate(x, ei, w)
+    Ts = [x, x - p]
+    for k in range(1, K - 1):
+        Ts.append((-p + (2 * k + 1) * Ts[k] - k * Ts[k - 1]) / (k + 1))
+    for k in range(1, K):
+        assert torch.equal(Tdev[k - 1], Ts[k]), (K, k, (Tdev[k - 1] - Ts[k]).abs().max())
+
+
 def test_conv_unsorted_nonsymmetric_operator(cuda):
     """General (sorting) CSR path incl. the transposed adjoint for a
     non-symmetric operator: gradient w.r.t. x must use L^T."""

@@ -211,3 +211,26 @@ def test_pad_batch_structure():
         assert float(getattr(p, "x_" + side)[n:].abs().sum()) == 0.0
     assert int(p.valid_mask_t.sum()) == b.x_t.shape[0]
     assert torch.equal(p.num_node1, b.num_node1) and torch.equal(p.num_edge1, b.num_edge1)
+
+
+def test_fastconv_adj_t_forms_agree():
+    """HodgeLaguerreFastConv.forward(x, adj_t) accepts the DEMO's
+    SparseTensor(row=ei[0], col=ei[1], value=w).t() (duck-typed .coo()), a
+    torch sparse tensor holding A^T, or (edge_index, edge_weight); all map to
+    the same propagate edge list (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:179-180)."""
+    from hlhgat import HodgeLaguerreFastConv
+    ei = torch.tensor([[0, 1, 1, 2, 3], [1, 0, 2, 3, 3]])
+    w = torch.tensor([0.5, 0.25, 1.5, 2.0, 3.0])
+
+    class _ST:  # torch_sparse.SparseTensor(...).t(): rows = targets, sorted
+        def coo(self):
+            perm = torch.argsort(ei[1] * 10 + ei[0])
+            return ei[1][perm], ei[0][perm], w[perm]
+
+    dense_t = torch.zeros(4, 4).index_put_((ei[1], ei[0]), w, accumulate=True)
+    for adj in (_ST(), dense_t.to_sparse_coo(), dense_t.to_sparse_csr(), (ei, w)):
+        e2, w2 = HodgeLaguerreFastConv.adj_to_edge_index(adj)
+        got = torch.zeros(4, 4).index_put_((e2[1], e2[0]), w2, accumulate=True)
+        assert torch.equal(got, dense_t)
+    assert HodgeLaguerreFastConv(4, 4, K=3)._kind != HodgeLaguerreFastConv(
+        4, 4, K=3, demo_recurrence=False)._kind

@@ -28,6 +28,27 @@ def test_conv_oracle_matches_reference(name):
         close(ws[k].grad, g[f"grad_w{k}"], 1e-6, f"grad_w{k}")
 
 
+@pytest.mark.parametrize("name", golden_names("demo_fastconv_"))
+def test_demo_fastconv_oracle_matches_reference(name):
+    """HL-HGAT-DEMO HodgeLaguerreFastConv as published (x at :561), vectors
+    from tests/golden/make_golden_demo.py."""
+    g = load_golden(name)
+    K = int(g["K"])
+    x = T(g["x"]).requires_grad_(True)
+    ws = [T(g[f"w{k}"]).requires_grad_(True) for k in range(K)]
+    b = T(g["bias"]).requires_grad_(True)
+    out = R.laguerre_fast_conv_demo(x, T(g["edge_index"]), T(g["edge_weight"]), ws, b)
+    close(out.detach(), g["out"], 1e-6, "out")
+    (out * T(g["R"])).sum().backward()
+    close(x.grad, g["grad_x"], 1e-6, "grad_x")
+    for k in range(K):
+        close(ws[k].grad, g[f"grad_w{k}"], 1e-6, f"grad_w{k}")
+    if K >= 3:  # the published recurrence really differs from the corrected one
+        ref = R.laguerre_conv(x.detach(), T(g["edge_index"]), T(g["edge_weight"]),
+                              [w.detach() for w in ws], b.detach())
+        assert (ref - T(g["out"])).abs().max() > 1e-3
+
+
 def _sd(g):
     return {k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")}
 
