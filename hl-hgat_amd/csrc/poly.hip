@@ -33,6 +33,13 @@ struct PolyArgs {
   int64_t n_rows;
   int d;
   float alpha, beta, gamma, div, p, q;
+  // halo tiles (optional; lcol != NULL selects k_poly_halo, see hlhgat_halo_t)
+  const int32_t* htile;
+  const int32_t* hptr;
+  const int32_t* hcols;
+  const uint16_t* lcol;
+  int64_t n_tiles;
+  int max_halo;
 };
 
 // Row r's CSR entries are staged LPR at a time: lane `sub` of the row group
@@ -45,6 +52,43 @@ struct PolyArgs {
 __device__ __forceinline__ unsigned xcd_slot(unsigned b, unsigned nb) {
   const unsigned x = b & 7u, k = b >> 3, per = nb >> 3, extra = nb & 7u;
   return x * per + (x < extra ? x : extra) + k;
+}
+
+// Row epilogue shared by k_poly_step and k_poly_halo (identical operations,
+// hence identical results):  Y = (alpha*rs*acc + beta*B + gamma*Z)/div + p*P + q*Q
+template <int V>
+__device__ __forceinline__ void poly_epilogue(const PolyArgs& a, int64_t row, int f,
+                                              typename VecT<V>::type acc, float rsv) {
+  using vt = typename VecT<V>::type;
+  const float* __restrict__ X = a.X;
+  vt out;
+#pragma unroll
+  for (int i = 0; i < V; ++i) vget(out, i) = a.alpha * (rsv * vget(acc, i));
+  if (a.beta != 0.f) {
+    vt xr = a.B ? vload<V>(a.B + row * a.ldb + f) : vload<V>(X + row * a.ldx + f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.beta * vget(xr, i);
+  }
+  if (a.Z) {
+    vt z = vload<V>(a.Z + row * a.ldz + f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.gamma * vget(z, i);
+  }
+  if (a.div != 1.f) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) / a.div;
+  }
+  if (a.P) {
+    vt pv = vload<V>(a.P + row * a.ldp + f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.p * vget(pv, i);
+  }
+  if (a.Q) {
+    vt qv = vload<V>(a.Q + row * a.ldq + f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.q * vget(qv, i);
+  }
+  vstore<V>(a.Y + row * a.ldy + f, out);
 }
 
 template <int V, int LPR>
@@ -107,34 +151,109 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
       }
     }
     if (!fok) continue;
-    vt out;
+    poly_epilogue<V>(a, row, f, acc, rsv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-staged SpMM / polynomial step over halo tiles (large Laplacians).
+//
+// At TSP scale (BASELINE config 5: L1 of 4 x 10k-node kNN graphs, n = 207k
+// rows, ~20 entries per row) k_poly_step is bound by the L2 -> CU gather
+// rate: every entry re-reads a 256-512 B feature row from L2.  Here one
+// workgroup owns a halo tile (hlhgat_halo_tiles: a run of the row schedule
+// whose rows reference <= max_halo distinct columns, ~5 uses per staged row in
+// RCM order): it stages those X rows -- one FS-float feature slice at a time
+// -- in LDS with coalesced row loads, then every row group walks its rows'
+// entries in CSR order gathering from LDS (ds_read_b128, 256-B pitch:
+// conflict-free).  Same per-row summation order and epilogue as k_poly_step,
+// so the results are bitwise equal.  Tiles are dealt XCD-contiguously
+// (xcd_slot) so neighbouring tiles -- which share much of their halo -- hit
+// the same L2.
+// ---------------------------------------------------------------------------
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_poly_halo(PolyArgs a) {
+  using vt = typename VecT<V>::type;
+  constexpr int FS = V * LPR;   // features per staged slice
+  constexpr int RG = 256 / LPR; // row groups per workgroup
+  extern __shared__ float4 halo_lds[];
+  float* img = reinterpret_cast<float*>(halo_lds);
+  const int64_t t = xcd_slot(blockIdx.x, gridDim.x);
+  if (t >= a.n_tiles) return;  // whole workgroup: uniform
+  const int p0 = a.htile[t], p1 = a.htile[t + 1];
+  const int hb = a.hptr[t], nh = a.hptr[t + 1] - hb;
+  const int sub = threadIdx.x % LPR, rg = threadIdx.x / LPR;
+  const float* __restrict__ X = a.X;
+  for (int f0 = 0; f0 < a.d; f0 += FS) {
+    const int f = f0 + sub * V;
+    const bool fok = f < a.d;
+    if (f0) __syncthreads();  // the previous slice's readers are done
+    for (int h = rg; h < nh; h += 4 * RG) {  // four row loads in flight per lane
+      vt v[4];
 #pragma unroll
-    for (int i = 0; i < V; ++i) vget(out, i) = a.alpha * (rsv * vget(acc, i));
-    if (a.beta != 0.f) {
-      vt xr = a.B ? vload<V>(a.B + row * a.ldb + f) : vload<V>(X + row * a.ldx + f);
+      for (int u = 0; u < 4; ++u) {
+        const int hh = h + u * RG;
+        if (hh < nh && fok) {
+          v[u] = vload<V>(X + (int64_t)a.hcols[hb + hh] * a.ldx + f);
+        } else {
 #pragma unroll
-      for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.beta * vget(xr, i);
+          for (int i = 0; i < V; ++i) vget(v[u], i) = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int hh = h + u * RG;
+        if (hh < nh) vstore<V>(img + hh * FS + sub * V, v[u]);
+      }
     }
-    if (a.Z) {
-      vt z = vload<V>(a.Z + row * a.ldz + f);
+    __syncthreads();
+    for (int p = p0 + rg; p < p1; p += RG) {
+      const int64_t row = a.order ? (int64_t)a.order[p] : (int64_t)p;
+      const int e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
+      const float rsv = a.rs ? a.rs[row] : 1.f;
+      vt acc;
 #pragma unroll
-      for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.gamma * vget(z, i);
-    }
-    if (a.div != 1.f) {
+      for (int i = 0; i < V; ++i) vget(acc, i) = 0.f;
+      for (int eb = e0; eb < e1; eb += LPR) {
+        const int me = eb + sub;
+        const int cm = me < e1 ? (int)a.lcol[me] : 0;
+        const float wm = me < e1 ? (a.val ? a.val[me] : 1.f) : 0.f;
+        const int cnt = e1 - eb < LPR ? e1 - eb : LPR;
+        int j = 0;
+        for (; j + 3 < cnt; j += 4) {
+          const int c0 = __shfl(cm, j, LPR), c1 = __shfl(cm, j + 1, LPR),
+                    c2 = __shfl(cm, j + 2, LPR), c3 = __shfl(cm, j + 3, LPR);
+          const float w0 = __shfl(wm, j, LPR), w1 = __shfl(wm, j + 1, LPR),
+                      w2 = __shfl(wm, j + 2, LPR), w3 = __shfl(wm, j + 3, LPR);
+          if (fok) {
+            vt x0 = vload<V>(img + c0 * FS + sub * V);
+            vt x1 = vload<V>(img + c1 * FS + sub * V);
+            vt x2 = vload<V>(img + c2 * FS + sub * V);
+            vt x3 = vload<V>(img + c3 * FS + sub * V);
 #pragma unroll
-      for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) / a.div;
-    }
-    if (a.P) {
-      vt pv = vload<V>(a.P + row * a.ldp + f);
+            for (int i = 0; i < V; ++i) {
+              float s = vget(acc, i);
+              s = s + w0 * vget(x0, i);
+              s = s + w1 * vget(x1, i);
+              s = s + w2 * vget(x2, i);
+              s = s + w3 * vget(x3, i);
+              vget(acc, i) = s;
+            }
+          }
+        }
+        for (; j < cnt; ++j) {
+          const int c = __shfl(cm, j, LPR);
+          const float w = __shfl(wm, j, LPR);
+          if (fok) {
+            vt x = vload<V>(img + c * FS + sub * V);
 #pragma unroll
-      for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.p * vget(pv, i);
+            for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
+          }
+        }
+      }
+      if (!fok) continue;
+      poly_epilogue<V>(a, row, f, acc, rsv);
     }
-    if (a.Q) {
-      vt qv = vload<V>(a.Q + row * a.ldq + f);
-#pragma unroll
-      for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.q * vget(qv, i);
-    }
-    vstore<V>(a.Y + row * a.ldy + f, out);
   }
 }
 
@@ -689,6 +808,8 @@ double poly_bytes(const PolyArgs& a, int64_t nnz) {
   return b + dense * row_bytes;
 }
 
+constexpr size_t kHaloLdsBytes = 64 * 1024;  // LDS image of one halo tile (2+ WGs / CU)
+
 int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
   HLH_CHECK_ARG(a.n_rows >= 0 && a.n_rows < (int64_t)INT32_MAX,
                 "poly_step: n_rows out of range");
@@ -708,6 +829,25 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
   const int l = pick_lpr(a.d, v);
   ProfScope prof(HLHGAT_PROF_POLY, s, poly_bytes(a, nnz),
                  2.0 * (double)nnz * a.d);
+  if (a.lcol && a.n_tiles > 0) {
+    const int lh = l > 16 ? 16 : l;  // FS = v * lh features per staged slice
+    const size_t shmem = (size_t)a.max_halo * v * lh * sizeof(float);
+    if (shmem <= kHaloLdsBytes) {
+      const unsigned grid = (unsigned)a.n_tiles;
+      switch (v * 100 + lh) {
+#define HLH_HALO_CASE(VV, LL) \
+  case VV * 100 + LL: launch(k_poly_halo<VV, LL>, grid, 256, shmem, s, &prof, a); break;
+        HLH_HALO_CASE(1, 1) HLH_HALO_CASE(1, 2) HLH_HALO_CASE(1, 4) HLH_HALO_CASE(1, 8)
+        HLH_HALO_CASE(1, 16) HLH_HALO_CASE(2, 1) HLH_HALO_CASE(2, 2) HLH_HALO_CASE(2, 4)
+        HLH_HALO_CASE(2, 8) HLH_HALO_CASE(2, 16) HLH_HALO_CASE(4, 1) HLH_HALO_CASE(4, 2)
+        HLH_HALO_CASE(4, 4) HLH_HALO_CASE(4, 8) HLH_HALO_CASE(4, 16)
+#undef HLH_HALO_CASE
+        default: break;
+      }
+      HLH_CHECK_LAUNCH();
+      return HLHGAT_OK;
+    }
+  }
   HLH_DISPATCH_VL(v, l, k_poly_step, a.n_rows, s, a, &prof);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
@@ -715,9 +855,18 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
 
 PolyArgs make_args(const int32_t* rowptr, const int32_t* col, const float* val,
                    int64_t n, const float* X, int64_t ldx, int64_t d, float* Y,
-                   int64_t ldy, const int32_t* order = nullptr) {
+                   int64_t ldy, const int32_t* order = nullptr,
+                   const hlhgat_halo_t* halo = nullptr) {
   PolyArgs a{};
   a.order = order;
+  if (halo && halo->lcol && halo->n_tiles > 0) {
+    a.htile = halo->tile_ptr;
+    a.hptr = halo->halo_ptr;
+    a.hcols = halo->halo;
+    a.lcol = halo->lcol;
+    a.n_tiles = halo->n_tiles;
+    a.max_halo = halo->max_halo;
+  }
   a.rowptr = rowptr;
   a.col = col;
   a.val = val;
@@ -743,22 +892,24 @@ using namespace hlhgat;
 
 extern "C" int hlhgat_spmm(const int32_t* rowptr, const int32_t* col,
                            const float* val, int64_t n_rows, int64_t nnz,
-                           const int32_t* row_order, const float* X, int64_t ldx,
+                           const int32_t* row_order, const hlhgat_halo_t* halo,
+                           const float* X, int64_t ldx,
                            int64_t d, float* Y, int64_t ldy, void* stream) {
-  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy, row_order);
+  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy, row_order, halo);
   return launch_poly(a, nnz, as_stream(stream));
 }
 
 extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
                                 const float* val, const float* rs,
                                 int64_t n_rows, int64_t nnz,
-                                const int32_t* row_order, const float* X,
+                                const int32_t* row_order, const hlhgat_halo_t* halo,
+                                const float* X,
                                 int64_t ldx, int64_t d, const float* Z,
                                 int64_t ldz, const float* P, int64_t ldp,
                                 const float* Q, int64_t ldq, float alpha,
                                 float beta, float gamma, float div, float p,
                                 float q, float* Y, int64_t ldy, void* stream) {
-  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy, row_order);
+  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy, row_order, halo);
   a.rs = rs;
   a.Z = Z;
   a.ldz = ldz;
@@ -778,7 +929,8 @@ extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
 extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
                                      const int32_t* col, const float* val,
                                      int64_t n, int64_t nnz,
-                                     const int32_t* row_order, const int32_t* tile_ptr,
+                                     const int32_t* row_order, const hlhgat_halo_t* halo,
+                                     const int32_t* tile_ptr,
                                      int64_t n_tiles, int64_t max_tile_rows,
                                      int64_t max_tile_nnz, const float* X,
                                      int64_t ldx, int64_t F, int K, float* T,
@@ -799,7 +951,7 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
   auto Tk = [&](int k) -> float* { return T + (int64_t)(k - 1) * blk; };
   // T_1
   {
-    PolyArgs a = make_args(rowptr, col, val, n, X, ldx, F, Tk(1), F, row_order);
+    PolyArgs a = make_args(rowptr, col, val, n, X, ldx, F, Tk(1), F, row_order, halo);
     if (kind != HLHGAT_POLY_CHEB) {  // Tx_1 = x - L x   (:494; DEMO :554)
       a.alpha = -1.f;
       a.beta = 1.f;
@@ -810,7 +962,7 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
   for (int k = 1; k + 1 < K; ++k) {
     const float* prev = (k == 1) ? X : Tk(k - 1);
     const int64_t ldprev = (k == 1) ? ldx : F;
-    PolyArgs a = make_args(rowptr, col, val, n, Tk(k), F, F, Tk(k + 1), F, row_order);
+    PolyArgs a = make_args(rowptr, col, val, n, Tk(k), F, F, Tk(k + 1), F, row_order, halo);
     a.Z = prev;
     a.ldz = ldprev;
     if (kind == HLHGAT_POLY_LAGUERRE_DEMO) {
@@ -845,7 +997,8 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
 extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                                      const int32_t* col_t, const float* val_t,
                                      int64_t n, int64_t nnz,
-                                     const int32_t* row_order, const int32_t* tile_ptr,
+                                     const int32_t* row_order, const hlhgat_halo_t* halo,
+                                     const int32_t* tile_ptr,
                                      int64_t n_tiles, int64_t max_tile_rows,
                                      int64_t max_tile_nnz, int64_t F, int K,
                                      float* G, void* stream) {
@@ -873,14 +1026,14 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
     hipLaunchKernelGGL(k_demo_adjoint_fold, dim3((unsigned)ceil_div(n * F, (int64_t)256)),
                        dim3(256), 0, s, d);
     HLH_CHECK_LAUNCH();
-    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(1), F, F, Gk(0), F, row_order);
+    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(1), F, F, Gk(0), F, row_order, halo);
     a.P = Gk(0);
     a.ldp = F;
     a.p = 1.f;
     return launch_poly(a, nnz, s);
   }
   for (int k = K - 1; k >= 1; --k) {
-    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F, row_order);
+    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F, row_order, halo);
     a.P = Gk(k - 1);
     a.ldp = F;
     a.p = 1.f;

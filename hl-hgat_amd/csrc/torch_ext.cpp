@@ -85,6 +85,28 @@ struct Csr {
   int64_t nnz;
 };
 
+// hlhgat_halo_t over the halo-tile tensors of an operator (see hlhgat.h)
+hlhgat_halo_t make_halo(const Tensor& tile, const Tensor& ptr, const Tensor& cols,
+                        const Tensor& lcol, int64_t max_halo) {
+  hlhgat_halo_t h{};
+  if (!lcol.defined()) return h;
+  TORCH_CHECK(tile.scalar_type() == at::kInt && ptr.scalar_type() == at::kInt &&
+                  cols.scalar_type() == at::kInt && lcol.element_size() == 2,
+              "hlhgat: halo tiles must be int32 (tile_ptr, halo_ptr, halo) and 16-bit lcol");
+  h.tile_ptr = tile.data_ptr<int>();
+  h.halo_ptr = ptr.data_ptr<int>();
+  h.halo = cols.data_ptr<int>();
+  h.lcol = reinterpret_cast<const uint16_t*>(lcol.data_ptr());
+  h.n_tiles = tile.numel() - 1;
+  h.max_halo = (int32_t)max_halo;
+  return h;
+}
+hlhgat_halo_t make_halo(const OptT& tile, const OptT& ptr, const OptT& cols, const OptT& lcol,
+                        int64_t max_halo) {
+  if (!(has(tile) && has(ptr) && has(cols) && has(lcol))) return hlhgat_halo_t{};
+  return make_halo(*tile, *ptr, *cols, *lcol, max_halo);
+}
+
 // One BN workspace per (device, stream): its arrival counters must not be
 // shared by launches that can run concurrently (node / edge chains run on two
 // streams, see hlhgat.ops.fork).  Stream-ordered reuse on one stream is safe.
@@ -240,7 +262,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
                         int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order,
-                        OptT tiles, int64_t tile_rows, int64_t tile_nnz, OptT valid) {
+                        OptT tiles, int64_t tile_rows, int64_t tile_nnz, OptT valid,
+                        OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_lcol, int64_t h_max) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -251,10 +274,14 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     const int64_t dout = W[0].size(0);
     void* s = stream_of(x);
     Tensor T = at::empty({std::max<int64_t>(K - 1, 0), N, F}, x.options());
+    // halo tiles describe A; they serve the adjoint only when A^T is A
+    const bool use_halo = has(h_lcol) && has(h_tile) && has(h_ptr) && has(h_cols);
+    const hlhgat_halo_t halo = make_halo(h_tile, h_ptr, h_cols, h_lcol, h_max);
     if (K > 1 && N > 0) {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
                                 nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
+                                use_halo ? &halo : nullptr,
                                 iptr(tiles), has(tiles) ? tiles->numel() - 1 : 0, tile_rows,
                                 tile_nnz, x2.data_ptr<float>(),
                                 ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
@@ -322,10 +349,17 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.other();
       em.other();
       em.opt(valid);
+      em.opt(h_tile);
+      em.opt(h_ptr);
+      em.opt(h_cols);
+      em.opt(h_lcol);
+      em.other();
       ctx->saved_data["edges"] = em.e;
       ctx->saved_data["tile_rows"] = tile_rows;
       ctx->saved_data["tile_nnz"] = tile_nnz;
+      ctx->saved_data["h_max"] = h_max;
     }
+    const bool halo_bwd = use_halo && t_rowptr.data_ptr() == a_rowptr.data_ptr();
     ctx->saved_data["xshape"] = x.sizes().vec();
     std::vector<Tensor> save = {x2,
                                 T,
@@ -341,7 +375,11 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                 invstd,
                                 has(bn_w) ? *bn_w : Tensor(),
                                 has(bias) ? *bias : Tensor(),
-                                has(bn_b) ? *bn_b : Tensor()};
+                                has(bn_b) ? *bn_b : Tensor(),
+                                halo_bwd ? *h_tile : Tensor(),
+                                halo_bwd ? *h_ptr : Tensor(),
+                                halo_bwd ? *h_cols : Tensor(),
+                                halo_bwd ? *h_lcol : Tensor()};
     for (const auto& w : W) save.push_back(w);
     ctx->save_for_backward(save);
     std::vector<int64_t> oshape = x.sizes().vec();
@@ -358,8 +396,13 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     auto sv = ctx->get_saved_variables();
     Tensor x2 = sv[0], T = sv[1], t_order = sv[2], tiles = sv[3], valid = sv[4],
            t_rowptr = sv[5], t_col = sv[6], t_val = sv[7], pre = sv[8], yout = sv[9],
-           mean = sv[10], invstd = sv[11], bn_w = sv[12], bias_p = sv[13], bn_b = sv[14];
-    std::vector<Tensor> W(sv.begin() + 15, sv.end());
+           mean = sv[10], invstd = sv[11], bn_w = sv[12], bias_p = sv[13], bn_b = sv[14],
+           h_tile = sv[15], h_ptr = sv[16], h_cols = sv[17], h_lcol = sv[18];
+    std::vector<Tensor> W(sv.begin() + 19, sv.end());
+    const bool use_halo = h_lcol.defined();
+    const hlhgat_halo_t halo =
+        use_halo ? make_halo(h_tile, h_ptr, h_cols, h_lcol, ctx->saved_data["h_max"].toInt())
+                 : hlhgat_halo_t{};
     const int64_t tile_rows = ctx->saved_data["tile_rows"].toInt();
     const int64_t tile_nnz = ctx->saved_data["tile_nnz"].toInt();
     void* s = stream_of(x2);
@@ -367,7 +410,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 25 + K;
+    const int64_t n_pos = 30 + K;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -427,6 +470,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                     nnz ? t_col.data_ptr<int>() : nullptr,
                                     (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
                                     N, nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
+                                    use_halo ? &halo : nullptr,
                                     tiles.defined() ? tiles.data_ptr<int>() : nullptr,
                                     tiles.defined() ? tiles.numel() - 1 : 0, tile_rows,
                                     tile_nnz, F, (int)K, Gs.data_ptr<float>(), s),
@@ -697,7 +741,8 @@ Tensor node_segment(const Tensor& rowptr, const Tensor& eids, int64_t n_nodes, i
   Tensor out = at::empty({n_nodes, x.size(1)}, x.options());
   if (n_nodes > 0) {
     chk(hlhgat_poly_step(rowptr.data_ptr<int>(), n_edges ? eids.data_ptr<int>() : nullptr,
-                         nullptr, rs, n_nodes, 2 * n_edges, nullptr, x.data_ptr<float>(), ld_of(x),
+                         nullptr, rs, n_nodes, 2 * n_edges, nullptr, nullptr, x.data_ptr<float>(),
+                         ld_of(x),
                          x.size(1), nullptr, 0, nullptr, 0, nullptr, 0, alpha, 0.f, 0.f, 1.f,
                          0.f, 0.f, out.data_ptr<float>(), ld_of(out), stream_of(x)),
         "poly_step(incidence)");
@@ -926,7 +971,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     }
     if (N > 0) {  // node side: h1_t = Qt + rD * |B1| P1, then its MLP
       chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
-                           rD.data_ptr<float>(), N, 2 * E, nullptr, Ys.data_ptr<float>() + de,
+                           rD.data_ptr<float>(), N, 2 * E, nullptr, nullptr,
+                           Ys.data_ptr<float>() + de,
                            de + dn, dn,
                            Yt.data_ptr<float>(), dn + de, nullptr, 0, nullptr, 0, 1.f, 0.f, 1.f,
                            1.f, 0.f, 0.f, h1t.data_ptr<float>(), dn, fk.main.stream()),
@@ -1012,7 +1058,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     // dP2[v] = 1/2 sum_{e ni v} dh1_s[e]  -> dYt[:, dn:]
     if (N > 0) {
       chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
-                           nullptr, N, 2 * E, nullptr, dYs.data_ptr<float>(), de + dn, de,
+                           nullptr, N, 2 * E, nullptr, nullptr, dYs.data_ptr<float>(), de + dn,
+                           de,
                            nullptr, 0,
                            nullptr, 0, nullptr, 0, 0.5f, 0.f, 0.f, 1.f, 0.f, 0.f,
                            dYt.data_ptr<float>() + dn, dn + de, fk.main.stream()),
@@ -1073,11 +1120,12 @@ Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_row
                OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
                int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT tiles,
-               int64_t tile_rows, int64_t tile_nnz, OptT valid) {
+               int64_t tile_rows, int64_t tile_nnz, OptT valid, OptT h_tile, OptT h_ptr,
+               OptT h_cols, OptT h_lcol, int64_t h_max) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
                          bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz,
-                         valid);
+                         valid, h_tile, h_ptr, h_cols, h_lcol, h_max);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

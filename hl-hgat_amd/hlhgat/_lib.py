@@ -33,16 +33,18 @@ SIGNATURES = {
                                            c_vp, c_vp]),
     "hlhgat_coo_check_sorted": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "hlhgat_incidence_csr": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
-    "hlhgat_spmm": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_i64, c_vp,
-                            c_i64, c_vp]),
-    "hlhgat_poly_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_i64,
-                                 c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32, c_f32,
-                                 c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
+    "hlhgat_halo_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
+                                  c_vp, c_vp, P_i64, P_i64]),
+    "hlhgat_spmm": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
+                            c_vp, c_i64, c_vp]),
+    "hlhgat_poly_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
+                                 c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32,
+                                 c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                      c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp,
-                                      c_vp]),
+                                      c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32,
+                                      c_vp, c_vp]),
     "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                      c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp]),
+                                      c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
@@ -80,6 +82,12 @@ POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
 PROF_POLY, PROF_PROJ = 0, 1
 MAX_BLOCKS = 16
+
+
+class HaloDesc(C.Structure):
+    """hlhgat_halo_t (include/hlhgat.h)."""
+    _fields_ = [("tile_ptr", c_vp), ("halo_ptr", c_vp), ("halo", c_vp), ("lcol", c_vp),
+                ("n_tiles", c_i64), ("max_halo", c_i32)]
 
 
 class HlhgatError(RuntimeError):

@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "graph_tiles", "static_caps", "pad_batch"]
+           "graph_tiles", "static_caps", "pad_batch", "halo_tiles"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
 _HODGE_KEYS = ("edge_index_s", "edge_index_t")
@@ -90,7 +90,7 @@ class Batch(PairData):
 
     def _mark(self) -> None:
         from . import ops
-        from .ops import mark_hodge, set_row_order, set_tiles, set_valid
+        from .ops import mark_hodge, set_halo, set_row_order, set_tiles, set_valid
         for k, ok in (getattr(self, "hodge_sorted", None) or {}).items():
             t = getattr(self, k, None)
             if ok and torch.is_tensor(t) and t.is_cuda:
@@ -105,6 +105,11 @@ class Batch(PairData):
                 set_tiles(t, tp, TILE_ROWS, TILE_NNZ)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(nv):
                 set_valid(t, nv)
+            side = k[-1]
+            hk = [getattr(self, h + "_" + side, None) for h in _HALO_KEYS]
+            if (torch.is_tensor(t) and t.is_cuda and all(torch.is_tensor(v) for v in hk)
+                    and self.hodge_sorted.get(k, False)):
+                set_halo(t, *hk, HALO_MAX)
         ei = getattr(self, "edge_index", None)
         if torch.is_tensor(ei) and ei.is_cuda:
             for kv in ("n_valid_t", "n_valid_s"):
@@ -169,6 +174,69 @@ def locality_order(edge_index, n: int) -> torch.Tensor:
     return torch.from_numpy(reverse_cuthill_mckee(A, symmetric_mode=True).astype(np.int64))
 
 
+HALO_MAX = 256        # distinct neighbour rows per halo tile (64 KB LDS image at 64 floats)
+HALO_ROWS = 128       # rows per halo tile
+_HALO_KEYS = ("halo_tile_ptr", "halo_ptr", "halo", "halo_lcol")
+
+
+def halo_tiles(edge_index, n: int, order=None, max_rows: int = HALO_ROWS,
+               max_halo: int = HALO_MAX) -> Optional[Dict[str, torch.Tensor]]:
+    """Halo tiles of a sorted symmetric Laplacian COO (the CSR the device path
+    builds from it: rows = edge_index[0], entries in COO order) for the
+    LDS-staged SpMM, visiting rows in `order` (e.g. locality_order).  Host
+    side, once per graph, like the row schedule; runs the library's native
+    builder (hlhgat_halo_tiles).  Returns tensors tile_ptr / halo_ptr / halo
+    (int32) and lcol (int16 holding uint16), or None if a row references more
+    than max_halo distinct columns."""
+    import ctypes as C
+    from ._lib import LIB, check
+    ei = np.asarray(edge_index)
+    nnz = ei.shape[1]
+    rowptr = np.zeros(n + 1, dtype=np.int32)
+    np.cumsum(np.bincount(ei[0], minlength=n), out=rowptr[1:])
+    col = np.ascontiguousarray(ei[1], dtype=np.int32)
+    ordr = None if order is None else np.ascontiguousarray(np.asarray(order), dtype=np.int32)
+    tile_ptr = np.zeros(n + 1, dtype=np.int32)
+    halo_ptr = np.zeros(n + 1, dtype=np.int32)
+    halo = np.zeros(max(nnz, 1), dtype=np.int32)
+    lcol = np.zeros(max(nnz, 1), dtype=np.uint16)
+    nt, nh = C.c_int64(0), C.c_int64(0)
+    vp = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    rc = LIB.hlhgat_halo_tiles(vp(rowptr), vp(col), n, n, vp(ordr), max_rows, max_halo,
+                               vp(tile_ptr), vp(halo_ptr), vp(halo), vp(lcol), C.byref(nt),
+                               C.byref(nh))
+    if rc != 0:
+        return None
+    check(rc, "halo_tiles")
+    t, h = nt.value, nh.value
+    return {"halo_tile_ptr": torch.from_numpy(tile_ptr[:t + 1].copy()),
+            "halo_ptr": torch.from_numpy(halo_ptr[:t + 1].copy()),
+            "halo": torch.from_numpy(halo[:h].copy()),
+            "halo_lcol": torch.from_numpy(lcol[:nnz].view(np.int16).copy())}
+
+
+def _collate_halo(b: "Batch", graphs: Sequence["PairData"], side: str) -> None:
+    """Concatenate per-graph halo tiles: positions and halo ids shift by the
+    graph's row offset, halo offsets by the halo entries before it; lcol is
+    tile-local and unchanged."""
+    keys = [k + "_" + side for k in _HALO_KEYS]
+    if not all(getattr(g, k, None) is not None for g in graphs for k in keys):
+        return
+    xk = "x_" + side
+    tp, hp, hc, lc = [np.zeros(1, np.int32)], [np.zeros(1, np.int32)], [], []
+    roff = hoff = 0
+    for g in graphs:
+        gtp, ghp, ghc, glc = (np.asarray(getattr(g, k)) for k in keys)
+        tp.append(gtp[1:] + roff)
+        hp.append(ghp[1:] + hoff)
+        hc.append(ghc + roff)
+        lc.append(glc)
+        roff += getattr(g, xk).size(0)
+        hoff += int(ghp[-1])
+    for k, parts in zip(keys, (tp, hp, hc, lc)):
+        setattr(b, k, torch.from_numpy(np.ascontiguousarray(np.concatenate(parts))))
+
+
 def is_sorted_symmetric(ei: np.ndarray, w: Optional[np.ndarray]) -> bool:
     """True if COO (ei, w) is sorted by (row, col) and equals its transpose."""
     if ei.shape[1] == 0:
@@ -193,6 +261,8 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     first = graphs[0]
     keys = first.keys()
     for k in keys:
+        if k.rsplit("_", 1)[0] in _HALO_KEYS:
+            continue  # _collate_halo
         vals = [getattr(g, k) for g in graphs]
         v0 = vals[0]
         if k in _INC_KEYS:
@@ -223,6 +293,8 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
             ok = all(getattr(g, "_hodge_sorted", False) for g in graphs)
         hs[k] = ok
     b.hodge_sorted = hs
+    for side in ("s", "t"):
+        _collate_halo(b, graphs, side)
     # whole-graph row tiles for the graph-local polynomial basis
     for key, xk, ek in (("tile_ptr_t", "x_t", "edge_index_t"), ("tile_ptr_s", "x_s", "edge_index_s")):
         if getattr(first, ek, None) is None:

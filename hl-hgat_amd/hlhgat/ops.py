@@ -149,6 +149,9 @@ class SparseCSR:
     tile_rows: int = 0                    # bound on the rows of any tile
     tile_nnz: int = 0                     # bound on the CSR entries of any tile
     valid: Optional[torch.Tensor] = None  # int32 [1]: rows >= valid are static-shape padding
+    # halo tiles (tile_ptr, halo_ptr, halo, lcol, max_halo) for the LDS-staged
+    # SpMM of large Laplacians (hodge_dataset.halo_tiles; hlhgat_halo_t)
+    halo: Optional[tuple] = None
 
 
 @dataclass
@@ -269,6 +272,41 @@ def set_valid(edge_index: torch.Tensor, n_valid: torch.Tensor, attr: str = "_hlh
     return edge_index
 
 
+def set_halo(edge_index: torch.Tensor, tile_ptr: torch.Tensor, halo_ptr: torch.Tensor,
+             halo: torch.Tensor, lcol: torch.Tensor, max_halo: int) -> torch.Tensor:
+    """Attach halo tiles (hodge_dataset.halo_tiles, built for this operator's
+    CSR and row schedule) to a sorted symmetric Laplacian's edge_index: its
+    SpMM / polynomial steps then stage each tile's neighbour rows in LDS
+    (k_poly_halo; bitwise the same results)."""
+    dev = edge_index.device
+    edge_index._hlhgat_halo = (  # type: ignore[attr-defined]
+        tile_ptr.to(dev, torch.int32).contiguous(), halo_ptr.to(dev, torch.int32).contiguous(),
+        halo.to(dev, torch.int32).contiguous(), lcol.to(dev, torch.int16).contiguous(),
+        int(max_halo))
+    return edge_index
+
+
+_HALO_ENABLED = os.environ.get("HLHGAT_HALO", "1") != "0"
+
+
+def _halo_desc(A: "SparseCSR"):
+    """ctypes pointer to an hlhgat_halo_t for A, or None."""
+    if A.halo is None or not _HALO_ENABLED:
+        return None
+    tp, hp, hc, lc, mh = A.halo
+    d = _lib.HaloDesc(tp.data_ptr(), hp.data_ptr(), hc.data_ptr(), lc.data_ptr(),
+                      tp.numel() - 1, mh)
+    return C.pointer(d)
+
+
+def _halo_args(A: "SparseCSR"):
+    """The (tile_ptr, halo_ptr, halo, lcol, max_halo) arguments of the C++
+    conv node (Nones when A has no halo tiles)."""
+    if A.halo is None or not _HALO_ENABLED:
+        return (None, None, None, None, 0)
+    return A.halo
+
+
 def _csr_sorted(row: torch.Tensor, col: torch.Tensor, w: Optional[torch.Tensor],
                 n_rows: int, n_cols: int) -> SparseCSR:
     nnz = row.numel()
@@ -331,6 +369,11 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
         a = _csr_sorted(ei[0], ei[1], w, n, n)
         a.order, a.tiles, a.tile_rows, a.tile_nnz = order, tiles, tile_rows, tile_nnz
         a.valid = valid
+        halo = getattr(edge_index, "_hlhgat_halo", None)
+        if halo is not None:  # built for the COO order = this CSR's entry order
+            if halo[3].numel() != a.nnz:
+                raise RuntimeError("hlhgat: halo tiles were built for a different operator")
+            a.halo = halo
         op = HodgeOperator(a, a)
     else:
         fwd = _csr_general(ei[1], ei[0], w, n, n)
@@ -370,7 +413,7 @@ def _poly_step(A: SparseCSR, X: torch.Tensor, Y: torch.Tensor, *, rs=None, Z=Non
     d = X.size(1)
     check(LIB.hlhgat_poly_step(
         A.rowptr.data_ptr(), A.col.data_ptr() if A.nnz else None, _ptr(A.val) if A.nnz else None,
-        _ptr(rs), A.n_rows, A.nnz, _ptr(A.order), X.data_ptr(), _ld(X), d,
+        _ptr(rs), A.n_rows, A.nnz, _ptr(A.order), _halo_desc(A), X.data_ptr(), _ld(X), d,
         _ptr(Z), _ld(Z) if Z is not None else 0, _ptr(P), _ld(P) if P is not None else 0,
         _ptr(Q), _ld(Q) if Q is not None else 0, alpha, beta, gamma, div, p, q,
         Y.data_ptr(), _ld(Y), _stream(X)), "poly_step")
@@ -384,7 +427,8 @@ def spmm(A: SparseCSR, X: torch.Tensor) -> torch.Tensor:
     if A.n_rows:
         check(LIB.hlhgat_spmm(A.rowptr.data_ptr(), A.col.data_ptr() if A.nnz else None,
                               _ptr(A.val) if A.nnz else None, A.n_rows, A.nnz,
-                              _ptr(A.order), X.data_ptr(), _ld(X), X.size(1), Y.data_ptr(),
+                              _ptr(A.order), _halo_desc(A), X.data_ptr(), _ld(X), X.size(1),
+                              Y.data_ptr(),
                               _ld(Y),
                               _stream(X)), "spmm")
     return Y
@@ -399,7 +443,7 @@ def poly_basis(op: HodgeOperator, X: torch.Tensor, K: int, kind: int) -> torch.T
         check(LIB.hlhgat_poly_basis_fwd(kind, A.rowptr.data_ptr(),
                                         A.col.data_ptr() if A.nnz else None,
                                         _ptr(A.val) if A.nnz else None, n, A.nnz,
-                                        _ptr(A.order), _ptr(A.tiles),
+                                        _ptr(A.order), _halo_desc(A), _ptr(A.tiles),
                                         A.tiles.numel() - 1 if A.tiles is not None else 0,
                                         A.tile_rows, A.tile_nnz, X.data_ptr(), _ld(X), F, K,
                                         T.data_ptr(),
@@ -483,11 +527,11 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
                             ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order,
-                            A.tiles, A.tile_rows, A.tile_nnz, A.valid)
+                            A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A))
     sink = out if (bn is None and not relu and x.dim() == 2) else None
     y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
                      bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order,
-                     A.tiles, A.tile_rows, A.tile_nnz, A.valid)
+                     A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A))
     if bn is not None:
         y = batch_norm_act(y, bn, relu, valid=A.valid)
     elif relu:

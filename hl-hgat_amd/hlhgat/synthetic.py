@@ -14,7 +14,8 @@ from typing import List
 import numpy as np
 import torch
 
-from .hodge_dataset import PairData, collate, dense_to_sparse, hodge_laplacians, locality_order
+from .hodge_dataset import (PairData, collate, dense_to_sparse, halo_tiles, hodge_laplacians,
+                            locality_order)
 
 __all__ = ["zinc_like_graph", "zinc_like_batch", "molecule_edges"]
 
@@ -108,7 +109,8 @@ def zinc_like_graph(seed: int, keig: int = 15) -> PairData:
     return g
 
 
-def tsp_like_graph(seed: int, n: int = 10000, k: int = 9, row_order: bool = True) -> PairData:
+def tsp_like_graph(seed: int, n: int = 10000, k: int = 9, row_order: bool = True,
+                   halo: bool = True) -> PairData:
     """TSP-like simplex graph (BASELINE config 5): n uniform points in [0,1]^2,
     symmetric k-NN edges (i<j), L0 = 2 B1 B1^T / lmax and L1 = 2 B1^T B1 / lmax
     built SPARSE (a dense E x E L1 would be ~10 GB at n = 10k), lmax of L0 by
@@ -151,6 +153,11 @@ def tsp_like_graph(seed: int, n: int = 10000, k: int = 9, row_order: bool = True
     if row_order:  # L2-locality schedules of the two Laplacians (SpMM row order)
         g.row_order_s = locality_order(eis.numpy(), E)
         g.row_order_t = locality_order(eit.numpy(), n)
+        if halo:  # LDS halo tiles along those schedules (k_poly_halo)
+            for side, eix, rows, o in (("s", eis, E, g.row_order_s), ("t", eit, n, g.row_order_t)):
+                ht = halo_tiles(eix.numpy(), rows, o.numpy())
+                for key, val in (ht or {}).items():
+                    setattr(g, key + "_" + side, val)
     g.edge_index = torch.from_numpy(ei)
     g.num_node1 = n
     g.num_edge1 = E

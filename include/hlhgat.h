@@ -105,7 +105,40 @@ int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
                          int64_t n_nodes, int32_t* rowptr, int32_t* edge_ids,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- halo tiles (LDS-staged SpMM for large Laplacians) ----------------- */
+/* A tiling of a CSR operator's rows for the LDS-staged SpMM: tile t owns the
+ * rows order[tile_ptr[t] .. tile_ptr[t+1]) (order = the operator's row
+ * schedule, NULL = natural) and the distinct columns its rows reference,
+ * halo[halo_ptr[t] .. halo_ptr[t+1]) (<= max_halo of them).  lcol[e] is the
+ * position of col[e] inside its row's tile halo.  One workgroup stages the
+ * tile's halo rows of X in LDS once and gathers every entry from there, so
+ * each X row is read from L2 once per tile instead of once per entry
+ * (TSP-scale L1: ~20 entries per row, ~5 uses per staged row).  Results are
+ * bitwise those of the plain SpMM (same per-row summation order).  Built on
+ * the HOST by hlhgat_halo_tiles, uploaded by the caller. */
+typedef struct hlhgat_halo {
+  const int32_t* tile_ptr;  /* [n_tiles+1] positions in the row schedule */
+  const int32_t* halo_ptr;  /* [n_tiles+1] offsets into halo */
+  const int32_t* halo;      /* distinct columns of each tile, ascending */
+  const uint16_t* lcol;     /* [nnz] tile-local column of each CSR entry */
+  int64_t n_tiles;
+  int32_t max_halo;         /* bound on any tile's halo (sizes the LDS image) */
+} hlhgat_halo_t;
+
+/* HOST function (host pointers, no stream): pack consecutive rows of the
+ * schedule greedily into tiles of <= max_rows rows and <= max_halo distinct
+ * columns.  Capacities: tile_ptr and halo_ptr n_rows+1, halo nnz, lcol nnz.
+ * Returns HLHGAT_EINVAL if one row alone references more than max_halo
+ * distinct columns (use the plain SpMM then). */
+int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                      int64_t n_cols, const int32_t* order, int32_t max_rows,
+                      int32_t max_halo, int32_t* tile_ptr, int32_t* halo_ptr,
+                      int32_t* halo, uint16_t* lcol, int64_t* n_tiles,
+                      int64_t* n_halo);
+
 /* ---- SpMM and fused polynomial step ----------------------------------- */
+/* `halo` (optional, below) selects the LDS-staged kernel: see hlhgat_halo_t.
+ * It must describe this operator with this row_order; NULL = plain kernel. */
 /* Y = A·X (PyG propagate with aggr='add', source_to_target, when A is the
  * CSR keyed by edge_index[1]).  X,Y [n][d] with row strides ldx, ldy.
  * row_order (optional, int32[n_rows], a permutation) is the order in which
@@ -114,8 +147,8 @@ int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
  * rows share an XCD's L2 at a time changes.  NULL = natural order. */
 int hlhgat_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
                 int64_t n_rows, int64_t nnz, const int32_t* row_order,
-                const float* X, int64_t ldx, int64_t d, float* Y, int64_t ldy,
-                void* stream);
+                const hlhgat_halo_t* halo, const float* X, int64_t ldx,
+                int64_t d, float* Y, int64_t ldy, void* stream);
 
 /* Generic fused step (one launch):
  *   Y = (alpha * rs[r] * (A·X)[r] + beta*X[r] + gamma*Z[r]) / div
@@ -125,7 +158,8 @@ int hlhgat_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
  * beta != 0; otherwise X may have any row count >= max(col)+1. */
 int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
                      const float* val, const float* rs, int64_t n_rows,
-                     int64_t nnz, const int32_t* row_order, const float* X,
+                     int64_t nnz, const int32_t* row_order,
+                     const hlhgat_halo_t* halo, const float* X,
                      int64_t ldx, int64_t d,
                      const float* Z, int64_t ldz, const float* P, int64_t ldp,
                      const float* Q, int64_t ldq, float alpha, float beta,
@@ -151,7 +185,8 @@ int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
  * separate launches. */
 int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
                           const float* val, int64_t n, int64_t nnz,
-                          const int32_t* row_order, const int32_t* tile_ptr,
+                          const int32_t* row_order, const hlhgat_halo_t* halo,
+                          const int32_t* tile_ptr,
                           int64_t n_tiles, int64_t max_tile_rows, int64_t max_tile_nnz,
                           const float* X, int64_t ldx, int64_t F, int K, float* T,
                           void* stream);
@@ -164,6 +199,7 @@ int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
 int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                           const int32_t* col_t, const float* val_t, int64_t n,
                           int64_t nnz, const int32_t* row_order,
+                          const hlhgat_halo_t* halo,
                           const int32_t* tile_ptr, int64_t n_tiles,
                           int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F,
                           int K, float* G, void* stream);

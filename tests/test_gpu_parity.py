@@ -628,3 +628,72 @@ def test_graph_local_basis_bitwise_equals_steps(cuda, kind, K, side, nnz_bound):
         conv.zero_grad()
     for a, c in zip(*res):
         assert torch.equal(a, c)
+
+
+# ---------------------------------------------------------------------------
+# LDS-staged halo-tile SpMM (k_poly_halo) == plain SpMM, bitwise
+# ---------------------------------------------------------------------------
+def _halo_ops(g, side, max_rows, max_halo):
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import halo_tiles
+    ei, w = getattr(g, "edge_index_" + side), getattr(g, "edge_weight_" + side)
+    n = getattr(g, "x_" + side).shape[0]
+    order = getattr(g, "row_order_" + side)
+    plain = ops.hodge_operator(ops.set_row_order(ops.mark_hodge(dev(ei)), order), dev(w), n)
+    ht = halo_tiles(ei.numpy(), n, order.numpy(), max_rows=max_rows, max_halo=max_halo)
+    ei_h = ops.set_row_order(ops.mark_hodge(dev(ei)), order)
+    ops.set_halo(ei_h, ht["halo_tile_ptr"], ht["halo_ptr"], ht["halo"], ht["halo_lcol"], max_halo)
+    halo = ops.hodge_operator(ei_h, dev(w), n)
+    assert halo.fwd.halo is not None and plain.fwd.halo is None
+    return ei, w, n, plain, halo, ei_h
+
+
+@pytest.mark.parametrize("d", [1, 6, 32, 64, 128, 200])
+@pytest.mark.parametrize("tiles", [(128, 256), (7, 48)])
+def test_halo_spmm_bitwise_equals_plain(cuda, d, tiles):
+    from hlhgat import ops
+    from hlhgat.synthetic import tsp_like_graph
+    g = tsp_like_graph(6, n=1200, k=7, halo=False)
+    for side in ("s", "t"):
+        ei, w, n, plain, halo, _ = _halo_ops(g, side, *tiles)
+        x = torch.randn(n, d, generator=torch.Generator().manual_seed(d))
+        y0 = ops.spmm(plain.fwd, dev(x))
+        y1 = ops.spmm(halo.fwd, dev(x))
+        assert torch.equal(y0, y1), (side, d, (y0 - y1).abs().max())
+        assert torch.equal(y1.cpu(), R.propagate(x, ei, w))
+        for kind in (ops.POLY_LAGUERRE, ops.POLY_CHEB, ops.POLY_LAGUERRE_DEMO):
+            assert torch.equal(ops.poly_basis(plain, dev(x), 4, kind),
+                               ops.poly_basis(halo, dev(x), 4, kind))
+
+
+def test_halo_conv_fwd_bwd_bitwise(cuda):
+    """HodgeLaguerreConv (+BN+ReLU node) forward and adjoint over halo tiles
+    equal the plain path bitwise; batch of two TSP-like graphs via collate."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph
+    b = collate([tsp_like_graph(7, n=900, k=7), tsp_like_graph(8, n=700, k=7)],
+                check_hodge=False)
+    n = b.x_s.shape[0]
+    torch.manual_seed(0)
+    conv = hlhgat.HodgeLaguerreConv(64, 64, K=4).to(cuda)
+    bn = torch.nn.BatchNorm1d(64).to(cuda)
+    x = torch.randn(n, 64, device=cuda)
+    outs = []
+    for use_halo in (False, True):
+        bd = collate([tsp_like_graph(7, n=900, k=7), tsp_like_graph(8, n=700, k=7)],
+                     check_hodge=False).to(cuda)
+        if use_halo:
+            assert getattr(bd.edge_index_s, "_hlhgat_halo", None) is not None
+        else:
+            bd.edge_index_s._hlhgat_halo = None
+        op = ops.hodge_operator(bd.edge_index_s, bd.edge_weight_s, n)
+        assert (op.fwd.halo is not None) == use_halo
+        xx = x.clone().requires_grad_(True)
+        y = conv.forward_bn(xx, bd.edge_index_s, bd.edge_weight_s, bn, relu=True)
+        (y * y).sum().backward()
+        outs.append((y.detach(), xx.grad.clone(), conv.lins[3].weight.grad.clone()))
+        conv.zero_grad()
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)

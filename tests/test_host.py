@@ -234,3 +234,44 @@ def test_fastconv_adj_t_forms_agree():
         assert torch.equal(got, dense_t)
     assert HodgeLaguerreFastConv(4, 4, K=3)._kind != HodgeLaguerreFastConv(
         4, 4, K=3, demo_recurrence=False)._kind
+
+
+def _check_halo(ei, n, order, ht, max_rows, max_halo):
+    tp, hp = ht["halo_tile_ptr"].numpy(), ht["halo_ptr"].numpy()
+    hc, lc = ht["halo"].numpy(), ht["halo_lcol"].numpy().view(np.uint16)
+    assert tp[0] == 0 and tp[-1] == n and np.all(np.diff(tp) > 0)
+    assert np.all(np.diff(tp) <= max_rows) and np.all(np.diff(hp) <= max_halo)
+    rowptr = np.concatenate([[0], np.cumsum(np.bincount(ei[0], minlength=n))])
+    sched = np.arange(n) if order is None else np.asarray(order)
+    for t in range(len(tp) - 1):
+        halo = hc[hp[t]:hp[t + 1]]
+        assert np.all(np.diff(halo) > 0)  # ascending, distinct
+        for r in sched[tp[t]:tp[t + 1]]:
+            e = np.arange(rowptr[r], rowptr[r + 1])
+            assert np.array_equal(halo[lc[e]], ei[1][e])
+
+
+def test_halo_tiles_invariants():
+    """hlhgat_halo_tiles (native host builder): tiles partition the row
+    schedule, each halo holds exactly its rows' distinct columns (sorted),
+    lcol points every CSR entry at its column inside the halo."""
+    from hlhgat.hodge_dataset import halo_tiles, locality_order
+    from hlhgat.synthetic import tsp_like_graph
+    g = tsp_like_graph(3, n=600, k=6, halo=False)
+    for ei, n, order in ((g.edge_index_s.numpy(), g.x_s.shape[0], g.row_order_s.numpy()),
+                         (g.edge_index_t.numpy(), g.x_t.shape[0], None)):
+        for max_rows, max_halo in ((128, 256), (16, 64), (3, 40)):
+            ht = halo_tiles(ei, n, order, max_rows=max_rows, max_halo=max_halo)
+            _check_halo(ei, n, order, ht, max_rows, max_halo)
+    assert locality_order(g.edge_index_s.numpy(), g.x_s.shape[0]).numel() == g.x_s.shape[0]
+
+
+def test_halo_tiles_reject_and_collate():
+    from hlhgat.hodge_dataset import collate, halo_tiles
+    from hlhgat.synthetic import tsp_like_graph
+    g = tsp_like_graph(4, n=400, k=6)
+    ei = g.edge_index_s.numpy()
+    assert halo_tiles(ei, g.x_s.shape[0], None, max_halo=3) is None  # a row has > 3 columns
+    b = collate([g, tsp_like_graph(5, n=300, k=6)], check_hodge=False)
+    ht = {k: getattr(b, k + "_s") for k in ("halo_tile_ptr", "halo_ptr", "halo", "halo_lcol")}
+    _check_halo(b.edge_index_s.numpy(), b.x_s.shape[0], b.row_order_s.numpy(), ht, 128, 256)
