@@ -295,39 +295,46 @@ extern "C" int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
 // Halo tiles for the LDS-staged SpMM (host side, run once per graph at
 // dataset-build time like the row schedule; see hlhgat_halo_t).
 // Greedy over the row schedule: a row joins the current tile unless that
-// would push the tile past max_rows rows or max_halo distinct columns.
+// would push the tile past max_rows rows, max_nnz entries or max_halo
+// distinct columns.
 // ---------------------------------------------------------------------------
 #include <algorithm>
 #include <vector>
 
 extern "C" int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
                                  int64_t n_cols, const int32_t* order, int32_t max_rows,
-                                 int32_t max_halo, int32_t* tile_ptr, int32_t* halo_ptr,
-                                 int32_t* halo, uint16_t* lcol, int64_t* n_tiles,
+                                 int32_t max_nnz, int32_t max_halo, int32_t* tile_ptr,
+                                 int32_t* halo_ptr, int32_t* halo, int32_t* srp, uint16_t* lcol,
+                                 int32_t* eperm, int32_t* hdr, int64_t* n_tiles,
                                  int64_t* n_halo) {
   HLH_CHECK_ARG(n_rows >= 0 && n_cols >= 0 && n_rows < INT32_MAX && n_cols < INT32_MAX,
                 "halo_tiles: bad sizes");
-  HLH_CHECK_ARG(max_rows > 0 && max_halo > 0 && max_halo <= 65535,
-                "halo_tiles: max_rows > 0 and 0 < max_halo <= 65535 required");
-  HLH_CHECK_ARG(rowptr && tile_ptr && halo_ptr && n_tiles && n_halo, "halo_tiles: NULL pointer");
+  HLH_CHECK_ARG(max_rows > 0 && max_nnz > 0 && max_halo > 0 && max_halo <= 65535,
+                "halo_tiles: max_rows, max_nnz > 0 and 0 < max_halo <= 65535 required");
+  HLH_CHECK_ARG(rowptr && tile_ptr && halo_ptr && srp && hdr && n_tiles && n_halo,
+                "halo_tiles: NULL pointer");
   const int64_t nnz = n_rows ? rowptr[n_rows] : 0;
-  HLH_CHECK_ARG(nnz == 0 || (col && halo && lcol), "halo_tiles: NULL pointer");
+  HLH_CHECK_ARG(nnz == 0 || (col && halo && lcol && eperm), "halo_tiles: NULL pointer");
   // owner[c] = tile that holds column c in its halo; probe[c] = last probe
   std::vector<int64_t> owner((size_t)n_cols, -1), probe((size_t)n_cols, -1);
   std::vector<int32_t> cols;  // current tile's halo, insertion order
   cols.reserve((size_t)max_halo);
-  int64_t t = 0, h = 0, p0 = 0, probes = 0;
+  int64_t t = 0, h = 0, p0 = 0, probes = 0, tile_nnz = 0;
   tile_ptr[0] = 0;
   halo_ptr[0] = 0;
+  srp[0] = 0;
   auto row_at = [&](int64_t p) -> int64_t { return order ? (int64_t)order[p] : p; };
   auto close_tile = [&](int64_t p_end) {
-    // halo ascending; lcol of every entry of the tile's rows
+    // halo ascending; tile-local column of every entry of the tile's rows
     std::sort(cols.begin(), cols.end());
     for (size_t i = 0; i < cols.size(); ++i) halo[h + (int64_t)i] = cols[i];
     for (int64_t p = p0; p < p_end; ++p) {
       const int64_t r = row_at(p);
-      for (int32_t e = rowptr[r]; e < rowptr[r + 1]; ++e)
-        lcol[e] = (uint16_t)(std::lower_bound(cols.begin(), cols.end(), col[e]) - cols.begin());
+      int64_t i = srp[p];
+      for (int32_t e = rowptr[r]; e < rowptr[r + 1]; ++e, ++i) {
+        lcol[i] = (uint16_t)(std::lower_bound(cols.begin(), cols.end(), col[e]) - cols.begin());
+        eperm[i] = e;
+      }
     }
     h += (int64_t)cols.size();
     ++t;
@@ -335,10 +342,12 @@ extern "C" int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int6
     halo_ptr[t] = (int32_t)h;
     cols.clear();
     p0 = p_end;
+    tile_nnz = 0;
   };
   for (int64_t p = 0; p < n_rows; ++p) {
     const int64_t r = row_at(p);
     HLH_CHECK_ARG(r >= 0 && r < n_rows, "halo_tiles: order[%lld] out of range", (long long)p);
+    const int64_t len = rowptr[r + 1] - rowptr[r];
     for (int pass = 0; pass < 2; ++pass) {
       // distinct columns this row would add to the current tile
       const int64_t id = probes++;
@@ -351,7 +360,8 @@ extern "C" int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int6
           ++add;
         }
       }
-      if ((int64_t)cols.size() + add <= max_halo && p - p0 < max_rows) {
+      if ((int64_t)cols.size() + add <= max_halo && p - p0 < max_rows &&
+          tile_nnz + len <= max_nnz) {
         for (int32_t e = rowptr[r]; e < rowptr[r + 1]; ++e) {
           const int32_t c = col[e];
           if (owner[c] != t) {
@@ -359,16 +369,46 @@ extern "C" int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int6
             cols.push_back(c);
           }
         }
+        tile_nnz += len;
+        srp[p + 1] = (int32_t)(srp[p] + len);
         break;
       }
       HLH_CHECK_ARG(p > p0 && pass == 0,
-                    "halo_tiles: row %lld references more than max_halo=%d columns",
-                    (long long)r, max_halo);
+                    "halo_tiles: row %lld exceeds max_halo=%d columns or max_nnz=%d entries",
+                    (long long)r, max_halo, max_nnz);
       close_tile(p);
     }
   }
   if (p0 < n_rows) close_tile(n_rows);
+  for (int64_t i = 0; i < t; ++i) {  // one 32-B header per tile (a single load in the kernel)
+    int32_t* q = hdr + 8 * i;
+    q[0] = tile_ptr[i];
+    q[1] = tile_ptr[i + 1] - tile_ptr[i];
+    q[2] = halo_ptr[i];
+    q[3] = halo_ptr[i + 1] - halo_ptr[i];
+    q[4] = srp[tile_ptr[i]];
+    q[5] = srp[tile_ptr[i + 1]] - srp[tile_ptr[i]];
+    q[6] = q[7] = 0;
+  }
   *n_tiles = t;
   *n_halo = h;
+  return HLHGAT_OK;
+}
+
+namespace {
+__global__ void k_gather_f32(const float* __restrict__ src, const int32_t* __restrict__ idx,
+                             int64_t n, float* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
+}
+}  // namespace
+
+extern "C" int hlhgat_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst,
+                                 void* stream) {
+  HLH_CHECK_ARG(n >= 0, "gather_f32: n < 0");
+  if (n == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(src && idx && dst, "gather_f32: NULL pointer");
+  k_gather_f32<<<grid_for(n), kThreads, 0, as_stream(stream)>>>(src, idx, n, dst);
+  HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

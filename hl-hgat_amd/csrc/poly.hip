@@ -13,6 +13,8 @@
 // CPU restatement in oracle/ (tests check this).
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace hlhgat;
 
 namespace {
@@ -34,12 +36,16 @@ struct PolyArgs {
   int d;
   float alpha, beta, gamma, div, p, q;
   // halo tiles (optional; lcol != NULL selects k_poly_halo, see hlhgat_halo_t)
+  const int32_t* hdr;
   const int32_t* htile;
   const int32_t* hptr;
   const int32_t* hcols;
+  const int32_t* srp;
   const uint16_t* lcol;
+  const float* sval;
   int64_t n_tiles;
-  int max_halo;
+  int max_halo, max_trows, max_tnnz, halo_fs;
+  int nt_store;  // streaming (non-temporal) stores of Y: keep L2 for the gathered X rows
 };
 
 // Row r's CSR entries are staged LPR at a time: lane `sub` of the row group
@@ -88,7 +94,12 @@ __device__ __forceinline__ void poly_epilogue(const PolyArgs& a, int64_t row, in
 #pragma unroll
     for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.q * vget(qv, i);
   }
-  vstore<V>(a.Y + row * a.ldy + f, out);
+  if (a.nt_store) {
+    float* yp = a.Y + row * a.ldy + f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) __builtin_nontemporal_store(vget(out, i), yp + i);
+  } else
+    vstore<V>(a.Y + row * a.ldy + f, out);
 }
 
 template <int V, int LPR>
@@ -163,95 +174,107 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
 // rate: every entry re-reads a 256-512 B feature row from L2.  Here one
 // workgroup owns a halo tile (hlhgat_halo_tiles: a run of the row schedule
 // whose rows reference <= max_halo distinct columns, ~5 uses per staged row in
-// RCM order): it stages those X rows -- one FS-float feature slice at a time
-// -- in LDS with coalesced row loads, then every row group walks its rows'
-// entries in CSR order gathering from LDS (ds_read_b128, 256-B pitch:
-// conflict-free).  Same per-row summation order and epilogue as k_poly_step,
-// so the results are bitwise equal.  Tiles are dealt XCD-contiguously
-// (xcd_slot) so neighbouring tiles -- which share much of their halo -- hit
-// the same L2.
+// RCM order).  Prologue: the tile's entries (tile-local column, value; laid
+// out in schedule order, so one contiguous range) and row offsets go to LDS
+// with bulk coalesced loads.  Then per FS-float feature slice: the halo rows
+// of X are staged in LDS (every load of the slice in flight at once), and
+// each row group sums its rows' entries from LDS in CSR order.  Same per-row
+// summation and epilogue as k_poly_step: bitwise equal results.  Tiles are
+// dealt XCD-contiguously (xcd_slot): neighbouring tiles share much of their
+// halo and hit the same L2.
 // ---------------------------------------------------------------------------
-template <int V, int LPR>
-__global__ __launch_bounds__(256) void k_poly_halo(PolyArgs a) {
+constexpr int kHaloIds = 8;  // halo row ids held per lane (max_halo <= 8 * row groups)
+
+template <int V, int LPR, int NT>
+__global__ __launch_bounds__(NT) void k_poly_halo(PolyArgs a) {
   using vt = typename VecT<V>::type;
-  constexpr int FS = V * LPR;   // features per staged slice
-  constexpr int RG = 256 / LPR; // row groups per workgroup
+  constexpr int FS = V * LPR;    // features per staged slice
+  constexpr int RG = NT / LPR;   // row groups per workgroup
+  constexpr int kHaloThreads = NT;
   extern __shared__ float4 halo_lds[];
-  float* img = reinterpret_cast<float*>(halo_lds);
+  float* img = reinterpret_cast<float*>(halo_lds);            // [max_halo][FS]
+  int2* ent = reinterpret_cast<int2*>(img + (int64_t)a.max_halo * FS);  // [max_tnnz] {col, w}
+  int* rp = reinterpret_cast<int*>(ent + a.max_tnnz);         // [max_trows + 1]
   const int64_t t = xcd_slot(blockIdx.x, gridDim.x);
   if (t >= a.n_tiles) return;  // whole workgroup: uniform
-  const int p0 = a.htile[t], p1 = a.htile[t + 1];
-  const int hb = a.hptr[t], nh = a.hptr[t + 1] - hb;
+  const int4 h0 = reinterpret_cast<const int4*>(a.hdr)[2 * t];
+  const int2 h1 = reinterpret_cast<const int2*>(a.hdr)[4 * t + 2];
+  const int p0 = h0.x, nr = h0.y, hb = h0.z, nh = h0.w, e_lo = h1.x, ne = h1.y;
   const int sub = threadIdx.x % LPR, rg = threadIdx.x / LPR;
+  // prologue, one burst: entries + row offsets to LDS, this lane's halo ids
+  // to registers (reused by every feature slice)
+  int hid[kHaloIds];
+#pragma unroll
+  for (int u = 0; u < kHaloIds; ++u) {
+    const int hh = rg + u * RG;
+    hid[u] = hh < nh ? a.hcols[hb + hh] : 0;
+  }
+  for (int i = threadIdx.x; i < ne; i += kHaloThreads)
+    ent[i] = make_int2((int)a.lcol[e_lo + i], __float_as_int(a.sval ? a.sval[e_lo + i] : 1.f));
+  for (int r = threadIdx.x; r <= nr; r += kHaloThreads) rp[r] = a.srp[p0 + r] - e_lo;
+  // this row group's first row id (epilogue), loaded with the prologue burst
+  const int64_t row_first =
+      rg < nr ? (a.order ? (int64_t)a.order[p0 + rg] : (int64_t)(p0 + rg)) : 0;
   const float* __restrict__ X = a.X;
   for (int f0 = 0; f0 < a.d; f0 += FS) {
     const int f = f0 + sub * V;
     const bool fok = f < a.d;
     if (f0) __syncthreads();  // the previous slice's readers are done
-    for (int h = rg; h < nh; h += 4 * RG) {  // four row loads in flight per lane
-      vt v[4];
+    {
+      vt v[kHaloIds];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int hh = h + u * RG;
+      for (int u = 0; u < kHaloIds; ++u) {
+        const int hh = rg + u * RG;
         if (hh < nh && fok) {
-          v[u] = vload<V>(X + (int64_t)a.hcols[hb + hh] * a.ldx + f);
+          v[u] = vload<V>(X + (int64_t)hid[u] * a.ldx + f);
         } else {
 #pragma unroll
           for (int i = 0; i < V; ++i) vget(v[u], i) = 0.f;
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int hh = h + u * RG;
+      for (int u = 0; u < kHaloIds; ++u) {
+        const int hh = rg + u * RG;
         if (hh < nh) vstore<V>(img + hh * FS + sub * V, v[u]);
       }
     }
     __syncthreads();
-    for (int p = p0 + rg; p < p1; p += RG) {
-      const int64_t row = a.order ? (int64_t)a.order[p] : (int64_t)p;
-      const int e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
-      const float rsv = a.rs ? a.rs[row] : 1.f;
+    if (!fok) continue;
+    for (int r = rg; r < nr; r += RG) {
+      const int e0 = rp[r], e1 = rp[r + 1];
       vt acc;
 #pragma unroll
       for (int i = 0; i < V; ++i) vget(acc, i) = 0.f;
-      for (int eb = e0; eb < e1; eb += LPR) {
-        const int me = eb + sub;
-        const int cm = me < e1 ? (int)a.lcol[me] : 0;
-        const float wm = me < e1 ? (a.val ? a.val[me] : 1.f) : 0.f;
-        const int cnt = e1 - eb < LPR ? e1 - eb : LPR;
-        int j = 0;
-        for (; j + 3 < cnt; j += 4) {
-          const int c0 = __shfl(cm, j, LPR), c1 = __shfl(cm, j + 1, LPR),
-                    c2 = __shfl(cm, j + 2, LPR), c3 = __shfl(cm, j + 3, LPR);
-          const float w0 = __shfl(wm, j, LPR), w1 = __shfl(wm, j + 1, LPR),
-                      w2 = __shfl(wm, j + 2, LPR), w3 = __shfl(wm, j + 3, LPR);
-          if (fok) {
-            vt x0 = vload<V>(img + c0 * FS + sub * V);
-            vt x1 = vload<V>(img + c1 * FS + sub * V);
-            vt x2 = vload<V>(img + c2 * FS + sub * V);
-            vt x3 = vload<V>(img + c3 * FS + sub * V);
+      int e = e0;
+      for (; e + 3 < e1; e += 4) {
+        const int2 q0 = ent[e], q1 = ent[e + 1], q2 = ent[e + 2], q3 = ent[e + 3];
+        const int c0 = q0.x, c1 = q1.x, c2 = q2.x, c3 = q3.x;
+        const float w0 = __int_as_float(q0.y), w1 = __int_as_float(q1.y),
+                    w2 = __int_as_float(q2.y), w3 = __int_as_float(q3.y);
+        vt x0 = vload<V>(img + c0 * FS + sub * V);
+        vt x1 = vload<V>(img + c1 * FS + sub * V);
+        vt x2 = vload<V>(img + c2 * FS + sub * V);
+        vt x3 = vload<V>(img + c3 * FS + sub * V);
 #pragma unroll
-            for (int i = 0; i < V; ++i) {
-              float s = vget(acc, i);
-              s = s + w0 * vget(x0, i);
-              s = s + w1 * vget(x1, i);
-              s = s + w2 * vget(x2, i);
-              s = s + w3 * vget(x3, i);
-              vget(acc, i) = s;
-            }
-          }
-        }
-        for (; j < cnt; ++j) {
-          const int c = __shfl(cm, j, LPR);
-          const float w = __shfl(wm, j, LPR);
-          if (fok) {
-            vt x = vload<V>(img + c * FS + sub * V);
-#pragma unroll
-            for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
-          }
+        for (int i = 0; i < V; ++i) {
+          float s = vget(acc, i);
+          s = s + w0 * vget(x0, i);
+          s = s + w1 * vget(x1, i);
+          s = s + w2 * vget(x2, i);
+          s = s + w3 * vget(x3, i);
+          vget(acc, i) = s;
         }
       }
-      if (!fok) continue;
+      for (; e < e1; ++e) {
+        const int2 q = ent[e];
+        vt x = vload<V>(img + q.x * FS + sub * V);
+        const float w = __int_as_float(q.y);
+#pragma unroll
+        for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
+      }
+      const int64_t row =
+          r == rg ? row_first : (a.order ? (int64_t)a.order[p0 + r] : (int64_t)(p0 + r));
+      const float rsv = a.rs ? a.rs[row] : 1.f;
       poly_epilogue<V>(a, row, f, acc, rsv);
     }
   }
@@ -808,7 +831,11 @@ double poly_bytes(const PolyArgs& a, int64_t nnz) {
   return b + dense * row_bytes;
 }
 
-constexpr size_t kHaloLdsBytes = 64 * 1024;  // LDS image of one halo tile (2+ WGs / CU)
+// LDS of one halo-tile workgroup: the X image (<= kHaloImgBytes) plus the
+// tile's entries and row offsets; <= 64 KB keeps >= 2 workgroups per CU.
+constexpr size_t kHaloImgBytes = 32 * 1024;
+constexpr double kNtStoreBytes = 48.0 * 1024 * 1024;
+constexpr size_t kHaloLdsBytes = 64 * 1024;
 
 int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
   HLH_CHECK_ARG(a.n_rows >= 0 && a.n_rows < (int64_t)INT32_MAX,
@@ -827,16 +854,40 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
                                a.Q ? a.ldq : 4, a.B ? a.ldb : 4},
                          {a.X, a.Y, a.Z, a.P, a.Q, a.B});
   const int l = pick_lpr(a.d, v);
+  // Streaming stores of Y once Y is a sizeable fraction of the 256 MB MALL
+  // (config 5: 53-106 MB per basis term): the stores then stop evicting the
+  // gathered X rows; measured on the TSP L1 Laguerre step at d = 128: 164 ->
+  // 116 us (profiles/r01_g_tsp_spmm.log).  Small (ZINC) operators keep
+  // ordinary stores -- their consumer re-reads Y from L2 / MALL right away.
+  // HLHGAT_NT=0/1 forces either way (A/B).
+  static const int nt_env = getenv("HLHGAT_NT") ? atoi(getenv("HLHGAT_NT")) : -1;
+  a.nt_store = nt_env >= 0 ? nt_env : ((double)a.n_rows * a.d * 4.0 >= kNtStoreBytes);
   ProfScope prof(HLHGAT_PROF_POLY, s, poly_bytes(a, nnz),
                  2.0 * (double)nnz * a.d);
   if (a.lcol && a.n_tiles > 0) {
-    const int lh = l > 16 ? 16 : l;  // FS = v * lh features per staged slice
-    const size_t shmem = (size_t)a.max_halo * v * lh * sizeof(float);
-    if (shmem <= kHaloLdsBytes) {
+    // slice width FS = v * lh: the widest power of two whose halo image fits
+    // kHaloImgBytes (several workgroups per CU), capped by the row's lanes
+    int lh = l > 16 ? 16 : l;
+    while (lh > 1 && (size_t)a.max_halo * v * lh * sizeof(float) > kHaloImgBytes) lh >>= 1;
+    // small tiles: 256-thread workgroups (more of them per CU); else 1024
+    const int nt = a.max_trows * lh <= 128 ? 128 : (a.max_trows * lh <= 256 ? 256 : 1024);
+    const bool ids_fit = a.max_halo <= kHaloIds * (nt / lh) && a.max_trows * lh <= 1024 * 8;
+    const size_t img = (size_t)a.max_halo * v * lh * sizeof(float);
+    const size_t shmem = img + (size_t)a.max_tnnz * sizeof(int2) +
+                         (size_t)(a.max_trows + 1) * sizeof(int) + 16;
+    if (shmem <= kHaloLdsBytes && ids_fit) {
+      a.halo_fs = v * lh;
       const unsigned grid = (unsigned)a.n_tiles;
       switch (v * 100 + lh) {
 #define HLH_HALO_CASE(VV, LL) \
-  case VV * 100 + LL: launch(k_poly_halo<VV, LL>, grid, 256, shmem, s, &prof, a); break;
+  case VV * 100 + LL:                                                                   \
+    if (nt == 128)                                                                      \
+      launch(k_poly_halo<VV, LL, 128>, grid, 128, (uint32_t)shmem, s, &prof, a);        \
+    else if (nt == 256)                                                                 \
+      launch(k_poly_halo<VV, LL, 256>, grid, 256, (uint32_t)shmem, s, &prof, a);        \
+    else                                                                                \
+      launch(k_poly_halo<VV, LL, 1024>, grid, 1024, (uint32_t)shmem, s, &prof, a);      \
+    break;
         HLH_HALO_CASE(1, 1) HLH_HALO_CASE(1, 2) HLH_HALO_CASE(1, 4) HLH_HALO_CASE(1, 8)
         HLH_HALO_CASE(1, 16) HLH_HALO_CASE(2, 1) HLH_HALO_CASE(2, 2) HLH_HALO_CASE(2, 4)
         HLH_HALO_CASE(2, 8) HLH_HALO_CASE(2, 16) HLH_HALO_CASE(4, 1) HLH_HALO_CASE(4, 2)
@@ -859,13 +910,18 @@ PolyArgs make_args(const int32_t* rowptr, const int32_t* col, const float* val,
                    const hlhgat_halo_t* halo = nullptr) {
   PolyArgs a{};
   a.order = order;
-  if (halo && halo->lcol && halo->n_tiles > 0) {
+  if (halo && halo->lcol && halo->srp && halo->hdr && halo->n_tiles > 0) {
+    a.hdr = halo->hdr;
     a.htile = halo->tile_ptr;
     a.hptr = halo->halo_ptr;
     a.hcols = halo->halo;
+    a.srp = halo->srp;
     a.lcol = halo->lcol;
+    a.sval = halo->sval;
     a.n_tiles = halo->n_tiles;
     a.max_halo = halo->max_halo;
+    a.max_trows = halo->max_rows;
+    a.max_tnnz = halo->max_nnz;
   }
   a.rowptr = rowptr;
   a.col = col;

@@ -85,26 +85,31 @@ struct Csr {
   int64_t nnz;
 };
 
-// hlhgat_halo_t over the halo-tile tensors of an operator (see hlhgat.h)
+// hlhgat_halo_t over the halo-tile tensors of an operator (see hlhgat.h);
+// bounds = {max_halo, max_rows, max_nnz}
 hlhgat_halo_t make_halo(const Tensor& tile, const Tensor& ptr, const Tensor& cols,
-                        const Tensor& lcol, int64_t max_halo) {
+                        const Tensor& srp, const Tensor& lcol, const Tensor& sval,
+                        const std::vector<int64_t>& bounds, const Tensor& hdr) {
   hlhgat_halo_t h{};
   if (!lcol.defined()) return h;
   TORCH_CHECK(tile.scalar_type() == at::kInt && ptr.scalar_type() == at::kInt &&
-                  cols.scalar_type() == at::kInt && lcol.element_size() == 2,
-              "hlhgat: halo tiles must be int32 (tile_ptr, halo_ptr, halo) and 16-bit lcol");
+                  cols.scalar_type() == at::kInt && srp.scalar_type() == at::kInt &&
+                  lcol.element_size() == 2 && bounds.size() == 3 && hdr.defined() &&
+                  hdr.scalar_type() == at::kInt,
+              "hlhgat: halo tiles must be int32 (tile_ptr, halo_ptr, halo, srp), 16-bit lcol "
+              "and 3 bounds");
+  h.hdr = hdr.data_ptr<int>();
   h.tile_ptr = tile.data_ptr<int>();
   h.halo_ptr = ptr.data_ptr<int>();
   h.halo = cols.data_ptr<int>();
+  h.srp = srp.data_ptr<int>();
   h.lcol = reinterpret_cast<const uint16_t*>(lcol.data_ptr());
+  h.sval = sval.defined() ? sval.data_ptr<float>() : nullptr;
   h.n_tiles = tile.numel() - 1;
-  h.max_halo = (int32_t)max_halo;
+  h.max_halo = (int32_t)bounds[0];
+  h.max_rows = (int32_t)bounds[1];
+  h.max_nnz = (int32_t)bounds[2];
   return h;
-}
-hlhgat_halo_t make_halo(const OptT& tile, const OptT& ptr, const OptT& cols, const OptT& lcol,
-                        int64_t max_halo) {
-  if (!(has(tile) && has(ptr) && has(cols) && has(lcol))) return hlhgat_halo_t{};
-  return make_halo(*tile, *ptr, *cols, *lcol, max_halo);
 }
 
 // One BN workspace per (device, stream): its arrival counters must not be
@@ -263,7 +268,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
                         int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order,
                         OptT tiles, int64_t tile_rows, int64_t tile_nnz, OptT valid,
-                        OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_lcol, int64_t h_max) {
+                        OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol,
+                        OptT h_sval, std::vector<int64_t> h_bounds, OptT h_hdr) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -275,8 +281,12 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     void* s = stream_of(x);
     Tensor T = at::empty({std::max<int64_t>(K - 1, 0), N, F}, x.options());
     // halo tiles describe A; they serve the adjoint only when A^T is A
-    const bool use_halo = has(h_lcol) && has(h_tile) && has(h_ptr) && has(h_cols);
-    const hlhgat_halo_t halo = make_halo(h_tile, h_ptr, h_cols, h_lcol, h_max);
+    const bool use_halo =
+        has(h_lcol) && has(h_tile) && has(h_ptr) && has(h_cols) && has(h_srp) && has(h_hdr);
+    const hlhgat_halo_t halo =
+        use_halo ? make_halo(*h_tile, *h_ptr, *h_cols, *h_srp, *h_lcol,
+                             has(h_sval) ? *h_sval : Tensor(), h_bounds, *h_hdr)
+                 : hlhgat_halo_t{};
     if (K > 1 && N > 0) {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
@@ -352,12 +362,15 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.opt(h_tile);
       em.opt(h_ptr);
       em.opt(h_cols);
+      em.opt(h_srp);
       em.opt(h_lcol);
+      em.opt(h_sval);
       em.other();
+      em.opt(h_hdr);
       ctx->saved_data["edges"] = em.e;
       ctx->saved_data["tile_rows"] = tile_rows;
       ctx->saved_data["tile_nnz"] = tile_nnz;
-      ctx->saved_data["h_max"] = h_max;
+      ctx->saved_data["h_bounds"] = h_bounds;
     }
     const bool halo_bwd = use_halo && t_rowptr.data_ptr() == a_rowptr.data_ptr();
     ctx->saved_data["xshape"] = x.sizes().vec();
@@ -379,7 +392,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                 halo_bwd ? *h_tile : Tensor(),
                                 halo_bwd ? *h_ptr : Tensor(),
                                 halo_bwd ? *h_cols : Tensor(),
-                                halo_bwd ? *h_lcol : Tensor()};
+                                halo_bwd ? *h_srp : Tensor(),
+                                halo_bwd ? *h_lcol : Tensor(),
+                                (halo_bwd && has(h_sval)) ? *h_sval : Tensor(),
+                                halo_bwd ? *h_hdr : Tensor()};
     for (const auto& w : W) save.push_back(w);
     ctx->save_for_backward(save);
     std::vector<int64_t> oshape = x.sizes().vec();
@@ -397,11 +413,13 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     Tensor x2 = sv[0], T = sv[1], t_order = sv[2], tiles = sv[3], valid = sv[4],
            t_rowptr = sv[5], t_col = sv[6], t_val = sv[7], pre = sv[8], yout = sv[9],
            mean = sv[10], invstd = sv[11], bn_w = sv[12], bias_p = sv[13], bn_b = sv[14],
-           h_tile = sv[15], h_ptr = sv[16], h_cols = sv[17], h_lcol = sv[18];
-    std::vector<Tensor> W(sv.begin() + 19, sv.end());
+           h_tile = sv[15], h_ptr = sv[16], h_cols = sv[17], h_srp = sv[18], h_lcol = sv[19],
+           h_sval = sv[20], h_hdr = sv[21];
+    std::vector<Tensor> W(sv.begin() + 22, sv.end());
     const bool use_halo = h_lcol.defined();
     const hlhgat_halo_t halo =
-        use_halo ? make_halo(h_tile, h_ptr, h_cols, h_lcol, ctx->saved_data["h_max"].toInt())
+        use_halo ? make_halo(h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval,
+                             ctx->saved_data["h_bounds"].toIntVector(), h_hdr)
                  : hlhgat_halo_t{};
     const int64_t tile_rows = ctx->saved_data["tile_rows"].toInt();
     const int64_t tile_nnz = ctx->saved_data["tile_nnz"].toInt();
@@ -410,7 +428,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 30 + K;
+    const int64_t n_pos = 33 + K;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -1121,11 +1139,13 @@ Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_row
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
                int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT tiles,
                int64_t tile_rows, int64_t tile_nnz, OptT valid, OptT h_tile, OptT h_ptr,
-               OptT h_cols, OptT h_lcol, int64_t h_max) {
+               OptT h_cols, OptT h_srp, OptT h_lcol, OptT h_sval,
+               std::vector<int64_t> h_bounds, OptT h_hdr) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
                          bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz,
-                         valid, h_tile, h_ptr, h_cols, h_lcol, h_max);
+                         valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds,
+                         h_hdr);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

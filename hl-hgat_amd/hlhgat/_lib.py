@@ -33,8 +33,9 @@ SIGNATURES = {
                                            c_vp, c_vp]),
     "hlhgat_coo_check_sorted": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "hlhgat_incidence_csr": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
-    "hlhgat_halo_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
-                                  c_vp, c_vp, P_i64, P_i64]),
+    "hlhgat_halo_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_i32, c_vp,
+                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, P_i64, P_i64]),
+    "hlhgat_gather_f32": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlhgat_spmm": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                             c_vp, c_i64, c_vp]),
     "hlhgat_poly_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
@@ -86,8 +87,9 @@ MAX_BLOCKS = 16
 
 class HaloDesc(C.Structure):
     """hlhgat_halo_t (include/hlhgat.h)."""
-    _fields_ = [("tile_ptr", c_vp), ("halo_ptr", c_vp), ("halo", c_vp), ("lcol", c_vp),
-                ("n_tiles", c_i64), ("max_halo", c_i32)]
+    _fields_ = [("hdr", c_vp), ("tile_ptr", c_vp), ("halo_ptr", c_vp), ("halo", c_vp), ("srp", c_vp),
+                ("lcol", c_vp), ("sval", c_vp), ("n_tiles", c_i64), ("max_halo", c_i32),
+                ("max_rows", c_i32), ("max_nnz", c_i32)]
 
 
 class HlhgatError(RuntimeError):

@@ -106,10 +106,10 @@ class Batch(PairData):
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(nv):
                 set_valid(t, nv)
             side = k[-1]
-            hk = [getattr(self, h + "_" + side, None) for h in _HALO_KEYS]
-            if (torch.is_tensor(t) and t.is_cuda and all(torch.is_tensor(v) for v in hk)
+            hk = {h: getattr(self, h + "_" + side, None) for h in _HALO_KEYS + ("halo_bounds",)}
+            if (torch.is_tensor(t) and t.is_cuda and all(torch.is_tensor(v) for v in hk.values())
                     and self.hodge_sorted.get(k, False)):
-                set_halo(t, *hk, HALO_MAX)
+                set_halo(t, hk)
         ei = getattr(self, "edge_index", None)
         if torch.is_tensor(ei) and ei.is_cuda:
             for kv in ("n_valid_t", "n_valid_s"):
@@ -174,22 +174,30 @@ def locality_order(edge_index, n: int) -> torch.Tensor:
     return torch.from_numpy(reverse_cuthill_mckee(A, symmetric_mode=True).astype(np.int64))
 
 
-HALO_MAX = 256        # distinct neighbour rows per halo tile (64 KB LDS image at 64 floats)
-HALO_ROWS = 128       # rows per halo tile
-_HALO_KEYS = ("halo_tile_ptr", "halo_ptr", "halo", "halo_lcol")
+# Halo-tile bounds: measured on the config-5 L1 (tools/tsp_spmm.py,
+# profiles/r01_g_tsp_spmm.log) small tiles win -- 24 rows, <= 160 halo rows
+# (a 20 KB LDS image at 32 floats) and <= 768 entries: 256-thread workgroups,
+# several per CU, whose load latency overlaps; 128-row / 256-halo tiles reuse
+# more (5.4x vs 3.6x) but leave too few workgroups in flight.
+HALO_MAX = 160        # distinct neighbour rows per halo tile
+HALO_ROWS = 24        # rows per halo tile
+HALO_NNZ = 768        # Laplacian entries per halo tile
+_HALO_KEYS = ("halo_tile_ptr", "halo_ptr", "halo", "halo_srp", "halo_lcol", "halo_eperm",
+              "halo_hdr")
 
 
 def halo_tiles(edge_index, n: int, order=None, max_rows: int = HALO_ROWS,
-               max_halo: int = HALO_MAX) -> Optional[Dict[str, torch.Tensor]]:
+               max_halo: int = HALO_MAX, max_nnz: int = HALO_NNZ
+               ) -> Optional[Dict[str, torch.Tensor]]:
     """Halo tiles of a sorted symmetric Laplacian COO (the CSR the device path
     builds from it: rows = edge_index[0], entries in COO order) for the
     LDS-staged SpMM, visiting rows in `order` (e.g. locality_order).  Host
     side, once per graph, like the row schedule; runs the library's native
-    builder (hlhgat_halo_tiles).  Returns tensors tile_ptr / halo_ptr / halo
-    (int32) and lcol (int16 holding uint16), or None if a row references more
-    than max_halo distinct columns."""
+    builder (hlhgat_halo_tiles).  Returns int32 tensors halo_tile_ptr /
+    halo_ptr / halo / halo_srp / halo_eperm, int16 halo_lcol (holding uint16)
+    and halo_bounds, or None if one row exceeds a bound."""
     import ctypes as C
-    from ._lib import LIB, check
+    from ._lib import LIB
     ei = np.asarray(edge_index)
     nnz = ei.shape[1]
     rowptr = np.zeros(n + 1, dtype=np.int32)
@@ -198,43 +206,60 @@ def halo_tiles(edge_index, n: int, order=None, max_rows: int = HALO_ROWS,
     ordr = None if order is None else np.ascontiguousarray(np.asarray(order), dtype=np.int32)
     tile_ptr = np.zeros(n + 1, dtype=np.int32)
     halo_ptr = np.zeros(n + 1, dtype=np.int32)
+    srp = np.zeros(n + 1, dtype=np.int32)
     halo = np.zeros(max(nnz, 1), dtype=np.int32)
     lcol = np.zeros(max(nnz, 1), dtype=np.uint16)
+    eperm = np.zeros(max(nnz, 1), dtype=np.int32)
+    hdr = np.zeros((max(n, 1), 8), dtype=np.int32)
     nt, nh = C.c_int64(0), C.c_int64(0)
     vp = lambda a: None if a is None else a.ctypes.data  # noqa: E731
-    rc = LIB.hlhgat_halo_tiles(vp(rowptr), vp(col), n, n, vp(ordr), max_rows, max_halo,
-                               vp(tile_ptr), vp(halo_ptr), vp(halo), vp(lcol), C.byref(nt),
-                               C.byref(nh))
+    rc = LIB.hlhgat_halo_tiles(vp(rowptr), vp(col), n, n, vp(ordr), max_rows, max_nnz, max_halo,
+                               vp(tile_ptr), vp(halo_ptr), vp(halo), vp(srp), vp(lcol), vp(eperm),
+                               vp(hdr), C.byref(nt), C.byref(nh))
     if rc != 0:
         return None
-    check(rc, "halo_tiles")
     t, h = nt.value, nh.value
     return {"halo_tile_ptr": torch.from_numpy(tile_ptr[:t + 1].copy()),
             "halo_ptr": torch.from_numpy(halo_ptr[:t + 1].copy()),
             "halo": torch.from_numpy(halo[:h].copy()),
-            "halo_lcol": torch.from_numpy(lcol[:nnz].view(np.int16).copy())}
+            "halo_srp": torch.from_numpy(srp),
+            "halo_lcol": torch.from_numpy(lcol[:nnz].view(np.int16).copy()),
+            "halo_eperm": torch.from_numpy(eperm[:nnz].copy()),
+            "halo_hdr": torch.from_numpy(hdr[:t].copy()),
+            "halo_bounds": torch.tensor([max_halo, max_rows, max_nnz], dtype=torch.int64)}
 
 
 def _collate_halo(b: "Batch", graphs: Sequence["PairData"], side: str) -> None:
-    """Concatenate per-graph halo tiles: positions and halo ids shift by the
-    graph's row offset, halo offsets by the halo entries before it; lcol is
-    tile-local and unchanged."""
+    """Concatenate per-graph halo tiles: schedule positions and halo ids shift
+    by the graph's row offset, halo offsets by the halo entries before it,
+    schedule-order entry offsets and eperm by the entries before it; lcol is
+    tile-local and unchanged.  All graphs must share the bounds."""
     keys = [k + "_" + side for k in _HALO_KEYS]
-    if not all(getattr(g, k, None) is not None for g in graphs for k in keys):
+    bk = "halo_bounds_" + side
+    if not all(getattr(g, k, None) is not None for g in graphs for k in keys + [bk]):
         return
-    xk = "x_" + side
-    tp, hp, hc, lc = [np.zeros(1, np.int32)], [np.zeros(1, np.int32)], [], []
-    roff = hoff = 0
+    bounds = np.asarray(getattr(graphs[0], bk))
+    if not all(np.array_equal(np.asarray(getattr(g, bk)), bounds) for g in graphs):
+        return
+    xk, ek = "x_" + side, "edge_index_" + side
+    z = [np.zeros(1, np.int32)]
+    tp, hp, srp, hc, lc, ep, hd = list(z), list(z), list(z), [], [], [], []
+    roff = hoff = eoff = 0
     for g in graphs:
-        gtp, ghp, ghc, glc = (np.asarray(getattr(g, k)) for k in keys)
+        gtp, ghp, ghc, gsrp, glc, gep, ghd = (np.asarray(getattr(g, k)) for k in keys)
+        hd.append(ghd + np.array([roff, 0, hoff, 0, eoff, 0, 0, 0], dtype=np.int32))
         tp.append(gtp[1:] + roff)
         hp.append(ghp[1:] + hoff)
+        srp.append(gsrp[1:] + eoff)
         hc.append(ghc + roff)
         lc.append(glc)
+        ep.append(gep + eoff)
         roff += getattr(g, xk).size(0)
         hoff += int(ghp[-1])
-    for k, parts in zip(keys, (tp, hp, hc, lc)):
+        eoff += int(np.asarray(getattr(g, ek)).shape[1])
+    for k, parts in zip(keys, (tp, hp, hc, srp, lc, ep, hd)):
         setattr(b, k, torch.from_numpy(np.ascontiguousarray(np.concatenate(parts))))
+    setattr(b, bk, torch.from_numpy(bounds.copy()))
 
 
 def is_sorted_symmetric(ei: np.ndarray, w: Optional[np.ndarray]) -> bool:
@@ -261,7 +286,7 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     first = graphs[0]
     keys = first.keys()
     for k in keys:
-        if k.rsplit("_", 1)[0] in _HALO_KEYS:
+        if k.rsplit("_", 1)[0] in _HALO_KEYS + ("halo_bounds",):
             continue  # _collate_halo
         vals = [getattr(g, k) for g in graphs]
         v0 = vals[0]

@@ -272,38 +272,51 @@ def set_valid(edge_index: torch.Tensor, n_valid: torch.Tensor, attr: str = "_hlh
     return edge_index
 
 
-def set_halo(edge_index: torch.Tensor, tile_ptr: torch.Tensor, halo_ptr: torch.Tensor,
-             halo: torch.Tensor, lcol: torch.Tensor, max_halo: int) -> torch.Tensor:
+def set_halo(edge_index: torch.Tensor, ht: dict) -> torch.Tensor:
     """Attach halo tiles (hodge_dataset.halo_tiles, built for this operator's
     CSR and row schedule) to a sorted symmetric Laplacian's edge_index: its
-    SpMM / polynomial steps then stage each tile's neighbour rows in LDS
-    (k_poly_halo; bitwise the same results)."""
+    SpMM / polynomial steps then stage each tile's entries and neighbour rows
+    in LDS (k_poly_halo; bitwise the same results)."""
     dev = edge_index.device
+    i32 = lambda k: ht[k].to(dev, torch.int32).contiguous()  # noqa: E731
     edge_index._hlhgat_halo = (  # type: ignore[attr-defined]
-        tile_ptr.to(dev, torch.int32).contiguous(), halo_ptr.to(dev, torch.int32).contiguous(),
-        halo.to(dev, torch.int32).contiguous(), lcol.to(dev, torch.int16).contiguous(),
-        int(max_halo))
+        i32("halo_tile_ptr"), i32("halo_ptr"), i32("halo"), i32("halo_srp"),
+        ht["halo_lcol"].to(dev, torch.int16).contiguous(), i32("halo_eperm"),
+        [int(v) for v in ht["halo_bounds"]], i32("halo_hdr"))
     return edge_index
 
 
 _HALO_ENABLED = os.environ.get("HLHGAT_HALO", "1") != "0"
 
 
+def _attach_halo(a: "SparseCSR", halo) -> None:
+    """A.halo = (tile_ptr, halo_ptr, halo, srp, lcol, sval, bounds); sval =
+    the CSR values in schedule order, gathered on device once per operator."""
+    tp, hp, hc, srp, lcol, eperm, bounds, hdr = halo
+    if lcol.numel() != a.nnz:
+        raise RuntimeError("hlhgat: halo tiles were built for a different operator")
+    sval = None
+    if a.val is not None and a.nnz:
+        sval = torch.empty_like(a.val)
+        check(LIB.hlhgat_gather_f32(a.val.data_ptr(), eperm.data_ptr(), a.nnz,
+                                    sval.data_ptr(), _stream(a.val)), "gather_f32")
+    a.halo = (tp, hp, hc, srp, lcol, sval, bounds, hdr)
+
+
 def _halo_desc(A: "SparseCSR"):
     """ctypes pointer to an hlhgat_halo_t for A, or None."""
     if A.halo is None or not _HALO_ENABLED:
         return None
-    tp, hp, hc, lc, mh = A.halo
-    d = _lib.HaloDesc(tp.data_ptr(), hp.data_ptr(), hc.data_ptr(), lc.data_ptr(),
-                      tp.numel() - 1, mh)
+    tp, hp, hc, srp, lc, sval, (mh, mr, mn), hdr = A.halo
+    d = _lib.HaloDesc(hdr.data_ptr(), tp.data_ptr(), hp.data_ptr(), hc.data_ptr(), srp.data_ptr(),
+                      lc.data_ptr(), _ptr(sval), tp.numel() - 1, mh, mr, mn)
     return C.pointer(d)
 
 
 def _halo_args(A: "SparseCSR"):
-    """The (tile_ptr, halo_ptr, halo, lcol, max_halo) arguments of the C++
-    conv node (Nones when A has no halo tiles)."""
+    """The halo arguments of the C++ conv node (Nones when A has none)."""
     if A.halo is None or not _HALO_ENABLED:
-        return (None, None, None, None, 0)
+        return (None, None, None, None, None, None, [0, 0, 0], None)
     return A.halo
 
 
@@ -371,9 +384,7 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
         a.valid = valid
         halo = getattr(edge_index, "_hlhgat_halo", None)
         if halo is not None:  # built for the COO order = this CSR's entry order
-            if halo[3].numel() != a.nnz:
-                raise RuntimeError("hlhgat: halo tiles were built for a different operator")
-            a.halo = halo
+            _attach_halo(a, halo)
         op = HodgeOperator(a, a)
     else:
         fwd = _csr_general(ei[1], ei[0], w, n, n)

@@ -107,34 +107,48 @@ int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
 
 /* ---- halo tiles (LDS-staged SpMM for large Laplacians) ----------------- */
 /* A tiling of a CSR operator's rows for the LDS-staged SpMM: tile t owns the
- * rows order[tile_ptr[t] .. tile_ptr[t+1]) (order = the operator's row
- * schedule, NULL = natural) and the distinct columns its rows reference,
- * halo[halo_ptr[t] .. halo_ptr[t+1]) (<= max_halo of them).  lcol[e] is the
- * position of col[e] inside its row's tile halo.  One workgroup stages the
- * tile's halo rows of X in LDS once and gathers every entry from there, so
- * each X row is read from L2 once per tile instead of once per entry
- * (TSP-scale L1: ~20 entries per row, ~5 uses per staged row).  Results are
- * bitwise those of the plain SpMM (same per-row summation order).  Built on
- * the HOST by hlhgat_halo_tiles, uploaded by the caller. */
+ * schedule positions [tile_ptr[t], tile_ptr[t+1]) (rows order[p], order = the
+ * operator's row schedule, NULL = natural) and the distinct columns those
+ * rows reference, halo[halo_ptr[t] .. halo_ptr[t+1]) (ascending).  The
+ * entries are re-laid in SCHEDULE order: position p's entries are
+ * [srp[p], srp[p+1]) of lcol (tile-local column = index into the tile's
+ * halo) and sval (the CSR values permuted the same way; NULL = all ones).
+ * One workgroup stages a tile's entries and the halo rows of X in LDS with
+ * bulk coalesced loads, then every row is summed from LDS: each X row is read
+ * from L2 once per tile instead of once per entry (TSP-scale L1: ~20 entries
+ * per row, ~5 uses per staged row).  Per-row summation order is the CSR
+ * order, so results are bitwise those of the plain SpMM.  Built on the HOST
+ * by hlhgat_halo_tiles; sval on device by hlhgat_gather_f32(val, eperm). */
 typedef struct hlhgat_halo {
-  const int32_t* tile_ptr;  /* [n_tiles+1] positions in the row schedule */
+  const int32_t* hdr;       /* [n_tiles][8] {p0, rows, halo0, n_halo, e0, n_entries, 0, 0} */
+  const int32_t* tile_ptr;  /* [n_tiles+1] schedule positions */
   const int32_t* halo_ptr;  /* [n_tiles+1] offsets into halo */
   const int32_t* halo;      /* distinct columns of each tile, ascending */
-  const uint16_t* lcol;     /* [nnz] tile-local column of each CSR entry */
+  const int32_t* srp;       /* [n_rows+1] entry offsets in schedule order */
+  const uint16_t* lcol;     /* [nnz] tile-local column, schedule order */
+  const float* sval;        /* [nnz] values, schedule order (NULL = ones) */
   int64_t n_tiles;
-  int32_t max_halo;         /* bound on any tile's halo (sizes the LDS image) */
+  int32_t max_halo;         /* bounds of any tile (size the LDS image) */
+  int32_t max_rows;
+  int32_t max_nnz;
 } hlhgat_halo_t;
 
 /* HOST function (host pointers, no stream): pack consecutive rows of the
- * schedule greedily into tiles of <= max_rows rows and <= max_halo distinct
- * columns.  Capacities: tile_ptr and halo_ptr n_rows+1, halo nnz, lcol nnz.
- * Returns HLHGAT_EINVAL if one row alone references more than max_halo
- * distinct columns (use the plain SpMM then). */
+ * schedule greedily into tiles of <= max_rows rows, <= max_nnz entries and
+ * <= max_halo distinct columns.  Outputs (capacities): tile_ptr, halo_ptr and
+ * srp n_rows+1; halo, lcol and eperm nnz (eperm[i] = CSR entry of
+ * schedule-ordered entry i); hdr 8*n_rows (per-tile header, see
+ * hlhgat_halo_t).  Returns HLHGAT_EINVAL if one row alone exceeds
+ * max_halo columns or max_nnz entries (use the plain SpMM then). */
 int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
                       int64_t n_cols, const int32_t* order, int32_t max_rows,
-                      int32_t max_halo, int32_t* tile_ptr, int32_t* halo_ptr,
-                      int32_t* halo, uint16_t* lcol, int64_t* n_tiles,
-                      int64_t* n_halo);
+                      int32_t max_nnz, int32_t max_halo, int32_t* tile_ptr,
+                      int32_t* halo_ptr, int32_t* halo, int32_t* srp, uint16_t* lcol,
+                      int32_t* eperm, int32_t* hdr, int64_t* n_tiles, int64_t* n_halo);
+
+/* dst[i] = src[idx[i]] for i < n (device; e.g. halo sval = val[eperm]). */
+int hlhgat_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst,
+                      void* stream);
 
 /* ---- SpMM and fused polynomial step ----------------------------------- */
 /* `halo` (optional, below) selects the LDS-staged kernel: see hlhgat_halo_t.

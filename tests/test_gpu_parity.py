@@ -642,7 +642,7 @@ def _halo_ops(g, side, max_rows, max_halo):
     plain = ops.hodge_operator(ops.set_row_order(ops.mark_hodge(dev(ei)), order), dev(w), n)
     ht = halo_tiles(ei.numpy(), n, order.numpy(), max_rows=max_rows, max_halo=max_halo)
     ei_h = ops.set_row_order(ops.mark_hodge(dev(ei)), order)
-    ops.set_halo(ei_h, ht["halo_tile_ptr"], ht["halo_ptr"], ht["halo"], ht["halo_lcol"], max_halo)
+    ops.set_halo(ei_h, ht)
     halo = ops.hodge_operator(ei_h, dev(w), n)
     assert halo.fwd.halo is not None and plain.fwd.halo is None
     return ei, w, n, plain, halo, ei_h

@@ -236,19 +236,24 @@ def test_fastconv_adj_t_forms_agree():
         4, 4, K=3, demo_recurrence=False)._kind
 
 
-def _check_halo(ei, n, order, ht, max_rows, max_halo):
+def _check_halo(ei, n, order, ht, max_rows, max_halo, max_nnz=3072):
     tp, hp = ht["halo_tile_ptr"].numpy(), ht["halo_ptr"].numpy()
-    hc, lc = ht["halo"].numpy(), ht["halo_lcol"].numpy().view(np.uint16)
+    hc, srp = ht["halo"].numpy(), ht["halo_srp"].numpy()
+    lc, ep = ht["halo_lcol"].numpy().view(np.uint16), ht["halo_eperm"].numpy()
     assert tp[0] == 0 and tp[-1] == n and np.all(np.diff(tp) > 0)
     assert np.all(np.diff(tp) <= max_rows) and np.all(np.diff(hp) <= max_halo)
+    assert np.all(np.diff(srp[tp]) <= max_nnz)
     rowptr = np.concatenate([[0], np.cumsum(np.bincount(ei[0], minlength=n))])
     sched = np.arange(n) if order is None else np.asarray(order)
+    assert srp[-1] == ei.shape[1] and np.array_equal(np.sort(ep), np.arange(ei.shape[1]))
     for t in range(len(tp) - 1):
         halo = hc[hp[t]:hp[t + 1]]
         assert np.all(np.diff(halo) > 0)  # ascending, distinct
-        for r in sched[tp[t]:tp[t + 1]]:
-            e = np.arange(rowptr[r], rowptr[r + 1])
-            assert np.array_equal(halo[lc[e]], ei[1][e])
+        for p in range(tp[t], tp[t + 1]):
+            r = sched[p]
+            i = np.arange(srp[p], srp[p + 1])
+            assert np.array_equal(ep[i], np.arange(rowptr[r], rowptr[r + 1]))
+            assert np.array_equal(halo[lc[i]], ei[1][ep[i]])
 
 
 def test_halo_tiles_invariants():
@@ -260,9 +265,14 @@ def test_halo_tiles_invariants():
     g = tsp_like_graph(3, n=600, k=6, halo=False)
     for ei, n, order in ((g.edge_index_s.numpy(), g.x_s.shape[0], g.row_order_s.numpy()),
                          (g.edge_index_t.numpy(), g.x_t.shape[0], None)):
-        for max_rows, max_halo in ((128, 256), (16, 64), (3, 40)):
-            ht = halo_tiles(ei, n, order, max_rows=max_rows, max_halo=max_halo)
-            _check_halo(ei, n, order, ht, max_rows, max_halo)
+        for max_rows, max_halo, max_nnz in ((128, 256, 3072), (16, 64, 3072), (3, 40, 3072),
+                                            (128, 256, 100)):
+            ht = halo_tiles(ei, n, order, max_rows=max_rows, max_halo=max_halo, max_nnz=max_nnz)
+            _check_halo(ei, n, order, ht, max_rows, max_halo, max_nnz)
+            hd = ht["halo_hdr"].numpy()
+            tp, hp, srp = ht["halo_tile_ptr"].numpy(), ht["halo_ptr"].numpy(), ht["halo_srp"].numpy()
+            assert np.array_equal(hd[:, 0], tp[:-1]) and np.array_equal(hd[:, 3], np.diff(hp))
+            assert np.array_equal(hd[:, 5], np.diff(srp[tp]))
     assert locality_order(g.edge_index_s.numpy(), g.x_s.shape[0]).numel() == g.x_s.shape[0]
 
 
@@ -273,5 +283,6 @@ def test_halo_tiles_reject_and_collate():
     ei = g.edge_index_s.numpy()
     assert halo_tiles(ei, g.x_s.shape[0], None, max_halo=3) is None  # a row has > 3 columns
     b = collate([g, tsp_like_graph(5, n=300, k=6)], check_hodge=False)
-    ht = {k: getattr(b, k + "_s") for k in ("halo_tile_ptr", "halo_ptr", "halo", "halo_lcol")}
+    ht = {k: getattr(b, k + "_s") for k in ("halo_tile_ptr", "halo_ptr", "halo", "halo_srp",
+                                             "halo_lcol", "halo_eperm", "halo_hdr")}
     _check_halo(b.edge_index_s.numpy(), b.x_s.shape[0], b.row_order_s.numpy(), ht, 128, 256)

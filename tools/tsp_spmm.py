@@ -48,7 +48,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--graphs", type=int, default=4)
     ap.add_argument("--d", type=int, nargs="+", default=[64, 128])
-    ap.add_argument("--tiles", nargs="+", default=["128:256", "64:128", "96:192"])
+    ap.add_argument("--tiles", nargs="+", default=["24:160:768", "32:192:1024"])
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     from hlhgat import ops
@@ -64,10 +64,10 @@ def main():
                 "rcm": ops.hodge_operator(ops.set_row_order(ops.mark_hodge(ei.to(dev)), order),
                                           w.to(dev), n)}
     for spec in args.tiles:
-        mr, mh = (int(v) for v in spec.split(":"))
-        ht = halo_tiles(ei.numpy(), n, order.numpy(), max_rows=mr, max_halo=mh)
+        mr, mh, mn = (int(v) for v in spec.split(":"))
+        ht = halo_tiles(ei.numpy(), n, order.numpy(), max_rows=mr, max_halo=mh, max_nnz=mn)
         e = ops.set_row_order(ops.mark_hodge(ei.to(dev)), order)
-        ops.set_halo(e, ht["halo_tile_ptr"], ht["halo_ptr"], ht["halo"], ht["halo_lcol"], mh)
+        ops.set_halo(e, ht)
         op = ops.hodge_operator(e, w.to(dev), n)
         op.info = {"tiles": ht["halo_tile_ptr"].numel() - 1,
                    "reuse": round(nnz / int(ht["halo_ptr"][-1]), 2)}
