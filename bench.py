@@ -108,6 +108,47 @@ def pmc_traffic(kernel="k_poly_step"):
     return None, None
 
 
+def cfg5_spmm(device, reps=20):
+    """The north-star SpMM roofline at BASELINE configs[4] (TSP-like simplex
+    graphs, 4 x 10k nodes per GPU, L1 n ~ 207k rows, nnz ~ 4.1M): Y = L1 X
+    and one fused Laguerre step, as the product runs them (dataset row
+    schedule + LDS halo tiles), each launch timed with hipExtLaunchKernel
+    stamps.  Algorithmic bytes: SpMM 8 nnz + 4 (n+1) + 8 n d,
+    step 8 nnz + 4 (n+1) + 12 n d.  A kernel-level figure; config 5's model
+    is not the bench workload."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph
+    b = collate([tsp_like_graph(s) for s in range(4)], check_hodge=False).to(device)
+    n, nnz = b.x_s.shape[0], b.edge_index_s.shape[1]
+    A = ops.hodge_operator(b.edge_index_s, b.edge_weight_s, n).fwd
+    out = {"config": f"BASELINE configs[4]: 4 TSP-like graphs (10k nodes, k=9 NN), L1 n={n} "
+                     f"nnz={nnz}; RCM row schedule + LDS halo tiles "
+                     f"({'on' if A.halo is not None else 'off'})",
+           "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    for d in (64, 128):
+        X = torch.randn(n, d, device=device)
+        Z = torch.randn(n, d, device=device)
+        Y = torch.empty(n, d, device=device)
+        for what, kw in (("spmm", {}),
+                         ("laguerre_step", dict(Z=Z, alpha=-1.0, beta=5.0, gamma=-2.0, div=3.0))):
+            for _ in range(3):
+                ops._poly_step(A, X, Y, **kw)
+            torch.cuda.synchronize()
+            ops.prof_reset()
+            ops.prof_enable(hlhgat._lib.PROF_POLY, True)
+            for _ in range(reps):
+                ops._poly_step(A, X, Y, **kw)
+            torch.cuda.synchronize()
+            ops.prof_enable(hlhgat._lib.PROF_POLY, False)
+            p = ops.prof_read(hlhgat._lib.PROF_POLY)
+            gbs = p["bytes"] / (p["ms"] * 1e-3) / 1e9
+            out[f"{what}_d{d}"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                   "avg_launch_us": round(p["ms"] * 1e3 / p["launches"], 1)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,6 +157,8 @@ def main():
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph replay")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="skip the config-5 (TSP) SpMM roofline measurement")
     ap.add_argument("--prof-steps", type=int, default=3,
                     help="eager steps with kernel event stamps for the roofline")
     args = ap.parse_args()
@@ -214,7 +257,11 @@ def main():
                       "launches": proj["launches"],
                       "avg_launch_us": round(proj["ms"] * 1e3 / max(proj["launches"], 1), 2)},
         "cpu_baseline": None,
+        "spmm_cfg5": None,
     }
+    if rank == 0 and world == 1 and not args.no_cfg5:
+        log("[rank 0] config-5 SpMM roofline")
+        result["spmm_cfg5"] = cfg5_spmm(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
         from hlhgat.synthetic import zinc_like_batch
