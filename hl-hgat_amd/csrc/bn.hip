@@ -27,8 +27,11 @@ using namespace hlhgat;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxParts = 128;
+constexpr int kMaxParts = 512;
+constexpr int kGroup = 16;                        // partitions per first-level group
+constexpr int kMaxGroups = kMaxParts / kGroup;
 constexpr int kMaxTiles = 1024;
+constexpr int kCounters = kMaxTiles * (1 + kMaxGroups);  // per tile: top + group counters
 constexpr int APPLY_RPT = 2;  // rows per thread in the elementwise apply kernels
 
 struct BnLayout {
@@ -42,9 +45,12 @@ struct BnLayout {
 };
 
 // Row partitions of the statistics pass: each partition is one workgroup
-// whose loads are all in flight within a couple of round trips, and the
-// last-arriving workgroup sums `parts` partials, so fewer, fatter partitions
-// shorten that serial tail.  HLHGAT_BN_PARTS overrides (A/B measurements).
+// whose loads are all in flight within a couple of round trips.  The
+// partials are combined by a two-level last-arriver tree (groups of kGroup
+// partitions, then the groups), so many thin partitions cost two short tails
+// instead of one long one.  In the ZINC step 64 partitions measured best
+// (256: 264k -> 251k graphs/s; more workgroups crowd the concurrent chain).
+// HLHGAT_BN_PARTS overrides (A/B measurements).
 int64_t bn_parts() {
   static int64_t v = [] {
     const char* e = getenv("HLHGAT_BN_PARTS");
@@ -76,8 +82,9 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
 }
 
 struct BnWs {
-  unsigned* count;   // [kMaxTiles] at offset 0 (zero between launches)
+  unsigned* count;   // [kCounters] at offset 0 (zero between launches)
   double* part;      // [parts][C][2]
+  double* gpart;     // [groups][C][2]
   float* coef;       // [3][C] (bwd: a, b, c)
 };
 
@@ -87,8 +94,8 @@ size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 // reads another launch's partials as a counter.
 size_t bn_ws_bytes(int64_t n, int64_t C) {
   (void)n;
-  return align_up(sizeof(unsigned) * kMaxTiles) + align_up(sizeof(double) * 2 * kMaxParts * C) +
-         align_up(sizeof(float) * 3 * C);
+  return align_up(sizeof(unsigned) * kCounters) + align_up(sizeof(double) * 2 * kMaxParts * C) +
+         align_up(sizeof(double) * 2 * kMaxGroups * C) + align_up(sizeof(float) * 3 * C);
 }
 
 BnWs carve(void* ws, int64_t n, int64_t C) {
@@ -96,9 +103,11 @@ BnWs carve(void* ws, int64_t n, int64_t C) {
   char* p = (char*)ws;
   BnWs w;
   w.count = (unsigned*)p;
-  p += align_up(sizeof(unsigned) * kMaxTiles);
+  p += align_up(sizeof(unsigned) * kCounters);
   w.part = (double*)p;
   p += align_up(sizeof(double) * 2 * kMaxParts * C);
+  w.gpart = (double*)p;
+  p += align_up(sizeof(double) * 2 * kMaxGroups * C);
   w.coef = (float*)p;
   return w;
 }
@@ -126,6 +135,7 @@ struct StatsArgs {
   int tpr, rp, tiles, parts;
   int64_t rows_per_part;
   double* part;
+  double* gpart;
   unsigned* count;
   // forward finalisation
   const float* weight;
@@ -192,30 +202,31 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
   }
 }
 
-// Final reduction in the last-arriving workgroup: all 256 threads take part
-// (column t % tile_c, partial group t / tile_c, 4 independent accumulators),
-// groups combined in fixed order through LDS -> deterministic.
-__device__ __forceinline__ void reduce_parts(const StatsArgs& a, int c0, int tile_c,
+// Sum of partials [first, first+count) of src ([*][C][2]) for the tile's
+// columns: all 256 threads take part (column t % tile_c, partial group
+// t / tile_c, loads in batches of 16), groups combined in fixed order through
+// LDS -> deterministic.  Result in out0/out1[0 .. tile_c).
+__device__ __forceinline__ void reduce_range(const double* src, int first, int count,
+                                             const StatsArgs& a, int c0, int tile_c,
                                              double* out0, double* out1) {
   __shared__ double fin[2][kThreads];
   const int groups = kThreads / tile_c > 0 ? kThreads / tile_c : 1;
   const int t = threadIdx.x % tile_c;
   const int grp = threadIdx.x / tile_c;
   const int c = c0 + t;
-  const int per = (a.parts + groups - 1) / groups;
+  const int per = (count + groups - 1) / groups;
   const int p0 = grp * per;
   double u0 = 0.0, u1 = 0.0;
   if (grp < groups && c < a.C) {
-    // batches of 16 independent loads in flight per thread
     for (int pb = 0; pb < per; pb += 16) {
       double v0[16], v1[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int p = p0 + pb + u;
-        const bool ok = pb + u < per && p < a.parts;
-        const double* src = a.part + ((int64_t)(ok ? p : 0) * a.C + c) * 2;
-        v0[u] = ok ? src[0] : 0.0;
-        v1[u] = ok ? src[1] : 0.0;
+        const bool ok = pb + u < per && p < count;
+        const double* q = src + ((int64_t)(first + (ok ? p : 0)) * a.C + c) * 2;
+        v0[u] = ok ? q[0] : 0.0;
+        v1[u] = ok ? q[1] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -237,6 +248,33 @@ __device__ __forceinline__ void reduce_parts(const StatsArgs& a, int c0, int til
     out1[threadIdx.x] = s1;
   }
   __syncthreads();
+}
+
+// Two-level last-arriver tree over the `parts` partials of this column tile:
+// the last workgroup of each group of kGroup partitions sums its group, the
+// last group sums the group partials.  Returns true (sums in out0/out1) in
+// the one workgroup that finalises; fixed summation order at both levels.
+__device__ __forceinline__ bool tree_reduce(const StatsArgs& a, int c0, int tile_c,
+                                            double* out0, double* out1) {
+  const int tile = blockIdx.y;
+  const int g = blockIdx.x / kGroup;
+  const int ng = (a.parts + kGroup - 1) / kGroup;
+  const int first = g * kGroup;
+  const int cnt = a.parts - first < kGroup ? a.parts - first : kGroup;
+  if (!arrive_last(a.count + kMaxTiles + tile * kMaxGroups + g, (unsigned)cnt)) return false;
+  reduce_range(a.part, first, cnt, a, c0, tile_c, out0, out1);
+  if (ng == 1) return true;
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+    const int c = c0 + t;
+    if (c < a.C) {
+      double* dst = a.gpart + ((int64_t)g * a.C + c) * 2;
+      dst[0] = out0[t];
+      dst[1] = out1[t];
+    }
+  }
+  if (!arrive_last(a.count + tile, (unsigned)ng)) return false;
+  reduce_range(a.gpart, 0, ng, a, c0, tile_c, out0, out1);
+  return true;
 }
 
 template <int V>
@@ -279,11 +317,10 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
     }
   }
   write_partials<V>(s0, s1, a, c0);
-  if (!arrive_last(a.count + blockIdx.y, (unsigned)a.parts)) return;
-  // last arriver of this column tile: finalise its columns
+  // the finalising workgroup of this column tile: finalise its columns
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  reduce_parts(a, c0, tile_c, sum0, sum1);
+  if (!tree_reduce(a, c0, tile_c, sum0, sum1)) return;
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
@@ -408,10 +445,9 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
     }
   }
   write_partials<V>(s0, s1, a, c0);
-  if (!arrive_last(a.count + blockIdx.y, (unsigned)a.parts)) return;
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  reduce_parts(a, c0, tile_c, sum0, sum1);
+  if (!tree_reduce(a, c0, tile_c, sum0, sum1)) return;
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
@@ -529,6 +565,7 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
                 "bn_fwd_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
   BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_fwd_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
   s.nvalid = n_valid;
@@ -542,6 +579,7 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
   s.parts = L.parts;
   s.rows_per_part = L.rows_per_part;
   s.part = w.part;
+  s.gpart = w.gpart;
   s.count = w.count;
   s.weight = weight;
   s.bias = bias;
@@ -585,6 +623,7 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
                 "bn_bwd_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
   BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
   s.nvalid = n_valid;
@@ -602,6 +641,7 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   s.parts = L.parts;
   s.rows_per_part = L.rows_per_part;
   s.part = w.part;
+  s.gpart = w.gpart;
   s.count = w.count;
   s.weight = weight;
   s.save_mean = const_cast<float*>(save_mean);
