@@ -12,7 +12,9 @@ from .hodge_cheb_conv import (HL_filter, HodgeChebConv, HodgeLaguerreConv,  # no
                               HodgeLaguerreFastConv, MSI, NodeEdgeInt, SAPool)
 from .hodge_dataset import (Batch, BoundaryOperator, PairData, adj2par1, collate,  # noqa: F401
                             degree)
-from .hodge_st_model import HL_HGCNN_TSP_dense_int3_pyr, HL_HGCNN_zinc_dense_int3_pyr  # noqa: F401
+from .hodge_st_model import (HL_HGCNN_CIFAR10SP_dense_int3_attpool,  # noqa: F401
+                             HL_HGCNN_pepfunc_dense_int3_attpool, HL_HGCNN_TSP_dense_int3_pyr,
+                             HL_HGCNN_zinc_dense_int3_pyr)
 from .nn import BatchNorm, Linear, Sequential, global_mean_pool  # noqa: F401
 
 __version__ = "0.1.0"

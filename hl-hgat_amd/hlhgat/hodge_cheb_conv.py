@@ -299,14 +299,23 @@ class HL_filter(nn.Module):
         return x_t0, x_s0
 
 
-def cluster_mean(x: Tensor, assign: Tensor) -> Tensor:
+def cluster_mean(x: Tensor, assign: Tensor, n_seg: Optional[int] = None) -> Tensor:
     """torch_scatter.scatter_mean(x, assign, dim=0) on the HIP segment-mean
-    kernel; members are grouped per cluster (stable) by the CSR builder."""
+    kernel; members are grouped per cluster (stable) by the CSR builder.
+    Members assigned inf (an edge dropped by MLGC, lib/Hodge_Dataset.py:262)
+    are left out, as the reference's x[~isinf(pos)] filter does, without a
+    host sync.  n_seg (the number of clusters, e.g. the coarse level's row
+    count) avoids the max() sync; default max(assign) + 1."""
     n = x.size(0)
-    idx = assign.view(-1).to(torch.long)
-    n_seg = int(idx.max().item()) + 1 if n else 0
+    a = assign.view(-1)
+    if n_seg is None:
+        fin = a[~torch.isinf(a)] if a.is_floating_point() else a
+        n_seg = int(fin.max().item()) + 1 if fin.numel() else 0
+    if a.is_floating_point():
+        a = torch.where(torch.isinf(a), torch.full_like(a, float(n_seg)), a)
+    idx = a.to(torch.long)
     ar = torch.arange(n, device=x.device)
-    csr = ops._csr_general(idx, ar, None, n_seg, max(n, 1))
+    csr = ops._csr_general(idx, ar, None, n_seg + 1, max(n, 1))
     return ops.segment_mean(x, csr.rowptr, n_seg, csr.col)
 
 
@@ -322,11 +331,8 @@ class SAPool(nn.Module):
         x_t0 = x_t0 * att_t
         x_s0 = x_s0 * att_s
         pos_t, pos_s = pos_ts[k], pos_ss[k]
-        x_t0 = cluster_mean(x_t0, pos_t)
-        keep = ~torch.isinf(pos_s).view(-1)
-        x_s0 = x_s0[keep]
-        pos_s = pos_s[keep]
-        x_s0 = cluster_mean(x_s0, pos_s)
+        x_t0 = cluster_mean(x_t0, pos_t, datas[k + 1].x_t.shape[0])
+        x_s0 = cluster_mean(x_s0, pos_s, datas[k + 1].x_s.shape[0])  # inf members dropped
         edge_index_s = datas[k + 1].edge_index_s.to(device)
         edge_weight_s = datas[k + 1].edge_weight_s.to(device)
         edge_index_t = datas[k + 1].edge_index_t.to(device)

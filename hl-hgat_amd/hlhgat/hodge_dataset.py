@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "graph_tiles", "static_caps", "pad_batch", "halo_tiles"]
+           "graph_tiles", "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
 _HODGE_KEYS = ("edge_index_s", "edge_index_t")
@@ -520,3 +520,82 @@ def hodge_laplacians(edge_index: np.ndarray, n: int):
     L0 = 2 * torch.matmul(par1, par1.T) / maxeig
     L1 = 2 * torch.matmul(par1.T, par1) / maxeig
     return L0, L1, maxeig, par1
+
+
+# ----------------------------------------------------------------------------
+# multi-level graph coarsening (MLGC) for the attention-pooling heads
+# ----------------------------------------------------------------------------
+def graclus(edge_index, n: int, weight=None, seed: int = 0) -> np.ndarray:
+    """Greedy graclus matching (restated from torch_cluster 1.6.0
+    graclus_cluster, the reference's dependency, absent here): self-loops
+    dropped, nodes visited in a random order (torch_cluster draws a
+    torch.randperm; here a seeded numpy permutation), each unmatched node u
+    is paired with its unmatched neighbour of largest weight (first in
+    ascending neighbour order on ties; unweighted = all ones) and both get
+    cluster id min(u, v); a node with no unmatched neighbour stays alone
+    (id u).  Returns int64 [n] cluster ids."""
+    ei = np.asarray(edge_index)
+    keep = ei[0] != ei[1]
+    r, c = ei[0][keep], ei[1][keep]
+    w = np.ones(r.size) if weight is None else np.asarray(weight, dtype=np.float64)[keep]
+    o = np.lexsort((c, r))
+    r, c, w = r[o], c[o], w[o]
+    ptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(r, minlength=n), out=ptr[1:])
+    out = -np.ones(n, dtype=np.int64)
+    for u in np.random.default_rng(seed).permutation(n):
+        if out[u] >= 0:
+            continue
+        out[u] = u
+        best, wbest = -1, 0.0
+        for e in range(ptr[u], ptr[u + 1]):
+            v = c[e]
+            if out[v] >= 0 or not w[e] > wbest:
+                continue
+            best, wbest = v, w[e]
+        if best >= 0:
+            out[u] = out[best] = min(u, best)
+    return out
+
+
+def mlgc(g: "PairData", seed: int = 0):
+    """One level of MLGC (lib/Hodge_Dataset.py:241-297): graclus on L0's
+    pattern with unit weights, cluster ids renumbered by ascending label, an
+    edge whose end nodes share a cluster is dropped (assignment inf), the
+    others map to the coarse edge (min, max) of their clusters, numbered in
+    first-seen edge order; the coarse graph gets Hodge Laplacians built as the
+    reference does (dense eigh, 2 B1 B1^T / lmax) and unit features.
+    Returns (coarse PairData, c_node [n, 1] float, c_edge [E, 1] float)."""
+    n = int(g.num_node1)
+    lab = graclus(np.asarray(g.edge_index_t), n, seed=seed)
+    uniq = np.unique(lab)
+    rank = {int(v): i for i, v in enumerate(uniq)}
+    c_node = np.array([rank[int(v)] for v in lab], dtype=np.int64)
+    ei = np.asarray(g.edge_index)
+    c_edge = np.zeros(ei.shape[1], dtype=np.float32)
+    key, e1 = {}, [[], []]
+    for i in range(ei.shape[1]):
+        a, b = int(c_node[ei[0][i]]), int(c_node[ei[1][i]])
+        if a == b:
+            c_edge[i] = np.inf
+            continue
+        lo, hi = min(a, b), max(a, b)
+        if (hi, lo) not in key:
+            key[(hi, lo)] = len(e1[0])
+            e1[0].append(lo)
+            e1[1].append(hi)
+        c_edge[i] = key[(hi, lo)]
+    ei1 = np.array(e1, dtype=np.int64).reshape(2, -1)
+    n1 = int(uniq.size)
+    L0, L1, _, _ = hodge_laplacians(ei1, n1)
+    eit, ewt = dense_to_sparse(L0)
+    eis, ews = dense_to_sparse(L1)
+    c = PairData(x_s=torch.ones(ei1.shape[1], 1), edge_index_s=eis, edge_weight_s=ews,
+                 x_t=torch.ones(n1, 1), edge_index_t=eit, edge_weight_t=ewt)
+    c.edge_index = torch.from_numpy(ei1)
+    c.num_node1 = n1
+    c.num_edge1 = int(ei1.shape[1])
+    c.num_nodes = n1
+    c._hodge_sorted = True
+    return (c, torch.from_numpy(c_node.astype(np.float32)).view(-1, 1),
+            torch.from_numpy(c_edge).view(-1, 1))

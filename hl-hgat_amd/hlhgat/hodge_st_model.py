@@ -11,12 +11,13 @@ import torch.nn as nn
 from torch.nn import Dropout, Linear
 
 from . import ops
-from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt
+from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt, cluster_mean
 from .hodge_dataset import adj2par1, degree
 from .nn import BatchNorm, Sequential, run_sequential
 
-__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr", "segment_ptr",
-           "mean_pool_sorted"]
+__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr",
+           "HL_HGCNN_CIFAR10SP_dense_int3_attpool", "HL_HGCNN_pepfunc_dense_int3_attpool",
+           "segment_ptr", "mean_pool_sorted"]
 
 
 def segment_ptr(counts: torch.Tensor, device) -> torch.Tensor:
@@ -220,3 +221,158 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         if len(self.mlp_channels) == 1:
             x_s = self.mlp(x_s, edge_index_s, edge_weight_s)
         return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch
+
+
+def _level_offsets(counts_next: torch.Tensor, counts: torch.Tensor, device) -> torch.Tensor:
+    """n_ahead[n_batch] of the attpool heads (lib/Hodge_ST_Model.py:1031-1036):
+    for every row of the fine level, the first coarse row of its graph."""
+    ahead = torch.zeros(counts_next.numel(), dtype=torch.float32, device=device)
+    ahead[1:] = torch.cumsum(counts_next.to(device), 0)[:-1].to(torch.float32)
+    return torch.repeat_interleave(ahead, counts.to(device))
+
+
+class _AttPoolHead(nn.Module):
+    """Shared body of the attention-pooling heads (two MLGC levels, ``datas``
+    = [fine batch with the cluster of each node / edge in feature column 0,
+    coarse batch]).  att_every_level: NEAtt{i} after every level on the dense
+    concatenation (main_pepfunc...:133-137); otherwise one NEAtt at pool_loc on
+    the level's last block output, normalised by its batch max
+    (lib/Hodge_ST_Model.py:1058-1064)."""
+
+    def __init__(self, channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                 dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, att_every_level):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.mlp_channels = mlp_channels
+        self.node_dim = node_dim + keig
+        self.edge_dim = edge_dim + keig
+        self.initial_channel = self.filters[0]
+        self.pool_loc = pool_loc
+        self.att_every_level = att_every_level
+        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, 1,
+                                      dropout_ratio)
+        gcn_insize = self.initial_channel
+        for i, gcn_outsize in enumerate(self.filters):
+            for j in range(self.channels[i]):
+                setattr(self, "NEInt{}{}".format(i, j), NodeEdgeInt(d=gcn_insize, dv=gcn_outsize))
+                setattr(self, "NEConv{}{}".format(i, j),
+                        _hl_block(gcn_outsize, gcn_outsize, gcn_outsize, K, dropout_ratio))
+                gcn_insize = gcn_insize + gcn_outsize
+            if att_every_level:
+                setattr(self, "NEAtt{}".format(i),
+                        NodeEdgeInt(d=gcn_insize, dv=gcn_outsize, only_att=True, l=l))
+            elif i == self.pool_loc:
+                setattr(self, "NEAtt{}".format(i),
+                        NodeEdgeInt(d=gcn_outsize, dv=gcn_outsize, only_att=True,
+                                    sigma=nn.ReLU(), l=l))
+        mlp_insize = self.filters[-1] * 2
+        for i, mlp_outsize in enumerate(mlp_channels):
+            setattr(self, "mlp%d" % i, nn.Sequential(
+                Linear(mlp_insize, mlp_outsize), nn.BatchNorm1d(mlp_outsize), nn.ReLU(),
+                nn.Dropout(dropout_ratio_mlp)))
+            mlp_insize = mlp_outsize
+        self.out = Linear(mlp_insize, num_classes)
+
+    def forward(self, datas, device="cuda:0", if_final_layer=False, if_att=False):
+        d0 = datas[0]
+        dev = d0.x_t.device
+        # global coarse index of every fine node / edge (pos_ts / pos_ss)
+        pos_t = d0.x_t[:, 0] + _level_offsets(datas[1].num_node1, d0.num_node1, dev)
+        pos_s = d0.x_s[:, 0] + _level_offsets(datas[1].num_edge1, d0.num_edge1, dev)
+        x_s, edge_index_s, edge_weight_s = d0.x_s[:, 1:], d0.edge_index_s, d0.edge_weight_s
+        x_t, edge_index_t, edge_weight_t = d0.x_t[:, 1:], d0.edge_index_t, d0.edge_weight_t
+        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                     edge_weight_s)
+        x_t0, x_s0 = x_t, x_s
+        k = 0
+        par_1 = adj2par1(d0.edge_index, x_t0.shape[0], x_s0.shape[0])
+        D = degree(d0.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        att_t = att_s = None
+        dense = x_t.is_cuda and ops.DENSE_SLAB
+        for i, _ in enumerate(self.channels):
+            # one dense slab per level: x0 (scaled / pooled) then the level's blocks
+            if dense:
+                w = x_t0.size(1) + self.channels[i] * self.filters[i]
+                dt = ops.DenseConcat(x_t0.size(0), w, x_t0)
+                ds = ops.DenseConcat(x_s0.size(0), w, x_s0)
+                dt.append(x_t0)
+                ds.append(x_s0)
+            for j in range(self.channels[i]):
+                if dense:
+                    x_t0, x_s0 = dt.view(), ds.view()
+                x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
+                conv = getattr(self, "NEConv{}{}".format(i, j))
+                if dense:
+                    _sink(conv, dt, ds, self.filters[i])
+                x_t, x_s = conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                edge_weight_s)
+                if dense:
+                    dt.append(x_t)
+                    ds.append(x_s)
+                else:
+                    x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                    x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            if dense:
+                x_t0, x_s0 = dt.view(), ds.view()
+            if self.att_every_level:
+                att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t0, x_s0, par_1, D)
+                x_t0 = x_t0 * att_t
+                x_s0 = x_s0 * att_s
+            if i == self.pool_loc:
+                if not self.att_every_level:
+                    att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t, x_s, par_1, D)
+                    att_t = att_t / att_t.max()
+                    att_s = att_s / att_s.max()
+                    x_t = x_t * att_t
+                    x_s = x_s * att_s
+                d1 = datas[k + 1]
+                x_t0 = cluster_mean(x_t0, pos_t, d1.x_t.shape[0])
+                x_s0 = cluster_mean(x_s0, pos_s, d1.x_s.shape[0])  # inf members dropped
+                edge_index_s, edge_weight_s = d1.edge_index_s, d1.edge_weight_s
+                edge_index_t, edge_weight_t = d1.edge_index_t, d1.edge_weight_t
+                k = 1
+                par_1 = adj2par1(d1.edge_index, x_t0.shape[0], x_s0.shape[0])
+                D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        dr = datas[min(len(self.channels) - 1, 1)]
+        x = torch.cat((mean_pool_sorted(x_s, dr.num_edge1),
+                       mean_pool_sorted(x_t, dr.num_node1)), -1)
+        for i, _ in enumerate(self.mlp_channels):
+            x = run_sequential(getattr(self, "mlp%d" % i), [x])
+        y = ops.linear_blocks([x], self.out.weight, self.out.bias)
+        if if_final_layer:
+            return x, y
+        if if_att:
+            return y, att_t, att_s
+        return y
+
+
+class HL_HGCNN_CIFAR10SP_dense_int3_attpool(_AttPoolHead):
+    """CIFAR10 superpixel classification head with attention pooling
+    (lib/Hodge_ST_Model.py:958-1091; BASELINE config 3 runs it with
+    channels=[2,2,2], filters=[64,128,256], mlp=[256], K=4, keig=10,
+    pool_loc=1, l=0.5, main_cifar10SP...:186-187)."""
+
+    def __init__(self, channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[], K=2,
+                 node_dim=5, l=0.5, edge_dim=4, num_classes=10, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, pool_loc=0, keig=10):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l,
+                         att_every_level=False)
+
+
+class HL_HGCNN_pepfunc_dense_int3_attpool(_AttPoolHead):
+    """Peptides-func head (main_pepfunc_HL_HGCNN_dense_int3_attpool.py:36-168,
+    the class BASELINE config 4 trains: NEAtt on the dense concatenation after
+    every level, l=0.5, sigmoid; structural pooling at pool_loc=1)."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=9, edge_dim=3, num_classes=10, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, pool_loc=0, keig=20):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, 0.5,
+                         att_every_level=True)
+
+    def forward(self, datas, device="cuda:0", if_att=False, if_final_layer=False):
+        # the pepfunc script orders the flags (if_att, if_final_layer) (:103)
+        return super().forward(datas, device, if_final_layer=if_final_layer, if_att=if_att)

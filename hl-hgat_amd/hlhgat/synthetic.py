@@ -15,9 +15,10 @@ import numpy as np
 import torch
 
 from .hodge_dataset import (PairData, collate, dense_to_sparse, halo_tiles, hodge_laplacians,
-                            locality_order)
+                            locality_order, mlgc)
 
-__all__ = ["zinc_like_graph", "zinc_like_batch", "molecule_edges"]
+__all__ = ["zinc_like_graph", "zinc_like_batch", "molecule_edges", "tsp_like_graph",
+           "cifar_like_graphs", "peptides_like_graphs", "two_level_batch", "knn_edges"]
 
 
 def molecule_edges(rng: np.random.Generator, n: int, extra_mean: float = 2.7) -> np.ndarray:
@@ -170,3 +171,71 @@ def zinc_like_batch(n_graphs: int, seed: int = 0, keig: int = 15,
                     check_hodge: bool = False):
     graphs: List[PairData] = [zinc_like_graph(seed * 1_000_003 + i, keig) for i in range(n_graphs)]
     return collate(graphs, check_hodge=check_hodge)
+
+
+# ----------------------------------------------------------------------------
+# two-level (MLGC) batches for the attention-pooling heads (configs 3 and 4)
+# ----------------------------------------------------------------------------
+def _two_level(ei: np.ndarray, n: int, x_t: torch.Tensor, x_s: torch.Tensor, y, seed: int):
+    """Level-0 PairData with the MLGC cluster of each node / edge in feature
+    column 0 (as CIFAR10SP_EigPE_MLGC.get / the pepfunc dataset prepend it,
+    main_cifar10SP...:101-105) and the coarse level-1 PairData."""
+    L0, L1, _, _ = hodge_laplacians(ei, n)
+    eit, ewt = dense_to_sparse(L0)
+    eis, ews = dense_to_sparse(L1)
+    g = PairData(x_s=x_s, edge_index_s=eis, edge_weight_s=ews, x_t=x_t, edge_index_t=eit,
+                 edge_weight_t=ewt, y=y)
+    g.edge_index = torch.from_numpy(ei)
+    g.num_node1 = n
+    g.num_edge1 = int(ei.shape[1])
+    g.num_nodes = n
+    g._hodge_sorted = True
+    coarse, c_node, c_edge = mlgc(g, seed=seed)
+    g.x_t = torch.cat([c_node, g.x_t], dim=-1)
+    g.x_s = torch.cat([c_edge, g.x_s], dim=-1)
+    return g, coarse
+
+
+def knn_edges(pts: np.ndarray, k: int) -> np.ndarray:
+    """Symmetric k-NN edge list (i<j, sorted, unique)."""
+    from scipy.spatial import cKDTree
+    n = pts.shape[0]
+    _, nbr = cKDTree(pts).query(pts, k=min(k + 1, n))
+    a = np.repeat(np.arange(n), nbr.shape[1] - 1)
+    b = nbr[:, 1:].reshape(-1)
+    i, j = np.minimum(a, b), np.maximum(a, b)
+    key = np.unique(i.astype(np.int64) * n + j)
+    return np.stack([key // n, key % n])
+
+
+def cifar_like_graphs(seed: int, n: int = 118, k: int = 8, keig: int = 10):
+    """CIFAR10 superpixel-like graph (BASELINE config 3): n
+    superpixels at uniform positions, symmetric 8-NN edges (~565 at n=118),
+    node features node_dim 5 + keig, edge features edge_dim 4 + keig
+    (lib/Hodge_ST_Model.py:958-961), one MLGC level.  Returns (level0, level1)."""
+    rng = np.random.default_rng(seed)
+    ei = knn_edges(rng.random((n, 2)), k)
+    x_t = torch.from_numpy(rng.standard_normal((n, 5 + keig)).astype(np.float32))
+    x_s = torch.from_numpy(rng.standard_normal((ei.shape[1], 4 + keig)).astype(np.float32))
+    return _two_level(ei, n, x_t, x_s, torch.tensor([int(rng.integers(10))]), seed)
+
+
+def peptides_like_graphs(seed: int, keig: int = 20):
+    """Peptides-func-like molecule (BASELINE config 4, SURVEY §8d: ~151 atoms,
+    ~154 bonds): node features 9 + keig, edge features 3 + keig
+    (main_pepfunc...:37-39), 10 binary labels, one MLGC level."""
+    rng = np.random.default_rng(seed)
+    n = int(np.clip(round(rng.normal(150.9, 20.0)), 40, 300))
+    ei = molecule_edges(rng, n)
+    x_t = torch.from_numpy(rng.standard_normal((n, 9 + keig)).astype(np.float32))
+    x_s = torch.from_numpy(rng.standard_normal((ei.shape[1], 3 + keig)).astype(np.float32))
+    y = torch.from_numpy(rng.integers(0, 2, (1, 10)).astype(np.float32))
+    return _two_level(ei, n, x_t, x_s, y, seed)
+
+
+def two_level_batch(kind: str, n_graphs: int, seed: int = 0, **kw):
+    """datas = [level-0 batch, level-1 batch] as the attpool heads take them."""
+    make = {"cifar": cifar_like_graphs, "peptides": peptides_like_graphs}[kind]
+    pairs = [make(seed * 1_000_003 + i, **kw) for i in range(n_graphs)]
+    return [collate([p[0] for p in pairs], check_hodge=False),
+            collate([p[1] for p in pairs], check_hodge=False)]

@@ -697,3 +697,50 @@ def test_halo_conv_fwd_bwd_bitwise(cuda):
         conv.zero_grad()
     for a, c in zip(*outs):
         assert torch.equal(a, c)
+
+
+def _attpool_case(cuda, name, cls, **kw):
+    import re
+    from hlhgat.hodge_dataset import Batch
+    g = load_golden(name)
+    m = cls(**kw)
+    m.load_state_dict({k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")})
+    m = m.to(cuda).train()
+    datas = []
+    for lv in range(2):
+        b = Batch()
+        for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s",
+                  "edge_weight_s", "edge_index", "num_node1", "num_edge1"):
+            setattr(b, k, dev(g[f"l{lv}/{k}"]))
+        datas.append(b)
+    out = m(datas)
+    close(out.detach().cpu(), g["out"], 1e-4, "out")
+    (out * dev(g["R"])).sum().backward()
+    for k, p in m.named_parameters():
+        if "nograd/" + k in g:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
+            continue
+        if re.search(r"module_[04]\.bias$", k) or re.search(r"mlp\d+\.0\.bias$", k):
+            # bias feeding a training-mode BatchNorm: analytically zero gradient
+            assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
+            continue
+        close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
+
+
+def test_attpool_cifar_model_vs_reference_golden(cuda):
+    """HL_HGCNN_CIFAR10SP_dense_int3_attpool (lib/Hodge_ST_Model.py:958-1091,
+    config 3 head): two MLGC levels, NEAtt(ReLU) / batch max at pool_loc,
+    inf-masked cluster means, level switch, readout; reference forward and
+    every parameter gradient within 1e-4 relative."""
+    import hlhgat
+    _attpool_case(cuda, "attpool_cifar_small", hlhgat.HL_HGCNN_CIFAR10SP_dense_int3_attpool,
+                  channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10,
+                  pool_loc=0, l=0.5)
+
+
+def test_attpool_pepfunc_model_vs_reference_golden(cuda):
+    """HL_HGCNN_pepfunc_dense_int3_attpool (main_pepfunc...:36-168, config 4
+    head): NEAtt(sigmoid, l=0.5) on the dense concatenation after every level."""
+    import hlhgat
+    _attpool_case(cuda, "attpool_pepfunc_small", hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool,
+                  channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)

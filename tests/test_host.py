@@ -286,3 +286,57 @@ def test_halo_tiles_reject_and_collate():
     ht = {k: getattr(b, k + "_s") for k in ("halo_tile_ptr", "halo_ptr", "halo", "halo_srp",
                                              "halo_lcol", "halo_eperm", "halo_hdr")}
     _check_halo(b.edge_index_s.numpy(), b.x_s.shape[0], b.row_order_s.numpy(), ht, 128, 256)
+
+
+def test_mlgc_matches_reference_golden():
+    """MLGC (lib/Hodge_Dataset.py:241-297) against the reference's own MLGC run
+    on the same graphs (tests/golden/make_golden_attpool.py).  torch_cluster is
+    absent, so the reference's graclus call was answered by hlhgat's graclus
+    restatement (labels stored): graclus itself is parity unpinned; renumbering,
+    edge assignment (inf = contracted edge), coarse B1 and L0/L1 are pinned."""
+    from hlhgat.hodge_dataset import PairData, graclus, mlgc
+    g = load_golden("mlgc_small")
+    for gi in range(3):
+        p = f"g{gi}/"
+        n = int(g[p + "num_node1"])
+        ei, eit = g[p + "edge_index"], g[p + "edge_index_t"]
+        assert np.array_equal(graclus(eit, n, seed=gi), g[p + "graclus"])
+        d = PairData(x_s=torch.zeros(ei.shape[1], 1), x_t=torch.zeros(n, 1),
+                     edge_index_t=torch.from_numpy(eit))
+        d.edge_index = torch.from_numpy(ei)
+        d.num_node1 = n
+        coarse, c_node, c_edge = mlgc(d, seed=gi)
+        assert np.array_equal(c_node.numpy().reshape(-1), g[p + "c_node"].reshape(-1))
+        ce, ref_ce = c_edge.numpy().reshape(-1), g[p + "c_edge"].reshape(-1)
+        assert np.array_equal(np.isinf(ce), np.isinf(ref_ce))
+        assert np.array_equal(ce[~np.isinf(ce)], ref_ce[~np.isinf(ref_ce)])
+        assert coarse.num_node1 == int(g[p + "coarse/num_node1"])
+        for k in ("edge_index", "edge_index_t", "edge_index_s"):
+            assert np.array_equal(getattr(coarse, k).numpy(), g[p + "coarse/" + k]), k
+        for k in ("edge_weight_t", "edge_weight_s", "x_t", "x_s"):
+            np.testing.assert_allclose(getattr(coarse, k).numpy(), g[p + "coarse/" + k],
+                                       rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_graclus_is_a_matching():
+    """Every graclus cluster has one or two members, a pair is joined by an
+    edge, its id is the smaller member, and no two unmatched neighbours remain
+    (greedy maximality, torch_cluster 1.6.0 graclus semantics)."""
+    from hlhgat.hodge_dataset import graclus
+    from hlhgat.synthetic import knn_edges
+    rng = np.random.default_rng(3)
+    ei = knn_edges(rng.random((300, 2)), 6)
+    sym = np.concatenate([ei, ei[::-1]], axis=1)
+    lab = graclus(sym, 300, seed=1)
+    adj = set(map(tuple, sym.T.tolist()))
+    alone = []
+    for c in np.unique(lab):
+        mem = np.flatnonzero(lab == c)
+        assert 1 <= mem.size <= 2 and c == mem.min()
+        if mem.size == 2:
+            assert (int(mem[0]), int(mem[1])) in adj
+        else:
+            alone.append(int(mem[0]))
+    alone = set(alone)
+    for u, v in adj:
+        assert not (u in alone and v in alone and u != v)
