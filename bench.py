@@ -122,10 +122,12 @@ def cfg5_spmm(device, reps=20):
     from hlhgat.synthetic import tsp_like_graph
     b = collate([tsp_like_graph(s) for s in range(4)], check_hodge=False).to(device)
     n, nnz = b.x_s.shape[0], b.edge_index_s.shape[1]
-    A = ops.hodge_operator(b.edge_index_s, b.edge_weight_s, n).fwd
+    op = ops.hodge_operator(b.edge_index_s, b.edge_weight_s, n)
+    A = op.fwd
     out = {"config": f"BASELINE configs[4]: 4 TSP-like graphs (10k nodes, k=9 NN), L1 n={n} "
                      f"nnz={nnz}; RCM row schedule + LDS halo tiles "
-                     f"({'on' if A.halo is not None else 'off'})",
+                     f"({'on' if A.halo is not None else 'off'}); factored L1 "
+                     f"({'on' if op.factor is not None else 'off'})",
            "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     for d in (64, 128):
         X = torch.randn(n, d, device=device)
@@ -146,6 +148,42 @@ def cfg5_spmm(device, reps=20):
             gbs = p["bytes"] / (p["ms"] * 1e-3) / 1e9
             out[f"{what}_d{d}"] = {"achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
                                    "avg_launch_us": round(p["ms"] * 1e3 / p["launches"], 1)}
+        if op.factor is None:
+            continue
+        # factored L1 = alpha B1^T B1 (hlhgat_hodge_factor_t): stage 1 (B1 X, node
+        # rows) + stage 2 (fused edge step); "equiv" = the SpMM problem's
+        # algorithmic bytes over the two launches' summed time, "own" = each
+        # stage's own algorithmic bytes over its time
+        work = torch.empty(int(hlhgat._lib.LIB.hlhgat_hodge_factor_work_floats(
+            op.factor_nodes, d)), device=device)
+        for what, kw, by in (
+                ("spmm", {}, 8 * nnz + 4 * (n + 1) + 8 * n * d),
+                ("laguerre_step", dict(Z=Z, alpha=-1.0, beta=5.0, gamma=-2.0, div=3.0),
+                 8 * nnz + 4 * (n + 1) + 12 * n * d)):
+            for _ in range(3):
+                ops._hodge_step(op, X, Y, work=work, **kw)
+            torch.cuda.synchronize()
+            ops.prof_reset()
+            classes = (hlhgat._lib.PROF_HODGE_NODE, hlhgat._lib.PROF_HODGE_EDGE)
+            for c in classes:
+                ops.prof_enable(c, True)
+            for _ in range(reps):
+                ops._hodge_step(op, X, Y, work=work, **kw)
+            torch.cuda.synchronize()
+            for c in classes:
+                ops.prof_enable(c, False)
+            pn, pe = (ops.prof_read(c) for c in classes)
+            us = (pn["ms"] + pe["ms"]) * 1e3 / reps
+            gbs = by / us / 1e3
+            out[f"factored_{what}_d{d}"] = {
+                "equiv_achieved": round(gbs, 1), "equiv_frac": round(gbs / HBM_PEAK_GBS, 4),
+                "us": round(us, 1),
+                "stage1_node": {"us": round(pn["ms"] * 1e3 / reps, 1),
+                                "own_frac": round(pn["bytes"] / (pn["ms"] * 1e-3) / 1e9
+                                                  / HBM_PEAK_GBS, 4)},
+                "stage2_edge": {"us": round(pe["ms"] * 1e3 / reps, 1),
+                                "own_frac": round(pe["bytes"] / (pe["ms"] * 1e-3) / 1e9
+                                                  / HBM_PEAK_GBS, 4)}}
     return out
 
 

@@ -46,6 +46,9 @@ struct PolyArgs {
   int64_t n_tiles;
   int max_halo, max_trows, max_tnnz, halo_fs;
   int nt_store;  // streaming (non-temporal) stores of Y: keep L2 for the gathered X rows
+  // Hodge-factored L1 edge step (k_hodge_edge_step): X = Z = B1 T (node rows)
+  const int2* ends;     // [n_rows] (i, j) of each edge
+  const float* ealpha;  // [n_rows] alpha_e = L1[e,e] / 2
 };
 
 // Row r's CSR entries are staged LPR at a time: lane `sub` of the row group
@@ -163,6 +166,63 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
     }
     if (!fok) continue;
     poly_epilogue<V>(a, row, f, acc, rsv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Second factor of the Hodge-factored L1 (hlhgat_hodge_factor_t):
+//   acc = alpha_e (Z[j] - Z[i]) = (-alpha_e) Z[i] + alpha_e Z[j]
+// (the CSR order of row e of alpha B1^T), then the same epilogue as
+// k_poly_step, so a factored Laguerre / Chebyshev step applies the
+// recurrence exactly as the CSR step does; the B operand carries T_k.
+// One lane group per edge: the edge's two node rows are the only gathers and
+// both are issued before any arithmetic (no rowptr / col hop).
+// ---------------------------------------------------------------------------
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_hodge_edge_step(PolyArgs a) {
+  using vt = typename VecT<V>::type;
+  // kEpg edges per lane group: their ends, then all 2 kEpg node-row gathers,
+  // are in flight together (the kernel is a latency chain ends -> Z -> Y;
+  // one edge per group left most of the HBM write bandwidth idle)
+  constexpr int kEpg = 4;
+  const int64_t grp = ((int64_t)xcd_slot(blockIdx.x, gridDim.x) * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  const int64_t s0 = grp * kEpg;
+  if (s0 >= a.n_rows) return;  // no cross-lane operations below
+  int64_t e[kEpg];
+  int2 ij[kEpg];
+  float al[kEpg];
+#pragma unroll
+  for (int u = 0; u < kEpg; ++u) {
+    const int64_t sl = s0 + u < a.n_rows ? s0 + u : s0;
+    e[u] = a.order ? (int64_t)a.order[sl] : sl;
+  }
+#pragma unroll
+  for (int u = 0; u < kEpg; ++u) {
+    ij[u] = a.ends[e[u]];
+    al[u] = a.ealpha[e[u]];
+  }
+  const float* __restrict__ Z = a.X;
+  for (int f = sub * V; f < a.d; f += LPR * V) {
+    vt zi[kEpg], zj[kEpg];
+#pragma unroll
+    for (int u = 0; u < kEpg; ++u) {
+      zi[u] = vload<V>(Z + (int64_t)ij[u].x * a.ldx + f);
+      zj[u] = vload<V>(Z + (int64_t)ij[u].y * a.ldx + f);
+    }
+#pragma unroll
+    for (int u = 0; u < kEpg; ++u) {
+      if (s0 + u >= a.n_rows) break;
+      vt acc;
+#pragma unroll
+      for (int c = 0; c < V; ++c) {
+        float s = 0.f;
+        s = s + (-al[u]) * vget(zi[u], c);
+        s = s + al[u] * vget(zj[u], c);
+        vget(acc, c) = s;
+      }
+      poly_epilogue<V>(a, e[u], f, acc, 1.f);
+    }
   }
 }
 
@@ -837,7 +897,8 @@ constexpr size_t kHaloImgBytes = 32 * 1024;
 constexpr double kNtStoreBytes = 48.0 * 1024 * 1024;
 constexpr size_t kHaloLdsBytes = 64 * 1024;
 
-int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
+int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s, int prof_class = HLHGAT_PROF_POLY,
+                double prof_bytes = -1.0) {
   HLH_CHECK_ARG(a.n_rows >= 0 && a.n_rows < (int64_t)INT32_MAX,
                 "poly_step: n_rows out of range");
   HLH_CHECK_ARG(a.d > 0, "poly_step: d must be > 0");
@@ -862,7 +923,7 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s) {
   // HLHGAT_NT=0/1 forces either way (A/B).
   static const int nt_env = getenv("HLHGAT_NT") ? atoi(getenv("HLHGAT_NT")) : -1;
   a.nt_store = nt_env >= 0 ? nt_env : ((double)a.n_rows * a.d * 4.0 >= kNtStoreBytes);
-  ProfScope prof(HLHGAT_PROF_POLY, s, poly_bytes(a, nnz),
+  ProfScope prof(prof_class, s, prof_bytes >= 0.0 ? prof_bytes : poly_bytes(a, nnz),
                  2.0 * (double)nnz * a.d);
   if (a.lcol && a.n_tiles > 0) {
     // slice width FS = v * lh: the widest power of two whose halo image fits
@@ -942,6 +1003,66 @@ PolyArgs make_args(const int32_t* rowptr, const int32_t* col, const float* val,
   return a;
 }
 
+// One application of the Hodge-factored L1 inside a poly step `a` (built as
+// for the CSR path: a.X = the SpMM operand, epilogue fields set):
+//   stage 1: work = B1 a.X            (k_poly_step over the signed incidence)
+//   stage 2: a.Y = epilogue(alpha B1^T work)   (k_hodge_edge_step)
+// The beta term keeps reading the ORIGINAL operand (a.B), as the CSR step
+// reads X.
+int launch_factored(PolyArgs a, const hlhgat_hodge_factor_t& f, float* work, hipStream_t s) {
+  HLH_CHECK_ARG(f.node_rowptr && f.ends && f.alpha && work && a.n_rows == f.n_edges &&
+                    (f.n_edges == 0 || (f.node_edge && f.node_sign)),
+                "hodge factor: incomplete descriptor or row count %lld != n_edges %lld",
+                (long long)a.n_rows, (long long)f.n_edges);
+  HLH_CHECK_ARG(!a.rs, "hodge factor: row scale not supported");
+  if (a.n_rows == 0) return HLHGAT_OK;
+  if (a.beta != 0.f && !a.B) {
+    a.B = a.X;
+    a.ldb = a.ldx;
+  }
+  {
+    PolyArgs b = make_args(f.node_rowptr, f.node_edge, f.node_sign, f.n_nodes, a.X, a.ldx, a.d,
+                           work, a.d, f.node_order);
+    // own algorithmic bytes: incidence CSR, the E edge rows of X read once, Z written
+    const double b1 = 16.0 * (double)f.n_edges + 4.0 * (double)(f.n_nodes + 1) +
+                      4.0 * (double)(f.n_edges + f.n_nodes) * a.d;
+    int rc = launch_poly(b, 2 * f.n_edges, s, HLHGAT_PROF_HODGE_NODE, b1);
+    if (rc) return rc;
+  }
+  a.X = work;
+  a.ldx = a.d;
+  a.order = f.edge_order;
+  a.ends = reinterpret_cast<const int2*>(f.ends);
+  a.ealpha = f.alpha;
+  a.lcol = nullptr;
+  a.n_tiles = 0;
+  const int v = pick_vec(a.d, {a.ldx, a.ldy, a.Z ? a.ldz : 4, a.P ? a.ldp : 4, a.Q ? a.ldq : 4,
+                               a.B ? a.ldb : 4},
+                         {a.X, a.Y, a.Z, a.P, a.Q, a.B});
+  const int l = pick_lpr(a.d, v);
+  static const int nt_env = getenv("HLHGAT_NT") ? atoi(getenv("HLHGAT_NT")) : -1;
+  a.nt_store = nt_env >= 0 ? nt_env : ((double)a.n_rows * a.d * 4.0 >= kNtStoreBytes);
+  // own algorithmic bytes: ends + alpha, Z read once, Y and the dense epilogue operands
+  int dense = 1 + (a.beta != 0.f) + (a.Z != nullptr) + (a.P != nullptr) + (a.Q != nullptr);
+  ProfScope prof(HLHGAT_PROF_HODGE_EDGE, s,
+                 12.0 * (double)a.n_rows + 4.0 * (double)(f.n_nodes + dense * a.n_rows) * a.d,
+                 4.0 * (double)a.n_rows * a.d);
+  HLH_DISPATCH_VL(v, l, k_hodge_edge_step, ceil_div(a.n_rows, (int64_t)4), s, a, &prof);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+// Runs one poly step on the CSR operator, or factored when fac != NULL.
+struct StepRunner {
+  int64_t nnz;
+  const hlhgat_hodge_factor_t* fac;
+  float* work;
+  hipStream_t s;
+  int operator()(PolyArgs& a) const {
+    return fac ? launch_factored(a, *fac, work, s) : launch_poly(a, nnz, s);
+  }
+};
+
 }  // namespace
 
 using namespace hlhgat;
@@ -982,15 +1103,12 @@ extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
   return launch_poly(a, nnz, as_stream(stream));
 }
 
-extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
-                                     const int32_t* col, const float* val,
-                                     int64_t n, int64_t nnz,
-                                     const int32_t* row_order, const hlhgat_halo_t* halo,
-                                     const int32_t* tile_ptr,
-                                     int64_t n_tiles, int64_t max_tile_rows,
-                                     int64_t max_tile_nnz, const float* X,
-                                     int64_t ldx, int64_t F, int K, float* T,
-                                     void* stream) {
+namespace {
+int basis_fwd_core(int kind, const int32_t* rowptr, const int32_t* col, const float* val,
+                   int64_t n, int64_t nnz, const int32_t* row_order, const hlhgat_halo_t* halo,
+                   const int32_t* tile_ptr, int64_t n_tiles, int64_t max_tile_rows,
+                   int64_t max_tile_nnz, const float* X, int64_t ldx, int64_t F, int K, float* T,
+                   const hlhgat_hodge_factor_t* fac, float* work, void* stream) {
   HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB ||
                     kind == HLHGAT_POLY_LAGUERRE_DEMO,
                 "poly_basis_fwd: bad kind %d", kind);
@@ -998,8 +1116,9 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
   if (K == 1 || n == 0) return HLHGAT_OK;
   HLH_CHECK_ARG(T, "poly_basis_fwd: T is NULL");
   hipStream_t s = as_stream(stream);
-  if (launch_local(true, kind, rowptr, col, val, n, nnz, tile_ptr, n_tiles, max_tile_rows,
-                   max_tile_nnz, X, ldx, F, K, T, s)) {
+  const StepRunner run{nnz, fac, work, s};
+  if (!fac && launch_local(true, kind, rowptr, col, val, n, nnz, tile_ptr, n_tiles, max_tile_rows,
+                           max_tile_nnz, X, ldx, F, K, T, s)) {
     HLH_CHECK_LAUNCH();
     return HLHGAT_OK;
   }
@@ -1012,7 +1131,7 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
       a.alpha = -1.f;
       a.beta = 1.f;
     }  // Cheb: Tx_1 = L x   (:416)
-    int rc = launch_poly(a, nnz, s);
+    int rc = run(a);
     if (rc) return rc;
   }
   for (int k = 1; k + 1 < K; ++k) {
@@ -1044,20 +1163,17 @@ extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr,
       a.alpha = 2.f;
       a.gamma = -1.f;
     }
-    int rc = launch_poly(a, nnz, s);
+    int rc = run(a);
     if (rc) return rc;
   }
   return HLHGAT_OK;
 }
 
-extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
-                                     const int32_t* col_t, const float* val_t,
-                                     int64_t n, int64_t nnz,
-                                     const int32_t* row_order, const hlhgat_halo_t* halo,
-                                     const int32_t* tile_ptr,
-                                     int64_t n_tiles, int64_t max_tile_rows,
-                                     int64_t max_tile_nnz, int64_t F, int K,
-                                     float* G, void* stream) {
+int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
+                   const float* val_t, int64_t n, int64_t nnz, const int32_t* row_order,
+                   const hlhgat_halo_t* halo, const int32_t* tile_ptr, int64_t n_tiles,
+                   int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F, int K, float* G,
+                   const hlhgat_hodge_factor_t* fac, float* work, void* stream) {
   HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB ||
                     kind == HLHGAT_POLY_LAGUERRE_DEMO,
                 "poly_basis_bwd: bad kind %d", kind);
@@ -1065,7 +1181,8 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
   if (K == 1 || n == 0) return HLHGAT_OK;
   HLH_CHECK_ARG(G, "poly_basis_bwd: G is NULL");
   hipStream_t s = as_stream(stream);
-  if (launch_local(false, kind, rowptr_t, col_t, val_t, n, nnz, tile_ptr, n_tiles,
+  const StepRunner run{nnz, fac, work, s};
+  if (!fac && launch_local(false, kind, rowptr_t, col_t, val_t, n, nnz, tile_ptr, n_tiles,
                    max_tile_rows,
                    max_tile_nnz, nullptr, F, F, K, G, s)) {
     HLH_CHECK_LAUNCH();
@@ -1086,7 +1203,7 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
     a.P = Gk(0);
     a.ldp = F;
     a.p = 1.f;
-    return launch_poly(a, nnz, s);
+    return run(a);
   }
   for (int k = K - 1; k >= 1; --k) {
     PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F, row_order, halo);
@@ -1108,10 +1225,86 @@ extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
       a.alpha = (k == 1) ? 1.f : 2.f;
       a.q = -1.f;
     }
-    int rc = launch_poly(a, nnz, s);
+    int rc = run(a);
     if (rc) return rc;
   }
   return HLHGAT_OK;
+}
+
+}  // namespace
+
+extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
+                                     const float* val, int64_t n, int64_t nnz,
+                                     const int32_t* row_order, const hlhgat_halo_t* halo,
+                                     const int32_t* tile_ptr, int64_t n_tiles,
+                                     int64_t max_tile_rows, int64_t max_tile_nnz,
+                                     const float* X, int64_t ldx, int64_t F, int K, float* T,
+                                     void* stream) {
+  return basis_fwd_core(kind, rowptr, col, val, n, nnz, row_order, halo, tile_ptr, n_tiles,
+                        max_tile_rows, max_tile_nnz, X, ldx, F, K, T, nullptr, nullptr, stream);
+}
+
+extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t, const int32_t* col_t,
+                                     const float* val_t, int64_t n, int64_t nnz,
+                                     const int32_t* row_order, const hlhgat_halo_t* halo,
+                                     const int32_t* tile_ptr, int64_t n_tiles,
+                                     int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F,
+                                     int K, float* G, void* stream) {
+  return basis_bwd_core(kind, rowptr_t, col_t, val_t, n, nnz, row_order, halo, tile_ptr,
+                        n_tiles, max_tile_rows, max_tile_nnz, F, K, G, nullptr, nullptr, stream);
+}
+
+extern "C" int64_t hlhgat_hodge_factor_work_floats(int64_t n_nodes, int64_t F) {
+  return n_nodes > 0 && F > 0 ? n_nodes * F : 1;
+}
+
+extern "C" int hlhgat_hodge_spmm(const hlhgat_hodge_factor_t* f, const float* X, int64_t ldx,
+                                 int64_t d, float* Y, int64_t ldy, float* work, void* stream) {
+  HLH_CHECK_ARG(f, "hodge_spmm: NULL factor");
+  HLH_CHECK_ARG(d > 0 && ldx >= d && ldy >= d && X && Y, "hodge_spmm: bad operands");
+  PolyArgs a = make_args(nullptr, nullptr, nullptr, f->n_edges, X, ldx, d, Y, ldy);
+  return launch_factored(a, *f, work, as_stream(stream));
+}
+
+extern "C" int hlhgat_hodge_poly_step(const hlhgat_hodge_factor_t* f, const float* X,
+                                      int64_t ldx, int64_t d, const float* Z, int64_t ldz,
+                                      const float* P, int64_t ldp, const float* Q, int64_t ldq,
+                                      float alpha, float beta, float gamma, float div, float p,
+                                      float q, float* Y, int64_t ldy, float* work, void* stream) {
+  HLH_CHECK_ARG(f, "hodge_poly_step: NULL factor");
+  HLH_CHECK_ARG(d > 0 && ldx >= d && ldy >= d && X && Y && (!Z || ldz >= d) &&
+                    (!P || ldp >= d) && (!Q || ldq >= d) && div != 0.f,
+                "hodge_poly_step: bad operands");
+  PolyArgs a = make_args(nullptr, nullptr, nullptr, f->n_edges, X, ldx, d, Y, ldy);
+  a.Z = Z;
+  a.ldz = ldz;
+  a.P = P;
+  a.ldp = ldp;
+  a.Q = Q;
+  a.ldq = ldq;
+  a.alpha = alpha;
+  a.beta = beta;
+  a.gamma = gamma;
+  a.div = div;
+  a.p = p;
+  a.q = q;
+  return launch_factored(a, *f, work, as_stream(stream));
+}
+
+extern "C" int hlhgat_poly_basis_fwd_factored(int kind, const hlhgat_hodge_factor_t* f,
+                                              const float* X, int64_t ldx, int64_t F, int K,
+                                              float* T, float* work, void* stream) {
+  HLH_CHECK_ARG(f, "poly_basis_fwd_factored: NULL factor");
+  return basis_fwd_core(kind, nullptr, nullptr, nullptr, f->n_edges, 0, nullptr, nullptr,
+                        nullptr, 0, 0, 0, X, ldx, F, K, T, f, work, stream);
+}
+
+extern "C" int hlhgat_poly_basis_bwd_factored(int kind, const hlhgat_hodge_factor_t* f,
+                                              int64_t F, int K, float* G, float* work,
+                                              void* stream) {
+  HLH_CHECK_ARG(f, "poly_basis_bwd_factored: NULL factor");
+  return basis_bwd_core(kind, nullptr, nullptr, nullptr, f->n_edges, 0, nullptr, nullptr,
+                        nullptr, 0, 0, 0, F, K, G, f, work, stream);
 }
 
 extern "C" int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,

@@ -112,6 +112,32 @@ hlhgat_halo_t make_halo(const Tensor& tile, const Tensor& ptr, const Tensor& col
   return h;
 }
 
+// hlhgat_hodge_factor_t over the factor tensors of an L1 operator
+// (hlhgat.ops.set_hodge_factor): {node_rowptr, node_edge, node_sign,
+// node_order, ends, alpha, edge_order}; an undefined / empty order = natural.
+hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_edges) {
+  hlhgat_hodge_factor_t h{};
+  TORCH_CHECK(f.size() == 7, "hlhgat: hodge factor needs 7 tensors");
+  auto opt_i = [](const Tensor& t) -> const int32_t* {
+    return (t.defined() && t.numel() > 0) ? t.data_ptr<int>() : nullptr;
+  };
+  TORCH_CHECK(f[0].scalar_type() == at::kInt && f[1].scalar_type() == at::kInt &&
+                  f[2].scalar_type() == at::kFloat && f[4].scalar_type() == at::kInt &&
+                  f[5].scalar_type() == at::kFloat && f[0].numel() == n_nodes + 1 &&
+                  f[4].numel() == 2 * n_edges && f[5].numel() == n_edges,
+              "hlhgat: bad hodge factor tensors");
+  h.node_rowptr = f[0].data_ptr<int>();
+  h.node_edge = n_edges ? f[1].data_ptr<int>() : nullptr;
+  h.node_sign = n_edges ? f[2].data_ptr<float>() : nullptr;
+  h.node_order = opt_i(f[3]);
+  h.n_nodes = n_nodes;
+  h.ends = f[4].data_ptr<int>();
+  h.alpha = f[5].data_ptr<float>();
+  h.edge_order = opt_i(f[6]);
+  h.n_edges = n_edges;
+  return h;
+}
+
 // One BN workspace per (device, stream): its arrival counters must not be
 // shared by launches that can run concurrently (node / edge chains run on two
 // streams, see hlhgat.ops.fork).  Stream-ordered reuse on one stream is safe.
@@ -269,7 +295,8 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order,
                         OptT tiles, int64_t tile_rows, int64_t tile_nnz, OptT valid,
                         OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol,
-                        OptT h_sval, std::vector<int64_t> h_bounds, OptT h_hdr) {
+                        OptT h_sval, std::vector<int64_t> h_bounds, OptT h_hdr,
+                        at::TensorList fac, int64_t fac_nodes) {
     req(x, "x");
     const int64_t N = x.size(0);
     const int64_t Cin = x.size(-1);
@@ -287,7 +314,14 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
         use_halo ? make_halo(*h_tile, *h_ptr, *h_cols, *h_srp, *h_lcol,
                              has(h_sval) ? *h_sval : Tensor(), h_bounds, *h_hdr)
                  : hlhgat_halo_t{};
-    if (K > 1 && N > 0) {
+    const bool factored = !fac.empty();
+    if (factored && K > 1 && N > 0) {
+      const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
+      Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x.options());
+      chk(hlhgat_poly_basis_fwd_factored((int)kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
+                                         (int)K, T.data_ptr<float>(), work.data_ptr<float>(), s),
+          "poly_basis_fwd_factored");
+    } else if (K > 1 && N > 0) {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
                                 nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
@@ -367,7 +401,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       em.opt(h_sval);
       em.other();
       em.opt(h_hdr);
+      em.list(fac);
+      em.other();
       ctx->saved_data["edges"] = em.e;
+      ctx->saved_data["fac_nodes"] = fac_nodes;
       ctx->saved_data["tile_rows"] = tile_rows;
       ctx->saved_data["tile_nnz"] = tile_nnz;
       ctx->saved_data["h_bounds"] = h_bounds;
@@ -397,6 +434,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                 (halo_bwd && has(h_sval)) ? *h_sval : Tensor(),
                                 halo_bwd ? *h_hdr : Tensor()};
     for (const auto& w : W) save.push_back(w);
+    for (const auto& t : fac) save.push_back(t);
     ctx->save_for_backward(save);
     std::vector<int64_t> oshape = x.sizes().vec();
     oshape.back() = dout;
@@ -415,7 +453,9 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
            mean = sv[10], invstd = sv[11], bn_w = sv[12], bias_p = sv[13], bn_b = sv[14],
            h_tile = sv[15], h_ptr = sv[16], h_cols = sv[17], h_srp = sv[18], h_lcol = sv[19],
            h_sval = sv[20], h_hdr = sv[21];
-    std::vector<Tensor> W(sv.begin() + 22, sv.end());
+    std::vector<Tensor> W(sv.begin() + 22, sv.begin() + 22 + K);
+    std::vector<Tensor> fac(sv.begin() + 22 + K, sv.end());
+    const int64_t fac_nodes = ctx->saved_data["fac_nodes"].toInt();
     const bool use_halo = h_lcol.defined();
     const hlhgat_halo_t halo =
         use_halo ? make_halo(h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval,
@@ -428,7 +468,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
     // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
     //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 33 + K;
+    const int64_t n_pos = 33 + K + (int64_t)fac.size() + 1;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
     Tensor dbn_w, dbn_b;
@@ -483,7 +523,13 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
           dA[k] = Gs.data_ptr<float>() + k * N * F;
         }
         proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
-        if (K > 1) {
+        if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
+          const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
+          Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x2.options());
+          chk(hlhgat_poly_basis_bwd_factored((int)kind, &hf, F, (int)K, Gs.data_ptr<float>(),
+                                             work.data_ptr<float>(), s),
+              "poly_basis_bwd_factored");
+        } else if (K > 1) {
           chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
                                     nnz ? t_col.data_ptr<int>() : nullptr,
                                     (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
@@ -1140,12 +1186,13 @@ Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_row
                int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT tiles,
                int64_t tile_rows, int64_t tile_nnz, OptT valid, OptT h_tile, OptT h_ptr,
                OptT h_cols, OptT h_srp, OptT h_lcol, OptT h_sval,
-               std::vector<int64_t> h_bounds, OptT h_hdr) {
+               std::vector<int64_t> h_bounds, OptT h_hdr, std::vector<Tensor> fac,
+               int64_t fac_nodes) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
                          bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz,
                          valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds,
-                         h_hdr);
+                         h_hdr, at::TensorList(fac), fac_nodes);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

@@ -46,6 +46,14 @@ SIGNATURES = {
                                       c_vp, c_vp]),
     "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                       c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp]),
+    "hlhgat_hodge_factor_work_floats": (c_i64, [c_i64, c_i64]),
+    "hlhgat_hodge_spmm": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "hlhgat_hodge_poly_step": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                       c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_vp,
+                                       c_i64, c_vp, c_vp]),
+    "hlhgat_poly_basis_fwd_factored": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_i64, c_i32, c_vp,
+                                               c_vp, c_vp]),
+    "hlhgat_poly_basis_bwd_factored": (c_i32, [c_i32, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
@@ -81,7 +89,7 @@ SIGNATURES = {
 # constants from include/hlhgat.h
 POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
-PROF_POLY, PROF_PROJ = 0, 1
+PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
 MAX_BLOCKS = 16
 
 
@@ -90,6 +98,13 @@ class HaloDesc(C.Structure):
     _fields_ = [("hdr", c_vp), ("tile_ptr", c_vp), ("halo_ptr", c_vp), ("halo", c_vp), ("srp", c_vp),
                 ("lcol", c_vp), ("sval", c_vp), ("n_tiles", c_i64), ("max_halo", c_i32),
                 ("max_rows", c_i32), ("max_nnz", c_i32)]
+
+
+class HodgeFactorDesc(C.Structure):
+    """hlhgat_hodge_factor_t (include/hlhgat.h)."""
+    _fields_ = [("node_rowptr", c_vp), ("node_edge", c_vp), ("node_sign", c_vp),
+                ("node_order", c_vp), ("n_nodes", c_i64), ("ends", c_vp), ("alpha", c_vp),
+                ("edge_order", c_vp), ("n_edges", c_i64)]
 
 
 class HlhgatError(RuntimeError):

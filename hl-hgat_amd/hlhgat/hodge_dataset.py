@@ -111,6 +111,10 @@ class Batch(PairData):
                     and self.hodge_sorted.get(k, False)):
                 set_halo(t, hk)
         ei = getattr(self, "edge_index", None)
+        eis = getattr(self, "edge_index_s", None)
+        if (getattr(self, "l1_factor", False) and torch.is_tensor(ei) and ei.is_cuda
+                and torch.is_tensor(eis) and eis.is_cuda):
+            ops.set_hodge_factor(eis, ei, self.x_t.size(0), getattr(self, "row_order_t", None))
         if torch.is_tensor(ei) and ei.is_cuda:
             for kv in ("n_valid_t", "n_valid_s"):
                 nv = getattr(self, kv, None)
@@ -318,6 +322,8 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
             ok = all(getattr(g, "_hodge_sorted", False) for g in graphs)
         hs[k] = ok
     b.hodge_sorted = hs
+    # factored L1 for large high-degree edge Laplacians (hlhgat.h, hodge factor)
+    b.l1_factor = bool(hs.get("edge_index_s")) and _factor_wanted(graphs)
     for side in ("s", "t"):
         _collate_halo(b, graphs, side)
     # whole-graph row tiles for the graph-local polynomial basis
@@ -330,6 +336,64 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
         if tp is not None:
             setattr(b, key, tp)
     return b
+
+
+FACTOR_MIN_ROW = 8.0  # L1 entries per row from which the factored L1 pays (hlhgat.h)
+
+
+def hodge_factor_ok(edge_index, n_nodes: int, edge_index_s, edge_weight_s) -> bool:
+    """True iff the L1 COO (edge_index_s, edge_weight_s) is EXACTLY
+    alpha_e * B1^T B1 for the boundary B1 of edge_index ([2, E], i < j;
+    adj2par1, lib/Hodge_Dataset.py:169-191), alpha_e = L1[e,e] / 2 -- the form
+    of every L1 the reference builds (2 B1^T B1 / lmax in fp32,
+    lib/Hodge_Dataset.py:451-456): diagonal 2 alpha, +alpha for two edges
+    sharing their tail or their head, -alpha for tail-to-head, every pair of
+    edges sharing a node present once, nothing else."""
+    ei = np.asarray(edge_index)
+    eis = np.asarray(edge_index_s)
+    w = np.asarray(edge_weight_s, dtype=np.float32).reshape(-1)
+    E = ei.shape[1] if ei.ndim == 2 else 0
+    if E == 0 or eis.shape[1] != w.size or np.any(ei[0] >= ei[1]):
+        return False
+    r, c = eis[0], eis[1]
+    if r.min() < 0 or max(r.max(), c.max()) >= E:
+        return False
+    diag = r == c
+    if int(diag.sum()) != E or not np.array_equal(np.sort(r[diag]), np.arange(E)):
+        return False
+    alpha = np.zeros(E, dtype=np.float32)
+    alpha[r[diag]] = w[diag] * np.float32(0.5)
+    a, b, p, q = ei[0][r], ei[1][r], ei[0][c], ei[1][c]
+    if np.any(~diag & (a == p) & (b == q)):
+        return False  # parallel edges
+    v = np.where(diag, 2, np.where((a == p) | (b == q), 1, np.where((a == q) | (b == p), -1, 0)))
+    if np.any(v == 0) or not np.array_equal(w, alpha[r] * v.astype(np.float32)):
+        return False
+    deg = np.bincount(ei.reshape(-1), minlength=int(n_nodes)).astype(np.int64)
+    if eis.shape[1] != E + int((deg * (deg - 1)).sum()):
+        return False
+    key = r.astype(np.int64) * E + c
+    return np.unique(key).size == key.size
+
+
+def _factor_wanted(graphs) -> bool:
+    """Collate-time choice of the factored L1: every graph's L1 is its
+    alpha B1^T B1 and the batch averages >= FACTOR_MIN_ROW entries per row
+    (ZINC ~4: the CSR path; CIFAR superpixels ~18, TSP ~20: factored)."""
+    E = sum(int(np.asarray(g.edge_index_s).shape[1]) for g in graphs)
+    rows = sum(int(g.x_s.shape[0]) for g in graphs)
+    if rows == 0 or E < FACTOR_MIN_ROW * rows:
+        return False
+    for g in graphs:
+        ok = getattr(g, "_l1_factor_ok", None)
+        if ok is None:
+            if getattr(g, "edge_index", None) is None or getattr(g, "edge_weight_s", None) is None:
+                return False
+            ok = hodge_factor_ok(g.edge_index, g.x_t.shape[0], g.edge_index_s, g.edge_weight_s)
+            g._l1_factor_ok = ok
+        if not ok:
+            return False
+    return True
 
 
 PAD_MIN_ROWS = 64  # padding rows share the padding entries: keep every padding row short
@@ -385,6 +449,7 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     out = Batch()
     for k, v in vars(b).items():
         setattr(out, k, v)
+    out.l1_factor = False  # padding edges are B1 self-loops: no alpha B1^T B1 identity
 
     def pad_rows(x, R):
         return torch.cat([x, x.new_zeros((R - x.size(0),) + tuple(x.shape[1:]))], 0)

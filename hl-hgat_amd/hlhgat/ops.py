@@ -157,9 +157,14 @@ class SparseCSR:
 @dataclass
 class HodgeOperator:
     """A Laplacian as used by propagate: fwd = CSR keyed by edge_index[1]
-    (Y[t] = sum w * X[s]), bwd = its transpose (keyed by edge_index[0])."""
+    (Y[t] = sum w * X[s]), bwd = its transpose (keyed by edge_index[0]).
+    ``factor`` (an L1 = alpha B1^T B1 declared by set_hodge_factor): the 7
+    tensors of hlhgat_hodge_factor_t and the node count; the polynomial
+    bases then run factored (hlhgat_poly_basis_*_factored)."""
     fwd: SparseCSR
     bwd: SparseCSR
+    factor: Optional[tuple] = None
+    factor_nodes: int = 0
 
 
 @dataclass
@@ -288,6 +293,44 @@ def set_halo(edge_index: torch.Tensor, ht: dict) -> torch.Tensor:
 
 _HALO_ENABLED = os.environ.get("HLHGAT_HALO", "1") != "0"
 
+# Factored L1 (hlhgat_hodge_factor_t): on for the operators collate declares
+# (hodge_dataset.hodge_factor_ok: exact identity, >= FACTOR_MIN_ROW entries per
+# row); HLHGAT_FACTOR=0 keeps the bitwise CSR path everywhere.
+FACTOR_ENABLED = os.environ.get("HLHGAT_FACTOR", "1") != "0"
+
+
+def set_hodge_factor(edge_index_s: torch.Tensor, edge_index: torch.Tensor, n_nodes: int,
+                     node_order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Declare that the L1 built from (edge_index_s, edge_weight_s) equals
+    alpha_e * B1^T B1 with B1 the boundary of ``edge_index`` ([2, E], i < j,
+    adj2par1 lib/Hodge_Dataset.py:169-191) on n_nodes nodes -- exactly, as
+    every L1 of the Hodge builder is (lib/Hodge_Dataset.py:451-456); the
+    caller has checked it (hodge_dataset.hodge_factor_ok).  Polynomial bases
+    over it then gather ~4 rows per edge instead of nnz/E (hlhgat.h)."""
+    edge_index_s._hlhgat_factor = (edge_index, int(n_nodes), node_order)  # type: ignore
+    return edge_index_s
+
+
+def _build_factor(op: "HodgeOperator", ei_s: torch.Tensor, w: torch.Tensor, decl) -> None:
+    """The device tensors of hlhgat_hodge_factor_t for op (no host sync)."""
+    edge_index, n_nodes, node_order = decl
+    E = op.fwd.n_rows
+    if edge_index.size(1) != E:
+        raise RuntimeError(f"hlhgat: hodge factor: B1 has {edge_index.size(1)} edges, "
+                           f"L1 has {E} rows")
+    inc = incidence(edge_index, n_nodes)
+    dev = ei_s.device
+    diag = ei_s[0] == ei_s[1]
+    alpha = torch.zeros(E, device=dev, dtype=torch.float32)
+    alpha.index_put_((ei_s[0],), torch.where(diag, w * 0.5, torch.zeros_like(w)),
+                     accumulate=True)
+    none_i = torch.empty(0, dtype=torch.int32, device=dev)
+    no = (node_order.to(dev, torch.int32).contiguous() if node_order is not None else none_i)
+    eo = op.fwd.order if op.fwd.order is not None else none_i
+    op.factor = (inc.rowptr, inc.edge_ids, _incidence_signs(inc), no,
+                 edge_index.t().to(torch.int32).contiguous(), alpha, eo)
+    op.factor_nodes = int(n_nodes)
+
 
 def _attach_halo(a: "SparseCSR", halo) -> None:
     """A.halo = (tile_ptr, halo_ptr, halo, srp, lcol, sval, bounds); sval =
@@ -318,6 +361,48 @@ def _halo_args(A: "SparseCSR"):
     if A.halo is None or not _HALO_ENABLED:
         return (None, None, None, None, None, None, [0, 0, 0], None)
     return A.halo
+
+
+def _factor_args(op: "HodgeOperator"):
+    """The factor arguments of the C++ conv node ([] = CSR path)."""
+    if op.factor is None:
+        return ([], 0)
+    return (list(op.factor), op.factor_nodes)
+
+
+def _factor_desc(op: "HodgeOperator"):
+    nr, ne, ns, no, ends, alpha, eo = op.factor
+    return C.pointer(_lib.HodgeFactorDesc(
+        nr.data_ptr(), ne.data_ptr() if ne.numel() else None, ns.data_ptr() if ns.numel() else None,
+        no.data_ptr() if no.numel() else None, op.factor_nodes, ends.data_ptr(),
+        alpha.data_ptr(), eo.data_ptr() if eo.numel() else None, op.fwd.n_rows))
+
+
+def hodge_spmm(op: "HodgeOperator", X: torch.Tensor) -> torch.Tensor:
+    """Y = L1 X through the factorisation (op must carry one; no autograd)."""
+    if op.factor is None:
+        raise RuntimeError("hlhgat: hodge_spmm needs a factored operator (set_hodge_factor)")
+    X = _rows2d(X, "X")
+    Y = torch.empty(op.fwd.n_rows, X.size(1), device=X.device, dtype=X.dtype)
+    work = torch.empty(int(LIB.hlhgat_hodge_factor_work_floats(op.factor_nodes, X.size(1))),
+                       device=X.device)
+    check(LIB.hlhgat_hodge_spmm(_factor_desc(op), X.data_ptr(), _ld(X), X.size(1), Y.data_ptr(),
+                                _ld(Y), work.data_ptr(), _stream(X)), "hodge_spmm")
+    return Y
+
+
+def _hodge_step(op: "HodgeOperator", X: torch.Tensor, Y: torch.Tensor, *, Z=None, P=None,
+                Q=None, alpha=1.0, beta=0.0, gamma=0.0, div=1.0, p=0.0, q=0.0,
+                work: Optional[torch.Tensor] = None) -> None:
+    """_poly_step with the factored L1 of op (hlhgat_hodge_poly_step)."""
+    if work is None:
+        work = torch.empty(int(LIB.hlhgat_hodge_factor_work_floats(op.factor_nodes, X.size(1))),
+                           device=X.device)
+    check(LIB.hlhgat_hodge_poly_step(
+        _factor_desc(op), X.data_ptr(), _ld(X), X.size(1), _ptr(Z), _ld(Z) if Z is not None else 0,
+        _ptr(P), _ld(P) if P is not None else 0, _ptr(Q), _ld(Q) if Q is not None else 0, alpha,
+        beta, gamma, div, p, q, Y.data_ptr(), _ld(Y), work.data_ptr(), _stream(X)),
+        "hodge_poly_step")
 
 
 def _csr_sorted(row: torch.Tensor, col: torch.Tensor, w: Optional[torch.Tensor],
@@ -386,6 +471,9 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
         if halo is not None:  # built for the COO order = this CSR's entry order
             _attach_halo(a, halo)
         op = HodgeOperator(a, a)
+        decl = getattr(edge_index, "_hlhgat_factor", None)
+        if decl is not None and FACTOR_ENABLED and w is not None:
+            _build_factor(op, ei, w, decl)
     else:
         fwd = _csr_general(ei[1], ei[0], w, n, n)
         bwd = _csr_general(ei[0], ei[1], w, n, n)
@@ -449,7 +537,13 @@ def poly_basis(op: HodgeOperator, X: torch.Tensor, K: int, kind: int) -> torch.T
     """T_1..T_{K-1} as a [K-1, n, F] slab (no autograd)."""
     n, F = X.size(0), X.size(1)
     T = torch.empty(max(K - 1, 0), n, F, device=X.device, dtype=X.dtype)
-    if K > 1 and n > 0:
+    if K > 1 and n > 0 and op.factor is not None:
+        work = torch.empty(int(LIB.hlhgat_hodge_factor_work_floats(op.factor_nodes, F)),
+                           device=X.device)
+        check(LIB.hlhgat_poly_basis_fwd_factored(kind, _factor_desc(op), X.data_ptr(), _ld(X), F,
+                                                 K, T.data_ptr(), work.data_ptr(), _stream(X)),
+              "poly_basis_fwd_factored")
+    elif K > 1 and n > 0:
         A = op.fwd
         check(LIB.hlhgat_poly_basis_fwd(kind, A.rowptr.data_ptr(),
                                         A.col.data_ptr() if A.nnz else None,
@@ -538,11 +632,13 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
                             ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order,
-                            A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A))
+                            A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A),
+                            *_factor_args(op))
     sink = out if (bn is None and not relu and x.dim() == 2) else None
     y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
                      bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order,
-                     A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A))
+                     A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A),
+                     *_factor_args(op))
     if bn is not None:
         y = batch_norm_act(y, bn, relu, valid=A.valid)
     elif relu:

@@ -218,6 +218,57 @@ int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                           int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F,
                           int K, float* G, void* stream);
 
+/* ---- Hodge-factored L1 (large, high-degree edge Laplacians) ------------ */
+/* Every L1 the reference builds is 2 B1^T B1 / lmax in fp32
+ * (lib/Hodge_Dataset.py:451-456, :780-799; MLGC :283-287): its entries are
+ * fl(2 v / lmax) with v in {2, +-1}, so L1 = alpha_e * B1^T B1 EXACTLY, with
+ * alpha_e = L1[e,e] / 2 (constant per graph).  Then
+ *     L1 X = alpha * B1^T (B1 X):   Z = B1 X   (node rows: signed sum of the
+ *                                              node's incident edge rows)
+ *                                   Y[e] = alpha_e (Z[j] - Z[i])
+ * which gathers ~4 feature rows per edge instead of nnz(L1)/E (~20 at
+ * BASELINE config 5, ~18 at config 3).  Same real-arithmetic result as the
+ * CSR SpMM; fp32 rounding differs (measured <= 3e-7 relative at config 5),
+ * so this path is NOT bitwise equal to propagate; the CSR path is.  The
+ * caller (hlhgat.ops.set_hodge_factor, checked on the host by
+ * hodge_dataset.hodge_factor_ok) guarantees the identity. */
+typedef struct hlhgat_hodge_factor {
+  const int32_t* node_rowptr; /* [n_nodes+1] incidence CSR of B1 (node rows) */
+  const int32_t* node_edge;   /* [2 n_edges] incident edge ids, ascending */
+  const float* node_sign;     /* [2 n_edges] -1 (node = edge_index[0][e]) / +1 */
+  const int32_t* node_order;  /* optional row schedule of the node rows */
+  int64_t n_nodes;
+  const int32_t* ends;        /* [n_edges][2] (edge_index[0][e], edge_index[1][e]) */
+  const float* alpha;         /* [n_edges] L1[e,e] / 2 */
+  const int32_t* edge_order;  /* optional row schedule of the edge rows */
+  int64_t n_edges;
+} hlhgat_hodge_factor_t;
+
+/* Floats of scratch (Z = B1 X) the factored entry points need for width F. */
+int64_t hlhgat_hodge_factor_work_floats(int64_t n_nodes, int64_t F);
+
+/* Y = L1 X through the factorisation (two launches).  X, Y [n_edges][d]. */
+int hlhgat_hodge_spmm(const hlhgat_hodge_factor_t* f, const float* X, int64_t ldx,
+                      int64_t d, float* Y, int64_t ldy, float* work, void* stream);
+
+/* hlhgat_poly_step with A = L1 factored: Y = (alpha (L1 X)[r] + beta X[r] +
+ * gamma Z[r]) / div + p P[r] + q Q[r]  (two launches; no row scale). */
+int hlhgat_hodge_poly_step(const hlhgat_hodge_factor_t* f, const float* X, int64_t ldx,
+                           int64_t d, const float* Z, int64_t ldz, const float* P, int64_t ldp,
+                           const float* Q, int64_t ldq, float alpha, float beta, float gamma,
+                           float div, float p, float q, float* Y, int64_t ldy, float* work,
+                           void* stream);
+
+/* hlhgat_poly_basis_fwd / _bwd with every L1 application factored (each
+ * step = one incidence launch + one fused edge-step launch whose epilogue is
+ * the recurrence's).  L1 is symmetric, so the adjoint uses the same factor.
+ * Replaces the same reference lines as hlhgat_poly_basis_fwd / _bwd. */
+int hlhgat_poly_basis_fwd_factored(int kind, const hlhgat_hodge_factor_t* f,
+                                   const float* X, int64_t ldx, int64_t F, int K, float* T,
+                                   float* work, void* stream);
+int hlhgat_poly_basis_bwd_factored(int kind, const hlhgat_hodge_factor_t* f, int64_t F,
+                                   int K, float* G, float* work, void* stream);
+
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
 #define HLHGAT_MAX_BLOCKS 16
 
@@ -342,7 +393,9 @@ int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
 /* ---- live kernel timing ------------------------------------------------ */
 #define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */
 #define HLHGAT_PROF_PROJ 1 /* MFMA projection forward */
-#define HLHGAT_PROF_NCLASS 2
+#define HLHGAT_PROF_HODGE_NODE 2 /* factored L1, stage 1: Z = B1 X (node rows) */
+#define HLHGAT_PROF_HODGE_EDGE 3 /* factored L1, stage 2: k_hodge_edge_step */
+#define HLHGAT_PROF_NCLASS 4
 /* Enable (1) / disable (0) event timing of the given kernel class. */
 int hlhgat_prof_enable(int kernel_class, int enable);
 int hlhgat_prof_reset(void);

@@ -744,3 +744,121 @@ def test_attpool_pepfunc_model_vs_reference_golden(cuda):
     import hlhgat
     _attpool_case(cuda, "attpool_pepfunc_small", hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool,
                   channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)
+
+
+# ---------------------------------------------------------------------------
+# Hodge-factored L1 (L1 = alpha B1^T B1, hlhgat_hodge_factor_t): same
+# real-arithmetic operator, different fp32 rounding -- 1e-5 relative, not bitwise
+# ---------------------------------------------------------------------------
+def _factored_pair(g, node_order=None, edge_order=None):
+    from hlhgat import ops
+    n = g.x_s.shape[0]
+    ei_c = ops.mark_hodge(dev(g.edge_index_s))
+    ei_f = ops.mark_hodge(dev(g.edge_index_s))
+    if edge_order is not None:
+        ops.set_row_order(ei_f, edge_order)
+    ops.set_hodge_factor(ei_f, dev(g.edge_index), g.x_t.shape[0], node_order)
+    w = dev(g.edge_weight_s)
+    op_c = ops.hodge_operator(ei_c, w, n)
+    op_f = ops.hodge_operator(ei_f, w, n)
+    assert op_c.factor is None and op_f.factor is not None
+    return op_c, op_f, ei_c, ei_f, w
+
+
+@pytest.mark.parametrize("d", [1, 3, 32, 64, 128])
+@pytest.mark.parametrize("sched", [False, True])
+def test_hodge_factored_spmm_matches_csr(cuda, d, sched):
+    """alpha B1^T (B1 X) == the CSR SpMM of L1 == the oracle's propagate
+    (TSP-like graph, config 5 structure; RCM schedules on both factors)."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import hodge_factor_ok
+    from hlhgat.synthetic import tsp_like_graph
+    g = tsp_like_graph(5, n=3000, k=9)
+    assert hodge_factor_ok(g.edge_index, g.x_t.shape[0], g.edge_index_s, g.edge_weight_s)
+    op_c, op_f, *_ = _factored_pair(g, g.row_order_t if sched else None,
+                                    g.row_order_s if sched else None)
+    x = torch.randn(g.x_s.shape[0], d, generator=torch.Generator().manual_seed(d))
+    ref = R.propagate(x, g.edge_index_s, g.edge_weight_s)
+    y = ops.hodge_spmm(op_f, dev(x)).cpu()
+    assert torch.equal(ops.spmm(op_c.fwd, dev(x)).cpu(), ref)
+    close(y, ref, 1e-5, "factored spmm")
+
+
+@pytest.mark.parametrize("kind,K", [("lag", 2), ("lag", 4), ("cheb", 4), ("demo", 4)])
+def test_hodge_factored_basis_matches_csr(cuda, kind, K):
+    from hlhgat import ops
+    from hlhgat.synthetic import tsp_like_graph
+    kd = {"lag": ops.POLY_LAGUERRE, "cheb": ops.POLY_CHEB, "demo": ops.POLY_LAGUERRE_DEMO}[kind]
+    g = tsp_like_graph(6, n=2000, k=8)
+    op_c, op_f, *_ = _factored_pair(g, g.row_order_t, g.row_order_s)
+    x = dev(torch.randn(g.x_s.shape[0], 48, generator=torch.Generator().manual_seed(1)))
+    Tc = ops.poly_basis(op_c, x, K, kd).cpu()
+    Tf = ops.poly_basis(op_f, x, K, kd).cpu()
+    for k in range(K - 1):
+        close(Tf[k], Tc[k], 1e-5, f"T_{k + 1}")
+
+
+@pytest.mark.parametrize("kind", ["lag", "cheb"])
+def test_hodge_factored_conv_bn_fwd_bwd(cuda, kind):
+    """HodgeLaguerreConv / HodgeChebConv -> BN -> ReLU (one C++ node) on a
+    factored L1: output, dX and every parameter gradient vs the CSR operator."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import cifar_like_graphs
+    from hlhgat.hodge_dataset import collate
+    b = collate([cifar_like_graphs(60 + s)[0] for s in range(4)])
+    assert b.l1_factor
+    cls = hlhgat.HodgeLaguerreConv if kind == "lag" else hlhgat.HodgeChebConv
+    torch.manual_seed(0)
+    conv = cls(32, 32, K=4).to(cuda)
+    bn = torch.nn.BatchNorm1d(32).to(cuda)
+    x = torch.randn(b.x_s.shape[0], 32, device=cuda)
+    res = []
+    for factored in (False, True):
+        ei = ops.mark_hodge(dev(b.edge_index_s))
+        if factored:
+            ops.set_hodge_factor(ei, dev(b.edge_index), b.x_t.shape[0])
+        op = ops.hodge_operator(ei, dev(b.edge_weight_s), b.x_s.shape[0])
+        assert (op.factor is not None) == factored
+        xx = x.clone().requires_grad_(True)
+        y = ops.hodge_poly_conv(xx, op, [l.weight for l in conv.lins], conv.bias,
+                                ops.POLY_LAGUERRE if kind == "lag" else ops.POLY_CHEB,
+                                bn=bn, relu=True)
+        (y * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+        res.append([y.detach().cpu(), xx.grad.cpu()] +
+                   [l.weight.grad.cpu().clone() for l in conv.lins] + [bn.weight.grad.cpu().clone()])
+        conv.zero_grad()
+        bn.zero_grad()
+    for i, (a, c) in enumerate(zip(res[1], res[0])):
+        close(a, c, 1e-5 if i == 0 else 1e-4, f"item {i}")
+
+
+def test_tsp_model_factored_vs_reference_golden(cuda):
+    """The config-5 head with its L1 factored (set_hodge_factor) against the
+    reference's own forward / backward (tsp_model_small): 1e-4 relative."""
+    import re
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import Batch, hodge_factor_ok
+    g = load_golden("tsp_model_small")
+    assert hodge_factor_ok(g["edge_index"], g["x_t"].shape[0], g["edge_index_s"],
+                           g["edge_weight_s"])
+    m = hlhgat.HL_HGCNN_TSP_dense_int3_pyr(channels=[1, 1], filters=[16, 16],
+                                           mlp_channels=[32], K=3)
+    m.load_state_dict({k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")})
+    m = m.to(cuda).train()
+    b = Batch()
+    for k in ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+              "edge_index", "num_node1", "num_edge1"):
+        setattr(b, k, dev(g[k]))
+    ops.mark_hodge(b.edge_index_s)
+    ops.set_hodge_factor(b.edge_index_s, b.edge_index, b.x_t.shape[0])
+    out, _ = m(b)
+    assert ops.hodge_operator(b.edge_index_s, b.edge_weight_s, b.x_s.shape[0]).factor is not None
+    close(out.detach().cpu(), g["out"], 1e-4, "out")
+    (out * dev(g["R"])).sum().backward()
+    for k, p in m.named_parameters():
+        if re.search(r"module_[04]\.bias$", k) and not k.startswith("out."):
+            assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
+            continue
+        close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)

@@ -340,3 +340,30 @@ def test_graclus_is_a_matching():
     alone = set(alone)
     for u, v in adj:
         assert not (u in alone and v in alone and u != v)
+
+
+def test_hodge_factor_check():
+    """hodge_factor_ok: every L1 the Hodge builder emits is alpha B1^T B1
+    exactly (lib/Hodge_Dataset.py:451-456) -- the reference's own TSP fixture,
+    CIFAR-like, ZINC-like and MLGC-coarsened graphs; a perturbed weight, a
+    dropped entry or a flipped edge orientation is rejected.  collate turns the
+    factored L1 on for high-degree batches only, pad_batch turns it off."""
+    from hlhgat.hodge_dataset import collate, hodge_factor_ok, pad_batch, static_caps
+    from hlhgat.synthetic import cifar_like_graphs, zinc_like_graph
+    g = load_golden("tsp_model_small")
+    assert hodge_factor_ok(g["edge_index"], g["x_t"].shape[0], g["edge_index_s"],
+                           g["edge_weight_s"])
+    for c in (cifar_like_graphs(1)[0], cifar_like_graphs(2)[1], zinc_like_graph(3)):
+        ei, eis, w = c.edge_index.numpy(), c.edge_index_s.numpy(), c.edge_weight_s.numpy()
+        n = c.x_t.shape[0]
+        assert hodge_factor_ok(ei, n, eis, w)
+        w2 = w.copy()
+        w2[3] = np.nextafter(w2[3], np.float32(np.inf))
+        assert not hodge_factor_ok(ei, n, eis, w2)
+        assert not hodge_factor_ok(ei, n, eis[:, 1:], w[1:])
+        assert not hodge_factor_ok(ei[::-1], n, eis, w)
+    assert collate([cifar_like_graphs(s)[0] for s in range(2)]).l1_factor
+    zb = collate([zinc_like_graph(s) for s in range(4)])
+    assert not zb.l1_factor
+    cb = collate([cifar_like_graphs(s)[0] for s in range(2)])
+    assert not pad_batch(cb, static_caps(cb)).l1_factor

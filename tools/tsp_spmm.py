@@ -7,6 +7,11 @@ Variants, all on the same operator and bitwise-equal outputs (checked):
   plain   k_poly_step, natural row order
   rcm     k_poly_step, RCM row schedule (hodge_dataset.locality_order)
   halo    k_poly_halo, LDS halo tiles along the RCM schedule (max_rows:max_halo)
+  factored  L1 = alpha B1^T B1 (hlhgat_hodge_factor_t): B1 X over the node rows,
+          then one fused edge step; NOT bitwise (checked to 1e-5 relative)
+Ops: spmm, laguerre_step (one fused step) and basis_k3 (T_1, T_2 of a K = 3
+Laguerre basis: 2 steps, 16 nnz + 8 (n+1) + 20 n d bytes; the only form the
+factored variant has besides spmm).
 Algorithmic bytes: SpMM 8 nnz + 4 (n+1) + 8 n d; Laguerre step
 (reads T_k, T_{k-1}) 8 nnz + 4 (n+1) + 12 n d.  Peak 8 TB/s.
 """
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--d", type=int, nargs="+", default=[64, 128])
     ap.add_argument("--tiles", nargs="+", default=["24:160:768", "32:192:1024"])
     ap.add_argument("--out", default="")
+    ap.add_argument("--no-factored", action="store_true")
     args = ap.parse_args()
     from hlhgat import ops
     from hlhgat.hodge_dataset import collate, halo_tiles
@@ -72,6 +78,12 @@ def main():
         op.info = {"tiles": ht["halo_tile_ptr"].numel() - 1,
                    "reuse": round(nnz / int(ht["halo_ptr"][-1]), 2)}
         variants[f"halo {spec}"] = op
+    if not args.no_factored:
+        ef = ops.set_row_order(ops.mark_hodge(ei.to(dev)), order)
+        ops.set_hodge_factor(ef, b.edge_index.to(dev), b.x_t.shape[0], b.row_order_t)
+        opf = ops.hodge_operator(ef, w.to(dev), n)
+        assert opf.factor is not None
+        variants["factored"] = opf
     res = []
     for d in args.d:
         X = torch.randn(n, d, device=dev)
@@ -80,16 +92,26 @@ def main():
         ref = None
         for name, op in variants.items():
             A = op.fwd
-            ops._poly_step(A, X, Y)
-            if ref is None:
-                ref = Y.clone()
-            assert torch.equal(Y, ref), f"{name}: results differ"
-            for what, fn, by in (
-                    ("spmm", lambda: ops._poly_step(A, X, Y),
-                     8 * nnz + 4 * (n + 1) + 8 * n * d),
-                    ("laguerre_step", lambda: ops._poly_step(A, X, Y, Z=Z, alpha=-1.0, beta=5.0,
-                                                             gamma=-2.0, div=3.0),
-                     8 * nnz + 4 * (n + 1) + 12 * n * d)):
+            fac = op.factor is not None
+            if fac:
+                Yf = ops.hodge_spmm(op, X)
+                err = float((Yf - ref).abs().max() / ref.abs().max())
+                assert err < 1e-5, f"{name}: {err}"
+                cases = [("spmm", lambda: ops.hodge_spmm(op, X),
+                          8 * nnz + 4 * (n + 1) + 8 * n * d)]
+            else:
+                ops._poly_step(A, X, Y)
+                if ref is None:
+                    ref = Y.clone()
+                assert torch.equal(Y, ref), f"{name}: results differ"
+                cases = [("spmm", lambda: ops._poly_step(A, X, Y),
+                          8 * nnz + 4 * (n + 1) + 8 * n * d),
+                         ("laguerre_step", lambda: ops._poly_step(A, X, Y, Z=Z, alpha=-1.0,
+                                                                  beta=5.0, gamma=-2.0, div=3.0),
+                          8 * nnz + 4 * (n + 1) + 12 * n * d)]
+            cases.append(("basis_k3", lambda: ops.poly_basis(op, X, 3, ops.POLY_LAGUERRE),
+                          16 * nnz + 8 * (n + 1) + 20 * n * d))
+            for what, fn, by in cases:
                 us = timeit(fn)
                 r = {"variant": name, "op": what, "d": d, "n": n, "nnz": nnz, "us": round(us, 1),
                      "GBps": round(by / us / 1e3, 1),
