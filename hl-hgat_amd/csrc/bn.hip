@@ -51,13 +51,16 @@ struct BnLayout {
 // instead of one long one.  In the ZINC step 64 partitions measured best
 // (256: 264k -> 251k graphs/s; more workgroups crowd the concurrent chain).
 // HLHGAT_BN_PARTS overrides (A/B measurements).
-int64_t bn_parts() {
-  static int64_t v = [] {
+// Larger batches (config 3 / 5 heads: 1.4e5-2e5 rows) get one partition per
+// 512 rows (up to kMaxParts): 64 workgroups leave most of the 256 CUs idle
+// there (k_bn_bwd_reduce ran at ~1 TB/s, profiles/r01_h_*_head_kernel_stats.md).
+int64_t bn_parts(int64_t n) {
+  static int64_t fixed = [] {
     const char* e = getenv("HLHGAT_BN_PARTS");
-    int64_t p = e ? atoll(e) : 64;
-    return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
+    return e ? atoll(e) : (int64_t)0;
   }();
-  return v;
+  int64_t p = fixed > 0 ? fixed : std::max<int64_t>(64, ceil_div(n, (int64_t)512));
+  return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
 }
 
 BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
@@ -71,7 +74,7 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   L.tiles = (int)ceil_div(C, L.tile_c);
   // <= kMaxParts row partitions per column tile (fat partitions keep the
   // last arriver's reduction to one batch of loads per thread)
-  int64_t parts = bn_parts();
+  int64_t parts = bn_parts(n);
   int64_t max_parts = ceil_div(n, (int64_t)L.rp * 2);
   if (parts > max_parts) parts = max_parts;
   if (parts < 1) parts = 1;

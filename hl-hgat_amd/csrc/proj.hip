@@ -881,7 +881,14 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   p.tiles_total = p.tile_start[nb];
   // aim for ~384 workgroups (1.5 per CU), each slice >= 128 rows: balances
   // MFMA parallelism against the split-slab traffic the reduce re-reads
-  int64_t splits = ceil_div(384, p.tiles_total > 0 ? p.tiles_total : 1);
+  const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
+  int64_t splits = ceil_div(384, tiles);
+  // large M (config 3 / 5 heads, 1e5+ rows): up to ~1536 workgroups as long
+  // as every slice keeps >= 4096 rows (the slab stays small against A);
+  // measured 13-22 % faster on the TSP / CIFAR NEInt and conv shapes
+  // (tools/kbench.py --big, profiles/r01_h_wsplit.log), ZINC shapes unchanged
+  const int64_t big = std::min<int64_t>(ceil_div(1536, tiles), M / 4096);
+  if (big > splits) splits = big;
   int64_t max_splits = ceil_div(M, 128);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;

@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--chain", type=int, default=20)
     ap.add_argument("--out", default="")
+    ap.add_argument("--big", action="store_true",
+                    help="config 3 / 5 projection shapes only (CIFAR / TSP heads)")
     args = ap.parse_args()
     from hlhgat import ops
     from hlhgat.synthetic import zinc_like_batch
@@ -90,6 +92,34 @@ def main():
     def rnd(*s):
         return torch.randn(*s, generator=g).to(dev)
 
+    if args.big:  # projection shapes of the config-3 / config-5 heads (M rows, N, blocks)
+        for M, N, kbs, tag in [(206858, 128, [928, 928], "TSP NEInt L2 edge Linear(1856,128)"),
+                               (206858, 128, [128] * 4, "TSP conv K=4 d=128"),
+                               (206858, 64, [416, 416], "TSP NEInt L1 edge Linear(832,64)"),
+                               (143192, 256, [448, 448], "CIFAR NEInt L2 edge Linear(896,256)"),
+                               (143192, 64, [64] * 4, "CIFAR conv K=4 d=64")]:
+            As = [rnd(M, k) for k in kbs]
+            W = rnd(N, sum(kbs))
+            Ws, o = [], 0
+            for k in kbs:
+                Ws.append(W[:, o:o + k])
+                o += k
+            out = torch.empty(M, N, device=dev)
+            fl = 2.0 * M * N * sum(kbs)
+            by = 4.0 * M * (sum(kbs) + N)
+            run(f"proj_fwd {tag}", lambda: ops._proj_fwd(As, Ws, M, N, None, out), by, fl)
+            G = rnd(M, N)
+            dAs = [torch.empty(M, k, device=dev) for k in kbs]
+            run(f"proj_bwd_data {tag}", lambda: ops._proj_bwd_data(G, Ws, kbs, dAs), by, fl)
+            dW = torch.empty_like(W)
+            dWs, o = [], 0
+            for k in kbs:
+                dWs.append(dW[:, o:o + k])
+                o += k
+            db = torch.empty(N, device=dev)
+            run(f"proj_bwd_weight {tag}", lambda: ops._proj_bwd_weight(G, As, dWs, db), by, fl)
+            del As, G, dAs
+        return
     zb = zinc_like_batch(1000, seed=1).to(dev)
     nt, ns = zb.x_t.shape[0], zb.x_s.shape[0]
     # ---- reference points: streaming copies / library GEMM at the same bytes --
