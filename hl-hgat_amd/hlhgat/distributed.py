@@ -57,11 +57,19 @@ def init_distributed(backend: str = None) -> Tuple[int, int, torch.device]:
     """Initialise the process group (RCCL on GPU, gloo on CPU); one process
     per GPU.  Returns (rank, world, device)."""
     rank, world, local = world_info()
+    # Rehearsal of the multi-rank path on a one-GPU box: HLHGAT_DIST_BACKEND=gloo
+    # with HLHGAT_SHARE_GPU=1 puts every rank on cuda:0 and exchanges through
+    # gloo (RCCL refuses two ranks on one device).  Production: nccl = RCCL.
+    backend = os.environ.get("HLHGAT_DIST_BACKEND", backend)
+    share = os.environ.get("HLHGAT_SHARE_GPU", "0") == "1"
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     if backend == "nccl":
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
+    elif share:
+        device = torch.device("cuda", 0)
+        torch.cuda.set_device(device)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
