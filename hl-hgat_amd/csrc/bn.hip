@@ -550,25 +550,22 @@ extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
   return (int64_t)bn_ws_bytes(n, C);
 }
 
-extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
-                                   const int32_t* n_valid, int64_t C,
-                                   const float* weight, const float* bias,
-                                   float* running_mean, float* running_var,
-                                   int64_t* num_batches_tracked, float momentum,
-                                   float eps, int relu, float* y, int64_t ldy,
-                                   float* save_mean, float* save_invstd,
-                                   void* workspace, int64_t workspace_bytes,
-                                   void* stream) {
-  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
-                "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
-  HLH_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
+extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
+                                     const int32_t* n_valid, int64_t C, float* running_mean,
+                                     float* running_var, int64_t* num_batches_tracked,
+                                     float momentum, float eps, float* save_mean,
+                                     float* save_invstd, void* workspace,
+                                     int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C,
+                "bn_stats_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(x && save_mean && save_invstd, "bn_stats_train: NULL pointer");
   HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
-                "bn_fwd_train: running_mean/var must both be given or both NULL");
+                "bn_stats_train: running_mean/var must both be given or both NULL");
   HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
-                "bn_fwd_train: workspace too small");
-  const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
+                "bn_stats_train: workspace too small");
+  const bool vec = bn_vec_ok(C, {ldx}, {x});
   BnLayout L = bn_layout(n, C, vec);
-  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_fwd_train: C too large");
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_stats_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
   s.nvalid = n_valid;
@@ -584,8 +581,6 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
   s.part = w.part;
   s.gpart = w.gpart;
   s.count = w.count;
-  s.weight = weight;
-  s.bias = bias;
   s.running_mean = running_mean;
   s.running_var = running_var;
   s.nbt = num_batches_tracked;
@@ -600,8 +595,22 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
   else
     k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_valid,
+                               int64_t C, const float* weight, const float* bias,
+                               const float* save_mean, const float* save_invstd, int relu,
+                               float* y, int64_t ldy, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
+                "bn_apply: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(x && y && save_mean && save_invstd, "bn_apply: NULL pointer");
+  const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
+  BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_apply: C too large");
   ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
               L.tpr, L.rp};
+  hipStream_t st = as_stream(stream);
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
     k_bn_apply<4><<<g2, kThreads, 0, st>>>(p);
@@ -609,6 +618,26 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
     k_bn_apply<1><<<g2, kThreads, 0, st>>>(p);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
+                                   const int32_t* n_valid, int64_t C,
+                                   const float* weight, const float* bias,
+                                   float* running_mean, float* running_var,
+                                   int64_t* num_batches_tracked, float momentum,
+                                   float eps, int relu, float* y, int64_t ldy,
+                                   float* save_mean, float* save_invstd,
+                                   void* workspace, int64_t workspace_bytes,
+                                   void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
+                "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(y, "bn_fwd_train: NULL pointer");
+  int rc = hlhgat_bn_stats_train(x, ldx, n, n_valid, C, running_mean, running_var,
+                                 num_batches_tracked, momentum, eps, save_mean, save_invstd,
+                                 workspace, workspace_bytes, stream);
+  if (rc) return rc;
+  return hlhgat_bn_apply(x, ldx, n, n_valid, C, weight, bias, save_mean, save_invstd, relu, y,
+                         ldy, stream);
 }
 
 extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,

@@ -67,6 +67,19 @@ struct FwdArgs {
   float* C;
   int64_t ldc;
   int accumulate;
+  // BatchNorm statistics of C in the epilogue (hlhgat_proj_fwd_bn; stats == 0: off)
+  int stats;
+  const int32_t* nvalid;  // rows >= *nvalid are padding (NULL: all M)
+  unsigned* count;        // [kStatTiles][1 + kStatGroups] arrival counters (zero between launches)
+  double* part;           // [gridDim.x][N][2] per-row-tile partials
+  double* gpart;          // [ng][N][2] group partials
+  int gs, ng;             // row tiles per group, groups
+  float* save_mean;
+  float* save_invstd;
+  float* running_mean;
+  float* running_var;
+  int64_t* nbt;
+  float momentum, eps;
 };
 
 template <int TM, int TN, bool VEC>
@@ -269,7 +282,111 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[TN], float*
   }
 }
 
+// ---- BatchNorm statistics in the projection epilogue (hlhgat_proj_fwd_bn) ----
+constexpr int kStatTiles = 256;   // column tiles (N <= 256 * 16)
+constexpr int kStatGroups = 128;  // row-tile groups of the first tree level
+
+// Release this workgroup's partial writes and count it in; true in the last
+// workgroup to arrive (which resets the counter for the next launch).  The
+// hand-off of MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, as
+// in bn.hip.
+__device__ __forceinline__ bool stat_arrive_last(unsigned* counter, unsigned total) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev =
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == total - 1) ? 1u : 0u;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      *counter = 0u;
+    }
+  }
+  __syncthreads();
+  return s_last != 0u;
+}
+
+// Column partials (sum, sum of squares; fp64) of this workgroup's valid rows,
+// from the 4 waves' LDS scratch tiles (the stored C values, bias included),
+// then the two-level tree; the last workgroup of the column tile finalises
+// mean / invstd / running statistics exactly as k_bn_stats does.
 template <int TN>
+__device__ void proj_bn_stats(const FwdArgs& a, const float* wl0, int n_base, int ncols) {
+  constexpr int CT = TN * 16, P = CT + 4;
+  __shared__ double sred[4][CT][2];
+  __shared__ double sfin[CT][2];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int64_t n_eff = a.M;
+  if (a.nvalid) {
+    const int64_t nv = (int64_t)*a.nvalid;
+    if (nv < n_eff) n_eff = nv;
+  }
+  if (lane < CT) {
+    const float* scr = wl0 + wave * 16 * P;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * 16;
+    double s0 = 0.0, s1 = 0.0;
+    for (int r = 0; r < 16; ++r) {
+      if (row0 + r >= n_eff) break;
+      const double v = (double)scr[r * P + lane];
+      s0 += v;
+      s1 += v * v;
+    }
+    sred[wave][lane][0] = s0;
+    sred[wave][lane][1] = s1;
+  }
+  __syncthreads();
+  const int pt = (int)blockIdx.x;
+  const int g = pt / a.gs;
+  if (threadIdx.x < 2 * CT) {
+    const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
+    const double v = ((sred[0][c][m] + sred[1][c][m]) + sred[2][c][m]) + sred[3][c][m];
+    if (c < ncols) a.part[((int64_t)pt * a.N + n_base + c) * 2 + m] = v;
+  }
+  const int tile = (int)blockIdx.y;
+  const int first = g * a.gs;
+  const int cnt = (int)gridDim.x - first < a.gs ? (int)gridDim.x - first : a.gs;
+  if (!stat_arrive_last(a.count + kStatTiles + tile * kStatGroups + g, (unsigned)cnt)) return;
+  double gsum = 0.0;
+  if (threadIdx.x < 2 * CT) {
+    const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
+    if (c < ncols)
+      for (int p = first; p < first + cnt; ++p) gsum += a.part[((int64_t)p * a.N + n_base + c) * 2 + m];
+    if (a.ng > 1 && c < ncols) a.gpart[((int64_t)g * a.N + n_base + c) * 2 + m] = gsum;
+  }
+  if (a.ng > 1) {
+    if (!stat_arrive_last(a.count + tile, (unsigned)a.ng)) return;
+    if (threadIdx.x < 2 * CT) {
+      const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
+      gsum = 0.0;
+      if (c < ncols)
+        for (int q = 0; q < a.ng; ++q) gsum += a.gpart[((int64_t)q * a.N + n_base + c) * 2 + m];
+    }
+  }
+  if (threadIdx.x < 2 * CT) sfin[threadIdx.x >> 1][threadIdx.x & 1] = gsum;
+  __syncthreads();
+  if (threadIdx.x < ncols) {
+    const int cc = n_base + threadIdx.x;
+    const double u0 = sfin[threadIdx.x][0], u1 = sfin[threadIdx.x][1];
+    const double nn = (double)(n_eff > 0 ? n_eff : 1);
+    const double mean = u0 / nn;
+    double var = u1 / nn - mean * mean;
+    if (var < 0.0) var = 0.0;
+    a.save_mean[cc] = (float)mean;
+    a.save_invstd[cc] = (float)(1.0 / sqrt(var + (double)a.eps));
+    if (a.running_mean) {
+      const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
+      a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
+      a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
+    }
+  }
+  if (a.nbt && tile == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+}
+
+template <int TN, bool STATS = false>
 __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
   __shared__ float wl[2][TN * 16][KCP];
   const int wave = threadIdx.x >> 6;
@@ -336,6 +453,7 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
                       (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
   store_tile_rows<TN>(acc, scratch, m_base, a.M, a.C + n_base, a.ldc, ncols,
                       a.bias ? a.bias + n_base : nullptr, a.accumulate, vec_ok);
+  if constexpr (STATS) proj_bn_stats<TN>(a, &wl[0][0][0], n_base, ncols);
 }
 
 // ---------------------------------------------------------------------------
@@ -915,6 +1033,44 @@ bool vec_ok(const float* p, int64_t ld, int64_t kb) {
   return aligned16(p) && (ld % 4) == 0 && (kb % 4) == 0;
 }
 
+// 16-column tiles per wave of the forward: enough waves to cover the 1024
+// SIMDs several times over (measured at the HL-HGAT shapes, tools/kbench.py):
+// small M -> 1, K <= 256 -> 2 (re-reading A from L2 is cheap), long K -> 4
+int fwd_tn(int64_t M, int64_t N, int64_t ktot) {
+  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
+  if (N <= 16) tn = 1;
+  else if (N <= 32 && tn > 2) tn = 2;
+  if (proj_tn()) {
+    const int cap = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
+    tn = proj_tn() < cap ? proj_tn() : cap;
+  }
+  return tn;
+}
+
+// workspace of hlhgat_proj_fwd_bn: [counters | fallback | part | gpart] with
+// `fallback` a hlhgat_bn_stats_train workspace for the unfused path.  Both
+// counter regions sit at FIXED offsets (the fallback's own counters come
+// first in it), so calls of any (M, N) on one workspace never see another
+// call's partials where they expect zeroed counters.
+struct StatPlan {
+  int64_t parts;
+  int gs, ng;
+  size_t count_bytes, fb_bytes, part_bytes, gpart_bytes, total;
+};
+size_t al256(size_t v) { return (v + 255) & ~size_t(255); }
+StatPlan stat_plan(int64_t M, int64_t N) {
+  StatPlan p{};
+  p.parts = std::max<int64_t>(1, ceil_div(M, (int64_t)64));
+  p.gs = (int)std::max<int64_t>(16, ceil_div(p.parts, (int64_t)kStatGroups));
+  p.ng = (int)ceil_div(p.parts, (int64_t)p.gs);
+  p.count_bytes = al256(sizeof(unsigned) * kStatTiles * (1 + kStatGroups));
+  p.fb_bytes = al256((size_t)hlhgat_bn_workspace_bytes(M > 0 ? M : 1, N));
+  p.part_bytes = al256(sizeof(double) * 2 * (size_t)p.parts * (size_t)N);
+  p.gpart_bytes = al256(sizeof(double) * 2 * (size_t)p.ng * (size_t)N);
+  p.total = p.count_bytes + p.fb_bytes + p.part_bytes + p.gpart_bytes;
+  return p;
+}
+
 }  // namespace
 
 using namespace hlhgat;
@@ -956,13 +1112,7 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   // 1, K <= 256 -> 2 (re-reading A from L2 is cheap), long K -> 4
   int64_t ktot = 0;
   for (int b = 0; b < nblocks; ++b) ktot += kb[b];
-  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
-  if (N <= 16) tn = 1;
-  else if (N <= 32 && tn > 2) tn = 2;
-  if (proj_tn()) {
-    const int cap = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
-    tn = proj_tn() < cap ? proj_tn() : cap;
-  }
+  const int tn = fwd_tn(M, N, ktot);
   const int tm = M >= 262144 ? 2 : 1;
   dim3 grid((unsigned)ceil_div(M, 4 * tm * 16), (unsigned)ceil_div(N, tn * 16));
   double bytes = 4.0 * (double)M * N;
@@ -989,6 +1139,88 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   } else {
     launch(k_proj_fwd<2, 4, false>, grid, 256, 0, s, &prof, a);
   }
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int64_t hlhgat_proj_fwd_bn_workspace_bytes(int64_t M, int64_t N) {
+  if (M < 0 || N <= 0) return 0;
+  return (int64_t)stat_plan(M, N).total;
+}
+
+extern "C" int hlhgat_proj_fwd_bn(int nblocks, const float* const* A, const int64_t* lda,
+                                  const float* const* W, const int64_t* ldw, const int64_t* kb,
+                                  int64_t M, int64_t N, const float* bias, float* C, int64_t ldc,
+                                  const int32_t* n_valid, float* running_mean, float* running_var,
+                                  int64_t* num_batches_tracked, float momentum, float eps,
+                                  float* save_mean, float* save_invstd, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_fwd_bn: nblocks=%d", nblocks);
+  HLH_CHECK_ARG(M >= 1 && N > 0 && N <= 16 * kStatTiles && ldc >= N && C,
+                "proj_fwd_bn: bad M/N/ldc/C");
+  HLH_CHECK_ARG(save_mean && save_invstd, "proj_fwd_bn: NULL statistics output");
+  HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                "proj_fwd_bn: running_mean/var must both be given or both NULL");
+  const StatPlan sp = stat_plan(M, N);
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)sp.total,
+                "proj_fwd_bn: workspace too small");
+  bool vec = true;
+  int64_t ktot = 0;
+  FwdArgs a{};
+  a.nb = nblocks;
+  a.M = M;
+  a.N = (int)N;
+  a.bias = bias;
+  a.C = C;
+  a.ldc = ldc;
+  double flops = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    HLH_CHECK_ARG(A[b] && W[b] && kb[b] > 0 && lda[b] >= kb[b] && ldw[b] >= kb[b],
+                  "proj_fwd_bn: bad block %d", b);
+    a.A[b] = A[b];
+    a.W[b] = W[b];
+    a.lda[b] = lda[b];
+    a.ldw[b] = ldw[b];
+    a.kb[b] = (int)kb[b];
+    vec = vec && vec_ok(A[b], lda[b], kb[b]) && vec_ok(W[b], ldw[b], kb[b]);
+    ktot += kb[b];
+    flops += 2.0 * (double)M * (double)N * (double)kb[b];
+  }
+  if (!vec) {  // unfused: projection, then the statistics pass over C
+    int rc = hlhgat_proj_fwd(nblocks, A, lda, W, ldw, kb, M, N, bias, C, ldc, 0, stream);
+    if (rc) return rc;
+    return hlhgat_bn_stats_train(C, ldc, M, n_valid, N, running_mean, running_var,
+                                 num_batches_tracked, momentum, eps, save_mean, save_invstd,
+                                 (char*)workspace + sp.count_bytes, (int64_t)sp.fb_bytes,
+                                 stream);
+  }
+  char* w = (char*)workspace;
+  a.stats = 1;
+  a.nvalid = n_valid;
+  a.count = reinterpret_cast<unsigned*>(w);
+  a.part = reinterpret_cast<double*>(w + sp.count_bytes + sp.fb_bytes);
+  a.gpart = reinterpret_cast<double*>(w + sp.count_bytes + sp.fb_bytes + sp.part_bytes);
+  a.gs = sp.gs;
+  a.ng = sp.ng;
+  a.save_mean = save_mean;
+  a.save_invstd = save_invstd;
+  a.running_mean = running_mean;
+  a.running_var = running_var;
+  a.nbt = num_batches_tracked;
+  a.momentum = momentum;
+  a.eps = eps;
+  const int tn = fwd_tn(M, N, ktot);
+  double bytes = 4.0 * (double)M * N;
+  for (int b = 0; b < nblocks; ++b) bytes += 4.0 * (double)M * kb[b] + 4.0 * N * kb[b];
+  hipStream_t s = as_stream(stream);
+  ProfScope prof(HLHGAT_PROF_PROJ, s, bytes, flops);
+  dim3 g((unsigned)sp.parts, (unsigned)ceil_div(N, (int64_t)tn * 16));
+  if (tn == 1)
+    launch(k_proj_fwd_lds<1, true>, g, 256, 0, s, &prof, a);
+  else if (tn == 2)
+    launch(k_proj_fwd_lds<2, true>, g, 256, 0, s, &prof, a);
+  else
+    launch(k_proj_fwd_lds<4, true>, g, 256, 0, s, &prof, a);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -256,6 +256,63 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
   return y;
 }
 
+// BatchNorm statistics in the projection epilogue (hlhgat_proj_fwd_bn):
+// OFF by default -- measured slower in every config (ZINC step 264k -> 236k
+// graphs/s, TSP head 41.9 -> 50.0 ms): each GEMM workgroup then drains its
+// C stores and takes an agent-scope atomic before retiring, which costs more
+// than the separate, well-overlapped statistics launch it removes.
+// HLHGAT_FUSED_BN_STATS=1 (or set_fused_bn_stats) turns it on.
+bool& fused_bn_flag() {
+  static bool on = [] {
+    const char* e = getenv("HLHGAT_FUSED_BN_STATS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+bool fused_bn_stats() { return fused_bn_flag(); }
+void set_fused_bn_stats(bool on) { fused_bn_flag() = on; }
+
+// One hlhgat_proj_fwd_bn workspace per (device, stream), as bn_workspace.
+Tensor pbn_workspace(const Tensor& like, int64_t M, int64_t N) {
+  static auto* cache = new std::unordered_map<uintptr_t, Tensor>();
+  const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
+  const int64_t need = hlhgat_proj_fwd_bn_workspace_bytes(M, N);
+  auto it = cache->find(key);
+  if (it == cache->end() || it->second.numel() < need) {
+    Tensor ws = at::empty({std::max<int64_t>(need, 1 << 20)}, like.options().dtype(at::kByte));
+    chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream_of(like)), "zero_fill");
+    (*cache)[key] = ws;
+  }
+  return (*cache)[key];
+}
+
+// pre = sum_b A_b W_b^T + bias with its BatchNorm statistics formed in the
+// GEMM epilogue, then y = BN apply (+ReLU) into y_into or a new tensor.
+Tensor proj_bn_forward(const std::vector<const float*>& A, const std::vector<int64_t>& lda,
+                       const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
+                       const std::vector<int64_t>& kb, int64_t M, int64_t N, const float* bias,
+                       Tensor& pre, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
+                       const Tensor* y_into = nullptr) {
+  void* s = stream_of(pre);
+  mean = at::empty({N}, pre.options());
+  invstd = at::empty({N}, pre.options());
+  Tensor ws = pbn_workspace(pre, M, N);
+  int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
+  chk(hlhgat_proj_fwd_bn((int)A.size(), A.data(), lda.data(), W.data(), ldw.data(), kb.data(), M,
+                         N, bias, pre.data_ptr<float>(), ld_of(pre), iptr(st.valid), mfptr(st.rm),
+                         mfptr(st.rv), nbt, (float)st.momentum, (float)st.eps,
+                         mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr(),
+                         ws.numel(), s),
+      "proj_fwd_bn");
+  Tensor y = y_into ? *y_into : at::empty({M, N}, pre.options());
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N && y.stride(1) == 1, "hlhgat: bad BN output view");
+  chk(hlhgat_bn_apply(pre.data_ptr<float>(), ld_of(pre), M, iptr(st.valid), N, fptr(st.w),
+                      fptr(st.b), mean.data_ptr<float>(), invstd.data_ptr<float>(), relu ? 1 : 0,
+                      y.data_ptr<float>(), ld_of(y), s),
+      "bn_apply");
+  return y;
+}
+
 // returns dx; fills dw/db when requested
 // dx_into: optional [n, C] row-strided destination (e.g. a column slice)
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
@@ -353,15 +410,21 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                       out_buf->device() == x.device(),
                   "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
     Tensor pre = (sink && bn_mode == 0) ? *out_buf : at::empty({M, dout}, x.options());
-    if (M > 0) {
-      proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, s);
-    } else if (has(bias)) {
-      pre.copy_(bias->expand_as(pre));
-    }
     Tensor out = pre, mean, invstd;
-    if (bn_mode > 0) {
+    if (bn_mode > 0 && M > 0 && fused_bn_stats()) {  // statistics in the GEMM epilogue
       BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
-      out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
+      out = proj_bn_forward(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, st, bn_mode == 2, mean,
+                            invstd, sink ? &*out_buf : nullptr);
+    } else {
+      if (M > 0) {
+        proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, s);
+      } else if (has(bias)) {
+        pre.copy_(bias->expand_as(pre));
+      }
+      if (bn_mode > 0) {
+        BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
+        out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
+      }
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, Cin, F, M, dout, K, kind, nnz, bn_mode,
                                                    has(bias) ? 1 : 0};
@@ -609,6 +672,34 @@ Tensor linear_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT
   return out;
 }
 
+// Linear(blocks) -> BatchNorm (+ReLU): h (the BN input) is returned through
+// `h`, the activation as the result; the statistics come from the GEMM
+// epilogue when fused_bn_stats().
+Tensor linear_bn_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT& b,
+                         const BnState& st, bool relu, Tensor& h, Tensor& mean, Tensor& invstd) {
+  const int64_t M = As[0].size(0), N = W.size(0);
+  if (M == 0 || !fused_bn_stats()) {
+    h = linear_forward(As, W, b);
+    return bn_forward(h, st, relu, mean, invstd);
+  }
+  const int nb = (int)As.size();
+  std::vector<const float*> Ap(nb), Wp(nb);
+  std::vector<int64_t> lda(nb), ldw(nb), kb(nb);
+  int64_t off = 0;
+  for (int i = 0; i < nb; ++i) {
+    Ap[i] = As[i].data_ptr<float>();
+    lda[i] = ld_of(As[i]);
+    kb[i] = As[i].size(1);
+    Wp[i] = W.data_ptr<float>() + off;
+    ldw[i] = W.stride(0);
+    off += kb[i];
+  }
+  TORCH_CHECK(off == W.size(1), "hlhgat: Linear expects ", W.size(1), " input features, got ",
+              off);
+  h = at::empty({M, N}, W.options());
+  return proj_bn_forward(Ap, lda, Wp, ldw, kb, M, N, fptr(b), h, st, relu, mean, invstd);
+}
+
 // grads of linear_forward; dAs[i] only where need_a[i]
 void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Tensor& W,
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
@@ -721,11 +812,11 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     }
     Tensor W0c = W0.stride(1) == 1 ? W0 : W0.contiguous();
     Tensor W3c = W3.stride(1) == 1 ? W3 : W3.contiguous();
-    Tensor h1 = linear_forward(blocks, W0c, b0);
-    Tensor m1, i1, m4, i4;
-    Tensor a1 = bn_forward(h1, BnState{g1, be1, rm1, rv1, nbt1, mom1, eps1}, true, m1, i1);
-    Tensor h2 = linear_forward({a1}, W3c, b3);
-    Tensor y = bn_forward(h2, BnState{g4, be4, rm4, rv4, nbt4, mom4, eps4}, true, m4, i4);
+    Tensor h1, h2, m1, i1, m4, i4;
+    Tensor a1 = linear_bn_forward(blocks, W0c, b0, BnState{g1, be1, rm1, rv1, nbt1, mom1, eps1},
+                                  true, h1, m1, i1);
+    Tensor y = linear_bn_forward({a1}, W3c, b3, BnState{g4, be4, rm4, rv4, nbt4, mom4, eps4},
+                                 true, h2, m4, i4);
     ctx->saved_data["nb"] = (int64_t)blocks.size();
     {
       EdgeMap em;
@@ -1004,9 +1095,9 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       o.a1 = bn_forward(h1, BnState{p[2], p[3], p[4], p[5], p[6], m1, e1, valid}, true, o.m1,
                         o.i1);
       Tensor W3 = p[7].stride(1) == 1 ? p[7] : p[7].contiguous();
-      o.h2 = linear_forward({o.a1}, W3, p[8]);
-      o.y = bn_forward(o.h2, BnState{p[9], p[10], p[11], p[12], p[13], m4, e4, valid}, true,
-                       o.m4, o.i4);
+      o.y = linear_bn_forward({o.a1}, W3, p[8],
+                              BnState{p[9], p[10], p[11], p[12], p[13], m4, e4, valid}, true,
+                              o.h2, o.m4, o.i4);
     };
     auto lin_into = [](const Tensor& A, const Tensor& W, const Tensor& b, Tensor& out) {
       if (A.size(0) > 0)
@@ -1236,6 +1327,7 @@ std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
+  m.def("set_fused_bn_stats", &set_fused_bn_stats);
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);

@@ -79,6 +79,14 @@ SIGNATURES = {
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                     c_vp]),
+    "hlhgat_bn_stats_train": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32,
+                                      c_f32, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_bn_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32,
+                                c_vp, c_i64, c_vp]),
+    "hlhgat_proj_fwd_bn_workspace_bytes": (c_i64, [c_i64, c_i64]),
+    "hlhgat_proj_fwd_bn": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
+                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp,
+                                   c_vp, c_i64, c_vp]),
     "hlhgat_zero_fill": (c_i32, [c_vp, c_sz, c_vp]),
     "hlhgat_copy2d_batched": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlhgat_prof_enable": (c_i32, [c_i32, c_i32]),

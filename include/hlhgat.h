@@ -368,6 +368,42 @@ int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
                         int64_t workspace_bytes, void* stream);
 /* Backward; y (the forward output) supplies the ReLU mask, NULL if no ReLU.
  * dweight/dbias may be NULL. */
+/* The two halves of hlhgat_bn_fwd_train: statistics only (save_mean /
+ * save_invstd, running stats, num_batches_tracked) and apply only
+ * (y = relu?(x * s + t) with s = weight * invstd, t = bias - mean * s; rows
+ * >= *n_valid written as 0). */
+int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n, const int32_t* n_valid,
+                          int64_t C, float* running_mean, float* running_var,
+                          int64_t* num_batches_tracked, float momentum, float eps,
+                          float* save_mean, float* save_invstd, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_valid, int64_t C,
+                    const float* weight, const float* bias, const float* save_mean,
+                    const float* save_invstd, int relu, float* y, int64_t ldy, void* stream);
+
+/* Projection + BatchNorm statistics in one launch: C = sum_b A_b W_b^T + bias
+ * (hlhgat_proj_fwd, accumulate = 0), and the training-mode BatchNorm1d
+ * statistics of C's first min(M, *n_valid) rows (as hlhgat_bn_stats_train)
+ * formed in the GEMM epilogue: fp64 column partials of every 64-row tile,
+ * combined by a deterministic two-level last-arriver tree, so the separate
+ * statistics pass over C (a launch and a full read per BatchNorm) is gone.
+ * The conv -> BN tail of every HL block (lib/Hodge_ST_Model.py:556-566) and
+ * the second Linear -> BN of NodeEdgeInt's WV_* (lib/Hodge_Cheb_Conv.py:
+ * 276-289).  Follow with hlhgat_bn_apply.  Shapes the fused epilogue does not
+ * cover (unaligned operands) fall back to hlhgat_proj_fwd +
+ * hlhgat_bn_stats_train on the same workspace (same results up to fp64
+ * summation order).  Workspace: hlhgat_proj_fwd_bn_workspace_bytes(M, N),
+ * zero-filled before its first use, not shared by concurrent launches; the
+ * kernels leave it reusable. */
+int64_t hlhgat_proj_fwd_bn_workspace_bytes(int64_t M, int64_t N);
+int hlhgat_proj_fwd_bn(int nblocks, const float* const* A, const int64_t* lda,
+                       const float* const* W, const int64_t* ldw, const int64_t* kb,
+                       int64_t M, int64_t N, const float* bias, float* C, int64_t ldc,
+                       const int32_t* n_valid, float* running_mean, float* running_var,
+                       int64_t* num_batches_tracked, float momentum, float eps,
+                       float* save_mean, float* save_invstd, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
                         const float* dy, int64_t lddy, int64_t n,
                         const int32_t* n_valid, int64_t C,

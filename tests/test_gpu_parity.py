@@ -862,3 +862,101 @@ def test_tsp_model_factored_vs_reference_golden(cuda):
             assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
             continue
         close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
+
+
+# ---------------------------------------------------------------------------
+# projection + BatchNorm statistics in the GEMM epilogue (hlhgat_proj_fwd_bn)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("M,N,kbs,nvalid", [(1000, 64, [64, 64, 64], None), (63, 32, [36], None),
+                                            (70001, 64, [128, 64], 69000), (5000, 256, [192], 4999),
+                                            (777, 16, [20, 8], None), (300, 48, [18, 18], 290)])
+def test_proj_fwd_bn_stats_match_torch(cuda, M, N, kbs, nvalid):
+    """C equals hlhgat_proj_fwd bitwise; mean / invstd / running stats /
+    num_batches_tracked equal a float64 torch evaluation over the first
+    n_valid rows (1e-6 relative); both the fused epilogue (kb % 4 == 0) and the
+    unfused fallback (kb = 18, 20) are exercised; the workspace is reused."""
+    import ctypes as C
+    from hlhgat import _lib, ops
+    g = torch.Generator().manual_seed(M + N)
+    As = [torch.randn(M, k, generator=g).to(cuda) for k in kbs]
+    W = torch.randn(N, sum(kbs), generator=g).to(cuda)
+    Ws, o = [], 0
+    for k in kbs:
+        Ws.append(W[:, o:o + k])
+        o += k
+    bias = torch.randn(N, generator=g).to(cuda)
+    ref_C = torch.empty(M, N, device=cuda)
+    ops._proj_fwd(As, Ws, M, N, bias, ref_C)
+    wsb = int(_lib.LIB.hlhgat_proj_fwd_bn_workspace_bytes(M, N))
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=cuda)
+    nv = torch.tensor([nvalid], dtype=torch.int32, device=cuda) if nvalid else None
+    n_eff = nvalid or M
+    rm, rv = torch.zeros(N, device=cuda), torch.ones(N, device=cuda)
+    nbt = torch.zeros(1, dtype=torch.int64, device=cuda)
+    arr = lambda ct, v: (ct * len(v))(*v)  # noqa: E731
+    for it in range(2):
+        Cm = torch.empty(M, N, device=cuda)
+        mean, invstd = torch.empty(N, device=cuda), torch.empty(N, device=cuda)
+        _lib.check(_lib.LIB.hlhgat_proj_fwd_bn(
+            len(kbs), arr(C.c_void_p, [a.data_ptr() for a in As]), arr(C.c_int64, [a.stride(0) for a in As]),
+            arr(C.c_void_p, [w.data_ptr() for w in Ws]), arr(C.c_int64, [w.stride(0) for w in Ws]),
+            arr(C.c_int64, kbs), M, N, bias.data_ptr(), Cm.data_ptr(), N,
+            nv.data_ptr() if nv is not None else None, rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(),
+            0.1, 1e-5, mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), wsb,
+            torch.cuda.current_stream().cuda_stream), "proj_fwd_bn")
+        torch.cuda.synchronize()
+        assert torch.equal(Cm, ref_C)
+        x = ref_C[:n_eff].double()
+        var, mu = torch.var_mean(x, dim=0, unbiased=False)
+        close(mean.cpu(), mu.cpu(), 1e-6, "mean")
+        close(invstd.cpu(), (1.0 / torch.sqrt(var + 1e-5)).cpu(), 1e-6, "invstd")
+    assert int(nbt.item()) == 2
+    unb = torch.var(x, dim=0, unbiased=True)
+    close(rm.cpu(), (0.19 * mu).float().cpu(), 1e-5, "running_mean")
+    close(rv.cpu(), (0.81 + 0.19 * unb).float().cpu(), 1e-5, "running_var")
+
+
+def test_fused_bn_stats_conv_matches_unfused(cuda):
+    """conv -> BN -> ReLU node and the NodeEdgeInt MLP with the statistics from
+    the GEMM epilogue equal the separate statistics pass (forward, dX, weight
+    and BN gradients, running stats) to fp64-summation-order noise."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(64, seed=3).to(cuda)
+    torch.manual_seed(0)
+    conv = hlhgat.HodgeLaguerreConv(32, 64, K=3).to(cuda)
+    nei = hlhgat.NodeEdgeInt(d=32, dv=64).to(cuda).train()
+    bn = torch.nn.BatchNorm1d(64).to(cuda)
+    xs = torch.randn(b.x_s.shape[0], 32, device=cuda)
+    xt = torch.randn(b.x_t.shape[0], 32, device=cuda)
+    from hlhgat.hodge_dataset import adj2par1, degree
+    outs = []
+    try:
+        for fused in (True, False):
+            ops._ext.set_fused_bn_stats(fused)
+            ops.clear_caches()
+            x = xs.clone().requires_grad_(True)
+            op = ops.hodge_operator(b.edge_index_s, b.edge_weight_s, b.x_s.shape[0])
+            y = ops.hodge_poly_conv(x, op, [l.weight for l in conv.lins], conv.bias,
+                                    ops.POLY_LAGUERRE, bn=bn, relu=True)
+            par = adj2par1(b.edge_index, b.x_t.shape[0], b.x_s.shape[0])
+            D = degree(b.edge_index.view(-1), num_nodes=b.x_t.shape[0]) + 1e-6
+            t1, s1 = nei(xt, x, par, D)
+            w = torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)
+            ((y * w).sum() + (t1 * t1).sum() + (s1 * w).sum()).backward()
+            outs.append({"y": y.detach().cpu(), "t1": t1.detach().cpu(), "gx": x.grad.cpu(),
+                         "gw": conv.lins[1].weight.grad.cpu().clone(),
+                         "gbn": bn.weight.grad.cpu().clone(), "rm": bn.running_mean.cpu().clone(),
+                         "gnei": [p.grad.cpu().clone() for p in nei.parameters() if p.grad is not None]})
+            conv.zero_grad()
+            nei.zero_grad()
+            bn.zero_grad()
+    finally:
+        ops._ext.set_fused_bn_stats(False)
+    for k in outs[0]:
+        if k == "gnei":
+            for a, c in zip(outs[0][k], outs[1][k]):
+                close(a, c, 1e-4, "NodeEdgeInt grad")
+        else:
+            close(outs[0][k], outs[1][k], 1e-5 if k in ("y", "t1", "rm") else 1e-4, k)
