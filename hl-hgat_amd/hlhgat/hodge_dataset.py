@@ -21,7 +21,8 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "graph_tiles", "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc"]
+           "graph_tiles", "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc",
+           "hodge_factor_ok", "hodge_coo_from_boundary"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
 _HODGE_KEYS = ("edge_index_s", "edge_index_t")
@@ -585,6 +586,37 @@ def hodge_laplacians(edge_index: np.ndarray, n: int):
     L0 = 2 * torch.matmul(par1, par1.T) / maxeig
     L1 = 2 * torch.matmul(par1.T, par1) / maxeig
     return L0, L1, maxeig, par1
+
+
+def hodge_coo_from_boundary(edge_index, n: int, lmax: float):
+    """Sparse (row-major sorted) COO of L0 = 2 B1 B1^T / lmax and
+    L1 = 2 B1^T B1 / lmax from the edge list (i<j) and a given lmax, with the
+    entries the reference's dense float32 construction produces
+    (lib/Hodge_Dataset.py:451-456: fl(fl(2 v) / lmax), v the integer entry of
+    B1 B1^T / B1^T B1; zeros dropped as dense_to_sparse does) -- without the
+    dense [E, E] L1 (1.37 M entries for the DEMO brain skeleton, ~10 GB dense
+    at BASELINE config 5).  Returns (ei_t, w_t, ei_s, w_s) as torch tensors."""
+    import scipy.sparse as sp
+    ei = np.asarray(edge_index, dtype=np.int64)
+    E = ei.shape[1]
+    B = sp.csr_matrix((np.concatenate([-np.ones(E), np.ones(E)]).astype(np.int64),
+                       (np.concatenate([ei[0], ei[1]]), np.concatenate([np.arange(E)] * 2))),
+                      shape=(n, E))
+    lam = np.float32(lmax)
+
+    def coo(M):
+        M = M.tocoo()
+        M.sum_duplicates()
+        o = np.lexsort((M.col, M.row))
+        r, c, v = M.row[o], M.col[o], M.data[o]
+        keep = v != 0
+        w = (np.float32(2.0) * v[keep].astype(np.float32)) / lam
+        return (torch.from_numpy(np.stack([r[keep], c[keep]]).astype(np.int64)),
+                torch.from_numpy(w.astype(np.float32)))
+
+    ei_t, w_t = coo(B @ B.T)
+    ei_s, w_s = coo(B.T @ B)
+    return ei_t, w_t, ei_s, w_s
 
 
 # ----------------------------------------------------------------------------

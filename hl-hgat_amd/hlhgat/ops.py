@@ -363,6 +363,21 @@ def _halo_args(A: "SparseCSR"):
     return A.halo
 
 
+def copy_words_batched(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
+    """dst.copy_(src) for contiguous same-size tensors whose byte size is a
+    multiple of 4, up to HLHGAT_MAX_COPY_BLOCKS per launch
+    (hlhgat_copy2d_batched over 4-byte words), on the current stream."""
+    n = len(srcs)
+    for i in range(0, n, 8):
+        ss, ds = srcs[i:i + 8], dsts[i:i + 8]
+        words = [t.numel() * t.element_size() // 4 for t in ss]
+        m = len(ss)
+        check(LIB.hlhgat_copy2d_batched(
+            m, _arr(C.c_void_p, [t.data_ptr() for t in ss]), _arr(C.c_int64, words),
+            _arr(C.c_void_p, [t.data_ptr() for t in ds]), _arr(C.c_int64, words),
+            _arr(C.c_int64, [1] * m), _arr(C.c_int64, words), _stream(ds[0])), "copy2d_batched")
+
+
 def _factor_args(op: "HodgeOperator"):
     """The factor arguments of the C++ conv node ([] = CSR path)."""
     if op.factor is None:

@@ -57,10 +57,23 @@ class _Captured:
         self.loss = loss
 
     def load(self, batch):
+        """Copy a batch into the graph's static buffers: every contiguous
+        same-device tensor goes into batched-copy launches (up to 8 tensors
+        per launch, hlhgat_copy2d_batched) instead of one copy launch each
+        (15 at the ZINC shape, ~75 us of serial copy kernels per step)."""
+        pend = []
         for k, v in _tensor_items(batch):
             dst = getattr(self.batch, k)
-            if dst.data_ptr() != v.data_ptr():
+            if dst.data_ptr() == v.data_ptr():
+                continue
+            if (v.is_cuda and dst.device == v.device and v.is_contiguous() and dst.is_contiguous()
+                    and v.dtype == dst.dtype and v.numel() == dst.numel()
+                    and (v.numel() * v.element_size()) % 4 == 0):
+                pend.append((v, dst))
+            else:
                 dst.copy_(v, non_blocking=True)
+        if pend:
+            ops.copy_words_batched([p[0] for p in pend], [p[1] for p in pend])
 
 
 class TrainStep:

@@ -960,3 +960,35 @@ def test_fused_bn_stats_conv_matches_unfused(cuda):
                 close(a, c, 1e-4, "NodeEdgeInt grad")
         else:
             close(outs[0][k], outs[1][k], 1e-5 if k in ("y", "t1", "rm") else 1e-4, k)
+
+
+@pytest.mark.parametrize("side,factored", [("t", False), ("s", False), ("s", True)])
+def test_brain_skeleton_conv_vs_reference_golden(cuda, side, factored):
+    """HodgeLaguerreConv(8, 8, K=3) on the reference's brain skeleton
+    (HL-HGAT-DEMO data: 268 nodes, 8997 edges, nnz(L1) 1.37 M, 152 entries
+    per L1 row; L0 / L1 rebuilt bitwise by hodge_coo_from_boundary) against
+    the reference's forward and gradients: CSR operator and factored L1."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import hodge_coo_from_boundary
+    g = load_golden("brain_skeleton")
+    n = int(g["n_nodes"])
+    ei_t, w_t, ei_s, w_s = hodge_coo_from_boundary(g["edge_index"], n, float(g["lmax"]))
+    e, w = (ei_t, w_t) if side == "t" else (ei_s, w_s)
+    e = ops.mark_hodge(dev(e))
+    if factored:
+        ops.set_hodge_factor(e, dev(g["edge_index"]), n)
+    conv = hlhgat.HodgeLaguerreConv(8, 8, K=3).to(cuda)
+    with torch.no_grad():
+        for k, lin in enumerate(conv.lins):
+            lin.weight.copy_(dev(g[f"{side}/w{k}"]))
+        conv.bias.copy_(dev(g[f"{side}/bias"]))
+    x = dev(g[f"{side}/x"]).requires_grad_(True)
+    out = conv(x, e, dev(w))
+    assert (ops.hodge_operator(e, dev(w), x.shape[0]).factor is not None) == factored
+    close(out.detach().cpu(), g[f"{side}/out"], 1e-5, "out")
+    (out * dev(g[f"{side}/R"])).sum().backward()
+    close(x.grad.cpu(), g[f"{side}/gx"], 1e-4, "dx")
+    close(conv.bias.grad.cpu(), g[f"{side}/gbias"], 1e-4, "dbias")
+    for k, lin in enumerate(conv.lins):
+        close(lin.weight.grad.cpu(), g[f"{side}/gw{k}"], 1e-4, f"dW{k}")
