@@ -105,8 +105,11 @@ __device__ __forceinline__ void poly_epilogue(const PolyArgs& a, int64_t row, in
     vstore<V>(a.Y + row * a.ldy + f, out);
 }
 
-template <int V, int LPR>
-__global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
+// DEPTH gathers in flight per lane (4; 8 for long rows, k_poly_step_deep).
+// Loads are issued DEPTH at a time, the adds stay in CSR order (bitwise the
+// same result for any DEPTH).
+template <int V, int LPR, int DEPTH>
+__device__ __forceinline__ void poly_step_body(const PolyArgs& a) {
   using vt = typename VecT<V>::type;
   // XCD-aware slots: blocks are dealt round-robin over the 8 XCDs, so block b
   // takes slot range xcd_slot(b): each XCD walks ONE contiguous range of the
@@ -133,6 +136,29 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
       const float wm = me < e1 ? (a.val ? a.val[me] : 1.f) : 0.f;
       const int cnt = e1 - eb < LPR ? e1 - eb : LPR;
       int j = 0;
+      if constexpr (DEPTH == 8) {
+        for (; j + 7 < cnt; j += 8) {  // eight gathers in flight per lane
+          int c[8];
+          float w[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            c[u] = __shfl(cm, j + u, LPR);
+            w[u] = __shfl(wm, j + u, LPR);
+          }
+          if (fok) {
+            vt x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = vload<V>(X + (int64_t)c[u] * a.ldx + f);
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+              float s = vget(acc, i);
+#pragma unroll
+              for (int u = 0; u < 8; ++u) s = s + w[u] * vget(x[u], i);
+              vget(acc, i) = s;
+            }
+          }
+        }
+      }
       for (; j + 3 < cnt; j += 4) {  // four gathers in flight per lane
         const int c0 = __shfl(cm, j, LPR), c1 = __shfl(cm, j + 1, LPR),
                   c2 = __shfl(cm, j + 2, LPR), c3 = __shfl(cm, j + 3, LPR);
@@ -167,6 +193,16 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
     if (!fok) continue;
     poly_epilogue<V>(a, row, f, acc, rsv);
   }
+}
+
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
+  poly_step_body<V, LPR, 4>(a);
+}
+
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_poly_step_deep(PolyArgs a) {
+  poly_step_body<V, LPR, 8>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -960,7 +996,12 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s, int prof_class = HLHGAT
       return HLHGAT_OK;
     }
   }
-  HLH_DISPATCH_VL(v, l, k_poly_step, a.n_rows, s, a, &prof);
+  // long rows (>= 12 entries on average: high-degree L1 such as the DEMO brain
+  // skeleton's 152 per row) keep 8 gathers in flight per lane
+  if (a.n_rows > 0 && nnz >= 12 * a.n_rows && l >= 8)
+    HLH_DISPATCH_VL(v, l, k_poly_step_deep, a.n_rows, s, a, &prof);
+  else
+    HLH_DISPATCH_VL(v, l, k_poly_step, a.n_rows, s, a, &prof);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

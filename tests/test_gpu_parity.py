@@ -932,8 +932,12 @@ def test_fused_bn_stats_conv_matches_unfused(cuda):
     xt = torch.randn(b.x_t.shape[0], 32, device=cuda)
     from hlhgat.hodge_dataset import adj2par1, degree
     outs = []
+    sd_bn = {k: v.clone() for k, v in bn.state_dict().items()}
+    sd_nei = {k: v.clone() for k, v in nei.state_dict().items()}
     try:
         for fused in (True, False):
+            bn.load_state_dict(sd_bn)  # same running statistics before each pass
+            nei.load_state_dict(sd_nei)
             ops._ext.set_fused_bn_stats(fused)
             ops.clear_caches()
             x = xs.clone().requires_grad_(True)
