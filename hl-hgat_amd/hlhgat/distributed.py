@@ -95,3 +95,37 @@ def max_over_ranks(value: float, device: torch.device = torch.device("cpu")) -> 
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class _GlobalMax(torch.autograd.Function):
+    """max over all elements on all ranks (all_reduce MAX; no host sync).
+    Backward: the gradient flows to the positions holding the global max
+    (torch.max's subgradient, ties split evenly on the owning ranks)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        m = x.max().reshape(1).clone()
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        ctx.save_for_backward(x, m)
+        return m.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, m = ctx.saved_tensors
+        hit = (x == m).to(x.dtype)
+        cnt = hit.sum().reshape(1)
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(cnt)
+        return hit * (g / cnt)
+
+
+def global_max(x: torch.Tensor) -> torch.Tensor:
+    """x.max() over the whole data-parallel batch: the attpool heads divide
+    the attention by its batch max (lib/Hodge_ST_Model.py:1061-1062), which
+    under graph sharding must span every rank's graphs to equal the
+    single-process result (parity caveat 2).  One process: x.max()."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return x.max()
+    return _GlobalMax.apply(x)
+

@@ -12,6 +12,7 @@ from torch.nn import Dropout, Linear
 
 from . import ops
 from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt, cluster_mean
+from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
 from .nn import BatchNorm, Sequential, run_sequential
 
@@ -322,8 +323,9 @@ class _AttPoolHead(nn.Module):
             if i == self.pool_loc:
                 if not self.att_every_level:
                     att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t, x_s, par_1, D)
-                    att_t = att_t / att_t.max()
-                    att_s = att_s / att_s.max()
+                    # batch-global max (all ranks under data parallelism)
+                    att_t = att_t / global_max(att_t)
+                    att_s = att_s / global_max(att_s)
                     x_t = x_t * att_t
                     x_s = x_s * att_s
                 d1 = datas[k + 1]

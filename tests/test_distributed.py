@@ -96,3 +96,38 @@ def test_ddp_gloo_two_ranks_matches_mean_of_shard_gradients():
     for k, v in ref.items():
         scale = max(1.0, float(v.abs().max()))
         assert float(abs(torch.from_numpy(g0[k]) - v).max()) <= 1e-5 * scale, k
+
+
+def _gmax_worker(rank, world, port, out_q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "hl-hgat_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from hlhgat.distributed import global_max, init_distributed
+    init_distributed("gloo")
+    x = torch.arange(5.0).mul(rank + 1).add(rank).requires_grad_(True)  # max on rank 1 only
+    m = global_max(x)
+    (3.0 * m).backward()
+    out_q.put((rank, float(m), x.grad.tolist()))
+    dist.destroy_process_group()
+
+
+def test_global_max_two_ranks_matches_single_process():
+    """att / att.max() of the attpool heads (lib/Hodge_ST_Model.py:1061-1062)
+    is a BATCH max: under graph sharding it must span every rank (SURVEY §8e
+    caveat 2).  global_max over 2 gloo ranks == max of the concatenation, and
+    its gradient lands where the single-process torch max puts it."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gmax_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (m, g)) for r, m, g in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+    xs = [torch.arange(5.0).mul(r + 1).add(r).requires_grad_(True) for r in range(world)]
+    m_ref = torch.cat(xs).max()
+    (3.0 * m_ref).backward()
+    for r in range(world):
+        assert res[r][0] == float(m_ref)
+        assert res[r][1] == xs[r].grad.tolist()
