@@ -63,13 +63,25 @@ int64_t bn_parts(int64_t n) {
   return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
 }
 
-BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
+// Threads per workgroup of the two reduction passes (statistics, backward
+// reduce): same partition count, 4x the rows in flight per partition with
+// 1024.  HLHGAT_BN_RED_THREADS=256|1024 (A/B).
+int bn_red_threads() {
+  static int v = [] {
+    const char* e = getenv("HLHGAT_BN_RED_THREADS");
+    const int t = e ? atoi(e) : 256;
+    return t == 1024 ? 1024 : 256;
+  }();
+  return v;
+}
+
+BnLayout bn_layout(int64_t n, int64_t C, bool vec, int nt = kThreads) {
   BnLayout L;
   L.v = vec ? 4 : 1;
   int lanes = (int)ceil_div(C, L.v);
   L.tpr = next_pow2(lanes);
   if (L.tpr > kThreads / L.v) L.tpr = kThreads / L.v;  // tile_c <= kThreads
-  L.rp = kThreads / L.tpr;
+  L.rp = nt / L.tpr;
   L.tile_c = L.tpr * L.v;
   L.tiles = (int)ceil_div(C, L.tile_c);
   // <= kMaxParts row partitions per column tile (fat partitions keep the
@@ -155,22 +167,36 @@ struct StatsArgs {
   float* dbias;
 };
 
+// Partials are handed to the last-arriving workgroup WRITE-THROUGH: 8-byte
+// agent-scope atomic stores (global_store_dwordx2 sc1) drained by every
+// storing wave, read back with sc1 loads -- no release fence (buffer_wbl2,
+// which writes back the XCD L2's dirty lines: the freshly written BN input
+// and everything else the concurrent stream left dirty, 1.7-6.5 us per
+// workgroup) and no acquire fence (cdna_hip_programming.md Guideline 16 R1;
+// MI355X_MICROARCH.md visibility table).
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Signal arrival; returns true in the last workgroup of this column tile.
+// Every wave has drained its write-through partial stores (vmcnt(0)) before
+// the barrier; ONE lane adds to the counter; the workgroup whose add returned
+// total-1 reads the partials (sc1 loads) after the second barrier.
 __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
     s_last = (prev == total - 1) ? 1u : 0u;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *counter = 0u;  // ready for the next launch (stream-ordered)
-    }
+    if (s_last) *counter = 0u;  // ready for the next launch (stream-ordered)
   }
   __syncthreads();
   return s_last != 0u;
@@ -178,10 +204,10 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
 
 // Block-level column partials: threads (row group rg, column lane cl) hold V
 // columns each; reduce over the rp row groups through LDS in fixed order.
-template <int V>
+template <int V, int NT>
 __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
                                                const StatsArgs& a, int c0) {
-  __shared__ double red[2][kThreads * 4];
+  __shared__ double red[2][NT * 4];
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
 #pragma unroll
@@ -190,7 +216,7 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
     red[1][rg * a.tpr * V + cl * V + v] = s1[v];
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < a.tpr * V; t += kThreads) {
+  for (int t = threadIdx.x; t < a.tpr * V; t += NT) {
     double u0 = 0.0, u1 = 0.0;
     for (int g = 0; g < a.rp; ++g) {
       u0 += red[0][g * a.tpr * V + t];
@@ -199,8 +225,8 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
     const int c = c0 + t;
     if (c < a.C) {
       double* dst = a.part + ((int64_t)blockIdx.x * a.C + c) * 2;
-      dst[0] = u0;
-      dst[1] = u1;
+      st_wt(dst, u0);
+      st_wt(dst + 1, u1);
     }
   }
 }
@@ -209,11 +235,12 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
 // columns: all 256 threads take part (column t % tile_c, partial group
 // t / tile_c, loads in batches of 16), groups combined in fixed order through
 // LDS -> deterministic.  Result in out0/out1[0 .. tile_c).
+template <int NT>
 __device__ __forceinline__ void reduce_range(const double* src, int first, int count,
                                              const StatsArgs& a, int c0, int tile_c,
                                              double* out0, double* out1) {
-  __shared__ double fin[2][kThreads];
-  const int groups = kThreads / tile_c > 0 ? kThreads / tile_c : 1;
+  __shared__ double fin[2][NT];
+  const int groups = NT / tile_c > 0 ? NT / tile_c : 1;
   const int t = threadIdx.x % tile_c;
   const int grp = threadIdx.x / tile_c;
   const int c = c0 + t;
@@ -228,8 +255,8 @@ __device__ __forceinline__ void reduce_range(const double* src, int first, int c
         const int p = p0 + pb + u;
         const bool ok = pb + u < per && p < count;
         const double* q = src + ((int64_t)(first + (ok ? p : 0)) * a.C + c) * 2;
-        v0[u] = ok ? q[0] : 0.0;
-        v1[u] = ok ? q[1] : 0.0;
+        v0[u] = ok ? ld_wt(q) : 0.0;
+        v1[u] = ok ? ld_wt(q + 1) : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -257,6 +284,7 @@ __device__ __forceinline__ void reduce_range(const double* src, int first, int c
 // the last workgroup of each group of kGroup partitions sums its group, the
 // last group sums the group partials.  Returns true (sums in out0/out1) in
 // the one workgroup that finalises; fixed summation order at both levels.
+template <int NT>
 __device__ __forceinline__ bool tree_reduce(const StatsArgs& a, int c0, int tile_c,
                                             double* out0, double* out1) {
   const int tile = blockIdx.y;
@@ -265,23 +293,23 @@ __device__ __forceinline__ bool tree_reduce(const StatsArgs& a, int c0, int tile
   const int first = g * kGroup;
   const int cnt = a.parts - first < kGroup ? a.parts - first : kGroup;
   if (!arrive_last(a.count + kMaxTiles + tile * kMaxGroups + g, (unsigned)cnt)) return false;
-  reduce_range(a.part, first, cnt, a, c0, tile_c, out0, out1);
+  reduce_range<NT>(a.part, first, cnt, a, c0, tile_c, out0, out1);
   if (ng == 1) return true;
-  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+  for (int t = threadIdx.x; t < tile_c; t += NT) {
     const int c = c0 + t;
     if (c < a.C) {
       double* dst = a.gpart + ((int64_t)g * a.C + c) * 2;
-      dst[0] = out0[t];
-      dst[1] = out1[t];
+      st_wt(dst, out0[t]);
+      st_wt(dst + 1, out1[t]);
     }
   }
   if (!arrive_last(a.count + tile, (unsigned)ng)) return false;
-  reduce_range(a.gpart, 0, ng, a, c0, tile_c, out0, out1);
+  reduce_range<NT>(a.gpart, 0, ng, a, c0, tile_c, out0, out1);
   return true;
 }
 
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
+template <int V, int NT>
+__global__ __launch_bounds__(NT) void k_bn_stats(StatsArgs a) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -319,12 +347,12 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
       }
     }
   }
-  write_partials<V>(s0, s1, a, c0);
+  write_partials<V, NT>(s0, s1, a, c0);
   // the finalising workgroup of this column tile: finalise its columns
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  if (!tree_reduce(a, c0, tile_c, sum0, sum1)) return;
-  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+  if (!tree_reduce<NT>(a, c0, tile_c, sum0, sum1)) return;
+  for (int t = threadIdx.x; t < tile_c; t += NT) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
     const double u0 = sum0[t], u1 = sum1[t];
@@ -398,8 +426,8 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
   }
 }
 
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
+template <int V, int NT>
+__global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -447,11 +475,11 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
       acc(xv, gv, yv);
     }
   }
-  write_partials<V>(s0, s1, a, c0);
+  write_partials<V, NT>(s0, s1, a, c0);
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  if (!tree_reduce(a, c0, tile_c, sum0, sum1)) return;
-  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+  if (!tree_reduce<NT>(a, c0, tile_c, sum0, sum1)) return;
+  for (int t = threadIdx.x; t < tile_c; t += NT) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
     const double sg = sum0[t], sgx = sum1[t];
@@ -564,7 +592,8 @@ extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
   HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
                 "bn_stats_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx}, {x});
-  BnLayout L = bn_layout(n, C, vec);
+  const int nt = bn_red_threads();
+  BnLayout L = bn_layout(n, C, vec, nt);
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_stats_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
@@ -590,10 +619,14 @@ extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
   s.save_invstd = save_invstd;
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
-  if (vec)
-    k_bn_stats<4><<<g1, kThreads, 0, st>>>(s);
+  if (nt == 1024 && vec)
+    k_bn_stats<4, 1024><<<g1, 1024, 0, st>>>(s);
+  else if (nt == 1024)
+    k_bn_stats<1, 1024><<<g1, 1024, 0, st>>>(s);
+  else if (vec)
+    k_bn_stats<4, kThreads><<<g1, kThreads, 0, st>>>(s);
   else
-    k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
+    k_bn_stats<1, kThreads><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -655,6 +688,8 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
                 "bn_bwd_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
   BnLayout L = bn_layout(n, C, vec);
+  const int nt = bn_red_threads();
+  const BnLayout Lr = bn_layout(n, C, vec, nt);
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s{};
@@ -667,11 +702,11 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   s.lddy = lddy;
   s.n = n;
   s.C = (int)C;
-  s.tpr = L.tpr;
-  s.rp = L.rp;
-  s.tiles = L.tiles;
-  s.parts = L.parts;
-  s.rows_per_part = L.rows_per_part;
+  s.tpr = Lr.tpr;
+  s.rp = Lr.rp;
+  s.tiles = Lr.tiles;
+  s.parts = Lr.parts;
+  s.rows_per_part = Lr.rows_per_part;
   s.part = w.part;
   s.gpart = w.gpart;
   s.count = w.count;
@@ -682,11 +717,15 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   s.dweight = dweight;
   s.dbias = dbias;
   hipStream_t st = as_stream(stream);
-  dim3 g1(L.parts, L.tiles);
-  if (vec)
-    k_bn_bwd_reduce<4><<<g1, kThreads, 0, st>>>(s);
+  dim3 g1(Lr.parts, Lr.tiles);
+  if (nt == 1024 && vec)
+    k_bn_bwd_reduce<4, 1024><<<g1, 1024, 0, st>>>(s);
+  else if (nt == 1024)
+    k_bn_bwd_reduce<1, 1024><<<g1, 1024, 0, st>>>(s);
+  else if (vec)
+    k_bn_bwd_reduce<4, kThreads><<<g1, kThreads, 0, st>>>(s);
   else
-    k_bn_bwd_reduce<1><<<g1, kThreads, 0, st>>>(s);
+    k_bn_bwd_reduce<1, kThreads><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
   BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);

@@ -286,25 +286,32 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[TN], float*
 constexpr int kStatTiles = 256;   // column tiles (N <= 256 * 16)
 constexpr int kStatGroups = 128;  // row-tile groups of the first tree level
 
-// Release this workgroup's partial writes and count it in; true in the last
-// workgroup to arrive (which resets the counter for the next launch).  The
-// hand-off of MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, as
-// in bn.hip.
+// Partials are handed over WRITE-THROUGH (8-byte agent-scope atomic stores =
+// global_store_dwordx2 sc1, drained by every storing wave; read back with sc1
+// loads): no release fence, whose buffer_wbl2 would write back the XCD L2's
+// dirty lines -- this workgroup's freshly stored C tile among them -- and no
+// acquire fence (cdna_hip_programming.md Guideline 16 R1), as in bn.hip.
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Count this workgroup in; true in the last workgroup to arrive (which resets
+// the counter for the next launch).
 __device__ __forceinline__ bool stat_arrive_last(unsigned* counter, unsigned total) {
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev =
         __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (prev == total - 1) ? 1u : 0u;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      *counter = 0u;
-    }
+    if (s_last) *counter = 0u;
   }
   __syncthreads();
   return s_last != 0u;
@@ -344,7 +351,7 @@ __device__ void proj_bn_stats(const FwdArgs& a, const float* wl0, int n_base, in
   if (threadIdx.x < 2 * CT) {
     const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
     const double v = ((sred[0][c][m] + sred[1][c][m]) + sred[2][c][m]) + sred[3][c][m];
-    if (c < ncols) a.part[((int64_t)pt * a.N + n_base + c) * 2 + m] = v;
+    if (c < ncols) st_wt(&a.part[((int64_t)pt * a.N + n_base + c) * 2 + m], v);
   }
   const int tile = (int)blockIdx.y;
   const int first = g * a.gs;
@@ -354,8 +361,9 @@ __device__ void proj_bn_stats(const FwdArgs& a, const float* wl0, int n_base, in
   if (threadIdx.x < 2 * CT) {
     const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
     if (c < ncols)
-      for (int p = first; p < first + cnt; ++p) gsum += a.part[((int64_t)p * a.N + n_base + c) * 2 + m];
-    if (a.ng > 1 && c < ncols) a.gpart[((int64_t)g * a.N + n_base + c) * 2 + m] = gsum;
+      for (int p = first; p < first + cnt; ++p)
+        gsum += ld_wt(&a.part[((int64_t)p * a.N + n_base + c) * 2 + m]);
+    if (a.ng > 1 && c < ncols) st_wt(&a.gpart[((int64_t)g * a.N + n_base + c) * 2 + m], gsum);
   }
   if (a.ng > 1) {
     if (!stat_arrive_last(a.count + tile, (unsigned)a.ng)) return;
@@ -363,7 +371,7 @@ __device__ void proj_bn_stats(const FwdArgs& a, const float* wl0, int n_base, in
       const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
       gsum = 0.0;
       if (c < ncols)
-        for (int q = 0; q < a.ng; ++q) gsum += a.gpart[((int64_t)q * a.N + n_base + c) * 2 + m];
+        for (int q = 0; q < a.ng; ++q) gsum += ld_wt(&a.gpart[((int64_t)q * a.N + n_base + c) * 2 + m]);
     }
   }
   if (threadIdx.x < 2 * CT) sfin[threadIdx.x >> 1][threadIdx.x & 1] = gsum;

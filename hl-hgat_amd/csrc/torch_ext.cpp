@@ -257,10 +257,12 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
 }
 
 // BatchNorm statistics in the projection epilogue (hlhgat_proj_fwd_bn):
-// OFF by default -- measured slower in every config (ZINC step 264k -> 236k
-// graphs/s, TSP head 41.9 -> 50.0 ms): each GEMM workgroup then drains its
-// C stores and takes an agent-scope atomic before retiring, which costs more
-// than the separate, well-overlapped statistics launch it removes.
+// OFF by default -- measured slower: first 264k -> 236k graphs/s (ZINC) with
+// release-fenced partials (each workgroup's buffer_wbl2 wrote back its own
+// freshly stored C tile), then, with write-through partials and no fences,
+// still 1.1 % slower in a same-box A/B (268.6k vs 265.6k): every GEMM
+// workgroup drains its C stores and takes an agent-scope atomic before
+// retiring, which costs about what the separate statistics launch does.
 // HLHGAT_FUSED_BN_STATS=1 (or set_fused_bn_stats) turns it on.
 bool& fused_bn_flag() {
   static bool on = [] {
