@@ -996,3 +996,34 @@ def test_brain_skeleton_conv_vs_reference_golden(cuda, side, factored):
     close(conv.bias.grad.cpu(), g[f"{side}/gbias"], 1e-4, "dbias")
     for k, lin in enumerate(conv.lins):
         close(lin.weight.grad.cpu(), g[f"{side}/gw{k}"], 1e-4, f"dW{k}")
+
+
+def test_hodge_factored_edge_cases(cuda):
+    """Factored L1 on a batch with isolated nodes (empty incidence rows), a
+    single-edge graph, a star (one node in every edge) and a triangle: equals
+    the CSR SpMM / basis; hodge_factor_ok holds for each graph."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import PairData, collate, hodge_coo_from_boundary, hodge_factor_ok
+    graphs = []
+    for ei, n in ((np.array([[0], [1]]), 2), (np.array([[0, 0, 0, 0], [1, 2, 3, 4]]), 6),
+                  (np.array([[0, 0, 1], [1, 2, 2]]), 3), (np.array([[1, 2], [2, 4]]), 7)):
+        ei_t, w_t, ei_s, w_s = hodge_coo_from_boundary(ei, n, 3.0)
+        assert hodge_factor_ok(ei, n, ei_s.numpy(), w_s.numpy())
+        g = PairData(x_s=torch.randn(ei.shape[1], 4), edge_index_s=ei_s, edge_weight_s=w_s,
+                     x_t=torch.randn(n, 4), edge_index_t=ei_t, edge_weight_t=w_t)
+        g.edge_index = torch.from_numpy(ei)
+        g.num_node1, g.num_edge1, g.num_nodes = n, ei.shape[1], n
+        g._hodge_sorted = True
+        graphs.append(g)
+    b = collate(graphs)
+    E = b.x_s.shape[0]
+    op_c = ops.hodge_operator(ops.mark_hodge(dev(b.edge_index_s)), dev(b.edge_weight_s), E)
+    e = ops.mark_hodge(dev(b.edge_index_s))
+    ops.set_hodge_factor(e, dev(b.edge_index), b.x_t.shape[0])
+    op_f = ops.hodge_operator(e, dev(b.edge_weight_s), E)
+    for d in (1, 4, 64):
+        x = dev(torch.randn(E, d, generator=torch.Generator().manual_seed(d)))
+        close(ops.hodge_spmm(op_f, x).cpu(), ops.spmm(op_c.fwd, x).cpu(), 1e-5, f"spmm d={d}")
+        Tf = ops.poly_basis(op_f, x, 4, ops.POLY_LAGUERRE).cpu()
+        Tc = ops.poly_basis(op_c, x, 4, ops.POLY_LAGUERRE).cpu()
+        close(Tf, Tc, 1e-5, f"basis d={d}")
