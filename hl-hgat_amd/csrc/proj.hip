@@ -675,6 +675,7 @@ struct BwdWeightArgs {
   float* part;
   int64_t rows_per_split;
   int tiles_n;
+  int xcd_map;  // remap (tile, split) so each XCD walks one contiguous range of them
 };
 
 __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
@@ -820,16 +821,29 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int wn = wave >> 1, wk = wave & 1;
+  // XCD-aware work order: workgroups are dealt round-robin over the 8 XCDs, so
+  // (tile, split) item w = xcd_slot(linear id) puts consecutive items -- the
+  // n-tiles sharing an A chunk, the k-tiles sharing a dC chunk of one split --
+  // on ONE XCD at about the same time: their shared chunks hit that XCD's L2
+  int by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (a.xcd_map) {
+    const unsigned Y = gridDim.y, total = gridDim.y * gridDim.z;
+    const unsigned L = blockIdx.y + blockIdx.z * Y;
+    const unsigned x = L & 7u, k = L >> 3, per = total >> 3, extra = total & 7u;
+    const unsigned w = x * per + (x < extra ? x : extra) + k;
+    by = (int)(w % Y);
+    bz = (int)(w / Y);
+  }
   int b = 0;
-  while (b + 1 < a.nb && (int)blockIdx.y >= a.tile_start[b + 1]) ++b;
-  const int t = (int)blockIdx.y - a.tile_start[b];
+  while (b + 1 < a.nb && by >= a.tile_start[b + 1]) ++b;
+  const int t = by - a.tile_start[b];
   const int n_base = (t % a.tiles_n) * 64;
   const int k_base = (t / a.tiles_n) * 64;
   const int kb = a.kb[b];
   const float* __restrict__ A = a.A[b];
   const int64_t lda = a.lda[b];
   const bool do_bias = a.bias_off >= 0 && b == 0 && k_base == 0;
-  const int64_t m_lo = (int64_t)blockIdx.z * a.rows_per_split;
+  const int64_t m_lo = (int64_t)bz * a.rows_per_split;
   int64_t m_hi = m_lo + a.rows_per_split;
   if (m_hi > a.M) m_hi = a.M;
 
@@ -890,7 +904,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
     __syncthreads();
   }
 
-  float* slab = a.part + (int64_t)blockIdx.z * a.part_stride + a.part_off[b];
+  float* slab = a.part + (int64_t)bz * a.part_stride + a.part_off[b];
   const int k = k_base + 32 * wk + cl;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -902,7 +916,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
     const float tot = bsum + __shfl_xor(bsum, 32, 64);
     const int n = n_base + 32 * wn + cl;
     if (rl == 0 && n < a.N)
-      a.part[(int64_t)blockIdx.z * a.part_stride + a.bias_off + n] = tot;
+      a.part[(int64_t)bz * a.part_stride + a.bias_off + n] = tot;
   }
 }
 
@@ -1025,6 +1039,16 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   p.rows_per_split = rps;
   p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
   return p;
+}
+
+// HLHGAT_WEIGHT_XCD=0 turns off the XCD-aware work order of the weight
+// gradient (A/B; results are identical either way)
+int weight_xcd_map() {
+  static int v = [] {
+    const char* e = getenv("HLHGAT_WEIGHT_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 // HLHGAT_PROJ_TN caps the 16-column tiles per wave (A/B of the wave count
@@ -1344,6 +1368,7 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   a.part = workspace;
   a.rows_per_split = p.rows_per_split;
   a.tiles_n = p.tiles_n;
+  a.xcd_map = weight_xcd_map();
   hipStream_t s = as_stream(stream);
   if (M == 0) {
     // no rows: gradient contribution is zero
