@@ -1,0 +1,321 @@
+// On-device Hodge Laplacian builder for block-diagonal batches of simplex
+// graphs.
+//
+// The reference builds, per graph, the dense boundary B1 [N, E], the dense
+// L0 = B1 B1^T, its largest eigenvalue with torch.linalg.eigh, and then the
+// dense L0 = 2 B1 B1^T / lmax and L1 = 2 B1^T B1 / lmax, keeping nonzeros with
+// dense_to_sparse (lib/Hodge_Dataset.py:451-468, :780-799): O(N^3) for lmax
+// and an E x E dense L1 (10 GB at BASELINE config 5).  Here, from the edge
+// list and the incidence CSR alone:
+//   * k_lanczos_lmax: lmax of every graph's L0 in ONE launch, one workgroup
+//     per graph: Lanczos on L0 x = deg .* x - A x (fp64, full
+//     re-orthogonalisation, <= 64 steps), then the largest eigenvalue of the
+//     tridiagonal matrix by Sturm-sequence bisection;
+//   * k_hodge_l0_rows / k_hodge_l1_rows: the sparse L0 / L1 rows in CSR
+//     (columns ascending, as dense_to_sparse orders them) with the
+//     reference's float32 entries fl(fl(2 v) / lmax): L0 row v = {v: deg(v),
+//     u in N(v): -1}; L1 row e = (i, j) = the merge of the incidence lists of
+//     i and j: {e: 2, f sharing its tail or head with e's tail or head: +1,
+//     tail-to-head: -1}.
+// Row sizes (prefix sums) come from the incidence CSR; no sort, no atomics.
+#include "common.h"
+
+using namespace hlhgat;
+
+namespace {
+
+constexpr int kLzThreads = 256;
+constexpr int kLzMaxSteps = 64;
+
+struct LanczosArgs {
+  const int32_t* inc_rowptr;  // incidence CSR (node -> incident edge ids, ascending)
+  const int32_t* inc_edge;
+  const int64_t* ei;          // [2][n_edges]
+  int64_t n_edges;
+  const int64_t* node_ptr;    // [n_graphs + 1]
+  int steps;
+  double* Q;                  // [steps + 1][n_nodes] Lanczos vectors
+  double* W;                  // [n_nodes] work vector
+  int64_t n_nodes;
+  double* lmax;               // [n_graphs]
+};
+
+__device__ double block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < kLzThreads / 64; ++w) s += red[w];
+  return s;
+}
+
+// y = L0 x on the graph's nodes [n0, n1): deg(v) x[v] - sum of x[other end]
+__device__ void l0_apply(const LanczosArgs& a, int64_t n0, int64_t n1, const double* x,
+                         double* y) {
+  for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) {
+    const int e0 = a.inc_rowptr[v], e1 = a.inc_rowptr[v + 1];
+    double s = (double)(e1 - e0) * x[v];
+    for (int p = e0; p < e1; ++p) {
+      const int64_t e = a.inc_edge[p];
+      const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
+      s -= x[i == v ? j : i];
+    }
+    y[v] = s;
+  }
+}
+
+// number of eigenvalues of the symmetric tridiagonal (al, be) below x
+__device__ int sturm_count(const double* al, const double* be, int k, double x) {
+  int c = 0;
+  double d = 1.0;
+  for (int i = 0; i < k; ++i) {
+    const double b2 = i ? be[i] * be[i] : 0.0;
+    d = (al[i] - x) - (i ? b2 / d : 0.0);
+    if (d == 0.0) d = -1e-300;
+    if (d < 0.0) ++c;
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(kLzThreads) void k_lanczos_lmax(LanczosArgs a) {
+  __shared__ double red[kLzThreads / 64];
+  __shared__ double al[kLzMaxSteps + 1], be[kLzMaxSteps + 2];
+  __shared__ int s_k;
+  const int g = blockIdx.x;
+  const int64_t n0 = a.node_ptr[g], n1 = a.node_ptr[g + 1], ng = n1 - n0;
+  const int m = (int)(ng < a.steps ? ng : a.steps);
+  auto Qv = [&](int j) { return a.Q + (int64_t)j * a.n_nodes; };
+  // deterministic start vector with a component along every eigenvector
+  double nrm = 0.0;
+  for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) {
+    const double q = 1.0 + (double)(((uint64_t)(v - n0) * 2654435761ull) % 1000ull) * 1e-3;
+    Qv(0)[v] = q;
+    nrm += q * q;
+  }
+  nrm = sqrt(block_sum(nrm, red));
+  for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) Qv(0)[v] /= nrm;
+  if (threadIdx.x == 0) s_k = m;
+  __syncthreads();
+  for (int j = 0; j < m; ++j) {
+    l0_apply(a, n0, n1, Qv(j), a.W);
+    __syncthreads();
+    // full re-orthogonalisation (two passes of classical Gram-Schmidt); the
+    // first coefficient against q_j is alpha_j
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int i = 0; i <= j; ++i) {
+        double d = 0.0;
+        for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) d += a.W[v] * Qv(i)[v];
+        d = block_sum(d, red);
+        if (pass == 0 && i == j && threadIdx.x == 0) al[j] = d;
+        if (pass == 1 && i == j && threadIdx.x == 0) al[j] += d;
+        for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) a.W[v] -= d * Qv(i)[v];
+        __syncthreads();
+      }
+    }
+    double b = 0.0;
+    for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) b += a.W[v] * a.W[v];
+    b = sqrt(block_sum(b, red));
+    __syncthreads();
+    if (j + 1 >= m) break;
+    const double scale = fabs(al[j]) > 1.0 ? fabs(al[j]) : 1.0;
+    if (b <= 1e-12 * scale) {  // invariant subspace found: T is complete
+      if (threadIdx.x == 0) s_k = j + 1;
+      __syncthreads();
+      break;
+    }
+    if (threadIdx.x == 0) be[j + 1] = b;
+    for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) Qv(j + 1)[v] = a.W[v] / b;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int k = s_k;
+    // Gershgorin bounds, then bisection for the largest eigenvalue
+    double lo = 0.0, hi = 0.0;
+    for (int i = 0; i < k; ++i) {
+      const double r = (i ? fabs(be[i]) : 0.0) + (i + 1 < k ? fabs(be[i + 1]) : 0.0);
+      lo = fmin(lo, al[i] - r);
+      hi = fmax(hi, al[i] + r);
+    }
+    for (int it = 0; it < 200 && hi - lo > 1e-15 * fmax(1.0, fabs(hi)); ++it) {
+      const double mid = 0.5 * (lo + hi);
+      if (sturm_count(al, be, k, mid) < k) lo = mid;  // some eigenvalue above mid
+      else hi = mid;
+    }
+    a.lmax[g] = ng > 0 ? hi : 0.0;
+  }
+}
+
+struct BuildArgs {
+  const int32_t* inc_rowptr;
+  const int32_t* inc_edge;
+  const int64_t* ei;
+  int64_t n_edges, n_nodes;
+  const float* lam_node;   // [n_nodes] lmax (float32) of each node's graph
+  const int32_t* rp;       // output row pointer of this operator
+  int32_t* col;
+  float* val;
+};
+
+__device__ __forceinline__ float hodge_w(int v, float lam) {
+  return (2.0f * (float)v) / lam;  // fl(fl(2 v) / lmax), the reference's float32 entry
+}
+
+// L0 row v: its neighbours and itself, columns ascending (selection by
+// repeated minimum: rows are short, deg <= a few hundred)
+__global__ __launch_bounds__(256) void k_hodge_l0_rows(BuildArgs a) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= a.n_nodes) return;
+  const int e0 = a.inc_rowptr[v], e1 = a.inc_rowptr[v + 1];
+  const int deg = e1 - e0;
+  if (deg == 0) return;  // isolated node: all-zero row, dropped as dense_to_sparse drops zeros
+  const float lam = a.lam_node[v];
+  int out = a.rp[v];
+  int64_t last = -1;
+  for (int k = 0; k <= deg; ++k) {  // deg neighbours + the diagonal
+    int64_t best = INT64_MAX;
+    if (v > last) best = v;
+    for (int p = e0; p < e1; ++p) {
+      const int64_t e = a.inc_edge[p];
+      const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
+      const int64_t u = (i == v) ? j : i;
+      if (u > last && u < best) best = u;
+    }
+    a.col[out] = (int32_t)best;
+    a.val[out] = hodge_w(best == v ? deg : -1, lam);
+    ++out;
+    last = best;
+  }
+}
+
+// L1 row e = (i, j): merge of the ascending incidence lists of i and j
+__global__ __launch_bounds__(256) void k_hodge_l1_rows(BuildArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.n_edges) return;
+  const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
+  const float lam = a.lam_node[i];
+  int p = a.inc_rowptr[i], pe = a.inc_rowptr[i + 1];
+  int q = a.inc_rowptr[j], qe = a.inc_rowptr[j + 1];
+  int out = a.rp[e];
+  while (p < pe || q < qe) {
+    const int32_t fp = p < pe ? a.inc_edge[p] : INT32_MAX;
+    const int32_t fq = q < qe ? a.inc_edge[q] : INT32_MAX;
+    const int32_t f = fp < fq ? fp : fq;
+    int v;
+    if (f == (int32_t)e) {
+      v = 2;
+      ++p;
+      ++q;  // e is in both lists
+    } else {
+      const int64_t fi = a.ei[f], fj = a.ei[a.n_edges + f];
+      // shared node s: +1 when s is the tail of both or the head of both
+      if (fp == f) {  // shares node i (e's tail)
+        v = (fi == i) ? 1 : -1;
+        ++p;
+      } else {        // shares node j (e's head)
+        v = (fj == j) ? 1 : -1;
+        ++q;
+      }
+    }
+    a.col[out] = f;
+    a.val[out] = hodge_w(v, lam);
+    ++out;
+  }
+}
+
+// row sizes: L0 deg(v) + [deg > 0]; L1 deg(i) + deg(j) - 1
+__global__ __launch_bounds__(256) void k_hodge_row_sizes(const int32_t* inc_rowptr,
+                                                         const int64_t* ei, int64_t n_edges,
+                                                         int64_t n_nodes, int32_t* sz0,
+                                                         int32_t* sz1) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < n_nodes) {
+    const int d = inc_rowptr[t + 1] - inc_rowptr[t];
+    sz0[t] = d > 0 ? d + 1 : 0;
+  }
+  if (t < n_edges) {
+    const int64_t i = ei[t], j = ei[n_edges + t];
+    sz1[t] = (inc_rowptr[i + 1] - inc_rowptr[i]) + (inc_rowptr[j + 1] - inc_rowptr[j]) - 1;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t hlhgat_hodge_lmax_workspace_bytes(int64_t n_nodes, int steps) {
+  if (n_nodes < 0 || steps < 1 || steps > kLzMaxSteps) return 0;
+  return (int64_t)sizeof(double) * n_nodes * (steps + 2);
+}
+
+extern "C" int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_edge,
+                                 const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
+                                 const int64_t* node_ptr, int64_t n_graphs, int steps,
+                                 double* lmax, void* workspace, int64_t workspace_bytes,
+                                 void* stream) {
+  HLH_CHECK_ARG(steps >= 1 && steps <= kLzMaxSteps, "hodge_lmax: steps must be 1..%d",
+                kLzMaxSteps);
+  HLH_CHECK_ARG(n_graphs >= 0 && n_nodes >= 0 && n_edges >= 0, "hodge_lmax: bad sizes");
+  if (n_graphs == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(inc_rowptr && node_ptr && lmax && workspace && (n_edges == 0 || (inc_edge && edge_index)),
+                "hodge_lmax: NULL pointer");
+  HLH_CHECK_ARG(workspace_bytes >= hlhgat_hodge_lmax_workspace_bytes(n_nodes, steps),
+                "hodge_lmax: workspace too small");
+  LanczosArgs a{};
+  a.inc_rowptr = inc_rowptr;
+  a.inc_edge = inc_edge;
+  a.ei = edge_index;
+  a.n_edges = n_edges;
+  a.node_ptr = node_ptr;
+  a.steps = steps;
+  a.Q = reinterpret_cast<double*>(workspace);
+  a.W = a.Q + (int64_t)(steps + 1) * n_nodes;
+  a.n_nodes = n_nodes;
+  a.lmax = lmax;
+  hipLaunchKernelGGL(k_lanczos_lmax, dim3((unsigned)n_graphs), dim3(kLzThreads), 0,
+                     as_stream(stream), a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_hodge_row_sizes(const int32_t* inc_rowptr, const int64_t* edge_index,
+                                      int64_t n_edges, int64_t n_nodes, int32_t* sizes_l0,
+                                      int32_t* sizes_l1, void* stream) {
+  HLH_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && inc_rowptr && sizes_l0 && sizes_l1 &&
+                    (n_edges == 0 || edge_index),
+                "hodge_row_sizes: bad arguments");
+  const int64_t n = n_nodes > n_edges ? n_nodes : n_edges;
+  if (n == 0) return HLHGAT_OK;
+  hipLaunchKernelGGL(k_hodge_row_sizes, dim3((unsigned)ceil_div(n, (int64_t)256)), dim3(256), 0,
+                     as_stream(stream), inc_rowptr, edge_index, n_edges, n_nodes, sizes_l0,
+                     sizes_l1);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_edge,
+                                  const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
+                                  const float* lam_node, const int32_t* rowptr_l0,
+                                  int32_t* col_l0, float* val_l0, const int32_t* rowptr_l1,
+                                  int32_t* col_l1, float* val_l1, void* stream) {
+  HLH_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && inc_rowptr && lam_node && rowptr_l0 &&
+                    rowptr_l1 && (n_edges == 0 || (inc_edge && edge_index && col_l0 && val_l0 &&
+                                                   col_l1 && val_l1)),
+                "hodge_build: bad arguments");
+  BuildArgs a{inc_rowptr, inc_edge, edge_index, n_edges, n_nodes, lam_node, rowptr_l0, col_l0,
+              val_l0};
+  hipStream_t s = as_stream(stream);
+  if (n_nodes > 0) {
+    hipLaunchKernelGGL(k_hodge_l0_rows, dim3((unsigned)ceil_div(n_nodes, (int64_t)256)),
+                       dim3(256), 0, s, a);
+    HLH_CHECK_LAUNCH();
+  }
+  if (n_edges > 0) {
+    a.rp = rowptr_l1;
+    a.col = col_l1;
+    a.val = val_l1;
+    hipLaunchKernelGGL(k_hodge_l1_rows, dim3((unsigned)ceil_div(n_edges, (int64_t)256)),
+                       dim3(256), 0, s, a);
+    HLH_CHECK_LAUNCH();
+  }
+  return HLHGAT_OK;
+}

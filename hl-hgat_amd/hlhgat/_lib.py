@@ -54,6 +54,12 @@ SIGNATURES = {
     "hlhgat_poly_basis_fwd_factored": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_i64, c_i32, c_vp,
                                                c_vp, c_vp]),
     "hlhgat_poly_basis_bwd_factored": (c_i32, [c_i32, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "hlhgat_hodge_lmax_workspace_bytes": (c_i64, [c_i64, c_i32]),
+    "hlhgat_hodge_lmax": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp,
+                                  c_i64, c_vp]),
+    "hlhgat_hodge_row_sizes": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "hlhgat_hodge_build": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                   c_vp, c_vp, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,

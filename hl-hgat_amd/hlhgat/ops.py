@@ -363,6 +363,64 @@ def _halo_args(A: "SparseCSR"):
     return A.halo
 
 
+def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tensor] = None,
+                steps: int = 64):
+    """Hodge Laplacians of a block-diagonal batch ON DEVICE (hlhgat_hodge_*):
+    edge_index int64 [2, E] (i < j, PairData offsets), node_counts per graph.
+    lmax per graph: given (float, as the reference's eigh result) or computed
+    by the on-device Lanczos (fp64).  Returns (ei_t, w_t, ei_s, w_s, lmax) with
+    the COO in the reference's dense_to_sparse order (row-major, zeros
+    dropped) and entries fl(fl(2 v) / lmax) (lib/Hodge_Dataset.py:451-468)."""
+    _req_dev(edge_index, "edge_index", torch.int64)
+    dev = edge_index.device
+    counts = torch.as_tensor(node_counts, dtype=torch.int64).to(dev)
+    B = counts.numel()
+    node_ptr = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+    node_ptr[1:] = torch.cumsum(counts, 0)
+    N = int(node_ptr[-1].item())
+    ei = edge_index.contiguous()
+    E = ei.size(1)
+    inc = incidence(ei, N)
+    st = _stream(ei)
+    if lmax is None:
+        wsb = int(LIB.hlhgat_hodge_lmax_workspace_bytes(N, steps))
+        ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=dev)
+        lam64 = torch.empty(B, dtype=torch.float64, device=dev)
+        check(LIB.hlhgat_hodge_lmax(inc.rowptr.data_ptr(), inc.edge_ids.data_ptr() if E else None,
+                                    ei.data_ptr() if E else None, E, N, node_ptr.data_ptr(), B,
+                                    steps, lam64.data_ptr(), ws.data_ptr(), wsb, st), "hodge_lmax")
+        lam = lam64.to(torch.float32)
+    else:
+        lam = torch.as_tensor(lmax, dtype=torch.float32).to(dev).reshape(B)
+    lam_node = torch.repeat_interleave(lam, counts, output_size=N).contiguous()
+    sz0 = torch.empty(N, dtype=torch.int32, device=dev)
+    sz1 = torch.empty(E, dtype=torch.int32, device=dev)
+    check(LIB.hlhgat_hodge_row_sizes(inc.rowptr.data_ptr(), _ptr(ei) if E else None, E, N,
+                                     sz0.data_ptr(), sz1.data_ptr(), st), "hodge_row_sizes")
+    rp0 = torch.zeros(N + 1, dtype=torch.int32, device=dev)
+    rp1 = torch.zeros(E + 1, dtype=torch.int32, device=dev)
+    rp0[1:] = torch.cumsum(sz0, 0)
+    rp1[1:] = torch.cumsum(sz1, 0)
+    nnz0, nnz1 = int(rp0[-1].item()), int(rp1[-1].item())
+    c0 = torch.empty(max(nnz0, 1), dtype=torch.int32, device=dev)
+    v0 = torch.empty(max(nnz0, 1), dtype=torch.float32, device=dev)
+    c1 = torch.empty(max(nnz1, 1), dtype=torch.int32, device=dev)
+    v1 = torch.empty(max(nnz1, 1), dtype=torch.float32, device=dev)
+    check(LIB.hlhgat_hodge_build(inc.rowptr.data_ptr(), inc.edge_ids.data_ptr() if E else None,
+                                 _ptr(ei) if E else None, E, N, lam_node.data_ptr(), rp0.data_ptr(),
+                                 c0.data_ptr(), v0.data_ptr(), rp1.data_ptr(), c1.data_ptr(),
+                                 v1.data_ptr(), st), "hodge_build")
+
+    def coo(rp, c, v, n, nnz):
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), (rp[1:] - rp[:-1]).long(),
+                                       output_size=nnz)
+        return torch.stack([rows, c[:nnz].long()]), v[:nnz]
+
+    ei_t, w_t = coo(rp0, c0, v0, N, nnz0)
+    ei_s, w_s = coo(rp1, c1, v1, E, nnz1)
+    return ei_t, w_t, ei_s, w_s, lam
+
+
 def copy_words_batched(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
     """dst.copy_(src) for contiguous same-size tensors whose byte size is a
     multiple of 4, up to HLHGAT_MAX_COPY_BLOCKS per launch

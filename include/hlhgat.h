@@ -269,6 +269,39 @@ int hlhgat_poly_basis_fwd_factored(int kind, const hlhgat_hodge_factor_t* f,
 int hlhgat_poly_basis_bwd_factored(int kind, const hlhgat_hodge_factor_t* f, int64_t F,
                                    int K, float* G, float* work, void* stream);
 
+/* ---- on-device Hodge Laplacian builder -------------- */
+/* Replaces the per-graph dense construction of the reference
+ * (lib/Hodge_Dataset.py:451-468, :780-799; DEMO notebook cells 11, 19):
+ * par1 = adj2par1(...).to_dense(); L0 = par1 par1^T; lmax = eigh(L0).max();
+ * L0 = 2 par1 par1^T / lmax; L1 = 2 par1^T par1 / lmax; dense_to_sparse.
+ * Input: a block-diagonal batch's edge list (int64 [2][E], i < j per edge,
+ * PairData offsets) and its incidence CSR (hlhgat_incidence_csr).
+ *
+ * hlhgat_hodge_lmax: lmax of every graph's L0 = B1 B1^T (graph g = nodes
+ * [node_ptr[g], node_ptr[g+1])), one workgroup per graph, fp64 Lanczos with
+ * full re-orthogonalisation (`steps` <= 64 iterations, exact for graphs of
+ * <= steps nodes) and Sturm bisection of the tridiagonal matrix.  The
+ * reference's float32 eigh agrees to its own rounding (~1e-7 relative), so
+ * entries built from this lmax may differ from the reference's by an ulp. */
+int64_t hlhgat_hodge_lmax_workspace_bytes(int64_t n_nodes, int steps);
+int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_edge,
+                      const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
+                      const int64_t* node_ptr, int64_t n_graphs, int steps, double* lmax,
+                      void* workspace, int64_t workspace_bytes, void* stream);
+/* Row sizes of L0 (deg(v) + 1, 0 for an isolated node) and L1 (deg(i) +
+ * deg(j) - 1); exclusive-scan them into the row pointers. */
+int hlhgat_hodge_row_sizes(const int32_t* inc_rowptr, const int64_t* edge_index,
+                           int64_t n_edges, int64_t n_nodes, int32_t* sizes_l0,
+                           int32_t* sizes_l1, void* stream);
+/* L0 / L1 in CSR, columns ascending, entries fl(fl(2 v) / lam_node[row's
+ * graph]) -- the reference's float32 arithmetic -- with v the integer entry
+ * of B1 B1^T (deg, -1) / B1^T B1 (2, +1 same-end, -1 tail-to-head). */
+int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_edge,
+                       const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
+                       const float* lam_node, const int32_t* rowptr_l0, int32_t* col_l0,
+                       float* val_l0, const int32_t* rowptr_l1, int32_t* col_l1,
+                       float* val_l1, void* stream);
+
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
 #define HLHGAT_MAX_BLOCKS 16
 
