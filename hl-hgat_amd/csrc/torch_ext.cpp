@@ -272,6 +272,29 @@ bool& fused_bn_flag() {
   return on;
 }
 bool fused_bn_stats() { return fused_bn_flag(); }
+
+// HLHGAT_FUSED_CONV=1: the graph-local fused conv forward (basis + projection
+// in one launch, bitwise the same results).  OFF by default: same-box A/B at
+// the ZINC step 270.7k -> 263.7k graphs/s -- one workgroup per tile walks
+// load / barrier / weight-stage / MFMA phases serially and holds 56 KB of LDS,
+// which costs more than the three short launches it replaces.
+// HLHGAT_GRAPH_LOCAL=1: the basis-only graph-local path (k_basis_local_*).
+bool& fused_conv_flag() {
+  static bool on = [] {
+    const char* e = getenv("HLHGAT_FUSED_CONV");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+bool fused_conv_env() { return fused_conv_flag(); }
+void set_fused_conv(bool on) { fused_conv_flag() = on; }
+bool graph_local_env() {
+  static const bool on = [] {
+    const char* e = getenv("HLHGAT_GRAPH_LOCAL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 void set_fused_bn_stats(bool on) { fused_bn_flag() = on; }
 
 // One hlhgat_proj_fwd_bn workspace per (device, stream), as bn_workspace.
@@ -374,18 +397,30 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                              has(h_sval) ? *h_sval : Tensor(), h_bounds, *h_hdr)
                  : hlhgat_halo_t{};
     const bool factored = !fac.empty();
+    // graph tiles: the fused graph-local conv (basis + projection, one launch)
+    // for the 64-wide ZINC-scale blocks; the basis-only local path on request
+    const bool local_basis = has(tiles) && graph_local_env();
+    const int64_t dout0 = W.empty() ? 0 : W[0].size(0);
+    bool fused_local = fused_conv_env() && !factored && has(tiles) && K > 1 && N > 0 &&
+                       x.dim() == 2 && F == 64 && Cin == 64 && dout0 == 64 && kind != 2 &&
+                       tile_rows >= 1 && tile_rows <= 64 && tile_nnz >= 1 &&
+                       ld_of(x2) % 4 == 0 && (reinterpret_cast<uintptr_t>(x2.data_ptr()) & 15) == 0;
+    for (int64_t k = 0; fused_local && k < K; ++k)
+      fused_local = W[k].stride(1) == 1 && W[k].stride(0) % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(W[k].data_ptr()) & 15) == 0;
     if (factored && K > 1 && N > 0) {
       const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
       Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x.options());
       chk(hlhgat_poly_basis_fwd_factored((int)kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
                                          (int)K, T.data_ptr<float>(), work.data_ptr<float>(), s),
           "poly_basis_fwd_factored");
-    } else if (K > 1 && N > 0) {
+    } else if (K > 1 && N > 0 && !fused_local) {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
                                 nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
                                 use_halo ? &halo : nullptr,
-                                iptr(tiles), has(tiles) ? tiles->numel() - 1 : 0, tile_rows,
+                                local_basis ? iptr(tiles) : nullptr,
+                                local_basis ? tiles->numel() - 1 : 0, tile_rows,
                                 tile_nnz, x2.data_ptr<float>(),
                                 ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
           "poly_basis_fwd");
@@ -413,7 +448,21 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                   "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
     Tensor pre = (sink && bn_mode == 0) ? *out_buf : at::empty({M, dout}, x.options());
     Tensor out = pre, mean, invstd;
-    if (bn_mode > 0 && M > 0 && fused_bn_stats()) {  // statistics in the GEMM epilogue
+    if (fused_local) {  // basis + projection in one graph-local launch
+      std::vector<int64_t> ldwv(K);
+      for (int64_t k = 0; k < K; ++k) ldwv[k] = W[k].stride(0);
+      chk(hlhgat_conv_local_fwd((int)kind, a_rowptr.data_ptr<int>(),
+                                nnz ? a_col.data_ptr<int>() : nullptr, nnz ? fptr(a_val) : nullptr,
+                                N, nnz, tiles->data_ptr<int>(), tiles->numel() - 1, tile_rows,
+                                tile_nnz, x2.data_ptr<float>(), ld_of(x2), F, (int)K,
+                                T.data_ptr<float>(), Wp.data(), ldwv.data(), fptr(bias), dout,
+                                pre.data_ptr<float>(), ld_of(pre), s),
+          "conv_local_fwd");
+      if (bn_mode > 0) {
+        BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
+        out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
+      }
+    } else if (bn_mode > 0 && M > 0 && fused_bn_stats()) {  // statistics in the GEMM epilogue
       BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
       out = proj_bn_forward(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, st, bn_mode == 2, mean,
                             invstd, sink ? &*out_buf : nullptr);
@@ -600,9 +649,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                                     (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
                                     N, nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
                                     use_halo ? &halo : nullptr,
-                                    tiles.defined() ? tiles.data_ptr<int>() : nullptr,
-                                    tiles.defined() ? tiles.numel() - 1 : 0, tile_rows,
-                                    tile_nnz, F, (int)K, Gs.data_ptr<float>(), s),
+                                    (tiles.defined() && graph_local_env())
+                                        ? tiles.data_ptr<int>() : nullptr,
+                                    (tiles.defined() && graph_local_env()) ? tiles.numel() - 1 : 0,
+                                    tile_rows, tile_nnz, F, (int)K, Gs.data_ptr<float>(), s),
               "poly_basis_bwd");
         }
       } else {
@@ -1330,6 +1380,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bn_stats", &set_fused_bn_stats);
+  m.def("set_fused_conv", &set_fused_conv);
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);

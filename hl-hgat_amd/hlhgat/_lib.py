@@ -60,6 +60,9 @@ SIGNATURES = {
     "hlhgat_hodge_row_sizes": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "hlhgat_hodge_build": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_vp]),
+    "hlhgat_conv_local_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                      c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, P_vp, P_i64, c_vp,
+                                      c_i64, c_vp, c_i64, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,

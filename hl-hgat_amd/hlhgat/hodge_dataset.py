@@ -102,7 +102,9 @@ class Batch(PairData):
             nv = getattr(self, kv, None)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(o):
                 set_row_order(t, o)
-            if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(tp) and ops.GRAPH_LOCAL:
+            if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(tp):
+                # whole-graph tiles: the fused graph-local conv forward uses them
+                # (and the basis-only local path when HLHGAT_GRAPH_LOCAL=1)
                 set_tiles(t, tp, TILE_ROWS, TILE_NNZ)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(nv):
                 set_valid(t, nv)

@@ -302,6 +302,22 @@ int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_edge,
                        float* val_l0, const int32_t* rowptr_l1, int32_t* col_l1,
                        float* val_l1, void* stream);
 
+/* ---- graph-local fused conv forward ------------------------------------ */
+/* out = sum_k T_k W_k^T + bias with T_0 = X and T_1..T_{K-1} the basis of
+ * hlhgat_poly_basis_fwd (LAGUERRE or CHEB), in ONE launch for block-diagonal
+ * batches of small graphs (graph tiles of <= 64 rows, hodge_dataset.
+ * graph_tiles): a workgroup keeps its tile's X and T_k in LDS and projects
+ * each T_k while it is resident (HodgeLaguerreConv.forward,
+ * lib/Hodge_Cheb_Conv.py:480-515).  Needs F = d_out = 64, 2 <= K <= 16,
+ * 16-B aligned operands.  T (K-1 blocks [n][F]) is written for the backward.
+ * Bitwise equal to hlhgat_poly_basis_fwd + hlhgat_proj_fwd. */
+int hlhgat_conv_local_fwd(int kind, const int32_t* rowptr, const int32_t* col,
+                          const float* val, int64_t n, int64_t nnz, const int32_t* tile_ptr,
+                          int64_t n_tiles, int64_t max_tile_rows, int64_t max_tile_nnz,
+                          const float* X, int64_t ldx, int64_t F, int K, float* T,
+                          const float* const* W, const int64_t* ldw, const float* bias,
+                          int64_t d_out, float* C, int64_t ldc, void* stream);
+
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
 #define HLHGAT_MAX_BLOCKS 16
 

@@ -1062,3 +1062,46 @@ def test_device_hodge_builder_matches_reference(cuda):
     assert torch.equal(ei_s.cpu(), b.edge_index_s) and torch.equal(w_s.cpu(), b.edge_weight_s)
     *_, lam_d = ops.hodge_build(dev(b.edge_index), b.num_node1.tolist())
     close(lam_d.cpu(), torch.tensor(lams), 2e-6, "lanczos lmax")
+
+
+@pytest.mark.parametrize("kind,K", [("lag", 2), ("lag", 3), ("lag", 4), ("cheb", 3)])
+@pytest.mark.parametrize("side", ["t", "s"])
+def test_fused_local_conv_bitwise_equals_unfused(cuda, kind, K, side):
+    """hlhgat_conv_local_fwd (basis + projection of a whole-graph tile in one
+    launch) == hlhgat_poly_basis_fwd + hlhgat_proj_fwd bitwise: conv -> BN ->
+    ReLU output, the saved basis (through dX) and every gradient (ZINC-like
+    batch, graph tiles from collate, 64 features in and out)."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(96, seed=21).to(cuda)
+    ei, w = getattr(b, "edge_index_" + side), getattr(b, "edge_weight_" + side)
+    n = getattr(b, "x_" + side).shape[0]
+    assert getattr(ei, "_hlhgat_tiles", None) is not None
+    torch.manual_seed(1)
+    cls = hlhgat.HodgeLaguerreConv if kind == "lag" else hlhgat.HodgeChebConv
+    conv = cls(64, 64, K=K).to(cuda)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    bn = torch.nn.BatchNorm1d(64).to(cuda)
+    sd_bn = {k: v.clone() for k, v in bn.state_dict().items()}
+    x0 = torch.randn(n, 64, device=cuda)
+    res = []
+    try:
+        for fused in (True, False):
+            ops._ext.set_fused_conv(fused)
+            bn.load_state_dict(sd_bn)
+            ops.clear_caches()
+            op = ops.hodge_operator(ei, w, n)
+            x = x0.clone().requires_grad_(True)
+            y = ops.hodge_poly_conv(x, op, [l.weight for l in conv.lins], conv.bias,
+                                    ops.POLY_LAGUERRE if kind == "lag" else ops.POLY_CHEB,
+                                    bn=bn, relu=True)
+            (y * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
+            res.append([y.detach().clone(), x.grad.clone(), conv.bias.grad.clone()] +
+                       [l.weight.grad.clone() for l in conv.lins])
+            conv.zero_grad()
+    finally:
+        ops._ext.set_fused_conv(False)
+    for a, c in zip(*res):
+        assert torch.equal(a, c)
