@@ -99,8 +99,11 @@ def max_over_ranks(value: float, device: torch.device = torch.device("cpu")) -> 
 
 class _GlobalMax(torch.autograd.Function):
     """max over all elements on all ranks (all_reduce MAX; no host sync).
-    Backward: the gradient flows to the positions holding the global max
-    (torch.max's subgradient, ties split evenly on the owning ranks)."""
+    Backward is the adjoint of that exchange: the data-parallel objective is
+    (1/W)·Σ_r L_r and every L_r depends on the one global max, so dΣL/dM =
+    Σ_r g_r is summed over ranks (one all_reduce with the tie count) and lands
+    on the positions holding the max (torch.max's subgradient, ties split
+    evenly); DDP's 1/W average then gives d/dθ of the global-batch loss."""
 
     @staticmethod
     def forward(ctx, x):
@@ -114,10 +117,10 @@ class _GlobalMax(torch.autograd.Function):
     def backward(ctx, g):
         x, m = ctx.saved_tensors
         hit = (x == m).to(x.dtype)
-        cnt = hit.sum().reshape(1)
+        gc = torch.stack([g.reshape(()).to(x.dtype), hit.sum()])
         if dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(cnt)
-        return hit * (g / cnt)
+            dist.all_reduce(gc)
+        return hit * (gc[0] / gc[1])
 
 
 def global_max(x: torch.Tensor) -> torch.Tensor:

@@ -106,7 +106,7 @@ def _gmax_worker(rank, world, port, out_q):
     init_distributed("gloo")
     x = torch.arange(5.0).mul(rank + 1).add(rank).requires_grad_(True)  # max on rank 1 only
     m = global_max(x)
-    (3.0 * m).backward()
+    (3.0 * (rank + 1) * m).backward()  # a different upstream gradient per rank
     out_q.put((rank, float(m), x.grad.tolist()))
     dist.destroy_process_group()
 
@@ -115,7 +115,9 @@ def test_global_max_two_ranks_matches_single_process():
     """att / att.max() of the attpool heads (lib/Hodge_ST_Model.py:1061-1062)
     is a BATCH max: under graph sharding it must span every rank (SURVEY §8e
     caveat 2).  global_max over 2 gloo ranks == max of the concatenation, and
-    its gradient lands where the single-process torch max puts it."""
+    its gradient is that of the data-parallel objective (1/W)·Σ_r L_r: each
+    rank's x.grad, averaged over ranks as DDP averages parameter gradients,
+    equals the single-process gradient of that objective."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -127,7 +129,8 @@ def test_global_max_two_ranks_matches_single_process():
         p.join(timeout=60)
     xs = [torch.arange(5.0).mul(r + 1).add(r).requires_grad_(True) for r in range(world)]
     m_ref = torch.cat(xs).max()
-    (3.0 * m_ref).backward()
+    sum(3.0 * (r + 1) * m_ref for r in range(world)).div(world).backward()
     for r in range(world):
         assert res[r][0] == float(m_ref)
-        assert res[r][1] == xs[r].grad.tolist()
+        assert [v / world for v in res[r][1]] == xs[r].grad.tolist()
+    assert any(v != 0 for v in res[1][1]) and not any(res[0][1])
