@@ -78,15 +78,22 @@ def init_distributed(backend: str = None) -> Tuple[int, int, torch.device]:
     return rank, world, device
 
 
-def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 32):
+def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 32,
+             find_unused_parameters: bool = None):
     """DistributedDataParallel with one gradient bucket per ~32 MB: the whole
     0.6-16 MB gradient of the SURVEY configs fits in one or two ring
-    all-reduces over the 7 xGMI links."""
+    all-reduces over the 7 xGMI links.  find_unused_parameters defaults to the
+    model's ``ddp_find_unused_parameters`` flag (the attpool heads, whose
+    unused NEAtt parameters would otherwise keep the bucket from ever being
+    reduced, leaving every gradient pre-scaled by 1/W and un-summed)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return model
+    if find_unused_parameters is None:
+        find_unused_parameters = bool(getattr(model, "ddp_find_unused_parameters", False))
     ids = [device.index] if device.type == "cuda" else None
     return torch.nn.parallel.DistributedDataParallel(
-        model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
+        model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
+        find_unused_parameters=find_unused_parameters)
 
 
 def max_over_ranks(value: float, device: torch.device = torch.device("cpu")) -> float:

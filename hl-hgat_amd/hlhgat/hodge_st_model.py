@@ -240,6 +240,11 @@ class _AttPoolHead(nn.Module):
     the level's last block output, normalised by its batch max
     (lib/Hodge_ST_Model.py:1058-1064)."""
 
+    # the reference builds NEAtt{i} for every level but uses only the pool_loc
+    # one in this mode: those parameters get no gradient, so DDP must look for
+    # unused parameters (hlhgat.distributed.wrap_ddp reads this flag)
+    ddp_find_unused_parameters = True
+
     def __init__(self, channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
                  dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, att_every_level):
         super().__init__()

@@ -134,3 +134,50 @@ def test_global_max_two_ranks_matches_single_process():
         assert res[r][0] == float(m_ref)
         assert [v / world for v in res[r][1]] == xs[r].grad.tolist()
     assert any(v != 0 for v in res[1][1]) and not any(res[0][1])
+
+
+class _PartlyUnused(torch.nn.Module):
+    """Stand-in for the attpool heads: a parameter the forward never uses."""
+    ddp_find_unused_parameters = True
+
+    def __init__(self):
+        super().__init__()
+        self.used = torch.nn.Linear(3, 2)
+        self.unused = torch.nn.Linear(3, 2)
+
+    def forward(self, x):
+        return self.used(x)
+
+
+def _unused_worker(rank, world, port, out_q):
+    sys.path[:0] = [REPO, os.path.join(REPO, "hl-hgat_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from hlhgat.distributed import init_distributed, wrap_ddp
+    _, _, dev = init_distributed("gloo")
+    torch.manual_seed(0)
+    m = _PartlyUnused()
+    ddp = wrap_ddp(m, dev)
+    ddp(torch.full((4, 3), float(rank + 1))).sum().backward()
+    out_q.put((rank, m.used.weight.grad.tolist(), m.unused.weight.grad))
+    dist.destroy_process_group()
+
+
+def test_ddp_unused_parameters_flag_gives_the_mean_gradient():
+    """wrap_ddp honours a model's ddp_find_unused_parameters flag: without it
+    the bucket holding an unused parameter is never reduced and every gradient
+    stays pre-scaled by 1/W (measured on the pepfunc head: tools/ddp_check.py)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_unused_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, gu)) for r, g, gu in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # d/dW sum(W x + b) over 4 rows of value v = 4 v per entry; mean over ranks v = 1, 2
+    for r in range(world):
+        assert res[r][0] == [[6.0] * 3] * 2
+        assert res[r][1] is None
