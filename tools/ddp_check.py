@@ -9,6 +9,7 @@
 - ZINC head (config 2), a different 64-graph shard per rank: the DDP gradient
   equals the mean of the two per-shard gradients, each computed in one process
   before the process group exists.
+- TSP head (config 5), 2 x 1500-node graphs per rank: as ZINC.
 - pepfunc attpool head (config 4), the SAME shard on both ranks: the attention
   is divided by the batch max over all ranks (hlhgat.distributed.global_max),
   which with identical shards equals the local max, so the DDP gradient equals
@@ -65,6 +66,25 @@ def pep_setup(dev):
     return model, loss, shards
 
 
+def tsp_setup(dev):
+    import hlhgat
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph
+    kw = dict(channels=[4, 4, 4], filters=[32, 64, 128], mlp_channels=[256], K=4)
+    shards = [collate([tsp_like_graph(11 + 2 * r + i, n=1500) for i in range(2)],
+                      check_hodge=False).to(dev) for r in range(2)]
+
+    def model():
+        torch.manual_seed(0)
+        return hlhgat.HL_HGCNN_TSP_dense_int3_pyr(**kw).to(dev).train()
+
+    def loss(m, b):
+        logits, _ = m(b)
+        return torch.nn.functional.binary_cross_entropy_with_logits(
+            logits.view(-1), b.y.view(-1).float())
+    return model, loss, shards
+
+
 def grads_of(m):
     return {k: (p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p))
             for k, p in m.named_parameters()}
@@ -80,7 +100,7 @@ def main():
     dev0 = torch.device("cuda", 0 if os.environ.get("HLHGAT_SHARE_GPU") == "1"
                         else int(os.environ.get("LOCAL_RANK", 0)))
     torch.cuda.set_device(dev0)
-    cases = {"zinc": zinc_setup(dev0), "pepfunc": pep_setup(dev0)}
+    cases = {"zinc": zinc_setup(dev0), "pepfunc": pep_setup(dev0), "tsp": tsp_setup(dev0)}
     # one-process references, before the process group exists
     refs, per_shard = {}, {}
     for name, (model, loss, shards) in cases.items():
