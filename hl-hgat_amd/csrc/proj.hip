@@ -559,16 +559,16 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
 // n of one column) is one ds_read_b128; dC rows stream into registers one
 // 64-wide n chunk ahead.
 template <int TN>
-__global__ __launch_bounds__(256) void k_proj_bwd_data_lds(BwdDataArgs a) {
-  __shared__ float wl[2][TN * 16][KCP];
+__device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, int by,
+                                                  float (*wl)[TN * 16][KCP]) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, i = lane & 15;
-  const int64_t m_base = ((int64_t)blockIdx.x * 4 + wave) * 16;
+  const int64_t m_base = ((int64_t)bx * 4 + wave) * 16;
   int b = 0;
-  while (b + 1 < a.nb && (int)blockIdx.y >= a.tile_start[b + 1]) ++b;
+  while (b + 1 < a.nb && by >= a.tile_start[b + 1]) ++b;
   const int kb = a.kb[b];
-  const int c_base = ((int)blockIdx.y - a.tile_start[b]) * (TN * 16);
+  const int c_base = (by - a.tile_start[b]) * (TN * 16);
   const float* __restrict__ W = a.W[b];
   const int64_t ldw = a.ldw[b];
   const int64_t row = m_base + i;
@@ -644,6 +644,12 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data_lds(BwdDataArgs a) {
   const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
   store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
                       a.accumulate, vec_ok);
+}
+
+template <int TN>
+__global__ __launch_bounds__(256) void k_proj_bwd_data_lds(BwdDataArgs a) {
+  __shared__ float wl[2][TN * 16][KCP];
+  bwd_data_lds_body<TN>(a, (int)blockIdx.x, (int)blockIdx.y, wl);
 }
 
 // ---------------------------------------------------------------------------
@@ -815,25 +821,23 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int WR = 32;  // rows per staged chunk
 
-__global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
-  __shared__ float gl[2][WR][64];
-  __shared__ float al[2][WR][64];
+// XCD-aware work order: workgroups are dealt round-robin over the 8 XCDs, so
+// (tile, split) item w = xcd_slot(linear id) puts consecutive items -- the
+// n-tiles sharing an A chunk, the k-tiles sharing a dC chunk of one split --
+// on ONE XCD at about the same time: their shared chunks hit that XCD's L2
+__device__ __forceinline__ void weight_item(unsigned L, unsigned Y, unsigned total, int& by,
+                                            int& bz) {
+  const unsigned x = L & 7u, k = L >> 3, per = total >> 3, extra = total & 7u;
+  const unsigned w = x * per + (x < extra ? x : extra) + k;
+  by = (int)(w % Y);
+  bz = (int)(w / Y);
+}
+
+__device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by, int bz,
+                                                  float (*gl)[WR][64], float (*al)[WR][64]) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int wn = wave >> 1, wk = wave & 1;
-  // XCD-aware work order: workgroups are dealt round-robin over the 8 XCDs, so
-  // (tile, split) item w = xcd_slot(linear id) puts consecutive items -- the
-  // n-tiles sharing an A chunk, the k-tiles sharing a dC chunk of one split --
-  // on ONE XCD at about the same time: their shared chunks hit that XCD's L2
-  int by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (a.xcd_map) {
-    const unsigned Y = gridDim.y, total = gridDim.y * gridDim.z;
-    const unsigned L = blockIdx.y + blockIdx.z * Y;
-    const unsigned x = L & 7u, k = L >> 3, per = total >> 3, extra = total & 7u;
-    const unsigned w = x * per + (x < extra ? x : extra) + k;
-    by = (int)(w % Y);
-    bz = (int)(w / Y);
-  }
   int b = 0;
   while (b + 1 < a.nb && by >= a.tile_start[b + 1]) ++b;
   const int t = by - a.tile_start[b];
@@ -920,6 +924,15 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
+  __shared__ float gl[2][WR][64];
+  __shared__ float al[2][WR][64];
+  int by = (int)blockIdx.y, bz = (int)blockIdx.z;
+  if (a.xcd_map)
+    weight_item(blockIdx.y + blockIdx.z * gridDim.y, gridDim.y, gridDim.y * gridDim.z, by, bz);
+  bwd_weight32_body(a, by, bz, gl, al);
+}
+
 struct ReduceArgs {
   int nb;
   int N;
@@ -981,6 +994,41 @@ __global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
     const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
     *dst = a.accumulate ? *dst + v : v;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Linear backward with the weight-gradient partials and the data gradient in
+// ONE launch: workgroups [0, n_w) are the weight gradient's (tile, split)
+// items (bwd_weight32_body), workgroups [n_w, ...) the data gradient's tiles
+// (bwd_data_lds_body); k_reduce_splits follows.  The same results, bit for
+// bit, as k_proj_bwd_weight32 -> k_reduce_splits -> k_proj_bwd_data_lds with
+// one dependent launch fewer.  (Reducing the splits in-kernel by the last
+// arriving split of a tile was measured 37 % slower at the ZINC step: one
+// workgroup then reads the tile's ~100 split partials alone.)
+// ---------------------------------------------------------------------------
+struct BwdFusedArgs {
+  BwdWeightArgs w;
+  BwdDataArgs d;
+  int n_w;   // weight workgroups: tiles_total * splits
+  int d_gx;  // data-gradient grid x
+};
+
+template <int TND>
+__global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
+  constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
+  __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
+  const int L = (int)blockIdx.x;
+  if (L >= a.n_w) {
+    const int l = L - a.n_w;
+    bwd_data_lds_body<TND>(a.d, l % a.d_gx, l / a.d_gx,
+                           reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
+    return;
+  }
+  const int Y = a.w.tile_start[a.w.nb];
+  int by = L % Y, bz = L / Y;
+  if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
+  bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
+                    reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
 // --- planning ------------------------------------------------------------------
@@ -1396,6 +1444,114 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   r.dbias = dbias;
   r.accumulate = accumulate;
   const int64_t total = r.elem_start[nblocks] + (dbias ? N : 0);
+  k_reduce_splits<<<(unsigned)ceil_div(total, 64), 256, 0, s>>>(r);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
+                               int nb_w, const float* const* A, const int64_t* lda,
+                               const int64_t* kb_w, float* const* dW, const int64_t* lddw,
+                               float* dbias, int nb_d, const float* const* W,
+                               const int64_t* ldw, const int64_t* kb_d, float* const* dA,
+                               const int64_t* ldda, float* workspace, int64_t workspace_floats,
+                               void* stream) {
+  HLH_CHECK_ARG(nb_w >= 0 && nb_w <= MAXB && nb_d >= 0 && nb_d <= MAXB,
+                "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
+  HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd: bad dC");
+  const bool want_w = nb_w > 0, want_d = nb_d > 0;
+  bool fuse = want_w && want_d && M > 0 && aligned16(dC) && (lddc % 4) == 0 &&
+              (N % 4) == 0;
+  WeightPlan p{};
+  if (want_w) {
+    p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr);
+    HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
+                  "proj_bwd: workspace too small");
+    for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
+  }
+  for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
+  if (!fuse) {  // the separate launches (any alignment, M == 0, one side only)
+    if (want_w) {
+      const int rc = hlhgat_proj_bwd_weight(nb_w, dC, lddc, A, lda, kb_w, M, N, dW, lddw, dbias,
+                                            0, workspace, workspace_floats, stream);
+      if (rc != HLHGAT_OK) return rc;
+    }
+    if (want_d) return hlhgat_proj_bwd_data(nb_d, dC, lddc, W, ldw, kb_d, M, N, dA, ldda, 0,
+                                            stream);
+    return HLHGAT_OK;
+  }
+  BwdFusedArgs f{};
+  BwdWeightArgs& a = f.w;
+  ReduceArgs r{};
+  r.nb = nb_w;
+  r.N = (int)N;
+  r.elem_start[0] = 0;
+  a.nb = nb_w;
+  a.M = M;
+  a.N = (int)N;
+  a.G = dC;
+  a.ldg = lddc;
+  for (int b = 0; b < nb_w; ++b) {
+    HLH_CHECK_ARG(A[b] && dW[b] && kb_w[b] > 0 && lda[b] >= kb_w[b] && lddw[b] >= kb_w[b],
+                  "proj_bwd: bad weight block %d", b);
+    a.A[b] = A[b];
+    a.lda[b] = lda[b];
+    a.kb[b] = (int)kb_w[b];
+    a.tile_start[b] = p.tile_start[b];
+    a.part_off[b] = p.part_off[b];
+    r.part_off[b] = p.part_off[b];
+    r.kb[b] = (int)kb_w[b];
+    r.dW[b] = dW[b];
+    r.lddw[b] = lddw[b];
+    r.elem_start[b + 1] = r.elem_start[b] + N * kb_w[b];
+  }
+  a.tile_start[nb_w] = p.tile_start[nb_w];
+  a.bias_off = p.bias_off;
+  a.part_stride = p.part_stride;
+  a.part = workspace;
+  a.rows_per_split = p.rows_per_split;
+  a.tiles_n = p.tiles_n;
+  a.xcd_map = weight_xcd_map();
+  f.n_w = p.tiles_total * p.splits;
+
+  BwdDataArgs& d = f.d;
+  d.nb = nb_d;
+  d.M = M;
+  d.N = (int)N;
+  d.G = dC;
+  d.ldg = lddc;
+  d.accumulate = 0;
+  int64_t ktot = 0;
+  for (int b = 0; b < nb_d; ++b) ktot += kb_d[b];
+  int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // as hlhgat_proj_bwd_data
+  if (proj_tn()) tnd = proj_tn() < 2 ? proj_tn() : 2;  // tile width only: same results
+  d.tile_start[0] = 0;
+  for (int b = 0; b < nb_d; ++b) {
+    HLH_CHECK_ARG(W[b] && dA[b] && kb_d[b] > 0 && ldw[b] >= kb_d[b] && ldda[b] >= kb_d[b],
+                  "proj_bwd: bad data block %d", b);
+    d.W[b] = W[b];
+    d.O[b] = dA[b];
+    d.ldw[b] = ldw[b];
+    d.ldo[b] = ldda[b];
+    d.kb[b] = (int)kb_d[b];
+    d.tile_start[b + 1] = d.tile_start[b] + (int)ceil_div(kb_d[b], tnd * 16);
+  }
+  f.d_gx = (int)ceil_div(M, 4 * 16);
+  const int64_t n_blocks = (int64_t)f.n_w + (int64_t)f.d_gx * d.tile_start[nb_d];
+  HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
+  hipStream_t s = as_stream(stream);
+  if (tnd == 1)
+    k_proj_bwd_fused<1><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+  else
+    k_proj_bwd_fused<2><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+  HLH_CHECK_LAUNCH();
+  r.splits = p.splits;
+  r.part = workspace;
+  r.part_stride = p.part_stride;
+  r.bias_off = p.bias_off;
+  r.dbias = dbias;
+  r.accumulate = 0;
+  const int64_t total = r.elem_start[nb_w] + (dbias ? N : 0);
   k_reduce_splits<<<(unsigned)ceil_div(total, 64), 256, 0, s>>>(r);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;

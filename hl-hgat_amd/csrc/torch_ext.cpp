@@ -224,6 +224,37 @@ void proj_bwd_weight(const Tensor& G, const std::vector<const float*>& A,
       "proj_bwd_weight");
 }
 
+// HLHGAT_FUSED_BWD=0 (or set_fused_bwd(false)): weight and data gradients
+// as separate launches instead of hlhgat_proj_bwd's single launch (A/B; the
+// results are bitwise the same).
+bool& fused_bwd_flag() {
+  static bool on = [] {
+    const char* e = getenv("HLHGAT_FUSED_BWD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+void set_fused_bwd(bool on) { fused_bwd_flag() = on; }
+
+// weight (+bias) and data gradients of one Linear: hlhgat_proj_bwd (weight
+// partials and data gradient in one launch, then the split reduction)
+void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
+                   const std::vector<int64_t>& lda, const std::vector<int64_t>& kbw,
+                   std::vector<float*>& dW, const std::vector<int64_t>& lddw, float* db,
+                   const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
+                   const std::vector<int64_t>& kbd, std::vector<float*>& dA,
+                   const std::vector<int64_t>& ldda, void* s) {
+  const int nbw = (int)A.size(), nbd = (int)W.size();
+  const int64_t M = G.size(0), N = G.size(1);
+  const int64_t wsf =
+      nbw ? hlhgat_proj_bwd_weight_workspace_floats(nbw, kbw.data(), M, N, db != nullptr) : 0;
+  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, G.options());
+  chk(hlhgat_proj_bwd(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(), kbw.data(),
+                      dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(), kbd.data(),
+                      dA.data(), ldda.data(), ws.data_ptr<float>(), wsf, s),
+      "proj_bwd");
+}
+
 void proj_bwd_data(const Tensor& G, const std::vector<const float*>& W,
                    const std::vector<int64_t>& ldw, const std::vector<int64_t>& kb,
                    std::vector<float*>& dA, const std::vector<int64_t>& ldda, void* s) {
@@ -605,6 +636,12 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     bool need_w = false;
     for (int64_t k = 0; k < K; ++k) need_w = need_w || need(ctx, 9 + k);
     const bool need_b = has_bias && need(ctx, 9 + K);
+    struct {
+      std::vector<float*> dWp;
+      std::vector<int64_t> lddw;
+      float* db = nullptr;
+      std::vector<Tensor> keep;  // the dW buffers stay allocated until the launch
+    } wdef;  // weight gradient deferred into the data gradient's launch
     if (need_w || need_b) {
       std::vector<Tensor> dW(K);
       std::vector<float*> dWp(K);
@@ -615,7 +652,12 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
         lddw[k] = Cin;
       }
       Tensor db = need_b ? grad_like(bias_p) : Tensor();
-      if (M > 0) {
+      if (M > 0 && need_x && fused_bwd_flag()) {
+        wdef.dWp = dWp;  // launched with the data gradient
+        wdef.lddw = lddw;
+        wdef.db = need_b ? db.data_ptr<float>() : nullptr;
+        wdef.keep = dW;
+      } else if (M > 0) {
         proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, s);
       } else {
         for (auto& t : dW) t.zero_();
@@ -636,7 +678,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
           ldw[k] = W[k].stride(0);
           dA[k] = Gs.data_ptr<float>() + k * N * F;
         }
-        proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
+        if (!wdef.dWp.empty())
+          proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s);
+        else
+          proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
         if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
           const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
           Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x2.options());
@@ -769,6 +814,13 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
   }
   dW = Tensor();
   db = Tensor();
+  bool any_a = false;
+  for (int i = 0; i < nb; ++i) any_a = any_a || need_a[i];
+  std::vector<const float*> wAp;  // weight gradient deferred into the data gradient's launch
+  std::vector<int64_t> wlda, wlddw;
+  std::vector<float*> wdWp;
+  float* wdb = nullptr;
+  Tensor wkeep, wkeep_b;  // the gradient buffers stay allocated until the launch
   if (need_w || need_b) {
     Tensor gw = need_w ? grad_like(W) : at::empty_like(W, at::MemoryFormat::Contiguous);
     Tensor gb = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
@@ -783,7 +835,17 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
         lda[i] = ld_of(As[i]);
         dWp[i] = gw.data_ptr<float>() + offs[i];
       }
-      proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, s);
+      if (any_a && fused_bwd_flag()) {
+        wAp = Ap;
+        wlda = lda;
+        wlddw = lddw;
+        wdWp = dWp;
+        wdb = need_b ? gb.data_ptr<float>() : nullptr;
+        wkeep = gw;
+        wkeep_b = gb;
+      } else {
+        proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, s);
+      }
     } else {
       gw.zero_();
       if (need_b) gb.zero_();
@@ -807,7 +869,12 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
       dA.push_back(dAs[i].data_ptr<float>());
       ldda.push_back(kb[i]);
     }
-    if (M > 0) proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s);
+    if (M > 0) {
+      if (!wAp.empty())
+        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s);
+      else
+        proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s);
+    }
   }
 }
 
@@ -1380,6 +1447,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bn_stats", &set_fused_bn_stats);
+  m.def("set_fused_bwd", &set_fused_bwd);
   m.def("set_fused_conv", &set_fused_conv);
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);

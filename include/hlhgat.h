@@ -354,6 +354,22 @@ int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
                            int accumulate, float* workspace,
                            int64_t workspace_floats, void* stream);
 
+/* The Linear backward (torch.nn.Linear / the HodgeLaguerreConv projections,
+ * lib/Hodge_Cheb_Conv.py:63-66 backward) in two launches when the operands are
+ * 16-B aligned: the weight / bias gradient's split partials of
+ * hlhgat_proj_bwd_weight (nb_w blocks; `workspace` sized by
+ * hlhgat_proj_bwd_weight_workspace_floats) together with the data gradient of
+ * hlhgat_proj_bwd_data (nb_d blocks) in one, then the split reduction;
+ * bit-identical to those two calls; either side may be empty (nb = 0).
+ * Unaligned operands fall back to the two calls.  accumulate = 0 only. */
+int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
+                    int nb_w, const float* const* A, const int64_t* lda,
+                    const int64_t* kb_w, float* const* dW, const int64_t* lddw,
+                    float* dbias, int nb_d, const float* const* W,
+                    const int64_t* ldw, const int64_t* kb_d, float* const* dA,
+                    const int64_t* ldda, float* workspace, int64_t workspace_floats,
+                    void* stream);
+
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
  * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge

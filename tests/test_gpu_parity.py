@@ -1105,3 +1105,62 @@ def test_fused_local_conv_bitwise_equals_unfused(cuda, kind, K, side):
         ops._ext.set_fused_conv(False)
     for a, c in zip(*res):
         assert torch.equal(a, c)
+
+
+def _grads_with_fused_bwd(fused, run):
+    from hlhgat import ops
+    try:
+        ops._ext.set_fused_bwd(fused)
+        return run()
+    finally:
+        ops._ext.set_fused_bwd(True)
+
+
+@pytest.mark.parametrize("M", [37, 5000, 70000])
+def test_fused_linear_backward_bitwise(cuda, M):
+    """hlhgat_proj_bwd (weight / bias split partials and the data gradient in
+    one launch, then the split reduction) == the separate weight / reduce /
+    data launches, bit for bit: three input blocks (concatenated
+    Linear input, lib/Hodge_Cheb_Conv.py:307-308), one of them 4-unaligned
+    (the fallback), and the aligned case."""
+    from hlhgat import ops
+    g = torch.Generator(device="cpu").manual_seed(M)
+    for widths in ([64, 128, 8], [64, 6, 32]):
+        blocks = [torch.randn(M, k, generator=g).to(cuda) for k in widths]
+        W = torch.randn(96, sum(widths), generator=g).to(cuda) * 0.1
+        b = torch.randn(96, generator=g).to(cuda)
+        R = torch.randn(M, 96, generator=g).to(cuda)
+
+        def run():
+            xs = [t.clone().requires_grad_(True) for t in blocks]
+            Wv, bv = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+            (ops.linear_blocks(xs, Wv, bv) * R).sum().backward()
+            return [Wv.grad, bv.grad] + [x.grad for x in xs]
+        a = _grads_with_fused_bwd(True, run)
+        c = _grads_with_fused_bwd(False, run)
+        ref = [R.t() @ torch.cat(blocks, 1), R.sum(0)] + list((R @ W).split(widths, 1))
+        for u, v, r in zip(a, c, ref):
+            assert torch.equal(u, v)
+            close(u.cpu(), r.cpu(), 1e-4, "linear grad vs torch")
+
+
+def test_fused_backward_zinc_model_bitwise(cuda):
+    """Every parameter gradient of the ZINC head (conv projections, NodeEdgeInt
+    MLPs, readout MLP) is bitwise the same with the one-launch Linear backward
+    as with the separate launches."""
+    import hlhgat
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(48, seed=5).to(cuda)
+
+    def run():
+        torch.manual_seed(0)
+        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2, 2], filters=[64, 64, 64],
+                                                mlp_channels=[256, 256], K=3,
+                                                keig=15).to(cuda).train()
+        torch.nn.functional.l1_loss(m(b).view(-1), b.y.view(-1)).backward()
+        return {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+    a = _grads_with_fused_bwd(True, run)
+    c = _grads_with_fused_bwd(False, run)
+    assert a.keys() == c.keys() and len(a) > 100
+    for k in a:
+        assert torch.equal(a[k], c[k]), k
