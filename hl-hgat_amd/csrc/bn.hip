@@ -736,3 +736,80 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
+
+// The two halves of hlhgat_bn_bwd_train, for a consumer that applies the
+// backward coefficients itself (hlhgat_proj_bwd_bn folds dx = A g + (B x + C)
+// into the projection gradient's operand loads).
+extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                                    const float* dy, int64_t lddy, int64_t n,
+                                    const int32_t* n_valid, int64_t C, const float* weight,
+                                    const float* save_mean, const float* save_invstd,
+                                    float* coef, float* dweight, float* dbias, void* workspace,
+                                    int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && (!y || ldy >= C),
+                "bn_bwd_reduce: bad sizes");
+  HLH_CHECK_ARG(x && dy && coef && save_mean && save_invstd, "bn_bwd_reduce: NULL pointer");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_bwd_reduce: workspace too small");
+  const bool vec = bn_vec_ok(C, {ldx, lddy, y ? ldy : 4}, {x, y, dy});
+  const int nt = bn_red_threads();
+  const BnLayout Lr = bn_layout(n, C, vec, nt);
+  HLH_CHECK_ARG(Lr.tiles <= kMaxTiles, "bn_bwd_reduce: C too large");
+  BnWs w = carve(workspace, n, C);
+  StatsArgs s{};
+  s.nvalid = n_valid;
+  s.x = x;
+  s.ldx = ldx;
+  s.y = y;
+  s.ldy = ldy;
+  s.dy = dy;
+  s.lddy = lddy;
+  s.n = n;
+  s.C = (int)C;
+  s.tpr = Lr.tpr;
+  s.rp = Lr.rp;
+  s.tiles = Lr.tiles;
+  s.parts = Lr.parts;
+  s.rows_per_part = Lr.rows_per_part;
+  s.part = w.part;
+  s.gpart = w.gpart;
+  s.count = w.count;
+  s.weight = weight;
+  s.save_mean = const_cast<float*>(save_mean);
+  s.save_invstd = const_cast<float*>(save_invstd);
+  s.coef = coef;
+  s.dweight = dweight;
+  s.dbias = dbias;
+  hipStream_t st = as_stream(stream);
+  dim3 g1(Lr.parts, Lr.tiles);
+  if (nt == 1024 && vec)
+    k_bn_bwd_reduce<4, 1024><<<g1, 1024, 0, st>>>(s);
+  else if (nt == 1024)
+    k_bn_bwd_reduce<1, 1024><<<g1, 1024, 0, st>>>(s);
+  else if (vec)
+    k_bn_bwd_reduce<4, kThreads><<<g1, kThreads, 0, st>>>(s);
+  else
+    k_bn_bwd_reduce<1, kThreads><<<g1, kThreads, 0, st>>>(s);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                                   const float* dy, int64_t lddy, int64_t n,
+                                   const int32_t* n_valid, int64_t C, const float* coef,
+                                   float* dx, int64_t lddx, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && lddx >= C && (!y || ldy >= C),
+                "bn_bwd_apply: bad sizes");
+  HLH_CHECK_ARG(x && dy && dx && coef, "bn_bwd_apply: NULL pointer");
+  const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
+  BnLayout L = bn_layout(n, C, vec);
+  BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, coef, L.tpr, L.rp};
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  hipStream_t st = as_stream(stream);
+  if (vec)
+    k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);
+  else
+    k_bn_bwd_apply<1><<<g2, kThreads, 0, st>>>(p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}

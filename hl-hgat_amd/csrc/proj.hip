@@ -467,7 +467,47 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
 // ---------------------------------------------------------------------------
 // data gradient: dA_b = dC W_b   (reduction over N)
 // ---------------------------------------------------------------------------
+// BatchNorm backward folded into the projection gradient's dC operand:
+// dC[m][c] = A_c g' + (B_c x[m][c] + C_c), g' = g masked by y > 0 (ReLU), rows
+// m >= n_valid zero -- k_bn_bwd_apply's expression (bn.hip), evaluated on load.
+struct BnT {
+  const float* x;
+  int64_t ldx;
+  const float* y;  // NULL: no ReLU mask
+  int64_t ldy;
+  const float* coef;  // [3][C]
+  const int32_t* nvalid;
+  int C;
+};
+
+__device__ __forceinline__ int64_t bn_rows(int64_t n, const int32_t* nvalid) {
+  if (!nvalid) return n;
+  const int64_t v = (int64_t)*nvalid;
+  return v < n ? (v < 0 ? 0 : v) : n;
+}
+
+// dC[m][c .. c+3] from the upstream gradient row g (= dy + m * lddy)
+__device__ __forceinline__ float4 bn_dz4(const BnT& t, const float* g, int64_t m, int c) {
+  const float4 gv = *reinterpret_cast<const float4*>(g + c);
+  const float4 xv = *reinterpret_cast<const float4*>(t.x + m * t.ldx + c);
+  float gg[4] = {gv.x, gv.y, gv.z, gv.w};
+  const float xx[4] = {xv.x, xv.y, xv.z, xv.w};
+  if (t.y) {
+    const float4 yv = *reinterpret_cast<const float4*>(t.y + m * t.ldy + c);
+    const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      if (!(yy[v] > 0.f)) gg[v] = 0.f;
+  }
+  float o[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+    o[v] = t.coef[c + v] * gg[v] + (t.coef[t.C + c + v] * xx[v] + t.coef[2 * t.C + c + v]);
+  return make_float4(o[0], o[1], o[2], o[3]);
+}
+
 struct BwdDataArgs {
+  BnT bn;
   int nb;
   int N;
   int64_t M;
@@ -558,7 +598,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
 // TRANSPOSED (wl[c][n], rows padded) so each lane's B fragment (4 consecutive
 // n of one column) is one ds_read_b128; dC rows stream into registers one
 // 64-wide n chunk ahead.
-template <int TN>
+template <int TN, bool BN = false>
 __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, int by,
                                                   float (*wl)[TN * 16][KCP]) {
   const int wave = threadIdx.x >> 6;
@@ -572,8 +612,19 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
   const float* __restrict__ W = a.W[b];
   const int64_t ldw = a.ldw[b];
   const int64_t row = m_base + i;
-  const bool gval = row < a.M;
+  const bool gval = row < a.M && (!BN || row < bn_rows(a.M, a.bn.nvalid));
   const float* grow = a.G + (gval ? row : 0) * a.ldg;
+  auto load_g = [&](int n0, float4 (&o)[4]) {
+    if (!BN) {
+      load_a_chunk(grow, gval, n0, a.N, q, o);
+      return;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = n0 + 16 * s + 4 * q;
+      o[s] = (gval && c < a.N) ? bn_dz4(a.bn, grow, row, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
 
   // staging: TN*16 columns x 64 n = TN*256 float4 over 256 threads; thread
   // loads W[n][c4*4 .. +3] (16 float4 per n row) and scatters 4 floats.
@@ -606,7 +657,7 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
   for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
   float4 wst[TN], gc[4];
   load_w(0, wst);
-  load_a_chunk(grow, gval, 0, a.N, q, gc);
+  load_g(0, gc);
   store_w(wl[0], wst);
   __syncthreads();
   int buf = 0;
@@ -615,7 +666,7 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
     float4 gn[4];
     if (has_next) {
       load_w(n0 + KC, wst);
-      load_a_chunk(grow, gval, n0 + KC, a.N, q, gn);
+      load_g(n0 + KC, gn);
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -666,6 +717,7 @@ constexpr int WT_ROWS = WT_TM * 16;
 constexpr int WT_COLS = WT_TN * 16;
 
 struct BwdWeightArgs {
+  BnT bn;
   int nb;
   int N;
   int64_t M;
@@ -833,6 +885,7 @@ __device__ __forceinline__ void weight_item(unsigned L, unsigned Y, unsigned tot
   bz = (int)(w / Y);
 }
 
+template <bool BN = false>
 __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by, int bz,
                                                   float (*gl)[WR][64], float (*al)[WR][64]) {
   const int wave = threadIdx.x >> 6;
@@ -853,14 +906,19 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
 
   // staging: each tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
   const int sr = threadIdx.x >> 4, sc = (threadIdx.x & 15) * 4;
+  const int64_t g_hi = BN ? bn_rows(a.M, a.bn.nvalid) : a.M;
   auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t m = m0 + sr + 16 * u;
       const bool mv = m < m_hi;
       const int n = n_base + sc, k = k_base + sc;
-      g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (BN)
+        g[u] = (mv && m < g_hi && n < a.N) ? bn_dz4(a.bn, a.G + m * a.ldg, m, n)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      else
+        g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
       x[u] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -1013,21 +1071,21 @@ struct BwdFusedArgs {
   int d_gx;  // data-gradient grid x
 };
 
-template <int TND>
+template <int TND, bool BN>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
   const int L = (int)blockIdx.x;
   if (L >= a.n_w) {
     const int l = L - a.n_w;
-    bwd_data_lds_body<TND>(a.d, l % a.d_gx, l / a.d_gx,
+    bwd_data_lds_body<TND, BN>(a.d, l % a.d_gx, l / a.d_gx,
                            reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
     return;
   }
   const int Y = a.w.tile_start[a.w.nb];
   int by = L % Y, bz = L / Y;
   if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
-  bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
+  bwd_weight32_body<BN>(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
                     reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
@@ -1449,13 +1507,18 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   return HLHGAT_OK;
 }
 
-extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
-                               int nb_w, const float* const* A, const int64_t* lda,
-                               const int64_t* kb_w, float* const* dW, const int64_t* lddw,
-                               float* dbias, int nb_d, const float* const* W,
-                               const int64_t* ldw, const int64_t* kb_d, float* const* dA,
-                               const int64_t* ldda, float* workspace, int64_t workspace_floats,
-                               void* stream) {
+extern "C" int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                                   const float* dy, int64_t lddy, int64_t n,
+                                   const int32_t* n_valid, int64_t C, const float* coef,
+                                   float* dx, int64_t lddx, void* stream);
+
+namespace {
+int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT* bn,
+                  float* dz_scratch, int nb_w, const float* const* A, const int64_t* lda,
+                  const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
+                  int nb_d, const float* const* W, const int64_t* ldw, const int64_t* kb_d,
+                  float* const* dA, const int64_t* ldda, float* workspace,
+                  int64_t workspace_floats, void* stream) {
   HLH_CHECK_ARG(nb_w >= 0 && nb_w <= MAXB && nb_d >= 0 && nb_d <= MAXB,
                 "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
   HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd: bad dC");
@@ -1470,6 +1533,23 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
     for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
+  if (bn) {
+    fuse = fuse && vec_ok(bn->x, bn->ldx, N) && (!bn->y || vec_ok(bn->y, bn->ldy, N)) &&
+           bn->C == N;
+    if (!fuse) {  // BatchNorm backward applied on its own, then the plain path
+      if (M == 0)
+        return proj_bwd_impl(0, N, dC, lddc, nullptr, nullptr, nb_w, A, lda, kb_w, dW, lddw,
+                             dbias, nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats,
+                             stream);
+      HLH_CHECK_ARG(dz_scratch, "proj_bwd_bn: dz_scratch required");
+      const int rc = hlhgat_bn_bwd_apply(bn->x, bn->ldx, bn->y, bn->ldy, dC, lddc, M,
+                                         bn->nvalid, N, bn->coef, dz_scratch, N, stream);
+      if (rc != HLHGAT_OK) return rc;
+      return proj_bwd_impl(M, N, dz_scratch, N, nullptr, nullptr, nb_w, A, lda, kb_w, dW, lddw,
+                           dbias, nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats,
+                           stream);
+    }
+  }
   if (!fuse) {  // the separate launches (any alignment, M == 0, one side only)
     if (want_w) {
       const int rc = hlhgat_proj_bwd_weight(nb_w, dC, lddc, A, lda, kb_w, M, N, dW, lddw, dbias,
@@ -1481,6 +1561,7 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
     return HLHGAT_OK;
   }
   BwdFusedArgs f{};
+  if (bn) f.w.bn = f.d.bn = *bn;
   BwdWeightArgs& a = f.w;
   ReduceArgs r{};
   r.nb = nb_w;
@@ -1540,10 +1621,14 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
   const int64_t n_blocks = (int64_t)f.n_w + (int64_t)f.d_gx * d.tile_start[nb_d];
   HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
   hipStream_t s = as_stream(stream);
-  if (tnd == 1)
-    k_proj_bwd_fused<1><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+  if (tnd == 1 && bn)
+    k_proj_bwd_fused<1, true><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+  else if (bn)
+    k_proj_bwd_fused<2, true><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+  else if (tnd == 1)
+    k_proj_bwd_fused<1, false><<<(unsigned)n_blocks, 256, 0, s>>>(f);
   else
-    k_proj_bwd_fused<2><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+    k_proj_bwd_fused<2, false><<<(unsigned)n_blocks, 256, 0, s>>>(f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
@@ -1555,4 +1640,31 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
   k_reduce_splits<<<(unsigned)ceil_div(total, 64), 256, 0, s>>>(r);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
+}
+}  // namespace
+
+extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
+                               int nb_w, const float* const* A, const int64_t* lda,
+                               const int64_t* kb_w, float* const* dW, const int64_t* lddw,
+                               float* dbias, int nb_d, const float* const* W,
+                               const int64_t* ldw, const int64_t* kb_d, float* const* dA,
+                               const int64_t* ldda, float* workspace, int64_t workspace_floats,
+                               void* stream) {
+  return proj_bwd_impl(M, N, dC, lddc, nullptr, nullptr, nb_w, A, lda, kb_w, dW, lddw, dbias,
+                       nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats, stream);
+}
+
+extern "C" int hlhgat_proj_bwd_bn(int64_t M, int64_t N, const float* dy, int64_t lddy,
+                                  const float* bn_x, int64_t ldx, const float* bn_y,
+                                  int64_t ldy, const float* coef, const int32_t* n_valid,
+                                  int nb_w, const float* const* A, const int64_t* lda,
+                                  const int64_t* kb_w, float* const* dW, const int64_t* lddw,
+                                  float* dbias, int nb_d, const float* const* W,
+                                  const int64_t* ldw, const int64_t* kb_d, float* const* dA,
+                                  const int64_t* ldda, float* dz_scratch, float* workspace,
+                                  int64_t workspace_floats, void* stream) {
+  HLH_CHECK_ARG(bn_x && coef && ldx >= N && (!bn_y || ldy >= N), "proj_bwd_bn: bad BN operands");
+  BnT t{bn_x, ldx, bn_y, ldy, coef, n_valid, (int)N};
+  return proj_bwd_impl(M, N, dy, lddy, &t, dz_scratch, nb_w, A, lda, kb_w, dW, lddw, dbias,
+                       nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats, stream);
 }

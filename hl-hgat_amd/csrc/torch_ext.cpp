@@ -395,6 +395,67 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
   return dx;
 }
 
+// HLHGAT_FOLD_BN_BWD=1 (or set_fold_bn_bwd(true)): fold the conv's BatchNorm
+// backward apply into the projection gradient's operand loads
+// (hlhgat_proj_bwd_bn, bitwise the same results).  OFF by default: same-box
+// A/B at the ZINC step 282.0k -> 267.3k graphs/s -- every dC element then
+// costs three loads (dy, x, y) and the per-channel coefficients in each of the
+// weight- and data-gradient workgroups that read it, more than the apply
+// launch it removes.
+bool& fold_bn_flag() {
+  static bool on = [] {
+    const char* e = getenv("HLHGAT_FOLD_BN_BWD");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+void set_fold_bn_bwd(bool on) { fold_bn_flag() = on; }
+
+// the statistics half of bn_backward: fills dw / db, returns coef [3, C]
+Tensor bn_backward_coef(const Tensor& x, const OptT& y, const Tensor& dyc, const OptT& w,
+                        const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
+                        Tensor& dw, Tensor& db, const Tensor* b_param, const Tensor& valid) {
+  const int64_t n = x.size(0), C = x.size(1);
+  dw = (need_w && has(w)) ? grad_like(w) : Tensor();
+  db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
+                                                 : at::empty({C}, x.options()))
+              : Tensor();
+  Tensor ws = bn_workspace(x, n, C);
+  Tensor coef = at::empty({3 * C}, x.options());
+  chk(hlhgat_bn_bwd_reduce(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
+                           dyc.data_ptr<float>(), ld_of(dyc), n,
+                           valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
+                           mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                           coef.data_ptr<float>(), dw.defined() ? dw.data_ptr<float>() : nullptr,
+                           db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
+                           ws.numel(), stream_of(x)),
+      "bn_bwd_reduce");
+  return coef;
+}
+
+// proj_bwd_both with the BN backward folded into the dC operand
+void proj_bwd_bn_both(const Tensor& dy, const Tensor& bx, const OptT& by, const Tensor& coef,
+                      const Tensor& valid, const std::vector<const float*>& A,
+                      const std::vector<int64_t>& lda, const std::vector<int64_t>& kbw,
+                      std::vector<float*>& dW, const std::vector<int64_t>& lddw, float* db,
+                      const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
+                      const std::vector<int64_t>& kbd, std::vector<float*>& dA,
+                      const std::vector<int64_t>& ldda, void* s) {
+  const int nbw = (int)A.size(), nbd = (int)W.size();
+  const int64_t M = dy.size(0), N = dy.size(1);
+  const int64_t wsf =
+      nbw ? hlhgat_proj_bwd_weight_workspace_floats(nbw, kbw.data(), M, N, db != nullptr) : 0;
+  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, dy.options());
+  Tensor dz = at::empty({M, N}, dy.options());  // used only by the unaligned fallback
+  chk(hlhgat_proj_bwd_bn(M, N, dy.data_ptr<float>(), ld_of(dy), bx.data_ptr<float>(), ld_of(bx),
+                         fptr(by), has(by) ? ld_of(*by) : 0, coef.data_ptr<float>(),
+                         valid.defined() ? valid.data_ptr<int32_t>() : nullptr, nbw, A.data(),
+                         lda.data(), kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(),
+                         ldw.data(), kbd.data(), dA.data(), ldda.data(), dz.data_ptr<float>(),
+                         ws.data_ptr<float>(), wsf, s),
+      "proj_bwd_bn");
+}
+
 // ---------------------------------------------------------------------------
 // conv (+ BN (+ ReLU))
 // ---------------------------------------------------------------------------
@@ -616,15 +677,6 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     const int64_t n_pos = 33 + K + (int64_t)fac.size() + 1;
     variable_list out(n_pos);
     const bool need_x = need(ctx, 0);
-    Tensor dbn_w, dbn_b;
-    if (bn_mode > 0) {
-      OptT y = bn_mode == 2 ? OptT(yout) : OptT();
-      OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-      G = bn_backward(pre, y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K), dbn_w,
-                      dbn_b, nullptr, &bn_b, valid);
-      out[10 + K] = dbn_w;
-      out[11 + K] = dbn_b;
-    }
     std::vector<const float*> Ap(K);
     std::vector<int64_t> lda(K), kb(K, Cin);
     Ap[0] = x2.data_ptr<float>();
@@ -642,6 +694,19 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       float* db = nullptr;
       std::vector<Tensor> keep;  // the dW buffers stay allocated until the launch
     } wdef;  // weight gradient deferred into the data gradient's launch
+    Tensor dbn_w, dbn_b, bn_coef;  // bn_coef: BN backward folded into the projection's
+    const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
+    if (bn_mode > 0) {
+      OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
+      if (need_x && (need_w || need_b) && M > 0 && fused_bwd_flag() && fold_bn_flag())
+        bn_coef = bn_backward_coef(pre, bn_y, G, w, mean, invstd, need(ctx, 10 + K),
+                                   need(ctx, 11 + K), dbn_w, dbn_b, &bn_b, valid);
+      else
+        G = bn_backward(pre, bn_y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K),
+                        dbn_w, dbn_b, nullptr, &bn_b, valid);
+      out[10 + K] = dbn_w;
+      out[11 + K] = dbn_b;
+    }
     if (need_w || need_b) {
       std::vector<Tensor> dW(K);
       std::vector<float*> dWp(K);
@@ -678,7 +743,10 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
           ldw[k] = W[k].stride(0);
           dA[k] = Gs.data_ptr<float>() + k * N * F;
         }
-        if (!wdef.dWp.empty())
+        if (!wdef.dWp.empty() && bn_coef.defined())
+          proj_bwd_bn_both(G, pre, bn_y, bn_coef, valid, Ap, lda, kb, wdef.dWp, wdef.lddw,
+                           wdef.db, Wp, ldw, kb, dA, ldda, s);
+        else if (!wdef.dWp.empty())
           proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s);
         else
           proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
@@ -1448,6 +1516,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bn_stats", &set_fused_bn_stats);
   m.def("set_fused_bwd", &set_fused_bwd);
+  m.def("set_fold_bn_bwd", &set_fold_bn_bwd);
   m.def("set_fused_conv", &set_fused_conv);
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);

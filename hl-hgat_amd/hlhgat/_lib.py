@@ -73,6 +73,13 @@ SIGNATURES = {
     "hlhgat_proj_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_i32, P_vp, P_i64, P_i64, P_vp,
                                 P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64, c_vp,
                                 c_i64, c_vp]),
+    "hlhgat_proj_bwd_bn": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
+                                   c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64, c_vp, c_i32,
+                                   P_vp, P_i64, P_i64, P_vp, P_i64, c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_bn_bwd_reduce": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_bn_bwd_apply": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                    c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_edge_gather2": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_f32,
                                     c_f32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_att_score_fwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,

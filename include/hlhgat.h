@@ -370,6 +370,22 @@ int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
                     const int64_t* ldda, float* workspace, int64_t workspace_floats,
                     void* stream);
 
+/* hlhgat_proj_bwd with the BatchNorm1d (+ReLU) backward in front of it
+ * folded into the dC operand loads (lib/Hodge_ST_Model.py:556-566 conv -> BN
+ * -> ReLU backward): dC = coef[0] g' + (coef[1] x + coef[2]) per channel with
+ * g' = dy masked by bn_y > 0 (bn_y NULL: no ReLU) and rows >= *n_valid zero,
+ * the coefficients from hlhgat_bn_bwd_reduce.  Bit-identical to
+ * hlhgat_bn_bwd_apply into a buffer followed by hlhgat_proj_bwd, which is
+ * what runs (into dz_scratch, [M][N]) when the operands are not 16-B aligned. */
+int hlhgat_proj_bwd_bn(int64_t M, int64_t N, const float* dy, int64_t lddy,
+                       const float* bn_x, int64_t ldx, const float* bn_y, int64_t ldy,
+                       const float* coef, const int32_t* n_valid, int nb_w,
+                       const float* const* A, const int64_t* lda, const int64_t* kb_w,
+                       float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
+                       const float* const* W, const int64_t* ldw, const int64_t* kb_d,
+                       float* const* dA, const int64_t* ldda, float* dz_scratch,
+                       float* workspace, int64_t workspace_floats, void* stream);
+
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
  * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge
@@ -468,6 +484,20 @@ int hlhgat_proj_fwd_bn(int nblocks, const float* const* A, const int64_t* lda,
                        int64_t* num_batches_tracked, float momentum, float eps,
                        float* save_mean, float* save_invstd, void* workspace,
                        int64_t workspace_bytes, void* stream);
+
+/* The statistics half of hlhgat_bn_bwd_train: dweight / dbias (each may be
+ * NULL) and the per-channel coefficients coef[3][C] of dx = coef[0] g' +
+ * (coef[1] x + coef[2]); no dx. */
+int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                         const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
+                         int64_t C, const float* weight, const float* save_mean,
+                         const float* save_invstd, float* coef, float* dweight, float* dbias,
+                         void* workspace, int64_t workspace_bytes, void* stream);
+
+/* The apply half: dx from hlhgat_bn_bwd_reduce's coefficients. */
+int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                        const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
+                        int64_t C, const float* coef, float* dx, int64_t lddx, void* stream);
 
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
                         const float* dy, int64_t lddy, int64_t n,

@@ -1107,13 +1107,15 @@ def test_fused_local_conv_bitwise_equals_unfused(cuda, kind, K, side):
         assert torch.equal(a, c)
 
 
-def _grads_with_fused_bwd(fused, run):
+def _grads_with_fused_bwd(fused, run, fold=True):
     from hlhgat import ops
     try:
         ops._ext.set_fused_bwd(fused)
+        ops._ext.set_fold_bn_bwd(fold)
         return run()
     finally:
         ops._ext.set_fused_bwd(True)
+        ops._ext.set_fold_bn_bwd(False)
 
 
 @pytest.mark.parametrize("M", [37, 5000, 70000])
@@ -1144,13 +1146,19 @@ def test_fused_linear_backward_bitwise(cuda, M):
             close(u.cpu(), r.cpu(), 1e-4, "linear grad vs torch")
 
 
-def test_fused_backward_zinc_model_bitwise(cuda):
+@pytest.mark.parametrize("padded", [False, True])
+def test_fused_backward_zinc_model_bitwise(cuda, padded):
     """Every parameter gradient of the ZINC head (conv projections, NodeEdgeInt
-    MLPs, readout MLP) is bitwise the same with the one-launch Linear backward
-    as with the separate launches."""
+    MLPs, readout MLP) is bitwise the same with the fused Linear backward, with
+    and without the conv BatchNorm backward folded into its operand loads, as
+    with the separate launches; padded: static-shape capacity rows (n_valid)."""
     import hlhgat
+    from hlhgat.hodge_dataset import pad_batch, static_caps
     from hlhgat.synthetic import zinc_like_batch
-    b = zinc_like_batch(48, seed=5).to(cuda)
+    b = zinc_like_batch(48, seed=5)
+    if padded:
+        b = pad_batch(b, static_caps(b, 128))
+    b = b.to(cuda)
 
     def run():
         torch.manual_seed(0)
@@ -1159,8 +1167,10 @@ def test_fused_backward_zinc_model_bitwise(cuda):
                                                 keig=15).to(cuda).train()
         torch.nn.functional.l1_loss(m(b).view(-1), b.y.view(-1)).backward()
         return {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
-    a = _grads_with_fused_bwd(True, run)
+    a = _grads_with_fused_bwd(True, run, fold=True)
+    f = _grads_with_fused_bwd(True, run, fold=False)
     c = _grads_with_fused_bwd(False, run)
-    assert a.keys() == c.keys() and len(a) > 100
+    assert a.keys() == c.keys() == f.keys() and len(a) > 100
     for k in a:
         assert torch.equal(a[k], c[k]), k
+        assert torch.equal(f[k], c[k]), k
