@@ -31,7 +31,9 @@ constexpr int kMaxParts = 512;
 constexpr int kGroup = 16;                        // partitions per first-level group
 constexpr int kMaxGroups = kMaxParts / kGroup;
 constexpr int kMaxTiles = 1024;
-constexpr int kCounters = kMaxTiles * (1 + kMaxGroups);  // per tile: top + group counters
+constexpr int kFlagBase = kMaxTiles * (1 + kMaxGroups);  // per tile: top + group counters
+// + per tile: the one-launch forward's "statistics ready" flag and leave counter
+constexpr int kCounters = kFlagBase + 2 * kMaxTiles;
 constexpr int APPLY_RPT = 2;  // rows per thread in the elementwise apply kernels
 
 struct BnLayout {
@@ -54,6 +56,20 @@ struct BnLayout {
 // Larger batches (config 3 / 5 heads: 1.4e5-2e5 rows) get one partition per
 // 512 rows (up to kMaxParts): 64 workgroups leave most of the 256 CUs idle
 // there (k_bn_bwd_reduce ran at ~1 TB/s, profiles/r01_h_*_head_kernel_stats.md).
+// HLHGAT_BN_ONE_LAUNCH=1: BatchNorm forward statistics and apply in one
+// launch (k_bn_train_fused; bitwise the same results).  OFF by default:
+// same-box A/B at the ZINC step 282.3k vs 283.1k graphs/s (noise) -- the
+// in-kernel wait for the finalising workgroup costs what the launch boundary
+// did, so the spin-wait is not worth carrying.
+bool& bn_one_launch_flag() {
+  static bool v = [] {
+    const char* e = getenv("HLHGAT_BN_ONE_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+bool bn_one_launch() { return bn_one_launch_flag(); }
+
 int64_t bn_parts(int64_t n) {
   static int64_t fixed = [] {
     const char* e = getenv("HLHGAT_BN_PARTS");
@@ -184,6 +200,15 @@ __device__ __forceinline__ double ld_wt(const double* p) {
       (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+__device__ __forceinline__ void st_wt32(float* p, float v) {
+  __hip_atomic_store((gu32_t*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt32(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load((gu32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Signal arrival; returns true in the last workgroup of this column tile.
 // Every wave has drained its write-through partial stores (vmcnt(0)) before
 // the barrier; ONE lane adds to the counter; the workgroup whose add returned
@@ -308,8 +333,30 @@ __device__ __forceinline__ bool tree_reduce(const StatsArgs& a, int c0, int tile
   return true;
 }
 
-template <int V, int NT>
-__global__ __launch_bounds__(NT) void k_bn_stats(StatsArgs a) {
+struct ApplyArgs {
+  const int32_t* nvalid;
+  const float* x;
+  int64_t ldx;
+  float* y;
+  int64_t ldy;
+  int64_t n;
+  int C;
+  const float* mean;
+  const float* invstd;
+  const float* weight;
+  const float* bias;
+  int relu;
+  int tpr, rp;
+};
+
+// Statistics (and, APPLY, the normalisation in the same launch): with APPLY
+// the finalising workgroup of a column tile publishes mean / invstd write-
+// through and raises the tile's flag; the other workgroups of the tile (all
+// co-resident: parts x tiles <= a few hundred workgroups of 256 threads) wait
+// for it, normalise the rows they summed, and the last to leave resets the
+// flag.  The wait is bounded so a stalled launch cannot hang the GPU.
+template <int V, int NT, bool APPLY>
+__device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArgs& p) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -351,42 +398,108 @@ __global__ __launch_bounds__(NT) void k_bn_stats(StatsArgs a) {
   // the finalising workgroup of this column tile: finalise its columns
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  if (!tree_reduce<NT>(a, c0, tile_c, sum0, sum1)) return;
-  for (int t = threadIdx.x; t < tile_c; t += NT) {
-    const int cc = c0 + t;
-    if (cc >= a.C) continue;
-    const double u0 = sum0[t], u1 = sum1[t];
-    const double nn = (double)(n_eff > 0 ? n_eff : 1);
-    const double mean = u0 / nn;
-    double var = u1 / nn - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-    a.save_mean[cc] = (float)mean;
-    a.save_invstd[cc] = invstd;
-    if (a.running_mean) {
-      const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
-      a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
-      a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
+  const bool fin = tree_reduce<NT>(a, c0, tile_c, sum0, sum1);
+  if (!APPLY && !fin) return;
+  if (fin) {
+    for (int t = threadIdx.x; t < tile_c; t += NT) {
+      const int cc = c0 + t;
+      if (cc >= a.C) continue;
+      const double u0 = sum0[t], u1 = sum1[t];
+      const double nn = (double)(n_eff > 0 ? n_eff : 1);
+      const double mean = u0 / nn;
+      double var = u1 / nn - mean * mean;
+      if (var < 0.0) var = 0.0;
+      const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+      if (APPLY) {
+        st_wt32(&a.save_mean[cc], (float)mean);
+        st_wt32(&a.save_invstd[cc], invstd);
+      } else {
+        a.save_mean[cc] = (float)mean;
+        a.save_invstd[cc] = invstd;
+      }
+      if (a.running_mean) {
+        const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
+        a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
+        a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
+      }
+    }
+    if (a.nbt && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  }
+  if (!APPLY) return;
+  unsigned* flag = a.count + kFlagBase + blockIdx.y;
+  unsigned* leave = flag + kMaxTiles;
+  if (fin) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (threadIdx.x == 0) {
+      unsigned it = 0;
+      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             ++it < (1u << 22))
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+  }
+  if (c < a.C) {
+    float sc[V], sh[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float w = p.weight ? p.weight[c + v] : 1.f;
+      const float b = p.bias ? p.bias[c + v] : 0.f;
+      sc[v] = w * ld_wt32(&p.invstd[c + v]);
+      sh[v] = b - ld_wt32(&p.mean[c + v]) * sc[v];
+    }
+    int64_t r_end = r_lo + a.rows_per_part;
+    if (r_end > a.n) r_end = a.n;
+    auto out = [&](int64_t r, vt xv) {
+      vt o;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float z = vget(xv, v) * sc[v] + sh[v];
+        vget(o, v) = r >= n_eff ? 0.f : ((p.relu && z < 0.f) ? 0.f : z);
+      }
+      vstore<V>(p.y + r * p.ldy + c, o);
+    };
+    int64_t r = r_lo + rg;
+    for (; r + 7 * a.rp < r_end; r += 8 * a.rp) {  // 8 rows in flight
+      vt x4[8] = {};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t rr = r + u * a.rp;
+        if (rr < n_eff) x4[u] = vload<V>(a.x + rr * a.ldx + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) out(r + u * a.rp, x4[u]);
+    }
+    for (; r < r_end; r += a.rp) {
+      vt xv{};
+      if (r < n_eff) xv = vload<V>(a.x + r * a.ldx + c);
+      out(r, xv);
     }
   }
-  if (a.nbt && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev =
+        __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // every workgroup of the tile has read the flag
+      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
-struct ApplyArgs {
-  const int32_t* nvalid;
-  const float* x;
-  int64_t ldx;
-  float* y;
-  int64_t ldy;
-  int64_t n;
-  int C;
-  const float* mean;
-  const float* invstd;
-  const float* weight;
-  const float* bias;
-  int relu;
-  int tpr, rp;
-};
+template <int V, int NT>
+__global__ __launch_bounds__(NT) void k_bn_stats(StatsArgs a) {
+  bn_stats_body<V, NT, false>(a, ApplyArgs{});
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_train_fused(StatsArgs a, ApplyArgs p) {
+  bn_stats_body<V, kThreads, true>(a, p);
+}
+
 
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
@@ -665,6 +778,54 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
   HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
                 "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
   HLH_CHECK_ARG(y, "bn_fwd_train: NULL pointer");
+  const bool vec = bn_vec_ok(C, {ldx}, {x});
+  // one launch only for grids of <= 256 workgroups: with the node / edge /
+  // interaction streams each running one, every waiting workgroup's tile
+  // peers still find a free slot (>= 6 such workgroups fit per CU)
+  const BnLayout L1 = bn_layout(n, C, vec, kThreads);
+  if (bn_one_launch() && bn_red_threads() == kThreads && (int64_t)L1.parts * L1.tiles <= 256 &&
+      vec == bn_vec_ok(C, {ldx, ldy}, {x, y})) {
+    // statistics and normalisation in one launch (k_bn_train_fused)
+    HLH_CHECK_ARG(x && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
+    HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                  "bn_fwd_train: running_mean/var must both be given or both NULL");
+    HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                  "bn_fwd_train: workspace too small");
+    BnLayout L = bn_layout(n, C, vec, kThreads);
+    HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_fwd_train: C too large");
+    BnWs w = carve(workspace, n, C);
+    StatsArgs s{};
+    s.nvalid = n_valid;
+    s.x = x;
+    s.ldx = ldx;
+    s.n = n;
+    s.C = (int)C;
+    s.tpr = L.tpr;
+    s.rp = L.rp;
+    s.tiles = L.tiles;
+    s.parts = L.parts;
+    s.rows_per_part = L.rows_per_part;
+    s.part = w.part;
+    s.gpart = w.gpart;
+    s.count = w.count;
+    s.running_mean = running_mean;
+    s.running_var = running_var;
+    s.nbt = num_batches_tracked;
+    s.momentum = momentum;
+    s.eps = eps;
+    s.save_mean = save_mean;
+    s.save_invstd = save_invstd;
+    ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias,
+                relu, L.tpr, L.rp};
+    hipStream_t st = as_stream(stream);
+    dim3 g1(L.parts, L.tiles);
+    if (vec)
+      k_bn_train_fused<4><<<g1, kThreads, 0, st>>>(s, p);
+    else
+      k_bn_train_fused<1><<<g1, kThreads, 0, st>>>(s, p);
+    HLH_CHECK_LAUNCH();
+    return HLHGAT_OK;
+  }
   int rc = hlhgat_bn_stats_train(x, ldx, n, n_valid, C, running_mean, running_var,
                                  num_batches_tracked, momentum, eps, save_mean, save_invstd,
                                  workspace, workspace_bytes, stream);
@@ -811,5 +972,10 @@ extern "C" int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, 
   else
     k_bn_bwd_apply<1><<<g2, kThreads, 0, st>>>(p);
   HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_set_bn_one_launch(int on) {
+  bn_one_launch_flag() = on != 0;
   return HLHGAT_OK;
 }

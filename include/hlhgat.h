@@ -499,6 +499,11 @@ int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy
                         const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
                         int64_t C, const float* coef, float* dx, int64_t lddx, void* stream);
 
+/* BatchNorm forward statistics and normalisation in one launch
+ * (k_bn_train_fused, grids of <= 256 workgroups) or as two; default 0
+ * (env HLHGAT_BN_ONE_LAUNCH).  Both give bitwise the same results. */
+int hlhgat_set_bn_one_launch(int on);
+
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
                         const float* dy, int64_t lddy, int64_t n,
                         const int32_t* n_valid, int64_t C,

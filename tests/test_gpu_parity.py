@@ -1174,3 +1174,45 @@ def test_fused_backward_zinc_model_bitwise(cuda, padded):
     for k in a:
         assert torch.equal(a[k], c[k]), k
         assert torch.equal(f[k], c[k]), k
+
+
+@pytest.mark.parametrize("n,C,relu,pad", [(700, 64, True, 0), (25600, 64, True, 333),
+                                          (25600, 256, False, 0), (4097, 6, True, 5),
+                                          (200000, 64, True, 0)])
+def test_bn_one_launch_bitwise(cuda, n, C, relu, pad):
+    """BatchNorm forward in one launch (k_bn_train_fused: statistics, a tile-
+    wide wait for the finalising workgroup, normalisation) == the statistics +
+    apply launches bit for bit: output, batch mean / invstd, running stats and
+    the backward through it; padded rows (n_valid) and an unaligned C (the
+    vector path off) included; n = 200000 exceeds the one-launch grid cap and
+    takes the two launches either way."""
+    from hlhgat import _lib, ops
+    g = torch.Generator(device="cpu").manual_seed(n + C)
+    x0 = (torch.randn(n, C, generator=g) * 3 + 1).to(cuda)
+    R = torch.randn(n, C, generator=g).to(cuda)
+    valid = torch.tensor([n - pad], dtype=torch.int32, device=cuda) if pad else None
+    outs = []
+    try:
+        for one in (1, 0):
+            _lib.check(_lib.LIB.hlhgat_set_bn_one_launch(one), "set_bn_one_launch")
+            torch.manual_seed(0)
+            bn = torch.nn.BatchNorm1d(C).to(cuda).train()
+            with torch.no_grad():
+                bn.weight.uniform_(0.5, 1.5)
+                bn.bias.uniform_(-0.5, 0.5)
+            x = x0.clone().requires_grad_(True)
+            y = ops.batch_norm_act(x, bn, relu=relu, valid=valid)
+            (y * R).sum().backward()
+            outs.append([y.detach(), x.grad, bn.weight.grad, bn.bias.grad, bn.running_mean,
+                         bn.running_var])
+    finally:
+        _lib.LIB.hlhgat_set_bn_one_launch(0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    nv = n - pad
+    ref = torch.nn.functional.batch_norm(x0[:nv].double(), None, None, training=True, eps=1e-5)
+    ref = ref * bn.weight.detach().double() + bn.bias.detach().double()
+    if relu:
+        ref = ref.clamp_min(0)
+    close(outs[0][0][:nv].cpu(), ref.float().cpu(), 1e-5, "bn forward vs fp64")
+    assert not outs[0][0][nv:].any()
