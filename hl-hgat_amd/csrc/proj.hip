@@ -1067,8 +1067,11 @@ __global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
 struct BwdFusedArgs {
   BwdWeightArgs w;
   BwdDataArgs d;
-  int n_w;   // weight workgroups: tiles_total * splits
-  int d_gx;  // data-gradient grid x
+  int n_w;     // weight workgroups: tiles_total * splits
+  int n_wpad;  // n_w rounded up to a multiple of 8 (the data items start on XCD 0)
+  int d_gx;    // data-gradient grid x
+  int n_d;     // data workgroups: d_gx * column tiles
+  int d_xcd;   // XCD-aware data order: the column tiles of one row block on one XCD
 };
 
 template <int TND, bool BN>
@@ -1076,12 +1079,27 @@ __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
   const int L = (int)blockIdx.x;
-  if (L >= a.n_w) {
-    const int l = L - a.n_w;
-    bwd_data_lds_body<TND, BN>(a.d, l % a.d_gx, l / a.d_gx,
-                           reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
+  if (L >= a.n_wpad) {
+    const int l = L - a.n_wpad;
+    int bx, by;
+    if (a.d_xcd) {
+      // w = xcd_slot(l): consecutive w on one XCD; w -> (column tile fastest,
+      // row block): a row block's dC rows are fetched into one XCD's L2 once
+      // for all its column tiles
+      const int tiles = a.n_d / a.d_gx;
+      int wy, wz;
+      weight_item((unsigned)l, 1u, (unsigned)a.n_d, wy, wz);
+      by = wz % tiles;
+      bx = wz / tiles;
+      (void)wy;
+    } else {
+      bx = l % a.d_gx;
+      by = l / a.d_gx;
+    }
+    bwd_data_lds_body<TND, BN>(a.d, bx, by, reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
     return;
   }
+  if (L >= a.n_w) return;  // alignment padding
   const int Y = a.w.tile_start[a.w.nb];
   int by = L % Y, bz = L / Y;
   if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
@@ -1152,6 +1170,16 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
 int weight_xcd_map() {
   static int v = [] {
     const char* e = getenv("HLHGAT_WEIGHT_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+// HLHGAT_DATA_XCD=0: plain (row block fastest) order of the fused backward's
+// data-gradient workgroups instead of the XCD-aware one (A/B; same results)
+int data_xcd_map() {
+  static int v = [] {
+    const char* e = getenv("HLHGAT_DATA_XCD");
     return e ? atoi(e) : 1;
   }();
   return v;
@@ -1618,7 +1646,10 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT
     d.tile_start[b + 1] = d.tile_start[b] + (int)ceil_div(kb_d[b], tnd * 16);
   }
   f.d_gx = (int)ceil_div(M, 4 * 16);
-  const int64_t n_blocks = (int64_t)f.n_w + (int64_t)f.d_gx * d.tile_start[nb_d];
+  f.n_wpad = (f.n_w + 7) & ~7;
+  f.n_d = f.d_gx * d.tile_start[nb_d];
+  f.d_xcd = data_xcd_map();
+  const int64_t n_blocks = (int64_t)f.n_wpad + (int64_t)f.n_d;
   HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
   hipStream_t s = as_stream(stream);
   if (tnd == 1 && bn)
