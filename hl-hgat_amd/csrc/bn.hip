@@ -56,15 +56,15 @@ struct BnLayout {
 // Larger batches (config 3 / 5 heads: 1.4e5-2e5 rows) get one partition per
 // 512 rows (up to kMaxParts): 64 workgroups leave most of the 256 CUs idle
 // there (k_bn_bwd_reduce ran at ~1 TB/s, profiles/r01_h_*_head_kernel_stats.md).
-// HLHGAT_BN_ONE_LAUNCH=1: BatchNorm forward statistics and apply in one
-// launch (k_bn_train_fused; bitwise the same results).  OFF by default:
-// same-box A/B at the ZINC step 282.3k vs 283.1k graphs/s (noise) -- the
-// in-kernel wait for the finalising workgroup costs what the launch boundary
-// did, so the spin-wait is not worth carrying.
+// HLHGAT_BN_ONE_LAUNCH=0: BatchNorm forward statistics and apply as two
+// launches instead of k_bn_train_fused (bitwise the same results).  Same-box
+// A/B at the ZINC step with 128 partitions: 288.6k -> 291.1k graphs/s over
+// five runs each (every one-launch run above every two-launch run; with 64
+// partitions it was neutral).
 bool& bn_one_launch_flag() {
   static bool v = [] {
     const char* e = getenv("HLHGAT_BN_ONE_LAUNCH");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -201,6 +201,9 @@ __device__ __forceinline__ double ld_wt(const double* p) {
   return __longlong_as_double(
       (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
+
+// wait timeouts of the one-launch BatchNorm (hlhgat_bn_wait_timeouts)
+__device__ unsigned g_bn_wait_timeouts = 0;
 
 typedef __attribute__((address_space(1))) unsigned gu32_t;
 __device__ __forceinline__ void st_wt32(float* p, float v) {
@@ -441,6 +444,9 @@ __device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArg
       while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
              ++it < (1u << 22))
         __builtin_amdgcn_s_sleep(1);
+      if (it >= (1u << 22))  // never expected: counted so the host can check
+        __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
   }
@@ -979,5 +985,11 @@ extern "C" int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, 
 
 extern "C" int hlhgat_set_bn_one_launch(int on) {
   bn_one_launch_flag() = on != 0;
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_wait_timeouts(unsigned* out) {
+  HLH_CHECK_ARG(out, "bn_wait_timeouts: NULL pointer");
+  HLH_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bn_wait_timeouts), sizeof(unsigned)));
   return HLHGAT_OK;
 }

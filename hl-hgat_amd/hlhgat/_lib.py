@@ -81,6 +81,7 @@ SIGNATURES = {
     "hlhgat_bn_bwd_apply": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
+    "hlhgat_bn_wait_timeouts": (c_i32, [c_vp]),
     "hlhgat_edge_gather2": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_f32,
                                     c_f32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_att_score_fwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64,

@@ -500,9 +500,14 @@ int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy
                         int64_t C, const float* coef, float* dx, int64_t lddx, void* stream);
 
 /* BatchNorm forward statistics and normalisation in one launch
- * (k_bn_train_fused, grids of <= 256 workgroups) or as two; default 0
+ * (k_bn_train_fused, grids of <= 256 workgroups) or as two; default 1
  * (env HLHGAT_BN_ONE_LAUNCH).  Both give bitwise the same results. */
 int hlhgat_set_bn_one_launch(int on);
+
+/* Times a one-launch BatchNorm workgroup gave up waiting for its tile's
+ * statistics (bounded wait; never expected, results would be wrong): reads
+ * the device counter (synchronising). */
+int hlhgat_bn_wait_timeouts(unsigned* out);
 
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
                         const float* dy, int64_t lddy, int64_t n,

@@ -1206,7 +1206,11 @@ def test_bn_one_launch_bitwise(cuda, n, C, relu, pad):
             outs.append([y.detach(), x.grad, bn.weight.grad, bn.bias.grad, bn.running_mean,
                          bn.running_var])
     finally:
-        _lib.LIB.hlhgat_set_bn_one_launch(0)
+        _lib.LIB.hlhgat_set_bn_one_launch(1)
+    import ctypes
+    t = ctypes.c_uint(7)
+    _lib.check(_lib.LIB.hlhgat_bn_wait_timeouts(ctypes.addressof(t)), "bn_wait_timeouts")
+    assert t.value == 0
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     nv = n - pad
