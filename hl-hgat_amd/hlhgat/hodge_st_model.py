@@ -16,6 +16,13 @@ from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
 from .nn import BatchNorm, Sequential, run_sequential
 
+# HLHGAT_PREP_OVERLAP=1: build the incidence CSR on a second side stream
+# beside HL_init_conv instead of after it (same results).  OFF by default:
+# same-box A/B at the ZINC step 289.5k -> 285.3k graphs/s (a third stream's
+# sort kernels slow the two conv chains more than the overlap saves).
+import os as _os
+_PREP_OVERLAP = _os.environ.get("HLHGAT_PREP_OVERLAP", "0") == "1"
+
 __all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr",
            "HL_HGCNN_CIFAR10SP_dense_int3_attpool", "HL_HGCNN_pepfunc_dense_int3_attpool",
            "segment_ptr", "mean_pool_sorted"]
@@ -98,22 +105,36 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
             dt = ops.DenseConcat(x_t.size(0), width, x_t)
             ds = ops.DenseConcat(x_s.size(0), width, x_s)
             _sink(self.HL_init_conv, dt, ds, self.initial_channel)
-        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
-                                     edge_weight_s)
+        n_t, n_s = x_t.shape[0], x_s.shape[0]
+        valid_t = getattr(data, "valid_mask_t", None)
+
+        def boundary():
+            # the reference rebuilds par_1 and D for every block group (:623-624)
+            # from the same edge_index, so the values are identical: build them
+            # once.  reference: degree(edge_index.view(-1)) sized max(index)+1
+            # (:624); that equals N_t whenever it does not crash (1/D broadcast
+            # over x_t rows), so size it by N_t and skip the host sync of max()
+            p1 = adj2par1(data.edge_index, n_t, n_s)
+            d = degree(data.edge_index.view(-1), num_nodes=n_t)
+            if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
+                d = d.masked_fill(~valid_t, 1.0)
+            if not x_t.is_cuda:
+                return p1, d, []
+            inc = p1.incidence()  # built here, cached for every NodeEdgeInt
+            return p1, d, [inc.rowptr, inc.edge_ids, inc.edge_index]  # fork orders them on main
+
+        # the incidence build (sort + CSR of |B1|): after HL_init_conv, or beside
+        # it on a second side stream (_PREP_OVERLAP); NodeEdgeInt needs it first
+        side_in = [t for t in (data.edge_index, valid_t) if t is not None]
+        (x_t, x_s), (par_1, D, _) = ops.fork(
+            lambda: self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                      edge_weight_s),
+            boundary, side_inputs=side_in,
+            device=x_t.device if (x_t.is_cuda and _PREP_OVERLAP) else None, slot=1)
         if dense:
             dt.append(x_t)
             ds.append(x_s)
         x_s0, x_t0 = x_s, x_t
-        # the reference rebuilds par_1 and D for every block group (:623-624) from
-        # the same edge_index, so the values are identical: build them once.
-        # reference: degree(edge_index.view(-1)) sized max(index)+1 (:624); that
-        # equals N_t whenever it does not crash (1/D broadcast over x_t rows),
-        # so size it by N_t and skip the host sync of max()
-        par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
-        D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0])
-        valid_t = getattr(data, "valid_mask_t", None)
-        if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
-            D = D.masked_fill(~valid_t, 1.0)
         for i, _ in enumerate(self.channels):
             for j in range(self.channels[i]):
                 if dense:

@@ -94,12 +94,14 @@ def set_stream_fork(enabled: bool) -> None:
     _FORK_ENABLED = bool(enabled)
 
 
-def side_stream(device: torch.device) -> torch.cuda.Stream:
+def side_stream(device: torch.device, slot: int = 0) -> torch.cuda.Stream:
+    """Side stream `slot` of the device (0: the edge chains; 1: batch
+    preparation that overlaps the first conv)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _SIDE_STREAMS.get(idx)
+    s = _SIDE_STREAMS.get((idx, slot))
     if s is None:
         s = torch.cuda.Stream(device=idx)
-        _SIDE_STREAMS[idx] = s
+        _SIDE_STREAMS[(idx, slot)] = s
     return s
 
 
@@ -111,7 +113,7 @@ def _tensors(x):
             yield from _tensors(v)
 
 
-def fork(fn_main, fn_side, side_inputs=(), device=None):
+def fork(fn_main, fn_side, side_inputs=(), device=None, slot=0):
     """Run fn_main() on the current stream and fn_side() on the side stream
     concurrently; returns (fn_main(), fn_side()) with the side results ordered
     before anything issued next on the current stream.  Tensors in
@@ -120,7 +122,7 @@ def fork(fn_main, fn_side, side_inputs=(), device=None):
     if not _FORK_ENABLED or device is None or device.type != "cuda":
         return fn_main(), fn_side()
     main = torch.cuda.current_stream(device)
-    side = side_stream(device)
+    side = side_stream(device, slot)
     side.wait_stream(main)
     with torch.cuda.stream(side):
         for t in _tensors(side_inputs):
