@@ -70,6 +70,19 @@ bool& bn_one_launch_flag() {
 }
 bool bn_one_launch() { return bn_one_launch_flag(); }
 
+// HLHGAT_BN_ONE_LAUNCH_BWD=1: the BatchNorm backward reduction and dx in one
+// launch (k_bn_bwd_fused; bitwise the same results, checked by the GPU test
+// with it on).  OFF: same-box A/B at the ZINC step with both directions in
+// one launch 286.5k -> 283.8k graphs/s, i.e. the backward variant loses what
+// the forward one gains (its apply re-reads x, dy and y behind the wait).
+bool bn_one_launch_bwd() {
+  static bool v = [] {
+    const char* e = getenv("HLHGAT_BN_ONE_LAUNCH_BWD");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int64_t bn_parts(int64_t n) {
   static int64_t fixed = [] {
     const char* e = getenv("HLHGAT_BN_PARTS");
@@ -547,8 +560,27 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
   }
 }
 
-template <int V, int NT>
-__global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
+struct BwdApplyArgs {
+  const int32_t* nvalid;
+  const float* x;
+  int64_t ldx;
+  const float* y;
+  int64_t ldy;
+  const float* dy;
+  int64_t lddy;
+  float* dx;
+  int64_t lddx;
+  int64_t n;
+  int C;
+  const float* coef;
+  int tpr, rp;
+};
+
+// Backward statistics (and, APPLY, dx in the same launch: the tile's
+// finalising workgroup publishes the coefficients write-through and raises
+// the flag, as in bn_stats_body)
+template <int V, int NT, bool APPLY>
+__device__ __forceinline__ void bn_bwd_body(const StatsArgs& a, const BwdApplyArgs& p) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -599,8 +631,9 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
   write_partials<V, NT>(s0, s1, a, c0);
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  if (!tree_reduce<NT>(a, c0, tile_c, sum0, sum1)) return;
-  for (int t = threadIdx.x; t < tile_c; t += NT) {
+  const bool fin = tree_reduce<NT>(a, c0, tile_c, sum0, sum1);
+  if (!APPLY && !fin) return;
+  for (int t = threadIdx.x; fin && t < tile_c; t += NT) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
     const double sg = sum0[t], sgx = sum1[t];
@@ -613,27 +646,87 @@ __global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
     const double A = w * is;
     const double B = -w * is * is * is * sgx / nn;
     const double Cc = -w * is * sg / nn - B * (double)a.save_mean[cc];
-    a.coef[cc] = (float)A;
-    a.coef[a.C + cc] = (float)B;
-    a.coef[2 * a.C + cc] = (float)Cc;
+    if (APPLY) {
+      st_wt32(&a.coef[cc], (float)A);
+      st_wt32(&a.coef[a.C + cc], (float)B);
+      st_wt32(&a.coef[2 * a.C + cc], (float)Cc);
+    } else {
+      a.coef[cc] = (float)A;
+      a.coef[a.C + cc] = (float)B;
+      a.coef[2 * a.C + cc] = (float)Cc;
+    }
+  }
+  if (!APPLY) return;
+  unsigned* flag = a.count + kFlagBase + blockIdx.y;
+  unsigned* leave = flag + kMaxTiles;
+  if (fin) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (threadIdx.x == 0) {
+      unsigned it = 0;
+      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             ++it < (1u << 22))
+        __builtin_amdgcn_s_sleep(1);
+      if (it >= (1u << 22))
+        __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+  if (c < a.C) {
+    float A[V], B[V], Cc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      A[v] = ld_wt32(&a.coef[c + v]);
+      B[v] = ld_wt32(&a.coef[a.C + c + v]);
+      Cc[v] = ld_wt32(&a.coef[2 * a.C + c + v]);
+    }
+    int64_t r_end = r_lo + a.rows_per_part;
+    if (r_end > a.n) r_end = a.n;
+    for (int64_t r = r_lo + rg; r < r_end; r += a.rp) {
+      vt o;
+      if (r >= n_eff) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) vget(o, v) = 0.f;
+      } else {
+        vt xv = vload<V>(a.x + r * a.ldx + c);
+        vt gv = vload<V>(a.dy + r * a.lddy + c);
+        vt yv = gv;
+        if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          float g = vget(gv, v);
+          if (a.y && !(vget(yv, v) > 0.f)) g = 0.f;
+          vget(o, v) = A[v] * g + (B[v] * vget(xv, v) + Cc[v]);
+        }
+      }
+      vstore<V>(p.dx + r * p.lddx + c, o);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev =
+        __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
-struct BwdApplyArgs {
-  const int32_t* nvalid;
-  const float* x;
-  int64_t ldx;
-  const float* y;
-  int64_t ldy;
-  const float* dy;
-  int64_t lddy;
-  float* dx;
-  int64_t lddx;
-  int64_t n;
-  int C;
-  const float* coef;
-  int tpr, rp;
-};
+template <int V, int NT>
+__global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
+  bn_bwd_body<V, NT, false>(a, BwdApplyArgs{});
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_fused(StatsArgs a, BwdApplyArgs p) {
+  bn_bwd_body<V, kThreads, true>(a, p);
+}
+
 
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
@@ -887,6 +980,17 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   s.dbias = dbias;
   hipStream_t st = as_stream(stream);
   dim3 g1(Lr.parts, Lr.tiles);
+  if (bn_one_launch_bwd() && nt == kThreads && (int64_t)Lr.parts * Lr.tiles <= 256) {
+    // dx in the same launch (k_bn_bwd_fused; bitwise the same results)
+    BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, Lr.tpr,
+                   Lr.rp};
+    if (vec)
+      k_bn_bwd_fused<4><<<g1, kThreads, 0, st>>>(s, p);
+    else
+      k_bn_bwd_fused<1><<<g1, kThreads, 0, st>>>(s, p);
+    HLH_CHECK_LAUNCH();
+    return HLHGAT_OK;
+  }
   if (nt == 1024 && vec)
     k_bn_bwd_reduce<4, 1024><<<g1, 1024, 0, st>>>(s);
   else if (nt == 1024)
