@@ -1,7 +1,14 @@
 """HL-HGAT training throughput on MI355X (BASELINE.json metric, config 2).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--eager]
-    (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+
+N > 1: one rank per GPU over RCCL.  Under torch.distributed.run (RANK set)
+every rank runs the step directly; run plainly, `--gpus N` starts the N ranks
+itself (a child torch.distributed.run on 127.0.0.1, spawned before anything
+touches the GPU) and only waits for them.  Every rank checks that the world
+size equals --gpus; rank 0 prints the JSON line with n_gpus = world size.
+`--dry-run` runs the same launcher, rendezvous, barrier and max-over-ranks
+timing on gloo / CPU with a trivial step (the CPU test of the launcher).
 
 A step = one training step of HL_HGCNN_zinc_dense_int3_pyr(channels=[2,2,2],
 filters=[64,64,64], mlp=[256,256], K=3, keig=15) on a 1000-graph batch of
@@ -19,8 +26,9 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -235,6 +243,64 @@ def isolated_poly_step(device, batch, reps=20, chain=20):
                         "and L1, replayed 20x, events around the replays"}
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start n ranks of this script under torch.distributed.run (one process
+    per GPU, rendezvous on 127.0.0.1) and wait for them.  The parent makes no
+    GPU call (it never even initialises HIP), so the children own the
+    devices; rank 0's JSON line reaches our stdout through the inherited
+    file descriptors.  Returns the launcher's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    log(f"[launcher] starting {n} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args):
+    """The multi-rank contract without a GPU: gloo rendezvous, world-size
+    check, barrier + timed trivial steps (an all-reduce of a 2.6 MB gradient-
+    sized buffer, the size of cfg2's bucket) + max over ranks, one JSON line
+    from rank 0 with the bench's keys."""
+    from hlhgat.distributed import init_distributed, max_over_ranks
+    rank, world, device = init_distributed("gloo")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: world size {world} != --gpus {args.gpus}")
+    buf = torch.ones(650_000)
+    for _ in range(args.warmup):
+        if world > 1:
+            dist.all_reduce(buf)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            dist.all_reduce(buf)
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, device)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "graphs/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3),
+                          "dry_run": True, "backend": dist.get_backend() if world > 1 else None,
+                          "ranks_seen": world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+METRIC = "graphs/sec HL-HGAT fwd+bwd, ZINC-12k simplex graphs, 1/2/4/8 MI355X"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -247,10 +313,22 @@ def main():
                     help="skip the config-5 (TSP) SpMM roofline measurement")
     ap.add_argument("--prof-steps", type=int, default=3,
                     help="eager steps with kernel event stamps for the roofline")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / timing contract on gloo + CPU, no model")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # not under torchrun: start the N ranks ourselves, before any GPU call
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
 
     from hlhgat.distributed import init_distributed, max_over_ranks
     rank, world, device = init_distributed("nccl")  # RCCL over xGMI; one process per GPU
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: world size {world} != --gpus {args.gpus} "
+                         f"(launch with --nproc-per-node {args.gpus}, or without torchrun)")
 
     import hlhgat
     from hlhgat import ops
@@ -319,7 +397,7 @@ def main():
     }
     proj_tfs = proj["flops"] / (proj["ms"] * 1e-3) / 1e12 if proj["ms"] > 0 else 0.0
     result = {
-        "metric": "graphs/sec HL-HGAT fwd+bwd, ZINC-12k simplex graphs, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(value, 1), "unit": "graphs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",

@@ -181,3 +181,38 @@ def test_ddp_unused_parameters_flag_gives_the_mean_gradient():
     for r in range(world):
         assert res[r][0] == [[6.0] * 3] * 2
         assert res[r][1] is None
+
+
+def _bench(argv, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    env = dict(os.environ)
+    env.pop("RANK", None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + argv, env=env,
+                       capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_spawns_n_ranks(n):
+    """`python bench.py --gpus N` (no torchrun env) starts N ranks itself and
+    rank 0 reports n_gpus == N (gloo dry run of the same launcher)."""
+    r, line = _bench(["--gpus", str(n), "--dry-run", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert line is not None and line["n_gpus"] == n and line["ranks_seen"] == n
+    assert line["dry_run"] is True and line["steps"] == 2
+
+
+def test_bench_rank_count_mismatch_fails():
+    """Under torchrun with 2 ranks, --gpus 3 must fail instead of reporting
+    a wrong n_gpus."""
+    import subprocess
+    env = dict(os.environ)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "3", "--dry-run", "--steps", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert r.returncode != 0
+    assert "world size 2 != --gpus 3" in (r.stdout + r.stderr)
