@@ -362,6 +362,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, device)
+    ops.check_device_errors()  # a kernel that reported unusable results voids the run
 
     # roofline pass: eager steps, SpMM / projection launches event-stamped
     ops.prof_reset()

@@ -10,6 +10,8 @@
 //                      invstd and the running-stat update (deterministic: the
 //                      last arriver sums the partials in workgroup order);
 //        k_bn_apply  — y = relu?(x * s + t).
+//        (default: k_bn_train_fused, both in ONE launch when the grid is
+//        provably co-resident; see hlhgat_bn_fwd_train)
 //   bwd: k_bn_bwd_reduce — partials of sum(g) and sum(g*(x-mean)), g = dy *
 //                      [y > 0]; the last arriver forms dweight, dbias and the
 //                      per-channel coefficients of dx;
@@ -70,19 +72,6 @@ bool& bn_one_launch_flag() {
 }
 bool bn_one_launch() { return bn_one_launch_flag(); }
 
-// HLHGAT_BN_ONE_LAUNCH_BWD=1: the BatchNorm backward reduction and dx in one
-// launch (k_bn_bwd_fused; bitwise the same results, checked by the GPU test
-// with it on).  OFF: same-box A/B at the ZINC step with both directions in
-// one launch 286.5k -> 283.8k graphs/s, i.e. the backward variant loses what
-// the forward one gains (its apply re-reads x, dy and y behind the wait).
-bool bn_one_launch_bwd() {
-  static bool v = [] {
-    const char* e = getenv("HLHGAT_BN_ONE_LAUNCH_BWD");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 int64_t bn_parts(int64_t n) {
   static int64_t fixed = [] {
     const char* e = getenv("HLHGAT_BN_PARTS");
@@ -92,18 +81,6 @@ int64_t bn_parts(int64_t n) {
   // 128 -> 287.2k, 256 -> 286.1k, 32 -> 265.8k graphs/s), ~512 rows each above
   int64_t p = fixed > 0 ? fixed : std::max<int64_t>(128, ceil_div(n, (int64_t)512));
   return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
-}
-
-// Threads per workgroup of the two reduction passes (statistics, backward
-// reduce): same partition count, 4x the rows in flight per partition with
-// 1024.  HLHGAT_BN_RED_THREADS=256|1024 (A/B).
-int bn_red_threads() {
-  static int v = [] {
-    const char* e = getenv("HLHGAT_BN_RED_THREADS");
-    const int t = e ? atoi(e) : 256;
-    return t == 1024 ? 1024 : 256;
-  }();
-  return v;
 }
 
 BnLayout bn_layout(int64_t n, int64_t C, bool vec, int nt = kThreads) {
@@ -196,6 +173,9 @@ struct StatsArgs {
   float* coef;
   float* dweight;
   float* dbias;
+  // one-launch forward: poll limit of the statistics wait, host-visible error word
+  unsigned poll_limit;
+  unsigned* err;
 };
 
 // Partials are handed to the last-arriving workgroup WRITE-THROUGH: 8-byte
@@ -217,6 +197,39 @@ __device__ __forceinline__ double ld_wt(const double* p) {
 
 // wait timeouts of the one-launch BatchNorm (hlhgat_bn_wait_timeouts)
 __device__ unsigned g_bn_wait_timeouts = 0;
+
+// A waiting workgroup that gives up (poll limit reached) must not normalise
+// with stale statistics: it writes NaN into its rows, counts the timeout and
+// raises HLHGAT_DEVERR_BN_WAIT in the host-visible error word
+// (hlhgat_device_errors), which hlhgat.train.TrainStep, the bench and
+// hlhgat.ops.check_device_errors turn into a Python exception.
+__device__ __forceinline__ void report_wait_timeout(unsigned* err) {
+  __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (err) __hip_atomic_store(err, (unsigned)HLHGAT_DEVERR_BN_WAIT, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Bounded wait of a non-finalising workgroup for its tile's statistics flag;
+// poll_limit == 0 (test hook) gives up at once.  Returns false on timeout.
+__device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned poll_limit, unsigned* err) {
+  __shared__ unsigned s_ok;
+  if (threadIdx.x == 0) {
+    unsigned ok = 0;
+    if (poll_limit > 0) {
+      for (unsigned it = 0; it < poll_limit; ++it) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    if (!ok) report_wait_timeout(err);
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0u;
+}
 
 typedef __attribute__((address_space(1))) unsigned gu32_t;
 __device__ __forceinline__ void st_wt32(float* p, float v) {
@@ -451,26 +464,17 @@ __device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArg
     __syncthreads();
     if (threadIdx.x == 0)
       __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    if (threadIdx.x == 0) {
-      unsigned it = 0;
-      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-             ++it < (1u << 22))
-        __builtin_amdgcn_s_sleep(1);
-      if (it >= (1u << 22))  // never expected: counted so the host can check
-        __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
   }
+  // a timed-out workgroup poisons its rows (NaN) instead of applying stale statistics
+  const bool ok = fin || wait_flag(flag, a.poll_limit, a.err);
   if (c < a.C) {
     float sc[V], sh[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float w = p.weight ? p.weight[c + v] : 1.f;
       const float b = p.bias ? p.bias[c + v] : 0.f;
-      sc[v] = w * ld_wt32(&p.invstd[c + v]);
-      sh[v] = b - ld_wt32(&p.mean[c + v]) * sc[v];
+      sc[v] = ok ? w * ld_wt32(&p.invstd[c + v]) : __builtin_nanf("");
+      sh[v] = ok ? b - ld_wt32(&p.mean[c + v]) * sc[v] : __builtin_nanf("");
     }
     int64_t r_end = r_lo + a.rows_per_part;
     if (r_end > a.n) r_end = a.n;
@@ -479,7 +483,7 @@ __device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArg
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         float z = vget(xv, v) * sc[v] + sh[v];
-        vget(o, v) = r >= n_eff ? 0.f : ((p.relu && z < 0.f) ? 0.f : z);
+        vget(o, v) = r >= n_eff ? 0.f : ((p.relu && z < 0.f) ? 0.f : z);  // NaN passes
       }
       vstore<V>(p.y + r * p.ldy + c, o);
     };
@@ -576,11 +580,10 @@ struct BwdApplyArgs {
   int tpr, rp;
 };
 
-// Backward statistics (and, APPLY, dx in the same launch: the tile's
-// finalising workgroup publishes the coefficients write-through and raises
-// the flag, as in bn_stats_body)
-template <int V, int NT, bool APPLY>
-__device__ __forceinline__ void bn_bwd_body(const StatsArgs& a, const BwdApplyArgs& p) {
+// Backward statistics: partials of sum(g), sum(g (x - mean)); the finalising
+// workgroup of a column tile forms dweight, dbias and dx's coefficients.
+template <int V, int NT>
+__device__ __forceinline__ void bn_bwd_body(const StatsArgs& a) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -632,8 +635,8 @@ __device__ __forceinline__ void bn_bwd_body(const StatsArgs& a, const BwdApplyAr
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
   const bool fin = tree_reduce<NT>(a, c0, tile_c, sum0, sum1);
-  if (!APPLY && !fin) return;
-  for (int t = threadIdx.x; fin && t < tile_c; t += NT) {
+  if (!fin) return;
+  for (int t = threadIdx.x; t < tile_c; t += NT) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
     const double sg = sum0[t], sgx = sum1[t];
@@ -646,85 +649,14 @@ __device__ __forceinline__ void bn_bwd_body(const StatsArgs& a, const BwdApplyAr
     const double A = w * is;
     const double B = -w * is * is * is * sgx / nn;
     const double Cc = -w * is * sg / nn - B * (double)a.save_mean[cc];
-    if (APPLY) {
-      st_wt32(&a.coef[cc], (float)A);
-      st_wt32(&a.coef[a.C + cc], (float)B);
-      st_wt32(&a.coef[2 * a.C + cc], (float)Cc);
-    } else {
-      a.coef[cc] = (float)A;
-      a.coef[a.C + cc] = (float)B;
-      a.coef[2 * a.C + cc] = (float)Cc;
-    }
-  }
-  if (!APPLY) return;
-  unsigned* flag = a.count + kFlagBase + blockIdx.y;
-  unsigned* leave = flag + kMaxTiles;
-  if (fin) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    if (threadIdx.x == 0) {
-      unsigned it = 0;
-      while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
-             ++it < (1u << 22))
-        __builtin_amdgcn_s_sleep(1);
-      if (it >= (1u << 22))
-        __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-  }
-  if (c < a.C) {
-    float A[V], B[V], Cc[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      A[v] = ld_wt32(&a.coef[c + v]);
-      B[v] = ld_wt32(&a.coef[a.C + c + v]);
-      Cc[v] = ld_wt32(&a.coef[2 * a.C + c + v]);
-    }
-    int64_t r_end = r_lo + a.rows_per_part;
-    if (r_end > a.n) r_end = a.n;
-    for (int64_t r = r_lo + rg; r < r_end; r += a.rp) {
-      vt o;
-      if (r >= n_eff) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) vget(o, v) = 0.f;
-      } else {
-        vt xv = vload<V>(a.x + r * a.ldx + c);
-        vt gv = vload<V>(a.dy + r * a.lddy + c);
-        vt yv = gv;
-        if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          float g = vget(gv, v);
-          if (a.y && !(vget(yv, v) > 0.f)) g = 0.f;
-          vget(o, v) = A[v] * g + (B[v] * vget(xv, v) + Cc[v]);
-        }
-      }
-      vstore<V>(p.dx + r * p.lddx + c, o);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev =
-        __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    a.coef[cc] = (float)A;
+    a.coef[a.C + cc] = (float)B;
+    a.coef[2 * a.C + cc] = (float)Cc;
   }
 }
-
 template <int V, int NT>
 __global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
-  bn_bwd_body<V, NT, false>(a, BwdApplyArgs{});
-}
-
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_bwd_fused(StatsArgs a, BwdApplyArgs p) {
-  bn_bwd_body<V, kThreads, true>(a, p);
+  bn_bwd_body<V, NT>(a);
 }
 
 
@@ -785,6 +717,53 @@ unsigned apply_grid_x(int64_t n, int rp) {
   return (unsigned)g;
 }
 
+StatsArgs stats_args(const BnLayout& L, const BnWs& w, const float* x, int64_t ldx, int64_t n,
+                     const int32_t* n_valid, int64_t C) {
+  StatsArgs s{};
+  s.nvalid = n_valid;
+  s.x = x;
+  s.ldx = ldx;
+  s.n = n;
+  s.C = (int)C;
+  s.tpr = L.tpr;
+  s.rp = L.rp;
+  s.tiles = L.tiles;
+  s.parts = L.parts;
+  s.rows_per_part = L.rows_per_part;
+  s.part = w.part;
+  s.gpart = w.gpart;
+  s.count = w.count;
+  return s;
+}
+
+// --- one-launch forward: co-residency and the poll limit -------------------
+// k_bn_train_fused's waiting workgroups need their tile's finalising
+// workgroup to be resident at the same time.  The launch is used only when
+// the whole grid fits in a QUARTER of the chip's resident-workgroup capacity
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs), so the node / edge /
+// interaction streams each running one such launch still leave room; and it
+// is capped at 256 workgroups.  Anything that still stalls a wait is caught
+// by the bounded poll (NaN rows + HLHGAT_DEVERR_BN_WAIT, never stale numbers).
+unsigned g_poll_limit = 1u << 22;
+
+int64_t fused_capacity(bool vec) {
+  static int64_t cap[2] = {-1, -1};
+  int64_t& c = cap[vec ? 1 : 0];
+  if (c >= 0) return c;
+  int dev = 0, cus = 0, occ = 0;
+  c = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return c;
+  hipError_t e = vec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           &occ, reinterpret_cast<const void*>(&k_bn_train_fused<4>), kThreads, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                           &occ, reinterpret_cast<const void*>(&k_bn_train_fused<1>), kThreads, 0);
+  if (e != hipSuccess) return c;
+  c = (int64_t)occ * cus / 4;
+  return c;
+}
+
 }  // namespace
 
 extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
@@ -806,24 +785,9 @@ extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
   HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
                 "bn_stats_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx}, {x});
-  const int nt = bn_red_threads();
-  BnLayout L = bn_layout(n, C, vec, nt);
+  BnLayout L = bn_layout(n, C, vec);
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_stats_train: C too large");
-  BnWs w = carve(workspace, n, C);
-  StatsArgs s{};
-  s.nvalid = n_valid;
-  s.x = x;
-  s.ldx = ldx;
-  s.n = n;
-  s.C = (int)C;
-  s.tpr = L.tpr;
-  s.rp = L.rp;
-  s.tiles = L.tiles;
-  s.parts = L.parts;
-  s.rows_per_part = L.rows_per_part;
-  s.part = w.part;
-  s.gpart = w.gpart;
-  s.count = w.count;
+  StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
   s.running_mean = running_mean;
   s.running_var = running_var;
   s.nbt = num_batches_tracked;
@@ -833,11 +797,7 @@ extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
   s.save_invstd = save_invstd;
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
-  if (nt == 1024 && vec)
-    k_bn_stats<4, 1024><<<g1, 1024, 0, st>>>(s);
-  else if (nt == 1024)
-    k_bn_stats<1, 1024><<<g1, 1024, 0, st>>>(s);
-  else if (vec)
+  if (vec)
     k_bn_stats<4, kThreads><<<g1, kThreads, 0, st>>>(s);
   else
     k_bn_stats<1, kThreads><<<g1, kThreads, 0, st>>>(s);
@@ -880,11 +840,9 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
                 "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
   HLH_CHECK_ARG(y, "bn_fwd_train: NULL pointer");
   const bool vec = bn_vec_ok(C, {ldx}, {x});
-  // one launch only for grids of <= 256 workgroups: with the node / edge /
-  // interaction streams each running one, every waiting workgroup's tile
-  // peers still find a free slot (>= 6 such workgroups fit per CU)
-  const BnLayout L1 = bn_layout(n, C, vec, kThreads);
-  if (bn_one_launch() && bn_red_threads() == kThreads && (int64_t)L1.parts * L1.tiles <= 256 &&
+  const BnLayout L = bn_layout(n, C, vec);
+  const int64_t grid = (int64_t)L.parts * L.tiles;
+  if (bn_one_launch() && grid <= 256 && grid <= fused_capacity(vec) &&
       vec == bn_vec_ok(C, {ldx, ldy}, {x, y})) {
     // statistics and normalisation in one launch (k_bn_train_fused)
     HLH_CHECK_ARG(x && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
@@ -892,23 +850,8 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
                   "bn_fwd_train: running_mean/var must both be given or both NULL");
     HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
                   "bn_fwd_train: workspace too small");
-    BnLayout L = bn_layout(n, C, vec, kThreads);
     HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_fwd_train: C too large");
-    BnWs w = carve(workspace, n, C);
-    StatsArgs s{};
-    s.nvalid = n_valid;
-    s.x = x;
-    s.ldx = ldx;
-    s.n = n;
-    s.C = (int)C;
-    s.tpr = L.tpr;
-    s.rp = L.rp;
-    s.tiles = L.tiles;
-    s.parts = L.parts;
-    s.rows_per_part = L.rows_per_part;
-    s.part = w.part;
-    s.gpart = w.gpart;
-    s.count = w.count;
+    StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
     s.running_mean = running_mean;
     s.running_var = running_var;
     s.nbt = num_batches_tracked;
@@ -916,6 +859,9 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
     s.eps = eps;
     s.save_mean = save_mean;
     s.save_invstd = save_invstd;
+    s.poll_limit = g_poll_limit;
+    s.err = hlhgat::device_error_word();
+    HLH_CHECK_ARG(s.err, "bn_fwd_train: no device error word (%s)", hlhgat_last_error());
     ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias,
                 relu, L.tpr, L.rp};
     hipStream_t st = as_stream(stream);
@@ -950,28 +896,13 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
                 "bn_bwd_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
   BnLayout L = bn_layout(n, C, vec);
-  const int nt = bn_red_threads();
-  const BnLayout Lr = bn_layout(n, C, vec, nt);
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_train: C too large");
   BnWs w = carve(workspace, n, C);
-  StatsArgs s{};
-  s.nvalid = n_valid;
-  s.x = x;
-  s.ldx = ldx;
+  StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
   s.y = y;
   s.ldy = ldy;
   s.dy = dy;
   s.lddy = lddy;
-  s.n = n;
-  s.C = (int)C;
-  s.tpr = Lr.tpr;
-  s.rp = Lr.rp;
-  s.tiles = Lr.tiles;
-  s.parts = Lr.parts;
-  s.rows_per_part = Lr.rows_per_part;
-  s.part = w.part;
-  s.gpart = w.gpart;
-  s.count = w.count;
   s.weight = weight;
   s.save_mean = const_cast<float*>(save_mean);
   s.save_invstd = const_cast<float*>(save_invstd);
@@ -979,23 +910,8 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   s.dweight = dweight;
   s.dbias = dbias;
   hipStream_t st = as_stream(stream);
-  dim3 g1(Lr.parts, Lr.tiles);
-  if (bn_one_launch_bwd() && nt == kThreads && (int64_t)Lr.parts * Lr.tiles <= 256) {
-    // dx in the same launch (k_bn_bwd_fused; bitwise the same results)
-    BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, Lr.tpr,
-                   Lr.rp};
-    if (vec)
-      k_bn_bwd_fused<4><<<g1, kThreads, 0, st>>>(s, p);
-    else
-      k_bn_bwd_fused<1><<<g1, kThreads, 0, st>>>(s, p);
-    HLH_CHECK_LAUNCH();
-    return HLHGAT_OK;
-  }
-  if (nt == 1024 && vec)
-    k_bn_bwd_reduce<4, 1024><<<g1, 1024, 0, st>>>(s);
-  else if (nt == 1024)
-    k_bn_bwd_reduce<1, 1024><<<g1, 1024, 0, st>>>(s);
-  else if (vec)
+  dim3 g1(L.parts, L.tiles);
+  if (vec)
     k_bn_bwd_reduce<4, kThreads><<<g1, kThreads, 0, st>>>(s);
   else
     k_bn_bwd_reduce<1, kThreads><<<g1, kThreads, 0, st>>>(s);
@@ -1010,85 +926,15 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   return HLHGAT_OK;
 }
 
-// The two halves of hlhgat_bn_bwd_train, for a consumer that applies the
-// backward coefficients itself (hlhgat_proj_bwd_bn folds dx = A g + (B x + C)
-// into the projection gradient's operand loads).
-extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                                    const float* dy, int64_t lddy, int64_t n,
-                                    const int32_t* n_valid, int64_t C, const float* weight,
-                                    const float* save_mean, const float* save_invstd,
-                                    float* coef, float* dweight, float* dbias, void* workspace,
-                                    int64_t workspace_bytes, void* stream) {
-  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && (!y || ldy >= C),
-                "bn_bwd_reduce: bad sizes");
-  HLH_CHECK_ARG(x && dy && coef && save_mean && save_invstd, "bn_bwd_reduce: NULL pointer");
-  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
-                "bn_bwd_reduce: workspace too small");
-  const bool vec = bn_vec_ok(C, {ldx, lddy, y ? ldy : 4}, {x, y, dy});
-  const int nt = bn_red_threads();
-  const BnLayout Lr = bn_layout(n, C, vec, nt);
-  HLH_CHECK_ARG(Lr.tiles <= kMaxTiles, "bn_bwd_reduce: C too large");
-  BnWs w = carve(workspace, n, C);
-  StatsArgs s{};
-  s.nvalid = n_valid;
-  s.x = x;
-  s.ldx = ldx;
-  s.y = y;
-  s.ldy = ldy;
-  s.dy = dy;
-  s.lddy = lddy;
-  s.n = n;
-  s.C = (int)C;
-  s.tpr = Lr.tpr;
-  s.rp = Lr.rp;
-  s.tiles = Lr.tiles;
-  s.parts = Lr.parts;
-  s.rows_per_part = Lr.rows_per_part;
-  s.part = w.part;
-  s.gpart = w.gpart;
-  s.count = w.count;
-  s.weight = weight;
-  s.save_mean = const_cast<float*>(save_mean);
-  s.save_invstd = const_cast<float*>(save_invstd);
-  s.coef = coef;
-  s.dweight = dweight;
-  s.dbias = dbias;
-  hipStream_t st = as_stream(stream);
-  dim3 g1(Lr.parts, Lr.tiles);
-  if (nt == 1024 && vec)
-    k_bn_bwd_reduce<4, 1024><<<g1, 1024, 0, st>>>(s);
-  else if (nt == 1024)
-    k_bn_bwd_reduce<1, 1024><<<g1, 1024, 0, st>>>(s);
-  else if (vec)
-    k_bn_bwd_reduce<4, kThreads><<<g1, kThreads, 0, st>>>(s);
-  else
-    k_bn_bwd_reduce<1, kThreads><<<g1, kThreads, 0, st>>>(s);
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                                   const float* dy, int64_t lddy, int64_t n,
-                                   const int32_t* n_valid, int64_t C, const float* coef,
-                                   float* dx, int64_t lddx, void* stream) {
-  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && lddx >= C && (!y || ldy >= C),
-                "bn_bwd_apply: bad sizes");
-  HLH_CHECK_ARG(x && dy && dx && coef, "bn_bwd_apply: NULL pointer");
-  const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
-  BnLayout L = bn_layout(n, C, vec);
-  BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, coef, L.tpr, L.rp};
-  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
-  hipStream_t st = as_stream(stream);
-  if (vec)
-    k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);
-  else
-    k_bn_bwd_apply<1><<<g2, kThreads, 0, st>>>(p);
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
-
 extern "C" int hlhgat_set_bn_one_launch(int on) {
   bn_one_launch_flag() = on != 0;
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_get_bn_one_launch(void) { return bn_one_launch_flag() ? 1 : 0; }
+
+extern "C" int hlhgat_set_bn_poll_limit(unsigned limit) {
+  g_poll_limit = limit;
   return HLHGAT_OK;
 }
 

@@ -18,6 +18,10 @@ namespace hlhgat {
 
 void set_error(const char* fmt, ...);
 
+// The host-visible device error word (hlhgat_device_errors), allocated on
+// first use; NULL (with the error set) if the pinned allocation fails.
+unsigned* device_error_word();
+
 #define HLH_CHECK_ARG(cond, ...)                     \
   do {                                               \
     if (!(cond)) {                                   \

@@ -548,150 +548,6 @@ __global__ __launch_bounds__(256) void k_basis_local_fwd(LocalArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Graph-local fused conv forward (F = d_out = 64, ZINC-scale tiles):
-//   out = sum_k T_k W_k^T + bias, T_0 = X, T_1.. the Laguerre / Chebyshev
-//   basis (lib/Hodge_Cheb_Conv.py:480-515 / :394-439)
-// ONE launch per conv instead of K-1 basis launches + the projection GEMM: a
-// workgroup stages its tile of whole graphs (X rows and CSR slice) in LDS,
-// projects T_0, then computes each T_{k+1} in LDS (written to the T slab for
-// the backward) and projects it while it is resident.  The projection is the
-// k_proj_fwd_lds arithmetic exactly (v_mfma_f32_16x16x4_f32, lane (q, i)
-// supplying k = 16 s + 4 q + j, blocks in k order, bias in the epilogue) and
-// the basis is k_basis_local_fwd's, so the results are bitwise those of the
-// unfused launches (tests/test_gpu_parity.py).
-// ---------------------------------------------------------------------------
-typedef float cl_floatx4 __attribute__((ext_vector_type(4)));
-constexpr int CL_F = 64;       // features in and out
-constexpr int CL_P = CL_F + 4;  // LDS row pitch (floats)
-
-struct ConvLocalArgs {
-  LocalArgs b;
-  const float* W[LOC_MAXK];
-  int64_t ldw[LOC_MAXK];
-  const float* bias;
-  float* C;
-  int64_t ldc;
-};
-
-__global__ __launch_bounds__(256) void k_conv_local_fwd(ConvLocalArgs ca) {
-  const LocalArgs& a = ca.b;
-  extern __shared__ float lds[];
-  float* bufA = lds;
-  float* bufB = lds + a.max_rows * CL_P;
-  float* wl = bufB + a.max_rows * CL_P;  // [64][CL_P] weight block, then epilogue scratch
-  const int t = (int)xcd_slot(blockIdx.x, gridDim.x);
-  const LocalTile T = stage_tile(a, reinterpret_cast<char*>(wl + 64 * CL_P), t);
-  const int r0 = T.r0, nr = T.nr;
-  const int64_t blk = a.n * a.F;
-  // basis lanes: 16 per row (float4), 16 row groups
-  const int sub = threadIdx.x % 16, grp = threadIdx.x / 16;
-  const int f = sub * 4;
-  for (int r = grp; r < nr; r += 16)
-    *reinterpret_cast<float4*>(bufA + r * CL_P + f) = vload<4>(a.X + (r0 + r) * a.ldx + f);
-  // projection lanes: wave w owns tile rows 16 w .. 16 w + 15
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, i = lane & 15;
-  const int m = wave * 16 + i;
-  cl_floatx4 acc[4];
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn) acc[tn] = cl_floatx4{0.f, 0.f, 0.f, 0.f};
-  auto project = [&](const float* S, int b) {
-    const float* W = ca.W[b];
-    const int64_t ldw = ca.ldw[b];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {  // W_b [64 out][64 in] -> LDS
-      const int idx = threadIdx.x + 256 * u;
-      const int rr = idx >> 4, c4 = idx & 15;
-      *reinterpret_cast<float4*>(&wl[rr * CL_P + 4 * c4]) =
-          *reinterpret_cast<const float4*>(W + (int64_t)rr * ldw + 4 * c4);
-    }
-    __syncthreads();  // W block and S rows visible
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < nr) av = *reinterpret_cast<const float4*>(S + m * CL_P + 16 * s4 + 4 * q);
-      float4 bv[4];
-#pragma unroll
-      for (int tn = 0; tn < 4; ++tn)
-        bv[tn] = *reinterpret_cast<const float4*>(&wl[(tn * 16 + i) * CL_P + 16 * s4 + 4 * q]);
-#pragma unroll
-      for (int tn = 0; tn < 4; ++tn) {
-        acc[tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv[tn].x, acc[tn], 0, 0, 0);
-        acc[tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv[tn].y, acc[tn], 0, 0, 0);
-        acc[tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv[tn].z, acc[tn], 0, 0, 0);
-        acc[tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv[tn].w, acc[tn], 0, 0, 0);
-      }
-    }
-    __syncthreads();  // wl free again
-  };
-  project(bufA, 0);  // (its first barrier also publishes X and the tile CSR)
-  float* prev = bufA;
-  float* cur = bufA;
-  float* nxt = bufB;
-  for (int k = 0; k + 1 < a.K; ++k) {
-    for (int r = grp; r < nr; r += 16) {  // T_{k+1}, as k_basis_local_fwd
-      float4 acc4 = local_gather<4>(T, r, cur, CL_P, f);
-      float4 o;
-      o.x = a.alpha[k] * (1.f * acc4.x);
-      o.y = a.alpha[k] * (1.f * acc4.y);
-      o.z = a.alpha[k] * (1.f * acc4.z);
-      o.w = a.alpha[k] * (1.f * acc4.w);
-      if (a.beta[k] != 0.f) {
-        const float4 xr = *reinterpret_cast<const float4*>(cur + r * CL_P + f);
-        o.x = o.x + a.beta[k] * xr.x;
-        o.y = o.y + a.beta[k] * xr.y;
-        o.z = o.z + a.beta[k] * xr.z;
-        o.w = o.w + a.beta[k] * xr.w;
-      }
-      if (a.hasz[k]) {
-        const float4 z = *reinterpret_cast<const float4*>(prev + r * CL_P + f);
-        o.x = o.x + a.gamma[k] * z.x;
-        o.y = o.y + a.gamma[k] * z.y;
-        o.z = o.z + a.gamma[k] * z.z;
-        o.w = o.w + a.gamma[k] * z.w;
-      }
-      if (a.div[k] != 1.f) {
-        o.x = o.x / a.div[k];
-        o.y = o.y / a.div[k];
-        o.z = o.z / a.div[k];
-        o.w = o.w / a.div[k];
-      }
-      *reinterpret_cast<float4*>(nxt + r * CL_P + f) = o;
-      vstore<4>(a.out + (int64_t)k * blk + (r0 + r) * a.F + f, o);
-    }
-    project(nxt, k + 1);
-    float* old_cur = cur;
-    cur = nxt;
-    prev = old_cur;
-    nxt = old_cur;
-  }
-  // epilogue (k_proj_fwd_lds's store_tile_rows): + bias, rows through LDS
-  float* scratch = wl + wave * 16 * CL_P;
-#pragma unroll
-  for (int tn = 0; tn < 4; ++tn) {
-    const int col = tn * 16 + i;
-    const float bv = ca.bias ? ca.bias[col] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = acc[tn][r];
-      if (ca.bias) v = v + bv;
-      scratch[(4 * q + r) * CL_P + col] = v;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int idx = lane + 64 * u;
-    const int r = idx >> 4, c4 = idx & 15;
-    const int row = wave * 16 + r;
-    if (row < nr)
-      *reinterpret_cast<float4*>(ca.C + (int64_t)(r0 + row) * ca.ldc + 4 * c4) =
-          *reinterpret_cast<const float4*>(&scratch[r * CL_P + 4 * c4]);
-  }
-}
-
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_basis_local_bwd(LocalArgs a) {
   using vt = typename VecT<V>::type;
@@ -1545,90 +1401,3 @@ extern "C" int hlhgat_segment_mean_bwd(const int32_t* seg_ptr,
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
-
-extern "C" int hlhgat_conv_local_fwd(int kind, const int32_t* rowptr, const int32_t* col,
-                                     const float* val, int64_t n, int64_t nnz,
-                                     const int32_t* tile_ptr, int64_t n_tiles,
-                                     int64_t max_tile_rows, int64_t max_tile_nnz, const float* X,
-                                     int64_t ldx, int64_t F, int K, float* T,
-                                     const float* const* W, const int64_t* ldw, const float* bias,
-                                     int64_t d_out, float* C, int64_t ldc, void* stream) {
-  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
-                "conv_local_fwd: kind %d not supported", kind);
-  HLH_CHECK_ARG(F == CL_F && d_out == CL_F && K >= 2 && K <= LOC_MAXK,
-                "conv_local_fwd: needs F = d_out = %d and 2 <= K <= %d", CL_F, LOC_MAXK);
-  HLH_CHECK_ARG(tile_ptr && n_tiles > 0 && max_tile_rows >= 1 && max_tile_rows <= 64 &&
-                    max_tile_nnz >= 1,
-                "conv_local_fwd: needs graph tiles of <= 64 rows");
-  HLH_CHECK_ARG(X && T && C && W && ldw && ldx % 4 == 0 && ldc % 4 == 0 &&
-                    (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
-                    (reinterpret_cast<uintptr_t>(C) & 15) == 0,
-                "conv_local_fwd: operands must be 16-B aligned with ld % 4 == 0");
-  for (int k = 0; k < K; ++k)
-    HLH_CHECK_ARG(W[k] && ldw[k] >= F && ldw[k] % 4 == 0 &&
-                      (reinterpret_cast<uintptr_t>(W[k]) & 15) == 0,
-                  "conv_local_fwd: weight %d must be 16-B aligned [64][>=64]", k);
-  if (n == 0) return HLHGAT_OK;
-  const int64_t shmem = (2 * max_tile_rows + 64) * (int64_t)CL_P * 4 + 4 * (max_tile_rows + 1) +
-                        8 * max_tile_nnz;
-  HLH_CHECK_ARG(shmem <= 160 * 1024, "conv_local_fwd: tile bounds exceed LDS");
-  ConvLocalArgs ca{};
-  LocalArgs& a = ca.b;
-  a.rowptr = rowptr;
-  a.col = col;
-  a.val = val;
-  a.tile_ptr = tile_ptr;
-  a.max_rows = (int)max_tile_rows;
-  a.max_nnz = (int)max_tile_nnz;
-  a.pitch = CL_P;
-  a.F = (int)F;
-  a.K = K;
-  a.X = X;
-  a.ldx = ldx;
-  a.out = T;
-  a.n = n;
-  for (int k = 0; k < LOC_MAXK; ++k) {
-    a.alpha[k] = 1.f;
-    a.beta[k] = 0.f;
-    a.gamma[k] = 0.f;
-    a.div[k] = 1.f;
-    a.q[k] = 0.f;
-    a.hasz[k] = 0;
-    a.hasq[k] = 0;
-  }
-  const bool lag = kind == HLHGAT_POLY_LAGUERRE;
-  if (lag) {  // same coefficients as hlhgat_poly_basis_fwd's steps
-    a.alpha[0] = -1.f;
-    a.beta[0] = 1.f;
-  }
-  for (int k = 1; k + 1 < K; ++k) {
-    a.hasz[k] = 1;
-    if (lag) {
-      a.alpha[k] = -1.f;
-      a.beta[k] = (float)(2 * k + 1);
-      a.gamma[k] = -(float)k;
-      a.div[k] = (float)(k + 1);
-    } else {
-      a.alpha[k] = 2.f;
-      a.gamma[k] = -1.f;
-    }
-  }
-  for (int k = 0; k < K; ++k) {
-    ca.W[k] = W[k];
-    ca.ldw[k] = ldw[k];
-  }
-  ca.bias = bias;
-  ca.C = C;
-  ca.ldc = ldc;
-  hipStream_t s = as_stream(stream);
-  // flops of the projection + algorithmic bytes of the fused conv (CSR, X in,
-  // T_1.. and C out, the weights)
-  ProfScope prof(HLHGAT_PROF_POLY, s,
-                 8.0 * (double)nnz + 4.0 * (double)(n + 1) + 4.0 * (double)n * F * (K + 1) +
-                     4.0 * (double)K * F * d_out,
-                 2.0 * (double)nnz * F * (K - 1));
-  launch(k_conv_local_fwd, dim3((unsigned)n_tiles), dim3(256), (uint32_t)shmem, s, &prof, ca);
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
-

@@ -67,19 +67,6 @@ struct FwdArgs {
   float* C;
   int64_t ldc;
   int accumulate;
-  // BatchNorm statistics of C in the epilogue (hlhgat_proj_fwd_bn; stats == 0: off)
-  int stats;
-  const int32_t* nvalid;  // rows >= *nvalid are padding (NULL: all M)
-  unsigned* count;        // [kStatTiles][1 + kStatGroups] arrival counters (zero between launches)
-  double* part;           // [gridDim.x][N][2] per-row-tile partials
-  double* gpart;          // [ng][N][2] group partials
-  int gs, ng;             // row tiles per group, groups
-  float* save_mean;
-  float* save_invstd;
-  float* running_mean;
-  float* running_var;
-  int64_t* nbt;
-  float momentum, eps;
 };
 
 template <int TM, int TN, bool VEC>
@@ -282,119 +269,7 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[TN], float*
   }
 }
 
-// ---- BatchNorm statistics in the projection epilogue (hlhgat_proj_fwd_bn) ----
-constexpr int kStatTiles = 256;   // column tiles (N <= 256 * 16)
-constexpr int kStatGroups = 128;  // row-tile groups of the first tree level
-
-// Partials are handed over WRITE-THROUGH (8-byte agent-scope atomic stores =
-// global_store_dwordx2 sc1, drained by every storing wave; read back with sc1
-// loads): no release fence, whose buffer_wbl2 would write back the XCD L2's
-// dirty lines -- this workgroup's freshly stored C tile among them -- and no
-// acquire fence (cdna_hip_programming.md Guideline 16 R1), as in bn.hip.
-typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-__device__ __forceinline__ void st_wt(double* p, double v) {
-  __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_wt(const double* p) {
-  return __longlong_as_double(
-      (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Count this workgroup in; true in the last workgroup to arrive (which resets
-// the counter for the next launch).
-__device__ __forceinline__ bool stat_arrive_last(unsigned* counter, unsigned total) {
-  __shared__ unsigned s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev =
-        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == total - 1) ? 1u : 0u;
-    if (s_last) *counter = 0u;
-  }
-  __syncthreads();
-  return s_last != 0u;
-}
-
-// Column partials (sum, sum of squares; fp64) of this workgroup's valid rows,
-// from the 4 waves' LDS scratch tiles (the stored C values, bias included),
-// then the two-level tree; the last workgroup of the column tile finalises
-// mean / invstd / running statistics exactly as k_bn_stats does.
 template <int TN>
-__device__ void proj_bn_stats(const FwdArgs& a, const float* wl0, int n_base, int ncols) {
-  constexpr int CT = TN * 16, P = CT + 4;
-  __shared__ double sred[4][CT][2];
-  __shared__ double sfin[CT][2];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int64_t n_eff = a.M;
-  if (a.nvalid) {
-    const int64_t nv = (int64_t)*a.nvalid;
-    if (nv < n_eff) n_eff = nv;
-  }
-  if (lane < CT) {
-    const float* scr = wl0 + wave * 16 * P;
-    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * 16;
-    double s0 = 0.0, s1 = 0.0;
-    for (int r = 0; r < 16; ++r) {
-      if (row0 + r >= n_eff) break;
-      const double v = (double)scr[r * P + lane];
-      s0 += v;
-      s1 += v * v;
-    }
-    sred[wave][lane][0] = s0;
-    sred[wave][lane][1] = s1;
-  }
-  __syncthreads();
-  const int pt = (int)blockIdx.x;
-  const int g = pt / a.gs;
-  if (threadIdx.x < 2 * CT) {
-    const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
-    const double v = ((sred[0][c][m] + sred[1][c][m]) + sred[2][c][m]) + sred[3][c][m];
-    if (c < ncols) st_wt(&a.part[((int64_t)pt * a.N + n_base + c) * 2 + m], v);
-  }
-  const int tile = (int)blockIdx.y;
-  const int first = g * a.gs;
-  const int cnt = (int)gridDim.x - first < a.gs ? (int)gridDim.x - first : a.gs;
-  if (!stat_arrive_last(a.count + kStatTiles + tile * kStatGroups + g, (unsigned)cnt)) return;
-  double gsum = 0.0;
-  if (threadIdx.x < 2 * CT) {
-    const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
-    if (c < ncols)
-      for (int p = first; p < first + cnt; ++p)
-        gsum += ld_wt(&a.part[((int64_t)p * a.N + n_base + c) * 2 + m]);
-    if (a.ng > 1 && c < ncols) st_wt(&a.gpart[((int64_t)g * a.N + n_base + c) * 2 + m], gsum);
-  }
-  if (a.ng > 1) {
-    if (!stat_arrive_last(a.count + tile, (unsigned)a.ng)) return;
-    if (threadIdx.x < 2 * CT) {
-      const int c = threadIdx.x >> 1, m = threadIdx.x & 1;
-      gsum = 0.0;
-      if (c < ncols)
-        for (int q = 0; q < a.ng; ++q) gsum += ld_wt(&a.gpart[((int64_t)q * a.N + n_base + c) * 2 + m]);
-    }
-  }
-  if (threadIdx.x < 2 * CT) sfin[threadIdx.x >> 1][threadIdx.x & 1] = gsum;
-  __syncthreads();
-  if (threadIdx.x < ncols) {
-    const int cc = n_base + threadIdx.x;
-    const double u0 = sfin[threadIdx.x][0], u1 = sfin[threadIdx.x][1];
-    const double nn = (double)(n_eff > 0 ? n_eff : 1);
-    const double mean = u0 / nn;
-    double var = u1 / nn - mean * mean;
-    if (var < 0.0) var = 0.0;
-    a.save_mean[cc] = (float)mean;
-    a.save_invstd[cc] = (float)(1.0 / sqrt(var + (double)a.eps));
-    if (a.running_mean) {
-      const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
-      a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
-      a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
-    }
-  }
-  if (a.nbt && tile == 0 && threadIdx.x == 0) a.nbt[0] += 1;
-}
-
-template <int TN, bool STATS = false>
 __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
   __shared__ float wl[2][TN * 16][KCP];
   const int wave = threadIdx.x >> 6;
@@ -461,53 +336,12 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
                       (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
   store_tile_rows<TN>(acc, scratch, m_base, a.M, a.C + n_base, a.ldc, ncols,
                       a.bias ? a.bias + n_base : nullptr, a.accumulate, vec_ok);
-  if constexpr (STATS) proj_bn_stats<TN>(a, &wl[0][0][0], n_base, ncols);
 }
 
 // ---------------------------------------------------------------------------
 // data gradient: dA_b = dC W_b   (reduction over N)
 // ---------------------------------------------------------------------------
-// BatchNorm backward folded into the projection gradient's dC operand:
-// dC[m][c] = A_c g' + (B_c x[m][c] + C_c), g' = g masked by y > 0 (ReLU), rows
-// m >= n_valid zero -- k_bn_bwd_apply's expression (bn.hip), evaluated on load.
-struct BnT {
-  const float* x;
-  int64_t ldx;
-  const float* y;  // NULL: no ReLU mask
-  int64_t ldy;
-  const float* coef;  // [3][C]
-  const int32_t* nvalid;
-  int C;
-};
-
-__device__ __forceinline__ int64_t bn_rows(int64_t n, const int32_t* nvalid) {
-  if (!nvalid) return n;
-  const int64_t v = (int64_t)*nvalid;
-  return v < n ? (v < 0 ? 0 : v) : n;
-}
-
-// dC[m][c .. c+3] from the upstream gradient row g (= dy + m * lddy)
-__device__ __forceinline__ float4 bn_dz4(const BnT& t, const float* g, int64_t m, int c) {
-  const float4 gv = *reinterpret_cast<const float4*>(g + c);
-  const float4 xv = *reinterpret_cast<const float4*>(t.x + m * t.ldx + c);
-  float gg[4] = {gv.x, gv.y, gv.z, gv.w};
-  const float xx[4] = {xv.x, xv.y, xv.z, xv.w};
-  if (t.y) {
-    const float4 yv = *reinterpret_cast<const float4*>(t.y + m * t.ldy + c);
-    const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-      if (!(yy[v] > 0.f)) gg[v] = 0.f;
-  }
-  float o[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v)
-    o[v] = t.coef[c + v] * gg[v] + (t.coef[t.C + c + v] * xx[v] + t.coef[2 * t.C + c + v]);
-  return make_float4(o[0], o[1], o[2], o[3]);
-}
-
 struct BwdDataArgs {
-  BnT bn;
   int nb;
   int N;
   int64_t M;
@@ -598,7 +432,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
 // TRANSPOSED (wl[c][n], rows padded) so each lane's B fragment (4 consecutive
 // n of one column) is one ds_read_b128; dC rows stream into registers one
 // 64-wide n chunk ahead.
-template <int TN, bool BN = false>
+template <int TN>
 __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, int by,
                                                   float (*wl)[TN * 16][KCP]) {
   const int wave = threadIdx.x >> 6;
@@ -612,19 +446,10 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
   const float* __restrict__ W = a.W[b];
   const int64_t ldw = a.ldw[b];
   const int64_t row = m_base + i;
-  const bool gval = row < a.M && (!BN || row < bn_rows(a.M, a.bn.nvalid));
+  const bool gval = row < a.M;
   const float* grow = a.G + (gval ? row : 0) * a.ldg;
-  auto load_g = [&](int n0, float4 (&o)[4]) {
-    if (!BN) {
-      load_a_chunk(grow, gval, n0, a.N, q, o);
-      return;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int c = n0 + 16 * s + 4 * q;
-      o[s] = (gval && c < a.N) ? bn_dz4(a.bn, grow, row, c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
+  auto load_g = [&](int n0, float4 (&o)[4]) { load_a_chunk(grow, gval, n0, a.N, q, o); };
+
 
   // staging: TN*16 columns x 64 n = TN*256 float4 over 256 threads; thread
   // loads W[n][c4*4 .. +3] (16 float4 per n row) and scatters 4 floats.
@@ -717,7 +542,6 @@ constexpr int WT_ROWS = WT_TM * 16;
 constexpr int WT_COLS = WT_TN * 16;
 
 struct BwdWeightArgs {
-  BnT bn;
   int nb;
   int N;
   int64_t M;
@@ -885,7 +709,6 @@ __device__ __forceinline__ void weight_item(unsigned L, unsigned Y, unsigned tot
   bz = (int)(w / Y);
 }
 
-template <bool BN = false>
 __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by, int bz,
                                                   float (*gl)[WR][64], float (*al)[WR][64]) {
   const int wave = threadIdx.x >> 6;
@@ -906,18 +729,13 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
 
   // staging: each tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
   const int sr = threadIdx.x >> 4, sc = (threadIdx.x & 15) * 4;
-  const int64_t g_hi = BN ? bn_rows(a.M, a.bn.nvalid) : a.M;
   auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t m = m0 + sr + 16 * u;
       const bool mv = m < m_hi;
       const int n = n_base + sc, k = k_base + sc;
-      if (BN)
-        g[u] = (mv && m < g_hi && n < a.N) ? bn_dz4(a.bn, a.G + m * a.ldg, m, n)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-      else
-        g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
+      g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
       x[u] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1074,7 +892,7 @@ struct BwdFusedArgs {
   int d_xcd;   // XCD-aware data order: the column tiles of one row block on one XCD
 };
 
-template <int TND, bool BN>
+template <int TND>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
@@ -1096,14 +914,14 @@ __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
       bx = l % a.d_gx;
       by = l / a.d_gx;
     }
-    bwd_data_lds_body<TND, BN>(a.d, bx, by, reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
+    bwd_data_lds_body<TND>(a.d, bx, by, reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
     return;
   }
   if (L >= a.n_w) return;  // alignment padding
   const int Y = a.w.tile_start[a.w.nb];
   int by = L % Y, bz = L / Y;
   if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
-  bwd_weight32_body<BN>(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
+  bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
                     reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
@@ -1185,16 +1003,6 @@ int data_xcd_map() {
   return v;
 }
 
-// HLHGAT_PROJ_TN caps the 16-column tiles per wave (A/B of the wave count
-// against the SIMD count; 0 = default)
-int proj_tn() {
-  static int v = [] {
-    const char* e = getenv("HLHGAT_PROJ_TN");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 bool vec_ok(const float* p, int64_t ld, int64_t kb) {
   return aligned16(p) && (ld % 4) == 0 && (kb % 4) == 0;
 }
@@ -1206,35 +1014,7 @@ int fwd_tn(int64_t M, int64_t N, int64_t ktot) {
   int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
   if (N <= 16) tn = 1;
   else if (N <= 32 && tn > 2) tn = 2;
-  if (proj_tn()) {
-    const int cap = N <= 16 ? 1 : (N <= 32 ? 2 : 4);
-    tn = proj_tn() < cap ? proj_tn() : cap;
-  }
   return tn;
-}
-
-// workspace of hlhgat_proj_fwd_bn: [counters | fallback | part | gpart] with
-// `fallback` a hlhgat_bn_stats_train workspace for the unfused path.  Both
-// counter regions sit at FIXED offsets (the fallback's own counters come
-// first in it), so calls of any (M, N) on one workspace never see another
-// call's partials where they expect zeroed counters.
-struct StatPlan {
-  int64_t parts;
-  int gs, ng;
-  size_t count_bytes, fb_bytes, part_bytes, gpart_bytes, total;
-};
-size_t al256(size_t v) { return (v + 255) & ~size_t(255); }
-StatPlan stat_plan(int64_t M, int64_t N) {
-  StatPlan p{};
-  p.parts = std::max<int64_t>(1, ceil_div(M, (int64_t)64));
-  p.gs = (int)std::max<int64_t>(16, ceil_div(p.parts, (int64_t)kStatGroups));
-  p.ng = (int)ceil_div(p.parts, (int64_t)p.gs);
-  p.count_bytes = al256(sizeof(unsigned) * kStatTiles * (1 + kStatGroups));
-  p.fb_bytes = al256((size_t)hlhgat_bn_workspace_bytes(M > 0 ? M : 1, N));
-  p.part_bytes = al256(sizeof(double) * 2 * (size_t)p.parts * (size_t)N);
-  p.gpart_bytes = al256(sizeof(double) * 2 * (size_t)p.ng * (size_t)N);
-  p.total = p.count_bytes + p.fb_bytes + p.part_bytes + p.gpart_bytes;
-  return p;
 }
 
 }  // namespace
@@ -1309,88 +1089,6 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   return HLHGAT_OK;
 }
 
-extern "C" int64_t hlhgat_proj_fwd_bn_workspace_bytes(int64_t M, int64_t N) {
-  if (M < 0 || N <= 0) return 0;
-  return (int64_t)stat_plan(M, N).total;
-}
-
-extern "C" int hlhgat_proj_fwd_bn(int nblocks, const float* const* A, const int64_t* lda,
-                                  const float* const* W, const int64_t* ldw, const int64_t* kb,
-                                  int64_t M, int64_t N, const float* bias, float* C, int64_t ldc,
-                                  const int32_t* n_valid, float* running_mean, float* running_var,
-                                  int64_t* num_batches_tracked, float momentum, float eps,
-                                  float* save_mean, float* save_invstd, void* workspace,
-                                  int64_t workspace_bytes, void* stream) {
-  HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_fwd_bn: nblocks=%d", nblocks);
-  HLH_CHECK_ARG(M >= 1 && N > 0 && N <= 16 * kStatTiles && ldc >= N && C,
-                "proj_fwd_bn: bad M/N/ldc/C");
-  HLH_CHECK_ARG(save_mean && save_invstd, "proj_fwd_bn: NULL statistics output");
-  HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
-                "proj_fwd_bn: running_mean/var must both be given or both NULL");
-  const StatPlan sp = stat_plan(M, N);
-  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)sp.total,
-                "proj_fwd_bn: workspace too small");
-  bool vec = true;
-  int64_t ktot = 0;
-  FwdArgs a{};
-  a.nb = nblocks;
-  a.M = M;
-  a.N = (int)N;
-  a.bias = bias;
-  a.C = C;
-  a.ldc = ldc;
-  double flops = 0;
-  for (int b = 0; b < nblocks; ++b) {
-    HLH_CHECK_ARG(A[b] && W[b] && kb[b] > 0 && lda[b] >= kb[b] && ldw[b] >= kb[b],
-                  "proj_fwd_bn: bad block %d", b);
-    a.A[b] = A[b];
-    a.W[b] = W[b];
-    a.lda[b] = lda[b];
-    a.ldw[b] = ldw[b];
-    a.kb[b] = (int)kb[b];
-    vec = vec && vec_ok(A[b], lda[b], kb[b]) && vec_ok(W[b], ldw[b], kb[b]);
-    ktot += kb[b];
-    flops += 2.0 * (double)M * (double)N * (double)kb[b];
-  }
-  if (!vec) {  // unfused: projection, then the statistics pass over C
-    int rc = hlhgat_proj_fwd(nblocks, A, lda, W, ldw, kb, M, N, bias, C, ldc, 0, stream);
-    if (rc) return rc;
-    return hlhgat_bn_stats_train(C, ldc, M, n_valid, N, running_mean, running_var,
-                                 num_batches_tracked, momentum, eps, save_mean, save_invstd,
-                                 (char*)workspace + sp.count_bytes, (int64_t)sp.fb_bytes,
-                                 stream);
-  }
-  char* w = (char*)workspace;
-  a.stats = 1;
-  a.nvalid = n_valid;
-  a.count = reinterpret_cast<unsigned*>(w);
-  a.part = reinterpret_cast<double*>(w + sp.count_bytes + sp.fb_bytes);
-  a.gpart = reinterpret_cast<double*>(w + sp.count_bytes + sp.fb_bytes + sp.part_bytes);
-  a.gs = sp.gs;
-  a.ng = sp.ng;
-  a.save_mean = save_mean;
-  a.save_invstd = save_invstd;
-  a.running_mean = running_mean;
-  a.running_var = running_var;
-  a.nbt = num_batches_tracked;
-  a.momentum = momentum;
-  a.eps = eps;
-  const int tn = fwd_tn(M, N, ktot);
-  double bytes = 4.0 * (double)M * N;
-  for (int b = 0; b < nblocks; ++b) bytes += 4.0 * (double)M * kb[b] + 4.0 * N * kb[b];
-  hipStream_t s = as_stream(stream);
-  ProfScope prof(HLHGAT_PROF_PROJ, s, bytes, flops);
-  dim3 g((unsigned)sp.parts, (unsigned)ceil_div(N, (int64_t)tn * 16));
-  if (tn == 1)
-    launch(k_proj_fwd_lds<1, true>, g, 256, 0, s, &prof, a);
-  else if (tn == 2)
-    launch(k_proj_fwd_lds<2, true>, g, 256, 0, s, &prof, a);
-  else
-    launch(k_proj_fwd_lds<4, true>, g, 256, 0, s, &prof, a);
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
-
 extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
                                     const float* const* W, const int64_t* ldw,
                                     const int64_t* kb, int64_t M, int64_t N,
@@ -1410,7 +1108,6 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   int64_t ktot = 0;
   for (int b = 0; b < nblocks; ++b) ktot += kb[b];
   int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // see proj_fwd
-  if (proj_tn()) tnd = proj_tn();
   a.tile_start[0] = 0;
   for (int b = 0; b < nblocks; ++b) {
     HLH_CHECK_ARG(W[b] && dA[b] && kb[b] > 0 && ldw[b] >= kb[b] && ldda[b] >= kb[b],
@@ -1535,14 +1232,8 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   return HLHGAT_OK;
 }
 
-extern "C" int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                                   const float* dy, int64_t lddy, int64_t n,
-                                   const int32_t* n_valid, int64_t C, const float* coef,
-                                   float* dx, int64_t lddx, void* stream);
-
 namespace {
-int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT* bn,
-                  float* dz_scratch, int nb_w, const float* const* A, const int64_t* lda,
+int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w, const float* const* A, const int64_t* lda,
                   const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
                   int nb_d, const float* const* W, const int64_t* ldw, const int64_t* kb_d,
                   float* const* dA, const int64_t* ldda, float* workspace,
@@ -1561,23 +1252,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT
     for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
-  if (bn) {
-    fuse = fuse && vec_ok(bn->x, bn->ldx, N) && (!bn->y || vec_ok(bn->y, bn->ldy, N)) &&
-           bn->C == N;
-    if (!fuse) {  // BatchNorm backward applied on its own, then the plain path
-      if (M == 0)
-        return proj_bwd_impl(0, N, dC, lddc, nullptr, nullptr, nb_w, A, lda, kb_w, dW, lddw,
-                             dbias, nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats,
-                             stream);
-      HLH_CHECK_ARG(dz_scratch, "proj_bwd_bn: dz_scratch required");
-      const int rc = hlhgat_bn_bwd_apply(bn->x, bn->ldx, bn->y, bn->ldy, dC, lddc, M,
-                                         bn->nvalid, N, bn->coef, dz_scratch, N, stream);
-      if (rc != HLHGAT_OK) return rc;
-      return proj_bwd_impl(M, N, dz_scratch, N, nullptr, nullptr, nb_w, A, lda, kb_w, dW, lddw,
-                           dbias, nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats,
-                           stream);
-    }
-  }
   if (!fuse) {  // the separate launches (any alignment, M == 0, one side only)
     if (want_w) {
       const int rc = hlhgat_proj_bwd_weight(nb_w, dC, lddc, A, lda, kb_w, M, N, dW, lddw, dbias,
@@ -1589,7 +1263,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT
     return HLHGAT_OK;
   }
   BwdFusedArgs f{};
-  if (bn) f.w.bn = f.d.bn = *bn;
   BwdWeightArgs& a = f.w;
   ReduceArgs r{};
   r.nb = nb_w;
@@ -1633,7 +1306,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT
   int64_t ktot = 0;
   for (int b = 0; b < nb_d; ++b) ktot += kb_d[b];
   int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // as hlhgat_proj_bwd_data
-  if (proj_tn()) tnd = proj_tn() < 2 ? proj_tn() : 2;  // tile width only: same results
   d.tile_start[0] = 0;
   for (int b = 0; b < nb_d; ++b) {
     HLH_CHECK_ARG(W[b] && dA[b] && kb_d[b] > 0 && ldw[b] >= kb_d[b] && ldda[b] >= kb_d[b],
@@ -1652,14 +1324,10 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, const BnT
   const int64_t n_blocks = (int64_t)f.n_wpad + (int64_t)f.n_d;
   HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
   hipStream_t s = as_stream(stream);
-  if (tnd == 1 && bn)
-    k_proj_bwd_fused<1, true><<<(unsigned)n_blocks, 256, 0, s>>>(f);
-  else if (bn)
-    k_proj_bwd_fused<2, true><<<(unsigned)n_blocks, 256, 0, s>>>(f);
-  else if (tnd == 1)
-    k_proj_bwd_fused<1, false><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+  if (tnd == 1)
+    k_proj_bwd_fused<1><<<(unsigned)n_blocks, 256, 0, s>>>(f);
   else
-    k_proj_bwd_fused<2, false><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+    k_proj_bwd_fused<2><<<(unsigned)n_blocks, 256, 0, s>>>(f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
@@ -1681,21 +1349,6 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
                                const int64_t* ldw, const int64_t* kb_d, float* const* dA,
                                const int64_t* ldda, float* workspace, int64_t workspace_floats,
                                void* stream) {
-  return proj_bwd_impl(M, N, dC, lddc, nullptr, nullptr, nb_w, A, lda, kb_w, dW, lddw, dbias,
-                       nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats, stream);
-}
-
-extern "C" int hlhgat_proj_bwd_bn(int64_t M, int64_t N, const float* dy, int64_t lddy,
-                                  const float* bn_x, int64_t ldx, const float* bn_y,
-                                  int64_t ldy, const float* coef, const int32_t* n_valid,
-                                  int nb_w, const float* const* A, const int64_t* lda,
-                                  const int64_t* kb_w, float* const* dW, const int64_t* lddw,
-                                  float* dbias, int nb_d, const float* const* W,
-                                  const int64_t* ldw, const int64_t* kb_d, float* const* dA,
-                                  const int64_t* ldda, float* dz_scratch, float* workspace,
-                                  int64_t workspace_floats, void* stream) {
-  HLH_CHECK_ARG(bn_x && coef && ldx >= N && (!bn_y || ldy >= N), "proj_bwd_bn: bad BN operands");
-  BnT t{bn_x, ldx, bn_y, ldy, coef, n_valid, (int)N};
-  return proj_bwd_impl(M, N, dy, lddy, &t, dz_scratch, nb_w, A, lda, kb_w, dW, lddw, dbias,
+  return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias,
                        nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats, stream);
 }

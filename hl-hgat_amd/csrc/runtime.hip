@@ -52,11 +52,53 @@ ProfScope::ProfScope(int kernel_class, hipStream_t s, double b, double f) {
   stop_ev = pc.stop[slot];
 }
 
+// --- device error word -------------------------------------------------------
+// One pinned, mapped, coherent host word shared by all devices: kernels store
+// an HLHGAT_DEVERR_* code into it with plain system-scope stores (no PCIe
+// atomics; reporters of different codes may overwrite each other, so any
+// nonzero value means "do not use these results"), the host reads it without
+// synchronising.
+namespace {
+std::mutex g_err_mu;
+unsigned* g_err_word = nullptr;
+}  // namespace
+
+unsigned* device_error_word() {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  if (!g_err_word) {
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, 64, hipHostMallocPortable | hipHostMallocMapped |
+                                             hipHostMallocCoherent);
+    if (e != hipSuccess) {
+      set_error("hipHostMalloc(device error word) failed: %s", hipGetErrorString(e));
+      return nullptr;
+    }
+    *static_cast<volatile unsigned*>(p) = 0u;
+    g_err_word = static_cast<unsigned*>(p);
+  }
+  return g_err_word;
+}
+
 }  // namespace hlhgat
 
 using namespace hlhgat;
 
-extern "C" int hlhgat_version(void) { return 100; }
+extern "C" int hlhgat_version(void) { return 101; }
+
+extern "C" int hlhgat_device_errors(unsigned* out) {
+  HLH_CHECK_ARG(out, "device_errors: NULL pointer");
+  unsigned* w = device_error_word();
+  HLH_CHECK_ARG(w, "device_errors: %s", hlhgat_last_error());
+  *out = *static_cast<volatile unsigned*>(w);
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_clear_device_errors(void) {
+  unsigned* w = device_error_word();
+  HLH_CHECK_ARG(w, "clear_device_errors: %s", hlhgat_last_error());
+  *static_cast<volatile unsigned*>(w) = 0u;
+  return HLHGAT_OK;
+}
 
 extern "C" const char* hlhgat_last_error(void) { return g_last_error.c_str(); }
 

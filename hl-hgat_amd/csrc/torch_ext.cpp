@@ -141,13 +141,23 @@ hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_e
 // One BN workspace per (device, stream): its arrival counters must not be
 // shared by launches that can run concurrently (node / edge chains run on two
 // streams, see hlhgat.ops.fork).  Stream-ordered reuse on one stream is safe.
+// A workspace that is outgrown is RETIRED, never freed: a hipGraph captured
+// earlier on that stream still holds its address, and a replay must not write
+// BN counters into memory the caching allocator has handed to another tensor.
+// (Sizes grow geometrically, so at most a handful are ever retired.)
 Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
   static auto* cache = new std::unordered_map<uintptr_t, Tensor>();  // leaked: outlives HIP teardown
+  static auto* retired = new std::vector<Tensor>();
   const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
   const int64_t need = hlhgat_bn_workspace_bytes(n, C);
   auto it = cache->find(key);
   if (it == cache->end() || it->second.numel() < need) {
-    Tensor ws = at::empty({std::max<int64_t>(need, 1 << 20)}, like.options().dtype(at::kByte));
+    int64_t bytes = std::max<int64_t>(need, 1 << 20);
+    if (it != cache->end()) {
+      bytes = std::max<int64_t>(bytes, 2 * it->second.numel());
+      retired->push_back(it->second);
+    }
+    Tensor ws = at::empty({bytes}, like.options().dtype(at::kByte));
     chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream_of(like)), "zero_fill");
     (*cache)[key] = ws;
   }
@@ -287,86 +297,15 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
   return y;
 }
 
-// BatchNorm statistics in the projection epilogue (hlhgat_proj_fwd_bn):
-// OFF by default -- measured slower: first 264k -> 236k graphs/s (ZINC) with
-// release-fenced partials (each workgroup's buffer_wbl2 wrote back its own
-// freshly stored C tile), then, with write-through partials and no fences,
-// still 1.1 % slower in a same-box A/B (268.6k vs 265.6k): every GEMM
-// workgroup drains its C stores and takes an agent-scope atomic before
-// retiring, which costs about what the separate statistics launch does.
-// HLHGAT_FUSED_BN_STATS=1 (or set_fused_bn_stats) turns it on.
-bool& fused_bn_flag() {
-  static bool on = [] {
-    const char* e = getenv("HLHGAT_FUSED_BN_STATS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-bool fused_bn_stats() { return fused_bn_flag(); }
-
-// HLHGAT_FUSED_CONV=1: the graph-local fused conv forward (basis + projection
-// in one launch, bitwise the same results).  OFF by default: same-box A/B at
-// the ZINC step 270.7k -> 263.7k graphs/s -- one workgroup per tile walks
-// load / barrier / weight-stage / MFMA phases serially and holds 56 KB of LDS,
-// which costs more than the three short launches it replaces.
-// HLHGAT_GRAPH_LOCAL=1: the basis-only graph-local path (k_basis_local_*).
-bool& fused_conv_flag() {
-  static bool on = [] {
-    const char* e = getenv("HLHGAT_FUSED_CONV");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-bool fused_conv_env() { return fused_conv_flag(); }
-void set_fused_conv(bool on) { fused_conv_flag() = on; }
+// HLHGAT_GRAPH_LOCAL=1: the graph-local polynomial basis (k_basis_local_*: a
+// workgroup walks the whole recurrence of a tile of whole graphs in LDS;
+// bitwise equal to the step launches and, at the ZINC shape, equal in cost).
 bool graph_local_env() {
   static const bool on = [] {
     const char* e = getenv("HLHGAT_GRAPH_LOCAL");
     return e && e[0] == '1';
   }();
   return on;
-}
-void set_fused_bn_stats(bool on) { fused_bn_flag() = on; }
-
-// One hlhgat_proj_fwd_bn workspace per (device, stream), as bn_workspace.
-Tensor pbn_workspace(const Tensor& like, int64_t M, int64_t N) {
-  static auto* cache = new std::unordered_map<uintptr_t, Tensor>();
-  const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
-  const int64_t need = hlhgat_proj_fwd_bn_workspace_bytes(M, N);
-  auto it = cache->find(key);
-  if (it == cache->end() || it->second.numel() < need) {
-    Tensor ws = at::empty({std::max<int64_t>(need, 1 << 20)}, like.options().dtype(at::kByte));
-    chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream_of(like)), "zero_fill");
-    (*cache)[key] = ws;
-  }
-  return (*cache)[key];
-}
-
-// pre = sum_b A_b W_b^T + bias with its BatchNorm statistics formed in the
-// GEMM epilogue, then y = BN apply (+ReLU) into y_into or a new tensor.
-Tensor proj_bn_forward(const std::vector<const float*>& A, const std::vector<int64_t>& lda,
-                       const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
-                       const std::vector<int64_t>& kb, int64_t M, int64_t N, const float* bias,
-                       Tensor& pre, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
-                       const Tensor* y_into = nullptr) {
-  void* s = stream_of(pre);
-  mean = at::empty({N}, pre.options());
-  invstd = at::empty({N}, pre.options());
-  Tensor ws = pbn_workspace(pre, M, N);
-  int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
-  chk(hlhgat_proj_fwd_bn((int)A.size(), A.data(), lda.data(), W.data(), ldw.data(), kb.data(), M,
-                         N, bias, pre.data_ptr<float>(), ld_of(pre), iptr(st.valid), mfptr(st.rm),
-                         mfptr(st.rv), nbt, (float)st.momentum, (float)st.eps,
-                         mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr(),
-                         ws.numel(), s),
-      "proj_fwd_bn");
-  Tensor y = y_into ? *y_into : at::empty({M, N}, pre.options());
-  TORCH_CHECK(y.size(0) == M && y.size(1) == N && y.stride(1) == 1, "hlhgat: bad BN output view");
-  chk(hlhgat_bn_apply(pre.data_ptr<float>(), ld_of(pre), M, iptr(st.valid), N, fptr(st.w),
-                      fptr(st.b), mean.data_ptr<float>(), invstd.data_ptr<float>(), relu ? 1 : 0,
-                      y.data_ptr<float>(), ld_of(y), s),
-      "bn_apply");
-  return y;
 }
 
 // returns dx; fills dw/db when requested
@@ -393,67 +332,6 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
                           ws.numel(), stream_of(x)),
       "bn_bwd_train");
   return dx;
-}
-
-// HLHGAT_FOLD_BN_BWD=1 (or set_fold_bn_bwd(true)): fold the conv's BatchNorm
-// backward apply into the projection gradient's operand loads
-// (hlhgat_proj_bwd_bn, bitwise the same results).  OFF by default: same-box
-// A/B at the ZINC step 282.0k -> 267.3k graphs/s -- every dC element then
-// costs three loads (dy, x, y) and the per-channel coefficients in each of the
-// weight- and data-gradient workgroups that read it, more than the apply
-// launch it removes.
-bool& fold_bn_flag() {
-  static bool on = [] {
-    const char* e = getenv("HLHGAT_FOLD_BN_BWD");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-void set_fold_bn_bwd(bool on) { fold_bn_flag() = on; }
-
-// the statistics half of bn_backward: fills dw / db, returns coef [3, C]
-Tensor bn_backward_coef(const Tensor& x, const OptT& y, const Tensor& dyc, const OptT& w,
-                        const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
-                        Tensor& dw, Tensor& db, const Tensor* b_param, const Tensor& valid) {
-  const int64_t n = x.size(0), C = x.size(1);
-  dw = (need_w && has(w)) ? grad_like(w) : Tensor();
-  db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
-                                                 : at::empty({C}, x.options()))
-              : Tensor();
-  Tensor ws = bn_workspace(x, n, C);
-  Tensor coef = at::empty({3 * C}, x.options());
-  chk(hlhgat_bn_bwd_reduce(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
-                           dyc.data_ptr<float>(), ld_of(dyc), n,
-                           valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
-                           mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                           coef.data_ptr<float>(), dw.defined() ? dw.data_ptr<float>() : nullptr,
-                           db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
-                           ws.numel(), stream_of(x)),
-      "bn_bwd_reduce");
-  return coef;
-}
-
-// proj_bwd_both with the BN backward folded into the dC operand
-void proj_bwd_bn_both(const Tensor& dy, const Tensor& bx, const OptT& by, const Tensor& coef,
-                      const Tensor& valid, const std::vector<const float*>& A,
-                      const std::vector<int64_t>& lda, const std::vector<int64_t>& kbw,
-                      std::vector<float*>& dW, const std::vector<int64_t>& lddw, float* db,
-                      const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
-                      const std::vector<int64_t>& kbd, std::vector<float*>& dA,
-                      const std::vector<int64_t>& ldda, void* s) {
-  const int nbw = (int)A.size(), nbd = (int)W.size();
-  const int64_t M = dy.size(0), N = dy.size(1);
-  const int64_t wsf =
-      nbw ? hlhgat_proj_bwd_weight_workspace_floats(nbw, kbw.data(), M, N, db != nullptr) : 0;
-  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, dy.options());
-  Tensor dz = at::empty({M, N}, dy.options());  // used only by the unaligned fallback
-  chk(hlhgat_proj_bwd_bn(M, N, dy.data_ptr<float>(), ld_of(dy), bx.data_ptr<float>(), ld_of(bx),
-                         fptr(by), has(by) ? ld_of(*by) : 0, coef.data_ptr<float>(),
-                         valid.defined() ? valid.data_ptr<int32_t>() : nullptr, nbw, A.data(),
-                         lda.data(), kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(),
-                         ldw.data(), kbd.data(), dA.data(), ldda.data(), dz.data_ptr<float>(),
-                         ws.data_ptr<float>(), wsf, s),
-      "proj_bwd_bn");
 }
 
 // ---------------------------------------------------------------------------
@@ -489,24 +367,15 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                              has(h_sval) ? *h_sval : Tensor(), h_bounds, *h_hdr)
                  : hlhgat_halo_t{};
     const bool factored = !fac.empty();
-    // graph tiles: the fused graph-local conv (basis + projection, one launch)
-    // for the 64-wide ZINC-scale blocks; the basis-only local path on request
+    // graph tiles: the graph-local basis on request (HLHGAT_GRAPH_LOCAL=1)
     const bool local_basis = has(tiles) && graph_local_env();
-    const int64_t dout0 = W.empty() ? 0 : W[0].size(0);
-    bool fused_local = fused_conv_env() && !factored && has(tiles) && K > 1 && N > 0 &&
-                       x.dim() == 2 && F == 64 && Cin == 64 && dout0 == 64 && kind != 2 &&
-                       tile_rows >= 1 && tile_rows <= 64 && tile_nnz >= 1 &&
-                       ld_of(x2) % 4 == 0 && (reinterpret_cast<uintptr_t>(x2.data_ptr()) & 15) == 0;
-    for (int64_t k = 0; fused_local && k < K; ++k)
-      fused_local = W[k].stride(1) == 1 && W[k].stride(0) % 4 == 0 &&
-                    (reinterpret_cast<uintptr_t>(W[k].data_ptr()) & 15) == 0;
     if (factored && K > 1 && N > 0) {
       const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
       Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x.options());
       chk(hlhgat_poly_basis_fwd_factored((int)kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
                                          (int)K, T.data_ptr<float>(), work.data_ptr<float>(), s),
           "poly_basis_fwd_factored");
-    } else if (K > 1 && N > 0 && !fused_local) {
+    } else if (K > 1 && N > 0) {
       chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
                                 nnz ? a_col.data_ptr<int>() : nullptr,
                                 nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
@@ -540,25 +409,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                   "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
     Tensor pre = (sink && bn_mode == 0) ? *out_buf : at::empty({M, dout}, x.options());
     Tensor out = pre, mean, invstd;
-    if (fused_local) {  // basis + projection in one graph-local launch
-      std::vector<int64_t> ldwv(K);
-      for (int64_t k = 0; k < K; ++k) ldwv[k] = W[k].stride(0);
-      chk(hlhgat_conv_local_fwd((int)kind, a_rowptr.data_ptr<int>(),
-                                nnz ? a_col.data_ptr<int>() : nullptr, nnz ? fptr(a_val) : nullptr,
-                                N, nnz, tiles->data_ptr<int>(), tiles->numel() - 1, tile_rows,
-                                tile_nnz, x2.data_ptr<float>(), ld_of(x2), F, (int)K,
-                                T.data_ptr<float>(), Wp.data(), ldwv.data(), fptr(bias), dout,
-                                pre.data_ptr<float>(), ld_of(pre), s),
-          "conv_local_fwd");
-      if (bn_mode > 0) {
-        BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
-        out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
-      }
-    } else if (bn_mode > 0 && M > 0 && fused_bn_stats()) {  // statistics in the GEMM epilogue
-      BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
-      out = proj_bn_forward(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, st, bn_mode == 2, mean,
-                            invstd, sink ? &*out_buf : nullptr);
-    } else {
+    {
       if (M > 0) {
         proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, s);
       } else if (has(bias)) {
@@ -694,16 +545,12 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
       float* db = nullptr;
       std::vector<Tensor> keep;  // the dW buffers stay allocated until the launch
     } wdef;  // weight gradient deferred into the data gradient's launch
-    Tensor dbn_w, dbn_b, bn_coef;  // bn_coef: BN backward folded into the projection's
+    Tensor dbn_w, dbn_b;
     const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
     if (bn_mode > 0) {
       OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-      if (need_x && (need_w || need_b) && M > 0 && fused_bwd_flag() && fold_bn_flag())
-        bn_coef = bn_backward_coef(pre, bn_y, G, w, mean, invstd, need(ctx, 10 + K),
-                                   need(ctx, 11 + K), dbn_w, dbn_b, &bn_b, valid);
-      else
-        G = bn_backward(pre, bn_y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K),
-                        dbn_w, dbn_b, nullptr, &bn_b, valid);
+      G = bn_backward(pre, bn_y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K),
+                      dbn_w, dbn_b, nullptr, &bn_b, valid);
       out[10 + K] = dbn_w;
       out[11 + K] = dbn_b;
     }
@@ -743,10 +590,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
           ldw[k] = W[k].stride(0);
           dA[k] = Gs.data_ptr<float>() + k * N * F;
         }
-        if (!wdef.dWp.empty() && bn_coef.defined())
-          proj_bwd_bn_both(G, pre, bn_y, bn_coef, valid, Ap, lda, kb, wdef.dWp, wdef.lddw,
-                           wdef.db, Wp, ldw, kb, dA, ldda, s);
-        else if (!wdef.dWp.empty())
+        if (!wdef.dWp.empty())
           proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s);
         else
           proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
@@ -838,31 +682,11 @@ Tensor linear_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT
 }
 
 // Linear(blocks) -> BatchNorm (+ReLU): h (the BN input) is returned through
-// `h`, the activation as the result; the statistics come from the GEMM
-// epilogue when fused_bn_stats().
+// `h`, the activation as the result.
 Tensor linear_bn_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT& b,
                          const BnState& st, bool relu, Tensor& h, Tensor& mean, Tensor& invstd) {
-  const int64_t M = As[0].size(0), N = W.size(0);
-  if (M == 0 || !fused_bn_stats()) {
-    h = linear_forward(As, W, b);
-    return bn_forward(h, st, relu, mean, invstd);
-  }
-  const int nb = (int)As.size();
-  std::vector<const float*> Ap(nb), Wp(nb);
-  std::vector<int64_t> lda(nb), ldw(nb), kb(nb);
-  int64_t off = 0;
-  for (int i = 0; i < nb; ++i) {
-    Ap[i] = As[i].data_ptr<float>();
-    lda[i] = ld_of(As[i]);
-    kb[i] = As[i].size(1);
-    Wp[i] = W.data_ptr<float>() + off;
-    ldw[i] = W.stride(0);
-    off += kb[i];
-  }
-  TORCH_CHECK(off == W.size(1), "hlhgat: Linear expects ", W.size(1), " input features, got ",
-              off);
-  h = at::empty({M, N}, W.options());
-  return proj_bn_forward(Ap, lda, Wp, ldw, kb, M, N, fptr(b), h, st, relu, mean, invstd);
+  h = linear_forward(As, W, b);
+  return bn_forward(h, st, relu, mean, invstd);
 }
 
 // grads of linear_forward; dAs[i] only where need_a[i]
@@ -1514,10 +1338,7 @@ std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
-  m.def("set_fused_bn_stats", &set_fused_bn_stats);
   m.def("set_fused_bwd", &set_fused_bwd);
-  m.def("set_fold_bn_bwd", &set_fold_bn_bwd);
-  m.def("set_fused_conv", &set_fused_conv);
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);

@@ -60,9 +60,6 @@ SIGNATURES = {
     "hlhgat_hodge_row_sizes": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "hlhgat_hodge_build": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_vp]),
-    "hlhgat_conv_local_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
-                                      c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, P_vp, P_i64, c_vp,
-                                      c_i64, c_vp, c_i64, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
@@ -73,14 +70,11 @@ SIGNATURES = {
     "hlhgat_proj_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_i32, P_vp, P_i64, P_i64, P_vp,
                                 P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64, c_vp,
                                 c_i64, c_vp]),
-    "hlhgat_proj_bwd_bn": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
-                                   c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64, c_vp, c_i32,
-                                   P_vp, P_i64, P_i64, P_vp, P_i64, c_vp, c_vp, c_i64, c_vp]),
-    "hlhgat_bn_bwd_reduce": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "hlhgat_bn_bwd_apply": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                    c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
+    "hlhgat_get_bn_one_launch": (c_i32, []),
+    "hlhgat_set_bn_poll_limit": (c_i32, [C.c_uint32]),
+    "hlhgat_device_errors": (c_i32, [c_vp]),
+    "hlhgat_clear_device_errors": (c_i32, []),
     "hlhgat_bn_wait_timeouts": (c_i32, [c_vp]),
     "hlhgat_edge_gather2": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_f32,
                                     c_f32, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp]),
@@ -104,10 +98,6 @@ SIGNATURES = {
                                       c_f32, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_bn_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32,
                                 c_vp, c_i64, c_vp]),
-    "hlhgat_proj_fwd_bn_workspace_bytes": (c_i64, [c_i64, c_i64]),
-    "hlhgat_proj_fwd_bn": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
-                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp,
-                                   c_vp, c_i64, c_vp]),
     "hlhgat_zero_fill": (c_i32, [c_vp, c_sz, c_vp]),
     "hlhgat_copy2d_batched": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlhgat_prof_enable": (c_i32, [c_i32, c_i32]),
@@ -118,6 +108,7 @@ SIGNATURES = {
 # constants from include/hlhgat.h
 POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
+DEVERR_BN_WAIT = 1
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
 MAX_BLOCKS = 16
 

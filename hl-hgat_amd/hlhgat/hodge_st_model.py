@@ -16,13 +16,6 @@ from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
 from .nn import BatchNorm, Sequential, run_sequential
 
-# HLHGAT_PREP_OVERLAP=1: build the incidence CSR on a second side stream
-# beside HL_init_conv instead of after it (same results).  OFF by default:
-# same-box A/B at the ZINC step 289.5k -> 285.3k graphs/s (a third stream's
-# sort kernels slow the two conv chains more than the overlap saves).
-import os as _os
-_PREP_OVERLAP = _os.environ.get("HLHGAT_PREP_OVERLAP", "0") == "1"
-
 __all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr",
            "HL_HGCNN_CIFAR10SP_dense_int3_attpool", "HL_HGCNN_pepfunc_dense_int3_attpool",
            "segment_ptr", "mean_pool_sorted"]
@@ -123,14 +116,12 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
             inc = p1.incidence()  # built here, cached for every NodeEdgeInt
             return p1, d, [inc.rowptr, inc.edge_ids, inc.edge_index]  # fork orders them on main
 
-        # the incidence build (sort + CSR of |B1|): after HL_init_conv, or beside
-        # it on a second side stream (_PREP_OVERLAP); NodeEdgeInt needs it first
-        side_in = [t for t in (data.edge_index, valid_t) if t is not None]
-        (x_t, x_s), (par_1, D, _) = ops.fork(
-            lambda: self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
-                                      edge_weight_s),
-            boundary, side_inputs=side_in,
-            device=x_t.device if (x_t.is_cuda and _PREP_OVERLAP) else None, slot=1)
+        # the incidence build (sort + CSR of |B1|) after HL_init_conv (building it
+        # on a third stream beside the conv measured 1.4 % slower: its sort
+        # kernels slow the two conv chains more than the overlap saves)
+        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                     edge_weight_s)
+        par_1, D, _ = boundary()
         if dense:
             dt.append(x_t)
             ds.append(x_s)

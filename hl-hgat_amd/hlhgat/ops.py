@@ -28,7 +28,7 @@ except ImportError as e:  # pragma: no cover - the build always produces it
 __all__ = [
     "SparseCSR", "HodgeOperator", "Incidence", "hodge_operator", "incidence",
     "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks", "mlp2", "nei_value",
-    "batch_norm_act",
+    "batch_norm_act", "check_device_errors", "clear_device_errors", "device_errors",
     "node_from_edges", "edge_from_nodes", "att_score", "segment_mean",
     "POLY_LAGUERRE", "POLY_CHEB", "POLY_LAGUERRE_DEMO", "SIGMA_SIGMOID", "SIGMA_RELU",
 ]
@@ -1054,6 +1054,39 @@ def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False
         raise ValueError(f"Expected more than 1 value per channel when training, got input "
                          f"size {tuple(x.shape)}")
     return _ext.bn_act(x, *_bn_args(bn), bool(relu), valid)
+
+
+# ----------------------------------------------------------------------------
+# device error word (include/hlhgat.h: hlhgat_device_errors)
+# ----------------------------------------------------------------------------
+_DEVERR_TEXT = {
+    _lib.DEVERR_BN_WAIT: "one-launch BatchNorm: a workgroup timed out waiting for its tile's "
+                         "statistics (its rows were written as NaN)",
+}
+
+
+def device_errors() -> int:
+    """The device error word as kernels that have COMPLETED so far left it
+    (no synchronisation)."""
+    w = C.c_uint32(0)
+    check(LIB.hlhgat_device_errors(C.byref(w)), "device_errors")
+    return int(w.value)
+
+
+def clear_device_errors() -> None:
+    check(LIB.hlhgat_clear_device_errors(), "clear_device_errors")
+
+
+def check_device_errors(sync: bool = True) -> None:
+    """Raise RuntimeError if a kernel reported results that must not be used
+    (sync=True first waits for all queued work on every stream)."""
+    if sync and torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+    w = device_errors()
+    if w:
+        what = _DEVERR_TEXT.get(w, f"device error code {w}")
+        raise RuntimeError(f"hlhgat: {what}; results since the last clear_device_errors() are "
+                           f"invalid")
 
 
 # ----------------------------------------------------------------------------

@@ -198,6 +198,10 @@ class TrainStep:
         return ent
 
     def __call__(self, batch) -> torch.Tensor:
+        # a kernel of an earlier step that reported unusable results (the
+        # device error word, read without synchronising) stops training here
+        if self._ext is not None:
+            ops.check_device_errors(sync=False)
         if not self.graphs:
             return self._eager(batch)
         key = batch_key(batch)

@@ -302,22 +302,6 @@ int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_edge,
                        float* val_l0, const int32_t* rowptr_l1, int32_t* col_l1,
                        float* val_l1, void* stream);
 
-/* ---- graph-local fused conv forward ------------------------------------ */
-/* out = sum_k T_k W_k^T + bias with T_0 = X and T_1..T_{K-1} the basis of
- * hlhgat_poly_basis_fwd (LAGUERRE or CHEB), in ONE launch for block-diagonal
- * batches of small graphs (graph tiles of <= 64 rows, hodge_dataset.
- * graph_tiles): a workgroup keeps its tile's X and T_k in LDS and projects
- * each T_k while it is resident (HodgeLaguerreConv.forward,
- * lib/Hodge_Cheb_Conv.py:480-515).  Needs F = d_out = 64, 2 <= K <= 16,
- * 16-B aligned operands.  T (K-1 blocks [n][F]) is written for the backward.
- * Bitwise equal to hlhgat_poly_basis_fwd + hlhgat_proj_fwd. */
-int hlhgat_conv_local_fwd(int kind, const int32_t* rowptr, const int32_t* col,
-                          const float* val, int64_t n, int64_t nnz, const int32_t* tile_ptr,
-                          int64_t n_tiles, int64_t max_tile_rows, int64_t max_tile_nnz,
-                          const float* X, int64_t ldx, int64_t F, int K, float* T,
-                          const float* const* W, const int64_t* ldw, const float* bias,
-                          int64_t d_out, float* C, int64_t ldc, void* stream);
-
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
 #define HLHGAT_MAX_BLOCKS 16
 
@@ -369,22 +353,6 @@ int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
                     const int64_t* ldw, const int64_t* kb_d, float* const* dA,
                     const int64_t* ldda, float* workspace, int64_t workspace_floats,
                     void* stream);
-
-/* hlhgat_proj_bwd with the BatchNorm1d (+ReLU) backward in front of it
- * folded into the dC operand loads (lib/Hodge_ST_Model.py:556-566 conv -> BN
- * -> ReLU backward): dC = coef[0] g' + (coef[1] x + coef[2]) per channel with
- * g' = dy masked by bn_y > 0 (bn_y NULL: no ReLU) and rows >= *n_valid zero,
- * the coefficients from hlhgat_bn_bwd_reduce.  Bit-identical to
- * hlhgat_bn_bwd_apply into a buffer followed by hlhgat_proj_bwd, which is
- * what runs (into dz_scratch, [M][N]) when the operands are not 16-B aligned. */
-int hlhgat_proj_bwd_bn(int64_t M, int64_t N, const float* dy, int64_t lddy,
-                       const float* bn_x, int64_t ldx, const float* bn_y, int64_t ldy,
-                       const float* coef, const int32_t* n_valid, int nb_w,
-                       const float* const* A, const int64_t* lda, const int64_t* kb_w,
-                       float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
-                       const float* const* W, const int64_t* ldw, const int64_t* kb_d,
-                       float* const* dA, const int64_t* ldda, float* dz_scratch,
-                       float* workspace, int64_t workspace_floats, void* stream);
 
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
@@ -462,51 +430,22 @@ int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_val
                     const float* weight, const float* bias, const float* save_mean,
                     const float* save_invstd, int relu, float* y, int64_t ldy, void* stream);
 
-/* Projection + BatchNorm statistics in one launch: C = sum_b A_b W_b^T + bias
- * (hlhgat_proj_fwd, accumulate = 0), and the training-mode BatchNorm1d
- * statistics of C's first min(M, *n_valid) rows (as hlhgat_bn_stats_train)
- * formed in the GEMM epilogue: fp64 column partials of every 64-row tile,
- * combined by a deterministic two-level last-arriver tree, so the separate
- * statistics pass over C (a launch and a full read per BatchNorm) is gone.
- * The conv -> BN tail of every HL block (lib/Hodge_ST_Model.py:556-566) and
- * the second Linear -> BN of NodeEdgeInt's WV_* (lib/Hodge_Cheb_Conv.py:
- * 276-289).  Follow with hlhgat_bn_apply.  Shapes the fused epilogue does not
- * cover (unaligned operands) fall back to hlhgat_proj_fwd +
- * hlhgat_bn_stats_train on the same workspace (same results up to fp64
- * summation order).  Workspace: hlhgat_proj_fwd_bn_workspace_bytes(M, N),
- * zero-filled before its first use, not shared by concurrent launches; the
- * kernels leave it reusable. */
-int64_t hlhgat_proj_fwd_bn_workspace_bytes(int64_t M, int64_t N);
-int hlhgat_proj_fwd_bn(int nblocks, const float* const* A, const int64_t* lda,
-                       const float* const* W, const int64_t* ldw, const int64_t* kb,
-                       int64_t M, int64_t N, const float* bias, float* C, int64_t ldc,
-                       const int32_t* n_valid, float* running_mean, float* running_var,
-                       int64_t* num_batches_tracked, float momentum, float eps,
-                       float* save_mean, float* save_invstd, void* workspace,
-                       int64_t workspace_bytes, void* stream);
-
-/* The statistics half of hlhgat_bn_bwd_train: dweight / dbias (each may be
- * NULL) and the per-channel coefficients coef[3][C] of dx = coef[0] g' +
- * (coef[1] x + coef[2]); no dx. */
-int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                         const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
-                         int64_t C, const float* weight, const float* save_mean,
-                         const float* save_invstd, float* coef, float* dweight, float* dbias,
-                         void* workspace, int64_t workspace_bytes, void* stream);
-
-/* The apply half: dx from hlhgat_bn_bwd_reduce's coefficients. */
-int hlhgat_bn_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                        const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
-                        int64_t C, const float* coef, float* dx, int64_t lddx, void* stream);
-
 /* BatchNorm forward statistics and normalisation in one launch
- * (k_bn_train_fused, grids of <= 256 workgroups) or as two; default 1
- * (env HLHGAT_BN_ONE_LAUNCH).  Both give bitwise the same results. */
+ * (k_bn_train_fused) or as two; default 1 (env HLHGAT_BN_ONE_LAUNCH=0 turns it
+ * off).  Both give bitwise the same results.  The one launch is taken only
+ * when its grid (<= 256 workgroups) fits in a quarter of the device's
+ * resident-workgroup capacity (occupancy x CUs), so every waiting workgroup's
+ * finaliser is co-resident; the wait is still bounded, and a workgroup that
+ * gives up writes NaN rows (never stale statistics), counts the timeout and
+ * raises HLHGAT_DEVERR_BN_WAIT in the device error word. */
 int hlhgat_set_bn_one_launch(int on);
+int hlhgat_get_bn_one_launch(void);
+/* Test hook: polls before a waiting workgroup gives up (default 2^22;
+ * 0 = give up at once, which forces the timeout path). */
+int hlhgat_set_bn_poll_limit(unsigned limit);
 
 /* Times a one-launch BatchNorm workgroup gave up waiting for its tile's
- * statistics (bounded wait; never expected, results would be wrong): reads
- * the device counter (synchronising). */
+ * statistics: reads the device counter (synchronising). */
 int hlhgat_bn_wait_timeouts(unsigned* out);
 
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
@@ -530,6 +469,16 @@ int hlhgat_zero_fill(void* p, size_t bytes, void* stream);
 int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
                           float* const* dst, const int64_t* ldd, const int64_t* rows,
                           const int64_t* cols, void* stream);
+
+/* ---- device error word ------------------------------------------------- */
+/* A host-visible (pinned, mapped) word that kernels raise bits in when they
+ * detect a condition whose results must not be used.  Reading it does not
+ * synchronise: it shows what kernels that have completed so far reported
+ * (callers synchronise first for an exact answer).  hlhgat.ops.
+ * check_device_errors / hlhgat.train.TrainStep raise RuntimeError on it. */
+#define HLHGAT_DEVERR_BN_WAIT 1u /* one-launch BatchNorm wait timed out (NaN rows) */
+int hlhgat_device_errors(unsigned* out);
+int hlhgat_clear_device_errors(void);
 
 /* ---- live kernel timing ------------------------------------------------ */
 #define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */

@@ -864,108 +864,6 @@ def test_tsp_model_factored_vs_reference_golden(cuda):
         close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
 
 
-# ---------------------------------------------------------------------------
-# projection + BatchNorm statistics in the GEMM epilogue (hlhgat_proj_fwd_bn)
-# ---------------------------------------------------------------------------
-@pytest.mark.parametrize("M,N,kbs,nvalid", [(1000, 64, [64, 64, 64], None), (63, 32, [36], None),
-                                            (70001, 64, [128, 64], 69000), (5000, 256, [192], 4999),
-                                            (777, 16, [20, 8], None), (300, 48, [18, 18], 290)])
-def test_proj_fwd_bn_stats_match_torch(cuda, M, N, kbs, nvalid):
-    """C equals hlhgat_proj_fwd bitwise; mean / invstd / running stats /
-    num_batches_tracked equal a float64 torch evaluation over the first
-    n_valid rows (1e-6 relative); both the fused epilogue (kb % 4 == 0) and the
-    unfused fallback (kb = 18, 20) are exercised; the workspace is reused."""
-    import ctypes as C
-    from hlhgat import _lib, ops
-    g = torch.Generator().manual_seed(M + N)
-    As = [torch.randn(M, k, generator=g).to(cuda) for k in kbs]
-    W = torch.randn(N, sum(kbs), generator=g).to(cuda)
-    Ws, o = [], 0
-    for k in kbs:
-        Ws.append(W[:, o:o + k])
-        o += k
-    bias = torch.randn(N, generator=g).to(cuda)
-    ref_C = torch.empty(M, N, device=cuda)
-    ops._proj_fwd(As, Ws, M, N, bias, ref_C)
-    wsb = int(_lib.LIB.hlhgat_proj_fwd_bn_workspace_bytes(M, N))
-    ws = torch.zeros(wsb, dtype=torch.uint8, device=cuda)
-    nv = torch.tensor([nvalid], dtype=torch.int32, device=cuda) if nvalid else None
-    n_eff = nvalid or M
-    rm, rv = torch.zeros(N, device=cuda), torch.ones(N, device=cuda)
-    nbt = torch.zeros(1, dtype=torch.int64, device=cuda)
-    arr = lambda ct, v: (ct * len(v))(*v)  # noqa: E731
-    for it in range(2):
-        Cm = torch.empty(M, N, device=cuda)
-        mean, invstd = torch.empty(N, device=cuda), torch.empty(N, device=cuda)
-        _lib.check(_lib.LIB.hlhgat_proj_fwd_bn(
-            len(kbs), arr(C.c_void_p, [a.data_ptr() for a in As]), arr(C.c_int64, [a.stride(0) for a in As]),
-            arr(C.c_void_p, [w.data_ptr() for w in Ws]), arr(C.c_int64, [w.stride(0) for w in Ws]),
-            arr(C.c_int64, kbs), M, N, bias.data_ptr(), Cm.data_ptr(), N,
-            nv.data_ptr() if nv is not None else None, rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(),
-            0.1, 1e-5, mean.data_ptr(), invstd.data_ptr(), ws.data_ptr(), wsb,
-            torch.cuda.current_stream().cuda_stream), "proj_fwd_bn")
-        torch.cuda.synchronize()
-        assert torch.equal(Cm, ref_C)
-        x = ref_C[:n_eff].double()
-        var, mu = torch.var_mean(x, dim=0, unbiased=False)
-        close(mean.cpu(), mu.cpu(), 1e-6, "mean")
-        close(invstd.cpu(), (1.0 / torch.sqrt(var + 1e-5)).cpu(), 1e-6, "invstd")
-    assert int(nbt.item()) == 2
-    unb = torch.var(x, dim=0, unbiased=True)
-    close(rm.cpu(), (0.19 * mu).float().cpu(), 1e-5, "running_mean")
-    close(rv.cpu(), (0.81 + 0.19 * unb).float().cpu(), 1e-5, "running_var")
-
-
-def test_fused_bn_stats_conv_matches_unfused(cuda):
-    """conv -> BN -> ReLU node and the NodeEdgeInt MLP with the statistics from
-    the GEMM epilogue equal the separate statistics pass (forward, dX, weight
-    and BN gradients, running stats) to fp64-summation-order noise."""
-    import hlhgat
-    from hlhgat import ops
-    from hlhgat.synthetic import zinc_like_batch
-    b = zinc_like_batch(64, seed=3).to(cuda)
-    torch.manual_seed(0)
-    conv = hlhgat.HodgeLaguerreConv(32, 64, K=3).to(cuda)
-    nei = hlhgat.NodeEdgeInt(d=32, dv=64).to(cuda).train()
-    bn = torch.nn.BatchNorm1d(64).to(cuda)
-    xs = torch.randn(b.x_s.shape[0], 32, device=cuda)
-    xt = torch.randn(b.x_t.shape[0], 32, device=cuda)
-    from hlhgat.hodge_dataset import adj2par1, degree
-    outs = []
-    sd_bn = {k: v.clone() for k, v in bn.state_dict().items()}
-    sd_nei = {k: v.clone() for k, v in nei.state_dict().items()}
-    try:
-        for fused in (True, False):
-            bn.load_state_dict(sd_bn)  # same running statistics before each pass
-            nei.load_state_dict(sd_nei)
-            ops._ext.set_fused_bn_stats(fused)
-            ops.clear_caches()
-            x = xs.clone().requires_grad_(True)
-            op = ops.hodge_operator(b.edge_index_s, b.edge_weight_s, b.x_s.shape[0])
-            y = ops.hodge_poly_conv(x, op, [l.weight for l in conv.lins], conv.bias,
-                                    ops.POLY_LAGUERRE, bn=bn, relu=True)
-            par = adj2par1(b.edge_index, b.x_t.shape[0], b.x_s.shape[0])
-            D = degree(b.edge_index.view(-1), num_nodes=b.x_t.shape[0]) + 1e-6
-            t1, s1 = nei(xt, x, par, D)
-            w = torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)
-            ((y * w).sum() + (t1 * t1).sum() + (s1 * w).sum()).backward()
-            outs.append({"y": y.detach().cpu(), "t1": t1.detach().cpu(), "gx": x.grad.cpu(),
-                         "gw": conv.lins[1].weight.grad.cpu().clone(),
-                         "gbn": bn.weight.grad.cpu().clone(), "rm": bn.running_mean.cpu().clone(),
-                         "gnei": [p.grad.cpu().clone() for p in nei.parameters() if p.grad is not None]})
-            conv.zero_grad()
-            nei.zero_grad()
-            bn.zero_grad()
-    finally:
-        ops._ext.set_fused_bn_stats(False)
-    for k in outs[0]:
-        if k == "gnei":
-            for a, c in zip(outs[0][k], outs[1][k]):
-                close(a, c, 1e-4, "NodeEdgeInt grad")
-        else:
-            close(outs[0][k], outs[1][k], 1e-5 if k in ("y", "t1", "rm") else 1e-4, k)
-
-
 @pytest.mark.parametrize("side,factored", [("t", False), ("s", False), ("s", True)])
 def test_brain_skeleton_conv_vs_reference_golden(cuda, side, factored):
     """HodgeLaguerreConv(8, 8, K=3) on the reference's brain skeleton
@@ -1064,58 +962,13 @@ def test_device_hodge_builder_matches_reference(cuda):
     close(lam_d.cpu(), torch.tensor(lams), 2e-6, "lanczos lmax")
 
 
-@pytest.mark.parametrize("kind,K", [("lag", 2), ("lag", 3), ("lag", 4), ("cheb", 3)])
-@pytest.mark.parametrize("side", ["t", "s"])
-def test_fused_local_conv_bitwise_equals_unfused(cuda, kind, K, side):
-    """hlhgat_conv_local_fwd (basis + projection of a whole-graph tile in one
-    launch) == hlhgat_poly_basis_fwd + hlhgat_proj_fwd bitwise: conv -> BN ->
-    ReLU output, the saved basis (through dX) and every gradient (ZINC-like
-    batch, graph tiles from collate, 64 features in and out)."""
-    import hlhgat
-    from hlhgat import ops
-    from hlhgat.synthetic import zinc_like_batch
-    b = zinc_like_batch(96, seed=21).to(cuda)
-    ei, w = getattr(b, "edge_index_" + side), getattr(b, "edge_weight_" + side)
-    n = getattr(b, "x_" + side).shape[0]
-    assert getattr(ei, "_hlhgat_tiles", None) is not None
-    torch.manual_seed(1)
-    cls = hlhgat.HodgeLaguerreConv if kind == "lag" else hlhgat.HodgeChebConv
-    conv = cls(64, 64, K=K).to(cuda)
-    with torch.no_grad():
-        conv.bias.uniform_(-0.5, 0.5)
-    bn = torch.nn.BatchNorm1d(64).to(cuda)
-    sd_bn = {k: v.clone() for k, v in bn.state_dict().items()}
-    x0 = torch.randn(n, 64, device=cuda)
-    res = []
-    try:
-        for fused in (True, False):
-            ops._ext.set_fused_conv(fused)
-            bn.load_state_dict(sd_bn)
-            ops.clear_caches()
-            op = ops.hodge_operator(ei, w, n)
-            x = x0.clone().requires_grad_(True)
-            y = ops.hodge_poly_conv(x, op, [l.weight for l in conv.lins], conv.bias,
-                                    ops.POLY_LAGUERRE if kind == "lag" else ops.POLY_CHEB,
-                                    bn=bn, relu=True)
-            (y * torch.linspace(-1, 1, y.numel(), device=cuda).view_as(y)).sum().backward()
-            res.append([y.detach().clone(), x.grad.clone(), conv.bias.grad.clone()] +
-                       [l.weight.grad.clone() for l in conv.lins])
-            conv.zero_grad()
-    finally:
-        ops._ext.set_fused_conv(False)
-    for a, c in zip(*res):
-        assert torch.equal(a, c)
-
-
-def _grads_with_fused_bwd(fused, run, fold=True):
+def _grads_with_fused_bwd(fused, run):
     from hlhgat import ops
     try:
         ops._ext.set_fused_bwd(fused)
-        ops._ext.set_fold_bn_bwd(fold)
         return run()
     finally:
         ops._ext.set_fused_bwd(True)
-        ops._ext.set_fold_bn_bwd(False)
 
 
 @pytest.mark.parametrize("M", [37, 5000, 70000])
@@ -1149,8 +1002,7 @@ def test_fused_linear_backward_bitwise(cuda, M):
 @pytest.mark.parametrize("padded", [False, True])
 def test_fused_backward_zinc_model_bitwise(cuda, padded):
     """Every parameter gradient of the ZINC head (conv projections, NodeEdgeInt
-    MLPs, readout MLP) is bitwise the same with the fused Linear backward, with
-    and without the conv BatchNorm backward folded into its operand loads, as
+    MLPs, readout MLP) is bitwise the same with the fused Linear backward as
     with the separate launches; padded: static-shape capacity rows (n_valid)."""
     import hlhgat
     from hlhgat.hodge_dataset import pad_batch, static_caps
@@ -1167,13 +1019,11 @@ def test_fused_backward_zinc_model_bitwise(cuda, padded):
                                                 keig=15).to(cuda).train()
         torch.nn.functional.l1_loss(m(b).view(-1), b.y.view(-1)).backward()
         return {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
-    a = _grads_with_fused_bwd(True, run, fold=True)
-    f = _grads_with_fused_bwd(True, run, fold=False)
+    a = _grads_with_fused_bwd(True, run)
     c = _grads_with_fused_bwd(False, run)
-    assert a.keys() == c.keys() == f.keys() and len(a) > 100
+    assert a.keys() == c.keys() and len(a) > 100
     for k in a:
         assert torch.equal(a[k], c[k]), k
-        assert torch.equal(f[k], c[k]), k
 
 
 @pytest.mark.parametrize("n,C,relu,pad", [(700, 64, True, 0), (25600, 64, True, 333),
@@ -1192,6 +1042,7 @@ def test_bn_one_launch_bitwise(cuda, n, C, relu, pad):
     R = torch.randn(n, C, generator=g).to(cuda)
     valid = torch.tensor([n - pad], dtype=torch.int32, device=cuda) if pad else None
     outs = []
+    prior = int(_lib.LIB.hlhgat_get_bn_one_launch())
     try:
         for one in (1, 0):
             _lib.check(_lib.LIB.hlhgat_set_bn_one_launch(one), "set_bn_one_launch")
@@ -1206,7 +1057,8 @@ def test_bn_one_launch_bitwise(cuda, n, C, relu, pad):
             outs.append([y.detach(), x.grad, bn.weight.grad, bn.bias.grad, bn.running_mean,
                          bn.running_var])
     finally:
-        _lib.LIB.hlhgat_set_bn_one_launch(1)
+        _lib.LIB.hlhgat_set_bn_one_launch(prior)
+    ops.check_device_errors()
     import ctypes
     t = ctypes.c_uint(7)
     _lib.check(_lib.LIB.hlhgat_bn_wait_timeouts(ctypes.addressof(t)), "bn_wait_timeouts")
@@ -1220,3 +1072,42 @@ def test_bn_one_launch_bitwise(cuda, n, C, relu, pad):
         ref = ref.clamp_min(0)
     close(outs[0][0][:nv].cpu(), ref.float().cpu(), 1e-5, "bn forward vs fp64")
     assert not outs[0][0][nv:].any()
+
+
+def test_bn_one_launch_timeout_raises(cuda):
+    """A one-launch BatchNorm workgroup that gives up waiting (forced here with
+    the test hook: poll limit 0) writes NaN rows, never stale statistics, and
+    raises the device error word: ops.check_device_errors and TrainStep raise
+    instead of returning numbers."""
+    import hlhgat
+    from hlhgat import _lib, ops
+    from hlhgat.train import TrainStep
+    from hlhgat.synthetic import zinc_like_batch
+    prior = int(_lib.LIB.hlhgat_get_bn_one_launch())
+    ops.check_device_errors()  # clean before
+    try:
+        _lib.check(_lib.LIB.hlhgat_set_bn_one_launch(1), "set_bn_one_launch")
+        _lib.check(_lib.LIB.hlhgat_set_bn_poll_limit(0), "set_bn_poll_limit")
+        bn = torch.nn.BatchNorm1d(64).to(cuda).train()
+        x = torch.randn(25600, 64, device=cuda)
+        y = ops.batch_norm_act(x, bn, relu=True)
+        with pytest.raises(RuntimeError, match="BatchNorm"):
+            ops.check_device_errors()
+        assert torch.isnan(y).any()  # the waiting workgroups' rows
+        ops.clear_device_errors()
+        b = zinc_like_batch(64, seed=2).to(cuda)
+        torch.manual_seed(0)
+        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[1], filters=[64], mlp_channels=[64],
+                                                K=3, keig=15).to(cuda).train()
+        step = TrainStep(m, lambda out, bb: torch.nn.functional.l1_loss(out.view(-1),
+                                                                        bb.y.view(-1)),
+                         graphs=False)
+        with pytest.raises(RuntimeError, match="BatchNorm"):
+            step(b)
+            torch.cuda.synchronize()
+            step(b)
+    finally:
+        _lib.LIB.hlhgat_set_bn_poll_limit(1 << 22)
+        _lib.LIB.hlhgat_set_bn_one_launch(prior)
+        torch.cuda.synchronize()
+        ops.clear_device_errors()
