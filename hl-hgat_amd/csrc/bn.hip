@@ -9,13 +9,13 @@
 //                      and, in the LAST workgroup to arrive, the final mean /
 //                      invstd and the running-stat update (deterministic: the
 //                      last arriver sums the partials in workgroup order);
-//        k_bn_apply  — y = relu?(x * s + t).
+//        k_bn_apply  — y = relu?((x - mean) * s + bias).
 //        (default: k_bn_train_fused, both in ONE launch when the grid is
 //        provably co-resident; see hlhgat_bn_fwd_train)
 //   bwd: k_bn_bwd_reduce — partials of sum(g) and sum(g*(x-mean)), g = dy *
 //                      [y > 0]; the last arriver forms dweight, dbias and the
 //                      per-channel coefficients of dx;
-//        k_bn_bwd_apply  — dx = a*g + b*x + c.
+//        k_bn_bwd_apply  — dx = a*g + b*(x - mean) + c (centred: no cancellation).
 // Inter-workgroup hand-off follows MI355X_MICROARCH.md / cdna_hip_programming.md
 // Guideline 16: plain stores, every wave's vmcnt(0), barrier, lane-0 agent
 // release fence, relaxed agent atomic ticket; the last arriver issues an
@@ -468,13 +468,13 @@ __device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArg
   // a timed-out workgroup poisons its rows (NaN) instead of applying stale statistics
   const bool ok = fin || wait_flag(flag, a.poll_limit, a.err);
   if (c < a.C) {
-    float sc[V], sh[V];
+    float sc[V], mu[V], sh[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float w = p.weight ? p.weight[c + v] : 1.f;
-      const float b = p.bias ? p.bias[c + v] : 0.f;
       sc[v] = ok ? w * ld_wt32(&p.invstd[c + v]) : __builtin_nanf("");
-      sh[v] = ok ? b - ld_wt32(&p.mean[c + v]) * sc[v] : __builtin_nanf("");
+      mu[v] = ok ? ld_wt32(&p.mean[c + v]) : __builtin_nanf("");
+      sh[v] = p.bias ? p.bias[c + v] : 0.f;
     }
     int64_t r_end = r_lo + a.rows_per_part;
     if (r_end > a.n) r_end = a.n;
@@ -482,7 +482,7 @@ __device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArg
       vt o;
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        float z = vget(xv, v) * sc[v] + sh[v];
+        float z = (vget(xv, v) - mu[v]) * sc[v] + sh[v];
         vget(o, v) = r >= n_eff ? 0.f : ((p.relu && z < 0.f) ? 0.f : z);  // NaN passes
       }
       vstore<V>(p.y + r * p.ldy + c, o);
@@ -533,13 +533,14 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
   const int rg = threadIdx.x / a.tpr;
   const int c = blockIdx.y * a.tpr * V + cl * V;
   if (c >= a.C) return;
-  float s[V], t[V];
+  float s[V], m[V], t[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const float w = a.weight ? a.weight[c + v] : 1.f;
     const float b = a.bias ? a.bias[c + v] : 0.f;
     s[v] = w * a.invstd[c + v];
-    t[v] = b - a.mean[c + v] * s[v];
+    m[v] = a.mean[c + v];
+    t[v] = b;
   }
   // APPLY_RPT rows per thread, all loads issued before any store
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
@@ -557,7 +558,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
     vt o;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      float z = vget(xv[u], v) * s[v] + t[v];
+      float z = (vget(xv[u], v) - m[v]) * s[v] + t[v];
       vget(o, v) = r >= n_eff ? 0.f : ((a.relu && z < 0.f) ? 0.f : z);
     }
     vstore<V>(a.y + r * a.ldy + c, o);
@@ -577,6 +578,7 @@ struct BwdApplyArgs {
   int64_t n;
   int C;
   const float* coef;
+  const float* mean;
   int tpr, rp;
 };
 
@@ -645,10 +647,12 @@ __device__ __forceinline__ void bn_bwd_body(const StatsArgs& a) {
     const double nn = (double)(n_eff > 0 ? n_eff : 1);
     if (a.dweight) a.dweight[cc] = (float)(sgx * is);
     if (a.dbias) a.dbias[cc] = (float)sg;
-    // dx = w*is*(g - sg/n - (x-mean)*is^2*sgx/n) = A*g + B*x + Cc
+    // dx = w*is*(g - sg/n - (x-mean)*is^2*sgx/n) = A*g + B*(x-mean) + Cc: the
+    // centred form, as torch evaluates it -- B*x + (Cc - B*mean) cancels
+    // catastrophically when a channel's variance is small against its mean
     const double A = w * is;
     const double B = -w * is * is * is * sgx / nn;
-    const double Cc = -w * is * sg / nn - B * (double)a.save_mean[cc];
+    const double Cc = -w * is * sg / nn;
     a.coef[cc] = (float)A;
     a.coef[a.C + cc] = (float)B;
     a.coef[2 * a.C + cc] = (float)Cc;
@@ -667,12 +671,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
   const int rg = threadIdx.x / a.tpr;
   const int c = blockIdx.y * a.tpr * V + cl * V;
   if (c >= a.C) return;
-  float A[V], B[V], Cc[V];
+  float A[V], B[V], Cc[V], mu[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     A[v] = a.coef[c + v];
     B[v] = a.coef[a.C + c + v];
     Cc[v] = a.coef[2 * a.C + c + v];
+    mu[v] = a.mean[c + v];
   }
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
   const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
@@ -695,7 +700,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     for (int v = 0; v < V; ++v) {
       float g = vget(gv[u], v);
       if (a.y && !(vget(yv[u], v) > 0.f)) g = 0.f;
-      vget(o, v) = r >= n_eff ? 0.f : A[v] * g + (B[v] * vget(xv[u], v) + Cc[v]);
+      vget(o, v) = r >= n_eff ? 0.f : A[v] * g + (B[v] * (vget(xv[u], v) - mu[v]) + Cc[v]);
     }
     vstore<V>(a.dx + r * a.lddx + c, o);
   }
@@ -916,7 +921,8 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   else
     k_bn_bwd_reduce<1, kThreads><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
-  BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, L.tpr, L.rp};
+  BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, save_mean,
+                 L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
     k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);

@@ -1333,6 +1333,439 @@ std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids
   return {r[0], r[1]};
 }
 
+
+// ---------------------------------------------------------------------------
+// torch.ops.hlhgat: the native op boundary of SURVEY.md §8(b), registered with
+// the dispatcher (schemas, HIP kernels under the CUDA key -- PyTorch-ROCm's
+// key for device tensors --, Meta kernels for FakeTensor / torch.compile
+// tracing, and Autograd kernels whose backward is itself a registered op).
+// Contract: fp32 features, int32 CSR, outputs allocated on x's device, the
+// current stream, errors as RuntimeError (TORCH_CHECK), no host sync.
+//
+//   spmm(rowptr, col, val?, x, t_rowptr?, t_col?, t_val?) -> y = A x
+//       PyG propagate over a CSR keyed by edge_index[1] (lib/Hodge_Cheb_Conv.py:
+//       442-443,518-519); the backward multiplies by A^T, given as the t_*
+//       CSR or, when omitted, A itself (every Hodge Laplacian is symmetric).
+//       Edge weights are data (no gradient), as in the reference models.
+//   poly_basis(rowptr, col, val?, x, K, kind, t_*?) -> T [K-1, n, F]
+//       T_1..T_{K-1} of the Laguerre (kind 0, :480-515), Chebyshev (1,
+//       :394-439) or DEMO (2) recurrence; backward = the adjoint recurrence.
+//   proj(A[], W, bias?) -> F.linear(cat(A, -1), W, bias) on fp32 MFMA
+//       (the HodgeLaguerreConv projections and Linear(cat[..]), :307-308).
+//   att_score(Qc, Qs, K, w_cross, w_self, sqrt_dk, sigma) -> a [n, 1]
+//       NodeEdgeInt only_att (:297-305), sigma 0 = Sigmoid, 1 = ReLU.
+//   segment_mean(x, seg_ptr, seg_rows?, n_seg) -> [n_seg, d]
+//       global_mean_pool / scatter_mean.
+//   csr_from_coo(row, col, val?, n_rows, sorted) -> (rowptr, col, val)
+// ---------------------------------------------------------------------------
+inline void req_i32(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.dim() == 1 && t.is_contiguous(),
+              "hlhgat: ", name, " must be a contiguous int32 1-D ROCm tensor");
+}
+inline void req_csr(const Tensor& rowptr, const Tensor& col, const OptT& val) {
+  req_i32(rowptr, "rowptr");
+  req_i32(col, "col");
+  TORCH_CHECK(rowptr.numel() >= 1, "hlhgat: rowptr needs n_rows + 1 >= 1 entries");
+  TORCH_CHECK(col.numel() < ((int64_t)1 << 31), "hlhgat: nnz must be < 2^31");
+  if (has(val))
+    TORCH_CHECK(val->is_cuda() && val->scalar_type() == at::kFloat && val->is_contiguous() &&
+                    val->numel() == col.numel(),
+                "hlhgat: val must be contiguous fp32 with one entry per column index");
+}
+inline void req_x(const Tensor& x, const char* name) {
+  req(x, name);
+  TORCH_CHECK(x.dim() == 2, "hlhgat: ", name, " must be 2-D");
+}
+
+Tensor spmm_hip(const Tensor& rowptr, const Tensor& col, const OptT& val, const Tensor& x,
+                const OptT& t_rowptr, const OptT& t_col, const OptT& t_val) {
+  (void)t_rowptr, (void)t_col, (void)t_val;
+  req_csr(rowptr, col, val);
+  req_x(x, "x");
+  const int64_t n = rowptr.numel() - 1, nnz = col.numel();
+  Tensor xc = rows2d(x);
+  Tensor y = at::empty({n, xc.size(1)}, xc.options());
+  if (n > 0 && xc.size(1) > 0)
+    chk(hlhgat_spmm(rowptr.data_ptr<int>(), nnz ? col.data_ptr<int>() : nullptr,
+                    nnz ? fptr(val) : nullptr, n, nnz, nullptr, nullptr, xc.data_ptr<float>(),
+                    ld_of(xc), xc.size(1), y.data_ptr<float>(), ld_of(y), stream_of(xc)),
+        "spmm");
+  return y;
+}
+Tensor spmm_meta(const Tensor& rowptr, const Tensor& col, const OptT& val, const Tensor& x,
+                 const OptT&, const OptT&, const OptT&) {
+  (void)col, (void)val;
+  return at::empty_symint({rowptr.sym_size(0) - 1, x.sym_size(1)}, x.options());
+}
+
+Tensor poly_basis_hip(const Tensor& rowptr, const Tensor& col, const OptT& val, const Tensor& x,
+                      int64_t K, int64_t kind, const OptT&, const OptT&, const OptT&) {
+  req_csr(rowptr, col, val);
+  req_x(x, "x");
+  TORCH_CHECK(K >= 1 && kind >= 0 && kind <= 2, "hlhgat: poly_basis needs K >= 1, kind 0..2");
+  const int64_t n = rowptr.numel() - 1, nnz = col.numel();
+  TORCH_CHECK(x.size(0) == n, "hlhgat: x has ", x.size(0), " rows, the operator ", n);
+  Tensor xc = rows2d(x);
+  const int64_t F = xc.size(1);
+  Tensor T = at::empty({K - 1, n, F}, xc.options());
+  if (K > 1 && n > 0 && F > 0)
+    chk(hlhgat_poly_basis_fwd((int)kind, rowptr.data_ptr<int>(),
+                              nnz ? col.data_ptr<int>() : nullptr, nnz ? fptr(val) : nullptr, n,
+                              nnz, nullptr, nullptr, nullptr, 0, 0, 0, xc.data_ptr<float>(),
+                              ld_of(xc), F, (int)K, T.data_ptr<float>(), stream_of(xc)),
+        "poly_basis_fwd");
+  return T;
+}
+Tensor poly_basis_meta(const Tensor& rowptr, const Tensor&, const OptT&, const Tensor& x,
+                       int64_t K, int64_t, const OptT&, const OptT&, const OptT&) {
+  return at::empty_symint({c10::SymInt(K - 1), rowptr.sym_size(0) - 1, x.sym_size(1)},
+                          x.options());
+}
+
+// gx of poly_basis given dT [K-1, n, F] (the adjoint recurrence over A^T)
+Tensor poly_basis_backward_hip(const Tensor& grad, const Tensor& rowptr, const Tensor& col,
+                               const OptT& val, int64_t K, int64_t kind) {
+  req_csr(rowptr, col, val);
+  const int64_t n = rowptr.numel() - 1, nnz = col.numel();
+  TORCH_CHECK(grad.dim() == 3 && grad.size(0) == K - 1 && grad.size(1) == n,
+              "hlhgat: poly_basis_backward: grad must be [K-1, n, F]");
+  const int64_t F = grad.size(2);
+  Tensor Gs = at::empty({K, n, F}, grad.options());
+  Gs[0].zero_();
+  if (K > 1) Gs.narrow(0, 1, K - 1).copy_(grad);
+  if (K > 1 && n > 0 && F > 0)
+    chk(hlhgat_poly_basis_bwd((int)kind, rowptr.data_ptr<int>(),
+                              nnz ? col.data_ptr<int>() : nullptr, nnz ? fptr(val) : nullptr, n,
+                              nnz, nullptr, nullptr, nullptr, 0, 0, 0, F, (int)K,
+                              Gs.data_ptr<float>(), stream_of(grad)),
+        "poly_basis_bwd");
+  return Gs[0].clone();
+}
+Tensor poly_basis_backward_meta(const Tensor& grad, const Tensor&, const Tensor&, const OptT&,
+                                int64_t, int64_t) {
+  return at::empty_symint({grad.sym_size(1), grad.sym_size(2)}, grad.options());
+}
+
+Tensor proj_hip(at::TensorList A, const Tensor& W, const OptT& bias) {
+  TORCH_CHECK(!A.empty() && (int64_t)A.size() <= HLHGAT_MAX_BLOCKS, "hlhgat: proj takes 1..",
+              HLHGAT_MAX_BLOCKS, " operand blocks");
+  req(W, "W");
+  TORCH_CHECK(W.dim() == 2, "hlhgat: W must be [N, sum K_b]");
+  std::vector<Tensor> As;
+  for (const auto& a : A) {
+    req_x(a, "A_b");
+    TORCH_CHECK(a.size(0) == A[0].size(0), "hlhgat: proj blocks must have equal rows");
+    As.push_back(rows2d(a));
+  }
+  if (has(bias)) req(*bias, "bias");
+  Tensor Wc = W.stride(1) == 1 ? W : W.contiguous();
+  return linear_forward(As, Wc, bias);
+}
+Tensor proj_meta(at::TensorList A, const Tensor& W, const OptT&) {
+  return at::empty_symint({A[0].sym_size(0), W.sym_size(0)}, W.options());
+}
+std::tuple<Tensor, Tensor, std::vector<Tensor>> proj_backward_hip(const Tensor& grad,
+                                                                   at::TensorList A,
+                                                                   const Tensor& W,
+                                                                   bool has_bias) {
+  std::vector<Tensor> As;
+  for (const auto& a : A) As.push_back(rows2d(a));
+  Tensor Wc = W.stride(1) == 1 ? W : W.contiguous();
+  Tensor dW, db;
+  std::vector<Tensor> dAs;
+  linear_backward(grad, As, Wc, true, has_bias, std::vector<bool>(As.size(), true), dW, db, dAs);
+  if (!db.defined()) db = at::empty({0}, W.options());
+  return {dW, db, dAs};
+}
+std::tuple<Tensor, Tensor, std::vector<Tensor>> proj_backward_meta(const Tensor& grad,
+                                                                    at::TensorList A,
+                                                                    const Tensor& W,
+                                                                    bool has_bias) {
+  std::vector<Tensor> dAs;
+  for (const auto& a : A) dAs.push_back(at::empty_symint(a.sym_sizes(), a.options()));
+  return {at::empty_symint(W.sym_sizes(), W.options()),
+          at::empty_symint({has_bias ? W.sym_size(0) : c10::SymInt(0)}, W.options()), dAs};
+}
+
+Tensor att_score_hip(const Tensor& Qc, const Tensor& Qs, const Tensor& K, double w_cross,
+                     double w_self, double sqrt_dk, int64_t sigma) {
+  req_x(Qc, "Qc");
+  req_x(Qs, "Qs");
+  req_x(K, "K");
+  TORCH_CHECK(Qc.sizes() == K.sizes() && Qs.sizes() == K.sizes(),
+              "hlhgat: att_score: Qc, Qs and K must have one shape [n, dk]");
+  Tensor qc = rows2d(Qc), qs = rows2d(Qs), k = rows2d(K);
+  Tensor a = at::empty({k.size(0), 1}, k.options());
+  if (k.size(0) > 0)
+    chk(hlhgat_att_score_fwd(k.size(0), k.size(1), qc.data_ptr<float>(), ld_of(qc),
+                             qs.data_ptr<float>(), ld_of(qs), k.data_ptr<float>(), ld_of(k),
+                             (float)w_cross, (float)w_self, (float)sqrt_dk, (int)sigma,
+                             a.data_ptr<float>(), stream_of(k)),
+        "att_score_fwd");
+  return a;
+}
+Tensor att_score_meta(const Tensor&, const Tensor&, const Tensor& K, double, double, double,
+                      int64_t) {
+  return at::empty_symint({K.sym_size(0), c10::SymInt(1)}, K.options());
+}
+std::tuple<Tensor, Tensor, Tensor> att_score_backward_hip(const Tensor& grad, const Tensor& Qc,
+                                                          const Tensor& Qs, const Tensor& K,
+                                                          const Tensor& a, double w_cross,
+                                                          double w_self, double sqrt_dk,
+                                                          int64_t sigma) {
+  Tensor qc = rows2d(Qc), qs = rows2d(Qs), k = rows2d(K);
+  Tensor ga = grad.contiguous();
+  const int64_t n = k.size(0), dk = k.size(1);
+  Tensor g = at::empty({3, n, dk}, k.options());
+  if (n > 0)
+    chk(hlhgat_att_score_bwd(n, dk, qc.data_ptr<float>(), ld_of(qc), qs.data_ptr<float>(),
+                             ld_of(qs), k.data_ptr<float>(), ld_of(k), (float)w_cross,
+                             (float)w_self, (float)sqrt_dk, (int)sigma, a.data_ptr<float>(),
+                             ga.data_ptr<float>(), g[0].data_ptr<float>(), g[1].data_ptr<float>(),
+                             g[2].data_ptr<float>(), dk, stream_of(k)),
+        "att_score_bwd");
+  return {g[0], g[1], g[2]};
+}
+std::tuple<Tensor, Tensor, Tensor> att_score_backward_meta(const Tensor&, const Tensor& Qc,
+                                                           const Tensor& Qs, const Tensor& K,
+                                                           const Tensor&, double, double, double,
+                                                           int64_t) {
+  return {at::empty_symint(Qc.sym_sizes(), Qc.options()),
+          at::empty_symint(Qs.sym_sizes(), Qs.options()),
+          at::empty_symint(K.sym_sizes(), K.options())};
+}
+
+Tensor segment_mean_hip(const Tensor& x, const Tensor& seg_ptr, const OptT& seg_rows,
+                        int64_t n_seg) {
+  req_x(x, "x");
+  req_i32(seg_ptr, "seg_ptr");
+  TORCH_CHECK(seg_ptr.numel() == n_seg + 1, "hlhgat: seg_ptr must have n_seg + 1 entries");
+  if (has(seg_rows)) req_i32(*seg_rows, "seg_rows");
+  Tensor xc = rows2d(x);
+  Tensor out = at::empty({n_seg, xc.size(1)}, xc.options());
+  if (n_seg > 0)
+    chk(hlhgat_segment_mean_fwd(seg_ptr.data_ptr<int>(), iptr(seg_rows), n_seg,
+                                xc.data_ptr<float>(), ld_of(xc), xc.size(1),
+                                out.data_ptr<float>(), ld_of(out), stream_of(xc)),
+        "segment_mean_fwd");
+  return out;
+}
+Tensor segment_mean_meta(const Tensor& x, const Tensor&, const OptT&, int64_t n_seg) {
+  return at::empty_symint({c10::SymInt(n_seg), x.sym_size(1)}, x.options());
+}
+Tensor segment_mean_backward_hip(const Tensor& grad, const Tensor& seg_ptr, const OptT& seg_rows,
+                                 int64_t n_rows) {
+  Tensor g = rows2d(grad);
+  const int64_t n_seg = seg_ptr.numel() - 1;
+  Tensor gx = has(seg_rows) ? at::zeros({n_rows, g.size(1)}, g.options())
+                            : at::empty({n_rows, g.size(1)}, g.options());
+  if (n_seg > 0)
+    chk(hlhgat_segment_mean_bwd(seg_ptr.data_ptr<int>(), iptr(seg_rows), n_seg,
+                                g.data_ptr<float>(), ld_of(g), g.size(1), gx.data_ptr<float>(),
+                                ld_of(gx), stream_of(g)),
+        "segment_mean_bwd");
+  return gx;
+}
+Tensor segment_mean_backward_meta(const Tensor& grad, const Tensor&, const OptT&,
+                                  int64_t n_rows) {
+  return at::empty_symint({c10::SymInt(n_rows), grad.sym_size(1)}, grad.options());
+}
+
+std::tuple<Tensor, Tensor, Tensor> csr_from_coo_hip(const Tensor& row, const Tensor& col,
+                                                    const OptT& val, int64_t n_rows,
+                                                    bool sorted) {
+  TORCH_CHECK(row.is_cuda() && col.is_cuda() && row.scalar_type() == at::kLong &&
+                  col.scalar_type() == at::kLong && row.dim() == 1 && row.sizes() == col.sizes(),
+              "hlhgat: csr_from_coo needs int64 ROCm row / col of one length");
+  const int64_t nnz = row.numel();
+  TORCH_CHECK(nnz < ((int64_t)1 << 31), "hlhgat: nnz must be < 2^31");
+  Tensor r = row.contiguous(), c = col.contiguous();
+  OptT v = has(val) ? OptT(val->contiguous()) : OptT();
+  if (has(v)) req(*v, "val");
+  Tensor rowptr = at::empty({n_rows + 1}, r.options().dtype(at::kInt));
+  Tensor col32 = at::empty({nnz}, r.options().dtype(at::kInt));
+  Tensor val32 = at::empty({has(v) ? nnz : 0}, r.options().dtype(at::kFloat));
+  void* s = stream_of(r);
+  if (sorted) {
+    chk(hlhgat_csr_from_sorted_coo(r.data_ptr<int64_t>(), c.data_ptr<int64_t>(), fptr(v), nnz,
+                                   n_rows, rowptr.data_ptr<int>(), col32.data_ptr<int>(),
+                                   has(v) ? val32.data_ptr<float>() : nullptr, s),
+        "csr_from_sorted_coo");
+  } else {
+    const int64_t wsb = (int64_t)hlhgat_csr_workspace_bytes(nnz);
+    Tensor ws = at::empty({std::max<int64_t>(wsb, 1)}, r.options().dtype(at::kByte));
+    int64_t n_cols = 1;  // only bounds the sort key: any value > max(col) works
+    if (nnz) n_cols = c.max().item<int64_t>() + 1;  // host sync: general (unsorted) path only
+    chk(hlhgat_csr_from_coo(nnz ? r.data_ptr<int64_t>() : nullptr,
+                            nnz ? c.data_ptr<int64_t>() : nullptr, fptr(v), nnz, n_rows, n_cols,
+                            rowptr.data_ptr<int>(), nnz ? col32.data_ptr<int>() : nullptr,
+                            (has(v) && nnz) ? val32.data_ptr<float>() : nullptr, nullptr,
+                            ws.data_ptr(), (size_t)wsb, s),
+        "csr_from_coo");
+  }
+  return {rowptr, col32, val32};
+}
+std::tuple<Tensor, Tensor, Tensor> csr_from_coo_meta(const Tensor& row, const Tensor&,
+                                                     const OptT& val, int64_t n_rows, bool) {
+  auto o = row.options();
+  return {at::empty({n_rows + 1}, o.dtype(at::kInt)), at::empty_symint(row.sym_sizes(),
+                                                                       o.dtype(at::kInt)),
+          at::empty_symint({has(val) ? row.sym_size(0) : c10::SymInt(0)}, o.dtype(at::kFloat))};
+}
+
+// --- autograd over the dispatcher ---------------------------------------------
+template <typename Sig>
+c10::TypedOperatorHandle<Sig> op_handle(const char* name) {
+  return c10::Dispatcher::singleton().findSchemaOrThrow(name, "").typed<Sig>();
+}
+using SpmmSig = Tensor(const Tensor&, const Tensor&, const OptT&, const Tensor&, const OptT&,
+                       const OptT&, const OptT&);
+using BasisSig = Tensor(const Tensor&, const Tensor&, const OptT&, const Tensor&, int64_t, int64_t,
+                        const OptT&, const OptT&, const OptT&);
+using BasisBwdSig = Tensor(const Tensor&, const Tensor&, const Tensor&, const OptT&, int64_t,
+                           int64_t);
+using ProjSig = Tensor(at::TensorList, const Tensor&, const OptT&);
+using ProjBwdSig = std::tuple<Tensor, Tensor, std::vector<Tensor>>(const Tensor&, at::TensorList,
+                                                                   const Tensor&, bool);
+using AttSig = Tensor(const Tensor&, const Tensor&, const Tensor&, double, double, double,
+                      int64_t);
+using AttBwdSig = std::tuple<Tensor, Tensor, Tensor>(const Tensor&, const Tensor&, const Tensor&,
+                                                     const Tensor&, const Tensor&, double, double,
+                                                     double, int64_t);
+using SegSig = Tensor(const Tensor&, const Tensor&, const OptT&, int64_t);
+using SegBwdSig = Tensor(const Tensor&, const Tensor&, const OptT&, int64_t);
+
+inline Tensor opt_or_undef(const OptT& t) { return has(t) ? *t : Tensor(); }
+inline OptT undef_to_opt(const Tensor& t) { return t.defined() ? OptT(t) : OptT(); }
+
+class SpmmOp : public torch::autograd::Function<SpmmOp> {
+ public:
+  static Tensor forward(AutogradContext* ctx, const Tensor& rowptr, const Tensor& col,
+                        const OptT& val, const Tensor& x, const OptT& t_rowptr, const OptT& t_col,
+                        const OptT& t_val) {
+    at::AutoDispatchBelowADInplaceOrView g;
+    const bool t = has(t_rowptr);
+    ctx->save_for_backward({t ? *t_rowptr : rowptr, t ? *t_col : col,
+                            t ? opt_or_undef(t_val) : opt_or_undef(val)});
+    static auto op = op_handle<SpmmSig>("hlhgat::spmm");
+    return op.call(rowptr, col, val, x, t_rowptr, t_col, t_val);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    static auto op = op_handle<SpmmSig>("hlhgat::spmm");
+    Tensor gx = op.call(sv[0], sv[1], undef_to_opt(sv[2]), grads[0], OptT(), OptT(), OptT());
+    return {Tensor(), Tensor(), Tensor(), gx, Tensor(), Tensor(), Tensor()};
+  }
+};
+
+class BasisOp : public torch::autograd::Function<BasisOp> {
+ public:
+  static Tensor forward(AutogradContext* ctx, const Tensor& rowptr, const Tensor& col,
+                        const OptT& val, const Tensor& x, int64_t K, int64_t kind,
+                        const OptT& t_rowptr, const OptT& t_col, const OptT& t_val) {
+    at::AutoDispatchBelowADInplaceOrView g;
+    const bool t = has(t_rowptr);
+    ctx->save_for_backward({t ? *t_rowptr : rowptr, t ? *t_col : col,
+                            t ? opt_or_undef(t_val) : opt_or_undef(val)});
+    ctx->saved_data["K"] = K;
+    ctx->saved_data["kind"] = kind;
+    static auto op = op_handle<BasisSig>("hlhgat::poly_basis");
+    return op.call(rowptr, col, val, x, K, kind, t_rowptr, t_col, t_val);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    static auto op = op_handle<BasisBwdSig>("hlhgat::poly_basis_backward");
+    Tensor gx = op.call(grads[0].contiguous(), sv[0], sv[1], undef_to_opt(sv[2]),
+                        ctx->saved_data["K"].toInt(), ctx->saved_data["kind"].toInt());
+    return {Tensor(), Tensor(), Tensor(), gx, Tensor(), Tensor(), Tensor(), Tensor(), Tensor()};
+  }
+};
+
+class ProjOp : public torch::autograd::Function<ProjOp> {
+ public:
+  static Tensor forward(AutogradContext* ctx, const Tensor& W, const OptT& bias,
+                        at::TensorList A) {
+    at::AutoDispatchBelowADInplaceOrView g;
+    std::vector<Tensor> save(A.begin(), A.end());
+    save.push_back(W);
+    ctx->save_for_backward(save);
+    ctx->saved_data["has_b"] = has(bias);
+    static auto op = op_handle<ProjSig>("hlhgat::proj");
+    return op.call(A, W, bias);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    Tensor W = sv.back();
+    std::vector<Tensor> A(sv.begin(), sv.end() - 1);
+    const bool hb = ctx->saved_data["has_b"].toBool();
+    static auto op = op_handle<ProjBwdSig>("hlhgat::proj_backward");
+    auto r = op.call(grads[0], A, W, hb);
+    variable_list out = {std::get<0>(r), hb ? std::get<1>(r) : Tensor()};
+    for (auto& t : std::get<2>(r)) out.push_back(t);
+    return out;
+  }
+};
+
+class AttOp : public torch::autograd::Function<AttOp> {
+ public:
+  static Tensor forward(AutogradContext* ctx, const Tensor& Qc, const Tensor& Qs, const Tensor& K,
+                        double wc, double ws, double sq, int64_t sigma) {
+    at::AutoDispatchBelowADInplaceOrView g;
+    static auto op = op_handle<AttSig>("hlhgat::att_score");
+    Tensor a = op.call(Qc, Qs, K, wc, ws, sq, sigma);
+    ctx->save_for_backward({Qc, Qs, K, a});
+    ctx->saved_data["c"] = std::vector<double>{wc, ws, sq};
+    ctx->saved_data["sigma"] = sigma;
+    return a;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    auto c = ctx->saved_data["c"].toDoubleVector();
+    static auto op = op_handle<AttBwdSig>("hlhgat::att_score_backward");
+    auto r = op.call(grads[0], sv[0], sv[1], sv[2], sv[3], c[0], c[1], c[2],
+                     ctx->saved_data["sigma"].toInt());
+    return {std::get<0>(r), std::get<1>(r), std::get<2>(r), Tensor(), Tensor(), Tensor(),
+            Tensor()};
+  }
+};
+
+class SegOp : public torch::autograd::Function<SegOp> {
+ public:
+  static Tensor forward(AutogradContext* ctx, const Tensor& x, const Tensor& seg_ptr,
+                        const OptT& seg_rows, int64_t n_seg) {
+    at::AutoDispatchBelowADInplaceOrView g;
+    ctx->save_for_backward({seg_ptr, opt_or_undef(seg_rows)});
+    ctx->saved_data["n"] = x.sym_size(0).guard_int(__FILE__, __LINE__);
+    static auto op = op_handle<SegSig>("hlhgat::segment_mean");
+    return op.call(x, seg_ptr, seg_rows, n_seg);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    static auto op = op_handle<SegBwdSig>("hlhgat::segment_mean_backward");
+    return {op.call(grads[0], sv[0], undef_to_opt(sv[1]), ctx->saved_data["n"].toInt()),
+            Tensor(), Tensor(), Tensor()};
+  }
+};
+
+Tensor spmm_ad(const Tensor& rowptr, const Tensor& col, const OptT& val, const Tensor& x,
+               const OptT& tr, const OptT& tc, const OptT& tv) {
+  return SpmmOp::apply(rowptr, col, val, x, tr, tc, tv);
+}
+Tensor poly_basis_ad(const Tensor& rowptr, const Tensor& col, const OptT& val, const Tensor& x,
+                     int64_t K, int64_t kind, const OptT& tr, const OptT& tc, const OptT& tv) {
+  return BasisOp::apply(rowptr, col, val, x, K, kind, tr, tc, tv);
+}
+Tensor proj_ad(at::TensorList A, const Tensor& W, const OptT& bias) {
+  return ProjOp::apply(W, bias, A);
+}
+Tensor att_score_ad(const Tensor& Qc, const Tensor& Qs, const Tensor& K, double wc, double ws,
+                    double sq, int64_t sigma) {
+  return AttOp::apply(Qc, Qs, K, wc, ws, sq, sigma);
+}
+Tensor segment_mean_ad(const Tensor& x, const Tensor& seg_ptr, const OptT& seg_rows,
+                       int64_t n_seg) {
+  return SegOp::apply(x, seg_ptr, seg_rows, n_seg);
+}
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1349,4 +1782,59 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("node_from_edges", &node_from_edges);
   m.def("edge_from_nodes", &edge_from_nodes);
   m.def("version", []() { return hlhgat_version(); });
+}
+
+TORCH_LIBRARY(hlhgat, m) {
+  m.def("spmm(Tensor rowptr, Tensor col, Tensor? val, Tensor x, Tensor? t_rowptr=None, "
+        "Tensor? t_col=None, Tensor? t_val=None) -> Tensor");
+  m.def("poly_basis(Tensor rowptr, Tensor col, Tensor? val, Tensor x, int K, int kind, "
+        "Tensor? t_rowptr=None, Tensor? t_col=None, Tensor? t_val=None) -> Tensor");
+  m.def("poly_basis_backward(Tensor grad, Tensor rowptr, Tensor col, Tensor? val, int K, "
+        "int kind) -> Tensor");
+  m.def("proj(Tensor[] A, Tensor W, Tensor? bias) -> Tensor");
+  m.def("proj_backward(Tensor grad, Tensor[] A, Tensor W, bool has_bias) -> "
+        "(Tensor, Tensor, Tensor[])");
+  m.def("att_score(Tensor Qc, Tensor Qs, Tensor K, float w_cross, float w_self, float sqrt_dk, "
+        "int sigma) -> Tensor");
+  m.def("att_score_backward(Tensor grad, Tensor Qc, Tensor Qs, Tensor K, Tensor a, "
+        "float w_cross, float w_self, float sqrt_dk, int sigma) -> (Tensor, Tensor, Tensor)");
+  m.def("segment_mean(Tensor x, Tensor seg_ptr, Tensor? seg_rows, int n_seg) -> Tensor");
+  m.def("segment_mean_backward(Tensor grad, Tensor seg_ptr, Tensor? seg_rows, int n_rows) -> "
+        "Tensor");
+  m.def("csr_from_coo(Tensor row, Tensor col, Tensor? val, int n_rows, bool sorted) -> "
+        "(Tensor, Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(hlhgat, CUDA, m) {  // PyTorch-ROCm dispatches HIP tensors under CUDA
+  m.impl("spmm", &spmm_hip);
+  m.impl("poly_basis", &poly_basis_hip);
+  m.impl("poly_basis_backward", &poly_basis_backward_hip);
+  m.impl("proj", &proj_hip);
+  m.impl("proj_backward", &proj_backward_hip);
+  m.impl("att_score", &att_score_hip);
+  m.impl("att_score_backward", &att_score_backward_hip);
+  m.impl("segment_mean", &segment_mean_hip);
+  m.impl("segment_mean_backward", &segment_mean_backward_hip);
+  m.impl("csr_from_coo", &csr_from_coo_hip);
+}
+
+TORCH_LIBRARY_IMPL(hlhgat, Meta, m) {
+  m.impl("spmm", &spmm_meta);
+  m.impl("poly_basis", &poly_basis_meta);
+  m.impl("poly_basis_backward", &poly_basis_backward_meta);
+  m.impl("proj", &proj_meta);
+  m.impl("proj_backward", &proj_backward_meta);
+  m.impl("att_score", &att_score_meta);
+  m.impl("att_score_backward", &att_score_backward_meta);
+  m.impl("segment_mean", &segment_mean_meta);
+  m.impl("segment_mean_backward", &segment_mean_backward_meta);
+  m.impl("csr_from_coo", &csr_from_coo_meta);
+}
+
+TORCH_LIBRARY_IMPL(hlhgat, Autograd, m) {
+  m.impl("spmm", &spmm_ad);
+  m.impl("poly_basis", &poly_basis_ad);
+  m.impl("proj", &proj_ad);
+  m.impl("att_score", &att_score_ad);
+  m.impl("segment_mean", &segment_mean_ad);
 }

@@ -151,7 +151,9 @@ def _sigma_code(sigma: nn.Module) -> int:
 
 def _as_boundary(par, n_nodes: int, n_edges: int) -> BoundaryOperator:
     if isinstance(par, BoundaryOperator):
-        return par
+        if par.transposed:
+            raise ValueError("NodeEdgeInt: par must be B1 [N_t, N_s] (adj2par1), not B1^T")
+        return par  # |B1| or B1: the value / attention paths use |B1| either way
     if torch.is_tensor(par) and par.is_sparse:
         return boundary_from_sparse(par)
     raise TypeError("NodeEdgeInt: par must come from adj2par1")

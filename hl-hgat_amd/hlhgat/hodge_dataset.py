@@ -497,34 +497,120 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
 
 
 class BoundaryOperator:
-    """|B1| / B1 of adj2par1 for the undirected edge list edge_index [2, E]
-    (column e: -1 at edge_index[0][e], +1 at edge_index[1][e]).
+    """B1 of adj2par1 for the undirected edge list edge_index [2, E] (column
+    e: -1 at edge_index[0][e], +1 at edge_index[1][e]), or a view of it:
+    ``.abs()`` (|B1|), ``.t()`` / ``.transpose(0, 1)`` (B1^T).
 
-    The product path consumes it as an incidence CSR (ops.incidence) built
-    once and shared by every NodeEdgeInt of a block group.  ``to_sparse_coo``
-    returns the reference's exact torch sparse tensor for interop."""
+    It stands in for the reference's torch sparse COO: ``torch.sparse.mm(P,
+    x)``, ``torch.mm``, ``torch.matmul`` and ``P @ x`` with P any of those
+    views run the HIP incidence kernels (ops.incidence_mm; bitwise the
+    coalesced sparse product, with autograd), so reference lines such as
+    ``torch.sparse.mm(par_1.transpose(0,1), x_t).abs()/2``
+    (lib/Hodge_ST_Model.py:848) and ``torch.sparse.mm(par.abs(), x_s)``
+    (lib/Hodge_Cheb_Conv.py:294) work unchanged.  The incidence CSR is built
+    once and shared by every view and every NodeEdgeInt of a block group.
+    ``to_sparse_coo`` returns the reference's exact torch sparse tensor."""
 
-    def __init__(self, edge_index: torch.Tensor, num_node: int, num_edge: int):
+    _MM = None  # the torch functions that mean "sparse @ dense" (set on first use)
+
+    def __init__(self, edge_index: torch.Tensor, num_node: int, num_edge: int,
+                 _transposed: bool = False, _absolute: bool = False, _base=None):
         self.edge_index = edge_index
         self.num_node = int(num_node)
         self.num_edge = int(num_edge)
         if edge_index.size(1) != self.num_edge:
             raise ValueError(f"adj2par1: edge_index has {edge_index.size(1)} edges, "
                              f"num_edge={num_edge}")
+        self.transposed = bool(_transposed)
+        self.absolute = bool(_absolute)
+        self._base = _base  # views share the base operator's incidence CSR
         self._inc = None
         # static-shape batches: valid node / edge row counts (pad_batch)
         self.valid_t = getattr(edge_index, "_hlhgat_valid_t", None)
         self.valid_s = getattr(edge_index, "_hlhgat_valid_s", None)
 
+    # -- tensor-like surface ---------------------------------------------------
     @property
     def shape(self):
-        return torch.Size([self.num_node, self.num_edge])
+        return (torch.Size([self.num_edge, self.num_node]) if self.transposed
+                else torch.Size([self.num_node, self.num_edge]))
+
+    def size(self, dim: Optional[int] = None):
+        return self.shape if dim is None else self.shape[dim]
+
+    def dim(self) -> int:
+        return 2
+
+    is_sparse = True
+    layout = torch.sparse_coo
+    dtype = torch.float32
+
+    @property
+    def device(self):
+        return self.edge_index.device
+
+    def _view(self, transposed: bool, absolute: bool) -> "BoundaryOperator":
+        return BoundaryOperator(self.edge_index, self.num_node, self.num_edge, transposed,
+                                absolute, self._base or self)
+
+    def abs(self) -> "BoundaryOperator":
+        return self._view(self.transposed, True)
+
+    def t(self) -> "BoundaryOperator":
+        return self._view(not self.transposed, self.absolute)
+
+    def transpose(self, dim0: int, dim1: int) -> "BoundaryOperator":
+        if sorted((dim0 % 2, dim1 % 2)) != [0, 1]:
+            raise ValueError("BoundaryOperator.transpose: only (0, 1)")
+        return self.t()
+
+    @property
+    def T(self) -> "BoundaryOperator":
+        return self.t()
+
+    def coalesce(self) -> "BoundaryOperator":
+        return self
+
+    def is_coalesced(self) -> bool:
+        return True
+
+    def to(self, device=None, *args, **kwargs) -> "BoundaryOperator":
+        if device is None or torch.device(device) == self.edge_index.device:
+            return self
+        return BoundaryOperator(self.edge_index.to(device), self.num_node, self.num_edge,
+                                self.transposed, self.absolute)
 
     def incidence(self):
+        if self._base is not None:
+            return self._base.incidence()
         if self._inc is None:
             from .ops import incidence
             self._inc = incidence(self.edge_index, self.num_node)
         return self._inc
+
+    # -- products (HIP) --------------------------------------------------------
+    def matmul(self, x: torch.Tensor) -> torch.Tensor:
+        from .ops import incidence_mm
+        if not (torch.is_tensor(x) and x.is_cuda):
+            raise RuntimeError("hlhgat: BoundaryOperator products run on the ROCm device only "
+                               "(use .to_sparse_coo() for a CPU torch sparse tensor)")
+        if x.dim() != 2:
+            raise RuntimeError(f"hlhgat: BoundaryOperator @ x needs a 2-D x, got {x.dim()}-D")
+        return incidence_mm(x, self.incidence(), self.transposed, not self.absolute)
+
+    __matmul__ = matmul
+    mm = matmul
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        if cls._MM is None:
+            cls._MM = {torch.sparse.mm, torch.mm, torch.matmul, torch.Tensor.mm,
+                       torch.Tensor.matmul, torch.Tensor.__matmul__}
+        kwargs = kwargs or {}
+        if func in cls._MM and len(args) == 2 and isinstance(args[0], BoundaryOperator) \
+                and torch.is_tensor(args[1]) and not kwargs:
+            return args[0].matmul(args[1])
+        return NotImplemented
 
     def to_sparse_coo(self) -> torch.Tensor:
         ei = self.edge_index
@@ -532,11 +618,18 @@ class BoundaryOperator:
         col_idx = torch.cat([torch.arange(E), torch.arange(E)]).to(ei.device)
         row_idx = torch.cat([ei[0], ei[1]])
         val = torch.cat([ei[0].new_full(ei[0].shape, -1), ei[0].new_full(ei[0].shape, 1)]).float()
-        return torch.sparse_coo_tensor(torch.stack([row_idx, col_idx]), val,
-                                       (self.num_node, self.num_edge))
+        P = torch.sparse_coo_tensor(torch.stack([row_idx, col_idx]), val,
+                                    (self.num_node, self.num_edge))
+        if self.absolute:
+            P = P.abs()
+        return P.t() if self.transposed else P
 
     def to_dense(self) -> torch.Tensor:
         return self.to_sparse_coo().to_dense()
+
+    def __repr__(self) -> str:
+        v = ("|B1|" if self.absolute else "B1") + ("^T" if self.transposed else "")
+        return f"BoundaryOperator({v}, shape={tuple(self.shape)}, device={self.device})"
 
 
 def adj2par1(edge_index: torch.Tensor, num_node: int, num_edge: int) -> BoundaryOperator:

@@ -29,7 +29,7 @@ __all__ = [
     "SparseCSR", "HodgeOperator", "Incidence", "hodge_operator", "incidence",
     "mark_hodge", "spmm", "poly_basis", "hodge_poly_conv", "linear_blocks", "mlp2", "nei_value",
     "batch_norm_act", "check_device_errors", "clear_device_errors", "device_errors",
-    "node_from_edges", "edge_from_nodes", "att_score", "segment_mean",
+    "node_from_edges", "edge_from_nodes", "incidence_mm", "att_score", "segment_mean",
     "POLY_LAGUERRE", "POLY_CHEB", "POLY_LAGUERRE_DEMO", "SIGMA_SIGMOID", "SIGMA_RELU",
 ]
 
@@ -945,6 +945,55 @@ def boundary_t(x_t: torch.Tensor, inc: Incidence) -> torch.Tensor:
     if x_t.size(0) != inc.n_nodes:
         raise RuntimeError(f"hlhgat: x_t has {x_t.size(0)} rows, |B1| has {inc.n_nodes} nodes")
     return _BoundaryTFn.apply(x_t, inc)
+
+
+class _IncidenceMMFn(torch.autograd.Function):
+    """One of the four products with B1 of adj2par1 (lib/Hodge_Dataset.py:
+    169-191) that torch.sparse.mm forms in the reference: B1 y, |B1| y (node
+    rows: incidence CSR, edges ascending = the coalesced order) and B1^T x,
+    |B1|^T x (edge rows: tail entry first).  The backward of each is the
+    transposed product."""
+
+    @staticmethod
+    def forward(ctx, x, inc, transposed, signed):
+        ctx.inc, ctx.transposed, ctx.signed = inc, transposed, signed
+        return _incidence_mm(x, inc, transposed, signed)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _rows2d(g.contiguous(), "grad")
+        return _incidence_mm(g, ctx.inc, not ctx.transposed, ctx.signed), None, None, None
+
+
+def _incidence_mm(x: torch.Tensor, inc: Incidence, transposed: bool, signed: bool):
+    d = x.size(1)
+    if transposed:  # edge rows: y[e] = c_i x[i] + x[j]
+        y = torch.empty(inc.n_edges, d, device=x.device, dtype=x.dtype)
+        if inc.n_edges:
+            check(LIB.hlhgat_edge_gather2(inc.edge_index.data_ptr(), inc.n_edges, x.data_ptr(),
+                                          _ld(x), d, None, None, -1.0 if signed else 1.0, 1.0,
+                                          None, 0, y.data_ptr(), _ld(y), 0, _stream(x)),
+                  "edge_gather2(B1^T)")
+        return y
+    A = SparseCSR(inc.rowptr, inc.edge_ids, _incidence_signs(inc) if signed else None,
+                  inc.n_nodes, inc.n_edges, 2 * inc.n_edges)
+    y = torch.empty(inc.n_nodes, d, device=x.device, dtype=x.dtype)
+    if inc.n_nodes:
+        _poly_step(A, x, y)
+    return y
+
+
+def incidence_mm(x: torch.Tensor, inc: Incidence, transposed: bool = False,
+                 signed: bool = True) -> torch.Tensor:
+    """torch.sparse.mm(P, x) for P = adj2par1(...) (signed) or its .abs(), or
+    their transposes: bitwise the coalesced sparse product (autograd)."""
+    _req_dev(x, "x")
+    x = _rows2d(x, "x")
+    rows = inc.n_nodes if transposed else inc.n_edges
+    if x.size(0) != rows:
+        raise RuntimeError(f"hlhgat: B1{'^T' if transposed else ''} product: x has {x.size(0)} "
+                           f"rows, expected {rows}")
+    return _IncidenceMMFn.apply(x, inc, bool(transposed), bool(signed))
 
 
 def edge_from_nodes(x_t: torch.Tensor, inc: Incidence) -> torch.Tensor:

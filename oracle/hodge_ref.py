@@ -14,6 +14,11 @@ PyTorch-CPU restatement of the HL-HGAT hot path, following the reference
   Ref* modules         same parameter names as the reference modules, so one
                        state_dict drives the oracle and the HIP product
   RefZincModel         lib/Hodge_ST_Model.py:544-646
+  RefTSPModel          lib/Hodge_ST_Model.py:756-855 (config 5 head)
+  RefCifarAttPool      lib/Hodge_ST_Model.py:958-1091 (config 3 head)
+  RefPepfuncAttPool    main_pepfunc_HL_HGCNN_dense_int3_attpool.py:36-168 (config 4)
+  RefHLFilter          lib/Hodge_Cheb_Conv.py:117-188
+  RefSAPool            lib/Hodge_Cheb_Conv.py:36-59
 """
 from __future__ import annotations
 
@@ -276,14 +281,14 @@ class RefNodeEdgeInt(nn.Module):
         return x_t1, x_s1
 
 
-def _ref_block(cin_t, cin_s, cout, K, dropout_ratio=0.0):
+def _ref_block(cin_t, cin_s, cout, K, dropout_ratio=0.0, act=nn.ReLU):
     layers = [(RefHodgeConv(cin_t, cout, K), "x_t, edge_index_t, edge_weight_t -> x_t"),
               (RefBatchNorm(cout), "x_t -> x_t"),
-              (nn.ReLU(), "x_t -> x_t"),
+              (act(), "x_t -> x_t"),
               (Dropout(p=dropout_ratio), "x_t -> x_t"),
               (RefHodgeConv(cin_s, cout, K), "x_s, edge_index_s, edge_weight_s -> x_s"),
               (RefBatchNorm(cout), "x_s -> x_s"),
-              (nn.ReLU(), "x_s -> x_s"),
+              (act(), "x_s -> x_s"),
               (Dropout(p=dropout_ratio), "x_s -> x_s"),
               (lambda x1, x2: [x1, x2], "x_t, x_s -> x")]
     return RefSequential("x_t, edge_index_t, edge_weight_t, x_s, edge_index_s, edge_weight_s",
@@ -337,3 +342,262 @@ class RefZincModel(nn.Module):
         for i, _ in enumerate(self.mlp_channels):
             x = getattr(self, f"mlp{i}")(x)
         return self.out(x)
+
+
+def _batch_vec(counts):
+    """torch.cat([torch.tensor([i] * n) for i, n in enumerate(counts)])
+    (lib/Hodge_ST_Model.py:824-828, :1031-1034)."""
+    return torch.cat([torch.full((int(c),), i, dtype=torch.long) for i, c in enumerate(counts)])
+
+
+class RefTSPModel(nn.Module):
+    """lib/Hodge_ST_Model.py:756-855 (HL_HGCNN_TSP_dense_int3_pyr): no keig
+    columns (:764-765), edge mask in x_s[:, 1:], readout |B1^T x_t| / 2 (:848),
+    K=1 conv MLP and output conv over L1; returns (logits * mask, s_batch)."""
+
+    def __init__(self, channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[], K=2,
+                 node_dim=2, edge_dim=1, num_classes=1, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, keig=20):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.mlp_channels = mlp_channels
+        c0 = filters[0]
+        self.HL_init_conv = _ref_block(node_dim, edge_dim, c0, K, dropout_ratio)
+        gin = c0
+        for i, gout in enumerate(filters):
+            for j in range(channels[i]):
+                setattr(self, f"NEInt{i}{j}", RefNodeEdgeInt(d=gin, dv=gout))
+                setattr(self, f"NEConv{i}{j}", _ref_block(gout, gout, gout, K, dropout_ratio))
+                gin = gout + gin
+        mlp_in = gout * 2                                                      # :806
+        if len(mlp_channels) == 1:                                             # :807-815
+            self.mlp = RefSequential("x_t, edge_index_t, edge_weight_t", [
+                (RefHodgeConv(mlp_in, mlp_channels[0], 1),
+                 "x_t, edge_index_t, edge_weight_t -> x_t"),
+                (RefBatchNorm(mlp_channels[0]), "x_t -> x_t"),
+                (nn.ReLU(), "x_t -> x_t"),
+                (Dropout(p=dropout_ratio), "x_t -> x_t")])
+            mlp_in = mlp_channels[0]
+        self.out = RefSequential("x_t, edge_index_t, edge_weight_t", [
+            (RefHodgeConv(mlp_in, num_classes, 1), "x_t, edge_index_t, edge_weight_t -> x_t")])
+
+    def forward(self, data):
+        s_batch = _batch_vec(data.num_edge1)
+        x_s, ei_s, ew_s = data.x_s[:, :1], data.edge_index_s, data.edge_weight_s  # :829
+        edge_mask = data.x_s[:, 1:]
+        x_t, ei_t, ew_t = data.x_t, data.edge_index_t, data.edge_weight_t
+        x_t, x_s = self.HL_init_conv(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+        x_s0, x_t0 = x_s, x_t
+        par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])            # :835
+        D = degree(data.edge_index.reshape(-1), num_nodes=x_t.shape[0]) + 1e-6    # :836
+        for i, _ in enumerate(self.channels):
+            for j in range(self.channels[i]):
+                x_t, x_s = getattr(self, f"NEInt{i}{j}")(x_t0, x_s0, par_1, D)
+                x_t, x_s = getattr(self, f"NEConv{i}{j}")(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+        par_x = par_1 if par_1.dtype == x_t.dtype else par_1.to(x_t.dtype)  # (fp64 studies)
+        x_t2s = torch.sparse.mm(par_x.transpose(0, 1), x_t).abs() / 2            # :848
+        x_s = torch.cat([x_s, x_t2s], dim=-1)
+        if len(self.mlp_channels) == 1:
+            x_s = self.mlp(x_s, ei_s, ew_s)
+        return self.out(x_s, ei_s, ew_s) * edge_mask, s_batch
+
+
+def _pos(datas, device=None):
+    """pos_ts / pos_ss of the attpool heads (lib/Hodge_ST_Model.py:1029-1038):
+    fine row -> global coarse index (float; inf for an edge MLGC dropped)."""
+    n_batch = _batch_vec(datas[0].num_node1)
+    s_batch = _batch_vec(datas[0].num_edge1)
+    n_ahead = torch.cumsum(torch.cat([torch.zeros(1), torch.as_tensor(datas[1].num_node1,
+                                                                      dtype=torch.float)]),
+                           dim=0, dtype=torch.long)[:-1]
+    s_ahead = torch.cumsum(torch.cat([torch.zeros(1), torch.as_tensor(datas[1].num_edge1,
+                                                                      dtype=torch.float)]),
+                           dim=0, dtype=torch.long)[:-1]
+    pos_t = (datas[0].x_t[:, 0] + n_ahead[n_batch]).view(-1, 1)
+    pos_s = (datas[0].x_s[:, 0] + s_ahead[s_batch]).view(-1, 1)
+    return [pos_t], [pos_s]
+
+
+def _pool(x_t0, x_s0, pos_t, pos_s):
+    """structural pooling (lib/Hodge_ST_Model.py:1065-1069): scatter_mean by
+    cluster, edges assigned inf dropped first."""
+    x_t0 = scatter_mean(x_t0, pos_t.to(torch.long))
+    keep = ~torch.isinf(pos_s).view(-1)
+    x_s0 = scatter_mean(x_s0[keep], pos_s[keep].to(torch.long))
+    return x_t0, x_s0
+
+
+class _RefAttPool(nn.Module):
+    """Shared constructor of the two attention-pooling heads."""
+
+    def __init__(self, channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                 dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, every_level):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.mlp_channels = mlp_channels
+        self.pool_loc = pool_loc
+        c0 = filters[0]
+        self.HL_init_conv = _ref_block(node_dim + keig, edge_dim + keig, c0, 1, dropout_ratio)
+        gin = c0
+        for i, gout in enumerate(filters):
+            for j in range(channels[i]):
+                setattr(self, f"NEInt{i}{j}", RefNodeEdgeInt(d=gin, dv=gout))
+                setattr(self, f"NEConv{i}{j}", _ref_block(gout, gout, gout, K, dropout_ratio))
+                gin = gin + gout
+            if every_level:   # main_pepfunc...:86-87
+                setattr(self, f"NEAtt{i}", RefNodeEdgeInt(d=gin, dv=gout, only_att=True, l=0.5))
+            elif i == pool_loc:  # lib/Hodge_ST_Model.py:1007-1010
+                setattr(self, f"NEAtt{i}", RefNodeEdgeInt(d=gout, dv=gout, only_att=True,
+                                                          sigma=nn.ReLU(), l=l))
+        mlp_in = filters[-1] * 2
+        for i, mo in enumerate(mlp_channels):
+            setattr(self, f"mlp{i}", nn.Sequential(Linear(mlp_in, mo), nn.BatchNorm1d(mo),
+                                                   nn.ReLU(), nn.Dropout(dropout_ratio_mlp)))
+            mlp_in = mo
+        self.out = Linear(mlp_in, num_classes)
+
+    def _readout(self, x_s, x_t, datas, i):
+        d = datas[min(i, 1)]                                                   # :1077-1081
+        x = torch.cat((global_mean_pool(x_s, _batch_vec(d.num_edge1)),
+                       global_mean_pool(x_t, _batch_vec(d.num_node1))), -1)
+        for m in range(len(self.mlp_channels)):
+            x = getattr(self, f"mlp{m}")(x)
+        return self.out(x)
+
+
+class RefCifarAttPool(_RefAttPool):
+    """lib/Hodge_ST_Model.py:958-1091 (HL_HGCNN_CIFAR10SP_dense_int3_attpool)."""
+
+    def __init__(self, channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[], K=2,
+                 node_dim=5, l=0.5, edge_dim=4, num_classes=10, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, pool_loc=0, keig=10):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, False)
+
+    def forward(self, datas):
+        data = datas[0]
+        pos_ts, pos_ss = _pos(datas)
+        x_s, ei_s, ew_s = data.x_s[:, 1:], data.edge_index_s, data.edge_weight_s
+        x_t, ei_t, ew_t = data.x_t[:, 1:], data.edge_index_t, data.edge_weight_t
+        x_t, x_s = self.HL_init_conv(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+        x_s0, x_t0 = x_s, x_t
+        k = 0
+        par_1 = adj2par1(datas[k].edge_index, x_t0.shape[0], x_s0.shape[0])
+        D = degree(datas[k].edge_index.reshape(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        for i, _ in enumerate(self.channels):
+            for j in range(self.channels[i]):
+                x_t, x_s = getattr(self, f"NEInt{i}{j}")(x_t0, x_s0, par_1, D)
+                x_t, x_s = getattr(self, f"NEConv{i}{j}")(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            if i == self.pool_loc:                                             # :1058-1074
+                att_t, att_s = getattr(self, f"NEAtt{i}")(x_t, x_s, par_1, D)
+                att_t = att_t / att_t.max()
+                att_s = att_s / att_s.max()
+                x_t = x_t * att_t
+                x_s = x_s * att_s
+                x_t0, x_s0 = _pool(x_t0, x_s0, pos_ts[k], pos_ss[k])
+                ei_s, ew_s = datas[k + 1].edge_index_s, datas[k + 1].edge_weight_s
+                ei_t, ew_t = datas[k + 1].edge_index_t, datas[k + 1].edge_weight_t
+                k = 1
+                par_1 = adj2par1(datas[k].edge_index, x_t0.shape[0], x_s0.shape[0])
+                D = degree(datas[k].edge_index.reshape(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        return self._readout(x_s, x_t, datas, i)
+
+
+class RefPepfuncAttPool(_RefAttPool):
+    """main_pepfunc_HL_HGCNN_dense_int3_attpool.py:36-168: NEAtt (sigmoid,
+    l = 0.5) on the dense concatenation after every level (:133-136)."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=9, edge_dim=3, num_classes=10, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, pool_loc=0, keig=20):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, 0.5, True)
+
+    def forward(self, datas):
+        data = datas[0]
+        pos_ts, pos_ss = _pos(datas)
+        x_s, ei_s, ew_s = data.x_s[:, 1:], data.edge_index_s, data.edge_weight_s
+        x_t, ei_t, ew_t = data.x_t[:, 1:], data.edge_index_t, data.edge_weight_t
+        x_t, x_s = self.HL_init_conv(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+        x_s0, x_t0 = x_s, x_t
+        k = 0
+        par_1 = adj2par1(datas[k].edge_index, x_t0.shape[0], x_s0.shape[0])
+        D = degree(datas[k].edge_index.reshape(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        for i, _ in enumerate(self.channels):
+            for j in range(self.channels[i]):
+                x_t, x_s = getattr(self, f"NEInt{i}{j}")(x_t0, x_s0, par_1, D)
+                x_t, x_s = getattr(self, f"NEConv{i}{j}")(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            att_t, att_s = getattr(self, f"NEAtt{i}")(x_t0, x_s0, par_1, D)     # :133-136
+            x_t0 = x_t0 * att_t
+            x_s0 = x_s0 * att_s
+            if i == self.pool_loc:                                             # :139-149
+                x_t0, x_s0 = _pool(x_t0, x_s0, pos_ts[k], pos_ss[k])
+                ei_s, ew_s = datas[k + 1].edge_index_s, datas[k + 1].edge_weight_s
+                ei_t, ew_t = datas[k + 1].edge_index_t, datas[k + 1].edge_weight_t
+                k = 1
+                par_1 = adj2par1(datas[k].edge_index, x_t0.shape[0], x_s0.shape[0])
+                D = degree(datas[k].edge_index.reshape(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        return self._readout(x_s, x_t, datas, i)
+
+
+class RefHLFilter(nn.Module):
+    """lib/Hodge_Cheb_Conv.py:117-188 (HL_filter): MSI + HL block per channel
+    with dense concatenation (if_dense) or plain stacking; LeakyReLU."""
+
+    def __init__(self, channels=2, filters=32, K=4, node_dim=64, edge_dim=64,
+                 dropout_ratio=0.0, leaky_slope=0.1, if_dense=True):
+        super().__init__()
+        self.channels = channels
+        self.if_dense = if_dense
+        t_in, s_in = node_dim, edge_dim
+        act = lambda: nn.LeakyReLU(negative_slope=leaky_slope)  # noqa: E731
+        for j in range(channels):
+            if if_dense:
+                setattr(self, f"MSI{j}", RefNodeEdgeInt(d=t_in, dv=filters))
+                setattr(self, f"NEConv{j}", _ref_block(filters, filters, filters, K,
+                                                       dropout_ratio, act))
+                t_in, s_in = t_in + filters, s_in + filters
+            else:
+                setattr(self, f"NEConv{j}", _ref_block(t_in, s_in, filters, K, dropout_ratio,
+                                                       act))
+                t_in = s_in = filters
+
+    def forward(self, x_t0, ei_t, ew_t, x_s0, ei_s, ew_s, par_1=None, D=None):
+        for j in range(self.channels):
+            if self.if_dense:
+                x_t, x_s = getattr(self, f"MSI{j}")(x_t0, x_s0, par_1, D)
+                x_t, x_s = getattr(self, f"NEConv{j}")(x_t, ei_t, ew_t, x_s, ei_s, ew_s)
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            else:
+                x_t0, x_s0 = getattr(self, f"NEConv{j}")(x_t0, ei_t, ew_t, x_s0, ei_s, ew_s)
+        return x_t0, x_s0
+
+
+class RefSAPool(nn.Module):
+    """lib/Hodge_Cheb_Conv.py:36-59 (SAPool): sigmoid attention on the dense
+    features, then structural pooling to level k+1."""
+
+    def __init__(self, d=64, dk=32):
+        super().__init__()
+        self.NEAtt = RefNodeEdgeInt(d=d, dk=dk, only_att=True, sigma=nn.Sigmoid())
+
+    def forward(self, x_t0, x_s0, par_1, D, datas, pos_ts, pos_ss, k):
+        att_t, att_s = self.NEAtt(x_t0, x_s0, par_1, D)
+        x_t0 = x_t0 * att_t
+        x_s0 = x_s0 * att_s
+        x_t0, x_s0 = _pool(x_t0, x_s0, pos_ts[k], pos_ss[k])
+        ei_s, ew_s = datas[k + 1].edge_index_s, datas[k + 1].edge_weight_s
+        ei_t, ew_t = datas[k + 1].edge_index_t, datas[k + 1].edge_weight_t
+        k += 1
+        par_1 = adj2par1(datas[k].edge_index, x_t0.shape[0], x_s0.shape[0])
+        D = degree(datas[k].edge_index.reshape(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        return x_t0, x_s0, par_1, D, k, ei_t, ew_t, ei_s, ew_s, att_t, att_s

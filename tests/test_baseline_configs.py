@@ -1,0 +1,390 @@
+"""Configs 3 / 4 / 5 at their OWN hyperparameters, plus HL_filter and SAPool.
+
+Fixtures: tests/golden/make_golden_baseline.py ran the REFERENCE's classes
+(lib/Hodge_ST_Model.py:756-855, :958-1091; main_pepfunc...:36-168;
+lib/Hodge_Cheb_Conv.py:36-59, :117-188) with parameters from
+baseline_params.fill_params and stored inputs, outputs and (sampled)
+gradients.
+
+* CPU (oracle pinning): the oracle's restatements reproduce the fixtures
+  (outputs 1e-5, gradients 1e-4 relative).
+* GPU (product parity, -m gpu): the HIP heads on the same inputs.  Outputs:
+  1e-4 relative to the fixture and to an fp64 evaluation of the oracle.
+  Gradients pass through 6 (configs 3/4) or 12 (config 5) dense blocks of
+  batch-statistics BatchNorm + ReLU.  There they are ill-conditioned: some
+  pre-ReLU values sit within fp32 rounding of 0, so a 1e-6 relative change of
+  the weights flips ReLU masks and moves fp64 gradients by up to 18 % (config
+  4 at level 0, measured with tools/baseline_err_table.py / grad_bisect.py and
+  reproduced here by `cond`).  So each parameter gradient of the HIP path must
+  be within 3x the larger of (a) the fp32 oracle's distance to fp64 and (b) the
+  fp64 gradient's own change under two 1e-6 relative weight perturbations,
+  floor 1e-4 relative (max-norm, full tensor); and its sampled fixture entries
+  within that bound of the fixture.  Biases feeding a training-mode BatchNorm
+  have an analytically zero gradient: fp32 noise, <= 3x the fp32 oracle's.
+"""
+import os
+import re
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, close, load_golden
+from oracle import hodge_ref as R
+
+sys.path.insert(0, GOLDEN)
+from baseline_params import fill_params, grad_view  # noqa: E402
+
+T = torch.from_numpy
+KEYS = ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+        "edge_index", "num_node1", "num_edge1")
+
+# the generator's model settings (tests/golden/make_golden_baseline.py)
+CFG3 = dict(channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[256], K=4, keig=10,
+            pool_loc=1, l=0.5)
+CFG4 = dict(channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[256], K=6, pool_loc=1)
+CFG5 = dict(channels=[4, 4, 4], filters=[32, 64, 128], mlp_channels=[256], K=4)
+HLF = {"hl_filter_dense": dict(channels=2, filters=16, K=3, node_dim=16, edge_dim=16,
+                               leaky_slope=0.1, if_dense=True),
+       "hl_filter_plain": dict(channels=2, filters=16, K=3, node_dim=12, edge_dim=8,
+                               leaky_slope=0.1, if_dense=False)}
+SAPOOL = dict(d=24, dk=8)
+HEADS = {"baseline_cfg3_cifar": ("RefCifarAttPool", "HL_HGCNN_CIFAR10SP_dense_int3_attpool", CFG3),
+         "baseline_cfg4_pepfunc": ("RefPepfuncAttPool", "HL_HGCNN_pepfunc_dense_int3_attpool",
+                                   CFG4),
+         "baseline_cfg5_tsp": ("RefTSPModel", "HL_HGCNN_TSP_dense_int3_pyr", CFG5)}
+
+
+class _D:
+    pass
+
+
+def _data(g, prefix="", dtype=None, device=None):
+    d = _D()
+    for k in KEYS:
+        v = T(g[prefix + k])
+        if dtype is not None and v.is_floating_point():
+            v = v.to(dtype)
+        if device is not None:
+            v = v.to(device)
+        setattr(d, k, v)
+    return d
+
+
+def _perturb(m, eps, seed):
+    """multiply every parameter by (1 + eps N(0,1)) (conditioning probe)"""
+    if not eps:
+        return
+    gen = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.mul_(1 + eps * torch.randn(p.shape, generator=gen, dtype=torch.float64).to(p.dtype))
+
+
+def _cond(m64, perturbed):
+    """per parameter: max over the perturbed fp64 runs of the max-norm relative
+    change of the gradient"""
+    base = dict(m64.named_parameters())
+    out = {}
+    for mp in perturbed:
+        for k, p in mp.named_parameters():
+            if p.grad is None or base[k].grad is None:
+                continue
+            sc = max(1.0, float(base[k].grad.abs().max()))
+            out[k] = max(out.get(k, 0.0), float((p.grad - base[k].grad).abs().max()) / sc)
+    return out
+
+
+def _bn_fed_bias(k):
+    return (re.search(r"module_[04]\.bias$", k) and not k.startswith("out.")) or \
+        re.search(r"mlp\d+\.0\.bias$", k) or re.search(r"WV_(Node|Edge)\.[03]\.bias$", k)
+
+
+def _run_oracle(name, g, dtype, eps=0.0, pseed=0):
+    cls_name, _, kw = HEADS[name]
+    m = getattr(R, cls_name)(**kw)
+    fill_params(m, int(g["seed"]))
+    m = m.to(dtype).train()
+    _perturb(m, eps, pseed)
+    if "tsp" in name:
+        out, s_batch = m(_data(g, "", dtype))
+    else:
+        out, s_batch = m([_data(g, "l0/", dtype), _data(g, "l1/", dtype)]), None
+    (out * T(g["R"]).to(dtype)).sum().backward()
+    return m, out.detach(), s_batch
+
+
+# ---------------------------------------------------------------------------
+# CPU: the oracle reproduces the reference at the BASELINE hyperparameters
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", sorted(HEADS))
+def test_oracle_head_matches_reference_at_baseline(name):
+    g = load_golden(name)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)  # the generator's CPU reduction order
+    try:
+        m, out, s_batch = _run_oracle(name, g, torch.float32)
+    finally:
+        torch.set_num_threads(nt)
+    close(out, g["out"], 1e-5, "out")
+    if s_batch is not None:
+        assert torch.equal(s_batch, T(g["s_batch"]))
+    n_checked = 0
+    for k, p in m.named_parameters():
+        if "nograd/" + k in g:
+            assert p.grad is None, k
+            continue
+        ref, got, scale = grad_view(g, k, p.grad)
+        # (biases feeding a BatchNorm included: their analytically-zero
+        # gradients are fp32 noise, which the oracle reproduces exactly)
+        assert float((ref - got).abs().max()) <= 1e-4 * scale, k
+        n_checked += 1
+    assert n_checked > 20
+
+
+def _hlf_inputs(g):
+    par = R.adj2par1(T(g["b/edge_index"]), g["x_t"].shape[0], g["x_s"].shape[0])
+    return (T(g["x_t"]).requires_grad_(True), T(g["b/edge_index_t"]), T(g["b/edge_weight_t"]),
+            T(g["x_s"]).requires_grad_(True), T(g["b/edge_index_s"]), T(g["b/edge_weight_s"]),
+            par, T(g["D"]))
+
+
+@pytest.mark.parametrize("name", sorted(HLF))
+def test_oracle_hl_filter(name):
+    g = load_golden(name)
+    m = R.RefHLFilter(**HLF[name])
+    fill_params(m, int(g["seed"]))
+    m.train()
+    x_t, ei_t, ew_t, x_s, ei_s, ew_s, par, D = _hlf_inputs(g)
+    y_t, y_s = m(x_t, ei_t, ew_t, x_s, ei_s, ew_s, par, D)
+    close(y_t.detach(), g["out_t"], 1e-5, "out_t")
+    close(y_s.detach(), g["out_s"], 1e-5, "out_s")
+    ((y_t * T(g["R_t"])).sum() + (y_s * T(g["R_s"])).sum()).backward()
+    close(x_t.grad, g["grad_x_t"], 1e-4, "grad_x_t")
+    close(x_s.grad, g["grad_x_s"], 1e-4, "grad_x_s")
+    for k, p in m.named_parameters():
+        ref, got, scale = grad_view(g, k, p.grad)
+        if _bn_fed_bias(k):
+            continue
+        assert float((ref - got).abs().max()) <= 1e-4 * scale, k
+
+
+def _sapool_inputs(g, device=None):
+    f = (lambda a: T(a).to(device)) if device else T
+    datas = [_data(g, "l0/", device=device), _data(g, "l1/", device=device)]
+    par_fn = R.adj2par1
+    return datas, f(g["pos_t"]), f(g["pos_s"]), f(g["x_t"]), f(g["x_s"]), f(g["D"]), par_fn
+
+
+def test_oracle_sapool():
+    g = load_golden("sapool")
+    m = R.RefSAPool(**SAPOOL)
+    fill_params(m, int(g["seed"]))
+    m.train()
+    datas, pos_t, pos_s, x_t, x_s, D, _ = _sapool_inputs(g)
+    x_t.requires_grad_(True)
+    x_s.requires_grad_(True)
+    par = R.adj2par1(datas[0].edge_index, x_t.shape[0], x_s.shape[0])
+    y_t, y_s, _, D1, k, *_, a_t, a_s = m(x_t, x_s, par, D, datas, [pos_t], [pos_s], 0)
+    assert k == int(g["k"])
+    close(D1, g["D1"], 0, "D1")
+    for a, e in ((y_t, "out_t"), (y_s, "out_s"), (a_t, "att_t"), (a_s, "att_s")):
+        close(a.detach(), g[e], 1e-5, e)
+    sum((a * T(g[r])).sum() for a, r in ((y_t, "R_t"), (y_s, "R_s"), (a_t, "R_at"),
+                                          (a_s, "R_as"))).backward()
+    close(x_t.grad, g["grad_x_t"], 1e-4, "grad_x_t")
+    close(x_s.grad, g["grad_x_s"], 1e-4, "grad_x_s")
+    for k, p in m.named_parameters():
+        ref, got, scale = grad_view(g, k, p.grad)
+        assert float((ref - got).abs().max()) <= 1e-4 * scale, k
+
+
+# ---------------------------------------------------------------------------
+# GPU: the HIP heads at the BASELINE hyperparameters
+# ---------------------------------------------------------------------------
+def _product_batch(g, prefix, cuda, factored):
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import Batch
+    b = Batch()
+    for k in KEYS:
+        setattr(b, k, T(g[prefix + k]).to(cuda))
+    # fixture COO came from collate(check_hodge=True): row-sorted, symmetric
+    ops.mark_hodge(b.edge_index_t)
+    ops.mark_hodge(b.edge_index_s)
+    if factored:
+        ops.set_hodge_factor(b.edge_index_s, b.edge_index, b.x_t.shape[0])
+    return b
+
+
+def _grad_gate(m_hip, m32, m64, g, cond):
+    """per-parameter: HIP vs fp64 oracle within 3x max(fp32 oracle vs fp64,
+    conditioning), floor 1e-4 relative; sampled fixture entries within the
+    same bound (module docstring)."""
+    p32 = dict(m32.named_parameters())
+    p64 = dict(m64.named_parameters())
+    worst = []
+    for k, p in m_hip.named_parameters():
+        if g is not None and "nograd/" + k in g:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
+            continue
+        e64 = p64[k].grad.double()
+        scale = max(1.0, float(e64.abs().max()))
+        hip = p.grad.detach().cpu().double()
+        if _bn_fed_bias(k):
+            # analytically zero: noise no larger than 3x the fp32 reference's
+            noise32 = float(p32[k].grad.abs().max()) / scale
+            assert float(hip.abs().max()) / scale <= max(3 * noise32, 1e-3), k
+            continue
+        err32 = float((p32[k].grad.double() - e64).abs().max()) / scale
+        errh = float((hip - e64).abs().max()) / scale
+        bound = max(3 * max(err32, cond.get(k, 0.0)), 1e-4)
+        assert errh <= bound, (k, errh, err32, cond.get(k))
+        if g is not None:
+            ref, got, sc = grad_view(g, k, p.grad)
+            assert float((ref - got).abs().max()) / sc <= bound + err32, (k, "fixture")
+        worst.append((errh / bound, k))
+    return max(worst)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,factored", [("baseline_cfg3_cifar", False),
+                                           ("baseline_cfg3_cifar", True),
+                                           ("baseline_cfg4_pepfunc", False),
+                                           ("baseline_cfg5_tsp", False),
+                                           ("baseline_cfg5_tsp", True)])
+def test_head_at_baseline_vs_reference(cuda, name, factored):
+    import hlhgat
+    from hlhgat import ops
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    g = load_golden(name)
+    _, cls_name, kw = HEADS[name]
+    m = getattr(hlhgat, cls_name)(**kw)
+    fill_params(m, int(g["seed"]))
+    m = m.to(cuda).train()
+    ops.clear_caches()
+    if "tsp" in name:
+        b = _product_batch(g, "", cuda, factored)
+        out, s_batch = m(b)
+        assert torch.equal(s_batch.cpu(), T(g["s_batch"]))
+        op = ops.hodge_operator(b.edge_index_s, b.edge_weight_s, b.x_s.shape[0])
+    else:
+        datas = [_product_batch(g, "l0/", cuda, factored), _product_batch(g, "l1/", cuda, False)]
+        out = m(datas)
+        op = ops.hodge_operator(datas[0].edge_index_s, datas[0].edge_weight_s,
+                                datas[0].x_s.shape[0])
+    assert (op.factor is not None) == factored
+    close(out.detach().cpu(), g["out"], 1e-4, "out vs reference")
+    (out * T(g["R"]).to(cuda)).sum().backward()
+    m32, _, _ = _run_oracle(name, g, torch.float32)
+    m64, out64, _ = _run_oracle(name, g, torch.float64)
+    cond = _cond(m64, [_run_oracle(name, g, torch.float64, 1e-6, s)[0] for s in (0, 1)])
+    close(out.detach().cpu(), out64, 1e-4, "out vs fp64 oracle")
+    _grad_gate(m, m32, m64, g, cond)
+    ops.check_device_errors()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(HLF))
+def test_hl_filter_vs_reference(cuda, name):
+    """HL_filter (lib/Hodge_Cheb_Conv.py:117-188), LeakyReLU(0.1), dense and
+    plain stacking: outputs 1e-5, input and parameter gradients 1e-4."""
+    import hlhgat
+    from hlhgat.hodge_dataset import adj2par1
+    g = load_golden(name)
+    m = hlhgat.HL_filter(**HLF[name])
+    fill_params(m, int(g["seed"]))
+    m = m.to(cuda).train()
+    d = lambda k: T(g[k]).to(cuda)  # noqa: E731
+    x_t = d("x_t").requires_grad_(True)
+    x_s = d("x_s").requires_grad_(True)
+    par = adj2par1(d("b/edge_index"), x_t.shape[0], x_s.shape[0])
+    y_t, y_s = m(x_t, d("b/edge_index_t"), d("b/edge_weight_t"), x_s, d("b/edge_index_s"),
+                 d("b/edge_weight_s"), par, d("D"))
+    close(y_t.detach().cpu(), g["out_t"], 1e-5, "out_t")
+    close(y_s.detach().cpu(), g["out_s"], 1e-5, "out_s")
+    ((y_t * d("R_t")).sum() + (y_s * d("R_s")).sum()).backward()
+    close(x_t.grad.cpu(), g["grad_x_t"], 1e-4, "grad_x_t")
+    close(x_s.grad.cpu(), g["grad_x_s"], 1e-4, "grad_x_s")
+    for k, p in m.named_parameters():
+        ref, got, scale = grad_view(g, k, p.grad)
+        if _bn_fed_bias(k):
+            assert float(got.abs().max()) < 1e-3 * scale, k
+            continue
+        assert float((ref - got).abs().max()) <= 1e-4 * scale, k
+
+
+@pytest.mark.gpu
+def test_sapool_vs_reference(cuda):
+    """SAPool (lib/Hodge_Cheb_Conv.py:36-59): sigmoid attention on the dense
+    features, inf-masked cluster means, level switch (k, coarse D)."""
+    import hlhgat
+    from hlhgat.hodge_dataset import adj2par1
+    g = load_golden("sapool")
+    m = hlhgat.SAPool(**SAPOOL)
+    fill_params(m, int(g["seed"]))
+    m = m.to(cuda).train()
+    datas, pos_t, pos_s, x_t, x_s, D, _ = _sapool_inputs(g, cuda)
+    x_t.requires_grad_(True)
+    x_s.requires_grad_(True)
+    par = adj2par1(datas[0].edge_index, x_t.shape[0], x_s.shape[0])
+    y_t, y_s, _, D1, k, *_, a_t, a_s = m(x_t, x_s, par, D, datas, [pos_t], [pos_s], 0,
+                                         device=cuda)
+    assert k == int(g["k"])
+    close(D1.cpu(), g["D1"], 0, "D1")
+    for a, e in ((y_t, "out_t"), (y_s, "out_s"), (a_t, "att_t"), (a_s, "att_s")):
+        close(a.detach().cpu(), g[e], 1e-5, e)
+    Rd = lambda k_: T(g[k_]).to(cuda)  # noqa: E731
+    sum((a * Rd(r)).sum() for a, r in ((y_t, "R_t"), (y_s, "R_s"), (a_t, "R_at"),
+                                        (a_s, "R_as"))).backward()
+    close(x_t.grad.cpu(), g["grad_x_t"], 1e-4, "grad_x_t")
+    close(x_s.grad.cpu(), g["grad_x_s"], 1e-4, "grad_x_s")
+    for k_, p in m.named_parameters():
+        ref, got, scale = grad_view(g, k_, p.grad)
+        assert float((ref - got).abs().max()) <= 1e-4 * scale, k_
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("factored", [False, True])
+def test_tsp_head_cfg5_2500_nodes_vs_oracle(cuda, factored):
+    """Config 5 at its own hyperparameters on one 2500-node TSP-like graph
+    (9-NN, ~12k edges, L1 ~ 240k entries), CSR and factored L1: HIP vs the
+    fp32 / fp64 oracle (no fixture: the oracle is pinned above)."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    gph = tsp_like_graph(91, n=2500, k=9)
+    b = collate([gph], check_hodge=False)
+    m = hlhgat.HL_HGCNN_TSP_dense_int3_pyr(**CFG5)
+    fill_params(m, 5)
+    m = m.to(cuda).train()
+    bd = collate([gph], check_hodge=False).to(cuda)  # Batch.to moves in place: keep b on CPU
+    if not factored:
+        bd.edge_index_s._hlhgat_factor = None
+    else:
+        ops.mark_hodge(bd.edge_index_s)  # Hodge builder output: sorted, symmetric
+        ops.set_hodge_factor(bd.edge_index_s, bd.edge_index, bd.x_t.shape[0])
+    ops.clear_caches()
+    out, _ = m(bd)
+    op = ops.hodge_operator(bd.edge_index_s, bd.edge_weight_s, bd.x_s.shape[0])
+    assert (op.factor is not None) == factored
+    Rg = torch.randn(out.shape, generator=torch.Generator().manual_seed(3))
+    (out * Rg.to(cuda)).sum().backward()
+    res = []
+    for dt, eps, ps in ((torch.float32, 0.0, 0), (torch.float64, 0.0, 0),
+                        (torch.float64, 1e-6, 0), (torch.float64, 1e-6, 1)):
+        mo = R.RefTSPModel(**CFG5)
+        fill_params(mo, 5)
+        mo = mo.to(dt).train()
+        _perturb(mo, eps, ps)
+        d = _D()
+        for k in KEYS:
+            v = getattr(b, k)
+            setattr(d, k, v.to(dt) if v.is_floating_point() else v)
+        o, _ = mo(d)
+        (o * Rg.to(dt)).sum().backward()
+        res.append((mo, o.detach()))
+    close(out.detach().cpu(), res[1][1], 1e-4, "out vs fp64 oracle")
+    _grad_gate(m, res[0][0], res[1][0], None, _cond(res[1][0], [res[2][0], res[3][0]]))

@@ -415,11 +415,14 @@ def test_zinc_model_cfg2_vs_oracle(cuda):
     """BASELINE config 2 model at a 200-graph batch: HIP product vs oracle.
 
     Tolerance: forward output 1e-4 relative.  Gradients pass through 6 blocks of
-    batch-statistics BN, where fp32 rounding noise is amplified: the fp32 oracle
+    batch-statistics BN + ReLU, where they are ill-conditioned: the fp32 oracle
     itself deviates from an fp64 evaluation by up to ~3e-2 (relative, max-norm)
-    on deep-layer weight gradients.  So each parameter gradient of the HIP path
-    must be as close to the fp64 oracle as the fp32 oracle is (<= 3x its error,
-    floor 1e-4 relative)."""
+    on deep-layer weight gradients, and a 1e-6 relative change of the weights
+    moves the fp64 gradients by as much (pre-ReLU values within rounding of 0
+    flip masks).  So each parameter gradient of the HIP path must be within 3x
+    the larger of the fp32 oracle's distance to fp64 and that conditioning
+    (two perturbed fp64 runs), floor 1e-4 relative (tests/test_baseline_configs.py
+    applies the same gate to configs 3-5)."""
     import hlhgat
     from hlhgat.synthetic import zinc_like_batch
     b = zinc_like_batch(200, seed=21)
@@ -443,6 +446,15 @@ def test_zinc_model_cfg2_vs_oracle(cuda):
         setattr(b64, k, v.double() if v.is_floating_point() else v)
     out_r = ref(b)
     out_64 = ref64(b64)
+    pert = []
+    for ps in (0, 1):  # conditioning probe: fp64 at weights * (1 + 1e-6 N(0,1))
+        mp = R.RefZincModel(**kw).double()
+        mp.load_state_dict(ref64.state_dict())
+        gen = torch.Generator().manual_seed(ps)
+        with torch.no_grad():
+            for p in mp.parameters():
+                p.mul_(1 + 1e-6 * torch.randn(p.shape, generator=gen, dtype=torch.float64))
+        pert.append((mp.train(), mp(b64)))
     bd = zinc_like_batch(200, seed=21).to(cuda)
     out = m(bd)
     close(out.detach().cpu(), out_r.detach(), 1e-4, "out")
@@ -450,14 +462,18 @@ def test_zinc_model_cfg2_vs_oracle(cuda):
     (out * dev(Rg)).sum().backward()
     (out_r * Rg).sum().backward()
     (out_64 * Rg.double()).sum().backward()
+    for mp, op in pert:
+        (op * Rg.double()).sum().backward()
     rp = dict(ref.named_parameters())
     r64 = dict(ref64.named_parameters())
+    pp = [dict(mp.named_parameters()) for mp, _ in pert]
     for k, p in m.named_parameters():
         e = r64[k].grad
         scale = max(1.0, e.abs().max().item())
         err_ref = (rp[k].grad.double() - e).abs().max().item() / scale
+        cond = max((q[k].grad - e).abs().max().item() / scale for q in pp)
         err_hip = (p.grad.cpu().double() - e).abs().max().item() / scale
-        assert err_hip <= max(3 * err_ref, 1e-4), (k, err_hip, err_ref)
+        assert err_hip <= max(3 * max(err_ref, cond), 1e-4), (k, err_hip, err_ref, cond)
 
 
 # ---------------------------------------------------------------------------
@@ -1111,3 +1127,41 @@ def test_bn_one_launch_timeout_raises(cuda):
         _lib.LIB.hlhgat_set_bn_one_launch(prior)
         torch.cuda.synchronize()
         ops.clear_device_errors()
+
+
+def test_boundary_operator_reference_lines_verbatim(cuda):
+    """The reference's own sparse products run unchanged on hlhgat.adj2par1:
+    torch.sparse.mm(par_1.transpose(0,1), x_t).abs()/2 (lib/Hodge_ST_Model.py:
+    848), torch.sparse.mm(par.abs(), x_s) and torch.sparse.mm(par.abs().
+    transpose(0,1), x_t) (lib/Hodge_Cheb_Conv.py:294-295), B1 @ y -- bitwise
+    the coalesced torch.sparse.mm of the reference's COO, gradients included."""
+    from hlhgat.hodge_dataset import adj2par1
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(30, seed=8)
+    N, E = b.x_t.shape[0], b.x_s.shape[0]
+    ref_P = R.adj2par1(b.edge_index, N, E).coalesce()
+    par_1 = adj2par1(dev(b.edge_index), N, E)
+    gen = torch.Generator().manual_seed(3)
+    x_t = torch.randn(N, 20, generator=gen)
+    x_s = torch.randn(E, 20, generator=gen)
+    cases = [
+        (lambda P, xt, xs: torch.sparse.mm(P.transpose(0, 1), xt).abs() / 2, "readout :848"),
+        (lambda P, xt, xs: torch.sparse.mm(P.abs(), xs), "|B1| x_s :294"),
+        (lambda P, xt, xs: torch.sparse.mm(P.abs().transpose(0, 1), xt) / 2, "|B1|^T x_t :295"),
+        (lambda P, xt, xs: torch.mm(P, xs), "B1 x_s"),
+        (lambda P, xt, xs: P.t() @ xt, "B1^T @ x_t"),
+    ]
+    for fn, what in cases:
+        xt_r, xs_r = x_t.clone().requires_grad_(True), x_s.clone().requires_grad_(True)
+        y_r = fn(ref_P, xt_r, xs_r)
+        xt_d, xs_d = dev(x_t).requires_grad_(True), dev(x_s).requires_grad_(True)
+        y_d = fn(par_1, xt_d, xs_d)
+        assert torch.equal(y_d.detach().cpu(), y_r.detach()), what
+        Rg = torch.randn(y_r.shape, generator=gen)
+        (y_r * Rg).sum().backward()
+        (y_d * dev(Rg)).sum().backward()
+        for a, r in ((xt_d, xt_r), (xs_d, xs_r)):
+            if r.grad is None:
+                assert a.grad is None or not a.grad.any(), what
+            else:
+                close(a.grad.cpu(), r.grad, 1e-6, what + " grad")

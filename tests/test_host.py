@@ -386,3 +386,25 @@ def test_brain_skeleton_coo_rebuild_matches_reference():
         assert float(w.double().sum()) == float(g[f"{side}/w_sum64"])
         assert float(w.double().abs().sum()) == float(g[f"{side}/w_abs_sum64"])
     assert hodge_factor_ok(g["edge_index"], int(g["n_nodes"]), ei_s.numpy(), w_s.numpy())
+
+
+def test_boundary_operator_views_match_reference_adj2par1():
+    """adj2par1 views (.abs(), .t(), .transpose(0, 1)) densify to the reference's
+    sparse B1 (adj2par1_small golden) and its |.| / transpose; products need the
+    ROCm device (no CPU fallback)."""
+    import pytest
+    import torch
+    from conftest import load_golden
+    from hlhgat.hodge_dataset import adj2par1
+    g = load_golden("adj2par1_small")
+    ei = torch.from_numpy(g["edge_index"])
+    P = adj2par1(ei, int(g["n_nodes"]), ei.shape[1])
+    dense = torch.from_numpy(g["dense"])
+    assert torch.equal(P.to_dense(), dense)
+    assert torch.equal(P.abs().to_dense(), dense.abs())
+    assert torch.equal(P.transpose(0, 1).to_dense(), dense.t())
+    assert torch.equal(P.t().abs().to_dense(), dense.abs().t())
+    assert P.t().shape == (ei.shape[1], int(g["n_nodes"])) and P.T.t().shape == P.shape
+    assert P.t().incidence is not None and P.abs()._base is P
+    with pytest.raises(RuntimeError, match="ROCm"):
+        torch.sparse.mm(P.transpose(0, 1), torch.ones(int(g["n_nodes"]), 3))

@@ -115,3 +115,58 @@ def test_oracle_propagate_is_sequential_scatter():
     out = R.propagate(x, ei, w)
     exp = torch.tensor([[6.0 - 5.0, 8.0 - 6.0], [0.5, 1.0], [15.0, 18.0]])
     assert torch.equal(out, exp)
+
+
+_KEYS = ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+         "edge_index", "num_node1", "num_edge1")
+
+
+def _data(g, prefix=""):
+    d = _D()
+    for k in _KEYS:
+        setattr(d, k, T(g[prefix + k]))
+    return d
+
+
+def _check_grads(m, g, tol=1e-4):
+    import re
+    for k, p in m.named_parameters():
+        if "nograd/" + k in g:
+            assert p.grad is None, k
+            continue
+        if re.search(r"module_[04]\.bias$", k) and not k.startswith("out."):
+            # a conv bias feeding a training-mode BatchNorm: analytically zero
+            # gradient, both sides hold fp32 rounding noise only
+            assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
+            continue
+        close(p.grad, g["grad/" + k], tol, "grad " + k)
+
+
+def test_tsp_model_oracle():
+    """RefTSPModel (lib/Hodge_ST_Model.py:756-855) vs the reference's own
+    forward / backward (tsp_model_small, make_golden.py tsp_case)."""
+    g = load_golden("tsp_model_small")
+    m = R.RefTSPModel(channels=[1, 1], filters=[16, 16], mlp_channels=[32], K=3)
+    m.load_state_dict(_sd(g))
+    m.train()
+    out, s_batch = m(_data(g))
+    assert torch.equal(s_batch, T(g["s_batch"]))
+    close(out.detach(), g["out"], 1e-5, "out")
+    (out * T(g["R"])).sum().backward()
+    _check_grads(m, g)
+
+
+@pytest.mark.parametrize("name", ["attpool_cifar_small", "attpool_pepfunc_small"])
+def test_attpool_oracle(name):
+    """RefCifarAttPool (lib/Hodge_ST_Model.py:958-1091) / RefPepfuncAttPool
+    (main_pepfunc...:36-168) vs the reference heads on two-level MLGC batches
+    (make_golden_attpool.py)."""
+    g = load_golden(name)
+    cls = R.RefCifarAttPool if "cifar" in name else R.RefPepfuncAttPool
+    m = cls(channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)
+    m.load_state_dict(_sd(g))
+    m.train()
+    out = m([_data(g, "l0/"), _data(g, "l1/")])
+    close(out.detach(), g["out"], 1e-5, "out")
+    (out * T(g["R"])).sum().backward()
+    _check_grads(m, g)
