@@ -4,22 +4,38 @@
 // (lib/Hodge_ST_Model.py:556-566) and every NodeEdgeInt value MLP is
 // Linear -> BatchNorm1d -> ReLU twice (lib/Hodge_Cheb_Conv.py:276-289), so
 // each conv output passes through a batch-statistics reduction over all
-// simplices.  Two launches per direction:
-//   fwd: k_bn_stats  — per-workgroup column partials (fp64 sum, sum of squares)
-//                      and, in the LAST workgroup to arrive, the final mean /
-//                      invstd and the running-stat update (deterministic: the
-//                      last arriver sums the partials in workgroup order);
-//        k_bn_apply  — y = relu?((x - mean) * s + bias).
-//        (default: k_bn_train_fused, both in ONE launch when the grid is
-//        provably co-resident; see hlhgat_bn_fwd_train)
-//   bwd: k_bn_bwd_reduce — partials of sum(g) and sum(g*(x-mean)), g = dy *
-//                      [y > 0]; the last arriver forms dweight, dbias and the
-//                      per-channel coefficients of dx;
-//        k_bn_bwd_apply  — dx = a*g + b*(x - mean) + c (centred: no cancellation).
-// Inter-workgroup hand-off follows MI355X_MICROARCH.md / cdna_hip_programming.md
-// Guideline 16: plain stores, every wave's vmcnt(0), barrier, lane-0 agent
-// release fence, relaxed agent atomic ticket; the last arriver issues an
-// agent acquire fence before reading the partials.
+// simplices (40 per direction in the config-2 step).
+//
+// The rows are split into `parts` row partitions x `tiles` column tiles, one
+// workgroup each; every workgroup writes fp64 column partials (forward: sum,
+// sum of squares; backward: sum g, sum g (x - mean), g = dy masked by the ReLU).
+//
+// Forward in ONE launch (default, k_bn_fwd_grid) when the whole grid is
+// provably co-resident: each workgroup keeps its rows in REGISTERS, writes its
+// partials, meets the other partitions of its column tile at a bounded grid
+// barrier, sums ALL partials itself in a fixed order (flat_reduce), and
+// normalises from the registers -- no second read of x, no last-arriver tail,
+// no flag hand-off.  Workgroup 0 of a tile writes the saved and running
+// statistics.  (The same structure for the backward ran 12 % faster alone,
+// 31.8 vs 35.5 us per fwd+bwd at the ZINC shape, but made the training step
+// 1.2 % SLOWER in a same-box A/B -- its register-heavy workgroups wait at the
+// barrier while the other stream's kernels need the CUs -- so it was removed.)
+//
+// Otherwise, and always for the backward: two launches, k_bn_stats /
+// k_bn_bwd_reduce (the last workgroup to arrive sums the partials -- in the
+// same flat order up to kFlatMax partitions, so both forward paths give
+// bitwise the same results; a two-level last-arriver tree above) then
+// k_bn_apply / k_bn_bwd_apply.
+//
+// Arithmetic (both paths): mean = S0/n, var = S1/n - mean^2 (fp64),
+// invstd = 1/sqrt(var + eps); y = relu?((x - mean) * w invstd + b);
+// dx = A g + (B (x - mean) + C) with A = w is, B = -w is^3 Sgx/n,
+// C = -w is Sg/n -- the centred forms, as torch evaluates them.
+//
+// Inter-workgroup hand-off (MI355X_MICROARCH.md / cdna_hip_programming.md
+// Guideline 16): partials are written through with agent-scope atomic stores
+// drained by vmcnt(0) before a barrier; one lane takes a relaxed agent atomic
+// ticket; readers use agent-scope atomic loads.
 #include "common.h"
 
 #include <cstdlib>
@@ -30,13 +46,15 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxParts = 512;
-constexpr int kGroup = 16;                        // partitions per first-level group
+constexpr int kFlatMax = 256;                     // flat reduction order up to this many parts
+constexpr int kGroup = 16;                        // partitions per first-level tree group
 constexpr int kMaxGroups = kMaxParts / kGroup;
 constexpr int kMaxTiles = 1024;
-constexpr int kFlagBase = kMaxTiles * (1 + kMaxGroups);  // per tile: top + group counters
-// + per tile: the one-launch forward's "statistics ready" flag and leave counter
-constexpr int kCounters = kFlagBase + 2 * kMaxTiles;
+constexpr int kGridBase = kMaxTiles * (1 + kMaxGroups);  // per tile: top + group counters
+// + per tile: the one-launch kernels' barrier arrival and leave counters
+constexpr int kCounters = kGridBase + 2 * kMaxTiles;
 constexpr int APPLY_RPT = 2;  // rows per thread in the elementwise apply kernels
+constexpr int kMaxRpt = 32;   // rows per thread the one-launch kernels hold in registers
 
 struct BnLayout {
   int v;       // floats per thread (4 or 1)
@@ -48,21 +66,8 @@ struct BnLayout {
   int64_t rows_per_part;
 };
 
-// Row partitions of the statistics pass: each partition is one workgroup
-// whose loads are all in flight within a couple of round trips.  The
-// partials are combined by a two-level last-arriver tree (groups of kGroup
-// partitions, then the groups), so many thin partitions cost two short tails
-// instead of one long one.  In the ZINC step 64 partitions measured best
-// (256: 264k -> 251k graphs/s; more workgroups crowd the concurrent chain).
-// HLHGAT_BN_PARTS overrides (A/B measurements).
-// Larger batches (config 3 / 5 heads: 1.4e5-2e5 rows) get one partition per
-// 512 rows (up to kMaxParts): 64 workgroups leave most of the 256 CUs idle
-// there (k_bn_bwd_reduce ran at ~1 TB/s, profiles/r01_h_*_head_kernel_stats.md).
-// HLHGAT_BN_ONE_LAUNCH=0: BatchNorm forward statistics and apply as two
-// launches instead of k_bn_train_fused (bitwise the same results).  Same-box
-// A/B at the ZINC step with 128 partitions: 288.6k -> 291.1k graphs/s over
-// five runs each (every one-launch run above every two-launch run; with 64
-// partitions it was neutral).
+// HLHGAT_BN_ONE_LAUNCH=0: two launches per direction even where one fits
+// (A/B; bitwise the same results).
 bool& bn_one_launch_flag() {
   static bool v = [] {
     const char* e = getenv("HLHGAT_BN_ONE_LAUNCH");
@@ -72,28 +77,31 @@ bool& bn_one_launch_flag() {
 }
 bool bn_one_launch() { return bn_one_launch_flag(); }
 
+// Row partitions: >= 128 (same-box A/B at the ZINC step, n ~ 25k: 64 ->
+// 281.8k, 128 -> 287.2k, 256 -> 286.1k, 32 -> 265.8k graphs/s), one per 512
+// rows above (config 3 / 5 heads, 1.4e5-2e5 rows: 64 workgroups left most of
+// the 256 CUs idle).  HLHGAT_BN_PARTS overrides (A/B).
 int64_t bn_parts(int64_t n) {
   static int64_t fixed = [] {
     const char* e = getenv("HLHGAT_BN_PARTS");
     return e ? atoll(e) : (int64_t)0;
   }();
-  // >= 128 partitions (same-box A/B at the ZINC step, n ~ 25k: 64 -> 281.8k,
-  // 128 -> 287.2k, 256 -> 286.1k, 32 -> 265.8k graphs/s), ~512 rows each above
   int64_t p = fixed > 0 ? fixed : std::max<int64_t>(128, ceil_div(n, (int64_t)512));
+  // small batches (the readout MLP: one row per graph): >= 64 rows per
+  // partition, so the finaliser's partial loads stay one batch deep
+  if (!fixed) p = std::min<int64_t>(p, std::max<int64_t>(1, ceil_div(n, (int64_t)64)));
   return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
 }
 
-BnLayout bn_layout(int64_t n, int64_t C, bool vec, int nt = kThreads) {
+BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   BnLayout L;
   L.v = vec ? 4 : 1;
   int lanes = (int)ceil_div(C, L.v);
   L.tpr = next_pow2(lanes);
   if (L.tpr > kThreads / L.v) L.tpr = kThreads / L.v;  // tile_c <= kThreads
-  L.rp = nt / L.tpr;
+  L.rp = kThreads / L.tpr;
   L.tile_c = L.tpr * L.v;
   L.tiles = (int)ceil_div(C, L.tile_c);
-  // <= kMaxParts row partitions per column tile (fat partitions keep the
-  // last arriver's reduction to one batch of loads per thread)
   int64_t parts = bn_parts(n);
   int64_t max_parts = ceil_div(n, (int64_t)L.rp * 2);
   if (parts > max_parts) parts = max_parts;
@@ -173,18 +181,14 @@ struct StatsArgs {
   float* coef;
   float* dweight;
   float* dbias;
-  // one-launch forward: poll limit of the statistics wait, host-visible error word
+  // one-launch kernels: output rows, poll limit of the barrier, error word
+  float* out;
+  int64_t ldo;
+  int relu;
   unsigned poll_limit;
   unsigned* err;
 };
 
-// Partials are handed to the last-arriving workgroup WRITE-THROUGH: 8-byte
-// agent-scope atomic stores (global_store_dwordx2 sc1) drained by every
-// storing wave, read back with sc1 loads -- no release fence (buffer_wbl2,
-// which writes back the XCD L2's dirty lines: the freshly written BN input
-// and everything else the concurrent stream left dirty, 1.7-6.5 us per
-// workgroup) and no acquire fence (cdna_hip_programming.md Guideline 16 R1;
-// MI355X_MICROARCH.md visibility table).
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 __device__ __forceinline__ void st_wt(double* p, double v) {
   __hip_atomic_store((gu64_t*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
@@ -195,11 +199,11 @@ __device__ __forceinline__ double ld_wt(const double* p) {
       (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// wait timeouts of the one-launch BatchNorm (hlhgat_bn_wait_timeouts)
+// wait timeouts of the one-launch kernels (hlhgat_bn_wait_timeouts)
 __device__ unsigned g_bn_wait_timeouts = 0;
 
-// A waiting workgroup that gives up (poll limit reached) must not normalise
-// with stale statistics: it writes NaN into its rows, counts the timeout and
+// A workgroup that gives up at the barrier (poll limit reached) must not use
+// partial statistics: it writes NaN into its rows, counts the timeout and
 // raises HLHGAT_DEVERR_BN_WAIT in the host-visible error word
 // (hlhgat_device_errors), which hlhgat.train.TrainStep, the bench and
 // hlhgat.ops.check_device_errors turn into a Python exception.
@@ -209,15 +213,52 @@ __device__ __forceinline__ void report_wait_timeout(unsigned* err) {
                               __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Bounded wait of a non-finalising workgroup for its tile's statistics flag;
-// poll_limit == 0 (test hook) gives up at once.  Returns false on timeout.
-__device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned poll_limit, unsigned* err) {
-  __shared__ unsigned s_ok;
+// Signal arrival; returns true in the last workgroup of `total`.  Every wave
+// has drained its write-through partial stores (vmcnt(0)) before the barrier;
+// ONE lane adds to the counter; the workgroup whose add returned total-1
+// resets it and reads the partials after the second barrier.
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
+    unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == total - 1) ? 1u : 0u;
+    if (s_last) *counter = 0u;  // ready for the next launch (stream-ordered)
+  }
+  __syncthreads();
+  return s_last != 0u;
+}
+
+// Grid barrier of the `total` workgroups of one column tile (all co-resident,
+// see pick_grid) on ONE 64-bit word: count in the low half, generation in the
+// high half.  Every workgroup adds 1; the one that completes the count turns
+// it back to 0 and bumps the generation in the same word (a single atomic add
+// of 2^32 - total), the others poll until the generation changes or the poll
+// limit runs out (poll_limit == 0, a test hook: give up at once).  Nothing is
+// left to reset afterwards, whatever `total` the next launch uses.  Returns
+// false on timeout.
+typedef __attribute__((address_space(1))) unsigned long long gu64c_t;
+__device__ __forceinline__ bool bar_wait(unsigned long long* word, unsigned total,
+                                         unsigned poll_limit, unsigned* err) {
+  __shared__ unsigned s_ok;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long old =
+        __hip_atomic_fetch_add((gu64c_t*)word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned ok = 0;
-    if (poll_limit > 0) {
+    if ((unsigned)(old & 0xffffffffull) == total - 1) {
+      __hip_atomic_fetch_add((gu64c_t*)word, (1ull << 32) - (unsigned long long)total,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = 1;
+    } else {
+      const unsigned gen = (unsigned)(old >> 32);
       for (unsigned it = 0; it < poll_limit; ++it) {
-        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        const unsigned long long w =
+            __hip_atomic_load((gu64c_t*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(w >> 32) != gen) {
           ok = 1;
           break;
         }
@@ -231,31 +272,9 @@ __device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned poll_limit, u
   return s_ok != 0u;
 }
 
-typedef __attribute__((address_space(1))) unsigned gu32_t;
-__device__ __forceinline__ void st_wt32(float* p, float v) {
-  __hip_atomic_store((gu32_t*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt32(const float* p) {
-  return __uint_as_float(
-      __hip_atomic_load((gu32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Signal arrival; returns true in the last workgroup of this column tile.
-// Every wave has drained its write-through partial stores (vmcnt(0)) before
-// the barrier; ONE lane adds to the counter; the workgroup whose add returned
-// total-1 reads the partials (sc1 loads) after the second barrier.
-__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
-  __shared__ unsigned s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == total - 1) ? 1u : 0u;
-    if (s_last) *counter = 0u;  // ready for the next launch (stream-ordered)
-  }
-  __syncthreads();
-  return s_last != 0u;
+// the barrier word of this launch's column tile (8-byte aligned: kGridBase is even)
+__device__ __forceinline__ unsigned long long* barrier_word(const StatsArgs& a) {
+  return reinterpret_cast<unsigned long long*>(a.count + kGridBase) + blockIdx.y;
 }
 
 // Block-level column partials: threads (row group rg, column lane cl) hold V
@@ -287,10 +306,56 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
   }
 }
 
+// The flat order (both paths, parts <= kFlatMax): thread group j of G =
+// NT / tile_c sums partials p = j, j + G, j + 2G, ... in ascending order
+// (loads in batches of 32), then the groups are added in order 0..G-1.
+// Result in out0 / out1[0 .. tile_c).
+template <int NT>
+__device__ __forceinline__ void flat_reduce(const double* src, int parts, const StatsArgs& a,
+                                            int c0, int tile_c, double* out0, double* out1) {
+  __shared__ double fin[2][NT];
+  const int G = NT / tile_c > 0 ? NT / tile_c : 1;
+  const int t = threadIdx.x % tile_c;
+  const int j = threadIdx.x / tile_c;
+  const int c = c0 + t;
+  double u0 = 0.0, u1 = 0.0;
+  if (j < G && c < a.C) {
+    for (int p0 = j; p0 < parts; p0 += 32 * G) {  // 32 loads of each in flight
+      double v0[32], v1[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int p = p0 + u * G;
+        const bool ok = p < parts;
+        const double* q = src + ((int64_t)(ok ? p : 0) * a.C + c) * 2;
+        v0[u] = ok ? ld_wt(q) : 0.0;
+        v1[u] = ok ? ld_wt(q + 1) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        u0 += v0[u];
+        u1 += v1[u];
+      }
+    }
+  }
+  fin[0][threadIdx.x] = u0;
+  fin[1][threadIdx.x] = u1;
+  __syncthreads();
+  if (threadIdx.x < tile_c) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int g = 0; g < G; ++g) {
+      s0 += fin[0][g * tile_c + threadIdx.x];
+      s1 += fin[1][g * tile_c + threadIdx.x];
+    }
+    out0[threadIdx.x] = s0;
+    out1[threadIdx.x] = s1;
+  }
+  __syncthreads();
+}
+
 // Sum of partials [first, first+count) of src ([*][C][2]) for the tile's
-// columns: all 256 threads take part (column t % tile_c, partial group
-// t / tile_c, loads in batches of 16), groups combined in fixed order through
-// LDS -> deterministic.  Result in out0/out1[0 .. tile_c).
+// columns (the tree levels, parts > kFlatMax): all threads take part (column
+// t % tile_c, partial group t / tile_c, loads in batches of 16), groups
+// combined in fixed order through LDS -> deterministic.
 template <int NT>
 __device__ __forceinline__ void reduce_range(const double* src, int first, int count,
                                              const StatsArgs& a, int c0, int tile_c,
@@ -336,21 +401,24 @@ __device__ __forceinline__ void reduce_range(const double* src, int first, int c
   __syncthreads();
 }
 
-// Two-level last-arriver tree over the `parts` partials of this column tile:
-// the last workgroup of each group of kGroup partitions sums its group, the
-// last group sums the group partials.  Returns true (sums in out0/out1) in
-// the one workgroup that finalises; fixed summation order at both levels.
+// The two-launch reduction: true (sums in out0/out1) in the one workgroup of
+// the column tile that finalises.  Flat order up to kFlatMax partitions
+// (one arrival counter), else a two-level last-arriver tree.
 template <int NT>
-__device__ __forceinline__ bool tree_reduce(const StatsArgs& a, int c0, int tile_c,
+__device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile_c,
                                             double* out0, double* out1) {
   const int tile = blockIdx.y;
+  if (a.parts <= kFlatMax) {
+    if (!arrive_last(a.count + tile, (unsigned)a.parts)) return false;
+    flat_reduce<NT>(a.part, a.parts, a, c0, tile_c, out0, out1);
+    return true;
+  }
   const int g = blockIdx.x / kGroup;
   const int ng = (a.parts + kGroup - 1) / kGroup;
   const int first = g * kGroup;
   const int cnt = a.parts - first < kGroup ? a.parts - first : kGroup;
   if (!arrive_last(a.count + kMaxTiles + tile * kMaxGroups + g, (unsigned)cnt)) return false;
   reduce_range<NT>(a.part, first, cnt, a, c0, tile_c, out0, out1);
-  if (ng == 1) return true;
   for (int t = threadIdx.x; t < tile_c; t += NT) {
     const int c = c0 + t;
     if (c < a.C) {
@@ -364,30 +432,40 @@ __device__ __forceinline__ bool tree_reduce(const StatsArgs& a, int c0, int tile
   return true;
 }
 
-struct ApplyArgs {
-  const int32_t* nvalid;
-  const float* x;
-  int64_t ldx;
-  float* y;
-  int64_t ldy;
-  int64_t n;
-  int C;
-  const float* mean;
-  const float* invstd;
-  const float* weight;
-  const float* bias;
-  int relu;
-  int tpr, rp;
-};
+// Forward finalisation of one column (both paths): mean, invstd, and the
+// running statistics when `update`.
+__device__ __forceinline__ void fwd_finalize(const StatsArgs& a, int cc, double u0, double u1,
+                                             int64_t n_eff, float& mean_f, float& invstd_f,
+                                             bool update) {
+  const double nn = (double)(n_eff > 0 ? n_eff : 1);
+  const double mean = u0 / nn;
+  double var = u1 / nn - mean * mean;
+  if (var < 0.0) var = 0.0;
+  mean_f = (float)mean;
+  invstd_f = (float)(1.0 / sqrt(var + (double)a.eps));
+  if (update && a.running_mean) {
+    const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
+    a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
+    a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
+  }
+}
 
-// Statistics (and, APPLY, the normalisation in the same launch): with APPLY
-// the finalising workgroup of a column tile publishes mean / invstd write-
-// through and raises the tile's flag; the other workgroups of the tile (all
-// co-resident: parts x tiles <= a few hundred workgroups of 256 threads) wait
-// for it, normalise the rows they summed, and the last to leave resets the
-// flag.  The wait is bounded so a stalled launch cannot hang the GPU.
-template <int V, int NT, bool APPLY>
-__device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArgs& p) {
+// Backward coefficients of one column (both paths): dx = A g + (B (x - mean) + C).
+__device__ __forceinline__ void bwd_coefs(float is_f, float w_f, double sg, double sgx,
+                                          int64_t n_eff, float& A, float& B, float& Cc) {
+  const double is = (double)is_f;
+  const double w = (double)w_f;
+  const double nn = (double)(n_eff > 0 ? n_eff : 1);
+  A = (float)(w * is);
+  B = (float)(-w * is * is * is * sgx / nn);
+  Cc = (float)(-w * is * sg / nn);
+}
+
+// ---------------------------------------------------------------------------
+// two-launch path
+// ---------------------------------------------------------------------------
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -425,106 +503,36 @@ __device__ __forceinline__ void bn_stats_body(const StatsArgs& a, const ApplyArg
       }
     }
   }
-  write_partials<V, NT>(s0, s1, a, c0);
-  // the finalising workgroup of this column tile: finalise its columns
+  write_partials<V, kThreads>(s0, s1, a, c0);
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  const bool fin = tree_reduce<NT>(a, c0, tile_c, sum0, sum1);
-  if (!APPLY && !fin) return;
-  if (fin) {
-    for (int t = threadIdx.x; t < tile_c; t += NT) {
-      const int cc = c0 + t;
-      if (cc >= a.C) continue;
-      const double u0 = sum0[t], u1 = sum1[t];
-      const double nn = (double)(n_eff > 0 ? n_eff : 1);
-      const double mean = u0 / nn;
-      double var = u1 / nn - mean * mean;
-      if (var < 0.0) var = 0.0;
-      const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-      if (APPLY) {
-        st_wt32(&a.save_mean[cc], (float)mean);
-        st_wt32(&a.save_invstd[cc], invstd);
-      } else {
-        a.save_mean[cc] = (float)mean;
-        a.save_invstd[cc] = invstd;
-      }
-      if (a.running_mean) {
-        const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
-        a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
-        a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
-      }
-    }
-    if (a.nbt && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1)) return;
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+    const int cc = c0 + t;
+    if (cc >= a.C) continue;
+    float m, is;
+    fwd_finalize(a, cc, sum0[t], sum1[t], n_eff, m, is, true);
+    a.save_mean[cc] = m;
+    a.save_invstd[cc] = is;
   }
-  if (!APPLY) return;
-  unsigned* flag = a.count + kFlagBase + blockIdx.y;
-  unsigned* leave = flag + kMaxTiles;
-  if (fin) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // a timed-out workgroup poisons its rows (NaN) instead of applying stale statistics
-  const bool ok = fin || wait_flag(flag, a.poll_limit, a.err);
-  if (c < a.C) {
-    float sc[V], mu[V], sh[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      const float w = p.weight ? p.weight[c + v] : 1.f;
-      sc[v] = ok ? w * ld_wt32(&p.invstd[c + v]) : __builtin_nanf("");
-      mu[v] = ok ? ld_wt32(&p.mean[c + v]) : __builtin_nanf("");
-      sh[v] = p.bias ? p.bias[c + v] : 0.f;
-    }
-    int64_t r_end = r_lo + a.rows_per_part;
-    if (r_end > a.n) r_end = a.n;
-    auto out = [&](int64_t r, vt xv) {
-      vt o;
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        float z = (vget(xv, v) - mu[v]) * sc[v] + sh[v];
-        vget(o, v) = r >= n_eff ? 0.f : ((p.relu && z < 0.f) ? 0.f : z);  // NaN passes
-      }
-      vstore<V>(p.y + r * p.ldy + c, o);
-    };
-    int64_t r = r_lo + rg;
-    for (; r + 7 * a.rp < r_end; r += 8 * a.rp) {  // 8 rows in flight
-      vt x4[8] = {};
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t rr = r + u * a.rp;
-        if (rr < n_eff) x4[u] = vload<V>(a.x + rr * a.ldx + c);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) out(r + u * a.rp, x4[u]);
-    }
-    for (; r < r_end; r += a.rp) {
-      vt xv{};
-      if (r < n_eff) xv = vload<V>(a.x + r * a.ldx + c);
-      out(r, xv);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev =
-        __hip_atomic_fetch_add(leave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {  // every workgroup of the tile has read the flag
-      __hip_atomic_store(leave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (a.nbt && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
 }
 
-template <int V, int NT>
-__global__ __launch_bounds__(NT) void k_bn_stats(StatsArgs a) {
-  bn_stats_body<V, NT, false>(a, ApplyArgs{});
-}
-
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_train_fused(StatsArgs a, ApplyArgs p) {
-  bn_stats_body<V, kThreads, true>(a, p);
-}
-
+struct ApplyArgs {
+  const int32_t* nvalid;
+  const float* x;
+  int64_t ldx;
+  float* y;
+  int64_t ldy;
+  int64_t n;
+  int C;
+  const float* mean;
+  const float* invstd;
+  const float* weight;
+  const float* bias;
+  int relu;
+  int tpr, rp;
+};
 
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
@@ -537,10 +545,9 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const float w = a.weight ? a.weight[c + v] : 1.f;
-    const float b = a.bias ? a.bias[c + v] : 0.f;
     s[v] = w * a.invstd[c + v];
     m[v] = a.mean[c + v];
-    t[v] = b;
+    t[v] = a.bias ? a.bias[c + v] : 0.f;
   }
   // APPLY_RPT rows per thread, all loads issued before any store
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
@@ -582,10 +589,11 @@ struct BwdApplyArgs {
   int tpr, rp;
 };
 
-// Backward statistics: partials of sum(g), sum(g (x - mean)); the finalising
-// workgroup of a column tile forms dweight, dbias and dx's coefficients.
-template <int V, int NT>
-__device__ __forceinline__ void bn_bwd_body(const StatsArgs& a) {
+// Backward statistics (two-launch path): partials of sum(g), sum(g (x - mean));
+// the finalising workgroup of a column tile forms dweight, dbias and dx's
+// coefficients.
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -633,36 +641,23 @@ __device__ __forceinline__ void bn_bwd_body(const StatsArgs& a) {
       acc(xv, gv, yv);
     }
   }
-  write_partials<V, NT>(s0, s1, a, c0);
+  write_partials<V, kThreads>(s0, s1, a, c0);
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  const bool fin = tree_reduce<NT>(a, c0, tile_c, sum0, sum1);
-  if (!fin) return;
-  for (int t = threadIdx.x; t < tile_c; t += NT) {
+  if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1)) return;
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
-    const double sg = sum0[t], sgx = sum1[t];
-    const double is = (double)a.save_invstd[cc];
-    const double w = a.weight ? (double)a.weight[cc] : 1.0;
-    const double nn = (double)(n_eff > 0 ? n_eff : 1);
-    if (a.dweight) a.dweight[cc] = (float)(sgx * is);
-    if (a.dbias) a.dbias[cc] = (float)sg;
-    // dx = w*is*(g - sg/n - (x-mean)*is^2*sgx/n) = A*g + B*(x-mean) + Cc: the
-    // centred form, as torch evaluates it -- B*x + (Cc - B*mean) cancels
-    // catastrophically when a channel's variance is small against its mean
-    const double A = w * is;
-    const double B = -w * is * is * is * sgx / nn;
-    const double Cc = -w * is * sg / nn;
-    a.coef[cc] = (float)A;
-    a.coef[a.C + cc] = (float)B;
-    a.coef[2 * a.C + cc] = (float)Cc;
+    float A, B, Cc;
+    bwd_coefs(a.save_invstd[cc], a.weight ? a.weight[cc] : 1.f, sum0[t], sum1[t], n_eff, A, B,
+              Cc);
+    if (a.dweight) a.dweight[cc] = (float)(sum1[t] * (double)a.save_invstd[cc]);
+    if (a.dbias) a.dbias[cc] = (float)sum0[t];
+    a.coef[cc] = A;
+    a.coef[a.C + cc] = B;
+    a.coef[2 * a.C + cc] = Cc;
   }
 }
-template <int V, int NT>
-__global__ __launch_bounds__(NT) void k_bn_bwd_reduce(StatsArgs a) {
-  bn_bwd_body<V, NT>(a);
-}
-
 
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
@@ -706,6 +701,100 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// one-launch path: rows held in registers across a grid barrier
+// ---------------------------------------------------------------------------
+// Forward: thread (rg, cl) owns rows r_lo + rg + j * rp (j < RPT) of its
+// partition; statistics rows stop at n_eff, output rows at n.
+template <int V, int RPT>
+__global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c0 = blockIdx.y * a.tpr * V;
+  const int c = c0 + cl * V;
+  const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
+  int64_t r_hi = r_lo + a.rows_per_part;
+  if (r_hi > n_eff) r_hi = n_eff;
+  vt xr[RPT];
+  double s0[V], s1[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
+  if (c < a.C) {
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int64_t r = r_lo + rg + (int64_t)j * a.rp;
+      if (r < r_hi) xr[j] = vload<V>(a.x + r * a.ldx + c);
+    }
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {  // row order, as k_bn_stats
+      const int64_t r = r_lo + rg + (int64_t)j * a.rp;
+      if (r < r_hi) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const double xd = (double)vget(xr[j], v);
+          s0[v] += xd;
+          s1[v] += xd * xd;
+        }
+      }
+    }
+  }
+  // per-column parameters fetched before the barrier (off the critical path)
+  float wv[V], bv[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const bool in = c + v < a.C;
+    wv[v] = (a.weight && in) ? a.weight[c + v] : 1.f;
+    bv[v] = (a.bias && in) ? a.bias[c + v] : 0.f;
+  }
+  write_partials<V, kThreads>(s0, s1, a, c0);
+  const bool ok = bar_wait(barrier_word(a), gridDim.x, a.poll_limit, a.err);
+  __shared__ double sum0[kThreads], sum1[kThreads];
+  __shared__ float sm[kThreads], ss[kThreads];
+  const int tile_c = a.tpr * V;
+  if (ok) flat_reduce<kThreads>(a.part, gridDim.x, a, c0, tile_c, sum0, sum1);
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+    const int cc = c0 + t;
+    float m = __builtin_nanf(""), is = __builtin_nanf("");
+    if (ok && cc < a.C) {
+      fwd_finalize(a, cc, sum0[t], sum1[t], n_eff, m, is, blockIdx.x == 0);
+      if (blockIdx.x == 0) {
+        a.save_mean[cc] = m;
+        a.save_invstd[cc] = is;
+      }
+    }
+    sm[t] = m;
+    ss[t] = is;
+  }
+  if (ok && a.nbt && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  __syncthreads();
+  if (c < a.C) {
+    float sc[V], mu[V], sh[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      sc[v] = wv[v] * ss[cl * V + v];  // NaN after a barrier timeout
+      mu[v] = sm[cl * V + v];
+      sh[v] = bv[v];
+    }
+    int64_t r_end = r_lo + a.rows_per_part;
+    if (r_end > a.n) r_end = a.n;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int64_t r = r_lo + rg + (int64_t)j * a.rp;
+      if (r < r_end) {
+        vt o;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float z = (vget(xr[j], v) - mu[v]) * sc[v] + sh[v];
+          vget(o, v) = r >= n_eff ? 0.f : ((a.relu && z < 0.f) ? 0.f : z);  // NaN passes
+        }
+        vstore<V>(a.out + r * a.ldo + c, o);
+      }
+    }
+  }
+}
+
 bool bn_vec_ok(int64_t C, std::initializer_list<int64_t> lds,
                std::initializer_list<const void*> ptrs) {
   if (C % 4) return false;
@@ -741,32 +830,75 @@ StatsArgs stats_args(const BnLayout& L, const BnWs& w, const float* x, int64_t l
   return s;
 }
 
-// --- one-launch forward: co-residency and the poll limit -------------------
-// k_bn_train_fused's waiting workgroups need their tile's finalising
-// workgroup to be resident at the same time.  The launch is used only when
-// the whole grid fits in a QUARTER of the chip's resident-workgroup capacity
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs), so the node / edge /
-// interaction streams each running one such launch still leave room; and it
-// is capped at 256 workgroups.  Anything that still stalls a wait is caught
-// by the bounded poll (NaN rows + HLHGAT_DEVERR_BN_WAIT, never stale numbers).
+// --- one-launch selection: co-residency and registers ------------------------
+// The one-launch kernels' barrier needs every workgroup of a column tile
+// resident at once.  They are used only when the whole grid fits in HALF of
+// the chip's resident-workgroup capacity for that kernel
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs): the HL blocks' node
+// and edge chains run on two streams (hlhgat.ops.fork) and each may be inside
+// one such launch at the same time; every other kernel on the device
+// completes without waiting, so it only delays residency.  Also: grid <= 256
+// workgroups, the partials use the flat order, and a thread's rows fit the
+// register budget (RPT <= kMaxRpt).  Anything that still stalls the barrier
+// is caught by the bounded poll (NaN rows + HLHGAT_DEVERR_BN_WAIT, never
+// numbers from partial statistics).
 unsigned g_poll_limit = 1u << 22;
 
-int64_t fused_capacity(bool vec) {
-  static int64_t cap[2] = {-1, -1};
-  int64_t& c = cap[vec ? 1 : 0];
-  if (c >= 0) return c;
+int64_t capacity_of(const void* kernel) {
+  static auto* cache = new std::vector<std::pair<const void*, int64_t>>();
+  for (const auto& kv : *cache)
+    if (kv.first == kernel) return kv.second;
   int dev = 0, cus = 0, occ = 0;
-  c = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return c;
-  hipError_t e = vec ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &occ, reinterpret_cast<const void*>(&k_bn_train_fused<4>), kThreads, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                           &occ, reinterpret_cast<const void*>(&k_bn_train_fused<1>), kThreads, 0);
-  if (e != hipSuccess) return c;
-  c = (int64_t)occ * cus / 4;
+  int64_t c = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kThreads, 0) == hipSuccess)
+    c = (int64_t)occ * cus / 2;
+  cache->push_back({kernel, c});
   return c;
+}
+
+int rpt_bucket(const BnLayout& L) {
+  const int64_t need = ceil_div(L.rows_per_part, (int64_t)L.rp);
+  if (need > kMaxRpt) return 0;
+  for (int r : {2, 4, 8, 16, 32})
+    if (need <= r) return r;
+  return 0;
+}
+
+
+using GridFn = void (*)(StatsArgs);
+
+GridFn fwd_grid_fn(bool vec, int rpt) {
+  switch (rpt * 2 + (vec ? 1 : 0)) {
+    case 4: return k_bn_fwd_grid<1, 2>;
+    case 5: return k_bn_fwd_grid<4, 2>;
+    case 8: return k_bn_fwd_grid<1, 4>;
+    case 9: return k_bn_fwd_grid<4, 4>;
+    case 16: return k_bn_fwd_grid<1, 8>;
+    case 17: return k_bn_fwd_grid<4, 8>;
+    case 32: return k_bn_fwd_grid<1, 16>;
+    case 33: return k_bn_fwd_grid<4, 16>;
+    case 64: return k_bn_fwd_grid<1, 32>;
+    case 65: return k_bn_fwd_grid<4, 32>;
+    default: return nullptr;
+  }
+}
+
+// The one-launch kernel for this layout, or nullptr (two launches).
+GridFn pick_grid(const BnLayout& L, bool vec) {
+  static const bool dbg = getenv("HLHGAT_BN_DEBUG") != nullptr;
+  if (!bn_one_launch() || L.parts > kFlatMax) return nullptr;
+  const int64_t grid = (int64_t)L.parts * L.tiles;
+  const int rpt = rpt_bucket(L);
+  GridFn f = rpt ? fwd_grid_fn(vec, rpt) : nullptr;
+  const int64_t cap = f ? capacity_of(reinterpret_cast<const void*>(f)) : 0;
+  if (dbg)
+    fprintf(stderr, "[hlhgat bn] parts %d tiles %d rows/part %lld rpt %d vec %d cap %lld -> %s\n",
+            L.parts, L.tiles, (long long)L.rows_per_part, rpt, (int)vec,
+            (long long)cap, (f && grid <= 256 && grid <= cap) ? "one launch" : "two launches");
+  if (!f || grid > 256 || grid > cap) return nullptr;
+  return f;
 }
 
 }  // namespace
@@ -803,9 +935,9 @@ extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    k_bn_stats<4, kThreads><<<g1, kThreads, 0, st>>>(s);
+    k_bn_stats<4><<<g1, kThreads, 0, st>>>(s);
   else
-    k_bn_stats<1, kThreads><<<g1, kThreads, 0, st>>>(s);
+    k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -843,20 +975,20 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
                                    void* stream) {
   HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
                 "bn_fwd_train: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
-  HLH_CHECK_ARG(y, "bn_fwd_train: NULL pointer");
-  const bool vec = bn_vec_ok(C, {ldx}, {x});
+  HLH_CHECK_ARG(x && y && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
+  HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                "bn_fwd_train: running_mean/var must both be given or both NULL");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_fwd_train: workspace too small");
+  const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
   const BnLayout L = bn_layout(n, C, vec);
-  const int64_t grid = (int64_t)L.parts * L.tiles;
-  if (bn_one_launch() && grid <= 256 && grid <= fused_capacity(vec) &&
-      vec == bn_vec_ok(C, {ldx, ldy}, {x, y})) {
-    // statistics and normalisation in one launch (k_bn_train_fused)
-    HLH_CHECK_ARG(x && save_mean && save_invstd, "bn_fwd_train: NULL pointer");
-    HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
-                  "bn_fwd_train: running_mean/var must both be given or both NULL");
-    HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
-                  "bn_fwd_train: workspace too small");
-    HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_fwd_train: C too large");
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_fwd_train: C too large");
+  // the two-launch path must see the same layout (vector width) to give the
+  // same bits: both use bn_vec_ok over x AND y here
+  if (GridFn f = pick_grid(L, vec)) {
     StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
+    s.weight = weight;
+    s.bias = bias;
     s.running_mean = running_mean;
     s.running_var = running_var;
     s.nbt = num_batches_tracked;
@@ -864,26 +996,41 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
     s.eps = eps;
     s.save_mean = save_mean;
     s.save_invstd = save_invstd;
+    s.out = y;
+    s.ldo = ldy;
+    s.relu = relu;
     s.poll_limit = g_poll_limit;
     s.err = hlhgat::device_error_word();
     HLH_CHECK_ARG(s.err, "bn_fwd_train: no device error word (%s)", hlhgat_last_error());
-    ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias,
-                relu, L.tpr, L.rp};
-    hipStream_t st = as_stream(stream);
-    dim3 g1(L.parts, L.tiles);
-    if (vec)
-      k_bn_train_fused<4><<<g1, kThreads, 0, st>>>(s, p);
-    else
-      k_bn_train_fused<1><<<g1, kThreads, 0, st>>>(s, p);
+    hipLaunchKernelGGL(f, dim3(L.parts, L.tiles), dim3(kThreads), 0, as_stream(stream), s);
     HLH_CHECK_LAUNCH();
     return HLHGAT_OK;
   }
-  int rc = hlhgat_bn_stats_train(x, ldx, n, n_valid, C, running_mean, running_var,
-                                 num_batches_tracked, momentum, eps, save_mean, save_invstd,
-                                 workspace, workspace_bytes, stream);
-  if (rc) return rc;
-  return hlhgat_bn_apply(x, ldx, n, n_valid, C, weight, bias, save_mean, save_invstd, relu, y,
-                         ldy, stream);
+  // two launches on the same layout
+  StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
+  s.running_mean = running_mean;
+  s.running_var = running_var;
+  s.nbt = num_batches_tracked;
+  s.momentum = momentum;
+  s.eps = eps;
+  s.save_mean = save_mean;
+  s.save_invstd = save_invstd;
+  hipStream_t st = as_stream(stream);
+  dim3 g1(L.parts, L.tiles);
+  if (vec)
+    k_bn_stats<4><<<g1, kThreads, 0, st>>>(s);
+  else
+    k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
+  HLH_CHECK_LAUNCH();
+  ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
+              L.tpr, L.rp};
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  if (vec)
+    k_bn_apply<4><<<g2, kThreads, 0, st>>>(p);
+  else
+    k_bn_apply<1><<<g2, kThreads, 0, st>>>(p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
 }
 
 extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
@@ -917,9 +1064,9 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    k_bn_bwd_reduce<4, kThreads><<<g1, kThreads, 0, st>>>(s);
+    k_bn_bwd_reduce<4><<<g1, kThreads, 0, st>>>(s);
   else
-    k_bn_bwd_reduce<1, kThreads><<<g1, kThreads, 0, st>>>(s);
+    k_bn_bwd_reduce<1><<<g1, kThreads, 0, st>>>(s);
   HLH_CHECK_LAUNCH();
   BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, save_mean,
                  L.tpr, L.rp};

@@ -431,13 +431,15 @@ int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_val
                     const float* save_invstd, int relu, float* y, int64_t ldy, void* stream);
 
 /* BatchNorm forward statistics and normalisation in one launch
- * (k_bn_train_fused) or as two; default 1 (env HLHGAT_BN_ONE_LAUNCH=0 turns it
- * off).  Both give bitwise the same results.  The one launch is taken only
- * when its grid (<= 256 workgroups) fits in a quarter of the device's
- * resident-workgroup capacity (occupancy x CUs), so every waiting workgroup's
- * finaliser is co-resident; the wait is still bounded, and a workgroup that
- * gives up writes NaN rows (never stale statistics), counts the timeout and
- * raises HLHGAT_DEVERR_BN_WAIT in the device error word. */
+ * (k_bn_fwd_grid: rows held in registers across a grid barrier) or as two;
+ * default 1 (env HLHGAT_BN_ONE_LAUNCH=0 turns it off).  Both give bitwise the
+ * same results.  The one launch is taken only when its grid (<= 256
+ * workgroups) fits in half of the device's resident-workgroup capacity for it
+ * (occupancy x CUs; the node and edge streams may each run one), so every
+ * workgroup of the barrier is co-resident; the wait is still bounded, and a
+ * workgroup that gives up writes NaN rows (never numbers from partial
+ * statistics), counts the timeout and raises HLHGAT_DEVERR_BN_WAIT in the
+ * device error word. */
 int hlhgat_set_bn_one_launch(int on);
 int hlhgat_get_bn_one_launch(void);
 /* Test hook: polls before a waiting workgroup gives up (default 2^22;

@@ -164,6 +164,11 @@ def main():
             o += k
         db = torch.empty(N, device=dev)
         run(f"proj_bwd_weight {tag}", lambda: ops._proj_bwd_weight(G, As, dWs, db), by, fl)
+        # the product's Linear backward: weight partials + data gradient in one
+        # launch, then the split reduction (torch.ops.hlhgat.proj_backward)
+        Acat = [a.contiguous() for a in As]
+        run(f"proj_bwd_fused {tag}",
+            lambda: torch.ops.hlhgat.proj_backward(G, Acat, W, True), 2 * by, 2 * fl)
     # ---- batch norm ----------------------------------------------------------
     for n, C in [(nt, 64), (ns, 64), (1000, 256)]:
         x = rnd(n, C).requires_grad_(True)
