@@ -243,6 +243,138 @@ def isolated_poly_step(device, batch, reps=20, chain=20):
                         "and L1, replayed 20x, events around the replays"}
 
 
+def kernel_roofline(p, bound, note):
+    """roofline entry of one event-stamped kernel class (hlhgat_prof_read)"""
+    if not p["launches"] or p["ms"] <= 0:
+        return None
+    sec = p["ms"] * 1e-3
+    if bound == "mfma":
+        ach, peak, unit = p["flops"] / sec / 1e12, FP32_MFMA_PEAK_TFS, "TFLOP/s"
+    else:
+        ach, peak, unit = p["bytes"] / sec / 1e9, HBM_PEAK_GBS, "GB/s"
+    return {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+            "frac": round(ach / peak, 4), "launches": p["launches"],
+            "avg_launch_us": round(p["ms"] * 1e3 / p["launches"], 2),
+            "per_launch": round((p["flops"] if bound == "mfma" else p["bytes"]) / p["launches"]),
+            "what": note}
+
+
+# BASELINE configs[2..4] heads (SURVEY §8d): per-GPU batch, model, loss
+HEADS = {
+    "cfg3_cifar_attpool": dict(kind="cifar", graphs=256, cls="HL_HGCNN_CIFAR10SP_dense_int3_attpool",
+                               ref="RefCifarAttPool", cpu_graphs=32,
+                               kw=dict(channels=[2, 2, 2], filters=[64, 128, 256],
+                                       mlp_channels=[256], K=4, keig=10, pool_loc=1, l=0.5)),
+    "cfg4_pepfunc_attpool": dict(kind="peptides", graphs=64, cls="HL_HGCNN_pepfunc_dense_int3_attpool",
+                                 ref="RefPepfuncAttPool", cpu_graphs=16,
+                                 kw=dict(channels=[2, 2, 2], filters=[64, 128, 256],
+                                         mlp_channels=[256], K=6, pool_loc=1)),
+    "cfg5_tsp_pyr": dict(kind="tsp", graphs=4, cls="HL_HGCNN_TSP_dense_int3_pyr",
+                         ref="RefTSPModel", cpu_graphs=1,
+                         kw=dict(channels=[4, 4, 4], filters=[32, 64, 128], mlp_channels=[256],
+                                 K=4)),
+}
+
+
+def _head_batch(kind, graphs, seed):
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph, two_level_batch
+    if kind == "tsp":
+        return collate([tsp_like_graph(seed * graphs + i) for i in range(graphs)],
+                       check_hodge=False)
+    return two_level_batch(kind, graphs, seed=seed)
+
+
+def _head_loss(kind, out, datas):
+    F = torch.nn.functional
+    if kind == "tsp":  # main_TSP...:316-321 (BCE on the masked edge logits)
+        return F.binary_cross_entropy_with_logits(out[0].view(-1), datas.y.view(-1).float())
+    y = datas[0].y
+    if kind == "cifar":  # main_cifar10SP: cross entropy
+        return F.cross_entropy(out, y.view(-1).long())
+    return F.binary_cross_entropy_with_logits(out, y.view(out.shape).float())  # pepfunc
+
+
+def heads_leg(device, steps=6, warmup=2, cpu_budget_s=8.0):
+    """BASELINE configs[2..4] on this GPU: graphs/s of a full training step
+    (fwd + loss + bwd + Adam, hlhgat.train.TrainStep, eager: the MLGC levels
+    change shape per batch) at the per-GPU batch of SURVEY §8d, and the CPU
+    oracle (the same head restated in oracle/hodge_ref.py) timed on a bounded
+    sample of the same data on the host cores."""
+    import hlhgat
+    from hlhgat.train import TrainStep
+    from oracle import hodge_ref as R
+    out = {}
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    for name, c in HEADS.items():
+        t0 = time.perf_counter()
+        raw = [_head_batch(c["kind"], c["graphs"], s) for s in range(2)]
+        gen_s = time.perf_counter() - t0
+        batches = [b.to(device) if c["kind"] == "tsp" else [x.to(device) for x in b] for b in raw]
+        torch.manual_seed(0)
+        m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
+        st = TrainStep(m, lambda o, d, k=c["kind"]: _head_loss(k, o, d), lr=1e-3, graphs=False)
+        for i in range(warmup):
+            st(batches[i % 2])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            st(batches[i % 2])
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        r = {"value": round(c["graphs"] / dt, 1), "unit": "graphs/s", "ms_per_step": round(dt * 1e3, 2),
+             "graphs_per_step": c["graphs"], "steps": steps, "head": c["cls"], "model": c["kw"],
+             "step": "fwd + loss + bwd + Adam, eager (TrainStep)", "data_gen_s": round(gen_s, 1)}
+        # CPU oracle on a bounded sample: the first cpu_graphs graphs of a batch
+        torch.set_num_threads(cores)
+        sb = _head_batch(c["kind"], c["cpu_graphs"], 0)
+        torch.manual_seed(0)
+        mr = getattr(R, c["ref"])(**c["kw"]).train()
+        opt = torch.optim.Adam(mr.parameters(), lr=1e-3)
+
+        def cpu_step():
+            o = mr(sb)
+            _head_loss(c["kind"], o, sb).backward()
+            opt.step()
+            opt.zero_grad()
+        times, t_start = [], time.perf_counter()
+        cpu_step()  # warm-up
+        while len(times) < 1 or (time.perf_counter() - t_start < cpu_budget_s and len(times) < 10):
+            t1 = time.perf_counter()
+            cpu_step()
+            times.append(time.perf_counter() - t1)
+        times.sort()
+        med = times[len(times) // 2]
+        r["cpu_baseline"] = {"value": round(c["cpu_graphs"] / med, 4), "unit": "graphs/s",
+                             "cores": cores, "kind": "port",
+                             "sample": f"{len(times)} oracle training steps on {c['cpu_graphs']} "
+                                       f"graph(s) of the same generator, median {med * 1e3:.0f} ms"}
+        out[name] = r
+        log(f"[heads] {name}: {r['value']} graphs/s (CPU oracle {r['cpu_baseline']['value']})")
+        del batches, m, st
+        torch.cuda.empty_cache()
+    return out
+
+
+def h2d_leg(batch_cpu, device, reps=10):
+    """The reference's loop copies each batch to the device every step
+    (data.to(device)); bench.py's `value` excludes it (inputs resident in
+    HBM).  Here: the PCIe time of one padded 1000-graph batch from pinned host
+    memory, and the step rate if that copy were serialised with every step."""
+    from hlhgat.train import _tensor_items
+    items = [(k, v.pin_memory()) for k, v in _tensor_items(batch_cpu)]
+    nbytes = sum(v.numel() * v.element_size() for _, v in items)
+    for _ in range(2):
+        [v.to(device, non_blocking=True) for _, v in items]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        [v.to(device, non_blocking=True) for _, v in items]
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"ms_per_batch": round(ms, 3), "bytes": nbytes, "GBps": round(nbytes / ms / 1e6, 1)}
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -311,6 +443,8 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no hipGraph replay")
     ap.add_argument("--no-cfg5", action="store_true",
                     help="skip the config-5 (TSP) SpMM roofline measurement")
+    ap.add_argument("--no-heads", action="store_true",
+                    help="skip the configs 3-5 heads (graphs/s + CPU oracle baseline each)")
     ap.add_argument("--prof-steps", type=int, default=3,
                     help="eager steps with kernel event stamps for the roofline")
     ap.add_argument("--dry-run", action="store_true",
@@ -364,18 +498,21 @@ def main():
     elapsed = max_over_ranks(elapsed, device)
     ops.check_device_errors()  # a kernel that reported unusable results voids the run
 
-    # roofline pass: eager steps, SpMM / projection launches event-stamped
+    # roofline pass: eager steps, SpMM / projection / BatchNorm launches event-stamped
+    L = hlhgat._lib
+    classes = (L.PROF_POLY, L.PROF_PROJ, L.PROF_PROJ_BWD, L.PROF_BN_FWD, L.PROF_BN_BWD)
     ops.prof_reset()
-    ops.prof_enable(hlhgat._lib.PROF_POLY, True)
-    ops.prof_enable(hlhgat._lib.PROF_PROJ, True)
+    for c in classes:
+        ops.prof_enable(c, True)
     for i in range(args.prof_steps):
         step._eager(batches[i % len(batches)])
     torch.cuda.synchronize()
-    ops.prof_enable(hlhgat._lib.PROF_POLY, False)
-    ops.prof_enable(hlhgat._lib.PROF_PROJ, False)
+    for c in classes:
+        ops.prof_enable(c, False)
+    ops.check_device_errors()
 
-    poly = ops.prof_read(hlhgat._lib.PROF_POLY)
-    proj = ops.prof_read(hlhgat._lib.PROF_PROJ)
+    poly = ops.prof_read(L.PROF_POLY)
+    proj = ops.prof_read(L.PROF_PROJ)
     ms_step = elapsed / args.steps * 1e3
     value = world * GRAPHS_PER_GPU * args.steps / elapsed
 
@@ -422,17 +559,36 @@ def main():
                       "launches": proj["launches"],
                       "avg_launch_us": round(proj["ms"] * 1e3 / max(proj["launches"], 1), 2)},
         "cpu_baseline": None,
+        "rooflines": {k: kernel_roofline(ops.prof_read(c), bound, note) for k, c, bound, note in (
+            ("k_proj_bwd_fused", L.PROF_PROJ_BWD, "mfma",
+             "Linear backward: weight-gradient split partials + data gradient, one launch; "
+             "flops 2 M N (sum K_w + sum K_d)"),
+            ("k_bn_fwd_grid", L.PROF_BN_FWD, "hbm",
+             "BatchNorm forward (statistics + normalise, one launch); bytes 8 n C"),
+            ("k_bn_bwd_reduce", L.PROF_BN_BWD, "hbm",
+             "BatchNorm backward statistics; bytes 12 n C (x, dy, y)"))},
         "spmm_cfg5": None,
+        "heads": None,
+        "h2d": None,
     }
     if rank == 0:
         roofline["isolated"] = isolated_poly_step(device, batches[0])
     if rank == 0 and world == 1 and not args.no_cfg5:
         log("[rank 0] config-5 SpMM roofline")
         result["spmm_cfg5"] = cfg5_spmm(device)
+    if rank == 0 and world == 1:
+        from hlhgat.hodge_dataset import pad_batch
+        from hlhgat.synthetic import zinc_like_batch
+        h = h2d_leg(pad_batch(zinc_like_batch(GRAPHS_PER_GPU, seed=1), caps), device)
+        h["value_if_serialised"] = round(GRAPHS_PER_GPU / (ms_step + h["ms_per_batch"]) * 1e3, 1)
+        result["h2d"] = h
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
         from hlhgat.synthetic import zinc_like_batch
         result["cpu_baseline"] = cpu_baseline(zinc_like_batch(GRAPHS_PER_GPU, seed=1))
+    if rank == 0 and world == 1 and not args.no_heads:
+        log("[rank 0] configs 3-5 heads")
+        result["heads"] = heads_leg(device)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

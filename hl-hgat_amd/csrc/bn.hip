@@ -1002,7 +1002,9 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
     s.poll_limit = g_poll_limit;
     s.err = hlhgat::device_error_word();
     HLH_CHECK_ARG(s.err, "bn_fwd_train: no device error word (%s)", hlhgat_last_error());
-    hipLaunchKernelGGL(f, dim3(L.parts, L.tiles), dim3(kThreads), 0, as_stream(stream), s);
+    // algorithmic bytes: x read once, y written once
+    ProfScope prof(HLHGAT_PROF_BN_FWD, as_stream(stream), 8.0 * (double)n * C, 0.0);
+    launch(f, dim3(L.parts, L.tiles), dim3(kThreads), 0, as_stream(stream), &prof, s);
     HLH_CHECK_LAUNCH();
     return HLHGAT_OK;
   }
@@ -1063,10 +1065,13 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   s.dbias = dbias;
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
-  if (vec)
-    k_bn_bwd_reduce<4><<<g1, kThreads, 0, st>>>(s);
-  else
-    k_bn_bwd_reduce<1><<<g1, kThreads, 0, st>>>(s);
+  {  // algorithmic bytes of the reduction: x, dy (and y for the ReLU mask) read once
+    ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
+    if (vec)
+      launch(k_bn_bwd_reduce<4>, g1, dim3(kThreads), 0, st, &prof, s);
+    else
+      launch(k_bn_bwd_reduce<1>, g1, dim3(kThreads), 0, st, &prof, s);
+  }
   HLH_CHECK_LAUNCH();
   BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, save_mean,
                  L.tpr, L.rp};

@@ -1324,10 +1324,24 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   const int64_t n_blocks = (int64_t)f.n_wpad + (int64_t)f.n_d;
   HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
   hipStream_t s = as_stream(stream);
+  // algorithmic flops of the launch: weight gradient 2 M N sum(kb_w) + data
+  // gradient 2 M N sum(kb_d); bytes: dC once, each A_b and dA_b once, the W
+  // blocks, the split slab written once
+  double flops = 0, bytes = 4.0 * (double)M * N;
+  for (int b = 0; b < nb_w; ++b) {
+    flops += 2.0 * (double)M * N * kb_w[b];
+    bytes += 4.0 * (double)M * kb_w[b];
+  }
+  for (int b = 0; b < nb_d; ++b) {
+    flops += 2.0 * (double)M * N * kb_d[b];
+    bytes += 4.0 * (double)M * kb_d[b] + 4.0 * N * kb_d[b];
+  }
+  bytes += 4.0 * (double)p.splits * p.part_stride;
+  ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
   if (tnd == 1)
-    k_proj_bwd_fused<1><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+    launch(k_proj_bwd_fused<1>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else
-    k_proj_bwd_fused<2><<<(unsigned)n_blocks, 256, 0, s>>>(f);
+    launch(k_proj_bwd_fused<2>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;

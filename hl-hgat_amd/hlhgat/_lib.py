@@ -110,6 +110,7 @@ POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
 DEVERR_BN_WAIT = 1
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
+PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD = 4, 5, 6
 MAX_BLOCKS = 16
 
 

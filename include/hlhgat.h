@@ -487,7 +487,10 @@ int hlhgat_clear_device_errors(void);
 #define HLHGAT_PROF_PROJ 1 /* MFMA projection forward */
 #define HLHGAT_PROF_HODGE_NODE 2 /* factored L1, stage 1: Z = B1 X (node rows) */
 #define HLHGAT_PROF_HODGE_EDGE 3 /* factored L1, stage 2: k_hodge_edge_step */
-#define HLHGAT_PROF_NCLASS 4
+#define HLHGAT_PROF_PROJ_BWD 4 /* Linear backward: k_proj_bwd_fused (weight partials + data grad) */
+#define HLHGAT_PROF_BN_FWD 5 /* BatchNorm forward: k_bn_fwd_grid / k_bn_stats + k_bn_apply */
+#define HLHGAT_PROF_BN_BWD 6 /* BatchNorm backward: k_bn_bwd_reduce + k_bn_bwd_apply */
+#define HLHGAT_PROF_NCLASS 7
 /* Enable (1) / disable (0) event timing of the given kernel class. */
 int hlhgat_prof_enable(int kernel_class, int enable);
 int hlhgat_prof_reset(void);
