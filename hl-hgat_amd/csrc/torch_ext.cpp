@@ -1000,12 +1000,16 @@ struct Fork {
   explicit Fork(int dev)
       : main(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)dev)),
         side(side_of(dev)) {}
-  static TStream side_of(int dev) {
+  static std::unordered_map<int, TStream>& registry() {
     static auto* streams = new std::unordered_map<int, TStream>();
-    auto it = streams->find(dev);
-    if (it == streams->end())
-      it = streams->emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
-                                     false, (c10::DeviceIndex)dev)).first;
+    return *streams;
+  }
+  static TStream side_of(int dev) {
+    auto& streams = registry();
+    auto it = streams.find(dev);
+    if (it == streams.end())
+      it = streams.emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
+                                    false, (c10::DeviceIndex)dev)).first;
     return it->second;
   }
   static hipEvent_t next_event() {
@@ -1029,6 +1033,56 @@ struct Fork {
       if (t.defined()) t.record_stream(main);
   }
 };
+
+// Rejoin every side stream that joined the capture of the current stream
+// (hlhgat.train.TrainStep calls this as the last captured operation): a
+// stream forked from the capture stream -- e.g. inside an autograd backward
+// node, which runs on autograd's device thread -- and never waited on again
+// leaves the capture "unjoined" at hipStreamEndCapture.  For each candidate
+// stream (the C++ Fork side streams of `device` + `extra`, raw hipStream_t
+// handles) whose capture id equals the current stream's, record an event on
+// it and make the capture stream wait for it.  Returns the number rejoined.
+int64_t join_capture_streams(int64_t device, std::vector<int64_t> extra) {
+  hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream();
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long cur_id = 0;
+  TORCH_CHECK(hipStreamGetCaptureInfo(cur, &st, &cur_id) == hipSuccess,
+              "hlhgat: hipStreamGetCaptureInfo");
+  if (st != hipStreamCaptureStatusActive) return 0;
+  std::vector<hipStream_t> cand;
+  auto& reg = Fork::registry();
+  auto it = reg.find((int)device);
+  if (it != reg.end()) cand.push_back(it->second.stream());
+  for (int64_t h : extra) cand.push_back(reinterpret_cast<hipStream_t>(h));
+  int64_t n = 0;
+  for (hipStream_t sd : cand) {
+    if (sd == cur) continue;
+    hipStreamCaptureStatus ss = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (hipStreamGetCaptureInfo(sd, &ss, &id) != hipSuccess) continue;
+    if (ss != hipStreamCaptureStatusActive || id != cur_id) continue;
+    hipEvent_t e = Fork::next_event();
+    TORCH_CHECK(hipEventRecord(e, sd) == hipSuccess, "hlhgat: hipEventRecord (capture join)");
+    TORCH_CHECK(hipStreamWaitEvent(cur, e, 0) == hipSuccess,
+                "hlhgat: hipStreamWaitEvent (capture join)");
+    ++n;
+  }
+  return n;
+}
+
+// Is `stream` (raw handle) still part of an active capture?
+bool stream_capturing(int64_t stream) {
+  hipStreamCaptureStatus ss = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  TORCH_CHECK(hipStreamGetCaptureInfo(reinterpret_cast<hipStream_t>(stream), &ss, &id) ==
+                  hipSuccess,
+              "hlhgat: hipStreamGetCaptureInfo");
+  return ss == hipStreamCaptureStatusActive;
+}
+
+int64_t fork_side_stream(int64_t device) {
+  return reinterpret_cast<int64_t>(Fork::side_of((int)device).stream());
+}
 
 // One launch for a set of strided rectangles (hlhgat_copy2d_batched);
 // src == nullptr zero-fills.
@@ -1772,6 +1826,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bwd", &set_fused_bwd);
+  m.def("join_capture_streams", &join_capture_streams);
+  m.def("stream_capturing", &stream_capturing);
+  m.def("fork_side_stream", &fork_side_stream);
   m.def("bn_act", &bn_act);
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);

@@ -105,6 +105,23 @@ def side_stream(device: torch.device, slot: int = 0) -> torch.cuda.Stream:
     return s
 
 
+def join_capture_streams(device: torch.device) -> int:
+    """Make the capturing current stream wait for every side stream (the C++
+    fork's and ops.side_stream's) that joined its capture -- the last
+    operation of a hipGraph capture (hlhgat.train.TrainStep)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    extra = [s.cuda_stream for (d, _), s in _SIDE_STREAMS.items() if d == idx]
+    return int(_ext.join_capture_streams(idx, extra))
+
+
+def side_streams_capturing(device: torch.device) -> List[int]:
+    """raw handles of the side streams still part of an active capture"""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    cand = [s.cuda_stream for (d, _), s in _SIDE_STREAMS.items() if d == idx]
+    cand.append(int(_ext.fork_side_stream(idx)))
+    return [h for h in cand if _ext.stream_capturing(h)]
+
+
 def _tensors(x):
     if torch.is_tensor(x):
         yield x

@@ -188,6 +188,16 @@ class TrainStep:
             loss = self._fwd_bwd(static)
             if self.world == 1:
                 self.opt.step()
+            # every stream forked from the capture (the node / edge side streams,
+            # forks inside autograd backward nodes, which run on autograd's
+            # device thread) rejoins it before hipStreamEndCapture: an unjoined
+            # fork is what crashed capture_end in round 1
+            if self._ext is not None:
+                ops.join_capture_streams(self.device)
+        left = ops.side_streams_capturing(self.device) if self._ext is not None else []
+        if left:
+            raise RuntimeError(f"TrainStep: {len(left)} side stream(s) still capturing after the "
+                               f"graph capture ended (unjoined fork); refusing the graph")
         ops.clear_caches()
         torch.cuda.current_stream(self.device).wait_stream(s)
         if len(self._graphs) >= self.max_graphs:

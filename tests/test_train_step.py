@@ -221,3 +221,60 @@ def test_padded_batches_share_one_graph(cuda):
     assert l_e == l_g
     for k in sd_e:
         assert torch.equal(sd_e[k], sd_g[k]), k
+
+
+class _SideEffectInBackward(torch.autograd.Function):
+    """Identity whose backward also runs work on a side stream forked from the
+    current (capture) stream and never joined back -- the shape of the round-1
+    variant whose hipGraph capture crashed at capture_end."""
+    buf = None
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        from hlhgat import ops
+        side = ops.side_stream(g.device)
+        side.wait_stream(torch.cuda.current_stream(g.device))
+        with torch.cuda.stream(side):
+            _SideEffectInBackward.buf.copy_(g.abs().sum().view(1))
+        g.record_stream(side)
+        return g
+
+
+class _TinyFork(_Tiny):
+    def forward(self, batch):
+        return self.b(_SideEffectInBackward.apply(torch.relu(self.a(batch.x))))
+
+
+@pytest.mark.gpu
+def test_capture_rejoins_fork_left_open_in_backward(cuda):
+    """TrainStep rejoins every side stream that joined the capture before
+    hipStreamEndCapture (ops.join_capture_streams), so a fork left open inside
+    a backward node neither breaks the capture nor loses its work: replayed
+    steps equal eager steps bitwise, the side work runs in every replay, and
+    no side stream is left capturing."""
+    from hlhgat import ops
+    from hlhgat.train import TrainStep
+    res = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        m = _TinyFork().to(cuda)
+        _SideEffectInBackward.buf = torch.zeros(1, device=cuda)
+        step = TrainStep(m, _loss, lr=1e-2, graphs=graphs)
+        bufs = []
+        for i in range(4):
+            b = _data(i)
+            step(_B(b.x.to(cuda), b.y.to(cuda)))
+            torch.cuda.synchronize()
+            bufs.append(_SideEffectInBackward.buf.clone())
+        if graphs:
+            assert step.stats["captures"] == 1 and step.stats["replay"] >= 2
+            assert ops.side_streams_capturing(cuda) == []
+        res.append(([p.detach().clone() for p in m.parameters()], bufs))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b)
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
