@@ -104,6 +104,24 @@ __device__ __forceinline__ void vstore(float* p, typename VecT<V>::type v) {
   *reinterpret_cast<typename VecT<V>::type*>(p) = v;
 }
 
+// Streaming (non-temporal) store of a whole vector as ONE dwordx2/x4 store.
+// __builtin_nontemporal_store on the float4 components one by one issues V
+// strided dword stores, each a partial cache line that the streaming path
+// writes out on its own (the 1.3x write amplification of the factored edge
+// step, profiles/r01_h_cfg5_pmc.txt); the clang vector type keeps it whole.
+template <int V>
+__device__ __forceinline__ void vstore_nt(float* p, typename VecT<V>::type v) {
+  if constexpr (V == 1) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    typedef float nv_t __attribute__((ext_vector_type(V)));
+    nv_t n;
+#pragma unroll
+    for (int i = 0; i < V; ++i) n[i] = (&v.x)[i];
+    __builtin_nontemporal_store(n, reinterpret_cast<nv_t*>(p));
+  }
+}
+
 // Element access on the vector types so kernels can loop over components.
 __device__ __forceinline__ float& vget(float& v, int) { return v; }
 __device__ __forceinline__ float& vget(float2& v, int i) { return (&v.x)[i]; }

@@ -97,11 +97,9 @@ __device__ __forceinline__ void poly_epilogue(const PolyArgs& a, int64_t row, in
 #pragma unroll
     for (int i = 0; i < V; ++i) vget(out, i) = vget(out, i) + a.q * vget(qv, i);
   }
-  if (a.nt_store) {
-    float* yp = a.Y + row * a.ldy + f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) __builtin_nontemporal_store(vget(out, i), yp + i);
-  } else
+  if (a.nt_store)
+    vstore_nt<V>(a.Y + row * a.ldy + f, out);
+  else
     vstore<V>(a.Y + row * a.ldy + f, out);
 }
 
