@@ -187,6 +187,9 @@ struct StatsArgs {
   int relu;
   unsigned poll_limit;
   unsigned* err;
+  // SyncBatchNorm (hlhgat_bn_sums_*): the finaliser writes this rank's fp64
+  // column sums [S0[C], S1[C], n_eff] here instead of finishing the statistics
+  double* sums_out;
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -432,33 +435,56 @@ __device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile
   return true;
 }
 
-// Forward finalisation of one column (both paths): mean, invstd, and the
+// Forward finalisation of one column (all paths, SyncBatchNorm included:
+// there n_eff and the sums are the totals over ranks): mean, invstd, and the
 // running statistics when `update`.
-__device__ __forceinline__ void fwd_finalize(const StatsArgs& a, int cc, double u0, double u1,
-                                             int64_t n_eff, float& mean_f, float& invstd_f,
-                                             bool update) {
-  const double nn = (double)(n_eff > 0 ? n_eff : 1);
+__device__ __forceinline__ void finalize_col(double u0, double u1, double n_eff, float eps,
+                                             float momentum, float* running_mean,
+                                             float* running_var, int cc, float& mean_f,
+                                             float& invstd_f, bool update) {
+  const double nn = n_eff > 0.0 ? n_eff : 1.0;
   const double mean = u0 / nn;
   double var = u1 / nn - mean * mean;
   if (var < 0.0) var = 0.0;
   mean_f = (float)mean;
-  invstd_f = (float)(1.0 / sqrt(var + (double)a.eps));
-  if (update && a.running_mean) {
-    const double unb = n_eff > 1 ? var * nn / (nn - 1.0) : var;
-    a.running_mean[cc] = (1.f - a.momentum) * a.running_mean[cc] + a.momentum * (float)mean;
-    a.running_var[cc] = (1.f - a.momentum) * a.running_var[cc] + a.momentum * (float)unb;
+  invstd_f = (float)(1.0 / sqrt(var + (double)eps));
+  if (update && running_mean) {
+    const double unb = n_eff > 1.0 ? var * nn / (nn - 1.0) : var;
+    running_mean[cc] = (1.f - momentum) * running_mean[cc] + momentum * (float)mean;
+    running_var[cc] = (1.f - momentum) * running_var[cc] + momentum * (float)unb;
   }
 }
 
-// Backward coefficients of one column (both paths): dx = A g + (B (x - mean) + C).
+__device__ __forceinline__ void fwd_finalize(const StatsArgs& a, int cc, double u0, double u1,
+                                             int64_t n_eff, float& mean_f, float& invstd_f,
+                                             bool update) {
+  finalize_col(u0, u1, (double)n_eff, a.eps, a.momentum, a.running_mean, a.running_var, cc,
+               mean_f, invstd_f, update);
+}
+
+// Backward coefficients of one column (all paths): dx = A g + (B (x - mean) + C).
 __device__ __forceinline__ void bwd_coefs(float is_f, float w_f, double sg, double sgx,
-                                          int64_t n_eff, float& A, float& B, float& Cc) {
+                                          double n_eff, float& A, float& B, float& Cc) {
   const double is = (double)is_f;
   const double w = (double)w_f;
-  const double nn = (double)(n_eff > 0 ? n_eff : 1);
+  const double nn = n_eff > 0.0 ? n_eff : 1.0;
   A = (float)(w * is);
   B = (float)(-w * is * is * is * sgx / nn);
   Cc = (float)(-w * is * sg / nn);
+}
+
+// SyncBatchNorm: the column tile's sums and the valid row count of this rank
+// (layout [S0[C], S1[C], n_eff], fp64: hlhgat_bn_sums_fwd / _bwd).
+__device__ __forceinline__ void write_sums(const StatsArgs& a, int c0, int tile_c,
+                                           const double* sum0, const double* sum1,
+                                           int64_t n_eff) {
+  for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+    const int cc = c0 + t;
+    if (cc >= a.C) continue;
+    a.sums_out[cc] = sum0[t];
+    a.sums_out[a.C + cc] = sum1[t];
+  }
+  if (blockIdx.y == 0 && threadIdx.x == 0) a.sums_out[2 * a.C] = (double)n_eff;
 }
 
 // ---------------------------------------------------------------------------
@@ -507,6 +533,10 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
   if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1)) return;
+  if (a.sums_out) {  // SyncBatchNorm: this rank's sums, finalised after the all-gather
+    write_sums(a, c0, tile_c, sum0, sum1, n_eff);
+    return;
+  }
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
@@ -645,6 +675,16 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
   if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1)) return;
+  if (a.sums_out) {  // SyncBatchNorm: local dweight / dbias, global coefficients later
+    write_sums(a, c0, tile_c, sum0, sum1, n_eff);
+    for (int t = threadIdx.x; t < tile_c; t += kThreads) {
+      const int cc = c0 + t;
+      if (cc >= a.C) continue;
+      if (a.dweight) a.dweight[cc] = (float)(sum1[t] * (double)a.save_invstd[cc]);
+      if (a.dbias) a.dbias[cc] = (float)sum0[t];
+    }
+    return;
+  }
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
@@ -698,6 +738,143 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
       vget(o, v) = r >= n_eff ? 0.f : A[v] * g + (B[v] * (vget(xv[u], v) - mu[v]) + Cc[v]);
     }
     vstore<V>(a.dx + r * a.lddx + c, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SyncBatchNorm apply kernels: every thread totals its columns' sums over the
+// gathered ranks IN RANK ORDER (the same fp64 operations in every workgroup
+// and on every rank, so all ranks hold the same statistics), then finishes
+// exactly as the single-rank kernels do.  One rank: 0 + S = S, so the
+// results are bitwise those of hlhgat_bn_fwd_train / hlhgat_bn_bwd_train on
+// the same layout.
+// ---------------------------------------------------------------------------
+struct SyncArgs {
+  const int32_t* nvalid;
+  const float* x;
+  int64_t ldx;
+  const float* y;   // bwd: forward output (ReLU mask) or NULL
+  int64_t ldy;
+  const float* dy;  // bwd only
+  int64_t lddy;
+  float* out;       // fwd: y; bwd: dx
+  int64_t ldo;
+  int64_t n;
+  int C;
+  int tpr, rp;
+  const double* gathered;  // [world][2C+1]
+  int world;
+  const float* weight;
+  const float* bias;
+  float* running_mean;
+  float* running_var;
+  int64_t* nbt;
+  float momentum, eps;
+  float* save_mean;    // fwd: written; bwd: read
+  float* save_invstd;  // fwd: written; bwd: read
+  int relu;
+};
+
+__device__ __forceinline__ void sync_totals(const SyncArgs& a, int cc, double& s0, double& s1,
+                                            double& cnt) {
+  s0 = s1 = cnt = 0.0;
+  const int64_t stride = 2 * (int64_t)a.C + 1;
+  for (int r = 0; r < a.world; ++r) {
+    const double* g = a.gathered + r * stride;
+    s0 += g[cc];
+    s1 += g[a.C + cc];
+    cnt += g[2 * a.C];
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_sync_apply(SyncArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c = blockIdx.y * a.tpr * V + cl * V;
+  if (c >= a.C) return;
+  float s[V], m[V], t[V];
+  const bool writer = blockIdx.x == 0 && rg == 0;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    double s0, s1, cnt;
+    sync_totals(a, c + v, s0, s1, cnt);
+    float mean, is;
+    finalize_col(s0, s1, cnt, a.eps, a.momentum, a.running_mean, a.running_var, c + v, mean, is,
+                 writer);
+    if (writer) {
+      a.save_mean[c + v] = mean;
+      a.save_invstd[c + v] = is;
+    }
+    const float w = a.weight ? a.weight[c + v] : 1.f;
+    s[v] = w * is;
+    m[v] = mean;
+    t[v] = a.bias ? a.bias[c + v] : 0.f;
+  }
+  if (a.nbt && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
+  const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
+  vt xv[APPLY_RPT];
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r < n_eff) xv[u] = vload<V>(a.x + r * a.ldx + c);
+  }
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r >= a.n) break;
+    vt o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float z = (vget(xv[u], v) - m[v]) * s[v] + t[v];
+      vget(o, v) = r >= n_eff ? 0.f : ((a.relu && z < 0.f) ? 0.f : z);
+    }
+    vstore<V>(a.out + r * a.ldo + c, o);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_sync_bwd_apply(SyncArgs a) {
+  using vt = typename VecT<V>::type;
+  const int cl = threadIdx.x % a.tpr;
+  const int rg = threadIdx.x / a.tpr;
+  const int c = blockIdx.y * a.tpr * V + cl * V;
+  if (c >= a.C) return;
+  float A[V], B[V], Cc[V], mu[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    double sg, sgx, cnt;
+    sync_totals(a, c + v, sg, sgx, cnt);
+    bwd_coefs(a.save_invstd[c + v], a.weight ? a.weight[c + v] : 1.f, sg, sgx, cnt, A[v], B[v],
+              Cc[v]);
+    mu[v] = a.save_mean[c + v];
+  }
+  const int64_t n_eff = eff_rows(a.n, a.nvalid);
+  const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
+  vt xv[APPLY_RPT], gv[APPLY_RPT], yv[APPLY_RPT];
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r < n_eff) {
+      xv[u] = vload<V>(a.x + r * a.ldx + c);
+      gv[u] = vload<V>(a.dy + r * a.lddy + c);
+      if (a.y) yv[u] = vload<V>(a.y + r * a.ldy + c);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < APPLY_RPT; ++u) {
+    const int64_t r = r0 + u * a.rp;
+    if (r >= a.n) break;
+    vt o;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float g = vget(gv[u], v);
+      if (a.y && !(vget(yv[u], v) > 0.f)) g = 0.f;
+      vget(o, v) = r >= n_eff ? 0.f : A[v] * g + (B[v] * (vget(xv[u], v) - mu[v]) + Cc[v]);
+    }
+    vstore<V>(a.out + r * a.ldo + c, o);
   }
 }
 
@@ -1080,6 +1257,158 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
     k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);
   else
     k_bn_bwd_apply<1><<<g2, kThreads, 0, st>>>(p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// SyncBatchNorm: sums -> (caller all-gathers [world][2C+1]) -> apply
+// ---------------------------------------------------------------------------
+extern "C" int64_t hlhgat_bn_sums_len(int64_t C) { return C > 0 ? 2 * C + 1 : 0; }
+
+extern "C" int hlhgat_bn_sums_fwd(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                                  int64_t n, const int32_t* n_valid, int64_t C, double* sums,
+                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && (!y || ldy >= C),
+                "bn_sums_fwd: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(x && sums, "bn_sums_fwd: NULL pointer");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_sums_fwd: workspace too small");
+  // the layout (hence the partial order) of hlhgat_bn_fwd_train over (x, y)
+  const bool vec = bn_vec_ok(C, {ldx, y ? ldy : 4}, {x, y});
+  const BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_sums_fwd: C too large");
+  StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
+  s.sums_out = sums;
+  dim3 g1(L.parts, L.tiles);
+  if (vec)
+    k_bn_stats<4><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+  else
+    k_bn_stats<1><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_sync_fwd_apply(const float* x, int64_t ldx, int64_t n,
+                                        const int32_t* n_valid, int64_t C,
+                                        const double* gathered, int world, const float* weight,
+                                        const float* bias, float* running_mean,
+                                        float* running_var, int64_t* num_batches_tracked,
+                                        float momentum, float eps, int relu, float* y,
+                                        int64_t ldy, float* save_mean, float* save_invstd,
+                                        void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C && world >= 1,
+                "bn_sync_fwd_apply: bad sizes n=%lld C=%lld world=%d", (long long)n,
+                (long long)C, world);
+  HLH_CHECK_ARG(x && y && gathered && save_mean && save_invstd, "bn_sync_fwd_apply: NULL pointer");
+  HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                "bn_sync_fwd_apply: running_mean/var must both be given or both NULL");
+  const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
+  const BnLayout L = bn_layout(n, C, vec);
+  SyncArgs a{};
+  a.nvalid = n_valid;
+  a.x = x;
+  a.ldx = ldx;
+  a.out = y;
+  a.ldo = ldy;
+  a.n = n;
+  a.C = (int)C;
+  a.tpr = L.tpr;
+  a.rp = L.rp;
+  a.gathered = gathered;
+  a.world = world;
+  a.weight = weight;
+  a.bias = bias;
+  a.running_mean = running_mean;
+  a.running_var = running_var;
+  a.nbt = num_batches_tracked;
+  a.momentum = momentum;
+  a.eps = eps;
+  a.save_mean = save_mean;
+  a.save_invstd = save_invstd;
+  a.relu = relu;
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  if (vec)
+    k_bn_sync_apply<4><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+  else
+    k_bn_sync_apply<1><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_sums_bwd(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                                  const float* dy, int64_t lddy, float* dx_layout,
+                                  int64_t lddx, int64_t n, const int32_t* n_valid, int64_t C,
+                                  const float* save_mean, const float* save_invstd,
+                                  double* sums, float* dweight, float* dbias, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && (!y || ldy >= C) &&
+                    (!dx_layout || lddx >= C),
+                "bn_sums_bwd: bad sizes");
+  HLH_CHECK_ARG(x && dy && sums && save_mean && save_invstd, "bn_sums_bwd: NULL pointer");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_sums_bwd: workspace too small");
+  // the layout of hlhgat_bn_bwd_train over (x, y, dy, dx)
+  const bool vec = bn_vec_ok(C, {ldx, lddy, dx_layout ? lddx : 4, y ? ldy : 4},
+                             {x, y, dy, dx_layout});
+  const BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_sums_bwd: C too large");
+  StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
+  s.y = y;
+  s.ldy = ldy;
+  s.dy = dy;
+  s.lddy = lddy;
+  s.save_mean = const_cast<float*>(save_mean);
+  s.save_invstd = const_cast<float*>(save_invstd);
+  s.dweight = dweight;
+  s.dbias = dbias;
+  s.sums_out = sums;
+  dim3 g1(L.parts, L.tiles);
+  if (vec)
+    k_bn_bwd_reduce<4><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+  else
+    k_bn_bwd_reduce<1><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float* y,
+                                        int64_t ldy, const float* dy, int64_t lddy, int64_t n,
+                                        const int32_t* n_valid, int64_t C, const float* weight,
+                                        const float* save_mean, const float* save_invstd,
+                                        const double* gathered, int world, float* dx,
+                                        int64_t lddx, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && lddx >= C && (!y || ldy >= C) &&
+                    world >= 1,
+                "bn_sync_bwd_apply: bad sizes");
+  HLH_CHECK_ARG(x && dy && dx && gathered && save_mean && save_invstd,
+                "bn_sync_bwd_apply: NULL pointer");
+  const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
+  const BnLayout L = bn_layout(n, C, vec);
+  SyncArgs a{};
+  a.nvalid = n_valid;
+  a.x = x;
+  a.ldx = ldx;
+  a.y = y;
+  a.ldy = ldy;
+  a.dy = dy;
+  a.lddy = lddy;
+  a.out = dx;
+  a.ldo = lddx;
+  a.n = n;
+  a.C = (int)C;
+  a.tpr = L.tpr;
+  a.rp = L.rp;
+  a.gathered = gathered;
+  a.world = world;
+  a.weight = weight;
+  a.save_mean = const_cast<float*>(save_mean);
+  a.save_invstd = const_cast<float*>(save_invstd);
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  if (vec)
+    k_bn_sync_bwd_apply<4><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+  else
+    k_bn_sync_bwd_apply<1><<<g2, kThreads, 0, as_stream(stream)>>>(a);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

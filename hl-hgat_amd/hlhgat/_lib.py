@@ -94,6 +94,18 @@ SIGNATURES = {
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                     c_vp]),
+    "hlhgat_bn_sums_len": (c_i64, [c_i64]),
+    "hlhgat_bn_sums_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
+                                   c_i64, c_vp]),
+    "hlhgat_bn_sync_fwd_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_i32, c_vp,
+                                         c_i64, c_vp, c_vp, c_vp]),
+    "hlhgat_bn_sums_bwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                   c_vp]),
+    "hlhgat_bn_sync_bwd_apply": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i64,
+                                         c_vp]),
     "hlhgat_bn_stats_train": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_f32,
                                       c_f32, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_bn_apply": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32,

@@ -7,8 +7,9 @@ exchange step is the per-step gradient all-reduce (torch DDP over RCCL /
 xGMI; backend "nccl" is RCCL on ROCm).  One graph never spans GPUs.
 
 BatchNorm statistics stay per rank by default (like the reference's per-batch
-statistics, computed on each rank's shard); SURVEY.md §8e notes the exact-
-parity caveats.
+statistics, computed on each rank's shard); convert_sync_batchnorm turns on
+SyncBatchNorm mode, whose statistics span every rank (parity
+caveat 1).
 """
 from __future__ import annotations
 
@@ -19,7 +20,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["world_info", "shard_range", "shard_graphs", "shard_by_weight", "init_distributed",
-           "wrap_ddp", "max_over_ranks"]
+           "wrap_ddp", "max_over_ranks", "convert_sync_batchnorm", "revert_sync_batchnorm"]
 
 
 def world_info() -> Tuple[int, int, int]:
@@ -94,6 +95,30 @@ def wrap_ddp(model: torch.nn.Module, device: torch.device, bucket_cap_mb: int = 
     return torch.nn.parallel.DistributedDataParallel(
         model, device_ids=ids, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
         find_unused_parameters=find_unused_parameters)
+
+
+def convert_sync_batchnorm(module: torch.nn.Module, process_group=None) -> torch.nn.Module:
+    """SyncBatchNorm mode for every BatchNorm1d of ``module`` (the role of
+    torch.nn.SyncBatchNorm.convert_sync_batchnorm): in training their batch
+    statistics (and the input gradient's sums) span all ranks of
+    ``process_group`` (None = the default group), so a model sharded by graph
+    normalises exactly as one process over the whole batch does.  The
+    modules stay BatchNorm1d (state_dict keys unchanged); the HIP kernels
+    exchange one fp64 [2C+1] vector per layer and direction
+    (include/hlhgat.h, hlhgat_bn_sums_*).  Returns ``module``."""
+    from .ops import _SyncGroup
+    for m in module.modules():
+        if isinstance(m, torch.nn.BatchNorm1d):
+            m._hlhgat_sync = _SyncGroup(process_group)
+    return module
+
+
+def revert_sync_batchnorm(module: torch.nn.Module) -> torch.nn.Module:
+    """Back to per-rank statistics (the default)."""
+    for m in module.modules():
+        if isinstance(m, torch.nn.BatchNorm1d) and hasattr(m, "_hlhgat_sync"):
+            del m._hlhgat_sync
+    return module
 
 
 def max_over_ranks(value: float, device: torch.device = torch.device("cpu")) -> float:

@@ -167,7 +167,8 @@ def _value_mlp(seq: nn.Sequential, blocks) -> Tensor:
     if (len(m) == 6 and isinstance(m[0], nn.Linear) and isinstance(m[1], nn.BatchNorm1d)
             and isinstance(m[2], nn.ReLU) and isinstance(m[3], nn.Linear)
             and isinstance(m[4], nn.BatchNorm1d) and isinstance(m[5], nn.ReLU)
-            and all(b.training or not b.track_running_stats for b in (m[1], m[4]))):
+            and all(b.training or not b.track_running_stats for b in (m[1], m[4]))
+            and all(ops.sync_bn_group(b) is None for b in (m[1], m[4]))):
         return ops.mlp2(blocks, seq)
     return run_sequential(seq, blocks)
 

@@ -719,7 +719,7 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
                            f"{op.fwd.n_rows}")
     A, At = op.fwd, op.bwd
     ws = list(weights)
-    if bn is not None and x.dim() == 2 and _bn_uses_batch_stats(bn):
+    if bn is not None and x.dim() == 2 and _bn_uses_batch_stats(bn) and sync_bn_group(bn) is None:
         if x.size(0) < 2 and bn.training:
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
@@ -787,8 +787,10 @@ class DenseConcat:
         if c1 > self.width:
             raise RuntimeError(f"hlhgat: DenseConcat overflow ({c1} > {self.width})")
         if y.data_ptr() != self.S.data_ptr() + 4 * c0 or y.stride(0) != self.S.stride(0):
-            with torch.no_grad():
-                self.S[:, c0:c1].copy_(y)
+            # through .data (its own version counter): columns [c0, c1) are
+            # outside every view handed out so far, and a tracked in-place
+            # copy would bump the version counter those views share with S
+            self.S.data[:, c0:c1].copy_(y.detach())
         self.parts.append(y)
         self.cols.append((c0, c1))
         self.owned.append(False)
@@ -865,7 +867,7 @@ def _mlp2_params(seq: torch.nn.Sequential):
     l0, b1, _, l3, b4, _ = m
     for b in (b1, b4):
         if not (b.training and b.affine and b.track_running_stats and b.momentum is not None
-                and b.running_mean is not None):
+                and b.running_mean is not None) or sync_bn_group(b) is not None:
             return None
     if l0.bias is None or l3.bias is None:
         return None
@@ -1119,7 +1121,129 @@ def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False
     if x.size(0) < 2 and bn.training:
         raise ValueError(f"Expected more than 1 value per channel when training, got input "
                          f"size {tuple(x.shape)}")
+    if sync_bn_group(bn) is not None:
+        return _SyncBatchNormFn.apply(x, bn.weight, bn.bias, bool(relu), valid,
+                                      sync_bn_group(bn), _bn_args(bn))
     return _ext.bn_act(x, *_bn_args(bn), bool(relu), valid)
+
+
+# ----------------------------------------------------------------------------
+# SyncBatchNorm (hlhgat.distributed.convert_sync_batchnorm): batch statistics
+# over every rank's rows -- the single-process statistics of the whole
+# data-parallel batch (parity caveat 1).
+# ----------------------------------------------------------------------------
+class _SyncGroup:
+    """Marker held by a BatchNorm1d in SyncBatchNorm mode: its process group
+    (None = the default group)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+
+def sync_bn_group(bn) -> Optional[_SyncGroup]:
+    """The _SyncGroup of a BatchNorm1d in SyncBatchNorm mode (training-mode
+    batch statistics only), else None."""
+    g = getattr(bn, "_hlhgat_sync", None)
+    if g is None or not _bn_uses_batch_stats(bn):
+        return None
+    return g
+
+
+_SYNC_WS = {}
+_SYNC_WS_RETIRED = []
+
+
+def _sync_workspace(x: torch.Tensor, n: int, Cc: int) -> torch.Tensor:
+    """Zeroed BatchNorm workspace per (device, stream); outgrown ones are
+    retired, not freed (a captured graph may still hold the address)."""
+    key = (x.device.index, _stream(x))
+    need = int(LIB.hlhgat_bn_workspace_bytes(n, Cc))
+    ws = _SYNC_WS.get(key)
+    if ws is None or ws.numel() < need:
+        if ws is not None:
+            _SYNC_WS_RETIRED.append(ws)
+        ws = torch.zeros(max(need, 1 << 20, 2 * (ws.numel() if ws is not None else 0)),
+                         dtype=torch.uint8, device=x.device)
+        _SYNC_WS[key] = ws
+    return ws
+
+
+def _all_gather_rows(t: torch.Tensor, group) -> torch.Tensor:
+    """[world, len(t)] gathered in rank order (RCCL all_gather_into_tensor;
+    gloo: list all_gather)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return t.view(1, -1)
+    world = dist.get_world_size(group)
+    if world == 1:
+        return t.view(1, -1)
+    out = torch.empty(world, t.numel(), dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, t, group=group)
+    else:
+        parts = list(out.unbind(0))
+        dist.all_gather(parts, t, group=group)
+        if parts[0].data_ptr() != out[0].data_ptr():
+            out = torch.stack(parts)
+    return out
+
+
+class _SyncBatchNormFn(torch.autograd.Function):
+    """BatchNorm1d (+ ReLU) with statistics over all ranks: local fp64 sums
+    (hlhgat_bn_sums_fwd) -> all-gather -> totals in rank order + apply
+    (hlhgat_bn_sync_fwd_apply).  Backward as torch.nn.SyncBatchNorm: global
+    sum g / sum g (x - mean) for dx, local dweight / dbias (DDP averages
+    them)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu, valid, sg, bn_args):
+        _, _, rm, rv, nbt, momentum, eps = bn_args
+        x = _rows2d(x, "x")
+        n, Cc = x.shape
+        y = torch.empty(n, Cc, device=x.device, dtype=x.dtype)
+        ws = _sync_workspace(x, n, Cc)
+        L = int(LIB.hlhgat_bn_sums_len(Cc))
+        sums = torch.empty(L, dtype=torch.float64, device=x.device)
+        check(LIB.hlhgat_bn_sums_fwd(x.data_ptr(), _ld(x), y.data_ptr(), _ld(y), n, _ptr(valid),
+                                     Cc, sums.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x)),
+              "bn_sums_fwd")
+        gathered = _all_gather_rows(sums, sg.group).contiguous()
+        mean = torch.empty(Cc, device=x.device, dtype=x.dtype)
+        invstd = torch.empty(Cc, device=x.device, dtype=x.dtype)
+        check(LIB.hlhgat_bn_sync_fwd_apply(
+            x.data_ptr(), _ld(x), n, _ptr(valid), Cc, gathered.data_ptr(), gathered.size(0),
+            _ptr(weight), _ptr(bias), _ptr(rm), _ptr(rv), _ptr(nbt), float(momentum), float(eps),
+            int(relu), y.data_ptr(), _ld(y), mean.data_ptr(), invstd.data_ptr(), _stream(x)),
+            "bn_sync_fwd_apply")
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd, valid)
+        ctx.sg = sg
+        ctx.has_b = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, weight, mean, invstd, valid = ctx.saved_tensors
+        gy = _rows2d(gy, "dy")
+        n, Cc = x.shape
+        dx = torch.empty_like(x)
+        need_w = weight is not None and ctx.needs_input_grad[1]
+        need_b = ctx.has_b and ctx.needs_input_grad[2]
+        dw = torch.empty(Cc, device=x.device, dtype=x.dtype) if need_w else None
+        db = torch.empty(Cc, device=x.device, dtype=x.dtype) if need_b else None
+        ws = _sync_workspace(x, n, Cc)
+        sums = torch.empty(int(LIB.hlhgat_bn_sums_len(Cc)), dtype=torch.float64, device=x.device)
+        check(LIB.hlhgat_bn_sums_bwd(
+            x.data_ptr(), _ld(x), _ptr(y), _ld(y) if y is not None else 0, gy.data_ptr(), _ld(gy),
+            dx.data_ptr(), _ld(dx), n, _ptr(valid), Cc, mean.data_ptr(), invstd.data_ptr(),
+            sums.data_ptr(), _ptr(dw), _ptr(db), ws.data_ptr(), ws.numel(), _stream(x)),
+            "bn_sums_bwd")
+        gathered = _all_gather_rows(sums, ctx.sg.group).contiguous()
+        check(LIB.hlhgat_bn_sync_bwd_apply(
+            x.data_ptr(), _ld(x), _ptr(y), _ld(y) if y is not None else 0, gy.data_ptr(), _ld(gy),
+            n, _ptr(valid), Cc, _ptr(weight), mean.data_ptr(), invstd.data_ptr(),
+            gathered.data_ptr(), gathered.size(0), dx.data_ptr(), _ld(dx), _stream(x)),
+            "bn_sync_bwd_apply")
+        return dx, dw, db, None, None, None, None
 
 
 # ----------------------------------------------------------------------------

@@ -458,6 +458,44 @@ int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy
                         float* dweight, float* dbias, void* workspace,
                         int64_t workspace_bytes, void* stream);
 
+/* ---- SyncBatchNorm (batch statistics over every data-parallel rank) ----- */
+/* torch.nn.SyncBatchNorm semantics for the BatchNorm1d layers of the path
+ * (lib/Hodge_ST_Model.py:556-566, lib/Hodge_Cheb_Conv.py:276-289) when the
+ * batch is sharded by graph over ranks (parity caveat 1):
+ *   1. hlhgat_bn_sums_fwd: this rank's fp64 column sums into
+ *      sums[hlhgat_bn_sums_len(C)] = [S0[C] = sum x, S1[C] = sum x^2, n_valid];
+ *   2. the caller all-gathers them into gathered[world][2C+1] (RCCL);
+ *   3. hlhgat_bn_sync_fwd_apply: every rank totals the gathered sums in rank
+ *      order (fp64), finishes mean / invstd / running statistics exactly as
+ *      hlhgat_bn_fwd_train does and writes y.
+ * Backward: hlhgat_bn_sums_bwd (sum g, sum g (x - mean) with g = dy masked
+ * by the ReLU of y; this rank's dweight / dbias, which data-parallel
+ * gradient averaging then combines as torch's SyncBatchNorm does), all-gather,
+ * hlhgat_bn_sync_bwd_apply (dx with the global sums and count).  y / dx of
+ * the _sums_ calls only select the layout (pass the tensors the apply will
+ * use): with one rank the results are bitwise those of hlhgat_bn_fwd_train /
+ * hlhgat_bn_bwd_train.  The workspace is hlhgat_bn_workspace_bytes' one. */
+int64_t hlhgat_bn_sums_len(int64_t C);
+int hlhgat_bn_sums_fwd(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n,
+                       const int32_t* n_valid, int64_t C, double* sums, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+int hlhgat_bn_sync_fwd_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_valid,
+                             int64_t C, const double* gathered, int world, const float* weight,
+                             const float* bias, float* running_mean, float* running_var,
+                             int64_t* num_batches_tracked, float momentum, float eps, int relu,
+                             float* y, int64_t ldy, float* save_mean, float* save_invstd,
+                             void* stream);
+int hlhgat_bn_sums_bwd(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                       const float* dy, int64_t lddy, float* dx_layout, int64_t lddx, int64_t n,
+                       const int32_t* n_valid, int64_t C, const float* save_mean,
+                       const float* save_invstd, double* sums, float* dweight, float* dbias,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                             const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
+                             int64_t C, const float* weight, const float* save_mean,
+                             const float* save_invstd, const double* gathered, int world,
+                             float* dx, int64_t lddx, void* stream);
+
 /* ---- workspaces --------------------------------------------------------- */
 /* Zero `bytes` (a multiple of 4) at p with a kernel on `stream` (graph-capture
  * safe; used to initialise the BatchNorm workspace counters). */
