@@ -276,15 +276,15 @@ __device__ __forceinline__ bool bar_wait(unsigned long long* word, unsigned tota
 }
 
 // the barrier word of this launch's column tile (8-byte aligned: kGridBase is even)
-__device__ __forceinline__ unsigned long long* barrier_word(const StatsArgs& a) {
-  return reinterpret_cast<unsigned long long*>(a.count + kGridBase) + blockIdx.y;
+__device__ __forceinline__ unsigned long long* barrier_word(const StatsArgs& a, const Blk& blk) {
+  return reinterpret_cast<unsigned long long*>(a.count + kGridBase) + blk.y;
 }
 
 // Block-level column partials: threads (row group rg, column lane cl) hold V
 // columns each; reduce over the rp row groups through LDS in fixed order.
 template <int V, int NT>
 __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
-                                               const StatsArgs& a, int c0) {
+                                               const StatsArgs& a, int c0, const Blk& blk) {
   __shared__ double red[2][NT * 4];
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
@@ -302,7 +302,7 @@ __device__ __forceinline__ void write_partials(double (&s0)[V], double (&s1)[V],
     }
     const int c = c0 + t;
     if (c < a.C) {
-      double* dst = a.part + ((int64_t)blockIdx.x * a.C + c) * 2;
+      double* dst = a.part + ((int64_t)blk.x * a.C + c) * 2;
       st_wt(dst, u0);
       st_wt(dst + 1, u1);
     }
@@ -409,14 +409,14 @@ __device__ __forceinline__ void reduce_range(const double* src, int first, int c
 // (one arrival counter), else a two-level last-arriver tree.
 template <int NT>
 __device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile_c,
-                                            double* out0, double* out1) {
-  const int tile = blockIdx.y;
+                                            double* out0, double* out1, const Blk& blk) {
+  const int tile = blk.y;
   if (a.parts <= kFlatMax) {
     if (!arrive_last(a.count + tile, (unsigned)a.parts)) return false;
     flat_reduce<NT>(a.part, a.parts, a, c0, tile_c, out0, out1);
     return true;
   }
-  const int g = blockIdx.x / kGroup;
+  const int g = blk.x / kGroup;
   const int ng = (a.parts + kGroup - 1) / kGroup;
   const int first = g * kGroup;
   const int cnt = a.parts - first < kGroup ? a.parts - first : kGroup;
@@ -477,27 +477,27 @@ __device__ __forceinline__ void bwd_coefs(float is_f, float w_f, double sg, doub
 // (layout [S0[C], S1[C], n_eff], fp64: hlhgat_bn_sums_fwd / _bwd).
 __device__ __forceinline__ void write_sums(const StatsArgs& a, int c0, int tile_c,
                                            const double* sum0, const double* sum1,
-                                           int64_t n_eff) {
+                                           int64_t n_eff, const Blk& blk) {
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     if (cc >= a.C) continue;
     a.sums_out[cc] = sum0[t];
     a.sums_out[a.C + cc] = sum1[t];
   }
-  if (blockIdx.y == 0 && threadIdx.x == 0) a.sums_out[2 * a.C] = (double)n_eff;
+  if (blk.y == 0 && threadIdx.x == 0) a.sums_out[2 * a.C] = (double)n_eff;
 }
 
 // ---------------------------------------------------------------------------
 // two-launch path
 // ---------------------------------------------------------------------------
 template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
+__device__ __forceinline__ void k_bn_stats_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
-  const int c0 = blockIdx.y * a.tpr * V;
+  const int c0 = blk.y * a.tpr * V;
   const int c = c0 + cl * V;
-  const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
+  const int64_t r_lo = (int64_t)blk.x * a.rows_per_part;
   int64_t r_hi = r_lo + a.rows_per_part;
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
   if (r_hi > n_eff) r_hi = n_eff;
@@ -529,12 +529,12 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
       }
     }
   }
-  write_partials<V, kThreads>(s0, s1, a, c0);
+  write_partials<V, kThreads>(s0, s1, a, c0, blk);
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1)) return;
+  if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1, blk)) return;
   if (a.sums_out) {  // SyncBatchNorm: this rank's sums, finalised after the all-gather
-    write_sums(a, c0, tile_c, sum0, sum1, n_eff);
+    write_sums(a, c0, tile_c, sum0, sum1, n_eff, blk);
     return;
   }
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
@@ -545,7 +545,24 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
     a.save_mean[cc] = m;
     a.save_invstd[cc] = is;
   }
-  if (a.nbt && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  if (a.nbt && blk.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
+  k_bn_stats_body<V>(a, blk_hw());
+}
+
+// node + edge sides of an HL block in one launch (launch groups, common.h)
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_stats_pair(Pair<StatsArgs> p) {
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    k_bn_stats_body<V>(p.a[0], b);
+  else
+    k_bn_stats_body<V>(p.a[1], b);
 }
 
 struct ApplyArgs {
@@ -565,11 +582,11 @@ struct ApplyArgs {
 };
 
 template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
+__device__ __forceinline__ void k_bn_apply_body(const ApplyArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
-  const int c = blockIdx.y * a.tpr * V + cl * V;
+  const int c = blk.y * a.tpr * V + cl * V;
   if (c >= a.C) return;
   float s[V], m[V], t[V];
 #pragma unroll
@@ -581,7 +598,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
   }
   // APPLY_RPT rows per thread, all loads issued before any store
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
-  const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
+  const int64_t r0 = (int64_t)blk.x * a.rp * APPLY_RPT + rg;
   vt xv[APPLY_RPT];
 #pragma unroll
   for (int u = 0; u < APPLY_RPT; ++u) {
@@ -600,6 +617,23 @@ __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
     }
     vstore<V>(a.y + r * a.ldy + c, o);
   }
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
+  k_bn_apply_body<V>(a, blk_hw());
+}
+
+// node + edge sides of an HL block in one launch (launch groups, common.h)
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_apply_pair(Pair<ApplyArgs> p) {
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    k_bn_apply_body<V>(p.a[0], b);
+  else
+    k_bn_apply_body<V>(p.a[1], b);
 }
 
 struct BwdApplyArgs {
@@ -623,13 +657,13 @@ struct BwdApplyArgs {
 // the finalising workgroup of a column tile forms dweight, dbias and dx's
 // coefficients.
 template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
+__device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
-  const int c0 = blockIdx.y * a.tpr * V;
+  const int c0 = blk.y * a.tpr * V;
   const int c = c0 + cl * V;
-  const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
+  const int64_t r_lo = (int64_t)blk.x * a.rows_per_part;
   int64_t r_hi = r_lo + a.rows_per_part;
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
   if (r_hi > n_eff) r_hi = n_eff;
@@ -671,12 +705,12 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
       acc(xv, gv, yv);
     }
   }
-  write_partials<V, kThreads>(s0, s1, a, c0);
+  write_partials<V, kThreads>(s0, s1, a, c0, blk);
   __shared__ double sum0[kThreads], sum1[kThreads];
   const int tile_c = a.tpr * V;
-  if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1)) return;
+  if (!last_reduce<kThreads>(a, c0, tile_c, sum0, sum1, blk)) return;
   if (a.sums_out) {  // SyncBatchNorm: local dweight / dbias, global coefficients later
-    write_sums(a, c0, tile_c, sum0, sum1, n_eff);
+    write_sums(a, c0, tile_c, sum0, sum1, n_eff, blk);
     for (int t = threadIdx.x; t < tile_c; t += kThreads) {
       const int cc = c0 + t;
       if (cc >= a.C) continue;
@@ -700,11 +734,28 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
 }
 
 template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
+  k_bn_bwd_reduce_body<V>(a, blk_hw());
+}
+
+// node + edge sides of an HL block in one launch (launch groups, common.h)
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce_pair(Pair<StatsArgs> p) {
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    k_bn_bwd_reduce_body<V>(p.a[0], b);
+  else
+    k_bn_bwd_reduce_body<V>(p.a[1], b);
+}
+
+template <int V>
+__device__ __forceinline__ void k_bn_bwd_apply_body(const BwdApplyArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
-  const int c = blockIdx.y * a.tpr * V + cl * V;
+  const int c = blk.y * a.tpr * V + cl * V;
   if (c >= a.C) return;
   float A[V], B[V], Cc[V], mu[V];
 #pragma unroll
@@ -715,7 +766,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     mu[v] = a.mean[c + v];
   }
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
-  const int64_t r0 = (int64_t)blockIdx.x * a.rp * APPLY_RPT + rg;
+  const int64_t r0 = (int64_t)blk.x * a.rp * APPLY_RPT + rg;
   vt xv[APPLY_RPT], gv[APPLY_RPT], yv[APPLY_RPT];
 #pragma unroll
   for (int u = 0; u < APPLY_RPT; ++u) {
@@ -739,6 +790,23 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
     }
     vstore<V>(a.dx + r * a.lddx + c, o);
   }
+}
+
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
+  k_bn_bwd_apply_body<V>(a, blk_hw());
+}
+
+// node + edge sides of an HL block in one launch (launch groups, common.h)
+template <int V>
+__global__ __launch_bounds__(kThreads) void k_bn_bwd_apply_pair(Pair<BwdApplyArgs> p) {
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    k_bn_bwd_apply_body<V>(p.a[0], b);
+  else
+    k_bn_bwd_apply_body<V>(p.a[1], b);
 }
 
 // ---------------------------------------------------------------------------
@@ -884,13 +952,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_sync_bwd_apply(SyncArgs a) {
 // Forward: thread (rg, cl) owns rows r_lo + rg + j * rp (j < RPT) of its
 // partition; statistics rows stop at n_eff, output rows at n.
 template <int V, int RPT>
-__global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
+__device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
   const int rg = threadIdx.x / a.tpr;
-  const int c0 = blockIdx.y * a.tpr * V;
+  const int c0 = blk.y * a.tpr * V;
   const int c = c0 + cl * V;
-  const int64_t r_lo = (int64_t)blockIdx.x * a.rows_per_part;
+  const int64_t r_lo = (int64_t)blk.x * a.rows_per_part;
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
   int64_t r_hi = r_lo + a.rows_per_part;
   if (r_hi > n_eff) r_hi = n_eff;
@@ -925,18 +993,18 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
     wv[v] = (a.weight && in) ? a.weight[c + v] : 1.f;
     bv[v] = (a.bias && in) ? a.bias[c + v] : 0.f;
   }
-  write_partials<V, kThreads>(s0, s1, a, c0);
-  const bool ok = bar_wait(barrier_word(a), gridDim.x, a.poll_limit, a.err);
+  write_partials<V, kThreads>(s0, s1, a, c0, blk);
+  const bool ok = bar_wait(barrier_word(a, blk), blk.gx, a.poll_limit, a.err);
   __shared__ double sum0[kThreads], sum1[kThreads];
   __shared__ float sm[kThreads], ss[kThreads];
   const int tile_c = a.tpr * V;
-  if (ok) flat_reduce<kThreads>(a.part, gridDim.x, a, c0, tile_c, sum0, sum1);
+  if (ok) flat_reduce<kThreads>(a.part, blk.gx, a, c0, tile_c, sum0, sum1);
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
     float m = __builtin_nanf(""), is = __builtin_nanf("");
     if (ok && cc < a.C) {
-      fwd_finalize(a, cc, sum0[t], sum1[t], n_eff, m, is, blockIdx.x == 0);
-      if (blockIdx.x == 0) {
+      fwd_finalize(a, cc, sum0[t], sum1[t], n_eff, m, is, blk.x == 0);
+      if (blk.x == 0) {
         a.save_mean[cc] = m;
         a.save_invstd[cc] = is;
       }
@@ -944,7 +1012,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
     sm[t] = m;
     ss[t] = is;
   }
-  if (ok && a.nbt && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  if (ok && a.nbt && blk.x == 0 && blk.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
   __syncthreads();
   if (c < a.C) {
     float sc[V], mu[V], sh[V];
@@ -970,6 +1038,23 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
       }
     }
   }
+}
+
+template <int V, int RPT>
+__global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
+  k_bn_fwd_grid_body<V, RPT>(a, blk_hw());
+}
+
+// node + edge sides of an HL block in one launch (launch groups, common.h)
+template <int V, int RPT>
+__global__ __launch_bounds__(kThreads) void k_bn_fwd_grid_pair(Pair<StatsArgs> p) {
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    k_bn_fwd_grid_body<V, RPT>(p.a[0], b);
+  else
+    k_bn_fwd_grid_body<V, RPT>(p.a[1], b);
 }
 
 bool bn_vec_ok(int64_t C, std::initializer_list<int64_t> lds,
@@ -1078,7 +1163,43 @@ GridFn pick_grid(const BnLayout& L, bool vec) {
   return f;
 }
 
+template <int V>
+void reg_bn_pairs() {
+  register_pair(reinterpret_cast<const void*>(k_bn_stats<V>),
+                reinterpret_cast<const void*>(k_bn_stats_pair<V>), false);
+  register_pair(reinterpret_cast<const void*>(k_bn_apply<V>),
+                reinterpret_cast<const void*>(k_bn_apply_pair<V>), false);
+  register_pair(reinterpret_cast<const void*>(k_bn_bwd_reduce<V>),
+                reinterpret_cast<const void*>(k_bn_bwd_reduce_pair<V>), false);
+  register_pair(reinterpret_cast<const void*>(k_bn_bwd_apply<V>),
+                reinterpret_cast<const void*>(k_bn_bwd_apply_pair<V>), false);
+}
+template <int V, int RPT>
+void reg_bn_grid_pair() {  // a grid barrier: the joint grid must be co-resident
+  register_pair(reinterpret_cast<const void*>(k_bn_fwd_grid<V, RPT>),
+                reinterpret_cast<const void*>(k_bn_fwd_grid_pair<V, RPT>), true);
+}
+
+const int g_bn_pairs = [] {
+  reg_bn_pairs<1>();
+  reg_bn_pairs<4>();
+  reg_bn_grid_pair<1, 2>(); reg_bn_grid_pair<1, 4>(); reg_bn_grid_pair<1, 8>();
+  reg_bn_grid_pair<1, 16>(); reg_bn_grid_pair<1, 32>();
+  reg_bn_grid_pair<4, 2>(); reg_bn_grid_pair<4, 4>(); reg_bn_grid_pair<4, 8>();
+  reg_bn_grid_pair<4, 16>(); reg_bn_grid_pair<4, 32>();
+  return 0;
+}();
+
 }  // namespace
+
+namespace hlhgat {
+// The pair of two one-launch BatchNorm grids waits at two grid barriers at
+// once: both grids together must fit the same half-capacity bound as one
+// grid alone (pick_grid).
+bool pair_coresident(const void* pair_kernel, int64_t blocks) {
+  return blocks <= capacity_of(pair_kernel);
+}
+}  // namespace hlhgat
 
 extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
   if (n < 0 || C <= 0) return 0;
@@ -1112,9 +1233,9 @@ extern "C" int hlhgat_bn_stats_train(const float* x, int64_t ldx, int64_t n,
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    k_bn_stats<4><<<g1, kThreads, 0, st>>>(s);
+    launch(k_bn_stats<4>, dim3(g1), dim3(kThreads), 0, st, nullptr, s);
   else
-    k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
+    launch(k_bn_stats<1>, dim3(g1), dim3(kThreads), 0, st, nullptr, s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1134,9 +1255,9 @@ extern "C" int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int
   hipStream_t st = as_stream(stream);
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
-    k_bn_apply<4><<<g2, kThreads, 0, st>>>(p);
+    launch(k_bn_apply<4>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   else
-    k_bn_apply<1><<<g2, kThreads, 0, st>>>(p);
+    launch(k_bn_apply<1>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1197,17 +1318,17 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    k_bn_stats<4><<<g1, kThreads, 0, st>>>(s);
+    launch(k_bn_stats<4>, dim3(g1), dim3(kThreads), 0, st, nullptr, s);
   else
-    k_bn_stats<1><<<g1, kThreads, 0, st>>>(s);
+    launch(k_bn_stats<1>, dim3(g1), dim3(kThreads), 0, st, nullptr, s);
   HLH_CHECK_LAUNCH();
   ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
               L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
-    k_bn_apply<4><<<g2, kThreads, 0, st>>>(p);
+    launch(k_bn_apply<4>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   else
-    k_bn_apply<1><<<g2, kThreads, 0, st>>>(p);
+    launch(k_bn_apply<1>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1254,9 +1375,9 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
                  L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
-    k_bn_bwd_apply<4><<<g2, kThreads, 0, st>>>(p);
+    launch(k_bn_bwd_apply<4>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   else
-    k_bn_bwd_apply<1><<<g2, kThreads, 0, st>>>(p);
+    launch(k_bn_bwd_apply<1>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1282,9 +1403,9 @@ extern "C" int hlhgat_bn_sums_fwd(const float* x, int64_t ldx, const float* y, i
   s.sums_out = sums;
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    k_bn_stats<4><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+    launch(k_bn_stats<4>, dim3(g1), dim3(kThreads), 0, as_stream(stream), nullptr, s);
   else
-    k_bn_stats<1><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+    launch(k_bn_stats<1>, dim3(g1), dim3(kThreads), 0, as_stream(stream), nullptr, s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1329,9 +1450,9 @@ extern "C" int hlhgat_bn_sync_fwd_apply(const float* x, int64_t ldx, int64_t n,
   a.relu = relu;
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
-    k_bn_sync_apply<4><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+    launch(k_bn_sync_apply<4>, dim3(g2), dim3(kThreads), 0, as_stream(stream), nullptr, a);
   else
-    k_bn_sync_apply<1><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+    launch(k_bn_sync_apply<1>, dim3(g2), dim3(kThreads), 0, as_stream(stream), nullptr, a);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1365,9 +1486,9 @@ extern "C" int hlhgat_bn_sums_bwd(const float* x, int64_t ldx, const float* y, i
   s.sums_out = sums;
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    k_bn_bwd_reduce<4><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+    launch(k_bn_bwd_reduce<4>, dim3(g1), dim3(kThreads), 0, as_stream(stream), nullptr, s);
   else
-    k_bn_bwd_reduce<1><<<g1, kThreads, 0, as_stream(stream)>>>(s);
+    launch(k_bn_bwd_reduce<1>, dim3(g1), dim3(kThreads), 0, as_stream(stream), nullptr, s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1406,9 +1527,9 @@ extern "C" int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float
   a.save_invstd = const_cast<float*>(save_invstd);
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
-    k_bn_sync_bwd_apply<4><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+    launch(k_bn_sync_bwd_apply<4>, dim3(g2), dim3(kThreads), 0, as_stream(stream), nullptr, a);
   else
-    k_bn_sync_bwd_apply<1><<<g2, kThreads, 0, as_stream(stream)>>>(a);
+    launch(k_bn_sync_bwd_apply<1>, dim3(g2), dim3(kThreads), 0, as_stream(stream), nullptr, a);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

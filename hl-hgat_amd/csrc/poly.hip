@@ -107,13 +107,13 @@ __device__ __forceinline__ void poly_epilogue(const PolyArgs& a, int64_t row, in
 // Loads are issued DEPTH at a time, the adds stay in CSR order (bitwise the
 // same result for any DEPTH).
 template <int V, int LPR, int DEPTH>
-__device__ __forceinline__ void poly_step_body(const PolyArgs& a) {
+__device__ __forceinline__ void poly_step_body(const PolyArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   // XCD-aware slots: blocks are dealt round-robin over the 8 XCDs, so block b
   // takes slot range xcd_slot(b): each XCD walks ONE contiguous range of the
   // (optionally locality-ordered) row schedule and its L2 sees the neighbours
   // of the rows it is working on.
-  const int64_t slot = ((int64_t)xcd_slot(blockIdx.x, gridDim.x) * 256 + threadIdx.x) / LPR;
+  const int64_t slot = ((int64_t)xcd_slot(blk.x, blk.gx) * 256 + threadIdx.x) / LPR;
   const int sub = threadIdx.x % LPR;
   const bool live = slot < a.n_rows;
   const int64_t row = live ? (a.order ? (int64_t)a.order[slot] : slot) : 0;
@@ -195,13 +195,39 @@ __device__ __forceinline__ void poly_step_body(const PolyArgs& a) {
 
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
-  poly_step_body<V, LPR, 4>(a);
+  poly_step_body<V, LPR, 4>(a, blk_hw());
 }
 
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_poly_step_deep(PolyArgs a) {
-  poly_step_body<V, LPR, 8>(a);
+  poly_step_body<V, LPR, 8>(a, blk_hw());
 }
+
+// node + edge steps of an HL block in one launch (launch groups, common.h)
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_poly_step_pair(Pair<PolyArgs> p) {
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    poly_step_body<V, LPR, 4>(p.a[0], b);
+  else
+    poly_step_body<V, LPR, 4>(p.a[1], b);
+}
+
+template <int V, int LPR>
+void reg_poly_pair() {
+  register_pair(reinterpret_cast<const void*>(k_poly_step<V, LPR>),
+                reinterpret_cast<const void*>(k_poly_step_pair<V, LPR>), false);
+}
+
+const int g_poly_pairs = [] {
+  reg_poly_pair<4, 1>(); reg_poly_pair<4, 2>(); reg_poly_pair<4, 4>(); reg_poly_pair<4, 8>();
+  reg_poly_pair<4, 16>(); reg_poly_pair<4, 32>(); reg_poly_pair<4, 64>();
+  reg_poly_pair<2, 16>(); reg_poly_pair<2, 32>(); reg_poly_pair<2, 64>();
+  reg_poly_pair<1, 16>(); reg_poly_pair<1, 32>(); reg_poly_pair<1, 64>();
+  return 0;
+}();
 
 // ---------------------------------------------------------------------------
 // Second factor of the Hodge-factored L1 (hlhgat_hodge_factor_t):
@@ -1235,8 +1261,8 @@ int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
     // the direct part of dX (block 0), then dX += L^T dS.
     HLH_CHECK_ARG(K <= LOC_MAXK, "poly_basis_bwd: DEMO recurrence needs K <= %d", LOC_MAXK);
     DemoArgs d{G, n * F, K};
-    hipLaunchKernelGGL(k_demo_adjoint_fold, dim3((unsigned)ceil_div(n * F, (int64_t)256)),
-                       dim3(256), 0, s, d);
+    launch(k_demo_adjoint_fold, dim3((unsigned)ceil_div(n * F, (int64_t)256)), dim3(256), 0, s,
+           nullptr, d);
     HLH_CHECK_LAUNCH();
     PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(1), F, F, Gk(0), F, row_order, halo);
     a.P = Gk(0);

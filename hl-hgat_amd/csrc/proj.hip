@@ -270,13 +270,13 @@ __device__ __forceinline__ void store_tile_rows(const floatx4 (&acc)[TN], float*
 }
 
 template <int TN>
-__global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
-  __shared__ float wl[2][TN * 16][KCP];
+__device__ __forceinline__ void proj_fwd_lds_body(const FwdArgs& a, Blk blk,
+                                                  float (*wl)[TN * 16][KCP]) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, i = lane & 15;
-  const int64_t m_base = ((int64_t)blockIdx.x * 4 + wave) * 16;
-  const int n_base = blockIdx.y * (TN * 16);
+  const int64_t m_base = ((int64_t)blk.x * 4 + wave) * 16;
+  const int n_base = blk.y * (TN * 16);
   const int64_t row = m_base + i;
   const bool aval = row < a.M;
 
@@ -336,6 +336,25 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
                       (reinterpret_cast<uintptr_t>(a.C) & 15) == 0;
   store_tile_rows<TN>(acc, scratch, m_base, a.M, a.C + n_base, a.ldc, ncols,
                       a.bias ? a.bias + n_base : nullptr, a.accumulate, vec_ok);
+}
+
+template <int TN>
+__global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
+  __shared__ float wl[2][TN * 16][KCP];
+  proj_fwd_lds_body<TN>(a, blk_hw(), wl);
+}
+
+// node + edge projections of an HL block in one launch (launch groups)
+template <int TN>
+__global__ __launch_bounds__(256) void k_proj_fwd_lds_pair(Pair<FwdArgs> p) {
+  __shared__ float wl[2][TN * 16][KCP];
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    proj_fwd_lds_body<TN>(p.a[0], b, wl);
+  else
+    proj_fwd_lds_body<TN>(p.a[1], b, wl);
 }
 
 // ---------------------------------------------------------------------------
@@ -828,10 +847,10 @@ struct ReduceArgs {
 // 64 consecutive output elements per workgroup; the 4 waves sum interleaved
 // subsets of the splits (coalesced 256-B reads per split), then combine in
 // fixed order through LDS -> deterministic and fully parallel.
-__global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
+__device__ __forceinline__ void reduce_splits_body(const ReduceArgs& a, Blk blk) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t e = (int64_t)blk.x * 64 + lane;
   const int64_t total = a.elem_start[a.nb] + (a.bias_off >= 0 ? a.N : 0);
   int64_t src = -1;
   float* dst = nullptr;
@@ -872,6 +891,12 @@ __global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
+  reduce_splits_body(a, blk_hw());
+}
+
+HLH_PAIR_KERNEL(k_reduce_splits_pair, ReduceArgs, reduce_splits_body)
+
 // ---------------------------------------------------------------------------
 // Linear backward with the weight-gradient partials and the data gradient in
 // ONE launch: workgroups [0, n_w) are the weight gradient's (tile, split)
@@ -893,10 +918,8 @@ struct BwdFusedArgs {
 };
 
 template <int TND>
-__global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
-  constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
-  __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
-  const int L = (int)blockIdx.x;
+__device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
+  const int L = (int)blk.x;
   if (L >= a.n_wpad) {
     const int l = L - a.n_wpad;
     int bx, by;
@@ -924,6 +947,43 @@ __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
                     reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
+
+template <int TND>
+__global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
+  constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
+  __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
+  proj_bwd_fused_body<TND>(a, blk_hw(), lds);
+}
+
+// node + edge Linear backwards of an HL block in one launch (launch groups)
+template <int TND>
+__global__ __launch_bounds__(256) void k_proj_bwd_fused_pair(Pair<BwdFusedArgs> p) {
+  constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
+  __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
+  int s;
+  Blk b;
+  if (!pair_blk(p, s, b)) return;
+  if (s == 0)
+    proj_bwd_fused_body<TND>(p.a[0], b, lds);
+  else
+    proj_bwd_fused_body<TND>(p.a[1], b, lds);
+}
+
+const int g_proj_pairs = [] {
+  register_pair(reinterpret_cast<const void*>(k_proj_fwd_lds<1>),
+                reinterpret_cast<const void*>(k_proj_fwd_lds_pair<1>), false);
+  register_pair(reinterpret_cast<const void*>(k_proj_fwd_lds<2>),
+                reinterpret_cast<const void*>(k_proj_fwd_lds_pair<2>), false);
+  register_pair(reinterpret_cast<const void*>(k_proj_fwd_lds<4>),
+                reinterpret_cast<const void*>(k_proj_fwd_lds_pair<4>), false);
+  register_pair(reinterpret_cast<const void*>(k_proj_bwd_fused<1>),
+                reinterpret_cast<const void*>(k_proj_bwd_fused_pair<1>), false);
+  register_pair(reinterpret_cast<const void*>(k_proj_bwd_fused<2>),
+                reinterpret_cast<const void*>(k_proj_bwd_fused_pair<2>), false);
+  register_pair(reinterpret_cast<const void*>(k_reduce_splits),
+                reinterpret_cast<const void*>(k_reduce_splits_pair), false);
+  return 0;
+}();
 
 // --- planning ------------------------------------------------------------------
 struct WeightPlan {
@@ -1128,20 +1188,20 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   if (vec)
   {
     if (tnd == 1)
-      k_proj_bwd_data_lds<1><<<grid, 256, 0, s>>>(a);
+      launch(k_proj_bwd_data_lds<1>, dim3(grid), dim3(256), 0, s, nullptr, a);
     else if (tnd == 2)
-      k_proj_bwd_data_lds<2><<<grid, 256, 0, s>>>(a);
+      launch(k_proj_bwd_data_lds<2>, dim3(grid), dim3(256), 0, s, nullptr, a);
     else
-      k_proj_bwd_data_lds<TN><<<grid, 256, 0, s>>>(a);
+      launch(k_proj_bwd_data_lds<TN>, dim3(grid), dim3(256), 0, s, nullptr, a);
   }
   else
   {
     if (tnd == 1)
-      k_proj_bwd_data<1, 1, false><<<grid, 256, 0, s>>>(a);
+      launch(k_proj_bwd_data<1, 1, false>, dim3(grid), dim3(256), 0, s, nullptr, a);
     else if (tnd == 2)
-      k_proj_bwd_data<1, 2, false><<<grid, 256, 0, s>>>(a);
+      launch(k_proj_bwd_data<1, 2, false>, dim3(grid), dim3(256), 0, s, nullptr, a);
     else
-      k_proj_bwd_data<1, TN, false><<<grid, 256, 0, s>>>(a);
+      launch(k_proj_bwd_data<1, TN, false>, dim3(grid), dim3(256), 0, s, nullptr, a);
   }
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
@@ -1203,6 +1263,7 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   hipStream_t s = as_stream(stream);
   if (M == 0) {
     // no rows: gradient contribution is zero
+    HLH_CHECK_ARG(!group_recording(), "proj_bwd_weight: M == 0 inside a launch group");
     if (!accumulate) {
       for (int b = 0; b < nblocks; ++b)
         for (int64_t n = 0; n < N; ++n)
@@ -1216,9 +1277,9 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   for (int b = 0; b < nblocks; ++b)
     vec = vec && aligned16(A[b]) && (lda[b] % 4) == 0 && (kb[b] % 4) == 0;
   if (vec)
-    k_proj_bwd_weight32<<<grid, 256, 0, s>>>(a);
+    launch(k_proj_bwd_weight32, dim3(grid), dim3(256), 0, s, nullptr, a);
   else
-    k_proj_bwd_weight<<<grid, 256, 0, s>>>(a);
+    launch(k_proj_bwd_weight, dim3(grid), dim3(256), 0, s, nullptr, a);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
@@ -1227,7 +1288,7 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   r.dbias = dbias;
   r.accumulate = accumulate;
   const int64_t total = r.elem_start[nblocks] + (dbias ? N : 0);
-  k_reduce_splits<<<(unsigned)ceil_div(total, 64), 256, 0, s>>>(r);
+  launch(k_reduce_splits, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, nullptr, r);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1350,7 +1411,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   r.dbias = dbias;
   r.accumulate = 0;
   const int64_t total = r.elem_start[nb_w] + (dbias ? N : 0);
-  k_reduce_splits<<<(unsigned)ceil_div(total, 64), 256, 0, s>>>(r);
+  launch(k_reduce_splits, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, nullptr, r);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -138,6 +138,46 @@ hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_e
   return h;
 }
 
+// ---------------------------------------------------------------------------
+// Launch groups (include/hlhgat.h hlhgat_group_*): while the node and edge
+// sides of an HL block are recorded, launches are deferred to the end of the
+// group, so every temporary a recorded launch reads or writes must outlive
+// the group: keep_alive() parks it until the group ends (a no-op otherwise).
+// ---------------------------------------------------------------------------
+std::vector<Tensor>*& keep_list() {
+  static thread_local std::vector<Tensor>* k = nullptr;
+  return k;
+}
+inline const Tensor& keep_alive(const Tensor& t) {
+  if (keep_list() && t.defined()) keep_list()->push_back(t);
+  return t;
+}
+
+struct LaunchGroup {
+  std::vector<Tensor> keep;
+  bool active = false;
+  void begin() {
+    chk(hlhgat_group_begin(), "group_begin");
+    active = true;
+    keep_list() = &keep;
+  }
+  void next() { chk(hlhgat_group_next(), "group_next"); }
+  int end(void* stream) {
+    int paired = 0;
+    active = false;
+    keep_list() = nullptr;
+    chk(hlhgat_group_end(stream, &paired), "group_end");
+    keep.clear();  // launches are enqueued: the caching allocator orders reuse on the stream
+    return paired;
+  }
+  ~LaunchGroup() {
+    if (active) {
+      hlhgat_group_abort();
+      keep_list() = nullptr;
+    }
+  }
+};
+
 // One BN workspace per (device, stream): its arrival counters must not be
 // shared by launches that can run concurrently (node / edge chains run on two
 // streams, see hlhgat.ops.fork).  Stream-ordered reuse on one stream is safe.
@@ -145,10 +185,12 @@ hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_e
 // earlier on that stream still holds its address, and a replay must not write
 // BN counters into memory the caching allocator has handed to another tensor.
 // (Sizes grow geometrically, so at most a handful are ever retired.)
-Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
+Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C, int slot = 0) {
   static auto* cache = new std::unordered_map<uintptr_t, Tensor>();  // leaked: outlives HIP teardown
   static auto* retired = new std::vector<Tensor>();
-  const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
+  // slot: the member of a launch group (its two sides' BatchNorms run in one launch)
+  const uintptr_t key =
+      (reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device()) * 2 + (slot & 1);
   const int64_t need = hlhgat_bn_workspace_bytes(n, C);
   auto it = cache->find(key);
   if (it == cache->end() || it->second.numel() < need) {
@@ -228,7 +270,7 @@ void proj_bwd_weight(const Tensor& G, const std::vector<const float*>& A,
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
       hlhgat_proj_bwd_weight_workspace_floats(nb, kb.data(), M, N, db != nullptr);
-  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, G.options());
+  Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
   chk(hlhgat_proj_bwd_weight(nb, G.data_ptr<float>(), ld_of(G), A.data(), lda.data(), kb.data(),
                              M, N, dW.data(), lddw.data(), db, 0, ws.data_ptr<float>(), wsf, s),
       "proj_bwd_weight");
@@ -246,6 +288,7 @@ bool& fused_bwd_flag() {
 }
 void set_fused_bwd(bool on) { fused_bwd_flag() = on; }
 
+
 // weight (+bias) and data gradients of one Linear: hlhgat_proj_bwd (weight
 // partials and data gradient in one launch, then the split reduction)
 void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
@@ -258,7 +301,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
       nbw ? hlhgat_proj_bwd_weight_workspace_floats(nbw, kbw.data(), M, N, db != nullptr) : 0;
-  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, G.options());
+  Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
   chk(hlhgat_proj_bwd(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(), kbw.data(),
                       dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(), kbd.data(),
                       dA.data(), ldda.data(), ws.data_ptr<float>(), wsf, s),
@@ -280,13 +323,13 @@ struct BnState {
 };
 
 Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
-                  const Tensor* y_into = nullptr) {
+                  const Tensor* y_into = nullptr, int slot = 0) {
   const int64_t n = x.size(0), C = x.size(1);
   Tensor y = y_into ? *y_into : at::empty({n, C}, x.options());
   TORCH_CHECK(y.size(0) == n && y.size(1) == C && y.stride(1) == 1, "hlhgat: bad BN output view");
   mean = at::empty({C}, x.options());
   invstd = at::empty({C}, x.options());
-  Tensor ws = bn_workspace(x, n, C);
+  Tensor ws = bn_workspace(x, n, C, slot);
   int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
   chk(hlhgat_bn_fwd_train(x.data_ptr<float>(), ld_of(x), n, iptr(st.valid), C, fptr(st.w),
                           fptr(st.b),
@@ -313,16 +356,17 @@ bool graph_local_env() {
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
                    const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
                    Tensor& dw, Tensor& db, const Tensor* dx_into = nullptr,
-                   const Tensor* b_param = nullptr, const Tensor& valid = Tensor()) {
+                   const Tensor* b_param = nullptr, const Tensor& valid = Tensor(),
+                   int slot = 0) {
   const int64_t n = x.size(0), C = x.size(1);
-  Tensor dyc = rows2d(dy);
+  Tensor dyc = keep_alive(rows2d(dy));
   Tensor dx = dx_into ? *dx_into : at::empty({n, C}, x.options());
   TORCH_CHECK(dx.size(0) == n && dx.size(1) == C && dx.stride(1) == 1, "hlhgat: bad dx view");
   dw = (need_w && has(w)) ? grad_like(w) : Tensor();
   db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
                                                  : at::empty({C}, x.options()))
               : Tensor();
-  Tensor ws = bn_workspace(x, n, C);
+  Tensor ws = bn_workspace(x, n, C, slot);
   chk(hlhgat_bn_bwd_train(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
                           dyc.data_ptr<float>(), ld_of(dyc), n,
                           valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
@@ -334,9 +378,396 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
   return dx;
 }
 
+// Two-stream fork inside one autograd node: the node (current) stream and a
+// persistent side stream per device, ordered by hipEvents (captured into a
+// hipGraph as branch dependencies).  Tensors allocated while the side stream
+// is current and then used on the node stream are record_stream()-ed.
+// (PyTorch-ROCm exposes HIP streams to torch as "cuda" streams: the
+// MasqueradingAsCUDA wrappers are the ones its allocator and guards accept.)
+using TStream = c10::hip::HIPStreamMasqueradingAsCUDA;
+using TStreamGuard = c10::hip::HIPStreamGuardMasqueradingAsCUDA;
+struct Fork {
+  TStream main, side;
+  explicit Fork(int dev)
+      : main(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)dev)),
+        side(side_of(dev)) {}
+  static std::unordered_map<int, TStream>& registry() {
+    static auto* streams = new std::unordered_map<int, TStream>();
+    return *streams;
+  }
+  static TStream side_of(int dev) {
+    auto& streams = registry();
+    auto it = streams.find(dev);
+    if (it == streams.end())
+      it = streams.emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
+                                    false, (c10::DeviceIndex)dev)).first;
+    return it->second;
+  }
+  static hipEvent_t next_event() {
+    static thread_local std::vector<hipEvent_t> pool;
+    static thread_local size_t k = 0;
+    if (pool.empty()) {
+      pool.resize(64);
+      for (auto& e : pool) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == 0);
+    }
+    return pool[k++ % pool.size()];
+  }
+  static void order(const TStream& from, const TStream& to) {
+    hipEvent_t e = next_event();
+    TORCH_CHECK(hipEventRecord(e, from.stream()) == hipSuccess, "hlhgat: hipEventRecord");
+    TORCH_CHECK(hipStreamWaitEvent(to.stream(), e, 0) == hipSuccess, "hlhgat: hipStreamWaitEvent");
+  }
+  void side_waits_main() { order(main, side); }
+  void main_waits_side() { order(side, main); }
+  void escape(std::initializer_list<Tensor> ts) {
+    for (const auto& t : ts)
+      if (t.defined()) t.record_stream(main);
+  }
+};
+
 // ---------------------------------------------------------------------------
 // conv (+ BN (+ ReLU))
 // ---------------------------------------------------------------------------
+// One side's conv (+ BN (+ ReLU)) arguments (the conv_bn signature below).
+struct ConvArgs {
+  Tensor x, a_rowptr, a_col;
+  OptT a_val;
+  Tensor t_rowptr, t_col;
+  OptT t_val;
+  int64_t nnz = 0, kind = 0;
+  std::vector<Tensor> W;
+  OptT bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt;
+  double momentum = 0.1, eps = 1e-5;
+  int64_t bn_mode = 0;
+  OptT out_buf, a_order, t_order, tiles;
+  int64_t tile_rows = 0, tile_nnz = 0;
+  OptT valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval;
+  std::vector<int64_t> h_bounds;
+  OptT h_hdr;
+  std::vector<Tensor> fac;
+  int64_t fac_nodes = 0;
+};
+
+// What one side's backward needs: the tensors (kSavedFixed, then W[0..K),
+// then the factor) and the sizes.
+constexpr size_t kSavedFixed = 22;
+struct ConvSaved {
+  std::vector<Tensor> t;
+  std::vector<int64_t> dims;  // N, Cin, F, M, dout, K, kind, nnz, bn_mode, has_bias
+  std::vector<int64_t> xshape, h_bounds;
+  int64_t fac_nodes = 0, tile_rows = 0, tile_nnz = 0;
+  void to_ctx(AutogradContext* ctx, const std::string& p) const {
+    ctx->saved_data[p + "dims"] = dims;
+    ctx->saved_data[p + "xshape"] = xshape;
+    ctx->saved_data[p + "h_bounds"] = h_bounds;
+    ctx->saved_data[p + "misc"] = std::vector<int64_t>{fac_nodes, tile_rows, tile_nnz,
+                                                       (int64_t)t.size()};
+  }
+  static ConvSaved from_ctx(AutogradContext* ctx, const std::string& p,
+                            const std::vector<Tensor>& all, size_t first) {
+    ConvSaved s;
+    s.dims = ctx->saved_data[p + "dims"].toIntVector();
+    s.xshape = ctx->saved_data[p + "xshape"].toIntVector();
+    s.h_bounds = ctx->saved_data[p + "h_bounds"].toIntVector();
+    const auto m = ctx->saved_data[p + "misc"].toIntVector();
+    s.fac_nodes = m[0];
+    s.tile_rows = m[1];
+    s.tile_nnz = m[2];
+    s.t.assign(all.begin() + first, all.begin() + first + m[3]);
+    return s;
+  }
+};
+
+// Which gradients one side's backward must produce.
+struct ConvNeeds {
+  bool x = false;
+  std::vector<bool> w;
+  bool bias = false, bn_w = false, bn_b = false;
+};
+struct ConvGrads {
+  Tensor dx, dbias, dbn_w, dbn_b;
+  std::vector<Tensor> dW;
+};
+
+// HodgeLaguerreConv / HodgeChebConv forward (+ BN (+ ReLU)) of one side;
+// `slot` = its member in a launch group (BatchNorm workspace).
+Tensor conv_forward(const ConvArgs& c, ConvSaved& sv, int slot) {
+  const Tensor& x = c.x;
+  req(x, "x");
+  const int64_t N = x.size(0);
+  const int64_t Cin = x.size(-1);
+  const int64_t K = (int64_t)c.W.size();
+  Tensor x2 = x.dim() == 2 ? rows2d(x) : x.contiguous().view({N, -1});
+  const int64_t F = x2.size(1);
+  const int64_t M = N * (F / Cin);
+  const int64_t dout = c.W[0].size(0);
+  void* s = stream_of(x);
+  Tensor T = at::empty({std::max<int64_t>(K - 1, 0), N, F}, x.options());
+  // halo tiles describe A; they serve the adjoint only when A^T is A
+  const bool use_halo = has(c.h_lcol) && has(c.h_tile) && has(c.h_ptr) && has(c.h_cols) &&
+                        has(c.h_srp) && has(c.h_hdr);
+  const hlhgat_halo_t halo =
+      use_halo ? make_halo(*c.h_tile, *c.h_ptr, *c.h_cols, *c.h_srp, *c.h_lcol,
+                           has(c.h_sval) ? *c.h_sval : Tensor(), c.h_bounds, *c.h_hdr)
+               : hlhgat_halo_t{};
+  const bool factored = !c.fac.empty();
+  // graph tiles: the graph-local basis on request (HLHGAT_GRAPH_LOCAL=1)
+  const bool local_basis = has(c.tiles) && graph_local_env();
+  if (factored && K > 1 && N > 0) {
+    const hlhgat_hodge_factor_t hf = make_factor(c.fac, c.fac_nodes, N);
+    Tensor work = keep_alive(
+        at::empty({hlhgat_hodge_factor_work_floats(c.fac_nodes, F)}, x.options()));
+    chk(hlhgat_poly_basis_fwd_factored((int)c.kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
+                                       (int)K, T.data_ptr<float>(), work.data_ptr<float>(), s),
+        "poly_basis_fwd_factored");
+  } else if (K > 1 && N > 0) {
+    chk(hlhgat_poly_basis_fwd((int)c.kind, c.a_rowptr.data_ptr<int>(),
+                              c.nnz ? c.a_col.data_ptr<int>() : nullptr,
+                              c.nnz ? fptr(c.a_val) : nullptr, N, c.nnz, iptr(c.a_order),
+                              use_halo ? &halo : nullptr,
+                              local_basis ? iptr(c.tiles) : nullptr,
+                              local_basis ? c.tiles->numel() - 1 : 0, c.tile_rows, c.tile_nnz,
+                              x2.data_ptr<float>(), ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
+        "poly_basis_fwd");
+  }
+  std::vector<const float*> Ap(K), Wp(K);
+  std::vector<int64_t> lda(K), ldw(K), kb(K, Cin);
+  Ap[0] = x2.data_ptr<float>();
+  lda[0] = x.dim() == 2 ? ld_of(x2) : Cin;
+  for (int64_t k = 1; k < K; ++k) {
+    Ap[k] = T.data_ptr<float>() + (k - 1) * N * F;
+    lda[k] = Cin;
+  }
+  for (int64_t k = 0; k < K; ++k) {
+    req(c.W[k], "lins[k].weight");
+    TORCH_CHECK(c.W[k].stride(1) == 1, "hlhgat: weights need unit inner stride");
+    Wp[k] = c.W[k].data_ptr<float>();
+    ldw[k] = c.W[k].stride(0);
+  }
+  // out_buf: caller-owned [M, dout] destination (a column block of the dense
+  // concatenation slab, hlhgat.ops.DenseConcat); the final output lands there
+  const bool sink = has(c.out_buf);
+  if (sink)
+    TORCH_CHECK(c.out_buf->size(0) == M && c.out_buf->size(1) == dout &&
+                    c.out_buf->stride(1) == 1 && c.out_buf->device() == x.device(),
+                "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
+  Tensor pre = (sink && c.bn_mode == 0) ? *c.out_buf : at::empty({M, dout}, x.options());
+  Tensor out = pre, mean, invstd;
+  if (M > 0) {
+    proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(c.bias), pre, s);
+  } else if (has(c.bias)) {
+    pre.copy_(c.bias->expand_as(pre));
+  }
+  if (c.bn_mode > 0) {
+    BnState st{c.bn_w, c.bn_b, c.bn_rm, c.bn_rv, c.bn_nbt, c.momentum, c.eps, c.valid};
+    out = bn_forward(pre, st, c.bn_mode == 2, mean, invstd, sink ? &*c.out_buf : nullptr, slot);
+  }
+  sv.dims = {N, Cin, F, M, dout, K, c.kind, c.nnz, c.bn_mode, has(c.bias) ? 1 : 0};
+  sv.fac_nodes = c.fac_nodes;
+  sv.tile_rows = c.tile_rows;
+  sv.tile_nnz = c.tile_nnz;
+  sv.h_bounds = c.h_bounds;
+  sv.xshape = x.sizes().vec();
+  const bool halo_bwd = use_halo && c.t_rowptr.data_ptr() == c.a_rowptr.data_ptr();
+  sv.t = {x2,
+          T,
+          has(c.t_order) ? *c.t_order : Tensor(),
+          has(c.tiles) ? *c.tiles : Tensor(),
+          has(c.valid) ? *c.valid : Tensor(),
+          c.t_rowptr,
+          c.t_col,
+          has(c.t_val) ? *c.t_val : Tensor(),
+          c.bn_mode > 0 ? pre : Tensor(),
+          c.bn_mode == 2 ? out : Tensor(),
+          mean,
+          invstd,
+          has(c.bn_w) ? *c.bn_w : Tensor(),
+          has(c.bias) ? *c.bias : Tensor(),
+          has(c.bn_b) ? *c.bn_b : Tensor(),
+          halo_bwd ? *c.h_tile : Tensor(),
+          halo_bwd ? *c.h_ptr : Tensor(),
+          halo_bwd ? *c.h_cols : Tensor(),
+          halo_bwd ? *c.h_srp : Tensor(),
+          halo_bwd ? *c.h_lcol : Tensor(),
+          (halo_bwd && has(c.h_sval)) ? *c.h_sval : Tensor(),
+          halo_bwd ? *c.h_hdr : Tensor()};
+  for (const auto& w : c.W) sv.t.push_back(w);
+  for (const auto& t : c.fac) sv.t.push_back(t);
+  std::vector<int64_t> oshape = x.sizes().vec();
+  oshape.back() = dout;
+  return out.view(oshape);
+}
+
+ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds& nd, int slot) {
+  const auto& d = sv.dims;
+  const int64_t N = d[0], Cin = d[1], F = d[2], M = d[3], dout = d[4], K = d[5], kind = d[6],
+                nnz = d[7], bn_mode = d[8];
+  const bool has_bias = d[9] != 0;
+  const auto& t = sv.t;
+  Tensor x2 = t[0], T = t[1], t_order = t[2], tiles = t[3], valid = t[4], t_rowptr = t[5],
+         t_col = t[6], t_val = t[7], pre = t[8], yout = t[9], mean = t[10], invstd = t[11],
+         bn_w = t[12], bias_p = t[13], bn_b = t[14], h_tile = t[15], h_ptr = t[16],
+         h_cols = t[17], h_srp = t[18], h_lcol = t[19], h_sval = t[20], h_hdr = t[21];
+  std::vector<Tensor> W(t.begin() + kSavedFixed, t.begin() + kSavedFixed + K);
+  std::vector<Tensor> fac(t.begin() + kSavedFixed + K, t.end());
+  const bool use_halo = h_lcol.defined();
+  const hlhgat_halo_t halo =
+      use_halo ? make_halo(h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, sv.h_bounds, h_hdr)
+               : hlhgat_halo_t{};
+  void* s = stream_of(x2);
+  // row-strided is fine (e.g. a column block of the gradient slab)
+  Tensor G = keep_alive(rows2d(grad.reshape({M, dout})));
+  ConvGrads out;
+  out.dW.resize(K);
+  std::vector<const float*> Ap(K);
+  std::vector<int64_t> lda(K), kb(K, Cin);
+  Ap[0] = x2.data_ptr<float>();
+  lda[0] = (int64_t)sv.xshape.size() == 2 ? ld_of(x2) : Cin;
+  for (int64_t k = 1; k < K; ++k) {
+    Ap[k] = T.data_ptr<float>() + (k - 1) * N * F;
+    lda[k] = Cin;
+  }
+  bool need_w = false;
+  for (int64_t k = 0; k < K; ++k) need_w = need_w || nd.w[k];
+  const bool need_b = has_bias && nd.bias;
+  struct {
+    std::vector<float*> dWp;
+    std::vector<int64_t> lddw;
+    float* db = nullptr;
+  } wdef;  // weight gradient deferred into the data gradient's launch
+  if (bn_mode > 0) {
+    const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
+    OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
+    G = keep_alive(bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w,
+                               out.dbn_b, nullptr, &bn_b, valid, slot));
+  }
+  if (need_w || need_b) {
+    std::vector<Tensor> dW(K);
+    std::vector<float*> dWp(K);
+    std::vector<int64_t> lddw(K);
+    for (int64_t k = 0; k < K; ++k) {
+      dW[k] = keep_alive(nd.w[k] ? grad_like(W[k]) : at::empty({dout, Cin}, x2.options()));
+      dWp[k] = dW[k].data_ptr<float>();
+      lddw[k] = Cin;
+    }
+    Tensor db = need_b ? grad_like(bias_p) : Tensor();
+    if (M > 0 && nd.x && fused_bwd_flag()) {
+      wdef.dWp = dWp;  // launched with the data gradient
+      wdef.lddw = lddw;
+      wdef.db = need_b ? db.data_ptr<float>() : nullptr;
+    } else if (M > 0) {
+      proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, s);
+    } else {
+      for (auto& tt : dW) tt.zero_();
+      if (need_b) db.zero_();
+    }
+    for (int64_t k = 0; k < K; ++k)
+      if (nd.w[k]) out.dW[k] = dW[k];
+    if (need_b) out.dbias = db;
+  }
+  if (nd.x) {
+    Tensor Gs = keep_alive(at::empty({K, N, F}, x2.options()));
+    if (M > 0) {
+      std::vector<const float*> Wp(K);
+      std::vector<int64_t> ldw(K), ldda(K, Cin);
+      std::vector<float*> dA(K);
+      for (int64_t k = 0; k < K; ++k) {
+        Wp[k] = W[k].data_ptr<float>();
+        ldw[k] = W[k].stride(0);
+        dA[k] = Gs.data_ptr<float>() + k * N * F;
+      }
+      if (!wdef.dWp.empty())
+        proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s);
+      else
+        proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
+      if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
+        const hlhgat_hodge_factor_t hf = make_factor(fac, sv.fac_nodes, N);
+        Tensor work = keep_alive(
+            at::empty({hlhgat_hodge_factor_work_floats(sv.fac_nodes, F)}, x2.options()));
+        chk(hlhgat_poly_basis_bwd_factored((int)kind, &hf, F, (int)K, Gs.data_ptr<float>(),
+                                           work.data_ptr<float>(), s),
+            "poly_basis_bwd_factored");
+      } else if (K > 1) {
+        const bool loc = tiles.defined() && graph_local_env();
+        chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
+                                  nnz ? t_col.data_ptr<int>() : nullptr,
+                                  (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr, N,
+                                  nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
+                                  use_halo ? &halo : nullptr, loc ? tiles.data_ptr<int>() : nullptr,
+                                  loc ? tiles.numel() - 1 : 0, sv.tile_rows, sv.tile_nnz, F,
+                                  (int)K, Gs.data_ptr<float>(), s),
+            "poly_basis_bwd");
+      }
+    } else {
+      Gs.zero_();
+    }
+    out.dx = Gs[0].view(sv.xshape);
+  }
+  return out;
+}
+
+// argument positions of conv_bn (needs_input_grad / gradient slots)
+constexpr int64_t kConvPosW = 9;  // W[0..K), then bias, bn_w, bn_b
+
+ConvNeeds conv_needs(AutogradContext* ctx, int64_t K, int64_t base) {
+  ConvNeeds nd;
+  nd.x = need(ctx, base);
+  nd.w.resize(K);
+  for (int64_t k = 0; k < K; ++k) nd.w[k] = need(ctx, base + kConvPosW + k);
+  nd.bias = need(ctx, base + kConvPosW + K);
+  nd.bn_w = need(ctx, base + kConvPosW + K + 1);
+  nd.bn_b = need(ctx, base + kConvPosW + K + 2);
+  return nd;
+}
+
+void edge_map_conv(EdgeMap& em, const ConvArgs& c) {
+  em.tensor();  // x
+  em.tensor();
+  em.tensor();
+  em.opt(c.a_val);
+  em.tensor();
+  em.tensor();
+  em.opt(c.t_val);
+  em.other();
+  em.other();
+  em.list(c.W);
+  em.opt(c.bias);
+  em.opt(c.bn_w);
+  em.opt(c.bn_b);
+  em.opt(c.bn_rm);
+  em.opt(c.bn_rv);
+  em.opt(c.bn_nbt);
+  em.other();
+  em.other();
+  em.other();
+  em.opt(c.out_buf);
+  em.opt(c.a_order);
+  em.opt(c.t_order);
+  em.opt(c.tiles);
+  em.other();
+  em.other();
+  em.opt(c.valid);
+  em.opt(c.h_tile);
+  em.opt(c.h_ptr);
+  em.opt(c.h_cols);
+  em.opt(c.h_srp);
+  em.opt(c.h_lcol);
+  em.opt(c.h_sval);
+  em.other();
+  em.opt(c.h_hdr);
+  em.list(c.fac);
+  em.other();
+}
+constexpr int64_t conv_positions(int64_t K, int64_t n_fac) { return 33 + K + n_fac + 1; }
+
+void put_grads(variable_list& out, int64_t base, int64_t K, const ConvGrads& g) {
+  out[base] = g.dx;
+  for (int64_t k = 0; k < K; ++k) out[base + kConvPosW + k] = g.dW[k];
+  out[base + kConvPosW + K] = g.dbias;
+  out[base + kConvPosW + K + 1] = g.dbn_w;
+  out[base + kConvPosW + K + 2] = g.dbn_b;
+}
+
 class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
  public:
   // x: [N, C] or [N, T, C]; A/At: CSR of L and L^T; W: K weights [dout, C]
@@ -349,274 +780,187 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol,
                         OptT h_sval, std::vector<int64_t> h_bounds, OptT h_hdr,
                         at::TensorList fac, int64_t fac_nodes) {
-    req(x, "x");
-    const int64_t N = x.size(0);
-    const int64_t Cin = x.size(-1);
-    const int64_t K = (int64_t)W.size();
-    Tensor x2 = x.dim() == 2 ? rows2d(x) : x.contiguous().view({N, -1});
-    const int64_t F = x2.size(1);
-    const int64_t M = N * (F / Cin);
-    const int64_t dout = W[0].size(0);
-    void* s = stream_of(x);
-    Tensor T = at::empty({std::max<int64_t>(K - 1, 0), N, F}, x.options());
-    // halo tiles describe A; they serve the adjoint only when A^T is A
-    const bool use_halo =
-        has(h_lcol) && has(h_tile) && has(h_ptr) && has(h_cols) && has(h_srp) && has(h_hdr);
-    const hlhgat_halo_t halo =
-        use_halo ? make_halo(*h_tile, *h_ptr, *h_cols, *h_srp, *h_lcol,
-                             has(h_sval) ? *h_sval : Tensor(), h_bounds, *h_hdr)
-                 : hlhgat_halo_t{};
-    const bool factored = !fac.empty();
-    // graph tiles: the graph-local basis on request (HLHGAT_GRAPH_LOCAL=1)
-    const bool local_basis = has(tiles) && graph_local_env();
-    if (factored && K > 1 && N > 0) {
-      const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
-      Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x.options());
-      chk(hlhgat_poly_basis_fwd_factored((int)kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
-                                         (int)K, T.data_ptr<float>(), work.data_ptr<float>(), s),
-          "poly_basis_fwd_factored");
-    } else if (K > 1 && N > 0) {
-      chk(hlhgat_poly_basis_fwd((int)kind, a_rowptr.data_ptr<int>(),
-                                nnz ? a_col.data_ptr<int>() : nullptr,
-                                nnz ? fptr(a_val) : nullptr, N, nnz, iptr(a_order),
-                                use_halo ? &halo : nullptr,
-                                local_basis ? iptr(tiles) : nullptr,
-                                local_basis ? tiles->numel() - 1 : 0, tile_rows,
-                                tile_nnz, x2.data_ptr<float>(),
-                                ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
-          "poly_basis_fwd");
-    }
-    std::vector<const float*> Ap(K), Wp(K);
-    std::vector<int64_t> lda(K), ldw(K), kb(K, Cin);
-    Ap[0] = x2.data_ptr<float>();
-    lda[0] = x.dim() == 2 ? ld_of(x2) : Cin;
-    for (int64_t k = 1; k < K; ++k) {
-      Ap[k] = T.data_ptr<float>() + (k - 1) * N * F;
-      lda[k] = Cin;
-    }
-    for (int64_t k = 0; k < K; ++k) {
-      req(W[k], "lins[k].weight");
-      TORCH_CHECK(W[k].stride(1) == 1, "hlhgat: weights need unit inner stride");
-      Wp[k] = W[k].data_ptr<float>();
-      ldw[k] = W[k].stride(0);
-    }
-    // out_buf: caller-owned [M, dout] destination (a column block of the dense
-    // concatenation slab, hlhgat.ops.DenseConcat); the final output lands there
-    const bool sink = has(out_buf);
-    if (sink)
-      TORCH_CHECK(out_buf->size(0) == M && out_buf->size(1) == dout && out_buf->stride(1) == 1 &&
-                      out_buf->device() == x.device(),
-                  "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
-    Tensor pre = (sink && bn_mode == 0) ? *out_buf : at::empty({M, dout}, x.options());
-    Tensor out = pre, mean, invstd;
-    {
-      if (M > 0) {
-        proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(bias), pre, s);
-      } else if (has(bias)) {
-        pre.copy_(bias->expand_as(pre));
-      }
-      if (bn_mode > 0) {
-        BnState st{bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, valid};
-        out = bn_forward(pre, st, bn_mode == 2, mean, invstd, sink ? &*out_buf : nullptr);
-      }
-    }
-    ctx->saved_data["dims"] = std::vector<int64_t>{N, Cin, F, M, dout, K, kind, nnz, bn_mode,
-                                                   has(bias) ? 1 : 0};
-    {
-      EdgeMap em;
-      em.tensor();  // x
-      em.tensor();
-      em.tensor();
-      em.opt(a_val);
-      em.tensor();
-      em.tensor();
-      em.opt(t_val);
-      em.other();
-      em.other();
-      em.list(W);
-      em.opt(bias);
-      em.opt(bn_w);
-      em.opt(bn_b);
-      em.opt(bn_rm);
-      em.opt(bn_rv);
-      em.opt(bn_nbt);
-      em.other();
-      em.other();
-      em.other();
-      em.opt(out_buf);
-      em.opt(a_order);
-      em.opt(t_order);
-      em.opt(tiles);
-      em.other();
-      em.other();
-      em.opt(valid);
-      em.opt(h_tile);
-      em.opt(h_ptr);
-      em.opt(h_cols);
-      em.opt(h_srp);
-      em.opt(h_lcol);
-      em.opt(h_sval);
-      em.other();
-      em.opt(h_hdr);
-      em.list(fac);
-      em.other();
-      ctx->saved_data["edges"] = em.e;
-      ctx->saved_data["fac_nodes"] = fac_nodes;
-      ctx->saved_data["tile_rows"] = tile_rows;
-      ctx->saved_data["tile_nnz"] = tile_nnz;
-      ctx->saved_data["h_bounds"] = h_bounds;
-    }
-    const bool halo_bwd = use_halo && t_rowptr.data_ptr() == a_rowptr.data_ptr();
-    ctx->saved_data["xshape"] = x.sizes().vec();
-    std::vector<Tensor> save = {x2,
-                                T,
-                                has(t_order) ? *t_order : Tensor(),
-                                has(tiles) ? *tiles : Tensor(),
-                                has(valid) ? *valid : Tensor(),
-                                t_rowptr,
-                                t_col,
-                                has(t_val) ? *t_val : Tensor(),
-                                bn_mode > 0 ? pre : Tensor(),
-                                bn_mode == 2 ? out : Tensor(),
-                                mean,
-                                invstd,
-                                has(bn_w) ? *bn_w : Tensor(),
-                                has(bias) ? *bias : Tensor(),
-                                has(bn_b) ? *bn_b : Tensor(),
-                                halo_bwd ? *h_tile : Tensor(),
-                                halo_bwd ? *h_ptr : Tensor(),
-                                halo_bwd ? *h_cols : Tensor(),
-                                halo_bwd ? *h_srp : Tensor(),
-                                halo_bwd ? *h_lcol : Tensor(),
-                                (halo_bwd && has(h_sval)) ? *h_sval : Tensor(),
-                                halo_bwd ? *h_hdr : Tensor()};
-    for (const auto& w : W) save.push_back(w);
-    for (const auto& t : fac) save.push_back(t);
-    ctx->save_for_backward(save);
-    std::vector<int64_t> oshape = x.sizes().vec();
-    oshape.back() = dout;
-    return out.view(oshape);
+    ConvArgs c{x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind, W.vec(), bias,
+               bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode, out_buf, a_order,
+               t_order, tiles, tile_rows, tile_nnz, valid, h_tile, h_ptr, h_cols, h_srp,
+               h_lcol, h_sval, h_bounds, h_hdr, fac.vec(), fac_nodes};
+    ConvSaved sv;
+    Tensor y = conv_forward(c, sv, 0);
+    EdgeMap em;
+    edge_map_conv(em, c);
+    ctx->saved_data["edges"] = em.e;
+    sv.to_ctx(ctx, "");
+    ctx->save_for_backward(sv.t);
+    return y;
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    auto d = ctx->saved_data["dims"].toIntVector();
-    const int64_t N = d[0], Cin = d[1], F = d[2], M = d[3], dout = d[4], K = d[5], kind = d[6],
-                  nnz = d[7], bn_mode = d[8];
-    const bool has_bias = d[9] != 0;
-    auto xshape = ctx->saved_data["xshape"].toIntVector();
-    auto sv = ctx->get_saved_variables();
-    Tensor x2 = sv[0], T = sv[1], t_order = sv[2], tiles = sv[3], valid = sv[4],
-           t_rowptr = sv[5], t_col = sv[6], t_val = sv[7], pre = sv[8], yout = sv[9],
-           mean = sv[10], invstd = sv[11], bn_w = sv[12], bias_p = sv[13], bn_b = sv[14],
-           h_tile = sv[15], h_ptr = sv[16], h_cols = sv[17], h_srp = sv[18], h_lcol = sv[19],
-           h_sval = sv[20], h_hdr = sv[21];
-    std::vector<Tensor> W(sv.begin() + 22, sv.begin() + 22 + K);
-    std::vector<Tensor> fac(sv.begin() + 22 + K, sv.end());
-    const int64_t fac_nodes = ctx->saved_data["fac_nodes"].toInt();
-    const bool use_halo = h_lcol.defined();
-    const hlhgat_halo_t halo =
-        use_halo ? make_halo(h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval,
-                             ctx->saved_data["h_bounds"].toIntVector(), h_hdr)
-                 : hlhgat_halo_t{};
-    const int64_t tile_rows = ctx->saved_data["tile_rows"].toInt();
-    const int64_t tile_nnz = ctx->saved_data["tile_nnz"].toInt();
-    void* s = stream_of(x2);
-    Tensor G = grads[0].reshape({M, dout});
-    G = rows2d(G);  // row-strided is fine (e.g. a column block of the gradient slab)
-    // positions: x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
-    //            W[0..K), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode
-    const int64_t n_pos = 33 + K + (int64_t)fac.size() + 1;
-    variable_list out(n_pos);
-    const bool need_x = need(ctx, 0);
-    std::vector<const float*> Ap(K);
-    std::vector<int64_t> lda(K), kb(K, Cin);
-    Ap[0] = x2.data_ptr<float>();
-    lda[0] = (int64_t)xshape.size() == 2 ? ld_of(x2) : Cin;
-    for (int64_t k = 1; k < K; ++k) {
-      Ap[k] = T.data_ptr<float>() + (k - 1) * N * F;
-      lda[k] = Cin;
+    ConvSaved sv = ConvSaved::from_ctx(ctx, "", ctx->get_saved_variables(), 0);
+    const int64_t K = sv.dims[5];
+    const int64_t n_fac = (int64_t)sv.t.size() - (int64_t)kSavedFixed - K;
+    variable_list out(conv_positions(K, n_fac));
+    put_grads(out, 0, K, conv_backward(sv, grads[0], conv_needs(ctx, K, 0), 0));
+    return out;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// The node (L0) and edge (L1) conv (+ BN (+ ReLU)) of one HL block as ONE
+// autograd node whose launches run as pairs (hlhgat_group_*): the i-th launch
+// of the node side and of the edge side -- polynomial step, projection,
+// BatchNorm, Linear backward, split reduction -- share one grid, instead of
+// two concurrent streams of half-size launches (lib/Hodge_ST_Model.py:556-566).
+// Each side's arithmetic is that of conv_bn: bitwise the same results.
+// ---------------------------------------------------------------------------
+ConvArgs conv_args_from(const Tensor& x, at::TensorList W, const OptT& bias, const OptT& bn_w,
+                        const OptT& bn_b, const std::vector<OptT>& aux,
+                        const std::vector<int64_t>& ints, const std::vector<double>& dbl,
+                        const std::vector<int64_t>& h_bounds, at::TensorList fac) {
+  // aux: a_rowptr a_col a_val t_rowptr t_col t_val bn_rm bn_rv bn_nbt out_buf a_order
+  //      t_order tiles valid h_tile h_ptr h_cols h_srp h_lcol h_sval h_hdr
+  // ints: nnz kind bn_mode tile_rows tile_nnz fac_nodes ; dbl: momentum eps
+  TORCH_CHECK(aux.size() == 21 && ints.size() == 6 && dbl.size() == 2,
+              "hlhgat: conv_bn_pair: bad side descriptor");
+  ConvArgs c;
+  c.x = x;
+  c.a_rowptr = *aux[0];
+  c.a_col = *aux[1];
+  c.a_val = aux[2];
+  c.t_rowptr = *aux[3];
+  c.t_col = *aux[4];
+  c.t_val = aux[5];
+  c.bn_rm = aux[6];
+  c.bn_rv = aux[7];
+  c.bn_nbt = aux[8];
+  c.out_buf = aux[9];
+  c.a_order = aux[10];
+  c.t_order = aux[11];
+  c.tiles = aux[12];
+  c.valid = aux[13];
+  c.h_tile = aux[14];
+  c.h_ptr = aux[15];
+  c.h_cols = aux[16];
+  c.h_srp = aux[17];
+  c.h_lcol = aux[18];
+  c.h_sval = aux[19];
+  c.h_hdr = aux[20];
+  c.nnz = ints[0];
+  c.kind = ints[1];
+  c.bn_mode = ints[2];
+  c.tile_rows = ints[3];
+  c.tile_nnz = ints[4];
+  c.fac_nodes = ints[5];
+  c.momentum = dbl[0];
+  c.eps = dbl[1];
+  c.W = W.vec();
+  c.bias = bias;
+  c.bn_w = bn_w;
+  c.bn_b = bn_b;
+  c.h_bounds = h_bounds;
+  c.fac = fac.vec();
+  return c;
+}
+
+// Positions: side s's x, W (a list), bias, bn_w, bn_b at s*5 + 0..4; the rest
+// carries no gradient.
+class ConvBNPairFn : public torch::autograd::Function<ConvBNPairFn> {
+ public:
+  static variable_list forward(AutogradContext* ctx, Tensor x0, at::TensorList W0, OptT bias0,
+                               OptT bnw0, OptT bnb0, Tensor x1, at::TensorList W1, OptT bias1,
+                               OptT bnw1, OptT bnb1, std::vector<OptT> aux0,
+                               std::vector<OptT> aux1, std::vector<int64_t> ints0,
+                               std::vector<int64_t> ints1, std::vector<double> dbl0,
+                               std::vector<double> dbl1, std::vector<int64_t> hb0,
+                               std::vector<int64_t> hb1, at::TensorList fac0,
+                               at::TensorList fac1) {
+    TORCH_CHECK(x0.device() == x1.device(), "hlhgat: conv_bn_pair: sides on different devices");
+    ConvArgs c0 = conv_args_from(x0, W0, bias0, bnw0, bnb0, aux0, ints0, dbl0, hb0, fac0);
+    ConvArgs c1 = conv_args_from(x1, W1, bias1, bnw1, bnb1, aux1, ints1, dbl1, hb1, fac1);
+    ConvSaved s0, s1;
+    Tensor y0, y1;
+    {
+      LaunchGroup g;
+      g.begin();
+      y0 = conv_forward(c0, s0, 0);
+      g.next();
+      y1 = conv_forward(c1, s1, 1);
+      ctx->saved_data["paired_fwd"] = (int64_t)g.end(stream_of(x0));
     }
-    bool need_w = false;
-    for (int64_t k = 0; k < K; ++k) need_w = need_w || need(ctx, 9 + k);
-    const bool need_b = has_bias && need(ctx, 9 + K);
-    struct {
-      std::vector<float*> dWp;
-      std::vector<int64_t> lddw;
-      float* db = nullptr;
-      std::vector<Tensor> keep;  // the dW buffers stay allocated until the launch
-    } wdef;  // weight gradient deferred into the data gradient's launch
-    Tensor dbn_w, dbn_b;
-    const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
-    if (bn_mode > 0) {
-      OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-      G = bn_backward(pre, bn_y, G, w, mean, invstd, need(ctx, 10 + K), need(ctx, 11 + K),
-                      dbn_w, dbn_b, nullptr, &bn_b, valid);
-      out[10 + K] = dbn_w;
-      out[11 + K] = dbn_b;
+    // needs_input_grad indexes: x0, W0..., [bias0], [bnw0], [bnb0], x1, W1..., ...
+    std::vector<int64_t> e;
+    int64_t n = 0;
+    auto side = [&](const ConvArgs& c) {
+      e.push_back(n++);
+      e.push_back(n);
+      n += (int64_t)c.W.size();
+      e.push_back(has(c.bias) ? n++ : -1);
+      e.push_back(has(c.bn_w) ? n++ : -1);
+      e.push_back(has(c.bn_b) ? n++ : -1);
+    };
+    side(c0);
+    side(c1);
+    ctx->saved_data["pair_edges"] = e;
+    s0.to_ctx(ctx, "0");
+    s1.to_ctx(ctx, "1");
+    std::vector<Tensor> all = s0.t;
+    all.insert(all.end(), s1.t.begin(), s1.t.end());
+    ctx->save_for_backward(all);
+    return {y0, y1};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const auto all = ctx->get_saved_variables();
+    ConvSaved s0 = ConvSaved::from_ctx(ctx, "0", all, 0);
+    ConvSaved s1 = ConvSaved::from_ctx(ctx, "1", all, s0.t.size());
+    const auto e = ctx->saved_data["pair_edges"].toIntVector();
+    auto needs = [&](int side, int64_t K) {
+      const int64_t* q = e.data() + 5 * side;
+      auto nig = [&](int64_t idx) { return idx >= 0 && ctx->needs_input_grad(idx); };
+      ConvNeeds nd;
+      nd.x = nig(q[0]);
+      nd.w.resize(K);
+      for (int64_t k = 0; k < K; ++k) nd.w[k] = nig(q[1] + k);
+      nd.bias = nig(q[2]);
+      nd.bn_w = nig(q[3]);
+      nd.bn_b = nig(q[4]);
+      return nd;
+    };
+    const int64_t K0 = s0.dims[5], K1 = s1.dims[5];
+    ConvGrads g0, g1;
+    Tensor gy0 = grads[0], gy1 = grads[1];
+    if (!grads[0].defined()) {
+      std::vector<int64_t> os = s0.xshape;
+      os.back() = s0.dims[4];
+      gy0 = at::zeros(os, s0.t[0].options());
     }
-    if (need_w || need_b) {
-      std::vector<Tensor> dW(K);
-      std::vector<float*> dWp(K);
-      std::vector<int64_t> lddw(K);
-      for (int64_t k = 0; k < K; ++k) {
-        dW[k] = need(ctx, 9 + k) ? grad_like(W[k]) : at::empty({dout, Cin}, x2.options());
-        dWp[k] = dW[k].data_ptr<float>();
-        lddw[k] = Cin;
-      }
-      Tensor db = need_b ? grad_like(bias_p) : Tensor();
-      if (M > 0 && need_x && fused_bwd_flag()) {
-        wdef.dWp = dWp;  // launched with the data gradient
-        wdef.lddw = lddw;
-        wdef.db = need_b ? db.data_ptr<float>() : nullptr;
-        wdef.keep = dW;
-      } else if (M > 0) {
-        proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, s);
-      } else {
-        for (auto& t : dW) t.zero_();
-        if (need_b) db.zero_();
-      }
-      for (int64_t k = 0; k < K; ++k)
-        if (need(ctx, 9 + k)) out[9 + k] = dW[k];
-      if (need_b) out[9 + K] = db;
+    if (!grads[1].defined()) {
+      std::vector<int64_t> os = s1.xshape;
+      os.back() = s1.dims[4];
+      gy1 = at::zeros(os, s1.t[0].options());
     }
-    if (need_x) {
-      Tensor Gs = at::empty({K, N, F}, x2.options());
-      if (M > 0) {
-        std::vector<const float*> Wp(K);
-        std::vector<int64_t> ldw(K), ldda(K, Cin);
-        std::vector<float*> dA(K);
-        for (int64_t k = 0; k < K; ++k) {
-          Wp[k] = W[k].data_ptr<float>();
-          ldw[k] = W[k].stride(0);
-          dA[k] = Gs.data_ptr<float>() + k * N * F;
-        }
-        if (!wdef.dWp.empty())
-          proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s);
-        else
-          proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
-        if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
-          const hlhgat_hodge_factor_t hf = make_factor(fac, fac_nodes, N);
-          Tensor work = at::empty({hlhgat_hodge_factor_work_floats(fac_nodes, F)}, x2.options());
-          chk(hlhgat_poly_basis_bwd_factored((int)kind, &hf, F, (int)K, Gs.data_ptr<float>(),
-                                             work.data_ptr<float>(), s),
-              "poly_basis_bwd_factored");
-        } else if (K > 1) {
-          chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
-                                    nnz ? t_col.data_ptr<int>() : nullptr,
-                                    (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
-                                    N, nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
-                                    use_halo ? &halo : nullptr,
-                                    (tiles.defined() && graph_local_env())
-                                        ? tiles.data_ptr<int>() : nullptr,
-                                    (tiles.defined() && graph_local_env()) ? tiles.numel() - 1 : 0,
-                                    tile_rows, tile_nnz, F, (int)K, Gs.data_ptr<float>(), s),
-              "poly_basis_bwd");
-        }
-      } else {
-        Gs.zero_();
-      }
-      out[0] = Gs[0].view(xshape);
+    {
+      LaunchGroup g;
+      g.begin();
+      g0 = conv_backward(s0, gy0, needs(0, K0), 0);
+      g.next();
+      g1 = conv_backward(s1, gy1, needs(1, K1), 1);
+      g.end(stream_of(s0.t[0]));
     }
+    // one gradient slot per forward argument, TensorList elements one each:
+    // x0 W0.. bias0 bnw0 bnb0 x1 W1.. bias1 bnw1 bnb1, 8 descriptor
+    // arguments, the factor tensors of both sides
+    variable_list out;
+    auto push_side = [&](const ConvGrads& g, int64_t K) {
+      out.push_back(g.dx);
+      for (int64_t k = 0; k < K; ++k) out.push_back(g.dW[k]);
+      out.push_back(g.dbias);
+      out.push_back(g.dbn_w);
+      out.push_back(g.dbn_b);
+    };
+    push_side(g0, K0);
+    push_side(g1, K1);
+    const size_t n_fac = (s0.t.size() - kSavedFixed - K0) + (s1.t.size() - kSavedFixed - K1);
+    out.resize(out.size() + 8 + n_fac);
     return out;
   }
 };
@@ -987,53 +1331,6 @@ class EdgeFromNodesFn : public torch::autograd::Function<EdgeFromNodesFn> {
 // then BN -> ReLU -> Linear -> BN -> ReLU per side as in the reference.
 // Same fp32 arithmetic up to summation order (1e-5 relative, tests).
 // ---------------------------------------------------------------------------
-// Two-stream fork inside one autograd node: the node (current) stream and a
-// persistent side stream per device, ordered by hipEvents (captured into a
-// hipGraph as branch dependencies).  Tensors allocated while the side stream
-// is current and then used on the node stream are record_stream()-ed.
-// (PyTorch-ROCm exposes HIP streams to torch as "cuda" streams: the
-// MasqueradingAsCUDA wrappers are the ones its allocator and guards accept.)
-using TStream = c10::hip::HIPStreamMasqueradingAsCUDA;
-using TStreamGuard = c10::hip::HIPStreamGuardMasqueradingAsCUDA;
-struct Fork {
-  TStream main, side;
-  explicit Fork(int dev)
-      : main(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)dev)),
-        side(side_of(dev)) {}
-  static std::unordered_map<int, TStream>& registry() {
-    static auto* streams = new std::unordered_map<int, TStream>();
-    return *streams;
-  }
-  static TStream side_of(int dev) {
-    auto& streams = registry();
-    auto it = streams.find(dev);
-    if (it == streams.end())
-      it = streams.emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
-                                    false, (c10::DeviceIndex)dev)).first;
-    return it->second;
-  }
-  static hipEvent_t next_event() {
-    static thread_local std::vector<hipEvent_t> pool;
-    static thread_local size_t k = 0;
-    if (pool.empty()) {
-      pool.resize(64);
-      for (auto& e : pool) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == 0);
-    }
-    return pool[k++ % pool.size()];
-  }
-  static void order(const TStream& from, const TStream& to) {
-    hipEvent_t e = next_event();
-    TORCH_CHECK(hipEventRecord(e, from.stream()) == hipSuccess, "hlhgat: hipEventRecord");
-    TORCH_CHECK(hipStreamWaitEvent(to.stream(), e, 0) == hipSuccess, "hlhgat: hipStreamWaitEvent");
-  }
-  void side_waits_main() { order(main, side); }
-  void main_waits_side() { order(side, main); }
-  void escape(std::initializer_list<Tensor> ts) {
-    for (const auto& t : ts)
-      if (t.defined()) t.record_stream(main);
-  }
-};
-
 // Rejoin every side stream that joined the capture of the current stream
 // (hlhgat.train.TrainStep calls this as the last captured operation): a
 // stream forked from the capture stream -- e.g. inside an autograd backward
@@ -1349,6 +1646,20 @@ Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_row
                          bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz,
                          valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds,
                          h_hdr, at::TensorList(fac), fac_nodes);
+}
+
+std::vector<Tensor> conv_bn_pair(Tensor x0, std::vector<Tensor> W0, OptT bias0, OptT bnw0,
+                                 OptT bnb0, Tensor x1, std::vector<Tensor> W1, OptT bias1,
+                                 OptT bnw1, OptT bnb1, std::vector<OptT> aux0,
+                                 std::vector<OptT> aux1, std::vector<int64_t> ints0,
+                                 std::vector<int64_t> ints1, std::vector<double> dbl0,
+                                 std::vector<double> dbl1, std::vector<int64_t> hb0,
+                                 std::vector<int64_t> hb1, std::vector<Tensor> fac0,
+                                 std::vector<Tensor> fac1) {
+  auto r = ConvBNPairFn::apply(x0, at::TensorList(W0), bias0, bnw0, bnb0, x1, at::TensorList(W1),
+                               bias1, bnw1, bnb1, aux0, aux1, ints0, ints1, dbl0, dbl1, hb0, hb1,
+                               at::TensorList(fac0), at::TensorList(fac1));
+  return {r[0], r[1]};
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,
@@ -1825,6 +2136,7 @@ Tensor segment_mean_ad(const Tensor& x, const Tensor& seg_ptr, const OptT& seg_r
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
+  m.def("conv_bn_pair", &conv_bn_pair);
   m.def("set_fused_bwd", &set_fused_bwd);
   m.def("join_capture_streams", &join_capture_streams);
   m.def("stream_capturing", &stream_capturing);

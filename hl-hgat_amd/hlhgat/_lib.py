@@ -94,6 +94,10 @@ SIGNATURES = {
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                     c_vp]),
+    "hlhgat_group_begin": (c_i32, []),
+    "hlhgat_group_next": (c_i32, []),
+    "hlhgat_group_end": (c_i32, [c_vp, c_vp]),
+    "hlhgat_group_abort": (c_i32, []),
     "hlhgat_bn_sums_len": (c_i64, [c_i64]),
     "hlhgat_bn_sums_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
                                    c_i64, c_vp]),

@@ -738,6 +738,43 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
     return y
 
 
+PAIR_CONV = os.environ.get("HLHGAT_PAIR_CONV", "0") == "1"
+
+
+def conv_pair_spec(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.Tensor],
+                   bias: Optional[torch.Tensor], kind: int, bn: Optional[torch.nn.BatchNorm1d],
+                   relu: bool, out: Optional[torch.Tensor] = None):
+    """One side of hodge_poly_conv_pair (the arguments hodge_poly_conv would
+    hand the fused conv -> BN (-> ReLU) node), or None when that side does not
+    take the fused path (no BN, running statistics, SyncBatchNorm, 3-D x)."""
+    if (not PAIR_CONV or bn is None or not x.is_cuda or x.dim() != 2
+            or not _bn_uses_batch_stats(bn) or sync_bn_group(bn) is not None
+            or x.size(0) != op.fwd.n_rows or x.size(0) < 2):
+        return None
+    A, At = op.fwd, op.bwd
+    w, b, rm, rv, nbt, mom, eps = _bn_args(bn)
+    h = _halo_args(A)
+    fac, fac_nodes = _factor_args(op)
+    aux = [A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, rm, rv, nbt, out, A.order,
+           At.order, A.tiles, A.valid, h[0], h[1], h[2], h[3], h[4], h[5], h[7]]
+    ints = [A.nnz, int(kind), 2 if relu else 1, A.tile_rows, A.tile_nnz, fac_nodes]
+    return (x, list(weights), bias, w, b, aux, ints, [float(mom), float(eps)], list(h[6]), fac)
+
+
+def hodge_poly_conv_pair(s0, s1):
+    """Two independent hodge_poly_conv(..., bn, relu) calls -- the node (L0)
+    and edge (L1) convs of one HL block (lib/Hodge_ST_Model.py:556-566) -- as
+    ONE C++ autograd node whose launches run as pairs (hlhgat_group_*: each
+    polynomial step, projection, BatchNorm and Linear-backward launch covers
+    both sides).  s0, s1 from conv_pair_spec; returns (y0, y1), bitwise the
+    two single calls' results."""
+    x0, W0, b0, bw0, bb0, aux0, i0, d0, hb0, f0 = s0
+    x1, W1, b1, bw1, bb1, aux1, i1, d1, hb1, f1 = s1
+    y0, y1 = _ext.conv_bn_pair(x0, W0, b0, bw0, bb0, x1, W1, b1, bw1, bb1, aux0, aux1, i0, i1,
+                               d0, d1, hb0, hb1, f0, f1)
+    return y0, y1
+
+
 # ----------------------------------------------------------------------------
 # Dense concatenation of the HL blocks in one slab
 # ----------------------------------------------------------------------------

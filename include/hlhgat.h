@@ -496,6 +496,29 @@ int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float* y, int64_
                              const float* save_invstd, const double* gathered, int world,
                              float* dx, int64_t lddx, void* stream);
 
+/* ---- launch groups (node / edge sides of an HL block in one launch) ----- */
+/* Every HL block runs the same layer on L0 (nodes) and L1 (edges)
+ * (lib/Hodge_ST_Model.py:556-566: HodgeLaguerreConv -> BatchNorm -> ReLU per
+ * side; lib/Hodge_Cheb_Conv.py:276-289: the WV_Node / WV_Edge MLPs).  Between
+ * hlhgat_group_begin() and hlhgat_group_end() the calls of this thread do not
+ * launch: the launches of the calls made before hlhgat_group_next() form
+ * member 0 (e.g. the node side), those after it member 1 (the edge side).
+ * hlhgat_group_end issues them on `stream`: the i-th launch of each member
+ * together as ONE launch when both are the same kernel and it has a pair
+ * variant (polynomial step, projection forward / backward, split
+ * reduction, BatchNorm kernels; a grid-barrier BatchNorm pair only when the
+ * joint grid is co-resident), otherwise one after the other; each member's
+ * launches keep their order.  Results are bitwise those of the ungrouped
+ * calls.  Rules: the two members must be independent; buffers the recorded
+ * calls use must stay allocated until hlhgat_group_end; the BatchNorm
+ * workspaces of the two members must differ; calls that cannot be deferred
+ * fail with HLHGAT_EINVAL inside a group.  *paired (may be NULL) receives the
+ * number of pair launches.  hlhgat_group_abort drops a group (error paths). */
+int hlhgat_group_begin(void);
+int hlhgat_group_next(void);
+int hlhgat_group_end(void* stream, int* paired);
+int hlhgat_group_abort(void);
+
 /* ---- workspaces --------------------------------------------------------- */
 /* Zero `bytes` (a multiple of 4) at p with a kernel on `stream` (graph-capture
  * safe; used to initialise the BatchNorm workspace counters). */
