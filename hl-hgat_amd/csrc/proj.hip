@@ -1297,7 +1297,7 @@ namespace {
 int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w, const float* const* A, const int64_t* lda,
                   const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
                   int nb_d, const float* const* W, const int64_t* ldw, const int64_t* kb_d,
-                  float* const* dA, const int64_t* ldda, float* workspace,
+                  float* const* dA, const int64_t* ldda, int accumulate_d, float* workspace,
                   int64_t workspace_floats, void* stream) {
   HLH_CHECK_ARG(nb_w >= 0 && nb_w <= MAXB && nb_d >= 0 && nb_d <= MAXB,
                 "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
@@ -1319,8 +1319,8 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
                                             0, workspace, workspace_floats, stream);
       if (rc != HLHGAT_OK) return rc;
     }
-    if (want_d) return hlhgat_proj_bwd_data(nb_d, dC, lddc, W, ldw, kb_d, M, N, dA, ldda, 0,
-                                            stream);
+    if (want_d) return hlhgat_proj_bwd_data(nb_d, dC, lddc, W, ldw, kb_d, M, N, dA, ldda,
+                                            accumulate_d, stream);
     return HLHGAT_OK;
   }
   BwdFusedArgs f{};
@@ -1363,7 +1363,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   d.N = (int)N;
   d.G = dC;
   d.ldg = lddc;
-  d.accumulate = 0;
+  d.accumulate = accumulate_d;
   int64_t ktot = 0;
   for (int b = 0; b < nb_d; ++b) ktot += kb_d[b];
   int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // as hlhgat_proj_bwd_data
@@ -1422,8 +1422,9 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
                                const int64_t* kb_w, float* const* dW, const int64_t* lddw,
                                float* dbias, int nb_d, const float* const* W,
                                const int64_t* ldw, const int64_t* kb_d, float* const* dA,
-                               const int64_t* ldda, float* workspace, int64_t workspace_floats,
-                               void* stream) {
+                               const int64_t* ldda, int accumulate_d, float* workspace,
+                               int64_t workspace_floats, void* stream) {
   return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias,
-                       nb_d, W, ldw, kb_d, dA, ldda, workspace, workspace_floats, stream);
+                       nb_d, W, ldw, kb_d, dA, ldda, accumulate_d, workspace, workspace_floats,
+                       stream);
 }

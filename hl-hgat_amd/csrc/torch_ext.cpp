@@ -296,7 +296,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
                    std::vector<float*>& dW, const std::vector<int64_t>& lddw, float* db,
                    const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
                    const std::vector<int64_t>& kbd, std::vector<float*>& dA,
-                   const std::vector<int64_t>& ldda, void* s) {
+                   const std::vector<int64_t>& ldda, void* s, int acc_d = 0) {
   const int nbw = (int)A.size(), nbd = (int)W.size();
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
@@ -304,15 +304,16 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
   chk(hlhgat_proj_bwd(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(), kbw.data(),
                       dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(), kbd.data(),
-                      dA.data(), ldda.data(), ws.data_ptr<float>(), wsf, s),
+                      dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(), wsf, s),
       "proj_bwd");
 }
 
 void proj_bwd_data(const Tensor& G, const std::vector<const float*>& W,
                    const std::vector<int64_t>& ldw, const std::vector<int64_t>& kb,
-                   std::vector<float*>& dA, const std::vector<int64_t>& ldda, void* s) {
+                   std::vector<float*>& dA, const std::vector<int64_t>& ldda, void* s,
+                   int acc = 0) {
   chk(hlhgat_proj_bwd_data((int)W.size(), G.data_ptr<float>(), ld_of(G), W.data(), ldw.data(),
-                           kb.data(), G.size(0), G.size(1), dA.data(), ldda.data(), 0, s),
+                           kb.data(), G.size(0), G.size(1), dA.data(), ldda.data(), acc, s),
       "proj_bwd_data");
 }
 
@@ -1034,9 +1035,12 @@ Tensor linear_bn_forward(const std::vector<Tensor>& As, const Tensor& W, const O
 }
 
 // grads of linear_forward; dAs[i] only where need_a[i]
+// dA_into (optional, one per block, undefined = fresh): row-strided views the
+// data gradient is ADDED into and returned as dAs (a DenseConcat gradient sink)
 void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Tensor& W,
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
-                     Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr) {
+                     Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr,
+                     const std::vector<Tensor>* dA_into = nullptr) {
   Tensor G = rows2d(Gin);
   const int64_t M = G.size(0), N = G.size(1);
   const int nb = (int)As.size();
@@ -1097,19 +1101,25 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
     std::vector<const float*> Wp;
     std::vector<int64_t> ldw, kbs, ldda;
     std::vector<float*> dA;
+    // accumulate into the given destinations only when every block has one
+    bool into = dA_into != nullptr;
+    for (int i : idx)
+      into = into && (int)dA_into->size() > i && (*dA_into)[i].defined() &&
+             (*dA_into)[i].size(0) == M && (*dA_into)[i].size(1) == kb[i] &&
+             (*dA_into)[i].stride(1) == 1;
     for (int i : idx) {
-      dAs[i] = at::empty({M, kb[i]}, W.options());
+      dAs[i] = into ? (*dA_into)[i] : at::empty({M, kb[i]}, W.options());
       Wp.push_back(W.data_ptr<float>() + offs[i]);
       ldw.push_back(W.stride(0));
       kbs.push_back(kb[i]);
       dA.push_back(dAs[i].data_ptr<float>());
-      ldda.push_back(kb[i]);
+      ldda.push_back(into ? dAs[i].stride(0) : kb[i]);
     }
     if (M > 0) {
       if (!wAp.empty())
-        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s);
+        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, into);
       else
-        proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s);
+        proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, into);
     }
   }
 }
@@ -1413,7 +1423,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                                Tensor eids, Tensor ei, Tensor rD, at::TensorList pn,
                                at::TensorList pe, double mom1n, double eps1n, double mom4n,
                                double eps4n, double mom1e, double eps1e, double mom4e,
-                               double eps4e, OptT valid_t, OptT valid_s) {
+                               double eps4e, OptT valid_t, OptT valid_s, OptT gsink_t,
+                               OptT gsink_s) {
     req(x_t, "x_t");
     req(x_s, "x_s");
     TORCH_CHECK(pn.size() == 14 && pe.size() == 14, "hlhgat: nei_value expects 14+14 params");
@@ -1506,6 +1517,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       for (int i = 0; i < 8; ++i) em.other();
       em.opt(valid_t);
       em.opt(valid_s);
+      em.opt(gsink_t);
+      em.opt(gsink_s);
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, E, d, dn, de};
@@ -1517,6 +1530,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                             pe[10],
                             // 40, 41: valid-row counts of the node / edge sides
                             has(valid_t) ? *valid_t : Tensor(), has(valid_s) ? *valid_s : Tensor()});
+    // gradient sinks of x_t / x_s (DenseConcat slab views): kept outside the
+    // saved variables -- other views' backwards add into the same slab in
+    // place before this node's backward runs, which is the point
+    if (has(gsink_t)) ctx->saved_data["gsink_t"] = *gsink_t;
+    if (has(gsink_s)) ctx->saved_data["gsink_s"] = *gsink_s;
     return {tn.y, te.y};
   }
 
@@ -1527,8 +1545,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     Tensor xt = sv[0], xs = sv[1], rowptr = sv[2], eids = sv[3], ei = sv[4], rD = sv[5],
            Wt = sv[6], Ws = sv[7];
     // positions: x_t 0, x_s 1, rowptr 2, eids 3, ei 4, rD 5, pn 6..19, pe 20..33, hyper 34..41,
-    //            valid_t 42, valid_s 43
-    variable_list out(44);
+    //            valid_t 42, valid_s 43, gsink_t 44, gsink_s 45
+    variable_list out(46);
     const int64_t PN = 6, PE = 20;
     Tensor dYt = at::empty({N, dn + de}, xt.options());
     Tensor dYs = at::empty({E, de + dn}, xt.options());
@@ -1587,9 +1605,16 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     std::vector<Tensor> dxt, dxs;
     {
       TStreamGuard g(fk.side);
-      linear_backward(dYs, {xs}, Ws, nW, nB, {need(ctx, 1)}, dWs, dbs, dxs);
+      // x_s's gradient added straight into the dense slab's gradient (sink)
+      const bool hs = ctx->saved_data.count("gsink_s") > 0;
+      const std::vector<Tensor> into_s{hs ? ctx->saved_data["gsink_s"].toTensor() : Tensor()};
+      linear_backward(dYs, {xs}, Ws, nW, nB, {need(ctx, 1)}, dWs, dbs, dxs, nullptr,
+                      hs ? &into_s : nullptr);
     }
-    linear_backward(dYt, {xt}, Wt, nW, nB, {need(ctx, 0)}, dWt, dbt, dxt);
+    const bool ht = ctx->saved_data.count("gsink_t") > 0;
+    const std::vector<Tensor> into_t{ht ? ctx->saved_data["gsink_t"].toTensor() : Tensor()};
+    linear_backward(dYt, {xt}, Wt, nW, nB, {need(ctx, 0)}, dWt, dbt, dxt, nullptr,
+                    ht ? &into_t : nullptr);
     fk.main_waits_side();
     fk.escape({dWs, dbs, dxs[0], out[PE + 2], out[PE + 3], out[PE + 7], out[PE + 8], out[PE + 9],
                out[PE + 10]});
@@ -1691,10 +1716,10 @@ std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids
                               Tensor rD, std::vector<Tensor> pn, std::vector<Tensor> pe,
                               double mom1n, double eps1n, double mom4n, double eps4n,
                               double mom1e, double eps1e, double mom4e, double eps4e,
-                              OptT valid_t, OptT valid_s) {
+                              OptT valid_t, OptT valid_s, OptT gsink_t, OptT gsink_s) {
   auto r = NEIntValueFn::apply(x_t, x_s, rowptr, eids, ei, rD, at::TensorList(pn),
                                at::TensorList(pe), mom1n, eps1n, mom4n, eps4n, mom1e, eps1e,
-                               mom4e, eps4e, valid_t, valid_s);
+                               mom4e, eps4e, valid_t, valid_s, gsink_t, gsink_s);
   return {r[0], r[1]};
 }
 

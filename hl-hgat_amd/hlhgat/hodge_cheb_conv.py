@@ -222,8 +222,10 @@ class NodeEdgeInt(nn.Module):
     def forward(self, x_t: Tensor, x_s: Tensor, par, D: Tensor):
         if not self.only_att and x_t.is_cuda and x_t.dim() == 2:
             bop = _as_boundary(par, x_t.size(0), x_s.size(0))
+            # one-shot gradient sinks set by the caller (DenseConcat.grad_sink)
+            gsink, self._hlhgat_gsink = getattr(self, "_hlhgat_gsink", (None, None)), (None, None)
             r = ops.nei_value(x_t, x_s, bop.incidence(), ops.reciprocal(D), self.WV_Node,
-                              self.WV_Edge, bop.valid_t, bop.valid_s)
+                              self.WV_Edge, bop.valid_t, bop.valid_s, gsink=gsink)
             if r is not None:
                 return r
         if getattr(par, "valid_t", None) is not None:

@@ -128,9 +128,12 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         x_s0, x_t0 = x_s, x_t
         for i, _ in enumerate(self.channels):
             for j in range(self.channels[i]):
+                neint = getattr(self, "NEInt{}{}".format(i, j))
                 if dense:
                     x_t0, x_s0 = dt.view(), ds.view()
-                x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
+                    # its input gradients go straight into the slab's gradient
+                    neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
+                x_t, x_s = neint(x_t0, x_s0, par_1, D)
                 conv = getattr(self, "NEConv{}{}".format(i, j))
                 if dense:
                     _sink(conv, dt, ds, self.filters[i])
@@ -214,9 +217,12 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0]) + 1e-6  # (:823)
         for i, _ in enumerate(self.channels):
             for j in range(self.channels[i]):
+                neint = getattr(self, "NEInt{}{}".format(i, j))
                 if dense:
                     x_t0, x_s0 = dt.view(), ds.view()
-                x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
+                    # its input gradients go straight into the slab's gradient
+                    neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
+                x_t, x_s = neint(x_t0, x_s0, par_1, D)
                 conv = getattr(self, "NEConv{}{}".format(i, j))
                 if dense:
                     _sink(conv, dt, ds, self.filters[i])
@@ -317,9 +323,12 @@ class _AttPoolHead(nn.Module):
                 dt.append(x_t0)
                 ds.append(x_s0)
             for j in range(self.channels[i]):
+                neint = getattr(self, "NEInt{}{}".format(i, j))
                 if dense:
                     x_t0, x_s0 = dt.view(), ds.view()
-                x_t, x_s = getattr(self, "NEInt{}{}".format(i, j))(x_t0, x_s0, par_1, D)
+                    # its input gradients go straight into the slab's gradient
+                    neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
+                x_t, x_s = neint(x_t0, x_s0, par_1, D)
                 conv = getattr(self, "NEConv{}{}".format(i, j))
                 if dense:
                     _sink(conv, dt, ds, self.filters[i])

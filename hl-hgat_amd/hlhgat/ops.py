@@ -779,6 +779,7 @@ def hodge_poly_conv_pair(s0, s1):
 # Dense concatenation of the HL blocks in one slab
 # ----------------------------------------------------------------------------
 DENSE_SLAB = os.environ.get("HLHGAT_DENSE_SLAB", "1") != "0"
+GRAD_SINK = os.environ.get("HLHGAT_GRAD_SINK", "1") != "0"
 
 
 class DenseConcat:
@@ -832,6 +833,19 @@ class DenseConcat:
         self.cols.append((c0, c1))
         self.owned.append(False)
 
+    def grad_sink(self) -> Optional[torch.Tensor]:
+        """The gradient slab's view of the current x0 = view() (columns
+        [0, used)): a consumer whose backward ADDS its input gradient into
+        this view (NodeEdgeInt, accumulate_d of hlhgat_proj_bwd) spares the
+        view's backward its add; the slab is zeroed here, once per forward."""
+        if (not GRAD_SINK or not torch.is_grad_enabled()
+                or not any(p.requires_grad for p in self.parts)):
+            return None
+        if self._state.G is None:
+            self._state.G = torch.zeros_like(self.S)
+            self._state.zeroed = True
+        return self._state.G[:, :self.used]
+
     def view(self) -> torch.Tensor:
         w = self.used
         if not torch.is_grad_enabled() or not any(p.requires_grad for p in self.parts):
@@ -847,6 +861,7 @@ class _DenseGrad:
     def __init__(self, S: torch.Tensor):
         self.S = S
         self.G: Optional[torch.Tensor] = None
+        self.zeroed = False  # G was zero-filled in the forward (grad_sink)
 
 
 class _DenseViewFn(torch.autograd.Function):
@@ -863,6 +878,9 @@ class _DenseViewFn(torch.autograd.Function):
             # initialises every column the narrower views accumulate into
             st.G = torch.empty_like(st.S)
             st.G[:, :w].copy_(g)
+        elif (st.zeroed and g.data_ptr() == st.G.data_ptr() and g.shape == (st.G.size(0), w)
+              and g.stride() == st.G[:, :w].stride()):
+            pass  # the consumer already added its gradient into the slab (grad_sink)
         else:
             st.G[:, :w].add_(g)
         grads = [st.G[:, c0:c1] if own else None for c0, c1, own in ctx.ranges]
@@ -916,7 +934,8 @@ def _mlp2_params(seq: torch.nn.Sequential):
 
 def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.Tensor,
               wv_node: torch.nn.Sequential, wv_edge: torch.nn.Sequential,
-              valid_t: Optional[torch.Tensor] = None, valid_s: Optional[torch.Tensor] = None):
+              valid_t: Optional[torch.Tensor] = None, valid_s: Optional[torch.Tensor] = None,
+              gsink=(None, None)):
     """NodeEdgeInt value path (lib/Hodge_Cheb_Conv.py:293-295,307-308) as one
     C++ node, first Linear projected before the |B1| gathers (torch_ext.cpp,
     NEIntValueFn); returns (x_t1, x_s1), or None when the WV_* modules are not
@@ -931,8 +950,16 @@ def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.
                            f"|B1| ({inc.n_nodes}, {inc.n_edges})")
     if rD.numel() != inc.n_nodes:
         raise RuntimeError(f"hlhgat: D has {rD.numel()} entries, |B1| has {inc.n_nodes} nodes")
+    # gsink: the DenseConcat gradient-slab views of x_t / x_s (DenseConcat.grad_sink):
+    # their gradients are added straight into the slab by the Linear backward
+    gt, gs = gsink
+    if gt is not None and (gt.shape != x_t.shape or gt.data_ptr() == x_t.data_ptr()):
+        gt = None
+    if gs is not None and (gs.shape != x_s.shape or gs.data_ptr() == x_s.data_ptr()):
+        gs = None
     r = _ext.nei_value(x_t, x_s, inc.rowptr, inc.edge_ids, inc.edge_index,
-                       rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1], valid_t, valid_s)
+                       rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1], valid_t, valid_s,
+                       gt, gs)
     return r[0], r[1]
 
 

@@ -345,14 +345,17 @@ int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
  * hlhgat_proj_bwd_weight_workspace_floats) together with the data gradient of
  * hlhgat_proj_bwd_data (nb_d blocks) in one, then the split reduction;
  * bit-identical to those two calls; either side may be empty (nb = 0).
- * Unaligned operands fall back to the two calls.  accumulate = 0 only. */
+ * Unaligned operands fall back to the two calls.  The weight gradient is
+ * written (accumulate = 0); accumulate_d != 0 adds the data gradient into
+ * dA (e.g. straight into the gradient slab of the dense concatenation,
+ * hlhgat.ops.DenseConcat). */
 int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
                     int nb_w, const float* const* A, const int64_t* lda,
                     const int64_t* kb_w, float* const* dW, const int64_t* lddw,
                     float* dbias, int nb_d, const float* const* W,
                     const int64_t* ldw, const int64_t* kb_d, float* const* dA,
-                    const int64_t* ldda, float* workspace, int64_t workspace_floats,
-                    void* stream);
+                    const int64_t* ldda, int accumulate_d, float* workspace,
+                    int64_t workspace_floats, void* stream);
 
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)

@@ -137,3 +137,31 @@ def test_zinc_train_step_paired_equals_unpaired(cuda):
         assert l0 == l1
         for k in s0:
             assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.gpu
+def test_dense_grad_sink_bitwise(cuda):
+    """NodeEdgeInt adding its input gradients straight into the dense slab's
+    gradient (DenseConcat.grad_sink, accumulate_d of hlhgat_proj_bwd) gives
+    the bits of the view-by-view accumulation: every parameter gradient of
+    the ZINC model."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(64, seed=11).to(cuda)
+    res = []
+    prev = ops.GRAD_SINK
+    for sink in (False, True):
+        ops.GRAD_SINK = sink
+        try:
+            torch.manual_seed(0)
+            m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2], filters=[64, 64],
+                                                    mlp_channels=[64], K=3,
+                                                    keig=15).to(cuda).train()
+            out = m(b)
+            torch.nn.functional.l1_loss(out.view(-1), b.y.view(-1)).backward()
+            res.append({k: p.grad.clone() for k, p in m.named_parameters()})
+        finally:
+            ops.GRAD_SINK = prev
+    for k in res[0]:
+        assert torch.equal(res[0][k], res[1][k]), k
