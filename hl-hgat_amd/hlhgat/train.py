@@ -33,6 +33,10 @@ from . import ops
 
 __all__ = ["TrainStep", "batch_key"]
 
+# HLHGAT_HIP_ADAM=0: torch's fused Adam instead of hlhgat_adam_flat (A/B)
+import os as _os  # noqa: E402
+HIP_ADAM = _os.environ.get("HLHGAT_HIP_ADAM", "1") != "0"
+
 
 def _tensor_items(batch):
     return [(k, v) for k, v in sorted(vars(batch).items())
@@ -123,6 +127,18 @@ class TrainStep:
         if dev.type == "cuda":
             kw.update(fused=True, capturable=self.graphs)
         self.opt = torch.optim.Adam([self.master], **kw)
+        self._hip_adam = dev.type == "cuda" and HIP_ADAM
+        if self._hip_adam:
+            # the optimiser state torch's fused Adam would create, updated by
+            # ONE hlhgat_adam_flat launch (torch's multi-tensor kernel runs a
+            # single 65536-element chunk per workgroup on this one flat
+            # tensor: ~10 workgroups, 0.1 ms per step at the ZINC size)
+            self.opt.state[self.master] = {
+                "step": torch.zeros((), dtype=torch.float32, device=dev),
+                "exp_avg": torch.zeros_like(self.flat),
+                "exp_avg_sq": torch.zeros_like(self.flat)}
+            self._arrive = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._hyper = (lr, betas, eps, weight_decay)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.max_graphs = max_graphs
         self._graphs: Dict[Tuple, _Captured] = {}
@@ -157,12 +173,21 @@ class TrainStep:
                 view.copy_(g)
                 p.grad = view
 
+    def _opt_step(self) -> None:
+        if not self._hip_adam:
+            self.opt.step()
+            return
+        st = self.opt.state[self.master]
+        lr, betas, eps, wd = self._hyper
+        ops.adam_flat(self.flat, self.flat_grad, st["exp_avg"], st["exp_avg_sq"], st["step"],
+                      self._arrive, lr, betas, eps, wd)
+
     def _exchange_and_update(self) -> None:
         if self.world > 1:
             # one contiguous bucket; mean over ranks as DDP
             dist.all_reduce(self.flat_grad)
             self.flat_grad.div_(self.world)
-        self.opt.step()
+        self._opt_step()
 
     def _eager(self, batch) -> torch.Tensor:
         ops.clear_caches()
@@ -187,7 +212,7 @@ class TrainStep:
         with torch.cuda.graph(g, pool=self._pool, stream=s):
             loss = self._fwd_bwd(static)
             if self.world == 1:
-                self.opt.step()
+                self._opt_step()
             # every stream forked from the capture (the node / edge side streams,
             # forks inside autograd backward nodes, which run on autograd's
             # device thread) rejoins it before hipStreamEndCapture: an unjoined

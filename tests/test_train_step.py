@@ -278,3 +278,33 @@ def test_capture_rejoins_fork_left_open_in_backward(cuda):
         assert torch.equal(a, b)
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wd", [0.0, 1e-3])
+def test_adam_flat_matches_torch_fused_adam(cuda, wd):
+    """hlhgat_adam_flat (one launch over the flat parameter buffer) against
+    torch.optim.Adam(fused=True, capturable=True) on the same tensor, 3 steps:
+    the same arithmetic up to FMA contraction (torch's kernel is built with
+    contraction on, hlhgat with -ffp-contract=off): a few ulp."""
+    from hlhgat import ops
+    n = 300_001
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=g).to(cuda)
+    grads = [torch.randn(n, generator=g).to(cuda) for _ in range(3)]
+    ref = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=wd,
+                           fused=True, capturable=True)
+    p = p0.clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.zeros((), device=cuda)
+    arrive = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for gr in grads:
+        ref.grad = gr.clone()
+        opt.step()
+        ops.adam_flat(p, gr, m, v, step, arrive, 1e-3, (0.9, 0.999), 1e-8, wd)
+    st = opt.state[ref]
+    assert float(step) == 3.0 and int(arrive) == 0
+    assert torch.allclose(p, ref.detach(), rtol=1e-6, atol=1e-7)
+    assert torch.allclose(m, st["exp_avg"], rtol=1e-5, atol=1e-7)
+    assert torch.allclose(v, st["exp_avg_sq"], rtol=1e-5, atol=1e-9)
