@@ -338,6 +338,15 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
         tp = graph_tiles(counts, nnz)
         if tp is not None:
             setattr(b, key, tp)
+    # graph segment offsets of the readout (global_mean_pool over the
+    # graph-contiguous rows, lib/Hodge_ST_Model.py:636), built here once
+    # instead of by four small device ops per pool in every step
+    for key, ck in (("seg_ptr_t", "num_node1"), ("seg_ptr_s", "num_edge1")):
+        c = getattr(b, ck, None)
+        if torch.is_tensor(c) and c.dim() == 1 and not c.is_floating_point():
+            ptr = torch.zeros(c.numel() + 1, dtype=torch.int32)
+            ptr[1:] = torch.cumsum(c, 0).to(torch.int32)
+            setattr(b, key, ptr)
     return b
 
 

@@ -29,10 +29,14 @@ def segment_ptr(counts: torch.Tensor, device) -> torch.Tensor:
     return ptr
 
 
-def mean_pool_sorted(x: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+def mean_pool_sorted(x: torch.Tensor, counts: torch.Tensor,
+                     ptr: torch.Tensor = None) -> torch.Tensor:
     """global_mean_pool(x, batch) for a graph-contiguous batch vector
-    (lib/Hodge_ST_Model.py:636) on the HIP segment-mean kernel."""
-    return ops.segment_mean(x, segment_ptr(counts, x.device), counts.numel())
+    (lib/Hodge_ST_Model.py:636) on the HIP segment-mean kernel; ``ptr`` =
+    the batch's precomputed int32 offsets (collate: seg_ptr_t / seg_ptr_s)."""
+    if ptr is None or ptr.device != x.device or ptr.numel() != counts.numel() + 1:
+        ptr = segment_ptr(counts, x.device)
+    return ops.segment_mean(x, ptr, counts.numel())
 
 
 def _hl_block(cin_t, cin_s, cout, K, dropout_ratio, act=nn.ReLU):
@@ -145,8 +149,9 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                 else:
                     x_t0 = torch.cat([x_t0, x_t], dim=-1)
                     x_s0 = torch.cat([x_s0, x_s], dim=-1)
-        x = torch.cat((mean_pool_sorted(x_s, data.num_edge1),
-                       mean_pool_sorted(x_t, data.num_node1)), -1)
+        x = torch.cat((mean_pool_sorted(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
+                       mean_pool_sorted(x_t, data.num_node1, getattr(data, "seg_ptr_t", None))),
+                      -1)
         for i, _ in enumerate(self.mlp_channels):
             x = run_sequential(getattr(self, "mlp%d" % i), [x])
         y = ops.linear_blocks([x], self.out.weight, self.out.bias)
@@ -363,8 +368,8 @@ class _AttPoolHead(nn.Module):
                 par_1 = adj2par1(d1.edge_index, x_t0.shape[0], x_s0.shape[0])
                 D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
         dr = datas[min(len(self.channels) - 1, 1)]
-        x = torch.cat((mean_pool_sorted(x_s, dr.num_edge1),
-                       mean_pool_sorted(x_t, dr.num_node1)), -1)
+        x = torch.cat((mean_pool_sorted(x_s, dr.num_edge1, getattr(dr, "seg_ptr_s", None)),
+                       mean_pool_sorted(x_t, dr.num_node1, getattr(dr, "seg_ptr_t", None))), -1)
         for i, _ in enumerate(self.mlp_channels):
             x = run_sequential(getattr(self, "mlp%d" % i), [x])
         y = ops.linear_blocks([x], self.out.weight, self.out.bias)
