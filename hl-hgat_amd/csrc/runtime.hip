@@ -341,8 +341,8 @@ extern "C" int hlhgat_copy2d_batched(int n, const float* const* src, const int64
 // torch's fused Adam (ADAM_MODE::ORIGINAL, L2 weight decay added to the
 // gradient; bias corrections from the device step count, as its capturable
 // path) evaluated with the same double-precision hyper-parameter arithmetic,
-// and the step count is incremented by the last workgroup to finish (every
-// workgroup reads it first), so the update is one launch.
+// and the step count is incremented by a one-thread launch afterwards (an
+// arrival counter of the update's workgroups on one address cost 10-60 us).
 namespace {
 struct AdamArgs {
   float* p;
@@ -351,16 +351,22 @@ struct AdamArgs {
   float* v;
   int64_t n;
   float* step;
-  unsigned* arrive;
   double lr, beta1, beta2, eps, wd;
 };
 
 __global__ __launch_bounds__(256) void k_adam_flat(AdamArgs a) {
-  const float s = *a.step + 1.0f;  // torch: state_steps += 1 (fp32), then the update
-  const double bc1 = 1.0 - pow(a.beta1, (double)s);
-  const double bc2 = 1.0 - pow(a.beta2, (double)s);
-  const float bias_correction1 = (float)bc1;
-  const float bias_correction2_sqrt = (float)sqrt(bc2);
+  // bias corrections once per workgroup (fp64 pow), broadcast through LDS
+  __shared__ float sh[2];
+  if (threadIdx.x == 0) {
+    const float s = *a.step + 1.0f;  // torch: state_steps += 1 (fp32), then the update
+    const double bc1 = 1.0 - pow(a.beta1, (double)s);
+    const double bc2 = 1.0 - pow(a.beta2, (double)s);
+    sh[0] = (float)bc1;
+    sh[1] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const float bias_correction1 = sh[0];
+  const float bias_correction2_sqrt = sh[1];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < a.n;
        i += (int64_t)gridDim.x * 256) {
     float param = a.p[i];
@@ -377,34 +383,28 @@ __global__ __launch_bounds__(256) void k_adam_flat(AdamArgs a) {
     a.m[i] = exp_avg;
     a.v[i] = exp_avg_sq;
   }
-  // the last workgroup to arrive publishes the incremented step (all have read it)
-  __shared__ unsigned last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev =
-        __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.step[0] = s;
-  }
 }
+
+__global__ void k_adam_step_inc(float* step) { step[0] = step[0] + 1.0f; }
 }  // namespace
 
 extern "C" int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg,
-                                float* exp_avg_sq, int64_t n, float* step, unsigned* arrive,
+                                float* exp_avg_sq, int64_t n, float* step,
                                 double lr, double beta1, double beta2, double eps,
                                 double weight_decay, void* stream) {
-  HLH_CHECK_ARG(n >= 0 && (n == 0 || (param && grad && exp_avg && exp_avg_sq)) && step && arrive,
+  HLH_CHECK_ARG(n >= 0 && (n == 0 || (param && grad && exp_avg && exp_avg_sq)) && step,
                 "adam_flat: NULL pointer or n < 0");
-  if (n == 0) return HLHGAT_OK;
-  int64_t g = ceil_div(n, 256);
+  if (n == 0) {
+    launch(k_adam_step_inc, dim3(1), dim3(1), 0, as_stream(stream), nullptr, step);
+    HLH_CHECK_LAUNCH();
+    return HLHGAT_OK;
+  }
+  int64_t g = ceil_div(n, 256 * 2);
   if (g > 2048) g = 2048;
-  AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, step, arrive, lr, beta1, beta2, eps,
-             weight_decay};
+  AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, step, lr, beta1, beta2, eps, weight_decay};
   launch(k_adam_flat, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, a);
+  HLH_CHECK_LAUNCH();
+  launch(k_adam_step_inc, dim3(1), dim3(1), 0, as_stream(stream), nullptr, step);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

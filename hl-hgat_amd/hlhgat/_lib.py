@@ -94,8 +94,8 @@ SIGNATURES = {
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                     c_vp]),
-    "hlhgat_adam_flat": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_f64, c_f64,
-                                 c_f64, c_f64, c_f64, c_vp]),
+    "hlhgat_adam_flat": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f64, c_f64, c_f64,
+                                 c_f64, c_f64, c_vp]),
     "hlhgat_group_begin": (c_i32, []),
     "hlhgat_group_next": (c_i32, []),
     "hlhgat_group_end": (c_i32, [c_vp, c_vp]),

@@ -1314,11 +1314,10 @@ class _SyncBatchNormFn(torch.autograd.Function):
 # Adam on a flat parameter buffer (hlhgat_adam_flat; hlhgat.train.TrainStep)
 # ----------------------------------------------------------------------------
 def adam_flat(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
-              exp_avg_sq: torch.Tensor, step: torch.Tensor, arrive: torch.Tensor, lr: float,
-              betas, eps: float, weight_decay: float) -> None:
-    """One torch.optim.Adam (fused, capturable) update of a flat fp32 buffer
-    in one launch; `step` fp32 [1] on device (incremented), `arrive` int32 [1]
-    zero-initialised scratch."""
+              exp_avg_sq: torch.Tensor, step: torch.Tensor, lr: float, betas, eps: float,
+              weight_decay: float) -> None:
+    """One torch.optim.Adam (fused, capturable) update of a flat fp32 buffer;
+    `step` the fp32 step count on device (incremented)."""
     for t, name in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"),
                     (exp_avg_sq, "exp_avg_sq"), (step, "step")):
         _req_dev(t, name)
@@ -1328,8 +1327,7 @@ def adam_flat(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
     if not (grad.numel() == exp_avg.numel() == exp_avg_sq.numel() == n):
         raise RuntimeError("hlhgat: adam_flat: buffer sizes differ")
     check(LIB.hlhgat_adam_flat(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
-                               exp_avg_sq.data_ptr(), n, step.data_ptr(), arrive.data_ptr(),
-                               float(lr), float(betas[0]), float(betas[1]), float(eps),
+                               exp_avg_sq.data_ptr(), n, step.data_ptr(), float(lr), float(betas[0]), float(betas[1]), float(eps),
                                float(weight_decay), _stream(param)), "adam_flat")
 
 

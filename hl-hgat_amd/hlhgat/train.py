@@ -137,7 +137,6 @@ class TrainStep:
                 "step": torch.zeros((), dtype=torch.float32, device=dev),
                 "exp_avg": torch.zeros_like(self.flat),
                 "exp_avg_sq": torch.zeros_like(self.flat)}
-            self._arrive = torch.zeros(1, dtype=torch.int32, device=dev)
             self._hyper = (lr, betas, eps, weight_decay)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.max_graphs = max_graphs
@@ -180,7 +179,7 @@ class TrainStep:
         st = self.opt.state[self.master]
         lr, betas, eps, wd = self._hyper
         ops.adam_flat(self.flat, self.flat_grad, st["exp_avg"], st["exp_avg_sq"], st["step"],
-                      self._arrive, lr, betas, eps, wd)
+                      lr, betas, eps, wd)
 
     def _exchange_and_update(self) -> None:
         if self.world > 1:

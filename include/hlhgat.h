@@ -526,13 +526,13 @@ int hlhgat_group_abort(void);
 /* torch.optim.Adam (fused, capturable; L2 weight decay added to the gradient)
  * on ONE flat fp32 parameter buffer of n elements (hlhgat.train.TrainStep
  * keeps every parameter there), the reference's optimiser
- * (main_zinc_*.py).  `step` is the device fp32 step count (incremented here,
- * as torch increments it before the update); `arrive` a device uint32 that
- * must be 0 before the first call (the kernels leave it 0).  Same
- * double-precision hyper-parameter arithmetic as torch's fused Adam. */
+ * (main_zinc_*.py).  `step` is the device fp32 step count: the update uses
+ * step + 1, as torch increments it before the update, and a one-thread
+ * launch then stores it.  Same double-precision hyper-parameter arithmetic
+ * as torch's fused Adam (up to FMA contraction). */
 int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                     int64_t n, float* step, unsigned* arrive, double lr, double beta1,
-                     double beta2, double eps, double weight_decay, void* stream);
+                     int64_t n, float* step, double lr, double beta1, double beta2, double eps,
+                     double weight_decay, void* stream);
 
 /* ---- workspaces --------------------------------------------------------- */
 /* Zero `bytes` (a multiple of 4) at p with a kernel on `stream` (graph-capture

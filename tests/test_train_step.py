@@ -298,13 +298,12 @@ def test_adam_flat_matches_torch_fused_adam(cuda, wd):
     p = p0.clone()
     m, v = torch.zeros_like(p), torch.zeros_like(p)
     step = torch.zeros((), device=cuda)
-    arrive = torch.zeros(1, dtype=torch.int32, device=cuda)
     for gr in grads:
         ref.grad = gr.clone()
         opt.step()
-        ops.adam_flat(p, gr, m, v, step, arrive, 1e-3, (0.9, 0.999), 1e-8, wd)
+        ops.adam_flat(p, gr, m, v, step, 1e-3, (0.9, 0.999), 1e-8, wd)
     st = opt.state[ref]
-    assert float(step) == 3.0 and int(arrive) == 0
+    assert float(step) == 3.0
     assert torch.allclose(p, ref.detach(), rtol=1e-6, atol=1e-7)
     assert torch.allclose(m, st["exp_avg"], rtol=1e-5, atol=1e-7)
     assert torch.allclose(v, st["exp_avg_sq"], rtol=1e-5, atol=1e-9)

@@ -2,7 +2,7 @@
 
     python tools/step_kernels.py run_kernel_trace.csv [--step -5]
 
-Steps are delimited by the fused Adam kernel; prints the dispatches of one
+Steps are delimited by the Adam kernel (k_adam_flat, or torch's fused Adam); prints the dispatches of one
 replayed step grouped by kernel name (count, total and mean duration) and the
 busy time per hardware queue.
 """
@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--step", type=int, default=-5)
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "FusedOptimizer" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows)
+           if "FusedOptimizer" in r["Kernel_Name"] or "k_adam_flat" in r["Kernel_Name"]]
     a, b = idx[args.step - 1], idx[args.step]
     st = rows[a + 1:b + 1]
     span = (int(st[-1]["End_Timestamp"]) - int(st[0]["Start_Timestamp"])) / 1e3
