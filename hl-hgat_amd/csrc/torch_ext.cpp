@@ -1036,11 +1036,12 @@ Tensor linear_bn_forward(const std::vector<Tensor>& As, const Tensor& W, const O
 
 // grads of linear_forward; dAs[i] only where need_a[i]
 // dA_into (optional, one per block, undefined = fresh): row-strided views the
-// data gradient is ADDED into and returned as dAs (a DenseConcat gradient sink)
+// data gradient is written (into_acc = 0) or ADDED (1) into and returned as
+// dAs (a DenseConcat gradient sink)
 void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Tensor& W,
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
                      Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr,
-                     const std::vector<Tensor>* dA_into = nullptr) {
+                     const std::vector<Tensor>* dA_into = nullptr, int into_acc = 1) {
   Tensor G = rows2d(Gin);
   const int64_t M = G.size(0), N = G.size(1);
   const int nb = (int)As.size();
@@ -1116,10 +1117,11 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
       ldda.push_back(into ? dAs[i].stride(0) : kb[i]);
     }
     if (M > 0) {
+      const int acc = into ? into_acc : 0;
       if (!wAp.empty())
-        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, into);
+        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, acc);
       else
-        proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, into);
+        proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, acc);
     }
   }
 }
@@ -1417,6 +1419,20 @@ struct SideMlp {  // [W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4, rm4, rv4
   Tensor h1, a1, m1, i1, h2, y, m4, i4;
 };
 
+// The DenseConcat gradient slab's host flag: 0 until a gradient has landed
+// in the slab.  Returns the accumulate mode for this writer and marks the
+// slab written (host-side, at backward issue: a captured graph replays the
+// same sequence).
+int sink_accumulate(AutogradContext* ctx, const char* key) {
+  Tensor f = ctx->saved_data[key].toTensor();
+  TORCH_CHECK(f.device().is_cpu() && f.scalar_type() == at::kInt && f.numel() == 1,
+              "hlhgat: gradient-sink flag must be a CPU int32 [1]");
+  int* w = f.data_ptr<int>();
+  const int acc = *w != 0 ? 1 : 0;
+  *w = 1;
+  return acc;
+}
+
 class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
  public:
   static variable_list forward(AutogradContext* ctx, Tensor x_t, Tensor x_s, Tensor rowptr,
@@ -1424,7 +1440,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                                at::TensorList pe, double mom1n, double eps1n, double mom4n,
                                double eps4n, double mom1e, double eps1e, double mom4e,
                                double eps4e, OptT valid_t, OptT valid_s, OptT gsink_t,
-                               OptT gsink_s) {
+                               OptT gsink_s, OptT gflag_t, OptT gflag_s) {
     req(x_t, "x_t");
     req(x_s, "x_s");
     TORCH_CHECK(pn.size() == 14 && pe.size() == 14, "hlhgat: nei_value expects 14+14 params");
@@ -1519,6 +1535,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       em.opt(valid_s);
       em.opt(gsink_t);
       em.opt(gsink_s);
+      em.opt(gflag_t);
+      em.opt(gflag_s);
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, E, d, dn, de};
@@ -1533,8 +1551,16 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     // gradient sinks of x_t / x_s (DenseConcat slab views): kept outside the
     // saved variables -- other views' backwards add into the same slab in
     // place before this node's backward runs, which is the point
-    if (has(gsink_t)) ctx->saved_data["gsink_t"] = *gsink_t;
-    if (has(gsink_s)) ctx->saved_data["gsink_s"] = *gsink_s;
+    // with a host int32 flag each ("slab written yet"): the first gradient to
+    // land in a slab overwrites, the later ones add (no zero fill of the slab)
+    if (has(gsink_t) && has(gflag_t)) {
+      ctx->saved_data["gsink_t"] = *gsink_t;
+      ctx->saved_data["gflag_t"] = *gflag_t;
+    }
+    if (has(gsink_s) && has(gflag_s)) {
+      ctx->saved_data["gsink_s"] = *gsink_s;
+      ctx->saved_data["gflag_s"] = *gflag_s;
+    }
     return {tn.y, te.y};
   }
 
@@ -1545,8 +1571,8 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     Tensor xt = sv[0], xs = sv[1], rowptr = sv[2], eids = sv[3], ei = sv[4], rD = sv[5],
            Wt = sv[6], Ws = sv[7];
     // positions: x_t 0, x_s 1, rowptr 2, eids 3, ei 4, rD 5, pn 6..19, pe 20..33, hyper 34..41,
-    //            valid_t 42, valid_s 43, gsink_t 44, gsink_s 45
-    variable_list out(46);
+    //            valid_t 42, valid_s 43, gsink_t 44, gsink_s 45, gflag_t 46, gflag_s 47
+    variable_list out(48);
     const int64_t PN = 6, PE = 20;
     Tensor dYt = at::empty({N, dn + de}, xt.options());
     Tensor dYs = at::empty({E, de + dn}, xt.options());
@@ -1609,12 +1635,12 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       const bool hs = ctx->saved_data.count("gsink_s") > 0;
       const std::vector<Tensor> into_s{hs ? ctx->saved_data["gsink_s"].toTensor() : Tensor()};
       linear_backward(dYs, {xs}, Ws, nW, nB, {need(ctx, 1)}, dWs, dbs, dxs, nullptr,
-                      hs ? &into_s : nullptr);
+                      hs ? &into_s : nullptr, hs ? sink_accumulate(ctx, "gflag_s") : 0);
     }
     const bool ht = ctx->saved_data.count("gsink_t") > 0;
     const std::vector<Tensor> into_t{ht ? ctx->saved_data["gsink_t"].toTensor() : Tensor()};
     linear_backward(dYt, {xt}, Wt, nW, nB, {need(ctx, 0)}, dWt, dbt, dxt, nullptr,
-                    ht ? &into_t : nullptr);
+                    ht ? &into_t : nullptr, ht ? sink_accumulate(ctx, "gflag_t") : 0);
     fk.main_waits_side();
     fk.escape({dWs, dbs, dxs[0], out[PE + 2], out[PE + 3], out[PE + 7], out[PE + 8], out[PE + 9],
                out[PE + 10]});
@@ -1716,10 +1742,12 @@ std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids
                               Tensor rD, std::vector<Tensor> pn, std::vector<Tensor> pe,
                               double mom1n, double eps1n, double mom4n, double eps4n,
                               double mom1e, double eps1e, double mom4e, double eps4e,
-                              OptT valid_t, OptT valid_s, OptT gsink_t, OptT gsink_s) {
+                              OptT valid_t, OptT valid_s, OptT gsink_t, OptT gsink_s,
+                              OptT gflag_t, OptT gflag_s) {
   auto r = NEIntValueFn::apply(x_t, x_s, rowptr, eids, ei, rD, at::TensorList(pn),
                                at::TensorList(pe), mom1n, eps1n, mom4n, eps4n, mom1e, eps1e,
-                               mom4e, eps4e, valid_t, valid_s, gsink_t, gsink_s);
+                               mom4e, eps4e, valid_t, valid_s, gsink_t, gsink_s, gflag_t,
+                               gflag_s);
   return {r[0], r[1]};
 }
 

@@ -837,14 +837,17 @@ class DenseConcat:
         """The gradient slab's view of the current x0 = view() (columns
         [0, used)): a consumer whose backward ADDS its input gradient into
         this view (NodeEdgeInt, accumulate_d of hlhgat_proj_bwd) spares the
-        view's backward its add; the slab is zeroed here, once per forward."""
+        view's backward its add.  Returns (view, flag): the host int32 flag
+        says whether a gradient has landed in the slab yet -- the first
+        writer overwrites, the later ones add, so the slab is never zeroed."""
         if (not GRAD_SINK or not torch.is_grad_enabled()
                 or not any(p.requires_grad for p in self.parts)):
             return None
         if self._state.G is None:
-            self._state.G = torch.zeros_like(self.S)
-            self._state.zeroed = True
-        return self._state.G[:, :self.used]
+            # not zero-filled: the first gradient to land overwrites (flag)
+            self._state.G = torch.empty_like(self.S)
+            self._state.sink = True
+        return self._state.G[:, :self.used], self._state.written
 
     def view(self) -> torch.Tensor:
         w = self.used
@@ -861,7 +864,8 @@ class _DenseGrad:
     def __init__(self, S: torch.Tensor):
         self.S = S
         self.G: Optional[torch.Tensor] = None
-        self.zeroed = False  # G was zero-filled in the forward (grad_sink)
+        self.sink = False  # G was handed out as a gradient sink (grad_sink)
+        self.written = torch.zeros(1, dtype=torch.int32)  # host flag: G holds a gradient
 
 
 class _DenseViewFn(torch.autograd.Function):
@@ -878,9 +882,12 @@ class _DenseViewFn(torch.autograd.Function):
             # initialises every column the narrower views accumulate into
             st.G = torch.empty_like(st.S)
             st.G[:, :w].copy_(g)
-        elif (st.zeroed and g.data_ptr() == st.G.data_ptr() and g.shape == (st.G.size(0), w)
+        elif (st.sink and g.data_ptr() == st.G.data_ptr() and g.shape == (st.G.size(0), w)
               and g.stride() == st.G[:, :w].stride()):
             pass  # the consumer already added its gradient into the slab (grad_sink)
+        elif st.sink and int(st.written[0]) == 0:
+            st.G[:, :w].copy_(g)  # first gradient into a sink slab: overwrite
+            st.written[0] = 1
         else:
             st.G[:, :w].add_(g)
         grads = [st.G[:, c0:c1] if own else None for c0, c1, own in ctx.ranges]
@@ -952,14 +959,14 @@ def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.
         raise RuntimeError(f"hlhgat: D has {rD.numel()} entries, |B1| has {inc.n_nodes} nodes")
     # gsink: the DenseConcat gradient-slab views of x_t / x_s (DenseConcat.grad_sink):
     # their gradients are added straight into the slab by the Linear backward
-    gt, gs = gsink
+    (gt, ft), (gs, fs) = [g if g is not None else (None, None) for g in gsink]
     if gt is not None and (gt.shape != x_t.shape or gt.data_ptr() == x_t.data_ptr()):
-        gt = None
+        gt = ft = None
     if gs is not None and (gs.shape != x_s.shape or gs.data_ptr() == x_s.data_ptr()):
-        gs = None
+        gs = fs = None
     r = _ext.nei_value(x_t, x_s, inc.rowptr, inc.edge_ids, inc.edge_index,
                        rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1], valid_t, valid_s,
-                       gt, gs)
+                       gt, gs, ft, fs)
     return r[0], r[1]
 
 
