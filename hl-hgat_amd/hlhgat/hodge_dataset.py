@@ -14,7 +14,7 @@ Host-side code (numpy / torch CPU), run once per graph outside the hot loop.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -118,6 +118,9 @@ class Batch(PairData):
         if (getattr(self, "l1_factor", False) and torch.is_tensor(ei) and ei.is_cuda
                 and torch.is_tensor(eis) and eis.is_cuda):
             ops.set_hodge_factor(eis, ei, self.x_t.size(0), getattr(self, "row_order_t", None))
+        ip, ie = getattr(self, "inc_rowptr", None), getattr(self, "inc_eids", None)
+        if torch.is_tensor(ei) and ei.is_cuda and torch.is_tensor(ip) and torch.is_tensor(ie):
+            ops.set_incidence(ei, ip, ie)
         if torch.is_tensor(ei) and ei.is_cuda:
             for kv in ("n_valid_t", "n_valid_s"):
                 nv = getattr(self, kv, None)
@@ -284,6 +287,25 @@ def is_sorted_symmetric(ei: np.ndarray, w: Optional[np.ndarray]) -> bool:
     return True
 
 
+def incidence_csr(edge_index, n_nodes: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Host build of the incidence CSR of |B1| for the edge list [2, E]
+    (adj2par1, lib/Hodge_Dataset.py:169-191: edge e is incident to
+    edge_index[0][e] and edge_index[1][e]): int32 rowptr [n_nodes+1] and
+    edge ids [2E], ascending within a node; a self-edge (padding) appears
+    twice.  The same CSR hlhgat_incidence_csr sorts on the device."""
+    ei = np.asarray(edge_index, dtype=np.int64).reshape(2, -1)
+    E = ei.shape[1]
+    if E and (ei.min() < 0 or ei.max() >= n_nodes):
+        raise ValueError(f"incidence_csr: node index out of range [0, {n_nodes})")
+    e = np.arange(E, dtype=np.int64)
+    keys = np.sort(np.concatenate([ei[0] * E + e, ei[1] * E + e]), kind="stable")
+    rowptr = np.zeros(n_nodes + 1, dtype=np.int32)
+    if E:
+        np.cumsum(np.bincount(keys // E, minlength=n_nodes), out=rowptr[1:])
+    return (torch.from_numpy(rowptr),
+            torch.from_numpy((keys % E if E else keys).astype(np.int32)))
+
+
 def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     """PyG-free equivalent of DataLoader collation for PairData
     (offsets from PairData.__inc__, lib/Hodge_Dataset.py:40-48)."""
@@ -338,6 +360,11 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
         tp = graph_tiles(counts, nnz)
         if tp is not None:
             setattr(b, key, tp)
+    # incidence CSR of |B1| (adj2par1) for the NodeEdgeInt gathers, built
+    # here instead of by a device radix sort in every step
+    ei = getattr(b, "edge_index", None)
+    if torch.is_tensor(ei) and torch.is_tensor(getattr(b, "x_t", None)):
+        b.inc_rowptr, b.inc_eids = incidence_csr(ei, b.x_t.size(0))
     # graph segment offsets of the readout (global_mean_pool over the
     # graph-contiguous rows, lib/Hodge_ST_Model.py:636), built here once
     # instead of by four small device ops per pool in every step
@@ -483,6 +510,8 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     if getattr(b, "edge_index", None) is not None:
         nodes = torch.from_numpy(nt + np.arange(Rs - ns) % (Rt - nt)).to(b.edge_index.dtype)
         out.edge_index = torch.cat([b.edge_index, torch.stack([nodes, nodes])], 1)
+        if getattr(b, "inc_rowptr", None) is not None:
+            out.inc_rowptr, out.inc_eids = incidence_csr(out.edge_index, Rt)
     for side, n, R, per_row in (("t", nt, Rt, pr_t), ("s", ns, Rs, pr_s)):
         o = getattr(b, "row_order_" + side, None)
         if o is not None:

@@ -576,6 +576,18 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
     return _HODGE_CACHE.put(keys, n, op)
 
 
+def set_incidence(edge_index: torch.Tensor, rowptr: torch.Tensor,
+                  edge_ids: torch.Tensor) -> torch.Tensor:
+    """Attach the incidence CSR of |B1| built with the batch
+    (hodge_dataset.incidence_csr, at collate): ``incidence`` then uses it
+    instead of sorting on the device.  It must be the CSR hlhgat_incidence_csr
+    builds (rows = nodes, incident edge ids ascending; tests check bitwise)."""
+    edge_index._hlhgat_incidence = (  # type: ignore[attr-defined]
+        rowptr.to(device=edge_index.device, dtype=torch.int32).contiguous(),
+        edge_ids.to(device=edge_index.device, dtype=torch.int32).contiguous())
+    return edge_index
+
+
 def incidence(edge_index: torch.Tensor, n_nodes: int) -> Incidence:
     """Incidence CSR of |B1| built from the undirected edge list (i<j)."""
     _req_dev(edge_index, "edge_index", torch.int64)
@@ -585,6 +597,13 @@ def incidence(edge_index: torch.Tensor, n_nodes: int) -> Incidence:
     ei = edge_index.contiguous()
     E = ei.size(1)
     dev = ei.device
+    pre = getattr(edge_index, "_hlhgat_incidence", None)
+    if pre is not None:
+        rowptr, eids = pre
+        if rowptr.numel() != n_nodes + 1 or eids.numel() != 2 * E:
+            raise RuntimeError(f"hlhgat: attached incidence CSR has {rowptr.numel() - 1} rows / "
+                               f"{eids.numel()} entries, expected {n_nodes} / {2 * E}")
+        return _INC_CACHE.put([edge_index], n_nodes, Incidence(rowptr, eids, ei, n_nodes, E))
     rowptr = torch.empty(n_nodes + 1, dtype=torch.int32, device=dev)
     eids = torch.empty(max(2 * E, 1), dtype=torch.int32, device=dev)[:2 * E]
     ws_bytes = int(LIB.hlhgat_csr_workspace_bytes(2 * E))

@@ -320,6 +320,23 @@ def test_incidence_gathers_bitexact(cuda):
     assert torch.equal(s2t_d, s2t)
 
 
+def test_collate_incidence_equals_device_build(cuda):
+    """The incidence CSR built at collate (plain and padded batches) is the
+    one hlhgat_incidence_csr sorts on the device, bit for bit, and the batch
+    path uses it (no device build)."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(40, seed=9)
+    for host in (b, pad_batch(b, static_caps(b, 256))):
+        n = host.x_t.shape[0]
+        built = ops.incidence(dev(host.edge_index), n)
+        bd = host.to(cuda)
+        inc = ops.incidence(bd.edge_index, n)
+        assert inc.rowptr.data_ptr() == bd.inc_rowptr.data_ptr()
+        assert torch.equal(inc.rowptr, built.rowptr) and torch.equal(inc.edge_ids, built.edge_ids)
+
+
 def test_segment_and_cluster_mean(cuda):
     from hlhgat import ops
     from hlhgat.hodge_cheb_conv import cluster_mean

@@ -213,6 +213,27 @@ def test_pad_batch_structure():
     assert torch.equal(p.num_node1, b.num_node1) and torch.equal(p.num_edge1, b.num_edge1)
 
 
+def test_incidence_csr_host_build():
+    """Collate-time incidence CSR of |B1| (hodge_dataset.incidence_csr): row v
+    lists the edges with an endpoint at v, ascending (adj2par1,
+    lib/Hodge_Dataset.py:169-191); pad_batch's self-edges appear twice."""
+    from hlhgat.hodge_dataset import incidence_csr, pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(20, seed=4)
+    for batch in (b, pad_batch(b, static_caps(b, 128))):
+        ei, n = batch.edge_index.numpy(), batch.x_t.shape[0]
+        rp, eids = batch.inc_rowptr.numpy(), batch.inc_eids.numpy()
+        assert rp.dtype == np.int32 and eids.dtype == np.int32
+        assert rp.shape == (n + 1,) and eids.shape == (2 * ei.shape[1],)
+        for v in range(n):
+            want = sorted(np.nonzero(ei[0] == v)[0].tolist() + np.nonzero(ei[1] == v)[0].tolist())
+            assert eids[rp[v]:rp[v + 1]].tolist() == want, v
+    rp, eids = incidence_csr(np.zeros((2, 0), dtype=np.int64), 3)
+    assert rp.tolist() == [0, 0, 0, 0] and eids.numel() == 0
+    with pytest.raises(ValueError):
+        incidence_csr(np.array([[0], [5]]), 3)
+
+
 def test_fastconv_adj_t_forms_agree():
     """HodgeLaguerreFastConv.forward(x, adj_t) accepts the DEMO's
     SparseTensor(row=ei[0], col=ei[1], value=w).t() (duck-typed .coo()), a
