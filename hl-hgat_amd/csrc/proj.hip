@@ -715,6 +715,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
 // conflicts, and no cross-wave reduction.  Partials go to the split slab.
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int WR = 32;  // rows per staged chunk
+constexpr int WDEPTH = 2;  // staged chunks in flight per workgroup (register ring; 4 measured no faster at the ZINC shapes and costs the fused kernel occupancy)
 
 // XCD-aware work order: workgroups are dealt round-robin over the 8 XCDs, so
 // (tile, split) item w = xcd_slot(linear id) puts consecutive items -- the
@@ -782,25 +783,27 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
       bsum = bsum + av;
     }
   };
-  // two chunks in flight in registers while one is consumed from LDS
-  float4 g0[2], x0[2], g1[2], x1[2];
+  // WDEPTH chunks in flight in a register ring while one is consumed from
+  // LDS: a slice of a few chunks costs about one memory round trip, not one
+  // per chunk.  Chunk c goes register slot c % WDEPTH -> LDS buffer c & 1;
+  // the one barrier per chunk also orders the buffer reuse (chunk c+2 is
+  // stored after every wave passed chunk c+1's barrier, i.e. finished c).
+  float4 gr[WDEPTH][2], xr[WDEPTH][2];
   const int64_t nchunk = m_hi > m_lo ? (m_hi - m_lo + WR - 1) / WR : 0;
-  if (nchunk > 0) load(m_lo, g0, x0);
-  if (nchunk > 1) load(m_lo + WR, g1, x1);
-  if (nchunk > 0) store(0, g0, x0);
-  __syncthreads();
-  for (int64_t c = 0; c < nchunk; c += 2) {
-    // chunk c in LDS[0], chunk c+1 in (g1, x1)
-    if (c + 2 < nchunk) load(m_lo + (c + 2) * WR, g0, x0);
-    compute(0);
-    if (c + 1 < nchunk) store(1, g1, x1);
-    __syncthreads();
-    if (c + 1 >= nchunk) break;
-    // chunk c+1 in LDS[1], chunk c+2 in (g0, x0)
-    if (c + 3 < nchunk) load(m_lo + (c + 3) * WR, g1, x1);
-    compute(1);
-    if (c + 2 < nchunk) store(0, g0, x0);
-    __syncthreads();
+#pragma unroll
+  for (int j = 0; j < WDEPTH; ++j)
+    if (j < nchunk) load(m_lo + j * WR, gr[j], xr[j]);
+  for (int64_t c0 = 0; c0 < nchunk; c0 += WDEPTH) {
+#pragma unroll
+    for (int j = 0; j < WDEPTH; ++j) {
+      const int64_t c = c0 + j;
+      if (c >= nchunk) break;
+      const int buf = (int)(c & 1);
+      store(buf, gr[j], xr[j]);
+      __syncthreads();
+      if (c + WDEPTH < nchunk) load(m_lo + (c + WDEPTH) * WR, gr[j], xr[j]);
+      compute(buf);
+    }
   }
 
   float* slab = a.part + (int64_t)bz * a.part_stride + a.part_off[b];
@@ -871,16 +874,17 @@ __device__ __forceinline__ void reduce_splits_body(const ReduceArgs& a, Blk blk)
   }
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   if (src >= 0) {
-    // splits grp, grp+4, ... in batches of 8 independent loads
-    for (int sp0 = grp; sp0 < a.splits; sp0 += 32) {
-      float v[8];
+    // splits grp, grp+4, ... in batches of 16 independent loads (a 120-split
+    // plan is two round trips per wave)
+    for (int sp0 = grp; sp0 < a.splits; sp0 += 64) {
+      float v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const int sp = sp0 + 4 * u;
         v[u] = sp < a.splits ? a.part[(int64_t)sp * a.part_stride + src] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s[u & 3] = s[u & 3] + v[u];
+      for (int u = 0; u < 16; ++u) s[u & 3] = s[u & 3] + v[u];
     }
   }
   red[grp][lane] = (s[0] + s[1]) + (s[2] + s[3]);

@@ -121,6 +121,9 @@ class Batch(PairData):
         ip, ie = getattr(self, "inc_rowptr", None), getattr(self, "inc_eids", None)
         if torch.is_tensor(ei) and ei.is_cuda and torch.is_tensor(ip) and torch.is_tensor(ie):
             ops.set_incidence(ei, ip, ie)
+        dg, rdg = getattr(self, "deg_t", None), getattr(self, "inv_deg_t", None)
+        if torch.is_tensor(dg) and dg.is_cuda and torch.is_tensor(rdg):
+            dg._hlhgat_rcp = rdg  # ops.reciprocal(deg_t) without a launch
         if torch.is_tensor(ei) and ei.is_cuda:
             for kv in ("n_valid_t", "n_valid_s"):
                 nv = getattr(self, kv, None)
@@ -306,6 +309,20 @@ def incidence_csr(edge_index, n_nodes: int) -> Tuple[torch.Tensor, torch.Tensor]
             torch.from_numpy((keys % E if E else keys).astype(np.int32)))
 
 
+def node_degree(inc_rowptr: torch.Tensor, valid: Optional[int] = None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """degree(edge_index.view(-1), N_t) (lib/Hodge_Cheb_Conv.py:359, the D of
+    NodeEdgeInt) from the incidence CSR, and its fp32 reciprocal (1/0 = inf
+    as on the device); rows >= valid (padding) get degree 1."""
+    rp = np.asarray(inc_rowptr, dtype=np.int64)
+    d = (rp[1:] - rp[:-1]).astype(np.float32)
+    if valid is not None:
+        d[valid:] = 1.0
+    with np.errstate(divide="ignore"):
+        r = np.float32(1.0) / d
+    return torch.from_numpy(d), torch.from_numpy(r.astype(np.float32))
+
+
 def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     """PyG-free equivalent of DataLoader collation for PairData
     (offsets from PairData.__inc__, lib/Hodge_Dataset.py:40-48)."""
@@ -365,6 +382,7 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     ei = getattr(b, "edge_index", None)
     if torch.is_tensor(ei) and torch.is_tensor(getattr(b, "x_t", None)):
         b.inc_rowptr, b.inc_eids = incidence_csr(ei, b.x_t.size(0))
+        b.deg_t, b.inv_deg_t = node_degree(b.inc_rowptr)
     # graph segment offsets of the readout (global_mean_pool over the
     # graph-contiguous rows, lib/Hodge_ST_Model.py:636), built here once
     # instead of by four small device ops per pool in every step
@@ -512,6 +530,8 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
         out.edge_index = torch.cat([b.edge_index, torch.stack([nodes, nodes])], 1)
         if getattr(b, "inc_rowptr", None) is not None:
             out.inc_rowptr, out.inc_eids = incidence_csr(out.edge_index, Rt)
+            # padding nodes: unit degree (the model's masked_fill, no 1/0)
+            out.deg_t, out.inv_deg_t = node_degree(out.inc_rowptr, valid=nt)
     for side, n, R, per_row in (("t", nt, Rt, pr_t), ("s", ns, Rs, pr_s)):
         o = getattr(b, "row_order_" + side, None)
         if o is not None:

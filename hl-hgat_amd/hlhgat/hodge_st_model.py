@@ -112,9 +112,11 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
             # (:624); that equals N_t whenever it does not crash (1/D broadcast
             # over x_t rows), so size it by N_t and skip the host sync of max()
             p1 = adj2par1(data.edge_index, n_t, n_s)
-            d = degree(data.edge_index.view(-1), num_nodes=n_t)
-            if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
-                d = d.masked_fill(~valid_t, 1.0)
+            d = getattr(data, "deg_t", None)  # built at collate (padding rows: 1)
+            if d is None or d.device != x_t.device or d.numel() != n_t:
+                d = degree(data.edge_index.view(-1), num_nodes=n_t)
+                if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
+                    d = d.masked_fill(~valid_t, 1.0)
             if not x_t.is_cuda:
                 return p1, d, []
             inc = p1.incidence()  # built here, cached for every NodeEdgeInt

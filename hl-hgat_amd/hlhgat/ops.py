@@ -242,6 +242,9 @@ def reciprocal(D: torch.Tensor) -> torch.Tensor:
     Gradients do not flow into D (the reference's D is an integer count)."""
     if D.requires_grad:
         return (1 / D).view(-1)
+    pre = getattr(D, "_hlhgat_rcp", None)  # built with the batch (hodge_dataset.node_degree)
+    if pre is not None and pre.shape == D.shape and pre.device == D.device:
+        return pre.view(-1)
     hit = _RCP_CACHE.get([D], None)
     if hit is not None:
         return hit

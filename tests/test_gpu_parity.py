@@ -335,6 +335,15 @@ def test_collate_incidence_equals_device_build(cuda):
         inc = ops.incidence(bd.edge_index, n)
         assert inc.rowptr.data_ptr() == bd.inc_rowptr.data_ptr()
         assert torch.equal(inc.rowptr, built.rowptr) and torch.equal(inc.edge_ids, built.edge_ids)
+        # the degree D and its reciprocal built with the batch: the device ops' bits
+        from hlhgat.hodge_dataset import degree
+        d = degree(bd.edge_index.view(-1), num_nodes=n)
+        vm = getattr(bd, "valid_mask_t", None)
+        if vm is not None:
+            d = d.masked_fill(~vm, 1.0)
+        assert torch.equal(bd.deg_t, d)
+        assert torch.equal(ops.reciprocal(bd.deg_t), (1 / d).view(-1))
+        assert ops.reciprocal(bd.deg_t).data_ptr() == bd.inv_deg_t.data_ptr()
 
 
 def test_segment_and_cluster_mean(cuda):

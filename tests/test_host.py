@@ -228,6 +228,12 @@ def test_incidence_csr_host_build():
         for v in range(n):
             want = sorted(np.nonzero(ei[0] == v)[0].tolist() + np.nonzero(ei[1] == v)[0].tolist())
             assert eids[rp[v]:rp[v + 1]].tolist() == want, v
+    from hlhgat.hodge_dataset import degree
+    d = degree(b.edge_index.reshape(-1), num_nodes=b.x_t.shape[0])
+    assert torch.equal(b.deg_t, d) and torch.equal(b.inv_deg_t, 1 / d)
+    p = pad_batch(b, static_caps(b, 128))
+    dp = degree(p.edge_index.reshape(-1), num_nodes=p.x_t.shape[0]).masked_fill(~p.valid_mask_t, 1)
+    assert torch.equal(p.deg_t, dp) and torch.equal(p.inv_deg_t, 1 / dp)
     rp, eids = incidence_csr(np.zeros((2, 0), dtype=np.int64), 3)
     assert rp.tolist() == [0, 0, 0, 0] and eids.numel() == 0
     with pytest.raises(ValueError):
