@@ -472,7 +472,7 @@ def main():
     batches, caps, real_rows = make_batches(args.batches, rank, device)  # each rank: its own
     torch.manual_seed(0)
     model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**MODEL_KW).to(device).train()
-    crit = torch.nn.L1Loss()
+    crit = hlhgat.nn.L1Loss()  # torch.nn.L1Loss, one HIP launch each way
 
     def loss_fn(out, b):
         return crit(out.view(-1, 1), b.y.view(-1, 1))

@@ -1067,6 +1067,18 @@ int data_xcd_map() {
   return v;
 }
 
+// Data-gradient tiles of 64 columns (TN 4) where the size rule picks more
+// than one 16-column tile: each staged dC row block serves 64 output columns
+// (+1.3 % at the ZINC step, same-box A/B); HLHGAT_BWD_TND=2 restores the
+// 32-column tiles (same results either way)
+int bwd_tnd() {
+  static int v = [] {
+    const char* e = getenv("HLHGAT_BWD_TND");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 bool vec_ok(const float* p, int64_t ld, int64_t kb) {
   return aligned16(p) && (ld % 4) == 0 && (kb % 4) == 0;
 }
@@ -1074,8 +1086,18 @@ bool vec_ok(const float* p, int64_t ld, int64_t kb) {
 // 16-column tiles per wave of the forward: enough waves to cover the 1024
 // SIMDs several times over (measured at the HL-HGAT shapes, tools/kbench.py):
 // small M -> 1, K <= 256 -> 2 (re-reading A from L2 is cheap), long K -> 4
+// HLHGAT_FWD_TN4_K: reduction length from which the forward takes 64-column
+// tiles (A/B; same results)
+int64_t fwd_tn4_k() {
+  static int64_t v = [] {
+    const char* e = getenv("HLHGAT_FWD_TN4_K");
+    return e ? (int64_t)atoll(e) : (int64_t)256;
+  }();
+  return v;
+}
+
 int fwd_tn(int64_t M, int64_t N, int64_t ktot) {
-  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
+  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= fwd_tn4_k() ? 4 : 2);
   if (N <= 16) tn = 1;
   else if (N <= 32 && tn > 2) tn = 2;
   return tn;
@@ -1172,6 +1194,7 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   int64_t ktot = 0;
   for (int b = 0; b < nblocks; ++b) ktot += kb[b];
   int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // see proj_fwd
+  if (tnd == 2 && bwd_tnd() == 4) tnd = TN;
   a.tile_start[0] = 0;
   for (int b = 0; b < nblocks; ++b) {
     HLH_CHECK_ARG(W[b] && dA[b] && kb[b] > 0 && ldw[b] >= kb[b] && ldda[b] >= kb[b],
@@ -1371,6 +1394,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   int64_t ktot = 0;
   for (int b = 0; b < nb_d; ++b) ktot += kb_d[b];
   int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // as hlhgat_proj_bwd_data
+  if (tnd == 2 && bwd_tnd() == 4) tnd = 4;
   d.tile_start[0] = 0;
   for (int b = 0; b < nb_d; ++b) {
     HLH_CHECK_ARG(W[b] && dA[b] && kb_d[b] > 0 && ldw[b] >= kb_d[b] && ldda[b] >= kb_d[b],
@@ -1405,8 +1429,10 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
   if (tnd == 1)
     launch(k_proj_bwd_fused<1>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
-  else
+  else if (tnd == 2)
     launch(k_proj_bwd_fused<2>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else
+    launch(k_proj_bwd_fused<4>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;

@@ -408,3 +408,59 @@ extern "C" int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg,
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
+
+// --- L1 loss (torch.nn.L1Loss, reduction "mean") ------------------------------
+// The regression loss of the ZINC training loop: torch runs it as sub / abs /
+// mean and the backward as five more elementwise launches, all on the step's
+// critical path between the forward and the backward.  Here one launch each:
+//   forward  loss = sum |x - y| / n  (one workgroup, fixed summation order);
+//   backward dx = (g / n) * sgn(x - y), the arithmetic of torch's MeanBackward
+//            (g / n) followed by AbsBackward (grad * sgn): bitwise torch's dx.
+namespace {
+__global__ __launch_bounds__(256) void k_l1_loss_fwd(const float* __restrict__ x,
+                                                     const float* __restrict__ y, int64_t n,
+                                                     float* __restrict__ loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += fabsf(x[i] - y[i]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / (float)n;
+}
+
+__global__ __launch_bounds__(256) void k_l1_loss_bwd(const float* __restrict__ x,
+                                                     const float* __restrict__ y, int64_t n,
+                                                     const float* __restrict__ gout,
+                                                     float* __restrict__ dx) {
+  const float q = gout[0] / (float)n;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const float d = x[i] - y[i];
+    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);  // torch.sgn: 0 for 0 and NaN
+    dx[i] = q * sg;
+  }
+}
+}  // namespace
+
+extern "C" int hlhgat_l1_loss_fwd(const float* x, const float* y, int64_t n, float* loss,
+                                  void* stream) {
+  HLH_CHECK_ARG(n > 0 && x && y && loss, "l1_loss_fwd: NULL pointer or n <= 0");
+  launch(k_l1_loss_fwd, dim3(1), dim3(256), 0, as_stream(stream), nullptr, x, y, n, loss);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_l1_loss_bwd(const float* x, const float* y, int64_t n, const float* gout,
+                                  float* dx, void* stream) {
+  HLH_CHECK_ARG(n > 0 && x && y && gout && dx, "l1_loss_bwd: NULL pointer or n <= 0");
+  int64_t g = ceil_div(n, 256);
+  if (g > 1024) g = 1024;
+  launch(k_l1_loss_bwd, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, x, y, n,
+         gout, dx);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}

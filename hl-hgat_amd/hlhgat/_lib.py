@@ -96,6 +96,8 @@ SIGNATURES = {
                                     c_vp]),
     "hlhgat_adam_flat": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f64, c_f64, c_f64,
                                  c_f64, c_f64, c_vp]),
+    "hlhgat_l1_loss_fwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hlhgat_l1_loss_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "hlhgat_group_begin": (c_i32, []),
     "hlhgat_group_next": (c_i32, []),
     "hlhgat_group_end": (c_i32, [c_vp, c_vp]),

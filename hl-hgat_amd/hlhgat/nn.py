@@ -16,7 +16,7 @@ from typing import Callable, List, Sequence, Tuple, Union
 import torch
 import torch.nn as tnn
 
-__all__ = ["Sequential", "BatchNorm", "Linear", "glorot", "global_mean_pool"]
+__all__ = ["Sequential", "BatchNorm", "Linear", "L1Loss", "glorot", "global_mean_pool"]
 
 
 def glorot(t: torch.Tensor) -> None:
@@ -86,6 +86,20 @@ class BatchNorm(tnn.Module):
 
 
 _ARROW = re.compile(r"\s*->\s*")
+
+
+class L1Loss(tnn.L1Loss):
+    """torch.nn.L1Loss (the ZINC training loss) whose mean reduction on ROCm
+    tensors runs as one HIP launch each way (ops.l1_loss: the same input
+    gradient bit for bit).  CPU tensors and other reductions go to torch."""
+
+    def forward(self, input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        if (self.reduction == "mean" and input.is_cuda and input.dtype == torch.float32
+                and input.shape == target.shape and not target.requires_grad
+                and input.numel() > 0):
+            from . import ops
+            return ops.l1_loss(input, target)
+        return super().forward(input, target)
 
 
 def _names(s: str) -> List[str]:

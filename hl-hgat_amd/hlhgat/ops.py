@@ -1360,6 +1360,42 @@ def adam_flat(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
                                float(weight_decay), _stream(param)), "adam_flat")
 
 
+class _L1LossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y):
+        loss = torch.empty((), device=x.device, dtype=torch.float32)
+        check(LIB.hlhgat_l1_loss_fwd(x.data_ptr(), y.data_ptr(), x.numel(), loss.data_ptr(),
+                                     _stream(x)), "l1_loss_fwd")
+        ctx.save_for_backward(x, y)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        g = g.contiguous()
+        dx = torch.empty_like(x)
+        check(LIB.hlhgat_l1_loss_bwd(x.data_ptr(), y.data_ptr(), x.numel(), g.data_ptr(),
+                                     dx.data_ptr(), _stream(x)), "l1_loss_bwd")
+        return dx, None
+
+
+def l1_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """torch.nn.functional.l1_loss(input, target) (mean) in one launch each way
+    (hlhgat_l1_loss_fwd / _bwd): the same input gradient bit for bit; the
+    loss value is the fp32 mean summed in a fixed order.  No gradient flows
+    into target (the regression labels)."""
+    _req_dev(input, "input")
+    if input.shape != target.shape:
+        raise RuntimeError(f"hlhgat: l1_loss shapes differ: {tuple(input.shape)} vs "
+                           f"{tuple(target.shape)}")
+    if target.requires_grad:
+        raise RuntimeError("hlhgat: l1_loss: target must not require grad")
+    if input.numel() == 0:
+        raise RuntimeError("hlhgat: l1_loss of an empty tensor")
+    x = input.contiguous()
+    return _L1LossFn.apply(x, target.to(torch.float32).contiguous())
+
+
 # ----------------------------------------------------------------------------
 # device error word (include/hlhgat.h: hlhgat_device_errors)
 # ----------------------------------------------------------------------------

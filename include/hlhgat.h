@@ -534,6 +534,16 @@ int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg, float* exp
                      int64_t n, float* step, double lr, double beta1, double beta2, double eps,
                      double weight_decay, void* stream);
 
+/* L1 loss, torch.nn.L1Loss(reduction="mean") of the ZINC training loop
+ * (torch's sub / abs / mean and its five backward launches):
+ *   fwd: loss[0] = sum_i |x_i - y_i| / n   (one workgroup, fixed order);
+ *   bwd: dx_i = (gout[0] / n) * sgn(x_i - y_i), torch's MeanBackward then
+ *        AbsBackward arithmetic (sgn(0) = sgn(NaN) = 0): bitwise torch's dx.
+ * gout is a device scalar (the upstream gradient of the loss). */
+int hlhgat_l1_loss_fwd(const float* x, const float* y, int64_t n, float* loss, void* stream);
+int hlhgat_l1_loss_bwd(const float* x, const float* y, int64_t n, const float* gout, float* dx,
+                       void* stream);
+
 /* ---- workspaces --------------------------------------------------------- */
 /* Zero `bytes` (a multiple of 4) at p with a kernel on `stream` (graph-capture
  * safe; used to initialise the BatchNorm workspace counters). */

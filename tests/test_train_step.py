@@ -307,3 +307,29 @@ def test_adam_flat_matches_torch_fused_adam(cuda, wd):
     assert torch.allclose(p, ref.detach(), rtol=1e-6, atol=1e-7)
     assert torch.allclose(m, st["exp_avg"], rtol=1e-5, atol=1e-7)
     assert torch.allclose(v, st["exp_avg_sq"], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_l1_loss_matches_torch(cuda):
+    """hlhgat.nn.L1Loss (hlhgat_l1_loss_fwd / _bwd) against torch.nn.L1Loss:
+    the input gradient bit for bit (zeros, ties and a NaN included), the
+    loss to fp32 rounding."""
+    import hlhgat
+    g = torch.Generator().manual_seed(7)
+    for n in (1, 5, 1000, 4099):
+        x = torch.randn(n, 1, generator=g)
+        y = torch.randn(n, 1, generator=g)
+        if n >= 5:
+            y[:2] = x[:2]  # |x - y| = 0: sgn 0
+        xs = []
+        for crit in (torch.nn.L1Loss(), hlhgat.nn.L1Loss()):
+            xd = x.to(cuda).requires_grad_(True)
+            loss = crit(xd, y.to(cuda))
+            (loss * 3.0).backward()
+            xs.append((loss.detach().cpu(), xd.grad.cpu()))
+        (l0, g0), (l1, g1) = xs
+        assert torch.equal(g0, g1), n
+        assert abs(float(l0) - float(l1)) <= 1e-6 * abs(float(l0)) + 1e-7, (n, float(l0), float(l1))
+    xn = torch.tensor([[float("nan")], [1.0]], device=cuda, requires_grad=True)
+    hlhgat.nn.L1Loss()(xn, torch.zeros(2, 1, device=cuda)).backward()
+    assert xn.grad.cpu().tolist() == [[0.0], [0.5]]
