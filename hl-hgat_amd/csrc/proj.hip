@@ -19,6 +19,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <cstring>
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -919,11 +920,18 @@ struct BwdFusedArgs {
   int d_gx;    // data-gradient grid x
   int n_d;     // data workgroups: d_gx * column tiles
   int d_xcd;   // XCD-aware data order: the column tiles of one row block on one XCD
+  int n_red;   // trailing workgroups: a deferred split reduction of an EARLIER launch
+  ReduceArgs red;
 };
 
 template <int TND>
 __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
   const int L = (int)blk.x;
+  if (L >= a.n_wpad + a.n_d) {
+    const int l = L - a.n_wpad - a.n_d;
+    if (l < a.n_red) reduce_splits_body(a.red, Blk{(unsigned)l, 0u, (unsigned)a.n_red, 1u});
+    return;
+  }
   if (L >= a.n_wpad) {
     const int l = L - a.n_wpad;
     int bx, by;
@@ -1321,11 +1329,36 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
 }
 
 namespace {
+static_assert(sizeof(ReduceArgs) + sizeof(int64_t) <= sizeof(hlhgat_reduce_desc_t),
+              "hlhgat_reduce_desc_t too small");
+
+int64_t reduce_blocks(const ReduceArgs& r) {
+  const int64_t total = r.elem_start[r.nb] + (r.bias_off >= 0 ? r.N : 0);
+  return ceil_div(total, 64);
+}
+
+int run_reduce(const ReduceArgs& r, hipStream_t s) {
+  launch(k_reduce_splits, dim3((unsigned)reduce_blocks(r)), dim3(256), 0, s, nullptr, r);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+constexpr int64_t kDescMagic = 0x686c6872656431LL;  // "hlhred1"
+
 int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w, const float* const* A, const int64_t* lda,
                   const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
                   int nb_d, const float* const* W, const int64_t* ldw, const int64_t* kb_d,
                   float* const* dA, const int64_t* ldda, int accumulate_d, float* workspace,
-                  int64_t workspace_floats, void* stream) {
+                  int64_t workspace_floats, void* stream,
+                  const hlhgat_reduce_desc_t* merge = nullptr,
+                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr) {
+  if (deferred) *deferred = 0;
+  const ReduceArgs* prev = nullptr;
+  if (merge) {
+    HLH_CHECK_ARG(merge->words[0] == kDescMagic, "proj_bwd: merge is not a reduce descriptor");
+    prev = reinterpret_cast<const ReduceArgs*>(&merge->words[1]);
+  }
+  if (group_recording()) defer_out = nullptr;  // launch groups: nothing deferred
   HLH_CHECK_ARG(nb_w >= 0 && nb_w <= MAXB && nb_d >= 0 && nb_d <= MAXB,
                 "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
   HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd: bad dC");
@@ -1340,6 +1373,11 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
+  if (prev && (!fuse || group_recording())) {  // run the merged reduction on its own first
+    const int rc = run_reduce(*prev, as_stream(stream));
+    if (rc != HLHGAT_OK) return rc;
+    prev = nullptr;
+  }
   if (!fuse) {  // the separate launches (any alignment, M == 0, one side only)
     if (want_w) {
       const int rc = hlhgat_proj_bwd_weight(nb_w, dC, lddc, A, lda, kb_w, M, N, dW, lddw, dbias,
@@ -1410,7 +1448,11 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   f.n_wpad = (f.n_w + 7) & ~7;
   f.n_d = f.d_gx * d.tile_start[nb_d];
   f.d_xcd = data_xcd_map();
-  const int64_t n_blocks = (int64_t)f.n_wpad + (int64_t)f.n_d;
+  if (prev) {
+    f.red = *prev;
+    f.n_red = (int)reduce_blocks(*prev);
+  }
+  const int64_t n_blocks = (int64_t)f.n_wpad + (int64_t)f.n_d + (int64_t)f.n_red;
   HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
   hipStream_t s = as_stream(stream);
   // algorithmic flops of the launch: weight gradient 2 M N sum(kb_w) + data
@@ -1440,12 +1482,35 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   r.bias_off = p.bias_off;
   r.dbias = dbias;
   r.accumulate = 0;
-  const int64_t total = r.elem_start[nb_w] + (dbias ? N : 0);
-  launch(k_reduce_splits, dim3((unsigned)ceil_div(total, 64)), dim3(256), 0, s, nullptr, r);
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
+  if (defer_out) {
+    memset(defer_out, 0, sizeof(*defer_out));
+    defer_out->words[0] = kDescMagic;
+    memcpy(&defer_out->words[1], &r, sizeof(r));
+    if (deferred) *deferred = 1;
+    return HLHGAT_OK;
+  }
+  return run_reduce(r, s);
 }
 }  // namespace
+
+extern "C" int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int64_t lddc,
+                                     int nb_w, const float* const* A, const int64_t* lda,
+                                     const int64_t* kb_w, float* const* dW, const int64_t* lddw,
+                                     float* dbias, int nb_d, const float* const* W,
+                                     const int64_t* ldw, const int64_t* kb_d, float* const* dA,
+                                     const int64_t* ldda, int accumulate_d, float* workspace,
+                                     int64_t workspace_floats, const hlhgat_reduce_desc_t* merge,
+                                     hlhgat_reduce_desc_t* defer_out, int* deferred,
+                                     void* stream) {
+  return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
+                       dA, ldda, accumulate_d, workspace, workspace_floats, stream, merge,
+                       defer_out, deferred);
+}
+
+extern "C" int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream) {
+  HLH_CHECK_ARG(desc && desc->words[0] == kDescMagic, "reduce_run: not a reduce descriptor");
+  return run_reduce(*reinterpret_cast<const ReduceArgs*>(&desc->words[1]), as_stream(stream));
+}
 
 extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
                                int nb_w, const float* const* A, const int64_t* lda,

@@ -20,8 +20,10 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <algorithm>
+#include <mutex>
 #include <optional>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/hlhgat.h"
@@ -221,11 +223,14 @@ struct BucketEntry {
   int64_t offset;
   int64_t numel;
   bool claimed;
+  bool double_use = false;  // claimed twice in one backward (a parameter used twice)
 };
 std::unordered_map<const void*, BucketEntry>& bucket() {
   static auto* m = new std::unordered_map<const void*, BucketEntry>();
   return *m;
 }
+
+void double_claim_hook(const BucketEntry& e);
 
 Tensor grad_like(const Tensor& p) {
   if (!p.defined()) return Tensor();
@@ -235,6 +240,10 @@ Tensor grad_like(const Tensor& p) {
       it->second.flat.device() == p.device()) {
     it->second.claimed = true;
     return it->second.flat.narrow(0, it->second.offset, p.numel()).view(p.sizes());
+  }
+  if (it != m.end() && it->second.claimed) {
+    it->second.double_use = true;  // never deferred again (deferred_ok)
+    double_claim_hook(it->second);
   }
   return at::empty(p.sizes(), p.options());
 }
@@ -249,6 +258,15 @@ void grad_bucket_set(std::vector<Tensor> params, Tensor flat_grad, std::vector<i
 }
 void grad_bucket_begin() {
   for (auto& kv : bucket()) kv.second.claimed = false;
+}
+// the bucket entry whose gradient region starts at p (nullptr: not in the bucket)
+const BucketEntry* bucket_entry_at(const void* p) {
+  for (const auto& kv : bucket()) {
+    const auto& e = kv.second;
+    if (static_cast<const char*>(e.flat.data_ptr()) + e.offset * e.flat.element_size() == p)
+      return &e;
+  }
+  return nullptr;
 }
 void grad_bucket_clear() { bucket().clear(); }
 
@@ -289,6 +307,96 @@ bool& fused_bwd_flag() {
 void set_fused_bwd(bool on) { fused_bwd_flag() = on; }
 
 
+// ---------------------------------------------------------------------------
+// Deferred split reductions (hlhgat_proj_bwd_defer; hlhgat.train.TrainStep
+// turns this on around its backward): a Linear backward whose gradients land
+// in the gradient bucket hands its split reduction to the NEXT Linear
+// backward on the same stream, which runs it as extra workgroups of its own
+// launch, so each backward chain loses one dependent launch per layer.  The
+// last one per stream is launched by reduce_flush() after the backward,
+// before anything reads the bucket.  Only bucket destinations are deferred:
+// autograd adopts those views without reading them (AccumulateGrad steals),
+// and nothing else reads the bucket before the flush.
+// ---------------------------------------------------------------------------
+struct PendingReduce {
+  hlhgat_reduce_desc_t desc;
+  Tensor ws;  // the split slab the reduction reads: alive until it has run
+  void* stream = nullptr;
+};
+struct DeferState {
+  bool on = false;
+  std::mutex mu;
+  std::unordered_map<void*, PendingReduce> pending;  // by stream
+  std::unordered_set<const void*> dests;             // deferred gradient destinations
+  bool violation = false;  // a deferred destination was claimed a second time
+};
+DeferState& defer_state() {
+  static auto* d = new DeferState();
+  return *d;
+}
+
+// a destination that may be deferred: a bucket region of a parameter that is
+// not used twice (a second use adds into .grad through AccumulateGrad, which
+// must not run before the deferred reduction; TrainStep's first, eager step
+// runs without deferral and finds those parameters)
+bool deferred_ok(const void* p) {
+  if (!p) return true;
+  const BucketEntry* e = bucket_entry_at(p);
+  return e && !e->double_use;
+}
+
+void double_claim_hook(const BucketEntry& e) {
+  auto& d = defer_state();
+  std::lock_guard<std::mutex> g(d.mu);
+  const void* p = static_cast<const char*>(e.flat.data_ptr()) + e.offset * e.flat.element_size();
+  if (d.on && d.dests.count(p)) d.violation = true;
+}
+
+void reduce_defer(bool on) {
+  auto& d = defer_state();
+  std::lock_guard<std::mutex> g(d.mu);
+  TORCH_CHECK(d.pending.empty(), "hlhgat: reduce_defer: split reductions still pending "
+                                 "(call reduce_flush first)");
+  d.on = on;
+  d.dests.clear();
+  d.violation = false;
+}
+
+// Run every pending reduction on the current stream (after its own stream's
+// work); returns the gradient destinations that were deferred this backward.
+std::vector<int64_t> reduce_flush(int64_t device) {
+  auto& d = defer_state();
+  std::lock_guard<std::mutex> g(d.mu);
+  auto main = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device);
+  static std::vector<hipEvent_t> events;  // reused: recorded and waited at once
+  size_t k = 0;
+  for (auto& kv : d.pending) {
+    if (kv.second.stream != (void*)main.stream()) {
+      if (k == events.size()) {
+        events.emplace_back();
+        TORCH_CHECK(hipEventCreateWithFlags(&events.back(), hipEventDisableTiming) == hipSuccess,
+                    "hlhgat: hipEventCreate");
+      }
+      hipEvent_t e = events[k++];
+      TORCH_CHECK(hipEventRecord(e, (hipStream_t)kv.second.stream) == hipSuccess,
+                  "hlhgat: hipEventRecord");
+      TORCH_CHECK(hipStreamWaitEvent(main.stream(), e, 0) == hipSuccess,
+                  "hlhgat: hipStreamWaitEvent");
+    }
+    chk(hlhgat_reduce_run(&kv.second.desc, main.stream()), "reduce_run");
+    kv.second.ws.record_stream(main);
+  }
+  d.pending.clear();
+  std::vector<int64_t> out;
+  for (const void* p : d.dests) out.push_back(reinterpret_cast<int64_t>(p));
+  d.dests.clear();
+  const bool bad = d.violation;
+  d.violation = false;
+  TORCH_CHECK(!bad, "hlhgat: a parameter whose split reduction was deferred received a second "
+                    "gradient in the same backward (set HLHGAT_DEFER_REDUCE=0)");
+  return out;
+}
+
 // weight (+bias) and data gradients of one Linear: hlhgat_proj_bwd (weight
 // partials and data gradient in one launch, then the split reduction)
 void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
@@ -302,10 +410,29 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   const int64_t wsf =
       nbw ? hlhgat_proj_bwd_weight_workspace_floats(nbw, kbw.data(), M, N, db != nullptr) : 0;
   Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
-  chk(hlhgat_proj_bwd(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(), kbw.data(),
-                      dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(), kbd.data(),
-                      dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(), wsf, s),
+  auto& d = defer_state();
+  std::unique_lock<std::mutex> g(d.mu);
+  bool defer = d.on && nbw > 0 && !keep_list() && deferred_ok(db);
+  for (int b = 0; b < nbw && defer; ++b) defer = deferred_ok(dW[b]);
+  auto it = d.pending.find(s);
+  PendingReduce prev;
+  const bool merge = it != d.pending.end();
+  if (merge) {
+    prev = it->second;
+    d.pending.erase(it);
+  }
+  hlhgat_reduce_desc_t out;
+  int deferred = 0;
+  chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
+                            kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(),
+                            kbd.data(), dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(), wsf,
+                            merge ? &prev.desc : nullptr, defer ? &out : nullptr, &deferred, s),
       "proj_bwd");
+  if (deferred) {
+    d.pending[s] = PendingReduce{out, ws, s};
+    for (int b = 0; b < nbw; ++b) d.dests.insert(dW[b]);
+    if (db) d.dests.insert(db);
+  }
 }
 
 void proj_bwd_data(const Tensor& G, const std::vector<const float*>& W,
@@ -2201,6 +2328,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_bucket_set", &grad_bucket_set);
   m.def("grad_bucket_begin", &grad_bucket_begin);
   m.def("grad_bucket_clear", &grad_bucket_clear);
+  m.def("reduce_defer", &reduce_defer);
+  m.def("reduce_flush", &reduce_flush);
   m.def("node_from_edges", &node_from_edges);
   m.def("edge_from_nodes", &edge_from_nodes);
   m.def("version", []() { return hlhgat_version(); });

@@ -70,6 +70,10 @@ SIGNATURES = {
     "hlhgat_proj_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_i32, P_vp, P_i64, P_i64, P_vp,
                                 P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64, c_i32,
                                 c_vp, c_i64, c_vp]),
+    "hlhgat_proj_bwd_defer": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_i32, P_vp, P_i64, P_i64,
+                                      P_vp, P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64,
+                                      c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "hlhgat_reduce_run": (c_i32, [c_vp, c_vp]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
     "hlhgat_get_bn_one_launch": (c_i32, []),
     "hlhgat_set_bn_poll_limit": (c_i32, [C.c_uint32]),

@@ -36,6 +36,9 @@ __all__ = ["TrainStep", "batch_key"]
 # HLHGAT_HIP_ADAM=0: torch's fused Adam instead of hlhgat_adam_flat (A/B)
 import os as _os  # noqa: E402
 HIP_ADAM = _os.environ.get("HLHGAT_HIP_ADAM", "1") != "0"
+# HLHGAT_DEFER_REDUCE=0: every Linear backward launches its own split
+# reduction instead of handing it to the next one on its stream (A/B)
+DEFER_REDUCE = _os.environ.get("HLHGAT_DEFER_REDUCE", "1") != "0"
 
 
 def _tensor_items(batch):
@@ -144,22 +147,37 @@ class TrainStep:
         self._pool = None
         self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
+        self._fwd_bwd_calls = 0
 
     # -- the step ---------------------------------------------------------
     def _fwd_bwd(self, batch) -> torch.Tensor:
         self.flat_grad.zero_()
+        # deferred split reductions (torch_ext.cpp): not in the first step,
+        # which finds the parameters used twice (those are never deferred)
+        defer = self._ext is not None and DEFER_REDUCE and self._fwd_bwd_calls > 0
+        self._fwd_bwd_calls += 1
         if self._ext is not None:
             for p in self.params:
                 p.grad = None
             self._ext.grad_bucket_begin()
-        out = self.model(batch)
-        loss = self.loss_fn(out, batch)
-        loss.backward()
+        dests = []
+        if defer:
+            self._ext.reduce_defer(True)
+        try:
+            out = self.model(batch)
+            loss = self.loss_fn(out, batch)
+            loss.backward()
+        finally:
+            if defer:
+                # the last reduction of each stream, before anything reads the bucket
+                dests = self._ext.reduce_flush(self.device.index if self.device.index is not None
+                                               else torch.cuda.current_device())
+                self._ext.reduce_defer(False)
         if self._ext is not None:
-            self._adopt_grads()
+            self._adopt_grads(set(dests))
         return loss.detach()
 
-    def _adopt_grads(self) -> None:
+    def _adopt_grads(self, deferred=frozenset()) -> None:
         """Every p.grad must be its flat_grad view: gradients produced outside
         the bucket (torch ops) are copied in; missing ones stay zero."""
         base = self.flat_grad.data_ptr()
@@ -169,6 +187,9 @@ class TrainStep:
             if g is None:
                 p.grad = view
             elif g.data_ptr() != base + 4 * off:
+                if base + 4 * off in deferred:
+                    raise RuntimeError("TrainStep: a gradient whose split reduction was deferred "
+                                       "was copied before it ran (set HLHGAT_DEFER_REDUCE=0)")
                 view.copy_(g)
                 p.grad = view
 

@@ -357,6 +357,32 @@ int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
                     const int64_t* ldda, int accumulate_d, float* workspace,
                     int64_t workspace_floats, void* stream);
 
+/* Deferred split reduction.  hlhgat_proj_bwd_defer is hlhgat_proj_bwd whose
+ * weight-gradient split reduction may be handed back instead of launched:
+ *   - defer_out != NULL and the one-launch path is taken: the reduction is
+ *     NOT launched; its descriptor goes to *defer_out and *deferred = 1.  The
+ *     caller must keep `workspace` alive and run the descriptor (merge it into
+ *     a later call on the same stream, or hlhgat_reduce_run) before anything
+ *     reads dW / dbias;
+ *   - merge != NULL: a descriptor deferred earlier ON THE SAME STREAM; its
+ *     reduction runs as extra workgroups of this call's launch (or as its own
+ *     launch first when this call cannot take the one-launch path).
+ * The reduction itself is unchanged, so dW / dbias are bitwise those of
+ * hlhgat_proj_bwd; what goes away is one dependent launch per Linear
+ * backward on the stream's chain.  Inside a launch group nothing is deferred. */
+typedef struct {
+  int64_t words[160];
+} hlhgat_reduce_desc_t;
+int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
+                          const float* const* A, const int64_t* lda, const int64_t* kb_w,
+                          float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
+                          const float* const* W, const int64_t* ldw, const int64_t* kb_d,
+                          float* const* dA, const int64_t* ldda, int accumulate_d,
+                          float* workspace, int64_t workspace_floats,
+                          const hlhgat_reduce_desc_t* merge, hlhgat_reduce_desc_t* defer_out,
+                          int* deferred, void* stream);
+int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream);
+
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
  * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge

@@ -164,6 +164,70 @@ def test_stream_fork_is_bitwise_neutral(cuda):
         assert torch.equal(sd0[k], sd1[k]), k
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [False, True])
+def test_deferred_split_reductions_bitwise(cuda, graphs):
+    """Split reductions handed to the next Linear backward on the stream
+    (hlhgat_proj_bwd_defer, TrainStep from its second step on) give the bits
+    of the per-layer launches: losses and every parameter / running
+    statistic after eager and graph-replayed steps, both streams."""
+    from hlhgat import train
+    from hlhgat.synthetic import zinc_like_batch
+    batches = [zinc_like_batch(40, seed=3).to(cuda), zinc_like_batch(33, seed=4).to(cuda)]
+    order = [0, 1, 0, 1, 0]
+    res = []
+    prev = train.DEFER_REDUCE
+    for defer in (False, True):
+        train.DEFER_REDUCE = defer
+        try:
+            res.append(_run(graphs, True, batches, order))
+        finally:
+            train.DEFER_REDUCE = prev
+    (l0, sd0, _), (l1, sd1, _) = res
+    assert l0 == l1
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+
+
+class _Twice(torch.nn.Module):
+    """One HIP Linear applied twice: its weight gets two gradients per step."""
+
+    def __init__(self):
+        super().__init__()
+        import hlhgat
+        self.a = hlhgat.nn.Linear(64, 64)
+        self.b = hlhgat.nn.Linear(64, 1)
+
+    def forward(self, batch):
+        return self.b(torch.relu(self.a(torch.relu(self.a(batch.x)))))
+
+
+@pytest.mark.gpu
+def test_deferred_reduction_skips_parameters_used_twice(cuda):
+    """A parameter used twice is never deferred (its second gradient adds into
+    .grad): TrainStep with deferral equals TrainStep without it."""
+    from hlhgat import train
+    from hlhgat.train import TrainStep
+    g = torch.Generator().manual_seed(2)
+    xb = _B(torch.randn(3000, 64, generator=g).to(cuda), torch.randn(3000, 1, generator=g).to(cuda))
+    res = []
+    prev = train.DEFER_REDUCE
+    for defer in (False, True):
+        train.DEFER_REDUCE = defer
+        try:
+            torch.manual_seed(0)
+            m = _Twice().to(cuda)
+            step = TrainStep(m, lambda o, b: torch.nn.functional.mse_loss(o, b.y), lr=1e-3,
+                             graphs=False)
+            losses = [float(step(xb)) for _ in range(4)]
+            res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+        finally:
+            train.DEFER_REDUCE = prev
+    assert res[0][0] == res[1][0]
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
 # ---------------------------------------------------------------------------
 # GPU: static-shape (padded) batches
 # ---------------------------------------------------------------------------
