@@ -296,8 +296,12 @@ __global__ __launch_bounds__(256) void k_copy2d_batched(CopyArgs a) {
   const int64_t total = a.start[a.n];
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * 256) {
-    int b = 0;
-    while (b + 1 < a.n && e >= a.start[b + 1]) ++b;
+    int lo = 0, hi = a.n - 1;  // the block holding element e (binary search)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (e >= a.start[mid]) lo = mid; else hi = mid - 1;
+    }
+    const int b = lo;
     const int64_t loc = e - a.start[b];
     const int64_t r = loc / a.cols[b], c = loc % a.cols[b];
     a.dst[b][r * a.ldd[b] + c] = a.src[b] ? a.src[b][r * a.lds[b] + c] : 0.f;

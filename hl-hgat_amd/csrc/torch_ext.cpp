@@ -307,6 +307,28 @@ bool& fused_bwd_flag() {
 void set_fused_bwd(bool on) { fused_bwd_flag() = on; }
 
 
+// One launch for a set of strided rectangles (hlhgat_copy2d_batched);
+// src == nullptr zero-fills.
+struct CopyBlocks {
+  std::vector<const float*> src;
+  std::vector<float*> dst;
+  std::vector<int64_t> lds, ldd, rows, cols;
+  void add(const float* s, int64_t ls, float* d, int64_t ld, int64_t r, int64_t c) {
+    src.push_back(s);
+    lds.push_back(ls);
+    dst.push_back(d);
+    ldd.push_back(ld);
+    rows.push_back(r);
+    cols.push_back(c);
+  }
+  void run(void* stream) {
+    if (src.empty()) return;
+    chk(hlhgat_copy2d_batched((int)src.size(), src.data(), lds.data(), dst.data(), ldd.data(),
+                              rows.data(), cols.data(), stream),
+        "copy2d_batched");
+  }
+};
+
 // ---------------------------------------------------------------------------
 // Deferred split reductions (hlhgat_proj_bwd_defer; hlhgat.train.TrainStep
 // turns this on around its backward): a Linear backward whose gradients land
@@ -329,6 +351,11 @@ struct DeferState {
   std::unordered_map<void*, PendingReduce> pending;  // by stream
   std::unordered_set<const void*> dests;             // deferred gradient destinations
   bool violation = false;  // a deferred destination was claimed a second time
+  struct Copies {
+    CopyBlocks cb;
+    std::vector<Tensor> keep;  // the sources, alive until the copies have run
+  };
+  std::unordered_map<void*, Copies> copies;  // by stream
 };
 DeferState& defer_state() {
   static auto* d = new DeferState();
@@ -345,6 +372,25 @@ bool deferred_ok(const void* p) {
   return e && !e->double_use;
 }
 
+// Gradient copies into the bucket (the NodeEdgeInt unpack) joining the
+// deferred work: false (run them now) unless every destination may be deferred.
+bool defer_copies(const CopyBlocks& cb, std::initializer_list<Tensor> dests,
+                  std::initializer_list<Tensor> keep, void* stream) {
+  auto& d = defer_state();
+  std::lock_guard<std::mutex> g(d.mu);
+  if (!d.on || cb.src.empty()) return false;
+  for (const auto& t : dests)
+    if (t.defined() && !deferred_ok(t.data_ptr())) return false;
+  auto& c = d.copies[stream];
+  for (size_t i = 0; i < cb.src.size(); ++i)
+    c.cb.add(cb.src[i], cb.lds[i], cb.dst[i], cb.ldd[i], cb.rows[i], cb.cols[i]);
+  for (const auto& t : keep)
+    if (t.defined()) c.keep.push_back(t);
+  for (const auto& t : dests)
+    if (t.defined()) d.dests.insert(t.data_ptr());
+  return true;
+}
+
 void double_claim_hook(const BucketEntry& e) {
   auto& d = defer_state();
   std::lock_guard<std::mutex> g(d.mu);
@@ -355,8 +401,8 @@ void double_claim_hook(const BucketEntry& e) {
 void reduce_defer(bool on) {
   auto& d = defer_state();
   std::lock_guard<std::mutex> g(d.mu);
-  TORCH_CHECK(d.pending.empty(), "hlhgat: reduce_defer: split reductions still pending "
-                                 "(call reduce_flush first)");
+  TORCH_CHECK(d.pending.empty() && d.copies.empty(),
+              "hlhgat: reduce_defer: deferred work still pending (call reduce_flush first)");
   d.on = on;
   d.dests.clear();
   d.violation = false;
@@ -387,6 +433,31 @@ std::vector<int64_t> reduce_flush(int64_t device) {
     kv.second.ws.record_stream(main);
   }
   d.pending.clear();
+  CopyBlocks all;
+  for (auto& kv : d.copies) {
+    if (kv.first != (void*)main.stream()) {
+      if (k == events.size()) {
+        events.emplace_back();
+        TORCH_CHECK(hipEventCreateWithFlags(&events.back(), hipEventDisableTiming) == hipSuccess,
+                    "hlhgat: hipEventCreate");
+      }
+      hipEvent_t e = events[k++];
+      TORCH_CHECK(hipEventRecord(e, (hipStream_t)kv.first) == hipSuccess, "hlhgat: hipEventRecord");
+      TORCH_CHECK(hipStreamWaitEvent(main.stream(), e, 0) == hipSuccess,
+                  "hlhgat: hipStreamWaitEvent");
+    }
+    const auto& c = kv.second.cb;
+    for (size_t i = 0; i < c.src.size(); ++i) {
+      if (all.src.size() == (size_t)HLHGAT_MAX_COPY_BLOCKS) {
+        all.run(main.stream());
+        all = CopyBlocks();
+      }
+      all.add(c.src[i], c.lds[i], c.dst[i], c.ldd[i], c.rows[i], c.cols[i]);
+    }
+    for (auto& t : kv.second.keep) t.record_stream(main);
+  }
+  all.run(main.stream());
+  d.copies.clear();
   std::vector<int64_t> out;
   for (const void* p : d.dests) out.push_back(reinterpret_cast<int64_t>(p));
   d.dests.clear();
@@ -1520,31 +1591,55 @@ int64_t fork_side_stream(int64_t device) {
   return reinterpret_cast<int64_t>(Fork::side_of((int)device).stream());
 }
 
-// One launch for a set of strided rectangles (hlhgat_copy2d_batched);
-// src == nullptr zero-fills.
-struct CopyBlocks {
-  std::vector<const float*> src;
-  std::vector<float*> dst;
-  std::vector<int64_t> lds, ldd, rows, cols;
-  void add(const float* s, int64_t ls, float* d, int64_t ld, int64_t r, int64_t c) {
-    src.push_back(s);
-    lds.push_back(ls);
-    dst.push_back(d);
-    ldd.push_back(ld);
-    rows.push_back(r);
-    cols.push_back(c);
-  }
-  void run(void* stream) {
-    if (src.empty()) return;
-    chk(hlhgat_copy2d_batched((int)src.size(), src.data(), lds.data(), dst.data(), ldd.data(),
-                              rows.data(), cols.data(), stream),
-        "copy2d_batched");
-  }
-};
-
 struct SideMlp {  // [W0, b0, g1, be1, rm1, rv1, nbt1, W3, b3, g4, be4, rm4, rv4, nbt4]
   Tensor h1, a1, m1, i1, h2, y, m4, i4;
 };
+
+// Wt = [Wn_b; We_a], Ws = [We_b; Wn_a], bt = [b_n; 0], bs = [b_e; 0]
+// (W0 = [W_a | W_b], lib/Hodge_Cheb_Conv.py:307-308) into one flat tensor
+// [Wt | Ws | bt | bs]: both sides' first Linear on x_t (x_s) is ONE GEMM.
+void pack_nei(CopyBlocks& cb, const Tensor& Wn, const Tensor& bn0, const Tensor& We,
+              const Tensor& be0, int64_t d, int64_t dn, int64_t de, Tensor& pk) {
+  const int64_t P = dn + de;
+  float* base = pk.data_ptr<float>();
+  float *Wt = base, *Ws = base + P * d, *bt = base + 2 * P * d, *bs = bt + P;
+  const float *pwn = Wn.data_ptr<float>(), *pwe = We.data_ptr<float>();
+  cb.add(pwn + d, Wn.stride(0), Wt, d, dn, d);
+  cb.add(pwe, We.stride(0), Wt + dn * d, d, de, d);
+  cb.add(pwe + d, We.stride(0), Ws, d, de, d);
+  cb.add(pwn, Wn.stride(0), Ws + de * d, d, dn, d);
+  cb.add(bn0.data_ptr<float>(), dn, bt, dn, 1, dn);
+  cb.add(nullptr, 0, bt + dn, de, 1, de);
+  cb.add(be0.data_ptr<float>(), de, bs, de, 1, de);
+  cb.add(nullptr, 0, bs + de, dn, 1, dn);
+}
+
+// Every NodeEdgeInt's pack of one forward in one launch (hlhgat.ops.nei_prepack):
+// groups[i] = {W0n, b0n, W0e, b0e}.
+std::vector<Tensor> nei_prepack(std::vector<std::vector<Tensor>> groups) {
+  std::vector<Tensor> out;
+  CopyBlocks cb;
+  void* s = nullptr;  // the current stream (nullptr is the legacy default stream)
+  for (auto& g : groups) {
+    TORCH_CHECK(g.size() == 4, "hlhgat: nei_prepack: {W0n, b0n, W0e, b0e} per module");
+    Tensor Wn = g[0].stride(1) == 1 ? g[0] : g[0].contiguous();
+    Tensor We = g[2].stride(1) == 1 ? g[2] : g[2].contiguous();
+    Tensor bn0 = g[1].contiguous(), be0 = g[3].contiguous();
+    req(Wn, "W0n");
+    const int64_t d = Wn.size(1) / 2, dn = Wn.size(0), de = We.size(0);
+    TORCH_CHECK(We.size(1) == 2 * d, "hlhgat: nei_prepack: W0n / W0e widths differ");
+    Tensor pk = at::empty({2 * (dn + de) * d + 2 * (dn + de)}, Wn.options());
+    if (cb.src.size() + 8 > (size_t)HLHGAT_MAX_COPY_BLOCKS) {
+      cb.run(stream_of(Wn));
+      cb = CopyBlocks();
+    }
+    pack_nei(cb, Wn, bn0, We, be0, d, dn, de, pk);
+    s = stream_of(Wn);
+    out.push_back(pk);
+  }
+  if (!groups.empty()) cb.run(s);
+  return out;
+}
 
 // The DenseConcat gradient slab's host flag: 0 until a gradient has landed
 // in the slab.  Returns the accumulate mode for this writer and marks the
@@ -1567,7 +1662,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                                at::TensorList pe, double mom1n, double eps1n, double mom4n,
                                double eps4n, double mom1e, double eps1e, double mom4e,
                                double eps4e, OptT valid_t, OptT valid_s, OptT gsink_t,
-                               OptT gsink_s, OptT gflag_t, OptT gflag_s) {
+                               OptT gsink_s, OptT gflag_t, OptT gflag_s, OptT packed) {
     req(x_t, "x_t");
     req(x_s, "x_s");
     TORCH_CHECK(pn.size() == 14 && pe.size() == 14, "hlhgat: nei_value expects 14+14 params");
@@ -1584,22 +1679,24 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     Tensor Wn = W0n.stride(1) == 1 ? W0n : W0n.contiguous();
     Tensor We = W0e.stride(1) == 1 ? W0e : W0e.contiguous();
     Tensor bn0 = pn[1].contiguous(), be0 = pe[1].contiguous();
-    Tensor Wt = at::empty({dn + de, d}, xt.options());
-    Tensor Ws = at::empty({de + dn, d}, xt.options());
-    Tensor bt = at::empty({dn + de}, xt.options());
-    Tensor bs = at::empty({de + dn}, xt.options());
-    {
+    const int64_t P = dn + de;
+    Tensor Wt, Ws, bt, bs;
+    if (has(packed)) {  // built for the whole forward by nei_prepack
+      TORCH_CHECK(packed->numel() == 2 * P * d + 2 * P && packed->is_contiguous(),
+                  "hlhgat: nei_value: packed weights have the wrong size");
+      Wt = packed->narrow(0, 0, P * d).view({P, d});
+      Ws = packed->narrow(0, P * d, P * d).view({P, d});
+      bt = packed->narrow(0, 2 * P * d, P);
+      bs = packed->narrow(0, 2 * P * d + P, P);
+    } else {
+      Tensor pk = at::empty({2 * P * d + 2 * P}, xt.options());
       CopyBlocks cb;
-      const float *pwn = Wn.data_ptr<float>(), *pwe = We.data_ptr<float>();
-      cb.add(pwn + d, Wn.stride(0), Wt.data_ptr<float>(), d, dn, d);
-      cb.add(pwe, We.stride(0), Wt.data_ptr<float>() + dn * d, d, de, d);
-      cb.add(pwe + d, We.stride(0), Ws.data_ptr<float>(), d, de, d);
-      cb.add(pwn, Wn.stride(0), Ws.data_ptr<float>() + de * d, d, dn, d);
-      cb.add(bn0.data_ptr<float>(), dn, bt.data_ptr<float>(), dn, 1, dn);
-      cb.add(nullptr, 0, bt.data_ptr<float>() + dn, de, 1, de);
-      cb.add(be0.data_ptr<float>(), de, bs.data_ptr<float>(), de, 1, de);
-      cb.add(nullptr, 0, bs.data_ptr<float>() + de, dn, 1, dn);
+      pack_nei(cb, Wn, bn0, We, be0, d, dn, de, pk);
       cb.run(stream_of(xt));
+      Wt = pk.narrow(0, 0, P * d).view({P, d});
+      Ws = pk.narrow(0, P * d, P * d).view({P, d});
+      bt = pk.narrow(0, 2 * P * d, P);
+      bs = pk.narrow(0, 2 * P * d + P, P);
     }
     Tensor Yt = at::empty({N, dn + de}, xt.options());  // [Qt | P2]
     Tensor Ys = at::empty({E, de + dn}, xt.options());  // [Qs | P1]
@@ -1664,6 +1761,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       em.opt(gsink_s);
       em.opt(gflag_t);
       em.opt(gflag_s);
+      em.opt(packed);
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, E, d, dn, de};
@@ -1698,8 +1796,9 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     Tensor xt = sv[0], xs = sv[1], rowptr = sv[2], eids = sv[3], ei = sv[4], rD = sv[5],
            Wt = sv[6], Ws = sv[7];
     // positions: x_t 0, x_s 1, rowptr 2, eids 3, ei 4, rD 5, pn 6..19, pe 20..33, hyper 34..41,
-    //            valid_t 42, valid_s 43, gsink_t 44, gsink_s 45, gflag_t 46, gflag_s 47
-    variable_list out(48);
+    //            valid_t 42, valid_s 43, gsink_t 44, gsink_s 45, gflag_t 46, gflag_s 47,
+    //            packed 48 (no gradient: the weights' gradients go to pn / pe)
+    variable_list out(49);
     const int64_t PN = 6, PE = 20;
     Tensor dYt = at::empty({N, dn + de}, xt.options());
     Tensor dYs = at::empty({E, de + dn}, xt.options());
@@ -1801,7 +1900,10 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
         out[PE + 1] = grad_like(sv[36]);
         cb.add(dbs.data_ptr<float>(), de, out[PE + 1].data_ptr<float>(), de, 1, de);
       }
-      cb.run(stream_of(xt));
+      // TrainStep: the unpack joins the deferred work flushed after the backward
+      if (!defer_copies(cb, {out[PN], out[PE], out[PN + 1], out[PE + 1]},
+                        {dWt, dWs, dbt, dbs}, stream_of(xt)))
+        cb.run(stream_of(xt));
     }
     (void)d;
     return out;
@@ -1870,11 +1972,11 @@ std::vector<Tensor> nei_value(Tensor x_t, Tensor x_s, Tensor rowptr, Tensor eids
                               double mom1n, double eps1n, double mom4n, double eps4n,
                               double mom1e, double eps1e, double mom4e, double eps4e,
                               OptT valid_t, OptT valid_s, OptT gsink_t, OptT gsink_s,
-                              OptT gflag_t, OptT gflag_s) {
+                              OptT gflag_t, OptT gflag_s, OptT packed) {
   auto r = NEIntValueFn::apply(x_t, x_s, rowptr, eids, ei, rD, at::TensorList(pn),
                                at::TensorList(pe), mom1n, eps1n, mom4n, eps4n, mom1e, eps1e,
                                mom4e, eps4e, valid_t, valid_s, gsink_t, gsink_s, gflag_t,
-                               gflag_s);
+                               gflag_s, packed);
   return {r[0], r[1]};
 }
 
@@ -2325,6 +2427,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);
   m.def("nei_value", &nei_value);
+  m.def("nei_prepack", &nei_prepack);
   m.def("grad_bucket_set", &grad_bucket_set);
   m.def("grad_bucket_begin", &grad_bucket_begin);
   m.def("grad_bucket_clear", &grad_bucket_clear);

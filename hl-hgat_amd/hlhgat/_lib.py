@@ -22,6 +22,8 @@ P_i64 = C.POINTER(c_i64)
 P_f64 = C.POINTER(c_f64)
 P_vp = C.POINTER(c_vp)
 
+MAX_COPY_BLOCKS = 64  # HLHGAT_MAX_COPY_BLOCKS
+
 # name -> (restype, argtypes); mirrors include/hlhgat.h exactly
 SIGNATURES = {
     "hlhgat_version": (c_i32, []),

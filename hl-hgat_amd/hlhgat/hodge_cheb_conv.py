@@ -224,8 +224,10 @@ class NodeEdgeInt(nn.Module):
             bop = _as_boundary(par, x_t.size(0), x_s.size(0))
             # one-shot gradient sinks set by the caller (DenseConcat.grad_sink)
             gsink, self._hlhgat_gsink = getattr(self, "_hlhgat_gsink", (None, None)), (None, None)
+            # one-shot weight pack built for the whole forward (ops.nei_prepack)
+            packed = ops.take_pack(self)
             r = ops.nei_value(x_t, x_s, bop.incidence(), ops.reciprocal(D), self.WV_Node,
-                              self.WV_Edge, bop.valid_t, bop.valid_s, gsink=gsink)
+                              self.WV_Edge, bop.valid_t, bop.valid_s, gsink=gsink, packed=packed)
             if r is not None:
                 return r
         if getattr(par, "valid_t", None) is not None:

@@ -104,6 +104,9 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
             _sink(self.HL_init_conv, dt, ds, self.initial_channel)
         n_t, n_s = x_t.shape[0], x_s.shape[0]
         valid_t = getattr(data, "valid_mask_t", None)
+        if dense:  # every NodeEdgeInt's first-Linear pack in one launch
+            ops.nei_prepack([getattr(self, "NEInt{}{}".format(i, j))
+                             for i, _ in enumerate(self.channels) for j in range(self.channels[i])])
 
         def boundary():
             # the reference rebuilds par_1 and D for every block group (:623-624)

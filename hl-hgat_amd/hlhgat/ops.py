@@ -448,8 +448,8 @@ def copy_words_batched(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor
     multiple of 4, up to HLHGAT_MAX_COPY_BLOCKS per launch
     (hlhgat_copy2d_batched over 4-byte words), on the current stream."""
     n = len(srcs)
-    for i in range(0, n, 8):
-        ss, ds = srcs[i:i + 8], dsts[i:i + 8]
+    for i in range(0, n, _lib.MAX_COPY_BLOCKS):
+        ss, ds = srcs[i:i + _lib.MAX_COPY_BLOCKS], dsts[i:i + _lib.MAX_COPY_BLOCKS]
         words = [t.numel() * t.element_size() // 4 for t in ss]
         m = len(ss)
         check(LIB.hlhgat_copy2d_batched(
@@ -961,10 +961,41 @@ def _mlp2_params(seq: torch.nn.Sequential):
             [float(b1.momentum), float(b1.eps), float(b4.momentum), float(b4.eps)])
 
 
+def nei_prepack(neints) -> None:
+    """Pack the first-Linear weights / biases of every NodeEdgeInt value path
+    in `neints` (hodge_cheb_conv.NodeEdgeInt modules) in ONE launch at the
+    start of the forward, instead of one pack launch inside each NodeEdgeInt
+    on the critical stream; each module consumes its pack once (nei_value)."""
+    mods, groups = [], []
+    for m in (neints if PREPACK else []):
+        pn, pe = _mlp2_params(m.WV_Node), _mlp2_params(m.WV_Edge)
+        if pn is None or pe is None or not pn[0][0].is_cuda:
+            continue
+        mods.append(m)
+        groups.append([pn[0][0], pn[0][1], pe[0][0], pe[0][1]])
+    global _PACK_EPOCH
+    _PACK_EPOCH += 1
+    if not mods:
+        return
+    for m, packed in zip(mods, _ext.nei_prepack(groups)):
+        m._hlhgat_packed = (_PACK_EPOCH, packed)
+
+
+_PACK_EPOCH = 0  # a pack is only used by the forward that built it
+# HLHGAT_PREPACK=0: each NodeEdgeInt packs its own weights (A/B; same results)
+PREPACK = os.environ.get("HLHGAT_PREPACK", "1") != "0"
+
+
+def take_pack(m) -> Optional[torch.Tensor]:
+    """The module's pack from the current forward's nei_prepack, consumed."""
+    p, m._hlhgat_packed = getattr(m, "_hlhgat_packed", None), None
+    return p[1] if p is not None and p[0] == _PACK_EPOCH else None
+
+
 def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.Tensor,
               wv_node: torch.nn.Sequential, wv_edge: torch.nn.Sequential,
               valid_t: Optional[torch.Tensor] = None, valid_s: Optional[torch.Tensor] = None,
-              gsink=(None, None)):
+              gsink=(None, None), packed: Optional[torch.Tensor] = None):
     """NodeEdgeInt value path (lib/Hodge_Cheb_Conv.py:293-295,307-308) as one
     C++ node, first Linear projected before the |B1| gathers (torch_ext.cpp,
     NEIntValueFn); returns (x_t1, x_s1), or None when the WV_* modules are not
@@ -988,7 +1019,7 @@ def nei_value(x_t: torch.Tensor, x_s: torch.Tensor, inc: "Incidence", rD: torch.
         gs = fs = None
     r = _ext.nei_value(x_t, x_s, inc.rowptr, inc.edge_ids, inc.edge_index,
                        rD.contiguous().view(-1), pn[0], pe[0], *pn[1], *pe[1], valid_t, valid_s,
-                       gt, gs, ft, fs)
+                       gt, gs, ft, fs, packed)
     return r[0], r[1]
 
 

@@ -579,7 +579,7 @@ int hlhgat_zero_fill(void* p, size_t bytes, void* stream);
  * dst[b][r*ldd[b] + c] = src[b] ? src[b][r*lds[b] + c] : 0, r < rows[b],
  * c < cols[b].  Packs the NodeEdgeInt first-Linear weights (replaces the
  * torch.cat of lib/Hodge_Cheb_Conv.py:307-308's split weight blocks). */
-#define HLHGAT_MAX_COPY_BLOCKS 8
+#define HLHGAT_MAX_COPY_BLOCKS 64
 int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
                           float* const* dst, const int64_t* ldd, const int64_t* rows,
                           const int64_t* cols, void* stream);

@@ -189,6 +189,28 @@ def test_deferred_split_reductions_bitwise(cuda, graphs):
         assert torch.equal(sd0[k], sd1[k]), k
 
 
+@pytest.mark.gpu
+def test_prepacked_neint_weights_bitwise(cuda):
+    """Every NodeEdgeInt's weight pack built in one launch per forward
+    (ops.nei_prepack) and the gradient unpack deferred to the flush give the
+    bits of the per-module packs: graph-replayed steps."""
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    batches = [zinc_like_batch(40, seed=5).to(cuda), zinc_like_batch(33, seed=6).to(cuda)]
+    res = []
+    prev = ops.PREPACK
+    for pre in (False, True):
+        ops.PREPACK = pre
+        try:
+            res.append(_run(True, True, batches, [0, 1, 0, 1]))
+        finally:
+            ops.PREPACK = prev
+    (l0, sd0, _), (l1, sd1, _) = res
+    assert l0 == l1
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+
+
 class _Twice(torch.nn.Module):
     """One HIP Linear applied twice: its weight gets two gradients per step."""
 
