@@ -269,6 +269,15 @@ const BucketEntry* bucket_entry_at(const void* p) {
   return nullptr;
 }
 void grad_bucket_clear() { bucket().clear(); }
+// parameters whose gradient is not ONE contribution of a HIP node (found by
+// TrainStep's first step): never deferred
+void grad_bucket_no_defer(std::vector<Tensor> params) {
+  auto& m = bucket();
+  for (const auto& p : params) {
+    auto it = m.find(p.data_ptr());
+    if (it != m.end()) it->second.double_use = true;
+  }
+}
 
 // out[M, N] = sum_b A_b W_b^T + bias
 void proj_fwd(const std::vector<const float*>& A, const std::vector<int64_t>& lda,
@@ -2431,6 +2440,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_bucket_set", &grad_bucket_set);
   m.def("grad_bucket_begin", &grad_bucket_begin);
   m.def("grad_bucket_clear", &grad_bucket_clear);
+  m.def("grad_bucket_no_defer", &grad_bucket_no_defer);
   m.def("reduce_defer", &reduce_defer);
   m.def("reduce_flush", &reduce_flush);
   m.def("node_from_edges", &node_from_edges);

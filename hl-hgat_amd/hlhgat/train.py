@@ -168,6 +168,15 @@ class TrainStep:
             loss = self.loss_fn(out, batch)
             loss.backward()
         finally:
+            if self._ext is not None and self._fwd_bwd_calls == 1:
+                # first step: only a parameter whose .grad IS its bucket view
+                # (ONE contribution, a HIP node's view that AccumulateGrad
+                # adopted unread) may have its reduction deferred; a summed,
+                # cloned or torch-produced gradient is never deferred
+                base = self.flat_grad.data_ptr()
+                self._ext.grad_bucket_no_defer(
+                    [p for p, off in zip(self.params, self._offsets)
+                     if p.grad is None or p.grad.data_ptr() != base + 4 * off])
             if defer:
                 # the last reduction of each stream, before anything reads the bucket
                 dests = self._ext.reduce_flush(self.device.index if self.device.index is not None
@@ -187,10 +196,10 @@ class TrainStep:
             if g is None:
                 p.grad = view
             elif g.data_ptr() != base + 4 * off:
-                if base + 4 * off in deferred:
-                    raise RuntimeError("TrainStep: a gradient whose split reduction was deferred "
-                                       "was copied before it ran (set HLHGAT_DEFER_REDUCE=0)")
-                view.copy_(g)
+                if base + 4 * off not in deferred:
+                    view.copy_(g)
+                # else: AccumulateGrad cloned the view before its deferred
+                # reduction ran; the bucket region itself holds the gradient
                 p.grad = view
 
     def _opt_step(self) -> None:

@@ -211,6 +211,58 @@ def test_prepacked_neint_weights_bitwise(cuda):
         assert torch.equal(sd0[k], sd1[k]), k
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["peptides", "cifar", "tsp"])
+def test_deferred_reductions_heads_bitwise(cuda, kind):
+    """The config 3 / 4 / 5 heads (attention pooling, MLGC levels, parameters
+    with torch-op gradients) under TrainStep with and without deferred split
+    reductions: the same losses and parameters, bit for bit."""
+    import hlhgat
+    from hlhgat import train
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph, two_level_batch
+    F = torch.nn.functional
+    if kind == "tsp":
+        raw = [collate([tsp_like_graph(s, n=300)], check_hodge=False) for s in (0, 1)]
+        batches = [b.to(cuda) for b in raw]
+        cls, kw = "HL_HGCNN_TSP_dense_int3_pyr", dict(channels=[2, 2, 2], filters=[16, 32, 32],
+                                                      mlp_channels=[32], K=4)
+
+        def loss_fn(o, d):
+            return F.binary_cross_entropy_with_logits(o[0].view(-1), d.y.view(-1).float())
+    else:
+        raw = [two_level_batch(kind, 6, seed=s) for s in (0, 1)]
+        batches = [[x.to(cuda) for x in b] for b in raw]
+        kw = dict(channels=[1, 1, 1], filters=[16, 32, 32], mlp_channels=[32], pool_loc=1)
+        if kind == "cifar":
+            cls = "HL_HGCNN_CIFAR10SP_dense_int3_attpool"
+            kw.update(K=3, keig=10, l=0.5)
+
+            def loss_fn(o, d):
+                return F.cross_entropy(o, d[0].y.view(-1).long())
+        else:
+            cls = "HL_HGCNN_pepfunc_dense_int3_attpool"
+            kw.update(K=3)
+
+            def loss_fn(o, d):
+                return F.binary_cross_entropy_with_logits(o, d[0].y.view(o.shape).float())
+    res = []
+    prev = train.DEFER_REDUCE
+    for defer in (False, True):
+        train.DEFER_REDUCE = defer
+        try:
+            torch.manual_seed(0)
+            m = getattr(hlhgat, cls)(**kw).to(cuda).train()
+            st = train.TrainStep(m, loss_fn, lr=1e-3, graphs=False)
+            losses = [float(st(batches[i % 2])) for i in range(4)]
+            res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+        finally:
+            train.DEFER_REDUCE = prev
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
 class _Twice(torch.nn.Module):
     """One HIP Linear applied twice: its weight gets two gradients per step."""
 
