@@ -360,6 +360,7 @@ struct DeferState {
   std::unordered_map<void*, PendingReduce> pending;  // by stream
   std::unordered_set<const void*> dests;             // deferred gradient destinations
   bool violation = false;  // a deferred destination was claimed a second time
+  std::unordered_set<void*> streams;  // streams that deferred or merged a reduction
   struct Copies {
     CopyBlocks cb;
     std::vector<Tensor> keep;  // the sources, alive until the copies have run
@@ -400,6 +401,15 @@ bool defer_copies(const CopyBlocks& cb, std::initializer_list<Tensor> dests,
   return true;
 }
 
+// may the gradient of parameter p (not yet claimed in this backward) be deferred?
+bool param_deferrable(const Tensor& p) {
+  if (!p.defined() || !defer_state().on) return false;
+  auto& m = bucket();
+  auto it = m.find(p.data_ptr());
+  return it != m.end() && !it->second.claimed && !it->second.double_use &&
+         it->second.numel == p.numel();
+}
+
 void double_claim_hook(const BucketEntry& e) {
   auto& d = defer_state();
   std::lock_guard<std::mutex> g(d.mu);
@@ -414,6 +424,7 @@ void reduce_defer(bool on) {
               "hlhgat: reduce_defer: deferred work still pending (call reduce_flush first)");
   d.on = on;
   d.dests.clear();
+  d.streams.clear();
   d.violation = false;
 }
 
@@ -425,36 +436,30 @@ std::vector<int64_t> reduce_flush(int64_t device) {
   auto main = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device);
   static std::vector<hipEvent_t> events;  // reused: recorded and waited at once
   size_t k = 0;
-  for (auto& kv : d.pending) {
-    if (kv.second.stream != (void*)main.stream()) {
-      if (k == events.size()) {
-        events.emplace_back();
-        TORCH_CHECK(hipEventCreateWithFlags(&events.back(), hipEventDisableTiming) == hipSuccess,
-                    "hlhgat: hipEventCreate");
-      }
-      hipEvent_t e = events[k++];
-      TORCH_CHECK(hipEventRecord(e, (hipStream_t)kv.second.stream) == hipSuccess,
-                  "hlhgat: hipEventRecord");
-      TORCH_CHECK(hipStreamWaitEvent(main.stream(), e, 0) == hipSuccess,
-                  "hlhgat: hipStreamWaitEvent");
+  // main waits for every stream that deferred, merged or queued copies: a
+  // merged reduction (on its own stream) may feed a copy queued on another
+  std::unordered_set<void*> waits = d.streams;
+  for (auto& kv : d.copies) waits.insert(kv.first);
+  for (void* st : waits) {
+    if (st == (void*)main.stream()) continue;
+    if (k == events.size()) {
+      events.emplace_back();
+      TORCH_CHECK(hipEventCreateWithFlags(&events.back(), hipEventDisableTiming) == hipSuccess,
+                  "hlhgat: hipEventCreate");
     }
+    hipEvent_t e = events[k++];
+    TORCH_CHECK(hipEventRecord(e, (hipStream_t)st) == hipSuccess, "hlhgat: hipEventRecord");
+    TORCH_CHECK(hipStreamWaitEvent(main.stream(), e, 0) == hipSuccess,
+                "hlhgat: hipStreamWaitEvent");
+  }
+  d.streams.clear();
+  for (auto& kv : d.pending) {
     chk(hlhgat_reduce_run(&kv.second.desc, main.stream()), "reduce_run");
     kv.second.ws.record_stream(main);
   }
   d.pending.clear();
   CopyBlocks all;
   for (auto& kv : d.copies) {
-    if (kv.first != (void*)main.stream()) {
-      if (k == events.size()) {
-        events.emplace_back();
-        TORCH_CHECK(hipEventCreateWithFlags(&events.back(), hipEventDisableTiming) == hipSuccess,
-                    "hlhgat: hipEventCreate");
-      }
-      hipEvent_t e = events[k++];
-      TORCH_CHECK(hipEventRecord(e, (hipStream_t)kv.first) == hipSuccess, "hlhgat: hipEventRecord");
-      TORCH_CHECK(hipStreamWaitEvent(main.stream(), e, 0) == hipSuccess,
-                  "hlhgat: hipStreamWaitEvent");
-    }
     const auto& c = kv.second.cb;
     for (size_t i = 0; i < c.src.size(); ++i) {
       if (all.src.size() == (size_t)HLHGAT_MAX_COPY_BLOCKS) {
@@ -484,7 +489,8 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
                    std::vector<float*>& dW, const std::vector<int64_t>& lddw, float* db,
                    const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
                    const std::vector<int64_t>& kbd, std::vector<float*>& dA,
-                   const std::vector<int64_t>& ldda, void* s, int acc_d = 0) {
+                   const std::vector<int64_t>& ldda, void* s, int acc_d = 0,
+                   bool force_defer = false) {
   const int nbw = (int)A.size(), nbd = (int)W.size();
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
@@ -492,9 +498,13 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
   auto& d = defer_state();
   std::unique_lock<std::mutex> g(d.mu);
-  bool defer = d.on && nbw > 0 && !keep_list() && deferred_ok(db);
-  for (int b = 0; b < nbw && defer; ++b) defer = deferred_ok(dW[b]);
-  auto it = d.pending.find(s);
+  // force_defer: private gradient buffers read only by deferred copies (the
+  // NodeEdgeInt unpack), which the flush runs after every reduction
+  bool defer = d.on && nbw > 0 && !keep_list() && (force_defer || deferred_ok(db));
+  for (int b = 0; b < nbw && defer && !force_defer; ++b) defer = deferred_ok(dW[b]);
+  // inside a launch group the launches are issued at the group's end: a
+  // pending reduction stays pending (merged later or run by the flush)
+  auto it = keep_list() ? d.pending.end() : d.pending.find(s);
   PendingReduce prev;
   const bool merge = it != d.pending.end();
   if (merge) {
@@ -508,6 +518,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
                             kbd.data(), dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(), wsf,
                             merge ? &prev.desc : nullptr, defer ? &out : nullptr, &deferred, s),
       "proj_bwd");
+  if (merge || deferred) d.streams.insert(s);
   if (deferred) {
     d.pending[s] = PendingReduce{out, ws, s};
     for (int b = 0; b < nbw; ++b) d.dests.insert(dW[b]);
@@ -1248,7 +1259,8 @@ Tensor linear_bn_forward(const std::vector<Tensor>& As, const Tensor& W, const O
 void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Tensor& W,
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
                      Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr,
-                     const std::vector<Tensor>* dA_into = nullptr, int into_acc = 1) {
+                     const std::vector<Tensor>* dA_into = nullptr, int into_acc = 1,
+                     bool force_defer = false) {
   Tensor G = rows2d(Gin);
   const int64_t M = G.size(0), N = G.size(1);
   const int nb = (int)As.size();
@@ -1326,7 +1338,8 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
     if (M > 0) {
       const int acc = into ? into_acc : 0;
       if (!wAp.empty())
-        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, acc);
+        proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, acc,
+                      force_defer);
       else
         proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, acc);
     }
@@ -1862,6 +1875,15 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
           "poly_step(nei node bwd)");
     }
     const bool nW = need(ctx, PN) || need(ctx, PE), nB = need(ctx, PN + 1) || need(ctx, PE + 1);
+    // TrainStep: every unpack destination deferrable -> the Wt / Ws split
+    // reductions are deferred too (their only reader is the deferred unpack)
+    static const bool nei_defer_env = [] {  // HLHGAT_DEFER_NEI=0: A/B
+      const char* e = getenv("HLHGAT_DEFER_NEI");
+      return !(e && e[0] == '0');
+    }();
+    const bool fdef = nei_defer_env && need(ctx, PN) && need(ctx, PE) && need(ctx, PN + 1) &&
+                      need(ctx, PE + 1) && param_deferrable(sv[30]) && param_deferrable(sv[35]) &&
+                      param_deferrable(sv[31]) && param_deferrable(sv[36]);
     Tensor dWt, dbt, dWs, dbs;
     std::vector<Tensor> dxt, dxs;
     {
@@ -1870,12 +1892,12 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       const bool hs = ctx->saved_data.count("gsink_s") > 0;
       const std::vector<Tensor> into_s{hs ? ctx->saved_data["gsink_s"].toTensor() : Tensor()};
       linear_backward(dYs, {xs}, Ws, nW, nB, {need(ctx, 1)}, dWs, dbs, dxs, nullptr,
-                      hs ? &into_s : nullptr, hs ? sink_accumulate(ctx, "gflag_s") : 0);
+                      hs ? &into_s : nullptr, hs ? sink_accumulate(ctx, "gflag_s") : 0, fdef);
     }
     const bool ht = ctx->saved_data.count("gsink_t") > 0;
     const std::vector<Tensor> into_t{ht ? ctx->saved_data["gsink_t"].toTensor() : Tensor()};
     linear_backward(dYt, {xt}, Wt, nW, nB, {need(ctx, 0)}, dWt, dbt, dxt, nullptr,
-                    ht ? &into_t : nullptr, ht ? sink_accumulate(ctx, "gflag_t") : 0);
+                    ht ? &into_t : nullptr, ht ? sink_accumulate(ctx, "gflag_t") : 0, fdef);
     fk.main_waits_side();
     fk.escape({dWs, dbs, dxs[0], out[PE + 2], out[PE + 3], out[PE + 7], out[PE + 8], out[PE + 9],
                out[PE + 10]});
@@ -1911,8 +1933,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       }
       // TrainStep: the unpack joins the deferred work flushed after the backward
       if (!defer_copies(cb, {out[PN], out[PE], out[PN + 1], out[PE + 1]},
-                        {dWt, dWs, dbt, dbs}, stream_of(xt)))
+                        {dWt, dWs, dbt, dbs}, stream_of(xt))) {
+        TORCH_CHECK(!fdef, "hlhgat: NodeEdgeInt gradient reductions deferred but the unpack "
+                           "could not be (set HLHGAT_DEFER_REDUCE=0)");
         cb.run(stream_of(xt));
+      }
     }
     (void)d;
     return out;
