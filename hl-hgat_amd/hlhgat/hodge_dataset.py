@@ -118,6 +118,13 @@ class Batch(PairData):
         if (getattr(self, "l1_factor", False) and torch.is_tensor(ei) and ei.is_cuda
                 and torch.is_tensor(eis) and eis.is_cuda):
             ops.set_hodge_factor(eis, ei, self.x_t.size(0), getattr(self, "row_order_t", None))
+        for side in ("t", "s"):
+            k = "edge_index_" + side
+            t = getattr(self, k, None)
+            rp, col = getattr(self, "csr_rowptr_" + side, None), getattr(self, "csr_col_" + side, None)
+            if (torch.is_tensor(t) and t.is_cuda and torch.is_tensor(rp) and torch.is_tensor(col)
+                    and self.hodge_sorted.get(k, False)):
+                ops.set_csr(t, rp, col)
         ip, ie = getattr(self, "inc_rowptr", None), getattr(self, "inc_eids", None)
         if torch.is_tensor(ei) and ei.is_cuda and torch.is_tensor(ip) and torch.is_tensor(ie):
             ops.set_incidence(ei, ip, ie)
@@ -309,6 +316,28 @@ def incidence_csr(edge_index, n_nodes: int) -> Tuple[torch.Tensor, torch.Tensor]
             torch.from_numpy((keys % E if E else keys).astype(np.int32)))
 
 
+def laplacian_csr(edge_index, n: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """CSR of a row-sorted Laplacian COO (rows edge_index[0]): int32 rowptr
+    [n+1] and int32 columns -- what hlhgat_csr_from_sorted_coo builds on the
+    device; built here by the data loader instead."""
+    ei = np.asarray(edge_index, dtype=np.int64).reshape(2, -1)
+    rowptr = np.zeros(n + 1, dtype=np.int32)
+    if ei.shape[1]:
+        np.cumsum(np.bincount(ei[0], minlength=n)[:n], out=rowptr[1:])
+    return torch.from_numpy(rowptr), torch.from_numpy(ei[1].astype(np.int32))
+
+
+def _attach_csr(b, sides=("t", "s")) -> None:
+    for side in sides:
+        k = "edge_index_" + side
+        ei, x = getattr(b, k, None), getattr(b, "x_" + side, None)
+        if torch.is_tensor(ei) and torch.is_tensor(x) and (getattr(b, "hodge_sorted", None)
+                                                            or {}).get(k, False):
+            rp, col = laplacian_csr(ei, x.size(0))
+            setattr(b, "csr_rowptr_" + side, rp)
+            setattr(b, "csr_col_" + side, col)
+
+
 def node_degree(inc_rowptr: torch.Tensor, valid: Optional[int] = None
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """degree(edge_index.view(-1), N_t) (lib/Hodge_Cheb_Conv.py:359, the D of
@@ -377,6 +406,8 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
         tp = graph_tiles(counts, nnz)
         if tp is not None:
             setattr(b, key, tp)
+    # Laplacian CSR (rowptr / int32 columns) for the sorted symmetric blocks
+    _attach_csr(b)
     # incidence CSR of |B1| (adj2par1) for the NodeEdgeInt gathers, built
     # here instead of by a device radix sort in every step
     ei = getattr(b, "edge_index", None)
@@ -525,6 +556,8 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
                                                         caps["nnz_t"])
     out.edge_index_s, out.edge_weight_s, pr_s = pad_coo(b.edge_index_s, b.edge_weight_s, ns, Rs,
                                                         caps["nnz_s"])
+    if getattr(b, "csr_rowptr_t", None) is not None or getattr(b, "csr_rowptr_s", None) is not None:
+        _attach_csr(out)  # the padded COO (zero-weight self-loops on padding rows)
     if getattr(b, "edge_index", None) is not None:
         nodes = torch.from_numpy(nt + np.arange(Rs - ns) % (Rt - nt)).to(b.edge_index.dtype)
         out.edge_index = torch.cat([b.edge_index, torch.stack([nodes, nodes])], 1)

@@ -39,6 +39,18 @@ def mean_pool_sorted(x: torch.Tensor, counts: torch.Tensor,
     return ops.segment_mean(x, ptr, counts.numel())
 
 
+def mean_pool_cat(parts) -> torch.Tensor:
+    """torch.cat([mean_pool_sorted(x, counts, ptr) ...], -1) as one output
+    written block by block (ops.segment_mean_cat): the readout of
+    lib/Hodge_ST_Model.py:636 without the cat launch."""
+    ptrs = []
+    for x, counts, ptr in parts:
+        if ptr is None or ptr.device != x.device or ptr.numel() != counts.numel() + 1:
+            ptr = segment_ptr(counts, x.device)
+        ptrs.append(ptr)
+    return ops.segment_mean_cat([x for x, _, _ in parts], ptrs, parts[0][1].numel())
+
+
 def _hl_block(cin_t, cin_s, cout, K, dropout_ratio, act=nn.ReLU):
     layers = [(HodgeLaguerreConv(cin_t, cout, K=K), "x_t, edge_index_t, edge_weight_t -> x_t"),
               (BatchNorm(cout), "x_t -> x_t"),
@@ -154,9 +166,8 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                 else:
                     x_t0 = torch.cat([x_t0, x_t], dim=-1)
                     x_s0 = torch.cat([x_s0, x_s], dim=-1)
-        x = torch.cat((mean_pool_sorted(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
-                       mean_pool_sorted(x_t, data.num_node1, getattr(data, "seg_ptr_t", None))),
-                      -1)
+        x = mean_pool_cat([(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
+                           (x_t, data.num_node1, getattr(data, "seg_ptr_t", None))])
         for i, _ in enumerate(self.mlp_channels):
             x = run_sequential(getattr(self, "mlp%d" % i), [x])
         y = ops.linear_blocks([x], self.out.weight, self.out.bias)
@@ -373,8 +384,8 @@ class _AttPoolHead(nn.Module):
                 par_1 = adj2par1(d1.edge_index, x_t0.shape[0], x_s0.shape[0])
                 D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
         dr = datas[min(len(self.channels) - 1, 1)]
-        x = torch.cat((mean_pool_sorted(x_s, dr.num_edge1, getattr(dr, "seg_ptr_s", None)),
-                       mean_pool_sorted(x_t, dr.num_node1, getattr(dr, "seg_ptr_t", None))), -1)
+        x = mean_pool_cat([(x_s, dr.num_edge1, getattr(dr, "seg_ptr_s", None)),
+                           (x_t, dr.num_node1, getattr(dr, "seg_ptr_t", None))])
         for i, _ in enumerate(self.mlp_channels):
             x = run_sequential(getattr(self, "mlp%d" % i), [x])
         y = ops.linear_blocks([x], self.out.weight, self.out.bias)

@@ -559,7 +559,11 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
     tiles, tile_rows, tile_nnz = getattr(edge_index, "_hlhgat_tiles", (None, 0, 0))
     valid = getattr(edge_index, "_hlhgat_valid", None)
     if getattr(edge_index, "_hlhgat_sorted_symmetric", False):
-        a = _csr_sorted(ei[0], ei[1], w, n, n)
+        pre = getattr(edge_index, "_hlhgat_csr", None)  # built at collate (set_csr)
+        if pre is not None and pre[0].numel() == n + 1 and pre[1].numel() == ei.size(1):
+            a = SparseCSR(pre[0], pre[1], w, n, n, ei.size(1))
+        else:
+            a = _csr_sorted(ei[0], ei[1], w, n, n)
         a.order, a.tiles, a.tile_rows, a.tile_nnz = order, tiles, tile_rows, tile_nnz
         a.valid = valid
         halo = getattr(edge_index, "_hlhgat_halo", None)
@@ -577,6 +581,17 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
             c.valid = valid
         op = HodgeOperator(fwd, bwd)
     return _HODGE_CACHE.put(keys, n, op)
+
+
+def set_csr(edge_index: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor) -> torch.Tensor:
+    """Attach the CSR of a sorted symmetric Laplacian COO built with the batch
+    (hodge_dataset.laplacian_csr, at collate): int32 rowptr over edge_index[0]
+    and int32 columns; the values are edge_weight itself.  hodge_operator then
+    uses it instead of hlhgat_csr_from_sorted_coo (the same arrays, bitwise)."""
+    edge_index._hlhgat_csr = (  # type: ignore[attr-defined]
+        rowptr.to(device=edge_index.device, dtype=torch.int32).contiguous(),
+        col.to(device=edge_index.device, dtype=torch.int32).contiguous())
+    return edge_index
 
 
 def set_incidence(edge_index: torch.Tensor, rowptr: torch.Tensor,
@@ -1212,6 +1227,55 @@ class _SegmentMeanFn(torch.autograd.Function):
                                           n_seg, g.data_ptr(), _ld(g), g.size(1), gx.data_ptr(),
                                           _ld(gx), _stream(g)), "segment_mean_bwd")
         return gx, None, None, None
+
+
+class _SegmentMeanCatFn(torch.autograd.Function):
+    """cat([segment_mean(x_i, ptr_i) for i], -1) with each mean written
+    straight into its column block (no cat launch); contiguous segments."""
+
+    @staticmethod
+    def forward(ctx, n_seg, ptrs, *xs):
+        widths = [x.size(1) for x in xs]
+        out = torch.empty(n_seg, sum(widths), device=xs[0].device, dtype=xs[0].dtype)
+        c0 = 0
+        for x, p, w in zip(xs, ptrs, widths):
+            check(LIB.hlhgat_segment_mean_fwd(p.data_ptr(), None, n_seg, x.data_ptr(), _ld(x), w,
+                                              out.data_ptr() + 4 * c0, _ld(out), _stream(x)),
+                  "segment_mean_fwd")
+            c0 += w
+        ctx.meta = (n_seg, widths, [x.size(0) for x in xs])
+        ctx.save_for_backward(*ptrs)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        n_seg, widths, rows = ctx.meta
+        g = _rows2d(g, "grad").contiguous()
+        gx, c0 = [], 0
+        for p, w, n in zip(ctx.saved_tensors, widths, rows):
+            t = torch.empty(n, w, device=g.device, dtype=g.dtype)
+            check(LIB.hlhgat_segment_mean_bwd(p.data_ptr(), None, n_seg, g.data_ptr() + 4 * c0,
+                                              _ld(g), w, t.data_ptr(), _ld(t), _stream(g)),
+                  "segment_mean_bwd")
+            gx.append(t)
+            c0 += w
+        return (None, None, *gx)
+
+
+def segment_mean_cat(xs: Sequence[torch.Tensor], seg_ptrs: Sequence[torch.Tensor],
+                     n_seg: int) -> torch.Tensor:
+    """torch.cat([segment_mean(x, p, n_seg) for x, p in zip(xs, seg_ptrs)], -1)
+    (the readout x = cat(mean_pool(x_s), mean_pool(x_t)),
+    lib/Hodge_ST_Model.py:636) without the cat: bitwise the same values."""
+    xs = [_rows2d(x, "x") for x in xs]
+    for x in xs:
+        _req_dev(x, "x")
+    for p in seg_ptrs:
+        _req_dev(p, "seg_ptr", torch.int32)
+        if p.numel() != n_seg + 1:
+            raise RuntimeError(f"hlhgat: segment_mean_cat: seg_ptr has {p.numel()} entries, "
+                               f"expected {n_seg + 1}")
+    return _SegmentMeanCatFn.apply(int(n_seg), list(seg_ptrs), *xs)
 
 
 def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,

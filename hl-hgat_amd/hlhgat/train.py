@@ -148,6 +148,7 @@ class TrainStep:
         self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
         self._fwd_bwd_calls = 0
+        self._ones = {}
 
     # -- the step ---------------------------------------------------------
     def _fwd_bwd(self, batch) -> torch.Tensor:
@@ -166,7 +167,12 @@ class TrainStep:
         try:
             out = self.model(batch)
             loss = self.loss_fn(out, batch)
-            loss.backward()
+            # the seed gradient from a cached ones tensor (no fill launch)
+            key = (loss.dtype, loss.device)
+            one = self._ones.get(key)
+            if one is None:
+                one = self._ones[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+            loss.backward(one if loss.dim() == 0 else None)
         finally:
             if self._ext is not None and self._fwd_bwd_calls == 1:
                 # first step: only a parameter whose .grad IS its bucket view

@@ -344,6 +344,39 @@ def test_collate_incidence_equals_device_build(cuda):
         assert torch.equal(bd.deg_t, d)
         assert torch.equal(ops.reciprocal(bd.deg_t), (1 / d).view(-1))
         assert ops.reciprocal(bd.deg_t).data_ptr() == bd.inv_deg_t.data_ptr()
+        # the Laplacian CSRs built with the batch: the device build's arrays
+        for side in ("t", "s"):
+            ei, w = getattr(bd, "edge_index_" + side), getattr(bd, "edge_weight_" + side)
+            rows = getattr(bd, "x_" + side).shape[0]
+            ref = ops._csr_sorted(ei[0], ei[1], w, rows, rows)
+            got = ops.hodge_operator(ei, w, rows).fwd
+            assert got.rowptr.data_ptr() == getattr(bd, "csr_rowptr_" + side).data_ptr()
+            assert torch.equal(got.rowptr, ref.rowptr) and torch.equal(got.col, ref.col)
+            assert torch.equal(got.val, ref.val)
+
+
+def test_segment_mean_cat_equals_cat(cuda):
+    """The readout's cat(mean_pool(x_s), mean_pool(x_t)) written block by
+    block (ops.segment_mean_cat): the values and both input gradients of the
+    torch.cat of two segment means, bit for bit."""
+    from hlhgat import ops
+    g = torch.Generator().manual_seed(12)
+    counts = [torch.randint(1, 9, (50,), generator=g) for _ in range(2)]
+    ptrs = [dev(torch.cat([torch.zeros(1, dtype=torch.int32), c.cumsum(0).to(torch.int32)]))
+            for c in counts]
+    xs = [dev(torch.randn(int(c.sum()), 24, generator=g)) for c in counts]
+    gy = dev(torch.randn(50, 48, generator=g))
+    res = []
+    for fused in (False, True):
+        xr = [x.clone().requires_grad_(True) for x in xs]
+        if fused:
+            y = ops.segment_mean_cat(xr, ptrs, 50)
+        else:
+            y = torch.cat([ops.segment_mean(x, p, 50) for x, p in zip(xr, ptrs)], -1)
+        y.backward(gy)
+        res.append([y.detach(), xr[0].grad, xr[1].grad])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
 
 
 def test_segment_and_cluster_mean(cuda):

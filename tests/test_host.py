@@ -234,6 +234,14 @@ def test_incidence_csr_host_build():
     p = pad_batch(b, static_caps(b, 128))
     dp = degree(p.edge_index.reshape(-1), num_nodes=p.x_t.shape[0]).masked_fill(~p.valid_mask_t, 1)
     assert torch.equal(p.deg_t, dp) and torch.equal(p.inv_deg_t, 1 / dp)
+    for batch in (b, p):  # Laplacian CSRs built with the batch (rows = edge_index[0])
+        for side in ("t", "s"):
+            ei = getattr(batch, "edge_index_" + side).numpy()
+            n = getattr(batch, "x_" + side).shape[0]
+            crp = getattr(batch, "csr_rowptr_" + side).numpy()
+            assert crp.dtype == np.int32 and crp.shape == (n + 1,)
+            assert np.array_equal(np.diff(crp), np.bincount(ei[0], minlength=n))
+            assert np.array_equal(getattr(batch, "csr_col_" + side).numpy(), ei[1])
     rp, eids = incidence_csr(np.zeros((2, 0), dtype=np.int64), 3)
     assert rp.tolist() == [0, 0, 0, 0] and eids.numel() == 0
     with pytest.raises(ValueError):
