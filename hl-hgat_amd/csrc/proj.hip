@@ -1094,18 +1094,9 @@ bool vec_ok(const float* p, int64_t ld, int64_t kb) {
 // 16-column tiles per wave of the forward: enough waves to cover the 1024
 // SIMDs several times over (measured at the HL-HGAT shapes, tools/kbench.py):
 // small M -> 1, K <= 256 -> 2 (re-reading A from L2 is cheap), long K -> 4
-// HLHGAT_FWD_TN4_K: reduction length from which the forward takes 64-column
-// tiles (A/B; same results)
-int64_t fwd_tn4_k() {
-  static int64_t v = [] {
-    const char* e = getenv("HLHGAT_FWD_TN4_K");
-    return e ? (int64_t)atoll(e) : (int64_t)256;
-  }();
-  return v;
-}
-
 int fwd_tn(int64_t M, int64_t N, int64_t ktot) {
-  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= fwd_tn4_k() ? 4 : 2);
+  // (64-column tiles from K = 0 measured equal at the ZINC step, round 2)
+  int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
   if (N <= 16) tn = 1;
   else if (N <= 32 && tn > 2) tn = 2;
   return tn;
