@@ -242,6 +242,13 @@ def test_incidence_csr_host_build():
             assert crp.dtype == np.int32 and crp.shape == (n + 1,)
             assert np.array_equal(np.diff(crp), np.bincount(ei[0], minlength=n))
             assert np.array_equal(getattr(batch, "csr_col_" + side).numpy(), ei[1])
+    # isolated nodes: degree 0 and 1/0 = inf, as degree() and torch's reciprocal give
+    from hlhgat.hodge_dataset import node_degree
+    rp, _ = incidence_csr(np.array([[0], [2]]), 4)
+    d, r = node_degree(rp)
+    assert d.tolist() == [1.0, 0.0, 1.0, 0.0] and torch.equal(r, 1 / d)
+    d, r = node_degree(rp, valid=3)
+    assert d.tolist() == [1.0, 0.0, 1.0, 1.0]
     rp, eids = incidence_csr(np.zeros((2, 0), dtype=np.int64), 3)
     assert rp.tolist() == [0, 0, 0, 0] and eids.numel() == 0
     with pytest.raises(ValueError):
