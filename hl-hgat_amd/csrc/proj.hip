@@ -1354,8 +1354,9 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
                 "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
   HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd: bad dC");
   const bool want_w = nb_w > 0, want_d = nb_d > 0;
-  bool fuse = want_w && want_d && M > 0 && aligned16(dC) && (lddc % 4) == 0 &&
-              (N % 4) == 0;
+  // weight-only calls (a Linear whose input needs no gradient) take the same
+  // launch with no data items, so they can merge / defer split reductions too
+  bool fuse = want_w && M > 0 && aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
   WeightPlan p{};
   if (want_w) {
     p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr);

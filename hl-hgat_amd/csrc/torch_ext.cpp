@@ -874,8 +874,12 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
       wdef.dWp = dWp;  // launched with the data gradient
       wdef.lddw = lddw;
       wdef.db = need_b ? db.data_ptr<float>() : nullptr;
-    } else if (M > 0) {
-      proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, s);
+    } else if (M > 0) {  // weight only: the one-launch path with no data items
+      std::vector<const float*> noW;
+      std::vector<int64_t> noL;
+      std::vector<float*> noD;
+      proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, noW, noL,
+                    noL, noD, noL, s);
     } else {
       for (auto& tt : dW) tt.zero_();
       if (need_b) db.zero_();
@@ -1303,8 +1307,12 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
         wdb = need_b ? gb.data_ptr<float>() : nullptr;
         wkeep = gw;
         wkeep_b = gb;
-      } else {
-        proj_bwd_weight(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, s);
+      } else {  // weight only: the one-launch path with no data items
+        std::vector<const float*> noW;
+        std::vector<int64_t> noL;
+        std::vector<float*> noD;
+        proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, noW,
+                      noL, noL, noD, noL, s);
       }
     } else {
       gw.zero_();
