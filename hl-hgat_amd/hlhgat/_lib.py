@@ -37,6 +37,8 @@ SIGNATURES = {
     "hlhgat_incidence_csr": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "hlhgat_halo_tiles": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i32, c_i32, c_i32, c_vp,
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, P_i64, P_i64]),
+    "hlhgat_graclus": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "hlhgat_mlgc_map": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, P_i64, P_i64]),
     "hlhgat_gather_f32": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlhgat_spmm": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                             c_vp, c_i64, c_vp]),

@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "graph_tiles", "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc",
+           "graph_tiles", "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
            "hodge_factor_ok", "hodge_coo_from_boundary"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
@@ -809,67 +809,76 @@ def hodge_coo_from_boundary(edge_index, n: int, lmax: float):
 # multi-level graph coarsening (MLGC) for the attention-pooling heads
 # ----------------------------------------------------------------------------
 def graclus(edge_index, n: int, weight=None, seed: int = 0) -> np.ndarray:
-    """Greedy graclus matching (restated from torch_cluster 1.6.0
-    graclus_cluster, the reference's dependency, absent here): self-loops
-    dropped, nodes visited in a random order (torch_cluster draws a
-    torch.randperm; here a seeded numpy permutation), each unmatched node u
-    is paired with its unmatched neighbour of largest weight (first in
-    ascending neighbour order on ties; unweighted = all ones) and both get
-    cluster id min(u, v); a node with no unmatched neighbour stays alone
-    (id u).  Returns int64 [n] cluster ids."""
-    ei = np.asarray(edge_index)
-    keep = ei[0] != ei[1]
-    r, c = ei[0][keep], ei[1][keep]
-    w = np.ones(r.size) if weight is None else np.asarray(weight, dtype=np.float64)[keep]
-    o = np.lexsort((c, r))
-    r, c, w = r[o], c[o], w[o]
-    ptr = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(np.bincount(r, minlength=n), out=ptr[1:])
-    out = -np.ones(n, dtype=np.int64)
-    for u in np.random.default_rng(seed).permutation(n):
-        if out[u] >= 0:
-            continue
-        out[u] = u
-        best, wbest = -1, 0.0
-        for e in range(ptr[u], ptr[u + 1]):
-            v = c[e]
-            if out[v] >= 0 or not w[e] > wbest:
-                continue
-            best, wbest = v, w[e]
-        if best >= 0:
-            out[u] = out[best] = min(u, best)
+    """Greedy graclus matching (torch_cluster 1.6.0 graclus_cluster, the
+    reference's dependency, absent here; called at lib/Hodge_Dataset.py:252,
+    :311), run by the library's native host builder (hlhgat_graclus):
+    self-loops dropped, nodes visited in a random order (torch_cluster draws
+    a torch.randperm; here a seeded numpy permutation), each unmatched node
+    paired with its unmatched neighbour of largest weight (first in ascending
+    neighbour order on ties; unweighted = all ones), both get cluster id
+    min(u, v); a node with no unmatched neighbour stays alone (id u).
+    Returns int64 [n] cluster ids."""
+    from ._lib import LIB, check
+    ei = np.ascontiguousarray(np.asarray(edge_index, dtype=np.int64).reshape(2, -1))
+    w = None if weight is None else np.ascontiguousarray(np.asarray(weight, dtype=np.float64))
+    perm = np.ascontiguousarray(np.random.default_rng(seed).permutation(n).astype(np.int64))
+    out = np.empty(n, dtype=np.int64)
+    check(LIB.hlhgat_graclus(ei.ctypes.data, None if w is None else w.ctypes.data,
+                             ei.shape[1], n, perm.ctypes.data, out.ctypes.data), "graclus")
     return out
 
 
-def mlgc(g: "PairData", seed: int = 0):
-    """One level of MLGC (lib/Hodge_Dataset.py:241-297): graclus on L0's
-    pattern with unit weights, cluster ids renumbered by ascending label, an
-    edge whose end nodes share a cluster is dropped (assignment inf), the
-    others map to the coarse edge (min, max) of their clusters, numbered in
-    first-seen edge order; the coarse graph gets Hodge Laplacians built as the
-    reference does (dense eigh, 2 B1 B1^T / lmax) and unit features.
-    Returns (coarse PairData, c_node [n, 1] float, c_edge [E, 1] float)."""
-    n = int(g.num_node1)
-    lab = graclus(np.asarray(g.edge_index_t), n, seed=seed)
-    uniq = np.unique(lab)
-    rank = {int(v): i for i, v in enumerate(uniq)}
-    c_node = np.array([rank[int(v)] for v in lab], dtype=np.int64)
-    ei = np.asarray(g.edge_index)
-    c_edge = np.zeros(ei.shape[1], dtype=np.float32)
-    key, e1 = {}, [[], []]
-    for i in range(ei.shape[1]):
-        a, b = int(c_node[ei[0][i]]), int(c_node[ei[1][i]])
-        if a == b:
-            c_edge[i] = np.inf
-            continue
-        lo, hi = min(a, b), max(a, b)
-        if (hi, lo) not in key:
-            key[(hi, lo)] = len(e1[0])
-            e1[0].append(lo)
-            e1[1].append(hi)
-        c_edge[i] = key[(hi, lo)]
-    ei1 = np.array(e1, dtype=np.int64).reshape(2, -1)
-    n1 = int(uniq.size)
+def mlgc_map(cluster, edge_index):
+    """Fine -> coarse assignment of one MLGC level (lib/Hodge_Dataset.py:
+    254-275) by the native host builder (hlhgat_mlgc_map): cluster ids
+    renumbered by ascending id; an edge inside one cluster gets inf, the
+    others the coarse edge (min, max) numbered in first-seen edge order.
+    Returns (c_node int64 [n], c_edge float32 [E], coarse edge_index int64
+    [2, E1], n1)."""
+    import ctypes as C
+    from ._lib import LIB, check
+    lab = np.ascontiguousarray(np.asarray(cluster, dtype=np.int64))
+    ei = np.ascontiguousarray(np.asarray(edge_index, dtype=np.int64).reshape(2, -1))
+    n, E = lab.size, ei.shape[1]
+    c_node = np.empty(n, dtype=np.int64)
+    c_edge = np.empty(E, dtype=np.float32)
+    e1 = np.empty((2, max(E, 1)), dtype=np.int64)
+    n1, ne = C.c_int64(0), C.c_int64(0)
+    check(LIB.hlhgat_mlgc_map(lab.ctypes.data, n, ei.ctypes.data, E, c_node.ctypes.data,
+                              c_edge.ctypes.data, e1.ctypes.data, C.byref(n1), C.byref(ne)),
+          "mlgc_map")
+    if E == 0:
+        e1 = e1[:, :0]
+    return c_node, c_edge, np.ascontiguousarray(e1.reshape(2, -1)[:, :ne.value]) if E else e1, \
+        int(n1.value)
+
+
+def to_undirected_mean(edge_index, weight, n: int):
+    """PyG to_undirected(edge_index, edge_weight, reduce='mean') as used by
+    MLGC_weighted (lib/Hodge_Dataset.py:310): both directions, coalesced in
+    (row, col) order, duplicate weights averaged.  Returns (int64 [2, E'],
+    float32 [E'])."""
+    ei = np.asarray(edge_index, dtype=np.int64)
+    w = np.asarray(weight, dtype=np.float32)
+    r = np.concatenate([ei[0], ei[1]])
+    c = np.concatenate([ei[1], ei[0]])
+    ww = np.concatenate([w, w])
+    o = np.lexsort((c, r))
+    r, c, ww = r[o], c[o], ww[o]
+    first = np.ones(r.size, dtype=bool)
+    first[1:] = (r[1:] != r[:-1]) | (c[1:] != c[:-1])
+    starts = np.flatnonzero(first)
+    seg = torch.from_numpy(np.cumsum(first) - 1)
+    # PyG's scatter mean: scatter_add in entry order, then / count
+    s = torch.zeros(starts.size).scatter_add_(0, seg, torch.from_numpy(ww))
+    cnt = torch.bincount(seg, minlength=starts.size).to(torch.float32)
+    return np.stack([r[starts], c[starts]]), (s / cnt).numpy()
+
+
+def _mlgc_level(ei1: np.ndarray, n1: int) -> "PairData":
+    """The coarse graph of one MLGC level (lib/Hodge_Dataset.py:275-294):
+    Hodge Laplacians built as the reference does (dense eigh,
+    2 B1 B1^T / lmax) and unit features."""
     L0, L1, _, _ = hodge_laplacians(ei1, n1)
     eit, ewt = dense_to_sparse(L0)
     eis, ews = dense_to_sparse(L1)
@@ -880,5 +889,29 @@ def mlgc(g: "PairData", seed: int = 0):
     c.num_edge1 = int(ei1.shape[1])
     c.num_nodes = n1
     c._hodge_sorted = True
-    return (c, torch.from_numpy(c_node.astype(np.float32)).view(-1, 1),
+    return c
+
+
+def mlgc(g: "PairData", seed: int = 0):
+    """One level of MLGC (lib/Hodge_Dataset.py:241-295): graclus on L0's
+    pattern with unit weights, then the fine -> coarse map (mlgc_map) and the
+    coarse graph's Hodge Laplacians.
+    Returns (coarse PairData, c_node [n, 1] float, c_edge [E, 1] float)."""
+    n = int(g.num_node1)
+    lab = graclus(np.asarray(g.edge_index_t), n, seed=seed)
+    c_node, c_edge, ei1, n1 = mlgc_map(lab, np.asarray(g.edge_index))
+    return (_mlgc_level(ei1, n1), torch.from_numpy(c_node.astype(np.float32)).view(-1, 1),
+            torch.from_numpy(c_edge).view(-1, 1))
+
+
+def mlgc_weighted(g: "PairData", seed: int = 0):
+    """MLGC_weighted (lib/Hodge_Dataset.py:298-353): graclus on the graph's
+    own edges made undirected, weighted by exp(-x_s[:, 0]^2) (duplicates
+    averaged), then the same map and coarse graph as mlgc."""
+    n = int(g.num_node1)
+    xs = np.asarray(g.x_s, dtype=np.float32)[:, 0]
+    ei_u, w_u = to_undirected_mean(np.asarray(g.edge_index), np.exp(-(xs * xs)), n)
+    lab = graclus(ei_u, n, weight=w_u, seed=seed)
+    c_node, c_edge, ei1, n1 = mlgc_map(lab, np.asarray(g.edge_index))
+    return (_mlgc_level(ei1, n1), torch.from_numpy(c_node.astype(np.float32)).view(-1, 1),
             torch.from_numpy(c_edge).view(-1, 1))

@@ -146,6 +146,29 @@ int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
                       int32_t* halo_ptr, int32_t* halo, int32_t* srp, uint16_t* lcol,
                       int32_t* eperm, int32_t* hdr, int64_t* n_tiles, int64_t* n_halo);
 
+/* ---- multi-level graph coarsening (HOST functions, host pointers) --------
+ * hlhgat_graclus replaces the torch_cluster 1.6.0 graclus_cluster call of
+ * MLGC / MLGC_weighted (lib/Hodge_Dataset.py:252-253, :311): greedy matching
+ * over edge_index [2, n_edges] (row-major: rows then cols; self-loops
+ * ignored; weight NULL = all ones) visiting nodes in perm order (the
+ * reference draws torch.randperm; the caller passes its permutation), each
+ * unmatched node paired with its unmatched neighbour of strictly largest
+ * weight (first in ascending column order on ties); both get id min(u, v),
+ * an unpaired node keeps id u.  cluster: [n_nodes] out. */
+int hlhgat_graclus(const int64_t* edge_index, const double* weight, int64_t n_edges,
+                   int64_t n_nodes, const int64_t* perm, int64_t* cluster);
+/* hlhgat_mlgc_map replaces the per-edge loop of MLGC (lib/Hodge_Dataset.py:
+ * 254-275, same at :312-333): c_node[u] = rank of cluster[u] among the
+ * distinct ids; c_edge[i] = +inf if edge i's ends share a coarse node, else
+ * the index of coarse edge (min, max) numbered in first-seen order, written
+ * to coarse_edges [2, n_edges capacity] (row 0 = min at [0..), row 1 = max
+ * at [n_edges..)).  Unlike the reference's float key imax + 1e-4 * imin,
+ * pairs never collide (the reference's key does once a level has > 10^4
+ * coarse nodes). */
+int hlhgat_mlgc_map(const int64_t* cluster, int64_t n_nodes, const int64_t* edge_index,
+                    int64_t n_edges, int64_t* c_node, float* c_edge, int64_t* coarse_edges,
+                    int64_t* n_coarse_nodes, int64_t* n_coarse_edges);
+
 /* dst[i] = src[idx[i]] for i < n (device; e.g. halo sval = val[eperm]). */
 int hlhgat_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst,
                       void* stream);

@@ -19,6 +19,10 @@ PyTorch-CPU restatement of the HL-HGAT hot path, following the reference
   RefPepfuncAttPool    main_pepfunc_HL_HGCNN_dense_int3_attpool.py:36-168 (config 4)
   RefHLFilter          lib/Hodge_Cheb_Conv.py:117-188
   RefSAPool            lib/Hodge_Cheb_Conv.py:36-59
+  graclus              torch_cluster 1.6.0 graclus_cluster (absent; parity
+                       unpinned), called at lib/Hodge_Dataset.py:252, :311
+  mlgc_map             lib/Hodge_Dataset.py:254-275 (MLGC's per-edge loop)
+  to_undirected_mean   PyG to_undirected(reduce='mean'), lib/Hodge_Dataset.py:310
 """
 from __future__ import annotations
 
@@ -601,3 +605,84 @@ class RefSAPool(nn.Module):
         par_1 = adj2par1(datas[k].edge_index, x_t0.shape[0], x_s0.shape[0])
         D = degree(datas[k].edge_index.reshape(-1), num_nodes=x_t0.shape[0]) + 1e-6
         return x_t0, x_s0, par_1, D, k, ei_t, ew_t, ei_s, ew_s, att_t, att_s
+
+
+# ----------------------------------------------------------------------------
+# MLGC (dataset preprocessing for the attention-pooling heads)
+# ----------------------------------------------------------------------------
+def graclus(edge_index, n: int, weight=None, perm=None) -> np.ndarray:
+    """Greedy graclus matching, torch_cluster 1.6.0 graclus_cluster (the
+    reference's dependency, absent here; called at lib/Hodge_Dataset.py:252
+    and :311): self-loops dropped, nodes visited in `perm` (the reference
+    draws torch.randperm), each unmatched node u paired with its unmatched
+    neighbour of strictly largest weight (first in ascending neighbour order
+    on ties; unweighted = all ones), both get id min(u, v); a node with no
+    unmatched neighbour keeps id u.  Parity unpinned (no fixture holds a
+    torch_cluster output).  Returns int64 [n]."""
+    ei = np.asarray(edge_index)
+    keep = ei[0] != ei[1]
+    r, c = ei[0][keep], ei[1][keep]
+    w = np.ones(r.size) if weight is None else np.asarray(weight, dtype=np.float64)[keep]
+    o = np.lexsort((c, r))
+    r, c, w = r[o], c[o], w[o]
+    ptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(r, minlength=n), out=ptr[1:])
+    out = -np.ones(n, dtype=np.int64)
+    for u in (range(n) if perm is None else perm):
+        if out[u] >= 0:
+            continue
+        out[u] = u
+        best, wbest = -1, 0.0
+        for e in range(ptr[u], ptr[u + 1]):
+            v = c[e]
+            if out[v] >= 0 or not w[e] > wbest:
+                continue
+            best, wbest = v, w[e]
+        if best >= 0:
+            out[u] = out[best] = min(u, best)
+    return out
+
+
+def mlgc_map(cluster, edge_index):
+    """The per-edge loop of MLGC (lib/Hodge_Dataset.py:254-275, :312-333):
+    cluster ids renumbered by ascending id; an edge inside one cluster gets
+    inf, the others the coarse edge (min, max) in first-seen order.  Keys are
+    (min, max) tuples where the reference uses imax + 1e-4 * imin (equal
+    below 10^4 coarse nodes).  Returns (c_node int64 [n], c_edge float32 [E],
+    coarse edge_index int64 [2, E1], n1)."""
+    lab = np.asarray(cluster)
+    uniq = np.unique(lab)
+    rank = {int(v): i for i, v in enumerate(uniq)}
+    c_node = np.array([rank[int(v)] for v in lab], dtype=np.int64)
+    ei = np.asarray(edge_index)
+    c_edge = np.zeros(ei.shape[1], dtype=np.float32)
+    key, e1 = {}, [[], []]
+    for i in range(ei.shape[1]):
+        a, b = int(c_node[ei[0][i]]), int(c_node[ei[1][i]])
+        if a == b:
+            c_edge[i] = np.inf
+            continue
+        lo, hi = min(a, b), max(a, b)
+        if (hi, lo) not in key:
+            key[(hi, lo)] = len(e1[0])
+            e1[0].append(lo)
+            e1[1].append(hi)
+        c_edge[i] = key[(hi, lo)]
+    return c_node, c_edge, np.array(e1, dtype=np.int64).reshape(2, -1), int(uniq.size)
+
+
+def to_undirected_mean(edge_index, weight, n: int):
+    """PyG to_undirected(edge_index, edge_weight, reduce='mean')
+    (lib/Hodge_Dataset.py:310): both directions, coalesced in (row, col)
+    order, duplicate weights averaged."""
+    ei = np.asarray(edge_index)
+    w = np.asarray(weight, dtype=np.float32)
+    r = np.concatenate([ei[0], ei[1]])
+    c = np.concatenate([ei[1], ei[0]])
+    ww = np.concatenate([w, w])
+    key = r.astype(np.int64) * n + c
+    uk, inv = np.unique(key, return_inverse=True)
+    s = np.zeros(uk.size, dtype=np.float32)
+    np.add.at(s, inv, ww)
+    cnt = np.bincount(inv, minlength=uk.size).astype(np.float32)
+    return np.stack([uk // n, uk % n]), s / cnt

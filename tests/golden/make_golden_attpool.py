@@ -12,6 +12,9 @@ Run in the build container only (the reference is not on the GPU box):
   everything in MLGC after the matching (cluster renumbering, edge assignment
   with inf for contracted edges, coarse B1, L0/L1 and their COO), while graclus
   itself stays "parity unpinned" (its labels are stored for the test).
+* mlgc_weighted_small.npz: the reference's MLGC_weighted (lib/Hodge_Dataset.py:
+  298-353), graclus and PyG's to_undirected(reduce='mean') answered by hlhgat's
+  restatements (inputs/outputs of both stored).
 * attpool_cifar_small.npz: HL_HGCNN_CIFAR10SP_dense_int3_attpool
   (lib/Hodge_ST_Model.py:958-1091) forward + backward on a 3-graph two-level
   batch of CIFAR-like superpixel graphs.
@@ -117,6 +120,53 @@ def mlgc_case(ref_ds):
     _save("mlgc_small", **arrays)
 
 
+def mlgc_weighted_case(ref_ds):
+    """MLGC_weighted (lib/Hodge_Dataset.py:298-353): torch_cluster's graclus
+    and PyG's to_undirected(reduce='mean') are absent, so both calls are
+    answered by hlhgat's restatements (their inputs and outputs are stored:
+    the edge weights the reference computes, exp(-x_s^2), are pinned; the
+    matching is parity unpinned); the map and coarse graph are the
+    reference's."""
+    from hlhgat.hodge_dataset import graclus, to_undirected_mean
+    from hlhgat.synthetic import cifar_like_graphs, peptides_like_graphs
+    seen = []
+
+    def to_undirected_standin(edge_index, edge_attr=None, num_nodes=None, reduce="add"):
+        assert reduce == "mean"
+        n = int(edge_index.max()) + 1 if num_nodes is None else int(num_nodes)
+        ei, w = to_undirected_mean(_np(edge_index), _np(edge_attr), n)
+        return torch.from_numpy(ei), torch.from_numpy(w)
+
+    def graclus_standin(row, col, weight, num_nodes):
+        lab = graclus(np.stack([_np(row), _np(col)]), int(num_nodes), weight=_np(weight),
+                      seed=100 + len(seen))
+        seen.append((_np(row), _np(col), _np(weight), lab))
+        return torch.from_numpy(lab)
+
+    ref_ds.graclus_cluster = graclus_standin
+    ref_ds.to_undirected = to_undirected_standin
+    arrays = {}
+    graphs = [cifar_like_graphs(41, n=30, k=5)[0], cifar_like_graphs(42, n=45, k=8)[0],
+              peptides_like_graphs(43)[0]]
+    for gi, g in enumerate(graphs):
+        g.x_t, g.x_s = g.x_t[:, 1:], g.x_s[:, 1:]  # drop the cluster column
+        coarse, c_node, c_edge = ref_ds.MLGC_weighted(g)
+        row, col, w, lab = seen[-1]
+        arrays[f"g{gi}/edge_index"] = _np(g.edge_index)
+        arrays[f"g{gi}/x_s"] = _np(g.x_s)
+        arrays[f"g{gi}/num_node1"] = np.int64(g.num_node1)
+        arrays[f"g{gi}/graclus_edge_index"] = np.stack([row, col])
+        arrays[f"g{gi}/graclus_weight"] = w
+        arrays[f"g{gi}/graclus"] = lab
+        arrays[f"g{gi}/c_node"] = _np(c_node)
+        arrays[f"g{gi}/c_edge"] = _np(c_edge)
+        for k in ("edge_index", "edge_index_t", "edge_weight_t", "edge_index_s",
+                  "edge_weight_s", "x_t", "x_s"):
+            arrays[f"g{gi}/coarse/{k}"] = _np(getattr(coarse, k))
+        arrays[f"g{gi}/coarse/num_node1"] = np.int64(coarse.num_node1)
+    _save("mlgc_weighted_small", **arrays)
+
+
 if __name__ == "__main__":
     ref_root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     import pyg_standin
@@ -130,6 +180,7 @@ if __name__ == "__main__":
     torch.set_num_threads(1)  # deterministic CPU reduction order
 
     mlgc_case(ref_ds)
+    mlgc_weighted_case(ref_ds)
 
     b0, b1 = two_level_batches([cifar_like_graphs(30 + s, n=24, k=5) for s in range(3)])
     torch.manual_seed(5)

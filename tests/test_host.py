@@ -450,3 +450,71 @@ def test_boundary_operator_views_match_reference_adj2par1():
     assert P.t().incidence is not None and P.abs()._base is P
     with pytest.raises(RuntimeError, match="ROCm"):
         torch.sparse.mm(P.transpose(0, 1), torch.ones(int(g["n_nodes"]), 3))
+
+
+def test_mlgc_weighted_matches_reference_golden():
+    """MLGC_weighted (lib/Hodge_Dataset.py:298-353) against the reference's own
+    run (tests/golden/make_golden_attpool.py): the weights the reference hands
+    to graclus (to_undirected mean of exp(-x_s^2)) are pinned through our
+    to_undirected_mean; graclus is parity unpinned (labels stored); the map
+    and coarse graph are pinned."""
+    from hlhgat.hodge_dataset import PairData, graclus, mlgc_weighted, to_undirected_mean
+    g = load_golden("mlgc_weighted_small")
+    for gi in range(3):
+        p = f"g{gi}/"
+        n = int(g[p + "num_node1"])
+        ei, xs = g[p + "edge_index"], g[p + "x_s"]
+        w_ref = np.exp(-(xs[:, 0].astype(np.float32) ** 2))
+        ei_u, w_u = to_undirected_mean(ei, w_ref, n)
+        assert np.array_equal(ei_u, g[p + "graclus_edge_index"])
+        np.testing.assert_allclose(w_u, g[p + "graclus_weight"], rtol=1e-6, atol=0)
+        assert np.array_equal(graclus(ei_u, n, weight=w_u, seed=100 + gi), g[p + "graclus"])
+        d = PairData(x_s=torch.from_numpy(xs), x_t=torch.zeros(n, 1))
+        d.edge_index = torch.from_numpy(ei)
+        d.num_node1 = n
+        coarse, c_node, c_edge = mlgc_weighted(d, seed=100 + gi)
+        assert np.array_equal(c_node.numpy().reshape(-1), g[p + "c_node"].reshape(-1))
+        ce, ref_ce = c_edge.numpy().reshape(-1), g[p + "c_edge"].reshape(-1)
+        assert np.array_equal(np.isinf(ce), np.isinf(ref_ce))
+        assert np.array_equal(ce[~np.isinf(ce)], ref_ce[~np.isinf(ref_ce)])
+        assert coarse.num_node1 == int(g[p + "coarse/num_node1"])
+        for k in ("edge_index", "edge_index_t", "edge_index_s"):
+            assert np.array_equal(getattr(coarse, k).numpy(), g[p + "coarse/" + k]), k
+        for k in ("edge_weight_t", "edge_weight_s", "x_t", "x_s"):
+            np.testing.assert_allclose(getattr(coarse, k).numpy(), g[p + "coarse/" + k],
+                                       rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_native_mlgc_equals_oracle_restatement():
+    """The native host builders (hlhgat_graclus / hlhgat_mlgc_map in
+    libhlhgat.so) against the oracle's pure-Python restatement
+    (oracle/hodge_ref.py graclus / mlgc_map / to_undirected_mean), bitwise, on
+    random multigraphs with self-loops, duplicates, isolated nodes, weights
+    with ties, and empty inputs."""
+    from hlhgat import hodge_dataset as hd
+    from oracle import hodge_ref as ref
+    rng = np.random.default_rng(11)
+    for n, E in [(0, 0), (1, 0), (4, 1), (7, 3), (60, 250), (400, 3000)]:
+        ei = rng.integers(0, max(n, 1), size=(2, E)) if n else np.zeros((2, 0), np.int64)
+        sym = np.concatenate([ei, ei[::-1]], axis=1)
+        for w in (None, rng.integers(0, 3, sym.shape[1]).astype(np.float64),
+                  rng.random(sym.shape[1])):
+            for seed in range(2):
+                perm = np.random.default_rng(seed).permutation(n)
+                lab = hd.graclus(sym, n, weight=w, seed=seed)
+                assert np.array_equal(lab, ref.graclus(sym, n, weight=w, perm=perm)), (n, E)
+                for a, b in zip(hd.mlgc_map(lab, ei), ref.mlgc_map(lab, ei)):
+                    assert np.array_equal(np.asarray(a), np.asarray(b)), (n, E)
+        if E:
+            w = rng.random(E).astype(np.float32)
+            for a, b in zip(hd.to_undirected_mean(ei, w, n), ref.to_undirected_mean(ei, w, n)):
+                assert np.array_equal(a, b)
+
+
+def test_native_mlgc_rejects_bad_input():
+    from hlhgat import hodge_dataset as hd
+    from hlhgat._lib import HlhgatError
+    with pytest.raises(HlhgatError, match="out of range"):
+        hd.graclus(np.array([[0, 5], [1, 0]]), 3)
+    with pytest.raises(HlhgatError, match="out of range"):
+        hd.mlgc_map(np.array([0, 0, 7]), np.array([[0], [1]]))
