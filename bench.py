@@ -297,8 +297,8 @@ def _head_loss(kind, out, datas):
 
 def heads_leg(device, steps=6, warmup=2, cpu_budget_s=8.0):
     """BASELINE configs[2..4] on this GPU: graphs/s of a full training step
-    (fwd + loss + bwd + Adam, hlhgat.train.TrainStep, eager: the MLGC levels
-    change shape per batch) at the per-GPU batch of SURVEY §8d, and the CPU
+    (fwd + loss + bwd + Adam, hlhgat.train.TrainStep replaying a hipGraph per
+    batch shape, and eager beside it) at the per-GPU batch of SURVEY §8d, and the CPU
     oracle (the same head restated in oracle/hodge_ref.py) timed on a bounded
     sample of the same data on the host cores."""
     import hlhgat
@@ -311,20 +311,31 @@ def heads_leg(device, steps=6, warmup=2, cpu_budget_s=8.0):
         raw = [_head_batch(c["kind"], c["graphs"], s) for s in range(2)]
         gen_s = time.perf_counter() - t0
         batches = [b.to(device) if c["kind"] == "tsp" else [x.to(device) for x in b] for b in raw]
-        torch.manual_seed(0)
-        m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
-        st = TrainStep(m, lambda o, d, k=c["kind"]: _head_loss(k, o, d), lr=1e-3, graphs=False)
-        for i in range(warmup):
-            st(batches[i % 2])
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            st(batches[i % 2])
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / steps
+        dts = {}
+        for graphs in (False, True):
+            torch.manual_seed(0)
+            m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
+            st = TrainStep(m, lambda o, d, k=c["kind"]: _head_loss(k, o, d), lr=1e-3,
+                           graphs=graphs)
+            for i in range(warmup):  # graphs: one eager step + capture per batch shape
+                st(batches[i % 2])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                st(batches[i % 2])
+            torch.cuda.synchronize()
+            dts[graphs] = (time.perf_counter() - t0) / steps
+            if graphs:
+                assert st.stats["replay"] == steps, st.stats
+            del m, st
+        dt = dts[True]
         r = {"value": round(c["graphs"] / dt, 1), "unit": "graphs/s", "ms_per_step": round(dt * 1e3, 2),
              "graphs_per_step": c["graphs"], "steps": steps, "head": c["cls"], "model": c["kw"],
-             "step": "fwd + loss + bwd + Adam, eager (TrainStep)", "data_gen_s": round(gen_s, 1)}
+             "step": "fwd + loss + bwd + Adam, TrainStep replaying one hipGraph per batch shape "
+                     "(2 synthetic batches alternating; a loader with varying shapes pays one "
+                     "eager step + capture per new shape, see eager_*)",
+             "eager_ms_per_step": round(dts[False] * 1e3, 2),
+             "eager_value": round(c["graphs"] / dts[False], 1), "data_gen_s": round(gen_s, 1)}
         # CPU oracle on a bounded sample: the first cpu_graphs graphs of a batch
         torch.set_num_threads(cores)
         sb = _head_batch(c["kind"], c["cpu_graphs"], 0)
@@ -351,7 +362,7 @@ def heads_leg(device, steps=6, warmup=2, cpu_budget_s=8.0):
                                        f"graph(s) of the same generator, median {med * 1e3:.0f} ms"}
         out[name] = r
         log(f"[heads] {name}: {r['value']} graphs/s (CPU oracle {r['cpu_baseline']['value']})")
-        del batches, m, st
+        del batches
         torch.cuda.empty_cache()
     return out
 

@@ -217,8 +217,9 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
 
     def forward(self, data, device="cuda:0"):
         dev = data.x_s.device
+        # output_size given: no host sync (the step can be captured)
         s_batch = torch.repeat_interleave(torch.arange(data.num_edge1.numel(), device=dev),
-                                          data.num_edge1.to(dev))
+                                          data.num_edge1.to(dev), output_size=data.x_s.size(0))
         x_s, edge_index_s, edge_weight_s = data.x_s[:, :1], data.edge_index_s, data.edge_weight_s
         edge_mask = data.x_s[:, 1:]
         x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
@@ -263,12 +264,14 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch
 
 
-def _level_offsets(counts_next: torch.Tensor, counts: torch.Tensor, device) -> torch.Tensor:
+def _level_offsets(counts_next: torch.Tensor, counts: torch.Tensor, device,
+                   rows: int) -> torch.Tensor:
     """n_ahead[n_batch] of the attpool heads (lib/Hodge_ST_Model.py:1031-1036):
-    for every row of the fine level, the first coarse row of its graph."""
+    for every row of the fine level (`rows` of them: no host sync), the first
+    coarse row of its graph."""
     ahead = torch.zeros(counts_next.numel(), dtype=torch.float32, device=device)
     ahead[1:] = torch.cumsum(counts_next.to(device), 0)[:-1].to(torch.float32)
-    return torch.repeat_interleave(ahead, counts.to(device))
+    return torch.repeat_interleave(ahead, counts.to(device), output_size=rows)
 
 
 class _AttPoolHead(nn.Module):
@@ -323,8 +326,10 @@ class _AttPoolHead(nn.Module):
         d0 = datas[0]
         dev = d0.x_t.device
         # global coarse index of every fine node / edge (pos_ts / pos_ss)
-        pos_t = d0.x_t[:, 0] + _level_offsets(datas[1].num_node1, d0.num_node1, dev)
-        pos_s = d0.x_s[:, 0] + _level_offsets(datas[1].num_edge1, d0.num_edge1, dev)
+        pos_t = d0.x_t[:, 0] + _level_offsets(datas[1].num_node1, d0.num_node1, dev,
+                                                 d0.x_t.size(0))
+        pos_s = d0.x_s[:, 0] + _level_offsets(datas[1].num_edge1, d0.num_edge1, dev,
+                                                 d0.x_s.size(0))
         x_s, edge_index_s, edge_weight_s = d0.x_s[:, 1:], d0.edge_index_s, d0.edge_weight_s
         x_t, edge_index_t, edge_weight_t = d0.x_t[:, 1:], d0.edge_index_t, d0.edge_weight_t
         x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,

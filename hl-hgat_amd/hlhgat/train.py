@@ -46,9 +46,27 @@ def _tensor_items(batch):
             if torch.is_tensor(v) and not k.startswith("_")]
 
 
+def _parts(batch):
+    """The batch objects of one step: a Batch, or the list of per-level
+    batches the attention-pooling heads take (`datas`)."""
+    return list(batch) if isinstance(batch, (list, tuple)) else [batch]
+
+
+def _clone_batch(batch):
+    static = type(batch).__new__(type(batch))
+    for k, v in vars(batch).items():
+        setattr(static, k, v.clone() if torch.is_tensor(v) else v)
+    if hasattr(static, "_mark"):
+        static._mark()  # sorted/symmetric Laplacian flags on the static tensors
+    return static
+
+
 def batch_key(batch) -> Tuple:
     """Shape signature of a batch: every tensor attribute's (name, shape,
-    dtype) plus the scalar attributes that change the launch sequence."""
+    dtype) plus the scalar attributes that change the launch sequence; for a
+    list of level batches, the tuple of their signatures."""
+    if isinstance(batch, (list, tuple)):
+        return ("levels",) + tuple(batch_key(b) for b in batch)
     key = [(k, tuple(v.shape), str(v.dtype)) for k, v in _tensor_items(batch)]
     key.append(("num_graphs", getattr(batch, "num_graphs", None)))
     hs = getattr(batch, "hodge_sorted", None)
@@ -69,8 +87,9 @@ class _Captured:
         per launch, hlhgat_copy2d_batched) instead of one copy launch each
         (15 at the ZINC shape, ~75 us of serial copy kernels per step)."""
         pend = []
-        for k, v in _tensor_items(batch):
-            dst = getattr(self.batch, k)
+        items = [(getattr(sb, k), v) for b, sb in zip(_parts(batch), _parts(self.batch))
+                 for k, v in _tensor_items(b)]
+        for dst, v in items:
             if dst.data_ptr() == v.data_ptr():
                 continue
             if (v.is_cuda and dst.device == v.device and v.is_contiguous() and dst.is_contiguous()
@@ -233,11 +252,8 @@ class TrainStep:
         return loss
 
     def _capture(self, batch, key) -> _Captured:
-        static = type(batch).__new__(type(batch))
-        for k, v in vars(batch).items():
-            setattr(static, k, v.clone() if torch.is_tensor(v) else v)
-        if hasattr(static, "_mark"):
-            static._mark()  # sorted/symmetric Laplacian flags on the static tensors
+        static = ([_clone_batch(b) for b in batch] if isinstance(batch, (list, tuple))
+                  else _clone_batch(batch))
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
