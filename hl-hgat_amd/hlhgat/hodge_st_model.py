@@ -389,6 +389,14 @@ class _AttPoolHead(nn.Module):
                 par_1 = adj2par1(d1.edge_index, x_t0.shape[0], x_s0.shape[0])
                 D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
         dr = datas[min(len(self.channels) - 1, 1)]
+        if x_t.size(0) != dr.x_t.size(0) or x_s.size(0) != dr.x_s.size(0):
+            # the reference's readout (lib/Hodge_ST_Model.py:1076-1080) pools the
+            # last block's rows by datas[min(i, 1)]'s graph sizes: a pool at the
+            # last level (or none with >1 level) leaves them mismatched
+            raise RuntimeError(
+                f"hlhgat: attpool readout rows ({x_t.size(0)}, {x_s.size(0)}) do not match "
+                f"level {min(len(self.channels) - 1, 1)}'s ({dr.x_t.size(0)}, {dr.x_s.size(0)}): "
+                f"pool_loc={self.pool_loc} must be below the last of {len(self.channels)} levels")
         x = mean_pool_cat([(x_s, dr.num_edge1, getattr(dr, "seg_ptr_s", None)),
                            (x_t, dr.num_node1, getattr(dr, "seg_ptr_t", None))])
         for i, _ in enumerate(self.mlp_channels):

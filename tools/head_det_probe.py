@@ -18,7 +18,7 @@ if os.environ.get("NOFORK") == "1":
 bs = {s: [x.to(cuda) for x in two_level_batch(kind, 6, seed=s)] for s in (1, 2)}
 torch.manual_seed(0)
 m = hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool(
-    channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=1).to(cuda).train()
+    channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0).to(cuda).train()
 for mod in m.modules():  # BN running stats would change between repetitions
     if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
         mod.momentum = 0.0

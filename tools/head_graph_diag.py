@@ -16,9 +16,9 @@ bs = {s: [x.to(cuda) for x in two_level_batch(kind, 6, seed=s)] for s in (1, 2)}
 def mk():
     if kind == "cifar":
         return hlhgat.HL_HGCNN_CIFAR10SP_dense_int3_attpool(
-            channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10, pool_loc=1)
+            channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10, pool_loc=0)
     return hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool(
-        channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=1)
+        channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)
 
 
 def loss(o, d):

@@ -19,11 +19,11 @@ bs = {s: [x.to(cuda) for x in two_level_batch(kind, 6, seed=s)] for s in (1, 2)}
 torch.manual_seed(0)
 if kind == "cifar":
     m = hlhgat.HL_HGCNN_CIFAR10SP_dense_int3_attpool(
-        channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10, pool_loc=1)
+        channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10, pool_loc=0)
     loss = lambda o, d: F.cross_entropy(o, d[0].y.view(-1).long())  # noqa: E731
 else:
     m = hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool(
-        channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=1)
+        channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)
     loss = lambda o, d: F.binary_cross_entropy_with_logits(o, d[0].y.view(o.shape).float())  # noqa: E731
 m = m.to(cuda).train()
 events = []
