@@ -1,0 +1,291 @@
+"""Training-step runtime: flat parameters, one-bucket gradient all-reduce and
+whole-step hipGraph replay.
+
+The reference trains with a plain eager loop (main_zinc_*.py: forward, L1
+loss, backward, Adam step per DataLoader batch, 'cuda:0').  At ZINC scale
+one such step is ~600 short kernels, so on MI355X the step is bound by launch
+issue and inter-kernel gaps, not by the kernels' bytes.  TrainStep keeps the
+reference's semantics (same model, loss, Adam with L2 weight decay) and
+executes the step MI355X-first:
+
+  * parameters and gradients live in two flat fp32 buffers (the model's
+    Parameters become views), so Adam is ONE fused multi-tensor launch over
+    one tensor and the data-parallel gradient exchange is ONE all-reduce of
+    one contiguous bucket over RCCL/xGMI (2.6 MB for cfg2);
+  * forward + loss + backward (+ Adam on one GPU) are captured into a
+    hipGraph per distinct batch shape and replayed; the node / edge chains
+    of every HL block are two graph branches (ops.fork);
+  * a batch is copied into the graph's static device buffers (D2D, inside the
+    step), so any batch of a captured shape reuses its graph.
+
+The first step of a new shape runs eagerly (that step IS the training step)
+and the capture happens right after it; capture records work without
+executing it, so no batch is trained twice.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+__all__ = ["TrainStep", "batch_key"]
+
+# HLHGAT_HIP_ADAM=0: torch's fused Adam instead of hlhgat_adam_flat (A/B)
+import os as _os  # noqa: E402
+HIP_ADAM = _os.environ.get("HLHGAT_HIP_ADAM", "1") != "0"
+# HLHGAT_DEFER_REDUCE=0: every Linear backward launches its own split
+# reduction instead of handing it to the next one on its stream (A/B)
+DEFER_REDUCE = _os.environ.get("HLHGAT_DEFER_REDUCE", "1") != "0"
+
+
+def _tensor_items(batch):
+    return [(k, v) for k, v in sorted(vars(batch).items())
+            if torch.is_tensor(v) and not k.startswith("_")]
+
+
+def batch_key(batch) -> Tuple:
+    """Shape signature of a batch: every tensor attribute's (name, shape,
+    dtype) plus the scalar attributes that change the launch sequence."""
+    key = [(k, tuple(v.shape), str(v.dtype)) for k, v in _tensor_items(batch)]
+    key.append(("num_graphs", getattr(batch, "num_graphs", None)))
+    hs = getattr(batch, "hodge_sorted", None)
+    if hs:
+        key.append(("hodge_sorted", tuple(sorted(hs.items()))))
+    return tuple(key)
+
+
+class _Captured:
+    def __init__(self, graph, static_batch, loss):
+        self.graph = graph
+        self.batch = static_batch
+        self.loss = loss
+
+    def load(self, batch):
+        """Copy a batch into the graph's static buffers: every contiguous
+        same-device tensor goes into batched-copy launches (up to 8 tensors
+        per launch, hlhgat_copy2d_batched) instead of one copy launch each
+        (15 at the ZINC shape, ~75 us of serial copy kernels per step)."""
+        pend = []
+        for k, v in _tensor_items(batch):
+            dst = getattr(self.batch, k)
+            if dst.data_ptr() == v.data_ptr():
+                continue
+            if (v.is_cuda and dst.device == v.device and v.is_contiguous() and dst.is_contiguous()
+                    and v.dtype == dst.dtype and v.numel() == dst.numel()
+                    and (v.numel() * v.element_size()) % 4 == 0):
+                pend.append((v, dst))
+            else:
+                dst.copy_(v, non_blocking=True)
+        if pend:
+            ops.copy_words_batched([p[0] for p in pend], [p[1] for p in pend])
+
+
+class TrainStep:
+    """step(batch) -> loss: forward, loss_fn(out, batch), backward, gradient
+    all-reduce (mean over ranks, as DDP) and Adam (L2 weight decay, as
+    torch.optim.Adam).
+
+    graphs=True replays a captured hipGraph per batch shape (requires a ROCm
+    device); graphs=False runs the same step eagerly (any device)."""
+
+    def __init__(self, model: torch.nn.Module, loss_fn: Callable, lr: float = 1e-3,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 graphs: bool = True, max_graphs: int = 32):
+        self.model = model
+        self.loss_fn = loss_fn
+        params = [p for p in model.parameters() if p.requires_grad]
+        if not params:
+            raise ValueError("TrainStep: model has no trainable parameters")
+        dev = params[0].device
+        self.device = dev
+        self.graphs = bool(graphs) and dev.type == "cuda"
+        n = sum(p.numel() for p in params)
+        self.flat = torch.empty(n, device=dev, dtype=torch.float32)
+        self.flat_grad = torch.zeros(n, device=dev, dtype=torch.float32)
+        off = 0
+        self._offsets = []
+        with torch.no_grad():
+            for p in params:
+                if p.dtype != torch.float32:
+                    raise ValueError("TrainStep: fp32 parameters expected")
+                k = p.numel()
+                self.flat[off:off + k].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + k].view_as(p)
+                p.grad = self.flat_grad[off:off + k].view_as(p)
+                self._offsets.append(off)
+                off += k
+        self.params = params
+        # HIP autograd nodes write parameter gradients straight into flat_grad
+        # (torch_ext.cpp, "Gradient bucket"): no per-parameter add / copy
+        self._ext = None
+        if dev.type == "cuda":
+            self._ext = ops._ext
+            self._ext.grad_bucket_set(params, self.flat_grad, self._offsets)
+        self.master = torch.nn.Parameter(self.flat)  # shares storage with the model
+        self.master.grad = self.flat_grad
+        kw = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        if dev.type == "cuda":
+            kw.update(fused=True, capturable=self.graphs)
+        self.opt = torch.optim.Adam([self.master], **kw)
+        self._hip_adam = dev.type == "cuda" and HIP_ADAM
+        if self._hip_adam:
+            # the optimiser state torch's fused Adam would create, updated by
+            # ONE hlhgat_adam_flat launch (torch's multi-tensor kernel runs a
+            # single 65536-element chunk per workgroup on this one flat
+            # tensor: ~10 workgroups, 0.1 ms per step at the ZINC size)
+            self.opt.state[self.master] = {
+                "step": torch.zeros((), dtype=torch.float32, device=dev),
+                "exp_avg": torch.zeros_like(self.flat),
+                "exp_avg_sq": torch.zeros_like(self.flat)}
+            self._hyper = (lr, betas, eps, weight_decay)
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.max_graphs = max_graphs
+        self._graphs: Dict[Tuple, _Captured] = {}
+        self._pool = None
+        self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
+        self.stats = {"eager": 0, "replay": 0, "captures": 0}
+        self._fwd_bwd_calls = 0
+        self._ones = {}
+
+    # -- the step ---------------------------------------------------------
+    def _fwd_bwd(self, batch) -> torch.Tensor:
+        self.flat_grad.zero_()
+        # deferred split reductions (torch_ext.cpp): not in the first step,
+        # which finds the parameters used twice (those are never deferred)
+        defer = self._ext is not None and DEFER_REDUCE and self._fwd_bwd_calls > 0
+        self._fwd_bwd_calls += 1
+        if self._ext is not None:
+            for p in self.params:
+                p.grad = None
+            self._ext.grad_bucket_begin()
+        dests = []
+        if defer:
+            self._ext.reduce_defer(True)
+        try:
+            out = self.model(batch)
+            loss = self.loss_fn(out, batch)
+            # the seed gradient from a cached ones tensor (no fill launch)
+            key = (loss.dtype, loss.device)
+            one = self._ones.get(key)
+            if one is None:
+                one = self._ones[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
+            loss.backward(one if loss.dim() == 0 else None)
+        finally:
+            if self._ext is not None and self._fwd_bwd_calls == 1:
+                # first step: only a parameter whose .grad IS its bucket view
+                # (ONE contribution, a HIP node's view that AccumulateGrad
+                # adopted unread) may have its reduction deferred; a summed,
+                # cloned or torch-produced gradient is never deferred
+                base = self.flat_grad.data_ptr()
+                self._ext.grad_bucket_no_defer(
+                    [p for p, off in zip(self.params, self._offsets)
+                     if p.grad is None or p.grad.data_ptr() != base + 4 * off])
+            if defer:
+                # the last reduction of each stream, before anything reads the bucket
+                dests = self._ext.reduce_flush(self.device.index if self.device.index is not None
+                                               else torch.cuda.current_device())
+                self._ext.reduce_defer(False)
+        if self._ext is not None:
+            self._adopt_grads(set(dests))
+        return loss.detach()
+
+    def _adopt_grads(self, deferred=frozenset()) -> None:
+        """Every p.grad must be its flat_grad view: gradients produced outside
+        the bucket (torch ops) are copied in; missing ones stay zero."""
+        base = self.flat_grad.data_ptr()
+        for p, off in zip(self.params, self._offsets):
+            g = p.grad
+            view = self.flat_grad[off:off + p.numel()].view_as(p)
+            if g is None:
+                p.grad = view
+            elif g.data_ptr() != base + 4 * off:
+                if base + 4 * off not in deferred:
+                    view.copy_(g)
+                # else: AccumulateGrad cloned the view before its deferred
+                # reduction ran; the bucket region itself holds the gradient
+                p.grad = view
+
+    def _opt_step(self) -> None:
+        if not self._hip_adam:
+            self.opt.step()
+            return
+        st = self.opt.state[self.master]
+        lr, betas, eps, wd = self._hyper
+        ops.adam_flat(self.flat, self.flat_grad, st["exp_avg"], st["exp_avg_sq"], st["step"],
+                      lr, betas, eps, wd)
+
+    def _exchange_and_update(self) -> None:
+        if self.world > 1:
+            # one contiguous bucket; mean over ranks as DDP
+            dist.all_reduce(self.flat_grad)
+            self.flat_grad.div_(self.world)
+        self._opt_step()
+
+    def _eager(self, batch) -> torch.Tensor:
+        ops.clear_caches()
+        loss = self._fwd_bwd(batch)
+        self._exchange_and_update()
+        ops.clear_caches()
+        self.stats["eager"] += 1
+        return loss
+
+    def _capture(self, batch, key) -> _Captured:
+        static = type(batch).__new__(type(batch))
+        for k, v in vars(batch).items():
+            setattr(static, k, v.clone() if torch.is_tensor(v) else v)
+        if hasattr(static, "_mark"):
+            static._mark()  # sorted/symmetric Laplacian flags on the static tensors
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        s = self._stream
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        ops.clear_caches()
+        with torch.cuda.graph(g, pool=self._pool, stream=s):
+            loss = self._fwd_bwd(static)
+            if self.world == 1:
+                self._opt_step()
+            # every stream forked from the capture (the node / edge side streams,
+            # forks inside autograd backward nodes, which run on autograd's
+            # device thread) rejoins it before hipStreamEndCapture: an unjoined
+            # fork is what crashed capture_end in round 1
+            if self._ext is not None:
+                ops.join_capture_streams(self.device)
+        left = ops.side_streams_capturing(self.device) if self._ext is not None else []
+        if left:
+            raise RuntimeError(f"TrainStep: {len(left)} side stream(s) still capturing after the "
+                               f"graph capture ended (unjoined fork); refusing the graph")
+        ops.clear_caches()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        if len(self._graphs) >= self.max_graphs:
+            self._graphs.pop(next(iter(self._graphs)))
+        ent = _Captured(g, static, loss)
+        self._graphs[key] = ent
+        self.stats["captures"] += 1
+        return ent
+
+    def __call__(self, batch) -> torch.Tensor:
+        # a kernel of an earlier step that reported unusable results (the
+        # device error word, read without synchronising) stops training here
+        if self._ext is not None:
+            ops.check_device_errors(sync=False)
+        if not self.graphs:
+            return self._eager(batch)
+        key = batch_key(batch)
+        ent = self._graphs.get(key)
+        if ent is None:
+            loss = self._eager(batch)
+            self._capture(batch, key)
+            return loss
+        ent.load(batch)
+        ent.graph.replay()
+        if self.world > 1:
+            self._exchange_and_update()
+        self.stats["replay"] += 1
+        return ent.loss
+
+    def state_dict(self):
+        return {"model": self.model.state_dict(), "opt": self.opt.state_dict()}
