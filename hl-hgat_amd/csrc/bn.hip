@@ -66,13 +66,10 @@ struct BnLayout {
   int64_t rows_per_part;
 };
 
-// HLHGAT_BN_ONE_LAUNCH=0: two launches per direction even where one fits
-// (A/B; bitwise the same results).
+// hlhgat_set_bn_one_launch(0): two launches per direction even where one
+// fits (tests; bitwise the same results).
 bool& bn_one_launch_flag() {
-  static bool v = [] {
-    const char* e = getenv("HLHGAT_BN_ONE_LAUNCH");
-    return !(e && e[0] == '0');
-  }();
+  static bool v = true;
   return v;
 }
 bool bn_one_launch() { return bn_one_launch_flag(); }
@@ -80,16 +77,12 @@ bool bn_one_launch() { return bn_one_launch_flag(); }
 // Row partitions: >= 128 (same-box A/B at the ZINC step, n ~ 25k: 64 ->
 // 281.8k, 128 -> 287.2k, 256 -> 286.1k, 32 -> 265.8k graphs/s), one per 512
 // rows above (config 3 / 5 heads, 1.4e5-2e5 rows: 64 workgroups left most of
-// the 256 CUs idle).  HLHGAT_BN_PARTS overrides (A/B).
+// the 256 CUs idle).
 int64_t bn_parts(int64_t n) {
-  static int64_t fixed = [] {
-    const char* e = getenv("HLHGAT_BN_PARTS");
-    return e ? atoll(e) : (int64_t)0;
-  }();
-  int64_t p = fixed > 0 ? fixed : std::max<int64_t>(128, ceil_div(n, (int64_t)512));
+  int64_t p = std::max<int64_t>(128, ceil_div(n, (int64_t)512));
   // small batches (the readout MLP: one row per graph): >= 64 rows per
   // partition, so the finaliser's partial loads stay one batch deep
-  if (!fixed) p = std::min<int64_t>(p, std::max<int64_t>(1, ceil_div(n, (int64_t)64)));
+  p = std::min<int64_t>(p, std::max<int64_t>(1, ceil_div(n, (int64_t)64)));
   return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
 }
 
@@ -553,18 +546,6 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(StatsArgs a) {
   k_bn_stats_body<V>(a, blk_hw());
 }
 
-// node + edge sides of an HL block in one launch (launch groups, common.h)
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_stats_pair(Pair<StatsArgs> p) {
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    k_bn_stats_body<V>(p.a[0], b);
-  else
-    k_bn_stats_body<V>(p.a[1], b);
-}
-
 struct ApplyArgs {
   const int32_t* nvalid;
   const float* x;
@@ -622,18 +603,6 @@ __device__ __forceinline__ void k_bn_apply_body(const ApplyArgs& a, Blk blk) {
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_apply(ApplyArgs a) {
   k_bn_apply_body<V>(a, blk_hw());
-}
-
-// node + edge sides of an HL block in one launch (launch groups, common.h)
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_apply_pair(Pair<ApplyArgs> p) {
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    k_bn_apply_body<V>(p.a[0], b);
-  else
-    k_bn_apply_body<V>(p.a[1], b);
 }
 
 struct BwdApplyArgs {
@@ -738,18 +707,6 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
   k_bn_bwd_reduce_body<V>(a, blk_hw());
 }
 
-// node + edge sides of an HL block in one launch (launch groups, common.h)
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce_pair(Pair<StatsArgs> p) {
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    k_bn_bwd_reduce_body<V>(p.a[0], b);
-  else
-    k_bn_bwd_reduce_body<V>(p.a[1], b);
-}
-
 template <int V>
 __device__ __forceinline__ void k_bn_bwd_apply_body(const BwdApplyArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
@@ -795,18 +752,6 @@ __device__ __forceinline__ void k_bn_bwd_apply_body(const BwdApplyArgs& a, Blk b
 template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_bwd_apply(BwdApplyArgs a) {
   k_bn_bwd_apply_body<V>(a, blk_hw());
-}
-
-// node + edge sides of an HL block in one launch (launch groups, common.h)
-template <int V>
-__global__ __launch_bounds__(kThreads) void k_bn_bwd_apply_pair(Pair<BwdApplyArgs> p) {
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    k_bn_bwd_apply_body<V>(p.a[0], b);
-  else
-    k_bn_bwd_apply_body<V>(p.a[1], b);
 }
 
 // ---------------------------------------------------------------------------
@@ -1045,18 +990,6 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
   k_bn_fwd_grid_body<V, RPT>(a, blk_hw());
 }
 
-// node + edge sides of an HL block in one launch (launch groups, common.h)
-template <int V, int RPT>
-__global__ __launch_bounds__(kThreads) void k_bn_fwd_grid_pair(Pair<StatsArgs> p) {
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    k_bn_fwd_grid_body<V, RPT>(p.a[0], b);
-  else
-    k_bn_fwd_grid_body<V, RPT>(p.a[1], b);
-}
-
 bool bn_vec_ok(int64_t C, std::initializer_list<int64_t> lds,
                std::initializer_list<const void*> ptrs) {
   if (C % 4) return false;
@@ -1149,57 +1082,18 @@ GridFn fwd_grid_fn(bool vec, int rpt) {
 
 // The one-launch kernel for this layout, or nullptr (two launches).
 GridFn pick_grid(const BnLayout& L, bool vec) {
-  static const bool dbg = getenv("HLHGAT_BN_DEBUG") != nullptr;
   if (!bn_one_launch() || L.parts > kFlatMax) return nullptr;
   const int64_t grid = (int64_t)L.parts * L.tiles;
   const int rpt = rpt_bucket(L);
   GridFn f = rpt ? fwd_grid_fn(vec, rpt) : nullptr;
   const int64_t cap = f ? capacity_of(reinterpret_cast<const void*>(f)) : 0;
-  if (dbg)
-    fprintf(stderr, "[hlhgat bn] parts %d tiles %d rows/part %lld rpt %d vec %d cap %lld -> %s\n",
-            L.parts, L.tiles, (long long)L.rows_per_part, rpt, (int)vec,
-            (long long)cap, (f && grid <= 256 && grid <= cap) ? "one launch" : "two launches");
   if (!f || grid > 256 || grid > cap) return nullptr;
   return f;
 }
 
-template <int V>
-void reg_bn_pairs() {
-  register_pair(reinterpret_cast<const void*>(k_bn_stats<V>),
-                reinterpret_cast<const void*>(k_bn_stats_pair<V>), false);
-  register_pair(reinterpret_cast<const void*>(k_bn_apply<V>),
-                reinterpret_cast<const void*>(k_bn_apply_pair<V>), false);
-  register_pair(reinterpret_cast<const void*>(k_bn_bwd_reduce<V>),
-                reinterpret_cast<const void*>(k_bn_bwd_reduce_pair<V>), false);
-  register_pair(reinterpret_cast<const void*>(k_bn_bwd_apply<V>),
-                reinterpret_cast<const void*>(k_bn_bwd_apply_pair<V>), false);
-}
-template <int V, int RPT>
-void reg_bn_grid_pair() {  // a grid barrier: the joint grid must be co-resident
-  register_pair(reinterpret_cast<const void*>(k_bn_fwd_grid<V, RPT>),
-                reinterpret_cast<const void*>(k_bn_fwd_grid_pair<V, RPT>), true);
-}
-
-const int g_bn_pairs = [] {
-  reg_bn_pairs<1>();
-  reg_bn_pairs<4>();
-  reg_bn_grid_pair<1, 2>(); reg_bn_grid_pair<1, 4>(); reg_bn_grid_pair<1, 8>();
-  reg_bn_grid_pair<1, 16>(); reg_bn_grid_pair<1, 32>();
-  reg_bn_grid_pair<4, 2>(); reg_bn_grid_pair<4, 4>(); reg_bn_grid_pair<4, 8>();
-  reg_bn_grid_pair<4, 16>(); reg_bn_grid_pair<4, 32>();
-  return 0;
-}();
 
 }  // namespace
 
-namespace hlhgat {
-// The pair of two one-launch BatchNorm grids waits at two grid barriers at
-// once: both grids together must fit the same half-capacity bound as one
-// grid alone (pick_grid).
-bool pair_coresident(const void* pair_kernel, int64_t blocks) {
-  return blocks <= capacity_of(pair_kernel);
-}
-}  // namespace hlhgat
 
 extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
   if (n < 0 || C <= 0) return 0;

@@ -10,10 +10,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdarg>
-#include <functional>
-#include <memory>
 #include <string>
-#include <tuple>
 
 #include "../../include/hlhgat.h"
 
@@ -74,141 +71,21 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 struct ProfScope {
   int slot = -1;
   hipEvent_t start_ev = nullptr, stop_ev = nullptr;
-  // what the scope measures, kept for launches deferred by a launch group
-  // (the slot is then taken when the launch is finally issued)
   int cls = -1;
   double bytes = 0.0, flops = 0.0;
   ProfScope(int kernel_class, hipStream_t s, double bytes, double flops);
 };
 
-// ---------------------------------------------------------------------------
-// Launch groups (hlhgat_group_begin / _next / _end, include/hlhgat.h): the
-// node-side and edge-side launch sequences of an HL block are recorded as the
-// two MEMBERS of a group instead of being issued; at the end the i-th launch
-// of member 0 and the i-th of member 1 become ONE launch of the kernel's pair
-// variant (both argument sets behind one grid: workgroups [0, start1) run
-// member 0's grid, the rest member 1's) whenever both are the same kernel and
-// a pair variant is registered, otherwise they are issued one after the
-// other.  Each member's launches stay in their recorded order.
-// ---------------------------------------------------------------------------
-struct Blk {  // a workgroup's coordinates in its member's (x, y) grid
+struct Blk {  // a workgroup's coordinates in its (x, y) grid
   unsigned x, y, gx, gy;
 };
 __device__ __forceinline__ Blk blk_hw() { return Blk{blockIdx.x, blockIdx.y, gridDim.x, gridDim.y}; }
 
-template <class A>
-struct Pair {
-  A a[2];
-  unsigned gx[2], gy[2];
-  unsigned start1;  // first workgroup of member 1 (a multiple of 8: it starts on XCD 0)
-};
-
-// Member s and the workgroup's coordinates in its grid; false for the
-// alignment padding between the two grids.
-template <class A>
-__device__ __forceinline__ bool pair_blk(const Pair<A>& p, int& s, Blk& b) {
-  unsigned L = blockIdx.x;
-  s = L >= p.start1 ? 1 : 0;
-  if (s) L -= p.start1;
-  b.gx = p.gx[s];
-  b.gy = p.gy[s];
-  b.x = L % b.gx;
-  b.y = L / b.gx;
-  return b.y < b.gy;
-}
-
-// Pair variant of a kernel whose body is BODY(const A&, Blk); each member's
-// branch reads its own argument block at a static offset.
-#define HLH_PAIR_KERNEL(NAME, A, BODY)                                          \
-  __global__ __launch_bounds__(256) void NAME(::hlhgat::Pair<A> p) {          \
-    int s;                                                                     \
-    ::hlhgat::Blk b;                                                           \
-    if (!::hlhgat::pair_blk(p, s, b)) return;                                  \
-    if (s == 0)                                                                \
-      BODY(p.a[0], b);                                                         \
-    else                                                                       \
-      BODY(p.a[1], b);                                                         \
-  }
-
-struct Recorded;
-using PairLauncher = void (*)(const Recorded&, const Recorded&, hipStream_t, const ProfScope*);
-struct Recorded {
-  const void* kernel = nullptr;
-  dim3 grid, block;
-  uint32_t shmem = 0;
-  int cls = -1;
-  double bytes = 0.0, flops = 0.0;
-  std::shared_ptr<void> args;                               // typed copy of the argument block
-  std::function<void(hipStream_t, const ProfScope*)> solo;  // issue alone
-  PairLauncher pair = nullptr;                              // issue with a partner (same kernel)
-};
-
-bool group_recording();         // this thread is recording a launch group
-void group_record(Recorded&& r);  // append to the current member
-
-// Registered pair variants: solo kernel -> (pair kernel, co-residency bound)
-struct PairEntry {
-  const void* pair_kernel;
-  bool needs_coresidency;  // grid-barrier kernels: the pair grid must fit (see bn.hip)
-};
-void register_pair(const void* solo, const void* pair, bool needs_coresidency);
-const PairEntry* find_pair(const void* solo);
-// bn.hip: may this many workgroups of `pair_kernel` wait at a grid barrier?
-bool pair_coresident(const void* pair_kernel, int64_t blocks);
-
-template <class A>
-void pair_launch_typed(const Recorded& r0, const Recorded& r1, hipStream_t s,
-                       const ProfScope* p) {
-  Pair<A> P;
-  P.a[0] = *static_cast<const A*>(r0.args.get());
-  P.a[1] = *static_cast<const A*>(r1.args.get());
-  P.gx[0] = r0.grid.x;
-  P.gy[0] = r0.grid.y;
-  P.gx[1] = r1.grid.x;
-  P.gy[1] = r1.grid.y;
-  const unsigned n0 = r0.grid.x * r0.grid.y;
-  P.start1 = (n0 + 7u) & ~7u;
-  const unsigned total = P.start1 + r1.grid.x * r1.grid.y;
-  auto* k = reinterpret_cast<void (*)(Pair<A>)>(const_cast<void*>(find_pair(r0.kernel)->pair_kernel));
-  const uint32_t shmem = r0.shmem > r1.shmem ? r0.shmem : r1.shmem;
-  if (p && p->start_ev)
-    hipExtLaunchKernelGGL(k, dim3(total), r0.block, shmem, s, p->start_ev, p->stop_ev, 0, P);
-  else
-    hipLaunchKernelGGL(k, dim3(total), r0.block, shmem, s, P);
-}
-
 // Launch `k` on `s`; when `p` holds a live ProfScope the launch goes through
-// hipExtLaunchKernelGGL with its start/stop events.  Inside a launch group
-// the launch is recorded instead (single-argument kernels keep a typed copy
-// so that a partner can be paired with it).
+// hipExtLaunchKernelGGL with its start/stop events.
 template <typename... KArgs, typename... Args>
 inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s,
                    const ProfScope* p, Args... args) {
-  if (group_recording()) {
-    Recorded r;
-    r.kernel = reinterpret_cast<const void*>(k);
-    r.grid = grid;
-    r.block = block;
-    r.shmem = shmem;
-    if (p) {
-      r.cls = p->cls;
-      r.bytes = p->bytes;
-      r.flops = p->flops;
-    }
-    r.solo = [=](hipStream_t st, const ProfScope* q) {
-      if (q && q->start_ev)
-        hipExtLaunchKernelGGL(k, grid, block, shmem, st, q->start_ev, q->stop_ev, 0, args...);
-      else
-        hipLaunchKernelGGL(k, grid, block, shmem, st, args...);
-    };
-    if constexpr (sizeof...(Args) == 1) {
-      using A = std::tuple_element_t<0, std::tuple<Args...>>;
-      r.args = std::make_shared<A>(args...);
-      r.pair = &pair_launch_typed<A>;
-    }
-    group_record(std::move(r));
-    return;
-  }
   if (p && p->start_ev)
     hipExtLaunchKernelGGL(k, grid, block, shmem, s, p->start_ev, p->stop_ev, 0, args...);
   else

@@ -203,32 +203,6 @@ __global__ __launch_bounds__(256) void k_poly_step_deep(PolyArgs a) {
   poly_step_body<V, LPR, 8>(a, blk_hw());
 }
 
-// node + edge steps of an HL block in one launch (launch groups, common.h)
-template <int V, int LPR>
-__global__ __launch_bounds__(256) void k_poly_step_pair(Pair<PolyArgs> p) {
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    poly_step_body<V, LPR, 4>(p.a[0], b);
-  else
-    poly_step_body<V, LPR, 4>(p.a[1], b);
-}
-
-template <int V, int LPR>
-void reg_poly_pair() {
-  register_pair(reinterpret_cast<const void*>(k_poly_step<V, LPR>),
-                reinterpret_cast<const void*>(k_poly_step_pair<V, LPR>), false);
-}
-
-const int g_poly_pairs = [] {
-  reg_poly_pair<4, 1>(); reg_poly_pair<4, 2>(); reg_poly_pair<4, 4>(); reg_poly_pair<4, 8>();
-  reg_poly_pair<4, 16>(); reg_poly_pair<4, 32>(); reg_poly_pair<4, 64>();
-  reg_poly_pair<2, 16>(); reg_poly_pair<2, 32>(); reg_poly_pair<2, 64>();
-  reg_poly_pair<1, 16>(); reg_poly_pair<1, 32>(); reg_poly_pair<1, 64>();
-  return 0;
-}();
-
 // ---------------------------------------------------------------------------
 // Second factor of the Hodge-factored L1 (hlhgat_hodge_factor_t):
 //   acc = alpha_e (Z[j] - Z[i]) = (-alpha_e) Z[i] + alpha_e Z[j]
@@ -400,241 +374,8 @@ __global__ __launch_bounds__(NT) void k_poly_halo(PolyArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Graph-local polynomial basis (block-diagonal batches, one launch per basis)
-//
-// A PairData batch is block-diagonal: every Laplacian entry of a graph's rows
-// points at rows of the same graph (lib/Hodge_Dataset.py:40-48).  A tile is a
-// run of whole graphs (<= max_rows rows, built at collate time); one workgroup
-// owns a tile, stages its rows of X in LDS and computes T_1 .. T_{K-1} there,
-// gathering neighbours from LDS.  Only X is read and only T_1.. written:
-// K-1 launches (and K-1 round trips through L2 of each T_k) become one.  The
-// adjoint is the same walk in reverse and writes only dX.  Each row's entries
-// are summed in CSR order with the same operations as k_poly_step, so the
-// results are bitwise those of the step-by-step path.
-// ---------------------------------------------------------------------------
-constexpr int LOC_MAXK = 16;
-constexpr int LOC_RPG = 8;  // max rows per row group (max_rows <= LOC_RPG * 256 / LPR)
-
-struct LocalArgs {
-  const int32_t* rowptr;
-  const int32_t* col;
-  const float* val;
-  const int32_t* tile_ptr;
-  int max_rows, max_nnz, pitch, F, K;
-  const float* X;  // fwd: T_0 (row stride ldx)
-  int64_t ldx;
-  float* out;      // fwd: T_1..T_{K-1} blocks; bwd: G_0..G_{K-1} blocks ([n][F] each)
-  int64_t n;
-  float alpha[LOC_MAXK], beta[LOC_MAXK], gamma[LOC_MAXK], div[LOC_MAXK], q[LOC_MAXK];
-  int hasz[LOC_MAXK], hasq[LOC_MAXK];
-};
-
-// Tile staging shared by both directions: the tile's CSR slice (row offsets,
-// tile-local columns, weights) goes to LDS once and serves all K-1 steps, so
-// the per-row loop touches no global memory on its critical path.
-struct LocalTile {
-  int r0, nr, e_lo;
-  const int* rp;   // LDS: nr+1 offsets relative to e_lo
-  const int* cl;   // LDS: tile-local column per entry (NULL: tile exceeds max_nnz)
-  const float* wv; // LDS: weight per entry
-  const int32_t* gcol;  // global fallback (columns, NOT tile-local)
-  const float* gval;
-};
-
-__device__ __forceinline__ LocalTile stage_tile(const LocalArgs& a, char* base, int t) {
-  LocalTile T;
-  T.r0 = a.tile_ptr[t];
-  T.nr = a.tile_ptr[t + 1] - T.r0;
-  T.e_lo = a.rowptr[T.r0];
-  int* rp = reinterpret_cast<int*>(base);
-  int* cl = rp + (a.max_rows + 1);
-  float* wv = reinterpret_cast<float*>(cl + a.max_nnz);
-  const int ne = a.rowptr[T.r0 + T.nr] - T.e_lo;
-  const bool fits = ne <= a.max_nnz;  // graph_tiles packs tiles so; otherwise read globally
-  for (int r = threadIdx.x; r <= T.nr; r += 256) rp[r] = a.rowptr[T.r0 + r] - T.e_lo;
-  if (fits) {
-    for (int e = threadIdx.x; e < ne; e += 256) {
-      int c = a.col[T.e_lo + e] - T.r0;
-      cl[e] = (c >= 0 && c < T.nr) ? c : 0;  // never leaves the tile (block-diagonal)
-      wv[e] = a.val ? a.val[T.e_lo + e] : 1.f;
-    }
-  }
-  T.rp = rp;
-  T.cl = fits ? cl : nullptr;
-  T.wv = fits ? wv : nullptr;
-  T.gcol = a.col + T.e_lo;
-  T.gval = a.val ? a.val + T.e_lo : nullptr;
-  return T;
-}
-
-// acc = sum_e w_e * S[c_e] over tile row r's entries, CSR order, 4 LDS reads in flight
-template <int V>
-__device__ __forceinline__ typename VecT<V>::type local_gather(const LocalTile& T, int r,
-                                                                const float* S, int pitch,
-                                                                int f) {
-  using vt = typename VecT<V>::type;
-  vt acc;
-#pragma unroll
-  for (int i = 0; i < V; ++i) vget(acc, i) = 0.f;
-  int e = T.rp[r];
-  const int e1 = T.rp[r + 1];
-  if (!T.cl) {  // oversized tile: entries from global memory, same order
-    for (; e < e1; ++e) {
-      int c = T.gcol[e] - T.r0;
-      c = (c >= 0 && c < T.nr) ? c : 0;
-      const float w = T.gval ? T.gval[e] : 1.f;
-      vt x = *reinterpret_cast<const vt*>(S + c * pitch + f);
-#pragma unroll
-      for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
-    }
-    return acc;
-  }
-  for (; e + 3 < e1; e += 4) {
-    const int c0 = T.cl[e], c1 = T.cl[e + 1], c2 = T.cl[e + 2], c3 = T.cl[e + 3];
-    const float w0 = T.wv[e], w1 = T.wv[e + 1], w2 = T.wv[e + 2], w3 = T.wv[e + 3];
-    vt x0 = *reinterpret_cast<const vt*>(S + c0 * pitch + f);
-    vt x1 = *reinterpret_cast<const vt*>(S + c1 * pitch + f);
-    vt x2 = *reinterpret_cast<const vt*>(S + c2 * pitch + f);
-    vt x3 = *reinterpret_cast<const vt*>(S + c3 * pitch + f);
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      float s = vget(acc, i);
-      s = s + w0 * vget(x0, i);
-      s = s + w1 * vget(x1, i);
-      s = s + w2 * vget(x2, i);
-      s = s + w3 * vget(x3, i);
-      vget(acc, i) = s;
-    }
-  }
-  for (; e < e1; ++e) {
-    vt x = *reinterpret_cast<const vt*>(S + T.cl[e] * pitch + f);
-    const float w = T.wv[e];
-#pragma unroll
-    for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
-  }
-  return acc;
-}
-
-template <int V, int LPR>
-__global__ __launch_bounds__(256) void k_basis_local_fwd(LocalArgs a) {
-  using vt = typename VecT<V>::type;
-  extern __shared__ float lds[];
-  const int t = (int)xcd_slot(blockIdx.x, gridDim.x);
-  const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
-  constexpr int G = 256 / LPR;
-  const int f = sub * V;
-  const bool fok = f < a.F;
-  float* bufA = lds;
-  float* bufB = lds + a.max_rows * a.pitch;
-  const LocalTile T = stage_tile(a, reinterpret_cast<char*>(bufB + a.max_rows * a.pitch), t);
-  const int r0 = T.r0, nr = T.nr;
-  const int64_t blk = a.n * a.F;
-  for (int r = grp; r < nr; r += G)
-    if (fok) *reinterpret_cast<vt*>(bufA + r * a.pitch + f) = vload<V>(a.X + (r0 + r) * a.ldx + f);
-  __syncthreads();
-  float* prev = bufA;  // T_{k-1}
-  float* cur = bufA;   // T_k (k = 0: X)
-  float* nxt = bufB;
-  for (int k = 0; k + 1 < a.K; ++k) {
-    // T_{k+1} = (alpha L T_k + beta T_k + gamma T_{k-1}) / div  -> nxt (may alias prev)
-    if (fok) {
-      for (int r = grp; r < nr; r += G) {
-        vt acc = local_gather<V>(T, r, cur, a.pitch, f);
-        vt o;
-#pragma unroll
-        for (int i = 0; i < V; ++i) vget(o, i) = a.alpha[k] * (1.f * vget(acc, i));
-        if (a.beta[k] != 0.f) {
-          vt xr = *reinterpret_cast<const vt*>(cur + r * a.pitch + f);
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) + a.beta[k] * vget(xr, i);
-        }
-        if (a.hasz[k]) {
-          vt z = *reinterpret_cast<const vt*>(prev + r * a.pitch + f);
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) + a.gamma[k] * vget(z, i);
-        }
-        if (a.div[k] != 1.f) {
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) / a.div[k];
-        }
-        *reinterpret_cast<vt*>(nxt + r * a.pitch + f) = o;
-        vstore<V>(a.out + (int64_t)k * blk + (r0 + r) * a.F + f, o);
-      }
-    }
-    __syncthreads();
-    // roll: T_k -> prev, T_{k+1} -> cur; T_{k+2} overwrites T_k's buffer (its
-    // gamma term reads T_k[r] before the same lanes write T_{k+2}[r])
-    float* old_cur = cur;
-    cur = nxt;
-    prev = old_cur;
-    nxt = old_cur;
-  }
-}
-
-template <int V, int LPR>
-__global__ __launch_bounds__(256) void k_basis_local_bwd(LocalArgs a) {
-  using vt = typename VecT<V>::type;
-  extern __shared__ float lds[];
-  const int t = (int)xcd_slot(blockIdx.x, gridDim.x);
-  const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
-  constexpr int G = 256 / LPR;
-  const int f = sub * V;
-  const bool fok = f < a.F;
-  const int64_t blk = a.n * a.F;
-  float* cur = lds;                           // G_k
-  float* other = lds + a.max_rows * a.pitch;  // G_{k+1}, then the new G_{k-1}
-  const LocalTile T = stage_tile(a, reinterpret_cast<char*>(other + a.max_rows * a.pitch), t);
-  const int r0 = T.r0, nr = T.nr;
-  for (int r = grp; r < nr; r += G)
-    if (fok)
-      *reinterpret_cast<vt*>(cur + r * a.pitch + f) =
-          vload<V>(a.out + (int64_t)(a.K - 1) * blk + (r0 + r) * a.F + f);
-  __syncthreads();
-  for (int k = a.K - 1; k >= 1; --k) {
-    // G_{k-1} += (alpha L^T G_k + beta G_k) / div + q G_{k+1}
-    if (fok) {
-      vt pv[LOC_RPG];  // this group's rows of G_{k-1}: all loads in flight first
-#pragma unroll
-      for (int u = 0; u < LOC_RPG; ++u) {
-        const int r = grp + u * G;
-        if (r < nr) pv[u] = vload<V>(a.out + (int64_t)(k - 1) * blk + (r0 + r) * a.F + f);
-      }
-#pragma unroll
-      for (int u = 0; u < LOC_RPG; ++u) {
-        const int r = grp + u * G;
-        if (r >= nr) break;
-        vt acc = local_gather<V>(T, r, cur, a.pitch, f);
-        vt o;
-#pragma unroll
-        for (int i = 0; i < V; ++i) vget(o, i) = a.alpha[k] * (1.f * vget(acc, i));
-        if (a.beta[k] != 0.f) {
-          vt xr = *reinterpret_cast<const vt*>(cur + r * a.pitch + f);
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) + a.beta[k] * vget(xr, i);
-        }
-        if (a.div[k] != 1.f) {
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) / a.div[k];
-        }
-#pragma unroll
-        for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) + 1.f * vget(pv[u], i);
-        if (a.hasq[k]) {
-          vt qv = *reinterpret_cast<const vt*>(other + r * a.pitch + f);
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(o, i) = vget(o, i) + a.q[k] * vget(qv, i);
-        }
-        *reinterpret_cast<vt*>(other + r * a.pitch + f) = o;
-      }
-    }
-    __syncthreads();
-    float* tmp = cur;
-    cur = other;
-    other = tmp;
-  }
-  for (int r = grp; r < nr; r += G)
-    if (fok) vstore<V>(a.out + (r0 + r) * a.F + f, *reinterpret_cast<const vt*>(cur + r * a.pitch + f));
-}
+// longest recurrence the DEMO adjoint fold unrolls
+constexpr int DEMO_MAXK = 16;
 
 // out[e] = ca*(sa[i]*x[i]) + cb*(sb[j]*x[j]) (+ z[e]) (+ out[e])
 struct Gather2Args {
@@ -695,6 +436,8 @@ struct SegArgs {
   int d;
   float* out;
   int64_t ldo;
+  int64_t n_rows;   // bwd, contiguous segments: rows of dx (0 = no fill)
+  int64_t n_fill;   // bwd: lane groups after the segment groups that zero-fill
 };
 
 template <int V, int LPR>
@@ -721,13 +464,32 @@ __global__ __launch_bounds__(256) void k_segment_mean_fwd(SegArgs a) {
   }
 }
 
-// dx[r] = dout[s] / max(|seg s|, 1) for each member r of segment s.
+// dx[r] = dout[s] / max(|seg s|, 1) for each member r of segment s.  With
+// contiguous segments the lane groups after the first n_seg write exact
+// zeros into the rows no segment covers, [0, ptr[0]) and [ptr[n_seg], n_rows)
+// (the adjoint of global_mean_pool is zero there, lib/Hodge_ST_Model.py:636):
+// padding rows of a padded batch never carry uninitialised memory upstream.
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_segment_mean_bwd(SegArgs a) {
   using vt = typename VecT<V>::type;
   const int64_t s = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
   const int sub = threadIdx.x % LPR;
-  if (s >= a.n_seg) return;
+  if (s >= a.n_seg) {
+    const int64_t z = s - a.n_seg;
+    if (z >= a.n_fill) return;
+    const int64_t lo = a.ptr[0], hi = a.ptr[a.n_seg];
+    vt zero;
+#pragma unroll
+    for (int c = 0; c < V; ++c) vget(zero, c) = 0.f;
+    for (int64_t r = z; r < a.n_rows; r += a.n_fill) {
+      if (r >= lo && r < hi) {
+        r = hi - 1 - ((hi - 1 - z) % a.n_fill);  // next stride point >= hi
+        continue;
+      }
+      for (int f = sub * V; f < a.d; f += LPR * V) vstore<V>(a.out + r * a.ldo + f, zero);
+    }
+    return;
+  }
   const int r0 = a.ptr[s], r1 = a.ptr[s + 1];
   const float cnt = (float)(r1 - r0 > 0 ? r1 - r0 : 1);
   // here x = dout (ldx), out = dx (ldo)
@@ -795,118 +557,6 @@ int pick_lpr(int64_t d, int v) {
     }                                                                          \
   } while (0)
 
-#define HLH_DISPATCH_LOCAL(V, L, KERNEL, GRID, SHMEM, STREAM, PROF, ARGS)                  \
-  do {                                                                                   \
-    switch ((V) * 100 + (L)) {                                                           \
-      case 101: launch(KERNEL<1, 1>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 102: launch(KERNEL<1, 2>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 104: launch(KERNEL<1, 4>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 108: launch(KERNEL<1, 8>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 116: launch(KERNEL<1, 16>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 132: launch(KERNEL<1, 32>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 164: launch(KERNEL<1, 64>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 201: launch(KERNEL<2, 1>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 202: launch(KERNEL<2, 2>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 204: launch(KERNEL<2, 4>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 208: launch(KERNEL<2, 8>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 216: launch(KERNEL<2, 16>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 232: launch(KERNEL<2, 32>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 264: launch(KERNEL<2, 64>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 401: launch(KERNEL<4, 1>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 402: launch(KERNEL<4, 2>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 404: launch(KERNEL<4, 4>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 408: launch(KERNEL<4, 8>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;       \
-      case 416: launch(KERNEL<4, 16>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 432: launch(KERNEL<4, 32>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      case 464: launch(KERNEL<4, 64>, GRID, 256, SHMEM, STREAM, PROF, ARGS); break;      \
-      default: break;                                                                    \
-    }                                                                                    \
-  } while (0)
-
-constexpr int64_t kLocalLdsBytes = 64 * 1024;
-
-// Graph-local basis launch if the tiles fit (returns 1 = launched, 0 = use the
-// step-by-step path).  fwd: X -> T_1..T_{K-1};  bwd: G blocks -> G_0.
-int launch_local(bool fwd, int kind, const int32_t* rowptr, const int32_t* col,
-                 const float* val, int64_t n, int64_t nnz, const int32_t* tile_ptr,
-                 int64_t n_tiles,
-                 int64_t max_rows, int64_t max_nnz, const float* X, int64_t ldx, int64_t F,
-                 int K, float* out, hipStream_t s) {
-  if (!tile_ptr || n_tiles <= 0 || max_rows <= 0 || max_nnz <= 0 || K > LOC_MAXK) return 0;
-  if (kind == HLHGAT_POLY_LAGUERRE_DEMO) return 0;  // step path only
-  const int v = pick_vec(F, {fwd ? ldx : F, F}, {fwd ? X : out, out});
-  const int l = pick_lpr(F, v);
-  if ((int64_t)l * v < F) return 0;  // one lane group must span the features
-  if (max_rows > (int64_t)LOC_RPG * (256 / l)) return 0;
-  const int pitch = l * v + 4;
-  const int64_t shmem = 2 * max_rows * (int64_t)pitch * 4 + 4 * (max_rows + 1) + 8 * max_nnz;
-  if (shmem > kLocalLdsBytes) return 0;
-  LocalArgs a{};
-  a.rowptr = rowptr;
-  a.col = col;
-  a.val = val;
-  a.tile_ptr = tile_ptr;
-  a.max_rows = (int)max_rows;
-  a.max_nnz = (int)max_nnz;
-  a.pitch = pitch;
-  a.F = (int)F;
-  a.K = K;
-  a.X = X;
-  a.ldx = ldx;
-  a.out = out;
-  a.n = n;
-  for (int k = 0; k < LOC_MAXK; ++k) {
-    a.alpha[k] = 1.f;
-    a.beta[k] = 0.f;
-    a.gamma[k] = 0.f;
-    a.div[k] = 1.f;
-    a.q[k] = 0.f;
-  }
-  const bool lag = kind == HLHGAT_POLY_LAGUERRE;
-  if (fwd) {  // same coefficients as hlhgat_poly_basis_fwd's steps
-    if (lag) {
-      a.alpha[0] = -1.f;
-      a.beta[0] = 1.f;
-    }
-    for (int k = 1; k + 1 < K; ++k) {
-      a.hasz[k] = 1;
-      if (lag) {
-        a.alpha[k] = -1.f;
-        a.beta[k] = (float)(2 * k + 1);
-        a.gamma[k] = -(float)k;
-        a.div[k] = (float)(k + 1);
-      } else {
-        a.alpha[k] = 2.f;
-        a.gamma[k] = -1.f;
-      }
-    }
-  } else {  // same coefficients as hlhgat_poly_basis_bwd's steps
-    for (int k = K - 1; k >= 1; --k) {
-      a.hasq[k] = k + 1 <= K - 1;
-      if (lag) {
-        a.alpha[k] = -1.f;
-        a.beta[k] = (float)(2 * k - 1);
-        a.div[k] = (float)k;
-        a.q[k] = -(float)k / (float)(k + 1);
-      } else {
-        a.alpha[k] = (k == 1) ? 1.f : 2.f;
-        a.q[k] = -1.f;
-      }
-    }
-  }
-  const dim3 grid((unsigned)n_tiles);
-  // algorithmic bytes: the CSR once, every dense [n][F] block
-  // once (fwd: X in, T_1..T_{K-1} out; bwd: G_0..G_{K-1} in, G_0 out)
-  ProfScope prof(HLHGAT_PROF_POLY, s,
-                 8.0 * (double)nnz + 4.0 * (double)(n + 1) + 4.0 * (double)n * F * K,
-                 2.0 * (double)nnz * F * (K - 1));
-  if (fwd)
-    HLH_DISPATCH_LOCAL(v, l, k_basis_local_fwd, grid, (unsigned)shmem, s, &prof, a);
-  else
-    HLH_DISPATCH_LOCAL(v, l, k_basis_local_bwd, grid, (unsigned)shmem, s, &prof, a);
-  return 1;
-}
-
 // Algorithmic bytes of one poly-step launch: CSR streamed once
 // (int32 col + fp32 val per nnz, int32 rowptr), the gathered operand counted
 // once per row (X read once), every dense row operand read once, Y written.
@@ -923,12 +573,12 @@ struct DemoArgs {
 __global__ __launch_bounds__(256) void k_demo_adjoint_fold(DemoArgs a) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= a.blk) return;
-  float g[LOC_MAXK];
+  float g[DEMO_MAXK];
 #pragma unroll
-  for (int k = 0; k < LOC_MAXK; ++k) g[k] = k < a.K ? a.G[k * a.blk + i] : 0.f;
+  for (int k = 0; k < DEMO_MAXK; ++k) g[k] = k < a.K ? a.G[k * a.blk + i] : 0.f;
   float ds = 0.f;
 #pragma unroll
-  for (int k = LOC_MAXK - 1; k >= 2; --k) {  // T_k from T_{k-1}, T_{k-2}, S
+  for (int k = DEMO_MAXK - 1; k >= 2; --k) {  // T_k from T_{k-1}, T_{k-2}, S
     if (k >= a.K) continue;
     const float gk = g[k] / (float)k;
     g[k - 1] = g[k - 1] + (float)(2 * k - 1) * gk;
@@ -980,9 +630,7 @@ int launch_poly(PolyArgs& a, int64_t nnz, hipStream_t s, int prof_class = HLHGAT
   // gathered X rows; measured on the TSP L1 Laguerre step at d = 128: 164 ->
   // 116 us (profiles/r01_g_tsp_spmm.log).  Small (ZINC) operators keep
   // ordinary stores -- their consumer re-reads Y from L2 / MALL right away.
-  // HLHGAT_NT=0/1 forces either way (A/B).
-  static const int nt_env = getenv("HLHGAT_NT") ? atoi(getenv("HLHGAT_NT")) : -1;
-  a.nt_store = nt_env >= 0 ? nt_env : ((double)a.n_rows * a.d * 4.0 >= kNtStoreBytes);
+  a.nt_store = (double)a.n_rows * a.d * 4.0 >= kNtStoreBytes;
   ProfScope prof(prof_class, s, prof_bytes >= 0.0 ? prof_bytes : poly_bytes(a, nnz),
                  2.0 * (double)nnz * a.d);
   if (a.lcol && a.n_tiles > 0) {
@@ -1105,8 +753,7 @@ int launch_factored(PolyArgs a, const hlhgat_hodge_factor_t& f, float* work, hip
                                a.B ? a.ldb : 4},
                          {a.X, a.Y, a.Z, a.P, a.Q, a.B});
   const int l = pick_lpr(a.d, v);
-  static const int nt_env = getenv("HLHGAT_NT") ? atoi(getenv("HLHGAT_NT")) : -1;
-  a.nt_store = nt_env >= 0 ? nt_env : ((double)a.n_rows * a.d * 4.0 >= kNtStoreBytes);
+  a.nt_store = (double)a.n_rows * a.d * 4.0 >= kNtStoreBytes;
   // own algorithmic bytes: ends + alpha, Z read once, Y and the dense epilogue operands
   int dense = 1 + (a.beta != 0.f) + (a.Z != nullptr) + (a.P != nullptr) + (a.Q != nullptr);
   ProfScope prof(HLHGAT_PROF_HODGE_EDGE, s,
@@ -1171,8 +818,7 @@ extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
 namespace {
 int basis_fwd_core(int kind, const int32_t* rowptr, const int32_t* col, const float* val,
                    int64_t n, int64_t nnz, const int32_t* row_order, const hlhgat_halo_t* halo,
-                   const int32_t* tile_ptr, int64_t n_tiles, int64_t max_tile_rows,
-                   int64_t max_tile_nnz, const float* X, int64_t ldx, int64_t F, int K, float* T,
+                   const float* X, int64_t ldx, int64_t F, int K, float* T,
                    const hlhgat_hodge_factor_t* fac, float* work, void* stream) {
   HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB ||
                     kind == HLHGAT_POLY_LAGUERRE_DEMO,
@@ -1182,11 +828,6 @@ int basis_fwd_core(int kind, const int32_t* rowptr, const int32_t* col, const fl
   HLH_CHECK_ARG(T, "poly_basis_fwd: T is NULL");
   hipStream_t s = as_stream(stream);
   const StepRunner run{nnz, fac, work, s};
-  if (!fac && launch_local(true, kind, rowptr, col, val, n, nnz, tile_ptr, n_tiles, max_tile_rows,
-                           max_tile_nnz, X, ldx, F, K, T, s)) {
-    HLH_CHECK_LAUNCH();
-    return HLHGAT_OK;
-  }
   const int64_t blk = n * F;
   auto Tk = [&](int k) -> float* { return T + (int64_t)(k - 1) * blk; };
   // T_1
@@ -1236,8 +877,7 @@ int basis_fwd_core(int kind, const int32_t* rowptr, const int32_t* col, const fl
 
 int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
                    const float* val_t, int64_t n, int64_t nnz, const int32_t* row_order,
-                   const hlhgat_halo_t* halo, const int32_t* tile_ptr, int64_t n_tiles,
-                   int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F, int K, float* G,
+                   const hlhgat_halo_t* halo, int64_t F, int K, float* G,
                    const hlhgat_hodge_factor_t* fac, float* work, void* stream) {
   HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB ||
                     kind == HLHGAT_POLY_LAGUERRE_DEMO,
@@ -1247,19 +887,13 @@ int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
   HLH_CHECK_ARG(G, "poly_basis_bwd: G is NULL");
   hipStream_t s = as_stream(stream);
   const StepRunner run{nnz, fac, work, s};
-  if (!fac && launch_local(false, kind, rowptr_t, col_t, val_t, n, nnz, tile_ptr, n_tiles,
-                   max_tile_rows,
-                   max_tile_nnz, nullptr, F, F, K, G, s)) {
-    HLH_CHECK_LAUNCH();
-    return HLHGAT_OK;
-  }
   const int64_t blk = n * F;
   auto Gk = [&](int k) -> float* { return G + (int64_t)k * blk; };
   if (kind == HLHGAT_POLY_LAGUERRE_DEMO) {
     // Every T_k (k >= 1) depends on x through S = L x and the recurrence:
     // one elementwise reverse sweep folds G_K-1..G_1 into dS (block 1) and
     // the direct part of dX (block 0), then dX += L^T dS.
-    HLH_CHECK_ARG(K <= LOC_MAXK, "poly_basis_bwd: DEMO recurrence needs K <= %d", LOC_MAXK);
+    HLH_CHECK_ARG(K <= DEMO_MAXK, "poly_basis_bwd: DEMO recurrence needs K <= %d", DEMO_MAXK);
     DemoArgs d{G, n * F, K};
     launch(k_demo_adjoint_fold, dim3((unsigned)ceil_div(n * F, (int64_t)256)), dim3(256), 0, s,
            nullptr, d);
@@ -1301,22 +935,18 @@ int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
 extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
                                      const float* val, int64_t n, int64_t nnz,
                                      const int32_t* row_order, const hlhgat_halo_t* halo,
-                                     const int32_t* tile_ptr, int64_t n_tiles,
-                                     int64_t max_tile_rows, int64_t max_tile_nnz,
                                      const float* X, int64_t ldx, int64_t F, int K, float* T,
                                      void* stream) {
-  return basis_fwd_core(kind, rowptr, col, val, n, nnz, row_order, halo, tile_ptr, n_tiles,
-                        max_tile_rows, max_tile_nnz, X, ldx, F, K, T, nullptr, nullptr, stream);
+  return basis_fwd_core(kind, rowptr, col, val, n, nnz, row_order, halo, X, ldx, F, K, T,
+                        nullptr, nullptr, stream);
 }
 
 extern "C" int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t, const int32_t* col_t,
                                      const float* val_t, int64_t n, int64_t nnz,
                                      const int32_t* row_order, const hlhgat_halo_t* halo,
-                                     const int32_t* tile_ptr, int64_t n_tiles,
-                                     int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F,
-                                     int K, float* G, void* stream) {
-  return basis_bwd_core(kind, rowptr_t, col_t, val_t, n, nnz, row_order, halo, tile_ptr,
-                        n_tiles, max_tile_rows, max_tile_nnz, F, K, G, nullptr, nullptr, stream);
+                                     int64_t F, int K, float* G, void* stream) {
+  return basis_bwd_core(kind, rowptr_t, col_t, val_t, n, nnz, row_order, halo, F, K, G,
+                        nullptr, nullptr, stream);
 }
 
 extern "C" int64_t hlhgat_hodge_factor_work_floats(int64_t n_nodes, int64_t F) {
@@ -1360,16 +990,16 @@ extern "C" int hlhgat_poly_basis_fwd_factored(int kind, const hlhgat_hodge_facto
                                               const float* X, int64_t ldx, int64_t F, int K,
                                               float* T, float* work, void* stream) {
   HLH_CHECK_ARG(f, "poly_basis_fwd_factored: NULL factor");
-  return basis_fwd_core(kind, nullptr, nullptr, nullptr, f->n_edges, 0, nullptr, nullptr,
-                        nullptr, 0, 0, 0, X, ldx, F, K, T, f, work, stream);
+  return basis_fwd_core(kind, nullptr, nullptr, nullptr, f->n_edges, 0, nullptr, nullptr, X, ldx,
+                        F, K, T, f, work, stream);
 }
 
 extern "C" int hlhgat_poly_basis_bwd_factored(int kind, const hlhgat_hodge_factor_t* f,
                                               int64_t F, int K, float* G, float* work,
                                               void* stream) {
   HLH_CHECK_ARG(f, "poly_basis_bwd_factored: NULL factor");
-  return basis_bwd_core(kind, nullptr, nullptr, nullptr, f->n_edges, 0, nullptr, nullptr,
-                        nullptr, 0, 0, 0, F, K, G, f, work, stream);
+  return basis_bwd_core(kind, nullptr, nullptr, nullptr, f->n_edges, 0, nullptr, nullptr, F, K,
+                        G, f, work, stream);
 }
 
 extern "C" int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
@@ -1400,7 +1030,7 @@ extern "C" int hlhgat_segment_mean_fwd(const int32_t* seg_ptr,
                 "segment_mean_fwd: bad sizes");
   if (n_seg == 0) return HLHGAT_OK;
   HLH_CHECK_ARG(seg_ptr && x && out, "segment_mean_fwd: NULL pointer");
-  SegArgs a{seg_ptr, seg_rows, n_seg, x, ldx, (int)d, out, ldo};
+  SegArgs a{seg_ptr, seg_rows, n_seg, x, ldx, (int)d, out, ldo, 0, 0};
   const int v = pick_vec(d, {ldx, ldo}, {x, out});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
@@ -1412,16 +1042,19 @@ extern "C" int hlhgat_segment_mean_fwd(const int32_t* seg_ptr,
 extern "C" int hlhgat_segment_mean_bwd(const int32_t* seg_ptr,
                                        const int32_t* seg_rows, int64_t n_seg,
                                        const float* dout, int64_t ldo, int64_t d,
-                                       float* dx, int64_t ldx, void* stream) {
-  HLH_CHECK_ARG(n_seg >= 0 && d > 0 && ldx >= d && ldo >= d,
+                                       float* dx, int64_t ldx, int64_t n_rows,
+                                       void* stream) {
+  HLH_CHECK_ARG(n_seg >= 0 && d > 0 && ldx >= d && ldo >= d && n_rows >= 0,
                 "segment_mean_bwd: bad sizes");
-  if (n_seg == 0) return HLHGAT_OK;
-  HLH_CHECK_ARG(seg_ptr && dout && dx, "segment_mean_bwd: NULL pointer");
-  SegArgs a{seg_ptr, seg_rows, n_seg, dout, ldo, (int)d, dx, ldx};
+  // listed members (scatter_mean): the caller zero-fills dx; no fill here
+  const int64_t n_fill = seg_rows ? 0 : (n_rows < 1024 ? n_rows : 1024);
+  if (n_seg == 0 && n_fill == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(seg_ptr && dx && (n_seg == 0 || dout), "segment_mean_bwd: NULL pointer");
+  SegArgs a{seg_ptr, seg_rows, n_seg, dout, ldo, (int)d, dx, ldx, n_rows, n_fill};
   const int v = pick_vec(d, {ldx, ldo}, {dout, dx});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
-  HLH_DISPATCH_VL(v, l, k_segment_mean_bwd, n_seg, s, a, nullptr);
+  HLH_DISPATCH_VL(v, l, k_segment_mean_bwd, n_seg + n_fill, s, a, nullptr);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

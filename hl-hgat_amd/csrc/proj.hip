@@ -345,19 +345,6 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
   proj_fwd_lds_body<TN>(a, blk_hw(), wl);
 }
 
-// node + edge projections of an HL block in one launch (launch groups)
-template <int TN>
-__global__ __launch_bounds__(256) void k_proj_fwd_lds_pair(Pair<FwdArgs> p) {
-  __shared__ float wl[2][TN * 16][KCP];
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    proj_fwd_lds_body<TN>(p.a[0], b, wl);
-  else
-    proj_fwd_lds_body<TN>(p.a[1], b, wl);
-}
-
 // ---------------------------------------------------------------------------
 // data gradient: dA_b = dC W_b   (reduction over N)
 // ---------------------------------------------------------------------------
@@ -900,8 +887,6 @@ __global__ __launch_bounds__(256) void k_reduce_splits(ReduceArgs a) {
   reduce_splits_body(a, blk_hw());
 }
 
-HLH_PAIR_KERNEL(k_reduce_splits_pair, ReduceArgs, reduce_splits_body)
-
 // ---------------------------------------------------------------------------
 // Linear backward with the weight-gradient partials and the data gradient in
 // ONE launch: workgroups [0, n_w) are the weight gradient's (tile, split)
@@ -967,36 +952,6 @@ __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   proj_bwd_fused_body<TND>(a, blk_hw(), lds);
 }
 
-// node + edge Linear backwards of an HL block in one launch (launch groups)
-template <int TND>
-__global__ __launch_bounds__(256) void k_proj_bwd_fused_pair(Pair<BwdFusedArgs> p) {
-  constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
-  __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
-  int s;
-  Blk b;
-  if (!pair_blk(p, s, b)) return;
-  if (s == 0)
-    proj_bwd_fused_body<TND>(p.a[0], b, lds);
-  else
-    proj_bwd_fused_body<TND>(p.a[1], b, lds);
-}
-
-const int g_proj_pairs = [] {
-  register_pair(reinterpret_cast<const void*>(k_proj_fwd_lds<1>),
-                reinterpret_cast<const void*>(k_proj_fwd_lds_pair<1>), false);
-  register_pair(reinterpret_cast<const void*>(k_proj_fwd_lds<2>),
-                reinterpret_cast<const void*>(k_proj_fwd_lds_pair<2>), false);
-  register_pair(reinterpret_cast<const void*>(k_proj_fwd_lds<4>),
-                reinterpret_cast<const void*>(k_proj_fwd_lds_pair<4>), false);
-  register_pair(reinterpret_cast<const void*>(k_proj_bwd_fused<1>),
-                reinterpret_cast<const void*>(k_proj_bwd_fused_pair<1>), false);
-  register_pair(reinterpret_cast<const void*>(k_proj_bwd_fused<2>),
-                reinterpret_cast<const void*>(k_proj_bwd_fused_pair<2>), false);
-  register_pair(reinterpret_cast<const void*>(k_reduce_splits),
-                reinterpret_cast<const void*>(k_reduce_splits_pair), false);
-  return 0;
-}();
-
 // --- planning ------------------------------------------------------------------
 struct WeightPlan {
   int tiles_n;
@@ -1008,15 +963,6 @@ struct WeightPlan {
   int64_t bias_off;
   int tile_start[MAXB + 1];
 };
-
-// HLHGAT_WSPLIT_ROWS: rows per weight-gradient split (A/B; 0 = plan below)
-int64_t wsplit_rows() {
-  static int64_t v = [] {
-    const char* e = getenv("HLHGAT_WSPLIT_ROWS");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  return v;
-}
 
 WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
                        bool with_bias) {
@@ -1048,44 +994,21 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   if (splits < 1) splits = 1;
   int64_t rps = ceil_div(M, splits);
   rps = ceil_div(rps, 64) * 64;
-  if (wsplit_rows() > 0) rps = ceil_div(wsplit_rows(), 64) * 64;
   if (rps < 64) rps = 64;
   p.rows_per_split = rps;
   p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
   return p;
 }
 
-// HLHGAT_WEIGHT_XCD=0 turns off the XCD-aware work order of the weight
-// gradient (A/B; results are identical either way)
-int weight_xcd_map() {
-  static int v = [] {
-    const char* e = getenv("HLHGAT_WEIGHT_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-// HLHGAT_DATA_XCD=0: plain (row block fastest) order of the fused backward's
-// data-gradient workgroups instead of the XCD-aware one (A/B; same results)
-int data_xcd_map() {
-  static int v = [] {
-    const char* e = getenv("HLHGAT_DATA_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
+// XCD-aware work orders of the weight gradient's items and of the fused
+// backward's data-gradient workgroups (results are identical in any order)
+constexpr int weight_xcd_map() { return 1; }
+constexpr int data_xcd_map() { return 1; }
 
 // Data-gradient tiles of 64 columns (TN 4) where the size rule picks more
 // than one 16-column tile: each staged dC row block serves 64 output columns
-// (+1.3 % at the ZINC step, same-box A/B); HLHGAT_BWD_TND=2 restores the
-// 32-column tiles (same results either way)
-int bwd_tnd() {
-  static int v = [] {
-    const char* e = getenv("HLHGAT_BWD_TND");
-    return e ? atoi(e) : 4;
-  }();
-  return v;
-}
+// (+1.3 % at the ZINC step against 32-column tiles, same-box A/B)
+constexpr int bwd_tnd() { return 4; }
 
 bool vec_ok(const float* p, int64_t ld, int64_t kb) {
   return aligned16(p) && (ld % 4) == 0 && (kb % 4) == 0;
@@ -1289,7 +1212,6 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   hipStream_t s = as_stream(stream);
   if (M == 0) {
     // no rows: gradient contribution is zero
-    HLH_CHECK_ARG(!group_recording(), "proj_bwd_weight: M == 0 inside a launch group");
     if (!accumulate) {
       for (int b = 0; b < nblocks; ++b)
         for (int64_t n = 0; n < N; ++n)
@@ -1349,7 +1271,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     HLH_CHECK_ARG(merge->words[0] == kDescMagic, "proj_bwd: merge is not a reduce descriptor");
     prev = reinterpret_cast<const ReduceArgs*>(&merge->words[1]);
   }
-  if (group_recording()) defer_out = nullptr;  // launch groups: nothing deferred
   HLH_CHECK_ARG(nb_w >= 0 && nb_w <= MAXB && nb_d >= 0 && nb_d <= MAXB,
                 "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
   HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd: bad dC");
@@ -1365,7 +1286,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
-  if (prev && (!fuse || group_recording())) {  // run the merged reduction on its own first
+  if (prev && !fuse) {  // run the merged reduction on its own first
     const int rc = run_reduce(*prev, as_stream(stream));
     if (rc != HLHGAT_OK) return rc;
     prev = nullptr;

@@ -39,7 +39,6 @@ ProfScope::ProfScope(int kernel_class, hipStream_t s, double b, double f)
     : cls(kernel_class), bytes(b), flops(f) {
   (void)s;
   if (kernel_class < 0 || kernel_class >= HLHGAT_PROF_NCLASS) return;
-  if (group_recording()) return;  // the slot is taken when the launch is issued
   std::lock_guard<std::mutex> lk(g_prof_mu);
   ProfClass& pc = g_prof[kernel_class];
   if (!pc.enabled) return;
@@ -53,56 +52,6 @@ ProfScope::ProfScope(int kernel_class, hipStream_t s, double b, double f)
   start_ev = pc.start[slot];
   stop_ev = pc.stop[slot];
 }
-
-// --- launch groups (common.h) ------------------------------------------------
-namespace {
-struct GroupState {
-  bool active = false;
-  int member = 0;
-  std::vector<Recorded> m[2];
-};
-thread_local GroupState g_group;
-
-std::mutex g_pair_mu;
-std::vector<std::pair<const void*, PairEntry>>& pair_table() {
-  static auto* t = new std::vector<std::pair<const void*, PairEntry>>();
-  return *t;
-}
-}  // namespace
-
-bool group_recording() { return g_group.active; }
-
-void group_record(Recorded&& r) { g_group.m[g_group.member].push_back(std::move(r)); }
-
-void register_pair(const void* solo, const void* pair, bool needs_coresidency) {
-  std::lock_guard<std::mutex> lk(g_pair_mu);
-  pair_table().push_back({solo, PairEntry{pair, needs_coresidency}});
-}
-
-const PairEntry* find_pair(const void* solo) {
-  std::lock_guard<std::mutex> lk(g_pair_mu);
-  for (const auto& kv : pair_table())
-    if (kv.first == solo) return &kv.second;
-  return nullptr;
-}
-
-namespace {
-// the i-th launches of the two members: one pair launch when possible
-bool can_pair(const Recorded& a, const Recorded& b) {
-  if (a.kernel != b.kernel || !a.pair || a.grid.z != 1 || b.grid.z != 1) return false;
-  if (a.block.x != b.block.x || a.block.y != b.block.y || a.block.z != b.block.z) return false;
-  const PairEntry* e = find_pair(a.kernel);
-  if (!e) return false;
-  const int64_t total = (int64_t)((a.grid.x * a.grid.y + 7u) & ~7u) + (int64_t)b.grid.x * b.grid.y;
-  if (total >= (int64_t)UINT32_MAX) return false;
-  return !e->needs_coresidency || pair_coresident(e->pair_kernel, total);
-}
-
-void issue_solo(const Recorded& r, hipStream_t s) {
-  ProfScope p(r.cls, s, r.bytes, r.flops);
-  r.solo(s, &p);
-}
-}  // namespace
 
 // --- device error word -------------------------------------------------------
 // One pinned, mapped, coherent host word shared by all devices: kernels store
@@ -153,55 +102,6 @@ extern "C" int hlhgat_clear_device_errors(void) {
 }
 
 extern "C" const char* hlhgat_last_error(void) { return g_last_error.c_str(); }
-
-extern "C" int hlhgat_group_begin(void) {
-  HLH_CHECK_ARG(!g_group.active, "group_begin: a launch group is already being recorded");
-  g_group.m[0].clear();
-  g_group.m[1].clear();
-  g_group.member = 0;
-  g_group.active = true;
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_group_next(void) {
-  HLH_CHECK_ARG(g_group.active && g_group.member == 0,
-                "group_next: no launch group, or its second member already started");
-  g_group.member = 1;
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_group_abort(void) {
-  g_group.active = false;
-  g_group.m[0].clear();
-  g_group.m[1].clear();
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_group_end(void* stream, int* paired) {
-  HLH_CHECK_ARG(g_group.active, "group_end: no launch group is being recorded");
-  g_group.active = false;
-  std::vector<Recorded> m0 = std::move(g_group.m[0]), m1 = std::move(g_group.m[1]);
-  g_group.m[0].clear();
-  g_group.m[1].clear();
-  hipStream_t s = as_stream(stream);
-  int np = 0;
-  const size_t n = m0.size() > m1.size() ? m0.size() : m1.size();
-  for (size_t i = 0; i < n; ++i) {
-    const Recorded* a = i < m0.size() ? &m0[i] : nullptr;
-    const Recorded* b = i < m1.size() ? &m1[i] : nullptr;
-    if (a && b && can_pair(*a, *b)) {
-      ProfScope p(a->cls, s, a->bytes + b->bytes, a->flops + b->flops);
-      a->pair(*a, *b, s, &p);
-      ++np;
-    } else {
-      if (a) issue_solo(*a, s);
-      if (b) issue_solo(*b, s);
-    }
-    HLH_CHECK_LAUNCH();
-  }
-  if (paired) *paired = np;
-  return HLHGAT_OK;
-}
 
 extern "C" int hlhgat_prof_enable(int kernel_class, int enable) {
   HLH_CHECK_ARG(kernel_class >= 0 && kernel_class < HLHGAT_PROF_NCLASS,

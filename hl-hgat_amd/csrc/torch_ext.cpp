@@ -140,46 +140,6 @@ hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_e
   return h;
 }
 
-// ---------------------------------------------------------------------------
-// Launch groups (include/hlhgat.h hlhgat_group_*): while the node and edge
-// sides of an HL block are recorded, launches are deferred to the end of the
-// group, so every temporary a recorded launch reads or writes must outlive
-// the group: keep_alive() parks it until the group ends (a no-op otherwise).
-// ---------------------------------------------------------------------------
-std::vector<Tensor>*& keep_list() {
-  static thread_local std::vector<Tensor>* k = nullptr;
-  return k;
-}
-inline const Tensor& keep_alive(const Tensor& t) {
-  if (keep_list() && t.defined()) keep_list()->push_back(t);
-  return t;
-}
-
-struct LaunchGroup {
-  std::vector<Tensor> keep;
-  bool active = false;
-  void begin() {
-    chk(hlhgat_group_begin(), "group_begin");
-    active = true;
-    keep_list() = &keep;
-  }
-  void next() { chk(hlhgat_group_next(), "group_next"); }
-  int end(void* stream) {
-    int paired = 0;
-    active = false;
-    keep_list() = nullptr;
-    chk(hlhgat_group_end(stream, &paired), "group_end");
-    keep.clear();  // launches are enqueued: the caching allocator orders reuse on the stream
-    return paired;
-  }
-  ~LaunchGroup() {
-    if (active) {
-      hlhgat_group_abort();
-      keep_list() = nullptr;
-    }
-  }
-};
-
 // One BN workspace per (device, stream): its arrival counters must not be
 // shared by launches that can run concurrently (node / edge chains run on two
 // streams, see hlhgat.ops.fork).  Stream-ordered reuse on one stream is safe.
@@ -187,12 +147,10 @@ struct LaunchGroup {
 // earlier on that stream still holds its address, and a replay must not write
 // BN counters into memory the caching allocator has handed to another tensor.
 // (Sizes grow geometrically, so at most a handful are ever retired.)
-Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C, int slot = 0) {
+Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
   static auto* cache = new std::unordered_map<uintptr_t, Tensor>();  // leaked: outlives HIP teardown
   static auto* retired = new std::vector<Tensor>();
-  // slot: the member of a launch group (its two sides' BatchNorms run in one launch)
-  const uintptr_t key =
-      (reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device()) * 2 + (slot & 1);
+  const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
   const int64_t need = hlhgat_bn_workspace_bytes(n, C);
   auto it = cache->find(key);
   if (it == cache->end() || it->second.numel() < need) {
@@ -297,20 +255,16 @@ void proj_bwd_weight(const Tensor& G, const std::vector<const float*>& A,
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
       hlhgat_proj_bwd_weight_workspace_floats(nb, kb.data(), M, N, db != nullptr);
-  Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
+  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, G.options());
   chk(hlhgat_proj_bwd_weight(nb, G.data_ptr<float>(), ld_of(G), A.data(), lda.data(), kb.data(),
                              M, N, dW.data(), lddw.data(), db, 0, ws.data_ptr<float>(), wsf, s),
       "proj_bwd_weight");
 }
 
-// HLHGAT_FUSED_BWD=0 (or set_fused_bwd(false)): weight and data gradients
-// as separate launches instead of hlhgat_proj_bwd's single launch (A/B; the
-// results are bitwise the same).
+// set_fused_bwd(false) (tests): weight and data gradients as separate
+// launches instead of hlhgat_proj_bwd's single launch (bitwise the same).
 bool& fused_bwd_flag() {
-  static bool on = [] {
-    const char* e = getenv("HLHGAT_FUSED_BWD");
-    return !(e && e[0] == '0');
-  }();
+  static bool on = true;
   return on;
 }
 void set_fused_bwd(bool on) { fused_bwd_flag() = on; }
@@ -478,7 +432,7 @@ std::vector<int64_t> reduce_flush(int64_t device) {
   const bool bad = d.violation;
   d.violation = false;
   TORCH_CHECK(!bad, "hlhgat: a parameter whose split reduction was deferred received a second "
-                    "gradient in the same backward (set HLHGAT_DEFER_REDUCE=0)");
+                    "gradient in the same backward (set hlhgat.train.DEFER_REDUCE = False)");
   return out;
 }
 
@@ -495,16 +449,14 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
       nbw ? hlhgat_proj_bwd_weight_workspace_floats(nbw, kbw.data(), M, N, db != nullptr) : 0;
-  Tensor ws = keep_alive(at::empty({std::max<int64_t>(wsf, 1)}, G.options()));
+  Tensor ws = at::empty({std::max<int64_t>(wsf, 1)}, G.options());
   auto& d = defer_state();
   std::unique_lock<std::mutex> g(d.mu);
   // force_defer: private gradient buffers read only by deferred copies (the
   // NodeEdgeInt unpack), which the flush runs after every reduction
-  bool defer = d.on && nbw > 0 && !keep_list() && (force_defer || deferred_ok(db));
+  bool defer = d.on && nbw > 0 && (force_defer || deferred_ok(db));
   for (int b = 0; b < nbw && defer && !force_defer; ++b) defer = deferred_ok(dW[b]);
-  // inside a launch group the launches are issued at the group's end: a
-  // pending reduction stays pending (merged later or run by the flush)
-  auto it = keep_list() ? d.pending.end() : d.pending.find(s);
+  auto it = d.pending.find(s);
   PendingReduce prev;
   const bool merge = it != d.pending.end();
   if (merge) {
@@ -542,13 +494,13 @@ struct BnState {
 };
 
 Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
-                  const Tensor* y_into = nullptr, int slot = 0) {
+                  const Tensor* y_into = nullptr) {
   const int64_t n = x.size(0), C = x.size(1);
   Tensor y = y_into ? *y_into : at::empty({n, C}, x.options());
   TORCH_CHECK(y.size(0) == n && y.size(1) == C && y.stride(1) == 1, "hlhgat: bad BN output view");
   mean = at::empty({C}, x.options());
   invstd = at::empty({C}, x.options());
-  Tensor ws = bn_workspace(x, n, C, slot);
+  Tensor ws = bn_workspace(x, n, C);
   int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
   chk(hlhgat_bn_fwd_train(x.data_ptr<float>(), ld_of(x), n, iptr(st.valid), C, fptr(st.w),
                           fptr(st.b),
@@ -559,33 +511,21 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
   return y;
 }
 
-// HLHGAT_GRAPH_LOCAL=1: the graph-local polynomial basis (k_basis_local_*: a
-// workgroup walks the whole recurrence of a tile of whole graphs in LDS;
-// bitwise equal to the step launches and, at the ZINC shape, equal in cost).
-bool graph_local_env() {
-  static const bool on = [] {
-    const char* e = getenv("HLHGAT_GRAPH_LOCAL");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 // returns dx; fills dw/db when requested
 // dx_into: optional [n, C] row-strided destination (e.g. a column slice)
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
                    const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
                    Tensor& dw, Tensor& db, const Tensor* dx_into = nullptr,
-                   const Tensor* b_param = nullptr, const Tensor& valid = Tensor(),
-                   int slot = 0) {
+                   const Tensor* b_param = nullptr, const Tensor& valid = Tensor()) {
   const int64_t n = x.size(0), C = x.size(1);
-  Tensor dyc = keep_alive(rows2d(dy));
+  Tensor dyc = rows2d(dy);
   Tensor dx = dx_into ? *dx_into : at::empty({n, C}, x.options());
   TORCH_CHECK(dx.size(0) == n && dx.size(1) == C && dx.stride(1) == 1, "hlhgat: bad dx view");
   dw = (need_w && has(w)) ? grad_like(w) : Tensor();
   db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
                                                  : at::empty({C}, x.options()))
               : Tensor();
-  Tensor ws = bn_workspace(x, n, C, slot);
+  Tensor ws = bn_workspace(x, n, C);
   chk(hlhgat_bn_bwd_train(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
                           dyc.data_ptr<float>(), ld_of(dyc), n,
                           valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
@@ -658,8 +598,7 @@ struct ConvArgs {
   OptT bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt;
   double momentum = 0.1, eps = 1e-5;
   int64_t bn_mode = 0;
-  OptT out_buf, a_order, t_order, tiles;
-  int64_t tile_rows = 0, tile_nnz = 0;
+  OptT out_buf, a_order, t_order;
   OptT valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval;
   std::vector<int64_t> h_bounds;
   OptT h_hdr;
@@ -669,18 +608,17 @@ struct ConvArgs {
 
 // What one side's backward needs: the tensors (kSavedFixed, then W[0..K),
 // then the factor) and the sizes.
-constexpr size_t kSavedFixed = 22;
+constexpr size_t kSavedFixed = 21;
 struct ConvSaved {
   std::vector<Tensor> t;
   std::vector<int64_t> dims;  // N, Cin, F, M, dout, K, kind, nnz, bn_mode, has_bias
   std::vector<int64_t> xshape, h_bounds;
-  int64_t fac_nodes = 0, tile_rows = 0, tile_nnz = 0;
+  int64_t fac_nodes = 0;
   void to_ctx(AutogradContext* ctx, const std::string& p) const {
     ctx->saved_data[p + "dims"] = dims;
     ctx->saved_data[p + "xshape"] = xshape;
     ctx->saved_data[p + "h_bounds"] = h_bounds;
-    ctx->saved_data[p + "misc"] = std::vector<int64_t>{fac_nodes, tile_rows, tile_nnz,
-                                                       (int64_t)t.size()};
+    ctx->saved_data[p + "misc"] = std::vector<int64_t>{fac_nodes, (int64_t)t.size()};
   }
   static ConvSaved from_ctx(AutogradContext* ctx, const std::string& p,
                             const std::vector<Tensor>& all, size_t first) {
@@ -690,9 +628,7 @@ struct ConvSaved {
     s.h_bounds = ctx->saved_data[p + "h_bounds"].toIntVector();
     const auto m = ctx->saved_data[p + "misc"].toIntVector();
     s.fac_nodes = m[0];
-    s.tile_rows = m[1];
-    s.tile_nnz = m[2];
-    s.t.assign(all.begin() + first, all.begin() + first + m[3]);
+    s.t.assign(all.begin() + first, all.begin() + first + m[1]);
     return s;
   }
 };
@@ -708,9 +644,8 @@ struct ConvGrads {
   std::vector<Tensor> dW;
 };
 
-// HodgeLaguerreConv / HodgeChebConv forward (+ BN (+ ReLU)) of one side;
-// `slot` = its member in a launch group (BatchNorm workspace).
-Tensor conv_forward(const ConvArgs& c, ConvSaved& sv, int slot) {
+// HodgeLaguerreConv / HodgeChebConv forward (+ BN (+ ReLU)) of one side.
+Tensor conv_forward(const ConvArgs& c, ConvSaved& sv) {
   const Tensor& x = c.x;
   req(x, "x");
   const int64_t N = x.size(0);
@@ -730,12 +665,9 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv, int slot) {
                            has(c.h_sval) ? *c.h_sval : Tensor(), c.h_bounds, *c.h_hdr)
                : hlhgat_halo_t{};
   const bool factored = !c.fac.empty();
-  // graph tiles: the graph-local basis on request (HLHGAT_GRAPH_LOCAL=1)
-  const bool local_basis = has(c.tiles) && graph_local_env();
   if (factored && K > 1 && N > 0) {
     const hlhgat_hodge_factor_t hf = make_factor(c.fac, c.fac_nodes, N);
-    Tensor work = keep_alive(
-        at::empty({hlhgat_hodge_factor_work_floats(c.fac_nodes, F)}, x.options()));
+    Tensor work = at::empty({hlhgat_hodge_factor_work_floats(c.fac_nodes, F)}, x.options());
     chk(hlhgat_poly_basis_fwd_factored((int)c.kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
                                        (int)K, T.data_ptr<float>(), work.data_ptr<float>(), s),
         "poly_basis_fwd_factored");
@@ -743,10 +675,7 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv, int slot) {
     chk(hlhgat_poly_basis_fwd((int)c.kind, c.a_rowptr.data_ptr<int>(),
                               c.nnz ? c.a_col.data_ptr<int>() : nullptr,
                               c.nnz ? fptr(c.a_val) : nullptr, N, c.nnz, iptr(c.a_order),
-                              use_halo ? &halo : nullptr,
-                              local_basis ? iptr(c.tiles) : nullptr,
-                              local_basis ? c.tiles->numel() - 1 : 0, c.tile_rows, c.tile_nnz,
-                              x2.data_ptr<float>(), ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
+                              use_halo ? &halo : nullptr, x2.data_ptr<float>(), ld_of(x2), F, (int)K, T.data_ptr<float>(), s),
         "poly_basis_fwd");
   }
   std::vector<const float*> Ap(K), Wp(K);
@@ -779,19 +708,16 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv, int slot) {
   }
   if (c.bn_mode > 0) {
     BnState st{c.bn_w, c.bn_b, c.bn_rm, c.bn_rv, c.bn_nbt, c.momentum, c.eps, c.valid};
-    out = bn_forward(pre, st, c.bn_mode == 2, mean, invstd, sink ? &*c.out_buf : nullptr, slot);
+    out = bn_forward(pre, st, c.bn_mode == 2, mean, invstd, sink ? &*c.out_buf : nullptr);
   }
   sv.dims = {N, Cin, F, M, dout, K, c.kind, c.nnz, c.bn_mode, has(c.bias) ? 1 : 0};
   sv.fac_nodes = c.fac_nodes;
-  sv.tile_rows = c.tile_rows;
-  sv.tile_nnz = c.tile_nnz;
   sv.h_bounds = c.h_bounds;
   sv.xshape = x.sizes().vec();
   const bool halo_bwd = use_halo && c.t_rowptr.data_ptr() == c.a_rowptr.data_ptr();
   sv.t = {x2,
           T,
           has(c.t_order) ? *c.t_order : Tensor(),
-          has(c.tiles) ? *c.tiles : Tensor(),
           has(c.valid) ? *c.valid : Tensor(),
           c.t_rowptr,
           c.t_col,
@@ -817,16 +743,16 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv, int slot) {
   return out.view(oshape);
 }
 
-ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds& nd, int slot) {
+ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds& nd) {
   const auto& d = sv.dims;
   const int64_t N = d[0], Cin = d[1], F = d[2], M = d[3], dout = d[4], K = d[5], kind = d[6],
                 nnz = d[7], bn_mode = d[8];
   const bool has_bias = d[9] != 0;
   const auto& t = sv.t;
-  Tensor x2 = t[0], T = t[1], t_order = t[2], tiles = t[3], valid = t[4], t_rowptr = t[5],
-         t_col = t[6], t_val = t[7], pre = t[8], yout = t[9], mean = t[10], invstd = t[11],
-         bn_w = t[12], bias_p = t[13], bn_b = t[14], h_tile = t[15], h_ptr = t[16],
-         h_cols = t[17], h_srp = t[18], h_lcol = t[19], h_sval = t[20], h_hdr = t[21];
+  Tensor x2 = t[0], T = t[1], t_order = t[2], valid = t[3], t_rowptr = t[4], t_col = t[5],
+         t_val = t[6], pre = t[7], yout = t[8], mean = t[9], invstd = t[10], bn_w = t[11],
+         bias_p = t[12], bn_b = t[13], h_tile = t[14], h_ptr = t[15], h_cols = t[16],
+         h_srp = t[17], h_lcol = t[18], h_sval = t[19], h_hdr = t[20];
   std::vector<Tensor> W(t.begin() + kSavedFixed, t.begin() + kSavedFixed + K);
   std::vector<Tensor> fac(t.begin() + kSavedFixed + K, t.end());
   const bool use_halo = h_lcol.defined();
@@ -835,7 +761,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
                : hlhgat_halo_t{};
   void* s = stream_of(x2);
   // row-strided is fine (e.g. a column block of the gradient slab)
-  Tensor G = keep_alive(rows2d(grad.reshape({M, dout})));
+  Tensor G = rows2d(grad.reshape({M, dout}));
   ConvGrads out;
   out.dW.resize(K);
   std::vector<const float*> Ap(K);
@@ -857,15 +783,15 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
   if (bn_mode > 0) {
     const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
     OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-    G = keep_alive(bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w,
-                               out.dbn_b, nullptr, &bn_b, valid, slot));
+    G = bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
+                    nullptr, &bn_b, valid);
   }
   if (need_w || need_b) {
     std::vector<Tensor> dW(K);
     std::vector<float*> dWp(K);
     std::vector<int64_t> lddw(K);
     for (int64_t k = 0; k < K; ++k) {
-      dW[k] = keep_alive(nd.w[k] ? grad_like(W[k]) : at::empty({dout, Cin}, x2.options()));
+      dW[k] = nd.w[k] ? grad_like(W[k]) : at::empty({dout, Cin}, x2.options());
       dWp[k] = dW[k].data_ptr<float>();
       lddw[k] = Cin;
     }
@@ -889,7 +815,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
     if (need_b) out.dbias = db;
   }
   if (nd.x) {
-    Tensor Gs = keep_alive(at::empty({K, N, F}, x2.options()));
+    Tensor Gs = at::empty({K, N, F}, x2.options());
     if (M > 0) {
       std::vector<const float*> Wp(K);
       std::vector<int64_t> ldw(K), ldda(K, Cin);
@@ -905,20 +831,16 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
         proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
       if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
         const hlhgat_hodge_factor_t hf = make_factor(fac, sv.fac_nodes, N);
-        Tensor work = keep_alive(
-            at::empty({hlhgat_hodge_factor_work_floats(sv.fac_nodes, F)}, x2.options()));
+        Tensor work = at::empty({hlhgat_hodge_factor_work_floats(sv.fac_nodes, F)}, x2.options());
         chk(hlhgat_poly_basis_bwd_factored((int)kind, &hf, F, (int)K, Gs.data_ptr<float>(),
                                            work.data_ptr<float>(), s),
             "poly_basis_bwd_factored");
       } else if (K > 1) {
-        const bool loc = tiles.defined() && graph_local_env();
         chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
                                   nnz ? t_col.data_ptr<int>() : nullptr,
                                   (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr, N,
                                   nnz, t_order.defined() ? t_order.data_ptr<int>() : nullptr,
-                                  use_halo ? &halo : nullptr, loc ? tiles.data_ptr<int>() : nullptr,
-                                  loc ? tiles.numel() - 1 : 0, sv.tile_rows, sv.tile_nnz, F,
-                                  (int)K, Gs.data_ptr<float>(), s),
+                                  use_halo ? &halo : nullptr, F, (int)K, Gs.data_ptr<float>(), s),
             "poly_basis_bwd");
       }
     } else {
@@ -966,9 +888,6 @@ void edge_map_conv(EdgeMap& em, const ConvArgs& c) {
   em.opt(c.out_buf);
   em.opt(c.a_order);
   em.opt(c.t_order);
-  em.opt(c.tiles);
-  em.other();
-  em.other();
   em.opt(c.valid);
   em.opt(c.h_tile);
   em.opt(c.h_ptr);
@@ -981,7 +900,7 @@ void edge_map_conv(EdgeMap& em, const ConvArgs& c) {
   em.list(c.fac);
   em.other();
 }
-constexpr int64_t conv_positions(int64_t K, int64_t n_fac) { return 33 + K + n_fac + 1; }
+constexpr int64_t conv_positions(int64_t K, int64_t n_fac) { return 30 + K + n_fac + 1; }
 
 void put_grads(variable_list& out, int64_t base, int64_t K, const ConvGrads& g) {
   out[base] = g.dx;
@@ -998,17 +917,16 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         OptT a_val, Tensor t_rowptr, Tensor t_col, OptT t_val, int64_t nnz,
                         int64_t kind, at::TensorList W, OptT bias, OptT bn_w, OptT bn_b,
                         OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-                        int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order,
-                        OptT tiles, int64_t tile_rows, int64_t tile_nnz, OptT valid,
+                        int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT valid,
                         OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol,
                         OptT h_sval, std::vector<int64_t> h_bounds, OptT h_hdr,
                         at::TensorList fac, int64_t fac_nodes) {
     ConvArgs c{x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind, W.vec(), bias,
                bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode, out_buf, a_order,
-               t_order, tiles, tile_rows, tile_nnz, valid, h_tile, h_ptr, h_cols, h_srp,
-               h_lcol, h_sval, h_bounds, h_hdr, fac.vec(), fac_nodes};
+               t_order, valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds, h_hdr,
+               fac.vec(), fac_nodes};
     ConvSaved sv;
-    Tensor y = conv_forward(c, sv, 0);
+    Tensor y = conv_forward(c, sv);
     EdgeMap em;
     edge_map_conv(em, c);
     ctx->saved_data["edges"] = em.e;
@@ -1022,168 +940,7 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
     const int64_t K = sv.dims[5];
     const int64_t n_fac = (int64_t)sv.t.size() - (int64_t)kSavedFixed - K;
     variable_list out(conv_positions(K, n_fac));
-    put_grads(out, 0, K, conv_backward(sv, grads[0], conv_needs(ctx, K, 0), 0));
-    return out;
-  }
-};
-
-// ---------------------------------------------------------------------------
-// The node (L0) and edge (L1) conv (+ BN (+ ReLU)) of one HL block as ONE
-// autograd node whose launches run as pairs (hlhgat_group_*): the i-th launch
-// of the node side and of the edge side -- polynomial step, projection,
-// BatchNorm, Linear backward, split reduction -- share one grid, instead of
-// two concurrent streams of half-size launches (lib/Hodge_ST_Model.py:556-566).
-// Each side's arithmetic is that of conv_bn: bitwise the same results.
-// ---------------------------------------------------------------------------
-ConvArgs conv_args_from(const Tensor& x, at::TensorList W, const OptT& bias, const OptT& bn_w,
-                        const OptT& bn_b, const std::vector<OptT>& aux,
-                        const std::vector<int64_t>& ints, const std::vector<double>& dbl,
-                        const std::vector<int64_t>& h_bounds, at::TensorList fac) {
-  // aux: a_rowptr a_col a_val t_rowptr t_col t_val bn_rm bn_rv bn_nbt out_buf a_order
-  //      t_order tiles valid h_tile h_ptr h_cols h_srp h_lcol h_sval h_hdr
-  // ints: nnz kind bn_mode tile_rows tile_nnz fac_nodes ; dbl: momentum eps
-  TORCH_CHECK(aux.size() == 21 && ints.size() == 6 && dbl.size() == 2,
-              "hlhgat: conv_bn_pair: bad side descriptor");
-  ConvArgs c;
-  c.x = x;
-  c.a_rowptr = *aux[0];
-  c.a_col = *aux[1];
-  c.a_val = aux[2];
-  c.t_rowptr = *aux[3];
-  c.t_col = *aux[4];
-  c.t_val = aux[5];
-  c.bn_rm = aux[6];
-  c.bn_rv = aux[7];
-  c.bn_nbt = aux[8];
-  c.out_buf = aux[9];
-  c.a_order = aux[10];
-  c.t_order = aux[11];
-  c.tiles = aux[12];
-  c.valid = aux[13];
-  c.h_tile = aux[14];
-  c.h_ptr = aux[15];
-  c.h_cols = aux[16];
-  c.h_srp = aux[17];
-  c.h_lcol = aux[18];
-  c.h_sval = aux[19];
-  c.h_hdr = aux[20];
-  c.nnz = ints[0];
-  c.kind = ints[1];
-  c.bn_mode = ints[2];
-  c.tile_rows = ints[3];
-  c.tile_nnz = ints[4];
-  c.fac_nodes = ints[5];
-  c.momentum = dbl[0];
-  c.eps = dbl[1];
-  c.W = W.vec();
-  c.bias = bias;
-  c.bn_w = bn_w;
-  c.bn_b = bn_b;
-  c.h_bounds = h_bounds;
-  c.fac = fac.vec();
-  return c;
-}
-
-// Positions: side s's x, W (a list), bias, bn_w, bn_b at s*5 + 0..4; the rest
-// carries no gradient.
-class ConvBNPairFn : public torch::autograd::Function<ConvBNPairFn> {
- public:
-  static variable_list forward(AutogradContext* ctx, Tensor x0, at::TensorList W0, OptT bias0,
-                               OptT bnw0, OptT bnb0, Tensor x1, at::TensorList W1, OptT bias1,
-                               OptT bnw1, OptT bnb1, std::vector<OptT> aux0,
-                               std::vector<OptT> aux1, std::vector<int64_t> ints0,
-                               std::vector<int64_t> ints1, std::vector<double> dbl0,
-                               std::vector<double> dbl1, std::vector<int64_t> hb0,
-                               std::vector<int64_t> hb1, at::TensorList fac0,
-                               at::TensorList fac1) {
-    TORCH_CHECK(x0.device() == x1.device(), "hlhgat: conv_bn_pair: sides on different devices");
-    ConvArgs c0 = conv_args_from(x0, W0, bias0, bnw0, bnb0, aux0, ints0, dbl0, hb0, fac0);
-    ConvArgs c1 = conv_args_from(x1, W1, bias1, bnw1, bnb1, aux1, ints1, dbl1, hb1, fac1);
-    ConvSaved s0, s1;
-    Tensor y0, y1;
-    {
-      LaunchGroup g;
-      g.begin();
-      y0 = conv_forward(c0, s0, 0);
-      g.next();
-      y1 = conv_forward(c1, s1, 1);
-      ctx->saved_data["paired_fwd"] = (int64_t)g.end(stream_of(x0));
-    }
-    // needs_input_grad indexes: x0, W0..., [bias0], [bnw0], [bnb0], x1, W1..., ...
-    std::vector<int64_t> e;
-    int64_t n = 0;
-    auto side = [&](const ConvArgs& c) {
-      e.push_back(n++);
-      e.push_back(n);
-      n += (int64_t)c.W.size();
-      e.push_back(has(c.bias) ? n++ : -1);
-      e.push_back(has(c.bn_w) ? n++ : -1);
-      e.push_back(has(c.bn_b) ? n++ : -1);
-    };
-    side(c0);
-    side(c1);
-    ctx->saved_data["pair_edges"] = e;
-    s0.to_ctx(ctx, "0");
-    s1.to_ctx(ctx, "1");
-    std::vector<Tensor> all = s0.t;
-    all.insert(all.end(), s1.t.begin(), s1.t.end());
-    ctx->save_for_backward(all);
-    return {y0, y1};
-  }
-
-  static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    const auto all = ctx->get_saved_variables();
-    ConvSaved s0 = ConvSaved::from_ctx(ctx, "0", all, 0);
-    ConvSaved s1 = ConvSaved::from_ctx(ctx, "1", all, s0.t.size());
-    const auto e = ctx->saved_data["pair_edges"].toIntVector();
-    auto needs = [&](int side, int64_t K) {
-      const int64_t* q = e.data() + 5 * side;
-      auto nig = [&](int64_t idx) { return idx >= 0 && ctx->needs_input_grad(idx); };
-      ConvNeeds nd;
-      nd.x = nig(q[0]);
-      nd.w.resize(K);
-      for (int64_t k = 0; k < K; ++k) nd.w[k] = nig(q[1] + k);
-      nd.bias = nig(q[2]);
-      nd.bn_w = nig(q[3]);
-      nd.bn_b = nig(q[4]);
-      return nd;
-    };
-    const int64_t K0 = s0.dims[5], K1 = s1.dims[5];
-    ConvGrads g0, g1;
-    Tensor gy0 = grads[0], gy1 = grads[1];
-    if (!grads[0].defined()) {
-      std::vector<int64_t> os = s0.xshape;
-      os.back() = s0.dims[4];
-      gy0 = at::zeros(os, s0.t[0].options());
-    }
-    if (!grads[1].defined()) {
-      std::vector<int64_t> os = s1.xshape;
-      os.back() = s1.dims[4];
-      gy1 = at::zeros(os, s1.t[0].options());
-    }
-    {
-      LaunchGroup g;
-      g.begin();
-      g0 = conv_backward(s0, gy0, needs(0, K0), 0);
-      g.next();
-      g1 = conv_backward(s1, gy1, needs(1, K1), 1);
-      g.end(stream_of(s0.t[0]));
-    }
-    // one gradient slot per forward argument, TensorList elements one each:
-    // x0 W0.. bias0 bnw0 bnb0 x1 W1.. bias1 bnw1 bnb1, 8 descriptor
-    // arguments, the factor tensors of both sides
-    variable_list out;
-    auto push_side = [&](const ConvGrads& g, int64_t K) {
-      out.push_back(g.dx);
-      for (int64_t k = 0; k < K; ++k) out.push_back(g.dW[k]);
-      out.push_back(g.dbias);
-      out.push_back(g.dbn_w);
-      out.push_back(g.dbn_b);
-    };
-    push_side(g0, K0);
-    push_side(g1, K1);
-    const size_t n_fac = (s0.t.size() - kSavedFixed - K0) + (s1.t.size() - kSavedFixed - K1);
-    out.resize(out.size() + 8 + n_fac);
+    put_grads(out, 0, K, conv_backward(sv, grads[0], conv_needs(ctx, K, 0)));
     return out;
   }
 };
@@ -1885,11 +1642,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     const bool nW = need(ctx, PN) || need(ctx, PE), nB = need(ctx, PN + 1) || need(ctx, PE + 1);
     // TrainStep: every unpack destination deferrable -> the Wt / Ws split
     // reductions are deferred too (their only reader is the deferred unpack)
-    static const bool nei_defer_env = [] {  // HLHGAT_DEFER_NEI=0: A/B
-      const char* e = getenv("HLHGAT_DEFER_NEI");
-      return !(e && e[0] == '0');
-    }();
-    const bool fdef = nei_defer_env && need(ctx, PN) && need(ctx, PE) && need(ctx, PN + 1) &&
+    const bool fdef = need(ctx, PN) && need(ctx, PE) && need(ctx, PN + 1) &&
                       need(ctx, PE + 1) && param_deferrable(sv[30]) && param_deferrable(sv[35]) &&
                       param_deferrable(sv[31]) && param_deferrable(sv[36]);
     Tensor dWt, dbt, dWs, dbs;
@@ -1958,30 +1711,14 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
 Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_rowptr, Tensor t_col,
                OptT t_val, int64_t nnz, int64_t kind, std::vector<Tensor> W, OptT bias, OptT bn_w,
                OptT bn_b, OptT bn_rm, OptT bn_rv, OptT bn_nbt, double momentum, double eps,
-               int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT tiles,
-               int64_t tile_rows, int64_t tile_nnz, OptT valid, OptT h_tile, OptT h_ptr,
-               OptT h_cols, OptT h_srp, OptT h_lcol, OptT h_sval,
+               int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT valid,
+               OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol, OptT h_sval,
                std::vector<int64_t> h_bounds, OptT h_hdr, std::vector<Tensor> fac,
                int64_t fac_nodes) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
-                         bn_mode, out_buf, a_order, t_order, tiles, tile_rows, tile_nnz,
-                         valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds,
+                         bn_mode, out_buf, a_order, t_order, valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds,
                          h_hdr, at::TensorList(fac), fac_nodes);
-}
-
-std::vector<Tensor> conv_bn_pair(Tensor x0, std::vector<Tensor> W0, OptT bias0, OptT bnw0,
-                                 OptT bnb0, Tensor x1, std::vector<Tensor> W1, OptT bias1,
-                                 OptT bnw1, OptT bnb1, std::vector<OptT> aux0,
-                                 std::vector<OptT> aux1, std::vector<int64_t> ints0,
-                                 std::vector<int64_t> ints1, std::vector<double> dbl0,
-                                 std::vector<double> dbl1, std::vector<int64_t> hb0,
-                                 std::vector<int64_t> hb1, std::vector<Tensor> fac0,
-                                 std::vector<Tensor> fac1) {
-  auto r = ConvBNPairFn::apply(x0, at::TensorList(W0), bias0, bnw0, bnb0, x1, at::TensorList(W1),
-                               bias1, bnw1, bnb1, aux0, aux1, ints0, ints1, dbl0, dbl1, hb0, hb1,
-                               at::TensorList(fac0), at::TensorList(fac1));
-  return {r[0], r[1]};
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,
@@ -2100,7 +1837,7 @@ Tensor poly_basis_hip(const Tensor& rowptr, const Tensor& col, const OptT& val, 
   if (K > 1 && n > 0 && F > 0)
     chk(hlhgat_poly_basis_fwd((int)kind, rowptr.data_ptr<int>(),
                               nnz ? col.data_ptr<int>() : nullptr, nnz ? fptr(val) : nullptr, n,
-                              nnz, nullptr, nullptr, nullptr, 0, 0, 0, xc.data_ptr<float>(),
+                              nnz, nullptr, nullptr, xc.data_ptr<float>(),
                               ld_of(xc), F, (int)K, T.data_ptr<float>(), stream_of(xc)),
         "poly_basis_fwd");
   return T;
@@ -2125,7 +1862,7 @@ Tensor poly_basis_backward_hip(const Tensor& grad, const Tensor& rowptr, const T
   if (K > 1 && n > 0 && F > 0)
     chk(hlhgat_poly_basis_bwd((int)kind, rowptr.data_ptr<int>(),
                               nnz ? col.data_ptr<int>() : nullptr, nnz ? fptr(val) : nullptr, n,
-                              nnz, nullptr, nullptr, nullptr, 0, 0, 0, F, (int)K,
+                              nnz, nullptr, nullptr, F, (int)K,
                               Gs.data_ptr<float>(), stream_of(grad)),
         "poly_basis_bwd");
   return Gs[0].clone();
@@ -2248,10 +1985,10 @@ Tensor segment_mean_backward_hip(const Tensor& grad, const Tensor& seg_ptr, cons
   const int64_t n_seg = seg_ptr.numel() - 1;
   Tensor gx = has(seg_rows) ? at::zeros({n_rows, g.size(1)}, g.options())
                             : at::empty({n_rows, g.size(1)}, g.options());
-  if (n_seg > 0)
+  if (n_rows > 0)
     chk(hlhgat_segment_mean_bwd(seg_ptr.data_ptr<int>(), iptr(seg_rows), n_seg,
                                 g.data_ptr<float>(), ld_of(g), g.size(1), gx.data_ptr<float>(),
-                                ld_of(gx), stream_of(g)),
+                                ld_of(gx), n_rows, stream_of(g)),
         "segment_mean_bwd");
   return gx;
 }
@@ -2460,7 +2197,6 @@ Tensor segment_mean_ad(const Tensor& x, const Tensor& seg_ptr, const OptT& seg_r
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
-  m.def("conv_bn_pair", &conv_bn_pair);
   m.def("set_fused_bwd", &set_fused_bwd);
   m.def("join_capture_streams", &join_capture_streams);
   m.def("stream_capturing", &stream_capturing);

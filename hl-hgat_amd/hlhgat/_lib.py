@@ -46,10 +46,9 @@ SIGNATURES = {
                                  c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32,
                                  c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                      c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32,
-                                      c_vp, c_vp]),
+                                      c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
-                                      c_vp, c_i64, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp]),
+                                      c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_hodge_factor_work_floats": (c_i64, [c_i64, c_i64]),
     "hlhgat_hodge_spmm": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "hlhgat_hodge_poly_step": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp,
@@ -94,7 +93,7 @@ SIGNATURES = {
     "hlhgat_segment_mean_fwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                         c_vp]),
     "hlhgat_segment_mean_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                        c_vp]),
+                                        c_i64, c_vp]),
     "hlhgat_bn_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "hlhgat_bn_fwd_train": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                     c_vp, c_f32, c_f32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
@@ -106,10 +105,6 @@ SIGNATURES = {
                                  c_f64, c_f64, c_vp]),
     "hlhgat_l1_loss_fwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlhgat_l1_loss_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
-    "hlhgat_group_begin": (c_i32, []),
-    "hlhgat_group_next": (c_i32, []),
-    "hlhgat_group_end": (c_i32, [c_vp, c_vp]),
-    "hlhgat_group_abort": (c_i32, []),
     "hlhgat_bn_sums_len": (c_i64, [c_i64]),
     "hlhgat_bn_sums_fwd": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
                                    c_i64, c_vp]),

@@ -77,18 +77,6 @@ class _HodgePolyConv(nn.Module):
         return ops.hodge_poly_conv(x, op, [lin.weight for lin in self.lins], self.bias,
                                    self._kind, bn=bn, relu=relu, out=out)
 
-    def pair_spec(self, x: Tensor, edge_index: Tensor, edge_weight: Optional[Tensor],
-                  bn: nn.BatchNorm1d, relu: bool):
-        """forward_bn's arguments as one side of ops.hodge_poly_conv_pair (the
-        node / edge convs of an HL block in one node), or None when this call
-        must take forward_bn itself."""
-        op = ops.hodge_operator(edge_index, edge_weight, x.size(0))
-        spec = ops.conv_pair_spec(x, op, [lin.weight for lin in self.lins], self.bias,
-                                  self._kind, bn, relu, getattr(self, "_hlhgat_out", None))
-        if spec is not None:
-            self._hlhgat_out = None  # the sink is consumed by the pair
-        return spec
-
     def __repr__(self) -> str:
         return (f"{self.__class__.__name__}({self.in_channels}, "
                 f"{self.out_channels}, K={len(self.lins)})")

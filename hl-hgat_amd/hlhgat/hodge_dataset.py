@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "graph_tiles", "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
+           "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
            "hodge_factor_ok", "hodge_coo_from_boundary"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
@@ -91,21 +91,17 @@ class Batch(PairData):
 
     def _mark(self) -> None:
         from . import ops
-        from .ops import mark_hodge, set_halo, set_row_order, set_tiles, set_valid
+        from .ops import mark_hodge, set_halo, set_row_order, set_valid
         for k, ok in (getattr(self, "hodge_sorted", None) or {}).items():
             t = getattr(self, k, None)
             if ok and torch.is_tensor(t) and t.is_cuda:
                 mark_hodge(t)
-        for k, ko, kt, kv in (("edge_index_s", "row_order_s", "tile_ptr_s", "n_valid_s"),
-                              ("edge_index_t", "row_order_t", "tile_ptr_t", "n_valid_t")):
-            t, o, tp = getattr(self, k, None), getattr(self, ko, None), getattr(self, kt, None)
+        for k, ko, kv in (("edge_index_s", "row_order_s", "n_valid_s"),
+                          ("edge_index_t", "row_order_t", "n_valid_t")):
+            t, o = getattr(self, k, None), getattr(self, ko, None)
             nv = getattr(self, kv, None)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(o):
                 set_row_order(t, o)
-            if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(tp):
-                # whole-graph tiles: the fused graph-local conv forward uses them
-                # (and the basis-only local path when HLHGAT_GRAPH_LOCAL=1)
-                set_tiles(t, tp, TILE_ROWS, TILE_NNZ)
             if torch.is_tensor(t) and t.is_cuda and torch.is_tensor(nv):
                 set_valid(t, nv)
             side = k[-1]
@@ -146,34 +142,6 @@ class Batch(PairData):
     def batch_s(self) -> torch.Tensor:
         return torch.repeat_interleave(torch.arange(self.num_graphs, device=self.x_s.device),
                                        self.num_edge1.to(self.x_s.device))
-
-
-TILE_ROWS = 64   # row bound of a graph tile (ZINC molecules have <= 38 atoms / 45 bonds)
-TILE_NNZ = 512   # CSR-entry bound of a graph tile (LDS: 2 x 64 x 68 floats + entries = 39 KB)
-
-
-def graph_tiles(counts, nnz, max_rows: int = TILE_ROWS,
-                max_nnz: int = TILE_NNZ) -> Optional[torch.Tensor]:
-    """Row tiles of a block-diagonal batch: consecutive WHOLE graphs packed
-    greedily into runs of <= max_rows rows and <= max_nnz Laplacian entries
-    (int32 [n_tiles+1] row offsets), or None if one graph alone exceeds a
-    bound.  Every Laplacian entry of a tile's rows stays inside the tile
-    (PairData batching offsets, lib/Hodge_Dataset.py:40-48), which is what the
-    graph-local basis kernels rely on."""
-    c = np.asarray(counts, dtype=np.int64).reshape(-1)
-    z = np.asarray(nnz, dtype=np.int64).reshape(-1)
-    if c.size == 0 or c.max() > max_rows or z.max() > max_nnz:
-        return None
-    ptr = [0]
-    acc = accz = 0
-    for k, kz in zip(c, z):
-        if (acc + k > max_rows or accz + kz > max_nnz) and acc > 0:
-            ptr.append(ptr[-1] + acc)
-            acc = accz = 0
-        acc += int(k)
-        accz += int(kz)
-    ptr.append(ptr[-1] + acc)
-    return torch.tensor(ptr, dtype=torch.int32)
 
 
 def locality_order(edge_index, n: int) -> torch.Tensor:
@@ -397,15 +365,6 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     b.l1_factor = bool(hs.get("edge_index_s")) and _factor_wanted(graphs)
     for side in ("s", "t"):
         _collate_halo(b, graphs, side)
-    # whole-graph row tiles for the graph-local polynomial basis
-    for key, xk, ek in (("tile_ptr_t", "x_t", "edge_index_t"), ("tile_ptr_s", "x_s", "edge_index_s")):
-        if getattr(first, ek, None) is None:
-            continue
-        counts = [getattr(g, xk).size(0) for g in graphs]
-        nnz = [np.asarray(getattr(g, ek)).shape[1] for g in graphs]
-        tp = graph_tiles(counts, nnz)
-        if tp is not None:
-            setattr(b, key, tp)
     # Laplacian CSR (rowptr / int32 columns) for the sorted symmetric blocks
     _attach_csr(b)
     # incidence CSR of |B1| (adj2par1) for the NodeEdgeInt gathers, built
@@ -499,18 +458,14 @@ def _roundup(v: int, q: int) -> int:
 
 def static_caps(b: "Batch", quantum: int = 512) -> Dict[str, int]:
     """Capacity bucket of a collated batch for hipGraph replay: node / edge
-    rows rounded up to `quantum` (at least one padding row), Laplacian entries
-    to 4*quantum, tile counts to a bound that holds for any batch of these
-    capacities.  Batches with equal caps share one captured training step."""
+    rows rounded up to `quantum` (at least PAD_MIN_ROWS padding rows),
+    Laplacian entries to 4*quantum.  Batches with equal caps share one
+    captured training step."""
     rows_t = _roundup(b.x_t.size(0) + PAD_MIN_ROWS, quantum)
     rows_s = _roundup(b.x_s.size(0) + PAD_MIN_ROWS, quantum)
     caps = {"rows_t": rows_t, "rows_s": rows_s,
             "nnz_t": _roundup(b.edge_index_t.size(1) + 1, 4 * quantum),
             "nnz_s": _roundup(b.edge_index_s.size(1) + 1, 4 * quantum)}
-    for side in ("t", "s"):
-        r, z = caps["rows_" + side], caps["nnz_" + side]
-        # greedy packing: two consecutive tiles always exceed a bound
-        caps["tiles_" + side] = 2 * max(-(-r // TILE_ROWS), -(-z // TILE_NNZ)) + 4
     return caps
 
 
@@ -526,8 +481,7 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
         their entries; no padding row is long);
       * the B1 edge list gets self-edges spread over the padding nodes;
       * n_valid_t / n_valid_s (int32 [1]) and valid_mask_t tell the BatchNorm
-        kernels and the degree normalisation which rows are real;
-      * graph tiles cover the padding rows and are padded with empty tiles.
+        kernels and the degree normalisation which rows are real.
     The real rows' values, gradients and statistics are those of the
     unpadded batch (tests/test_train_step.py)."""
     nt, ns = b.x_t.size(0), b.x_s.size(0)
@@ -552,9 +506,9 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
                 torch.cat([w, w.new_zeros(extra)]), per_row)
 
     out.x_t, out.x_s = pad_rows(b.x_t, Rt), pad_rows(b.x_s, Rs)
-    out.edge_index_t, out.edge_weight_t, pr_t = pad_coo(b.edge_index_t, b.edge_weight_t, nt, Rt,
+    out.edge_index_t, out.edge_weight_t, _ = pad_coo(b.edge_index_t, b.edge_weight_t, nt, Rt,
                                                         caps["nnz_t"])
-    out.edge_index_s, out.edge_weight_s, pr_s = pad_coo(b.edge_index_s, b.edge_weight_s, ns, Rs,
+    out.edge_index_s, out.edge_weight_s, _ = pad_coo(b.edge_index_s, b.edge_weight_s, ns, Rs,
                                                         caps["nnz_s"])
     if getattr(b, "csr_rowptr_t", None) is not None or getattr(b, "csr_rowptr_s", None) is not None:
         _attach_csr(out)  # the padded COO (zero-weight self-loops on padding rows)
@@ -565,22 +519,10 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
             out.inc_rowptr, out.inc_eids = incidence_csr(out.edge_index, Rt)
             # padding nodes: unit degree (the model's masked_fill, no 1/0)
             out.deg_t, out.inv_deg_t = node_degree(out.inc_rowptr, valid=nt)
-    for side, n, R, per_row in (("t", nt, Rt, pr_t), ("s", ns, Rs, pr_s)):
+    for side, n, R in (("t", nt, Rt), ("s", ns, Rs)):
         o = getattr(b, "row_order_" + side, None)
         if o is not None:
             setattr(out, "row_order_" + side, torch.cat([o, torch.arange(n, R, dtype=o.dtype)]))
-        tp = getattr(b, "tile_ptr_" + side, None)
-        if tp is not None:
-            # padding rows are isolated: pack them under the same row / entry bounds
-            pads = graph_tiles(np.ones(R - n, dtype=np.int64), per_row)
-            if pads is None:
-                raise ValueError("pad_batch: a padding row exceeds the tile entry bound")
-            tp = torch.cat([tp, pads[1:] + n])
-            cap = caps["tiles_" + side]
-            if tp.numel() - 1 > cap:
-                raise ValueError(f"pad_batch: {tp.numel() - 1} tiles exceed the cap {cap}")
-            tp = torch.cat([tp, tp[-1:].expand(cap + 1 - tp.numel())])
-            setattr(out, "tile_ptr_" + side, tp.contiguous())
         setattr(out, "n_valid_" + side, torch.tensor([n], dtype=torch.int32))
     out.valid_mask_t = torch.arange(Rt) < nt
     out.num_nodes = Rt

@@ -157,7 +157,6 @@ class Sequential(tnn.Module):
                 self._fuse[i] = ("bn_relu", 2)
             i += self._fuse[i][1] if self._fuse[i] else 1
         self._split = self._two_chains()
-        self._pair = self._pair_entries()
 
     def _two_chains(self):
         """Index s such that entries [0, s) and [s, n-1) touch disjoint
@@ -175,55 +174,6 @@ class Sequential(tnn.Module):
                 if last_in & a and last_in & b:
                     return s
         return None
-
-    def _pair_entries(self):
-        """(i0, i1) when each of the two chains is ONE fused conv -> BN (->
-        ReLU) entry followed only by Dropouts on the same variable (every HL
-        block, lib/Hodge_ST_Model.py:556-566): both convs can then run as one
-        paired node (ops.hodge_poly_conv_pair)."""
-        s = self._split
-        if s is None:
-            return None
-        picks = []
-        for lo, hi in ((0, s), (s, self._n - 1)):
-            f = self._fuse[lo]
-            if not (f and f[0].startswith("conv_bn")):
-                return None
-            if not all(isinstance(getattr(self, f"module_{j}"), tnn.Dropout)
-                       for j in range(lo + f[1], hi)):
-                return None
-            picks.append(lo)
-        return tuple(picks)
-
-    def _run_pair(self, env) -> bool:
-        """Both chains as one paired conv node; False (nothing run) when either
-        side cannot take that path at run time."""
-        specs = []
-        for i in self._pair:
-            fn = getattr(self, f"module_{i}")
-            ins, outs = self._routes[i]
-            lo, hi = (0, self._split) if i == self._pair[0] else (self._split, self._n - 1)
-            if not hasattr(fn, "pair_spec") or not all(
-                    getattr(self, f"module_{j}").p == 0.0 or not self.training
-                    for j in range(i + self._fuse[i][1], hi)):
-                return False
-            bn = getattr(self, f"module_{i + 1}").module
-            specs.append((fn, [env[n] for n in ins], bn, self._fuse[i][0] == "conv_bn_relu"))
-        got = []
-        for fn, args, bn, relu in specs:
-            sp = fn.pair_spec(*args, bn=bn, relu=relu)
-            got.append(sp)
-        if any(sp is None for sp in got):
-            # a side that cannot pair: its sink (if consumed) is restored below
-            for (fn, _, _, _), sp, i in zip(specs, got, self._pair):
-                if sp is not None and sp[5][9] is not None:
-                    fn._hlhgat_out = sp[5][9]
-            return False
-        from .ops import hodge_poly_conv_pair
-        ys = hodge_poly_conv_pair(got[0], got[1])
-        for i, y in zip(self._pair, ys):
-            env[self._routes[i][1][0]] = y
-        return True
 
     def _run(self, env, lo, hi):
         out = None
@@ -263,8 +213,6 @@ class Sequential(tnn.Module):
         dev = next((a.device for a in args if torch.is_tensor(a)), None)
         if s is None or dev is None:
             return self._run(env, 0, self._n)
-        if self._pair is not None and self._run_pair(env):
-            return self._run(env, self._n - 1, self._n)
         # node chain on the current stream, edge chain on the side stream
         from .ops import fork
         side_env = dict(env)

@@ -164,9 +164,6 @@ class SparseCSR:
     n_cols: int
     nnz: int
     order: Optional[torch.Tensor] = None  # int32 [n_rows] row schedule (locality_order)
-    tiles: Optional[torch.Tensor] = None  # int32 [n_tiles+1] whole-graph row tiles (graph_tiles)
-    tile_rows: int = 0                    # bound on the rows of any tile
-    tile_nnz: int = 0                     # bound on the CSR entries of any tile
     valid: Optional[torch.Tensor] = None  # int32 [1]: rows >= valid are static-shape padding
     # halo tiles (tile_ptr, halo_ptr, halo, lcol, max_halo) for the LDS-staged
     # SpMM of large Laplacians (hodge_dataset.halo_tiles; hlhgat_halo_t)
@@ -271,25 +268,6 @@ def set_row_order(edge_index: torch.Tensor, order: torch.Tensor) -> torch.Tensor
     return edge_index
 
 
-# Graph-local bases for collated batches (Batch._mark attaches the whole-graph
-# tiles).  Off by default: at the ZINC shape one graph-local launch costs what
-# its K-1 step launches cost (tools/kbench.py "basis" cases, profiles/), so the
-# simpler step path runs; HLHGAT_GRAPH_LOCAL=1 turns it on.
-GRAPH_LOCAL = os.environ.get("HLHGAT_GRAPH_LOCAL", "0") == "1"
-
-
-def set_tiles(edge_index: torch.Tensor, tile_ptr: torch.Tensor, tile_rows: int,
-              tile_nnz: int) -> torch.Tensor:
-    """Declare that the operator built from edge_index is block-diagonal over
-    the row tiles tile_ptr (runs of whole graphs, each <= tile_rows rows and
-    <= tile_nnz CSR entries, hodge_dataset.graph_tiles): its polynomial bases
-    then run graph-local, one launch per basis."""
-    edge_index._hlhgat_tiles = (tile_ptr.to(device=edge_index.device,  # type: ignore
-                                            dtype=torch.int32).contiguous(), int(tile_rows),
-                                int(tile_nnz))
-    return edge_index
-
-
 def set_valid(edge_index: torch.Tensor, n_valid: torch.Tensor, attr: str = "_hlhgat_valid"
               ) -> torch.Tensor:
     """Declare the rows >= n_valid (device int32 [1]) of the operator built
@@ -312,8 +290,6 @@ def set_halo(edge_index: torch.Tensor, ht: dict) -> torch.Tensor:
         [int(v) for v in ht["halo_bounds"]], i32("halo_hdr"))
     return edge_index
 
-
-_HALO_ENABLED = os.environ.get("HLHGAT_HALO", "1") != "0"
 
 # Factored L1 (hlhgat_hodge_factor_t): on for the operators collate declares
 # (hodge_dataset.hodge_factor_ok: exact identity, >= FACTOR_MIN_ROW entries per
@@ -370,7 +346,7 @@ def _attach_halo(a: "SparseCSR", halo) -> None:
 
 def _halo_desc(A: "SparseCSR"):
     """ctypes pointer to an hlhgat_halo_t for A, or None."""
-    if A.halo is None or not _HALO_ENABLED:
+    if A.halo is None:
         return None
     tp, hp, hc, srp, lc, sval, (mh, mr, mn), hdr = A.halo
     d = _lib.HaloDesc(hdr.data_ptr(), tp.data_ptr(), hp.data_ptr(), hc.data_ptr(), srp.data_ptr(),
@@ -380,7 +356,7 @@ def _halo_desc(A: "SparseCSR"):
 
 def _halo_args(A: "SparseCSR"):
     """The halo arguments of the C++ conv node (Nones when A has none)."""
-    if A.halo is None or not _HALO_ENABLED:
+    if A.halo is None:
         return (None, None, None, None, None, None, [0, 0, 0], None)
     return A.halo
 
@@ -556,7 +532,6 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
     order = getattr(edge_index, "_hlhgat_row_order", None)
     if order is not None and order.numel() != n:
         raise RuntimeError(f"hlhgat: row schedule has {order.numel()} entries, operator {n} rows")
-    tiles, tile_rows, tile_nnz = getattr(edge_index, "_hlhgat_tiles", (None, 0, 0))
     valid = getattr(edge_index, "_hlhgat_valid", None)
     if getattr(edge_index, "_hlhgat_sorted_symmetric", False):
         pre = getattr(edge_index, "_hlhgat_csr", None)  # built at collate (set_csr)
@@ -564,7 +539,7 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
             a = SparseCSR(pre[0], pre[1], w, n, n, ei.size(1))
         else:
             a = _csr_sorted(ei[0], ei[1], w, n, n)
-        a.order, a.tiles, a.tile_rows, a.tile_nnz = order, tiles, tile_rows, tile_nnz
+        a.order = order
         a.valid = valid
         halo = getattr(edge_index, "_hlhgat_halo", None)
         if halo is not None:  # built for the COO order = this CSR's entry order
@@ -576,8 +551,8 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
     else:
         fwd = _csr_general(ei[1], ei[0], w, n, n)
         bwd = _csr_general(ei[0], ei[1], w, n, n)
-        for c in (fwd, bwd):  # the transpose of a block-diagonal operator has the same tiles
-            c.order, c.tiles, c.tile_rows, c.tile_nnz = order, tiles, tile_rows, tile_nnz
+        for c in (fwd, bwd):
+            c.order = order
             c.valid = valid
         op = HodgeOperator(fwd, bwd)
     return _HODGE_CACHE.put(keys, n, op)
@@ -677,10 +652,8 @@ def poly_basis(op: HodgeOperator, X: torch.Tensor, K: int, kind: int) -> torch.T
         check(LIB.hlhgat_poly_basis_fwd(kind, A.rowptr.data_ptr(),
                                         A.col.data_ptr() if A.nnz else None,
                                         _ptr(A.val) if A.nnz else None, n, A.nnz,
-                                        _ptr(A.order), _halo_desc(A), _ptr(A.tiles),
-                                        A.tiles.numel() - 1 if A.tiles is not None else 0,
-                                        A.tile_rows, A.tile_nnz, X.data_ptr(), _ld(X), F, K,
-                                        T.data_ptr(),
+                                        _ptr(A.order), _halo_desc(A), X.data_ptr(), _ld(X), F,
+                                        K, T.data_ptr(),
                                         _stream(X)), "poly_basis_fwd")
     return T
 
@@ -761,13 +734,11 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
                             ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order,
-                            A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A),
-                            *_factor_args(op))
+                            A.valid, *_halo_args(A), *_factor_args(op))
     sink = out if (bn is None and not relu and x.dim() == 2) else None
     y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
                      bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order,
-                     A.tiles, A.tile_rows, A.tile_nnz, A.valid, *_halo_args(A),
-                     *_factor_args(op))
+                     A.valid, *_halo_args(A), *_factor_args(op))
     if bn is not None:
         y = batch_norm_act(y, bn, relu, valid=A.valid)
     elif relu:
@@ -775,48 +746,11 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
     return y
 
 
-PAIR_CONV = os.environ.get("HLHGAT_PAIR_CONV", "0") == "1"
-
-
-def conv_pair_spec(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.Tensor],
-                   bias: Optional[torch.Tensor], kind: int, bn: Optional[torch.nn.BatchNorm1d],
-                   relu: bool, out: Optional[torch.Tensor] = None):
-    """One side of hodge_poly_conv_pair (the arguments hodge_poly_conv would
-    hand the fused conv -> BN (-> ReLU) node), or None when that side does not
-    take the fused path (no BN, running statistics, SyncBatchNorm, 3-D x)."""
-    if (not PAIR_CONV or bn is None or not x.is_cuda or x.dim() != 2
-            or not _bn_uses_batch_stats(bn) or sync_bn_group(bn) is not None
-            or x.size(0) != op.fwd.n_rows or x.size(0) < 2):
-        return None
-    A, At = op.fwd, op.bwd
-    w, b, rm, rv, nbt, mom, eps = _bn_args(bn)
-    h = _halo_args(A)
-    fac, fac_nodes = _factor_args(op)
-    aux = [A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, rm, rv, nbt, out, A.order,
-           At.order, A.tiles, A.valid, h[0], h[1], h[2], h[3], h[4], h[5], h[7]]
-    ints = [A.nnz, int(kind), 2 if relu else 1, A.tile_rows, A.tile_nnz, fac_nodes]
-    return (x, list(weights), bias, w, b, aux, ints, [float(mom), float(eps)], list(h[6]), fac)
-
-
-def hodge_poly_conv_pair(s0, s1):
-    """Two independent hodge_poly_conv(..., bn, relu) calls -- the node (L0)
-    and edge (L1) convs of one HL block (lib/Hodge_ST_Model.py:556-566) -- as
-    ONE C++ autograd node whose launches run as pairs (hlhgat_group_*: each
-    polynomial step, projection, BatchNorm and Linear-backward launch covers
-    both sides).  s0, s1 from conv_pair_spec; returns (y0, y1), bitwise the
-    two single calls' results."""
-    x0, W0, b0, bw0, bb0, aux0, i0, d0, hb0, f0 = s0
-    x1, W1, b1, bw1, bb1, aux1, i1, d1, hb1, f1 = s1
-    y0, y1 = _ext.conv_bn_pair(x0, W0, b0, bw0, bb0, x1, W1, b1, bw1, bb1, aux0, aux1, i0, i1,
-                               d0, d1, hb0, hb1, f0, f1)
-    return y0, y1
-
-
 # ----------------------------------------------------------------------------
 # Dense concatenation of the HL blocks in one slab
 # ----------------------------------------------------------------------------
-DENSE_SLAB = os.environ.get("HLHGAT_DENSE_SLAB", "1") != "0"
-GRAD_SINK = os.environ.get("HLHGAT_GRAD_SINK", "1") != "0"
+DENSE_SLAB = True   # tests set False: the torch.cat concatenation
+GRAD_SINK = True
 
 
 class DenseConcat:
@@ -997,8 +931,8 @@ def nei_prepack(neints) -> None:
 
 
 _PACK_EPOCH = 0  # a pack is only used by the forward that built it
-# HLHGAT_PREPACK=0: each NodeEdgeInt packs its own weights (A/B; same results)
-PREPACK = os.environ.get("HLHGAT_PREPACK", "1") != "0"
+# PREPACK = False (tests): each NodeEdgeInt packs its own weights (same results)
+PREPACK = True
 
 
 def take_pack(m) -> Optional[torch.Tensor]:
@@ -1225,7 +1159,7 @@ class _SegmentMeanFn(torch.autograd.Function):
                                                       dtype=g.dtype)
         check(LIB.hlhgat_segment_mean_bwd(seg_ptr.data_ptr(), _ptr(seg_rows) if listed else None,
                                           n_seg, g.data_ptr(), _ld(g), g.size(1), gx.data_ptr(),
-                                          _ld(gx), _stream(g)), "segment_mean_bwd")
+                                          _ld(gx), n_rows, _stream(g)), "segment_mean_bwd")
         return gx, None, None, None
 
 
@@ -1255,7 +1189,7 @@ class _SegmentMeanCatFn(torch.autograd.Function):
         for p, w, n in zip(ctx.saved_tensors, widths, rows):
             t = torch.empty(n, w, device=g.device, dtype=g.dtype)
             check(LIB.hlhgat_segment_mean_bwd(p.data_ptr(), None, n_seg, g.data_ptr() + 4 * c0,
-                                              _ld(g), w, t.data_ptr(), _ld(t), _stream(g)),
+                                              _ld(g), w, t.data_ptr(), _ld(t), n, _stream(g)),
                   "segment_mean_bwd")
             gx.append(t)
             c0 += w

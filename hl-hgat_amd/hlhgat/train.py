@@ -33,12 +33,11 @@ from . import ops
 
 __all__ = ["TrainStep", "batch_key"]
 
-# HLHGAT_HIP_ADAM=0: torch's fused Adam instead of hlhgat_adam_flat (A/B)
-import os as _os  # noqa: E402
-HIP_ADAM = _os.environ.get("HLHGAT_HIP_ADAM", "1") != "0"
-# HLHGAT_DEFER_REDUCE=0: every Linear backward launches its own split
-# reduction instead of handing it to the next one on its stream (A/B)
-DEFER_REDUCE = _os.environ.get("HLHGAT_DEFER_REDUCE", "1") != "0"
+# HIP_ADAM = False: torch's fused Adam instead of hlhgat_adam_flat
+HIP_ADAM = True
+# DEFER_REDUCE = False (tests): every Linear backward launches its own split
+# reduction instead of handing it to the next one on its stream (same bits)
+DEFER_REDUCE = True
 
 
 def _tensor_items(batch):

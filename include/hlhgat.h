@@ -213,18 +213,9 @@ int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
  *        T_{k+1} = (-A X + (2k+1) T_k - k T_{k-1}) / (k+1)
  *        (HL-HGAT-DEMO/lib/Hodge_Cheb_Conv.py:554,561,566; K <= 16)
  * X: [n][F] row stride ldx.  T: (K-1) contiguous blocks of [n][F]. */
-/* tile_ptr (optional, int32[n_tiles+1], with max_tile_rows >= every tile's
- * row count): row ranges of runs of WHOLE graphs of a block-diagonal batch
- * (hodge_dataset.graph_tiles); max_tile_nnz bounds a tile's CSR entries (a
- * larger tile is still correct, its entries are read from global memory).
- * When given and a tile fits in LDS, the whole basis is one graph-local
- * launch (bitwise the same values); otherwise (or NULL) the K-1 steps run as
- * separate launches. */
 int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
                           const float* val, int64_t n, int64_t nnz,
                           const int32_t* row_order, const hlhgat_halo_t* halo,
-                          const int32_t* tile_ptr,
-                          int64_t n_tiles, int64_t max_tile_rows, int64_t max_tile_nnz,
                           const float* X, int64_t ldx, int64_t F, int K, float* T,
                           void* stream);
 
@@ -236,9 +227,7 @@ int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
 int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                           const int32_t* col_t, const float* val_t, int64_t n,
                           int64_t nnz, const int32_t* row_order,
-                          const hlhgat_halo_t* halo,
-                          const int32_t* tile_ptr, int64_t n_tiles,
-                          int64_t max_tile_rows, int64_t max_tile_nnz, int64_t F,
+                          const hlhgat_halo_t* halo, int64_t F,
                           int K, float* G, void* stream);
 
 /* ---- Hodge-factored L1 (large, high-degree edge Laplacians) ------------ */
@@ -392,7 +381,7 @@ int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t lddc,
  *     launch first when this call cannot take the one-launch path).
  * The reduction itself is unchanged, so dW / dbias are bitwise those of
  * hlhgat_proj_bwd; what goes away is one dependent launch per Linear
- * backward on the stream's chain.  Inside a launch group nothing is deferred. */
+ * backward on the stream's chain. */
 typedef struct {
   int64_t words[160];
 } hlhgat_reduce_desc_t;
@@ -440,11 +429,16 @@ int hlhgat_att_score_bwd(int64_t n, int64_t dk, const float* Qc, int64_t ldqc,
 int hlhgat_segment_mean_fwd(const int32_t* seg_ptr, const int32_t* seg_rows,
                             int64_t n_seg, const float* x, int64_t ldx,
                             int64_t d, float* out, int64_t ldo, void* stream);
-/* dx[r] = dout[seg(r)] / |seg| for every row r listed in a segment; rows in
- * no segment are left untouched (caller zero-fills). */
+/* dx[r] = dout[seg(r)] / |seg| for every row r of a segment.  Contiguous
+ * segments (seg_rows NULL): rows [0, seg_ptr[0]) and [seg_ptr[n_seg], n_rows)
+ * of dx get exact zeros (global_mean_pool's adjoint, lib/Hodge_ST_Model.py:636),
+ * so every one of the n_rows rows is written.  Listed members (scatter_mean):
+ * n_rows is ignored and rows in no segment are left untouched (caller
+ * zero-fills). */
 int hlhgat_segment_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
                             int64_t n_seg, const float* dout, int64_t ldo,
-                            int64_t d, float* dx, int64_t ldx, void* stream);
+                            int64_t d, float* dx, int64_t ldx, int64_t n_rows,
+                            void* stream);
 
 /* ---- BatchNorm1d (training) + optional fused ReLU ---------------------- */
 /* gnn.BatchNorm / nn.BatchNorm1d in training mode over x [n][C] (batch
@@ -547,29 +541,6 @@ int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float* y, int64_
                              int64_t C, const float* weight, const float* save_mean,
                              const float* save_invstd, const double* gathered, int world,
                              float* dx, int64_t lddx, void* stream);
-
-/* ---- launch groups (node / edge sides of an HL block in one launch) ----- */
-/* Every HL block runs the same layer on L0 (nodes) and L1 (edges)
- * (lib/Hodge_ST_Model.py:556-566: HodgeLaguerreConv -> BatchNorm -> ReLU per
- * side; lib/Hodge_Cheb_Conv.py:276-289: the WV_Node / WV_Edge MLPs).  Between
- * hlhgat_group_begin() and hlhgat_group_end() the calls of this thread do not
- * launch: the launches of the calls made before hlhgat_group_next() form
- * member 0 (e.g. the node side), those after it member 1 (the edge side).
- * hlhgat_group_end issues them on `stream`: the i-th launch of each member
- * together as ONE launch when both are the same kernel and it has a pair
- * variant (polynomial step, projection forward / backward, split
- * reduction, BatchNorm kernels; a grid-barrier BatchNorm pair only when the
- * joint grid is co-resident), otherwise one after the other; each member's
- * launches keep their order.  Results are bitwise those of the ungrouped
- * calls.  Rules: the two members must be independent; buffers the recorded
- * calls use must stay allocated until hlhgat_group_end; the BatchNorm
- * workspaces of the two members must differ; calls that cannot be deferred
- * fail with HLHGAT_EINVAL inside a group.  *paired (may be NULL) receives the
- * number of pair launches.  hlhgat_group_abort drops a group (error paths). */
-int hlhgat_group_begin(void);
-int hlhgat_group_next(void);
-int hlhgat_group_end(void* stream, int* paired);
-int hlhgat_group_abort(void);
 
 /* ---- optimizer ------------------------------------------------------------ */
 /* torch.optim.Adam (fused, capturable; L2 weight decay added to the gradient)

@@ -203,9 +203,6 @@ def test_pad_batch_structure():
     for side in ("t", "s"):
         ei, w = getattr(p, "edge_index_" + side), getattr(p, "edge_weight_" + side)
         assert is_sorted_symmetric(ei.numpy(), w.numpy())
-        tp = getattr(p, "tile_ptr_" + side)
-        assert tp.numel() == caps["tiles_" + side] + 1
-        assert int(tp[-1]) == caps["rows_" + side] and bool((tp[1:] >= tp[:-1]).all())
         n = getattr(b, "x_" + side).shape[0]
         assert int(getattr(p, "n_valid_" + side)) == n
         assert float(getattr(p, "x_" + side)[n:].abs().sum()) == 0.0

@@ -187,22 +187,15 @@ def main():
         by = 8 * A.nnz + 4 * (n + 1) + 12 * n * 64
         run(f"laguerre_step {name} d=64",
             lambda: ops._poly_step(A, X, Y, Z=Z, alpha=-1.0, beta=3.0, gamma=-1.0, div=2.0), by)
-    # ---- Laguerre basis K=3: graph-local one-launch vs two step launches ---------
-    import hlhgat
+    # ---- Laguerre basis K=3 (two step launches) ----------------------------------
     for side in ("t", "s"):
         ei = getattr(zb, "edge_index_" + side)
         w = getattr(zb, "edge_weight_" + side)
         n = getattr(zb, "x_" + side).shape[0]
         X = rnd(n, 64)
-        for tiled in (False, True):
-            e = ops.mark_hodge(ei.clone())
-            if tiled:
-                ops.set_tiles(e, getattr(zb, "tile_ptr_" + side), hlhgat.hodge_dataset.TILE_ROWS,
-                              hlhgat.hodge_dataset.TILE_NNZ)
-            op = ops.hodge_operator(e, w, n)
-            by = 8 * op.fwd.nnz + 4 * (n + 1) + 4 * n * 64 * 3
-            run(f"basis K=3 L_{side} d=64 {'local' if tiled else 'steps'}",
-                lambda: ops.poly_basis(op, X, 3, ops.POLY_LAGUERRE), by)
+        op = ops.hodge_operator(ops.mark_hodge(ei.clone()), w, n)
+        by = 8 * op.fwd.nnz + 4 * (n + 1) + 4 * n * 64 * 3
+        run(f"basis K=3 L_{side} d=64", lambda: ops.poly_basis(op, X, 3, ops.POLY_LAGUERRE), by)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
