@@ -13,8 +13,11 @@ timing on gloo / CPU with a trivial step (the CPU test of the launcher).
 A step = one training step of HL_HGCNN_zinc_dense_int3_pyr(channels=[2,2,2],
 filters=[64,64,64], mlp=[256,256], K=3, keig=15) on a 1000-graph batch of
 synthetic ZINC-like simplex graphs per GPU (weak scaling): the batch is
-copied into the step's static buffers, CSR / incidence construction for the
-batch, forward, L1 loss, backward, gradient all-reduce (N > 1) and Adam.
+copied into the step's static buffers, then forward, L1 loss, backward,
+gradient all-reduce (N > 1) and Adam.  The batch's CSR / incidence / degree /
+segment tables come with it from the data loader (collate), as the
+reference's DataLoader hands the step a collated batch; the `loader` leg
+times that host work.
 Inputs are resident in HBM before the timed region (8 distinct batches,
 rotated, padded to one capacity bucket).  The step runs as ONE replayed
 hipGraph for every batch of the bucket (hlhgat.train.TrainStep +
@@ -54,14 +57,120 @@ def make_batches(n_batches, rank, device, quantum=512):
     """n_batches distinct synthetic 1000-graph batches, padded to ONE capacity
     bucket (the max of their static_caps) so that a single captured hipGraph
     replays every one of them -- as a training loop pads its DataLoader
-    batches to the dataset's bucket (hodge_dataset.pad_batch)."""
-    from hlhgat.hodge_dataset import pad_batch, static_caps
-    from hlhgat.synthetic import zinc_like_batch
-    raw = [zinc_like_batch(GRAPHS_PER_GPU, seed=1 + rank * 101 + i) for i in range(n_batches)]
-    cs = [static_caps(b, quantum) for b in raw]
+    batches to the dataset's bucket.  The graphs are packed once
+    (hodge_dataset.PackedGraphs, the InMemoryDataset-style storage) and each
+    batch is collated by the native loader (hlhgat_collate: bitwise
+    collate + pad_batch, tests/test_host.py)."""
+    import numpy as np
+    from hlhgat.hodge_dataset import PackedGraphs
+    from hlhgat.synthetic import zinc_like_graph
+    graphs = [zinc_like_graph((1 + rank * 101 + i) * 1_000_003 + j, 15)
+              for i in range(n_batches) for j in range(GRAPHS_PER_GPU)]
+    ds = PackedGraphs(graphs, check_hodge=False)
+    idxs = [np.arange(i * GRAPHS_PER_GPU, (i + 1) * GRAPHS_PER_GPU) for i in range(n_batches)]
+    cs = [ds.caps_for(i, quantum) for i in idxs]
     caps = {k: max(c[k] for c in cs) for k in cs[0]}
-    real = sum(b.x_t.size(0) + b.x_s.size(0) for b in raw) / n_batches
-    return [pad_batch(b, caps).to(device) for b in raw], caps, real
+    real = sum(sum(ds.sizes(i)[:2]) for i in idxs) / n_batches
+    return [ds.collate(i, caps).to(device) for i in idxs], caps, real, ds.collate(idxs[0]), ds
+
+
+def loader_leg(ds, step, caps, device, ms_step, steps=16):
+    """The data loader beside the step (the reference feeds every step from a
+    DataLoader with 4 workers and copies the batch in, main_zinc...:151-162,
+    223-225).  Here: graphs/s of hlhgat.loader.GraphLoader (native collate +
+    padding + batch tables into pinned memory) with W worker threads; the
+    Python collate + pad_batch on one core for comparison; and the training
+    loop fed by the loader end to end -- collation on 4 threads, the H2D copy
+    of batch i+1 on a copy stream while step i runs, the replayed step."""
+    import numpy as np
+    from hlhgat.hodge_dataset import collate, pad_batch
+    from hlhgat.loader import GraphLoader
+    n = len(ds) // GRAPHS_PER_GPU
+    out = {"graphs_per_batch": GRAPHS_PER_GPU, "batches": n,
+           "reference_loop": "torch_geometric DataLoader(num_workers=4) + data.to(device) per step"}
+    rates = {}
+    for w in (1, 2, 4):
+        ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=w, prefetch=2 * w, pin=True)
+        list(ld)  # warm (page faults, pinned pool)
+        t0 = time.perf_counter()
+        nb = 0
+        for _ in range(2):
+            for _b in ld:
+                nb += 1
+        rates[str(w)] = round(nb * GRAPHS_PER_GPU / (time.perf_counter() - t0), 1)
+    out["native_collate_graphs_per_s"] = rates
+    graphs = [ds.graph(i) for i in range(GRAPHS_PER_GPU)]
+    t0 = time.perf_counter()
+    for _ in range(2):
+        pad_batch(collate(graphs, check_hodge=False), caps)
+    out["python_collate_graphs_per_s_1core"] = round(2 * GRAPHS_PER_GPU / (time.perf_counter() - t0), 1)
+    # the loader-fed loop: GraphLoader(4 threads, pinned) -> copy stream -> replayed step
+    ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=4, prefetch=8, pin=True)
+    cs = torch.cuda.Stream(device=device)
+    main = torch.cuda.current_stream(device)
+
+    def upload(b):
+        with torch.cuda.stream(cs):
+            bd = b.to(device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        for v in vars(bd).values():
+            if torch.is_tensor(v) and v.is_cuda:
+                v.record_stream(main)
+        return bd, ev
+
+    def batches():
+        while True:
+            for b in ld:
+                yield b
+
+    src = batches()
+    nxt = upload(next(src))
+    for i in range(steps + 2):
+        if i == 2:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        bd, ev = nxt
+        nxt = upload(next(src))
+        main.wait_event(ev)
+        step(bd)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out["loader_fed"] = {"value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
+                         "ms_per_step": round(dt * 1e3, 3), "workers": 4, "pinned": True,
+                         "steps": steps,
+                         "what": "training steps fed by GraphLoader end to end: native collate "
+                                 "on 4 threads, H2D of the next batch on a copy stream during "
+                                 "the step, copy-in + replayed step"}
+    out["device_resident_ms_per_step"] = round(ms_step, 3)
+    return out
+
+
+def parity_check(model, batch_dev, batch_cpu, tol=1e-4):
+    """The timed workload at full size against the oracle: the first step's
+    training-mode forward of the 1000-graph (padded) batch on the HIP path vs
+    the oracle (oracle/hodge_ref.py, pinned to the reference's golden vectors)
+    on the same, unpadded graphs with the same parameters.  Run on a copy of
+    the model (a training-mode forward moves the BatchNorm running stats)."""
+    import copy
+    from oracle.hodge_ref import RefZincModel
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    torch.set_num_threads(cores)
+    m = copy.deepcopy(model).train()
+    with torch.no_grad():
+        out = m(batch_dev).float().cpu()
+    ref = RefZincModel(**MODEL_KW)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    with torch.no_grad():
+        exp = ref.train()(batch_cpu)
+    del m
+    scale = max(1.0, float(exp.abs().max()))
+    err = float((out - exp).abs().max()) / scale
+    return {"graphs": int(batch_cpu.num_graphs), "outputs": int(exp.numel()),
+            "max_rel_err": err, "tol": tol, "pass": bool(err <= tol),
+            "what": "first-step training-mode forward of the timed 1000-graph batch (padded, "
+                    "HIP) vs the oracle on the same unpadded graphs and parameters; "
+                    "max|d| / max(1, max|oracle|)"}
 
 
 def cpu_baseline(batch_cpu, budget_s=15.0):
@@ -451,6 +560,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-loader", action="store_true",
+                    help="skip the data-loader leg (native collate rates, loader-fed steps)")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the full-size first-step forward check against the oracle")
     ap.add_argument("--eager", action="store_true", help="no hipGraph replay")
     ap.add_argument("--no-cfg5", action="store_true",
                     help="skip the config-5 (TSP) SpMM roofline measurement")
@@ -480,9 +593,13 @@ def main():
     from hlhgat.train import TrainStep
 
     log(f"[rank {rank}] generating {args.batches} x {GRAPHS_PER_GPU} synthetic graphs")
-    batches, caps, real_rows = make_batches(args.batches, rank, device)  # each rank: its own
+    batches, caps, real_rows, raw0, dataset = make_batches(args.batches, rank, device)  # per rank
     torch.manual_seed(0)
     model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**MODEL_KW).to(device).train()
+    pcheck = None
+    if rank == 0 and not args.no_parity_check:
+        pcheck = parity_check(model, batches[0], raw0)
+        log(f"[rank 0] parity check vs oracle (1000 graphs): {pcheck['max_rel_err']:.2e}")
     crit = hlhgat.nn.L1Loss()  # torch.nn.L1Loss, one HIP launch each way
 
     def loss_fn(out, b):
@@ -553,8 +670,11 @@ def main():
         "data": "synthetic ZINC-like simplex graphs (random-init weights; no dataset offline)",
         "config": {"workload": "BASELINE configs[1]: ZINC-12k-scale, HL_HGCNN_zinc_dense_int3_pyr "
                                "channels=[2,2,2] filters=[64,64,64] K=3 mlp=[256,256] keig=15; "
-                               "step = batch copy-in + CSR build + fwd + L1 + bwd "
-                               "(+ grad all-reduce) + Adam",
+                               "step = copy of the device-resident batch into the step's "
+                               "static buffers + fwd + L1 + bwd (+ grad all-reduce) + Adam; "
+                               "the batch tables (Laplacian / incidence CSRs, degrees, "
+                               "segment offsets) are built by the data loader at collate "
+                               "time, outside the step (see loader)",
                    "execution": "eager" if args.eager else
                    f"one hipGraph for the capacity bucket (captured in warmup, "
                    f"{step.stats['captures']} capture(s)), replayed for {args.batches} distinct "
@@ -570,6 +690,7 @@ def main():
                       "launches": proj["launches"],
                       "avg_launch_us": round(proj["ms"] * 1e3 / max(proj["launches"], 1), 2)},
         "cpu_baseline": None,
+        "parity_check": pcheck,
         "rooflines": {k: kernel_roofline(ops.prof_read(c), bound, note) for k, c, bound, note in (
             ("k_proj_bwd_fused", L.PROF_PROJ_BWD, "mfma",
              "Linear backward: weight-gradient split partials + data gradient, one launch; "
@@ -581,6 +702,7 @@ def main():
         "spmm_cfg5": None,
         "heads": None,
         "h2d": None,
+        "loader": None,
     }
     if rank == 0:
         roofline["isolated"] = isolated_poly_step(device, batches[0])
@@ -588,15 +710,16 @@ def main():
         log("[rank 0] config-5 SpMM roofline")
         result["spmm_cfg5"] = cfg5_spmm(device)
     if rank == 0 and world == 1:
-        from hlhgat.hodge_dataset import pad_batch
-        from hlhgat.synthetic import zinc_like_batch
-        h = h2d_leg(pad_batch(zinc_like_batch(GRAPHS_PER_GPU, seed=1), caps), device)
+        import numpy as np
+        h = h2d_leg(dataset.collate(np.arange(GRAPHS_PER_GPU), caps), device)
         h["value_if_serialised"] = round(GRAPHS_PER_GPU / (ms_step + h["ms_per_batch"]) * 1e3, 1)
         result["h2d"] = h
+    if rank == 0 and world == 1 and not args.no_loader:
+        log("[rank 0] loader leg")
+        result["loader"] = loader_leg(dataset, step, caps, device, ms_step)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
-        from hlhgat.synthetic import zinc_like_batch
-        result["cpu_baseline"] = cpu_baseline(zinc_like_batch(GRAPHS_PER_GPU, seed=1))
+        result["cpu_baseline"] = cpu_baseline(raw0)
     if rank == 0 and world == 1 and not args.no_heads:
         log("[rank 0] configs 3-5 heads")
         result["heads"] = heads_leg(device)

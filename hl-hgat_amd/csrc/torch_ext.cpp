@@ -1442,6 +1442,27 @@ int sink_accumulate(AutogradContext* ctx, const char* key) {
   return acc;
 }
 
+// Activation tap (test infrastructure, hlhgat.nn.TAP): while on, the
+// NodeEdgeInt value node keeps a copy of its hidden post-ReLU activations
+// (node side, then edge side) for the frozen-mask gradient checks.
+struct TapState {
+  bool on = false;
+  std::vector<Tensor> taken;
+};
+TapState& tap_state() {
+  static auto* t = new TapState();
+  return *t;
+}
+void set_tap(bool on) {
+  tap_state().on = on;
+  tap_state().taken.clear();
+}
+std::vector<Tensor> take_tap() {
+  std::vector<Tensor> out;
+  out.swap(tap_state().taken);
+  return out;
+}
+
 class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
  public:
   static variable_list forward(AutogradContext* ctx, Tensor x_t, Tensor x_s, Tensor rowptr,
@@ -1535,6 +1556,10 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     }
     side(pn, h1t, mom1n, eps1n, mom4n, eps4n, valid_t, tn);
     fk.main_waits_side();
+    if (tap_state().on) {
+      tap_state().taken.push_back(tn.a1.clone());
+      tap_state().taken.push_back(te.a1.clone());
+    }
     fk.escape({te.a1, te.m1, te.i1, te.h2, te.y, te.m4, te.i4});
     {
       EdgeMap em;
@@ -2198,6 +2223,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bwd", &set_fused_bwd);
+  m.def("set_tap", &set_tap);
+  m.def("take_tap", &take_tap);
   m.def("join_capture_streams", &join_capture_streams);
   m.def("stream_capturing", &stream_capturing);
   m.def("fork_side_stream", &fork_side_stream);

@@ -40,6 +40,8 @@ SIGNATURES = {
     "hlhgat_graclus": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "hlhgat_mlgc_map": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, P_i64, P_i64]),
     "hlhgat_gather_f32": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hlhgat_collate_sizes": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_collate": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_spmm": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64,
                             c_vp, c_i64, c_vp]),
     "hlhgat_poly_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
@@ -149,6 +151,27 @@ class HodgeFactorDesc(C.Structure):
     _fields_ = [("node_rowptr", c_vp), ("node_edge", c_vp), ("node_sign", c_vp),
                 ("node_order", c_vp), ("n_nodes", c_i64), ("ends", c_vp), ("alpha", c_vp),
                 ("edge_order", c_vp), ("n_edges", c_i64)]
+
+
+class PackedGraphsDesc(C.Structure):
+    """hlhgat_packed_graphs_t (include/hlhgat.h)."""
+    _fields_ = [("n_graphs", c_i64), ("node_ptr", c_vp), ("edge_ptr", c_vp), ("lt_ptr", c_vp),
+                ("ls_ptr", c_vp), ("x_t", c_vp), ("f_t", c_i64), ("x_s", c_vp), ("f_s", c_i64),
+                ("lt_row", c_vp), ("lt_col", c_vp), ("lt_w", c_vp), ("ls_row", c_vp),
+                ("ls_col", c_vp), ("ls_w", c_vp), ("b1_src", c_vp), ("b1_dst", c_vp),
+                ("y", c_vp), ("y_dim", c_i64)]
+
+
+class CollatedDesc(C.Structure):
+    """hlhgat_collated_t (include/hlhgat.h)."""
+    _fields_ = [("rows_t", c_i64), ("rows_s", c_i64), ("nnz_t", c_i64), ("nnz_s", c_i64),
+                ("x_t", c_vp), ("x_s", c_vp), ("edge_index_t", c_vp), ("edge_weight_t", c_vp),
+                ("edge_index_s", c_vp), ("edge_weight_s", c_vp), ("edge_index", c_vp),
+                ("y", c_vp), ("num_node1", c_vp), ("num_edge1", c_vp), ("csr_rowptr_t", c_vp),
+                ("csr_col_t", c_vp), ("csr_rowptr_s", c_vp), ("csr_col_s", c_vp),
+                ("inc_rowptr", c_vp), ("inc_eids", c_vp), ("deg_t", c_vp), ("inv_deg_t", c_vp),
+                ("seg_ptr_t", c_vp), ("seg_ptr_s", c_vp), ("valid_mask_t", c_vp),
+                ("n_t", c_i64), ("n_s", c_i64)]
 
 
 class HlhgatError(RuntimeError):

@@ -22,6 +22,7 @@ import torch.nn as nn
 from torch import Tensor
 from torch.nn import Dropout, Parameter
 
+from . import nn as _nn
 from . import ops
 from .hodge_dataset import BoundaryOperator, adj2par1, boundary_from_sparse, degree
 from .nn import BatchNorm, Linear, Sequential, run_sequential
@@ -214,8 +215,18 @@ class NodeEdgeInt(nn.Module):
             gsink, self._hlhgat_gsink = getattr(self, "_hlhgat_gsink", (None, None)), (None, None)
             # one-shot weight pack built for the whole forward (ops.nei_prepack)
             packed = ops.take_pack(self)
+            tapping = _nn.TAP is not None
+            if tapping:
+                ops._ext.set_tap(True)
             r = ops.nei_value(x_t, x_s, bop.incidence(), ops.reciprocal(D), self.WV_Node,
                               self.WV_Edge, bop.valid_t, bop.valid_s, gsink=gsink, packed=packed)
+            if tapping:
+                hidden = ops._ext.take_tap()
+                ops._ext.set_tap(False)
+                if r is not None:  # hidden ReLUs (inside the node), then the outputs
+                    for mod, y in zip((self.WV_Node[2], self.WV_Edge[2], self.WV_Node[5],
+                                       self.WV_Edge[5]), list(hidden) + list(r)):
+                        _nn.tap(mod, y)
             if r is not None:
                 return r
         if getattr(par, "valid_t", None) is not None:
@@ -239,6 +250,9 @@ class NodeEdgeInt(nn.Module):
             qc_s = ops.linear_blocks([x_t2s], self.WQ_Node.weight, self.WQ_Node.bias)
             a_s = ops.att_score(qc_s, kq_s[:, dk:], kq_s[:, :dk], 1 - self.lambda_Edge,
                                 self.lambda_Edge, sq, code)
+            if isinstance(self.sigma, nn.ReLU):
+                _nn.tap(self.sigma, a_t)
+                _nn.tap(self.sigma, a_s)
             return a_t, a_s
         # node and edge MLPs are independent: edge side on the side stream
         return ops.fork(lambda: _value_mlp(self.WV_Node, [x_s2t, x_t]),

@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "static_caps", "pad_batch", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
+           "static_caps", "pad_batch", "PackedGraphs", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
            "hodge_factor_ok", "hodge_coo_from_boundary"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
@@ -527,6 +527,187 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     out.valid_mask_t = torch.arange(Rt) < nt
     out.num_nodes = Rt
     return out
+
+
+class PackedGraphs:
+    """A dataset of PairData simplex graphs packed back to back (the
+    InMemoryDataset storage the reference's Hodge_Dataset keeps,
+    lib/Hodge_Dataset.py:27-48): per-graph slices of x_t, x_s, the L0 / L1
+    COO (graph-local, row-sorted, symmetric), the B1 edge list and y.
+
+    ``collate(idx, caps)`` builds the batch of graphs ``idx`` in ONE native
+    call (hlhgat_collate, csrc/collate.hip): bitwise the Batch of
+    ``pad_batch(collate([self.graphs[i] for i in idx]), caps)`` (or of
+    ``collate`` alone when caps is None), tables included, with no Python
+    work per graph.  ``pin=True`` allocates the batch in pinned host memory
+    (asynchronous copy-in)."""
+
+    _KEYS = ("x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+             "edge_index")
+
+    def __init__(self, graphs: Sequence[PairData], check_hodge: bool = True):
+        from . import _lib
+        self._lib = _lib
+        G = len(graphs)
+        if G == 0:
+            raise ValueError("PackedGraphs: no graphs")
+        for g in graphs:
+            for k in self._KEYS:
+                if getattr(g, k, None) is None:
+                    raise ValueError(f"PackedGraphs: graph without {k}")
+        a = lambda v, dt: np.ascontiguousarray(np.asarray(v), dtype=dt)  # noqa: E731
+        self.f_t = int(graphs[0].x_t.shape[1])
+        self.f_s = int(graphs[0].x_s.shape[1])
+        if any(g.x_t.shape[1] != self.f_t or g.x_s.shape[1] != self.f_s for g in graphs):
+            raise ValueError("PackedGraphs: feature widths differ between graphs")
+        cnt = lambda f: np.concatenate([[0], np.cumsum([f(g) for g in graphs])]).astype(np.int64)  # noqa: E731
+        self.node_ptr = cnt(lambda g: g.x_t.shape[0])
+        self.edge_ptr = cnt(lambda g: g.x_s.shape[0])
+        self.lt_ptr = cnt(lambda g: np.asarray(g.edge_index_t).shape[1])
+        self.ls_ptr = cnt(lambda g: np.asarray(g.edge_index_s).shape[1])
+        for g in graphs:
+            if np.asarray(g.edge_index).shape[1] != g.x_s.shape[0]:
+                raise ValueError("PackedGraphs: edge_index must have one column per x_s row")
+        self.x_t = np.concatenate([a(g.x_t, np.float32) for g in graphs])
+        self.x_s = np.concatenate([a(g.x_s, np.float32) for g in graphs])
+        cat = lambda k, i, dt: np.concatenate([a(getattr(g, k), np.int64)[i].astype(dt)  # noqa: E731
+                                               for g in graphs])
+        self.lt_row, self.lt_col = cat("edge_index_t", 0, np.int32), cat("edge_index_t", 1, np.int32)
+        self.ls_row, self.ls_col = cat("edge_index_s", 0, np.int32), cat("edge_index_s", 1, np.int32)
+        self.b1_src, self.b1_dst = cat("edge_index", 0, np.int32), cat("edge_index", 1, np.int32)
+        self.lt_w = np.concatenate([a(g.edge_weight_t, np.float32).reshape(-1) for g in graphs])
+        self.ls_w = np.concatenate([a(g.edge_weight_s, np.float32).reshape(-1) for g in graphs])
+        ys = [getattr(g, "y", None) for g in graphs]
+        if all(y is not None for y in ys):
+            self.y = np.stack([a(y, np.float32).reshape(-1) for y in ys])
+            self.y_dim = int(self.y.shape[1])
+            self._y_dtype = torch.as_tensor(ys[0]).dtype
+        else:
+            self.y, self.y_dim, self._y_dtype = np.zeros((G, 0), np.float32), 0, None
+        if self._y_dtype is not None and self._y_dtype != torch.float32:
+            raise ValueError("PackedGraphs: y must be float32")
+        if check_hodge:
+            sorted_sym = {k: all(is_sorted_symmetric(np.asarray(getattr(g, k)),
+                                                     np.asarray(getattr(g, w)))
+                                 for g in graphs)
+                          for k, w in (("edge_index_s", "edge_weight_s"),
+                                       ("edge_index_t", "edge_weight_t"))}
+        else:
+            ok = all(getattr(g, "_hodge_sorted", False) for g in graphs)
+            sorted_sym = {"edge_index_s": ok, "edge_index_t": ok}
+        if not all(sorted_sym.values()):
+            raise ValueError("PackedGraphs: every Laplacian COO must be row-sorted and symmetric "
+                             "(the Hodge builder's dense_to_sparse output)")
+        self.hodge_sorted = sorted_sym
+        self.n_graphs = G
+        self._desc = _lib.PackedGraphsDesc(
+            G, self.node_ptr.ctypes.data, self.edge_ptr.ctypes.data, self.lt_ptr.ctypes.data,
+            self.ls_ptr.ctypes.data, self.x_t.ctypes.data, self.f_t, self.x_s.ctypes.data,
+            self.f_s, self.lt_row.ctypes.data, self.lt_col.ctypes.data, self.lt_w.ctypes.data,
+            self.ls_row.ctypes.data, self.ls_col.ctypes.data, self.ls_w.ctypes.data,
+            self.b1_src.ctypes.data, self.b1_dst.ctypes.data, self.y.ctypes.data, self.y_dim)
+
+    def __len__(self) -> int:
+        return self.n_graphs
+
+    def graph(self, i: int) -> PairData:
+        """Graph i as a PairData (views of the packed arrays)."""
+        n0, n1 = self.node_ptr[i], self.node_ptr[i + 1]
+        e0, e1 = self.edge_ptr[i], self.edge_ptr[i + 1]
+        t0, t1 = self.lt_ptr[i], self.lt_ptr[i + 1]
+        s0, s1 = self.ls_ptr[i], self.ls_ptr[i + 1]
+        T = lambda v: torch.from_numpy(np.ascontiguousarray(v))  # noqa: E731
+        ei = lambda r, c: T(np.stack([r, c]).astype(np.int64))  # noqa: E731
+        return PairData(edge_index_s=ei(self.ls_row[s0:s1], self.ls_col[s0:s1]),
+                        x_s=T(self.x_s[e0:e1]), edge_index_t=ei(self.lt_row[t0:t1],
+                                                               self.lt_col[t0:t1]),
+                        x_t=T(self.x_t[n0:n1]), edge_weight_s=T(self.ls_w[s0:s1]),
+                        edge_weight_t=T(self.lt_w[t0:t1]),
+                        edge_index=ei(self.b1_src[e0:e1], self.b1_dst[e0:e1]),
+                        y=T(self.y[i]) if self.y_dim else None)
+
+    def _factor_ok(self, i: int) -> bool:
+        cache = self.__dict__.setdefault("_fac", {})
+        if i not in cache:
+            g = self.graph(i)
+            cache[i] = hodge_factor_ok(g.edge_index, g.x_t.shape[0], g.edge_index_s,
+                                       g.edge_weight_s)
+        return cache[i]
+
+    def sizes(self, idx) -> Tuple[int, int, int, int]:
+        """(nodes, edges, L0 entries, L1 entries) of the graphs idx."""
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        out = np.zeros(4, dtype=np.int64)
+        self._lib.check(self._lib.LIB.hlhgat_collate_sizes(C_ref(self._desc), idx.ctypes.data,
+                                                           idx.size, out.ctypes.data),
+                        "collate_sizes")
+        return tuple(int(v) for v in out)
+
+    def caps_for(self, idx, quantum: int = 512) -> Dict[str, int]:
+        """static_caps of the batch of graphs idx (without building it)."""
+        n_t, n_s, z_t, z_s = self.sizes(idx)
+        return {"rows_t": _roundup(n_t + PAD_MIN_ROWS, quantum),
+                "rows_s": _roundup(n_s + PAD_MIN_ROWS, quantum),
+                "nnz_t": _roundup(z_t + 1, 4 * quantum), "nnz_s": _roundup(z_s + 1, 4 * quantum)}
+
+    def collate(self, idx, caps: Optional[Dict[str, int]] = None, pin: bool = False) -> "Batch":
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        B = int(idx.size)
+        n_t, n_s, z_t, z_s = self.sizes(idx)
+        padded = caps is not None
+        Rt, Rs = (caps["rows_t"], caps["rows_s"]) if padded else (n_t, n_s)
+        Zt, Zs = (caps["nnz_t"], caps["nnz_s"]) if padded else (z_t, z_s)
+        if padded and (Rt <= n_t or Rs <= n_s):
+            raise ValueError(f"PackedGraphs.collate: caps ({Rt}, {Rs}) must exceed the rows "
+                             f"({n_t}, {n_s})")
+        if padded and (Zt < z_t or Zs < z_s):
+            raise ValueError(f"PackedGraphs.collate: {z_t} / {z_s} Laplacian entries exceed "
+                             f"the caps {Zt} / {Zs}")
+        e = lambda shape, dt: torch.empty(shape, dtype=dt, pin_memory=pin)  # noqa: E731
+        f32, i32, i64 = torch.float32, torch.int32, torch.int64
+        t = {"x_t": e((Rt, self.f_t), f32), "x_s": e((Rs, self.f_s), f32),
+             "edge_index_t": e((2, Zt), i64), "edge_weight_t": e((Zt,), f32),
+             "edge_index_s": e((2, Zs), i64), "edge_weight_s": e((Zs,), f32),
+             "edge_index": e((2, Rs), i64), "y": e((B * self.y_dim,), f32),
+             "num_node1": e((B,), i64), "num_edge1": e((B,), i64),
+             "csr_rowptr_t": e((Rt + 1,), i32), "csr_col_t": e((Zt,), i32),
+             "csr_rowptr_s": e((Rs + 1,), i32), "csr_col_s": e((Zs,), i32),
+             "inc_rowptr": e((Rt + 1,), i32), "inc_eids": e((2 * Rs,), i32),
+             "deg_t": e((Rt,), f32), "inv_deg_t": e((Rt,), f32),
+             "seg_ptr_t": e((B + 1,), i32), "seg_ptr_s": e((B + 1,), i32),
+             "valid_mask_t": e((Rt,), torch.bool)}
+        o = self._lib.CollatedDesc(Rt, Rs, Zt, Zs, *[t[k].data_ptr() for k in (
+            "x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
+            "edge_index", "y", "num_node1", "num_edge1", "csr_rowptr_t", "csr_col_t",
+            "csr_rowptr_s", "csr_col_s", "inc_rowptr", "inc_eids", "deg_t", "inv_deg_t",
+            "seg_ptr_t", "seg_ptr_s", "valid_mask_t")], 0, 0)
+        self._lib.check(self._lib.LIB.hlhgat_collate(C_ref(self._desc), idx.ctypes.data, B,
+                                                     C_ref(o)), "collate")
+        b = Batch()
+        b.num_graphs = B
+        for k in self._KEYS:
+            setattr(b, k, t[k])
+        if self.y_dim:
+            b.y = t["y"]
+        b.num_node1, b.num_edge1 = t["num_node1"], t["num_edge1"]
+        b.num_nodes = Rt
+        b.hodge_sorted = dict(self.hodge_sorted)
+        # factored L1 as collate decides it (never for padded batches: pad_batch)
+        b.l1_factor = (not padded and z_s >= FACTOR_MIN_ROW * n_s and n_s > 0
+                       and all(self._factor_ok(int(i)) for i in idx))
+        for k in ("csr_rowptr_t", "csr_col_t", "csr_rowptr_s", "csr_col_s", "inc_rowptr",
+                  "inc_eids", "deg_t", "inv_deg_t", "seg_ptr_t", "seg_ptr_s"):
+            setattr(b, k, t[k])
+        if padded:
+            b.n_valid_t = torch.tensor([n_t], dtype=i32)
+            b.n_valid_s = torch.tensor([n_s], dtype=i32)
+            b.valid_mask_t = t["valid_mask_t"]
+        return b
+
+
+def C_ref(struct):
+    import ctypes
+    return ctypes.byref(struct)
 
 
 class BoundaryOperator:

@@ -287,6 +287,12 @@ class _AttPoolHead(nn.Module):
     # unused parameters (hlhgat.distributed.wrap_ddp reads this flag)
     ddp_find_unused_parameters = True
 
+    @property
+    def forward_collectives(self) -> bool:
+        """The pool_loc attention is divided by its batch max over every rank
+        (distributed.global_max) when it is not applied at every level."""
+        return not self.att_every_level
+
     def __init__(self, channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
                  dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, att_every_level):
         super().__init__()

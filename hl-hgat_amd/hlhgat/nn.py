@@ -87,6 +87,18 @@ class BatchNorm(tnn.Module):
 
 _ARROW = re.compile(r"\s*->\s*")
 
+# Activation tap (test infrastructure): while TAP is a dict, every ReLU site
+# -- fused into a conv / BatchNorm node or not -- records a copy of its output
+# under the nn.ReLU module it stands for, one entry per call in call order.
+# The frozen-mask gradient checks (tests/test_frozen_mask_grads.py) rebuild
+# the ReLU masks of the HIP forward from it.
+TAP = None
+
+
+def tap(mod, y) -> None:
+    if TAP is not None and torch.is_tensor(y):
+        TAP.setdefault(mod, []).append(y.detach().clone())
+
 
 class L1Loss(tnn.L1Loss):
     """torch.nn.L1Loss (the ZINC training loss) whose mean reduction on ROCm
@@ -187,15 +199,20 @@ class Sequential(tnn.Module):
                     out = env[ins[0]]  # identity: no copy kernel
                 else:
                     out = fn(*[env[n] for n in ins])
+                    if isinstance(fn, tnn.ReLU):
+                        tap(fn, out)
                 i += 1
             elif fuse[0] == "bn_relu":
                 from .ops import batch_norm_act
                 out = batch_norm_act(env[ins[0]], fn.module, relu=True)
+                tap(getattr(self, f"module_{i + 1}"), out)
                 i += 2
             else:
                 bn = getattr(self, f"module_{i + 1}").module
                 out = fn.forward_bn(*[env[n] for n in ins], bn=bn,
                                     relu=fuse[0] == "conv_bn_relu")
+                if fuse[0] == "conv_bn_relu":
+                    tap(getattr(self, f"module_{i + 2}"), out)
                 i += fuse[1]
             if len(outs) == 1:
                 env[outs[0]] = out
@@ -249,11 +266,15 @@ def run_sequential(seq: tnn.Sequential, blocks) -> torch.Tensor:
         elif isinstance(m, tnn.BatchNorm1d):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], tnn.ReLU)
             h = batch_norm_act(h, m, relu=relu)
+            if relu:
+                tap(mods[i + 1], h)
             i += relu
         elif isinstance(m, tnn.Dropout) and (m.p == 0.0 or not m.training):
             pass
         else:
             h = m(h if h is not None else torch.cat(list(blocks), -1))
+            if isinstance(m, tnn.ReLU):
+                tap(m, h)
         i += 1
     return h
 

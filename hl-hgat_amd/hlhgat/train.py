@@ -31,13 +31,24 @@ import torch.distributed as dist
 
 from . import ops
 
-__all__ = ["TrainStep", "batch_key"]
+__all__ = ["TrainStep", "batch_key", "forward_collectives"]
 
 # HIP_ADAM = False: torch's fused Adam instead of hlhgat_adam_flat
 HIP_ADAM = True
 # DEFER_REDUCE = False (tests): every Linear backward launches its own split
 # reduction instead of handing it to the next one on its stream (same bits)
 DEFER_REDUCE = True
+
+
+def forward_collectives(model: torch.nn.Module) -> bool:
+    """True when the model's training forward exchanges data between ranks:
+    SyncBatchNorm layers (hlhgat.distributed.convert_sync_batchnorm) or a
+    head that declares ``forward_collectives`` (the CIFAR attpool head's
+    batch-global max, hodge_st_model._AttPoolHead)."""
+    if getattr(model, "forward_collectives", False):
+        return True
+    return any(ops.sync_bn_group(m) is not None for m in model.modules()
+               if isinstance(m, torch.nn.modules.batchnorm._BatchNorm))
 
 
 def _tensor_items(batch):
@@ -112,6 +123,12 @@ class TrainStep:
     def __init__(self, model: torch.nn.Module, loss_fn: Callable, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  graphs: bool = True, max_graphs: int = 32):
+        if isinstance(model, torch.nn.parallel.DistributedDataParallel):
+            # DDP would all-reduce the gradients in its hooks and TrainStep again in
+            # its bucket (two reductions, and DDP's gradient_as_bucket_view fights the
+            # flat gradient views): TrainStep IS the data-parallel wrapper
+            raise ValueError("TrainStep: pass the bare module, not a DistributedDataParallel "
+                             "wrapper -- TrainStep reduces the gradients itself (one bucket)")
         self.model = model
         self.loss_fn = loss_fn
         params = [p for p in model.parameters() if p.requires_grad]
@@ -160,6 +177,14 @@ class TrainStep:
                 "exp_avg_sq": torch.zeros_like(self.flat)}
             self._hyper = (lr, betas, eps, weight_decay)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.graphs_off = None
+        if self.graphs and self.world > 1 and dist.get_backend() != "nccl" \
+                and forward_collectives(model):
+            # a collective inside the forward (SyncBatchNorm statistics, the
+            # attpool heads' batch-global max) runs on the host under gloo and
+            # cannot be captured: this step runs eagerly (RCCL ones can)
+            self.graphs = False
+            self.graphs_off = "forward collectives under a host (gloo) backend"
         self.max_graphs = max_graphs
         self._graphs: Dict[Tuple, _Captured] = {}
         self._pool = None

@@ -169,6 +169,70 @@ int hlhgat_mlgc_map(const int64_t* cluster, int64_t n_nodes, const int64_t* edge
                     int64_t n_edges, int64_t* c_node, float* c_edge, int64_t* coarse_edges,
                     int64_t* n_coarse_nodes, int64_t* n_coarse_edges);
 
+/* ---- native data loader (HOST functions, host pointers) -----------------
+ * Replaces the reference's per-step DataLoader collation of PairData
+ * (lib/Hodge_Dataset.py:40-48; main_zinc_HL_HGCNN_dense_int3_pyr.py:223-225)
+ * plus the batch tables the device step reads.  A packed dataset holds every
+ * graph's arrays back to back (InMemoryDataset-style slices, graph-local
+ * indices): */
+typedef struct {
+  int64_t n_graphs;
+  const int64_t* node_ptr; /* [G+1] x_t rows (nodes) per graph, cumulative */
+  const int64_t* edge_ptr; /* [G+1] x_s rows (edges) */
+  const int64_t* lt_ptr;   /* [G+1] L0 COO entries */
+  const int64_t* ls_ptr;   /* [G+1] L1 COO entries */
+  const float* x_t;        /* [N][f_t] */
+  int64_t f_t;
+  const float* x_s;        /* [E][f_s] */
+  int64_t f_s;
+  const int32_t* lt_row;   /* L0 COO, graph-local node ids, row-sorted */
+  const int32_t* lt_col;
+  const float* lt_w;
+  const int32_t* ls_row;   /* L1 COO, graph-local edge ids, row-sorted */
+  const int32_t* ls_col;
+  const float* ls_w;
+  const int32_t* b1_src;   /* [E] B1 edge list (edge_index), graph-local */
+  const int32_t* b1_dst;
+  const float* y;          /* [G][y_dim] (y_dim 0: none) */
+  int64_t y_dim;
+} hlhgat_packed_graphs_t;
+/* The collated batch: capacities in (rows_t, rows_s, nnz_t, nnz_s equal to
+ * the batch's sizes = no padding; rows above them = hodge_dataset.pad_batch's
+ * padding), caller-allocated outputs (the table pointers may be NULL to skip
+ * a table); n_t / n_s out = the real rows. */
+typedef struct {
+  int64_t rows_t, rows_s, nnz_t, nnz_s;
+  float* x_t;               /* [rows_t][f_t] */
+  float* x_s;               /* [rows_s][f_s] */
+  int64_t* edge_index_t;    /* [2][nnz_t] */
+  float* edge_weight_t;     /* [nnz_t] */
+  int64_t* edge_index_s;    /* [2][nnz_s] */
+  float* edge_weight_s;     /* [nnz_s] */
+  int64_t* edge_index;      /* [2][rows_s] */
+  float* y;                 /* [B][y_dim] */
+  int64_t* num_node1;       /* [B] */
+  int64_t* num_edge1;       /* [B] */
+  int32_t* csr_rowptr_t;    /* [rows_t+1] */
+  int32_t* csr_col_t;       /* [nnz_t] */
+  int32_t* csr_rowptr_s;    /* [rows_s+1] */
+  int32_t* csr_col_s;       /* [nnz_s] */
+  int32_t* inc_rowptr;      /* [rows_t+1] incidence CSR of |B1| */
+  int32_t* inc_eids;        /* [2 rows_s] */
+  float* deg_t;             /* [rows_t] degree (padding rows: 1) */
+  float* inv_deg_t;         /* [rows_t] fp32 1 / degree */
+  int32_t* seg_ptr_t;       /* [B+1] */
+  int32_t* seg_ptr_s;       /* [B+1] */
+  uint8_t* valid_mask_t;    /* [rows_t] row < n_t */
+  int64_t n_t, n_s;         /* out */
+} hlhgat_collated_t;
+/* sizes[4] = (nodes, edges, L0 entries, L1 entries) of the graphs idx[0..n). */
+int hlhgat_collate_sizes(const hlhgat_packed_graphs_t* d, const int64_t* idx, int64_t n_idx,
+                         int64_t* sizes);
+/* Collate graphs idx[0..B) (in that order) into *out: bitwise the arrays of
+ * hodge_dataset.collate followed by pad_batch. */
+int hlhgat_collate(const hlhgat_packed_graphs_t* d, const int64_t* idx, int64_t B,
+                   hlhgat_collated_t* out);
+
 /* dst[i] = src[idx[i]] for i < n (device; e.g. halo sval = val[eperm]). */
 int hlhgat_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst,
                       void* stream);

@@ -217,13 +217,30 @@ def _product_batch(g, prefix, cuda, factored):
     return b
 
 
-def _grad_gate(m_hip, m32, m64, g, cond):
+def write_gate_log(case, rows):
+    """The per-parameter bounds a gate applied, as
+    gpurun_out/grad_gates/<case>.json (copied into profiles/ per round)."""
+    import json
+    from conftest import REPO
+    out_dir = os.path.join(REPO, "gpurun_out", "grad_gates")
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, case + ".json"), "w") as f:
+        json.dump({"case": case, "params": rows}, f, indent=1)
+    tight = [r for r in rows if r.get("bound") is not None]
+    loose = sorted(tight, key=lambda r: -r["bound"])[:3]
+    print(f"[gate] {case}: {len(rows)} params; loosest bounds " +
+          ", ".join(f"{r['param']} {r['bound']:.1e} (err {r['err']:.1e})" for r in loose))
+
+
+def _grad_gate(m_hip, m32, m64, g, cond, case=None):
     """per-parameter: HIP vs fp64 oracle within 3x max(fp32 oracle vs fp64,
     conditioning), floor 1e-4 relative; sampled fixture entries within the
-    same bound (module docstring)."""
+    same bound (module docstring).  The applied bounds are logged
+    (write_gate_log) when `case` is given."""
     p32 = dict(m32.named_parameters())
     p64 = dict(m64.named_parameters())
     worst = []
+    rows = []
     for k, p in m_hip.named_parameters():
         if g is not None and "nograd/" + k in g:
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
@@ -234,16 +251,24 @@ def _grad_gate(m_hip, m32, m64, g, cond):
         if _bn_fed_bias(k):
             # analytically zero: noise no larger than 3x the fp32 reference's
             noise32 = float(p32[k].grad.abs().max()) / scale
+            rows.append({"param": k, "err": float(hip.abs().max()) / scale, "bound": None,
+                         "noise_bound": max(3 * noise32, 1e-3), "kind": "bn-fed bias"})
             assert float(hip.abs().max()) / scale <= max(3 * noise32, 1e-3), k
             continue
         err32 = float((p32[k].grad.double() - e64).abs().max()) / scale
         errh = float((hip - e64).abs().max()) / scale
         bound = max(3 * max(err32, cond.get(k, 0.0)), 1e-4)
+        rows.append({"param": k, "err": errh, "bound": bound, "err_fp32_oracle": err32,
+                     "cond": cond.get(k, 0.0)})
+        if case is not None and errh > bound:
+            write_gate_log(case, rows)
         assert errh <= bound, (k, errh, err32, cond.get(k))
         if g is not None:
             ref, got, sc = grad_view(g, k, p.grad)
             assert float((ref - got).abs().max()) / sc <= bound + err32, (k, "fixture")
         worst.append((errh / bound, k))
+    if case is not None:
+        write_gate_log(case, rows)
     return max(worst)
 
 
@@ -280,7 +305,7 @@ def test_head_at_baseline_vs_reference(cuda, name, factored):
     m64, out64, _ = _run_oracle(name, g, torch.float64)
     cond = _cond(m64, [_run_oracle(name, g, torch.float64, 1e-6, s)[0] for s in (0, 1)])
     close(out.detach().cpu(), out64, 1e-4, "out vs fp64 oracle")
-    _grad_gate(m, m32, m64, g, cond)
+    _grad_gate(m, m32, m64, g, cond, case=f"cond_{name}{'_factored' if factored else ''}")
     ops.check_device_errors()
 
 
@@ -387,4 +412,5 @@ def test_tsp_head_cfg5_2500_nodes_vs_oracle(cuda, factored):
         (o * Rg.to(dt)).sum().backward()
         res.append((mo, o.detach()))
     close(out.detach().cpu(), res[1][1], 1e-4, "out vs fp64 oracle")
-    _grad_gate(m, res[0][0], res[1][0], None, _cond(res[1][0], [res[2][0], res[3][0]]))
+    _grad_gate(m, res[0][0], res[1][0], None, _cond(res[1][0], [res[2][0], res[3][0]]),
+               case=f"cond_cfg5_tsp_2500{'_factored' if factored else ''}")

@@ -44,8 +44,8 @@ def test_errors_surface_without_gpu():
     """Argument validation runs before any HIP call and reports a message."""
     import torch  # noqa: F401
     from hlhgat import _lib
-    rc = _lib.LIB.hlhgat_poly_basis_fwd(7, None, None, None, 10, 0, None, None, None, 0, 0, 0,
-                                        None, 1, 1, 3, None, None)
+    rc = _lib.LIB.hlhgat_poly_basis_fwd(7, None, None, None, 10, 0, None, None, None, 1, 1, 3,
+                                        None, None)
     assert rc == 1
     assert b"bad kind" in _lib.LIB.hlhgat_last_error()
     rc = _lib.LIB.hlhgat_spmm(None, None, None, 4, 0, None, None, None, 1, 0, None, 1, None)

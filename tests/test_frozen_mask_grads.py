@@ -1,0 +1,190 @@
+"""Whole-model gradients held to 1e-4 with the ReLU masks frozen (-m gpu).
+
+Why: the heads stack 6-12 dense blocks of batch-statistics BatchNorm + ReLU.
+Pre-activations within fp32 rounding of 0 make the HIP path (fp32, MFMA
+summation order) and an fp64 evaluation disagree on a few ReLU masks, and a
+flipped mask moves deep-layer gradients by up to ~18 % (relative, max-norm;
+tests/test_baseline_configs.py measures it as `cond`).  That gate therefore
+bounds the HIP gradient by 3x the conditioning.  Here the conditioning is
+taken out instead:
+
+  1. the HIP forward runs with hlhgat.nn.TAP on: every ReLU site (fused into a
+     conv / BatchNorm / NodeEdgeInt node or not) records its output, so the
+     masks the HIP forward actually applied are known (y > 0);
+  2. the fp64 oracle (oracle/hodge_ref.py, pinned to the reference by the
+     golden fixtures) runs with each nn.ReLU replaced by multiplication with
+     the HIP mask of the same module and call;
+  3. both backward passes use the same upstream gradient.
+
+In exact arithmetic the two now compute the same function, so every
+parameter gradient must match to 1e-4 relative (max|hip - fp64| <=
+1e-4 * max(1, max|fp64|)).  Biases that feed a training-mode BatchNorm have
+an analytically zero gradient and are checked to be noise (<= 1e-3 of the
+gradient scale).  Each test writes its per-parameter table to
+gpurun_out/grad_gates/<case>.json.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as tnn
+
+from conftest import REPO, close, load_golden
+from oracle import hodge_ref as R
+
+import test_baseline_configs as TB  # noqa: E402  (fixtures' helpers and settings)
+
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+from baseline_params import fill_params  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+T = torch.from_numpy
+TOL = 1e-4
+
+
+class MaskedReLU(tnn.Module):
+    """ReLU with the mask of a recorded forward: x * [y_hip > 0], call by call."""
+
+    def __init__(self, masks):
+        super().__init__()
+        self.masks = masks
+        self.i = 0
+
+    def forward(self, x):
+        assert self.i < len(self.masks), "more ReLU calls than the HIP forward made"
+        m = self.masks[self.i]
+        self.i += 1
+        assert tuple(m.shape) == tuple(x.shape), (m.shape, x.shape)
+        return x * m.to(x.dtype)
+
+
+def _run_tapped(fn):
+    from hlhgat import nn as hnn
+    hnn.TAP = {}
+    try:
+        out = fn()
+        taps = hnn.TAP
+    finally:
+        hnn.TAP = None
+    return out, taps
+
+
+def _freeze(ref, m_hip, taps):
+    """Replace every nn.ReLU of the oracle `ref` by the HIP forward's masks."""
+    names = {id(mod): n for n, mod in m_hip.named_modules()}
+    by_name = {names[id(mod)]: [(y > 0).cpu() for y in ys] for mod, ys in taps.items()}
+    masked = []
+    for name, mod in list(ref.named_modules()):
+        if not isinstance(mod, tnn.ReLU):
+            continue
+        assert name in by_name, f"HIP forward recorded no ReLU output for {name}"
+        parent = ref.get_submodule(name.rsplit(".", 1)[0]) if "." in name else ref
+        mm = MaskedReLU(by_name[name])
+        setattr(parent, name.rsplit(".", 1)[-1], mm)
+        masked.append(mm)
+    return masked
+
+
+def _check(case, m_hip, ref64, masked):
+    for mm in masked:
+        assert mm.i == len(mm.masks), "fewer ReLU calls than the HIP forward made"
+    p64 = dict(ref64.named_parameters())
+    rows, bad = [], []
+    for k, p in m_hip.named_parameters():
+        e = p64[k].grad
+        if p.grad is None or e is None:
+            assert (p.grad is None or float(p.grad.abs().max()) == 0.0) and \
+                (e is None or float(e.abs().max()) == 0.0), k
+            continue
+        scale = max(1.0, float(e.abs().max()))
+        err = float((p.grad.detach().cpu().double() - e).abs().max()) / scale
+        if TB._bn_fed_bias(k):
+            rows.append({"param": k, "err": err, "bound": 1e-3, "kind": "bn-fed bias (noise)"})
+            if err > 1e-3:
+                bad.append((k, err))
+            continue
+        rows.append({"param": k, "err": err, "bound": TOL, "scale": scale})
+        if err > TOL:
+            bad.append((k, err))
+    out_dir = os.path.join(REPO, "gpurun_out", "grad_gates")
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, f"frozen_{case}.json"), "w") as f:
+        json.dump({"case": case, "tol": TOL, "n_masks": sum(len(m.masks) for m in masked),
+                   "worst": max(r["err"] for r in rows if r["bound"] == TOL),
+                   "params": rows}, f, indent=1)
+    worst = max((r["err"], r["param"]) for r in rows if r["bound"] == TOL)
+    print(f"[frozen-mask] {case}: {len(rows)} params, worst {worst[0]:.2e} ({worst[1]})")
+    assert not bad, bad
+
+
+def _d64(b):
+    d = TB._D()
+    for k in TB.KEYS:
+        v = getattr(b, k)
+        setattr(d, k, v.double() if torch.is_tensor(v) and v.is_floating_point() else v)
+    return d
+
+
+def test_frozen_mask_grads_cfg2_zinc_200(cuda):
+    """Config 2 (6 blocks K=3 d=64, mlp [256, 256]) on 200 ZINC-like graphs."""
+    import hlhgat
+    from hlhgat.synthetic import zinc_like_batch
+    kw = dict(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256], K=3, keig=15)
+    b = zinc_like_batch(200, seed=21)
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**kw)
+    ref64 = R.RefZincModel(**kw).double()
+    ref64.load_state_dict({k: v.double() if v.is_floating_point() else v
+                           for k, v in m.state_dict().items()})
+    m = m.to(cuda).train()
+    bd = zinc_like_batch(200, seed=21).to(cuda)
+    out, taps = _run_tapped(lambda: m(bd))
+    Rg = torch.randn(out.shape, generator=torch.Generator().manual_seed(5))
+    (out * Rg.to(cuda)).sum().backward()
+    masked = _freeze(ref64, m, taps)
+    out64 = ref64.train()(_d64(b))
+    close(out.detach().cpu(), out64.detach(), 1e-4, "out vs fp64 oracle (frozen masks)")
+    (out64 * Rg.double()).sum().backward()
+    _check("cfg2_zinc_200", m, ref64, masked)
+
+
+@pytest.mark.parametrize("name,factored", [("baseline_cfg3_cifar", False),
+                                           ("baseline_cfg3_cifar", True),
+                                           ("baseline_cfg4_pepfunc", False),
+                                           ("baseline_cfg5_tsp", False),
+                                           ("baseline_cfg5_tsp", True)])
+def test_frozen_mask_grads_heads_at_baseline(cuda, name, factored):
+    """Configs 3 / 4 / 5 at their own hyperparameters on the reference
+    fixtures' inputs (tests/golden/make_golden_baseline.py)."""
+    import hlhgat
+    from hlhgat import ops
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    g = load_golden(name)
+    cls_ref, cls_name, kw = TB.HEADS[name]
+    m = getattr(hlhgat, cls_name)(**kw)
+    fill_params(m, int(g["seed"]))
+    m = m.to(cuda).train()
+    ops.clear_caches()
+    if "tsp" in name:
+        b = TB._product_batch(g, "", cuda, factored)
+        (out, _), taps = _run_tapped(lambda: m(b))
+    else:
+        datas = [TB._product_batch(g, "l0/", cuda, factored),
+                 TB._product_batch(g, "l1/", cuda, False)]
+        out, taps = _run_tapped(lambda: m(datas))
+    (out * T(g["R"]).to(cuda)).sum().backward()
+    ref64 = getattr(R, cls_ref)(**kw)
+    fill_params(ref64, int(g["seed"]))
+    ref64 = ref64.double().train()
+    masked = _freeze(ref64, m, taps)
+    if "tsp" in name:
+        out64, _ = ref64(TB._data(g, "", torch.float64))
+    else:
+        out64 = ref64([TB._data(g, "l0/", torch.float64), TB._data(g, "l1/", torch.float64)])
+    close(out.detach().cpu(), out64.detach(), 1e-4, "out vs fp64 oracle (frozen masks)")
+    (out64 * T(g["R"]).double()).sum().backward()
+    _check(f"{name}{'_factored' if factored else ''}", m, ref64, masked)
+    ops.check_device_errors()

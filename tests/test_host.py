@@ -515,3 +515,79 @@ def test_native_mlgc_rejects_bad_input():
         hd.graclus(np.array([[0, 5], [1, 0]]), 3)
     with pytest.raises(HlhgatError, match="out of range"):
         hd.mlgc_map(np.array([0, 0, 7]), np.array([[0], [1]]))
+
+
+# ---------------------------------------------------------------------------
+# native loader: PackedGraphs.collate (hlhgat_collate) == collate + pad_batch
+# ---------------------------------------------------------------------------
+def _same_batch(a, b):
+    ta = {k for k, v in vars(a).items() if torch.is_tensor(v)}
+    tb = {k for k, v in vars(b).items() if torch.is_tensor(v)}
+    assert ta == tb, (sorted(ta - tb), sorted(tb - ta))
+    for k in ta:
+        x, y = getattr(a, k), getattr(b, k)
+        assert x.dtype == y.dtype and x.shape == y.shape and torch.equal(x, y), k
+    for k in ("num_graphs", "num_nodes", "hodge_sorted", "l1_factor"):
+        assert getattr(a, k) == getattr(b, k), k
+
+
+def test_native_collate_equals_python_collate_and_pad():
+    """hlhgat_collate (csrc/collate.hip) builds, bitwise, every array of
+    hodge_dataset.collate (unpadded) and of collate + pad_batch (padded):
+    features, offset COO blocks, B1 edge list, y, graph sizes, the Laplacian
+    / incidence CSRs, degrees, segment offsets and the padding."""
+    import numpy as np
+    from hlhgat.hodge_dataset import PackedGraphs, collate, pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_graph
+    gs = [zinc_like_graph(5000 + i, keig=15) for i in range(160)]
+    ds = PackedGraphs(gs)
+    for idx in (np.arange(37), np.random.RandomState(3).permutation(160)[:101], np.array([7])):
+        ref = collate([gs[i] for i in idx], check_hodge=False)
+        _same_batch(ds.collate(idx), ref)
+        assert ds.sizes(idx) == (ref.x_t.shape[0], ref.x_s.shape[0], ref.edge_index_t.shape[1],
+                                 ref.edge_index_s.shape[1])
+        for q in (64, 512):
+            caps = static_caps(ref, q)
+            assert ds.caps_for(idx, q) == caps
+            _same_batch(ds.collate(idx, caps), pad_batch(ref, caps))
+
+
+def test_native_collate_rejects_bad_input():
+    import numpy as np
+    import pytest
+    from hlhgat._lib import HlhgatError
+    from hlhgat.hodge_dataset import PackedGraphs
+    from hlhgat.synthetic import zinc_like_graph
+    ds = PackedGraphs([zinc_like_graph(i, keig=15) for i in range(4)])
+    with pytest.raises(HlhgatError, match="out of range"):
+        ds.collate(np.array([0, 4]))
+    caps = ds.caps_for(np.arange(4), 64)
+    with pytest.raises(ValueError):
+        ds.collate(np.arange(4), dict(caps, rows_t=10))
+    g = zinc_like_graph(9, keig=15)
+    g.edge_index_t = g.edge_index_t.flip(1)  # not row-sorted
+    with pytest.raises(ValueError, match="row-sorted"):
+        PackedGraphs([g])
+
+
+def test_graph_loader_batches_in_order_and_shuffled():
+    """GraphLoader: native collation on worker threads, batches in order;
+    one capacity bucket per epoch; a shuffled epoch covers every graph once."""
+    import numpy as np
+    from hlhgat.hodge_dataset import PackedGraphs, collate, pad_batch
+    from hlhgat.loader import GraphLoader
+    from hlhgat.synthetic import zinc_like_graph
+    gs = [zinc_like_graph(7000 + i, keig=15) for i in range(90)]
+    ds = PackedGraphs(gs)
+    ld = GraphLoader(ds, 20, workers=3, prefetch=2)
+    got = list(ld)
+    assert len(got) == len(ld) == 4
+    caps = ld.epoch_caps(ld.batch_indices(0))
+    for i, b in enumerate(got):
+        _same_batch(b, pad_batch(collate(gs[20 * i:20 * i + 20], check_hodge=False), caps))
+    sh = GraphLoader(ds, 30, shuffle=True, caps=False, seed=5)
+    seen = np.concatenate(sh.batch_indices(0))
+    assert sorted(seen.tolist()) == list(range(90))
+    assert not np.array_equal(seen, np.arange(90))
+    b0 = next(iter(sh))
+    _same_batch(b0, collate([gs[i] for i in sh.batch_indices(0)[0]], check_hodge=False))
