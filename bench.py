@@ -53,7 +53,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_batches(n_batches, rank, device, quantum=512):
+def make_batches(n_batches, rank, device, quantum=512, caps=None):
     """n_batches distinct synthetic 1000-graph batches, padded to ONE capacity
     bucket (the max of their static_caps) so that a single captured hipGraph
     replays every one of them -- as a training loop pads its DataLoader
@@ -68,8 +68,9 @@ def make_batches(n_batches, rank, device, quantum=512):
               for i in range(n_batches) for j in range(GRAPHS_PER_GPU)]
     ds = PackedGraphs(graphs, check_hodge=False)
     idxs = [np.arange(i * GRAPHS_PER_GPU, (i + 1) * GRAPHS_PER_GPU) for i in range(n_batches)]
-    cs = [ds.caps_for(i, quantum) for i in idxs]
-    caps = {k: max(c[k] for c in cs) for k in cs[0]}
+    if caps is None:
+        cs = [ds.caps_for(i, quantum) for i in idxs]
+        caps = {k: max(c[k] for c in cs) for k in cs[0]}
     real = sum(sum(ds.sizes(i)[:2]) for i in idxs) / n_batches
     return [ds.collate(i, caps).to(device) for i in idxs], caps, real, ds.collate(idxs[0]), ds
 
@@ -144,6 +145,128 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16):
                                  "the step, copy-in + replayed step"}
     out["device_resident_ms_per_step"] = round(ms_step, 3)
     return out
+
+
+# kernel classes of the replayed step whose rooflines the bench reports
+# (name regex in the rocprofv3 trace, hlhgat_prof class, bound)
+REPLAY_CLASSES = {
+    "k_poly_step": (r"k_poly_step<", "PROF_POLY", "hbm"),
+    "k_proj_bwd_fused": (r"k_proj_bwd_fused<", "PROF_PROJ_BWD", "mfma"),
+    "k_proj_fwd": (r"k_proj_fwd", "PROF_PROJ", "mfma"),
+    "k_bn_fwd_grid": (r"k_bn_fwd_grid<", "PROF_BN_FWD", "hbm"),
+    "k_bn_bwd_reduce": (r"k_bn_bwd_reduce<", "PROF_BN_BWD", "hbm"),
+}
+
+
+def replay_probe(args):
+    """Child mode (--replay-probe, run under rocprofv3 by replay_census): the
+    timed workload's replayed step -- same model, same capacity bucket, two
+    of the batches -- warmed up, captured, then replayed; nothing else."""
+    from hlhgat.distributed import init_distributed
+    import hlhgat
+    from hlhgat.train import TrainStep
+    caps = json.loads(args.replay_probe)
+    _, _, device = init_distributed("nccl")
+    batches, _, _, _, _ = make_batches(2, 0, device, caps=caps)
+    torch.manual_seed(0)
+    model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**MODEL_KW).to(device).train()
+    crit = hlhgat.nn.L1Loss()
+    step = TrainStep(model, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                     weight_decay=1e-3, graphs=True)
+    for i in range(args.warmup + args.steps):
+        step(batches[i % 2])
+    torch.cuda.synchronize()
+    assert step.stats["replay"] >= args.steps, step.stats
+
+
+def replay_census(caps, eager, steps=12, warmup=4, timeout=300):
+    """Kernel durations INSIDE the replayed training step: this script's
+    --replay-probe child under `rocprofv3 --kernel-trace` (a child process,
+    started after this process's own GPU work; no exec).  Per replayed step
+    (delimited by the Adam kernel): dispatches, span, the union of busy time
+    over all queues (idle = span - busy), and per kernel class the summed
+    duration.  `eager`: the algorithmic bytes / flops per step of each class
+    from the stamped eager pass (same launches), so achieved = work per step
+    / replayed kernel time per step."""
+    import csv
+    import re
+    import shutil
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="hlhgat_replay_")
+    cmd = [rp, "--kernel-trace", "-d", d, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--replay-probe", json.dumps(caps),
+           "--steps", str(steps), "--warmup", str(warmup)]
+    try:
+        r = subprocess.run(cmd, timeout=timeout, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, env=dict(os.environ, TMPDIR="/tmp"))
+        if r.returncode != 0:
+            return None, f"replay probe exited {r.returncode}: {r.stderr.decode()[-300:]}"
+        traces = [os.path.join(root, f) for root, _, fs in os.walk(d) for f in fs
+                  if f.endswith("kernel_trace.csv")]
+        if not traces:
+            return None, "no kernel trace written"
+        rows = sorted(csv.DictReader(open(traces[0])), key=lambda x: int(x["Start_Timestamp"]))
+    except (OSError, subprocess.SubprocessError) as e:
+        return None, f"replay probe failed: {e}"
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    marks = [i for i, x in enumerate(rows) if "k_adam_flat" in x["Kernel_Name"]]
+    if len(marks) < steps:
+        return None, f"only {len(marks)} steps in the trace"
+    sel = list(zip(marks[-steps:-1], marks[-steps + 1:]))  # the last steps-1 full replays
+    per = {k: [0.0, 0] for k in REPLAY_CLASSES}
+    spans, busys, disp = [], [], []
+    for a, b in sel:
+        st = rows[a + 1:b + 1]
+        iv = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in st)
+        span = iv[-1][1] - iv[0][0] if iv else 0
+        busy, cur_s, cur_e = 0, None, None
+        for s0, e0 in iv:
+            if cur_e is None or s0 > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s0, e0
+            else:
+                cur_e = max(cur_e, e0)
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        spans.append(span)
+        busys.append(busy)
+        disp.append(len(st))
+        for x in st:
+            for k, (pat, _, _) in REPLAY_CLASSES.items():
+                if re.search(pat, x["Kernel_Name"]):
+                    per[k][0] += (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3
+                    per[k][1] += 1
+    n = len(sel)
+    span_us = sum(spans) / n / 1e3
+    busy_us = sum(busys) / n / 1e3
+    out = {"steps_traced": n, "dispatches_per_step": round(sum(disp) / n, 1),
+           "span_us": round(span_us, 1), "busy_us": round(busy_us, 1),
+           "idle_us": round(span_us - busy_us, 1),
+           "idle_frac": round((span_us - busy_us) / span_us, 4) if span_us else None,
+           "kernels": {}}
+    for k, (pat, cls, bound) in REPLAY_CLASSES.items():
+        us, cnt = per[k][0] / n, per[k][1] / n
+        e = eager.get(k)
+        if not cnt or not e:
+            continue
+        work = e["flops"] if bound == "mfma" else e["bytes"]  # per step
+        if bound == "mfma":
+            ach, peak, unit = work / (us * 1e-6) / 1e12, FP32_MFMA_PEAK_TFS, "TFLOP/s"
+        else:
+            ach, peak, unit = work / (us * 1e-6) / 1e9, HBM_PEAK_GBS, "GB/s"
+        out["kernels"][k] = {"bound": bound, "achieved": round(ach, 2), "peak": peak,
+                             "unit": unit, "frac": round(ach / peak, 4),
+                             "launches_per_step": round(cnt, 1),
+                             "avg_launch_us": round(us / cnt, 2),
+                             "time_per_step_us": round(us, 1),
+                             "work_per_step": round(work),
+                             "eager_launches_per_step": e["launches"]}
+    return out, None
 
 
 def parity_check(model, batch_dev, batch_cpu, tol=1e-4):
@@ -385,76 +508,142 @@ HEADS = {
 }
 
 
-def _head_batch(kind, graphs, seed):
-    from hlhgat.hodge_dataset import collate
-    from hlhgat.synthetic import tsp_like_graph, two_level_batch
+def _head_pool(kind, n, seed=0):
+    """A pool of n host graphs (PairData, or MLGC level pairs for the attpool
+    heads) of the head's generator; batches are drawn from it."""
+    from hlhgat.synthetic import cifar_like_graphs, peptides_like_graphs, tsp_like_graph
     if kind == "tsp":
-        return collate([tsp_like_graph(seed * graphs + i) for i in range(graphs)],
-                       check_hodge=False)
-    return two_level_batch(kind, graphs, seed=seed)
+        return [tsp_like_graph(seed * 1000 + i) for i in range(n)]
+    make = {"cifar": cifar_like_graphs, "peptides": peptides_like_graphs}[kind]
+    return [make(seed * 1_000_003 + i) for i in range(n)]
+
+
+def _head_collate(kind, items):
+    from hlhgat.hodge_dataset import collate
+    if kind == "tsp":
+        return collate(items, check_hodge=False)
+    return [collate([p[0] for p in items], check_hodge=False),
+            collate([p[1] for p in items], check_hodge=False)]
+
+
+def _head_batch(kind, graphs, seed):
+    """One unpadded batch of `graphs` fresh graphs (the CPU-oracle sample)."""
+    return _head_collate(kind, _head_pool(kind, graphs, seed))
 
 
 def _head_loss(kind, out, datas):
     F = torch.nn.functional
-    if kind == "tsp":  # main_TSP...:316-321 (BCE on the masked edge logits)
-        return F.binary_cross_entropy_with_logits(out[0].view(-1), datas.y.view(-1).float())
+    if kind == "tsp":  # main_TSP...:316-321 (BCE on the masked edge logits), mean over
+        # the batch's real edges (padding edges carry a zero mask and label)
+        return F.binary_cross_entropy_with_logits(
+            out[0].view(-1), datas.y.view(-1).float(), reduction="sum") / datas.num_edge1.sum()
     y = datas[0].y
     if kind == "cifar":  # main_cifar10SP: cross entropy
         return F.cross_entropy(out, y.view(-1).long())
     return F.binary_cross_entropy_with_logits(out, y.view(out.shape).float())  # pepfunc
 
 
-def heads_leg(device, steps=6, warmup=2, cpu_budget_s=8.0):
+HEAD_PROF = (("k_poly_step", "PROF_POLY", "hbm"), ("hodge_node (factored L1, B1 X)",
+             "PROF_HODGE_NODE", "hbm"), ("hodge_edge (factored L1 edge step)", "PROF_HODGE_EDGE",
+             "hbm"), ("k_proj_fwd", "PROF_PROJ", "mfma"), ("k_proj_bwd_fused", "PROF_PROJ_BWD",
+             "mfma"), ("k_bn_fwd_grid", "PROF_BN_FWD", "hbm"), ("k_bn_bwd_reduce",
+             "PROF_BN_BWD", "hbm"))
+
+
+def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
     """BASELINE configs[2..4] on this GPU: graphs/s of a full training step
-    (fwd + loss + bwd + Adam, hlhgat.train.TrainStep replaying a hipGraph per
-    batch shape, and eager beside it) at the per-GPU batch of SURVEY §8d, and the CPU
-    oracle (the same head restated in oracle/hodge_ref.py) timed on a bounded
-    sample of the same data on the host cores."""
+    (fwd + loss + bwd + Adam) at the per-GPU batch of SURVEY §8d.  n_batches
+    DISTINCT batches (random draws from a pool of graphs) padded to ONE
+    capacity bucket (hodge_dataset.pad_levels / pad_batch), so
+    hlhgat.train.TrainStep captures one hipGraph and replays it for every
+    batch -- as a loader padding to the dataset's bucket would; the eager
+    step beside it.  Per head: the padding overhead, a kernel roofline
+    breakdown from an event-stamped eager step, and the CPU oracle (the same
+    head restated in oracle/hodge_ref.py) on a bounded sample."""
+    import numpy as np
     import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import level_caps, pad_batch, pad_levels, static_caps
     from hlhgat.train import TrainStep
     from oracle import hodge_ref as R
+    L = hlhgat._lib
     out = {}
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     for name, c in HEADS.items():
+        kind, G = c["kind"], c["graphs"]
         t0 = time.perf_counter()
-        raw = [_head_batch(c["kind"], c["graphs"], s) for s in range(2)]
+        pool = _head_pool(kind, 2 * G)
+        rng = np.random.RandomState(7)
+        raw = [_head_collate(kind, [pool[i] for i in rng.choice(len(pool), G, replace=False)])
+               for _ in range(n_batches)]
+        if kind == "tsp":
+            cs = [static_caps(b, 512) for b in raw]
+            caps = {k: max(x[k] for x in cs) for k in cs[0]}
+            padded = [pad_batch(b, caps) for b in raw]
+            rows = lambda b: b.x_t.size(0) + b.x_s.size(0)  # noqa: E731
+        else:
+            caps = level_caps(raw, 512)
+            padded = [pad_levels(b, caps) for b in raw]
+            rows = lambda bl: sum(b.x_t.size(0) + b.x_s.size(0) for b in bl)  # noqa: E731
+        overhead = sum(rows(p) for p in padded) / sum(rows(b) for b in raw) - 1
         gen_s = time.perf_counter() - t0
-        batches = [b.to(device) if c["kind"] == "tsp" else [x.to(device) for x in b] for b in raw]
-        dts = {}
+        dev = lambda b: b.to(device) if kind == "tsp" else [x.to(device) for x in b]  # noqa: E731
+        batches = [dev(b) for b in padded]
+        dts, stats = {}, {}
         for graphs in (False, True):
             torch.manual_seed(0)
             m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
-            st = TrainStep(m, lambda o, d, k=c["kind"]: _head_loss(k, o, d), lr=1e-3,
-                           graphs=graphs)
-            for i in range(warmup):  # graphs: one eager step + capture per batch shape
-                st(batches[i % 2])
+            st = TrainStep(m, lambda o, d, k=kind: _head_loss(k, o, d), lr=1e-3, graphs=graphs)
+            for i in range(warmup):  # graphs: one eager step + the capture
+                st(batches[i % n_batches])
             torch.cuda.synchronize()
-            t0 = time.perf_counter()
+            t1 = time.perf_counter()
             for i in range(steps):
-                st(batches[i % 2])
+                st(batches[(warmup + i) % n_batches])
             torch.cuda.synchronize()
-            dts[graphs] = (time.perf_counter() - t0) / steps
+            dts[graphs] = (time.perf_counter() - t1) / steps
+            stats[graphs] = dict(st.stats)
             if graphs:
-                assert st.stats["replay"] == steps, st.stats
+                assert st.stats["captures"] == 1 and st.stats["replay"] == steps, st.stats
+                # kernel breakdown: one event-stamped eager step of the same model
+                ops.prof_reset()
+                for _, cls, _ in HEAD_PROF:
+                    ops.prof_enable(getattr(L, cls), True)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                st._eager(batches[0])
+                torch.cuda.synchronize()
+                eager_ms = (time.perf_counter() - t2) * 1e3
+                for _, cls, _ in HEAD_PROF:
+                    ops.prof_enable(getattr(L, cls), False)
+                brk = {}
+                for nm, cls, bound in HEAD_PROF:
+                    kr = kernel_roofline(ops.prof_read(getattr(L, cls)), bound, "")
+                    if kr:
+                        kr.pop("what")
+                        kr["ms_per_step"] = round(kr["avg_launch_us"] * kr["launches"] / 1e3, 3)
+                        brk[nm] = kr
             del m, st
         dt = dts[True]
-        r = {"value": round(c["graphs"] / dt, 1), "unit": "graphs/s", "ms_per_step": round(dt * 1e3, 2),
-             "graphs_per_step": c["graphs"], "steps": steps, "head": c["cls"], "model": c["kw"],
-             "step": "fwd + loss + bwd + Adam, TrainStep replaying one hipGraph per batch shape "
-                     "(2 synthetic batches alternating; a loader with varying shapes pays one "
-                     "eager step + capture per new shape, see eager_*)",
+        r = {"value": round(G / dt, 1), "unit": "graphs/s", "ms_per_step": round(dt * 1e3, 2),
+             "graphs_per_step": G, "steps": steps, "head": c["cls"], "model": c["kw"],
+             "step": f"fwd + loss + bwd + Adam; {n_batches} distinct batches padded to one "
+                     f"capacity bucket, ONE captured hipGraph replayed for all of them",
+             "captures": stats[True]["captures"], "padding_overhead": round(overhead, 4),
+             "caps": caps,
              "eager_ms_per_step": round(dts[False] * 1e3, 2),
-             "eager_value": round(c["graphs"] / dts[False], 1), "data_gen_s": round(gen_s, 1)}
-        # CPU oracle on a bounded sample: the first cpu_graphs graphs of a batch
+             "eager_value": round(G / dts[False], 1), "data_gen_s": round(gen_s, 1),
+             "kernels_eager_step": {"ms": round(eager_ms, 2), "classes": brk}}
+        # CPU oracle on a bounded sample: cpu_graphs fresh graphs
         torch.set_num_threads(cores)
-        sb = _head_batch(c["kind"], c["cpu_graphs"], 0)
+        sb = _head_batch(kind, c["cpu_graphs"], 0)
         torch.manual_seed(0)
         mr = getattr(R, c["ref"])(**c["kw"]).train()
         opt = torch.optim.Adam(mr.parameters(), lr=1e-3)
 
         def cpu_step():
             o = mr(sb)
-            _head_loss(c["kind"], o, sb).backward()
+            _head_loss(kind, o, sb).backward()
             opt.step()
             opt.zero_grad()
         times, t_start = [], time.perf_counter()
@@ -470,7 +659,8 @@ def heads_leg(device, steps=6, warmup=2, cpu_budget_s=8.0):
                              "sample": f"{len(times)} oracle training steps on {c['cpu_graphs']} "
                                        f"graph(s) of the same generator, median {med * 1e3:.0f} ms"}
         out[name] = r
-        log(f"[heads] {name}: {r['value']} graphs/s (CPU oracle {r['cpu_baseline']['value']})")
+        log(f"[heads] {name}: {r['value']} graphs/s replayed, {r['eager_value']} eager, "
+            f"padding {overhead:.1%} (CPU oracle {r['cpu_baseline']['value']})")
         del batches
         torch.cuda.empty_cache()
     return out
@@ -571,6 +761,9 @@ def main():
                     help="skip the configs 3-5 heads (graphs/s + CPU oracle baseline each)")
     ap.add_argument("--prof-steps", type=int, default=3,
                     help="eager steps with kernel event stamps for the roofline")
+    ap.add_argument("--replay-probe", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--no-replay-census", action="store_true",
+                    help="rooflines from the eager stamped pass only (no rocprofv3 child)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / timing contract on gloo + CPU, no model")
     args = ap.parse_args()
@@ -581,6 +774,8 @@ def main():
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.dry_run:
         return dry_run(args)
+    if args.replay_probe:
+        return replay_probe(args)
 
     from hlhgat.distributed import init_distributed, max_over_ranks
     rank, world, device = init_distributed("nccl")  # RCCL over xGMI; one process per GPU
@@ -692,6 +887,8 @@ def main():
         "cpu_baseline": None,
         "parity_check": pcheck,
         "rooflines": {k: kernel_roofline(ops.prof_read(c), bound, note) for k, c, bound, note in (
+            ("k_proj_fwd", L.PROF_PROJ, "mfma",
+             "projection forward (fp32 MFMA, W staged in LDS); flops 2 M N sum K"),
             ("k_proj_bwd_fused", L.PROF_PROJ_BWD, "mfma",
              "Linear backward: weight-gradient split partials + data gradient, one launch; "
              "flops 2 M N (sum K_w + sum K_d)"),
@@ -704,8 +901,44 @@ def main():
         "h2d": None,
         "loader": None,
     }
+    result_eager_rooflines = dict(result["rooflines"])
     if rank == 0:
         roofline["isolated"] = isolated_poly_step(device, batches[0])
+    if rank == 0 and world == 1 and not args.eager and not args.no_replay_census:
+        # rooflines of the REPLAYED step: kernel time per step from a rocprofv3
+        # trace of the replayed workload, work per step from the stamped pass
+        eager_work = {}
+        for k, (_, cls, _) in REPLAY_CLASSES.items():
+            p = ops.prof_read(getattr(L, cls))
+            if p["launches"]:
+                eager_work[k] = {"bytes": p["bytes"] / args.prof_steps,
+                                 "flops": p["flops"] / args.prof_steps,
+                                 "launches": p["launches"] / args.prof_steps}
+        log("[rank 0] replay census (rocprofv3 child)")
+        census, why = replay_census(caps, eager_work)
+        if census is None:
+            log(f"[rank 0] replay census unavailable: {why}")
+            result["step_census"] = {"unavailable": why}
+        else:
+            kc = census.pop("kernels")
+            result["step_census"] = census
+            kp = kc.get("k_poly_step")
+            if kp:
+                eager_fig = {k: roofline[k] for k in ("achieved", "frac", "avg_launch_us",
+                                                      "launches", "measured")}
+                roofline.update(achieved=kp["achieved"], frac=kp["frac"],
+                                avg_launch_us=kp["avg_launch_us"],
+                                launches=kp["launches_per_step"],
+                                algorithmic_bytes_per_launch=round(
+                                    kp["work_per_step"] / kp["launches_per_step"]),
+                                measured="kernel durations inside the replayed step "
+                                         "(rocprofv3 --kernel-trace of the same workload, "
+                                         f"{census['steps_traced']} replays), algorithmic "
+                                         "bytes per step from the stamped eager pass")
+                roofline["eager"] = eager_fig
+            result["rooflines"] = {k: dict(v, what=(result["rooflines"].get(k) or {}).get(
+                "what", "")) for k, v in kc.items() if k != "k_poly_step"}
+            result["rooflines_eager"] = {k: v for k, v in result_eager_rooflines.items()}
     if rank == 0 and world == 1 and not args.no_cfg5:
         log("[rank 0] config-5 SpMM roofline")
         result["spmm_cfg5"] = cfg5_spmm(device)

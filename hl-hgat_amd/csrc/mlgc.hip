@@ -24,12 +24,15 @@ inline uint64_t pair_key(int64_t lo, int64_t hi) {
 
 }  // namespace
 
-// Greedy graclus matching (torch_cluster 1.6.0 graclus_cluster, called at
-// lib/Hodge_Dataset.py:252 and :311): self-loops dropped, every node's
-// neighbours in ascending column order, nodes visited in perm order; an
-// unmatched node takes its unmatched neighbour of strictly largest weight
-// (> 0; the first one on ties) and both get id min(u, v); otherwise it stays
-// alone with id u.
+// Greedy graclus matching (torch_cluster 1.6.0 graclus_cluster, its weighted
+// branch -- the reference always passes a weight, ones_like for MLGC --
+// called at lib/Hodge_Dataset.py:252 and :311): self-loops dropped, every
+// node's neighbours in ascending column order, nodes visited in perm order;
+// an unmatched node u keeps the LAST unmatched neighbour whose weight is >=
+// the best so far (best starts at 0, so zero weights match) and both get id
+// min(u, v); with no unmatched neighbour u stays alone with id u.  Restated
+// from torch_cluster's published graclus_cpu (not in the reference tree):
+// parity unpinned.
 extern "C" int hlhgat_graclus(const int64_t* edge_index, const double* weight, int64_t n_edges,
                               int64_t n_nodes, const int64_t* perm, int64_t* cluster) {
   HLH_CHECK_ARG(n_edges >= 0 && n_nodes >= 0, "graclus: bad sizes");
@@ -71,16 +74,17 @@ extern "C" int hlhgat_graclus(const int64_t* edge_index, const double* weight, i
     const int64_t u = perm[i];
     HLH_CHECK_ARG(u >= 0 && u < n_nodes, "graclus: perm[%lld] out of range", (long long)i);
     if (cluster[u] >= 0) continue;
-    cluster[u] = u;
-    int64_t best = -1;
+    int64_t best = u;
     double wbest = 0.0;
     for (int64_t p = deg[(size_t)u]; p < deg[(size_t)u + 1]; ++p) {
       const int64_t v = nb[(size_t)p];
-      if (cluster[v] >= 0 || !(nw[(size_t)p] > wbest)) continue;
-      best = v;
-      wbest = nw[(size_t)p];
+      if (cluster[v] >= 0) continue;
+      if (nw[(size_t)p] >= wbest) {  // ties: the LAST such neighbour
+        best = v;
+        wbest = nw[(size_t)p];
+      }
     }
-    if (best >= 0) cluster[u] = cluster[best] = std::min(u, best);
+    cluster[u] = cluster[best] = std::min(u, best);
   }
   return HLHGAT_OK;
 }

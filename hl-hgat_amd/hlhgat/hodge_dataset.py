@@ -21,7 +21,7 @@ import torch
 
 __all__ = ["PairData", "Batch", "collate", "adj2par1", "BoundaryOperator", "degree",
            "hodge_laplacians", "dense_to_sparse", "is_sorted_symmetric", "locality_order",
-           "static_caps", "pad_batch", "PackedGraphs", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
+           "static_caps", "pad_batch", "level_caps", "pad_levels", "PackedGraphs", "halo_tiles", "graclus", "mlgc", "mlgc_weighted", "mlgc_map", "to_undirected_mean",
            "hodge_factor_ok", "hodge_coo_from_boundary"]
 
 _INC_KEYS = ("edge_index_s", "edge_index_t", "edge_index", "row_order_s", "row_order_t")
@@ -469,6 +469,37 @@ def static_caps(b: "Batch", quantum: int = 512) -> Dict[str, int]:
     return caps
 
 
+def level_caps(levels: Sequence[Sequence["Batch"]], quantum: int = 512) -> List[Dict[str, int]]:
+    """static_caps per MLGC level, the max over several level-batch lists
+    (the attpool heads' `datas`): one capacity bucket for all of them."""
+    out = []
+    for lv in zip(*levels):
+        cs = [static_caps(b, quantum) for b in lv]
+        out.append({k: max(c[k] for c in cs) for k in cs[0]})
+    return out
+
+
+def pad_levels(datas: Sequence["Batch"], caps: Sequence[Dict[str, int]]) -> List["Batch"]:
+    """Static-shape copy of an attpool level-batch list (datas = [fine level
+    with the MLGC cluster of each node / edge in feature column 0, coarse
+    level], lib/Hodge_ST_Model.py:1029-1038, main_pepfunc...:111-118): every
+    level padded by pad_batch to its caps, and the fine level's padding rows
+    put in NO cluster -- their column 0 (the cluster id the heads add the
+    graph offsets to) is inf, so cluster_mean drops them as it drops the edges
+    MLGC removed (lib/Hodge_ST_Model.py:1067-1069).  Real rows, the pooled
+    features and every gradient equal the unpadded list's
+    (tests/test_train_step.py)."""
+    if len(datas) != len(caps):
+        raise ValueError("pad_levels: one caps dict per level")
+    out = [pad_batch(b, c) for b, c in zip(datas, caps)]
+    p0, b0 = out[0], datas[0]
+    for key in ("x_t", "x_s"):
+        x = getattr(p0, key).clone()
+        x[getattr(b0, key).size(0):, 0] = float("inf")
+        setattr(p0, key, x)
+    return out
+
+
 def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     """Static-shape copy of a collated host batch (hlhgat.train replays one
     hipGraph for every batch of the same caps).
@@ -491,7 +522,14 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     out = Batch()
     for k, v in vars(b).items():
         setattr(out, k, v)
-    out.l1_factor = False  # padding edges are B1 self-loops: no alpha B1^T B1 identity
+    # Factored L1 (alpha_e B1^T B1) stays valid: a padding edge is a B1
+    # self-edge, a zero column of B1, and its L1 row holds only zero-weight
+    # self-loops, so alpha_e = 0 -- its row of alpha B1^T B1 is zero like its CSR
+    # row, and the real edges' incidence never reaches the padding nodes.
+    out.l1_factor = getattr(b, "l1_factor", False)
+    for k in list(vars(out)):
+        if k.startswith(tuple(_HALO_KEYS)) or k.startswith("halo_bounds"):
+            delattr(out, k)  # halo tiles describe the unpadded CSR: plain schedule here
 
     def pad_rows(x, R):
         return torch.cat([x, x.new_zeros((R - x.size(0),) + tuple(x.shape[1:]))], 0)
@@ -506,6 +544,13 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
                 torch.cat([w, w.new_zeros(extra)]), per_row)
 
     out.x_t, out.x_s = pad_rows(b.x_t, Rt), pad_rows(b.x_s, Rs)
+    y = getattr(b, "y", None)
+    if torch.is_tensor(y) and y.dim() >= 1 and getattr(b, "num_graphs", None) != y.size(0):
+        # per-simplex labels (TSP: one per edge, main_TSP...:316-321): zero rows
+        if y.size(0) == ns:
+            out.y = pad_rows(y, Rs)
+        elif y.size(0) == nt:
+            out.y = pad_rows(y, Rt)
     out.edge_index_t, out.edge_weight_t, _ = pad_coo(b.edge_index_t, b.edge_weight_t, nt, Rt,
                                                         caps["nnz_t"])
     out.edge_index_s, out.edge_weight_s, _ = pad_coo(b.edge_index_s, b.edge_weight_s, ns, Rs,
@@ -937,9 +982,11 @@ def graclus(edge_index, n: int, weight=None, seed: int = 0) -> np.ndarray:
     :311), run by the library's native host builder (hlhgat_graclus):
     self-loops dropped, nodes visited in a random order (torch_cluster draws
     a torch.randperm; here a seeded numpy permutation), each unmatched node
-    paired with its unmatched neighbour of largest weight (first in ascending
-    neighbour order on ties; unweighted = all ones), both get cluster id
-    min(u, v); a node with no unmatched neighbour stays alone (id u).
+    paired with the LAST of its unmatched neighbours (ascending column order)
+    whose weight is >= the best so far, from 0 -- torch_cluster's weighted
+    branch, which the reference always takes (MLGC passes ones_like) -- both
+    get cluster id min(u, v); a node with no unmatched neighbour stays alone
+    (id u).  Parity unpinned (no torch_cluster output exists here).
     Returns int64 [n] cluster ids."""
     from ._lib import LIB, check
     ei = np.ascontiguousarray(np.asarray(edge_index, dtype=np.int64).reshape(2, -1))

@@ -218,8 +218,8 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
     def forward(self, data, device="cuda:0"):
         dev = data.x_s.device
         # output_size given: no host sync (the step can be captured)
-        s_batch = torch.repeat_interleave(torch.arange(data.num_edge1.numel(), device=dev),
-                                          data.num_edge1.to(dev), output_size=data.x_s.size(0))
+        s_batch = _per_row(torch.arange(data.num_edge1.numel(), device=dev), data.num_edge1,
+                           data.x_s.size(0), fill=data.num_edge1.numel())  # padding: no graph
         x_s, edge_index_s, edge_weight_s = data.x_s[:, :1], data.edge_index_s, data.edge_weight_s
         edge_mask = data.x_s[:, 1:]
         x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
@@ -264,14 +264,35 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch
 
 
+def _per_row(vals: torch.Tensor, counts: torch.Tensor, rows: int, fill=0) -> torch.Tensor:
+    """repeat_interleave(vals, counts) over `rows` rows without a host sync:
+    rows beyond sum(counts) (static-shape padding rows, in no graph) get
+    `fill` -- the count of that tail is computed on the device, so the output
+    is fully written whatever the padding (never an uninitialised tail)."""
+    dev = vals.device
+    counts = counts.to(dev).to(torch.int64)
+    tail = (rows - counts.sum()).clamp(min=0).reshape(1)
+    v = torch.cat([vals, torch.full((1,), fill, dtype=vals.dtype, device=dev)])
+    return torch.repeat_interleave(v, torch.cat([counts, tail]), output_size=rows)
+
+
 def _level_offsets(counts_next: torch.Tensor, counts: torch.Tensor, device,
                    rows: int) -> torch.Tensor:
     """n_ahead[n_batch] of the attpool heads (lib/Hodge_ST_Model.py:1031-1036):
     for every row of the fine level (`rows` of them: no host sync), the first
-    coarse row of its graph."""
+    coarse row of its graph; padding rows get 0 (their cluster id is inf)."""
     ahead = torch.zeros(counts_next.numel(), dtype=torch.float32, device=device)
     ahead[1:] = torch.cumsum(counts_next.to(device), 0)[:-1].to(torch.float32)
-    return torch.repeat_interleave(ahead, counts.to(device), output_size=rows)
+    return _per_row(ahead, counts, rows)
+
+
+def _valid_rows(x: torch.Tensor, n_valid) -> torch.Tensor:
+    """x with its static-shape padding rows (>= n_valid, a device int32 [1])
+    set to -inf, so a max over it is the max over the real rows."""
+    if n_valid is None:
+        return x
+    keep = torch.arange(x.size(0), device=x.device) < n_valid.to(x.device)
+    return x.masked_fill(~keep.view(-1, *([1] * (x.dim() - 1))), float("-inf"))
 
 
 class _AttPoolHead(nn.Module):
@@ -381,9 +402,11 @@ class _AttPoolHead(nn.Module):
             if i == self.pool_loc:
                 if not self.att_every_level:
                     att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t, x_s, par_1, D)
-                    # batch-global max (all ranks under data parallelism)
-                    att_t = att_t / global_max(att_t)
-                    att_s = att_s / global_max(att_s)
+                    # batch-global max (all ranks under data parallelism) over
+                    # the real rows (padding rows of a static-shape level excluded)
+                    dk = datas[k]
+                    att_t = att_t / global_max(_valid_rows(att_t, getattr(dk, "n_valid_t", None)))
+                    att_s = att_s / global_max(_valid_rows(att_s, getattr(dk, "n_valid_s", None)))
                     x_t = x_t * att_t
                     x_s = x_s * att_s
                 d1 = datas[k + 1]

@@ -152,9 +152,11 @@ int hlhgat_halo_tiles(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
  * over edge_index [2, n_edges] (row-major: rows then cols; self-loops
  * ignored; weight NULL = all ones) visiting nodes in perm order (the
  * reference draws torch.randperm; the caller passes its permutation), each
- * unmatched node paired with its unmatched neighbour of strictly largest
- * weight (first in ascending column order on ties); both get id min(u, v),
- * an unpaired node keeps id u.  cluster: [n_nodes] out. */
+ * unmatched node paired with the last of its unmatched neighbours (ascending
+ * column order) whose weight is >= the best so far, starting from 0 (the
+ * weighted branch of torch_cluster's graclus_cpu: ties to the last, zero
+ * weights match); both get id min(u, v), an unpaired node keeps id u.
+ * cluster: [n_nodes] out. */
 int hlhgat_graclus(const int64_t* edge_index, const double* weight, int64_t n_edges,
                    int64_t n_nodes, const int64_t* perm, int64_t* cluster);
 /* hlhgat_mlgc_map replaces the per-edge loop of MLGC (lib/Hodge_Dataset.py:

@@ -613,12 +613,16 @@ class RefSAPool(nn.Module):
 def graclus(edge_index, n: int, weight=None, perm=None) -> np.ndarray:
     """Greedy graclus matching, torch_cluster 1.6.0 graclus_cluster (the
     reference's dependency, absent here; called at lib/Hodge_Dataset.py:252
-    and :311): self-loops dropped, nodes visited in `perm` (the reference
-    draws torch.randperm), each unmatched node u paired with its unmatched
-    neighbour of strictly largest weight (first in ascending neighbour order
-    on ties; unweighted = all ones), both get id min(u, v); a node with no
-    unmatched neighbour keeps id u.  Parity unpinned (no fixture holds a
-    torch_cluster output).  Returns int64 [n]."""
+    and :311, both times WITH a weight -- ones_like for MLGC -- so its
+    weighted branch): self-loops dropped, neighbours in CSR order (row-sorted
+    COO, columns ascending), nodes visited in `perm` (the reference draws
+    torch.randperm); an unmatched node u scans its unmatched neighbours and
+    keeps the last one whose weight is >= the best so far (best starts at 0:
+    ties go to the LAST neighbour, zero weights match), then u and that
+    neighbour get id min(u, v); with no unmatched neighbour u keeps id u.
+    Restated from torch_cluster's published graclus_cpu; no copy of it is in
+    the reference tree and no fixture holds its output: parity unpinned.
+    Returns int64 [n]."""
     ei = np.asarray(edge_index)
     keep = ei[0] != ei[1]
     r, c = ei[0][keep], ei[1][keep]
@@ -631,15 +635,14 @@ def graclus(edge_index, n: int, weight=None, perm=None) -> np.ndarray:
     for u in (range(n) if perm is None else perm):
         if out[u] >= 0:
             continue
-        out[u] = u
-        best, wbest = -1, 0.0
+        best, wbest = u, 0.0
         for e in range(ptr[u], ptr[u + 1]):
             v = c[e]
-            if out[v] >= 0 or not w[e] > wbest:
+            if out[v] >= 0:
                 continue
-            best, wbest = v, w[e]
-        if best >= 0:
-            out[u] = out[best] = min(u, best)
+            if w[e] >= wbest:
+                best, wbest = v, w[e]
+        out[u] = out[best] = min(u, best)
     return out
 
 

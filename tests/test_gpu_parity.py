@@ -839,7 +839,8 @@ def _attpool_case(cuda, name, cls, **kw):
         if "nograd/" + k in g:
             assert p.grad is None or float(p.grad.abs().max()) == 0.0, k
             continue
-        if re.search(r"module_[04]\.bias$", k) or re.search(r"mlp\d+\.0\.bias$", k):
+        if re.search(r"module_[04]\.bias$", k) or re.search(r"mlp\d+\.0\.bias$", k) or \
+                re.search(r"WV_(Node|Edge)\.[03]\.bias$", k):
             # bias feeding a training-mode BatchNorm: analytically zero gradient
             assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
             continue

@@ -405,7 +405,15 @@ def test_hodge_factor_check():
     zb = collate([zinc_like_graph(s) for s in range(4)])
     assert not zb.l1_factor
     cb = collate([cifar_like_graphs(s)[0] for s in range(2)])
-    assert not pad_batch(cb, static_caps(cb)).l1_factor
+    # padding edges are zero columns of B1 with alpha_e = 0: the factor holds
+    # for the padded batch too (hodge_dataset.pad_batch)
+    pb = pad_batch(cb, static_caps(cb))
+    assert pb.l1_factor
+    ei, eis, w = pb.edge_index.numpy(), pb.edge_index_s.numpy(), pb.edge_weight_s.numpy()
+    ns, nt = cb.x_s.shape[0], cb.x_t.shape[0]
+    real = (eis[0] < ns) & (eis[1] < ns)
+    assert hodge_factor_ok(ei[:, :ns], nt, eis[:, real], w[real])
+    assert np.all(w[~real] == 0) and np.all(eis[0][~real] == eis[1][~real])
 
 
 def test_brain_skeleton_coo_rebuild_matches_reference():

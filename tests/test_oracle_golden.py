@@ -134,9 +134,10 @@ def _check_grads(m, g, tol=1e-4):
         if "nograd/" + k in g:
             assert p.grad is None, k
             continue
-        if re.search(r"module_[04]\.bias$", k) and not k.startswith("out."):
-            # a conv bias feeding a training-mode BatchNorm: analytically zero
-            # gradient, both sides hold fp32 rounding noise only
+        if (re.search(r"module_[04]\.bias$", k) and not k.startswith("out.")) or \
+                re.search(r"mlp\d+\.0\.bias$", k) or re.search(r"WV_(Node|Edge)\.[03]\.bias$", k):
+            # a conv / Linear bias feeding a training-mode BatchNorm: analytically
+            # zero gradient, both sides hold fp32 rounding noise only
             assert float(p.grad.abs().max()) < 1e-3 and float(np.abs(g["grad/" + k]).max()) < 1e-3
             continue
         close(p.grad, g["grad/" + k], tol, "grad " + k)

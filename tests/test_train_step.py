@@ -530,3 +530,111 @@ def test_attpool_rejects_pool_at_last_level(cuda):
         channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=1).to(cuda)
     with pytest.raises(RuntimeError, match="pool_loc=1 must be below the last"):
         m(b)
+
+
+# ---------------------------------------------------------------------------
+# GPU: static-shape level-batch lists (attpool heads) and TSP batches
+# ---------------------------------------------------------------------------
+def _head_case(kind):
+    """(raw host batches [3], model factory, loss) of a small config 3/4/5 head."""
+    import hlhgat
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import tsp_like_graph, two_level_batch
+    F = torch.nn.functional
+    if kind == "tsp":
+        raw = [collate([tsp_like_graph(s, n=300 + 40 * s, k=6)], check_hodge=False)
+               for s in (1, 2, 3)]
+        mk = lambda: hlhgat.HL_HGCNN_TSP_dense_int3_pyr(  # noqa: E731
+            channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3)
+        # BCE over the real edges (padding edges: zero mask, zero label; the
+        # mean taken over the real count so padding leaves the objective alone)
+        loss = lambda o, d: F.binary_cross_entropy_with_logits(  # noqa: E731
+            o[0].view(-1), d.y.view(-1).float(), weight=d.x_s[:, 1],
+            reduction="sum") / d.num_edge1.sum()
+        return raw, mk, loss
+    raw = [two_level_batch(kind, 5 + s, seed=s) for s in (1, 2, 3)]
+    if kind == "cifar":
+        mk = lambda: hlhgat.HL_HGCNN_CIFAR10SP_dense_int3_attpool(  # noqa: E731
+            channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10, pool_loc=0)
+        loss = lambda o, d: F.cross_entropy(o, d[0].y.view(-1).long())  # noqa: E731
+    else:
+        mk = lambda: hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool(  # noqa: E731
+            channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)
+        loss = lambda o, d: F.binary_cross_entropy_with_logits(  # noqa: E731
+            o, d[0].y.view(o.shape).float())
+    return raw, mk, loss
+
+
+def _pad_all(kind, raw, quantum=128):
+    from hlhgat.hodge_dataset import level_caps, pad_batch, pad_levels
+    if kind == "tsp":
+        caps = _caps_for(raw, quantum)
+        return [pad_batch(b, caps) for b in raw]
+    caps = level_caps(raw, quantum)
+    return [pad_levels(b, caps) for b in raw]
+
+
+def _dev(b, cuda):
+    return [x.to(cuda) for x in b] if isinstance(b, list) else b.to(cuda)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["peptides", "cifar", "tsp"])
+def test_padded_levels_match_unpadded(cuda, kind):
+    """Static-shape level-batch lists (hodge_dataset.pad_levels: padding rows
+    in no MLGC cluster, pos = inf) and padded TSP batches: the head's outputs,
+    every parameter gradient and the running statistics equal the unpadded
+    batch's (BN statistics, the attention's batch max and the readout over
+    real rows only)."""
+    raw, mk, loss = _head_case(kind)
+    padded = _pad_all(kind, raw)
+    res = []
+    for batch in (raw[0], padded[0]):
+        torch.manual_seed(0)
+        m = mk().to(cuda).train()
+        d = _dev(batch, cuda)
+        out = m(d)
+        o = out[0] if isinstance(out, tuple) else out
+        if kind == "tsp":  # per-edge logits: compare the real edges
+            o = o[:raw[0].x_s.size(0)]
+            loss(out, d).backward()
+        else:
+            loss(out, d).backward()
+        res.append((o.detach().cpu(), {k: p.grad.detach().cpu().clone()
+                                       for k, p in m.named_parameters() if p.grad is not None},
+                    {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+    (o0, g0, s0), (o1, g1, s1) = res
+    assert torch.allclose(o0, o1, rtol=1e-5, atol=1e-6), (o0 - o1).abs().max()
+    assert set(g0) == set(g1)
+    for k in g0:
+        scale = g0[k].abs().max().clamp_min(1e-6)
+        assert ((g0[k] - g1[k]).abs().max() / scale) < 1e-4, k
+        assert torch.isfinite(g1[k]).all(), k
+    for k in s0:
+        if s0[k].dtype.is_floating_point:
+            assert torch.allclose(s0[k], s1[k], rtol=1e-5, atol=1e-6), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["peptides", "cifar", "tsp"])
+def test_padded_levels_share_one_graph(cuda, kind):
+    """Three batches of different shapes padded to one bucket replay ONE
+    captured step (the level-batch copy-in loads each batch's data: losses
+    differ between batches), bitwise equal to eager steps."""
+    raw, mk, loss = _head_case(kind)
+    batches = [_dev(b, cuda) for b in _pad_all(kind, raw)]
+    order = [0, 1, 2, 1, 0, 2]
+    from hlhgat.train import TrainStep
+    res = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        m = mk().to(cuda).train()
+        st = TrainStep(m, loss, lr=1e-3, graphs=graphs)
+        ls = [float(st(batches[i]).detach()) for i in order]
+        res.append((ls, {k: v.detach().clone() for k, v in m.state_dict().items()}, st.stats))
+    (l_e, sd_e, _), (l_g, sd_g, stg) = res
+    assert stg["captures"] == 1 and stg["replay"] == len(order) - 1, stg
+    assert len(set(l_g[:3])) == 3  # each replay ran on its own batch's data
+    assert l_e == l_g
+    for k in sd_e:
+        assert torch.equal(sd_e[k], sd_g[k]), k
