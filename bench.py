@@ -550,6 +550,42 @@ HEAD_PROF = (("k_poly_step", "PROF_POLY", "hbm"), ("hodge_node (factored L1, B1 
              "PROF_BN_BWD", "hbm"))
 
 
+def cifar_pipeline_leg(device, c, G, n_batches=4):
+    """Config 3 WITH the reference's per-sample work (its Dataset.get() runs
+    every epoch, main_cifar10SP...:67-125): hlhgat.pipeline.SuperpixelPipeline
+    builds each 256-graph batch from raw superpixel samples (dropout_edge
+    augmentation, device Hodge builder + lambda_max, batched eigh PE, native
+    MLGC, both levels collated on the device), then the training step runs
+    on it (eagerly: every augmented batch has its own shape)."""
+    import hlhgat
+    from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    from hlhgat.train import TrainStep
+    raw = [superpixel_raw(5000 + i) for i in range(n_batches * G)]
+    pipe = SuperpixelPipeline(raw, keig=c["kw"]["keig"] + 1, aug=True)
+    torch.manual_seed(0)
+    m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
+    st = TrainStep(m, lambda o, d: _head_loss("cifar", o, d), lr=1e-3, graphs=False)
+    st(pipe.batch(range(G), seed=99, device=device))  # warm-up
+    torch.cuda.synchronize()
+    t_pipe = t_step = 0.0
+    for b in range(n_batches):
+        t0 = time.perf_counter()
+        datas = pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        st(datas)
+        torch.cuda.synchronize()
+        t_pipe += t1 - t0
+        t_step += time.perf_counter() - t1
+    return {"value": round(n_batches * G / (t_pipe + t_step), 1), "unit": "graphs/s",
+            "pipeline_graphs_per_s": round(n_batches * G / t_pipe, 1),
+            "pipeline_ms_per_batch": round(t_pipe / n_batches * 1e3, 1),
+            "step_ms_per_batch": round(t_step / n_batches * 1e3, 1),
+            "what": "raw superpixel samples -> SuperpixelPipeline (device Hodge builder, "
+                    "batched eigh PE, native MLGC, dropout_edge) -> eager training step, "
+                    "serial; batches of " + str(G)}
+
+
 def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
     """BASELINE configs[2..4] on this GPU: graphs/s of a full training step
     (fwd + loss + bwd + Adam) at the per-GPU batch of SURVEY §8d.  n_batches
@@ -658,6 +694,8 @@ def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
                              "cores": cores, "kind": "port",
                              "sample": f"{len(times)} oracle training steps on {c['cpu_graphs']} "
                                        f"graph(s) of the same generator, median {med * 1e3:.0f} ms"}
+        if kind == "cifar":
+            r["with_per_sample_work"] = cifar_pipeline_leg(device, c, G)
         out[name] = r
         log(f"[heads] {name}: {r['value']} graphs/s replayed, {r['eager_value']} eager, "
             f"padding {overhead:.1%} (CPU oracle {r['cpu_baseline']['value']})")

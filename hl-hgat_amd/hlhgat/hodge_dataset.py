@@ -976,7 +976,7 @@ def hodge_coo_from_boundary(edge_index, n: int, lmax: float):
 # ----------------------------------------------------------------------------
 # multi-level graph coarsening (MLGC) for the attention-pooling heads
 # ----------------------------------------------------------------------------
-def graclus(edge_index, n: int, weight=None, seed: int = 0) -> np.ndarray:
+def graclus(edge_index, n: int, weight=None, seed: int = 0, perm=None) -> np.ndarray:
     """Greedy graclus matching (torch_cluster 1.6.0 graclus_cluster, the
     reference's dependency, absent here; called at lib/Hodge_Dataset.py:252,
     :311), run by the library's native host builder (hlhgat_graclus):
@@ -987,11 +987,16 @@ def graclus(edge_index, n: int, weight=None, seed: int = 0) -> np.ndarray:
     branch, which the reference always takes (MLGC passes ones_like) -- both
     get cluster id min(u, v); a node with no unmatched neighbour stays alone
     (id u).  Parity unpinned (no torch_cluster output exists here).
+    perm: an explicit node order (replaces the seeded permutation).
     Returns int64 [n] cluster ids."""
     from ._lib import LIB, check
     ei = np.ascontiguousarray(np.asarray(edge_index, dtype=np.int64).reshape(2, -1))
     w = None if weight is None else np.ascontiguousarray(np.asarray(weight, dtype=np.float64))
-    perm = np.ascontiguousarray(np.random.default_rng(seed).permutation(n).astype(np.int64))
+    if perm is None:
+        perm = np.random.default_rng(seed).permutation(n)
+    perm = np.ascontiguousarray(np.asarray(perm, dtype=np.int64))
+    if perm.shape != (n,):
+        raise ValueError(f"graclus: perm must have {n} entries")
     out = np.empty(n, dtype=np.int64)
     check(LIB.hlhgat_graclus(ei.ctypes.data, None if w is None else w.ctypes.data,
                              ei.shape[1], n, perm.ctypes.data, out.ctypes.data), "graclus")

@@ -170,6 +170,30 @@ def sparse_matmul(src, other, reduce="sum"):
     return out.index_add_(0, src.row, msg)
 
 
+def to_undirected(edge_index, edge_attr=None, num_nodes=None, reduce="add"):
+    """torch_geometric.utils.to_undirected (documented semantics): both
+    directions, coalesced (sorted by row * N + col), duplicate attributes
+    reduced by `reduce`; returns (edge_index, edge_attr) when edge_attr is
+    given, else edge_index."""
+    n = int(edge_index.max()) + 1 if num_nodes is None else int(num_nodes)
+    row = torch.cat([edge_index[0], edge_index[1]])
+    col = torch.cat([edge_index[1], edge_index[0]])
+    key = row * n + col
+    uniq, inv = torch.unique(key, sorted=True, return_inverse=True)
+    ei = torch.stack([uniq // n, uniq % n])
+    if edge_attr is None:
+        return ei
+    a = torch.cat([edge_attr, edge_attr])
+    out = torch.zeros((uniq.numel(),) + tuple(a.shape[1:]), dtype=a.dtype)
+    if reduce == "min":
+        out = out.fill_(float("inf")).scatter_reduce(0, inv, a, "amin", include_self=True)
+    elif reduce == "mean":
+        out = out.scatter_reduce(0, inv, a, "mean", include_self=False)
+    else:
+        out = out.index_add(0, inv, a)
+    return ei, out
+
+
 def install():
     tg = _mod("torch_geometric")
     tg.__path__ = []
@@ -216,7 +240,8 @@ def install():
     loader.DataLoader = _Placeholder
     utils = _mod("torch_geometric.utils")
     utils.__path__ = []
-    for name in ("add_self_loops", "to_undirected", "coalesce", "to_scipy_sparse_matrix",
+    utils.to_undirected = to_undirected
+    for name in ("add_self_loops", "coalesce", "to_scipy_sparse_matrix",
                  "subgraph", "unbatch_edge_index", "softmax", "unbatch",
                  "remove_isolated_nodes"):
         setattr(utils, name, _Placeholder)

@@ -1,0 +1,120 @@
+"""Config-3 per-sample data path (hlhgat.pipeline.SuperpixelPipeline) against
+the reference's own CIFAR10SP_EigPE_MLGC.get()
+(main_cifar10SP_HL_HGCNN_dense_int3_attpool.py:67-125; fixture
+tests/golden/make_golden_pipeline.py: augmentation off, graclus node orders
+stored).
+
+Columns: level 0 x_t = [cluster, x(3), pos(2), PE(9), 0], x_s = [cluster,
+attr, |x_i - x_j|(3), |PE_i + PE_j|(9), 0]; the reference multiplies the last
+keig - 1 = 10 columns by random signs, so those are compared in absolute
+value.
+
+* CPU (the restatement, device="cpu": the reference's arithmetic): every
+  index array, weight and non-PE column bitwise; PE columns |.| bitwise.
+* GPU (device path: Lanczos lambda_max, device Hodge builder, batched
+  rocSOLVER eigh): indices and the cluster maps exact; Laplacian weights and
+  the coarse level within 1e-6 relative (lambda_max by Lanczos, not eigh);
+  non-PE columns exact; PE columns |.| within 1e-4 where the eigenvalue is
+  separated from its neighbours by > 1e-3 (an eigenvector is defined up to
+  sign, and up to rotation inside a cluster of near-equal eigenvalues).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import close, load_golden
+
+G = "pipeline_cifar_get"
+
+
+def _pipe_and_batch(device, i):
+    from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    g = load_golden(G)
+    raw = superpixel_raw(int(g[f"s{i}/seed"]), n=int(g[f"s{i}/n"]), k=int(g[f"s{i}/k"]))
+    p = SuperpixelPipeline([raw], keig=int(g["keig"]), aug=False)
+    return g, p.batch([0], seed=0, device=device, perms=[g[f"s{i}/perm"]])
+
+
+def _pe_gaps(L0_coo, w, n, k=10):
+    """Smallest distance of eigenvalues 1..k-1 of the fixture's L0 to their
+    neighbours."""
+    L = np.zeros((n, n))
+    L[L0_coo[0], L0_coo[1]] = w
+    ev = np.linalg.eigvalsh(L)
+    return [min(ev[j] - ev[j - 1], ev[j + 1] - ev[j]) for j in range(1, k)]
+
+
+N_FIXED_T, N_FIXED_S = 6, 5  # columns before the sign-flipped ones
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_pipeline_host_matches_reference_get(i):
+    g, (l0, l1) = _pipe_and_batch("cpu", i)
+    p = f"s{i}/"
+    for lv, b in ((0, l0), (1, l1)):
+        for key in ("edge_index", "edge_index_t", "edge_index_s"):
+            assert np.array_equal(getattr(b, key).numpy(), g[p + f"l{lv}/{key}"]), (lv, key)
+        for key in ("edge_weight_t", "edge_weight_s"):
+            assert np.array_equal(getattr(b, key).numpy(), g[p + f"l{lv}/{key}"]), (lv, key)
+    assert np.array_equal(l1.x_t.numpy(), g[p + "l1/x_t"])
+    assert np.array_equal(l1.x_s.numpy(), g[p + "l1/x_s"])
+    for key, nf in (("x_t", N_FIXED_T), ("x_s", N_FIXED_S)):
+        got, ref = getattr(l0, key).numpy(), g[p + f"l0/{key}"]
+        assert got.shape == ref.shape, key
+        assert np.array_equal(got[:, :nf], ref[:, :nf]), key
+        assert np.array_equal(np.abs(got[:, nf:]), np.abs(ref[:, nf:])), key
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_pipeline_device_matches_reference_get(cuda, i):
+    g, (l0, l1) = _pipe_and_batch(cuda, i)
+    p = f"s{i}/"
+    for lv, b in ((0, l0), (1, l1)):
+        for key in ("edge_index", "edge_index_t", "edge_index_s"):
+            assert np.array_equal(getattr(b, key).cpu().numpy(), g[p + f"l{lv}/{key}"]), (lv, key)
+        for key in ("edge_weight_t", "edge_weight_s"):
+            close(getattr(b, key).cpu(), g[p + f"l{lv}/{key}"], 1e-6, f"l{lv} {key}")
+    assert np.array_equal(l1.x_t.cpu().numpy(), g[p + "l1/x_t"])
+    n = int(g[p + "n"])
+    gaps = _pe_gaps(g[p + "l0/edge_index_t"], g[p + "l0/edge_weight_t"], n)
+    ok = [j for j, gap in enumerate(gaps) if gap > 1e-3]
+    assert len(ok) >= 5, gaps
+    xt, rt = l0.x_t.cpu().numpy(), g[p + "l0/x_t"]
+    assert np.array_equal(xt[:, :N_FIXED_T], rt[:, :N_FIXED_T])
+    pe_cols = [N_FIXED_T + j for j in ok]
+    close(np.abs(xt[:, pe_cols]), np.abs(rt[:, pe_cols]), 1e-4, "node PE |.|")
+    xs, rs = l0.x_s.cpu().numpy(), g[p + "l0/x_s"]
+    assert np.array_equal(xs[:, :N_FIXED_S], rs[:, :N_FIXED_S])
+    # edge PE |pe_i + pe_j| is invariant under the eigenvector's sign
+    ecols = [N_FIXED_S + j for j in ok]
+    close(np.abs(xs[:, ecols]), np.abs(rs[:, ecols]), 1e-4, "edge PE |.|")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["mlgc_small", "mlgc_weighted_small"])
+def test_mlgc_device_coarse_level_matches_reference(cuda, name):
+    """MLGC with its coarse level built on the device, as the pipeline does:
+    the stored graclus labels (graclus itself parity unpinned) -> the native
+    fine -> coarse map (hlhgat_mlgc_map) -> the coarse graph's Hodge
+    Laplacians by the device builder (Lanczos lambda_max + hlhgat_hodge_build)
+    against the reference's own MLGC / MLGC_weighted (lib/Hodge_Dataset.py:
+    241-353, tests/golden/make_golden_attpool.py): maps and indices exact,
+    weights within 1e-6 relative."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import mlgc_map
+    g = load_golden(name)
+    for gi in range(3):
+        p = f"g{gi}/"
+        c_node, c_edge, ei1, n1 = mlgc_map(g[p + "graclus"], g[p + "edge_index"])
+        assert np.array_equal(c_node.reshape(-1), g[p + "c_node"].reshape(-1))
+        ref_ce = g[p + "c_edge"].reshape(-1)
+        assert np.array_equal(np.isinf(c_edge), np.isinf(ref_ce))
+        assert np.array_equal(c_edge[~np.isinf(c_edge)], ref_ce[~np.isinf(ref_ce)])
+        assert n1 == int(g[p + "coarse/num_node1"])
+        assert np.array_equal(ei1, g[p + "coarse/edge_index"])
+        ei_t, w_t, ei_s, w_s, _ = ops.hodge_build(torch.from_numpy(ei1).to(cuda), [n1])
+        assert np.array_equal(ei_t.cpu().numpy(), g[p + "coarse/edge_index_t"])
+        assert np.array_equal(ei_s.cpu().numpy(), g[p + "coarse/edge_index_s"])
+        close(w_t.cpu(), g[p + "coarse/edge_weight_t"], 1e-6, "coarse L0")
+        close(w_s.cpu(), g[p + "coarse/edge_weight_s"], 1e-6, "coarse L1")

@@ -16,8 +16,8 @@ step() {  # name timeout cmd...
   esac
   return 0
 }
-NEW=${NEW:-"tests/test_frozen_mask_grads.py tests/test_multirank_trainstep.py tests/test_train_step.py"}
-KSEL=${KSEL:-"frozen or two_ranks or padded_levels"}
+NEW=${NEW:-"tests/test_frozen_mask_grads.py tests/test_multirank_trainstep.py tests/test_train_step.py tests/test_pipeline.py"}
+KSEL=${KSEL:-"frozen or two_ranks or padded_levels or pipeline or mlgc"}
 step new_tests 500 python -u -m pytest $NEW -k "$KSEL" -m gpu -v -s -p no:cacheprovider --timeout 200 --timeout-method thread
 [ "${NEW_ONLY:-0}" = 1 ] && exit 0
 step pytest_gpu 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
