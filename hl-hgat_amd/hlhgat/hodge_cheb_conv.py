@@ -229,7 +229,8 @@ class NodeEdgeInt(nn.Module):
                         _nn.tap(mod, y)
             if r is not None:
                 return r
-        if getattr(par, "valid_t", None) is not None:
+        if not self.only_att and getattr(par, "valid_t", None) is not None:
+            # the unfused value path's BatchNorms would count the padding rows
             raise RuntimeError("hlhgat: static-shape (padded) batches need the fused "
                                "NodeEdgeInt value path (training-mode WV_* MLPs)")
         x_s2t, x_t2s = self.interact(x_t, x_s, par, D)

@@ -89,14 +89,41 @@ def _to(b, dev):
     return [x.to(dev) for x in b] if isinstance(b, list) else b.to(dev)
 
 
-def _rank_worker(rank, world, port, q, kind):
+def _save_shards(shards, path):
+    """[step][rank] batches (a Batch or a level list) as plain tensor dicts."""
+    def one(b):
+        d = {k: v for k, v in vars(b).items() if torch.is_tensor(v) and not k.startswith("_")}
+        d["__meta"] = {"num_graphs": int(b.num_graphs), "hodge_sorted": dict(b.hodge_sorted),
+                       "l1_factor": bool(getattr(b, "l1_factor", False)),
+                       "num_nodes": int(getattr(b, "num_nodes", 0))}
+        return d
+    torch.save([[[one(x) for x in b] if isinstance(b, list) else one(b) for b in row]
+                for row in shards], path)
+
+
+def _load_shards(path):
+    from hlhgat.hodge_dataset import Batch
+
+    def one(d):
+        b = Batch()
+        meta = d.pop("__meta")
+        for k, v in d.items():
+            setattr(b, k, v)
+        for k, v in meta.items():
+            setattr(b, k, v)
+        return b
+    raw = torch.load(path, weights_only=True)
+    return [[[one(x) for x in b] if isinstance(b, list) else one(b) for b in row] for row in raw]
+
+
+def _rank_worker(rank, world, port, q, kind, path):
     import faulthandler
     faulthandler.dump_traceback_later(150, exit=True)  # a stuck rank shows where
     _env(rank, world, port, share_gpu=True)
     from hlhgat.distributed import init_distributed
     from hlhgat.train import TrainStep
     r, w, dev = init_distributed()
-    shards = _zinc_shards(w) if kind == "zinc" else _head_shards(kind, w)
+    shards = _load_shards(path)  # the parent's exact inputs
     model = _model(kind, dev)
     st = TrainStep(model, _loss(kind), lr=1e-3, weight_decay=1e-3, graphs=True)
     losses = []
@@ -108,7 +135,7 @@ def _rank_worker(rank, world, port, q, kind):
     dist.destroy_process_group()
 
 
-def _emulate(kind, cuda, world=2):
+def _emulate(kind, cuda, shards, world=2):
     """One process: per step, each shard's gradient at the same parameters,
     (g_0 + g_1) / 2 as all_reduce(SUM) + div_(world) computes it, one Adam.
     CIFAR: hodge_st_model.global_max replaced by an emulation that takes the
@@ -118,7 +145,6 @@ def _emulate(kind, cuda, world=2):
     gradients)."""
     from hlhgat import hodge_st_model as HM
     from hlhgat.train import TrainStep
-    shards = _zinc_shards(world) if kind == "zinc" else _head_shards(kind, world)
     model = _model(kind, cuda)
     st = TrainStep(model, _loss(kind), lr=1e-3, weight_decay=1e-3, graphs=False)
     real_gm = HM.global_max
@@ -203,8 +229,11 @@ class _EmuMax(torch.autograd.Function):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["zinc", "peptides", "cifar"])
-def test_trainstep_two_ranks_bitwise_one_process(cuda, kind):
-    res = _run_ranks(_rank_worker, 2, kind, timeout=200)
+def test_trainstep_two_ranks_bitwise_one_process(cuda, kind, tmp_path):
+    shards = _zinc_shards(2) if kind == "zinc" else _head_shards(kind, 2)
+    path = str(tmp_path / "shards.pt")
+    _save_shards(shards, path)
+    res = _run_ranks(_rank_worker, 2, kind, path, timeout=200)
     for r in range(2):
         st = res[r]["stats"]
         if kind == "cifar":
@@ -212,7 +241,7 @@ def test_trainstep_two_ranks_bitwise_one_process(cuda, kind):
         else:
             assert res[r]["graphs"] and st["replay"] >= 2, st
     assert np.array_equal(res[0]["flat"], res[1]["flat"]), "ranks hold different parameters"
-    want = _emulate(kind, cuda)
+    want = _emulate(kind, cuda, _load_shards(path))
     diff = np.abs(res[0]["flat"] - want).max()
     assert np.array_equal(res[0]["flat"], want), f"{kind}: max |diff| {diff:.3e}"
 

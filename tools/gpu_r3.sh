@@ -20,6 +20,6 @@ NEW=${NEW:-"tests/test_frozen_mask_grads.py tests/test_multirank_trainstep.py te
 KSEL=${KSEL:-"frozen or two_ranks or padded_levels or pipeline or mlgc"}
 step new_tests 500 python -u -m pytest $NEW -k "$KSEL" -m gpu -v -s -p no:cacheprovider --timeout 200 --timeout-method thread
 [ "${NEW_ONLY:-0}" = 1 ] && exit 0
-step pytest_gpu 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+[ "${SKIP_SUITE:-0}" = 1 ] || step pytest_gpu 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
 step bench 600 python bench.py
 echo "=== done"
