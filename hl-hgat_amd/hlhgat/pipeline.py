@@ -226,7 +226,7 @@ class SuperpixelPipeline:
         from . import ops
         B = len(idx)
         n_off = np.concatenate([[0], np.cumsum(ns)])
-        ei_b = np.concatenate([e + o for e, o in zip(eis, n_off[:-1])], axis=1)
+        ei_b = np.ascontiguousarray(np.concatenate([e + o for e, o in zip(eis, n_off[:-1])], axis=1))
         E_g = [int(e.shape[1]) for e in eis]
         ei_d = torch.from_numpy(ei_b).to(dev)
         ei_t, w_t, ei_s, w_s, lam = ops.hodge_build(ei_d, ns)
@@ -266,15 +266,15 @@ class SuperpixelPipeline:
         lv0.edge_index_t, lv0.edge_weight_t = ei_t, w_t
         lv0.edge_index_s, lv0.edge_weight_s = ei_s, w_s
         lv0.edge_index = ei_d
-        lv0.y = torch.cat(self.y).to(dev)
+        lv0.y = torch.cat([self.y[i] for i in idx]).to(dev)
         lv0.num_node1 = torch.tensor(ns)
         lv0.num_edge1 = torch.tensor(E_g)
         lv0.num_nodes = int(n_off[-1])
         # coarse level: the MLGC graphs, Laplacians on the device again
         n1 = [int(c[3]) for c in cmaps]
         o1 = np.concatenate([[0], np.cumsum(n1)])
-        ei1 = torch.from_numpy(np.concatenate([c[2] + o for c, o in zip(cmaps, o1[:-1])],
-                                              axis=1)).to(dev)
+        ei1 = torch.from_numpy(np.ascontiguousarray(np.concatenate(
+            [c[2] + o for c, o in zip(cmaps, o1[:-1])], axis=1))).to(dev)
         c_t, c_wt, c_s, c_ws, _ = ops.hodge_build(ei1, n1)
         lv1 = Batch()
         lv1.num_graphs = B

@@ -71,6 +71,8 @@ def test_pipeline_device_matches_reference_get(cuda, i):
     g, (l0, l1) = _pipe_and_batch(cuda, i)
     p = f"s{i}/"
     for lv, b in ((0, l0), (1, l1)):
+        for key, v in vars(b).items():  # the heads .view() these (edge_index, x_*)
+            assert not torch.is_tensor(v) or v.is_contiguous(), (lv, key)
         for key in ("edge_index", "edge_index_t", "edge_index_s"):
             assert np.array_equal(getattr(b, key).cpu().numpy(), g[p + f"l{lv}/{key}"]), (lv, key)
         for key in ("edge_weight_t", "edge_weight_s"):
@@ -118,3 +120,27 @@ def test_mlgc_device_coarse_level_matches_reference(cuda, name):
         assert np.array_equal(ei_s.cpu().numpy(), g[p + "coarse/edge_index_s"])
         close(w_t.cpu(), g[p + "coarse/edge_weight_t"], 1e-6, "coarse L0")
         close(w_s.cpu(), g[p + "coarse/edge_weight_s"], 1e-6, "coarse L1")
+
+
+@pytest.mark.gpu
+def test_pipeline_device_batch_matches_host_batch(cuda):
+    """A multi-sample batch (the three fixture samples, stored graclus orders)
+    on the device equals the host restatement's batch: the collation offsets,
+    labels and per-graph counts exact, Laplacian weights within 1e-6."""
+    from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    g = load_golden(G)
+    raws = [superpixel_raw(int(g[f"s{i}/seed"]), n=int(g[f"s{i}/n"]), k=int(g[f"s{i}/k"]))
+            for i in range(3)]
+    for r, y in zip(raws, (3, 7, 1)):
+        r.y = torch.tensor([y])
+    p = SuperpixelPipeline(raws, keig=int(g["keig"]), aug=False)
+    perms = [g[f"s{i}/perm"] for i in range(3)]
+    host = p.batch([2, 0, 1], seed=0, device="cpu", perms=[perms[2], perms[0], perms[1]])
+    devb = p.batch([2, 0, 1], seed=0, device=cuda, perms=[perms[2], perms[0], perms[1]])
+    for lv, (h, d) in enumerate(zip(host, devb)):
+        for key in ("edge_index", "edge_index_t", "edge_index_s", "num_node1", "num_edge1"):
+            assert np.array_equal(getattr(h, key).numpy(), getattr(d, key).cpu().numpy()), (lv, key)
+        for key in ("edge_weight_t", "edge_weight_s"):
+            close(getattr(d, key).cpu(), getattr(h, key), 1e-6, f"l{lv} {key}")
+        assert h.x_t.shape == d.x_t.shape and h.x_s.shape == d.x_s.shape, lv
+    assert host[0].y.tolist() == devb[0].y.cpu().tolist() == [1, 3, 7]
