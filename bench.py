@@ -153,6 +153,7 @@ REPLAY_CLASSES = {
     "k_poly_step": (r"k_poly_step<", "PROF_POLY", "hbm"),
     "k_proj_bwd_fused": (r"k_proj_bwd_fused<", "PROF_PROJ_BWD", "mfma"),
     "k_proj_fwd": (r"k_proj_fwd", "PROF_PROJ", "mfma"),
+    "k_proj_bn_fwd": (r"k_proj_bn_fwd", "PROF_PROJ_BN", "mfma"),
     "k_bn_fwd_grid": (r"k_bn_fwd_grid<", "PROF_BN_FWD", "hbm"),
     "k_bn_bwd_reduce": (r"k_bn_bwd_reduce<", "PROF_BN_BWD", "hbm"),
 }
@@ -545,7 +546,8 @@ def _head_loss(kind, out, datas):
 
 HEAD_PROF = (("k_poly_step", "PROF_POLY", "hbm"), ("hodge_node (factored L1, B1 X)",
              "PROF_HODGE_NODE", "hbm"), ("hodge_edge (factored L1 edge step)", "PROF_HODGE_EDGE",
-             "hbm"), ("k_proj_fwd", "PROF_PROJ", "mfma"), ("k_proj_bwd_fused", "PROF_PROJ_BWD",
+             "hbm"), ("k_proj_fwd", "PROF_PROJ", "mfma"), ("k_proj_bn_fwd", "PROF_PROJ_BN", "mfma"),
+             ("k_proj_bwd_fused", "PROF_PROJ_BWD",
              "mfma"), ("k_bn_fwd_grid", "PROF_BN_FWD", "hbm"), ("k_bn_bwd_reduce",
              "PROF_BN_BWD", "hbm"))
 
@@ -876,7 +878,8 @@ def main():
 
     # roofline pass: eager steps, SpMM / projection / BatchNorm launches event-stamped
     L = hlhgat._lib
-    classes = (L.PROF_POLY, L.PROF_PROJ, L.PROF_PROJ_BWD, L.PROF_BN_FWD, L.PROF_BN_BWD)
+    classes = (L.PROF_POLY, L.PROF_PROJ, L.PROF_PROJ_BWD, L.PROF_PROJ_BN, L.PROF_BN_FWD,
+               L.PROF_BN_BWD)
     ops.prof_reset()
     for c in classes:
         ops.prof_enable(c, True)
@@ -945,6 +948,8 @@ def main():
             ("k_proj_bwd_fused", L.PROF_PROJ_BWD, "mfma",
              "Linear backward: weight-gradient split partials + data gradient, one launch; "
              "flops 2 M N (sum K_w + sum K_d)"),
+            ("k_proj_bn_fwd", L.PROF_PROJ_BN, "mfma",
+             "projection + BatchNorm (+ReLU) forward in one launch; flops 2 M N sum K"),
             ("k_bn_fwd_grid", L.PROF_BN_FWD, "hbm",
              "BatchNorm forward (statistics + normalise, one launch); bytes 8 n C"),
             ("k_bn_bwd_reduce", L.PROF_BN_BWD, "hbm",

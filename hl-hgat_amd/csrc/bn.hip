@@ -36,7 +36,7 @@
 // Guideline 16): partials are written through with agent-scope atomic stores
 // drained by vmcnt(0) before a barrier; one lane takes a relaxed agent atomic
 // ticket; readers use agent-scope atomic loads.
-#include "common.h"
+#include "gemm_core.h"
 
 #include <cstdlib>
 
@@ -990,6 +990,196 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
   k_bn_fwd_grid_body<V, RPT>(a, blk_hw());
 }
 
+// ---------------------------------------------------------------------------
+// Projection + BatchNorm (+ ReLU) forward in ONE launch (hlhgat_proj_bn_fwd)
+//
+// Every BatchNorm of the HL blocks and of the NodeEdgeInt MLPs reads the
+// output of the Linear / conv projection just before it (lib/Hodge_ST_Model.py:
+// 556-566, lib/Hodge_Cheb_Conv.py:276-289).  Here the projection's workgroups
+// (64 rows x 64 columns each, proj_fwd_lds_mainloop) keep their output tile
+// in registers and finish the BatchNorm themselves:
+//   1. x = A W^T + bias is stored (the backward needs it) and the tile's fp64
+//      column sums over its valid rows are formed in a fixed order (rows of a
+//      lane, lanes q by xor 16 then 32, waves 0..3) and written through;
+//   2. a two-level last-arriver tree per 64-column tile: the last workgroup of
+//      each group of kGroup partials sums them (reduce_range, fixed order),
+//      the last group sums the group partials, finalises mean / invstd and the
+//      running statistics, and bumps the tile's generation word;
+//   3. every other workgroup polls that word (bounded: a timeout writes NaN
+//      rows and raises HLHGAT_DEVERR_BN_WAIT, as k_bn_fwd_grid), reads the
+//      statistics and normalises its tile from the registers: y = relu?((x -
+//      mean) * (w invstd) + b), rows >= n_valid written as 0.
+// All workgroups must be co-resident (the host checks half of the chip's
+// capacity, as for k_bn_fwd_grid).  Against projection -> k_bn_fwd_grid this
+// saves the BatchNorm launch, its read of x and its own load latency.  The
+// statistics are the same sums in a different fp64 order (not bitwise the
+// two-kernel path; equal to 1e-6, tests/test_gpu_parity.py).
+// ---------------------------------------------------------------------------
+struct ProjBnArgs {
+  FwdArgs g;    // the projection: g.C = x (pre-BatchNorm), g.ldc
+  StatsArgs s;  // the BatchNorm: s.out = y, partials / counters / error word
+};
+
+constexpr int kPbTN = 4;  // 64 columns per workgroup: one BatchNorm column tile
+
+__device__ __forceinline__ unsigned long long* gen_word(const StatsArgs& a, int tile) {
+  return reinterpret_cast<unsigned long long*>(a.count + kGridBase) + tile;
+}
+
+__global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
+  __shared__ __attribute__((aligned(16))) float wl[2][kPbTN * 16][KCP];
+  __shared__ unsigned s_gen0, s_ok;
+  const FwdArgs& g = a.g;
+  const StatsArgs& s = a.s;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  const int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+  const int64_t m_base = ((int64_t)bx * 4 + wave) * 16;
+  const int n_base = by * (kPbTN * 16);
+  floatx4 acc[kPbTN];
+  proj_fwd_lds_mainloop<kPbTN>(g, bx, by, wl, acc);
+  // x = acc + bias, as store_tile_rows adds it
+  if (g.bias) {
+#pragma unroll
+    for (int tn = 0; tn < kPbTN; ++tn) {
+      const float bv = g.bias[n_base + tn * 16 + i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[tn][r] = acc[tn][r] + bv;
+    }
+  }
+  // LDS after the main loop: per-wave row-store scratch in the first 17 KB,
+  // the column sums behind it
+  float* scratch = &wl[0][0][0] + wave * 16 * (kPbTN * 16 + 4);
+  double* red = reinterpret_cast<double*>(&wl[0][0][0] + 4 * 16 * (kPbTN * 16 + 4));  // [2][4][64]
+  double* sum0 = red + 2 * 4 * 64;  // [64]
+  double* sum1 = sum0 + 64;         // [64]
+  const bool vx = (g.ldc % 4) == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0;
+  store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr, 0,
+                         vx);
+  const int64_t n_eff = eff_rows(s.n, s.nvalid);
+#pragma unroll
+  for (int tn = 0; tn < kPbTN; ++tn) {
+    double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m_base + 4 * q + r < n_eff) {
+        const double xd = (double)acc[tn][r];
+        u0 += xd;
+        u1 += xd * xd;
+      }
+    }
+    u0 += __shfl_xor(u0, 16, 64);
+    u1 += __shfl_xor(u1, 16, 64);
+    u0 += __shfl_xor(u0, 32, 64);
+    u1 += __shfl_xor(u1, 32, 64);
+    if (q == 0) {
+      red[(0 * 4 + wave) * 64 + tn * 16 + i] = u0;
+      red[(1 * 4 + wave) * 64 + tn * 16 + i] = u1;
+    }
+  }
+  __syncthreads();
+  unsigned long long* word = gen_word(s, by);
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    const double v0 = ((red[0 * 256 + t] + red[0 * 256 + 64 + t]) + red[0 * 256 + 128 + t]) +
+                      red[0 * 256 + 192 + t];
+    const double v1 = ((red[1 * 256 + t] + red[1 * 256 + 64 + t]) + red[1 * 256 + 128 + t]) +
+                      red[1 * 256 + 192 + t];
+    double* dst = s.part + ((int64_t)bx * s.C + n_base + t) * 2;
+    st_wt(dst, v0);
+    st_wt(dst + 1, v1);
+  }
+  if (threadIdx.x == 0)  // the generation before this workgroup's arrival
+    s_gen0 = (unsigned)(__hip_atomic_load((gu64c_t*)word, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) >> 32);
+  const int parts = (int)gridDim.x;
+  const int grp = bx / kGroup, ng = (parts + kGroup - 1) / kGroup;
+  const int first = grp * kGroup;
+  const int cnt = parts - first < kGroup ? parts - first : kGroup;
+  bool top = false;
+  if (arrive_last(s.count + kMaxTiles + by * kMaxGroups + grp, (unsigned)cnt)) {
+    reduce_range<kThreads>(s.part, first, cnt, s, n_base, 64, sum0, sum1);
+    if (threadIdx.x < 64) {
+      double* dst = s.gpart + ((int64_t)grp * s.C + n_base + threadIdx.x) * 2;
+      st_wt(dst, sum0[threadIdx.x]);
+      st_wt(dst + 1, sum1[threadIdx.x]);
+    }
+    top = arrive_last(s.count + by, (unsigned)ng);
+  }
+  float* sm = reinterpret_cast<float*>(sum1 + 64);  // [64]
+  float* ss = sm + 64;                              // [64]
+  if (top) {
+    reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
+    if (threadIdx.x < 64) {
+      const int cc = n_base + threadIdx.x;
+      float m, is;
+      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, true);
+      __hip_atomic_store(reinterpret_cast<unsigned*>(s.save_mean + cc), __float_as_uint(m),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<unsigned*>(s.save_invstd + cc), __float_as_uint(is),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm[threadIdx.x] = m;
+      ss[threadIdx.x] = is;
+    }
+    if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add((gu64c_t*)word, 1ull << 32, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (threadIdx.x == 0) {
+      unsigned ok = 0;
+      for (unsigned it = 0; it < s.poll_limit; ++it) {
+        const unsigned long long w =
+            __hip_atomic_load((gu64c_t*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(w >> 32) != s_gen0) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) report_wait_timeout(s.err);
+      s_ok = ok;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int cc = n_base + threadIdx.x;
+      float m = __builtin_nanf(""), is = __builtin_nanf("");
+      if (s_ok) {
+        m = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(s.save_mean + cc),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        is = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(s.save_invstd + cc),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      sm[threadIdx.x] = m;
+      ss[threadIdx.x] = is;
+    }
+  }
+  __syncthreads();
+  // y from the registers (k_bn_fwd_grid's arithmetic)
+#pragma unroll
+  for (int tn = 0; tn < kPbTN; ++tn) {
+    const int cl = tn * 16 + i, cc = n_base + cl;
+    const float sc = (s.weight ? s.weight[cc] : 1.f) * ss[cl];  // NaN after a timeout
+    const float mu = sm[cl];
+    const float sh = s.bias ? s.bias[cc] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = (acc[tn][r] - mu) * sc + sh;
+      acc[tn][r] = m_base + 4 * q + r >= n_eff ? 0.f : ((s.relu && z < 0.f) ? 0.f : z);
+    }
+  }
+  const bool vy = (s.ldo % 4) == 0 && (reinterpret_cast<uintptr_t>(s.out) & 15) == 0;
+  store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, s.out + n_base, s.ldo, kPbTN * 16, nullptr,
+                         0, vy);
+}
+
+bool& proj_bn_fused_flag() {
+  static bool v = true;
+  return v;
+}
+
 bool bn_vec_ok(int64_t C, std::initializer_list<int64_t> lds,
                std::initializer_list<const void*> ptrs) {
   if (C % 4) return false;
@@ -1224,6 +1414,107 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
   else
     launch(k_bn_apply<1>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+// Projection + BatchNorm (+ ReLU) forward (see k_proj_bn_fwd): one launch where
+// the projection's grid fits co-resident, else hlhgat_proj_fwd then
+// hlhgat_bn_fwd_train on x.
+extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
+                                  const float* const* W, const int64_t* ldw, const int64_t* kb,
+                                  int64_t M, int64_t N, const float* bias, float* x, int64_t ldx,
+                                  const int32_t* n_valid, const float* bn_weight,
+                                  const float* bn_bias, float* running_mean, float* running_var,
+                                  int64_t* num_batches_tracked, float momentum, float eps,
+                                  int relu, float* y, int64_t ldy, float* save_mean,
+                                  float* save_invstd, void* workspace, int64_t workspace_bytes,
+                                  void* stream) {
+  HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_bn_fwd: nblocks=%d", nblocks);
+  HLH_CHECK_ARG(M >= 1 && N >= 1 && N < (1 << 20) && ldx >= N && ldy >= N,
+                "proj_bn_fwd: bad sizes M=%lld N=%lld", (long long)M, (long long)N);
+  HLH_CHECK_ARG(x && y && save_mean && save_invstd, "proj_bn_fwd: NULL pointer");
+  HLH_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                "proj_bn_fwd: running_mean/var must both be given or both NULL");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(M, N),
+                "proj_bn_fwd: workspace too small");
+  bool vec = true;
+  int64_t ktot = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    HLH_CHECK_ARG(A[b] && W[b] && kb[b] > 0 && lda[b] >= kb[b] && ldw[b] >= kb[b],
+                  "proj_bn_fwd: bad block %d", b);
+    vec = vec && aligned16(A[b]) && aligned16(W[b]) && lda[b] % 4 == 0 && ldw[b] % 4 == 0 &&
+          kb[b] % 4 == 0;
+    ktot += kb[b];
+  }
+  const unsigned gx = (unsigned)ceil_div(M, (int64_t)64), gy = (unsigned)(N / 64);
+  bool fused = proj_bn_fused_flag() && vec && N % 64 == 0 && gy <= (unsigned)kMaxTiles &&
+               gx <= (unsigned)kMaxParts;
+  if (fused) {
+    const int64_t cap = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd));
+    fused = (int64_t)gx * gy <= cap;
+  }
+  if (!fused) {
+    const int rc = hlhgat_proj_fwd(nblocks, A, lda, W, ldw, kb, M, N, bias, x, ldx, 0, stream);
+    if (rc != HLHGAT_OK) return rc;
+    return hlhgat_bn_fwd_train(x, ldx, M, n_valid, N, bn_weight, bn_bias, running_mean,
+                               running_var, num_batches_tracked, momentum, eps, relu, y, ldy,
+                               save_mean, save_invstd, workspace, workspace_bytes, stream);
+  }
+  ProjBnArgs a{};
+  a.g.nb = nblocks;
+  a.g.M = M;
+  a.g.N = (int)N;
+  a.g.bias = bias;
+  a.g.C = x;
+  a.g.ldc = ldx;
+  for (int b = 0; b < nblocks; ++b) {
+    a.g.A[b] = A[b];
+    a.g.W[b] = W[b];
+    a.g.lda[b] = lda[b];
+    a.g.ldw[b] = ldw[b];
+    a.g.kb[b] = (int)kb[b];
+  }
+  BnWs w = carve(workspace, M, N);
+  StatsArgs& s = a.s;
+  s.nvalid = n_valid;
+  s.n = M;
+  s.C = (int)N;
+  s.part = w.part;
+  s.gpart = w.gpart;
+  s.count = w.count;
+  s.weight = bn_weight;
+  s.bias = bn_bias;
+  s.running_mean = running_mean;
+  s.running_var = running_var;
+  s.nbt = num_batches_tracked;
+  s.momentum = momentum;
+  s.eps = eps;
+  s.save_mean = save_mean;
+  s.save_invstd = save_invstd;
+  s.out = y;
+  s.ldo = ldy;
+  s.relu = relu;
+  s.poll_limit = g_poll_limit;
+  s.err = hlhgat::device_error_word();
+  HLH_CHECK_ARG(s.err, "proj_bn_fwd: no device error word (%s)", hlhgat_last_error());
+  // algorithmic: A read once, x and y written once; flops of the projection
+  const double flops = 2.0 * (double)M * (double)N * (double)ktot;
+  const double bytes = 4.0 * (double)M * ((double)ktot + 2.0 * (double)N);
+  hipStream_t st = as_stream(stream);
+  ProfScope prof(HLHGAT_PROF_PROJ_BN, st, bytes, flops);
+  launch(k_proj_bn_fwd, dim3(gx, gy), dim3(kThreads), 0, st, &prof, a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_set_proj_bn_fused(int on) {
+  proj_bn_fused_flag() = on != 0;
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_proj_bn_fused_capacity(int64_t* out) {
+  HLH_CHECK_ARG(out, "proj_bn_fused_capacity: NULL pointer");
+  *out = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd));
   return HLHGAT_OK;
 }
 

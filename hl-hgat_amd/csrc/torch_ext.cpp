@@ -511,6 +511,30 @@ Tensor bn_forward(const Tensor& x, const BnState& st, bool relu, Tensor& mean, T
   return y;
 }
 
+// x = sum_b A_b W_b^T + bias, then BatchNorm (+ReLU) of x into y: one launch
+// where the grid fits (hlhgat_proj_bn_fwd), else the projection then
+// bn_forward's kernels.  x must be a fresh [M, N] tensor (kept for backward).
+Tensor proj_bn_forward(const std::vector<const float*>& A, const std::vector<int64_t>& lda,
+                       const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
+                       const std::vector<int64_t>& kb, int64_t M, int64_t N, const float* bias,
+                       Tensor& x, const BnState& st, bool relu, Tensor& mean, Tensor& invstd,
+                       const Tensor* y_into = nullptr) {
+  Tensor y = y_into ? *y_into : at::empty({M, N}, x.options());
+  TORCH_CHECK(y.size(0) == M && y.size(1) == N && y.stride(1) == 1, "hlhgat: bad BN output view");
+  mean = at::empty({N}, x.options());
+  invstd = at::empty({N}, x.options());
+  Tensor ws = bn_workspace(x, M, N);
+  int64_t* nbt = has(st.nbt) ? st.nbt->data_ptr<int64_t>() : nullptr;
+  chk(hlhgat_proj_bn_fwd((int)A.size(), A.data(), lda.data(), W.data(), ldw.data(), kb.data(), M,
+                         N, bias, x.data_ptr<float>(), ld_of(x), iptr(st.valid), fptr(st.w),
+                         fptr(st.b), mfptr(st.rm), mfptr(st.rv), nbt, (float)st.momentum,
+                         (float)st.eps, relu ? 1 : 0, y.data_ptr<float>(), ld_of(y),
+                         mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr(),
+                         ws.numel(), stream_of(x)),
+      "proj_bn_fwd");
+  return y;
+}
+
 // returns dx; fills dw/db when requested
 // dx_into: optional [n, C] row-strided destination (e.g. a column slice)
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
@@ -701,14 +725,20 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv) {
                 "hlhgat: conv output buffer must be a row-major [", M, ", ", dout, "] view");
   Tensor pre = (sink && c.bn_mode == 0) ? *c.out_buf : at::empty({M, dout}, x.options());
   Tensor out = pre, mean, invstd;
-  if (M > 0) {
-    proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(c.bias), pre, s);
-  } else if (has(c.bias)) {
-    pre.copy_(c.bias->expand_as(pre));
-  }
-  if (c.bn_mode > 0) {
+  if (M > 0 && c.bn_mode > 0) {
     BnState st{c.bn_w, c.bn_b, c.bn_rm, c.bn_rv, c.bn_nbt, c.momentum, c.eps, c.valid};
-    out = bn_forward(pre, st, c.bn_mode == 2, mean, invstd, sink ? &*c.out_buf : nullptr);
+    out = proj_bn_forward(Ap, lda, Wp, ldw, kb, M, dout, fptr(c.bias), pre, st, c.bn_mode == 2,
+                          mean, invstd, sink ? &*c.out_buf : nullptr);
+  } else {
+    if (M > 0) {
+      proj_fwd(Ap, lda, Wp, ldw, kb, M, dout, fptr(c.bias), pre, s);
+    } else if (has(c.bias)) {
+      pre.copy_(c.bias->expand_as(pre));
+    }
+    if (c.bn_mode > 0) {
+      BnState st{c.bn_w, c.bn_b, c.bn_rm, c.bn_rv, c.bn_nbt, c.momentum, c.eps, c.valid};
+      out = bn_forward(pre, st, c.bn_mode == 2, mean, invstd, sink ? &*c.out_buf : nullptr);
+    }
   }
   sv.dims = {N, Cin, F, M, dout, K, c.kind, c.nnz, c.bn_mode, has(c.bias) ? 1 : 0};
   sv.fac_nodes = c.fac_nodes;
@@ -984,33 +1014,53 @@ class BNActFn : public torch::autograd::Function<BNActFn> {
 // ---------------------------------------------------------------------------
 // Linear over blocks: out = cat(As, -1) @ W^T + b, W column-split per block
 // ---------------------------------------------------------------------------
-Tensor linear_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT& b) {
-  const int64_t M = As[0].size(0), N = W.size(0);
+struct LinearOperands {
+  std::vector<const float*> Ap, Wp;
+  std::vector<int64_t> lda, ldw, kb;
+};
+LinearOperands linear_operands(const std::vector<Tensor>& As, const Tensor& W) {
   const int nb = (int)As.size();
-  std::vector<const float*> Ap(nb), Wp(nb);
-  std::vector<int64_t> lda(nb), ldw(nb), kb(nb);
+  LinearOperands o;
+  o.Ap.resize(nb);
+  o.Wp.resize(nb);
+  o.lda.resize(nb);
+  o.ldw.resize(nb);
+  o.kb.resize(nb);
   int64_t off = 0;
   for (int i = 0; i < nb; ++i) {
-    Ap[i] = As[i].data_ptr<float>();
-    lda[i] = ld_of(As[i]);
-    kb[i] = As[i].size(1);
-    Wp[i] = W.data_ptr<float>() + off;
-    ldw[i] = W.stride(0);
-    off += kb[i];
+    o.Ap[i] = As[i].data_ptr<float>();
+    o.lda[i] = ld_of(As[i]);
+    o.kb[i] = As[i].size(1);
+    o.Wp[i] = W.data_ptr<float>() + off;
+    o.ldw[i] = W.stride(0);
+    off += o.kb[i];
   }
   TORCH_CHECK(off == W.size(1), "hlhgat: Linear expects ", W.size(1), " input features, got ",
               off);
+  return o;
+}
+
+Tensor linear_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT& b) {
+  const int64_t M = As[0].size(0), N = W.size(0);
+  LinearOperands o = linear_operands(As, W);
   Tensor out = at::empty({M, N}, W.options());
-  if (M > 0) proj_fwd(Ap, lda, Wp, ldw, kb, M, N, fptr(b), out, stream_of(W));
+  if (M > 0) proj_fwd(o.Ap, o.lda, o.Wp, o.ldw, o.kb, M, N, fptr(b), out, stream_of(W));
   return out;
 }
 
 // Linear(blocks) -> BatchNorm (+ReLU): h (the BN input) is returned through
-// `h`, the activation as the result.
+// `h`, the activation as the result (one launch where it fits).
 Tensor linear_bn_forward(const std::vector<Tensor>& As, const Tensor& W, const OptT& b,
                          const BnState& st, bool relu, Tensor& h, Tensor& mean, Tensor& invstd) {
-  h = linear_forward(As, W, b);
-  return bn_forward(h, st, relu, mean, invstd);
+  const int64_t M = As[0].size(0), N = W.size(0);
+  if (M == 0) {
+    h = linear_forward(As, W, b);
+    return bn_forward(h, st, relu, mean, invstd);
+  }
+  LinearOperands o = linear_operands(As, W);
+  h = at::empty({M, N}, W.options());
+  return proj_bn_forward(o.Ap, o.lda, o.Wp, o.ldw, o.kb, M, N, fptr(b), h, st, relu, mean,
+                         invstd);
 }
 
 // grads of linear_forward; dAs[i] only where need_a[i]

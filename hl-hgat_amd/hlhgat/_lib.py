@@ -79,6 +79,11 @@ SIGNATURES = {
                                       P_vp, P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64,
                                       c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "hlhgat_reduce_run": (c_i32, [c_vp, c_vp]),
+    "hlhgat_proj_bn_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
+                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                   c_f32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_set_proj_bn_fused": (c_i32, [c_i32]),
+    "hlhgat_proj_bn_fused_capacity": (c_i32, [P_i64]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
     "hlhgat_get_bn_one_launch": (c_i32, []),
     "hlhgat_set_bn_poll_limit": (c_i32, [C.c_uint32]),
@@ -135,7 +140,7 @@ POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
 DEVERR_BN_WAIT = 1
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
-PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD = 4, 5, 6
+PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD, PROF_PROJ_BN = 4, 5, 6, 7
 MAX_BLOCKS = 16
 
 

@@ -552,6 +552,29 @@ int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_val
  * workgroup that gives up writes NaN rows (never numbers from partial
  * statistics), counts the timeout and raises HLHGAT_DEVERR_BN_WAIT in the
  * device error word. */
+/* Projection + BatchNorm1d (+ ReLU) forward, training mode: the
+ * hlhgat_proj_fwd GEMM x = sum_b A_b W_b^T + bias (stored to x: the backward
+ * reads it), then hlhgat_bn_fwd_train on x into y -- in ONE launch
+ * (k_proj_bn_fwd: the projection's workgroups finish the BatchNorm from
+ * their registers after a bounded grid-wide reduction) when N % 64 == 0, the
+ * operands are 16-B aligned with ld % 4 == 0, ceil(M / 64) <= 512 and the
+ * grid fits half of the chip's resident capacity; otherwise the two calls.
+ * Replaces Linear -> BatchNorm1d -> ReLU and HodgeLaguerreConv -> BatchNorm
+ * -> ReLU (lib/Hodge_Cheb_Conv.py:276-289, lib/Hodge_ST_Model.py:556-566).
+ * Statistics equal the two-call path's to fp64 summation order (not
+ * bitwise).  Workspace: hlhgat_bn_workspace_bytes(M, N). */
+int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
+                       const float* const* W, const int64_t* ldw, const int64_t* kb, int64_t M,
+                       int64_t N, const float* bias, float* x, int64_t ldx,
+                       const int32_t* n_valid, const float* bn_weight, const float* bn_bias,
+                       float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                       float momentum, float eps, int relu, float* y, int64_t ldy,
+                       float* save_mean, float* save_invstd, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+/* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
+int hlhgat_set_proj_bn_fused(int on);
+/* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */
+int hlhgat_proj_bn_fused_capacity(int64_t* out);
 int hlhgat_set_bn_one_launch(int on);
 int hlhgat_get_bn_one_launch(void);
 /* Test hook: polls before a waiting workgroup gives up (default 2^22;
@@ -662,7 +685,8 @@ int hlhgat_clear_device_errors(void);
 #define HLHGAT_PROF_PROJ_BWD 4 /* Linear backward: k_proj_bwd_fused (weight partials + data grad) */
 #define HLHGAT_PROF_BN_FWD 5 /* BatchNorm forward: k_bn_fwd_grid / k_bn_stats + k_bn_apply */
 #define HLHGAT_PROF_BN_BWD 6 /* BatchNorm backward: k_bn_bwd_reduce + k_bn_bwd_apply */
-#define HLHGAT_PROF_NCLASS 7
+#define HLHGAT_PROF_PROJ_BN 7 /* projection + BatchNorm forward in one launch: k_proj_bn_fwd */
+#define HLHGAT_PROF_NCLASS 8
 /* Enable (1) / disable (0) event timing of the given kernel class. */
 int hlhgat_prof_enable(int kernel_class, int enable);
 int hlhgat_prof_reset(void);

@@ -1269,3 +1269,116 @@ def test_boundary_operator_reference_lines_verbatim(cuda):
                 assert a.grad is None or not a.grad.any(), what
             else:
                 close(a.grad.cpu(), r.grad, 1e-6, what + " grad")
+
+
+def _proj_bn_call(cuda, As, W, bias, bn, valid, relu, fused):
+    """hlhgat_proj_bn_fwd through the C-ABI: returns x, y, mean, invstd."""
+    import ctypes
+    from hlhgat import _lib
+    L = _lib.LIB
+    M, N, nb = As[0].shape[0], W.shape[0], len(As)
+    kb = [a.shape[1] for a in As]
+    offs = [sum(kb[:i]) for i in range(nb)]
+    A_p = (ctypes.c_void_p * nb)(*[a.data_ptr() for a in As])
+    lda = (ctypes.c_int64 * nb)(*[a.stride(0) for a in As])
+    W_p = (ctypes.c_void_p * nb)(*[W.data_ptr() + 4 * o for o in offs])
+    ldw = (ctypes.c_int64 * nb)(*([W.stride(0)] * nb))
+    kbs = (ctypes.c_int64 * nb)(*kb)
+    x = torch.empty(M, N, device=cuda)
+    y = torch.empty(M, N, device=cuda)
+    mean = torch.empty(N, device=cuda)
+    invstd = torch.empty(N, device=cuda)
+    ws = torch.zeros(int(L.hlhgat_bn_workspace_bytes(M, N)), dtype=torch.uint8, device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib.check(L.hlhgat_set_proj_bn_fused(1 if fused else 0), "set_proj_bn_fused")
+    try:
+        _lib.check(L.hlhgat_proj_bn_fwd(
+            nb, A_p, lda, W_p, ldw, kbs, M, N, bias.data_ptr() if bias is not None else None,
+            x.data_ptr(), N, valid.data_ptr() if valid is not None else None,
+            bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+            bn.running_var.data_ptr(), bn.num_batches_tracked.data_ptr(), 0.1, 1e-5,
+            1 if relu else 0, y.data_ptr(), N, mean.data_ptr(), invstd.data_ptr(),
+            ws.data_ptr(), ws.numel(), s), "proj_bn_fwd")
+    finally:
+        L.hlhgat_set_proj_bn_fused(1)
+    torch.cuda.synchronize()
+    return x, y, mean, invstd
+
+
+@pytest.mark.parametrize("M,N,kb,pad,relu,expect_fused", [
+    (23157, 64, [64, 64, 64], 0, True, True),       # cfg2 node conv K=3
+    (25600, 64, [384, 384], 333, True, True),      # NodeEdgeInt Linear(768, 64), padded rows
+    (9728, 128, [128, 128], 0, True, True),        # heads: 128 columns = two BN tiles
+    (700, 256, [256], 0, False, True),             # readout-sized, no ReLU
+    (4097, 64, [36, 36, 36], 5, True, True),       # init conv widths
+    (40000, 64, [64, 64, 64], 0, True, False),     # > 512 row blocks: two calls
+    (3000, 32, [32], 0, True, False)])             # N % 64 != 0: two calls
+def test_proj_bn_fused_matches_two_calls(cuda, M, N, kb, pad, relu, expect_fused):
+    """hlhgat_proj_bn_fwd (k_proj_bn_fwd: projection + BatchNorm + ReLU in one
+    launch, statistics by a last-arriver tree) against its two-call path
+    (hlhgat_proj_fwd, hlhgat_bn_fwd_train): x bitwise, y / batch statistics /
+    running statistics within 1e-6 (fp64 sums in another order), padded rows 0,
+    fused launches deterministic run to run, both against an fp64 evaluation
+    (1e-5)."""
+    import ctypes
+    from hlhgat import _lib, ops
+    cap = ctypes.c_int64(0)
+    _lib.check(_lib.LIB.hlhgat_proj_bn_fused_capacity(ctypes.byref(cap)), "capacity")
+    assert cap.value >= 400  # the cfg2 shapes (<= 400 row blocks) take the fused launch
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    As = [torch.randn(M, k, generator=g).to(cuda) for k in kb]
+    W = (torch.randn(N, sum(kb), generator=g) / sum(kb) ** 0.5).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    valid = torch.tensor([M - pad], dtype=torch.int32, device=cuda) if pad else None
+    res = []
+    for fused in (True, True, False):
+        torch.manual_seed(0)
+        bn = torch.nn.BatchNorm1d(N).to(cuda).train()
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        ops.prof_reset()
+        ops.prof_enable(_lib.PROF_PROJ_BN, True)
+        out = _proj_bn_call(cuda, As, W, bias, bn, valid, relu, fused)
+        ops.prof_enable(_lib.PROF_PROJ_BN, False)
+        launches = ops.prof_read(_lib.PROF_PROJ_BN)["launches"]
+        assert launches == (1 if (fused and expect_fused) else 0), launches
+        res.append(list(out) + [bn.running_mean.clone(), bn.running_var.clone(),
+                                bn.num_batches_tracked.clone()])
+    ops.check_device_errors()
+    (f1, f2, two) = res
+    for a, b in zip(f1, f2):
+        assert torch.equal(a, b)  # deterministic
+    assert torch.equal(f1[0], two[0])  # x: the same GEMM arithmetic
+    for i, nm in ((1, "y"), (2, "mean"), (3, "invstd"), (4, "running_mean"), (5, "running_var")):
+        close(f1[i].cpu(), two[i].cpu(), 1e-6, nm)
+    assert torch.equal(f1[6], two[6])
+    nv = M - pad
+    xr = sum(a.double() @ W[:, o:o + a.shape[1]].double().T
+             for a, o in zip(As, [sum(kb[:i]) for i in range(len(kb))])) + bias.double()
+    ref = torch.nn.functional.batch_norm(xr[:nv], None, None, training=True, eps=1e-5)
+    ref = ref * bn.weight.detach().double() + bn.bias.detach().double()
+    if relu:
+        ref = ref.clamp_min(0)
+    close(f1[1][:nv].cpu(), ref.float().cpu(), 1e-5, "y vs fp64")
+    assert not f1[1][nv:].any()
+
+
+def test_proj_bn_fused_timeout_raises(cuda):
+    """A k_proj_bn_fwd workgroup that gives up waiting for the statistics
+    (poll limit 0) writes NaN rows and raises the device error word."""
+    from hlhgat import _lib, ops
+    ops.check_device_errors()
+    try:
+        _lib.check(_lib.LIB.hlhgat_set_bn_poll_limit(0), "set_bn_poll_limit")
+        As = [torch.randn(25600, 64, device=cuda) for _ in range(3)]
+        W = torch.randn(64, 192, device=cuda)
+        bn = torch.nn.BatchNorm1d(64).to(cuda).train()
+        _, y, _, _ = _proj_bn_call(cuda, As, W, None, bn, None, True, True)
+        with pytest.raises(RuntimeError, match="BatchNorm"):
+            ops.check_device_errors()
+        assert torch.isnan(y).any()
+    finally:
+        _lib.LIB.hlhgat_set_bn_poll_limit(1 << 22)
+        torch.cuda.synchronize()
+        ops.clear_device_errors()

@@ -169,6 +169,47 @@ def main():
         Acat = [a.contiguous() for a in As]
         run(f"proj_bwd_fused {tag}",
             lambda: torch.ops.hlhgat.proj_backward(G, Acat, W, True), 2 * by, 2 * fl)
+    # ---- projection + BatchNorm forward (hlhgat_proj_bn_fwd) -----------------
+    import ctypes
+    from hlhgat import _lib
+    L = _lib.LIB
+    for M, kbs, tag in [(nt, [64, 64, 64], "conv K=3 d=64"), (ns, [384, 384], "Linear(768,64)")]:
+        N = 64
+        As = [rnd(M, k) for k in kbs]
+        W = rnd(N, sum(kbs))
+        bias = rnd(N)
+        bn = torch.nn.BatchNorm1d(N).to(dev).train()
+        nb = len(kbs)
+        offs = [sum(kbs[:i]) for i in range(nb)]
+        A_p = (ctypes.c_void_p * nb)(*[a.data_ptr() for a in As])
+        lda = (ctypes.c_int64 * nb)(*[a.stride(0) for a in As])
+        W_p = (ctypes.c_void_p * nb)(*[W.data_ptr() + 4 * o for o in offs])
+        ldw = (ctypes.c_int64 * nb)(*([W.stride(0)] * nb))
+        kb_ = (ctypes.c_int64 * nb)(*kbs)
+        x = torch.empty(M, N, device=dev)
+        y = torch.empty(M, N, device=dev)
+        mean = torch.empty(N, device=dev)
+        inv = torch.empty(N, device=dev)
+        ws = torch.zeros(int(L.hlhgat_bn_workspace_bytes(M, N)), dtype=torch.uint8, device=dev)
+
+        def pb():
+            L.hlhgat_proj_bn_fwd(nb, A_p, lda, W_p, ldw, kb_, M, N, bias.data_ptr(),
+                                 x.data_ptr(), N, None, bn.weight.data_ptr(),
+                                 bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+                                 bn.running_var.data_ptr(), bn.num_batches_tracked.data_ptr(),
+                                 0.1, 1e-5, 1, y.data_ptr(), N, mean.data_ptr(),
+                                 inv.data_ptr(), ws.data_ptr(), ws.numel(),
+                                 torch.cuda.current_stream().cuda_stream)
+        fl = 2.0 * M * N * sum(kbs)
+        L.hlhgat_set_proj_bn_fused(1)
+        run(f"proj_bn_fwd fused {tag}", pb, None, fl)
+        L.hlhgat_set_bn_poll_limit(0)
+        run(f"proj_bn_fwd fused NO-WAIT (timing probe, NaN rows) {tag}", pb, None, fl)
+        L.hlhgat_set_bn_poll_limit(1 << 22)
+        L.hlhgat_clear_device_errors()
+        L.hlhgat_set_proj_bn_fused(0)
+        run(f"proj_bn_fwd two-call {tag}", pb, None, fl)
+        L.hlhgat_set_proj_bn_fused(1)
     # ---- batch norm ----------------------------------------------------------
     for n, C in [(nt, 64), (ns, 64), (1000, 256)]:
         x = rnd(n, C).requires_grad_(True)
