@@ -1513,6 +1513,18 @@ std::vector<Tensor> take_tap() {
   return out;
 }
 
+// Chain mode (hlhgat.ops.Chains): the HL blocks' node and edge chains stay on
+// their two streams for the whole block section of a forward, so the
+// NodeEdgeInt forward neither waits for the main stream before its edge-side
+// GEMM (its inputs come from the edge chain itself) nor joins the main stream
+// at its end (the edge outputs feed the edge chain); only the exchange of the
+// two first-layer GEMM results remains a cross-stream dependency.
+bool& chain_flag() {
+  static bool on = false;
+  return on;
+}
+void set_chain(bool on) { chain_flag() = on; }
+
 class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
  public:
   static variable_list forward(AutogradContext* ctx, Tensor x_t, Tensor x_s, Tensor rowptr,
@@ -1577,7 +1589,18 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     };
     SideMlp tn, te;
     Fork fk(xt.get_device());
-    fk.side_waits_main();
+    const bool chain = chain_flag();
+    if (chain) {
+      // Ys / h1s are written on the side stream and Yt read there after the
+      // exchange, with no join at the end: keep their blocks for the side stream
+      Yt.record_stream(fk.side);
+      Ys.record_stream(fk.side);
+      h1s.record_stream(fk.side);
+    }
+    // the edge GEMM needs this node's own weight pack (built on the main
+    // stream above) unless a forward-wide pack (nei_prepack) was ordered before
+    // the chains began
+    if (!chain || !has(packed)) fk.side_waits_main();
     {  // edge side: first-layer GEMM on the side stream
       TStreamGuard g(fk.side);
       lin_into(xs, Ws, bs, Ys);
@@ -1605,7 +1628,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
           "poly_step(nei node)");
     }
     side(pn, h1t, mom1n, eps1n, mom4n, eps4n, valid_t, tn);
-    fk.main_waits_side();
+    if (!chain || tap_state().on) fk.main_waits_side();
     if (tap_state().on) {
       tap_state().taken.push_back(tn.a1.clone());
       tap_state().taken.push_back(te.a1.clone());
@@ -2282,6 +2305,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear", &linear);
   m.def("mlp2", &mlp2);
   m.def("nei_value", &nei_value);
+  m.def("set_chain", &set_chain);
   m.def("nei_prepack", &nei_prepack);
   m.def("grad_bucket_set", &grad_bucket_set);
   m.def("grad_bucket_begin", &grad_bucket_begin);

@@ -6,6 +6,8 @@ segment pointers built from num_node1 / num_edge1.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.nn as nn
 from torch.nn import Dropout, Linear
@@ -140,32 +142,39 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         # the incidence build (sort + CSR of |B1|) after HL_init_conv (building it
         # on a third stream beside the conv measured 1.4 % slower: its sort
         # kernels slow the two conv chains more than the overlap saves)
-        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
-                                     edge_weight_s)
-        par_1, D, _ = boundary()
-        if dense:
-            dt.append(x_t)
-            ds.append(x_s)
-        x_s0, x_t0 = x_s, x_t
-        for i, _ in enumerate(self.channels):
-            for j in range(self.channels[i]):
-                neint = getattr(self, "NEInt{}{}".format(i, j))
-                if dense:
-                    x_t0, x_s0 = dt.view(), ds.view()
-                    # its input gradients go straight into the slab's gradient
-                    neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
-                x_t, x_s = neint(x_t0, x_s0, par_1, D)
-                conv = getattr(self, "NEConv{}{}".format(i, j))
-                if dense:
-                    _sink(conv, dt, ds, self.filters[i])
-                x_t, x_s = conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
-                                edge_weight_s)
-                if dense:
-                    dt.append(x_t)
-                    ds.append(x_s)
-                else:
-                    x_t0 = torch.cat([x_t0, x_t], dim=-1)
-                    x_s0 = torch.cat([x_s0, x_s], dim=-1)
+        # the node and edge chains of the block section on two streams with one
+        # cross-stream exchange per block (ops.Chains) where the fused paths run
+        chains = ops.Chains(x_t.device) if dense else contextlib.nullcontext()
+        with chains as ch:
+            x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                         edge_weight_s)
+            par_1, D, _ = boundary()
+            if dense:
+                ch.sync_side()  # the incidence tables (main) feed the edge chain
+                dt.append(x_t)
+                ds.append(x_s)
+            x_s0, x_t0 = x_s, x_t
+            for i, _ in enumerate(self.channels):
+                for j in range(self.channels[i]):
+                    neint = getattr(self, "NEInt{}{}".format(i, j))
+                    if dense:
+                        x_t0, x_s0 = dt.view(), ds.view()
+                        # its input gradients go straight into the slab's gradient
+                        neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
+                    x_t, x_s = neint(x_t0, x_s0, par_1, D)
+                    conv = getattr(self, "NEConv{}{}".format(i, j))
+                    if dense:
+                        _sink(conv, dt, ds, self.filters[i])
+                    x_t, x_s = conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                    edge_weight_s)
+                    if dense:
+                        dt.append(x_t)
+                        ds.append(x_s)
+                    else:
+                        x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                        x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            if dense:
+                x_s = ch.to_main(x_s)
         x = mean_pool_cat([(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
                            (x_t, data.num_node1, getattr(data, "seg_ptr_t", None))])
         for i, _ in enumerate(self.mlp_channels):

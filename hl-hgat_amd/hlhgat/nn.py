@@ -230,9 +230,20 @@ class Sequential(tnn.Module):
         dev = next((a.device for a in args if torch.is_tensor(a)), None)
         if s is None or dev is None:
             return self._run(env, 0, self._n)
-        # node chain on the current stream, edge chain on the side stream
-        from .ops import fork
+        from .ops import active_chains, fork
         side_env = dict(env)
+        ch = active_chains(dev)
+        if ch is not None:
+            # the block section's two chains (ops.Chains): the edge half on the
+            # side stream, no fork wait and no join
+            with torch.cuda.stream(ch.side):
+                self._run(side_env, s, self._n - 1)
+            self._run(env, 0, s)
+            for r in self._routes[s:self._n - 1]:
+                for k in r[1]:
+                    env[k] = side_env[k]
+            return self._run(env, self._n - 1, self._n)
+        # node chain on the current stream, edge chain on the side stream
         side_in = [env[n] for r in self._routes[s:self._n - 1] for n in r[0]
                    if n in env and torch.is_tensor(env[n])]
         fork(lambda: self._run(env, 0, s), lambda: self._run(side_env, s, self._n - 1),

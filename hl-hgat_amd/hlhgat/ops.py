@@ -130,6 +130,77 @@ def _tensors(x):
             yield from _tensors(v)
 
 
+_CHAIN = None  # the active Chains, or None
+
+
+class Chains:
+    """The node and edge chains of a model's HL blocks on two streams for the
+    whole block section of a forward, instead of a fork / join per block
+    (lib/Hodge_ST_Model.py:608-633: each block's node and edge convs are
+    independent; only NodeEdgeInt exchanges features between them).
+
+    Inside ``with Chains(device) as ch:`` a two-chain Sequential (an HL block)
+    runs its edge half on the side stream without waiting for the main stream
+    and without a join, and the fused NodeEdgeInt keeps its edge MLP on the
+    side stream (torch_ext.cpp chain mode): the exchange of the two
+    first-layer GEMM results is the only cross-stream dependency per block.
+    Entering makes the side stream wait for the main stream (the batch, the
+    slabs, the weight packs); ``ch.sync_side()`` does so again (e.g. after
+    tables built on the main stream); leaving joins the side stream into the
+    main stream.  Values are unchanged (the same kernels in the same order on
+    each stream).  A cross-stream hazard of a hipGraph capture is caught the
+    same way as for ``fork``: the side stream is joined before capture end."""
+
+    def __init__(self, device):
+        self.device = device
+        self.on = (_FORK_ENABLED and device is not None and device.type == "cuda"
+                   and _ext is not None)
+
+    def __enter__(self):
+        global _CHAIN
+        if self.on:
+            if _CHAIN is not None:
+                raise RuntimeError("hlhgat: Chains do not nest")
+            self.main = torch.cuda.current_stream(self.device)
+            # the C++ fork's side stream: the fused NodeEdgeInt's edge half runs
+            # there, so the edge convs must too (one edge stream, no syncs between)
+            idx = (self.device.index if self.device.index is not None
+                   else torch.cuda.current_device())
+            self.side = torch.cuda.ExternalStream(int(_ext.fork_side_stream(idx)),
+                                                  device=self.device)
+            self.side.wait_stream(self.main)
+            _CHAIN = self
+            _ext.set_chain(True)
+        return self
+
+    def sync_side(self) -> None:
+        if self.on:
+            self.side.wait_stream(self.main)
+
+    def to_main(self, *ts):
+        """Side-chain tensors handed to the main stream after the join."""
+        if self.on:
+            for t in _tensors(ts):
+                t.record_stream(self.main)
+        return ts if len(ts) != 1 else ts[0]
+
+    def __exit__(self, *exc):
+        global _CHAIN
+        if self.on:
+            _ext.set_chain(False)
+            _CHAIN = None
+            self.main.wait_stream(self.side)
+        return False
+
+
+def active_chains(device):
+    """The active Chains on `device`, or None."""
+    ch = _CHAIN
+    if ch is None or device is None or ch.device != device:
+        return None
+    return ch
+
+
 def fork(fn_main, fn_side, side_inputs=(), device=None, slot=0):
     """Run fn_main() on the current stream and fn_side() on the side stream
     concurrently; returns (fn_main(), fn_side()) with the side results ordered

@@ -154,11 +154,17 @@ def test_graph_replay_equals_eager(cuda):
 
 
 @pytest.mark.gpu
-def test_stream_fork_is_bitwise_neutral(cuda):
+@pytest.mark.parametrize("graphs", [False, True])
+def test_stream_fork_is_bitwise_neutral(cuda, graphs):
+    """Two streams (the block section's node / edge chains, ops.Chains, and
+    the NodeEdgeInt / backward forks) give the bits of one stream: eager and
+    graph-replayed steps over two batch shapes (a missing cross-stream
+    dependency shows up as a changed loss or parameter)."""
     from hlhgat.synthetic import zinc_like_batch
-    batches = [zinc_like_batch(40, seed=7).to(cuda)]
-    l0, sd0, _ = _run(False, False, batches, [0, 0])
-    l1, sd1, _ = _run(False, True, batches, [0, 0])
+    batches = [zinc_like_batch(40, seed=7).to(cuda), zinc_like_batch(33, seed=8).to(cuda)]
+    order = [0, 1, 0, 1, 1, 0]
+    l0, sd0, _ = _run(graphs, False, batches, order)
+    l1, sd1, _ = _run(graphs, True, batches, order)
     assert l0 == l1
     for k in sd0:
         assert torch.equal(sd0[k], sd1[k]), k
