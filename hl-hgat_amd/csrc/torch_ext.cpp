@@ -1524,6 +1524,12 @@ bool& chain_flag() {
   return on;
 }
 void set_chain(bool on) { chain_flag() = on; }
+// the backward half of chain mode (test / A-B hook; on by default)
+bool& chain_bwd_flag() {
+  static bool on = true;
+  return on;
+}
+void set_chain_bwd(bool on) { chain_bwd_flag() = on; }
 
 class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
  public:
@@ -1650,6 +1656,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       ctx->saved_data["edges"] = em.e;
     }
     ctx->saved_data["dims"] = std::vector<int64_t>{N, E, d, dn, de};
+    if (chain && chain_bwd_flag()) ctx->saved_data["chain"] = true;
     ctx->save_for_backward({xt, xs, rowptr, eids, ei, rD, Wt, Ws, pn[2], pn[7], pn[9], pe[2],
                             pe[7], pe[9], tn.h1, tn.a1, tn.m1, tn.i1, tn.h2, tn.y, tn.m4, tn.i4,
                             te.h1, te.a1, te.m1, te.i1, te.h2, te.y, te.m4, te.i4,
@@ -1708,8 +1715,25 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       out[P + 9] = dg4;
       out[P + 10] = dbe4;
     };
+    const bool nW = need(ctx, PN) || need(ctx, PE), nB = need(ctx, PN + 1) || need(ctx, PE + 1);
+    // TrainStep: every unpack destination deferrable -> the Wt / Ws split
+    // reductions are deferred too (their only reader is the deferred unpack)
+    const bool fdef = need(ctx, PN) && need(ctx, PE) && need(ctx, PN + 1) &&
+                      need(ctx, PE + 1) && param_deferrable(sv[30]) && param_deferrable(sv[35]) &&
+                      param_deferrable(sv[31]) && param_deferrable(sv[36]);
+    // chain mode (forward under ops.Chains) with every gradient deferred to the
+    // flush: the edge half starts without waiting for the main stream (its
+    // output gradient comes from the edge chain) and is not joined at the end
+    // (its consumers are the edge chain and the flush, which waits for every
+    // deferring stream); only the exchange stays
+    const bool chain_b = fdef && ctx->saved_data.count("chain") > 0;
     Fork fk(xt.get_device());
-    fk.side_waits_main();
+    if (chain_b) {
+      dYs.record_stream(fk.side);
+      dYt.record_stream(fk.side);
+    } else {
+      fk.side_waits_main();
+    }
     {  // edge side MLP backward on the side stream -> dYs[:, :de]
       TStreamGuard g(fk.side);
       side_bwd(grads[1], PE, sv[11], sv[12], sv[13], 22, dYs.narrow(1, 0, de), 35, sv[41]);
@@ -1737,12 +1761,6 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                            dYt.data_ptr<float>() + dn, dn + de, fk.main.stream()),
           "poly_step(nei node bwd)");
     }
-    const bool nW = need(ctx, PN) || need(ctx, PE), nB = need(ctx, PN + 1) || need(ctx, PE + 1);
-    // TrainStep: every unpack destination deferrable -> the Wt / Ws split
-    // reductions are deferred too (their only reader is the deferred unpack)
-    const bool fdef = need(ctx, PN) && need(ctx, PE) && need(ctx, PN + 1) &&
-                      need(ctx, PE + 1) && param_deferrable(sv[30]) && param_deferrable(sv[35]) &&
-                      param_deferrable(sv[31]) && param_deferrable(sv[36]);
     Tensor dWt, dbt, dWs, dbs;
     std::vector<Tensor> dxt, dxs;
     {
@@ -1757,7 +1775,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     const std::vector<Tensor> into_t{ht ? ctx->saved_data["gsink_t"].toTensor() : Tensor()};
     linear_backward(dYt, {xt}, Wt, nW, nB, {need(ctx, 0)}, dWt, dbt, dxt, nullptr,
                     ht ? &into_t : nullptr, ht ? sink_accumulate(ctx, "gflag_t") : 0, fdef);
-    fk.main_waits_side();
+    if (!chain_b) fk.main_waits_side();
     fk.escape({dWs, dbs, dxs[0], out[PE + 2], out[PE + 3], out[PE + 7], out[PE + 8], out[PE + 9],
                out[PE + 10]});
     out[0] = dxt[0];
@@ -2306,6 +2324,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp2", &mlp2);
   m.def("nei_value", &nei_value);
   m.def("set_chain", &set_chain);
+  m.def("set_chain_bwd", &set_chain_bwd);
   m.def("nei_prepack", &nei_prepack);
   m.def("grad_bucket_set", &grad_bucket_set);
   m.def("grad_bucket_begin", &grad_bucket_begin);

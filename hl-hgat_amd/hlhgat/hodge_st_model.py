@@ -158,9 +158,13 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                 for j in range(self.channels[i]):
                     neint = getattr(self, "NEInt{}{}".format(i, j))
                     if dense:
-                        x_t0, x_s0 = dt.view(), ds.view()
+                        x_t0 = dt.view()
+                        gs_t = dt.grad_sink()
+                        with ch.side_context():  # the edge slab's view / gradient: edge chain
+                            x_s0 = ds.view()
+                            gs_s = ds.grad_sink()
                         # its input gradients go straight into the slab's gradient
-                        neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
+                        neint._hlhgat_gsink = (gs_t, gs_s)
                     x_t, x_s = neint(x_t0, x_s0, par_1, D)
                     conv = getattr(self, "NEConv{}{}".format(i, j))
                     if dense:

@@ -7,6 +7,7 @@ reproduces are cited per function (paths relative to deepika090/HL-HGAT).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 import os
@@ -131,6 +132,7 @@ def _tensors(x):
 
 
 _CHAIN = None  # the active Chains, or None
+CHAINS_ENABLED = True  # A/B hook: False = a fork / join per HL block
 
 
 class Chains:
@@ -153,8 +155,8 @@ class Chains:
 
     def __init__(self, device):
         self.device = device
-        self.on = (_FORK_ENABLED and device is not None and device.type == "cuda"
-                   and _ext is not None)
+        self.on = (CHAINS_ENABLED and _FORK_ENABLED and device is not None
+                   and device.type == "cuda" and _ext is not None)
 
     def __enter__(self):
         global _CHAIN
@@ -176,6 +178,10 @@ class Chains:
     def sync_side(self) -> None:
         if self.on:
             self.side.wait_stream(self.main)
+
+    def side_context(self):
+        """Issue (and record for autograd) on the edge chain's stream."""
+        return torch.cuda.stream(self.side) if self.on else contextlib.nullcontext()
 
     def to_main(self, *ts):
         """Side-chain tensors handed to the main stream after the join."""
