@@ -43,7 +43,15 @@ struct FwdArgs {
 // each lane streams its A row chunk straight into registers one chunk ahead.
 // ---------------------------------------------------------------------------
 constexpr int KC = 64;
-constexpr int KCP = KC + 4;
+// LDS row pitch of a staged W chunk: 64 floats, with the 16-B slots of row r
+// XOR-swizzled by r & 15 (slot k/4 of row r lives at slot (k/4) ^ (r & 15)).
+// A ds_read_b128 lane group of the main loop (lanes (q, i) reading row
+// tn*16 + i, slot 4s + q) then touches 16 distinct slots and a ds_write_b128
+// group of 8 lanes 8 distinct bank quads: both conflict-free
+// (MI355X_MICROARCH.md §LDS), where the former 68-float padding left the
+// reads 2-way conflicted (SQ_LDS_BANK_CONFLICT ~0.4 of the LDS cycles).
+constexpr int KCP = KC;
+__device__ __forceinline__ int wswz(int row, int slot) { return slot ^ (row & 15); }
 
 template <int TN>
 struct WStage {
@@ -75,7 +83,7 @@ __device__ __forceinline__ void store_w_chunk(float (*lds)[KCP], const WStage<TN
   for (int u = 0; u < TN; ++u) {
     const int idx = threadIdx.x + 256 * u;
     const int r = idx >> 4, c4 = idx & 15;
-    *reinterpret_cast<float4*>(&lds[r][4 * c4]) = st.v[u];
+    *reinterpret_cast<float4*>(&lds[r][4 * wswz(r, c4)]) = st.v[u];
   }
 }
 
@@ -193,7 +201,7 @@ __device__ __forceinline__ void proj_fwd_lds_mainloop(const FwdArgs& a, int bx, 
       float4 bf[TN];
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
-        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][16 * s + 4 * q]);
+        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][4 * wswz(i, 4 * s + q)]);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         acc[tn] = mfma16(ac[s].x, bf[tn].x, acc[tn]);

@@ -452,7 +452,21 @@ __global__ __launch_bounds__(256) void k_segment_mean_fwd(SegArgs a) {
     vt acc;
 #pragma unroll
     for (int c = 0; c < V; ++c) vget(acc, c) = 0.f;
-    for (int t = r0; t < r1; ++t) {
+    int t = r0;
+    // 8 member rows in flight, summed in member order (the sequential sum)
+    for (; t + 8 <= r1; t += 8) {
+      vt xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t r = a.rows ? a.rows[t + u] : t + u;
+        xv[u] = vload<V>(a.x + r * a.ldx + f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int c = 0; c < V; ++c) vget(acc, c) = vget(acc, c) + vget(xv[u], c);
+    }
+    for (; t < r1; ++t) {
       const int64_t r = a.rows ? a.rows[t] : t;
       vt xv = vload<V>(a.x + r * a.ldx + f);
 #pragma unroll

@@ -266,12 +266,14 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
 
 
   // staging: TN*16 columns x 64 n = TN*256 float4 over 256 threads; thread
-  // loads W[n][c4*4 .. +3] (16 float4 per n row) and scatters 4 floats.
+  // loads W[n][c4*4 .. +3] (a half-wave covers 32 consecutive n of one c4)
+  // and scatters the 4 floats into the transposed, swizzled tile
+  // (conflict-free ds_write_b32: the 32 lanes hit 32 distinct banks)
   auto load_w = [&](int n0, float4 (&st)[TN]) {
 #pragma unroll
     for (int u = 0; u < TN; ++u) {
       const int idx = threadIdx.x + 256 * u;
-      const int nl = idx / (TN * 4), c4 = idx % (TN * 4);
+      const int nl = idx & 63, c4 = idx >> 6;
       const int n = n0 + nl, c = c_base + 4 * c4;
       if (n < a.N && c < kb)
         st[u] = *reinterpret_cast<const float4*>(W + (int64_t)n * ldw + c);
@@ -283,11 +285,12 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
 #pragma unroll
     for (int u = 0; u < TN; ++u) {
       const int idx = threadIdx.x + 256 * u;
-      const int nl = idx / (TN * 4), c4 = idx % (TN * 4);
-      lds[4 * c4 + 0][nl] = st[u].x;
-      lds[4 * c4 + 1][nl] = st[u].y;
-      lds[4 * c4 + 2][nl] = st[u].z;
-      lds[4 * c4 + 3][nl] = st[u].w;
+      const int nl = idx & 63, c4 = idx >> 6;
+      const int r0 = 4 * c4;
+      lds[r0 + 0][4 * wswz(r0 + 0, nl >> 2) + (nl & 3)] = st[u].x;
+      lds[r0 + 1][4 * wswz(r0 + 1, nl >> 2) + (nl & 3)] = st[u].y;
+      lds[r0 + 2][4 * wswz(r0 + 2, nl >> 2) + (nl & 3)] = st[u].z;
+      lds[r0 + 3][4 * wswz(r0 + 3, nl >> 2) + (nl & 3)] = st[u].w;
     }
   };
 
@@ -312,7 +315,7 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
       float4 bf[TN];
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
-        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][16 * s + 4 * q]);
+        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][4 * wswz(i, 4 * s + q)]);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         acc[tn] = mfma16(gc[s].x, bf[tn].x, acc[tn]);
@@ -334,6 +337,93 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
   const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
   store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
                       a.accumulate, vec_ok);
+}
+
+// Data gradient, one workgroup per 64-row block covering EVERY column tile of
+// every block (N <= 64: the workgroup's whole dC chunk stays in registers), so
+// dC is read once per row block instead of once per column tile; the W tiles
+// go through two LDS buffers (the next one loaded while the current one feeds
+// the MFMAs) and the epilogue has its own scratch.  Per element the same MFMA
+// sequence as bwd_data_lds_body: bitwise the same dA.
+template <int TN>
+__device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx, float* lds) {
+  float (*wl)[TN * 16][KCP] = reinterpret_cast<float (*)[TN * 16][KCP]>(lds);
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int q = lane >> 4, i = lane & 15;
+  float* scratch = lds + 2 * TN * 16 * KCP + wave * 16 * (TN * 16 + 4);
+  const int64_t m_base = ((int64_t)bx * 4 + wave) * 16;
+  const int64_t row = m_base + i;
+  const bool gval = row < a.M;
+  float4 gc[4];
+  load_a_chunk(a.G + (gval ? row : 0) * a.ldg, gval, 0, a.N, q, gc);
+  const int ntiles = a.tile_start[a.nb];
+  auto tile_of = [&](int t, int& b, int& c_base) {
+    b = 0;
+    while (b + 1 < a.nb && t >= a.tile_start[b + 1]) ++b;
+    c_base = (t - a.tile_start[b]) * (TN * 16);
+  };
+  auto load_w = [&](int t, float4 (&st)[TN]) {  // as bwd_data_lds_body's staging
+    int b, c_base;
+    tile_of(t, b, c_base);
+    const float* __restrict__ W = a.W[b];
+    const int64_t ldw = a.ldw[b];
+    const int kb = a.kb[b];
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int nl = idx & 63, c4 = idx >> 6;
+      const int c = c_base + 4 * c4;
+      st[u] = (nl < a.N && c < kb) ? *reinterpret_cast<const float4*>(W + (int64_t)nl * ldw + c)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_w = [&](float (*dst)[KCP], const float4 (&st)[TN]) {
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int idx = threadIdx.x + 256 * u;
+      const int nl = idx & 63, c4 = idx >> 6;
+      const int r0 = 4 * c4;
+      dst[r0 + 0][4 * wswz(r0 + 0, nl >> 2) + (nl & 3)] = st[u].x;
+      dst[r0 + 1][4 * wswz(r0 + 1, nl >> 2) + (nl & 3)] = st[u].y;
+      dst[r0 + 2][4 * wswz(r0 + 2, nl >> 2) + (nl & 3)] = st[u].z;
+      dst[r0 + 3][4 * wswz(r0 + 3, nl >> 2) + (nl & 3)] = st[u].w;
+    }
+  };
+  float4 wst[TN];
+  load_w(0, wst);
+  store_w(wl[0], wst);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const bool has_next = t + 1 < ntiles;
+    if (has_next) load_w(t + 1, wst);
+    floatx4 acc[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float4 bf[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][4 * wswz(i, 4 * s + q)]);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        acc[tn] = mfma16(gc[s].x, bf[tn].x, acc[tn]);
+        acc[tn] = mfma16(gc[s].y, bf[tn].y, acc[tn]);
+        acc[tn] = mfma16(gc[s].z, bf[tn].z, acc[tn]);
+        acc[tn] = mfma16(gc[s].w, bf[tn].w, acc[tn]);
+      }
+    }
+    int b, c_base;
+    tile_of(t, b, c_base);
+    const int ncols = a.kb[b] - c_base < TN * 16 ? a.kb[b] - c_base : TN * 16;
+    const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
+    store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
+                        a.accumulate, vec_ok);
+    if (has_next) store_w(wl[buf ^ 1], wst);
+    __syncthreads();
+  }
 }
 
 template <int TN>
@@ -716,12 +806,16 @@ struct BwdFusedArgs {
   ReduceArgs red;
 };
 
-template <int TND>
+template <int TND, bool ROWS>
 __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
   const int L = (int)blk.x;
   if (L >= a.n_wpad + a.n_d) {
     const int l = L - a.n_wpad - a.n_d;
     if (l < a.n_red) reduce_splits_body(a.red, Blk{(unsigned)l, 0u, (unsigned)a.n_red, 1u});
+    return;
+  }
+  if (ROWS && L >= a.n_wpad) {  // one workgroup per row block, every column tile
+    bwd_data_rows_body<TND>(a.d, L - a.n_wpad, lds);
     return;
   }
   if (L >= a.n_wpad) {
@@ -752,11 +846,19 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
                     reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
-template <int TND>
+template <int TND, bool ROWS>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
-  constexpr int kW = 2 * WR * 64 * 2, kD = 2 * TND * 16 * KCP;
+  // ROWS: two W buffers + the epilogue scratch (bwd_data_rows_body)
+  constexpr int kW = 2 * WR * 64 * 2;
+  constexpr int kD = ROWS ? 2 * TND * 16 * KCP + 4 * 16 * (TND * 16 + 4) : 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
-  proj_bwd_fused_body<TND>(a, blk_hw(), lds);
+  proj_bwd_fused_body<TND, ROWS>(a, blk_hw(), lds);
+}
+
+// A/B hook (hlhgat_set_proj_bwd_rows): row-block data-gradient workgroups
+bool& proj_bwd_rows_flag() {
+  static bool v = true;
+  return v;
 }
 
 // --- planning ------------------------------------------------------------------
@@ -1166,7 +1268,13 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   f.d_gx = (int)ceil_div(M, 4 * 16);
   f.n_wpad = (f.n_w + 7) & ~7;
-  f.n_d = f.d_gx * d.tile_start[nb_d];
+  // N <= 64 (one dC chunk): one data workgroup per row block for every column
+  // tile (dC read once); else one per (row block, column tile)
+  bool vec_d = aligned16(dC) && lddc % 4 == 0;
+  for (int b = 0; b < nb_d; ++b)
+    vec_d = vec_d && aligned16(W[b]) && ldw[b] % 4 == 0 && kb_d[b] % 4 == 0;
+  const bool rows = proj_bwd_rows_flag() && tnd == 4 && N <= KC && vec_d;
+  f.n_d = rows ? f.d_gx : f.d_gx * d.tile_start[nb_d];
   f.d_xcd = data_xcd_map();
   if (prev) {
     f.red = *prev;
@@ -1189,12 +1297,14 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   bytes += 4.0 * (double)p.splits * p.part_stride;
   ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-  if (tnd == 1)
-    launch(k_proj_bwd_fused<1>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  if (rows)
+    launch(k_proj_bwd_fused<4, true>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else if (tnd == 1)
+    launch(k_proj_bwd_fused<1, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else if (tnd == 2)
-    launch(k_proj_bwd_fused<2>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+    launch(k_proj_bwd_fused<2, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else
-    launch(k_proj_bwd_fused<4>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+    launch(k_proj_bwd_fused<4, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
@@ -1242,4 +1352,9 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
   return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias,
                        nb_d, W, ldw, kb_d, dA, ldda, accumulate_d, workspace, workspace_floats,
                        stream);
+}
+
+extern "C" int hlhgat_set_proj_bwd_rows(int on) {
+  proj_bwd_rows_flag() = on != 0;
+  return HLHGAT_OK;
 }

@@ -147,11 +147,10 @@ hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_e
 // earlier on that stream still holds its address, and a replay must not write
 // BN counters into memory the caching allocator has handed to another tensor.
 // (Sizes grow geometrically, so at most a handful are ever retired.)
-Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
+Tensor bn_workspace_for(void* stream, int device, int64_t need) {
   static auto* cache = new std::unordered_map<uintptr_t, Tensor>();  // leaked: outlives HIP teardown
   static auto* retired = new std::vector<Tensor>();
-  const uintptr_t key = reinterpret_cast<uintptr_t>(stream_of(like)) * 64 + like.get_device();
-  const int64_t need = hlhgat_bn_workspace_bytes(n, C);
+  const uintptr_t key = reinterpret_cast<uintptr_t>(stream) * 64 + device;
   auto it = cache->find(key);
   if (it == cache->end() || it->second.numel() < need) {
     int64_t bytes = std::max<int64_t>(need, 1 << 20);
@@ -159,11 +158,27 @@ Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
       bytes = std::max<int64_t>(bytes, 2 * it->second.numel());
       retired->push_back(it->second);
     }
-    Tensor ws = at::empty({bytes}, like.options().dtype(at::kByte));
-    chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream_of(like)), "zero_fill");
+    Tensor ws = at::empty({bytes}, at::TensorOptions()
+                                        .device(at::kCUDA, (c10::DeviceIndex)device)
+                                        .dtype(at::kByte));
+    chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream), "zero_fill");
     (*cache)[key] = ws;
   }
   return (*cache)[key];
+}
+
+Tensor bn_workspace(const Tensor& like, int64_t n, int64_t C) {
+  return bn_workspace_for(stream_of(like), like.get_device(), hlhgat_bn_workspace_bytes(n, C));
+}
+
+// A workspace for `stream` big enough for C channels, zero-filled and
+// synchronised NOW: hlhgat.train.TrainStep calls it before a capture, so the
+// zero fill of a workspace first met during the capture is not recorded into
+// the graph (and replayed every step; the counters reset themselves).
+void bn_workspace_reserve(int64_t stream, int64_t device, int64_t C) {
+  void* s = reinterpret_cast<void*>(stream);
+  bn_workspace_for(s, (int)device, hlhgat_bn_workspace_bytes(1, C));
+  TORCH_CHECK(hipStreamSynchronize((hipStream_t)s) == hipSuccess, "hlhgat: hipStreamSynchronize");
 }
 
 // ---------------------------------------------------------------------------
@@ -1198,8 +1213,31 @@ class LinearFn : public torch::autograd::Function<LinearFn> {
   }
 };
 
+// Activation tap (test infrastructure, hlhgat.nn.TAP): while on, the
+// NodeEdgeInt value node and the two-layer MLP node keep a copy of their
+// hidden post-ReLU activations (NodeEdgeInt: node side, then edge side) for
+// the frozen-mask gradient checks.
+struct TapState {
+  bool on = false;
+  std::vector<Tensor> taken;
+};
+TapState& tap_state() {
+  static auto* t = new TapState();
+  return *t;
+}
+void set_tap(bool on) {
+  tap_state().on = on;
+  tap_state().taken.clear();
+}
+std::vector<Tensor> take_tap() {
+  std::vector<Tensor> out;
+  out.swap(tap_state().taken);
+  return out;
+}
+
 // ---------------------------------------------------------------------------
-// NodeEdgeInt WV_* : Linear(blocks) -> BN -> ReLU -> Linear -> BN -> ReLU
+// Linear(blocks) -> BN -> ReLU -> Linear -> BN -> ReLU (NodeEdgeInt WV_*, two
+// layers of a readout MLP)
 // ---------------------------------------------------------------------------
 class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
  public:
@@ -1219,6 +1257,7 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
                                   true, h1, m1, i1);
     Tensor y = linear_bn_forward({a1}, W3c, b3, BnState{g4, be4, rm4, rv4, nbt4, mom4, eps4},
                                  true, h2, m4, i4);
+    if (tap_state().on) tap_state().taken.push_back(a1.clone());  // the hidden ReLU
     ctx->saved_data["nb"] = (int64_t)blocks.size();
     {
       EdgeMap em;
@@ -1492,26 +1531,6 @@ int sink_accumulate(AutogradContext* ctx, const char* key) {
   return acc;
 }
 
-// Activation tap (test infrastructure, hlhgat.nn.TAP): while on, the
-// NodeEdgeInt value node keeps a copy of its hidden post-ReLU activations
-// (node side, then edge side) for the frozen-mask gradient checks.
-struct TapState {
-  bool on = false;
-  std::vector<Tensor> taken;
-};
-TapState& tap_state() {
-  static auto* t = new TapState();
-  return *t;
-}
-void set_tap(bool on) {
-  tap_state().on = on;
-  tap_state().taken.clear();
-}
-std::vector<Tensor> take_tap() {
-  std::vector<Tensor> out;
-  out.swap(tap_state().taken);
-  return out;
-}
 
 // Chain mode (hlhgat.ops.Chains): the HL blocks' node and edge chains stay on
 // their two streams for the whole block section of a forward, so the
@@ -2324,6 +2343,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp2", &mlp2);
   m.def("nei_value", &nei_value);
   m.def("set_chain", &set_chain);
+  m.def("bn_workspace_reserve", &bn_workspace_reserve);
   m.def("set_chain_bwd", &set_chain_bwd);
   m.def("nei_prepack", &nei_prepack);
   m.def("grad_bucket_set", &grad_bucket_set);

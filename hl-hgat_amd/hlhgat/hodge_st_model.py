@@ -16,7 +16,7 @@ from . import ops
 from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt, cluster_mean
 from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
-from .nn import BatchNorm, Sequential, run_sequential
+from .nn import BatchNorm, Sequential, run_mlp_stack
 
 __all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr",
            "HL_HGCNN_CIFAR10SP_dense_int3_attpool", "HL_HGCNN_pepfunc_dense_int3_attpool",
@@ -41,16 +41,20 @@ def mean_pool_sorted(x: torch.Tensor, counts: torch.Tensor,
     return ops.segment_mean(x, ptr, counts.numel())
 
 
-def mean_pool_cat(parts) -> torch.Tensor:
+READOUT_ON_CHAIN = True  # A/B hook: False = the edge readout on the main stream
+
+
+def mean_pool_cat(parts, side=None) -> torch.Tensor:
     """torch.cat([mean_pool_sorted(x, counts, ptr) ...], -1) as one output
     written block by block (ops.segment_mean_cat): the readout of
-    lib/Hodge_ST_Model.py:636 without the cat launch."""
+    lib/Hodge_ST_Model.py:636 without the cat launch.  side: the edge chain's
+    stream for the first part (ops.Chains)."""
     ptrs = []
     for x, counts, ptr in parts:
         if ptr is None or ptr.device != x.device or ptr.numel() != counts.numel() + 1:
             ptr = segment_ptr(counts, x.device)
         ptrs.append(ptr)
-    return ops.segment_mean_cat([x for x, _, _ in parts], ptrs, parts[0][1].numel())
+    return ops.segment_mean_cat([x for x, _, _ in parts], ptrs, parts[0][1].numel(), side=side)
 
 
 def _hl_block(cin_t, cin_s, cout, K, dropout_ratio, act=nn.ReLU):
@@ -177,12 +181,12 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                     else:
                         x_t0 = torch.cat([x_t0, x_t], dim=-1)
                         x_s0 = torch.cat([x_s0, x_s], dim=-1)
-            if dense:
-                x_s = ch.to_main(x_s)
-        x = mean_pool_cat([(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
-                           (x_t, data.num_node1, getattr(data, "seg_ptr_t", None))])
-        for i, _ in enumerate(self.mlp_channels):
-            x = run_sequential(getattr(self, "mlp%d" % i), [x])
+            # the readout; x_s's mean on the edge chain (joined when the chains end)
+            x = mean_pool_cat([(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
+                               (x_t, data.num_node1, getattr(data, "seg_ptr_t", None))],
+                              side=ch.side if (dense and ch.on and READOUT_ON_CHAIN) else None)
+        x = run_mlp_stack([getattr(self, "mlp%d" % i) for i in range(len(self.mlp_channels))],
+                          [x])
         y = ops.linear_blocks([x], self.out.weight, self.out.bias)
         if if_final_layer:
             return x, y
@@ -441,8 +445,8 @@ class _AttPoolHead(nn.Module):
                 f"pool_loc={self.pool_loc} must be below the last of {len(self.channels)} levels")
         x = mean_pool_cat([(x_s, dr.num_edge1, getattr(dr, "seg_ptr_s", None)),
                            (x_t, dr.num_node1, getattr(dr, "seg_ptr_t", None))])
-        for i, _ in enumerate(self.mlp_channels):
-            x = run_sequential(getattr(self, "mlp%d" % i), [x])
+        x = run_mlp_stack([getattr(self, "mlp%d" % i) for i in range(len(self.mlp_channels))],
+                          [x])
         y = ops.linear_blocks([x], self.out.weight, self.out.bias)
         if if_final_layer:
             return x, y

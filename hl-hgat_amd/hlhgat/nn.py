@@ -290,6 +290,51 @@ def run_sequential(seq: tnn.Sequential, blocks) -> torch.Tensor:
     return h
 
 
+def _bn_relu_layer(mods, i):
+    """mods[i:i+3] is Linear -> training-mode BatchNorm1d -> ReLU."""
+    from .ops import sync_bn_group
+    return (i + 3 <= len(mods) and isinstance(mods[i], tnn.Linear)
+            and isinstance(mods[i + 1], tnn.BatchNorm1d) and isinstance(mods[i + 2], tnn.ReLU)
+            and (mods[i + 1].training or not mods[i + 1].track_running_stats)
+            and sync_bn_group(mods[i + 1]) is None)
+
+
+MLP_PAIRS = True  # A/B hook: False = run_mlp_stack runs module by module
+
+
+def run_mlp_stack(seqs, blocks) -> torch.Tensor:
+    """The readout MLP of the heads (consecutive nn.Sequential layers Linear ->
+    BatchNorm1d -> ReLU -> Dropout, lib/Hodge_ST_Model.py:589-597): identity
+    dropouts dropped, every two consecutive Linear -> BN -> ReLU layers run as
+    ONE fused node (ops.mlp2: each Linear + BatchNorm in one launch), the rest
+    module by module (run_sequential).  The same arithmetic as running the
+    layers one by one."""
+    from . import ops
+    mods = [m for seq in seqs for m in seq
+            if not (isinstance(m, tnn.Dropout) and (m.p == 0.0 or not m.training))]
+    h, i = None, 0
+    while i < len(mods):
+        if MLP_PAIRS and _bn_relu_layer(mods, i) and _bn_relu_layer(mods, i + 3):
+            tapping = TAP is not None
+            if tapping:
+                ops._ext.set_tap(True)
+            h = ops.mlp2(blocks if h is None else [h], mods[i:i + 6])
+            if tapping:
+                hidden = ops._ext.take_tap()
+                ops._ext.set_tap(False)
+                tap(mods[i + 2], hidden[0])
+                tap(mods[i + 5], h)
+            i += 6
+        else:
+            j = i + 1
+            while j < len(mods) and not (MLP_PAIRS and _bn_relu_layer(mods, j)
+                                         and _bn_relu_layer(mods, j + 3)):
+                j += 1
+            h = run_sequential(tnn.Sequential(*mods[i:j]), blocks if h is None else [h])
+            i = j
+    return h
+
+
 def global_mean_pool(x: torch.Tensor, batch: torch.Tensor, size: int = None) -> torch.Tensor:
     """torch_geometric.nn.global_mean_pool over a sorted batch vector
     (PairData batches are graph-contiguous), on the HIP segment-mean kernel."""

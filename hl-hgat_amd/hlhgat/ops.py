@@ -1245,16 +1245,22 @@ class _SegmentMeanCatFn(torch.autograd.Function):
     straight into its column block (no cat launch); contiguous segments."""
 
     @staticmethod
-    def forward(ctx, n_seg, ptrs, *xs):
+    def forward(ctx, n_seg, ptrs, side, *xs):
+        # side: the edge chain's stream (ops.Chains) for part 0, whose input
+        # was produced there and whose gradient is consumed there
         widths = [x.size(1) for x in xs]
         out = torch.empty(n_seg, sum(widths), device=xs[0].device, dtype=xs[0].dtype)
+        if side is not None:
+            out.record_stream(side)
         c0 = 0
-        for x, p, w in zip(xs, ptrs, widths):
+        for i, (x, p, w) in enumerate(zip(xs, ptrs, widths)):
+            st = side.cuda_stream if (side is not None and i == 0) else _stream(x)
             check(LIB.hlhgat_segment_mean_fwd(p.data_ptr(), None, n_seg, x.data_ptr(), _ld(x), w,
-                                              out.data_ptr() + 4 * c0, _ld(out), _stream(x)),
+                                              out.data_ptr() + 4 * c0, _ld(out), st),
                   "segment_mean_fwd")
             c0 += w
         ctx.meta = (n_seg, widths, [x.size(0) for x in xs])
+        ctx.side = side
         ctx.save_for_backward(*ptrs)
         return out
 
@@ -1262,19 +1268,28 @@ class _SegmentMeanCatFn(torch.autograd.Function):
     def backward(ctx, g):
         n_seg, widths, rows = ctx.meta
         g = _rows2d(g, "grad").contiguous()
+        side = ctx.side
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(g.device))
+            g.record_stream(side)
         gx, c0 = [], 0
-        for p, w, n in zip(ctx.saved_tensors, widths, rows):
-            t = torch.empty(n, w, device=g.device, dtype=g.dtype)
-            check(LIB.hlhgat_segment_mean_bwd(p.data_ptr(), None, n_seg, g.data_ptr() + 4 * c0,
-                                              _ld(g), w, t.data_ptr(), _ld(t), n, _stream(g)),
-                  "segment_mean_bwd")
+        for i, (p, w, n) in enumerate(zip(ctx.saved_tensors, widths, rows)):
+            on_side = side is not None and i == 0
+            with (torch.cuda.stream(side) if on_side else contextlib.nullcontext()):
+                t = torch.empty(n, w, device=g.device, dtype=g.dtype)
+                check(LIB.hlhgat_segment_mean_bwd(p.data_ptr(), None, n_seg,
+                                                  g.data_ptr() + 4 * c0, _ld(g), w, t.data_ptr(),
+                                                  _ld(t), n, _stream(t)),
+                      "segment_mean_bwd")
+            if on_side:
+                t.record_stream(torch.cuda.current_stream(g.device))
             gx.append(t)
             c0 += w
-        return (None, None, *gx)
+        return (None, None, None, *gx)
 
 
 def segment_mean_cat(xs: Sequence[torch.Tensor], seg_ptrs: Sequence[torch.Tensor],
-                     n_seg: int) -> torch.Tensor:
+                     n_seg: int, side=None) -> torch.Tensor:
     """torch.cat([segment_mean(x, p, n_seg) for x, p in zip(xs, seg_ptrs)], -1)
     (the readout x = cat(mean_pool(x_s), mean_pool(x_t)),
     lib/Hodge_ST_Model.py:636) without the cat: bitwise the same values."""
@@ -1286,7 +1301,7 @@ def segment_mean_cat(xs: Sequence[torch.Tensor], seg_ptrs: Sequence[torch.Tensor
         if p.numel() != n_seg + 1:
             raise RuntimeError(f"hlhgat: segment_mean_cat: seg_ptr has {p.numel()} entries, "
                                f"expected {n_seg + 1}")
-    return _SegmentMeanCatFn.apply(int(n_seg), list(seg_ptrs), *xs)
+    return _SegmentMeanCatFn.apply(int(n_seg), list(seg_ptrs), side, *xs)
 
 
 def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,

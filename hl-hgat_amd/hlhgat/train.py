@@ -85,6 +85,9 @@ def batch_key(batch) -> Tuple:
     return tuple(key)
 
 
+BN_RESERVE_CHANNELS = 2048  # BatchNorm workspace reserved per capture stream
+
+
 class _Captured:
     def __init__(self, graph, static_batch, loss):
         self.graph = graph
@@ -282,6 +285,14 @@ class TrainStep:
             self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         s = self._stream
+        if self._ext is not None and BN_RESERVE_CHANNELS:
+            # BatchNorm workspaces of every stream the capture uses, made (and
+            # zeroed) outside the capture: no zero fill recorded into the graph
+            idx = self.device.index if self.device.index is not None else \
+                torch.cuda.current_device()
+            for h in [s.cuda_stream, int(self._ext.fork_side_stream(idx))] + \
+                    [ops.side_stream(self.device, k).cuda_stream for k in (0, 1)]:
+                self._ext.bn_workspace_reserve(int(h), idx, BN_RESERVE_CHANNELS)
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
         with torch.cuda.graph(g, pool=self._pool, stream=s):

@@ -571,6 +571,10 @@ int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
                        float momentum, float eps, int relu, float* y, int64_t ldy,
                        float* save_mean, float* save_invstd, void* workspace,
                        int64_t workspace_bytes, void* stream);
+/* 0: the fused Linear backward (hlhgat_proj_bwd / _defer) uses one
+ * data-gradient workgroup per (row block, 64-column tile) instead of one per
+ * row block covering every column tile (N <= 64); bitwise the same (tests). */
+int hlhgat_set_proj_bwd_rows(int on);
 /* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
 int hlhgat_set_proj_bn_fused(int on);
 /* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */

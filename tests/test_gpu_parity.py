@@ -437,10 +437,10 @@ def test_padded_batch_readout_grad_padding_rows_exactly_zero(cuda, monkeypatch):
     seen = {}
     real = ops.segment_mean_cat
 
-    def spy(xs, ptrs, n_seg):
+    def spy(xs, ptrs, n_seg, side=None):
         for i, x in enumerate(xs):
             x.register_hook(lambda gr, i=i: seen.__setitem__(i, gr.detach().clone()))
-        return real(xs, ptrs, n_seg)
+        return real(xs, ptrs, n_seg, side=side)
 
     monkeypatch.setattr(hodge_st_model.ops, "segment_mean_cat", spy)
     torch.manual_seed(0)
@@ -1117,6 +1117,40 @@ def test_fused_linear_backward_bitwise(cuda, M):
         for u, v, r in zip(a, c, ref):
             assert torch.equal(u, v)
             close(u.cpu(), r.cpu(), 1e-4, "linear grad vs torch")
+
+
+@pytest.mark.parametrize("M", [9000, 25000])
+@pytest.mark.parametrize("widths,N", [([64, 64, 64], 64), ([384, 384], 64), ([36, 36, 36], 32),
+                                      ([128], 48)])
+def test_fused_linear_backward_row_blocks_bitwise(cuda, M, widths, N):
+    """The fused Linear backward's data gradient with one workgroup per row
+    block covering every column tile (N <= 64, hlhgat_set_proj_bwd_rows) ==
+    one workgroup per (row block, column tile), bit for bit, and both against
+    torch: the conv (K = 3, d = 64), NodeEdgeInt Linear(768, 64) and
+    narrower shapes."""
+    from hlhgat import _lib, ops
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    blocks = [torch.randn(M, k, generator=g).to(cuda) for k in widths]
+    W = torch.randn(N, sum(widths), generator=g).to(cuda) * 0.1
+    b = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda)
+
+    def run():
+        xs = [t.clone().requires_grad_(True) for t in blocks]
+        Wv, bv = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        (ops.linear_blocks(xs, Wv, bv) * R).sum().backward()
+        return [Wv.grad, bv.grad] + [x.grad for x in xs]
+    res = []
+    for rows in (1, 0):
+        _lib.check(_lib.LIB.hlhgat_set_proj_bwd_rows(rows), "set_proj_bwd_rows")
+        try:
+            res.append(run())
+        finally:
+            _lib.LIB.hlhgat_set_proj_bwd_rows(1)
+    ref = [R.t() @ torch.cat(blocks, 1), R.sum(0)] + list((R @ W).split(widths, 1))
+    for u, v, r in zip(res[0], res[1], ref):
+        assert torch.equal(u, v)
+        close(u.cpu(), r.cpu(), 1e-4, "linear grad vs torch")
 
 
 @pytest.mark.parametrize("padded", [False, True])

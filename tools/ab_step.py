@@ -9,6 +9,10 @@ Variants (A/B hooks, not product settings):
   nochain     ops.CHAINS_ENABLED = False (a fork / join per HL block)
   nochainbwd  chain-mode forward, the NodeEdgeInt backward with its own fork / join
   nofusedbn   projection and BatchNorm forward as two launches
+  norows      Linear backward data gradient per (row block, column tile)
+  nomlp2      the readout MLP module by module (no two-layer fused node)
+  noreadside  the edge readout mean on the main stream
+  noreserve   BatchNorm workspaces not reserved before the capture
 """
 import argparse
 import json
@@ -26,9 +30,15 @@ import torch  # noqa: E402
 
 def set_variant(name, on):
     from hlhgat import ops, _lib
+    name = name.rstrip("0123456789")  # base1, base2: repeats of one variant
     ops.CHAINS_ENABLED = not (on and name == "nochain")
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
+    _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
+    from hlhgat import nn as hnn, hodge_st_model, train
+    hnn.MLP_PAIRS = not (on and name == "nomlp2")
+    hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")
+    train.BN_RESERVE_CHANNELS = 0 if (on and name == "noreserve") else 2048
 
 
 def main():
