@@ -35,6 +35,12 @@ import subprocess
 import sys
 import time
 
+# the replayed step is two chains of kernels: let the HIP runtime run a
+# captured graph on two hardware queues (its default, four, adds cross-queue
+# dependencies: 2.74 -> 2.68 ms per step and 2.12 -> 1.83 ms of host time per
+# replay, same-box sweep tools/probes/graph_env_sweep.sh); read at HIP init
+os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 for p in (REPO, os.path.join(REPO, "hl-hgat_amd")):
     if p not in sys.path:

@@ -11,7 +11,7 @@ import hlhgat  # noqa: E402
 from hlhgat.train import TrainStep  # noqa: E402
 
 dev = torch.device("cuda:0")
-batches, caps, _ = bench.make_batches(8, 0, dev)
+batches, caps, _, _, ds = bench.make_batches(8, 0, dev)
 torch.manual_seed(0)
 model = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**bench.MODEL_KW).to(dev).train()
 crit = hlhgat.nn.L1Loss()
@@ -41,3 +41,16 @@ for rep in range(3):
     t2 = time.perf_counter()
     print(f"enqueue {1e3 * (t1 - t0) / 40:.3f} ms/step, total {1e3 * (t2 - t0) / 40:.3f} ms/step, "
           + ", ".join(f"{k} {1e3 * v / 40:.3f}" for k, v in parts.items()), flush=True)
+
+# the loader-fed loop's host side: one pinned batch's H2D (all its tensors)
+import numpy as np  # noqa: E402
+idx = np.arange(1000)
+pb = ds.collate(idx, caps, pin=True)
+n_t = sum(1 for v in vars(pb).values() if torch.is_tensor(v))
+for rep in range(3):
+    t0 = time.perf_counter()
+    for i in range(20):
+        bd = pb.to(dev, non_blocking=True)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f"upload: {n_t} tensors, host {1e3 * (t1 - t0) / 20:.3f} ms/batch", flush=True)
