@@ -133,19 +133,30 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16):
 
     src = batches()
     nxt = upload(next(src))
+    host = {"wait_loader": 0.0, "upload": 0.0, "step_call": 0.0}
     for i in range(steps + 2):
         if i == 2:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            host = {k: 0.0 for k in host}
         bd, ev = nxt
-        nxt = upload(next(src))
+        ta = time.perf_counter()
+        b_next = next(src)
+        tb = time.perf_counter()
+        nxt = upload(b_next)
+        tc = time.perf_counter()
         main.wait_event(ev)
         step(bd)
+        td = time.perf_counter()
+        host["wait_loader"] += tb - ta
+        host["upload"] += tc - tb
+        host["step_call"] += td - tc
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     out["loader_fed"] = {"value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
                          "ms_per_step": round(dt * 1e3, 3), "workers": 4, "pinned": True,
                          "steps": steps,
+                         "host_ms_per_step": {k: round(v / steps * 1e3, 3) for k, v in host.items()},
                          "what": "training steps fed by GraphLoader end to end: native collate "
                                  "on 4 threads, H2D of the next batch on a copy stream during "
                                  "the step, copy-in + replayed step"}
