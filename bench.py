@@ -153,6 +153,7 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16):
         host["step_call"] += td - tc
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
+    src.close()  # stop the loader's collation threads before the next leg
     out["loader_fed"] = {"value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
                          "ms_per_step": round(dt * 1e3, 3), "workers": 4, "pinned": True,
                          "steps": steps,
