@@ -82,12 +82,27 @@ class Batch(PairData):
     hodge_sorted: Dict[str, bool]
 
     def to(self, device, non_blocking: bool = False):
+        self._check_counts()
         for k in self.keys():
             v = getattr(self, k)
             if torch.is_tensor(v):
                 setattr(self, k, v.to(device, non_blocking=non_blocking))
         self._mark()
         return self
+
+    def _check_counts(self) -> None:
+        """Per-graph row counts must not exceed the row count: the forward's
+        repeat_interleave(..., output_size=rows) (no host sync, capturable)
+        trusts it, and a larger sum would write past the output.  Checked on
+        the host copy only (never a device sync); rows beyond the sum are
+        padding and are allowed."""
+        for kc, kx in (("num_node1", "x_t"), ("num_edge1", "x_s")):
+            c, x = getattr(self, kc, None), getattr(self, kx, None)
+            if torch.is_tensor(c) and torch.is_tensor(x) and not c.is_cuda:
+                tot = int(c.sum())
+                if tot > x.shape[0]:
+                    raise ValueError(f"Batch.{kc} sums to {tot} but {kx} has "
+                                     f"{x.shape[0]} rows")
 
     def _mark(self) -> None:
         from . import ops

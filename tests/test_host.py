@@ -210,6 +210,20 @@ def test_pad_batch_structure():
     assert torch.equal(p.num_node1, b.num_node1) and torch.equal(p.num_edge1, b.num_edge1)
 
 
+def test_batch_to_rejects_counts_beyond_rows():
+    """Batch.to checks on the host that the per-graph counts fit the rows
+    (the capturable forward's repeat_interleave(output_size=rows) trusts it);
+    padded rows beyond the sum are fine."""
+    from hlhgat.hodge_dataset import pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(5, seed=1)
+    pad_batch(b, static_caps(b, 128)).to("cpu")  # sum < rows: padding, accepted
+    b.num_edge1 = b.num_edge1.clone()
+    b.num_edge1[0] += 1
+    with pytest.raises(ValueError, match="num_edge1 sums to"):
+        b.to("cpu")
+
+
 def test_incidence_csr_host_build():
     """Collate-time incidence CSR of |B1| (hodge_dataset.incidence_csr): row v
     lists the edges with an endpoint at v, ascending (adj2par1,

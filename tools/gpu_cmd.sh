@@ -1,4 +1,22 @@
-set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "bn_fold" -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/t23.log 2>&1
-timeout -k 10 300 python tools/ab_step.py base nofold base2 nofold2 --rounds 8 > gpurun_out/ab23.log 2>&1 && \
-timeout -k 10 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/suite23.log 2>&1
+#!/bin/bash
+# Scratch GPU command: the newest tests, a same-process A/B, the suite, smoke, bench.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?; echo "=== $name rc=$rc"; tail -n 4 "gpurun_out/$name.log" | cut -c1-2000
+  case $rc in
+    0|1) ;;
+    *) tail -n 60 "gpurun_out/$name.log"; exit $rc ;;
+  esac
+  return 0
+}
+step t_fold 300 python -u -m pytest tests/test_gpu_parity.py -k "fold or tn8 or rows" -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread
+step ab 300 python tools/ab_step.py base nofold notn8 base2 nofold2 notn82 --rounds 6
+step suite 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py
+echo "=== done"
