@@ -1518,64 +1518,6 @@ extern "C" int hlhgat_proj_bn_fused_capacity(int64_t* out) {
   return HLHGAT_OK;
 }
 
-namespace {
-// the backward statistics launch: dweight / dbias and dx's coefficients
-// (A, B, Cc per column) into coef; dx_layout: the dx the layout is chosen
-// for (its pitch / alignment join the vector test), or null
-int bn_bwd_reduce_launch(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                         const float* dy, int64_t lddy, const float* dx_layout, int64_t lddx,
-                         int64_t n, const int32_t* n_valid, int64_t C, const float* weight,
-                         const float* save_mean, const float* save_invstd, float* coef,
-                         float* dweight, float* dbias, void* workspace, hipStream_t st,
-                         BnLayout& L, bool& vec) {
-  vec = bn_vec_ok(C, {ldx, lddy, dx_layout ? lddx : 4, y ? ldy : 4}, {x, y, dy, dx_layout});
-  L = bn_layout(n, C, vec);
-  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd: C too large");
-  BnWs w = carve(workspace, n, C);
-  StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
-  s.y = y;
-  s.ldy = ldy;
-  s.dy = dy;
-  s.lddy = lddy;
-  s.weight = weight;
-  s.save_mean = const_cast<float*>(save_mean);
-  s.save_invstd = const_cast<float*>(save_invstd);
-  s.coef = coef ? coef : w.coef;
-  s.dweight = dweight;
-  s.dbias = dbias;
-  dim3 g1(L.parts, L.tiles);
-  {  // algorithmic bytes of the reduction: x, dy (and y for the ReLU mask) read once
-    ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
-    if (vec)
-      launch(k_bn_bwd_reduce<4>, g1, dim3(kThreads), 0, st, &prof, s);
-    else
-      launch(k_bn_bwd_reduce<1>, g1, dim3(kThreads), 0, st, &prof, s);
-  }
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
-}  // namespace
-
-extern "C" int hlhgat_bn_bwd_coefs(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                                   const float* dy, int64_t lddy, int64_t n,
-                                   const int32_t* n_valid, int64_t C, const float* weight,
-                                   const float* save_mean, const float* save_invstd, float* coef,
-                                   float* dweight, float* dbias, void* workspace,
-                                   int64_t workspace_bytes, void* stream) {
-  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && (!y || ldy >= C),
-                "bn_bwd_coefs: bad sizes");
-  HLH_CHECK_ARG(x && dy && coef && save_mean && save_invstd, "bn_bwd_coefs: NULL pointer");
-  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
-                "bn_bwd_coefs: workspace too small");
-  BnLayout L;
-  bool vec;
-  // the layout hlhgat_bn_bwd_train picks for a dense dx of dy's pitch: the
-  // same partials, so the same coefficients, bit for bit
-  return bn_bwd_reduce_launch(x, ldx, y, ldy, dy, lddy, dy, C, n, n_valid, C, weight, save_mean,
-                              save_invstd, coef, dweight, dbias, workspace, as_stream(stream), L,
-                              vec);
-}
-
 extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
                                    int64_t ldy, const float* dy, int64_t lddy,
                                    int64_t n, const int32_t* n_valid, int64_t C,
@@ -1589,14 +1531,31 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   HLH_CHECK_ARG(x && dy && dx && save_mean && save_invstd, "bn_bwd_train: NULL pointer");
   HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
                 "bn_bwd_train: workspace too small");
-  hipStream_t st = as_stream(stream);
-  BnLayout L;
-  bool vec;
-  const int rc = bn_bwd_reduce_launch(x, ldx, y, ldy, dy, lddy, dx, lddx, n, n_valid, C, weight,
-                                      save_mean, save_invstd, nullptr, dweight, dbias, workspace,
-                                      st, L, vec);
-  if (rc != HLHGAT_OK) return rc;
+  const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
+  BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_train: C too large");
   BnWs w = carve(workspace, n, C);
+  StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
+  s.y = y;
+  s.ldy = ldy;
+  s.dy = dy;
+  s.lddy = lddy;
+  s.weight = weight;
+  s.save_mean = const_cast<float*>(save_mean);
+  s.save_invstd = const_cast<float*>(save_invstd);
+  s.coef = w.coef;
+  s.dweight = dweight;
+  s.dbias = dbias;
+  hipStream_t st = as_stream(stream);
+  dim3 g1(L.parts, L.tiles);
+  {  // algorithmic bytes of the reduction: x, dy (and y for the ReLU mask) read once
+    ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
+    if (vec)
+      launch(k_bn_bwd_reduce<4>, g1, dim3(kThreads), 0, st, &prof, s);
+    else
+      launch(k_bn_bwd_reduce<1>, g1, dim3(kThreads), 0, st, &prof, s);
+  }
+  HLH_CHECK_LAUNCH();
   BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, save_mean,
                  L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);

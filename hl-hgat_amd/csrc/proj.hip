@@ -170,82 +170,6 @@ struct BwdDataArgs {
   int accumulate;
 };
 
-// BatchNorm backward folded into the Linear backward's dC loads
-// (hlhgat_proj_bwd_bn_defer): dC is the input gradient of y = BN(x) (+ReLU),
-// dx = A g + (B (x - mean) + Cc) with g = dy masked by y > 0 and rows >=
-// n_valid zero -- k_bn_bwd_apply's expression, so the same bits
-// (-ffp-contract=off) without the apply launch or dx in memory.
-struct BnFold {
-  const float* x;
-  int64_t ldx;
-  const float* y;  // ReLU mask source (null: no ReLU)
-  int64_t ldy;
-  const float* coef;  // [3][C]: A, B, Cc of k_bn_bwd_reduce; null: dC as given
-  const float* mean;
-  const int32_t* nvalid;
-  int C;
-};
-
-__device__ __forceinline__ int64_t fold_rows(const BnFold& f, int64_t M) {
-  if (!f.nvalid) return M;
-  const int64_t v = (int64_t)*f.nvalid;
-  return v < M ? (v < 0 ? 0 : v) : M;
-}
-
-struct FoldCols {  // the BatchNorm coefficients of 4 consecutive columns
-  float4 A, B, Cc, mu;
-};
-
-__device__ __forceinline__ FoldCols fold_cols(const BnFold& f, int n) {
-  FoldCols c;
-  if (n < f.C) {
-    c.A = *reinterpret_cast<const float4*>(f.coef + n);
-    c.B = *reinterpret_cast<const float4*>(f.coef + f.C + n);
-    c.Cc = *reinterpret_cast<const float4*>(f.coef + 2 * f.C + n);
-    c.mu = *reinterpret_cast<const float4*>(f.mean + n);
-  } else {
-    c.A = c.B = c.Cc = c.mu = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  return c;
-}
-
-__device__ __forceinline__ float fold1(float A, float B, float Cc, float mu, float g, float x,
-                                       float y, bool relu) {
-  if (relu && !(y > 0.f)) g = 0.f;
-  return A * g + (B * (x - mu) + Cc);
-}
-
-// dC[m][n..n+3] from dy's float4 g (row m < n_eff, n + 3 < C)
-__device__ __forceinline__ float4 fold4(const BnFold& f, const FoldCols& c, int64_t m, int n,
-                                        float4 g) {
-  const float4 x = *reinterpret_cast<const float4*>(f.x + m * f.ldx + n);
-  const bool relu = f.y != nullptr;
-  const float4 y = relu ? *reinterpret_cast<const float4*>(f.y + m * f.ldy + n) : g;
-  float4 o;
-  o.x = fold1(c.A.x, c.B.x, c.Cc.x, c.mu.x, g.x, x.x, y.x, relu);
-  o.y = fold1(c.A.y, c.B.y, c.Cc.y, c.mu.y, g.y, x.y, y.y, relu);
-  o.z = fold1(c.A.z, c.B.z, c.Cc.z, c.mu.z, g.z, x.z, y.z, relu);
-  o.w = fold1(c.A.w, c.B.w, c.Cc.w, c.mu.w, g.w, x.w, y.w, relu);
-  return o;
-}
-
-// a 64-wide dC chunk of one row for the data gradient (load_a_chunk's
-// layout), folded through the BatchNorm backward when f.coef is set
-__device__ __forceinline__ void load_g_chunk(const BnFold& f, const float* grow, int64_t row,
-                                             bool valid, int64_t n_eff, int n0, int N, int q,
-                                             float4 (&o)[4]) {
-  load_a_chunk(grow, valid, n0, N, q, o);
-  if (!f.coef) return;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int n = n0 + 16 * s + 4 * q;
-    if (valid && row < n_eff && n < N)
-      o[s] = fold4(f, fold_cols(f, n), row, n, o[s]);
-    else
-      o[s] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
 template <int TM, int TN, bool VEC>
 __global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
   const int wave = threadIdx.x >> 6;
@@ -324,8 +248,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data(BwdDataArgs a) {
 // 64-wide n chunk ahead.
 template <int TN>
 __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, int by,
-                                                  float (*wl)[TN * 16][KCP],
-                                                  const BnFold& fold = BnFold{}) {
+                                                  float (*wl)[TN * 16][KCP]) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int q = lane >> 4, i = lane & 15;
@@ -339,10 +262,7 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
   const int64_t row = m_base + i;
   const bool gval = row < a.M;
   const float* grow = a.G + (gval ? row : 0) * a.ldg;
-  const int64_t n_eff = fold.coef ? fold_rows(fold, a.M) : a.M;
-  auto load_g = [&](int n0, float4 (&o)[4]) {
-    load_g_chunk(fold, grow, row, gval, n_eff, n0, a.N, q, o);
-  };
+  auto load_g = [&](int n0, float4 (&o)[4]) { load_a_chunk(grow, gval, n0, a.N, q, o); };
 
 
   // staging: TN*16 columns x 64 n = TN*256 float4 over 256 threads; thread
@@ -420,16 +340,13 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
 }
 
 // Data gradient, one workgroup per 64-row block covering EVERY column tile of
-// every block (N <= 64 * NCH: the workgroup's dC rows stay in registers as
-// NCH chunks of 64), so dC is read once per row block instead of once per
-// column tile.  The stages (column tile, n chunk) go through two LDS buffers
-// (the next W chunk loaded while the current one feeds the MFMAs); the
-// epilogue has its own scratch.  Per element the same MFMA sequence as
-// bwd_data_lds_body (n chunks ascending, then s, then the 4 k of a lane):
-// bitwise the same dA.
-template <int TN, int NCH>
-__device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx, float* lds,
-                                                   const BnFold& fold) {
+// every block (N <= 64: the workgroup's whole dC chunk stays in registers), so
+// dC is read once per row block instead of once per column tile; the W tiles
+// go through two LDS buffers (the next one loaded while the current one feeds
+// the MFMAs) and the epilogue has its own scratch.  Per element the same MFMA
+// sequence as bwd_data_lds_body: bitwise the same dA.
+template <int TN>
+__device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx, float* lds) {
   float (*wl)[TN * 16][KCP] = reinterpret_cast<float (*)[TN * 16][KCP]>(lds);
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -438,22 +355,17 @@ __device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx,
   const int64_t m_base = ((int64_t)bx * 4 + wave) * 16;
   const int64_t row = m_base + i;
   const bool gval = row < a.M;
-  float4 gc[NCH][4];
-  const int64_t n_eff = fold.coef ? fold_rows(fold, a.M) : a.M;
-#pragma unroll
-  for (int ch = 0; ch < NCH; ++ch)
-    load_g_chunk(fold, a.G + (gval ? row : 0) * a.ldg, row, gval, n_eff, ch * KC, a.N, q, gc[ch]);
+  float4 gc[4];
+  load_a_chunk(a.G + (gval ? row : 0) * a.ldg, gval, 0, a.N, q, gc);
   const int ntiles = a.tile_start[a.nb];
-  const int nstages = ntiles * NCH;
   auto tile_of = [&](int t, int& b, int& c_base) {
     b = 0;
     while (b + 1 < a.nb && t >= a.tile_start[b + 1]) ++b;
     c_base = (t - a.tile_start[b]) * (TN * 16);
   };
-  auto load_w = [&](int st_i, float4 (&st)[TN]) {  // as bwd_data_lds_body's staging
+  auto load_w = [&](int t, float4 (&st)[TN]) {  // as bwd_data_lds_body's staging
     int b, c_base;
-    tile_of(st_i / NCH, b, c_base);
-    const int n0 = (st_i % NCH) * KC;
+    tile_of(t, b, c_base);
     const float* __restrict__ W = a.W[b];
     const int64_t ldw = a.ldw[b];
     const int kb = a.kb[b];
@@ -461,9 +373,9 @@ __device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx,
     for (int u = 0; u < TN; ++u) {
       const int idx = threadIdx.x + 256 * u;
       const int nl = idx & 63, c4 = idx >> 6;
-      const int n = n0 + nl, c = c_base + 4 * c4;
-      st[u] = (n < a.N && c < kb) ? *reinterpret_cast<const float4*>(W + (int64_t)n * ldw + c)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int c = c_base + 4 * c4;
+      st[u] = (nl < a.N && c < kb) ? *reinterpret_cast<const float4*>(W + (int64_t)nl * ldw + c)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store_w = [&](float (*dst)[KCP], const float4 (&st)[TN]) {
@@ -482,42 +394,33 @@ __device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx,
   load_w(0, wst);
   store_w(wl[0], wst);
   __syncthreads();
-  floatx4 acc[TN];
-  for (int t = 0; t < nstages; ++t) {
+  for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    const int ch = t % NCH;
-    const bool has_next = t + 1 < nstages;
+    const bool has_next = t + 1 < ntiles;
     if (has_next) load_w(t + 1, wst);
-    if (ch == 0) {
+    floatx4 acc[TN];
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      if (c != ch) continue;  // registers indexed statically
+    for (int s = 0; s < 4; ++s) {
+      float4 bf[TN];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float4 bf[TN];
+      for (int tn = 0; tn < TN; ++tn)
+        bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][4 * wswz(i, 4 * s + q)]);
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          bf[tn] = *reinterpret_cast<const float4*>(&wl[buf][tn * 16 + i][4 * wswz(i, 4 * s + q)]);
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          acc[tn] = mfma16(gc[c][s].x, bf[tn].x, acc[tn]);
-          acc[tn] = mfma16(gc[c][s].y, bf[tn].y, acc[tn]);
-          acc[tn] = mfma16(gc[c][s].z, bf[tn].z, acc[tn]);
-          acc[tn] = mfma16(gc[c][s].w, bf[tn].w, acc[tn]);
-        }
+      for (int tn = 0; tn < TN; ++tn) {
+        acc[tn] = mfma16(gc[s].x, bf[tn].x, acc[tn]);
+        acc[tn] = mfma16(gc[s].y, bf[tn].y, acc[tn]);
+        acc[tn] = mfma16(gc[s].z, bf[tn].z, acc[tn]);
+        acc[tn] = mfma16(gc[s].w, bf[tn].w, acc[tn]);
       }
     }
-    if (ch == NCH - 1) {
-      int b, c_base;
-      tile_of(t / NCH, b, c_base);
-      const int ncols = a.kb[b] - c_base < TN * 16 ? a.kb[b] - c_base : TN * 16;
-      const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
-      store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
-                          a.accumulate, vec_ok);
-    }
+    int b, c_base;
+    tile_of(t, b, c_base);
+    const int ncols = a.kb[b] - c_base < TN * 16 ? a.kb[b] - c_base : TN * 16;
+    const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
+    store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
+                        a.accumulate, vec_ok);
     if (has_next) store_w(wl[buf ^ 1], wst);
     __syncthreads();
   }
@@ -712,8 +615,7 @@ __device__ __forceinline__ void weight_item(unsigned L, unsigned Y, unsigned tot
 }
 
 __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by, int bz,
-                                                  float (*gl)[WR][64], float (*al)[WR][64],
-                                                  const BnFold& fold = BnFold{}) {
+                                                  float (*gl)[WR][64], float (*al)[WR][64]) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int wn = wave >> 1, wk = wave & 1;
@@ -732,11 +634,6 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
 
   // staging: each tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
   const int sr = threadIdx.x >> 4, sc = (threadIdx.x & 15) * 4;
-  // folded BatchNorm backward: this thread's 4 columns' coefficients once
-  const bool folded = fold.coef != nullptr;
-  const int64_t n_eff = folded ? fold_rows(fold, a.M) : a.M;
-  FoldCols fc{};
-  if (folded) fc = fold_cols(fold, n_base + sc);
   auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -745,9 +642,6 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
       const int n = n_base + sc, k = k_base + sc;
       g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (folded)
-        g[u] = (mv && n < a.N && m < n_eff) ? fold4(fold, fc, m, n, g[u])
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
       x[u] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -910,10 +804,9 @@ struct BwdFusedArgs {
   int d_xcd;   // XCD-aware data order: the column tiles of one row block on one XCD
   int n_red;   // trailing workgroups: a deferred split reduction of an EARLIER launch
   ReduceArgs red;
-  BnFold fold;  // dC through a BatchNorm backward (fold.coef set) or as given
 };
 
-template <int TND, int ROWS>
+template <int TND, bool ROWS>
 __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
   const int L = (int)blk.x;
   if (L >= a.n_wpad + a.n_d) {
@@ -921,8 +814,8 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
     if (l < a.n_red) reduce_splits_body(a.red, Blk{(unsigned)l, 0u, (unsigned)a.n_red, 1u});
     return;
   }
-  if (ROWS > 0 && L >= a.n_wpad) {  // one workgroup per row block, every column tile
-    bwd_data_rows_body<TND, (ROWS > 0 ? ROWS : 1)>(a.d, L - a.n_wpad, lds, a.fold);
+  if (ROWS && L >= a.n_wpad) {  // one workgroup per row block, every column tile
+    bwd_data_rows_body<TND>(a.d, L - a.n_wpad, lds);
     return;
   }
   if (L >= a.n_wpad) {
@@ -942,7 +835,7 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
       bx = l % a.d_gx;
       by = l / a.d_gx;
     }
-    bwd_data_lds_body<TND>(a.d, bx, by, reinterpret_cast<float (*)[TND * 16][KCP]>(lds), a.fold);
+    bwd_data_lds_body<TND>(a.d, bx, by, reinterpret_cast<float (*)[TND * 16][KCP]>(lds));
     return;
   }
   if (L >= a.n_w) return;  // alignment padding
@@ -950,23 +843,21 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
   int by = L % Y, bz = L / Y;
   if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
   bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
-                    reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64), a.fold);
+                    reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
-template <int TND, int ROWS>
+template <int TND, bool ROWS>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
-  // ROWS (dC chunks held per row block, 0 = one workgroup per column tile):
-  // two W buffers + the epilogue scratch (bwd_data_rows_body)
+  // ROWS: two W buffers + the epilogue scratch (bwd_data_rows_body)
   constexpr int kW = 2 * WR * 64 * 2;
   constexpr int kD = ROWS ? 2 * TND * 16 * KCP + 4 * 16 * (TND * 16 + 4) : 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
   proj_bwd_fused_body<TND, ROWS>(a, blk_hw(), lds);
 }
 
-// A/B hook (hlhgat_set_proj_bwd_rows): the most dC chunks of 64 columns a
-// row-block data-gradient workgroup holds (0: one workgroup per column tile)
-int& proj_bwd_rows_flag() {
-  static int v = 2;
+// A/B hook (hlhgat_set_proj_bwd_rows): row-block data-gradient workgroups
+bool& proj_bwd_rows_flag() {
+  static bool v = true;
   return v;
 }
 
@@ -1035,20 +926,11 @@ bool vec_ok(const float* p, int64_t ld, int64_t kb) {
 // 16-column tiles per wave of the forward: enough waves to cover the 1024
 // SIMDs several times over (measured at the HL-HGAT shapes, tools/kbench.py):
 // small M -> 1, K <= 256 -> 2 (re-reading A from L2 is cheap), long K -> 4
-bool& fwd_tn8_flag() {  // A/B hook (hlhgat_set_proj_fwd_tn8)
-  static bool v = true;
-  return v;
-}
-
 int fwd_tn(int64_t M, int64_t N, int64_t ktot) {
   // (64-column tiles from K = 0 measured equal at the ZINC step, round 2)
   int tn = ceil_div(M, 16) * ceil_div(N, 16) < 4096 ? 1 : (ktot >= 256 ? 4 : 2);
   if (N <= 16) tn = 1;
   else if (N <= 32 && tn > 2) tn = 2;
-  // long reductions over many rows (the config 3 / 5 heads' NodeEdgeInt and
-  // wide convs): 128-column tiles read each A row chunk once for 128 output
-  // columns instead of twice
-  if (fwd_tn8_flag() && tn == 4 && N >= 128 && ktot >= 512 && M >= 32768) tn = 8;
   return tn;
 }
 
@@ -1105,10 +987,8 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
       launch(k_proj_fwd_lds<1>, g, 256, 0, s, &prof, a);
     else if (tn == 2)
       launch(k_proj_fwd_lds<2>, g, 256, 0, s, &prof, a);
-    else if (tn == 4)
-      launch(k_proj_fwd_lds<4>, g, 256, 0, s, &prof, a);
     else
-      launch(k_proj_fwd_lds<8>, g, 256, 0, s, &prof, a);
+      launch(k_proj_fwd_lds<4>, g, 256, 0, s, &prof, a);
   } else if (tm == 1 && tn == 1) {
     launch(k_proj_fwd<1, 1, false>, grid, 256, 0, s, &prof, a);
   } else if (tm == 1 && tn == 2) {
@@ -1293,8 +1173,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
                   float* const* dA, const int64_t* ldda, int accumulate_d, float* workspace,
                   int64_t workspace_floats, void* stream,
                   const hlhgat_reduce_desc_t* merge = nullptr,
-                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr,
-                  const hlhgat_bn_fold_t* fold = nullptr) {
+                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr) {
   if (deferred) *deferred = 0;
   const ReduceArgs* prev = nullptr;
   if (merge) {
@@ -1316,16 +1195,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
-  if (fold) {  // the BatchNorm backward runs inside the fused launch's dC loads
-    HLH_CHECK_ARG(fold->x && fold->coef && fold->mean && fold->C == N && fold->ldx >= N &&
-                      (!fold->y || fold->ldy >= N),
-                  "proj_bwd_bn: bad fold");
-    HLH_CHECK_ARG(fuse && vec_ok(fold->x, fold->ldx, N) &&
-                      (!fold->y || vec_ok(fold->y, fold->ldy, N)) && aligned16(fold->coef) &&
-                      aligned16(fold->mean),
-                  "proj_bwd_bn: operands not foldable (weight gradient, M > 0, 16-byte "
-                  "aligned rows of widths %% 4 == 0 required)");
-  }
   if (prev && !fuse) {  // run the merged reduction on its own first
     const int rc = run_reduce(*prev, as_stream(stream));
     if (rc != HLHGAT_OK) return rc;
@@ -1399,25 +1268,14 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   f.d_gx = (int)ceil_div(M, 4 * 16);
   f.n_wpad = (f.n_w + 7) & ~7;
-  // N <= 128 (one or two dC chunks): one data workgroup per row block for
-  // every column tile (dC read once); else one per (row block, column tile)
+  // N <= 64 (one dC chunk): one data workgroup per row block for every column
+  // tile (dC read once); else one per (row block, column tile)
   bool vec_d = aligned16(dC) && lddc % 4 == 0;
   for (int b = 0; b < nb_d; ++b)
     vec_d = vec_d && aligned16(W[b]) && ldw[b] % 4 == 0 && kb_d[b] % 4 == 0;
-  const int nch = (int)ceil_div(N, KC);
-  const int rows = (tnd == 4 && vec_d && nch <= proj_bwd_rows_flag()) ? nch : 0;
+  const bool rows = proj_bwd_rows_flag() && tnd == 4 && N <= KC && vec_d;
   f.n_d = rows ? f.d_gx : f.d_gx * d.tile_start[nb_d];
   f.d_xcd = data_xcd_map();
-  if (fold) {
-    f.fold.x = fold->x;
-    f.fold.ldx = fold->ldx;
-    f.fold.y = fold->y;
-    f.fold.ldy = fold->ldy;
-    f.fold.coef = fold->coef;
-    f.fold.mean = fold->mean;
-    f.fold.nvalid = fold->n_valid;
-    f.fold.C = (int)N;
-  }
   if (prev) {
     f.red = *prev;
     f.n_red = (int)reduce_blocks(*prev);
@@ -1439,16 +1297,14 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   bytes += 4.0 * (double)p.splits * p.part_stride;
   ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-  if (rows == 1)
-    launch(k_proj_bwd_fused<4, 1>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
-  else if (rows == 2)
-    launch(k_proj_bwd_fused<4, 2>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  if (rows)
+    launch(k_proj_bwd_fused<4, true>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else if (tnd == 1)
-    launch(k_proj_bwd_fused<1, 0>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+    launch(k_proj_bwd_fused<1, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else if (tnd == 2)
-    launch(k_proj_bwd_fused<2, 0>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+    launch(k_proj_bwd_fused<2, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else
-    launch(k_proj_bwd_fused<4, 0>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+    launch(k_proj_bwd_fused<4, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
@@ -1481,24 +1337,6 @@ extern "C" int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int6
                        defer_out, deferred);
 }
 
-extern "C" int hlhgat_proj_bwd_bn_defer(int64_t M, int64_t N, const float* dy, int64_t lddy,
-                                        const hlhgat_bn_fold_t* fold, int nb_w,
-                                        const float* const* A, const int64_t* lda,
-                                        const int64_t* kb_w, float* const* dW,
-                                        const int64_t* lddw, float* dbias, int nb_d,
-                                        const float* const* W, const int64_t* ldw,
-                                        const int64_t* kb_d, float* const* dA,
-                                        const int64_t* ldda, int accumulate_d, float* workspace,
-                                        int64_t workspace_floats,
-                                        const hlhgat_reduce_desc_t* merge,
-                                        hlhgat_reduce_desc_t* defer_out, int* deferred,
-                                        void* stream) {
-  HLH_CHECK_ARG(fold, "proj_bwd_bn: NULL fold");
-  return proj_bwd_impl(M, N, dy, lddy, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
-                       dA, ldda, accumulate_d, workspace, workspace_floats, stream, merge,
-                       defer_out, deferred, fold);
-}
-
 extern "C" int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream) {
   HLH_CHECK_ARG(desc && desc->words[0] == kDescMagic, "reduce_run: not a reduce descriptor");
   return run_reduce(*reinterpret_cast<const ReduceArgs*>(&desc->words[1]), as_stream(stream));
@@ -1516,13 +1354,7 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
                        stream);
 }
 
-extern "C" int hlhgat_set_proj_bwd_rows(int max_chunks) {
-  HLH_CHECK_ARG(max_chunks >= 0 && max_chunks <= 2, "set_proj_bwd_rows: max_chunks %d", max_chunks);
-  proj_bwd_rows_flag() = max_chunks;
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_set_proj_fwd_tn8(int on) {
-  fwd_tn8_flag() = on != 0;
+extern "C" int hlhgat_set_proj_bwd_rows(int on) {
+  proj_bwd_rows_flag() = on != 0;
   return HLHGAT_OK;
 }

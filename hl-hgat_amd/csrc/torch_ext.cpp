@@ -459,7 +459,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
                    const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
                    const std::vector<int64_t>& kbd, std::vector<float*>& dA,
                    const std::vector<int64_t>& ldda, void* s, int acc_d = 0,
-                   bool force_defer = false, const hlhgat_bn_fold_t* fold = nullptr) {
+                   bool force_defer = false) {
   const int nbw = (int)A.size(), nbd = (int)W.size();
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
@@ -480,20 +480,11 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   }
   hlhgat_reduce_desc_t out;
   int deferred = 0;
-  if (fold)
-    chk(hlhgat_proj_bwd_bn_defer(M, N, G.data_ptr<float>(), ld_of(G), fold, nbw, A.data(),
-                                 lda.data(), kbw.data(), dW.data(), lddw.data(), db, nbd,
-                                 W.data(), ldw.data(), kbd.data(), dA.data(), ldda.data(), acc_d,
-                                 ws.data_ptr<float>(), wsf, merge ? &prev.desc : nullptr,
-                                 defer ? &out : nullptr, &deferred, s),
-        "proj_bwd_bn");
-  else
-    chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
-                              kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(),
-                              kbd.data(), dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(),
-                              wsf, merge ? &prev.desc : nullptr, defer ? &out : nullptr,
-                              &deferred, s),
-        "proj_bwd");
+  chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
+                            kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(),
+                            kbd.data(), dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(), wsf,
+                            merge ? &prev.desc : nullptr, defer ? &out : nullptr, &deferred, s),
+      "proj_bwd");
   if (merge || deferred) d.streams.insert(s);
   if (deferred) {
     d.pending[s] = PendingReduce{out, ws, s};
@@ -583,75 +574,6 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
                           ws.numel(), stream_of(x)),
       "bn_bwd_train");
   return dx;
-}
-
-// The BatchNorm backward folded into the following Linear backward
-// (hlhgat_proj_bwd_bn_defer): only the statistics launch runs here; dx is
-// formed inside the Linear backward's operand loads (no apply launch, no dx
-// in memory), bitwise bn_backward + the Linear backward on its dx.
-bool& bn_fold_flag() {  // A/B hook (set_bn_fold)
-  static bool v = true;
-  return v;
-}
-
-bool vec_rows(const float* p, int64_t ld, int64_t w) {
-  return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0 && w % 4 == 0;
-}
-
-struct BnFold {
-  hlhgat_bn_fold_t d{};
-  Tensor coef;  // [3C]: A, B, Cc
-  const hlhgat_bn_fold_t* ptr() const { return coef.defined() ? &d : nullptr; }
-};
-
-// dy must be the row-strided gradient the Linear backward is then given
-void bn_backward_fold(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
-                      const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
-                      Tensor& dw, Tensor& db, const Tensor* b_param, const Tensor& valid,
-                      BnFold& f) {
-  const int64_t n = x.size(0), C = x.size(1);
-  dw = (need_w && has(w)) ? grad_like(w) : Tensor();
-  db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
-                                                 : at::empty({C}, x.options()))
-              : Tensor();
-  f.coef = at::empty({3 * C}, x.options());
-  Tensor ws = bn_workspace(x, n, C);
-  const int32_t* nv = valid.defined() ? valid.data_ptr<int32_t>() : nullptr;
-  chk(hlhgat_bn_bwd_coefs(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
-                          dy.data_ptr<float>(), ld_of(dy), n, nv, C, fptr(w),
-                          mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                          f.coef.data_ptr<float>(), dw.defined() ? dw.data_ptr<float>() : nullptr,
-                          db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
-                          ws.numel(), stream_of(x)),
-      "bn_bwd_coefs");
-  f.d.x = x.data_ptr<float>();
-  f.d.ldx = ld_of(x);
-  f.d.y = fptr(y);
-  f.d.ldy = has(y) ? ld_of(*y) : 0;
-  f.d.coef = f.coef.data_ptr<float>();
-  f.d.mean = mean.data_ptr<float>();
-  f.d.n_valid = nv;
-  f.d.C = C;
-}
-
-// the fold's operand test (hlhgat_proj_bwd_bn_defer's one-launch path): dy,
-// the BatchNorm's x / y, the Linear's input blocks A_b and weight blocks
-bool fold_operands_ok(const Tensor& dy, const Tensor& x, const OptT& y,
-                      const std::vector<const float*>& A, const std::vector<int64_t>& lda,
-                      const std::vector<int64_t>& kb, const std::vector<const float*>& W,
-                      const std::vector<int64_t>& ldw, const std::vector<int64_t>& kbd) {
-  const int64_t M = dy.size(0), N = dy.size(1);
-  if (!bn_fold_flag() || M <= 0 || A.empty() || dy.stride(1) != 1) return false;
-  if (!vec_rows(dy.data_ptr<float>(), ld_of(dy), N) || x.stride(1) != 1 ||
-      !vec_rows(x.data_ptr<float>(), ld_of(x), N))
-    return false;
-  if (has(y) && (y->stride(1) != 1 || !vec_rows(y->data_ptr<float>(), ld_of(*y), N)))
-    return false;
-  for (size_t b = 0; b < A.size(); ++b)
-    if (!vec_rows(A[b], lda[b], kb[b])) return false;
-  for (size_t b = 0; b < W.size(); ++b)
-    if (!vec_rows(W[b], ldw[b], kbd[b])) return false;
-  return true;
 }
 
 // Two-stream fork inside one autograd node: the node (current) stream and a
@@ -903,29 +825,11 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
     std::vector<int64_t> lddw;
     float* db = nullptr;
   } wdef;  // weight gradient deferred into the data gradient's launch
-  BnFold fold;  // the BatchNorm backward inside the projection backward's launch
   if (bn_mode > 0) {
     const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
     OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-    // foldable when the projection backward is one launch with a weight
-    // gradient (hlhgat_proj_bwd_bn_defer)
-    bool can_fold = (need_w || need_b) && M > 0 && (!nd.x || fused_bwd_flag());
-    if (can_fold) {
-      std::vector<const float*> Wp;
-      std::vector<int64_t> ldw, kbd;
-      for (int64_t k = 0; k < K && nd.x; ++k) {
-        Wp.push_back(W[k].data_ptr<float>());
-        ldw.push_back(W[k].stride(0));
-        kbd.push_back(Cin);
-      }
-      can_fold = fold_operands_ok(G, pre, bn_y, Ap, lda, kb, Wp, ldw, kbd);
-    }
-    if (can_fold)
-      bn_backward_fold(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
-                       &bn_b, valid, fold);
-    else
-      G = bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
-                      nullptr, &bn_b, valid);
+    G = bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
+                    nullptr, &bn_b, valid);
   }
   if (need_w || need_b) {
     std::vector<Tensor> dW(K);
@@ -946,7 +850,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
       std::vector<int64_t> noL;
       std::vector<float*> noD;
       proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, noW, noL,
-                    noL, noD, noL, s, 0, false, fold.ptr());
+                    noL, noD, noL, s);
     } else {
       for (auto& tt : dW) tt.zero_();
       if (need_b) db.zero_();
@@ -966,13 +870,10 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
         ldw[k] = W[k].stride(0);
         dA[k] = Gs.data_ptr<float>() + k * N * F;
       }
-      if (!wdef.dWp.empty()) {
-        proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s, 0,
-                      false, fold.ptr());
-      } else {
-        TORCH_CHECK(!fold.ptr(), "hlhgat: folded BatchNorm backward without a weight gradient");
+      if (!wdef.dWp.empty())
+        proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s);
+      else
         proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
-      }
       if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
         const hlhgat_hodge_factor_t hf = make_factor(fac, sv.fac_nodes, N);
         Tensor work = at::empty({hlhgat_hodge_factor_work_floats(sv.fac_nodes, F)}, x2.options());
@@ -1185,7 +1086,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
                      Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr,
                      const std::vector<Tensor>* dA_into = nullptr, int into_acc = 1,
-                     bool force_defer = false, const hlhgat_bn_fold_t* fold = nullptr) {
+                     bool force_defer = false) {
   Tensor G = rows2d(Gin);
   const int64_t M = G.size(0), N = G.size(1);
   const int nb = (int)As.size();
@@ -1233,7 +1134,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
         std::vector<int64_t> noL;
         std::vector<float*> noD;
         proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, noW,
-                      noL, noL, noD, noL, s, 0, false, fold);
+                      noL, noL, noD, noL, s);
       }
     } else {
       gw.zero_();
@@ -1266,41 +1167,13 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
     }
     if (M > 0) {
       const int acc = into ? into_acc : 0;
-      if (!wAp.empty()) {
+      if (!wAp.empty())
         proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, acc,
-                      force_defer, fold);
-      } else {
-        TORCH_CHECK(!fold, "hlhgat: folded BatchNorm backward without a weight gradient");
+                      force_defer);
+      else
         proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, acc);
-      }
     }
   }
-}
-
-// the fold test for a BatchNorm whose input gradient feeds linear_backward
-// (G = rows2d of the BatchNorm's output gradient; x, y: its input / output)
-bool linear_fold_ok(const Tensor& G, const Tensor& x, const OptT& y,
-                    const std::vector<Tensor>& As, const Tensor& W, bool need_w, bool need_b,
-                    const std::vector<bool>& need_a) {
-  bool any_a = false;
-  for (bool b : need_a) any_a = any_a || b;
-  if (!(need_w || need_b) || (any_a && !fused_bwd_flag()) || W.stride(1) != 1) return false;
-  std::vector<const float*> Ap, Wp;
-  std::vector<int64_t> lda, kb, ldw, kbd;
-  int64_t off = 0;
-  for (size_t i = 0; i < As.size(); ++i) {
-    if (As[i].stride(1) != 1) return false;
-    Ap.push_back(As[i].data_ptr<float>());
-    lda.push_back(ld_of(As[i]));
-    kb.push_back(As[i].size(1));
-    if (need_a[i]) {
-      Wp.push_back(W.data_ptr<float>() + off);
-      ldw.push_back(W.stride(0));
-      kbd.push_back(As[i].size(1));
-    }
-    off += As[i].size(1);
-  }
-  return fold_operands_ok(G, x, y, Ap, lda, kb, Wp, ldw, kbd);
 }
 
 class LinearFn : public torch::autograd::Function<LinearFn> {
@@ -1428,40 +1301,27 @@ class MLP2Fn : public torch::autograd::Function<MLP2Fn> {
     const int64_t P = nb;
     variable_list out(nb + 18);
     Tensor dg4, dbe4, dg1, dbe1;
-    // each BatchNorm backward folded into the Linear backward after it where
-    // the operands allow (bn_backward_fold), else its own apply launch
-    Tensor dh2 = rows2d(grads[0]);
-    BnFold f2, f1;
-    const OptT og4 = g4.defined() ? OptT(g4) : OptT();
-    if (linear_fold_ok(dh2, h2, OptT(y), {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true}))
-      bn_backward_fold(h2, OptT(y), dh2, og4, m4, i4, need(ctx, P + 9), need(ctx, P + 10), dg4,
-                       dbe4, &be4, Tensor(), f2);
-    else
-      dh2 = bn_backward(h2, OptT(y), grads[0], og4, m4, i4, need(ctx, P + 9), need(ctx, P + 10),
-                        dg4, dbe4, nullptr, &be4);
+    Tensor dh2 = bn_backward(h2, OptT(y), grads[0], g4.defined() ? OptT(g4) : OptT(), m4, i4,
+                             need(ctx, P + 9), need(ctx, P + 10), dg4,
+                             dbe4, nullptr, &be4);
     out[P + 9] = dg4;
     out[P + 10] = dbe4;
     Tensor dW3, db3, dW0, db0;
     std::vector<Tensor> da1;
     linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true},
-                    dW3, db3, da1, &b3, nullptr, 1, false, f2.ptr());
+                    dW3, db3, da1, &b3);
     out[P + 7] = dW3;
     out[P + 8] = db3;
-    std::vector<bool> need_a(nb);
-    for (int64_t i = 0; i < nb; ++i) need_a[i] = need(ctx, i);
-    Tensor dh1 = rows2d(da1[0]);
-    const OptT og1 = g1.defined() ? OptT(g1) : OptT();
-    if (linear_fold_ok(dh1, h1, OptT(a1), blocks, W0, need(ctx, P), need(ctx, P + 1), need_a))
-      bn_backward_fold(h1, OptT(a1), dh1, og1, m1, i1, need(ctx, P + 2), need(ctx, P + 3), dg1,
-                       dbe1, &be1, Tensor(), f1);
-    else
-      dh1 = bn_backward(h1, OptT(a1), da1[0], og1, m1, i1, need(ctx, P + 2), need(ctx, P + 3),
-                        dg1, dbe1, nullptr, &be1);
+    Tensor dh1 = bn_backward(h1, OptT(a1), da1[0], g1.defined() ? OptT(g1) : OptT(), m1, i1,
+                             need(ctx, P + 2), need(ctx, P + 3), dg1,
+                             dbe1, nullptr, &be1);
     out[P + 2] = dg1;
     out[P + 3] = dbe1;
+    std::vector<bool> need_a(nb);
+    for (int64_t i = 0; i < nb; ++i) need_a[i] = need(ctx, i);
     std::vector<Tensor> dblocks;
     linear_backward(dh1, blocks, W0, need(ctx, P), need(ctx, P + 1), need_a,
-                    dW0, db0, dblocks, &b0, nullptr, 1, false, f1.ptr());
+                    dW0, db0, dblocks, &b0);
     out[P] = dW0;
     out[P + 1] = db0;
     for (int64_t i = 0; i < nb; ++i) out[i] = dblocks[i];
@@ -1860,17 +1720,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
              y = sv[o0 + 5], m4 = sv[o0 + 6], i4 = sv[o0 + 7];
       Tensor dg4, dbe4, dg1, dbe1, dW3, db3;
       Tensor gyc = gy.defined() ? gy : at::zeros_like(y);
-      Tensor dh2 = rows2d(gyc);
-      BnFold f2;  // the second BatchNorm's backward inside the W3 Linear backward
-      if (linear_fold_ok(dh2, h2, OptT(y), {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true}))
-        bn_backward_fold(h2, OptT(y), dh2, OptT(g4), m4, i4, need(ctx, P + 9), need(ctx, P + 10),
-                         dg4, dbe4, &be4, valid, f2);
-      else
-        dh2 = bn_backward(h2, OptT(y), gyc, OptT(g4), m4, i4, need(ctx, P + 9),
-                          need(ctx, P + 10), dg4, dbe4, nullptr, &be4, valid);
+      Tensor dh2 = bn_backward(h2, OptT(y), gyc, OptT(g4), m4, i4, need(ctx, P + 9),
+                               need(ctx, P + 10), dg4, dbe4, nullptr, &be4, valid);
       std::vector<Tensor> da1;
       linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true}, dW3, db3, da1,
-                      &b3, nullptr, 1, false, f2.ptr());
+                      &b3);
       bn_backward(h1, OptT(a1), da1[0], OptT(g1), m1, i1, need(ctx, P + 2), need(ctx, P + 3), dg1,
                   dbe1, &dest, &be1, valid);
       out[P + 2] = dg1;
@@ -2491,8 +2345,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_chain", &set_chain);
   m.def("bn_workspace_reserve", &bn_workspace_reserve);
   m.def("set_chain_bwd", &set_chain_bwd);
-  m.def("set_bn_fold", [](bool on) { bn_fold_flag() = on; },
-        "A/B hook: BatchNorm backward folded into the following Linear backward");
   m.def("nei_prepack", &nei_prepack);
   m.def("grad_bucket_set", &grad_bucket_set);
   m.def("grad_bucket_begin", &grad_bucket_begin);

@@ -79,18 +79,11 @@ SIGNATURES = {
                                       P_vp, P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64,
                                       c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "hlhgat_reduce_run": (c_i32, [c_vp, c_vp]),
-    "hlhgat_proj_bwd_bn_defer": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, P_vp, P_i64,
-                                         P_i64, P_vp, P_i64, c_vp, c_i32, P_vp, P_i64, P_i64,
-                                         P_vp, P_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
-                                         c_vp]),
-    "hlhgat_bn_bwd_coefs": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_proj_bn_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                    c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
                                    c_f32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_set_proj_bn_fused": (c_i32, [c_i32]),
     "hlhgat_set_proj_bwd_rows": (c_i32, [c_i32]),
-    "hlhgat_set_proj_fwd_tn8": (c_i32, [c_i32]),
     "hlhgat_proj_bn_fused_capacity": (c_i32, [P_i64]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
     "hlhgat_get_bn_one_launch": (c_i32, []),

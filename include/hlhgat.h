@@ -461,42 +461,6 @@ int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int64_t lddc, i
                           int* deferred, void* stream);
 int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream);
 
-/* BatchNorm backward folded into the Linear backward (the conv / MLP
- * projection before a training-mode BatchNorm(+ReLU), lib/Hodge_ST_Model.py's
- * Linear -> BatchNorm1d -> ReLU and HodgeLaguerreConv -> BatchNorm pairs):
- * the Linear's output gradient is dx = A g + (B (x - mean) + Cc) with g = dy
- * masked by y > 0 (y NULL: no ReLU) and rows >= *n_valid zero, formed inside
- * the one-launch Linear backward's operand loads instead of by an apply
- * launch into memory.  coef = [A[C], B[C], Cc[C]] from hlhgat_bn_bwd_coefs
- * (which also writes dweight / dbias).  Results are bitwise those of
- * hlhgat_bn_bwd_train followed by hlhgat_proj_bwd_defer on its dx. */
-typedef struct {
-  const float* x; /* BatchNorm input (the projection output) [M, C] */
-  int64_t ldx;
-  const float* y; /* BatchNorm(+ReLU) output, the ReLU mask; NULL: no ReLU */
-  int64_t ldy;
-  const float* coef; /* [3 * C] */
-  const float* mean; /* save_mean [C] */
-  const int32_t* n_valid; /* device int32 or NULL */
-  int64_t C;
-} hlhgat_bn_fold_t;
-int hlhgat_bn_bwd_coefs(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                        const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
-                        int64_t C, const float* weight, const float* save_mean,
-                        const float* save_invstd, float* coef, float* dweight, float* dbias,
-                        void* workspace, int64_t workspace_bytes, void* stream);
-/* hlhgat_proj_bwd_defer with dC = the folded BatchNorm backward of dy.
- * Requires the one-launch path (a weight gradient, M > 0, 16-byte aligned
- * rows of widths % 4 == 0 for dy, x, y, A_b, W_b): HLHGAT_EINVAL otherwise. */
-int hlhgat_proj_bwd_bn_defer(int64_t M, int64_t N, const float* dy, int64_t lddy,
-                             const hlhgat_bn_fold_t* fold, int nb_w, const float* const* A,
-                             const int64_t* lda, const int64_t* kb_w, float* const* dW,
-                             const int64_t* lddw, float* dbias, int nb_d, const float* const* W,
-                             const int64_t* ldw, const int64_t* kb_d, float* const* dA,
-                             const int64_t* ldda, int accumulate_d, float* workspace,
-                             int64_t workspace_floats, const hlhgat_reduce_desc_t* merge,
-                             hlhgat_reduce_desc_t* defer_out, int* deferred, void* stream);
-
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
  * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge
@@ -607,13 +571,10 @@ int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
                        float momentum, float eps, int relu, float* y, int64_t ldy,
                        float* save_mean, float* save_invstd, void* workspace,
                        int64_t workspace_bytes, void* stream);
-/* 0: hlhgat_proj_fwd never uses 128-column tiles (tests; bitwise the same). */
-int hlhgat_set_proj_fwd_tn8(int on);
-/* The fused Linear backward (hlhgat_proj_bwd / _defer) runs its data gradient
- * with one workgroup per row block covering every column tile when dC has at
- * most max_chunks chunks of 64 columns (default 2: N <= 128), else one per
- * (row block, 64-column tile); 0 never.  Bitwise the same (tests, A/B). */
-int hlhgat_set_proj_bwd_rows(int max_chunks);
+/* 0: the fused Linear backward (hlhgat_proj_bwd / _defer) uses one
+ * data-gradient workgroup per (row block, 64-column tile) instead of one per
+ * row block covering every column tile (N <= 64); bitwise the same (tests). */
+int hlhgat_set_proj_bwd_rows(int on);
 /* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
 int hlhgat_set_proj_bn_fused(int on);
 /* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */

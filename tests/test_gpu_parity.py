@@ -1121,13 +1121,13 @@ def test_fused_linear_backward_bitwise(cuda, M):
 
 @pytest.mark.parametrize("M", [9000, 25000])
 @pytest.mark.parametrize("widths,N", [([64, 64, 64], 64), ([384, 384], 64), ([36, 36, 36], 32),
-                                      ([128], 48), ([256, 256], 128), ([96], 100)])
+                                      ([128], 48)])
 def test_fused_linear_backward_row_blocks_bitwise(cuda, M, widths, N):
     """The fused Linear backward's data gradient with one workgroup per row
-    block covering every column tile (N <= 128: one or two dC chunks held,
-    hlhgat_set_proj_bwd_rows) == one workgroup per (row block, column tile),
-    bit for bit, and both against torch: the conv (K = 3, d = 64),
-    NodeEdgeInt Linear(768, 64), two-chunk and narrower shapes."""
+    block covering every column tile (N <= 64, hlhgat_set_proj_bwd_rows) ==
+    one workgroup per (row block, column tile), bit for bit, and both against
+    torch: the conv (K = 3, d = 64), NodeEdgeInt Linear(768, 64) and
+    narrower shapes."""
     from hlhgat import _lib, ops
     g = torch.Generator(device="cpu").manual_seed(M + N)
     blocks = [torch.randn(M, k, generator=g).to(cuda) for k in widths]
@@ -1141,12 +1141,12 @@ def test_fused_linear_backward_row_blocks_bitwise(cuda, M, widths, N):
         (ops.linear_blocks(xs, Wv, bv) * R).sum().backward()
         return [Wv.grad, bv.grad] + [x.grad for x in xs]
     res = []
-    for rows in (2, 0):
+    for rows in (1, 0):
         _lib.check(_lib.LIB.hlhgat_set_proj_bwd_rows(rows), "set_proj_bwd_rows")
         try:
             res.append(run())
         finally:
-            _lib.LIB.hlhgat_set_proj_bwd_rows(2)
+            _lib.LIB.hlhgat_set_proj_bwd_rows(1)
     ref = [R.t() @ torch.cat(blocks, 1), R.sum(0)] + list((R @ W).split(widths, 1))
     for u, v, r in zip(res[0], res[1], ref):
         assert torch.equal(u, v)
@@ -1178,91 +1178,6 @@ def test_fused_backward_zinc_model_bitwise(cuda, padded):
     assert a.keys() == c.keys() and len(a) > 100
     for k in a:
         assert torch.equal(a[k], c[k]), k
-
-
-def _grads_with_bn_fold(on, run):
-    from hlhgat import ops
-    try:
-        ops._ext.set_bn_fold(on)
-        return run()
-    finally:
-        ops._ext.set_bn_fold(True)
-
-
-@pytest.mark.parametrize("padded", [False, True])
-def test_bn_fold_zinc_model_bitwise(cuda, padded):
-    """The BatchNorm backward folded into the Linear backward after it
-    (hlhgat_bn_bwd_coefs + hlhgat_proj_bwd_bn_defer: the conv projections'
-    BatchNorm, the NodeEdgeInt second BatchNorm, both readout MLP BatchNorms)
-    == the statistics + apply launches and the Linear backward on the stored
-    dx, bit for bit, for every parameter gradient; padded: static-shape capacity rows (n_valid: dx rows >= n_valid are 0)."""
-    import hlhgat
-    from hlhgat.hodge_dataset import pad_batch, static_caps
-    from hlhgat.synthetic import zinc_like_batch
-    b = zinc_like_batch(48, seed=7)
-    if padded:
-        b = pad_batch(b, static_caps(b, 128))
-    b = b.to(cuda)
-
-    def run():
-        torch.manual_seed(0)
-        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2, 2], filters=[64, 64, 64],
-                                                mlp_channels=[256, 256], K=3,
-                                                keig=15).to(cuda).train()
-        torch.nn.functional.l1_loss(m(b).view(-1), b.y.view(-1)).backward()
-        return {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
-    a = _grads_with_bn_fold(True, run)
-    c = _grads_with_bn_fold(False, run)
-    assert a.keys() == c.keys() and len(a) > 100
-    for k in a:
-        assert torch.equal(a[k], c[k]), k
-
-
-@pytest.mark.parametrize("M,widths,hidden,out,frozen", [
-    (9000, [64, 64, 64], 64, 64, False), (25000, [384], 64, 64, False),
-    (1000, [128], 256, 256, False), (5000, [64, 32], 64, 64, True), (777, [36, 36], 96, 64, False)])
-def test_bn_fold_mlp2_bitwise(cuda, M, widths, hidden, out, frozen):
-    """The two-layer Linear -> BatchNorm -> ReLU node (ops.mlp2, the readout
-    MLP pair) with each BatchNorm backward folded into the Linear backward
-    after it == unfolded, bit for bit, and against torch's modules at 1e-4;
-    frozen: the first Linear's weight needs no gradient (its BatchNorm then
-    keeps the apply launch where the Linear has no weight items)."""
-    from hlhgat import ops
-    g = torch.Generator(device="cpu").manual_seed(M + hidden)
-    xs0 = [torch.randn(M, k, generator=g).to(cuda) for k in widths]
-    R = torch.randn(M, out, generator=g).to(cuda)
-
-    def make():
-        torch.manual_seed(1)
-        seq = torch.nn.Sequential(torch.nn.Linear(sum(widths), hidden),
-                                  torch.nn.BatchNorm1d(hidden), torch.nn.ReLU(),
-                                  torch.nn.Linear(hidden, out), torch.nn.BatchNorm1d(out),
-                                  torch.nn.ReLU()).to(cuda).train()
-        with torch.no_grad():
-            for i in (1, 4):
-                seq[i].weight.uniform_(0.5, 1.5)
-                seq[i].bias.uniform_(-0.5, 0.5)
-        if frozen:
-            seq[0].weight.requires_grad_(False)
-            seq[0].bias.requires_grad_(False)
-        return seq
-
-    def run():
-        seq = make()
-        xs = [t.clone().requires_grad_(True) for t in xs0]
-        (ops.mlp2(xs, seq) * R).sum().backward()
-        return [p.grad for p in seq.parameters() if p.grad is not None] + [x.grad for x in xs]
-    a = _grads_with_bn_fold(True, run)
-    c = _grads_with_bn_fold(False, run)
-    assert len(a) == len(c)
-    for u, v in zip(a, c):
-        assert torch.equal(u, v)
-    seq = make().cpu().double()  # the torch reference in fp64 on the host
-    xs = [t.cpu().double().requires_grad_(True) for t in xs0]
-    (seq(torch.cat(xs, 1)) * R.cpu().double()).sum().backward()
-    ref = [p.grad for p in seq.parameters() if p.grad is not None] + [x.grad for x in xs]
-    for u, r in zip(a, ref):
-        close(u.cpu(), r, 1e-4, "mlp2 grad vs torch fp64")
 
 
 @pytest.mark.parametrize("n,C,relu,pad", [(700, 64, True, 0), (25600, 64, True, 333),

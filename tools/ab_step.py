@@ -10,10 +10,6 @@ Variants (A/B hooks, not product settings):
   nochainbwd  chain-mode forward, the NodeEdgeInt backward with its own fork / join
   nofusedbn   projection and BatchNorm forward as two launches
   norows      Linear backward data gradient per (row block, column tile)
-  rows1       row-block data gradient only for N <= 64 (one dC chunk)
-  notn8       projection forward never on 128-column tiles
-  nofold      BatchNorm backward with its own apply launch (not folded into the
-              Linear backward)
   nomlp2      the readout MLP module by module (no two-layer fused node)
   noreadside  the edge readout mean on the main stream
   noreserve   BatchNorm workspaces not reserved before the capture
@@ -38,10 +34,7 @@ def set_variant(name, on):
     ops.CHAINS_ENABLED = not (on and name == "nochain")
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
-    _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else
-                                      1 if (on and name == "rows1") else 2)
-    _lib.LIB.hlhgat_set_proj_fwd_tn8(0 if (on and name == "notn8") else 1)
-    ops._ext.set_bn_fold(not (on and name == "nofold"))
+    _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")

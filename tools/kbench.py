@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--big", action="store_true",
                     help="config 3 / 5 projection shapes only (CIFAR / TSP heads)")
     args = ap.parse_args()
-    from hlhgat import _lib, ops
+    from hlhgat import ops
     from hlhgat.synthetic import zinc_like_batch
     dev = torch.device("cuda:0")
     pat = re.compile(args.only)
@@ -108,10 +108,6 @@ def main():
             fl = 2.0 * M * N * sum(kbs)
             by = 4.0 * M * (sum(kbs) + N)
             run(f"proj_fwd {tag}", lambda: ops._proj_fwd(As, Ws, M, N, None, out), by, fl)
-            _lib.LIB.hlhgat_set_proj_fwd_tn8(0)
-            run(f"proj_fwd (64-col tiles) {tag}", lambda: ops._proj_fwd(As, Ws, M, N, None, out),
-                by, fl)
-            _lib.LIB.hlhgat_set_proj_fwd_tn8(1)
             G = rnd(M, N)
             dAs = [torch.empty(M, k, device=dev) for k in kbs]
             run(f"proj_bwd_data {tag}", lambda: ops._proj_bwd_data(G, Ws, kbs, dAs), by, fl)
