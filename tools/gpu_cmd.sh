@@ -1,5 +1,5 @@
 #!/bin/bash
-# Scratch GPU command: the newest tests, a same-process A/B, the suite, smoke, bench.
+# Scratch GPU command: the newest tests, a same-process A/B, kernel microbench.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -14,9 +14,8 @@ step() {  # name timeout cmd...
   esac
   return 0
 }
-step t_fold 300 python -u -m pytest tests/test_gpu_parity.py -k "fold or tn8 or rows" -m gpu -v -p no:cacheprovider --timeout 200 --timeout-method thread
-step ab 300 python tools/ab_step.py base nofold notn8 base2 nofold2 notn82 --rounds 6
-step suite 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
-step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
+step t_new 300 python -u -m pytest tests/test_gpu_parity.py -k "prefetch or spmm or basis or laguerre" -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+step ab 300 python tools/ab_step.py base nopf base2 nopf2 --rounds 6
+step kb 200 python tools/kbench.py --only "laguerre|basis|proj_fwd conv|proj_bn_fwd fused conv"
+step t_mr 300 python -u -m pytest tests/test_multirank_trainstep.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
 echo "=== done"
