@@ -103,9 +103,45 @@ __device__ __forceinline__ void poly_epilogue(const PolyArgs& a, int64_t row, in
     vstore<V>(a.Y + row * a.ldy + f, out);
 }
 
+// Entries j .. j+rem-1 (rem <= NB) of the row's staged chunk in ONE batch: all
+// rem gathers issued before the first add, the adds in CSR order (so bitwise
+// the same sums as one entry at a time).  Without it a row's last entries
+// were one dependent gather each, and a ZINC row has 2-6 entries in all:
+// 3-4 round trips to L2 per row instead of one.  Source lanes past the group
+// wrap (__shfl width LPR); their values are never used.
+template <int V, int NB, int LPR>
+__device__ __forceinline__ void gather_batch(const float* __restrict__ X, int64_t ldx, int f,
+                                             bool fok, int cm, float wm, int j, int rem,
+                                             typename VecT<V>::type& acc) {
+  using vt = typename VecT<V>::type;
+  int c[NB];
+  float w[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    c[u] = __shfl(cm, j + u, LPR);
+    w[u] = __shfl(wm, j + u, LPR);
+  }
+  if (!fok) return;
+  vt x[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u)
+    if (u < rem) x[u] = vload<V>(X + (int64_t)c[u] * ldx + f);
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    float s = vget(acc, i);
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      if (u < rem) s = s + w[u] * vget(x[u], i);
+    vget(acc, i) = s;
+  }
+}
+
 // DEPTH gathers in flight per lane (4; 8 for long rows, k_poly_step_deep).
 // Loads are issued DEPTH at a time, the adds stay in CSR order (bitwise the
-// same result for any DEPTH).
+// same result for any DEPTH).  A staged chunk of <= 8 entries (every ZINC
+// row) and the < 4 entries after the 4-batches go as one gather_batch
+// (same-process A/B at the cfg2 step: +0.3-0.6 %; the L0 Laguerre step
+// 5.95 -> 5.6 us in a chain, profiles/r03_l_ab_poly_batch.txt).
 template <int V, int LPR, int DEPTH>
 __device__ __forceinline__ void poly_step_body(const PolyArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
@@ -134,6 +170,10 @@ __device__ __forceinline__ void poly_step_body(const PolyArgs& a, Blk blk) {
       const float wm = me < e1 ? (a.val ? a.val[me] : 1.f) : 0.f;
       const int cnt = e1 - eb < LPR ? e1 - eb : LPR;
       int j = 0;
+      if (cnt <= 8) {
+        gather_batch<V, 8, LPR>(X, a.ldx, f, fok, cm, wm, 0, cnt, acc);
+        continue;
+      }
       if constexpr (DEPTH == 8) {
         for (; j + 7 < cnt; j += 8) {  // eight gathers in flight per lane
           int c[8];
@@ -178,15 +218,7 @@ __device__ __forceinline__ void poly_step_body(const PolyArgs& a, Blk blk) {
           }
         }
       }
-      for (; j < cnt; ++j) {
-        const int c = __shfl(cm, j, LPR);
-        const float w = __shfl(wm, j, LPR);
-        if (fok) {
-          vt x = vload<V>(X + (int64_t)c * a.ldx + f);
-#pragma unroll
-          for (int i = 0; i < V; ++i) vget(acc, i) = vget(acc, i) + w * vget(x, i);
-        }
-      }
+      if (j < cnt) gather_batch<V, 3, LPR>(X, a.ldx, f, fok, cm, wm, j, cnt - j, acc);
     }
     if (!fok) continue;
     poly_epilogue<V>(a, row, f, acc, rsv);

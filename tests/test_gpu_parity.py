@@ -105,6 +105,30 @@ def test_spmm_skewed_rows(cuda):
     close(ops.spmm(op.fwd, dev(x)).cpu(), R.propagate(x, ei, w), 1e-6, "skew")
 
 
+@pytest.mark.parametrize("d", [3, 64, 128])
+def test_poly_step_ragged_rows_bitexact(cuda, d):
+    """Rows of 0..40 entries (every tail length of the batched gathers: a
+    chunk of <= 8 entries in one batch, 4-wide batches and a < 4 tail above,
+    chunks of 16 staged entries): the Laguerre basis equals the oracle's
+    recurrence over propagate bit for bit."""
+    from hlhgat import ops
+    gen = torch.Generator().manual_seed(3)
+    n = 400
+    deg = torch.arange(n) % 41
+    rows = torch.repeat_interleave(torch.arange(n), deg)
+    cols = torch.randint(0, n, (rows.numel(),), generator=gen)
+    o = torch.argsort(rows * n + cols, stable=True)
+    ei = torch.stack([rows[o], cols[o]]).contiguous()
+    w = torch.randn(ei.size(1), generator=gen)
+    x = torch.randn(n, d, generator=gen)
+    ref = _ref_basis(x, ei, w, 3, "laguerre")
+    op = ops.hodge_operator(dev(ei), dev(w), n)
+    T = ops.poly_basis(op, dev(x), 3, ops.POLY_LAGUERRE).cpu()
+    for k in range(2):
+        assert torch.equal(T[k], ref[k]), k
+    assert torch.equal(ops.spmm(op.fwd, dev(x)).cpu(), R.propagate(x, ei, w))
+
+
 # ---------------------------------------------------------------------------
 # polynomial basis (bit-exact) and full conv vs golden
 # ---------------------------------------------------------------------------

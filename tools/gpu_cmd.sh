@@ -14,8 +14,7 @@ step() {  # name timeout cmd...
   esac
   return 0
 }
-step t_new 300 python -u -m pytest tests/test_gpu_parity.py -k "prefetch or spmm or basis or laguerre" -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
-step ab 300 python tools/ab_step.py base nopf base2 nopf2 --rounds 6
-step kb 200 python tools/kbench.py --only "laguerre|basis|proj_fwd conv|proj_bn_fwd fused conv"
-step t_mr 300 python -u -m pytest tests/test_multirank_trainstep.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+step t_new 300 python -u -m pytest tests/test_gpu_parity.py -k "batch_hook or spmm or basis or laguerre or cheb" -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+step ab 300 python tools/ab_step.py base nobatch base2 nobatch2 --rounds 6
+step kb 200 python tools/kbench.py --only "laguerre|basis"
 echo "=== done"
