@@ -42,6 +42,9 @@ def mean_pool_sorted(x: torch.Tensor, counts: torch.Tensor,
 
 
 READOUT_ON_CHAIN = True  # A/B hook: False = the edge readout on the main stream
+# A/B hook: True = the edge chain waits for the main stream after HL_init_conv
+# even when the batch carries its incidence / degree tables (nothing to wait for)
+SYNC_SIDE_ALWAYS = False
 
 
 def mean_pool_cat(parts, side=None) -> torch.Tensor:
@@ -134,14 +137,19 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
             # over x_t rows), so size it by N_t and skip the host sync of max()
             p1 = adj2par1(data.edge_index, n_t, n_s)
             d = getattr(data, "deg_t", None)  # built at collate (padding rows: 1)
-            if d is None or d.device != x_t.device or d.numel() != n_t:
+            # device work issued here (degree / incidence builds on the main
+            # stream) must be ordered before the edge chain uses it; batches
+            # from collate carry both tables and issue none
+            launched = d is None or d.device != x_t.device or d.numel() != n_t
+            if launched:
                 d = degree(data.edge_index.view(-1), num_nodes=n_t)
                 if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
                     d = d.masked_fill(~valid_t, 1.0)
             if not x_t.is_cuda:
-                return p1, d, []
-            inc = p1.incidence()  # built here, cached for every NodeEdgeInt
-            return p1, d, [inc.rowptr, inc.edge_ids, inc.edge_index]  # fork orders them on main
+                return p1, d, False
+            launched = launched or getattr(data.edge_index, "_hlhgat_incidence", None) is None
+            p1.incidence()  # built here (or taken from collate), cached for every NodeEdgeInt
+            return p1, d, launched
 
         # the incidence build (sort + CSR of |B1|) after HL_init_conv (building it
         # on a third stream beside the conv measured 1.4 % slower: its sort
@@ -152,9 +160,10 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         with chains as ch:
             x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
                                          edge_weight_s)
-            par_1, D, _ = boundary()
+            par_1, D, launched = boundary()
             if dense:
-                ch.sync_side()  # the incidence tables (main) feed the edge chain
+                if launched or SYNC_SIDE_ALWAYS:
+                    ch.sync_side()  # tables built on main feed the edge chain
                 dt.append(x_t)
                 ds.append(x_s)
             x_s0, x_t0 = x_s, x_t

@@ -10,6 +10,7 @@ Variants (A/B hooks, not product settings):
   nochainbwd  chain-mode forward, the NodeEdgeInt backward with its own fork / join
   nofusedbn   projection and BatchNorm forward as two launches
   norows      Linear backward data gradient per (row block, column tile)
+  sync        the edge chain waits for main after HL_init_conv (collate tables)
   nomlp2      the readout MLP module by module (no two-layer fused node)
   noreadside  the edge readout mean on the main stream
   noreserve   BatchNorm workspaces not reserved before the capture
@@ -38,6 +39,7 @@ def set_variant(name, on):
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")
+    hodge_st_model.SYNC_SIDE_ALWAYS = on and name == "sync"
     train.BN_RESERVE_CHANNELS = 0 if (on and name == "noreserve") else 2048
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Scratch GPU command: the newest tests, a same-process A/B, kernel microbench.
+# Scratch GPU command: tests of the chain / replay paths, same-process A/B, timeline.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -14,7 +14,11 @@ step() {  # name timeout cmd...
   esac
   return 0
 }
-step t_new 300 python -u -m pytest tests/test_gpu_parity.py -k "batch_hook or spmm or basis or laguerre or cheb" -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
-step ab 300 python tools/ab_step.py base nobatch base2 nobatch2 --rounds 6
-step kb 200 python tools/kbench.py --only "laguerre|basis"
+step t_new 500 python -u -m pytest tests/test_train_step.py tests/test_multirank_trainstep.py tests/test_gpu_parity.py -k "fork or replay or graph or zinc or chain or train or rank or padded" -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread
+step ab 400 python tools/ab_step.py base sync oneexec base2 sync2 oneexec2 --rounds 6
+CAPS='{"rows_t": 23552, "rows_s": 25600, "nnz_t": 75776, "nnz_s": 112640}'
+rm -rf gpurun_out/tl
+step trace 300 rocprofv3 --kernel-trace -d gpurun_out/tl -o run --output-format csv -- python3 bench.py --replay-probe "$CAPS" --steps 12 --warmup 4
+T=$(find gpurun_out/tl -name '*kernel_trace.csv' | head -1)
+python tools/replay_timeline.py "$T" --steps 3 --out gpurun_out/timeline2.csv && rm -rf gpurun_out/tl
 echo "=== done"
