@@ -69,8 +69,20 @@ def main():
             b.synchronize()
             ms = a.elapsed_time(b) / args.steps
             res.setdefault(s_us, []).append(round(ms - s_us / 1e3, 4))
+    # host time per step call (no synchronisation inside the loop)
+    lead["sleep_us"] = 0
+    torch.cuda.synchronize()
+    hs = []
+    for i in range(args.steps * 2):
+        t0 = time.perf_counter()
+        st(batches[i % len(batches)])
+        hs.append((time.perf_counter() - t0) * 1e3)
+    torch.cuda.synchronize()
+    hs.sort()
     print(json.dumps({"cycles_per_us": round(cyc_per_us, 1),
-                      "step_minus_sleep_ms": {str(k): v for k, v in res.items()}}))
+                      "step_minus_sleep_ms": {str(k): v for k, v in res.items()},
+                      "host_ms_per_call_median": round(hs[len(hs) // 2], 4),
+                      "host_ms_per_call_min": round(hs[0], 4)}))
 
 
 if __name__ == "__main__":
