@@ -4,8 +4,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/probes/launch_lead.py --steps 20 --rounds 3 > gpurun_out/lead.log 2>&1
-rc=$?; echo "=== lead rc=$rc"; grep -v amdgpu.ids gpurun_out/lead.log | tail -5
+timeout -k 10 400 python tools/ab_step.py base noupload base2 noupload2 --rounds 6 > gpurun_out/ab.log 2>&1
+rc=$?; echo "=== ab rc=$rc"; grep -v amdgpu.ids gpurun_out/ab.log | tail -5
 [ $rc -eq 0 ] || exit $rc
-DEBUG_HIP_FORCE_GRAPH_QUEUES=4 timeout -k 10 300 python tools/probes/launch_lead.py --steps 20 --rounds 2 > gpurun_out/lead4.log 2>&1
-rc=$?; echo "=== lead4 rc=$rc"; grep -v amdgpu.ids gpurun_out/lead4.log | tail -3
+timeout -k 10 300 python tools/probes/launch_lead.py --steps 20 --rounds 2 > gpurun_out/lead.log 2>&1
+rc=$?; echo "=== lead rc=$rc"; grep -v amdgpu.ids gpurun_out/lead.log | tail -3
