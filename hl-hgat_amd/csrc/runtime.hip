@@ -171,6 +171,7 @@ extern "C" int hlhgat_zero_fill(void* p, size_t bytes, void* stream) {
   int64_t g = ceil_div(n, 256);
   if (g > 1024) g = 1024;
   k_zero_words<<<(unsigned)g, 256, 0, as_stream(stream)>>>(static_cast<uint32_t*>(p), n);
+  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -233,6 +234,7 @@ extern "C" int hlhgat_copy2d_batched(int n, const float* const* src, const int64
   int64_t g = ceil_div(total, 256);
   if (g > 2048) g = 2048;
   k_copy2d_batched<<<(unsigned)g, 256, 0, as_stream(stream)>>>(a);
+  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

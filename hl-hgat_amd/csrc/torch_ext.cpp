@@ -1593,10 +1593,19 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       bt = pk.narrow(0, 2 * P * d, P);
       bs = pk.narrow(0, 2 * P * d + P, P);
     }
+    Fork fk(xt.get_device());
     Tensor Yt = at::empty({N, dn + de}, xt.options());  // [Qt | P2]
-    Tensor Ys = at::empty({E, de + dn}, xt.options());  // [Qs | P1]
     Tensor h1t = at::empty({N, dn}, xt.options());
-    Tensor h1s = at::empty({E, de}, xt.options());
+    // Ys / h1s are first written on the side stream, which in chain mode does
+    // not wait for the main stream: their blocks come from the side stream's
+    // pool (a block main freed may still be read by main's queued kernels)
+    Tensor Ys, h1s;
+    {
+      TStreamGuard g(fk.side);
+      Ys = at::empty({E, de + dn}, xt.options());  // [Qs | P1]
+      h1s = at::empty({E, de}, xt.options());
+    }
+    Ys.record_stream(fk.main);  // read by the node side's gather on main
     auto side = [&](const at::TensorList& p, const Tensor& h1, double m1, double e1, double m4,
                     double e4, const OptT& valid, SideMlp& o) {
       o.h1 = h1;
@@ -1613,15 +1622,10 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                  {A.size(1)}, A.size(0), W.size(0), b.data_ptr<float>(), out, stream_of(A));
     };
     SideMlp tn, te;
-    Fork fk(xt.get_device());
     const bool chain = chain_flag();
-    if (chain) {
-      // Ys / h1s are written on the side stream and Yt read there after the
-      // exchange, with no join at the end: keep their blocks for the side stream
-      Yt.record_stream(fk.side);
-      Ys.record_stream(fk.side);
-      h1s.record_stream(fk.side);
-    }
+    // Yt is read on the side stream after the exchange (no join at the end in
+    // chain mode): keep its block for the side stream
+    if (chain) Yt.record_stream(fk.side);
     // the edge GEMM needs this node's own weight pack (built on the main
     // stream above) unless a forward-wide pack (nei_prepack) was ordered before
     // the chains began
@@ -1711,8 +1715,16 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     //            packed 48 (no gradient: the weights' gradients go to pn / pe)
     variable_list out(49);
     const int64_t PN = 6, PE = 20;
+    Fork fk(xt.get_device());
     Tensor dYt = at::empty({N, dn + de}, xt.options());
-    Tensor dYs = at::empty({E, de + dn}, xt.options());
+    // dYs is first written on the side stream (which in chain mode does not
+    // wait for main): a block of the side stream's pool, kept for main's read
+    Tensor dYs;
+    {
+      TStreamGuard g(fk.side);
+      dYs = at::empty({E, de + dn}, xt.options());
+    }
+    dYs.record_stream(fk.main);
     auto side_bwd = [&](const Tensor& gy, int64_t P, const Tensor& g1, const Tensor& W3,
                         const Tensor& g4, int o0, Tensor dest, int q0, const Tensor& valid) {
       const Tensor &be1 = sv[q0 + 2], &b3 = sv[q0 + 3], &be4 = sv[q0 + 4];
@@ -1746,9 +1758,7 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     // (its consumers are the edge chain and the flush, which waits for every
     // deferring stream); only the exchange stays
     const bool chain_b = fdef && ctx->saved_data.count("chain") > 0;
-    Fork fk(xt.get_device());
     if (chain_b) {
-      dYs.record_stream(fk.side);
       dYt.record_stream(fk.side);
     } else {
       fk.side_waits_main();

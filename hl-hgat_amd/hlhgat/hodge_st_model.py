@@ -165,7 +165,8 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                 if launched or SYNC_SIDE_ALWAYS:
                     ch.sync_side()  # tables built on main feed the edge chain
                 dt.append(x_t)
-                ds.append(x_s)
+                with ch.side_context():  # a copy (no sink: eval, SyncBN) on x_s's chain
+                    ds.append(x_s)
             x_s0, x_t0 = x_s, x_t
             for i, _ in enumerate(self.channels):
                 for j in range(self.channels[i]):
@@ -186,7 +187,8 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                                     edge_weight_s)
                     if dense:
                         dt.append(x_t)
-                        ds.append(x_s)
+                        with ch.side_context():  # x_s was produced on the edge chain
+                            ds.append(x_s)
                     else:
                         x_t0 = torch.cat([x_t0, x_t], dim=-1)
                         x_s0 = torch.cat([x_s0, x_s], dim=-1)

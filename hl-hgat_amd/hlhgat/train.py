@@ -29,7 +29,7 @@ from typing import Callable, Dict, Optional, Tuple
 import torch
 import torch.distributed as dist
 
-from . import ops
+from . import _lib, ops
 
 __all__ = ["TrainStep", "batch_key", "forward_collectives"]
 
@@ -38,6 +38,9 @@ HIP_ADAM = True
 # DEFER_REDUCE = False (tests): every Linear backward launches its own split
 # reduction instead of handing it to the next one on its stream (same bits)
 DEFER_REDUCE = True
+# LANES = False: replay the captured graph as one hipGraph (torch's replay)
+# instead of one linear graph per stream lane (ops.Lanes)
+LANES = True
 
 
 def forward_collectives(model: torch.nn.Module) -> bool:
@@ -89,10 +92,17 @@ BN_RESERVE_CHANNELS = 2048  # BatchNorm workspace reserved per capture stream
 
 
 class _Captured:
-    def __init__(self, graph, static_batch, loss):
+    def __init__(self, graph, static_batch, loss, lanes=None):
         self.graph = graph
         self.batch = static_batch
         self.loss = loss
+        self.lanes = lanes  # ops.Lanes, or None: torch's replay of `graph`
+
+    def replay(self, device) -> None:
+        if self.lanes is not None:
+            self.lanes.launch(torch.cuda.current_stream(device).cuda_stream)
+        else:
+            self.graph.replay()
 
     def load(self, batch):
         """Copy a batch into the graph's static buffers: every contiguous
@@ -193,6 +203,14 @@ class TrainStep:
         self._pool = None
         self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
+        # lane replay (ops.Lanes): not for a step with random numbers (torch's
+        # replay advances the generator offsets; a lane replay would not) or
+        # with collectives inside the captured graph
+        self.lanes_off = None
+        if any(isinstance(m, torch.nn.Dropout) and m.p > 0 for m in model.modules()):
+            self.lanes_off = "dropout with p > 0 (random numbers in the graph)"
+        elif self.world > 1 and forward_collectives(model):
+            self.lanes_off = "collectives inside the captured graph"
         self._fwd_bwd_calls = 0
         self._ones = {}
 
@@ -283,7 +301,8 @@ class TrainStep:
                   else _clone_batch(batch))
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        g = torch.cuda.CUDAGraph()
+        use_lanes = LANES and self._ext is not None and self.lanes_off is None
+        g = torch.cuda.CUDAGraph(keep_graph=use_lanes)
         s = self._stream
         if self._ext is not None and BN_RESERVE_CHANNELS:
             # BatchNorm workspaces of every stream the capture uses, made (and
@@ -295,25 +314,40 @@ class TrainStep:
                 self._ext.bn_workspace_reserve(int(h), idx, BN_RESERVE_CHANNELS)
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        with torch.cuda.graph(g, pool=self._pool, stream=s):
-            loss = self._fwd_bwd(static)
-            if self.world == 1:
-                self._opt_step()
-            # every stream forked from the capture (the node / edge side streams,
-            # forks inside autograd backward nodes, which run on autograd's
-            # device thread) rejoins it before hipStreamEndCapture: an unjoined
-            # fork is what crashed capture_end in round 1
-            if self._ext is not None:
-                ops.join_capture_streams(self.device)
+        if use_lanes:
+            ops.capture_record(True)
+        try:
+            with torch.cuda.graph(g, pool=self._pool, stream=s):
+                loss = self._fwd_bwd(static)
+                if self.world == 1:
+                    self._opt_step()
+                # every stream forked from the capture (the node / edge side streams,
+                # forks inside autograd backward nodes, which run on autograd's
+                # device thread) rejoins it before hipStreamEndCapture: an unjoined
+                # fork is what crashed capture_end in round 1
+                if self._ext is not None:
+                    ops.join_capture_streams(self.device)
+        finally:
+            if use_lanes:
+                ops.capture_record(False)
         left = ops.side_streams_capturing(self.device) if self._ext is not None else []
         if left:
             raise RuntimeError(f"TrainStep: {len(left)} side stream(s) still capturing after the "
                                f"graph capture ended (unjoined fork); refusing the graph")
         ops.clear_caches()
         torch.cuda.current_stream(self.device).wait_stream(s)
+        lanes = None
+        if use_lanes:
+            try:
+                lanes = ops.Lanes(g.raw_cuda_graph(), s.cuda_stream)
+                self.stats["lanes"] = lanes.info()
+            except _lib.HlhgatError as e:  # e.g. a node type the split does not handle
+                self.lanes_off = f"lane split refused the graph: {e}"
+            if lanes is None:
+                g.instantiate()
         if len(self._graphs) >= self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
-        ent = _Captured(g, static, loss)
+        ent = _Captured(g, static, loss, lanes)
         self._graphs[key] = ent
         self.stats["captures"] += 1
         return ent
@@ -332,7 +366,7 @@ class TrainStep:
             self._capture(batch, key)
             return loss
         ent.load(batch)
-        ent.graph.replay()
+        ent.replay(self.device)
         if self.world > 1:
             self._exchange_and_update()
         self.stats["replay"] += 1

@@ -113,17 +113,28 @@ def laguerre_fast_conv_demo(x, edge_index, edge_weight, weights, bias):
     return out
 
 
+def _prop_ntc(x, edge_index, edge_weight):
+    """The 3-D branch of lib/Hodge_Cheb_Conv.py:409-414 / :421-425: [N, T, C]
+    transposed to [N, C, T], flattened per row, propagated, and back.  (The
+    reference flattens with .view(), which raises unless T == 1 or C == 1;
+    .reshape() gives the same rows wherever .view() succeeds.)"""
+    if x.dim() != 3:
+        return propagate(x, edge_index, edge_weight)
+    n, t, c = x.shape
+    y = propagate(x.transpose(1, 2).reshape(n, -1), edge_index, edge_weight)
+    return y.view(n, c, -1).transpose(1, 2)
+
+
 def cheb_conv(x, edge_index, edge_weight, weights, bias):
-    """lib/Hodge_Cheb_Conv.py:394-439 (2-D x; the 3-D path only permutes
-    features inside each propagated row)."""
+    """lib/Hodge_Cheb_Conv.py:394-439 (2-D and 3-D x)."""
     Tx_0 = x
     Tx_1 = x
     out = F.linear(Tx_0, weights[0])
     if len(weights) > 1:
-        Tx_1 = propagate(x, edge_index, edge_weight)                      # :416
+        Tx_1 = _prop_ntc(x, edge_index, edge_weight)                      # :409-416
         out = out + F.linear(Tx_1, weights[1])
     for w in weights[2:]:
-        Tx_2 = propagate(Tx_1, edge_index, edge_weight)                   # :430
+        Tx_2 = _prop_ntc(Tx_1, edge_index, edge_weight)                   # :421-430
         Tx_2 = 2. * Tx_2 - Tx_0                                           # :432
         out = out + F.linear(Tx_2, w)
         Tx_0, Tx_1 = Tx_1, Tx_2

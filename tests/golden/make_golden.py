@@ -49,18 +49,24 @@ def conv_cases(ref, b):
         for K in Ks:
             for side in ("t", "s"):
                 cases.append((kind, K, side, 2))
-    cases.append(("laguerre", 3, "t", 3))  # 3-D input [N, T, C]
-    for kind, K, side, ndim in cases:
+    cases = [c + (3, 12, "") for c in cases]
+    cases.append(("laguerre", 3, "t", 3, 3, 12, ""))  # 3-D input [N, T, C]
+    # 3-D Chebyshev (:409-428): the reference transposes to [N, C, T] and then
+    # .view()s it, which raises for T > 1 and C > 1 (a non-contiguous view);
+    # the shapes it accepts are T = 1 or C = 1
+    cases.append(("cheb", 4, "s", 3, 1, 12, "_T1"))
+    cases.append(("cheb", 4, "t", 3, 3, 1, "_C1"))
+    for kind, K, side, ndim, T, cin, tag in cases:
         ei = getattr(b, "edge_index_" + side)
         ew = getattr(b, "edge_weight_" + side)
         n = getattr(b, "x_" + side).shape[0]
-        cin, cout = 12, 16
+        cout = 16
         torch.manual_seed(K * 7 + (side == "s"))
         cls = ref.HodgeLaguerreConv if kind == "laguerre" else ref.HodgeChebConv
         conv = cls(cin, cout, K=K)
         with torch.no_grad():
             conv.bias.uniform_(-0.5, 0.5)  # reference zero-inits; exercise the bias path
-        shape = (n, cin) if ndim == 2 else (n, 3, cin)
+        shape = (n, cin) if ndim == 2 else (n, T, cin)
         x = torch.randn(*shape, generator=gen).requires_grad_(True)
         out = conv(x, ei, ew)
         R = torch.randn(out.shape, generator=gen)
@@ -70,7 +76,7 @@ def conv_cases(ref, b):
         for k, lin in enumerate(conv.lins):
             arrays[f"w{k}"] = _np(lin.weight)
             arrays[f"grad_w{k}"] = _np(lin.weight.grad)
-        _save(f"conv_{kind}_K{K}_{side}_{ndim}d", K=np.int64(K), **arrays)
+        _save(f"conv_{kind}_K{K}_{side}_{ndim}d{tag}", K=np.int64(K), **arrays)
 
 
 def nei_cases(ref, b):

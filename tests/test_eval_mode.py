@@ -147,3 +147,33 @@ def test_hip_eval_matches_reference(cuda, name):
     err = close(out.cpu(), g["out"], 1e-5, "eval out")
     ops.check_device_errors()
     print(f"[eval] {name}: running stats max err {worst:.2e}, eval out max err {err:.2e}")
+
+
+@pytest.mark.gpu
+def test_eval_chains_bitwise_one_stream(cuda):
+    """Eval mode with the node / edge chains on two streams (ops.Chains):
+    BatchNorm on running statistics does not write into the dense slab's sink,
+    so DenseConcat copies each edge block; the copy runs on the edge chain
+    (where the block was produced).  Outputs equal the one-stream run bit for
+    bit, repeated with the allocator churned between runs."""
+    import hlhgat
+    from hlhgat import ops
+    g, train, ev = _inputs("eval_cfg2_zinc", lambda gg, p: _product_data(gg, p, cuda))
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**CASES["eval_cfg2_zinc"][2])
+    fill_params(m, int(g["seed"]))
+    m = m.to(cuda).eval()
+    outs = {}
+    prev = ops.CHAINS_ENABLED
+    try:
+        for on in (False, True, True):
+            ops.CHAINS_ENABLED = on
+            ops.clear_caches()
+            with torch.no_grad():
+                junk = [torch.full((1 << 20,), float(i), device=cuda) for i in range(8)]
+                del junk  # freed main-stream blocks, reused by the next forward
+                outs.setdefault(on, []).append(_call(m, ev).cpu())
+    finally:
+        ops.CHAINS_ENABLED = prev
+    torch.cuda.synchronize()
+    for o in outs[True]:
+        assert torch.equal(o, outs[False][0])

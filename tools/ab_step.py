@@ -14,6 +14,7 @@ Variants (A/B hooks, not product settings):
   nomlp2      the readout MLP module by module (no two-layer fused node)
   noreadside  the edge readout mean on the main stream
   noreserve   BatchNorm workspaces not reserved before the capture
+  nolanes     torch's replay of the whole captured graph (no stream lanes)
 """
 import argparse
 import json
@@ -41,6 +42,7 @@ def set_variant(name, on):
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")
     hodge_st_model.SYNC_SIDE_ALWAYS = on and name == "sync"
     train.BN_RESERVE_CHANNELS = 0 if (on and name == "noreserve") else 2048
+    train.LANES = not (on and name == "nolanes")
 
 
 def main():
