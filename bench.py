@@ -739,6 +739,89 @@ def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
     return out
 
 
+WORKLOADS = {"cfg2": None, "cfg3": "cfg3_cifar_attpool", "cfg4": "cfg4_pepfunc_attpool",
+             "cfg5": "cfg5_tsp_pyr"}
+
+
+def head_workload(args, rank, world, device):
+    """`--workload cfg3|cfg4|cfg5`: the BASELINE configs[2..4] head as the
+    bench's measured step on `world` GPUs, sharded by graph (each rank trains
+    its own per-GPU batch of the head's size, weak scaling) through TrainStep:
+    captured hipGraph per rank, one-bucket gradient all-reduce over RCCL, HIP
+    Adam -- the reference's per-step loop (main_pepfunc...:171-199,
+    main_TSP...:357-441) on device-resident batches.  Barrier + synchronise
+    around exactly `steps` steps, max over ranks, one JSON line from rank 0."""
+    import numpy as np
+    import hlhgat
+    from hlhgat.distributed import max_over_ranks
+    from hlhgat.hodge_dataset import level_caps, pad_batch, pad_levels, static_caps
+    from hlhgat.train import TrainStep
+    name = WORKLOADS[args.workload]
+    c = HEADS[name]
+    kind, G = c["kind"], c["graphs"]
+    log(f"[rank {rank}] {name}: generating {args.batches} x {G} synthetic graphs")
+    pool = _head_pool(kind, 2 * G, seed=rank)  # each rank its own shard of graphs
+    rng = np.random.RandomState(7 + rank)
+    raw = [_head_collate(kind, [pool[i] for i in rng.choice(len(pool), G, replace=False)])
+           for _ in range(args.batches)]
+    if kind == "tsp":
+        cs = [static_caps(b, 512) for b in raw]
+        caps = {k: max(x[k] for x in cs) for k in cs[0]}
+    else:
+        caps = level_caps(raw, 512)
+    if world > 1:
+        # one capacity bucket on every rank, the largest of any rank: the same
+        # step shape everywhere (padding rows are inert)
+        dicts = [caps] if kind == "tsp" else caps
+        flat = [(i, k) for i, d in enumerate(dicts) for k in sorted(d)]
+        t = torch.tensor([dicts[i][k] for i, k in flat], dtype=torch.int64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        for (i, k), v in zip(flat, t.tolist()):
+            dicts[i][k] = int(v)
+    if kind == "tsp":
+        padded = [pad_batch(b, caps).to(device) for b in raw]
+    else:
+        padded = [[x.to(device) for x in pad_levels(b, caps)] for b in raw]
+    torch.manual_seed(0)
+    m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
+    step = TrainStep(m, lambda o, d, k=kind: _head_loss(k, o, d), lr=1e-3,
+                     graphs=not args.eager)
+    for i in range(args.warmup):
+        step(padded[i % len(padded)])
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] warmup done {step.stats} lanes_off={step.lanes_off}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(padded[i % len(padded)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, device)
+    hlhgat.ops.check_device_errors()
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        print(json.dumps({
+            "metric": f"graphs/sec HL-HGAT fwd+bwd, {name} head, 1/2/4/8 MI355X",
+            "value": round(world * G * args.steps / elapsed, 1), "unit": "graphs/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic simplex graphs of the config's shape (random-init weights)",
+            "config": {"workload": f"BASELINE {name}: {c['cls']} {c['kw']}", "graphs_per_gpu": G,
+                       "global_batch": world * G, "parallelism": f"dp{world}",
+                       "execution": "eager" if args.eager else
+                       f"captured hipGraph per rank ({step.stats.get('captures')} capture(s)), "
+                       f"{'lane replay' if 'lanes' in step.stats else 'graph replay'}, "
+                       f"gradient all-reduce over {'RCCL' if world > 1 else 'none'}",
+                       "caps": caps},
+            "stats": {k: v for k, v in step.stats.items()}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def h2d_leg(batch_cpu, device, reps=10):
     """The reference's loop copies each batch to the device every step
     (data.to(device)); bench.py's `value` excludes it (inputs resident in
@@ -790,7 +873,12 @@ def dry_run(args):
     rank, world, device = init_distributed("gloo")
     if world != args.gpus:
         raise SystemExit(f"bench.py: world size {world} != --gpus {args.gpus}")
-    buf = torch.ones(650_000)
+    n_par = 650_000  # cfg2's gradient bucket
+    if args.workload != "cfg2":  # the head's own bucket (model built on the CPU)
+        import hlhgat
+        c = HEADS[WORKLOADS[args.workload]]
+        n_par = sum(p.numel() for p in getattr(hlhgat, c["cls"])(**c["kw"]).parameters())
+    buf = torch.ones(n_par)
     for _ in range(args.warmup):
         if world > 1:
             dist.all_reduce(buf)
@@ -808,7 +896,8 @@ def dry_run(args):
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 3),
                           "dry_run": True, "backend": dist.get_backend() if world > 1 else None,
-                          "ranks_seen": world}), flush=True)
+                          "ranks_seen": world, "workload": args.workload,
+                          "bucket_floats": n_par}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -839,6 +928,10 @@ def main():
                     help="rooflines from the eager stamped pass only (no rocprofv3 child)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rendezvous / timing contract on gloo + CPU, no model")
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS),
+                    help="cfg2 (default): BASELINE configs[1], the ZINC model, the headline; "
+                         "cfg3 / cfg4 / cfg5: the configs[2..4] head as the measured step "
+                         "(sharded by graph over --gpus ranks)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
@@ -855,6 +948,8 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: world size {world} != --gpus {args.gpus} "
                          f"(launch with --nproc-per-node {args.gpus}, or without torchrun)")
+    if args.workload != "cfg2":
+        return head_workload(args, rank, world, device)
 
     import hlhgat
     from hlhgat import ops

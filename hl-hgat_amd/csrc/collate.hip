@@ -124,6 +124,26 @@ extern "C" int hlhgat_collate(const hlhgat_packed_graphs_t* d, const int64_t* id
     const int64_t e0 = d->edge_ptr[g], e1 = d->edge_ptr[g + 1];
     const int64_t t0 = d->lt_ptr[g], t1 = d->lt_ptr[g + 1];
     const int64_t s0 = d->ls_ptr[g], s1 = d->ls_ptr[g + 1];
+    // the packed dataset is input data: every index must lie inside its own
+    // graph and each Laplacian COO must be row-sorted (coo_csr below counts
+    // rows into rowptr), else no write happens
+    HLH_CHECK_ARG(n1 >= n0 && e1 >= e0 && t1 >= t0 && s1 >= s0,
+                  "collate: graph %lld has negative sizes", (long long)g);
+    for (int64_t k = t0; k < t1; ++k)
+      HLH_CHECK_ARG(d->lt_row[k] >= 0 && d->lt_row[k] < n1 - n0 && d->lt_col[k] >= 0 &&
+                        d->lt_col[k] < n1 - n0 && (k == t0 || d->lt_row[k] >= d->lt_row[k - 1]),
+                    "collate: graph %lld: L0 entry %lld out of range or not row-sorted",
+                    (long long)g, (long long)(k - t0));
+    for (int64_t k = s0; k < s1; ++k)
+      HLH_CHECK_ARG(d->ls_row[k] >= 0 && d->ls_row[k] < e1 - e0 && d->ls_col[k] >= 0 &&
+                        d->ls_col[k] < e1 - e0 && (k == s0 || d->ls_row[k] >= d->ls_row[k - 1]),
+                    "collate: graph %lld: L1 entry %lld out of range or not row-sorted",
+                    (long long)g, (long long)(k - s0));
+    for (int64_t e = e0; e < e1; ++e)
+      HLH_CHECK_ARG(d->b1_src[e] >= 0 && d->b1_src[e] < n1 - n0 && d->b1_dst[e] >= 0 &&
+                        d->b1_dst[e] < n1 - n0,
+                    "collate: graph %lld: B1 edge %lld out of range", (long long)g,
+                    (long long)(e - e0));
     std::memcpy(o->x_t + nt * Ft, d->x_t + n0 * Ft, sizeof(float) * (size_t)((n1 - n0) * Ft));
     std::memcpy(o->x_s + ns * Fs, d->x_s + e0 * Fs, sizeof(float) * (size_t)((e1 - e0) * Fs));
     for (int64_t k = t0; k < t1; ++k) {  // L0 COO: node offset

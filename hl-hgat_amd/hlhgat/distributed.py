@@ -121,6 +121,19 @@ def revert_sync_batchnorm(module: torch.nn.Module) -> torch.nn.Module:
     return module
 
 
+# Tests: run the collectives of a one-rank group too (RCCL on a world-size-1
+# nccl group on a one-GPU box), so the captured-collective paths execute
+COLLECTIVES_AT_WORLD_1 = False
+
+
+def collectives_on(group=None) -> bool:
+    """True when the data-parallel collectives run: an initialised process
+    group of more than one rank (or of one, with COLLECTIVES_AT_WORLD_1)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or COLLECTIVES_AT_WORLD_1
+
+
 def max_over_ranks(value: float, device: torch.device = torch.device("cpu")) -> float:
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return value
@@ -140,7 +153,7 @@ class _GlobalMax(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         m = x.max().reshape(1).clone()
-        if dist.is_initialized() and dist.get_world_size() > 1:
+        if collectives_on():
             dist.all_reduce(m, op=dist.ReduceOp.MAX)
         ctx.save_for_backward(x, m)
         return m.reshape(())
@@ -150,7 +163,7 @@ class _GlobalMax(torch.autograd.Function):
         x, m = ctx.saved_tensors
         hit = (x == m).to(x.dtype)
         gc = torch.stack([g.reshape(()).to(x.dtype), hit.sum()])
-        if dist.is_initialized() and dist.get_world_size() > 1:
+        if collectives_on():
             dist.all_reduce(gc)
         return hit * (gc[0] / gc[1])
 
@@ -160,7 +173,7 @@ def global_max(x: torch.Tensor) -> torch.Tensor:
     the attention by its batch max (lib/Hodge_ST_Model.py:1061-1062), which
     under graph sharding must span every rank's graphs to equal the
     single-process result (parity caveat 2).  One process: x.max()."""
-    if not (dist.is_initialized() and dist.get_world_size() > 1):
+    if not collectives_on():
         return x.max()
     return _GlobalMax.apply(x)
 

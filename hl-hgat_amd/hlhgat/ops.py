@@ -1392,8 +1392,9 @@ def _all_gather_rows(t: torch.Tensor, group) -> torch.Tensor:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return t.view(1, -1)
+    from .distributed import collectives_on
     world = dist.get_world_size(group)
-    if world == 1:
+    if not collectives_on(group):
         return t.view(1, -1)
     out = torch.empty(world, t.numel(), dtype=t.dtype, device=t.device)
     if dist.get_backend(group) == "nccl":

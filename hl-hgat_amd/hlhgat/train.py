@@ -30,8 +30,9 @@ import torch
 import torch.distributed as dist
 
 from . import _lib, ops
+from .distributed import collectives_on
 
-__all__ = ["TrainStep", "batch_key", "forward_collectives"]
+__all__ = ["TrainStep", "InferStep", "batch_key", "forward_collectives"]
 
 # HIP_ADAM = False: torch's fused Adam instead of hlhgat_adam_flat
 HIP_ADAM = True
@@ -190,8 +191,15 @@ class TrainStep:
                 "exp_avg_sq": torch.zeros_like(self.flat)}
             self._hyper = (lr, betas, eps, weight_decay)
         self.world = dist.get_world_size() if dist.is_initialized() else 1
+        # the gradient exchange runs (world > 1, or a one-rank group in the
+        # tests' COLLECTIVES_AT_WORLD_1 mode)
+        self._exchange = collectives_on()
+        # under RCCL the all-reduce, the 1/W scale and Adam are captured into
+        # the step's graph; under gloo (host collectives) they run after it
+        self._exchange_in_graph = (self.graphs and self._exchange
+                                   and dist.get_backend() == "nccl")
         self.graphs_off = None
-        if self.graphs and self.world > 1 and dist.get_backend() != "nccl" \
+        if self.graphs and self._exchange and dist.get_backend() != "nccl" \
                 and forward_collectives(model):
             # a collective inside the forward (SyncBatchNorm statistics, the
             # attpool heads' batch-global max) runs on the host under gloo and
@@ -209,8 +217,6 @@ class TrainStep:
         self.lanes_off = None
         if any(isinstance(m, torch.nn.Dropout) and m.p > 0 for m in model.modules()):
             self.lanes_off = "dropout with p > 0 (random numbers in the graph)"
-        elif self.world > 1 and forward_collectives(model):
-            self.lanes_off = "collectives inside the captured graph"
         self._fwd_bwd_calls = 0
         self._ones = {}
 
@@ -282,7 +288,7 @@ class TrainStep:
                       lr, betas, eps, wd)
 
     def _exchange_and_update(self) -> None:
-        if self.world > 1:
+        if self._exchange:
             # one contiguous bucket; mean over ranks as DDP
             dist.all_reduce(self.flat_grad)
             self.flat_grad.div_(self.world)
@@ -319,7 +325,9 @@ class TrainStep:
         try:
             with torch.cuda.graph(g, pool=self._pool, stream=s):
                 loss = self._fwd_bwd(static)
-                if self.world == 1:
+                if self._exchange_in_graph:
+                    self._exchange_and_update()  # RCCL all-reduce + scale + Adam, captured
+                elif not self._exchange:
                     self._opt_step()
                 # every stream forked from the capture (the node / edge side streams,
                 # forks inside autograd backward nodes, which run on autograd's
@@ -367,10 +375,105 @@ class TrainStep:
             return loss
         ent.load(batch)
         ent.replay(self.device)
-        if self.world > 1:
+        if self._exchange and not self._exchange_in_graph:
             self._exchange_and_update()
         self.stats["replay"] += 1
         return ent.loss
 
     def state_dict(self):
         return {"model": self.model.state_dict(), "opt": self.opt.state_dict()}
+
+
+class InferStep:
+    """Evaluation / serving: the reference's test() loop body
+    (main_zinc_HL_HGCNN_dense_int3_pyr.py:165-177, main_pepfunc...:201-225):
+    model.eval() and ``out = model(data)`` under torch.no_grad(), one batch
+    per call.  graphs=True captures the eval forward into a hipGraph per batch
+    shape (the first call of a shape runs eagerly, then captures) and replays
+    it as stream lanes (ops.Lanes); the returned output is the graph's static
+    buffer, valid until the next call with a batch of the same shape (clone
+    it to keep it)."""
+
+    def __init__(self, model: torch.nn.Module, graphs: bool = True, max_graphs: int = 32):
+        self.model = model
+        params = list(model.parameters())
+        dev = params[0].device if params else torch.device("cpu")
+        self.device = dev
+        self.graphs = bool(graphs) and dev.type == "cuda"
+        self.max_graphs = max_graphs
+        self._graphs: Dict[Tuple, _Captured] = {}
+        self._pool = None
+        self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
+        self.stats = {"eager": 0, "replay": 0, "captures": 0}
+        self.lanes_off = None
+        if any(isinstance(m, torch.nn.Dropout) and m.p > 0 and m.training
+               for m in model.modules()):
+            self.lanes_off = "dropout in training mode"
+
+    def _forward(self, batch):
+        was = self.model.training
+        self.model.eval()
+        try:
+            with torch.no_grad():
+                return self.model(batch)
+        finally:
+            self.model.train(was)
+
+    def _capture(self, batch, key):
+        static = ([_clone_batch(b) for b in batch] if isinstance(batch, (list, tuple))
+                  else _clone_batch(batch))
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        use_lanes = LANES and ops._ext is not None and self.lanes_off is None
+        g = torch.cuda.CUDAGraph(keep_graph=use_lanes)
+        s = self._stream
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        ops.clear_caches()
+        if use_lanes:
+            ops.capture_record(True)
+        try:
+            with torch.cuda.graph(g, pool=self._pool, stream=s):
+                out = self._forward(static)
+                ops.join_capture_streams(self.device)
+        finally:
+            if use_lanes:
+                ops.capture_record(False)
+        left = ops.side_streams_capturing(self.device)
+        if left:
+            raise RuntimeError(f"InferStep: {len(left)} side stream(s) still capturing after the "
+                               f"graph capture ended (unjoined fork); refusing the graph")
+        ops.clear_caches()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        lanes = None
+        if use_lanes:
+            try:
+                lanes = ops.Lanes(g.raw_cuda_graph(), s.cuda_stream)
+                self.stats["lanes"] = lanes.info()
+            except _lib.HlhgatError as e:
+                self.lanes_off = f"lane split refused the graph: {e}"
+            if lanes is None:
+                g.instantiate()
+        if len(self._graphs) >= self.max_graphs:
+            self._graphs.pop(next(iter(self._graphs)))
+        ent = _Captured(g, static, out, lanes)
+        self._graphs[key] = ent
+        self.stats["captures"] += 1
+        return ent
+
+    def __call__(self, batch):
+        if ops._ext is not None:
+            ops.check_device_errors(sync=False)
+        if not self.graphs:
+            self.stats["eager"] += 1
+            return self._forward(batch)
+        key = batch_key(batch)
+        ent = self._graphs.get(key)
+        if ent is None:
+            out = self._forward(batch)
+            self.stats["eager"] += 1
+            self._capture(batch, key)
+            return out
+        ent.load(batch)
+        ent.replay(self.device)
+        self.stats["replay"] += 1
+        return ent.loss  # the captured forward's output

@@ -205,6 +205,18 @@ def test_bench_gpus_n_spawns_n_ranks(n):
     assert line["dry_run"] is True and line["steps"] == 2
 
 
+@pytest.mark.parametrize("workload", ["cfg4", "cfg5"])
+def test_bench_workload_dry_run(workload):
+    """`--workload cfg4|cfg5` (BASELINE configs[3] peptides, configs[4] TSP:
+    the 8-GPU configs) goes through the same launcher: 2 ranks, the head's
+    own gradient bucket all-reduced on gloo."""
+    r, line = _bench(["--gpus", "2", "--dry-run", "--workload", workload, "--steps", "2",
+                      "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["workload"] == workload
+    assert line["bucket_floats"] > 1_000_000
+
+
 def test_bench_rank_count_mismatch_fails():
     """Under torchrun with 2 ranks, --gpus 3 must fail instead of reporting
     a wrong n_gpus."""

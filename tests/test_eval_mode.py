@@ -177,3 +177,33 @@ def test_eval_chains_bitwise_one_stream(cuda):
     torch.cuda.synchronize()
     for o in outs[True]:
         assert torch.equal(o, outs[False][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["eval_cfg2_zinc", "eval_cfg4_pepfunc"])
+def test_infer_step_replay_matches_eager_and_reference(cuda, name):
+    """hlhgat.train.InferStep (the reference's test() loop body, captured per
+    batch shape and replayed as stream lanes): replayed outputs equal the
+    eager eval forward bit for bit, and the reference's eval output within
+    1e-5."""
+    import hlhgat
+    from hlhgat.train import InferStep
+    g, _, ev = _inputs(name, lambda gg, p: _product_data(gg, p, cuda))
+    bufs = {k[4:]: T(np.asarray(g[k])) for k in g if k.startswith("buf/")}
+    m = getattr(hlhgat, CASES[name][1])(**CASES[name][2])
+    fill_params(m, int(g["seed"]))
+    m.load_state_dict(bufs, strict=False)
+    m = m.to(cuda).train()
+    inf = InferStep(m)
+    outs = [_call_out(inf(ev)).clone() for _ in range(4)]
+    torch.cuda.synchronize()
+    assert inf.stats["captures"] == 1 and inf.stats["replay"] == 3, inf.stats
+    assert "lanes" in inf.stats, (inf.stats, inf.lanes_off)
+    assert m.training  # InferStep restores the mode it found
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    close(outs[0].cpu(), g["out"], 1e-5, "eval out (InferStep)")
+
+
+def _call_out(out):
+    return out[0] if isinstance(out, tuple) else out

@@ -590,6 +590,17 @@ def test_native_collate_rejects_bad_input():
     g.edge_index_t = g.edge_index_t.flip(1)  # not row-sorted
     with pytest.raises(ValueError, match="row-sorted"):
         PackedGraphs([g])
+    # the native collate validates the packed arrays themselves (they point
+    # into host memory it writes through): indices outside their graph, and
+    # rows out of order, are refused before any write
+    for arr, v, what in (("lt_col", 10 ** 6, "L0 entry"), ("ls_row", -1, "L1 entry"),
+                         ("b1_dst", 999, "B1 edge"), ("lt_row", 0, "L0 entry")):
+        ds2 = PackedGraphs([zinc_like_graph(i, keig=15) for i in range(3)])
+        a = getattr(ds2, arr)
+        k = int(ds2.lt_ptr[2]) - 1 if arr == "lt_row" else 5  # lt_row: unsorted in graph 1
+        a[k] = v
+        with pytest.raises(HlhgatError, match=what):
+            ds2.collate(np.arange(3))
 
 
 def test_graph_loader_batches_in_order_and_shuffled():
