@@ -7,7 +7,11 @@
 // O(E log deg) for the matching and O(E) hashing for the edge map, no Python
 // per-edge loops.
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <limits>
 #include <numeric>
 #include <unordered_map>
@@ -133,5 +137,85 @@ extern "C" int hlhgat_mlgc_map(const int64_t* cluster, int64_t n_nodes, const in
   }
   *n_coarse_nodes = rank[(size_t)n_nodes];
   *n_coarse_edges = ne;
+  return HLHGAT_OK;
+}
+
+// One MLGC level for a whole batch of graphs (SuperpixelPipeline.batch, the
+// reference's per-sample get(), main_cifar10SP...:67-125): per graph, graclus
+// on L0's pattern (the i<j edge list both ways, unit weights, node order
+// perm) and the fine -> coarse map -- hlhgat_graclus + hlhgat_mlgc_map per
+// graph, the graphs spread over n_threads host threads.  All indices are
+// LOCAL to their graph; graph g's nodes are [node_ptr[g], node_ptr[g+1]) of
+// perm / c_node, its edges [edge_ptr[g], edge_ptr[g+1]) of edges ([2][E]) /
+// c_edge, and its coarse edges are written from column edge_ptr[g] of
+// coarse_edges ([2][E], row stride E), coarse_n[g] / coarse_e[g] sizes.
+extern "C" int hlhgat_mlgc_batch(int64_t n_graphs, const int64_t* node_ptr,
+                                 const int64_t* edge_ptr, const int64_t* edges,
+                                 const int64_t* perm, int n_threads, int64_t* c_node,
+                                 float* c_edge, int64_t* coarse_edges, int64_t* coarse_n,
+                                 int64_t* coarse_e) {
+  HLH_CHECK_ARG(n_graphs >= 0 && node_ptr && edge_ptr && coarse_n && coarse_e,
+                "mlgc_batch: bad arguments");
+  const int64_t N = n_graphs ? node_ptr[n_graphs] : 0, E = n_graphs ? edge_ptr[n_graphs] : 0;
+  HLH_CHECK_ARG(node_ptr[0] == 0 && edge_ptr[0] == 0 && (N == 0 || (perm && c_node)) &&
+                    (E == 0 || (edges && c_edge && coarse_edges)),
+                "mlgc_batch: bad offsets or NULL arrays");
+  for (int64_t g = 0; g < n_graphs; ++g)
+    HLH_CHECK_ARG(node_ptr[g + 1] >= node_ptr[g] && edge_ptr[g + 1] >= edge_ptr[g],
+                  "mlgc_batch: offsets of graph %lld decrease", (long long)g);
+  std::atomic<int64_t> next{0};
+  std::atomic<int> rc_first{HLHGAT_OK};
+  std::mutex msg_mu;
+  std::string msg;
+  auto worker = [&]() {
+    std::vector<int64_t> both, ei, cl, ce;
+    for (;;) {
+      const int64_t g = next.fetch_add(1);
+      if (g >= n_graphs || rc_first.load() != HLHGAT_OK) return;
+      const int64_t n0 = node_ptr[g], n = node_ptr[g + 1] - n0;
+      const int64_t e0 = edge_ptr[g], m = edge_ptr[g + 1] - e0;
+      ei.resize((size_t)(2 * m));
+      both.resize((size_t)(4 * m));
+      for (int64_t k = 0; k < m; ++k) {
+        const int64_t i = edges[e0 + k], j = edges[E + e0 + k];
+        ei[(size_t)k] = i;
+        ei[(size_t)(m + k)] = j;
+        both[(size_t)k] = i;                // rows: i then j
+        both[(size_t)(m + k)] = j;
+        both[(size_t)(2 * m + k)] = j;      // cols: j then i
+        both[(size_t)(3 * m + k)] = i;
+      }
+      cl.resize((size_t)n);
+      ce.resize((size_t)std::max<int64_t>(2 * m, 2));
+      int64_t n1 = 0, ne = 0;
+      int rc = hlhgat_graclus(both.data(), nullptr, 2 * m, n, perm + n0, cl.data());
+      if (rc == HLHGAT_OK)
+        rc = hlhgat_mlgc_map(cl.data(), n, ei.data(), m, c_node + n0, c_edge + e0, ce.data(),
+                             &n1, &ne);
+      if (rc != HLHGAT_OK) {
+        int ok = HLHGAT_OK;
+        if (rc_first.compare_exchange_strong(ok, rc)) {
+          std::lock_guard<std::mutex> lk(msg_mu);
+          msg = std::string("graph ") + std::to_string(g) + ": " + hlhgat_last_error();
+        }
+        return;
+      }
+      for (int64_t k = 0; k < ne; ++k) {
+        coarse_edges[e0 + k] = ce[(size_t)k];
+        coarse_edges[E + e0 + k] = ce[(size_t)(m + k)];
+      }
+      coarse_n[g] = n1;
+      coarse_e[g] = ne;
+    }
+  };
+  const int T = std::max(1, std::min<int>(n_threads, (int)std::min<int64_t>(n_graphs, 64)));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+  if (rc_first.load() != HLHGAT_OK) {
+    hlhgat::set_error("mlgc_batch: %s", msg.c_str());
+    return rc_first.load();
+  }
   return HLHGAT_OK;
 }

@@ -39,6 +39,8 @@ SIGNATURES = {
                                   c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, P_i64, P_i64]),
     "hlhgat_graclus": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "hlhgat_mlgc_map": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, P_i64, P_i64]),
+    "hlhgat_mlgc_batch": (c_i32, [c_i64, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp]),
     "hlhgat_gather_f32": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlhgat_collate_sizes": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_collate": (c_i32, [c_vp, c_vp, c_i64, c_vp]),

@@ -16,6 +16,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import os
+
 import numpy as np
 import torch
 
@@ -1041,6 +1043,48 @@ def mlgc_map(cluster, edge_index):
         e1 = e1[:, :0]
     return c_node, c_edge, np.ascontiguousarray(e1.reshape(2, -1)[:, :ne.value]) if E else e1, \
         int(n1.value)
+
+
+def mlgc_batch(edge_lists, ns, perms, threads: int = 0):
+    """One MLGC level for a batch of graphs by one native call
+    (hlhgat_mlgc_batch): per graph, graclus over its i<j edge list taken both
+    ways with unit weights in node order perms[g], then mlgc_map -- the same
+    results as [mlgc_map(graclus(both, n, ones, perm=p), ei) ...] graph by
+    graph, on host threads.  Returns [(c_node, c_edge, coarse edge_index, n1)]
+    per graph, like mlgc_map."""
+    from ._lib import LIB, check
+    G = len(ns)
+    node_ptr = np.zeros(G + 1, np.int64)
+    node_ptr[1:] = np.cumsum(np.asarray(ns, np.int64))
+    ms = [int(np.asarray(e).shape[1]) for e in edge_lists]
+    edge_ptr = np.zeros(G + 1, np.int64)
+    edge_ptr[1:] = np.cumsum(np.asarray(ms, np.int64))
+    E = int(edge_ptr[-1])
+    edges = np.ascontiguousarray(np.concatenate(
+        [np.asarray(e, np.int64).reshape(2, -1) for e in edge_lists], axis=1)
+        if G else np.zeros((2, 0), np.int64))
+    perm = np.ascontiguousarray(np.concatenate([np.asarray(p, np.int64) for p in perms])
+                                if G else np.zeros(0, np.int64))
+    if perm.size != node_ptr[-1]:
+        raise ValueError("mlgc_batch: one permutation of each graph's nodes expected")
+    c_node = np.empty(int(node_ptr[-1]), np.int64)
+    c_edge = np.empty(E, np.float32)
+    ce = np.empty((2, max(E, 1)), np.int64)
+    cn = np.empty(G, np.int64)
+    cm = np.empty(G, np.int64)
+    threads = threads or min(8, os.cpu_count() or 1)
+    check(LIB.hlhgat_mlgc_batch(G, node_ptr.ctypes.data, edge_ptr.ctypes.data, edges.ctypes.data,
+                                perm.ctypes.data, threads, c_node.ctypes.data, c_edge.ctypes.data,
+                                ce.ctypes.data, cn.ctypes.data, cm.ctypes.data), "mlgc_batch")
+    ce = ce.reshape(2, -1)
+    out = []
+    for g in range(G):
+        n0, n1_ = node_ptr[g], node_ptr[g + 1]
+        e0, e1 = edge_ptr[g], edge_ptr[g + 1]
+        out.append((c_node[n0:n1_], c_edge[e0:e1],
+                    np.ascontiguousarray(ce[:, e0:e0 + cm[g]]) if E else np.zeros((2, 0), np.int64),
+                    int(cn[g])))
+    return out
 
 
 def to_undirected_mean(edge_index, weight, n: int):

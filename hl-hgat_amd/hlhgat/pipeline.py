@@ -46,7 +46,7 @@ import numpy as np
 import torch
 
 from .hodge_dataset import (Batch, PairData, collate, dense_to_sparse, graclus, hodge_laplacians,
-                            mlgc_map)
+                            mlgc_batch, mlgc_map)
 
 __all__ = ["SuperpixelPipeline", "to_undirected_min", "superpixel_raw"]
 
@@ -151,12 +151,9 @@ class SuperpixelPipeline:
         ns = [int(self.n[i]) for i in idx]
         # MLGC on the host: graclus on L0's pattern (= the edges, both ways; its
         # self-loops are dropped by graclus) with unit weights, the fine -> coarse map
-        cmaps = []
-        for b, (ei, n) in enumerate(zip(eis, ns)):
-            both = np.concatenate([ei, ei[::-1]], axis=1)
-            perm = perms[b] if perms is not None else rng.permutation(n)
-            lab = graclus(both, n, weight=np.ones(both.shape[1]), perm=perm)
-            cmaps.append(mlgc_map(lab, ei))
+        # (all graphs in one native call on host threads: hlhgat_mlgc_batch)
+        pl = [perms[b] if perms is not None else rng.permutation(n) for b, n in enumerate(ns)]
+        cmaps = mlgc_batch(eis, ns, pl)
         if str(device) == "cpu":
             lv0, lv1 = self._levels_host(idx, eis, attrs, ns, cmaps)
         else:

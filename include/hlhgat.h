@@ -170,6 +170,20 @@ int hlhgat_graclus(const int64_t* edge_index, const double* weight, int64_t n_ed
 int hlhgat_mlgc_map(const int64_t* cluster, int64_t n_nodes, const int64_t* edge_index,
                     int64_t n_edges, int64_t* c_node, float* c_edge, int64_t* coarse_edges,
                     int64_t* n_coarse_nodes, int64_t* n_coarse_edges);
+/* One MLGC level for a batch of graphs, the per-sample work of the
+ * reference's CIFAR10SP get() (main_cifar10SP_HL_HGCNN_dense_int3_attpool.py:
+ * 94-103: MLGC on every sample): per graph g, hlhgat_graclus over its i<j
+ * edge list taken both ways (unit weights, node order perm) then
+ * hlhgat_mlgc_map over the i<j list, the graphs spread over n_threads host
+ * threads.  Indices are local to each graph: its nodes are [node_ptr[g],
+ * node_ptr[g+1]) of perm / c_node, its edges [edge_ptr[g], edge_ptr[g+1]) of
+ * edges ([2][E], E = edge_ptr[n_graphs]) / c_edge; its coarse edges go to
+ * columns [edge_ptr[g], edge_ptr[g] + coarse_e[g]) of coarse_edges ([2][E]);
+ * coarse_n[g] = its coarse node count. */
+int hlhgat_mlgc_batch(int64_t n_graphs, const int64_t* node_ptr, const int64_t* edge_ptr,
+                      const int64_t* edges, const int64_t* perm, int n_threads, int64_t* c_node,
+                      float* c_edge, int64_t* coarse_edges, int64_t* coarse_n,
+                      int64_t* coarse_e);
 
 /* ---- native data loader (HOST functions, host pointers) -----------------
  * Replaces the reference's per-step DataLoader collation of PairData

@@ -624,3 +624,30 @@ def test_graph_loader_batches_in_order_and_shuffled():
     assert not np.array_equal(seen, np.arange(90))
     b0 = next(iter(sh))
     _same_batch(b0, collate([gs[i] for i in sh.batch_indices(0)[0]], check_hodge=False))
+
+
+def test_native_mlgc_batch_equals_per_graph():
+    """hlhgat_mlgc_batch (one call, host threads) gives per graph exactly the
+    per-graph graclus(both directions, unit weights, perm) + mlgc_map."""
+    import numpy as np
+    from hlhgat.hodge_dataset import graclus, mlgc_batch, mlgc_map
+    from hlhgat.synthetic import knn_edges
+    rng = np.random.default_rng(4)
+    eis, ns, perms = [], [], []
+    for g in range(23):
+        n = int(rng.integers(1, 90))
+        ei = (knn_edges(rng.random((n, 2)), min(8, max(n - 1, 1))) if n > 1
+              else np.zeros((2, 0), np.int64))
+        ei = np.asarray(ei, np.int64)
+        ei = ei[:, ei[0] < ei[1]]
+        eis.append(ei)
+        ns.append(n)
+        perms.append(rng.permutation(n))
+    for threads in (1, 4):
+        got = mlgc_batch(eis, ns, perms, threads=threads)
+        for ei, n, p, (cn, ce, e1, n1) in zip(eis, ns, perms, got):
+            both = np.concatenate([ei, ei[::-1]], axis=1)
+            lab = graclus(both, n, weight=np.ones(both.shape[1]), perm=p)
+            rn, rce, re1, rn1 = mlgc_map(lab, ei)
+            assert np.array_equal(cn, rn) and np.array_equal(ce, rce)
+            assert np.array_equal(e1, re1) and n1 == rn1

@@ -39,8 +39,12 @@ ZKW = dict(channels=[1, 1], filters=[32, 32], mlp_channels=[32], K=3, keig=15)
 HEADKW = {"peptides": dict(channels=[1, 1], filters=[32, 64], mlp_channels=[64], K=3,
                            pool_loc=0),
           "cifar": dict(channels=[1, 1], filters=[32, 64], mlp_channels=[64], K=3, keig=10,
-                        pool_loc=0, l=0.5)}
+                        pool_loc=0, l=0.5),
+          # BASELINE configs[3] itself (peptides under 8-GPU DDP): K=6, pool_loc=1
+          "peptides_cfg4": dict(channels=[2, 2, 2], filters=[64, 128, 256], mlp_channels=[256],
+                                K=6, pool_loc=1)}
 HEADCLS = {"peptides": "HL_HGCNN_pepfunc_dense_int3_attpool",
+           "peptides_cfg4": "HL_HGCNN_pepfunc_dense_int3_attpool",
            "cifar": "HL_HGCNN_CIFAR10SP_dense_int3_attpool"}
 
 
@@ -61,7 +65,8 @@ def _zinc_shards(world=2):
 def _head_shards(kind, world=2):
     """[step][rank] level-batch lists; two shapes per rank, alternating."""
     from hlhgat.synthetic import two_level_batch
-    base = [[two_level_batch(kind, 6, seed=40 + 2 * r + a) for r in range(world)]
+    gen = "peptides" if kind.startswith("peptides") else kind
+    base = [[two_level_batch(gen, 6, seed=40 + 2 * r + a) for r in range(world)]
             for a in range(2)]
     return [base[s % 2] for s in range(STEPS)]
 
@@ -228,7 +233,7 @@ class _EmuMax(torch.autograd.Function):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["zinc", "peptides", "cifar"])
+@pytest.mark.parametrize("kind", ["zinc", "peptides", "peptides_cfg4", "cifar"])
 def test_trainstep_two_ranks_bitwise_one_process(cuda, kind, tmp_path):
     shards = _zinc_shards(2) if kind == "zinc" else _head_shards(kind, 2)
     path = str(tmp_path / "shards.pt")
