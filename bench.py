@@ -35,10 +35,11 @@ import subprocess
 import sys
 import time
 
-# the replayed step is two chains of kernels: let the HIP runtime run a
-# captured graph on two hardware queues (its default, four, adds cross-queue
-# dependencies: 2.74 -> 2.68 ms per step and 2.12 -> 1.83 ms of host time per
-# replay, same-box sweep tools/probes/graph_env_sweep.sh); read at HIP init
+# A launcher setting, not a product one: the step replays as stream lanes
+# (linear graphs), which this does not touch; it only shapes
+# the whole-graph replay that TrainStep falls back to (two hardware queues
+# instead of the runtime's four: 2.74 -> 2.68 ms per step).
+# Read at HIP init; a value set by the user wins.
 os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -237,10 +238,14 @@ def replay_census(caps, eager, steps=12, warmup=4, timeout=300):
         return None, f"only {len(marks)} steps in the trace"
     sel = list(zip(marks[-steps:-1], marks[-steps + 1:]))  # the last steps-1 full replays
     per = {k: [0.0, 0] for k in REPLAY_CLASSES}
-    spans, busys, disp = [], [], []
+    spans, busys, disp, sync = [], [], [], []
     for a, b in sel:
         st = rows[a + 1:b + 1]
-        iv = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in st)
+        # lane replay's signal / wait kernels (lanes.hip) are counted apart; a
+        # wait spinning on the other lane is not work, so not "busy"
+        sync.append(sum(1 for x in st if "k_lane_" in x["Kernel_Name"]))
+        iv = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in st
+                    if "k_lane_wait" not in x["Kernel_Name"])
         span = iv[-1][1] - iv[0][0] if iv else 0
         busy, cur_s, cur_e = 0, None, None
         for s0, e0 in iv:
@@ -264,6 +269,8 @@ def replay_census(caps, eager, steps=12, warmup=4, timeout=300):
     span_us = sum(spans) / n / 1e3
     busy_us = sum(busys) / n / 1e3
     out = {"steps_traced": n, "dispatches_per_step": round(sum(disp) / n, 1),
+           "lane_sync_dispatches_per_step": round(sum(sync) / n, 1),
+           "model_dispatches_per_step": round((sum(disp) - sum(sync)) / n, 1),
            "span_us": round(span_us, 1), "busy_us": round(busy_us, 1),
            "idle_us": round(span_us - busy_us, 1),
            "idle_frac": round((span_us - busy_us) / span_us, 4) if span_us else None,
@@ -583,40 +590,96 @@ def _guarded(name, fn, *a):
         return {"error": repr(e)[:400]}
 
 
-def cifar_pipeline_leg(device, c, G, n_batches=4):
+def cifar_pipeline_leg(device, c, G, n_batches=8):
     """Config 3 WITH the reference's per-sample work (its Dataset.get() runs
-    every epoch, main_cifar10SP...:67-125): hlhgat.pipeline.SuperpixelPipeline
-    builds each 256-graph batch from raw superpixel samples (dropout_edge
+    every epoch in num_workers DataLoader processes beside training,
+    main_cifar10SP...:67-125,214): hlhgat.pipeline.SuperpixelPipeline builds
+    each 256-graph batch from raw superpixel samples (dropout_edge
     augmentation, device Hodge builder + lambda_max, batched eigh PE, native
-    MLGC, both levels collated on the device), then the training step runs
-    on it (eagerly: every augmented batch has its own shape)."""
+    batched MLGC, both levels on the device) on a producer thread and its own
+    stream, pads both levels to one capacity bucket (pad_levels on the
+    device), and hands it over; the training step replays ONE captured graph
+    for every batch (TrainStep, lane replay) while the next batch is built.
+    Reported: the overlapped rate, and the pipeline alone / the serial sum."""
+    import queue
+    import threading
     import hlhgat
+    from hlhgat.hodge_dataset import level_caps, pad_levels
     from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
     from hlhgat.train import TrainStep
     raw = [superpixel_raw(5000 + i) for i in range(n_batches * G)]
     pipe = SuperpixelPipeline(raw, keig=c["kw"]["keig"] + 1, aug=True)
+
+    # the capacity bucket: the levels of every batch the timed run will build
+    # (augmentation is seeded, so the pre-pass sees the same shapes); a
+    # loader would take the dataset's bucket.  A capture is never made while
+    # the producer thread runs (a global-mode capture refuses other threads'
+    # allocations), so every timed step must replay.
+    caps = level_caps([pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device)
+                       for b in range(n_batches)], 512)
+
+    def fit(datas):
+        return pad_levels(datas, caps)
+
     torch.manual_seed(0)
     m = getattr(hlhgat, c["cls"])(**c["kw"]).to(device).train()
-    st = TrainStep(m, lambda o, d: _head_loss("cifar", o, d), lr=1e-3, graphs=False)
-    st(pipe.batch(range(G), seed=99, device=device))  # warm-up
+    st = TrainStep(m, lambda o, d: _head_loss("cifar", o, d), lr=1e-3, graphs=True)
+    main = torch.cuda.current_stream(device)
+
+    def produce(q, seeds):
+        s = torch.cuda.Stream(device=device)
+        with torch.cuda.stream(s):
+            for k, b in enumerate(seeds):
+                datas = fit(pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device))
+                for lv in datas:  # consumed on the main stream (the step's copy-in)
+                    for v in vars(lv).values():
+                        if torch.is_tensor(v) and v.is_cuda:
+                            v.record_stream(main)
+                ev = torch.cuda.Event()
+                ev.record(s)
+                q.put((datas, ev))
+        q.put(None)
+
+    def run(seeds):
+        q = queue.Queue(maxsize=2)
+        th = threading.Thread(target=produce, args=(q, seeds), daemon=True)
+        th.start()
+        n = 0
+        while True:
+            it = q.get()
+            if it is None:
+                break
+            datas, ev = it
+            main.wait_event(ev)
+            st(datas)
+            n += 1
+        th.join()
+        return n
+    for b in (0, 1):  # warm-up, serial: the eager step + capture of the bucket, a replay
+        st(fit(pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device)))
     torch.cuda.synchronize()
-    t_pipe = t_step = 0.0
+    n_cap = st.stats["captures"]
+    t0 = time.perf_counter()
+    nb = run(list(range(n_batches)))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert st.stats["captures"] == n_cap, "a timed batch left the capacity bucket"
+    # the pipeline alone (same producer, no training)
+    t1 = time.perf_counter()
     for b in range(n_batches):
-        t0 = time.perf_counter()
-        datas = pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        st(datas)
-        torch.cuda.synchronize()
-        t_pipe += t1 - t0
-        t_step += time.perf_counter() - t1
-    return {"value": round(n_batches * G / (t_pipe + t_step), 1), "unit": "graphs/s",
+        fit(pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device))
+    torch.cuda.synchronize()
+    t_pipe = time.perf_counter() - t1
+    return {"value": round(nb * G / dt, 1), "unit": "graphs/s",
+            "ms_per_batch": round(dt / nb * 1e3, 2),
             "pipeline_graphs_per_s": round(n_batches * G / t_pipe, 1),
             "pipeline_ms_per_batch": round(t_pipe / n_batches * 1e3, 1),
-            "step_ms_per_batch": round(t_step / n_batches * 1e3, 1),
-            "what": "raw superpixel samples -> SuperpixelPipeline (device Hodge builder, "
-                    "batched eigh PE, native MLGC, dropout_edge) -> eager training step, "
-                    "serial; batches of " + str(G)}
+            "captures": st.stats["captures"], "replays": st.stats["replay"],
+            "lanes": "lanes" in st.stats, "caps": caps,
+            "what": "raw superpixel samples -> SuperpixelPipeline (dropout_edge, device Hodge "
+                    "builder, batched eigh PE, native batched MLGC) on a producer thread + its "
+                    "own stream, padded to one capacity bucket -> replayed training step, "
+                    "overlapped; batches of " + str(G)}
 
 
 def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):

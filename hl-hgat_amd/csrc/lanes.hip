@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <mutex>
 #include <queue>
 #include <unordered_map>
@@ -515,6 +516,29 @@ extern "C" int hlhgat_lanes_build(void* graph, void* origin_stream, int n_lanes,
     return fail(HLHGAT_EHIP);
   }
   *out = reinterpret_cast<hlhgat_lanes_t>(Lx);
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_graph_kernel_count(void* graph, const char* name_part, int64_t* kernels,
+                                         int64_t* matching) {
+  HLH_CHECK_ARG(graph && name_part && kernels && matching, "graph_kernel_count: NULL argument");
+  hipGraph_t G = reinterpret_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  HLH_CHECK_HIP(hipGraphGetNodes(G, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) HLH_CHECK_HIP(hipGraphGetNodes(G, nodes.data(), &n));
+  *kernels = 0;
+  *matching = 0;
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    HLH_CHECK_HIP(hipGraphNodeGetType(nd, &t));
+    if (t != hipGraphNodeTypeKernel) continue;
+    ++*kernels;
+    hipKernelNodeParams kp{};
+    if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess || !kp.func) continue;
+    const char* nm = hipKernelNameRefByPtr(kp.func, nullptr);
+    if (nm && std::strstr(nm, name_part)) ++*matching;
+  }
   return HLHGAT_OK;
 }
 

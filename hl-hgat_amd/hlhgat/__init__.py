@@ -7,15 +7,6 @@ arithmetic runs in hand-written HIP kernels behind the C-ABI of
 include/hlhgat.h (libhlhgat.so).  There is no CPU fallback: importing this
 package loads the HIP library or raises.
 """
-import os as _os
-
-# Captured training steps are two chains of kernels (the HL blocks' node and
-# edge chains): run a hipGraph on two hardware queues, not the runtime's
-# default four, which adds cross-queue dependencies (same-box sweep: 2.74 ->
-# 2.68 ms per config-2 step, DESIGN.md §14).  Read when HIP initialises; a
-# value set by the user wins.
-_os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
-
 from . import ops  # noqa: F401,E402  (loads libhlhgat.so; raises if missing)
 from .hodge_cheb_conv import (HL_filter, HodgeChebConv, HodgeLaguerreConv,  # noqa: F401,E402
                               HodgeLaguerreFastConv, MSI, NodeEdgeInt, SAPool)

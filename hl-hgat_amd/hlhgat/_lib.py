@@ -143,6 +143,7 @@ SIGNATURES = {
     "hlhgat_lanes_info": (c_i32, [c_vp, P_i64, c_i32]),
     "hlhgat_lanes_counters": (c_i32, [c_vp, c_vp, c_i32]),
     "hlhgat_lanes_destroy": (c_i32, [c_vp]),
+    "hlhgat_graph_kernel_count": (c_i32, [c_vp, C.c_char_p, P_i64, P_i64]),
 }
 
 # constants from include/hlhgat.h

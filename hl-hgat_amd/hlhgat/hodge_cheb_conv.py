@@ -233,6 +233,22 @@ class NodeEdgeInt(nn.Module):
             # the unfused value path's BatchNorms would count the padding rows
             raise RuntimeError("hlhgat: static-shape (padded) batches need the fused "
                                "NodeEdgeInt value path (training-mode WV_* MLPs)")
+        ch = ops.active_chains(x_t.device) if x_t.is_cuda else None
+        if ch is not None and ch.on:
+            # the unfused path (eval mode, SyncBatchNorm, attention) runs on the
+            # current (node-chain) stream: x_s comes from the edge chain, and
+            # both outputs go back to it -- a full exchange with the edge chain
+            # (the fused path exchanges only the first-layer GEMM results)
+            ch.main.wait_stream(ch.side)
+            x_s.record_stream(ch.main)
+            r = self._unfused(x_t, x_s, par, D)
+            ch.sync_side()
+            for t in r:
+                t.record_stream(ch.side)
+            return r
+        return self._unfused(x_t, x_s, par, D)
+
+    def _unfused(self, x_t: Tensor, x_s: Tensor, par, D: Tensor):
         x_s2t, x_t2s = self.interact(x_t, x_s, par, D)
         if self.only_att:
             code = _sigma_code(self.sigma)

@@ -534,6 +534,7 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     unpadded batch (tests/test_train_step.py)."""
     nt, ns = b.x_t.size(0), b.x_s.size(0)
     Rt, Rs = caps["rows_t"], caps["rows_s"]
+    dev = b.x_t.device  # a device batch (e.g. SuperpixelPipeline's) is padded on the device
     if Rt <= nt or Rs <= ns:
         raise ValueError(f"pad_batch: caps ({Rt}, {Rs}) must exceed the rows ({nt}, {ns})")
     out = Batch()
@@ -556,7 +557,7 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
         if extra < 0:
             raise ValueError(f"pad_batch: {ei.size(1)} Laplacian entries exceed the cap {Z}")
         per_row = _spread(extra, R - n)
-        rows = torch.from_numpy(np.repeat(np.arange(n, R), per_row)).to(ei.dtype)
+        rows = torch.from_numpy(np.repeat(np.arange(n, R), per_row)).to(ei.device, ei.dtype)
         return (torch.cat([ei, torch.stack([rows, rows])], 1),
                 torch.cat([w, w.new_zeros(extra)]), per_row)
 
@@ -575,7 +576,8 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     if getattr(b, "csr_rowptr_t", None) is not None or getattr(b, "csr_rowptr_s", None) is not None:
         _attach_csr(out)  # the padded COO (zero-weight self-loops on padding rows)
     if getattr(b, "edge_index", None) is not None:
-        nodes = torch.from_numpy(nt + np.arange(Rs - ns) % (Rt - nt)).to(b.edge_index.dtype)
+        nodes = torch.from_numpy(nt + np.arange(Rs - ns) % (Rt - nt)).to(b.edge_index.device,
+                                                                          b.edge_index.dtype)
         out.edge_index = torch.cat([b.edge_index, torch.stack([nodes, nodes])], 1)
         if getattr(b, "inc_rowptr", None) is not None:
             out.inc_rowptr, out.inc_eids = incidence_csr(out.edge_index, Rt)
@@ -584,10 +586,13 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     for side, n, R in (("t", nt, Rt), ("s", ns, Rs)):
         o = getattr(b, "row_order_" + side, None)
         if o is not None:
-            setattr(out, "row_order_" + side, torch.cat([o, torch.arange(n, R, dtype=o.dtype)]))
-        setattr(out, "n_valid_" + side, torch.tensor([n], dtype=torch.int32))
-    out.valid_mask_t = torch.arange(Rt) < nt
+            setattr(out, "row_order_" + side,
+                    torch.cat([o, torch.arange(n, R, dtype=o.dtype, device=o.device)]))
+        setattr(out, "n_valid_" + side, torch.tensor([n], dtype=torch.int32, device=dev))
+    out.valid_mask_t = torch.arange(Rt, device=dev) < nt
     out.num_nodes = Rt
+    if dev.type == "cuda":
+        out._mark()  # the device-side declarations Batch.to makes (sorted, valid rows, factor)
     return out
 
 

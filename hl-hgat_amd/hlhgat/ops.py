@@ -1572,6 +1572,15 @@ def capture_recorded() -> int:
     return int(n.value)
 
 
+def graph_kernel_count(graph_handle: int, name_part: str) -> Tuple[int, int]:
+    """(kernel nodes, kernel nodes whose name contains name_part) of a
+    captured hipGraph (e.g. torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph())."""
+    k, m = C.c_int64(), C.c_int64()
+    check(LIB.hlhgat_graph_kernel_count(C.c_void_p(int(graph_handle)), name_part.encode(),
+                                        C.byref(k), C.byref(m)), "graph_kernel_count")
+    return int(k.value), int(m.value)
+
+
 class Lanes:
     """A captured step split into one linear hipGraph per stream lane (the
     node chain and the edge chain), synchronised by device counters;

@@ -743,6 +743,10 @@ int hlhgat_lanes_info(hlhgat_lanes_t lanes, int64_t* info, int n_info);
  * of these is k), then per wait the number of times it timed out. */
 int hlhgat_lanes_counters(hlhgat_lanes_t lanes, unsigned* out, int n);
 int hlhgat_lanes_destroy(hlhgat_lanes_t lanes);
+/* Introspection of a captured graph: its kernel nodes, and those whose
+ * kernel name contains name_part (e.g. "ncclDevKernel": RCCL's kernels). */
+int hlhgat_graph_kernel_count(void* graph, const char* name_part, int64_t* kernels,
+                              int64_t* matching);
 
 #ifdef __cplusplus
 }
