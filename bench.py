@@ -35,10 +35,9 @@ import subprocess
 import sys
 import time
 
-# A launcher setting, not a product one: the step replays as stream lanes
-# (linear graphs), which this does not touch; it only shapes
-# the whole-graph replay that TrainStep falls back to (two hardware queues
-# instead of the runtime's four: 2.74 -> 2.68 ms per step).
+# A launcher setting, not a product one (the package sets nothing in the
+# process environment): the replayed step's hipGraph on two hardware queues
+# instead of the runtime's four (2.74 -> 2.68 ms per step).
 # Read at HIP init; a value set by the user wins.
 os.environ.setdefault("DEBUG_HIP_FORCE_GRAPH_QUEUES", "2")
 
@@ -238,14 +237,10 @@ def replay_census(caps, eager, steps=12, warmup=4, timeout=300):
         return None, f"only {len(marks)} steps in the trace"
     sel = list(zip(marks[-steps:-1], marks[-steps + 1:]))  # the last steps-1 full replays
     per = {k: [0.0, 0] for k in REPLAY_CLASSES}
-    spans, busys, disp, sync = [], [], [], []
+    spans, busys, disp = [], [], []
     for a, b in sel:
         st = rows[a + 1:b + 1]
-        # lane replay's signal / wait kernels (lanes.hip) are counted apart; a
-        # wait spinning on the other lane is not work, so not "busy"
-        sync.append(sum(1 for x in st if "k_lane_" in x["Kernel_Name"]))
-        iv = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in st
-                    if "k_lane_wait" not in x["Kernel_Name"])
+        iv = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in st)
         span = iv[-1][1] - iv[0][0] if iv else 0
         busy, cur_s, cur_e = 0, None, None
         for s0, e0 in iv:
@@ -269,8 +264,6 @@ def replay_census(caps, eager, steps=12, warmup=4, timeout=300):
     span_us = sum(spans) / n / 1e3
     busy_us = sum(busys) / n / 1e3
     out = {"steps_traced": n, "dispatches_per_step": round(sum(disp) / n, 1),
-           "lane_sync_dispatches_per_step": round(sum(sync) / n, 1),
-           "model_dispatches_per_step": round((sum(disp) - sum(sync)) / n, 1),
            "span_us": round(span_us, 1), "busy_us": round(busy_us, 1),
            "idle_us": round(span_us - busy_us, 1),
            "idle_frac": round((span_us - busy_us) / span_us, 4) if span_us else None,
@@ -599,7 +592,7 @@ def cifar_pipeline_leg(device, c, G, n_batches=8):
     batched MLGC, both levels on the device) on a producer thread and its own
     stream, pads both levels to one capacity bucket (pad_levels on the
     device), and hands it over; the training step replays ONE captured graph
-    for every batch (TrainStep, lane replay) while the next batch is built.
+    for every batch (TrainStep) while the next batch is built.
     Reported: the overlapped rate, and the pipeline alone / the serial sum."""
     import queue
     import threading
@@ -675,7 +668,7 @@ def cifar_pipeline_leg(device, c, G, n_batches=8):
             "pipeline_graphs_per_s": round(n_batches * G / t_pipe, 1),
             "pipeline_ms_per_batch": round(t_pipe / n_batches * 1e3, 1),
             "captures": st.stats["captures"], "replays": st.stats["replay"],
-            "lanes": "lanes" in st.stats, "caps": caps,
+            "caps": caps,
             "what": "raw superpixel samples -> SuperpixelPipeline (dropout_edge, device Hodge "
                     "builder, batched eigh PE, native batched MLGC) on a producer thread + its "
                     "own stream, padded to one capacity bucket -> replayed training step, "
@@ -852,7 +845,7 @@ def head_workload(args, rank, world, device):
     for i in range(args.warmup):
         step(padded[i % len(padded)])
     torch.cuda.synchronize()
-    log(f"[rank {rank}] warmup done {step.stats} lanes_off={step.lanes_off}")
+    log(f"[rank {rank}] warmup done {step.stats} graphs_off={step.graphs_off}")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -877,7 +870,7 @@ def head_workload(args, rank, world, device):
                        "global_batch": world * G, "parallelism": f"dp{world}",
                        "execution": "eager" if args.eager else
                        f"captured hipGraph per rank ({step.stats.get('captures')} capture(s)), "
-                       f"{'lane replay' if 'lanes' in step.stats else 'graph replay'}, "
+                       f"replayed, "
                        f"gradient all-reduce over {'RCCL' if world > 1 else 'none'}",
                        "caps": caps},
             "stats": {k: v for k, v in step.stats.items()}}), flush=True)

@@ -183,7 +183,6 @@ extern "C" int hlhgat_att_score_fwd(int64_t n, int64_t dk, const float* Qc,
   const unsigned grid = (unsigned)ceil_div(n, 256 / l);
   hipStream_t s = as_stream(stream);
   HLH_ATT_DISPATCH(k_att_fwd, v, l, grid, s, a);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -228,7 +227,6 @@ extern "C" int hlhgat_att_score_bwd(int64_t n, int64_t dk, const float* Qc,
   const unsigned grid = (unsigned)ceil_div(n, 256 / l);
   hipStream_t s = as_stream(stream);
   HLH_ATT_DISPATCH(k_att_bwd, v, l, grid, s, a);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

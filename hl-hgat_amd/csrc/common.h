@@ -7,7 +7,6 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
-#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdarg>
@@ -82,14 +81,6 @@ struct Blk {  // a workgroup's coordinates in its (x, y) grid
 };
 __device__ __forceinline__ Blk blk_hw() { return Blk{blockIdx.x, blockIdx.y, gridDim.x, gridDim.y}; }
 
-// Capture recorder (lanes.hip, hlhgat_capture_record): while on, a launch on
-// a capturing stream notes (its graph node, the stream).
-extern std::atomic<int> g_capture_record;
-void capture_note_slow(hipStream_t s);
-inline void capture_note(hipStream_t s) {
-  if (g_capture_record.load(std::memory_order_relaxed)) capture_note_slow(s);
-}
-
 // Launch `k` on `s`; when `p` holds a live ProfScope the launch goes through
 // hipExtLaunchKernelGGL with its start/stop events.
 template <typename... KArgs, typename... Args>
@@ -99,7 +90,6 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t shmem, h
     hipExtLaunchKernelGGL(k, grid, block, shmem, s, p->start_ev, p->stop_ev, 0, args...);
   else
     hipLaunchKernelGGL(k, grid, block, shmem, s, args...);
-  capture_note(s);
 }
 
 }  // namespace hlhgat

@@ -185,7 +185,6 @@ extern "C" int hlhgat_coo_check_sorted(const int64_t* row, const int64_t* col,
   HLH_CHECK_ARG(row && col, "coo_check_sorted: NULL index");
   k_check_sorted<<<grid_for(nnz), kThreads, 0, s>>>(row, col, nnz, n_rows,
                                                     n_cols, flag_dev);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -205,12 +204,10 @@ extern "C" int hlhgat_csr_from_sorted_coo(const int64_t* row, const int64_t* col
   hipStream_t s = as_stream(stream);
   k_rowptr_sorted_rows<<<grid_for(n_rows + 1), kThreads, 0, s>>>(row, nnz, n_rows,
                                                                  rowptr);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   if (nnz > 0) {
     k_convert_sorted<<<grid_for(nnz), kThreads, 0, s>>>(col, w, nnz, col_out,
                                                         val_out);
-    capture_note(s);
     HLH_CHECK_LAUNCH();
   }
   return HLHGAT_OK;
@@ -241,7 +238,6 @@ extern "C" int hlhgat_csr_from_coo(const int64_t* row, const int64_t* col,
   const uint64_t nc = (uint64_t)n_cols;
   k_make_keys<<<grid_for(nnz), kThreads, 0, s>>>(row, col, nnz, nc, ws.keys_in,
                                                  ws.idx_in);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   int end_bit = bits_for((uint64_t)n_rows * nc);
   size_t temp = ws.temp_bytes;
@@ -250,11 +246,9 @@ extern "C" int hlhgat_csr_from_coo(const int64_t* row, const int64_t* col,
       0, end_bit, s));
   k_finish_sorted_keys<<<grid_for(nnz), kThreads, 0, s>>>(
       ws.keys_out, ws.idx_out, w, nnz, nc, col_out, val_out, perm);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   k_rowptr_from_keys<<<grid_for(n_rows + 1), kThreads, 0, s>>>(ws.keys_out, nnz,
                                                                n_rows, nc, rowptr);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -282,7 +276,6 @@ extern "C" int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
   const uint64_t ne = (uint64_t)n_edges;
   k_make_incidence_keys<<<grid_for(nnz), kThreads, 0, s>>>(edge_index, n_edges,
                                                            ws.keys_in);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   int end_bit = bits_for((uint64_t)n_nodes * ne);
   size_t temp = ws.temp_bytes;
@@ -291,11 +284,9 @@ extern "C" int hlhgat_incidence_csr(const int64_t* edge_index, int64_t n_edges,
                                                   end_bit, s));
   k_finish_sorted_keys<<<grid_for(nnz), kThreads, 0, s>>>(
       ws.keys_out, nullptr, nullptr, nnz, ne, edge_ids, nullptr, nullptr);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   k_rowptr_from_keys<<<grid_for(n_nodes + 1), kThreads, 0, s>>>(
       ws.keys_out, nnz, n_nodes, ne, rowptr);
-  capture_note(s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -418,7 +409,6 @@ extern "C" int hlhgat_gather_f32(const float* src, const int32_t* idx, int64_t n
   if (n == 0) return HLHGAT_OK;
   HLH_CHECK_ARG(src && idx && dst, "gather_f32: NULL pointer");
   k_gather_f32<<<grid_for(n), kThreads, 0, as_stream(stream)>>>(src, idx, n, dst);
-  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -273,7 +273,6 @@ extern "C" int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_e
   a.lmax = lmax;
   hipLaunchKernelGGL(k_lanczos_lmax, dim3((unsigned)n_graphs), dim3(kLzThreads), 0,
                      as_stream(stream), a);
-  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -289,7 +288,6 @@ extern "C" int hlhgat_hodge_row_sizes(const int32_t* inc_rowptr, const int64_t* 
   hipLaunchKernelGGL(k_hodge_row_sizes, dim3((unsigned)ceil_div(n, (int64_t)256)), dim3(256), 0,
                      as_stream(stream), inc_rowptr, edge_index, n_edges, n_nodes, sizes_l0,
                      sizes_l1);
-  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -309,7 +307,6 @@ extern "C" int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_
   if (n_nodes > 0) {
     hipLaunchKernelGGL(k_hodge_l0_rows, dim3((unsigned)ceil_div(n_nodes, (int64_t)256)),
                        dim3(256), 0, s, a);
-    capture_note(s);
     HLH_CHECK_LAUNCH();
   }
   if (n_edges > 0) {
@@ -318,7 +315,6 @@ extern "C" int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_
     a.val = val_l1;
     hipLaunchKernelGGL(k_hodge_l1_rows, dim3((unsigned)ceil_div(n_edges, (int64_t)256)),
                        dim3(256), 0, s, a);
-    capture_note(s);
     HLH_CHECK_LAUNCH();
   }
   return HLHGAT_OK;

@@ -1,6 +1,7 @@
 // Library-level state: error messages, version, live kernel timing.
 #include "common.h"
 
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -171,7 +172,6 @@ extern "C" int hlhgat_zero_fill(void* p, size_t bytes, void* stream) {
   int64_t g = ceil_div(n, 256);
   if (g > 1024) g = 1024;
   k_zero_words<<<(unsigned)g, 256, 0, as_stream(stream)>>>(static_cast<uint32_t*>(p), n);
-  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -234,7 +234,6 @@ extern "C" int hlhgat_copy2d_batched(int n, const float* const* src, const int64
   int64_t g = ceil_div(total, 256);
   if (g > 2048) g = 2048;
   k_copy2d_batched<<<(unsigned)g, 256, 0, as_stream(stream)>>>(a);
-  capture_note(as_stream(stream));
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -368,5 +367,31 @@ extern "C" int hlhgat_l1_loss_bwd(const float* x, const float* y, int64_t n, con
   launch(k_l1_loss_bwd, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, x, y, n,
          gout, dx);
   HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+// Introspection of a captured graph (tests/test_rccl_capture.py: the RCCL
+// kernels inside a captured training step): kernel nodes, and those whose
+// kernel name contains name_part.
+extern "C" int hlhgat_graph_kernel_count(void* graph, const char* name_part, int64_t* kernels,
+                                         int64_t* matching) {
+  HLH_CHECK_ARG(graph && name_part && kernels && matching, "graph_kernel_count: NULL argument");
+  hipGraph_t G = reinterpret_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  HLH_CHECK_HIP(hipGraphGetNodes(G, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) HLH_CHECK_HIP(hipGraphGetNodes(G, nodes.data(), &n));
+  *kernels = 0;
+  *matching = 0;
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    HLH_CHECK_HIP(hipGraphNodeGetType(nd, &t));
+    if (t != hipGraphNodeTypeKernel) continue;
+    ++*kernels;
+    hipKernelNodeParams kp{};
+    if (hipGraphKernelNodeGetParams(nd, &kp) != hipSuccess || !kp.func) continue;
+    const char* nm = hipKernelNameRefByPtr(kp.func, nullptr);
+    if (nm && std::strstr(nm, name_part)) ++*matching;
+  }
   return HLHGAT_OK;
 }

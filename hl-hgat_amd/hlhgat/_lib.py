@@ -136,13 +136,6 @@ SIGNATURES = {
     "hlhgat_prof_enable": (c_i32, [c_i32, c_i32]),
     "hlhgat_prof_reset": (c_i32, []),
     "hlhgat_prof_read": (c_i32, [c_i32, P_i64, P_f64, P_f64, P_f64]),
-    "hlhgat_capture_record": (c_i32, [c_i32]),
-    "hlhgat_capture_recorded": (c_i32, [P_i64]),
-    "hlhgat_lanes_build": (c_i32, [c_vp, c_vp, c_i32, P_vp]),
-    "hlhgat_lanes_launch": (c_i32, [c_vp, c_vp]),
-    "hlhgat_lanes_info": (c_i32, [c_vp, P_i64, c_i32]),
-    "hlhgat_lanes_counters": (c_i32, [c_vp, c_vp, c_i32]),
-    "hlhgat_lanes_destroy": (c_i32, [c_vp]),
     "hlhgat_graph_kernel_count": (c_i32, [c_vp, C.c_char_p, P_i64, P_i64]),
 }
 
@@ -150,7 +143,6 @@ SIGNATURES = {
 POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
 DEVERR_BN_WAIT = 1
-DEVERR_LANE_WAIT = 2
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
 PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD, PROF_PROJ_BN = 4, 5, 6, 7
 MAX_BLOCKS = 16

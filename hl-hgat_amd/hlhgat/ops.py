@@ -1528,8 +1528,6 @@ def l1_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
 _DEVERR_TEXT = {
     _lib.DEVERR_BN_WAIT: "one-launch BatchNorm: a workgroup timed out waiting for its tile's "
                          "statistics (its rows were written as NaN)",
-    _lib.DEVERR_LANE_WAIT: "lane replay: a cross-lane wait timed out (the step's results are "
-                           "unordered)",
 }
 
 
@@ -1558,20 +1556,8 @@ def check_device_errors(sync: bool = True) -> None:
 
 
 # ----------------------------------------------------------------------------
-# lane replay of a captured step (include/hlhgat.h: hlhgat_lanes_*, lanes.hip)
+# captured-graph introspection (include/hlhgat.h: hlhgat_graph_kernel_count)
 # ----------------------------------------------------------------------------
-def capture_record(on: bool) -> None:
-    """Note (graph node, stream) for every kernel launched on a capturing
-    stream while on (on=True also forgets earlier notes)."""
-    check(LIB.hlhgat_capture_record(int(bool(on))), "capture_record")
-
-
-def capture_recorded() -> int:
-    n = C.c_int64()
-    check(LIB.hlhgat_capture_recorded(C.byref(n)), "capture_recorded")
-    return int(n.value)
-
-
 def graph_kernel_count(graph_handle: int, name_part: str) -> Tuple[int, int]:
     """(kernel nodes, kernel nodes whose name contains name_part) of a
     captured hipGraph (e.g. torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph())."""
@@ -1579,49 +1565,6 @@ def graph_kernel_count(graph_handle: int, name_part: str) -> Tuple[int, int]:
     check(LIB.hlhgat_graph_kernel_count(C.c_void_p(int(graph_handle)), name_part.encode(),
                                         C.byref(k), C.byref(m)), "graph_kernel_count")
     return int(k.value), int(m.value)
-
-
-class Lanes:
-    """A captured step split into one linear hipGraph per stream lane (the
-    node chain and the edge chain), synchronised by device counters;
-    replayed on two dedicated streams."""
-
-    def __init__(self, graph_handle: int, origin_stream: int):
-        h = C.c_void_p()
-        check(LIB.hlhgat_lanes_build(C.c_void_p(int(graph_handle)), C.c_void_p(int(origin_stream)),
-                                     2, C.byref(h)), "lanes_build")
-        self._h = h
-
-    def launch(self, stream: int) -> None:
-        check(LIB.hlhgat_lanes_launch(self._h, C.c_void_p(int(stream))), "lanes_launch")
-
-    def info(self) -> dict:
-        v = (C.c_int64 * 6)()
-        check(LIB.hlhgat_lanes_info(self._h, v, 6), "lanes_info")
-        return {"lanes": v[0], "nodes": [v[1], v[2]], "signals": v[3], "waits": v[4],
-                "empty_dropped": v[5]}
-
-    def counters(self) -> Tuple[List[int], List[int]]:
-        """(signal counters + the waits' own counters, timeouts per wait);
-        synchronises the lanes.  After k replays every counter is k and every
-        timeout count 0."""
-        i = self.info()
-        n = i["signals"] + 2 * i["waits"]
-        v = (C.c_uint32 * max(n, 1))()
-        check(LIB.hlhgat_lanes_counters(self._h, v, n), "lanes_counters")
-        k = i["signals"] + i["waits"]
-        return list(v[:k]), list(v[k:n])
-
-    def close(self) -> None:
-        if getattr(self, "_h", None) is not None and self._h.value:
-            LIB.hlhgat_lanes_destroy(self._h)
-            self._h = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 # ----------------------------------------------------------------------------

@@ -29,7 +29,7 @@ from typing import Callable, Dict, Optional, Tuple
 import torch
 import torch.distributed as dist
 
-from . import _lib, ops
+from . import ops
 from .distributed import collectives_on
 
 __all__ = ["TrainStep", "InferStep", "batch_key", "forward_collectives"]
@@ -39,9 +39,10 @@ HIP_ADAM = True
 # DEFER_REDUCE = False (tests): every Linear backward launches its own split
 # reduction instead of handing it to the next one on its stream (same bits)
 DEFER_REDUCE = True
-# LANES = False: replay the captured graph as one hipGraph (torch's replay)
-# instead of one linear graph per stream lane (ops.Lanes)
-LANES = True
+# KEEP_GRAPHS = True (tests, introspection): captures keep their hipGraph_t
+# (torch.cuda.CUDAGraph(keep_graph=True), then instantiate), so
+# ops.graph_kernel_count can inspect a captured step
+KEEP_GRAPHS = False
 
 
 def forward_collectives(model: torch.nn.Module) -> bool:
@@ -93,17 +94,10 @@ BN_RESERVE_CHANNELS = 2048  # BatchNorm workspace reserved per capture stream
 
 
 class _Captured:
-    def __init__(self, graph, static_batch, loss, lanes=None):
+    def __init__(self, graph, static_batch, loss):
         self.graph = graph
         self.batch = static_batch
         self.loss = loss
-        self.lanes = lanes  # ops.Lanes, or None: torch's replay of `graph`
-
-    def replay(self, device) -> None:
-        if self.lanes is not None:
-            self.lanes.launch(torch.cuda.current_stream(device).cuda_stream)
-        else:
-            self.graph.replay()
 
     def load(self, batch):
         """Copy a batch into the graph's static buffers: every contiguous
@@ -199,7 +193,15 @@ class TrainStep:
         self._exchange_in_graph = (self.graphs and self._exchange
                                    and dist.get_backend() == "nccl")
         self.graphs_off = None
-        if self.graphs and self._exchange and dist.get_backend() != "nccl" \
+        sync_bn = any(ops.sync_bn_group(m) is not None for m in model.modules()
+                      if isinstance(m, torch.nn.modules.batchnorm._BatchNorm))
+        if self.graphs and self._exchange and dist.get_backend() == "nccl" and sync_bn:
+            # measured on MI355X (tests/test_rccl_capture.py): capturing the
+            # SyncBatchNorm all-gathers (RCCL) ends in a segfault inside
+            # hipStreamEndCapture; the all-reduce of the attpool heads captures
+            self.graphs = False
+            self.graphs_off = "SyncBatchNorm all-gathers under RCCL do not capture"
+        elif self.graphs and self._exchange and dist.get_backend() != "nccl" \
                 and forward_collectives(model):
             # a collective inside the forward (SyncBatchNorm statistics, the
             # attpool heads' batch-global max) runs on the host under gloo and
@@ -211,12 +213,6 @@ class TrainStep:
         self._pool = None
         self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
-        # lane replay (ops.Lanes): not for a step with random numbers (torch's
-        # replay advances the generator offsets; a lane replay would not) or
-        # with collectives inside the captured graph
-        self.lanes_off = None
-        if any(isinstance(m, torch.nn.Dropout) and m.p > 0 for m in model.modules()):
-            self.lanes_off = "dropout with p > 0 (random numbers in the graph)"
         self._fwd_bwd_calls = 0
         self._ones = {}
 
@@ -307,8 +303,7 @@ class TrainStep:
                   else _clone_batch(batch))
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        use_lanes = LANES and self._ext is not None and self.lanes_off is None
-        g = torch.cuda.CUDAGraph(keep_graph=use_lanes)
+        g = torch.cuda.CUDAGraph(keep_graph=KEEP_GRAPHS)
         s = self._stream
         if self._ext is not None and BN_RESERVE_CHANNELS:
             # BatchNorm workspaces of every stream the capture uses, made (and
@@ -320,42 +315,29 @@ class TrainStep:
                 self._ext.bn_workspace_reserve(int(h), idx, BN_RESERVE_CHANNELS)
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        if use_lanes:
-            ops.capture_record(True)
-        try:
-            with torch.cuda.graph(g, pool=self._pool, stream=s):
-                loss = self._fwd_bwd(static)
-                if self._exchange_in_graph:
-                    self._exchange_and_update()  # RCCL all-reduce + scale + Adam, captured
-                elif not self._exchange:
-                    self._opt_step()
-                # every stream forked from the capture (the node / edge side streams,
-                # forks inside autograd backward nodes, which run on autograd's
-                # device thread) rejoins it before hipStreamEndCapture: an unjoined
-                # fork is what crashed capture_end in round 1
-                if self._ext is not None:
-                    ops.join_capture_streams(self.device)
-        finally:
-            if use_lanes:
-                ops.capture_record(False)
+        with torch.cuda.graph(g, pool=self._pool, stream=s):
+            loss = self._fwd_bwd(static)
+            if self._exchange_in_graph:
+                self._exchange_and_update()  # RCCL all-reduce + scale + Adam, captured
+            elif not self._exchange:
+                self._opt_step()
+            # every stream forked from the capture (the node / edge side streams,
+            # forks inside autograd backward nodes, which run on autograd's
+            # device thread) rejoins it before hipStreamEndCapture: an unjoined
+            # fork is what crashed capture_end in round 1
+            if self._ext is not None:
+                ops.join_capture_streams(self.device)
         left = ops.side_streams_capturing(self.device) if self._ext is not None else []
         if left:
             raise RuntimeError(f"TrainStep: {len(left)} side stream(s) still capturing after the "
                                f"graph capture ended (unjoined fork); refusing the graph")
         ops.clear_caches()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        lanes = None
-        if use_lanes:
-            try:
-                lanes = ops.Lanes(g.raw_cuda_graph(), s.cuda_stream)
-                self.stats["lanes"] = lanes.info()
-            except _lib.HlhgatError as e:  # e.g. a node type the split does not handle
-                self.lanes_off = f"lane split refused the graph: {e}"
-            if lanes is None:
-                g.instantiate()
+        if KEEP_GRAPHS:
+            g.instantiate()
         if len(self._graphs) >= self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
-        ent = _Captured(g, static, loss, lanes)
+        ent = _Captured(g, static, loss)
         self._graphs[key] = ent
         self.stats["captures"] += 1
         return ent
@@ -374,7 +356,7 @@ class TrainStep:
             self._capture(batch, key)
             return loss
         ent.load(batch)
-        ent.replay(self.device)
+        ent.graph.replay()
         if self._exchange and not self._exchange_in_graph:
             self._exchange_and_update()
         self.stats["replay"] += 1
@@ -390,7 +372,7 @@ class InferStep:
     model.eval() and ``out = model(data)`` under torch.no_grad(), one batch
     per call.  graphs=True captures the eval forward into a hipGraph per batch
     shape (the first call of a shape runs eagerly, then captures) and replays
-    it as stream lanes (ops.Lanes); the returned output is the graph's static
+    it; the returned output is the graph's static
     buffer, valid until the next call with a batch of the same shape (clone
     it to keep it)."""
 
@@ -405,10 +387,6 @@ class InferStep:
         self._pool = None
         self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
-        self.lanes_off = None
-        if any(isinstance(m, torch.nn.Dropout) and m.p > 0 and m.training
-               for m in model.modules()):
-            self.lanes_off = "dropout in training mode"
 
     def _forward(self, batch):
         was = self.model.training
@@ -424,38 +402,24 @@ class InferStep:
                   else _clone_batch(batch))
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
-        use_lanes = LANES and ops._ext is not None and self.lanes_off is None
-        g = torch.cuda.CUDAGraph(keep_graph=use_lanes)
+        g = torch.cuda.CUDAGraph(keep_graph=KEEP_GRAPHS)
         s = self._stream
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        if use_lanes:
-            ops.capture_record(True)
-        try:
-            with torch.cuda.graph(g, pool=self._pool, stream=s):
-                out = self._forward(static)
-                ops.join_capture_streams(self.device)
-        finally:
-            if use_lanes:
-                ops.capture_record(False)
+        with torch.cuda.graph(g, pool=self._pool, stream=s):
+            out = self._forward(static)
+            ops.join_capture_streams(self.device)
         left = ops.side_streams_capturing(self.device)
         if left:
             raise RuntimeError(f"InferStep: {len(left)} side stream(s) still capturing after the "
                                f"graph capture ended (unjoined fork); refusing the graph")
         ops.clear_caches()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        lanes = None
-        if use_lanes:
-            try:
-                lanes = ops.Lanes(g.raw_cuda_graph(), s.cuda_stream)
-                self.stats["lanes"] = lanes.info()
-            except _lib.HlhgatError as e:
-                self.lanes_off = f"lane split refused the graph: {e}"
-            if lanes is None:
-                g.instantiate()
+        if KEEP_GRAPHS:
+            g.instantiate()
         if len(self._graphs) >= self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
-        ent = _Captured(g, static, out, lanes)
+        ent = _Captured(g, static, out)
         self._graphs[key] = ent
         self.stats["captures"] += 1
         return ent
@@ -474,6 +438,6 @@ class InferStep:
             self._capture(batch, key)
             return out
         ent.load(batch)
-        ent.replay(self.device)
+        ent.graph.replay()
         self.stats["replay"] += 1
         return ent.loss  # the captured forward's output

@@ -692,7 +692,6 @@ int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
  * (callers synchronise first for an exact answer).  hlhgat.ops.
  * check_device_errors / hlhgat.train.TrainStep raise RuntimeError on it. */
 #define HLHGAT_DEVERR_BN_WAIT 1u /* one-launch BatchNorm wait timed out (NaN rows) */
-#define HLHGAT_DEVERR_LANE_WAIT 2u /* lane replay: a cross-lane wait timed out */
 int hlhgat_device_errors(unsigned* out);
 int hlhgat_clear_device_errors(void);
 
@@ -714,35 +713,7 @@ int hlhgat_prof_reset(void);
 int hlhgat_prof_read(int kernel_class, int64_t* launches, double* total_ms,
                      double* total_bytes, double* total_flops);
 
-/* ---- lane replay of a captured step (runtime) ------------ */
-/* Not a reference interface: the reference trains eagerly (main_zinc...:
- * forward, loss, backward, optimizer.step per batch).  These replace the
- * replay of a whole-step hipGraph (hlhgat.train.TrainStep).
- *
- * hlhgat_capture_record(1): from now on every kernel this library launches on
- * a capturing stream notes (graph node, stream); (1) also forgets earlier
- * notes, (0) stops noting.  hlhgat_capture_recorded: number of notes. */
-int hlhgat_capture_record(int on);
-int hlhgat_capture_recorded(int64_t* n);
-/* Split a captured graph (hipGraph_t) into one LINEAR graph per lane: the
- * nodes noted on `origin_stream` form lane 0, nodes noted on any other stream
- * lane 1, others take their latest predecessor's lane; every cross-lane edge
- * becomes a signal kernel in the producing lane and a wait kernel in the
- * consuming one.  n_lanes must be 2.  The captured graph must stay alive
- * (its memory) but is not modified. */
-typedef struct hlhgat_lanes_s* hlhgat_lanes_t;
-int hlhgat_lanes_build(void* graph, void* origin_stream, int n_lanes, hlhgat_lanes_t* out);
-/* Replay: both lanes start after the work already on `stream`, and `stream`
- * waits for both. */
-int hlhgat_lanes_launch(hlhgat_lanes_t lanes, void* stream);
-/* info[0..5] = lanes, nodes in lane 0, nodes in lane 1, signals, waits,
- * dropped empty nodes. */
-int hlhgat_lanes_info(hlhgat_lanes_t lanes, int64_t* info, int n_info);
-/* Synchronises the lanes and copies their counters: n = signals + 2 * waits
- * words: the signal counters, the waits' own counters (after k replays each
- * of these is k), then per wait the number of times it timed out. */
-int hlhgat_lanes_counters(hlhgat_lanes_t lanes, unsigned* out, int n);
-int hlhgat_lanes_destroy(hlhgat_lanes_t lanes);
+/* ---- captured-graph introspection (runtime) ----------------------------- */
 /* Introspection of a captured graph: its kernel nodes, and those whose
  * kernel name contains name_part (e.g. "ncclDevKernel": RCCL's kernels). */
 int hlhgat_graph_kernel_count(void* graph, const char* name_part, int64_t* kernels,

@@ -183,9 +183,8 @@ def test_eval_chains_bitwise_one_stream(cuda):
 @pytest.mark.parametrize("name", ["eval_cfg2_zinc", "eval_cfg4_pepfunc"])
 def test_infer_step_replay_matches_eager_and_reference(cuda, name):
     """hlhgat.train.InferStep (the reference's test() loop body, captured per
-    batch shape and replayed as stream lanes): replayed outputs equal the
-    eager eval forward bit for bit, and the reference's eval output within
-    1e-5."""
+    batch shape and replayed): replayed outputs equal the eager eval forward
+    bit for bit, and the reference's eval output within 1e-5."""
     import hlhgat
     from hlhgat.train import InferStep
     g, _, ev = _inputs(name, lambda gg, p: _product_data(gg, p, cuda))
@@ -198,7 +197,6 @@ def test_infer_step_replay_matches_eager_and_reference(cuda, name):
     outs = [_call_out(inf(ev)).clone() for _ in range(4)]
     torch.cuda.synchronize()
     assert inf.stats["captures"] == 1 and inf.stats["replay"] == 3, inf.stats
-    assert "lanes" in inf.stats, (inf.stats, inf.lanes_off)
     assert m.training  # InferStep restores the mode it found
     for o in outs[1:]:
         assert torch.equal(o, outs[0])

@@ -40,10 +40,16 @@ def test_rccl_collectives_captured_replay_equals_eager(cuda, case):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert res["losses_equal"] and not res["param_diffs"], res
+    if case == "zinc_sync_bn":
+        # capturing the SyncBatchNorm all-gathers segfaults in hipStreamEndCapture
+        # (measured): TrainStep runs such a model eagerly under RCCL, and says so
+        assert res["graphs_off"] and res["captures"] == 0, res
+        return
     assert res["captures"] == 2 and res["replay"] >= 3, res
     assert res["exchange_in_graph"] is True
-    assert res["collective_kernels_in_step"] > 0, res  # RCCL kernels inside the graphs
-    assert res["losses_equal"] and not res["param_diffs"], res
+    # RCCL's kernels inside the graphs (names resolved: ours are found by name)
+    assert res["own_kernels_in_graphs"] > 0 and res["foreign_kernels_in_graphs"] > 0, res
 
 
 def _child(case):
@@ -56,9 +62,8 @@ def _child(case):
     from hlhgat import distributed as hd
     from hlhgat.train import TrainStep
     hd.COLLECTIVES_AT_WORLD_1 = True
-    if os.environ.get("HLHGAT_LANES") == "0":
-        from hlhgat import train
-        train.LANES = False
+    from hlhgat import train
+    train.KEEP_GRAPHS = True  # the captured hipGraph_t stays inspectable
 
     def note(*a):
         print("[child]", *a, file=sys.stderr, flush=True)
@@ -102,19 +107,18 @@ def _child(case):
         torch.cuda.synchronize()
         res.append((ls, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, st))
     (l_e, sd_e, _), (l_g, sd_g, st) = res
-    # the RCCL kernels inside the captured step graphs
-    n_coll = 0
+    # kernels in the captured step graphs that are not this library's (k_*):
+    # RCCL's (and torch's few elementwise ones, which the eager step has too)
+    n_coll, n_ours = 0, 0
     for ent in st._graphs.values():
-        if ent.lanes is not None:  # keep_graph capture: the raw graph is there
-            n_coll += hlhgat.ops.graph_kernel_count(ent.graph.raw_cuda_graph(), "nccl")[1]
-        else:
-            n_coll = -1  # torch's instantiated graph: not introspectable
-            break
+        k, ours = hlhgat.ops.graph_kernel_count(ent.graph.raw_cuda_graph(), "k_")
+        n_coll += k - ours
+        n_ours += ours
     hlhgat.ops.check_device_errors()
     print(json.dumps({"captures": st.stats["captures"], "replay": st.stats["replay"],
-                      "lanes": st.stats.get("lanes"), "lanes_off": st.lanes_off,
                       "exchange_in_graph": st._exchange_in_graph,
-                      "collective_kernels_in_step": n_coll,
+                      "foreign_kernels_in_graphs": n_coll, "own_kernels_in_graphs": n_ours,
+                      "graphs_off": st.graphs_off,
                       "losses_equal": l_e == l_g, "losses": [l_e, l_g],
                       "param_diffs": [k for k in sd_e if not torch.equal(sd_e[k], sd_g[k])]}))
     dist.destroy_process_group()

@@ -120,15 +120,10 @@ def test_two_rank_gloo_matches_mean_gradient():
 KW = dict(channels=[1, 1], filters=[32, 32], mlp_channels=[64], K=3, keig=15)
 
 
-def _check_lanes(step):
-    """No device error, and every lane counter of every captured shape equal
-    (each signal and each wait ran once per replay of its shape)."""
+def _check_errors():
+    """No kernel raised the device error word during the run."""
     from hlhgat import ops
     assert ops.device_errors() == 0, ops.device_errors()
-    for ent in step._graphs.values():
-        if ent.lanes is not None:
-            c, tmo = ent.lanes.counters()
-            assert len(set(c)) <= 1 and not any(tmo), (c, tmo)
 
 
 def _run(graphs, fork, batches, order):
@@ -154,14 +149,12 @@ def _run(graphs, fork, batches, order):
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) * 1e3
                 print(f"   host call {th:.1f} ms", flush=True)
-                cnt = [e.lanes.counters() for e in step._graphs.values() if e.lanes is not None]
                 print(f"[_run graphs={graphs} fork={fork}] step {k} shape {i}: {dt:.1f} ms "
-                      f"err {ops.device_errors()} counters {[sorted(set(c)) for c, _ in cnt]} "
-                      f"timeouts {[t for _, t in cnt]}", flush=True)
+                      f"err {ops.device_errors()} stats {step.stats}", flush=True)
         else:
             losses = [float(step(batches[i])) for i in order]
         torch.cuda.synchronize()
-        _check_lanes(step)
+        _check_errors()
         sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
         return losses, sd, dict(step.stats)
     finally:
@@ -180,38 +173,6 @@ def test_graph_replay_equals_eager(cuda):
     assert l_e == l_g
     for k in sd_e:
         assert torch.equal(sd_e[k], sd_g[k]), k
-
-
-@pytest.mark.gpu
-def test_lane_replay_equals_graph_replay(cuda):
-    """The captured step split into one linear graph per stream lane with
-    device signal / wait kernels at the cross-lane edges (ops.Lanes) gives the
-    bits of torch's replay of the captured graph and of the eager step."""
-    from hlhgat import ops, train
-    from hlhgat.synthetic import zinc_like_batch
-    batches = [zinc_like_batch(40, seed=3).to(cuda), zinc_like_batch(33, seed=4).to(cuda)]
-    order = [0, 1, 0, 1, 1, 0, 0]
-    res = []
-    prev = train.LANES
-    for lanes in (False, True):
-        train.LANES = lanes
-        try:
-            res.append(_run(True, True, batches, order))
-        finally:
-            train.LANES = prev
-    (l0, sd0, st0), (l1, sd1, st1) = res
-    assert "lanes" not in st0
-    info = st1["lanes"]
-    assert info["lanes"] == 2 and min(info["nodes"]) > 0 and info["signals"] > 0, info
-    assert st1["captures"] == 2 and st1["replay"] == 5, st1
-    assert ops.device_errors() == 0
-    assert l0 == l1
-    for k in sd0:
-        assert torch.equal(sd0[k], sd1[k]), k
-    l_e, sd_e, _ = _run(False, True, batches, order)
-    assert l_e == l1
-    for k in sd_e:
-        assert torch.equal(sd_e[k], sd1[k]), k
 
 
 @pytest.mark.gpu
@@ -579,7 +540,6 @@ def test_head_graph_replay_equals_eager(cuda, kind):
         res.append((ls, {k: v.detach().clone() for k, v in m.state_dict().items()}, st.stats))
     (l_e, sd_e, _), (l_g, sd_g, stg) = res
     assert stg["captures"] == 2 and stg["replay"] == 3, stg
-    assert "lanes" in stg, stg  # replayed as stream lanes (ops.Lanes)
     assert l_e == l_g
     for k in sd_e:
         assert torch.equal(sd_e[k], sd_g[k]), k

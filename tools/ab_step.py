@@ -14,7 +14,6 @@ Variants (A/B hooks, not product settings):
   nomlp2      the readout MLP module by module (no two-layer fused node)
   noreadside  the edge readout mean on the main stream
   noreserve   BatchNorm workspaces not reserved before the capture
-  nolanes     torch's replay of the whole captured graph (no stream lanes)
 """
 import argparse
 import json
@@ -42,7 +41,6 @@ def set_variant(name, on):
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")
     hodge_st_model.SYNC_SIDE_ALWAYS = on and name == "sync"
     train.BN_RESERVE_CHANNELS = 0 if (on and name == "noreserve") else 2048
-    train.LANES = not (on and name == "nolanes")
 
 
 def main():
@@ -79,6 +77,8 @@ def main():
                 st(batches[i % len(batches)])
             torch.cuda.synchronize()
             res[v].append((time.perf_counter() - t0) / args.steps * 1e3)
+    from hlhgat import ops as _ops
+    _ops.check_device_errors()  # a timed-out wait / barrier voids the A/B
     out = {v: {"ms_median": sorted(x)[len(x) // 2], "ms_min": min(x),
                "ms": [round(t, 4) for t in x]} for v, x in res.items()}
     print(json.dumps(out))

@@ -1,5 +1,5 @@
 """InferStep probe: the config-2 ZINC eval forward (eval fixture inputs) --
-eager vs replayed (lanes on / off, chains on / off); max |diff| per replay."""
+eager vs replayed (chains on / off); max |diff| per replay."""
 import os
 import sys
 
@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 def main():
     import hlhgat
-    from hlhgat import ops, train
+    from hlhgat import ops
     from hlhgat.train import InferStep
     import test_eval_mode as TE
     from baseline_params import fill_params
@@ -23,9 +23,8 @@ def main():
     name = "eval_cfg2_zinc"
     g, _, ev = TE._inputs(name, lambda gg, p: TE._product_data(gg, p, cuda))
     bufs = {k[4:]: torch.from_numpy(np.asarray(g[k])) for k in g if k.startswith("buf/")}
-    for lanes in (False, True):
+    if True:
         for chains in (False, True):
-            train.LANES = lanes
             ops.CHAINS_ENABLED = chains
             m = getattr(hlhgat, TE.CASES[name][1])(**TE.CASES[name][2])
             fill_params(m, int(g["seed"]))
@@ -39,7 +38,7 @@ def main():
                 e2 = m(ev).clone()
                 m.train()
             d = [float((o - outs[0]).abs().max()) for o in outs[1:]]
-            print(f"lanes={lanes} chains={chains}: stats {inf.stats} lanes_off {inf.lanes_off} "
+            print(f"chains={chains}: stats {inf.stats} "
                   f"replay-vs-eager {d} eager-vs-eager {float((e2 - outs[0]).abs().max())} "
                   f"vs ref {float((outs[0].cpu() - torch.from_numpy(g['out'])).abs().max()):.2e}",
                   flush=True)
