@@ -93,7 +93,7 @@ def _freeze(ref, m_hip, taps):
     return masked
 
 
-def _check(case, m_hip, ref64, masked, ref32=None):
+def _check(case, m_hip, ref64, masked, ref32=None, cond=None):
     for mm in masked:
         assert mm.i == len(mm.masks), "fewer ReLU calls than the HIP forward made"
     p64 = dict(ref64.named_parameters())
@@ -116,21 +116,26 @@ def _check(case, m_hip, ref64, masked, ref32=None):
                 bad.append((k, err, noise32))
             continue
         err32 = (float((p32[k].grad.double() - e).abs().max()) / scale) if k in p32 else 0.0
-        bound = max(TOL, 3 * err32)
+        c = (cond or {}).get(k, 0.0)
+        bound = max(TOL, 3 * max(err32, c))
+        floor = "1e-4" if bound == TOL else ("3x fp32 (frozen)" if err32 >= c else
+                                              "3x fp64 conditioning (frozen)")
         rows.append({"param": k, "err": err, "bound": bound, "err_fp32_frozen": err32,
-                     "scale": scale, "floor": "1e-4" if bound == TOL else "3x fp32 (frozen)"})
+                     "cond_fp64_frozen": c, "scale": scale, "floor": floor})
         if err > bound:
             bad.append((k, err, err32))
     out_dir = os.path.join(REPO, "gpurun_out", "grad_gates")
     os.makedirs(out_dir, exist_ok=True)
     tight = [r for r in rows if "err_fp32_frozen" in r]
     n_floor = sum(r["floor"] != "1e-4" for r in tight)
+    n_cond = sum(r["floor"].startswith("3x fp64") for r in tight)
     worst = max((r["err"], r["param"]) for r in tight)
     worst32 = max(r["err_fp32_frozen"] for r in tight)
     with open(os.path.join(out_dir, f"frozen_{case}.json"), "w") as f:
         json.dump({"case": case, "tol": TOL, "n_masks": sum(len(m.masks) for m in masked),
                    "worst_hip": worst[0], "worst_fp32_oracle_frozen": worst32,
-                   "params_at_fp32_floor": n_floor, "params": rows}, f, indent=1)
+                   "params_at_fp32_floor": n_floor, "params_at_fp64_conditioning": n_cond,
+                   "params": rows}, f, indent=1)
     print(f"[frozen-mask] {case}: {len(tight)} params, worst HIP {worst[0]:.2e} ({worst[1]}), "
           f"worst fp32 oracle {worst32:.2e}; {n_floor} params bounded by the fp32 floor")
     assert not bad, bad
@@ -244,8 +249,9 @@ def _as_d(b, dtype):
 
 
 def _to_dev(b, cuda, factored):
+    import copy
     from hlhgat import ops
-    bd = b.to(cuda)
+    bd = copy.copy(b).to(cuda)  # Batch.to moves in place: keep the host batch for the oracle
     ops.mark_hodge(bd.edge_index_t)
     ops.mark_hodge(bd.edge_index_s)
     if factored:
@@ -255,12 +261,18 @@ def _to_dev(b, cuda, factored):
 
 @pytest.mark.parametrize("name,kind,factored", [("cfg3_cifar_16", "cifar", True),
                                                 ("cfg4_pepfunc_16", "peptides", False),
-                                                ("cfg5_tsp_4x2500", "tsp", True)])
+                                                ("cfg5_tsp_4x2500", "tsp", True),
+                                                ("cfg5_tsp_4x2500_csr", "tsp", False)])
 def test_frozen_mask_grads_heads_realistic_batches(cuda, name, kind, factored):
     """Configs 3 / 4 / 5 at their own hyperparameters on realistic batches:
     every parameter gradient within 1e-4 of the fp64 oracle (frozen masks),
     or within 3x the fp32 oracle's own error where that is larger (each such
-    parameter named in the gate log with its fp32 error)."""
+    parameter named in the gate log with its fp32 error).  TSP (12 blocks of
+    batch-statistics BatchNorm over 10k nodes / 52k edges) is ill-conditioned
+    in fp32 itself (the fp32 oracle is up to ~1e-2 from fp64): there the bound
+    also admits 3x the fp64 gradient's own change under two 1e-6 relative
+    parameter perturbations WITH THE SAME frozen masks (a conditioning probe
+    with no mask flip), logged per parameter."""
     import hlhgat
     from hlhgat import ops
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -298,5 +310,22 @@ def test_frozen_mask_grads_heads_realistic_batches(cuda, name, kind, factored):
         (o * Rg.to(dt)).sum().backward()
         outs.append(o)
     close(out.detach().cpu(), outs[0].detach(), 1e-4, "out vs fp64 oracle (frozen masks)")
-    _check(name, m, ref64, masked, ref32)
+    cond = None
+    if kind == "tsp":
+        cond = {}
+        base = dict(ref64.named_parameters())
+        for ps in (0, 1):
+            rp = getattr(R, cls_ref)(**kw)
+            fill_params(rp, seed)
+            rp = rp.double().train()
+            TB._perturb(rp, 1e-6, ps)
+            _freeze(rp, m, taps)
+            o, _ = rp(_as_d(raw, torch.float64))
+            (o * Rg.double()).sum().backward()
+            for k, p in rp.named_parameters():
+                if p.grad is None or base[k].grad is None:
+                    continue
+                sc = max(1.0, float(base[k].grad.abs().max()))
+                cond[k] = max(cond.get(k, 0.0), float((p.grad - base[k].grad).abs().max()) / sc)
+    _check(name, m, ref64, masked, ref32, cond)
     ops.check_device_errors()
