@@ -878,6 +878,31 @@ def head_workload(args, rank, world, device):
         dist.destroy_process_group()
 
 
+def eval_leg(model, batches, steps=20):
+    """The reference's evaluation loop body (main_zinc...:165-177: model.eval(),
+    out = model(data) under torch.no_grad(), per batch) on the timed workload's
+    device-resident batches: hlhgat.train.InferStep replays one captured eval
+    forward per batch shape; the eager forward beside it."""
+    from hlhgat.train import InferStep
+    out = {}
+    for graphs in (False, True):
+        inf = InferStep(model, graphs=graphs)
+        for i in range(3):
+            inf(batches[i % len(batches)])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            inf(batches[i % len(batches)])
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        out["replayed" if graphs else "eager"] = {
+            "value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
+            "ms_per_batch": round(dt * 1e3, 3), "stats": dict(inf.stats)}
+    out["what"] = ("model.eval() + torch.no_grad() forward of the timed workload's padded "
+                   "1000-graph batches (BatchNorm on running statistics)")
+    return out
+
+
 def h2d_leg(batch_cpu, device, reps=10):
     """The reference's loop copies each batch to the device every step
     (data.to(device)); bench.py's `value` excludes it (inputs resident in
@@ -1125,6 +1150,7 @@ def main():
              "BatchNorm backward statistics; bytes 12 n C (x, dy, y)"))},
         "spmm_cfg5": None,
         "heads": None,
+        "eval": None,
         "h2d": None,
         "loader": None,
     }
@@ -1174,6 +1200,9 @@ def main():
         h = h2d_leg(dataset.collate(np.arange(GRAPHS_PER_GPU), caps), device)
         h["value_if_serialised"] = round(GRAPHS_PER_GPU / (ms_step + h["ms_per_batch"]) * 1e3, 1)
         result["h2d"] = h
+    if rank == 0 and world == 1:
+        log("[rank 0] eval leg")
+        result["eval"] = _guarded("eval", eval_leg, model, batches)
     if rank == 0 and world == 1 and not args.no_loader:
         log("[rank 0] loader leg")
         result["loader"] = loader_leg(dataset, step, caps, device, ms_step)
