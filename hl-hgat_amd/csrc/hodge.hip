@@ -7,10 +7,10 @@
 // dense_to_sparse (lib/Hodge_Dataset.py:451-468, :780-799): O(N^3) for lmax
 // and an E x E dense L1 (10 GB at BASELINE config 5).  Here, from the edge
 // list and the incidence CSR alone:
-//   * k_lanczos_lmax: lmax of every graph's L0 in ONE launch, one workgroup
-//     per graph: Lanczos on L0 x = deg .* x - A x (fp64, full
-//     re-orthogonalisation, <= 64 steps), then the largest eigenvalue of the
-//     tridiagonal matrix by Sturm-sequence bisection;
+//   * k_lanczos_lmax: lmax of every graph's L0 in ONE launch, one
+//     wave per graph: Lanczos on L0 x = deg .* x - A x (fp64, three-term
+//     recurrence with local re-orthogonalisation, <= 64 steps), then the
+//     largest eigenvalue of the tridiagonal matrix by Sturm-sequence bisection;
 //   * k_hodge_l0_rows / k_hodge_l1_rows: the sparse L0 / L1 rows in CSR
 //     (columns ascending, as dense_to_sparse orders them) with the
 //     reference's float32 entries fl(fl(2 v) / lmax): L0 row v = {v: deg(v),
@@ -24,8 +24,9 @@ using namespace hlhgat;
 
 namespace {
 
-constexpr int kLzThreads = 256;
+constexpr int kLzThreads = 64;          // one wave per graph
 constexpr int kLzMaxSteps = 64;
+constexpr int kLzLdsBytes = 48 * 1024;  // a graph's vectors + local adjacency, when they fit
 
 struct LanczosArgs {
   const int32_t* inc_rowptr;  // incidence CSR (node -> incident edge ids, ascending)
@@ -34,36 +35,15 @@ struct LanczosArgs {
   int64_t n_edges;
   const int64_t* node_ptr;    // [n_graphs + 1]
   int steps;
-  double* Q;                  // [steps + 1][n_nodes] Lanczos vectors
-  double* W;                  // [n_nodes] work vector
+  double* Q;                  // [3][n_nodes] q_{j-1}, q_j, w for graphs that miss the LDS
   int64_t n_nodes;
   double* lmax;               // [n_graphs]
 };
 
-__device__ double block_sum(double v, double* red) {
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  __syncthreads();
-  if (lane == 0) red[wave] = v;
-  __syncthreads();
-  double s = 0.0;
-  for (int w = 0; w < kLzThreads / 64; ++w) s += red[w];
-  return s;
-}
-
-// y = L0 x on the graph's nodes [n0, n1): deg(v) x[v] - sum of x[other end]
-__device__ void l0_apply(const LanczosArgs& a, int64_t n0, int64_t n1, const double* x,
-                         double* y) {
-  for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) {
-    const int e0 = a.inc_rowptr[v], e1 = a.inc_rowptr[v + 1];
-    double s = (double)(e1 - e0) * x[v];
-    for (int p = e0; p < e1; ++p) {
-      const int64_t e = a.inc_edge[p];
-      const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
-      s -= x[i == v ? j : i];
-    }
-    y[v] = s;
-  }
+  return v;
 }
 
 // number of eigenvalues of the symmetric tridiagonal (al, be) below x
@@ -79,72 +59,159 @@ __device__ int sturm_count(const double* al, const double* be, int k, double x) 
   return c;
 }
 
-__global__ __launch_bounds__(kLzThreads) void k_lanczos_lmax(LanczosArgs a) {
-  __shared__ double red[kLzThreads / 64];
-  __shared__ double al[kLzMaxSteps + 1], be[kLzMaxSteps + 2];
-  __shared__ int s_k;
-  const int g = blockIdx.x;
-  const int64_t n0 = a.node_ptr[g], n1 = a.node_ptr[g + 1], ng = n1 - n0;
-  const int m = (int)(ng < a.steps ? ng : a.steps);
-  auto Qv = [&](int j) { return a.Q + (int64_t)j * a.n_nodes; };
+// Lanczos on one graph's L0 (n nodes, local ids; apply(x, y): y = L0 x) by
+// the three-term recurrence with a local re-orthogonalisation against q_j
+// (one extra dot product per step) and no global one: loss of orthogonality
+// only adds ghost copies of converged Ritz values, it does not move the
+// largest one past lambda_max (Paige), so lambda_max converges as with full
+// re-orthogonalisation at 3 wave reductions per step instead of 2 (j + 1)
+// block reductions (full Gram-Schmidt made this kernel ~3 ms for 256 CIFAR
+// graphs, profiles/r04_pipeline/).  Lane l owns the nodes l, l + 64, ... in
+// every loop, so q_{j-1}, q_j and w are lane-private except for the
+// neighbour reads of apply.  Returns the size k of the tridiagonal (al, be).
+template <typename Apply>
+__device__ int lanczos(Apply apply, int n, int m, double* qp, double* q, double* w, double* al,
+                       double* be) {
+  const int lane = threadIdx.x;
   // deterministic start vector with a component along every eigenvector
   double nrm = 0.0;
-  for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) {
-    const double q = 1.0 + (double)(((uint64_t)(v - n0) * 2654435761ull) % 1000ull) * 1e-3;
-    Qv(0)[v] = q;
-    nrm += q * q;
+  for (int v = lane; v < n; v += kLzThreads) {
+    const double x = 1.0 + (double)(((uint64_t)v * 2654435761ull) % 1000ull) * 1e-3;
+    q[v] = x;
+    qp[v] = 0.0;
+    nrm += x * x;
   }
-  nrm = sqrt(block_sum(nrm, red));
-  for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) Qv(0)[v] /= nrm;
-  if (threadIdx.x == 0) s_k = m;
+  nrm = sqrt(wave_sum(nrm));
+  for (int v = lane; v < n; v += kLzThreads) q[v] /= nrm;
   __syncthreads();
+  int k = m;
+  double beta = 0.0;
   for (int j = 0; j < m; ++j) {
-    l0_apply(a, n0, n1, Qv(j), a.W);
-    __syncthreads();
-    // full re-orthogonalisation (two passes of classical Gram-Schmidt); the
-    // first coefficient against q_j is alpha_j
-    for (int pass = 0; pass < 2; ++pass) {
-      for (int i = 0; i <= j; ++i) {
-        double d = 0.0;
-        for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) d += a.W[v] * Qv(i)[v];
-        d = block_sum(d, red);
-        if (pass == 0 && i == j && threadIdx.x == 0) al[j] = d;
-        if (pass == 1 && i == j && threadIdx.x == 0) al[j] += d;
-        for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) a.W[v] -= d * Qv(i)[v];
-        __syncthreads();
-      }
+    apply(q, w);
+    double d = 0.0;
+    for (int v = lane; v < n; v += kLzThreads) {
+      const double t = w[v] - beta * qp[v];
+      w[v] = t;
+      d += t * q[v];
     }
-    double b = 0.0;
-    for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) b += a.W[v] * a.W[v];
-    b = sqrt(block_sum(b, red));
-    __syncthreads();
+    double alpha = wave_sum(d);
+    d = 0.0;
+    for (int v = lane; v < n; v += kLzThreads) {
+      const double t = w[v] - alpha * q[v];
+      w[v] = t;
+      d += t * q[v];
+    }
+    const double c = wave_sum(d);  // local re-orthogonalisation
+    alpha += c;
+    d = 0.0;
+    for (int v = lane; v < n; v += kLzThreads) {
+      const double t = w[v] - c * q[v];
+      w[v] = t;
+      d += t * t;
+    }
+    const double b = sqrt(wave_sum(d));
+    if (lane == 0) al[j] = alpha;
     if (j + 1 >= m) break;
-    const double scale = fabs(al[j]) > 1.0 ? fabs(al[j]) : 1.0;
+    const double scale = fabs(alpha) > 1.0 ? fabs(alpha) : 1.0;
     if (b <= 1e-12 * scale) {  // invariant subspace found: T is complete
-      if (threadIdx.x == 0) s_k = j + 1;
-      __syncthreads();
+      k = j + 1;
       break;
     }
-    if (threadIdx.x == 0) be[j + 1] = b;
-    for (int64_t v = n0 + threadIdx.x; v < n1; v += kLzThreads) Qv(j + 1)[v] = a.W[v] / b;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const int k = s_k;
-    // Gershgorin bounds, then bisection for the largest eigenvalue
-    double lo = 0.0, hi = 0.0;
-    for (int i = 0; i < k; ++i) {
-      const double r = (i ? fabs(be[i]) : 0.0) + (i + 1 < k ? fabs(be[i + 1]) : 0.0);
-      lo = fmin(lo, al[i] - r);
-      hi = fmax(hi, al[i] + r);
+    if (lane == 0) be[j + 1] = b;
+    for (int v = lane; v < n; v += kLzThreads) {
+      qp[v] = q[v];
+      q[v] = w[v] / b;
     }
-    for (int it = 0; it < 200 && hi - lo > 1e-15 * fmax(1.0, fabs(hi)); ++it) {
-      const double mid = 0.5 * (lo + hi);
-      if (sturm_count(al, be, k, mid) < k) lo = mid;  // some eigenvalue above mid
-      else hi = mid;
-    }
-    a.lmax[g] = ng > 0 ? hi : 0.0;
+    beta = b;
+    __syncthreads();  // apply reads the neighbours' q
   }
+  __syncthreads();
+  return k;
+}
+
+// lambda_max of every graph's L0 = deg .* x - A x, one wave per graph.  A
+// graph whose vectors and local adjacency (node -> neighbour ids) fit in
+// kLzLdsBytes runs from the LDS (the CIFAR / ZINC / peptide graphs: ~8 KB);
+// a larger one (brain skeleton, TSP) walks the incidence CSR in global
+// memory with its vectors in the workspace.
+__global__ __launch_bounds__(kLzThreads) void k_lanczos_lmax(LanczosArgs a) {
+  extern __shared__ __align__(16) unsigned char lz_lds[];
+  __shared__ double al[kLzMaxSteps + 1], be[kLzMaxSteps + 2];
+  const int g = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t n0 = a.node_ptr[g], n1 = a.node_ptr[g + 1];
+  const int n = (int)(n1 - n0);
+  const int m = n < a.steps ? n : a.steps;
+  int k = 0;
+  if (n > 0) {
+    const int base = a.inc_rowptr[n0];
+    const int nnz = a.inc_rowptr[n1] - base;  // 2 E of this graph
+    const int64_t need = 24ll * n + 4ll * (n + 1) + 4ll * nnz;
+    if (need <= kLzLdsBytes) {
+      double* qp = reinterpret_cast<double*>(lz_lds);
+      double* q = qp + n;
+      double* w = q + n;
+      int* rp = reinterpret_cast<int*>(w + n);
+      int* nb = rp + n + 1;
+      for (int v = lane; v <= n; v += kLzThreads) rp[v] = a.inc_rowptr[n0 + v] - base;
+      for (int v = lane; v < n; v += kLzThreads) {
+        const int e0 = a.inc_rowptr[n0 + v], e1 = a.inc_rowptr[n0 + v + 1];
+        for (int p = e0; p < e1; ++p) {
+          const int64_t e = a.inc_edge[p];
+          const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
+          nb[p - base] = (int)((i == n0 + v ? j : i) - n0);
+        }
+      }
+      __syncthreads();
+      auto apply = [&](const double* x, double* y) {
+        for (int v = lane; v < n; v += kLzThreads) {
+          const int p0 = rp[v], p1 = rp[v + 1];
+          double s = (double)(p1 - p0) * x[v];
+          for (int p = p0; p < p1; ++p) s -= x[nb[p]];
+          y[v] = s;
+        }
+      };
+      k = lanczos(apply, n, m, qp, q, w, al, be);
+    } else {
+      double* qp = a.Q + n0;
+      double* q = a.Q + a.n_nodes + n0;
+      double* w = a.Q + 2 * a.n_nodes + n0;
+      auto apply = [&](const double* x, double* y) {
+        for (int v = lane; v < n; v += kLzThreads) {
+          const int e0 = a.inc_rowptr[n0 + v], e1 = a.inc_rowptr[n0 + v + 1];
+          double s = (double)(e1 - e0) * x[v];
+          for (int p = e0; p < e1; ++p) {
+            const int64_t e = a.inc_edge[p];
+            const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
+            s -= x[(i == n0 + v ? j : i) - n0];
+          }
+          y[v] = s;
+        }
+      };
+      k = lanczos(apply, n, m, qp, q, w, al, be);
+    }
+  }
+  // Gershgorin bounds, then multisection for the largest eigenvalue: the 64
+  // lanes count the Sturm sequence at 64 interior points of [lo, hi] at once
+  // (the interval shrinks 65-fold per pass; bisection by one lane cost ~0.4 ms
+  // of serial fp64 divides per launch)
+  double lo = 0.0, hi = 0.0;
+  for (int i = 0; i < k; ++i) {
+    const double r = (i ? fabs(be[i]) : 0.0) + (i + 1 < k ? fabs(be[i + 1]) : 0.0);
+    lo = fmin(lo, al[i] - r);
+    hi = fmax(hi, al[i] + r);
+  }
+  for (int it = 0; it < 40 && k > 0 && hi - lo > 1e-15 * fmax(1.0, fabs(hi)); ++it) {
+    const double h = (hi - lo) / (double)(kLzThreads + 1);
+    const bool above = sturm_count(al, be, k, lo + h * (double)(lane + 1)) < k;
+    const unsigned long long mask = __ballot(above);  // lanes 0 .. t: an eigenvalue above
+    const int t = mask ? 63 - __clzll(mask) : -1;
+    const double nlo = t >= 0 ? lo + h * (double)(t + 1) : lo;
+    const double nhi = t < kLzThreads - 1 ? lo + h * (double)(t + 2) : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  if (lane == 0) a.lmax[g] = n > 0 ? hi : 0.0;
 }
 
 struct BuildArgs {
@@ -244,7 +311,7 @@ __global__ __launch_bounds__(256) void k_hodge_row_sizes(const int32_t* inc_rowp
 
 extern "C" int64_t hlhgat_hodge_lmax_workspace_bytes(int64_t n_nodes, int steps) {
   if (n_nodes < 0 || steps < 1 || steps > kLzMaxSteps) return 0;
-  return (int64_t)sizeof(double) * n_nodes * (steps + 2);
+  return (int64_t)sizeof(double) * n_nodes * 3;
 }
 
 extern "C" int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_edge,
@@ -268,10 +335,9 @@ extern "C" int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_e
   a.node_ptr = node_ptr;
   a.steps = steps;
   a.Q = reinterpret_cast<double*>(workspace);
-  a.W = a.Q + (int64_t)(steps + 1) * n_nodes;
   a.n_nodes = n_nodes;
   a.lmax = lmax;
-  hipLaunchKernelGGL(k_lanczos_lmax, dim3((unsigned)n_graphs), dim3(kLzThreads), 0,
+  hipLaunchKernelGGL(k_lanczos_lmax, dim3((unsigned)n_graphs), dim3(kLzThreads), kLzLdsBytes,
                      as_stream(stream), a);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;

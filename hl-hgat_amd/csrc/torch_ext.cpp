@@ -1594,6 +1594,12 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       bs = pk.narrow(0, 2 * P * d + P, P);
     }
     Fork fk(xt.get_device());
+    const bool chain = chain_flag();
+    // the edge GEMM needs this node's own weight pack (built on the main
+    // stream above) unless a forward-wide pack (nei_prepack) was ordered before
+    // the chains began; outside chain mode this also makes the side stream
+    // part of a capture before anything is allocated on it
+    if (!chain || !has(packed)) fk.side_waits_main();
     Tensor Yt = at::empty({N, dn + de}, xt.options());  // [Qt | P2]
     Tensor h1t = at::empty({N, dn}, xt.options());
     // Ys / h1s are first written on the side stream, which in chain mode does
@@ -1622,14 +1628,9 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                  {A.size(1)}, A.size(0), W.size(0), b.data_ptr<float>(), out, stream_of(A));
     };
     SideMlp tn, te;
-    const bool chain = chain_flag();
     // Yt is read on the side stream after the exchange (no join at the end in
     // chain mode): keep its block for the side stream
     if (chain) Yt.record_stream(fk.side);
-    // the edge GEMM needs this node's own weight pack (built on the main
-    // stream above) unless a forward-wide pack (nei_prepack) was ordered before
-    // the chains began
-    if (!chain || !has(packed)) fk.side_waits_main();
     {  // edge side: first-layer GEMM on the side stream
       TStreamGuard g(fk.side);
       lin_into(xs, Ws, bs, Ys);
@@ -1715,16 +1716,6 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     //            packed 48 (no gradient: the weights' gradients go to pn / pe)
     variable_list out(49);
     const int64_t PN = 6, PE = 20;
-    Fork fk(xt.get_device());
-    Tensor dYt = at::empty({N, dn + de}, xt.options());
-    // dYs is first written on the side stream (which in chain mode does not
-    // wait for main): a block of the side stream's pool, kept for main's read
-    Tensor dYs;
-    {
-      TStreamGuard g(fk.side);
-      dYs = at::empty({E, de + dn}, xt.options());
-    }
-    dYs.record_stream(fk.main);
     auto side_bwd = [&](const Tensor& gy, int64_t P, const Tensor& g1, const Tensor& W3,
                         const Tensor& g4, int o0, Tensor dest, int q0, const Tensor& valid) {
       const Tensor &be1 = sv[q0 + 2], &b3 = sv[q0 + 3], &be4 = sv[q0 + 4];
@@ -1758,11 +1749,20 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     // (its consumers are the edge chain and the flush, which waits for every
     // deferring stream); only the exchange stays
     const bool chain_b = fdef && ctx->saved_data.count("chain") > 0;
-    if (chain_b) {
-      dYt.record_stream(fk.side);
-    } else {
-      fk.side_waits_main();
+    Fork fk(xt.get_device());
+    // outside chain mode the side stream waits for main first (which also
+    // makes it part of a capture before anything is allocated on it)
+    if (!chain_b) fk.side_waits_main();
+    Tensor dYt = at::empty({N, dn + de}, xt.options());
+    // dYs is first written on the side stream (which in chain mode does not
+    // wait for main): a block of the side stream's pool, kept for main's read
+    Tensor dYs;
+    {
+      TStreamGuard g(fk.side);
+      dYs = at::empty({E, de + dn}, xt.options());
     }
+    dYs.record_stream(fk.main);
+    if (chain_b) dYt.record_stream(fk.side);
     {  // edge side MLP backward on the side stream -> dYs[:, :de]
       TStreamGuard g(fk.side);
       side_bwd(grads[1], PE, sv[11], sv[12], sv[13], 22, dYs.narrow(1, 0, de), 35, sv[41]);

@@ -229,8 +229,11 @@ class NodeEdgeInt(nn.Module):
                         _nn.tap(mod, y)
             if r is not None:
                 return r
-        if not self.only_att and getattr(par, "valid_t", None) is not None:
-            # the unfused value path's BatchNorms would count the padding rows
+        if (not self.only_att and getattr(par, "valid_t", None) is not None
+                and any(isinstance(m, nn.BatchNorm1d) and ops._bn_uses_batch_stats(m)
+                        for m in list(self.WV_Node) + list(self.WV_Edge))):
+            # the unfused value path's batch-statistics BatchNorms would count
+            # the padding rows (eval mode, on running statistics, is row-wise)
             raise RuntimeError("hlhgat: static-shape (padded) batches need the fused "
                                "NodeEdgeInt value path (training-mode WV_* MLPs)")
         ch = ops.active_chains(x_t.device) if x_t.is_cuda else None

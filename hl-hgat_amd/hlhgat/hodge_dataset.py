@@ -1050,26 +1050,46 @@ def mlgc_map(cluster, edge_index):
         int(n1.value)
 
 
-def mlgc_batch(edge_lists, ns, perms, threads: int = 0):
+class MLGCBatch:
+    """hlhgat_mlgc_batch's flat outputs for G graphs: c_node [N] and c_edge
+    [E] (per graph, concatenated), ce [2, E] holding graph g's coarse edges
+    (local coarse ids) at the head of its edge slot edge_ptr[g] ..
+    edge_ptr[g] + cm[g], cn [G] coarse node counts, cm [G] coarse edge
+    counts."""
+
+    def __init__(self, node_ptr, edge_ptr, c_node, c_edge, ce, cn, cm):
+        self.node_ptr, self.edge_ptr = node_ptr, edge_ptr
+        self.c_node, self.c_edge, self.ce, self.cn, self.cm = c_node, c_edge, ce, cn, cm
+
+    def per_graph(self):
+        """[(c_node, c_edge, coarse edge_index, n1)] per graph, like mlgc_map."""
+        out = []
+        for g in range(self.cn.size):
+            n0, n1_ = self.node_ptr[g], self.node_ptr[g + 1]
+            e0, e1 = self.edge_ptr[g], self.edge_ptr[g + 1]
+            out.append((self.c_node[n0:n1_], self.c_edge[e0:e1],
+                        np.ascontiguousarray(self.ce[:, e0:e0 + self.cm[g]]), int(self.cn[g])))
+        return out
+
+
+def mlgc_batch_flat(edges, edge_counts, ns, perm, threads: int = 0) -> MLGCBatch:
     """One MLGC level for a batch of graphs by one native call
-    (hlhgat_mlgc_batch): per graph, graclus over its i<j edge list taken both
-    ways with unit weights in node order perms[g], then mlgc_map -- the same
-    results as [mlgc_map(graclus(both, n, ones, perm=p), ei) ...] graph by
-    graph, on host threads.  Returns [(c_node, c_edge, coarse edge_index, n1)]
-    per graph, like mlgc_map."""
+    (hlhgat_mlgc_batch) on flat arrays: edges int64 [2, E] (each graph's i<j
+    edges in local node ids, graph after graph), edge_counts [G], ns [G],
+    perm [N] (graph g's graclus node order, local ids, in its node slot).
+    Per graph: graclus over the edges taken both ways with unit weights, then
+    mlgc_map -- the same results as mlgc_map(graclus(both, n, ones, perm=p),
+    ei) graph by graph, on host threads."""
     from ._lib import LIB, check
-    G = len(ns)
+    ns = np.asarray(ns, np.int64)
+    G = ns.size
     node_ptr = np.zeros(G + 1, np.int64)
-    node_ptr[1:] = np.cumsum(np.asarray(ns, np.int64))
-    ms = [int(np.asarray(e).shape[1]) for e in edge_lists]
+    node_ptr[1:] = np.cumsum(ns)
     edge_ptr = np.zeros(G + 1, np.int64)
-    edge_ptr[1:] = np.cumsum(np.asarray(ms, np.int64))
+    edge_ptr[1:] = np.cumsum(np.asarray(edge_counts, np.int64))
     E = int(edge_ptr[-1])
-    edges = np.ascontiguousarray(np.concatenate(
-        [np.asarray(e, np.int64).reshape(2, -1) for e in edge_lists], axis=1)
-        if G else np.zeros((2, 0), np.int64))
-    perm = np.ascontiguousarray(np.concatenate([np.asarray(p, np.int64) for p in perms])
-                                if G else np.zeros(0, np.int64))
+    edges = np.ascontiguousarray(np.asarray(edges, np.int64).reshape(2, E))
+    perm = np.ascontiguousarray(np.asarray(perm, np.int64).reshape(-1))
     if perm.size != node_ptr[-1]:
         raise ValueError("mlgc_batch: one permutation of each graph's nodes expected")
     c_node = np.empty(int(node_ptr[-1]), np.int64)
@@ -1081,15 +1101,20 @@ def mlgc_batch(edge_lists, ns, perms, threads: int = 0):
     check(LIB.hlhgat_mlgc_batch(G, node_ptr.ctypes.data, edge_ptr.ctypes.data, edges.ctypes.data,
                                 perm.ctypes.data, threads, c_node.ctypes.data, c_edge.ctypes.data,
                                 ce.ctypes.data, cn.ctypes.data, cm.ctypes.data), "mlgc_batch")
-    ce = ce.reshape(2, -1)
-    out = []
-    for g in range(G):
-        n0, n1_ = node_ptr[g], node_ptr[g + 1]
-        e0, e1 = edge_ptr[g], edge_ptr[g + 1]
-        out.append((c_node[n0:n1_], c_edge[e0:e1],
-                    np.ascontiguousarray(ce[:, e0:e0 + cm[g]]) if E else np.zeros((2, 0), np.int64),
-                    int(cn[g])))
-    return out
+    return MLGCBatch(node_ptr, edge_ptr, c_node, c_edge, ce.reshape(2, -1)[:, :E], cn, cm)
+
+
+def mlgc_batch(edge_lists, ns, perms, threads: int = 0):
+    """mlgc_batch_flat over per-graph lists: edge_lists[g] int64 [2, E_g],
+    perms[g] a permutation of graph g's nodes.  Returns [(c_node, c_edge,
+    coarse edge_index, n1)] per graph, like mlgc_map."""
+    G = len(ns)
+    edges = (np.concatenate([np.asarray(e, np.int64).reshape(2, -1) for e in edge_lists], axis=1)
+             if G else np.zeros((2, 0), np.int64))
+    perm = (np.concatenate([np.asarray(p, np.int64) for p in perms]) if G
+            else np.zeros(0, np.int64))
+    counts = [int(np.asarray(e).reshape(2, -1).shape[1]) for e in edge_lists]
+    return mlgc_batch_flat(edges, counts, ns, perm, threads).per_graph()
 
 
 def to_undirected_mean(edge_index, weight, n: int):

@@ -438,21 +438,28 @@ def _halo_args(A: "SparseCSR"):
     return A.halo
 
 
+_CHECK_SIZES = os.environ.get("HLHGAT_CHECK_SIZES", "0") == "1"
+
+
 def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tensor] = None,
-                steps: int = 64):
+                steps: int = 64, sizes=None):
     """Hodge Laplacians of a block-diagonal batch ON DEVICE (hlhgat_hodge_*):
     edge_index int64 [2, E] (i < j, PairData offsets), node_counts per graph.
     lmax per graph: given (float, as the reference's eigh result) or computed
     by the on-device Lanczos (fp64).  Returns (ei_t, w_t, ei_s, w_s, lmax) with
     the COO in the reference's dense_to_sparse order (row-major, zeros
-    dropped) and entries fl(fl(2 v) / lmax) (lib/Hodge_Dataset.py:451-468)."""
+    dropped) and entries fl(fl(2 v) / lmax) (lib/Hodge_Dataset.py:451-468).
+    sizes = (N, nnz(L0), nnz(L1)) when the caller knows them (nnz(L0) = the
+    non-isolated nodes + 2 E, nnz(L1) = sum deg^2 - E): then nothing here
+    waits on the device (HLHGAT_CHECK_SIZES=1 compares them with the device's
+    own row sizes)."""
     _req_dev(edge_index, "edge_index", torch.int64)
     dev = edge_index.device
     counts = torch.as_tensor(node_counts, dtype=torch.int64).to(dev)
     B = counts.numel()
     node_ptr = torch.zeros(B + 1, dtype=torch.int64, device=dev)
     node_ptr[1:] = torch.cumsum(counts, 0)
-    N = int(node_ptr[-1].item())
+    N = int(sizes[0]) if sizes is not None else int(node_ptr[-1].item())
     ei = edge_index.contiguous()
     E = ei.size(1)
     inc = incidence(ei, N)
@@ -476,7 +483,14 @@ def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tens
     rp1 = torch.zeros(E + 1, dtype=torch.int32, device=dev)
     rp0[1:] = torch.cumsum(sz0, 0)
     rp1[1:] = torch.cumsum(sz1, 0)
-    nnz0, nnz1 = int(rp0[-1].item()), int(rp1[-1].item())
+    if sizes is not None:
+        nnz0, nnz1 = int(sizes[1]), int(sizes[2])
+        if _CHECK_SIZES:
+            got = (int(node_ptr[-1].item()), int(rp0[-1].item()), int(rp1[-1].item()))
+            if got != (N, nnz0, nnz1):
+                raise RuntimeError(f"hlhgat: hodge_build sizes {tuple(sizes)} != device {got}")
+    else:
+        nnz0, nnz1 = int(rp0[-1].item()), int(rp1[-1].item())
     c0 = torch.empty(max(nnz0, 1), dtype=torch.int32, device=dev)
     v0 = torch.empty(max(nnz0, 1), dtype=torch.float32, device=dev)
     c1 = torch.empty(max(nnz1, 1), dtype=torch.int32, device=dev)

@@ -46,7 +46,7 @@ import numpy as np
 import torch
 
 from .hodge_dataset import (Batch, PairData, collate, dense_to_sparse, graclus, hodge_laplacians,
-                            mlgc_batch, mlgc_map)
+                            mlgc_batch, mlgc_batch_flat, mlgc_map)
 
 __all__ = ["SuperpixelPipeline", "to_undirected_min", "superpixel_raw"]
 
@@ -115,28 +115,67 @@ class SuperpixelPipeline:
             keep = ei[0] < ei[1]
             self.ei.append(ei[:, keep])
             self.attr.append(a[keep])
+        # the same, concatenated (local node ids), for the vectorised batch gather
+        self.m = np.array([e.shape[1] for e in self.ei], dtype=np.int64)
+        self.e_off = np.concatenate([[0], np.cumsum(self.m)]).astype(np.int64)
+        self.ei_all = (np.concatenate(self.ei, axis=1) if len(self.ei)
+                       else np.zeros((2, 0), np.int64))
+        self.attr_all = (np.concatenate(self.attr) if len(self.attr)
+                         else np.zeros(0, np.float32))
+        self.x_all = np.concatenate(self.x) if len(self.x) else np.zeros((0, 3), np.float32)
+        self.pos_all = np.concatenate(self.pos) if len(self.pos) else np.zeros((0, 2), np.float32)
+        self.n_off = np.concatenate([[0], np.cumsum(self.n)]).astype(np.int64)
+        self.y_all = (torch.cat([y.reshape(-1) for y in self.y]) if len(self.y)
+                      else torch.zeros(0, dtype=torch.int64))
 
     def __len__(self) -> int:
         return len(self.n)
 
     # -- host steps ------------------------------------------------------------
-    def _dropout(self, idx, rng) -> List[np.ndarray]:
-        """Edge keep-masks: dropout_edge(p=0.5) on the samples drawn for
-        augmentation (torch.rand(1) > 0.75, main_cifar10SP...:74-77)."""
-        masks = []
-        for i in idx:
-            E = self.ei[i].shape[1]
-            if self.aug and rng.random() > 0.75:
-                masks.append(rng.random(E) >= 0.5)
-            else:
-                masks.append(np.ones(E, dtype=bool))
-        return masks
+    @staticmethod
+    def _segments(starts, lengths):
+        """Concatenated index ranges [starts[b], starts[b] + lengths[b])."""
+        tot = int(lengths.sum())
+        if tot == 0:
+            return np.zeros(0, np.int64)
+        off = np.concatenate([[0], np.cumsum(lengths)[:-1]])
+        return np.repeat(starts - off, lengths) + np.arange(tot, dtype=np.int64)
 
-    def _pe_sign(self, rng, width):
-        """The reference's random PE sign flips: ones on the first columns,
-        +-1 on the last keig - 1 (main_cifar10SP...:113-124)."""
-        return np.concatenate([np.ones(width - (self.keig - 1), np.float32),
-                               (-1 + 2 * rng.integers(0, 2, self.keig - 1)).astype(np.float32)])
+    def _select(self, idx, rng):
+        """The batch's graphs, vectorised over the batch: dropout_edge(p = 0.5)
+        on the samples drawn for augmentation (torch.rand(1) > 0.75,
+        main_cifar10SP...:74-77), then the kept i<j edges (local node ids),
+        their attributes and per-graph edge counts, and graclus's random node
+        order per graph (keys drawn once, sorted within each graph)."""
+        B = len(idx)
+        ns = self.n[idx]
+        m = self.m[idx]
+        eidx = self._segments(self.e_off[idx], m)
+        gid_e = np.repeat(np.arange(B), m)
+        if self.aug:
+            drop = rng.random(B) > 0.75
+            keep = ~drop[gid_e] | (rng.random(eidx.size) >= 0.5)
+        else:
+            keep = np.ones(eidx.size, dtype=bool)
+        eidx, gid_e = eidx[keep], gid_e[keep]
+        ei = self.ei_all[:, eidx]
+        attr = self.attr_all[eidx]
+        E_g = np.bincount(gid_e, minlength=B).astype(np.int64)
+        # a random permutation of each graph's nodes: argsort of random keys
+        # per row of a [B, nmax] table whose padding keys sort last
+        nmax = int(ns.max()) if B else 0
+        pad = np.arange(nmax)[None, :] >= ns[:, None]
+        keys = rng.random((B, nmax))
+        keys[pad] = 2.0
+        perm = np.argsort(keys, axis=1)[~pad]
+        return ns, ei, attr, E_g, gid_e, perm
+
+    def _pe_signs(self, rng, B, width):
+        """The reference's random PE sign flips for B graphs: ones on the first
+        columns, +-1 on the last keig - 1 (main_cifar10SP...:113-124)."""
+        s = np.ones((B, width), np.float32)
+        s[:, width - (self.keig - 1):] = -1 + 2 * rng.integers(0, 2, (B, self.keig - 1))
+        return s
 
     # -- the batch -------------------------------------------------------------
     def batch(self, idx, seed: int = 0, device="cuda", perms=None) -> List[Batch]:
@@ -144,30 +183,52 @@ class SuperpixelPipeline:
         augmentation, graclus's node order and the sign flips (perms: an
         explicit graclus node order per graph, e.g. to replay a fixture)."""
         rng = np.random.default_rng(seed)
-        idx = [int(i) for i in idx]
-        masks = self._dropout(idx, rng)
-        eis = [self.ei[i][:, m] for i, m in zip(idx, masks)]
-        attrs = [self.attr[i][m] for i, m in zip(idx, masks)]
-        ns = [int(self.n[i]) for i in idx]
+        idx = np.asarray([int(i) for i in idx], dtype=np.int64)
+        self._tick(None)
+        ns, ei, attr, E_g, gid_e, perm = self._select(idx, rng)
+        if perms is not None:
+            perm = np.concatenate([np.asarray(p, np.int64) for p in perms])
+        self._tick("dropout + edge lists")
         # MLGC on the host: graclus on L0's pattern (= the edges, both ways; its
         # self-loops are dropped by graclus) with unit weights, the fine -> coarse map
         # (all graphs in one native call on host threads: hlhgat_mlgc_batch)
-        pl = [perms[b] if perms is not None else rng.permutation(n) for b, n in enumerate(ns)]
-        cmaps = mlgc_batch(eis, ns, pl)
+        mg = mlgc_batch_flat(ei, E_g, ns, perm)
+        self._tick("MLGC (native batch)")
         if str(device) == "cpu":
-            lv0, lv1 = self._levels_host(idx, eis, attrs, ns, cmaps)
+            e_off = np.concatenate([[0], np.cumsum(E_g)])
+            eis = [ei[:, e_off[b]:e_off[b + 1]] for b in range(len(idx))]
+            attrs = [attr[e_off[b]:e_off[b + 1]] for b in range(len(idx))]
+            lv0, lv1 = self._levels_host(idx, eis, attrs, [int(n) for n in ns], mg.per_graph())
         else:
-            lv0, lv1 = self._levels_device(idx, eis, attrs, ns, cmaps, torch.device(device))
-        # sign flips of the PE columns (after the cluster column is prepended)
-        st = torch.from_numpy(np.stack([self._pe_sign(rng, lv0.x_t.shape[1]) for _ in idx]))
-        ss = torch.from_numpy(np.stack([self._pe_sign(rng, lv0.x_s.shape[1]) for _ in idx]))
-        nt = torch.as_tensor(lv0.num_node1).to(lv0.x_t.device)
-        ne = torch.as_tensor(lv0.num_edge1).to(lv0.x_t.device)
-        lv0.x_t = lv0.x_t * torch.repeat_interleave(st.to(lv0.x_t.device), nt, dim=0,
-                                                    output_size=lv0.x_t.shape[0])
-        lv0.x_s = lv0.x_s * torch.repeat_interleave(ss.to(lv0.x_t.device), ne, dim=0,
-                                                    output_size=lv0.x_s.shape[0])
+            lv0, lv1 = self._levels_device(idx, ei, attr, ns, E_g, gid_e, mg, torch.device(device))
+        # sign flips of the PE columns (after the cluster column is prepended),
+        # one row of signs per graph broadcast over its nodes / edges
+        B = len(idx)
+        sg = np.concatenate([self._pe_signs(rng, B, lv0.x_t.shape[1]),
+                             self._pe_signs(rng, B, lv0.x_s.shape[1])], 1)
+        sg = torch.from_numpy(sg).to(lv0.x_t.device, non_blocking=True)
+        wt = lv0.x_t.shape[1]
+        lv0.x_t.mul_(sg[:, :wt].index_select(0, lv0._gid_t))
+        lv0.x_s.mul_(sg[:, wt:].index_select(0, lv0._gid_s))
+        del lv0._gid_t, lv0._gid_s
+        self._tick("PE sign flips")
         return [lv0, lv1]
+
+    # stage timing (tools/probes/pipeline_stages.py): PROFILE = True makes
+    # every stage boundary synchronise the device and accumulate its ms
+    PROFILE = False
+
+    def _tick(self, name):
+        if not self.PROFILE:
+            return
+        import time
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+        now = time.perf_counter()
+        if name is not None:
+            st = self.__dict__.setdefault("stage_ms", {})
+            st[name] = st.get(name, 0.0) + (now - self._t0) * 1e3
+        self._t0 = now
 
     def _features(self, i, ei, attr, pe):
         """x_t = [x, pos, pe], x_s = [attr, |x_i - x_j|, |pe_i + pe_j|], each
@@ -217,72 +278,111 @@ class SuperpixelPipeline:
             c.num_node1, c.num_edge1, c.num_nodes = n1, int(ei1.shape[1]), n1
             c._hodge_sorted = True
             f1.append(c)
-        return collate(f0, check_hodge=False), collate(f1, check_hodge=False)
+        lv0 = collate(f0, check_hodge=False)
+        lv0._gid_t = torch.repeat_interleave(torch.arange(len(f0)), torch.as_tensor(ns))
+        lv0._gid_s = torch.repeat_interleave(torch.arange(len(f0)),
+                                             torch.as_tensor([e.shape[1] for e in eis]))
+        return lv0, collate(f1, check_hodge=False)
 
-    def _levels_device(self, idx, eis, attrs, ns, cmaps, dev):
+    def _levels_device(self, idx, ei, attr, ns, E_g, gid_e, mg, dev):
+        """Both levels on the device.  The host arrays travel in two uploads
+        (one int64, one float32; the device tensors are views of them); the Hodge builder gets its sizes from the host (the nnz of L0
+        and L1 follow from the degrees), so nothing here waits on the device
+        but the eigh's own error check."""
         from . import ops
         B = len(idx)
-        n_off = np.concatenate([[0], np.cumsum(ns)])
-        ei_b = np.ascontiguousarray(np.concatenate([e + o for e, o in zip(eis, n_off[:-1])], axis=1))
-        E_g = [int(e.shape[1]) for e in eis]
-        ei_d = torch.from_numpy(ei_b).to(dev)
-        ei_t, w_t, ei_s, w_s, lam = ops.hodge_build(ei_d, ns)
+        N, E = int(ns.sum()), int(ei.shape[1])
+        n_off = np.concatenate([[0], np.cumsum(ns)]).astype(np.int64)
+        gid_n = np.repeat(np.arange(B), ns)
+        ei_b = ei + n_off[gid_e]  # block-diagonal batch (PairData offsets)
+        # coarse level: each graph's coarse edges at the head of its edge slot
+        n1 = mg.cn
+        m1 = mg.cm
+        o1 = np.concatenate([[0], np.cumsum(n1)]).astype(np.int64)
+        e_off = np.concatenate([[0], np.cumsum(E_g)]).astype(np.int64)
+        cidx = self._segments(e_off[:-1], m1)
+        gid_c = np.repeat(np.arange(B), m1)
+        ei1 = mg.ce[:, cidx] + o1[gid_c]
+        N1, E1 = int(o1[-1]), int(ei1.shape[1])
+        nodes = self._segments(self.n_off[idx], ns)
+
+        def nnz(e, n):
+            deg = np.bincount(e.reshape(-1), minlength=n)
+            return int((deg > 0).sum()) + 2 * e.shape[1], int((deg * deg).sum()) - e.shape[1]
+        ints = [ei_b.reshape(-1), ei1.reshape(-1), ns, E_g, n1, m1,
+                self.y_all.numpy()[idx].astype(np.int64), gid_n, gid_e]
+        flts = [self.x_all[nodes].reshape(-1), self.pos_all[nodes].reshape(-1), attr,
+                mg.c_node.astype(np.float32), mg.c_edge]
+        idev = torch.from_numpy(np.concatenate(ints)).to(dev)
+        fdev = torch.from_numpy(np.concatenate(flts)).to(dev)
+
+        def cut(t, sizes):
+            out, o = [], 0
+            for z in sizes:
+                out.append(t[o:o + z])
+                o += z
+            return out
+        ei_d, ei1_d, ns_d, Eg_d, n1_d, m1_d, y_d, gid_d, gide_d = cut(
+            idev, [a.size for a in ints])
+        ei_d, ei1_d = ei_d.view(2, E), ei1_d.view(2, E1)
+        x, pos, attr_d, c_node, c_edge = cut(fdev, [a.size for a in flts])
+        x, pos = x.view(N, 3), pos.view(N, 2)
+        self._tick("device levels: edge upload")
+        ei_t, w_t, ei_s, w_s, lam = ops.hodge_build(ei_d, ns_d, sizes=(N,) + nnz(ei_b, N))
+        self._tick("device levels: Hodge build (fine)")
         # eig_pe on the device: ONE batched eigh of the block-padded L0 stack
         # (padding rows / columns carry a diagonal above every real eigenvalue,
         # so each graph's smallest eigenpairs are its own, with zero padding)
-        nmax = max(ns)
+        nmax = int(ns.max())
         big = 10.0  # > lambda(L0) <= 2 after the 2 / lmax scaling
         L = torch.zeros(B, nmax, nmax, device=dev)
-        gid = torch.repeat_interleave(torch.arange(B, device=dev),
-                                      torch.as_tensor(ns, device=dev), output_size=int(n_off[-1]))
-        loc = torch.arange(int(n_off[-1]), device=dev) - torch.as_tensor(n_off[:-1], device=dev)[gid]
-        L[gid[ei_t[0]], loc[ei_t[0]], loc[ei_t[1]]] = w_t
-        pad = torch.arange(nmax, device=dev).unsqueeze(0) >= torch.as_tensor(ns, device=dev).unsqueeze(1)
-        L = L + torch.diag_embed(pad.to(L.dtype) * big)
+        loc = torch.arange(N, device=dev) - ns_d.cumsum(0).sub_(ns_d)[gid_d]
+        L[gid_d[ei_t[0]], loc[ei_t[0]], loc[ei_t[1]]] = w_t
+        pad = torch.arange(nmax, device=dev).unsqueeze(0) >= ns_d.unsqueeze(1)
+        L.diagonal(dim1=1, dim2=2).add_(pad.to(L.dtype) * big)
+        self._tick("device levels: L0 stack")
         vals, vecs = torch.linalg.eigh(L)  # ascending per graph
-        pe_all = vecs[:, :, 1:self.pe_k]  # [B, nmax, k-1]
-        pe = pe_all[gid, loc]  # [N, k-1]
-        # features on the device
-        x = torch.from_numpy(np.concatenate([self.x[i] for i in idx])).to(dev)
-        pos = torch.from_numpy(np.concatenate([self.pos[i] for i in idx])).to(dev)
-        attr = torch.from_numpy(np.concatenate(attrs)).to(dev)
+        self._tick("device levels: batched eigh")
+        pe = vecs[:, :, 1:self.pe_k][gid_d, loc]  # [N, k-1]
         src, dst = ei_d[0], ei_d[1]
-        node = torch.cat([x, pos, pe], 1)
-        edge = torch.cat([attr.view(-1, 1), (x[src] - x[dst]).abs(), (pe[src] + pe[dst]).abs()], 1)
-        c_node = torch.from_numpy(np.concatenate([c[0] for c in cmaps]).astype(np.float32)).to(dev)
-        c_edge = torch.from_numpy(np.concatenate([c[1] for c in cmaps])).to(dev)
-
-        def width(a, w):
-            if a.shape[1] < w:
-                a = torch.cat([a, a.new_zeros(a.shape[0], w - a.shape[1])], 1)
-            return a[:, :w].contiguous()
+        wt, ws = self.NODE_DIM + self.keig, self.EDGE_DIM + self.keig
+        k1 = pe.shape[1]
         lv0 = Batch()
         lv0.num_graphs = B
-        lv0.x_t = width(torch.cat([c_node.view(-1, 1), node], 1), self.NODE_DIM + self.keig)
-        lv0.x_s = width(torch.cat([c_edge.view(-1, 1), edge], 1), self.EDGE_DIM + self.keig)
+        # x_t = [cluster, x, pos, pe, 0...], x_s = [cluster, attr, |x_i - x_j|,
+        # |pe_i + pe_j|, 0...] written straight into their padded widths
+        xt = torch.zeros(N, wt, device=dev)
+        xt[:, 0] = c_node
+        xt[:, 1:4] = x
+        xt[:, 4:6] = pos
+        xt[:, 6:6 + k1] = pe[:, :wt - 6]
+        xs = torch.zeros(E, ws, device=dev)
+        xs[:, 0] = c_edge
+        xs[:, 1] = attr_d
+        xs[:, 2:5] = (x[src] - x[dst]).abs()
+        xs[:, 5:5 + k1] = (pe[src] + pe[dst]).abs()[:, :ws - 5]
+        lv0.x_t, lv0.x_s = xt, xs
         lv0.edge_index_t, lv0.edge_weight_t = ei_t, w_t
         lv0.edge_index_s, lv0.edge_weight_s = ei_s, w_s
         lv0.edge_index = ei_d
-        lv0.y = torch.cat([self.y[i] for i in idx]).to(dev)
-        lv0.num_node1 = torch.tensor(ns)
-        lv0.num_edge1 = torch.tensor(E_g)
-        lv0.num_nodes = int(n_off[-1])
-        # coarse level: the MLGC graphs, Laplacians on the device again
-        n1 = [int(c[3]) for c in cmaps]
-        o1 = np.concatenate([[0], np.cumsum(n1)])
-        ei1 = torch.from_numpy(np.ascontiguousarray(np.concatenate(
-            [c[2] + o for c, o in zip(cmaps, o1[:-1])], axis=1))).to(dev)
-        c_t, c_wt, c_s, c_ws, _ = ops.hodge_build(ei1, n1)
+        lv0.y = y_d
+        # per-graph counts on the device, as Batch.to leaves them (the step's
+        # forward reads them inside a capture)
+        lv0.num_node1, lv0.num_edge1 = ns_d, Eg_d
+        lv0.num_nodes = N
+        lv0._gid_t, lv0._gid_s = gid_d, gide_d
+        self._tick("device levels: features")
+        c_t, c_wt, c_s, c_ws, _ = ops.hodge_build(ei1_d, n1_d, sizes=(N1,) + nnz(ei1, N1))
+        self._tick("device levels: Hodge build (coarse)")
         lv1 = Batch()
         lv1.num_graphs = B
-        lv1.x_t = torch.ones(int(o1[-1]), 1, device=dev)
-        lv1.x_s = torch.ones(ei1.shape[1], 1, device=dev)
+        lv1.x_t = torch.ones(N1, 1, device=dev)
+        lv1.x_s = torch.ones(E1, 1, device=dev)
         lv1.edge_index_t, lv1.edge_weight_t = c_t, c_wt
         lv1.edge_index_s, lv1.edge_weight_s = c_s, c_ws
-        lv1.edge_index = ei1
-        lv1.num_node1 = torch.tensor(n1)
-        lv1.num_edge1 = torch.tensor([int(c[2].shape[1]) for c in cmaps])
-        lv1.num_nodes = int(o1[-1])
+        lv1.edge_index = ei1_d
+        lv1.num_node1, lv1.num_edge1 = n1_d, m1_d
+        lv1.num_nodes = N1
         for lv in (lv0, lv1):
             lv.hodge_sorted = {"edge_index_s": True, "edge_index_t": True}
             lv.l1_factor = False
@@ -291,7 +391,7 @@ class SuperpixelPipeline:
         # fl(fl(2 v) / lmax), v in {2, +-1}): the factored L1 holds by
         # construction -- declared where it pays (hodge_dataset.FACTOR_MIN_ROW)
         from .hodge_dataset import FACTOR_MIN_ROW
-        if ei_s.shape[1] >= FACTOR_MIN_ROW * max(ei_d.shape[1], 1):
+        if ei_s.shape[1] >= FACTOR_MIN_ROW * max(E, 1):
             ops.set_hodge_factor(lv0.edge_index_s, lv0.edge_index, lv0.num_nodes)
             lv0.l1_factor = True
         return lv0, lv1

@@ -370,9 +370,12 @@ int hlhgat_poly_basis_bwd_factored(int kind, const hlhgat_hodge_factor_t* f, int
  * PairData offsets) and its incidence CSR (hlhgat_incidence_csr).
  *
  * hlhgat_hodge_lmax: lmax of every graph's L0 = B1 B1^T (graph g = nodes
- * [node_ptr[g], node_ptr[g+1])), one workgroup per graph, fp64 Lanczos with
- * full re-orthogonalisation (`steps` <= 64 iterations, exact for graphs of
- * <= steps nodes) and Sturm bisection of the tridiagonal matrix.  The
+ * [node_ptr[g], node_ptr[g+1])), one wave per graph (vectors and the local
+ * adjacency in LDS when they fit in 48 KB), fp64 Lanczos by the three-term
+ * recurrence with local re-orthogonalisation (`steps` <= 64 iterations; the
+ * largest Ritz value converges first and loss of orthogonality only adds
+ * ghost copies) and Sturm bisection of the tridiagonal matrix.  Workspace:
+ * 3 n_nodes doubles (the vectors of graphs that miss the LDS).  The
  * reference's float32 eigh agrees to its own rounding (~1e-7 relative), so
  * entries built from this lmax may differ from the reference's by an ulp. */
 int64_t hlhgat_hodge_lmax_workspace_bytes(int64_t n_nodes, int steps);

@@ -205,3 +205,34 @@ def test_infer_step_replay_matches_eager_and_reference(cuda, name):
 
 def _call_out(out):
     return out[0] if isinstance(out, tuple) else out
+
+
+@pytest.mark.gpu
+def test_infer_step_padded_batch_equals_unpadded(cuda):
+    """Eval on a static-shape (padded) batch: the NodeEdgeInt value path runs
+    unfused in eval mode (BatchNorm on running statistics is row-wise, so the
+    padding rows change nothing); InferStep's replayed outputs on the padded
+    batch equal the eager eval forward on the unpadded one."""
+    import hlhgat
+    from hlhgat.hodge_dataset import pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_batch
+    from hlhgat.train import InferStep
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**CFG2)
+    m = m.to(cuda).train()
+    with torch.no_grad():  # move the running statistics off their initial values
+        for s in (1, 2):
+            m(zinc_like_batch(60, seed=s).to(cuda))
+    raw = zinc_like_batch(50, seed=7)
+    padded = pad_batch(raw, static_caps(raw, 512))
+    m.eval()
+    with torch.no_grad():
+        ref = m(zinc_like_batch(50, seed=7).to(cuda)).cpu()
+    m.train()
+    inf = InferStep(m)
+    pb = padded.to(cuda)
+    outs = [inf(pb).clone().cpu() for _ in range(3)]
+    assert inf.stats["replay"] == 2, inf.stats
+    for o in outs:
+        assert o.shape == ref.shape
+        close(o, ref.numpy(), 1e-5, "padded eval vs unpadded")

@@ -123,11 +123,15 @@ def test_mlgc_device_coarse_level_matches_reference(cuda, name):
 
 
 @pytest.mark.gpu
-def test_pipeline_device_batch_matches_host_batch(cuda):
+def test_pipeline_device_batch_matches_host_batch(cuda, monkeypatch):
     """A multi-sample batch (the three fixture samples, stored graclus orders)
     on the device equals the host restatement's batch: the collation offsets,
-    labels and per-graph counts exact, Laplacian weights within 1e-6."""
+    labels and per-graph counts exact, Laplacian weights within 1e-6.  The
+    host-side Hodge sizes the pipeline hands hodge_build are checked against
+    the device's row sizes (HLHGAT_CHECK_SIZES)."""
+    from hlhgat import ops
     from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    monkeypatch.setattr(ops, "_CHECK_SIZES", True)
     g = load_golden(G)
     raws = [superpixel_raw(int(g[f"s{i}/seed"]), n=int(g[f"s{i}/n"]), k=int(g[f"s{i}/k"]))
             for i in range(3)]
@@ -144,3 +148,68 @@ def test_pipeline_device_batch_matches_host_batch(cuda):
             close(getattr(d, key).cpu(), getattr(h, key), 1e-6, f"l{lv} {key}")
         assert h.x_t.shape == d.x_t.shape and h.x_s.shape == d.x_s.shape, lv
     assert host[0].y.tolist() == devb[0].y.cpu().tolist() == [1, 3, 7]
+
+
+@pytest.mark.gpu
+def test_pipeline_device_augmented_batch_sizes_and_features(cuda, monkeypatch):
+    """An augmented 64-graph batch (dropout_edge on, random graclus orders):
+    the host-computed Hodge sizes equal the device's, every device tensor is
+    consistent with the host restatement of the SAME draw (same seed -> same
+    masks, orders and signs): indices and counts exact, weights within 1e-6,
+    non-PE feature columns exact."""
+    from hlhgat import ops
+    from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    monkeypatch.setattr(ops, "_CHECK_SIZES", True)
+    raws = [superpixel_raw(900 + i) for i in range(64)]
+    p = SuperpixelPipeline(raws, keig=11, aug=True)
+    idx = list(range(63, -1, -2)) + list(range(0, 64, 2))
+    host = p.batch(idx, seed=5, device="cpu")
+    devb = p.batch(idx, seed=5, device=cuda)
+    assert host[0].edge_index.shape[1] < int(p.m[idx].sum())  # dropout ran
+    for lv, (h, d) in enumerate(zip(host, devb)):
+        for key in ("edge_index", "edge_index_t", "edge_index_s", "num_node1", "num_edge1"):
+            assert np.array_equal(getattr(h, key).numpy(), getattr(d, key).cpu().numpy()), (lv, key)
+        for key in ("edge_weight_t", "edge_weight_s"):
+            close(getattr(d, key).cpu(), getattr(h, key), 1e-6, f"l{lv} {key}")
+    assert torch.equal(host[0].y, devb[0].y.cpu())
+    for key, nf in (("x_t", N_FIXED_T), ("x_s", N_FIXED_S)):
+        hv, dv = getattr(host[0], key), getattr(devb[0], key).cpu()
+        assert hv.shape == dv.shape, key
+        assert torch.equal(hv[:, :nf], dv[:, :nf]), key
+    assert torch.equal(host[1].x_t, devb[1].x_t.cpu()) and torch.equal(host[1].x_s, devb[1].x_s.cpu())
+
+
+@pytest.mark.gpu
+def test_lanczos_lmax_matches_fp64_eigh_on_superpixel_batch(cuda):
+    """hlhgat_hodge_lmax (three-term Lanczos, local re-orthogonalisation) on
+    256 augmented superpixel graphs and their MLGC coarse graphs: every
+    lambda_max within 1e-7 relative of numpy's fp64 eigvalsh of the dense L0
+    (the reference takes float32 torch.linalg.eigh, good to ~1e-7)."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import mlgc_batch_flat
+    from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    raws = [superpixel_raw(2000 + i, n=60 + (i % 7) * 15) for i in range(256)]
+    p = SuperpixelPipeline(raws, keig=11, aug=True)
+    rng = np.random.default_rng(3)
+    ns, ei, _, E_g, gid_e, perm = p._select(np.arange(256), rng)
+    mg = mlgc_batch_flat(ei, E_g, ns, perm)
+    e_off = np.concatenate([[0], np.cumsum(E_g)])
+    levels = [(ei, E_g, ns), (np.concatenate([mg.ce[:, e_off[b]:e_off[b] + mg.cm[b]]
+                                              for b in range(256)], 1), mg.cm, mg.cn)]
+    for lv, (e, m, n) in enumerate(levels):
+        n_off = np.concatenate([[0], np.cumsum(n)])
+        eb = e + n_off[np.repeat(np.arange(len(n)), m)]
+        *_, lam = ops.hodge_build(torch.from_numpy(eb).to(cuda), list(n))
+        ref = []
+        eo = np.concatenate([[0], np.cumsum(m)])
+        for b in range(len(n)):
+            L = np.zeros((n[b], n[b]))
+            ee = e[:, eo[b]:eo[b + 1]]
+            np.add.at(L, (ee[0], ee[1]), -1.0)
+            np.add.at(L, (ee[1], ee[0]), -1.0)
+            L[np.diag_indices(n[b])] = -L.sum(1)
+            ref.append(np.linalg.eigvalsh(L)[-1])
+        got = lam.double().cpu().numpy()
+        # lam is float32 of the fp64 Lanczos value: compare at float32 resolution
+        rel = np.abs(got - np.asarray(ref)) / np.asarray(ref)
+        assert rel.max() <= 1e-7, (lv, rel.max(), int(rel.argmax()))

@@ -1,27 +1,15 @@
 #!/bin/bash
-# k_poly_step in the replayed step (kernel trace kept for the overlap
-# analysis), L2 hit rates in the step vs isolated (PMC, dispatch-serialised),
-# and the per-node cost of the replay (tools/probes/packet_cost.py)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+mkdir -p gpurun_out/r04_c_pipe2
 export TMPDIR=/tmp
-rm -rf gpurun_out/pc_0
-timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/pc_0 -o run --output-format csv -- python3 tools/probes/poly_context.py > gpurun_out/pc_0.log 2>&1
-rc=$?; echo "=== trace rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/pc_0.log; exit 1; }
-T=$(find gpurun_out/pc_0 -name '*kernel_trace.csv' | head -1)
-cp "$T" gpurun_out/r04_a_trace.csv
-rm -rf gpurun_out/pmc_step gpurun_out/pmc_iso
-timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum -d gpurun_out/pmc_step -o p --output-format csv -- python3 tools/probes/poly_context.py --steps 3 > gpurun_out/pmc_step.log 2>&1
-echo "=== pmc step rc=$?"
-timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum -d gpurun_out/pmc_iso -o p --output-format csv -- python3 tools/kbench.py --only poly --reps 5 --chain 5 > gpurun_out/pmc_iso.log 2>&1
-echo "=== pmc iso rc=$?"
-for d in step iso; do
-  C=$(find gpurun_out/pmc_$d -name '*counter_collection.csv' | head -1)
-  python3 tools/pmc_kernel.py "$C" --match k_poly_step > gpurun_out/r04_a_pmc_poly_$d.txt 2>&1
-  echo "--- $d"; head -12 gpurun_out/r04_a_pmc_poly_$d.txt
-done
-rm -rf gpurun_out/pmc_step gpurun_out/pmc_iso gpurun_out/pc_0
-timeout -k 10 300 python3 tools/probes/packet_cost.py > gpurun_out/r04_a_packet_cost.log 2>&1
-echo "=== packet cost rc=$?"; grep -v amdgpu.ids gpurun_out/r04_a_packet_cost.log | tail -1
+export DEBUG_HIP_FORCE_GRAPH_QUEUES=2
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_pipeline.py tests/test_gpu_parity.py -k "pipeline or lanczos or hodge_builder or mlgc" > gpurun_out/r04_c_pipe_tests.log 2>&1
+rc=$?; echo "=== tests rc=$rc"; tail -3 gpurun_out/r04_c_pipe_tests.log; [ $rc = 0 ] || exit 1
+timeout -k 10 300 python tools/probes/pipeline_stages.py --batches 4 > gpurun_out/r04_c_pipe.log 2>&1
+echo "=== stages rc=$?"; tail -1 gpurun_out/r04_c_pipe.log
+timeout -k 10 300 python tools/probes/cfg3_pipe.py > gpurun_out/r04_c_cfg3.log 2>&1
+echo "=== cfg3 rc=$?"; tail -1 gpurun_out/r04_c_cfg3.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_c_pipe2 -o run -- python tools/probes/pipeline_stages.py --batches 4 > gpurun_out/r04_c_pipe_prof.log 2>&1
+echo "=== prof rc=$?"
 exit 0
