@@ -19,6 +19,7 @@
 //     tail-to-head: -1}.
 // Row sizes (prefix sums) come from the incidence CSR; no sort, no atomics.
 #include "common.h"
+#include "tridiag.h"
 
 using namespace hlhgat;
 
@@ -44,19 +45,6 @@ __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
-}
-
-// number of eigenvalues of the symmetric tridiagonal (al, be) below x
-__device__ int sturm_count(const double* al, const double* be, int k, double x) {
-  int c = 0;
-  double d = 1.0;
-  for (int i = 0; i < k; ++i) {
-    const double b2 = i ? be[i] * be[i] : 0.0;
-    d = (al[i] - x) - (i ? b2 / d : 0.0);
-    if (d == 0.0) d = -1e-300;
-    if (d < 0.0) ++c;
-  }
-  return c;
 }
 
 // Lanczos on one graph's L0 (n nodes, local ids; apply(x, y): y = L0 x) by
@@ -193,24 +181,10 @@ __global__ __launch_bounds__(kLzThreads) void k_lanczos_lmax(LanczosArgs a) {
   }
   // Gershgorin bounds, then multisection for the largest eigenvalue: the 64
   // lanes count the Sturm sequence at 64 interior points of [lo, hi] at once
-  // (the interval shrinks 65-fold per pass; bisection by one lane cost ~0.4 ms
-  // of serial fp64 divides per launch)
-  double lo = 0.0, hi = 0.0;
-  for (int i = 0; i < k; ++i) {
-    const double r = (i ? fabs(be[i]) : 0.0) + (i + 1 < k ? fabs(be[i + 1]) : 0.0);
-    lo = fmin(lo, al[i] - r);
-    hi = fmax(hi, al[i] + r);
-  }
-  for (int it = 0; it < 40 && k > 0 && hi - lo > 1e-15 * fmax(1.0, fabs(hi)); ++it) {
-    const double h = (hi - lo) / (double)(kLzThreads + 1);
-    const bool above = sturm_count(al, be, k, lo + h * (double)(lane + 1)) < k;
-    const unsigned long long mask = __ballot(above);  // lanes 0 .. t: an eigenvalue above
-    const int t = mask ? 63 - __clzll(mask) : -1;
-    const double nlo = t >= 0 ? lo + h * (double)(t + 1) : lo;
-    const double nhi = t < kLzThreads - 1 ? lo + h * (double)(t + 2) : hi;
-    lo = nlo;
-    hi = nhi;
-  }
+  // (bisection by one lane cost ~0.4 ms of serial fp64 divides per launch)
+  double lo, hi;
+  gershgorin(al, be, k, lo, hi);
+  if (k > 0) hi = wave_eigenvalue(al, be, k, k - 1, lo, hi, 1e-15 * fmax(1.0, fabs(hi)));
   if (lane == 0) a.lmax[g] = n > 0 ? hi : 0.0;
 }
 

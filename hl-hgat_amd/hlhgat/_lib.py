@@ -64,6 +64,9 @@ SIGNATURES = {
     "hlhgat_hodge_lmax_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "hlhgat_hodge_lmax": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp,
                                   c_i64, c_vp]),
+    "hlhgat_eig_pe_workspace_bytes": (c_i64, [c_i64, c_i64, c_i32]),
+    "hlhgat_eig_pe": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp,
+                              c_i64, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_hodge_row_sizes": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "hlhgat_hodge_build": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                    c_vp, c_vp, c_vp]),

@@ -517,6 +517,17 @@ def pad_levels(datas: Sequence["Batch"], caps: Sequence[Dict[str, int]]) -> List
     return out
 
 
+def _h2d(a: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """A host array on dev without blocking the host: staged through pinned
+    memory and copied asynchronously on the current stream (a pageable copy
+    would wait for the stream's queued kernels -- on a loader thread, for its
+    own device work of the batch)."""
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if torch.device(dev).type != "cuda":
+        return t
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     """Static-shape copy of a collated host batch (hlhgat.train replays one
     hipGraph for every batch of the same caps).
@@ -557,7 +568,7 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
         if extra < 0:
             raise ValueError(f"pad_batch: {ei.size(1)} Laplacian entries exceed the cap {Z}")
         per_row = _spread(extra, R - n)
-        rows = torch.from_numpy(np.repeat(np.arange(n, R), per_row)).to(ei.device, ei.dtype)
+        rows = _h2d(np.repeat(np.arange(n, R), per_row).astype(np.int64), ei.device).to(ei.dtype)
         return (torch.cat([ei, torch.stack([rows, rows])], 1),
                 torch.cat([w, w.new_zeros(extra)]), per_row)
 
@@ -576,8 +587,8 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     if getattr(b, "csr_rowptr_t", None) is not None or getattr(b, "csr_rowptr_s", None) is not None:
         _attach_csr(out)  # the padded COO (zero-weight self-loops on padding rows)
     if getattr(b, "edge_index", None) is not None:
-        nodes = torch.from_numpy(nt + np.arange(Rs - ns) % (Rt - nt)).to(b.edge_index.device,
-                                                                          b.edge_index.dtype)
+        nodes = _h2d((nt + np.arange(Rs - ns) % (Rt - nt)).astype(np.int64),
+                     b.edge_index.device).to(b.edge_index.dtype)
         out.edge_index = torch.cat([b.edge_index, torch.stack([nodes, nodes])], 1)
         if getattr(b, "inc_rowptr", None) is not None:
             out.inc_rowptr, out.inc_eids = incidence_csr(out.edge_index, Rt)
@@ -588,7 +599,7 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
         if o is not None:
             setattr(out, "row_order_" + side,
                     torch.cat([o, torch.arange(n, R, dtype=o.dtype, device=o.device)]))
-        setattr(out, "n_valid_" + side, torch.tensor([n], dtype=torch.int32, device=dev))
+        setattr(out, "n_valid_" + side, torch.full((1,), n, dtype=torch.int32, device=dev))
     out.valid_mask_t = torch.arange(Rt, device=dev) < nt
     out.num_nodes = Rt
     if dev.type == "cuda":

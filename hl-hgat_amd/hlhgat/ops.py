@@ -510,6 +510,50 @@ def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tens
     return ei_t, w_t, ei_s, w_s, lam
 
 
+def eig_pe(edge_index: torch.Tensor, node_counts, k: int, max_nodes: Optional[int] = None,
+           n_nodes: Optional[int] = None):
+    """Eigenvector PE of every graph of a block-diagonal batch and its
+    lambda_max, on the device in one launch (hlhgat_eig_pe; the reference's
+    per-sample eig_pe(L0) and eigh(L0).max(), lib/Hodge_Dataset.py:97-112,
+    :782): edge_index int64 [2, E] (i < j, PairData offsets), node_counts per
+    graph (a host sequence, or a device tensor with max_nodes given; n_nodes,
+    their sum, spares a device read).
+    Returns (pe float32 [N, k - 1]: eigenvectors 1 .. k-1 of each graph's L0,
+    ascending, zero columns past a graph's own size; lmax float64 [B])."""
+    _req_dev(edge_index, "edge_index", torch.int64)
+    dev = edge_index.device
+    if torch.is_tensor(node_counts) and node_counts.is_cuda:
+        if max_nodes is None:
+            raise ValueError("eig_pe: max_nodes is required with device node counts")
+        counts = node_counts.to(torch.int64)
+        N = None if n_nodes is None else int(n_nodes)
+    else:
+        host = [int(c) for c in node_counts]
+        mx = max(host) if host else 0
+        if max_nodes is not None and int(max_nodes) < mx:
+            raise ValueError(f"eig_pe: max_nodes {max_nodes} < largest graph {mx}")
+        max_nodes = mx if max_nodes is None else int(max_nodes)
+        counts = torch.tensor(host, dtype=torch.int64).to(dev)
+        N = sum(host)
+    B = counts.numel()
+    node_ptr = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+    node_ptr[1:] = torch.cumsum(counts, 0)
+    if N is None:
+        N = int(node_ptr[-1].item())
+    ei = edge_index.contiguous()
+    E = ei.size(1)
+    inc = incidence(ei, N)
+    pe = torch.empty(N, k - 1, dtype=torch.float32, device=dev)
+    lmax = torch.empty(B, dtype=torch.float64, device=dev)
+    wsb = int(LIB.hlhgat_eig_pe_workspace_bytes(B, int(max_nodes), k))
+    ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=dev)
+    check(LIB.hlhgat_eig_pe(inc.rowptr.data_ptr(), inc.edge_ids.data_ptr() if E else None,
+                            ei.data_ptr() if E else None, E, N, node_ptr.data_ptr(), B,
+                            int(max_nodes), k, pe.data_ptr(), k - 1, lmax.data_ptr(), ws.data_ptr(),
+                            wsb, _stream(ei)), "eig_pe")
+    return pe, lmax
+
+
 def copy_words_batched(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
     """dst.copy_(src) for contiguous same-size tensors whose byte size is a
     multiple of 4, up to HLHGAT_MAX_COPY_BLOCKS per launch

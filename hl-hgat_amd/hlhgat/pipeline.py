@@ -18,11 +18,13 @@ SuperpixelPipeline does the same for a whole batch of graphs at once:
     at construction: they do not change between epochs), the dropout masks,
     graclus + the MLGC map (native, hlhgat_graclus / hlhgat_mlgc_map), the
     offsets of the block-diagonal batch;
-  device: both levels' Hodge Laplacians and lambda_max for every graph in
-    two launches each (hlhgat_hodge_lmax: fp64 Lanczos, one workgroup per
-    graph; hlhgat_hodge_build: the L0 / L1 rows in the reference's
-    dense_to_sparse order), the eigenvector PE as ONE batched dense eigh of
-    the block-padded L0 stack (rocSOLVER through torch.linalg.eigh), the
+  device: the eigenvector PE and lambda_max of every level-0 graph in ONE
+    launch (hlhgat_eig_pe: per graph, fp64 Lanczos with full
+    re-orthogonalisation, Sturm multisection, inverse iteration; it replaced
+    a batched rocSOLVER eigh of the block-padded L0 stack, 3.9 ms and a host
+    sync per 256 graphs), the coarse level's lambda_max (hlhgat_hodge_lmax),
+    both levels' Hodge Laplacians (hlhgat_hodge_build: the L0 / L1 rows in
+    the reference's dense_to_sparse order, sizes known on the host), the
     feature concatenations, the sign flips;
 
 and returns the two level batches on the device, collated, marked sorted /
@@ -33,8 +35,8 @@ arithmetic (dense eigh lambda_max, hodge_laplacians) -- the restatement the
 golden test pins (tests/golden/make_golden_pipeline.py).
 
 Parity: structure, features, cluster maps and coarse graphs are exact;
-lambda_max (Lanczos vs eigh) within 1e-6 relative, so the Laplacian entries
-are; PE columns equal the reference's up to sign (the reference flips them at
+lambda_max (fp64 Lanczos vs float32 eigh) within 1e-6 relative, so the
+Laplacian entries are; PE columns equal the reference's up to sign (the reference flips them at
 random, and an eigenvector's sign is arbitrary), checked where the
 eigenvalue is separated from its neighbours.
 """
@@ -45,8 +47,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
-from .hodge_dataset import (Batch, PairData, collate, dense_to_sparse, graclus, hodge_laplacians,
-                            mlgc_batch, mlgc_batch_flat, mlgc_map)
+from .hodge_dataset import (Batch, PairData, _h2d, collate, dense_to_sparse, graclus,
+                            hodge_laplacians, mlgc_batch, mlgc_batch_flat, mlgc_map)
 
 __all__ = ["SuperpixelPipeline", "to_undirected_min", "superpixel_raw"]
 
@@ -206,7 +208,7 @@ class SuperpixelPipeline:
         B = len(idx)
         sg = np.concatenate([self._pe_signs(rng, B, lv0.x_t.shape[1]),
                              self._pe_signs(rng, B, lv0.x_s.shape[1])], 1)
-        sg = torch.from_numpy(sg).to(lv0.x_t.device, non_blocking=True)
+        sg = _h2d(sg, lv0.x_t.device)
         wt = lv0.x_t.shape[1]
         lv0.x_t.mul_(sg[:, :wt].index_select(0, lv0._gid_t))
         lv0.x_s.mul_(sg[:, wt:].index_select(0, lv0._gid_s))
@@ -285,8 +287,9 @@ class SuperpixelPipeline:
         return lv0, collate(f1, check_hodge=False)
 
     def _levels_device(self, idx, ei, attr, ns, E_g, gid_e, mg, dev):
-        """Both levels on the device.  The host arrays travel in two uploads
-        (one int64, one float32; the device tensors are views of them); the Hodge builder gets its sizes from the host (the nnz of L0
+        """Both levels on the device.  The host arrays travel in two
+        asynchronous uploads from pinned memory (one int64, one float32; the
+        device tensors are views of them); the Hodge builder gets its sizes from the host (the nnz of L0
         and L1 follow from the degrees), so nothing here waits on the device
         but the eigh's own error check."""
         from . import ops
@@ -313,8 +316,8 @@ class SuperpixelPipeline:
                 self.y_all.numpy()[idx].astype(np.int64), gid_n, gid_e]
         flts = [self.x_all[nodes].reshape(-1), self.pos_all[nodes].reshape(-1), attr,
                 mg.c_node.astype(np.float32), mg.c_edge]
-        idev = torch.from_numpy(np.concatenate(ints)).to(dev)
-        fdev = torch.from_numpy(np.concatenate(flts)).to(dev)
+        idev = _h2d(np.concatenate(ints), dev)
+        fdev = _h2d(np.concatenate(flts), dev)
 
         def cut(t, sizes):
             out, o = [], 0
@@ -328,22 +331,14 @@ class SuperpixelPipeline:
         x, pos, attr_d, c_node, c_edge = cut(fdev, [a.size for a in flts])
         x, pos = x.view(N, 3), pos.view(N, 2)
         self._tick("device levels: edge upload")
-        ei_t, w_t, ei_s, w_s, lam = ops.hodge_build(ei_d, ns_d, sizes=(N,) + nnz(ei_b, N))
+        # eig_pe and lambda_max of every graph in one launch (hlhgat_eig_pe:
+        # fp64 Lanczos with full re-orthogonalisation per graph), then the
+        # Hodge Laplacians with that lambda_max
+        pe, lam64 = ops.eig_pe(ei_d, ns_d, self.pe_k, max_nodes=int(ns.max()), n_nodes=N)
+        self._tick("device levels: eig_pe + lambda_max")
+        ei_t, w_t, ei_s, w_s, lam = ops.hodge_build(ei_d, ns_d, lmax=lam64.to(torch.float32),
+                                                    sizes=(N,) + nnz(ei_b, N))
         self._tick("device levels: Hodge build (fine)")
-        # eig_pe on the device: ONE batched eigh of the block-padded L0 stack
-        # (padding rows / columns carry a diagonal above every real eigenvalue,
-        # so each graph's smallest eigenpairs are its own, with zero padding)
-        nmax = int(ns.max())
-        big = 10.0  # > lambda(L0) <= 2 after the 2 / lmax scaling
-        L = torch.zeros(B, nmax, nmax, device=dev)
-        loc = torch.arange(N, device=dev) - ns_d.cumsum(0).sub_(ns_d)[gid_d]
-        L[gid_d[ei_t[0]], loc[ei_t[0]], loc[ei_t[1]]] = w_t
-        pad = torch.arange(nmax, device=dev).unsqueeze(0) >= ns_d.unsqueeze(1)
-        L.diagonal(dim1=1, dim2=2).add_(pad.to(L.dtype) * big)
-        self._tick("device levels: L0 stack")
-        vals, vecs = torch.linalg.eigh(L)  # ascending per graph
-        self._tick("device levels: batched eigh")
-        pe = vecs[:, :, 1:self.pe_k][gid_d, loc]  # [N, k-1]
         src, dst = ei_d[0], ei_d[1]
         wt, ws = self.NODE_DIM + self.keig, self.EDGE_DIM + self.keig
         k1 = pe.shape[1]

@@ -32,7 +32,7 @@ import torch.distributed as dist
 from . import ops
 from .distributed import collectives_on
 
-__all__ = ["TrainStep", "InferStep", "batch_key", "forward_collectives"]
+__all__ = ["Staged", "TrainStep", "InferStep", "batch_key", "forward_collectives"]
 
 # HIP_ADAM = False: torch's fused Adam instead of hlhgat_adam_flat
 HIP_ADAM = True
@@ -98,6 +98,13 @@ class _Captured:
         self.graph = graph
         self.batch = static_batch
         self.loss = loss
+        self.slots = [self]  # TrainStep.stage: the graphs of this shape, used in turn
+        self.free = None     # event after this graph's last replay (its buffers reusable)
+
+    def released(self, stream):
+        if self.free is None:
+            self.free = torch.cuda.Event()
+        self.free.record(stream)
 
     def load(self, batch):
         """Copy a batch into the graph's static buffers: every contiguous
@@ -118,6 +125,19 @@ class _Captured:
                 dst.copy_(v, non_blocking=True)
         if pend:
             ops.copy_words_batched([p[0] for p in pend], [p[1] for p in pend])
+
+
+STAGE_SLOTS = 2  # captured graphs per batch shape that TrainStep.stage fills in turn
+
+
+class Staged:
+    """A batch uploaded for a coming step by TrainStep.stage: either already
+    in the static buffers of the captured graph `slot`, or in fresh device
+    tensors (`batch`); `event` marks the end of the upload."""
+    __slots__ = ("batch", "event", "slot", "key")
+
+    def __init__(self, batch, event, slot, key):
+        self.batch, self.event, self.slot, self.key = batch, event, slot, key
 
 
 class TrainStep:
@@ -298,9 +318,15 @@ class TrainStep:
         self.stats["eager"] += 1
         return loss
 
-    def _capture(self, batch, key) -> _Captured:
-        static = ([_clone_batch(b) for b in batch] if isinstance(batch, (list, tuple))
-                  else _clone_batch(batch))
+    def _capture(self, batch, key, slot_of: Optional[_Captured] = None) -> _Captured:
+        if slot_of is not None:  # a staged device batch becomes the new slot's buffers
+            static = batch
+            for b in _parts(static):
+                if hasattr(b, "_mark"):
+                    b._mark()
+        else:
+            static = ([_clone_batch(b) for b in batch] if isinstance(batch, (list, tuple))
+                      else _clone_batch(batch))
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph(keep_graph=KEEP_GRAPHS)
@@ -335,18 +361,99 @@ class TrainStep:
         torch.cuda.current_stream(self.device).wait_stream(s)
         if KEEP_GRAPHS:
             g.instantiate()
+        ent = _Captured(g, static, loss)
+        self.stats["captures"] += 1
+        if slot_of is not None:
+            slot_of.slots.append(ent)
+            return ent
         if len(self._graphs) >= self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
-        ent = _Captured(g, static, loss)
         self._graphs[key] = ent
-        self.stats["captures"] += 1
         return ent
+
+    def stage(self, batch, stream: Optional["torch.cuda.Stream"] = None) -> Staged:
+        """Upload a host batch (pinned CPU tensors, e.g. hlhgat.loader.
+        GraphLoader's) for a coming step, on `stream` (default: a copy stream
+        of this TrainStep), and return the handle to pass to step(...).  Once
+        the batch shape has STAGE_SLOTS captured graphs, the tensors go
+        straight into the static buffers of the graph that replays next, after
+        its previous replay has released them (double buffering): the step
+        then replays with no copy-in at all.  Until then (first steps of a
+        shape) the batch goes to fresh device tensors, which the step adopts
+        as the next graph's static buffers."""
+        if not self.graphs:
+            raise RuntimeError("TrainStep.stage needs graphs=True (a ROCm device)")
+        if stream is None:
+            if getattr(self, "_copy_stream", None) is None:
+                self._copy_stream = torch.cuda.Stream(device=self.device)
+            stream = self._copy_stream
+        key = batch_key(batch)
+        ent = self._graphs.get(key)
+        main = torch.cuda.current_stream(self.device)
+        ev = torch.cuda.Event()
+        if ent is None or len(ent.slots) < STAGE_SLOTS:
+            with torch.cuda.stream(stream):
+                dev = [self._upload(b) for b in _parts(batch)]
+                if not isinstance(batch, (list, tuple)):
+                    dev = dev[0]
+                ev.record(stream)
+            for b in _parts(dev):
+                for _, v in _tensor_items(b):
+                    v.record_stream(main)
+            return Staged(dev, ev, None, key)
+        k = getattr(ent, "next_slot", 0)
+        ent.next_slot = (k + 1) % len(ent.slots)
+        slot = ent.slots[k]
+        if slot.free is not None:
+            stream.wait_event(slot.free)
+        with torch.cuda.stream(stream):
+            for b, sb in zip(_parts(batch), _parts(slot.batch)):
+                for name, v in _tensor_items(b):
+                    getattr(sb, name).copy_(v, non_blocking=True)
+            ev.record(stream)
+        return Staged(None, ev, slot, key)
+
+    def _upload(self, b):
+        """A device copy of batch object b that shares no storage with it
+        (it may become a graph's static buffers, which later uploads
+        overwrite)."""
+        out = type(b).__new__(type(b))
+        for k, v in vars(b).items():
+            if torch.is_tensor(v):
+                d = v.to(self.device, non_blocking=True)
+                setattr(out, k, d.clone() if d.data_ptr() == v.data_ptr() else d)
+            else:
+                setattr(out, k, v)
+        if hasattr(out, "_mark"):
+            out._mark()
+        return out
+
+    def _replay(self, ent: _Captured) -> torch.Tensor:
+        ent.graph.replay()
+        ent.released(torch.cuda.current_stream(self.device))
+        if self._exchange and not self._exchange_in_graph:
+            self._exchange_and_update()
+        self.stats["replay"] += 1
+        return ent.loss
+
+    def _call_staged(self, st: Staged) -> torch.Tensor:
+        torch.cuda.current_stream(self.device).wait_event(st.event)
+        if st.slot is not None:
+            return self._replay(st.slot)
+        ent = self._graphs.get(st.key)
+        if ent is None or len(ent.slots) >= STAGE_SLOTS:
+            return self(st.batch)
+        # one more slot for this shape: the staged tensors are its static
+        # buffers; capturing does not run the step, the first replay does
+        return self._replay(self._capture(st.batch, st.key, slot_of=ent))
 
     def __call__(self, batch) -> torch.Tensor:
         # a kernel of an earlier step that reported unusable results (the
         # device error word, read without synchronising) stops training here
         if self._ext is not None:
             ops.check_device_errors(sync=False)
+        if isinstance(batch, Staged):
+            return self._call_staged(batch)
         if not self.graphs:
             return self._eager(batch)
         key = batch_key(batch)
@@ -356,11 +463,7 @@ class TrainStep:
             self._capture(batch, key)
             return loss
         ent.load(batch)
-        ent.graph.replay()
-        if self._exchange and not self._exchange_in_graph:
-            self._exchange_and_update()
-        self.stats["replay"] += 1
-        return ent.loss
+        return self._replay(ent)
 
     def state_dict(self):
         return {"model": self.model.state_dict(), "opt": self.opt.state_dict()}

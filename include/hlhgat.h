@@ -383,6 +383,26 @@ int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_edge,
                       const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
                       const int64_t* node_ptr, int64_t n_graphs, int steps, double* lmax,
                       void* workspace, int64_t workspace_bytes, void* stream);
+/* hlhgat_eig_pe: the eigenvector positional encodings of every graph of the
+ * batch and its lambda_max in ONE launch, replacing the reference's per-sample
+ * dense eighs (eig_pe, lib/Hodge_Dataset.py:97-112, called at
+ * main_cifar10SP_HL_HGCNN_dense_int3_attpool.py:86-91 on L0 = 2 B1 B1^T / lmax,
+ * and torch.linalg.eigh(L0).max(), lib/Hodge_Dataset.py:782).  Per graph, one
+ * workgroup, fp64: Lanczos with full re-orthogonalisation (restarted when an
+ * invariant subspace closes), eigenvalues of the tridiagonal matrix by Sturm
+ * multisection, its eigenvectors by inverse iteration, pe = Q y.  Output:
+ * pe[v][0 .. k-2] (float32, row stride ldpe) = eigenvectors 1 .. k-1 of the
+ * unscaled L0 = B1 B1^T (ascending eigenvalues; the same vectors as the
+ * scaled L0's), zero columns where the graph has fewer than k nodes;
+ * lmax[g] = the largest eigenvalue of the unscaled L0 (fp64).  Eigenvectors
+ * are defined up to sign (and rotation within equal eigenvalues).
+ * max_nodes >= every graph's node count (sizes the workspace slice a graph
+ * too large for the LDS uses); 2 <= k <= 64. */
+int64_t hlhgat_eig_pe_workspace_bytes(int64_t n_graphs, int64_t max_nodes, int k);
+int hlhgat_eig_pe(const int32_t* inc_rowptr, const int32_t* inc_edge, const int64_t* edge_index,
+                  int64_t n_edges, int64_t n_nodes, const int64_t* node_ptr, int64_t n_graphs,
+                  int64_t max_nodes, int k, float* pe, int64_t ldpe, double* lmax,
+                  void* workspace, int64_t workspace_bytes, void* stream);
 /* Row sizes of L0 (deg(v) + 1, 0 for an isolated node) and L1 (deg(i) +
  * deg(j) - 1); exclusive-scan them into the row pointers. */
 int hlhgat_hodge_row_sizes(const int32_t* inc_rowptr, const int64_t* edge_index,

@@ -11,8 +11,9 @@ value.
 
 * CPU (the restatement, device="cpu": the reference's arithmetic): every
   index array, weight and non-PE column bitwise; PE columns |.| bitwise.
-* GPU (device path: Lanczos lambda_max, device Hodge builder, batched
-  rocSOLVER eigh): indices and the cluster maps exact; Laplacian weights and
+* GPU (device path: hlhgat_eig_pe for the PE and level-0 lambda_max, Lanczos
+  lambda_max for the coarse level, device Hodge builder): indices and the
+  cluster maps exact; Laplacian weights and
   the coarse level within 1e-6 relative (lambda_max by Lanczos, not eigh);
   non-PE columns exact; PE columns |.| within 1e-4 where the eigenvalue is
   separated from its neighbours by > 1e-3 (an eigenvector is defined up to

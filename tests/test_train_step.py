@@ -668,3 +668,51 @@ def test_padded_levels_share_one_graph(cuda, kind):
     assert l_e == l_g
     for k in sd_e:
         assert torch.equal(sd_e[k], sd_g[k]), k
+
+
+@pytest.mark.gpu
+def test_staged_double_buffered_steps_bitwise(cuda):
+    """TrainStep.stage (the loader-fed path: host batches uploaded on a copy
+    stream straight into the static buffers of the graph that replays next,
+    two captured graphs per shape used in turn, the next batch staged while
+    the current step runs) gives the bits of step(device batch): losses and
+    every parameter / running statistic, two shapes interleaved."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.synthetic import zinc_like_batch
+    from hlhgat.train import Staged, TrainStep
+    import copy
+    b2 = copy.copy(zinc_like_batch(40, seed=3))  # the shape of [0], other values
+    g = torch.Generator().manual_seed(11)
+    b2.x_t = b2.x_t + 0.25 * torch.randn(b2.x_t.shape, generator=g)
+    b2.x_s = b2.x_s + 0.25 * torch.randn(b2.x_s.shape, generator=g)
+    b2.y = b2.y + 0.5
+    host = [zinc_like_batch(40, seed=3), zinc_like_batch(33, seed=4), b2]
+    order = [0, 1, 0, 2, 1, 0, 2, 1, 1, 0, 2]
+    l_ref, sd_ref, _ = _run(True, True, [copy.copy(b).to(cuda) for b in host], order)
+    assert all(not b.x_t.is_cuda for b in host)  # Batch.to works in place: copies went
+    ops.set_stream_fork(True)
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
+    crit = torch.nn.L1Loss()
+    step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                     weight_decay=1e-3, graphs=True)
+    cs = torch.cuda.Stream(device=cuda)
+    losses = []
+    nxt = step.stage(host[order[0]], cs)
+    slots_used = 0
+    for k in range(len(order)):
+        cur = nxt
+        if k + 1 < len(order):
+            nxt = step.stage(host[order[k + 1]], cs)
+        assert isinstance(cur, Staged)
+        slots_used += cur.slot is not None
+        losses.append(float(step(cur)))
+    torch.cuda.synchronize()
+    _check_errors()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    assert losses == l_ref, (losses, l_ref)
+    for key in sd_ref:
+        assert torch.equal(sd_ref[key], sd[key]), key
+    # two shapes x two slots captured; later steps went straight into a slot
+    assert step.stats["captures"] == 4 and slots_used >= 5, (step.stats, slots_used)

@@ -36,13 +36,28 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tp = 0.0
+    pads = []
     for b in range(B):
         d = pipe.batch(range(b * G, (b + 1) * G), seed=b, device=dev)
+        torch.cuda.synchronize()
         t1 = time.perf_counter()
         pad_levels(d, caps)
         torch.cuda.synchronize()
-        tp += time.perf_counter() - t1
+        t2 = time.perf_counter()
+        pad_levels(d, caps)
+        torch.cuda.synchronize()
+        pads.append((round((t2 - t1) * 1e3, 2), round((time.perf_counter() - t2) * 1e3, 2)))
+        tp += t2 - t1
+    print("pad_levels ms (first, again) per batch:", pads, flush=True)
     tot = (time.perf_counter() - t0) / B * 1e3
+    # where pad_levels spends its host time (torch.profiler, CPU ops)
+    from torch.profiler import ProfilerActivity, profile
+    d = pipe.batch(range(0, G), seed=0, device=dev)
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU]) as prof:
+        pad_levels(d, caps)
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=12), flush=True)
     st = {k: round(v / B, 2) for k, v in pipe.stage_ms.items()}
     st["pad_levels"] = round(tp / B * 1e3, 2)
     print(json.dumps({"ms_per_batch": round(tot, 2), "graphs": G, "stages_ms": st}))
