@@ -183,7 +183,74 @@ struct StatsArgs {
   // SyncBatchNorm (hlhgat_bn_sums_*): the finaliser writes this rank's fp64
   // column sums [S0[C], S1[C], n_eff] here instead of finishing the statistics
   double* sums_out;
+  // input rows produced in the launch (hlhgat_bn_fwd_produced), written to
+  // xw (ldx) for the backward
+  const int64_t* pei;  // edge rows: [2][n] endpoints
+  const int32_t* prow;  // node rows: incidence CSR (node -> incident edge ids)
+  const int32_t* peid;
+  const float* prs;     // node rows: per-row scale
+  const float* pp;      // gathered rows
+  int64_t ldp;
+  const float* pz;      // per-row addend
+  int64_t ldz;
+  float pca, pcb;
+  float* xw;
 };
+
+// The NodeEdgeInt hidden layer's input rows, computed where the BatchNorm
+// reads them (bitwise the producers' own arithmetic):
+//   PROD 1 (edge rows, hlhgat_edge_gather2 with sa = sb = NULL):
+//     x[e] = z[e] + (ca (1 p[i]) + cb (1 p[j]))
+//   PROD 2 (node rows, hlhgat_poly_step over the binary incidence with
+//     rs, alpha = gamma = 1): x[v] = 1 (rs[v] sum_{CSR order} p[eid]) + 1 z[v]
+template <int PROD, int V>
+__device__ __forceinline__ typename VecT<V>::type produce_row(const StatsArgs& a, int64_t r,
+                                                              int c) {
+  using vt = typename VecT<V>::type;
+  vt o;
+  if constexpr (PROD == 1) {
+    const int64_t i = a.pei[r], j = a.pei[a.n + r];
+    const float si = 1.f, sj = 1.f;
+    vt xi = vload<V>(a.pp + i * a.ldp + c);
+    vt xj = vload<V>(a.pp + j * a.ldp + c);
+    vt zv = vload<V>(a.pz + r * a.ldz + c);
+#pragma unroll
+    for (int v = 0; v < V; ++v) vget(o, v) = a.pca * (si * vget(xi, v)) + a.pcb * (sj * vget(xj, v));
+#pragma unroll
+    for (int v = 0; v < V; ++v) vget(o, v) = vget(zv, v) + vget(o, v);
+  } else {
+    const int e0 = a.prow[r], e1 = a.prow[r + 1];
+    vt acc;
+#pragma unroll
+    for (int v = 0; v < V; ++v) vget(acc, v) = 0.f;
+    const float w = 1.f;
+    int p = e0;
+    for (; p + 1 < e1; p += 2) {  // two gathers in flight, adds in CSR order
+      vt x0 = vload<V>(a.pp + (int64_t)a.peid[p] * a.ldp + c);
+      vt x1 = vload<V>(a.pp + (int64_t)a.peid[p + 1] * a.ldp + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float s = vget(acc, v);
+        s = s + w * vget(x0, v);
+        s = s + w * vget(x1, v);
+        vget(acc, v) = s;
+      }
+    }
+    for (; p < e1; ++p) {
+      vt x0 = vload<V>(a.pp + (int64_t)a.peid[p] * a.ldp + c);
+#pragma unroll
+      for (int v = 0; v < V; ++v) vget(acc, v) = vget(acc, v) + w * vget(x0, v);
+    }
+    const float rsv = a.prs[r];
+    const float alpha = 1.f, gamma = 1.f;
+    vt zv = vload<V>(a.pz + r * a.ldz + c);
+#pragma unroll
+    for (int v = 0; v < V; ++v) vget(o, v) = alpha * (rsv * vget(acc, v));
+#pragma unroll
+    for (int v = 0; v < V; ++v) vget(o, v) = vget(o, v) + gamma * vget(zv, v);
+  }
+  return o;
+}
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 __device__ __forceinline__ void st_wt(double* p, double v) {
@@ -896,7 +963,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_sync_bwd_apply(SyncArgs a) {
 // ---------------------------------------------------------------------------
 // Forward: thread (rg, cl) owns rows r_lo + rg + j * rp (j < RPT) of its
 // partition; statistics rows stop at n_eff, output rows at n.
-template <int V, int RPT>
+template <int V, int RPT, int PROD = 0>
 __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
@@ -912,10 +979,24 @@ __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) 
 #pragma unroll
   for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
   if (c < a.C) {
+    if constexpr (PROD != 0) {
+      // every row of the partition (padding rows too: the producer wrote them)
+      int64_t r_end = r_lo + a.rows_per_part;
+      if (r_end > a.n) r_end = a.n;
 #pragma unroll
-    for (int j = 0; j < RPT; ++j) {
-      const int64_t r = r_lo + rg + (int64_t)j * a.rp;
-      if (r < r_hi) xr[j] = vload<V>(a.x + r * a.ldx + c);
+      for (int j = 0; j < RPT; ++j) {
+        const int64_t r = r_lo + rg + (int64_t)j * a.rp;
+        if (r < r_end) {
+          xr[j] = produce_row<PROD, V>(a, r, c);
+          vstore<V>(a.xw + r * a.ldx + c, xr[j]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int64_t r = r_lo + rg + (int64_t)j * a.rp;
+        if (r < r_hi) xr[j] = vload<V>(a.x + r * a.ldx + c);
+      }
     }
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {  // row order, as k_bn_stats
@@ -988,6 +1069,11 @@ __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) 
 template <int V, int RPT>
 __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
   k_bn_fwd_grid_body<V, RPT>(a, blk_hw());
+}
+
+template <int RPT, int PROD>
+__global__ __launch_bounds__(kThreads) void k_bn_fwd_produced(StatsArgs a) {
+  k_bn_fwd_grid_body<4, RPT, PROD>(a, blk_hw());
 }
 
 // ---------------------------------------------------------------------------
@@ -1270,6 +1356,29 @@ GridFn fwd_grid_fn(bool vec, int rpt) {
   }
 }
 
+// hlhgat_set_bn_produced(0): the producer's own launch before the BatchNorm
+// (A/B; bitwise the same results)
+bool& bn_produced_flag() {
+  static bool v = true;
+  return v;
+}
+
+GridFn produced_fn(int prod, int rpt) {
+  switch (rpt * 4 + prod) {
+    case 9: return k_bn_fwd_produced<2, 1>;
+    case 10: return k_bn_fwd_produced<2, 2>;
+    case 17: return k_bn_fwd_produced<4, 1>;
+    case 18: return k_bn_fwd_produced<4, 2>;
+    case 33: return k_bn_fwd_produced<8, 1>;
+    case 34: return k_bn_fwd_produced<8, 2>;
+    case 65: return k_bn_fwd_produced<16, 1>;
+    case 66: return k_bn_fwd_produced<16, 2>;
+    case 129: return k_bn_fwd_produced<32, 1>;
+    case 130: return k_bn_fwd_produced<32, 2>;
+    default: return nullptr;
+  }
+}
+
 // The one-launch kernel for this layout, or nullptr (two launches).
 GridFn pick_grid(const BnLayout& L, bool vec) {
   if (!bn_one_launch() || L.parts > kFlatMax) return nullptr;
@@ -1284,6 +1393,86 @@ GridFn pick_grid(const BnLayout& L, bool vec) {
 
 }  // namespace
 
+
+extern "C" int hlhgat_bn_fwd_produced(int mode, const int64_t* edge_index,
+                                      const int32_t* inc_rowptr, const int32_t* inc_eids,
+                                      int64_t inc_nnz, const float* row_scale, const float* p,
+                                      int64_t ldp, float ca, float cb, const float* z,
+                                      int64_t ldz, float* x, int64_t ldx, int64_t n,
+                                      const int32_t* n_valid, int64_t C, const float* weight,
+                                      const float* bias, float* running_mean,
+                                      float* running_var, int64_t* num_batches_tracked,
+                                      float momentum, float eps, int relu, float* y, int64_t ldy,
+                                      float* save_mean, float* save_invstd, void* workspace,
+                                      int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(mode == HLHGAT_BN_PRODUCE_EDGE_GATHER || mode == HLHGAT_BN_PRODUCE_NODE_INCIDENCE,
+                "bn_fwd_produced: bad mode %d", mode);
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C && ldp >= C &&
+                    ldz >= C,
+                "bn_fwd_produced: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(p && z && x && y && save_mean && save_invstd, "bn_fwd_produced: NULL pointer");
+  const bool edge = mode == HLHGAT_BN_PRODUCE_EDGE_GATHER;
+  HLH_CHECK_ARG(edge ? edge_index != nullptr
+                     : (inc_rowptr && row_scale && (inc_nnz == 0 || inc_eids)),
+                "bn_fwd_produced: missing producer arrays");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_fwd_produced: workspace too small");
+  const bool vec = bn_vec_ok(C, {ldx, ldy, ldp, ldz}, {x, y, p, z});
+  const BnLayout L = bn_layout(n, C, vec);
+  GridFn f = nullptr;
+  if (vec && bn_one_launch() && bn_produced_flag() && L.parts <= kFlatMax &&
+      L.tiles <= kMaxTiles) {
+    const int rpt = rpt_bucket(L);
+    f = rpt ? produced_fn(edge ? 1 : 2, rpt) : nullptr;
+    const int64_t cap = f ? capacity_of(reinterpret_cast<const void*>(f)) : 0;
+    if ((int64_t)L.parts * L.tiles > 256 || (int64_t)L.parts * L.tiles > cap) f = nullptr;
+  }
+  if (!f) {  // the producer's own launch, then the BatchNorm
+    int rc;
+    if (edge)
+      rc = hlhgat_edge_gather2(edge_index, n, p, ldp, (int)C, nullptr, nullptr, ca, cb, z, ldz, x,
+                               ldx, 0, stream);
+    else
+      rc = hlhgat_poly_step(inc_rowptr, inc_nnz ? inc_eids : nullptr, nullptr, row_scale, n,
+                            inc_nnz, nullptr, nullptr, p, ldp, (int)C, z, ldz, nullptr, 0, nullptr,
+                            0, 1.f, 0.f, 1.f, 1.f, 0.f, 0.f, x, ldx, stream);
+    if (rc != HLHGAT_OK) return rc;
+    return hlhgat_bn_fwd_train(x, ldx, n, n_valid, C, weight, bias, running_mean, running_var,
+                               num_batches_tracked, momentum, eps, relu, y, ldy, save_mean,
+                               save_invstd, workspace, workspace_bytes, stream);
+  }
+  StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
+  s.weight = weight;
+  s.bias = bias;
+  s.running_mean = running_mean;
+  s.running_var = running_var;
+  s.nbt = num_batches_tracked;
+  s.momentum = momentum;
+  s.eps = eps;
+  s.save_mean = save_mean;
+  s.save_invstd = save_invstd;
+  s.out = y;
+  s.ldo = ldy;
+  s.relu = relu;
+  s.poll_limit = g_poll_limit;
+  s.err = hlhgat::device_error_word();
+  HLH_CHECK_ARG(s.err, "bn_fwd_produced: no device error word (%s)", hlhgat_last_error());
+  s.pei = edge_index;
+  s.prow = inc_rowptr;
+  s.peid = inc_eids;
+  s.prs = row_scale;
+  s.pp = p;
+  s.ldp = ldp;
+  s.pz = z;
+  s.ldz = ldz;
+  s.pca = ca;
+  s.pcb = cb;
+  s.xw = x;
+  ProfScope prof(HLHGAT_PROF_BN_FWD, as_stream(stream), 8.0 * (double)n * C, 0.0);
+  launch(f, dim3(L.parts, L.tiles), dim3(kThreads), 0, as_stream(stream), &prof, s);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
 
 extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
   if (n < 0 || C <= 0) return 0;
@@ -1567,6 +1756,43 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   return HLHGAT_OK;
 }
 
+extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                                    const float* dy, int64_t lddy, int64_t n,
+                                    const int32_t* n_valid, int64_t C, const float* weight,
+                                    const float* save_mean, const float* save_invstd,
+                                    float* coef, float* dweight, float* dbias, void* workspace,
+                                    int64_t workspace_bytes, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && (!y || ldy >= C),
+                "bn_bwd_reduce: bad sizes");
+  HLH_CHECK_ARG(x && dy && coef && save_mean && save_invstd, "bn_bwd_reduce: NULL pointer");
+  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
+                "bn_bwd_reduce: workspace too small");
+  // the layout hlhgat_bn_bwd_train picks for an aligned dx: the same bits
+  const bool vec = bn_vec_ok(C, {ldx, lddy, y ? ldy : 4}, {x, y, dy});
+  BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_reduce: C too large");
+  BnWs w = carve(workspace, n, C);
+  StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
+  s.y = y;
+  s.ldy = ldy;
+  s.dy = dy;
+  s.lddy = lddy;
+  s.weight = weight;
+  s.save_mean = const_cast<float*>(save_mean);
+  s.save_invstd = const_cast<float*>(save_invstd);
+  s.coef = coef;
+  s.dweight = dweight;
+  s.dbias = dbias;
+  hipStream_t st = as_stream(stream);
+  ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
+  if (vec)
+    launch(k_bn_bwd_reduce<4>, dim3(L.parts, L.tiles), dim3(kThreads), 0, st, &prof, s);
+  else
+    launch(k_bn_bwd_reduce<1>, dim3(L.parts, L.tiles), dim3(kThreads), 0, st, &prof, s);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
 // ---------------------------------------------------------------------------
 // SyncBatchNorm: sums -> (caller all-gathers [world][2C+1]) -> apply
 // ---------------------------------------------------------------------------
@@ -1716,6 +1942,11 @@ extern "C" int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float
   else
     launch(k_bn_sync_bwd_apply<1>, dim3(g2), dim3(kThreads), 0, as_stream(stream), nullptr, a);
   HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_set_bn_produced(int on) {
+  bn_produced_flag() = on != 0;
   return HLHGAT_OK;
 }
 

@@ -257,13 +257,15 @@ struct AdamArgs {
   int64_t n;
   float* step;
   double lr, beta1, beta2, eps, wd;
+  int prepared;  // *step already holds this update's count (hlhgat_adam_prepare)
 };
 
 __global__ __launch_bounds__(256) void k_adam_flat(AdamArgs a) {
   // bias corrections once per workgroup (fp64 pow), broadcast through LDS
   __shared__ float sh[2];
   if (threadIdx.x == 0) {
-    const float s = *a.step + 1.0f;  // torch: state_steps += 1 (fp32), then the update
+    // torch: state_steps += 1 (fp32), then the update
+    const float s = a.prepared ? *a.step : *a.step + 1.0f;
     const double bc1 = 1.0 - pow(a.beta1, (double)s);
     const double bc2 = 1.0 - pow(a.beta2, (double)s);
     sh[0] = (float)bc1;
@@ -291,7 +293,44 @@ __global__ __launch_bounds__(256) void k_adam_flat(AdamArgs a) {
 }
 
 __global__ void k_adam_step_inc(float* step) { step[0] = step[0] + 1.0f; }
+
+// zero the gradient buffer (float4 stores) and increment the step count
+__global__ __launch_bounds__(256) void k_adam_prepare(float* g, int64_t n, float* step) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t == 0) step[0] = step[0] + 1.0f;
+  const int64_t n4 = n / 4;
+  float4* g4 = reinterpret_cast<float4*>(g);
+  for (int64_t i = t; i < n4; i += (int64_t)gridDim.x * 256) g4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = 4 * n4 + t; i < n; i += (int64_t)gridDim.x * 256) g[i] = 0.f;
+}
 }  // namespace
+
+extern "C" int hlhgat_adam_prepare(float* grad, int64_t n, float* step, void* stream) {
+  HLH_CHECK_ARG(n >= 0 && (n == 0 || grad) && step, "adam_prepare: NULL pointer or n < 0");
+  HLH_CHECK_ARG(n == 0 || aligned16(grad), "adam_prepare: grad must be 16-byte aligned");
+  int64_t g = ceil_div(n / 4 + 1, (int64_t)256);
+  if (g > 1024) g = 1024;
+  launch(k_adam_prepare, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, grad, n,
+         step);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_adam_flat_prepared(float* param, const float* grad, float* exp_avg,
+                                         float* exp_avg_sq, int64_t n, const float* step,
+                                         double lr, double beta1, double beta2, double eps,
+                                         double weight_decay, void* stream) {
+  HLH_CHECK_ARG(n >= 0 && (n == 0 || (param && grad && exp_avg && exp_avg_sq)) && step,
+                "adam_flat_prepared: NULL pointer or n < 0");
+  if (n == 0) return HLHGAT_OK;
+  int64_t g = ceil_div(n, 256 * 2);
+  if (g > 2048) g = 2048;
+  AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, const_cast<float*>(step), lr, beta1, beta2,
+             eps, weight_decay, 1};
+  launch(k_adam_flat, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
 
 extern "C" int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg,
                                 float* exp_avg_sq, int64_t n, float* step,
@@ -306,7 +345,7 @@ extern "C" int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg,
   }
   int64_t g = ceil_div(n, 256 * 2);
   if (g > 2048) g = 2048;
-  AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, step, lr, beta1, beta2, eps, weight_decay};
+  AdamArgs a{param, grad, exp_avg, exp_avg_sq, n, step, lr, beta1, beta2, eps, weight_decay, 0};
   launch(k_adam_flat, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, a);
   HLH_CHECK_LAUNCH();
   launch(k_adam_step_inc, dim3(1), dim3(1), 0, as_stream(stream), nullptr, step);

@@ -64,6 +64,16 @@ SIGNATURES = {
     "hlhgat_hodge_lmax_workspace_bytes": (c_i64, [c_i64, c_i32]),
     "hlhgat_hodge_lmax": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp,
                                   c_i64, c_vp]),
+    "hlhgat_bn_bwd_reduce": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                     c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_proj_bwd_bn_defer": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "hlhgat_set_bn_produced": (c_i32, [c_i32]),
+    "hlhgat_bn_fwd_produced": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_f32,
+                                       c_f32, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_i32, c_vp, c_i64,
+                                       c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_eig_pe_workspace_bytes": (c_i64, [c_i64, c_i64, c_i32]),
     "hlhgat_eig_pe": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp,
                               c_i64, c_vp, c_vp, c_i64, c_vp]),
@@ -114,6 +124,9 @@ SIGNATURES = {
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                     c_vp]),
+    "hlhgat_adam_prepare": (c_i32, [c_vp, c_i64, c_vp, c_vp]),
+    "hlhgat_adam_flat_prepared": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f64, c_f64,
+                                          c_f64, c_f64, c_f64, c_vp]),
     "hlhgat_adam_flat": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f64, c_f64, c_f64,
                                  c_f64, c_f64, c_vp]),
     "hlhgat_l1_loss_fwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),

@@ -607,6 +607,25 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
     return out
 
 
+ARENA_ALIGN = 256
+
+
+def arena_alloc(shapes: Dict[str, tuple], pin: bool = False, device=None):
+    """One uint8 buffer holding tensors of the given {name: (shape, dtype)}
+    back to back (ARENA_ALIGN-byte aligned, in the dict's order); returns
+    (arena, {name: view}).  The same shapes give the same layout, so two
+    arenas of one batch shape copy into each other whole."""
+    offs, off = {}, 0
+    for k, (shape, dt) in shapes.items():
+        nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+        offs[k] = (off, nb)
+        off += (nb + ARENA_ALIGN - 1) // ARENA_ALIGN * ARENA_ALIGN
+    arena = torch.empty(max(off, 1), dtype=torch.uint8, pin_memory=pin, device=device)
+    views = {k: arena[o:o + nb].view(shapes[k][1]).view(shapes[k][0])
+             for k, (o, nb) in offs.items()}
+    return arena, views
+
+
 class PackedGraphs:
     """A dataset of PairData simplex graphs packed back to back (the
     InMemoryDataset storage the reference's Hodge_Dataset keeps,
@@ -741,19 +760,23 @@ class PackedGraphs:
         if padded and (Zt < z_t or Zs < z_s):
             raise ValueError(f"PackedGraphs.collate: {z_t} / {z_s} Laplacian entries exceed "
                              f"the caps {Zt} / {Zs}")
-        e = lambda shape, dt: torch.empty(shape, dtype=dt, pin_memory=pin)  # noqa: E731
         f32, i32, i64 = torch.float32, torch.int32, torch.int64
-        t = {"x_t": e((Rt, self.f_t), f32), "x_s": e((Rs, self.f_s), f32),
-             "edge_index_t": e((2, Zt), i64), "edge_weight_t": e((Zt,), f32),
-             "edge_index_s": e((2, Zs), i64), "edge_weight_s": e((Zs,), f32),
-             "edge_index": e((2, Rs), i64), "y": e((B * self.y_dim,), f32),
-             "num_node1": e((B,), i64), "num_edge1": e((B,), i64),
-             "csr_rowptr_t": e((Rt + 1,), i32), "csr_col_t": e((Zt,), i32),
-             "csr_rowptr_s": e((Rs + 1,), i32), "csr_col_s": e((Zs,), i32),
-             "inc_rowptr": e((Rt + 1,), i32), "inc_eids": e((2 * Rs,), i32),
-             "deg_t": e((Rt,), f32), "inv_deg_t": e((Rt,), f32),
-             "seg_ptr_t": e((B + 1,), i32), "seg_ptr_s": e((B + 1,), i32),
-             "valid_mask_t": e((Rt,), torch.bool)}
+        # every tensor of the batch is a view of ONE host arena (pinned when
+        # asked): hlhgat.train.TrainStep.stage uploads it in one copy into a
+        # device arena of the same layout (the static buffers of a graph)
+        shapes = {"x_t": ((Rt, self.f_t), f32), "x_s": ((Rs, self.f_s), f32),
+                  "edge_index_t": ((2, Zt), i64), "edge_weight_t": ((Zt,), f32),
+                  "edge_index_s": ((2, Zs), i64), "edge_weight_s": ((Zs,), f32),
+                  "edge_index": ((2, Rs), i64), "y": ((B * self.y_dim,), f32),
+                  "num_node1": ((B,), i64), "num_edge1": ((B,), i64),
+                  "csr_rowptr_t": ((Rt + 1,), i32), "csr_col_t": ((Zt,), i32),
+                  "csr_rowptr_s": ((Rs + 1,), i32), "csr_col_s": ((Zs,), i32),
+                  "inc_rowptr": ((Rt + 1,), i32), "inc_eids": ((2 * Rs,), i32),
+                  "deg_t": ((Rt,), f32), "inv_deg_t": ((Rt,), f32),
+                  "seg_ptr_t": ((B + 1,), i32), "seg_ptr_s": ((B + 1,), i32),
+                  "valid_mask_t": ((Rt,), torch.bool),
+                  "n_valid_t": ((1,), i32), "n_valid_s": ((1,), i32)}
+        arena, t = arena_alloc(shapes, pin)
         o = self._lib.CollatedDesc(Rt, Rs, Zt, Zs, *[t[k].data_ptr() for k in (
             "x_t", "x_s", "edge_index_t", "edge_weight_t", "edge_index_s", "edge_weight_s",
             "edge_index", "y", "num_node1", "num_edge1", "csr_rowptr_t", "csr_col_t",
@@ -777,9 +800,12 @@ class PackedGraphs:
                   "inc_eids", "deg_t", "inv_deg_t", "seg_ptr_t", "seg_ptr_s"):
             setattr(b, k, t[k])
         if padded:
-            b.n_valid_t = torch.tensor([n_t], dtype=i32)
-            b.n_valid_s = torch.tensor([n_s], dtype=i32)
+            t["n_valid_t"][0] = n_t
+            t["n_valid_s"][0] = n_s
+            b.n_valid_t = t["n_valid_t"]
+            b.n_valid_s = t["n_valid_s"]
             b.valid_mask_t = t["valid_mask_t"]
+        b._arena = arena
         return b
 
 

@@ -1526,11 +1526,24 @@ class _SyncBatchNormFn(torch.autograd.Function):
 # ----------------------------------------------------------------------------
 # Adam on a flat parameter buffer (hlhgat_adam_flat; hlhgat.train.TrainStep)
 # ----------------------------------------------------------------------------
+def adam_prepare(grad: torch.Tensor, step: torch.Tensor) -> None:
+    """Zero the flat gradient buffer and increment the device step count in
+    one launch (hlhgat_adam_prepare); adam_flat(..., prepared=True) then
+    uses that count."""
+    _req_dev(grad, "grad")
+    _req_dev(step, "step")
+    if not grad.is_contiguous():
+        raise RuntimeError("hlhgat: adam_prepare: grad must be contiguous")
+    check(LIB.hlhgat_adam_prepare(grad.data_ptr(), grad.numel(), step.data_ptr(), _stream(grad)),
+          "adam_prepare")
+
+
 def adam_flat(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
               exp_avg_sq: torch.Tensor, step: torch.Tensor, lr: float, betas, eps: float,
-              weight_decay: float) -> None:
+              weight_decay: float, prepared: bool = False) -> None:
     """One torch.optim.Adam (fused, capturable) update of a flat fp32 buffer;
-    `step` the fp32 step count on device (incremented)."""
+    `step` the fp32 step count on device (incremented; prepared=True: already
+    incremented by adam_prepare)."""
     for t, name in ((param, "param"), (grad, "grad"), (exp_avg, "exp_avg"),
                     (exp_avg_sq, "exp_avg_sq"), (step, "step")):
         _req_dev(t, name)
@@ -1539,9 +1552,10 @@ def adam_flat(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor,
     n = param.numel()
     if not (grad.numel() == exp_avg.numel() == exp_avg_sq.numel() == n):
         raise RuntimeError("hlhgat: adam_flat: buffer sizes differ")
-    check(LIB.hlhgat_adam_flat(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
-                               exp_avg_sq.data_ptr(), n, step.data_ptr(), float(lr), float(betas[0]), float(betas[1]), float(eps),
-                               float(weight_decay), _stream(param)), "adam_flat")
+    fn = LIB.hlhgat_adam_flat_prepared if prepared else LIB.hlhgat_adam_flat
+    check(fn(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(), n,
+             step.data_ptr(), float(lr), float(betas[0]), float(betas[1]), float(eps),
+             float(weight_decay), _stream(param)), "adam_flat")
 
 
 class _L1LossFn(torch.autograd.Function):

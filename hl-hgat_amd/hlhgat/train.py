@@ -69,7 +69,26 @@ def _parts(batch):
 
 def _clone_batch(batch):
     static = type(batch).__new__(type(batch))
+    arena = getattr(batch, "_arena", None)
+    if arena is not None and arena.is_cuda and _in_arena(batch, arena):
+        # keep the one-arena layout (TrainStep.stage then refills it in one copy)
+        da = arena.clone()
+        for k, v in vars(batch).items():
+            if k == "_arena":
+                continue
+            if torch.is_tensor(v):
+                o = v.data_ptr() - arena.data_ptr()
+                nb = v.numel() * v.element_size()
+                setattr(static, k, da[o:o + nb].view(v.dtype).view(v.shape))
+            else:
+                setattr(static, k, v)
+        static._arena = da
+        if hasattr(static, "_mark"):
+            static._mark()
+        return static
     for k, v in vars(batch).items():
+        if k == "_arena":
+            continue
         setattr(static, k, v.clone() if torch.is_tensor(v) else v)
     if hasattr(static, "_mark"):
         static._mark()  # sorted/symmetric Laplacian flags on the static tensors
@@ -91,6 +110,29 @@ def batch_key(batch) -> Tuple:
 
 
 BN_RESERVE_CHANNELS = 2048  # BatchNorm workspace reserved per capture stream
+
+
+def _in_arena(b, arena) -> bool:
+    """Every tensor attribute of b is a contiguous view inside arena."""
+    lo, hi = arena.data_ptr(), arena.data_ptr() + arena.numel()
+    for _, v in _tensor_items(b):
+        p = v.data_ptr()
+        if not v.is_contiguous() or p < lo or p + v.numel() * v.element_size() > hi:
+            return False
+    return True
+
+
+def _same_layout(b, ha, sb, da) -> bool:
+    """b's tensors sit in host arena ha at the offsets sb's sit in device
+    arena da (same shapes: then one arena copy updates every static tensor)."""
+    if ha.numel() != da.numel():
+        return False
+    for k, v in _tensor_items(b):
+        w = getattr(sb, k, None)
+        if (w is None or w.shape != v.shape or w.dtype != v.dtype
+                or w.data_ptr() - da.data_ptr() != v.data_ptr() - ha.data_ptr()):
+            return False
+    return True
 
 
 class _Captured:
@@ -237,8 +279,19 @@ class TrainStep:
         self._ones = {}
 
     # -- the step ---------------------------------------------------------
-    def _fwd_bwd(self, batch) -> torch.Tensor:
+    def _prepare(self) -> bool:
+        """Start of a step: zero the gradient bucket.  With the HIP Adam the
+        step count is incremented in the same launch (hlhgat_adam_prepare);
+        returns whether it was (the update then must not count again)."""
+        if self._hip_adam:
+            ops.adam_prepare(self.flat_grad, self.opt.state[self.master]["step"])
+            return True
         self.flat_grad.zero_()
+        return False
+
+    def _fwd_bwd(self, batch, zeroed: bool = False) -> torch.Tensor:
+        if not zeroed:
+            self.flat_grad.zero_()
         # deferred split reductions (torch_ext.cpp): not in the first step,
         # which finds the parameters used twice (those are never deferred)
         defer = self._ext is not None and DEFER_REDUCE and self._fwd_bwd_calls > 0
@@ -294,26 +347,27 @@ class TrainStep:
                 # reduction ran; the bucket region itself holds the gradient
                 p.grad = view
 
-    def _opt_step(self) -> None:
+    def _opt_step(self, prepared: bool = False) -> None:
         if not self._hip_adam:
             self.opt.step()
             return
         st = self.opt.state[self.master]
         lr, betas, eps, wd = self._hyper
         ops.adam_flat(self.flat, self.flat_grad, st["exp_avg"], st["exp_avg_sq"], st["step"],
-                      lr, betas, eps, wd)
+                      lr, betas, eps, wd, prepared=prepared)
 
-    def _exchange_and_update(self) -> None:
+    def _exchange_and_update(self, prepared: bool = False) -> None:
         if self._exchange:
             # one contiguous bucket; mean over ranks as DDP
             dist.all_reduce(self.flat_grad)
             self.flat_grad.div_(self.world)
-        self._opt_step()
+        self._opt_step(prepared)
 
     def _eager(self, batch) -> torch.Tensor:
         ops.clear_caches()
-        loss = self._fwd_bwd(batch)
-        self._exchange_and_update()
+        prepared = self._prepare()
+        loss = self._fwd_bwd(batch, zeroed=True)
+        self._exchange_and_update(prepared)
         ops.clear_caches()
         self.stats["eager"] += 1
         return loss
@@ -342,11 +396,12 @@ class TrainStep:
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
         with torch.cuda.graph(g, pool=self._pool, stream=s):
-            loss = self._fwd_bwd(static)
+            prepared = self._prepare()
+            loss = self._fwd_bwd(static, zeroed=True)
             if self._exchange_in_graph:
-                self._exchange_and_update()  # RCCL all-reduce + scale + Adam, captured
+                self._exchange_and_update(prepared)  # RCCL all-reduce + scale + Adam, captured
             elif not self._exchange:
-                self._opt_step()
+                self._opt_step(prepared)
             # every stream forked from the capture (the node / edge side streams,
             # forks inside autograd backward nodes, which run on autograd's
             # device thread) rejoins it before hipStreamEndCapture: an unjoined
@@ -408,6 +463,11 @@ class TrainStep:
             stream.wait_event(slot.free)
         with torch.cuda.stream(stream):
             for b, sb in zip(_parts(batch), _parts(slot.batch)):
+                ha, da = getattr(b, "_arena", None), getattr(sb, "_arena", None)
+                if (ha is not None and da is not None and _in_arena(b, ha)
+                        and _same_layout(b, ha, sb, da)):
+                    da.copy_(ha, non_blocking=True)  # the whole batch in one copy
+                    continue
                 for name, v in _tensor_items(b):
                     getattr(sb, name).copy_(v, non_blocking=True)
             ev.record(stream)
@@ -416,14 +476,33 @@ class TrainStep:
     def _upload(self, b):
         """A device copy of batch object b that shares no storage with it
         (it may become a graph's static buffers, which later uploads
-        overwrite)."""
+        overwrite).  A batch whose tensors all live in one host arena
+        (PackedGraphs.collate) goes up in one copy, as views of a device
+        arena with the same layout."""
         out = type(b).__new__(type(b))
-        for k, v in vars(b).items():
-            if torch.is_tensor(v):
-                d = v.to(self.device, non_blocking=True)
-                setattr(out, k, d.clone() if d.data_ptr() == v.data_ptr() else d)
-            else:
-                setattr(out, k, v)
+        arena = getattr(b, "_arena", None)
+        if arena is not None and not arena.is_cuda and _in_arena(b, arena):
+            da = arena.to(self.device, non_blocking=True)
+            base = arena.data_ptr()
+            for k, v in vars(b).items():
+                if k == "_arena":
+                    continue
+                if torch.is_tensor(v):
+                    o = v.data_ptr() - base
+                    nb = v.numel() * v.element_size()
+                    setattr(out, k, da[o:o + nb].view(v.dtype).view(v.shape))
+                else:
+                    setattr(out, k, v)
+            out._arena = da
+        else:
+            for k, v in vars(b).items():
+                if k == "_arena":
+                    continue
+                if torch.is_tensor(v):
+                    d = v.to(self.device, non_blocking=True)
+                    setattr(out, k, d.clone() if d.data_ptr() == v.data_ptr() else d)
+                else:
+                    setattr(out, k, v)
         if hasattr(out, "_mark"):
             out._mark()
         return out
@@ -432,7 +511,8 @@ class TrainStep:
         ent.graph.replay()
         ent.released(torch.cuda.current_stream(self.device))
         if self._exchange and not self._exchange_in_graph:
-            self._exchange_and_update()
+            # the graph began with _prepare (the step counted when HIP Adam)
+            self._exchange_and_update(prepared=self._hip_adam)
         self.stats["replay"] += 1
         return ent.loss
 

@@ -498,6 +498,36 @@ int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int64_t lddc, i
                           int* deferred, void* stream);
 int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream);
 
+/* Linear backward fed by a BatchNorm (+ReLU) backward (every HL block's
+ * conv -> BatchNorm -> ReLU, lib/Hodge_ST_Model.py:556-566, and the
+ * NodeEdgeInt MLPs' Linear -> BatchNorm1d -> ReLU, lib/Hodge_Cheb_Conv.py:
+ * 276-289): hlhgat_proj_bwd_defer whose dC is the BatchNorm's input gradient
+ * formed where the kernel loads it, dC = A g + (B (x - mean) + C) with g = dy
+ * masked by the ReLU output (the coefficients from hlhgat_bn_bwd_reduce) --
+ * k_bn_bwd_apply's arithmetic, so the weights' and inputs' gradients are
+ * bitwise those of hlhgat_bn_bwd_train followed by hlhgat_proj_bwd_defer,
+ * without the apply launch or dC in memory.  Needs the one-launch path
+ * (16-byte aligned operands, N % 4 == 0, nb_w >= 1, M > 0): EINVAL
+ * otherwise. */
+typedef struct {
+  const float* x;     /* the BatchNorm's input [M][N], row stride ldx */
+  int64_t ldx;
+  const float* y;     /* its (+ReLU) output for the mask, or NULL (no ReLU) */
+  int64_t ldy;
+  const float* coef;  /* [3][N]: A, B, C (hlhgat_bn_bwd_reduce) */
+  const float* mean;  /* [N] saved batch mean */
+  const int32_t* n_valid; /* rows >= *n_valid are padding (dC = 0), or NULL */
+} hlhgat_bn_bwd_prologue_t;
+int hlhgat_proj_bwd_bn_defer(int64_t M, int64_t N, const float* dy, int64_t lddy,
+                             const hlhgat_bn_bwd_prologue_t* bn, int nb_w,
+                             const float* const* A, const int64_t* lda, const int64_t* kb_w,
+                             float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
+                             const float* const* W, const int64_t* ldw, const int64_t* kb_d,
+                             float* const* dA, const int64_t* ldda, int accumulate_d,
+                             float* workspace, int64_t workspace_floats,
+                             const hlhgat_reduce_desc_t* merge, hlhgat_reduce_desc_t* defer_out,
+                             int* deferred, void* stream);
+
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
  * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge
@@ -622,10 +652,42 @@ int hlhgat_get_bn_one_launch(void);
  * 0 = give up at once, which forces the timeout path). */
 int hlhgat_set_bn_poll_limit(unsigned limit);
 
+/* BatchNorm (+ReLU) training forward whose input rows are produced in the
+ * same launch (the NodeEdgeInt hidden layer, lib/Hodge_Cheb_Conv.py:276-289:
+ * the first Linear's halves combined over B1, then BatchNorm1d + ReLU):
+ *   HLHGAT_BN_PRODUCE_EDGE_GATHER: x[e] = z[e] + (ca p[i_e] + cb p[j_e])
+ *     (edge_index [2][n]; = hlhgat_edge_gather2 with sa = sb = NULL);
+ *   HLHGAT_BN_PRODUCE_NODE_INCIDENCE: x[v] = row_scale[v] sum p[eid] + z[v]
+ *     over node v's incidence CSR row (= hlhgat_poly_step over the binary
+ *     incidence, alpha = gamma = 1).
+ * x is written (the backward's input) and y = BN(x) as hlhgat_bn_fwd_train,
+ * bitwise the producer's launch followed by hlhgat_bn_fwd_train; that pair is
+ * what runs when the one-launch grid does not fit. */
+/* hlhgat_set_bn_produced(0): the producer's launch, then the BatchNorm (A/B). */
+int hlhgat_set_bn_produced(int on);
+#define HLHGAT_BN_PRODUCE_EDGE_GATHER 1
+#define HLHGAT_BN_PRODUCE_NODE_INCIDENCE 2
+int hlhgat_bn_fwd_produced(int mode, const int64_t* edge_index, const int32_t* inc_rowptr,
+                           const int32_t* inc_eids, int64_t inc_nnz, const float* row_scale,
+                           const float* p, int64_t ldp, float ca, float cb, const float* z,
+                           int64_t ldz, float* x, int64_t ldx, int64_t n, const int32_t* n_valid,
+                           int64_t C, const float* weight, const float* bias,
+                           float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, float momentum, float eps, int relu,
+                           float* y, int64_t ldy, float* save_mean, float* save_invstd,
+                           void* workspace, int64_t workspace_bytes, void* stream);
 /* Times a one-launch BatchNorm workgroup gave up waiting for its tile's
  * statistics: reads the device counter (synchronising). */
 int hlhgat_bn_wait_timeouts(unsigned* out);
 
+/* The reduction half of hlhgat_bn_bwd_train: dweight, dbias and dx's
+ * coefficients coef[3][C] (A, B, C of dx = A g + (B (x - mean) + C)), for a
+ * consumer that forms dx itself (hlhgat_proj_bwd_bn_defer). */
+int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
+                         const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
+                         int64_t C, const float* weight, const float* save_mean,
+                         const float* save_invstd, float* coef, float* dweight, float* dbias,
+                         void* workspace, int64_t workspace_bytes, void* stream);
 int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy,
                         const float* dy, int64_t lddy, int64_t n,
                         const int32_t* n_valid, int64_t C,
@@ -683,6 +745,16 @@ int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float* y, int64_
 int hlhgat_adam_flat(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                      int64_t n, float* step, double lr, double beta1, double beta2, double eps,
                      double weight_decay, void* stream);
+/* The same update split around the step's backward, one launch fewer:
+ * hlhgat_adam_prepare (at the start of the step) zeroes the n-element
+ * gradient buffer and increments `step`; hlhgat_adam_flat_prepared (after the
+ * backward) is hlhgat_adam_flat using `step` as already incremented.  The
+ * pair gives the bits of zeroing the gradient + hlhgat_adam_flat. */
+int hlhgat_adam_prepare(float* grad, int64_t n, float* step, void* stream);
+int hlhgat_adam_flat_prepared(float* param, const float* grad, float* exp_avg,
+                              float* exp_avg_sq, int64_t n, const float* step, double lr,
+                              double beta1, double beta2, double eps, double weight_decay,
+                              void* stream);
 
 /* L1 loss, torch.nn.L1Loss(reduction="mean") of the ZINC training loop
  * (torch's sub / abs / mean and its five backward launches):

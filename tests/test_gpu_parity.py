@@ -722,6 +722,54 @@ def test_nei_value_projected_first_matches_gather_first(cuda, d, dv, monkeypatch
         close(new[k], ref[k], 1e-4 if k.startswith(("g", "grad")) else 1e-5, k)
 
 
+@pytest.mark.parametrize("d,dv", [(64, 64), (96, 64), (40, 24)])
+def test_nei_produced_bn_bitwise(cuda, d, dv):
+    """The NodeEdgeInt hidden layer's input rows produced inside its BatchNorm
+    launch (hlhgat_bn_fwd_produced: the edge gather h1_s = Qs + (P2[i] +
+    P2[j]) / 2 and the node incidence sum h1_t = Qt + rD |B1| P1 in the
+    one-launch BN) == the producer launches (hlhgat_edge_gather2 /
+    hlhgat_poly_step) followed by the BatchNorm launches, bit for bit:
+    outputs, input gradients, every parameter gradient and the running
+    statistics (dv = 24: the unaligned width takes the producer launches
+    either way)."""
+    import hlhgat
+    from hlhgat import _lib
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(60, seed=23)
+    N_t, N_s = b.x_t.shape[0], b.x_s.shape[0]
+    g = torch.Generator().manual_seed(d)
+    xt0, xs0 = torch.randn(N_t, d, generator=g), torch.randn(N_s, d, generator=g)
+    Rt, Rs = torch.randn(N_t, dv, generator=g), torch.randn(N_s, dv, generator=g)
+    D = R.degree(b.edge_index.reshape(-1), N_t)
+    torch.manual_seed(5)
+    sd0 = {k: v.clone() for k, v in hlhgat.NodeEdgeInt(d=d, dv=dv).state_dict().items()}
+
+    def run():
+        m = hlhgat.NodeEdgeInt(d=d, dv=dv)
+        m.load_state_dict(sd0)
+        m = m.to(cuda).train()
+        x_t = dev(xt0).requires_grad_(True)
+        x_s = dev(xs0).requires_grad_(True)
+        par = hlhgat.adj2par1(dev(b.edge_index), N_t, N_s)
+        a, c = m(x_t, x_s, par, dev(D))
+        ((a * dev(Rt)).sum() + (c * dev(Rs)).sum()).backward()
+        res = {"out_t": a, "out_s": c, "gx_t": x_t.grad, "gx_s": x_s.grad}
+        res.update({"grad/" + k: p.grad for k, p in m.named_parameters()})
+        res.update({"buf/" + k: v for k, v in m.state_dict().items() if "running" in k})
+        return {k: v.detach().cpu() for k, v in res.items()}
+
+    prior = int(_lib.LIB.hlhgat_get_bn_one_launch())
+    try:
+        outs = []
+        for one in (1, 0):
+            _lib.check(_lib.LIB.hlhgat_set_bn_one_launch(one), "set_bn_one_launch")
+            outs.append(run())
+    finally:
+        _lib.LIB.hlhgat_set_bn_one_launch(prior)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 # ---------------------------------------------------------------------------
 # row schedules (locality_order) and XCD-aware slots never change results
 # ---------------------------------------------------------------------------
@@ -1199,6 +1247,44 @@ def test_fused_backward_zinc_model_bitwise(cuda, padded):
         return {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
     a = _grads_with_fused_bwd(True, run)
     c = _grads_with_fused_bwd(False, run)
+    assert a.keys() == c.keys() and len(a) > 100
+    for k in a:
+        assert torch.equal(a[k], c[k]), k
+
+
+@pytest.mark.parametrize("padded", [False, True])
+def test_bn_backward_fold_zinc_model_bitwise(cuda, padded):
+    """BatchNorm backward folded into the consuming Linear backward
+    (hlhgat_bn_bwd_reduce + hlhgat_proj_bwd_bn_defer: the conv -> BN -> ReLU
+    layers and the NodeEdgeInt W3 -> BN -> ReLU) == hlhgat_bn_bwd_train
+    (reduce + apply) then hlhgat_proj_bwd_defer, bit for bit: every
+    parameter gradient of the ZINC head, padded (n_valid) or not."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import pad_batch, static_caps
+    from hlhgat.synthetic import zinc_like_batch
+    b = zinc_like_batch(48, seed=6)
+    if padded:
+        b = pad_batch(b, static_caps(b, 128))
+    b = b.to(cuda)
+
+    def run():
+        torch.manual_seed(0)
+        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 2, 2], filters=[64, 64, 64],
+                                                mlp_channels=[256, 256], K=3,
+                                                keig=15).to(cuda).train()
+        torch.nn.functional.l1_loss(m(b).view(-1), b.y.view(-1)).backward()
+        g = {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+        g.update({k: v.clone() for k, v in m.state_dict().items() if "running" in k})
+        return g
+    res = []
+    for fold in (True, False):
+        ops._ext.set_bn_fold(fold)
+        try:
+            res.append(run())
+        finally:
+            ops._ext.set_bn_fold(True)
+    a, c = res
     assert a.keys() == c.keys() and len(a) > 100
     for k in a:
         assert torch.equal(a[k], c[k]), k

@@ -543,8 +543,9 @@ def test_native_mlgc_rejects_bad_input():
 # native loader: PackedGraphs.collate (hlhgat_collate) == collate + pad_batch
 # ---------------------------------------------------------------------------
 def _same_batch(a, b):
-    ta = {k for k, v in vars(a).items() if torch.is_tensor(v)}
-    tb = {k for k, v in vars(b).items() if torch.is_tensor(v)}
+    # (_arena: the storage PackedGraphs.collate carves its tensors from)
+    ta = {k for k, v in vars(a).items() if torch.is_tensor(v) and k != "_arena"}
+    tb = {k for k, v in vars(b).items() if torch.is_tensor(v) and k != "_arena"}
     assert ta == tb, (sorted(ta - tb), sorted(tb - ta))
     for k in ta:
         x, y = getattr(a, k), getattr(b, k)

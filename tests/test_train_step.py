@@ -716,3 +716,47 @@ def test_staged_double_buffered_steps_bitwise(cuda):
         assert torch.equal(sd_ref[key], sd[key]), key
     # two shapes x two slots captured; later steps went straight into a slot
     assert step.stats["captures"] == 4 and slots_used >= 5, (step.stats, slots_used)
+
+
+@pytest.mark.gpu
+def test_staged_arena_batches_single_copy_bitwise(cuda):
+    """PackedGraphs.collate batches (pinned, every tensor a view of one host
+    arena): TrainStep.stage uploads each into a graph's device arena of the
+    same layout in ONE copy; losses and parameters equal those of
+    step(device batch) with per-tensor copy-in, bit for bit."""
+    import hlhgat
+    import numpy as np
+    from hlhgat.hodge_dataset import PackedGraphs
+    from hlhgat.synthetic import zinc_like_graph
+    from hlhgat.train import TrainStep
+    ds = PackedGraphs([zinc_like_graph(500 + i) for i in range(60)], check_hodge=False)
+    idx = [np.arange(k * 12, (k + 1) * 12) for k in range(5)]
+    cs = [ds.caps_for(i, 128) for i in idx]
+    caps = {k: max(c[k] for c in cs) for k in cs[0]}
+    order = [0, 1, 2, 3, 4, 1, 0, 3]
+    l_ref, sd_ref, _ = _run(True, True, [ds.collate(idx[i], caps).to(cuda) for i in range(5)],
+                            order)
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
+    crit = torch.nn.L1Loss()
+    step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                     weight_decay=1e-3, graphs=True)
+    cs_ = torch.cuda.Stream(device=cuda)
+    host = [ds.collate(idx[i], caps, pin=True) for i in order]
+    assert all(hasattr(b, "_arena") and b._arena.is_pinned() for b in host)
+    losses, nxt = [], step.stage(host[0], cs_)
+    single = 0
+    for k in range(len(order)):
+        cur = nxt
+        if k + 1 < len(order):
+            nxt = step.stage(host[k + 1], cs_)
+        if cur.slot is not None:
+            single += hasattr(cur.slot.batch, "_arena")
+        losses.append(float(step(cur)))
+    torch.cuda.synchronize()
+    _check_errors()
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    assert losses == l_ref, (losses, l_ref)
+    for key in sd_ref:
+        assert torch.equal(sd_ref[key], sd[key]), key
+    assert step.stats["captures"] == 2 and single >= 4, (step.stats, single)

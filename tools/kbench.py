@@ -139,6 +139,8 @@ def main():
                            (nt, 64, [36, 36, 36], "init conv d=36"),
                            (ns, 64, [18, 18, 18], "init conv d=18"),
                            (ns, 64, [384, 384], "MSI Linear(768,64)"),
+                           (nt, 128, [64], "NEI Wt pack Linear(64,128) nodes"),
+                           (ns, 128, [64], "NEI Ws pack Linear(64,128) edges"),
                            (ns, 64, [128, 128], "MSI Linear(256,64)"),
                            (ns, 64, [64], "MSI Linear(64,64)"),
                            (1000, 256, [128, 128], "mlp Linear(256,256)"),
