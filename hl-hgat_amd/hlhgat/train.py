@@ -24,6 +24,8 @@ executing it, so no batch is trained twice.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
@@ -135,6 +137,36 @@ def _same_layout(b, ha, sb, da) -> bool:
     return True
 
 
+@contextlib.contextmanager
+def _no_gc():
+    """No cyclic garbage collection while a graph is being captured: a
+    collection that frees another capture's graph, pool or event then calls
+    HIP APIs the global capture mode refuses, and the destructor aborts the
+    process (measured: a collection inside a capture's forward).  Pending
+    garbage is collected first, outside the capture."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
+# Events of TrainStep.stage live as long as the process: an event destroyed
+# by the garbage collector while ANOTHER stream is capturing (global capture
+# mode) aborts the process (hipEventDestroy is refused during a capture), so
+# every staging event comes from a per-TrainStep ring kept here.
+_EVENTS_KEEP = []
+
+
+def _event():
+    ev = torch.cuda.Event()
+    _EVENTS_KEEP.append(ev)
+    return ev
+
+
 class _Captured:
     def __init__(self, graph, static_batch, loss):
         self.graph = graph
@@ -142,10 +174,11 @@ class _Captured:
         self.loss = loss
         self.slots = [self]  # TrainStep.stage: the graphs of this shape, used in turn
         self.free = None     # event after this graph's last replay (its buffers reusable)
+        self.pending = 0     # staged uploads into this graph's buffers not yet stepped
 
     def released(self, stream):
         if self.free is None:
-            self.free = torch.cuda.Event()
+            self.free = _event()
         self.free.record(stream)
 
     def load(self, batch):
@@ -170,6 +203,7 @@ class _Captured:
 
 
 STAGE_SLOTS = 2  # captured graphs per batch shape that TrainStep.stage fills in turn
+STAGE_RING = 8   # staged batches that may be outstanding (uploaded, not yet stepped)
 
 
 class Staged:
@@ -395,7 +429,7 @@ class TrainStep:
                 self._ext.bn_workspace_reserve(int(h), idx, BN_RESERVE_CHANNELS)
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        with torch.cuda.graph(g, pool=self._pool, stream=s):
+        with _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s):
             prepared = self._prepare()
             loss = self._fwd_bwd(static, zeroed=True)
             if self._exchange_in_graph:
@@ -445,7 +479,15 @@ class TrainStep:
         key = batch_key(batch)
         ent = self._graphs.get(key)
         main = torch.cuda.current_stream(self.device)
-        ev = torch.cuda.Event()
+        self._staging = True
+        # a ring of events (kept for the process, see _EVENTS_KEEP): at most
+        # STAGE_RING staged batches may be outstanding
+        ring = getattr(self, "_stage_ring", None)
+        if ring is None:
+            ring = self._stage_ring = [_event() for _ in range(STAGE_RING)]
+            self._stage_next = 0
+        ev = ring[self._stage_next]
+        self._stage_next = (self._stage_next + 1) % STAGE_RING
         if ent is None or len(ent.slots) < STAGE_SLOTS:
             with torch.cuda.stream(stream):
                 dev = [self._upload(b) for b in _parts(batch)]
@@ -459,8 +501,11 @@ class TrainStep:
         k = getattr(ent, "next_slot", 0)
         ent.next_slot = (k + 1) % len(ent.slots)
         slot = ent.slots[k]
+        slot.pending += 1
         if slot.free is not None:
             stream.wait_event(slot.free)
+        else:  # replayed before staging began (no release event): after all of main
+            stream.wait_stream(main)
         with torch.cuda.stream(stream):
             for b, sb in zip(_parts(batch), _parts(slot.batch)):
                 ha, da = getattr(b, "_arena", None), getattr(sb, "_arena", None)
@@ -509,7 +554,8 @@ class TrainStep:
 
     def _replay(self, ent: _Captured) -> torch.Tensor:
         ent.graph.replay()
-        ent.released(torch.cuda.current_stream(self.device))
+        if getattr(self, "_staging", False):  # stage() waits for the slot's release
+            ent.released(torch.cuda.current_stream(self.device))
         if self._exchange and not self._exchange_in_graph:
             # the graph began with _prepare (the step counted when HIP Adam)
             self._exchange_and_update(prepared=self._hip_adam)
@@ -519,10 +565,16 @@ class TrainStep:
     def _call_staged(self, st: Staged) -> torch.Tensor:
         torch.cuda.current_stream(self.device).wait_event(st.event)
         if st.slot is not None:
+            st.slot.pending -= 1
             return self._replay(st.slot)
         ent = self._graphs.get(st.key)
-        if ent is None or len(ent.slots) >= STAGE_SLOTS:
+        if ent is None:
             return self(st.batch)
+        if len(ent.slots) >= STAGE_SLOTS:
+            free = [sl for sl in ent.slots if sl.pending == 0]
+            if free:  # copy-in into a graph no staged upload is waiting for
+                free[0].load(st.batch)
+                return self._replay(free[0])
         # one more slot for this shape: the staged tensors are its static
         # buffers; capturing does not run the step, the first replay does
         return self._replay(self._capture(st.batch, st.key, slot_of=ent))
@@ -542,8 +594,11 @@ class TrainStep:
             loss = self._eager(batch)
             self._capture(batch, key)
             return loss
-        ent.load(batch)
-        return self._replay(ent)
+        free = [sl for sl in ent.slots if sl.pending == 0]
+        if not free:  # every graph of the shape awaits a staged batch: one more
+            return self._replay(self._capture(self._upload(batch), key, slot_of=ent))
+        free[0].load(batch)
+        return self._replay(free[0])
 
     def state_dict(self):
         return {"model": self.model.state_dict(), "opt": self.opt.state_dict()}
@@ -589,7 +644,7 @@ class InferStep:
         s = self._stream
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        with torch.cuda.graph(g, pool=self._pool, stream=s):
+        with _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s):
             out = self._forward(static)
             ops.join_capture_streams(self.device)
         left = ops.side_streams_capturing(self.device)

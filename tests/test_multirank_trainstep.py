@@ -97,7 +97,10 @@ def _to(b, dev):
 def _save_shards(shards, path):
     """[step][rank] batches (a Batch or a level list) as plain tensor dicts."""
     def one(b):
-        d = {k: v for k, v in vars(b).items() if torch.is_tensor(v) and not k.startswith("_")}
+        # (clones: PackedGraphs.collate carves every tensor from one arena,
+        # which torch.save refuses to store as differently typed views)
+        d = {k: v.clone() for k, v in vars(b).items()
+             if torch.is_tensor(v) and not k.startswith("_")}
         d["__meta"] = {"num_graphs": int(b.num_graphs), "hodge_sorted": dict(b.hodge_sorted),
                        "l1_factor": bool(getattr(b, "l1_factor", False)),
                        "num_nodes": int(getattr(b, "num_nodes", 0))}
