@@ -1356,10 +1356,14 @@ GridFn fwd_grid_fn(bool vec, int rpt) {
   }
 }
 
-// hlhgat_set_bn_produced(0): the producer's own launch before the BatchNorm
-// (A/B; bitwise the same results)
+// hlhgat_set_bn_produced(1): the rows produced inside the one-launch
+// BatchNorm.  Off by default: same-box A/B of the replayed config-2 step
+// (tools/ab_step.py, round 4) 2.80 ms with the producer's own launch vs 2.87
+// ms produced in the grid-barrier launch -- the gathers lose the parallelism
+// of their own wide launch inside the co-resident (<= 256 workgroup) grid.
+// Bitwise the same results either way.
 bool& bn_produced_flag() {
-  static bool v = true;
+  static bool v = false;
   return v;
 }
 

@@ -588,8 +588,12 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
 // BatchNorm backward folded into the Linear backward that consumes its dx
 // (hlhgat_proj_bwd_bn_defer): only the reduction launches here; the consumer
 // forms dx where it loads it.  `ok` = the consumer takes the fused launch.
+// Off by default: measured in the replayed config-2 step (round 4), the
+// prologue's extra x / y / coefficient loads inside the fused Linear
+// backward cost more (k_proj_bwd_fused 1.32 -> 1.96 ms per step) than the 28
+// apply launches it removes; kept as an option, bitwise either way.
 bool& bn_fold_flag() {
-  static bool v = true;
+  static bool v = false;
   return v;
 }
 void set_bn_fold(bool on) { bn_fold_flag() = on; }

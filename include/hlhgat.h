@@ -663,7 +663,9 @@ int hlhgat_set_bn_poll_limit(unsigned limit);
  * x is written (the backward's input) and y = BN(x) as hlhgat_bn_fwd_train,
  * bitwise the producer's launch followed by hlhgat_bn_fwd_train; that pair is
  * what runs when the one-launch grid does not fit. */
-/* hlhgat_set_bn_produced(0): the producer's launch, then the BatchNorm (A/B). */
+/* hlhgat_set_bn_produced(on): 1 = rows produced inside the one-launch
+ * BatchNorm; 0 (default, measured faster in the config-2 step) = the
+ * producer's launch, then the BatchNorm.  Bitwise the same either way. */
 int hlhgat_set_bn_produced(int on);
 #define HLHGAT_BN_PRODUCE_EDGE_GATHER 1
 #define HLHGAT_BN_PRODUCE_NODE_INCIDENCE 2

@@ -758,14 +758,13 @@ def test_nei_produced_bn_bitwise(cuda, d, dv):
         res.update({"buf/" + k: v for k, v in m.state_dict().items() if "running" in k})
         return {k: v.detach().cpu() for k, v in res.items()}
 
-    prior = int(_lib.LIB.hlhgat_get_bn_one_launch())
     try:
         outs = []
-        for one in (1, 0):
-            _lib.check(_lib.LIB.hlhgat_set_bn_one_launch(one), "set_bn_one_launch")
+        for produced in (1, 0):  # (0, the default: the producer's own launch)
+            _lib.check(_lib.LIB.hlhgat_set_bn_produced(produced), "set_bn_produced")
             outs.append(run())
     finally:
-        _lib.LIB.hlhgat_set_bn_one_launch(prior)
+        _lib.LIB.hlhgat_set_bn_produced(0)
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
 
@@ -1283,7 +1282,7 @@ def test_bn_backward_fold_zinc_model_bitwise(cuda, padded):
         try:
             res.append(run())
         finally:
-            ops._ext.set_bn_fold(True)
+            ops._ext.set_bn_fold(False)
     a, c = res
     assert a.keys() == c.keys() and len(a) > 100
     for k in a:

@@ -14,8 +14,8 @@ Variants (A/B hooks, not product settings):
   nomlp2      the readout MLP module by module (no two-layer fused node)
   noreadside  the edge readout mean on the main stream
   noreserve   BatchNorm workspaces not reserved before the capture
-  noprodbn    NodeEdgeInt hidden-layer rows by their own launch before the BatchNorm
-  nobnfold    BatchNorm backward as reduce + apply before the Linear backward
+  prodbn      NodeEdgeInt hidden-layer rows produced inside the BatchNorm (off by default)
+  bnfold      BatchNorm backward folded into the Linear backward (off by default)
 """
 import argparse
 import json
@@ -38,8 +38,8 @@ def set_variant(name, on):
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
     _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
-    _lib.LIB.hlhgat_set_bn_produced(0 if (on and name == "noprodbn") else 1)
-    ops._ext.set_bn_fold(not (on and name == "nobnfold"))
+    _lib.LIB.hlhgat_set_bn_produced(1 if (on and name == "prodbn") else 0)
+    ops._ext.set_bn_fold(on and name == "bnfold")
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")
