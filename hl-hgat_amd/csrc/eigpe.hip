@@ -9,7 +9,8 @@
 // 256-graph batch (tridiagonalisation + divide and conquer, 100+ launches,
 // and a host sync on its info word; profiles/r04_pipeline/).
 //
-// Here one workgroup per graph, everything in fp64:
+// Here one workgroup per graph (the grid capped at half the CUs, each
+// workgroup taking graphs in turn), everything in fp64:
 //   1. Lanczos on L0 = deg .* x - A x with FULL re-orthogonalisation (two
 //      classical Gram-Schmidt passes against every previous vector) for n
 //      steps, restarting with a fresh vector orthogonal to the basis when an
@@ -33,6 +34,8 @@
 #include "common.h"
 #include "tridiag.h"
 
+#include <algorithm>
+
 using namespace hlhgat;
 
 namespace {
@@ -55,6 +58,7 @@ struct EigArgs {
   double* lmax;
   double* ws;  // [n_graphs][ws_per_graph] for graphs that miss the LDS
   int64_t ws_per_graph;
+  int64_t n_graphs;
 };
 
 __device__ __forceinline__ double wsum(double v) {
@@ -418,20 +422,21 @@ __global__ __launch_bounds__(kEpThreads) void k_eig_pe(EigArgs a) {
   __shared__ double red[kEpThreads / 64];
   __shared__ double lam[kEpMaxK + 1];
   __shared__ int clus[kEpMaxK + 1];
-  const int g = blockIdx.x;
-  const int64_t n0 = a.node_ptr[g];
-  const int n = (int)(a.node_ptr[g + 1] - n0);
-  if (n <= 0) {
-    if (threadIdx.x == 0) a.lmax[g] = 0.0;
-    return;
+  for (int64_t g = blockIdx.x; g < a.n_graphs; g += gridDim.x) {
+    const int64_t n0 = a.node_ptr[g];
+    const int n = (int)(a.node_ptr[g + 1] - n0);
+    if (n <= 0) {
+      if (threadIdx.x == 0) a.lmax[g] = 0.0;
+      continue;
+    }
+    const int nnz = a.inc_rowptr[n0 + n] - a.inc_rowptr[n0];
+    if (small_bytes(n, nnz, a.k) <= kEpLdsBytes)
+      eig_pe_graph<true>(a, (int)g, n0, n, ep_lds, red, lam, clus);
+    else
+      eig_pe_graph<false>(a, (int)g, n0, n,
+                          reinterpret_cast<char*>(a.ws + g * a.ws_per_graph), red, lam, clus);
+    __syncthreads();  // the next graph reuses the LDS
   }
-  const int nnz = a.inc_rowptr[n0 + n] - a.inc_rowptr[n0];
-  if (small_bytes(n, nnz, a.k) <= kEpLdsBytes)
-    eig_pe_graph<true>(a, g, n0, n, ep_lds, red, lam, clus);
-  else
-    eig_pe_graph<false>(a, g, n0, n,
-                        reinterpret_cast<char*>(a.ws + (int64_t)g * a.ws_per_graph), red, lam,
-                        clus);
 }
 
 int64_t per_graph_doubles(int64_t max_nodes, int k) {
@@ -480,7 +485,17 @@ extern "C" int hlhgat_eig_pe(const int32_t* inc_rowptr, const int32_t* inc_edge,
   a.lmax = lmax;
   a.ws = reinterpret_cast<double*>(workspace);
   a.ws_per_graph = per_graph_doubles(max_nodes, k);
-  hipLaunchKernelGGL(k_eig_pe, dim3((unsigned)n_graphs), dim3(kEpThreads), kEpLdsBytes,
+  a.n_graphs = n_graphs;
+  // at most half the CUs: a workgroup holds a whole CU's LDS, and the
+  // pipeline runs beside the training step, whose one-launch BatchNorm needs
+  // its grid co-resident (a full-chip eig_pe starved it into its barrier
+  // timeout, measured in the config-3 overlap leg); graphs beyond the grid
+  // are taken in turn by the same workgroups
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t grid = std::min<int64_t>(n_graphs, std::max(1, cus / 2));
+  hipLaunchKernelGGL(k_eig_pe, dim3((unsigned)grid), dim3(kEpThreads), kEpLdsBytes,
                      as_stream(stream), a);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
