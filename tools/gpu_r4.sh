@@ -3,11 +3,6 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-export DEBUG_HIP_FORCE_GRAPH_QUEUES=2
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_eig_pe.py tests/test_pipeline.py > gpurun_out/r04_n_tests.log 2>&1
-rc=$?; echo "=== tests rc=$rc"; tail -1 gpurun_out/r04_n_tests.log; [ $rc = 0 ] || exit 1
-timeout -k 10 300 python tools/probes/cfg3_pipe.py > gpurun_out/r04_n_cfg3.log 2>&1
-echo "=== cfg3 rc=$?"; tail -1 gpurun_out/r04_n_cfg3.log
-timeout -k 10 300 python tools/probes/eig_probe.py > gpurun_out/r04_n_eig.log 2>&1
-echo "=== eig rc=$?"; tail -1 gpurun_out/r04_n_eig.log
+timeout -k 10 700 python bench.py > gpurun_out/r04_q_bench.json 2> gpurun_out/r04_q_bench.err
+echo "=== bench rc=$?"; grep -n "FAILED\|re-run\|Error\|heads\]" gpurun_out/r04_q_bench.err | head
 exit 0
