@@ -1321,10 +1321,17 @@ int64_t capacity_of(const void* kernel) {
     if (kv.first == kernel) return kv.second;
   int dev = 0, cus = 0, occ = 0;
   int64_t c = 0;
+  // the share of the chip one barrier grid may take: 1 / HLHGAT_BN_COLOCATE
+  // (default 2: two chains' barrier launches resident at once)
+  static const int share = [] {
+    const char* e = std::getenv("HLHGAT_BN_COLOCATE");
+    const int v = e ? std::atoi(e) : 2;
+    return v >= 1 && v <= 16 ? v : 2;
+  }();
   if (hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kThreads, 0) == hipSuccess)
-    c = (int64_t)occ * cus / 2;
+    c = (int64_t)occ * cus / share;
   cache->push_back({kernel, c});
   return c;
 }
