@@ -140,7 +140,8 @@ __device__ __forceinline__ Work carve(char* p, int n, int k, bool adjacency) {
 // (shuffle-combined), each node's update by `split` slices of the basis
 // (partials through u, summed in slice order); 4 independent accumulators
 // keep 4 LDS reads in flight per lane.
-__device__ __forceinline__ double orthogonalise(const Work& W, int n, int cnt) {
+__device__ __forceinline__ double orthogonalise(const Work& W, int n, int cnt, double* red,
+                                                double* nrm2) {
   const int tid = threadIdx.x;
   int parts = 1;
   while (parts < kEpSplit && parts * 2 * cnt <= kEpThreads) parts *= 2;
@@ -149,6 +150,7 @@ __device__ __forceinline__ double orthogonalise(const Work& W, int n, int cnt) {
   const int slice = (cnt + split - 1) / split;
   double last = 0.0;
   for (int pass = 0; pass < 2; ++pass) {
+    double ss = 0.0;
     for (int r0 = 0; r0 < cnt * parts; r0 += kEpThreads) {
       const int t = r0 + tid;
       const int i = t / parts, p = t % parts;
@@ -184,19 +186,35 @@ __device__ __forceinline__ double orthogonalise(const Work& W, int n, int cnt) {
       }
       for (; i < i1; ++i) s0 += W.h[i] * W.Q[(int64_t)i * W.ldq + v];
       const double sum = (s0 + s1) + (s2 + s3);
-      if (split == 1) W.w[v] -= sum;
-      else W.u[(int64_t)sl * n + v] = sum;
+      if (split == 1) {
+        const double nw = W.w[v] - sum;
+        W.w[v] = nw;
+        ss += nw * nw;
+      } else {
+        W.u[(int64_t)sl * n + v] = sum;
+      }
     }
     if (split > 1) {
       __syncthreads();
       for (int v = tid; v < n; v += kEpThreads) {
         double sum = 0.0;
         for (int sl = 0; sl < split; ++sl) sum += W.u[(int64_t)sl * n + v];
-        W.w[v] -= sum;
+        const double nw = W.w[v] - sum;
+        W.w[v] = nw;
+        ss += nw * nw;
       }
+    }
+    if (pass == 1) {
+      // |w|^2 of the result in the pass's closing barrier (no block_sum after)
+      ss = wsum(ss);
+      if ((tid & 63) == 0) red[tid >> 6] = ss;
     }
     __syncthreads();
   }
+  double tot = 0.0;
+#pragma unroll
+  for (int wv = 0; wv < kEpThreads / 64; ++wv) tot += red[wv];
+  *nrm2 = tot;
   return last;
 }
 
@@ -319,13 +337,12 @@ __device__ __forceinline__ void eig_pe_graph(const EigArgs& a, int g, int64_t n0
   for (int j = 0; j < n; ++j) {
     apply(W.Q + (int64_t)j * W.ldq, W.w);
     __syncthreads();
-    const double alpha = orthogonalise(W, n, j + 1);
+    double ww;
+    const double alpha = orthogonalise(W, n, j + 1, red, &ww);
     if (tid == 0) W.al[j] = alpha;
     scale = fmax(scale, fabs(alpha));
     if (j + 1 == n) break;
-    double ss = 0.0;
-    for (int v = tid; v < n; v += kEpThreads) ss += W.w[v] * W.w[v];
-    double b = sqrt(block_sum(ss, red));
+    double b = sqrt(ww);
     scale = fmax(scale, b);
     double* qn = W.Q + (int64_t)(j + 1) * W.ldq;
     if (b > 1e-10 * scale) {
@@ -339,10 +356,8 @@ __device__ __forceinline__ void eig_pe_graph(const EigArgs& a, int g, int64_t n0
         for (int v = tid; v < n; v += kEpThreads)
           W.w[v] = hash_unit(((uint64_t)g << 20) + (uint64_t)j, (uint64_t)v + 7919ull * attempt);
         __syncthreads();
-        orthogonalise(W, n, j + 1);
-        ss = 0.0;
-        for (int v = tid; v < n; v += kEpThreads) ss += W.w[v] * W.w[v];
-        b = sqrt(block_sum(ss, red));
+        orthogonalise(W, n, j + 1, red, &ww);
+        b = sqrt(ww);
         if (b > 1e-3 || attempt >= 8) break;  // |r| ~ sqrt(n / 3) before the projection
       }
       for (int v = tid; v < n; v += kEpThreads) qn[v] = b > 0.0 ? W.w[v] / b : 0.0;
