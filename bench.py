@@ -1055,6 +1055,7 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] warmup done {step.stats}")
 
+    ops.bn_giveups_reset()  # synchronises: before the timed region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1067,6 +1068,7 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, device)
     ops.check_device_errors()  # a kernel that reported unusable results voids the run
+    giveups_timed = ops.bn_giveups()["count"]
 
     # roofline pass: eager steps, SpMM / projection / BatchNorm launches event-stamped
     L = hlhgat._lib
@@ -1208,23 +1210,14 @@ def main():
         torch.cuda.synchronize()
         ops.clear_device_errors()
         heads = _guarded("heads", heads_leg, device)
-        if "one-launch BatchNorm" in str(heads.get("error", "")):
-            # a grid-barrier BatchNorm timed out (flagged, its rows NaN: never a
-            # silent wrong number).  Measured only after the other legs of this
-            # process, not in a fresh one (tools/probes/heads_bn_probe.py); the
-            # heads are re-run with the two-launch BatchNorm and say so.
-            log("[rank 0] heads: re-run with the two-launch BatchNorm")
-            torch.cuda.synchronize()
-            ops.clear_device_errors()
-            hlhgat._lib.LIB.hlhgat_set_bn_one_launch(0)
-            try:
-                heads = _guarded("heads", heads_leg, device)
-            finally:
-                hlhgat._lib.LIB.hlhgat_set_bn_one_launch(1)
-            heads["bn_one_launch"] = ("off: the first run's one-launch BatchNorm barrier timed "
-                                      "out in this process (DESIGN.md §17)")
         result["heads"] = heads
     if rank == 0:
+        # one-launch BatchNorm workgroups that handed their rows to the
+        # finaliser over the whole process (correct results)
+        gu = ops.bn_giveups()
+        result["bn_barrier"] = {"giveups_timed_region": giveups_timed,
+                                "giveups_since_timed_region": gu["count"],
+                                "log": gu["log"][:8], "wait_us": 1000}
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -51,8 +51,10 @@ constexpr int kGroup = 16;                        // partitions per first-level 
 constexpr int kMaxGroups = kMaxParts / kGroup;
 constexpr int kMaxTiles = 1024;
 constexpr int kGridBase = kMaxTiles * (1 + kMaxGroups);  // per tile: top + group counters
-// + per tile: the one-launch kernels' barrier arrival and leave counters
+// + per tile: the one-launch kernels' barrier / generation word (64-bit)
 constexpr int kCounters = kGridBase + 2 * kMaxTiles;
+// give-up slots of the one-launch kernels, one 64-bit word per workgroup
+constexpr int kMaxSlots = 4096;
 constexpr int APPLY_RPT = 2;  // rows per thread in the elementwise apply kernels
 constexpr int kMaxRpt = 32;   // rows per thread the one-launch kernels hold in registers
 
@@ -107,6 +109,7 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
 
 struct BnWs {
   unsigned* count;   // [kCounters] at offset 0 (zero between launches)
+  unsigned long long* slots;  // [kMaxSlots] (tagged by generation, never reset)
   double* part;      // [parts][C][2]
   double* gpart;     // [groups][C][2]
   float* coef;       // [3][C] (bwd: a, b, c)
@@ -118,7 +121,8 @@ size_t align_up(size_t v) { return (v + 255) & ~size_t(255); }
 // reads another launch's partials as a counter.
 size_t bn_ws_bytes(int64_t n, int64_t C) {
   (void)n;
-  return align_up(sizeof(unsigned) * kCounters) + align_up(sizeof(double) * 2 * kMaxParts * C) +
+  return align_up(sizeof(unsigned) * kCounters) + align_up(sizeof(unsigned long long) * kMaxSlots) +
+         align_up(sizeof(double) * 2 * kMaxParts * C) +
          align_up(sizeof(double) * 2 * kMaxGroups * C) + align_up(sizeof(float) * 3 * C);
 }
 
@@ -128,6 +132,8 @@ BnWs carve(void* ws, int64_t n, int64_t C) {
   BnWs w;
   w.count = (unsigned*)p;
   p += align_up(sizeof(unsigned) * kCounters);
+  w.slots = (unsigned long long*)p;
+  p += align_up(sizeof(unsigned long long) * kMaxSlots);
   w.part = (double*)p;
   p += align_up(sizeof(double) * 2 * kMaxParts * C);
   w.gpart = (double*)p;
@@ -174,83 +180,18 @@ struct StatsArgs {
   float* coef;
   float* dweight;
   float* dbias;
-  // one-launch kernels: output rows, poll limit of the barrier, error word
+  // one-launch kernels: output rows, the wait bound of the barrier
+  // (microseconds), the error word, the tile's give-up slots
   float* out;
   int64_t ldo;
   int relu;
-  unsigned poll_limit;
+  unsigned wait_us;
   unsigned* err;
+  unsigned long long* slots;
   // SyncBatchNorm (hlhgat_bn_sums_*): the finaliser writes this rank's fp64
   // column sums [S0[C], S1[C], n_eff] here instead of finishing the statistics
   double* sums_out;
-  // input rows produced in the launch (hlhgat_bn_fwd_produced), written to
-  // xw (ldx) for the backward
-  const int64_t* pei;  // edge rows: [2][n] endpoints
-  const int32_t* prow;  // node rows: incidence CSR (node -> incident edge ids)
-  const int32_t* peid;
-  const float* prs;     // node rows: per-row scale
-  const float* pp;      // gathered rows
-  int64_t ldp;
-  const float* pz;      // per-row addend
-  int64_t ldz;
-  float pca, pcb;
-  float* xw;
 };
-
-// The NodeEdgeInt hidden layer's input rows, computed where the BatchNorm
-// reads them (bitwise the producers' own arithmetic):
-//   PROD 1 (edge rows, hlhgat_edge_gather2 with sa = sb = NULL):
-//     x[e] = z[e] + (ca (1 p[i]) + cb (1 p[j]))
-//   PROD 2 (node rows, hlhgat_poly_step over the binary incidence with
-//     rs, alpha = gamma = 1): x[v] = 1 (rs[v] sum_{CSR order} p[eid]) + 1 z[v]
-template <int PROD, int V>
-__device__ __forceinline__ typename VecT<V>::type produce_row(const StatsArgs& a, int64_t r,
-                                                              int c) {
-  using vt = typename VecT<V>::type;
-  vt o;
-  if constexpr (PROD == 1) {
-    const int64_t i = a.pei[r], j = a.pei[a.n + r];
-    const float si = 1.f, sj = 1.f;
-    vt xi = vload<V>(a.pp + i * a.ldp + c);
-    vt xj = vload<V>(a.pp + j * a.ldp + c);
-    vt zv = vload<V>(a.pz + r * a.ldz + c);
-#pragma unroll
-    for (int v = 0; v < V; ++v) vget(o, v) = a.pca * (si * vget(xi, v)) + a.pcb * (sj * vget(xj, v));
-#pragma unroll
-    for (int v = 0; v < V; ++v) vget(o, v) = vget(zv, v) + vget(o, v);
-  } else {
-    const int e0 = a.prow[r], e1 = a.prow[r + 1];
-    vt acc;
-#pragma unroll
-    for (int v = 0; v < V; ++v) vget(acc, v) = 0.f;
-    const float w = 1.f;
-    int p = e0;
-    for (; p + 1 < e1; p += 2) {  // two gathers in flight, adds in CSR order
-      vt x0 = vload<V>(a.pp + (int64_t)a.peid[p] * a.ldp + c);
-      vt x1 = vload<V>(a.pp + (int64_t)a.peid[p + 1] * a.ldp + c);
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        float s = vget(acc, v);
-        s = s + w * vget(x0, v);
-        s = s + w * vget(x1, v);
-        vget(acc, v) = s;
-      }
-    }
-    for (; p < e1; ++p) {
-      vt x0 = vload<V>(a.pp + (int64_t)a.peid[p] * a.ldp + c);
-#pragma unroll
-      for (int v = 0; v < V; ++v) vget(acc, v) = vget(acc, v) + w * vget(x0, v);
-    }
-    const float rsv = a.prs[r];
-    const float alpha = 1.f, gamma = 1.f;
-    vt zv = vload<V>(a.pz + r * a.ldz + c);
-#pragma unroll
-    for (int v = 0; v < V; ++v) vget(o, v) = alpha * (rsv * vget(acc, v));
-#pragma unroll
-    for (int v = 0; v < V; ++v) vget(o, v) = vget(o, v) + gamma * vget(zv, v);
-  }
-  return o;
-}
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 __device__ __forceinline__ void st_wt(double* p, double v) {
@@ -262,25 +203,58 @@ __device__ __forceinline__ double ld_wt(const double* p) {
       (long long)__hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// wait timeouts of the one-launch kernels (hlhgat_bn_wait_timeouts)
+// --- the one-launch kernels' barrier --------------------------------------
+// A workgroup of a one-launch kernel (k_bn_fwd_grid, k_proj_bn_fwd) arrives
+// (its partials written through), then waits for the workgroup that arrives
+// LAST -- the finaliser -- to publish the tile's statistics by bumping the
+// tile's generation word.  Nothing in the design may depend on every
+// workgroup being resident at once: the hardware places the workgroups of
+// concurrent kernels (the other chain's, RCCL's, a user's) as it likes, and
+// two barrier grids of different resource shapes on two queues can each hold
+// CUs the other one's unplaced workgroups need.  So the wait is bounded in
+// TIME (wait_us of the 100 MHz constant clock), and a workgroup whose wait
+// runs out does not fail: it leaves its rows to the finaliser and exits,
+// freeing its CU for the workgroups still unplaced:
+//   waiter  : slot[blk] = (gen0 << 2) | 1 ("left")  --  seq_cst, agent scope
+//             then reads the generation again; if it has moved, it races the
+//             finaliser for the slot (CAS left -> taken) and normalises its
+//             own rows from its registers when it wins;
+//   finaliser: after bumping the generation, reads every slot of its tile and
+//             takes (CAS left -> taken) each one marked "left" in THIS
+//             generation, then normalises those rows from x in memory with
+//             the same fp32 operations.
+// Of the waiter's (slot store, generation load) and the finaliser's
+// (generation bump, slot load) at least one side sees the other's write, so
+// every row is normalised exactly once, by its owner or by the finaliser,
+// with bitwise the same result; the slots are tagged with the generation,
+// so a slot left in an earlier launch never matches.  No workgroup waits for
+// anything without a time bound, so the kernel cannot deadlock whatever the
+// residency.  A give-up is counted (hlhgat_bn_wait_timeouts) and logged
+// (hlhgat_bn_giveup_log: tile, arrivals, total, generations) -- it costs
+// time, never correctness.
+//
+// The counters reset themselves (an arrival word returns to 0, the
+// generation only grows); a counter found beyond its total (state written by
+// something else) raises HLHGAT_DEVERR_BN_STATE in the host-visible error
+// word: the statistics of that launch are not trusted.
 __device__ unsigned g_bn_wait_timeouts = 0;
+__device__ unsigned g_bn_log_n = 0;
+__device__ hlhgat_bn_giveup_t g_bn_log[HLHGAT_BN_LOG_MAX];
 
-// A workgroup that gives up at the barrier (poll limit reached) must not use
-// partial statistics: it writes NaN into its rows, counts the timeout and
-// raises HLHGAT_DEVERR_BN_WAIT in the host-visible error word
-// (hlhgat_device_errors), which hlhgat.train.TrainStep, the bench and
-// hlhgat.ops.check_device_errors turn into a Python exception.
-__device__ __forceinline__ void report_wait_timeout(unsigned* err) {
-  __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (err) __hip_atomic_store(err, (unsigned)HLHGAT_DEVERR_BN_WAIT, __ATOMIC_RELAXED,
+constexpr uint64_t kTicksPerUs = 100;  // s_memrealtime runs at 100 MHz
+enum : unsigned { kKidBnGrid = 1, kKidProjBn = 2 };
+
+__device__ __forceinline__ void report_state_error(unsigned* err) {
+  if (err) __hip_atomic_store(err, (unsigned)HLHGAT_DEVERR_BN_STATE, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Signal arrival; returns true in the last workgroup of `total`.  Every wave
 // has drained its write-through partial stores (vmcnt(0)) before the barrier;
 // ONE lane adds to the counter; the workgroup whose add returned total-1
-// resets it and reads the partials after the second barrier.
-__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
+// resets it (an atomic store: the word is only ever touched by atomics) and
+// reads the partials after the second barrier.
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total, unsigned* err) {
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -288,51 +262,145 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned total) {
     unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
     s_last = (prev == total - 1) ? 1u : 0u;
-    if (s_last) *counter = 0u;  // ready for the next launch (stream-ordered)
+    if (prev >= total) report_state_error(err);
+    if (s_last)  // ready for the next launch (stream-ordered)
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   return s_last != 0u;
 }
 
-// Grid barrier of the `total` workgroups of one column tile (all co-resident,
-// see pick_grid) on ONE 64-bit word: count in the low half, generation in the
-// high half.  Every workgroup adds 1; the one that completes the count turns
-// it back to 0 and bumps the generation in the same word (a single atomic add
-// of 2^32 - total), the others poll until the generation changes or the poll
-// limit runs out (poll_limit == 0, a test hook: give up at once).  Nothing is
-// left to reset afterwards, whatever `total` the next launch uses.  Returns
-// false on timeout.
 typedef __attribute__((address_space(1))) unsigned long long gu64c_t;
-__device__ __forceinline__ bool bar_wait(unsigned long long* word, unsigned total,
-                                         unsigned poll_limit, unsigned* err) {
-  __shared__ unsigned s_ok;
+
+__device__ __forceinline__ unsigned long long slot_mark(unsigned gen0) {
+  return ((unsigned long long)gen0 << 2) | 1ull;  // "left"; | 2 = "taken"
+}
+
+// Thread 0 of a waiting workgroup: poll the tile's generation word for at most
+// wait_us; true when it moved (the statistics are final).  wait_us == 0 looks
+// once (a test hook that forces the give-up path).
+__device__ __forceinline__ bool poll_gen(unsigned long long* word, unsigned gen0,
+                                         unsigned wait_us) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t lim = (uint64_t)wait_us * kTicksPerUs;
+  for (;;) {
+    const unsigned long long w =
+        __hip_atomic_load((gu64c_t*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(w >> 32) != gen0) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= lim) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Thread 0 of a workgroup whose wait ran out (see above).  Returns true when
+// the workgroup reclaimed its rows (the statistics are final by then).
+// `arr` / `total`: the arrival counter and the count it waits for (log only).
+__device__ __forceinline__ bool give_up(unsigned long long* word, unsigned long long* slot,
+                                        unsigned gen0, unsigned kid, const unsigned* arr,
+                                        bool arr_low64, unsigned total, unsigned wait_us) {
+  const unsigned long long mark = slot_mark(gen0);
+  __hip_atomic_store((gu64c_t*)slot, mark, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long w =
+      __hip_atomic_load((gu64c_t*)word, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  bool mine = false;
+  if ((unsigned)(w >> 32) != gen0) {
+    unsigned long long exp = mark;
+    mine = __hip_atomic_compare_exchange_strong((gu64c_t*)slot, &exp, mark + 1ull,
+                                                __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __hip_atomic_fetch_add(&g_bn_wait_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned k =
+      __hip_atomic_fetch_add(&g_bn_log_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (k < HLHGAT_BN_LOG_MAX) {
+    hlhgat_bn_giveup_t r;
+    r.kernel = kid;
+    r.tile = blockIdx.y;
+    r.block = blockIdx.x;
+    r.total = total;
+    r.arrivals = arr_low64
+                     ? (unsigned)(__hip_atomic_load((gu64c_t*)arr, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffull)
+                     : __hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r.gen0 = gen0;
+    r.gen_seen = (unsigned)(w >> 32);
+    r.wait_us = wait_us;
+    r.outcome = mine ? 1u : 2u;
+    g_bn_log[k] = r;
+  }
+  return mine;
+}
+
+// The finaliser, after its generation bump: take every slot of [slots,
+// slots + n) left in this generation; taken[j] (LDS) = 1 for those.  Relaxed
+// loads issued after the bump returned; a match is taken with a seq_cst CAS.
+// Returns (in every thread) whether any was taken.
+template <int NT>
+__device__ __forceinline__ bool take_left(unsigned long long* slots, int n, unsigned gen0,
+                                          unsigned char* taken) {
+  __shared__ unsigned s_any;
+  if (threadIdx.x == 0) s_any = 0u;
+  __syncthreads();
+  const unsigned long long mark = slot_mark(gen0);
+  for (int j = threadIdx.x; j < n; j += NT) {
+    unsigned char t = 0;
+    const unsigned long long v =
+        __hip_atomic_load((gu64c_t*)(slots + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == mark) {
+      unsigned long long exp = mark;
+      if (__hip_atomic_compare_exchange_strong((gu64c_t*)(slots + j), &exp, mark + 1ull,
+                                               __ATOMIC_SEQ_CST, __ATOMIC_SEQ_CST,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        t = 1;
+        s_any = 1u;
+      }
+    }
+    taken[j] = t;
+  }
+  __syncthreads();
+  return s_any != 0u;
+}
+
+// Grid barrier of the `total` workgroups of one column tile on ONE 64-bit
+// word: arrival count in the low half, generation in the high half.  Every
+// workgroup adds 1; the one that completes the count turns it back to 0 and
+// bumps the generation in the same word (one atomic add of 2^32 - total): it
+// is the finaliser (kFinal) and returns at once.  The others wait (above):
+// kOwn = normalise your own rows, kLeft = the finaliser does.  *gen0 = the
+// generation of this launch.  Nothing is left to reset afterwards, whatever
+// `total` the next launch uses.
+enum : unsigned { kOwn = 0, kFinal = 1, kLeft = 2 };
+__device__ __forceinline__ unsigned bar_wait(unsigned long long* word, unsigned long long* slot,
+                                             unsigned total, unsigned wait_us, unsigned* err,
+                                             unsigned* gen0_out) {
+  __shared__ unsigned s_role, s_gen0;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long old =
         __hip_atomic_fetch_add((gu64c_t*)word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned ok = 0;
-    if ((unsigned)(old & 0xffffffffull) == total - 1) {
+    const unsigned gen0 = (unsigned)(old >> 32);
+    const unsigned arrived = (unsigned)(old & 0xffffffffull);
+    unsigned role;
+    if (arrived >= total) report_state_error(err);
+    if (arrived == total - 1) {
       __hip_atomic_fetch_add((gu64c_t*)word, (1ull << 32) - (unsigned long long)total,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ok = 1;
+      role = kFinal;
+    } else if (poll_gen(word, gen0, wait_us)) {
+      role = kOwn;
     } else {
-      const unsigned gen = (unsigned)(old >> 32);
-      for (unsigned it = 0; it < poll_limit; ++it) {
-        const unsigned long long w =
-            __hip_atomic_load((gu64c_t*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned)(w >> 32) != gen) {
-          ok = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
+      role = give_up(word, slot, gen0, kKidBnGrid, reinterpret_cast<const unsigned*>(word), true,
+                     total, wait_us)
+                 ? kOwn
+                 : kLeft;
     }
-    if (!ok) report_wait_timeout(err);
-    s_ok = ok;
+    s_role = role;
+    s_gen0 = gen0;
   }
   __syncthreads();
-  return s_ok != 0u;
+  *gen0_out = s_gen0;
+  return s_role;
 }
 
 // the barrier word of this launch's column tile (8-byte aligned: kGridBase is even)
@@ -472,7 +540,7 @@ __device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile
                                             double* out0, double* out1, const Blk& blk) {
   const int tile = blk.y;
   if (a.parts <= kFlatMax) {
-    if (!arrive_last(a.count + tile, (unsigned)a.parts)) return false;
+    if (!arrive_last(a.count + tile, (unsigned)a.parts, a.err)) return false;
     flat_reduce<NT>(a.part, a.parts, a, c0, tile_c, out0, out1);
     return true;
   }
@@ -480,7 +548,8 @@ __device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile
   const int ng = (a.parts + kGroup - 1) / kGroup;
   const int first = g * kGroup;
   const int cnt = a.parts - first < kGroup ? a.parts - first : kGroup;
-  if (!arrive_last(a.count + kMaxTiles + tile * kMaxGroups + g, (unsigned)cnt)) return false;
+  if (!arrive_last(a.count + kMaxTiles + tile * kMaxGroups + g, (unsigned)cnt, a.err))
+    return false;
   reduce_range<NT>(a.part, first, cnt, a, c0, tile_c, out0, out1);
   for (int t = threadIdx.x; t < tile_c; t += NT) {
     const int c = c0 + t;
@@ -490,7 +559,7 @@ __device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile
       st_wt(dst + 1, out1[t]);
     }
   }
-  if (!arrive_last(a.count + tile, (unsigned)ng)) return false;
+  if (!arrive_last(a.count + tile, (unsigned)ng, a.err)) return false;
   reduce_range<NT>(a.gpart, 0, ng, a, c0, tile_c, out0, out1);
   return true;
 }
@@ -963,7 +1032,22 @@ __global__ __launch_bounds__(kThreads) void k_bn_sync_bwd_apply(SyncArgs a) {
 // ---------------------------------------------------------------------------
 // Forward: thread (rg, cl) owns rows r_lo + rg + j * rp (j < RPT) of its
 // partition; statistics rows stop at n_eff, output rows at n.
-template <int V, int RPT, int PROD = 0>
+template <int V>
+__device__ __forceinline__ typename VecT<V>::type bn_row_out(typename VecT<V>::type x,
+                                                             const float (&mu)[V],
+                                                             const float (&sc)[V],
+                                                             const float (&sh)[V], bool pad,
+                                                             int relu) {
+  typename VecT<V>::type o;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const float z = (vget(x, v) - mu[v]) * sc[v] + sh[v];
+    vget(o, v) = pad ? 0.f : ((relu && z < 0.f) ? 0.f : z);
+  }
+  return o;
+}
+
+template <int V, int RPT>
 __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
@@ -979,24 +1063,10 @@ __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) 
 #pragma unroll
   for (int v = 0; v < V; ++v) s0[v] = s1[v] = 0.0;
   if (c < a.C) {
-    if constexpr (PROD != 0) {
-      // every row of the partition (padding rows too: the producer wrote them)
-      int64_t r_end = r_lo + a.rows_per_part;
-      if (r_end > a.n) r_end = a.n;
 #pragma unroll
-      for (int j = 0; j < RPT; ++j) {
-        const int64_t r = r_lo + rg + (int64_t)j * a.rp;
-        if (r < r_end) {
-          xr[j] = produce_row<PROD, V>(a, r, c);
-          vstore<V>(a.xw + r * a.ldx + c, xr[j]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < RPT; ++j) {
-        const int64_t r = r_lo + rg + (int64_t)j * a.rp;
-        if (r < r_hi) xr[j] = vload<V>(a.x + r * a.ldx + c);
-      }
+    for (int j = 0; j < RPT; ++j) {
+      const int64_t r = r_lo + rg + (int64_t)j * a.rp;
+      if (r < r_hi) xr[j] = vload<V>(a.x + r * a.ldx + c);
     }
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {  // row order, as k_bn_stats
@@ -1020,17 +1090,23 @@ __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) 
     bv[v] = (a.bias && in) ? a.bias[c + v] : 0.f;
   }
   write_partials<V, kThreads>(s0, s1, a, c0, blk);
-  const bool ok = bar_wait(barrier_word(a, blk), blk.gx, a.poll_limit, a.err);
+  unsigned long long* tile_slots = a.slots + (int64_t)blk.y * blk.gx;
+  unsigned gen0 = 0;
+  const unsigned role =
+      bar_wait(barrier_word(a, blk), tile_slots + blk.x, blk.gx, a.wait_us, a.err, &gen0);
+  if (role == kLeft) return;  // the finaliser normalises these rows
   __shared__ double sum0[kThreads], sum1[kThreads];
   __shared__ float sm[kThreads], ss[kThreads];
   const int tile_c = a.tpr * V;
-  if (ok) flat_reduce<kThreads>(a.part, blk.gx, a, c0, tile_c, sum0, sum1);
+  flat_reduce<kThreads>(a.part, blk.gx, a, c0, tile_c, sum0, sum1);
+  // the finaliser writes the saved and running statistics (exactly once)
+  const bool fin = role == kFinal;
   for (int t = threadIdx.x; t < tile_c; t += kThreads) {
     const int cc = c0 + t;
-    float m = __builtin_nanf(""), is = __builtin_nanf("");
-    if (ok && cc < a.C) {
-      fwd_finalize(a, cc, sum0[t], sum1[t], n_eff, m, is, blk.x == 0);
-      if (blk.x == 0) {
+    float m = 0.f, is = 0.f;
+    if (cc < a.C) {
+      fwd_finalize(a, cc, sum0[t], sum1[t], n_eff, m, is, fin);
+      if (fin) {
         a.save_mean[cc] = m;
         a.save_invstd[cc] = is;
       }
@@ -1038,30 +1114,37 @@ __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) 
     sm[t] = m;
     ss[t] = is;
   }
-  if (ok && a.nbt && blk.x == 0 && blk.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
+  if (fin && a.nbt && blk.y == 0 && threadIdx.x == 0) a.nbt[0] += 1;
   __syncthreads();
-  if (c < a.C) {
-    float sc[V], mu[V], sh[V];
+  float sc[V], mu[V], sh[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      sc[v] = wv[v] * ss[cl * V + v];  // NaN after a barrier timeout
-      mu[v] = sm[cl * V + v];
-      sh[v] = bv[v];
-    }
+  for (int v = 0; v < V; ++v) {
+    sc[v] = wv[v] * ss[cl * V + v];
+    mu[v] = sm[cl * V + v];
+    sh[v] = bv[v];
+  }
+  if (c < a.C) {
     int64_t r_end = r_lo + a.rows_per_part;
     if (r_end > a.n) r_end = a.n;
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
       const int64_t r = r_lo + rg + (int64_t)j * a.rp;
-      if (r < r_end) {
-        vt o;
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          const float z = (vget(xr[j], v) - mu[v]) * sc[v] + sh[v];
-          vget(o, v) = r >= n_eff ? 0.f : ((a.relu && z < 0.f) ? 0.f : z);  // NaN passes
-        }
-        vstore<V>(a.out + r * a.ldo + c, o);
-      }
+      if (r < r_end) vstore<V>(a.out + r * a.ldo + c, bn_row_out<V>(xr[j], mu, sc, sh, r >= n_eff, a.relu));
+    }
+  }
+  if (!fin) return;
+  // rows of partitions whose owners gave up: from x in memory, same operations
+  __shared__ unsigned char taken[kMaxParts];
+  if (!take_left<kThreads>(tile_slots, (int)blk.gx, gen0, taken)) return;
+  if (c >= a.C) return;
+  for (unsigned p = 0; p < blk.gx; ++p) {
+    if (!taken[p]) continue;
+    const int64_t p_lo = (int64_t)p * a.rows_per_part;
+    int64_t p_end = p_lo + a.rows_per_part;
+    if (p_end > a.n) p_end = a.n;
+    for (int64_t r = p_lo + rg; r < p_end; r += a.rp) {
+      vt xv = vload<V>(a.x + (r < n_eff ? r : 0) * a.ldx + c);
+      vstore<V>(a.out + r * a.ldo + c, bn_row_out<V>(xv, mu, sc, sh, r >= n_eff, a.relu));
     }
   }
 }
@@ -1069,11 +1152,6 @@ __device__ __forceinline__ void k_bn_fwd_grid_body(const StatsArgs& a, Blk blk) 
 template <int V, int RPT>
 __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
   k_bn_fwd_grid_body<V, RPT>(a, blk_hw());
-}
-
-template <int RPT, int PROD>
-__global__ __launch_bounds__(kThreads) void k_bn_fwd_produced(StatsArgs a) {
-  k_bn_fwd_grid_body<4, RPT, PROD>(a, blk_hw());
 }
 
 // ---------------------------------------------------------------------------
@@ -1091,12 +1169,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_produced(StatsArgs a) {
 //      each group of kGroup partials sums them (reduce_range, fixed order),
 //      the last group sums the group partials, finalises mean / invstd and the
 //      running statistics, and bumps the tile's generation word;
-//   3. every other workgroup polls that word (bounded: a timeout writes NaN
-//      rows and raises HLHGAT_DEVERR_BN_WAIT, as k_bn_fwd_grid), reads the
-//      statistics and normalises its tile from the registers: y = relu?((x -
-//      mean) * (w invstd) + b), rows >= n_valid written as 0.
-// All workgroups must be co-resident (the host checks half of the chip's
-// capacity, as for k_bn_fwd_grid).  Against projection -> k_bn_fwd_grid this
+//   3. every other workgroup polls that word, reads the statistics and
+//      normalises its tile from the registers: y = relu?((x - mean) *
+//      (w invstd) + b), rows >= n_valid written as 0.  The wait is bounded
+//      in time; a workgroup whose wait runs out leaves its tile to the
+//      finaliser, which normalises it from the stored x (the barrier protocol
+//      above: no residency assumption, bitwise the same y).
+// Against projection -> k_bn_fwd_grid this
 // saves the BatchNorm launch, its read of x and its own load latency.  The
 // statistics are the same sums in a different fp64 order (not bitwise the
 // two-kernel path; equal to 1e-6, tests/test_gpu_parity.py).
@@ -1183,17 +1262,18 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   const int first = grp * kGroup;
   const int cnt = parts - first < kGroup ? parts - first : kGroup;
   bool top = false;
-  if (arrive_last(s.count + kMaxTiles + by * kMaxGroups + grp, (unsigned)cnt)) {
+  if (arrive_last(s.count + kMaxTiles + by * kMaxGroups + grp, (unsigned)cnt, s.err)) {
     reduce_range<kThreads>(s.part, first, cnt, s, n_base, 64, sum0, sum1);
     if (threadIdx.x < 64) {
       double* dst = s.gpart + ((int64_t)grp * s.C + n_base + threadIdx.x) * 2;
       st_wt(dst, sum0[threadIdx.x]);
       st_wt(dst + 1, sum1[threadIdx.x]);
     }
-    top = arrive_last(s.count + by, (unsigned)ng);
+    top = arrive_last(s.count + by, (unsigned)ng, s.err);
   }
   float* sm = reinterpret_cast<float*>(sum1 + 64);  // [64]
   float* ss = sm + 64;                              // [64]
+  unsigned long long* tile_slots = s.slots + (int64_t)by * gridDim.x;
   if (top) {
     reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
     if (threadIdx.x < 64) {
@@ -1215,31 +1295,23 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
                              __HIP_MEMORY_SCOPE_AGENT);
   } else {
     if (threadIdx.x == 0) {
-      unsigned ok = 0;
-      for (unsigned it = 0; it < s.poll_limit; ++it) {
-        const unsigned long long w =
-            __hip_atomic_load((gu64c_t*)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned)(w >> 32) != s_gen0) {
-          ok = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!ok) report_wait_timeout(s.err);
+      unsigned ok = poll_gen(word, s_gen0, s.wait_us) ? 1u : 0u;
+      if (!ok)
+        ok = give_up(word, tile_slots + bx, s_gen0, kKidProjBn, s.count + by, false,
+                     (unsigned)ng, s.wait_us)
+                 ? 1u
+                 : 0u;
       s_ok = ok;
     }
     __syncthreads();
+    if (!s_ok) return;  // the finaliser normalises this tile from the stored x
     if (threadIdx.x < 64) {
       const int cc = n_base + threadIdx.x;
-      float m = __builtin_nanf(""), is = __builtin_nanf("");
-      if (s_ok) {
-        m = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(s.save_mean + cc),
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        is = __uint_as_float(__hip_atomic_load(reinterpret_cast<unsigned*>(s.save_invstd + cc),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      }
-      sm[threadIdx.x] = m;
-      ss[threadIdx.x] = is;
+      sm[threadIdx.x] = __uint_as_float(__hip_atomic_load(
+          reinterpret_cast<unsigned*>(s.save_mean + cc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      ss[threadIdx.x] = __uint_as_float(__hip_atomic_load(
+          reinterpret_cast<unsigned*>(s.save_invstd + cc), __ATOMIC_RELAXED,
+          __HIP_MEMORY_SCOPE_AGENT));
     }
   }
   __syncthreads();
@@ -1247,7 +1319,7 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
 #pragma unroll
   for (int tn = 0; tn < kPbTN; ++tn) {
     const int cl = tn * 16 + i, cc = n_base + cl;
-    const float sc = (s.weight ? s.weight[cc] : 1.f) * ss[cl];  // NaN after a timeout
+    const float sc = (s.weight ? s.weight[cc] : 1.f) * ss[cl];
     const float mu = sm[cl];
     const float sh = s.bias ? s.bias[cc] : 0.f;
 #pragma unroll
@@ -1259,6 +1331,39 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   const bool vy = (s.ldo % 4) == 0 && (reinterpret_cast<uintptr_t>(s.out) & 15) == 0;
   store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, s.out + n_base, s.ldo, kPbTN * 16, nullptr,
                          0, vy);
+  if (!top) return;
+  // row blocks whose owners gave up: y from the x they stored, same operations
+  __shared__ unsigned char taken[kMaxParts];
+  if (!take_left<kThreads>(tile_slots, parts, s_gen0, taken)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // their x stores (released at give-up)
+  const int c4 = threadIdx.x & 15, rr = threadIdx.x >> 4;
+  float sc[4], mu[4], sh[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int cl = 4 * c4 + v, cc = n_base + cl;
+    sc[v] = (s.weight ? s.weight[cc] : 1.f) * ss[cl];
+    mu[v] = sm[cl];
+    sh[v] = s.bias ? s.bias[cc] : 0.f;
+  }
+  for (int p = 0; p < parts; ++p) {
+    if (!taken[p]) continue;
+    for (int64_t r = (int64_t)p * 64 + rr; r < (int64_t)p * 64 + 64 && r < g.M; r += 16) {
+      float4 xv;
+      const float* xp = g.C + r * g.ldc + n_base + 4 * c4;
+      if (vx) xv = *reinterpret_cast<const float4*>(xp);
+      else xv = make_float4(xp[0], xp[1], xp[2], xp[3]);
+      const float4 o = bn_row_out<4>(xv, mu, sc, sh, r >= n_eff, s.relu);
+      float* yp = s.out + r * s.ldo + n_base + 4 * c4;
+      if (vy) {
+        *reinterpret_cast<float4*>(yp) = o;
+      } else {
+        yp[0] = o.x;
+        yp[1] = o.y;
+        yp[2] = o.z;
+        yp[3] = o.w;
+      }
+    }
+  }
 }
 
 bool& proj_bn_fused_flag() {
@@ -1298,22 +1403,22 @@ StatsArgs stats_args(const BnLayout& L, const BnWs& w, const float* x, int64_t l
   s.part = w.part;
   s.gpart = w.gpart;
   s.count = w.count;
+  s.slots = w.slots;
+  s.err = hlhgat::device_error_word();
   return s;
 }
 
-// --- one-launch selection: co-residency and registers ------------------------
-// The one-launch kernels' barrier needs every workgroup of a column tile
-// resident at once.  They are used only when the whole grid fits in HALF of
-// the chip's resident-workgroup capacity for that kernel
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs): the HL blocks' node
-// and edge chains run on two streams (hlhgat.ops.fork) and each may be inside
-// one such launch at the same time; every other kernel on the device
-// completes without waiting, so it only delays residency.  Also: grid <= 256
-// workgroups, the partials use the flat order, and a thread's rows fit the
-// register budget (RPT <= kMaxRpt).  Anything that still stalls the barrier
-// is caught by the bounded poll (NaN rows + HLHGAT_DEVERR_BN_WAIT, never
-// numbers from partial statistics).
-unsigned g_poll_limit = 1u << 22;
+// --- one-launch selection: grid size and registers -------------------------
+// The one-launch kernels are taken when the grid is at most half of the
+// chip's resident-workgroup capacity for that kernel
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs / 2), at most 256
+// workgroups (the partials use the flat order) and a thread's rows fit the
+// register budget (RPT <= kMaxRpt).  That sizing is for speed only: the
+// barrier itself assumes nothing about residency (the bounded wait and the
+// finaliser's hand-over above), so a launch beside any other kernels -- the
+// other chain's barrier grid, RCCL, a whole-CU kernel -- completes with the
+// same bits, at worst one wait bound later.
+unsigned g_wait_us = 1000;
 
 int64_t capacity_of(const void* kernel) {
   static auto* cache = new std::vector<std::pair<const void*, int64_t>>();
@@ -1322,7 +1427,7 @@ int64_t capacity_of(const void* kernel) {
   int dev = 0, cus = 0, occ = 0;
   int64_t c = 0;
   // the share of the chip one barrier grid may take: 1 / HLHGAT_BN_COLOCATE
-  // (default 2: two chains' barrier launches resident at once)
+  // (default 2: the two chains' barrier launches usually overlap)
   static const int share = [] {
     const char* e = std::getenv("HLHGAT_BN_COLOCATE");
     const int v = e ? std::atoi(e) : 2;
@@ -1363,33 +1468,6 @@ GridFn fwd_grid_fn(bool vec, int rpt) {
   }
 }
 
-// hlhgat_set_bn_produced(1): the rows produced inside the one-launch
-// BatchNorm.  Off by default: same-box A/B of the replayed config-2 step
-// (tools/ab_step.py, round 4) 2.80 ms with the producer's own launch vs 2.87
-// ms produced in the grid-barrier launch -- the gathers lose the parallelism
-// of their own wide launch inside the co-resident (<= 256 workgroup) grid.
-// Bitwise the same results either way.
-bool& bn_produced_flag() {
-  static bool v = false;
-  return v;
-}
-
-GridFn produced_fn(int prod, int rpt) {
-  switch (rpt * 4 + prod) {
-    case 9: return k_bn_fwd_produced<2, 1>;
-    case 10: return k_bn_fwd_produced<2, 2>;
-    case 17: return k_bn_fwd_produced<4, 1>;
-    case 18: return k_bn_fwd_produced<4, 2>;
-    case 33: return k_bn_fwd_produced<8, 1>;
-    case 34: return k_bn_fwd_produced<8, 2>;
-    case 65: return k_bn_fwd_produced<16, 1>;
-    case 66: return k_bn_fwd_produced<16, 2>;
-    case 129: return k_bn_fwd_produced<32, 1>;
-    case 130: return k_bn_fwd_produced<32, 2>;
-    default: return nullptr;
-  }
-}
-
 // The one-launch kernel for this layout, or nullptr (two launches).
 GridFn pick_grid(const BnLayout& L, bool vec) {
   if (!bn_one_launch() || L.parts > kFlatMax) return nullptr;
@@ -1404,86 +1482,6 @@ GridFn pick_grid(const BnLayout& L, bool vec) {
 
 }  // namespace
 
-
-extern "C" int hlhgat_bn_fwd_produced(int mode, const int64_t* edge_index,
-                                      const int32_t* inc_rowptr, const int32_t* inc_eids,
-                                      int64_t inc_nnz, const float* row_scale, const float* p,
-                                      int64_t ldp, float ca, float cb, const float* z,
-                                      int64_t ldz, float* x, int64_t ldx, int64_t n,
-                                      const int32_t* n_valid, int64_t C, const float* weight,
-                                      const float* bias, float* running_mean,
-                                      float* running_var, int64_t* num_batches_tracked,
-                                      float momentum, float eps, int relu, float* y, int64_t ldy,
-                                      float* save_mean, float* save_invstd, void* workspace,
-                                      int64_t workspace_bytes, void* stream) {
-  HLH_CHECK_ARG(mode == HLHGAT_BN_PRODUCE_EDGE_GATHER || mode == HLHGAT_BN_PRODUCE_NODE_INCIDENCE,
-                "bn_fwd_produced: bad mode %d", mode);
-  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C && ldp >= C &&
-                    ldz >= C,
-                "bn_fwd_produced: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
-  HLH_CHECK_ARG(p && z && x && y && save_mean && save_invstd, "bn_fwd_produced: NULL pointer");
-  const bool edge = mode == HLHGAT_BN_PRODUCE_EDGE_GATHER;
-  HLH_CHECK_ARG(edge ? edge_index != nullptr
-                     : (inc_rowptr && row_scale && (inc_nnz == 0 || inc_eids)),
-                "bn_fwd_produced: missing producer arrays");
-  HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
-                "bn_fwd_produced: workspace too small");
-  const bool vec = bn_vec_ok(C, {ldx, ldy, ldp, ldz}, {x, y, p, z});
-  const BnLayout L = bn_layout(n, C, vec);
-  GridFn f = nullptr;
-  if (vec && bn_one_launch() && bn_produced_flag() && L.parts <= kFlatMax &&
-      L.tiles <= kMaxTiles) {
-    const int rpt = rpt_bucket(L);
-    f = rpt ? produced_fn(edge ? 1 : 2, rpt) : nullptr;
-    const int64_t cap = f ? capacity_of(reinterpret_cast<const void*>(f)) : 0;
-    if ((int64_t)L.parts * L.tiles > 256 || (int64_t)L.parts * L.tiles > cap) f = nullptr;
-  }
-  if (!f) {  // the producer's own launch, then the BatchNorm
-    int rc;
-    if (edge)
-      rc = hlhgat_edge_gather2(edge_index, n, p, ldp, (int)C, nullptr, nullptr, ca, cb, z, ldz, x,
-                               ldx, 0, stream);
-    else
-      rc = hlhgat_poly_step(inc_rowptr, inc_nnz ? inc_eids : nullptr, nullptr, row_scale, n,
-                            inc_nnz, nullptr, nullptr, p, ldp, (int)C, z, ldz, nullptr, 0, nullptr,
-                            0, 1.f, 0.f, 1.f, 1.f, 0.f, 0.f, x, ldx, stream);
-    if (rc != HLHGAT_OK) return rc;
-    return hlhgat_bn_fwd_train(x, ldx, n, n_valid, C, weight, bias, running_mean, running_var,
-                               num_batches_tracked, momentum, eps, relu, y, ldy, save_mean,
-                               save_invstd, workspace, workspace_bytes, stream);
-  }
-  StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
-  s.weight = weight;
-  s.bias = bias;
-  s.running_mean = running_mean;
-  s.running_var = running_var;
-  s.nbt = num_batches_tracked;
-  s.momentum = momentum;
-  s.eps = eps;
-  s.save_mean = save_mean;
-  s.save_invstd = save_invstd;
-  s.out = y;
-  s.ldo = ldy;
-  s.relu = relu;
-  s.poll_limit = g_poll_limit;
-  s.err = hlhgat::device_error_word();
-  HLH_CHECK_ARG(s.err, "bn_fwd_produced: no device error word (%s)", hlhgat_last_error());
-  s.pei = edge_index;
-  s.prow = inc_rowptr;
-  s.peid = inc_eids;
-  s.prs = row_scale;
-  s.pp = p;
-  s.ldp = ldp;
-  s.pz = z;
-  s.ldz = ldz;
-  s.pca = ca;
-  s.pcb = cb;
-  s.xw = x;
-  ProfScope prof(HLHGAT_PROF_BN_FWD, as_stream(stream), 8.0 * (double)n * C, 0.0);
-  launch(f, dim3(L.parts, L.tiles), dim3(kThreads), 0, as_stream(stream), &prof, s);
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
 
 extern "C" int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C) {
   if (n < 0 || C <= 0) return 0;
@@ -1581,8 +1579,7 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
     s.out = y;
     s.ldo = ldy;
     s.relu = relu;
-    s.poll_limit = g_poll_limit;
-    s.err = hlhgat::device_error_word();
+    s.wait_us = g_wait_us;
     HLH_CHECK_ARG(s.err, "bn_fwd_train: no device error word (%s)", hlhgat_last_error());
     // algorithmic bytes: x read once, y written once
     ProfScope prof(HLHGAT_PROF_BN_FWD, as_stream(stream), 8.0 * (double)n * C, 0.0);
@@ -1648,7 +1645,7 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   }
   const unsigned gx = (unsigned)ceil_div(M, (int64_t)64), gy = (unsigned)(N / 64);
   bool fused = proj_bn_fused_flag() && vec && N % 64 == 0 && gy <= (unsigned)kMaxTiles &&
-               gx <= (unsigned)kMaxParts;
+               gx <= (unsigned)kMaxParts && (int64_t)gx * gy <= kMaxSlots;
   if (fused) {
     const int64_t cap = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd));
     fused = (int64_t)gx * gy <= cap;
@@ -1682,6 +1679,7 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   s.part = w.part;
   s.gpart = w.gpart;
   s.count = w.count;
+  s.slots = w.slots;
   s.weight = bn_weight;
   s.bias = bn_bias;
   s.running_mean = running_mean;
@@ -1694,7 +1692,7 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   s.out = y;
   s.ldo = ldy;
   s.relu = relu;
-  s.poll_limit = g_poll_limit;
+  s.wait_us = g_wait_us;
   s.err = hlhgat::device_error_word();
   HLH_CHECK_ARG(s.err, "proj_bn_fwd: no device error word (%s)", hlhgat_last_error());
   // algorithmic: A read once, x and y written once; flops of the projection
@@ -1956,11 +1954,6 @@ extern "C" int hlhgat_bn_sync_bwd_apply(const float* x, int64_t ldx, const float
   return HLHGAT_OK;
 }
 
-extern "C" int hlhgat_set_bn_produced(int on) {
-  bn_produced_flag() = on != 0;
-  return HLHGAT_OK;
-}
-
 extern "C" int hlhgat_set_bn_one_launch(int on) {
   bn_one_launch_flag() = on != 0;
   return HLHGAT_OK;
@@ -1968,13 +1961,33 @@ extern "C" int hlhgat_set_bn_one_launch(int on) {
 
 extern "C" int hlhgat_get_bn_one_launch(void) { return bn_one_launch_flag() ? 1 : 0; }
 
-extern "C" int hlhgat_set_bn_poll_limit(unsigned limit) {
-  g_poll_limit = limit;
+extern "C" int hlhgat_set_bn_wait_us(unsigned wait_us) {
+  g_wait_us = wait_us;
   return HLHGAT_OK;
 }
 
 extern "C" int hlhgat_bn_wait_timeouts(unsigned* out) {
   HLH_CHECK_ARG(out, "bn_wait_timeouts: NULL pointer");
   HLH_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bn_wait_timeouts), sizeof(unsigned)));
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_giveup_log(hlhgat_bn_giveup_t* out, int max, int* logged) {
+  HLH_CHECK_ARG(logged && (max <= 0 || out), "bn_giveup_log: NULL pointer");
+  unsigned n = 0;
+  HLH_CHECK_HIP(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_bn_log_n), sizeof(unsigned)));
+  *logged = (int)n;
+  int k = (int)n < HLHGAT_BN_LOG_MAX ? (int)n : HLHGAT_BN_LOG_MAX;
+  if (k > max) k = max;
+  if (k > 0)
+    HLH_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bn_log), sizeof(hlhgat_bn_giveup_t) * k));
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_giveup_reset(void) {
+  const unsigned z = 0;
+  HLH_CHECK_HIP(hipDeviceSynchronize());
+  HLH_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bn_log_n), &z, sizeof(unsigned)));
+  HLH_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bn_wait_timeouts), &z, sizeof(unsigned)));
   return HLHGAT_OK;
 }

@@ -449,7 +449,8 @@ __global__ __launch_bounds__(kEpThreads) void k_eig_pe(EigArgs a) {
       eig_pe_graph<true>(a, (int)g, n0, n, ep_lds, red, lam, clus);
     else
       eig_pe_graph<false>(a, (int)g, n0, n,
-                          reinterpret_cast<char*>(a.ws + g * a.ws_per_graph), red, lam, clus);
+                          reinterpret_cast<char*>(a.ws + (int64_t)blockIdx.x * a.ws_per_graph),
+                          red, lam, clus);
     __syncthreads();  // the next graph reuses the LDS
   }
 }
@@ -460,11 +461,24 @@ int64_t per_graph_doubles(int64_t max_nodes, int k) {
          (int64_t)kEpSolvers * 5 * n + 8;
 }
 
+// One workgroup per CU (a workgroup holds a whole CU's LDS); graphs beyond
+// the grid are taken in turn by the same workgroups, so the workspace (for
+// graphs too large for the LDS) is one slice per WORKGROUP.  The full chip:
+// the training step's one-launch BatchNorms beside it no longer need their
+// grids resident (bn.hip: a workgroup whose wait runs out hands its rows to
+// the finaliser), so nothing has to be throttled for them.
+int64_t eig_pe_grid(int64_t n_graphs) {
+  int cus = 256, dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return std::max<int64_t>(1, std::min<int64_t>(n_graphs, cus));
+}
+
 }  // namespace
 
 extern "C" int64_t hlhgat_eig_pe_workspace_bytes(int64_t n_graphs, int64_t max_nodes, int k) {
   if (n_graphs < 0 || max_nodes < 0 || k < 2 || k > kEpMaxK) return 0;
-  return (int64_t)sizeof(double) * n_graphs * per_graph_doubles(max_nodes, k);
+  return (int64_t)sizeof(double) * eig_pe_grid(n_graphs) * per_graph_doubles(max_nodes, k);
 }
 
 extern "C" int hlhgat_eig_pe(const int32_t* inc_rowptr, const int32_t* inc_edge,
@@ -501,15 +515,7 @@ extern "C" int hlhgat_eig_pe(const int32_t* inc_rowptr, const int32_t* inc_edge,
   a.ws = reinterpret_cast<double*>(workspace);
   a.ws_per_graph = per_graph_doubles(max_nodes, k);
   a.n_graphs = n_graphs;
-  // at most half the CUs: a workgroup holds a whole CU's LDS, and the
-  // pipeline runs beside the training step, whose one-launch BatchNorm needs
-  // its grid co-resident (a full-chip eig_pe starved it into its barrier
-  // timeout, measured in the config-3 overlap leg); graphs beyond the grid
-  // are taken in turn by the same workgroups
-  int cus = 256, dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t grid = std::min<int64_t>(n_graphs, std::max(1, cus / 2));
+  const int64_t grid = eig_pe_grid(n_graphs);
   hipLaunchKernelGGL(k_eig_pe, dim3((unsigned)grid), dim3(kEpThreads), kEpLdsBytes,
                      as_stream(stream), a);
   HLH_CHECK_LAUNCH();

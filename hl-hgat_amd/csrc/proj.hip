@@ -153,50 +153,6 @@ __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// BatchNorm backward prologue of the fused Linear backward
-// (hlhgat_proj_bwd_bn_defer): G holds dy, the gradient of a BatchNorm (+ReLU)
-// output, and every G element the kernel loads becomes that BatchNorm's input
-// gradient dC = A g + (B (x - mean) + C), g = dy masked by the ReLU output --
-// k_bn_bwd_apply's arithmetic -- so dC is never written to memory.
-// ---------------------------------------------------------------------------
-struct BnPro {
-  const float* x;  // BN input [M][N] (row stride ldx)
-  int64_t ldx;
-  const float* y;  // BN (+ReLU) output for the mask, or NULL
-  int64_t ldy;
-  const float* coef;  // [3][N] (NULL: no prologue)
-  const float* mean;
-  const int32_t* nvalid;
-  int N;
-};
-
-__device__ __forceinline__ int64_t bn_pro_rows(const BnPro& p, int64_t M) {
-  if (!p.nvalid) return M;
-  const int64_t v = (int64_t)p.nvalid[0];
-  return v < M ? v : M;
-}
-
-// dy[m][c .. c+3] -> dC[m][c .. c+3] (m < M, c + 3 < N)
-__device__ __forceinline__ float4 bn_pro4(const BnPro& p, int64_t m, int c, float4 g,
-                                          int64_t n_eff) {
-  const float4 xv = *reinterpret_cast<const float4*>(p.x + m * p.ldx + c);
-  const float4 yv = p.y ? *reinterpret_cast<const float4*>(p.y + m * p.ldy + c) : g;
-  const float4 A = *reinterpret_cast<const float4*>(p.coef + c);
-  const float4 B = *reinterpret_cast<const float4*>(p.coef + p.N + c);
-  const float4 Cc = *reinterpret_cast<const float4*>(p.coef + 2 * p.N + c);
-  const float4 mu = *reinterpret_cast<const float4*>(p.mean + c);
-  float4 o;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    float gg = (&g.x)[v];
-    if (p.y && !((&yv.x)[v] > 0.f)) gg = 0.f;
-    (&o.x)[v] = m >= n_eff ? 0.f
-                           : (&A.x)[v] * gg + ((&B.x)[v] * ((&xv.x)[v] - (&mu.x)[v]) + (&Cc.x)[v]);
-  }
-  return o;
-}
-
-// ---------------------------------------------------------------------------
 // data gradient: dA_b = dC W_b   (reduction over N)
 // ---------------------------------------------------------------------------
 struct BwdDataArgs {
@@ -212,7 +168,6 @@ struct BwdDataArgs {
   int kb[MAXB];
   int tile_start[MAXB + 1];
   int accumulate;
-  BnPro bn;  // fused path only (bn.coef NULL elsewhere)
 };
 
 template <int TM, int TN, bool VEC>
@@ -307,17 +262,7 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
   const int64_t row = m_base + i;
   const bool gval = row < a.M;
   const float* grow = a.G + (gval ? row : 0) * a.ldg;
-  const int64_t bn_neff = a.bn.coef ? bn_pro_rows(a.bn, a.M) : 0;
-  auto load_g = [&](int n0, float4 (&o)[4]) {
-    load_a_chunk(grow, gval, n0, a.N, q, o);
-    if (a.bn.coef && gval) {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int k = n0 + 16 * s + 4 * q;
-        if (k < a.N) o[s] = bn_pro4(a.bn, row, k, o[s], bn_neff);
-      }
-    }
-  };
+  auto load_g = [&](int n0, float4 (&o)[4]) { load_a_chunk(grow, gval, n0, a.N, q, o); };
 
 
   // staging: TN*16 columns x 64 n = TN*256 float4 over 256 threads; thread
@@ -412,14 +357,6 @@ __device__ __forceinline__ void bwd_data_rows_body(const BwdDataArgs& a, int bx,
   const bool gval = row < a.M;
   float4 gc[4];
   load_a_chunk(a.G + (gval ? row : 0) * a.ldg, gval, 0, a.N, q, gc);
-  if (a.bn.coef && gval) {
-    const int64_t bn_neff = bn_pro_rows(a.bn, a.M);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int k = 16 * s + 4 * q;
-      if (k < a.N) gc[s] = bn_pro4(a.bn, row, k, gc[s], bn_neff);
-    }
-  }
   const int ntiles = a.tile_start[a.nb];
   auto tile_of = [&](int t, int& b, int& c_base) {
     b = 0;
@@ -525,7 +462,6 @@ struct BwdWeightArgs {
   int64_t rows_per_split;
   int tiles_n;
   int xcd_map;  // remap (tile, split) so each XCD walks one contiguous range of them
-  BnPro bn;     // fused path only (bn.coef NULL elsewhere)
 };
 
 __global__ __launch_bounds__(256) void k_proj_bwd_weight(BwdWeightArgs a) {
@@ -698,7 +634,6 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
 
   // staging: each tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
   const int sr = threadIdx.x >> 4, sc = (threadIdx.x & 15) * 4;
-  const int64_t bn_neff = a.bn.coef ? bn_pro_rows(a.bn, a.M) : 0;
   auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -707,7 +642,6 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
       const int n = n_base + sc, k = k_base + sc;
       g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
-      if (a.bn.coef && mv && n < a.N) g[u] = bn_pro4(a.bn, m, n, g[u], bn_neff);
       x[u] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -1239,8 +1173,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
                   float* const* dA, const int64_t* ldda, int accumulate_d, float* workspace,
                   int64_t workspace_floats, void* stream,
                   const hlhgat_reduce_desc_t* merge = nullptr,
-                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr,
-                  const hlhgat_bn_bwd_prologue_t* bnp = nullptr) {
+                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr) {
   if (deferred) *deferred = 0;
   const ReduceArgs* prev = nullptr;
   if (merge) {
@@ -1262,24 +1195,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
-  BnPro bn{};
-  if (bnp) {
-    HLH_CHECK_ARG(fuse, "proj_bwd_bn: the BatchNorm prologue needs the fused launch (16-byte "
-                        "aligned operands, N %% 4 == 0, a weight gradient, M > 0)");
-    HLH_CHECK_ARG(bnp->x && bnp->coef && bnp->mean && aligned16(bnp->x) &&
-                      aligned16(bnp->coef) && aligned16(bnp->mean) && bnp->ldx % 4 == 0 &&
-                      bnp->ldx >= N && (!bnp->y || (aligned16(bnp->y) && bnp->ldy % 4 == 0 &&
-                                                    bnp->ldy >= N)),
-                  "proj_bwd_bn: bad BatchNorm prologue operands");
-    bn.x = bnp->x;
-    bn.ldx = bnp->ldx;
-    bn.y = bnp->y;
-    bn.ldy = bnp->ldy;
-    bn.coef = bnp->coef;
-    bn.mean = bnp->mean;
-    bn.nvalid = bnp->n_valid;
-    bn.N = (int)N;
-  }
   if (prev && !fuse) {  // run the merged reduction on its own first
     const int rc = run_reduce(*prev, as_stream(stream));
     if (rc != HLHGAT_OK) return rc;
@@ -1327,7 +1242,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   a.rows_per_split = p.rows_per_split;
   a.tiles_n = p.tiles_n;
   a.xcd_map = weight_xcd_map();
-  a.bn = bn;
   f.n_w = p.tiles_total * p.splits;
 
   BwdDataArgs& d = f.d;
@@ -1337,7 +1251,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   d.G = dC;
   d.ldg = lddc;
   d.accumulate = accumulate_d;
-  d.bn = bn;
   int64_t ktot = 0;
   for (int b = 0; b < nb_d; ++b) ktot += kb_d[b];
   int tnd = ceil_div(M, 16) * ceil_div(ktot, 16) < 4096 ? 1 : 2;  // as hlhgat_proj_bwd_data
@@ -1422,24 +1335,6 @@ extern "C" int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int6
   return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
                        dA, ldda, accumulate_d, workspace, workspace_floats, stream, merge,
                        defer_out, deferred);
-}
-
-extern "C" int hlhgat_proj_bwd_bn_defer(int64_t M, int64_t N, const float* dy, int64_t lddy,
-                                        const hlhgat_bn_bwd_prologue_t* bn, int nb_w,
-                                        const float* const* A, const int64_t* lda,
-                                        const int64_t* kb_w, float* const* dW,
-                                        const int64_t* lddw, float* dbias, int nb_d,
-                                        const float* const* W, const int64_t* ldw,
-                                        const int64_t* kb_d, float* const* dA,
-                                        const int64_t* ldda, int accumulate_d, float* workspace,
-                                        int64_t workspace_floats,
-                                        const hlhgat_reduce_desc_t* merge,
-                                        hlhgat_reduce_desc_t* defer_out, int* deferred,
-                                        void* stream) {
-  HLH_CHECK_ARG(bn, "proj_bwd_bn: NULL prologue");
-  return proj_bwd_impl(M, N, dy, lddy, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
-                       dA, ldda, accumulate_d, workspace, workspace_floats, stream, merge,
-                       defer_out, deferred, bn);
 }
 
 extern "C" int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream) {

@@ -434,3 +434,31 @@ extern "C" int hlhgat_graph_kernel_count(void* graph, const char* name_part, int
   }
   return HLHGAT_OK;
 }
+
+// --- test hook: hold CUs (tests/test_gpu_parity.py::test_bn_one_launch_beside_cu_hog)
+// Workgroups [0, hold) each keep their CU's LDS (dynamic, lds_bytes) for
+// `usec` microseconds of the 100 MHz constant clock, sleeping; the rest exit
+// at once.  Every workgroup exits on its own time bound.
+namespace {
+__global__ __launch_bounds__(64) void k_occupy(int hold, unsigned usec) {
+  extern __shared__ float occ_lds[];
+  if ((int)blockIdx.x >= hold) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t lim = (uint64_t)usec * 100u;
+  if (threadIdx.x == 0) occ_lds[0] = 0.f;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < lim) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
+
+extern "C" int hlhgat_test_occupy(int workgroups, int hold, int lds_bytes, unsigned usec,
+                                  void* stream) {
+  HLH_CHECK_ARG(workgroups >= 1 && workgroups <= 65536 && hold >= 0 && lds_bytes >= 0 &&
+                    lds_bytes <= 160 * 1024 && usec <= 2000000u,
+                "test_occupy: bad arguments");
+  HLH_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_occupy),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+  launch(k_occupy, dim3((unsigned)workgroups), dim3(64), (uint32_t)lds_bytes, as_stream(stream),
+         nullptr, hold, usec);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}

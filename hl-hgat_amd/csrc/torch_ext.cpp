@@ -147,6 +147,12 @@ hlhgat_hodge_factor_t make_factor(at::TensorList f, int64_t n_nodes, int64_t n_e
 // earlier on that stream still holds its address, and a replay must not write
 // BN counters into memory the caching allocator has handed to another tensor.
 // (Sizes grow geometrically, so at most a handful are ever retired.)
+// The block is allocated FROM THE KEYED STREAM's pool and zero-filled on that
+// stream: a block taken from another stream's pool (the current one, when
+// TrainStep reserves a workspace for its capture streams) may still be written
+// by kernels queued on that stream after the fill, which would leave counter
+// words non-zero and every later launch on the workspace waiting for an
+// arrival count it can never reach.
 Tensor bn_workspace_for(void* stream, int device, int64_t need) {
   static auto* cache = new std::unordered_map<uintptr_t, Tensor>();  // leaked: outlives HIP teardown
   static auto* retired = new std::vector<Tensor>();
@@ -158,9 +164,15 @@ Tensor bn_workspace_for(void* stream, int device, int64_t need) {
       bytes = std::max<int64_t>(bytes, 2 * it->second.numel());
       retired->push_back(it->second);
     }
-    Tensor ws = at::empty({bytes}, at::TensorOptions()
-                                        .device(at::kCUDA, (c10::DeviceIndex)device)
-                                        .dtype(at::kByte));
+    Tensor ws;
+    {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(
+          c10::hip::getStreamFromExternalMasqueradingAsCUDA(
+              reinterpret_cast<hipStream_t>(stream), (c10::DeviceIndex)device));
+      ws = at::empty({bytes}, at::TensorOptions()
+                                  .device(at::kCUDA, (c10::DeviceIndex)device)
+                                  .dtype(at::kByte));
+    }
     chk(hlhgat_zero_fill(ws.data_ptr(), (size_t)ws.numel(), stream), "zero_fill");
     (*cache)[key] = ws;
   }
@@ -459,7 +471,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
                    const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
                    const std::vector<int64_t>& kbd, std::vector<float*>& dA,
                    const std::vector<int64_t>& ldda, void* s, int acc_d = 0,
-                   bool force_defer = false, const hlhgat_bn_bwd_prologue_t* bnp = nullptr) {
+                   bool force_defer = false) {
   const int nbw = (int)A.size(), nbd = (int)W.size();
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
@@ -480,15 +492,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   }
   hlhgat_reduce_desc_t out;
   int deferred = 0;
-  if (bnp)
-    chk(hlhgat_proj_bwd_bn_defer(M, N, G.data_ptr<float>(), ld_of(G), bnp, nbw, A.data(),
-                                 lda.data(), kbw.data(), dW.data(), lddw.data(), db, nbd,
-                                 W.data(), ldw.data(), kbd.data(), dA.data(), ldda.data(), acc_d,
-                                 ws.data_ptr<float>(), wsf, merge ? &prev.desc : nullptr,
-                                 defer ? &out : nullptr, &deferred, s),
-        "proj_bwd_bn");
-  else
-    chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
+  chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
                               kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(),
                               kbd.data(), dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(),
                               wsf, merge ? &prev.desc : nullptr, defer ? &out : nullptr,
@@ -585,64 +589,8 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
   return dx;
 }
 
-// BatchNorm backward folded into the Linear backward that consumes its dx
-// (hlhgat_proj_bwd_bn_defer): only the reduction launches here; the consumer
-// forms dx where it loads it.  `ok` = the consumer takes the fused launch.
-// Off by default: measured in the replayed config-2 step (round 4), the
-// prologue's extra x / y / coefficient loads inside the fused Linear
-// backward cost more (k_proj_bwd_fused 1.32 -> 1.96 ms per step) than the 28
-// apply launches it removes; kept as an option, bitwise either way.
-bool& bn_fold_flag() {
-  static bool v = false;
-  return v;
-}
-void set_bn_fold(bool on) { bn_fold_flag() = on; }
-
 inline bool al4(const void* p, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(p) & 15) == 0 && ld % 4 == 0;
-}
-
-struct BnFold {
-  bool on = false;
-  Tensor coef;
-  hlhgat_bn_bwd_prologue_t pro{};
-};
-
-// on the fold: dw / db filled, returns true (G stays dy); else false
-bool bn_backward_fold(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
-                      const Tensor& mean, const Tensor& invstd, bool need_w, bool need_b,
-                      Tensor& dw, Tensor& db, const Tensor* b_param, const Tensor& valid,
-                      bool ok, BnFold& f) {
-  f.on = false;
-  const int64_t n = x.size(0), C = x.size(1);
-  ok = ok && bn_fold_flag() && n > 0 && C % 4 == 0 && dy.dim() == 2 && dy.stride(1) == 1 &&
-       al4(dy.data_ptr(), dy.stride(0)) && x.stride(1) == 1 && al4(x.data_ptr(), x.stride(0)) &&
-       (!has(y) || (y->stride(1) == 1 && al4(y->data_ptr(), y->stride(0)))) &&
-       al4(mean.data_ptr(), 0);
-  if (!ok) return false;
-  dw = (need_w && has(w)) ? grad_like(*w) : Tensor();
-  db = need_b ? ((b_param && b_param->defined()) ? grad_like(*b_param)
-                                                 : at::empty({C}, x.options()))
-              : Tensor();
-  f.coef = at::empty({3 * C}, x.options());
-  Tensor ws = bn_workspace(x, n, C);
-  chk(hlhgat_bn_bwd_reduce(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
-                           dy.data_ptr<float>(), ld_of(dy), n,
-                           valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
-                           mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                           f.coef.data_ptr<float>(), dw.defined() ? dw.data_ptr<float>() : nullptr,
-                           db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(),
-                           ws.numel(), stream_of(x)),
-      "bn_bwd_reduce");
-  f.pro.x = x.data_ptr<float>();
-  f.pro.ldx = ld_of(x);
-  f.pro.y = fptr(y);
-  f.pro.ldy = has(y) ? ld_of(*y) : 0;
-  f.pro.coef = f.coef.data_ptr<float>();
-  f.pro.mean = mean.data_ptr<float>();
-  f.pro.n_valid = valid.defined() ? valid.data_ptr<int32_t>() : nullptr;
-  f.on = true;
-  return true;
 }
 
 // Two-stream fork inside one autograd node: the node (current) stream and a
@@ -894,21 +842,12 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
     std::vector<int64_t> lddw;
     float* db = nullptr;
   } wdef;  // weight gradient deferred into the data gradient's launch
-  BnFold fold;
   if (bn_mode > 0) {
     const OptT bn_y = bn_mode == 2 ? OptT(yout) : OptT();
     OptT w = bn_w.defined() ? OptT(bn_w) : OptT();
-    // the fold needs the one fused Linear-backward launch below
-    bool ok = (need_w || need_b) && M > 0 && (!nd.x || fused_bwd_flag()) && dout % 4 == 0;
-    for (int64_t k = 0; k < K && ok; ++k)
-      ok = al4(Ap[k], lda[k]) && Cin % 4 == 0 && al4(W[k].data_ptr(), W[k].stride(0)) &&
-           W[k].stride(1) == 1;
-    if (!bn_backward_fold(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
-                          &bn_b, valid, ok, fold))
-      G = bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
-                      nullptr, &bn_b, valid);
+    G = bn_backward(pre, bn_y, G, w, mean, invstd, nd.bn_w, nd.bn_b, out.dbn_w, out.dbn_b,
+                    nullptr, &bn_b, valid);
   }
-  const hlhgat_bn_bwd_prologue_t* bnp = fold.on ? &fold.pro : nullptr;
   if (need_w || need_b) {
     std::vector<Tensor> dW(K);
     std::vector<float*> dWp(K);
@@ -928,7 +867,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
       std::vector<int64_t> noL;
       std::vector<float*> noD;
       proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, noW, noL,
-                    noL, noD, noL, s, 0, false, bnp);
+                    noL, noD, noL, s, 0, false);
     } else {
       for (auto& tt : dW) tt.zero_();
       if (need_b) db.zero_();
@@ -950,7 +889,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
       }
       if (!wdef.dWp.empty())
         proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s, 0,
-                      false, bnp);
+                      false);
       else
         proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
       if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
@@ -1165,7 +1104,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
                      bool need_w, bool need_b, const std::vector<bool>& need_a, Tensor& dW,
                      Tensor& db, std::vector<Tensor>& dAs, const Tensor* b_param = nullptr,
                      const std::vector<Tensor>* dA_into = nullptr, int into_acc = 1,
-                     bool force_defer = false, const hlhgat_bn_bwd_prologue_t* bnp = nullptr) {
+                     bool force_defer = false) {
   Tensor G = rows2d(Gin);
   const int64_t M = G.size(0), N = G.size(1);
   const int nb = (int)As.size();
@@ -1213,7 +1152,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
         std::vector<int64_t> noL;
         std::vector<float*> noD;
         proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, noW,
-                      noL, noL, noD, noL, s, 0, false, bnp);
+                      noL, noL, noD, noL, s, 0, false);
       }
     } else {
       gw.zero_();
@@ -1248,7 +1187,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
       const int acc = into ? into_acc : 0;
       if (!wAp.empty())
         proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, acc,
-                      force_defer, bnp);
+                      force_defer);
       else
         proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, acc);
     }
@@ -1691,11 +1630,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       h1s = at::empty({E, de}, xt.options());
     }
     Ys.record_stream(fk.main);  // read by the node side's gather on main
-    // the hidden layer's input rows are produced inside its BatchNorm launch
-    // (hlhgat_bn_fwd_produced): edge rows h1_s = Qs + (P2[i] + P2[j]) / 2,
-    // node rows h1_t = Qt + rD * |B1| P1
+    // the hidden layer's input rows: edge rows h1_s = Qs + (P2[i] + P2[j]) / 2
+    // (hlhgat_edge_gather2), node rows h1_t = Qt + rD * |B1| P1 (hlhgat_poly_step
+    // over the binary incidence), then its BatchNorm
     struct Producer {
-      int mode;
+      bool edge;
       const float* p;
       int64_t ldp;
       const float* z;
@@ -1708,23 +1647,20 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
       const BnState bst{p[2], p[3], p[4], p[5], p[6], m1, e1, valid};
       if (pr) {
         const int64_t n = h1.size(0), C = h1.size(1);
-        o.a1 = at::empty({n, C}, h1.options());
-        o.m1 = at::empty({C}, h1.options());
-        o.i1 = at::empty({C}, h1.options());
-        Tensor ws = bn_workspace(h1, n, C);
-        int64_t* nbt = has(bst.nbt) ? bst.nbt->data_ptr<int64_t>() : nullptr;
-        chk(hlhgat_bn_fwd_produced(
-                pr->mode, ei.data_ptr<int64_t>(), rowptr.data_ptr<int>(),
-                E ? eids.data_ptr<int>() : nullptr, 2 * E, rD.data_ptr<float>(), pr->p, pr->ldp,
-                pr->ca, pr->cb, pr->z, pr->ldz, h1.data_ptr<float>(), ld_of(h1), n,
-                iptr(bst.valid), C, fptr(bst.w), fptr(bst.b), mfptr(bst.rm), mfptr(bst.rv), nbt,
-                (float)bst.momentum, (float)bst.eps, 1, o.a1.data_ptr<float>(), ld_of(o.a1),
-                o.m1.data_ptr<float>(), o.i1.data_ptr<float>(), ws.data_ptr(), ws.numel(),
-                stream_of(h1)),
-            "bn_fwd_produced");
-      } else {
-        o.a1 = bn_forward(h1, bst, true, o.m1, o.i1);
+        if (pr->edge)
+          chk(hlhgat_edge_gather2(ei.data_ptr<int64_t>(), n, pr->p, pr->ldp, (int)C, nullptr,
+                                  nullptr, pr->ca, pr->cb, pr->z, pr->ldz, h1.data_ptr<float>(),
+                                  ld_of(h1), 0, stream_of(h1)),
+              "edge_gather2");
+        else
+          chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr,
+                               nullptr, rD.data_ptr<float>(), n, 2 * E, nullptr, nullptr, pr->p,
+                               pr->ldp, (int)C, pr->z, pr->ldz, nullptr, 0, nullptr, 0, 1.f, 0.f,
+                               1.f, 1.f, 0.f, 0.f, h1.data_ptr<float>(), ld_of(h1),
+                               stream_of(h1)),
+              "poly_step");
       }
+      o.a1 = bn_forward(h1, bst, true, o.m1, o.i1);
       Tensor W3 = p[7].stride(1) == 1 ? p[7] : p[7].contiguous();
       o.y = linear_bn_forward({o.a1}, W3, p[8],
                               BnState{p[9], p[10], p[11], p[12], p[13], m4, e4, valid}, true,
@@ -1748,12 +1684,12 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     fk.main_waits_side();  // main needs Ys
     {  // edge side: h1_s = Qs + (P2[i] + P2[j]) / 2, then its MLP
       TStreamGuard g(fk.side);
-      const Producer pr{HLHGAT_BN_PRODUCE_EDGE_GATHER, Yt.data_ptr<float>() + dn, dn + de,
+      const Producer pr{true, Yt.data_ptr<float>() + dn, dn + de,
                         Ys.data_ptr<float>(), de + dn, 0.5f, 0.5f};
       side(pe, h1s, mom1e, eps1e, mom4e, eps4e, valid_s, te, E > 0 ? &pr : nullptr);
     }
     {  // node side: h1_t = Qt + rD * |B1| P1, then its MLP
-      const Producer pr{HLHGAT_BN_PRODUCE_NODE_INCIDENCE, Ys.data_ptr<float>() + de, de + dn,
+      const Producer pr{false, Ys.data_ptr<float>() + de, de + dn,
                         Yt.data_ptr<float>(), dn + de, 1.f, 1.f};
       side(pn, h1t, mom1n, eps1n, mom4n, eps4n, valid_t, tn, N > 0 ? &pr : nullptr);
     }
@@ -1822,22 +1758,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
              y = sv[o0 + 5], m4 = sv[o0 + 6], i4 = sv[o0 + 7];
       Tensor dg4, dbe4, dg1, dbe1, dW3, db3;
       Tensor gyc = gy.defined() ? gy : at::zeros_like(y);
-      // h2's BatchNorm backward folded into W3's backward when it takes the
-      // fused launch (hlhgat_proj_bwd_bn_defer)
-      const bool ok = (need(ctx, P + 7) || need(ctx, P + 8)) && h2.size(0) > 0 &&
-                      fused_bwd_flag() && al4(a1.data_ptr(), ld_of(a1)) &&
-                      a1.size(1) % 4 == 0 && W3.stride(1) == 1 &&
-                      al4(W3.data_ptr(), W3.stride(0));
-      BnFold fold;
-      Tensor dh2 = gyc;
-      if (!bn_backward_fold(h2, OptT(y), rows2d(gyc), OptT(g4), m4, i4, need(ctx, P + 9),
-                            need(ctx, P + 10), dg4, dbe4, &be4, valid, ok, fold))
-        dh2 = bn_backward(h2, OptT(y), gyc, OptT(g4), m4, i4, need(ctx, P + 9),
-                          need(ctx, P + 10), dg4, dbe4, nullptr, &be4, valid);
+      Tensor dh2 = bn_backward(h2, OptT(y), gyc, OptT(g4), m4, i4, need(ctx, P + 9),
+                               need(ctx, P + 10), dg4, dbe4, nullptr, &be4, valid);
       std::vector<Tensor> da1;
-      linear_backward(fold.on ? rows2d(gyc) : dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8),
-                      {true}, dW3, db3, da1, &b3, nullptr, 1, false,
-                      fold.on ? &fold.pro : nullptr);
+      linear_backward(dh2, {a1}, W3, need(ctx, P + 7), need(ctx, P + 8), {true}, dW3, db3, da1,
+                      &b3, nullptr, 1, false);
       bn_backward(h1, OptT(a1), da1[0], OptT(g1), m1, i1, need(ctx, P + 2), need(ctx, P + 3), dg1,
                   dbe1, &dest, &be1, valid);
       out[P + 2] = dg1;
@@ -2453,7 +2378,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bwd", &set_fused_bwd);
-  m.def("set_bn_fold", &set_bn_fold);
   m.def("set_tap", &set_tap);
   m.def("take_tap", &take_tap);
   m.def("join_capture_streams", &join_capture_streams);

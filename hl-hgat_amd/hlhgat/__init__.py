@@ -13,8 +13,12 @@ from .hodge_cheb_conv import (HL_filter, HodgeChebConv, HodgeLaguerreConv,  # no
 from .hodge_dataset import (Batch, BoundaryOperator, PairData, adj2par1, collate,  # noqa: F401,E402
                             degree)
 from .hodge_st_model import (HL_HGCNN_CIFAR10SP_dense_int3_attpool,  # noqa: F401,E402
-                             HL_HGCNN_pepfunc_dense_int3_attpool, HL_HGCNN_TSP_dense_int3_pyr,
-                             HL_HGCNN_zinc_dense_int3_pyr)
+                             HL_HGCNN_CIFAR10SP_dense_int3_pyr, HL_HGCNN_pepfunc_dense_int3_pyr,
+                             HL_HGCNN_TSP_dense_int3_pyr, HL_HGCNN_zinc_dense_int3_attpool,
+                             HL_HGCNN_zinc_dense_int3_pyr, HL_HGCNN_zinc_dense_poolint3_pyr)
+# the peptides training script's own head (BASELINE config 4), which shadows
+# the library class of that name there (hodge_st_model's)
+from .main_pepfunc import HL_HGCNN_pepfunc_dense_int3_attpool  # noqa: F401,E402
 from .nn import BatchNorm, Linear, Sequential, global_mean_pool  # noqa: F401,E402
 
 __version__ = "0.1.0"

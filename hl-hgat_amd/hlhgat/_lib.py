@@ -66,14 +66,6 @@ SIGNATURES = {
                                   c_i64, c_vp]),
     "hlhgat_bn_bwd_reduce": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp]),
-    "hlhgat_proj_bwd_bn_defer": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp,
-                                         c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
-                                         c_vp, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
-    "hlhgat_set_bn_produced": (c_i32, [c_i32]),
-    "hlhgat_bn_fwd_produced": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_f32,
-                                       c_f32, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp,
-                                       c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_i32, c_vp, c_i64,
-                                       c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_eig_pe_workspace_bytes": (c_i64, [c_i64, c_i64, c_i32]),
     "hlhgat_eig_pe": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp,
                               c_i64, c_vp, c_vp, c_i64, c_vp]),
@@ -102,7 +94,10 @@ SIGNATURES = {
     "hlhgat_proj_bn_fused_capacity": (c_i32, [P_i64]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
     "hlhgat_get_bn_one_launch": (c_i32, []),
-    "hlhgat_set_bn_poll_limit": (c_i32, [C.c_uint32]),
+    "hlhgat_set_bn_wait_us": (c_i32, [C.c_uint32]),
+    "hlhgat_bn_giveup_log": (c_i32, [c_vp, c_i32, c_vp]),
+    "hlhgat_bn_giveup_reset": (c_i32, []),
+    "hlhgat_test_occupy": (c_i32, [c_i32, c_i32, c_i32, C.c_uint32, c_vp]),
     "hlhgat_device_errors": (c_i32, [c_vp]),
     "hlhgat_clear_device_errors": (c_i32, []),
     "hlhgat_bn_wait_timeouts": (c_i32, [c_vp]),
@@ -158,10 +153,18 @@ SIGNATURES = {
 # constants from include/hlhgat.h
 POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
-DEVERR_BN_WAIT = 1
+DEVERR_BN_STATE = 1
+BN_LOG_MAX = 64
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
 PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD, PROF_PROJ_BN = 4, 5, 6, 7
 MAX_BLOCKS = 16
+
+
+class BnGiveup(C.Structure):
+    """hlhgat_bn_giveup_t (include/hlhgat.h): one give-up of a one-launch
+    BatchNorm workgroup, as it recorded it."""
+    _fields_ = [(f, C.c_uint32) for f in ("kernel", "tile", "block", "total", "arrivals", "gen0",
+                                          "gen_seen", "wait_us", "outcome")]
 
 
 class HaloDesc(C.Structure):

@@ -18,8 +18,10 @@ from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
 from .nn import BatchNorm, Sequential, run_mlp_stack
 
-__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_TSP_dense_int3_pyr",
-           "HL_HGCNN_CIFAR10SP_dense_int3_attpool", "HL_HGCNN_pepfunc_dense_int3_attpool",
+__all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_pepfunc_dense_int3_pyr",
+           "HL_HGCNN_CIFAR10SP_dense_int3_pyr", "HL_HGCNN_zinc_dense_poolint3_pyr",
+           "HL_HGCNN_TSP_dense_int3_pyr", "HL_HGCNN_CIFAR10SP_dense_int3_attpool",
+           "HL_HGCNN_zinc_dense_int3_attpool", "HL_HGCNN_pepfunc_dense_int3_attpool",
            "segment_ptr", "mean_pool_sorted"]
 
 
@@ -80,14 +82,18 @@ def _sink(block, dt, ds, width):
     block.module_4._hlhgat_out = ds.sink(width)
 
 
-class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
-    """ZINC regression head (lib/Hodge_ST_Model.py:544-646): HL_init_conv,
-    then per block NEInt{i}{j} (NodeEdgeInt on the dense concatenation) and
-    NEConv{i}{j} (Laguerre on L0 and L1), mean readout, MLP."""
+class _PyrHead(nn.Module):
+    """The dense pyramid heads without pooling (lib/Hodge_ST_Model.py:307-407
+    pepfunc, :544-646 ZINC, :858-955 CIFAR10SP): HL_init_conv, then per block
+    NEInt{i}{j} (NodeEdgeInt on the dense concatenation) and NEConv{i}{j}
+    (Laguerre on L0 and L1), mean readout, MLP.  They differ only in the
+    initial convs' order (init_K: K, or 1 for CIFAR10SP :870-875), the degree
+    (deg_eps: degree + 1e-6 in pepfunc :385 and CIFAR10SP :935, the bare
+    degree in ZINC :624) and NodeEdgeInt's attention mix l (unused by its value
+    path; CIFAR10SP :889)."""
 
-    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
-                 K=2, node_dim=21, edge_dim=3, num_classes=1, dropout_ratio=0.0,
-                 dropout_ratio_mlp=0.0, keig=7):
+    def __init__(self, channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                 dropout_ratio, dropout_ratio_mlp, keig, init_K, deg_eps, nei_l=0.9):
         super().__init__()
         self.channels = channels
         self.filters = filters
@@ -95,12 +101,14 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         self.node_dim = node_dim + keig
         self.edge_dim = edge_dim + keig
         self.initial_channel = self.filters[0]
-        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, K,
+        self._deg_eps = deg_eps
+        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, init_K,
                                       dropout_ratio)
         gcn_insize = self.initial_channel
         for i, gcn_outsize in enumerate(self.filters):
             for j in range(self.channels[i]):
-                setattr(self, "NEInt{}{}".format(i, j), NodeEdgeInt(d=gcn_insize, dv=gcn_outsize))
+                setattr(self, "NEInt{}{}".format(i, j),
+                        NodeEdgeInt(d=gcn_insize, dv=gcn_outsize, l=nei_l))
                 setattr(self, "NEConv{}{}".format(i, j),
                         _hl_block(gcn_outsize, gcn_outsize, gcn_outsize, K, dropout_ratio))
                 gcn_insize = gcn_outsize + gcn_insize
@@ -145,6 +153,8 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
                 d = degree(data.edge_index.view(-1), num_nodes=n_t)
                 if valid_t is not None:  # static-shape padding rows: unit degree, no 1/0
                     d = d.masked_fill(~valid_t, 1.0)
+            if self._deg_eps:
+                d = d + self._deg_eps
             if not x_t.is_cuda:
                 return p1, d, False
             launched = launched or getattr(data.edge_index, "_hlhgat_incidence", None) is None
@@ -202,6 +212,134 @@ class HL_HGCNN_zinc_dense_int3_pyr(nn.Module):
         if if_final_layer:
             return x, y
         return y
+
+
+class HL_HGCNN_zinc_dense_int3_pyr(_PyrHead):
+    """ZINC regression head (lib/Hodge_ST_Model.py:544-646; BASELINE configs
+    1-2): degree without the 1e-6 (:624)."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=21, edge_dim=3, num_classes=1, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, keig=7):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, keig, init_K=K, deg_eps=0.0)
+
+
+class HL_HGCNN_pepfunc_dense_int3_pyr(_PyrHead):
+    """Peptides-func pyramid head (lib/Hodge_ST_Model.py:307-407): the ZINC
+    structure with peptides widths and degree + 1e-6 (:385)."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=9, edge_dim=3, num_classes=10, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, keig=20):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, keig, init_K=K, deg_eps=1e-6)
+
+
+class HL_HGCNN_CIFAR10SP_dense_int3_pyr(_PyrHead):
+    """CIFAR10 superpixel pyramid head (lib/Hodge_ST_Model.py:858-955): K=1
+    initial convs (:870-875), NodeEdgeInt(l=l) (:889), degree + 1e-6 (:935)."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=5, edge_dim=4, num_classes=10, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, l=0.9, keig=10):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, keig, init_K=1, deg_eps=1e-6,
+                         nei_l=l)
+
+
+class HL_HGCNN_zinc_dense_poolint3_pyr(nn.Module):
+    """ZINC head with the interaction AFTER the convs of a level
+    (lib/Hodge_ST_Model.py:649-749): per level i, NEConv{i}{j} runs the
+    Laguerre convs on the dense concatenation itself (width gcn_insize ->
+    gcn_outsize) and appends its outputs, then ONE NEInt{i} mixes the whole
+    concatenation and appends its outputs too; readout of the last NEInt's
+    outputs.  Degree without the 1e-6 (:729)."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=21, edge_dim=3, num_classes=1, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, keig=7):
+        super().__init__()
+        self.channels = channels
+        self.filters = filters
+        self.mlp_channels = mlp_channels
+        self.node_dim = node_dim + keig
+        self.edge_dim = edge_dim + keig
+        self.initial_channel = self.filters[0]
+        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, K,
+                                      dropout_ratio)
+        gcn_insize = self.initial_channel
+        for i, gcn_outsize in enumerate(self.filters):
+            for j in range(self.channels[i]):
+                setattr(self, "NEConv{}{}".format(i, j),
+                        _hl_block(gcn_insize, gcn_insize, gcn_outsize, K, dropout_ratio))
+                gcn_insize = gcn_outsize + gcn_insize
+            setattr(self, "NEInt{}".format(i), NodeEdgeInt(d=gcn_insize, dv=gcn_outsize))
+            gcn_insize = gcn_outsize + gcn_insize
+        mlp_insize = self.filters[-1] * 2
+        for i, mlp_outsize in enumerate(mlp_channels):
+            setattr(self, "mlp%d" % i, nn.Sequential(
+                Linear(mlp_insize, mlp_outsize), nn.BatchNorm1d(mlp_outsize), nn.ReLU(),
+                nn.Dropout(dropout_ratio_mlp)))
+            mlp_insize = mlp_outsize
+        self.out = Linear(mlp_insize, num_classes)
+
+    def forward(self, data, device="cuda:0"):
+        x_s, edge_index_s, edge_weight_s = data.x_s, data.edge_index_s, data.edge_weight_s
+        x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
+        width = self.initial_channel + sum((c + 1) * f for c, f in zip(self.channels, self.filters))
+        dense = x_t.is_cuda and x_t.dim() == 2 and ops.DENSE_SLAB
+        if dense:
+            dt = ops.DenseConcat(x_t.size(0), width, x_t)
+            ds = ops.DenseConcat(x_s.size(0), width, x_s)
+            _sink(self.HL_init_conv, dt, ds, self.initial_channel)
+        n_t, n_s = x_t.shape[0], x_s.shape[0]
+        x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
+                                     edge_weight_s)
+        if dense:
+            dt.append(x_t)
+            ds.append(x_s)
+        x_s0, x_t0 = x_s, x_t
+        # par_1 and D from the same edge_index at every level (:728-729): once;
+        # degree sized by N_t (the reference's max(index)+1 equals it whenever
+        # its 1/D broadcast over x_t rows does not fail)
+        par_1 = adj2par1(data.edge_index, n_t, n_s)
+        D = getattr(data, "deg_t", None)
+        if D is None or D.device != x_t.device or D.numel() != n_t:
+            D = degree(data.edge_index.view(-1), num_nodes=n_t)
+            valid_t = getattr(data, "valid_mask_t", None)
+            if valid_t is not None:
+                D = D.masked_fill(~valid_t, 1.0)
+        for i, _ in enumerate(self.channels):
+            for j in range(self.channels[i]):
+                conv = getattr(self, "NEConv{}{}".format(i, j))
+                if dense:
+                    x_t0, x_s0 = dt.view(), ds.view()
+                    _sink(conv, dt, ds, self.filters[i])
+                x_t, x_s = conv(x_t0, edge_index_t, edge_weight_t, x_s0, edge_index_s,
+                                edge_weight_s)
+                if dense:
+                    dt.append(x_t)
+                    ds.append(x_s)
+                else:
+                    x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                    x_s0 = torch.cat([x_s0, x_s], dim=-1)
+            neint = getattr(self, "NEInt{}".format(i))
+            if dense:
+                x_t0, x_s0 = dt.view(), ds.view()
+                neint._hlhgat_gsink = (dt.grad_sink(), ds.grad_sink())
+            x_t, x_s = neint(x_t0, x_s0, par_1, D)
+            if dense:
+                dt.append(x_t)
+                ds.append(x_s)
+            else:
+                x_t0 = torch.cat([x_t0, x_t], dim=-1)
+                x_s0 = torch.cat([x_s0, x_s], dim=-1)
+        x = mean_pool_cat([(x_s, data.num_edge1, getattr(data, "seg_ptr_s", None)),
+                           (x_t, data.num_node1, getattr(data, "seg_ptr_t", None))])
+        x = run_mlp_stack([getattr(self, "mlp%d" % i) for i in range(len(self.mlp_channels))],
+                          [x])
+        return ops.linear_blocks([x], self.out.weight, self.out.bias)
 
 
 class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
@@ -326,10 +464,17 @@ def _valid_rows(x: torch.Tensor, n_valid) -> torch.Tensor:
 class _AttPoolHead(nn.Module):
     """Shared body of the attention-pooling heads (two MLGC levels, ``datas``
     = [fine batch with the cluster of each node / edge in feature column 0,
-    coarse batch]).  att_every_level: NEAtt{i} after every level on the dense
-    concatenation (main_pepfunc...:133-137); otherwise one NEAtt at pool_loc on
-    the level's last block output, normalised by its batch max
-    (lib/Hodge_ST_Model.py:1058-1064)."""
+    coarse batch]).  att_mode:
+      "every": NEAtt{i} (sigmoid) after every level on the dense
+        concatenation, which it scales (main_pepfunc...:133-137);
+      "concat": one NEAtt at pool_loc (sigmoid) on the dense concatenation,
+        which it scales before pooling (lib/Hodge_ST_Model.py:223-226,276-280);
+      "block": one NEAtt at pool_loc (ReLU) on the level's last block output,
+        which it scales (the dense concatenation is pooled unscaled), divided
+        by its batch max when att_max_norm (CIFAR10SP :1058-1064; ZINC
+        :462-465,515-519 does not divide).
+    init_K: the initial convs' order (1, or K for ZINC :425-430); deg_eps: the
+    1e-6 added to the degree (0 for ZINC :504)."""
 
     # the reference builds NEAtt{i} for every level but uses only the pool_loc
     # one in this mode: those parameters get no gradient, so DDP must look for
@@ -339,12 +484,14 @@ class _AttPoolHead(nn.Module):
     @property
     def forward_collectives(self) -> bool:
         """The pool_loc attention is divided by its batch max over every rank
-        (distributed.global_max) when it is not applied at every level."""
-        return not self.att_every_level
+        (distributed.global_max)."""
+        return self.att_mode == "block" and self.att_max_norm
 
     def __init__(self, channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
-                 dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, att_every_level):
+                 dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, att_mode,
+                 att_max_norm=True, init_K=1, deg_eps=1e-6):
         super().__init__()
+        assert att_mode in ("every", "concat", "block")
         self.channels = channels
         self.filters = filters
         self.mlp_channels = mlp_channels
@@ -352,8 +499,11 @@ class _AttPoolHead(nn.Module):
         self.edge_dim = edge_dim + keig
         self.initial_channel = self.filters[0]
         self.pool_loc = pool_loc
-        self.att_every_level = att_every_level
-        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, 1,
+        self.att_mode = att_mode
+        self.att_every_level = att_mode == "every"
+        self.att_max_norm = att_max_norm
+        self._deg_eps = deg_eps
+        self.HL_init_conv = _hl_block(self.node_dim, self.edge_dim, self.initial_channel, init_K,
                                       dropout_ratio)
         gcn_insize = self.initial_channel
         for i, gcn_outsize in enumerate(self.filters):
@@ -362,10 +512,10 @@ class _AttPoolHead(nn.Module):
                 setattr(self, "NEConv{}{}".format(i, j),
                         _hl_block(gcn_outsize, gcn_outsize, gcn_outsize, K, dropout_ratio))
                 gcn_insize = gcn_insize + gcn_outsize
-            if att_every_level:
+            if att_mode == "every" or (att_mode == "concat" and i == self.pool_loc):
                 setattr(self, "NEAtt{}".format(i),
                         NodeEdgeInt(d=gcn_insize, dv=gcn_outsize, only_att=True, l=l))
-            elif i == self.pool_loc:
+            elif att_mode == "block" and i == self.pool_loc:
                 setattr(self, "NEAtt{}".format(i),
                         NodeEdgeInt(d=gcn_outsize, dv=gcn_outsize, only_att=True,
                                     sigma=nn.ReLU(), l=l))
@@ -392,7 +542,7 @@ class _AttPoolHead(nn.Module):
         x_t0, x_s0 = x_t, x_s
         k = 0
         par_1 = adj2par1(d0.edge_index, x_t0.shape[0], x_s0.shape[0])
-        D = degree(d0.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
+        D = degree(d0.edge_index.view(-1), num_nodes=x_t0.shape[0]) + self._deg_eps
         att_t = att_s = None
         dense = x_t.is_cuda and ops.DENSE_SLAB
         for i, _ in enumerate(self.channels):
@@ -423,18 +573,21 @@ class _AttPoolHead(nn.Module):
                     x_s0 = torch.cat([x_s0, x_s], dim=-1)
             if dense:
                 x_t0, x_s0 = dt.view(), ds.view()
-            if self.att_every_level:
+            if self.att_mode == "every" or (self.att_mode == "concat" and i == self.pool_loc):
                 att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t0, x_s0, par_1, D)
                 x_t0 = x_t0 * att_t
                 x_s0 = x_s0 * att_s
             if i == self.pool_loc:
-                if not self.att_every_level:
+                if self.att_mode == "block":
                     att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t, x_s, par_1, D)
-                    # batch-global max (all ranks under data parallelism) over
-                    # the real rows (padding rows of a static-shape level excluded)
-                    dk = datas[k]
-                    att_t = att_t / global_max(_valid_rows(att_t, getattr(dk, "n_valid_t", None)))
-                    att_s = att_s / global_max(_valid_rows(att_s, getattr(dk, "n_valid_s", None)))
+                    if self.att_max_norm:
+                        # batch-global max (all ranks under data parallelism) over
+                        # the real rows (padding rows of a static-shape level excluded)
+                        dk = datas[k]
+                        att_t = att_t / global_max(_valid_rows(att_t,
+                                                               getattr(dk, "n_valid_t", None)))
+                        att_s = att_s / global_max(_valid_rows(att_s,
+                                                               getattr(dk, "n_valid_s", None)))
                     x_t = x_t * att_t
                     x_s = x_s * att_s
                 d1 = datas[k + 1]
@@ -444,7 +597,7 @@ class _AttPoolHead(nn.Module):
                 edge_index_t, edge_weight_t = d1.edge_index_t, d1.edge_weight_t
                 k = 1
                 par_1 = adj2par1(d1.edge_index, x_t0.shape[0], x_s0.shape[0])
-                D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + 1e-6
+                D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + self._deg_eps
         dr = datas[min(len(self.channels) - 1, 1)]
         if x_t.size(0) != dr.x_t.size(0) or x_s.size(0) != dr.x_s.size(0):
             # the reference's readout (lib/Hodge_ST_Model.py:1076-1080) pools the
@@ -476,22 +629,39 @@ class HL_HGCNN_CIFAR10SP_dense_int3_attpool(_AttPoolHead):
                  node_dim=5, l=0.5, edge_dim=4, num_classes=10, dropout_ratio=0.0,
                  dropout_ratio_mlp=0.0, pool_loc=0, keig=10):
         super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
-                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l,
-                         att_every_level=False)
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, l, att_mode="block")
+
+
+class HL_HGCNN_zinc_dense_int3_attpool(_AttPoolHead):
+    """ZINC head with attention pooling (lib/Hodge_ST_Model.py:412-541): K-order
+    initial convs, NEAtt (ReLU, l=0.9) at pool_loc on the level's last block
+    output WITHOUT the batch-max division, degree without the 1e-6."""
+
+    def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
+                 K=2, node_dim=21, edge_dim=3, num_classes=1, dropout_ratio=0.0,
+                 dropout_ratio_mlp=0.0, pool_loc=0, keig=7):
+        super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, 0.9,
+                         att_mode="block", att_max_norm=False, init_K=K, deg_eps=0.0)
+
+    def forward(self, datas, device="cuda:0"):
+        return super().forward(datas, device)
 
 
 class HL_HGCNN_pepfunc_dense_int3_attpool(_AttPoolHead):
-    """Peptides-func head (main_pepfunc_HL_HGCNN_dense_int3_attpool.py:36-168,
-    the class BASELINE config 4 trains: NEAtt on the dense concatenation after
-    every level, l=0.5, sigmoid; structural pooling at pool_loc=1)."""
+    """Peptides-func head of lib/Hodge_ST_Model.py:173-304: NEAtt (sigmoid,
+    l=0.9) only at pool_loc, on the dense concatenation, which it scales
+    before pooling.  The training script main_pepfunc_HL_HGCNN_dense_int3_attpool.py
+    redefines a class of this name (NEAtt after every level, l=0.5; BASELINE
+    config 4): hlhgat.main_pepfunc.HL_HGCNN_pepfunc_dense_int3_attpool, which
+    is also what ``hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool`` names."""
 
     def __init__(self, channels=[2, 2, 2, 2], filters=[64, 128, 256, 512], mlp_channels=[],
                  K=2, node_dim=9, edge_dim=3, num_classes=10, dropout_ratio=0.0,
                  dropout_ratio_mlp=0.0, pool_loc=0, keig=20):
         super().__init__(channels, filters, mlp_channels, K, node_dim, edge_dim, num_classes,
-                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, 0.5,
-                         att_every_level=True)
+                         dropout_ratio, dropout_ratio_mlp, pool_loc, keig, 0.9,
+                         att_mode="concat")
 
-    def forward(self, datas, device="cuda:0", if_att=False, if_final_layer=False):
-        # the pepfunc script orders the flags (if_att, if_final_layer) (:103)
-        return super().forward(datas, device, if_final_layer=if_final_layer, if_att=if_att)
+    def forward(self, datas, device="cuda:0"):
+        return super().forward(datas, device)

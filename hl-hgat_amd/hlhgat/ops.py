@@ -1598,8 +1598,9 @@ def l1_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
 # device error word (include/hlhgat.h: hlhgat_device_errors)
 # ----------------------------------------------------------------------------
 _DEVERR_TEXT = {
-    _lib.DEVERR_BN_WAIT: "one-launch BatchNorm: a workgroup timed out waiting for its tile's "
-                         "statistics (its rows were written as NaN)",
+    _lib.DEVERR_BN_STATE: "BatchNorm: an arrival counter was found beyond its total (the "
+                          "workspace was written by something else or shared by concurrent "
+                          "launches); that launch's statistics are not trusted",
 }
 
 
@@ -1625,6 +1626,26 @@ def check_device_errors(sync: bool = True) -> None:
         what = _DEVERR_TEXT.get(w, f"device error code {w}")
         raise RuntimeError(f"hlhgat: {what}; results since the last clear_device_errors() are "
                            f"invalid")
+
+
+def bn_giveups() -> dict:
+    """Give-ups of the one-launch BatchNorm barrier since the last
+    bn_giveups_reset(): a workgroup whose wait for its tile's statistics ran
+    out (hlhgat_set_bn_wait_us) and handed its rows to the finalising
+    workgroup.  Correct results either way; this is where the time went.
+    Synchronises the device."""
+    n = C.c_uint32(0)
+    check(LIB.hlhgat_bn_wait_timeouts(C.byref(n)), "bn_wait_timeouts")
+    recs = (_lib.BnGiveup * _lib.BN_LOG_MAX)()
+    logged = C.c_int32(0)
+    check(LIB.hlhgat_bn_giveup_log(recs, _lib.BN_LOG_MAX, C.byref(logged)), "bn_giveup_log")
+    k = min(int(logged.value), _lib.BN_LOG_MAX)
+    log = [{f: int(getattr(recs[i], f)) for f, _ in _lib.BnGiveup._fields_} for i in range(k)]
+    return {"count": int(n.value), "log": log}
+
+
+def bn_giveups_reset() -> None:
+    check(LIB.hlhgat_bn_giveup_reset(), "bn_giveup_reset")
 
 
 # ----------------------------------------------------------------------------

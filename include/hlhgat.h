@@ -397,7 +397,8 @@ int hlhgat_hodge_lmax(const int32_t* inc_rowptr, const int32_t* inc_edge,
  * lmax[g] = the largest eigenvalue of the unscaled L0 (fp64).  Eigenvectors
  * are defined up to sign (and rotation within equal eigenvalues).
  * max_nodes >= every graph's node count (sizes the workspace slice a graph
- * too large for the LDS uses); 2 <= k <= 64. */
+ * too large for the LDS uses: one slice per workgroup, min(n_graphs, CUs)
+ * workgroups, so the size depends on the current device); 2 <= k <= 64. */
 int64_t hlhgat_eig_pe_workspace_bytes(int64_t n_graphs, int64_t max_nodes, int k);
 int hlhgat_eig_pe(const int32_t* inc_rowptr, const int32_t* inc_edge, const int64_t* edge_index,
                   int64_t n_edges, int64_t n_nodes, const int64_t* node_ptr, int64_t n_graphs,
@@ -498,36 +499,6 @@ int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int64_t lddc, i
                           int* deferred, void* stream);
 int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream);
 
-/* Linear backward fed by a BatchNorm (+ReLU) backward (every HL block's
- * conv -> BatchNorm -> ReLU, lib/Hodge_ST_Model.py:556-566, and the
- * NodeEdgeInt MLPs' Linear -> BatchNorm1d -> ReLU, lib/Hodge_Cheb_Conv.py:
- * 276-289): hlhgat_proj_bwd_defer whose dC is the BatchNorm's input gradient
- * formed where the kernel loads it, dC = A g + (B (x - mean) + C) with g = dy
- * masked by the ReLU output (the coefficients from hlhgat_bn_bwd_reduce) --
- * k_bn_bwd_apply's arithmetic, so the weights' and inputs' gradients are
- * bitwise those of hlhgat_bn_bwd_train followed by hlhgat_proj_bwd_defer,
- * without the apply launch or dC in memory.  Needs the one-launch path
- * (16-byte aligned operands, N % 4 == 0, nb_w >= 1, M > 0): EINVAL
- * otherwise. */
-typedef struct {
-  const float* x;     /* the BatchNorm's input [M][N], row stride ldx */
-  int64_t ldx;
-  const float* y;     /* its (+ReLU) output for the mask, or NULL (no ReLU) */
-  int64_t ldy;
-  const float* coef;  /* [3][N]: A, B, C (hlhgat_bn_bwd_reduce) */
-  const float* mean;  /* [N] saved batch mean */
-  const int32_t* n_valid; /* rows >= *n_valid are padding (dC = 0), or NULL */
-} hlhgat_bn_bwd_prologue_t;
-int hlhgat_proj_bwd_bn_defer(int64_t M, int64_t N, const float* dy, int64_t lddy,
-                             const hlhgat_bn_bwd_prologue_t* bn, int nb_w,
-                             const float* const* A, const int64_t* lda, const int64_t* kb_w,
-                             float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
-                             const float* const* W, const int64_t* ldw, const int64_t* kb_d,
-                             float* const* dA, const int64_t* ldda, int accumulate_d,
-                             float* workspace, int64_t workspace_floats,
-                             const hlhgat_reduce_desc_t* merge, hlhgat_reduce_desc_t* defer_out,
-                             int* deferred, void* stream);
-
 /* ---- boundary-operator interaction ------------------------------------ */
 /* out[e] = ca*sa[i]*x[i] + cb*sb[j]*x[j] (+ z[e]) (+ out[e] if accumulate)
  * with (i,j) = edge_index[:,e] (sa/sb per-node scale vectors, z a per-edge
@@ -610,15 +581,15 @@ int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_val
                     const float* save_invstd, int relu, float* y, int64_t ldy, void* stream);
 
 /* BatchNorm forward statistics and normalisation in one launch
- * (k_bn_fwd_grid: rows held in registers across a grid barrier) or as two;
- * default 1 (env HLHGAT_BN_ONE_LAUNCH=0 turns it off).  Both give bitwise the
- * same results.  The one launch is taken only when its grid (<= 256
- * workgroups) fits in half of the device's resident-workgroup capacity for it
- * (occupancy x CUs; the node and edge streams may each run one), so every
- * workgroup of the barrier is co-resident; the wait is still bounded, and a
- * workgroup that gives up writes NaN rows (never numbers from partial
- * statistics), counts the timeout and raises HLHGAT_DEVERR_BN_WAIT in the
- * device error word. */
+ * (k_bn_fwd_grid: rows held in registers while the finalising workgroup --
+ * the last to arrive -- publishes the statistics) or as two; default 1 (env
+ * HLHGAT_BN_ONE_LAUNCH=0 turns it off).  Both give bitwise the same results.
+ * The one launch is taken when its grid (<= 256 workgroups) is at most half
+ * of the device's resident-workgroup capacity for it.  It assumes nothing
+ * about residency: a workgroup waits for the statistics at most
+ * hlhgat_set_bn_wait_us microseconds, then hands its rows to the finaliser
+ * and exits (the finaliser normalises them from x with the same operations),
+ * so the launch completes with the same bits beside any other kernels. */
 /* Projection + BatchNorm1d (+ ReLU) forward, training mode: the
  * hlhgat_proj_fwd GEMM x = sum_b A_b W_b^T + bias (stored to x: the backward
  * reads it), then hlhgat_bn_fwd_train on x into y -- in ONE launch
@@ -626,6 +597,8 @@ int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int32_t* n_val
  * their registers after a bounded grid-wide reduction) when N % 64 == 0, the
  * operands are 16-B aligned with ld % 4 == 0, ceil(M / 64) <= 512 and the
  * grid fits half of the chip's resident capacity; otherwise the two calls.
+ * Its wait is bounded like k_bn_fwd_grid's: a workgroup that gives up leaves
+ * its tile to the finaliser, which normalises it from the stored x.
  * Replaces Linear -> BatchNorm1d -> ReLU and HodgeLaguerreConv -> BatchNorm
  * -> ReLU (lib/Hodge_Cheb_Conv.py:276-289, lib/Hodge_ST_Model.py:556-566).
  * Statistics equal the two-call path's to fp64 summation order (not
@@ -648,43 +621,38 @@ int hlhgat_set_proj_bn_fused(int on);
 int hlhgat_proj_bn_fused_capacity(int64_t* out);
 int hlhgat_set_bn_one_launch(int on);
 int hlhgat_get_bn_one_launch(void);
-/* Test hook: polls before a waiting workgroup gives up (default 2^22;
- * 0 = give up at once, which forces the timeout path). */
-int hlhgat_set_bn_poll_limit(unsigned limit);
+/* Microseconds a one-launch BatchNorm workgroup waits for its tile's
+ * statistics before it hands its rows to the finaliser (default 1000; 0 =
+ * hand over at once unless already final: a test hook that forces the
+ * hand-over path, bitwise the same results). */
+int hlhgat_set_bn_wait_us(unsigned wait_us);
 
-/* BatchNorm (+ReLU) training forward whose input rows are produced in the
- * same launch (the NodeEdgeInt hidden layer, lib/Hodge_Cheb_Conv.py:276-289:
- * the first Linear's halves combined over B1, then BatchNorm1d + ReLU):
- *   HLHGAT_BN_PRODUCE_EDGE_GATHER: x[e] = z[e] + (ca p[i_e] + cb p[j_e])
- *     (edge_index [2][n]; = hlhgat_edge_gather2 with sa = sb = NULL);
- *   HLHGAT_BN_PRODUCE_NODE_INCIDENCE: x[v] = row_scale[v] sum p[eid] + z[v]
- *     over node v's incidence CSR row (= hlhgat_poly_step over the binary
- *     incidence, alpha = gamma = 1).
- * x is written (the backward's input) and y = BN(x) as hlhgat_bn_fwd_train,
- * bitwise the producer's launch followed by hlhgat_bn_fwd_train; that pair is
- * what runs when the one-launch grid does not fit. */
-/* hlhgat_set_bn_produced(on): 1 = rows produced inside the one-launch
- * BatchNorm; 0 (default, measured faster in the config-2 step) = the
- * producer's launch, then the BatchNorm.  Bitwise the same either way. */
-int hlhgat_set_bn_produced(int on);
-#define HLHGAT_BN_PRODUCE_EDGE_GATHER 1
-#define HLHGAT_BN_PRODUCE_NODE_INCIDENCE 2
-int hlhgat_bn_fwd_produced(int mode, const int64_t* edge_index, const int32_t* inc_rowptr,
-                           const int32_t* inc_eids, int64_t inc_nnz, const float* row_scale,
-                           const float* p, int64_t ldp, float ca, float cb, const float* z,
-                           int64_t ldz, float* x, int64_t ldx, int64_t n, const int32_t* n_valid,
-                           int64_t C, const float* weight, const float* bias,
-                           float* running_mean, float* running_var,
-                           int64_t* num_batches_tracked, float momentum, float eps, int relu,
-                           float* y, int64_t ldy, float* save_mean, float* save_invstd,
-                           void* workspace, int64_t workspace_bytes, void* stream);
 /* Times a one-launch BatchNorm workgroup gave up waiting for its tile's
- * statistics: reads the device counter (synchronising). */
+ * statistics (and handed its rows over): reads the device counter
+ * (synchronising). */
 int hlhgat_bn_wait_timeouts(unsigned* out);
+/* The first HLHGAT_BN_LOG_MAX give-ups since the last reset, as recorded by
+ * the workgroup that gave up: *logged = give-ups recorded in all (may exceed
+ * what is copied); out[0 .. min(*logged, max, HLHGAT_BN_LOG_MAX)). */
+#define HLHGAT_BN_LOG_MAX 64
+typedef struct {
+  uint32_t kernel;    /* 1 = k_bn_fwd_grid, 2 = k_proj_bn_fwd */
+  uint32_t tile;      /* column tile (blockIdx.y) */
+  uint32_t block;     /* row partition / row block (blockIdx.x) */
+  uint32_t total;     /* arrivals the finaliser needs (workgroups; groups for k_proj_bn_fwd) */
+  uint32_t arrivals;  /* arrivals counted when the wait ran out */
+  uint32_t gen0;      /* the tile's generation when the workgroup arrived */
+  uint32_t gen_seen;  /* the generation read after giving up */
+  uint32_t wait_us;   /* the wait bound in force */
+  uint32_t outcome;   /* 1 = reclaimed its rows (final by then), 2 = handed to the finaliser */
+} hlhgat_bn_giveup_t;
+int hlhgat_bn_giveup_log(hlhgat_bn_giveup_t* out, int max, int* logged);
+/* Zero the give-up counter and log (synchronises the device). */
+int hlhgat_bn_giveup_reset(void);
 
 /* The reduction half of hlhgat_bn_bwd_train: dweight, dbias and dx's
  * coefficients coef[3][C] (A, B, C of dx = A g + (B (x - mean) + C)), for a
- * consumer that forms dx itself (hlhgat_proj_bwd_bn_defer). */
+ * consumer that forms dx itself. */
 int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,
                          const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
                          int64_t C, const float* weight, const float* save_mean,
@@ -788,9 +756,18 @@ int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
  * synchronise: it shows what kernels that have completed so far reported
  * (callers synchronise first for an exact answer).  hlhgat.ops.
  * check_device_errors / hlhgat.train.TrainStep raise RuntimeError on it. */
-#define HLHGAT_DEVERR_BN_WAIT 1u /* one-launch BatchNorm wait timed out (NaN rows) */
+/* a BatchNorm arrival counter was found beyond its total (its workspace was
+ * written by something else, or shared by concurrent launches): that launch's
+ * statistics are not trusted */
+#define HLHGAT_DEVERR_BN_STATE 1u
 int hlhgat_device_errors(unsigned* out);
 int hlhgat_clear_device_errors(void);
+
+/* Test hook: `workgroups` workgroups of 64 threads with lds_bytes of LDS
+ * each; the first `hold` of them stay resident for `usec` microseconds (time
+ * bounded), the others exit at once -- a kernel that holds most CUs while
+ * another stream's kernel runs (tests of the BatchNorm barrier). */
+int hlhgat_test_occupy(int workgroups, int hold, int lds_bytes, unsigned usec, void* stream);
 
 /* ---- live kernel timing ------------------------------------------------ */
 #define HLHGAT_PROF_POLY 0 /* SpMM / fused polynomial step kernel */

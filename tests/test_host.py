@@ -652,3 +652,37 @@ def test_native_mlgc_batch_equals_per_graph():
             rn, rce, re1, rn1 = mlgc_map(lab, ei)
             assert np.array_equal(cn, rn) and np.array_equal(ce, rce)
             assert np.array_equal(e1, re1) and n1 == rn1
+
+
+@pytest.mark.parametrize("name,cls,kw", [
+    ("head_pepfunc_pyr_small", "HL_HGCNN_pepfunc_dense_int3_pyr",
+     dict(channels=[1, 1], filters=[16, 16], mlp_channels=[32], K=3, node_dim=21, edge_dim=3,
+          keig=15)),
+    ("head_cifar_pyr_small", "HL_HGCNN_CIFAR10SP_dense_int3_pyr",
+     dict(channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, node_dim=21, edge_dim=3,
+          keig=15, l=0.5)),
+    ("head_zinc_poolint3_small", "HL_HGCNN_zinc_dense_poolint3_pyr",
+     dict(channels=[1, 1], filters=[16, 16], mlp_channels=[32], K=3, keig=15)),
+    ("head_zinc_attpool_small", "HL_HGCNN_zinc_dense_int3_attpool",
+     dict(channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, node_dim=5, edge_dim=4,
+          keig=10, pool_loc=0)),
+    ("head_pepfunc_attpool_lib_small", "hodge_st_model.HL_HGCNN_pepfunc_dense_int3_attpool",
+     dict(channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)),
+    ("attpool_pepfunc_small", "HL_HGCNN_pepfunc_dense_int3_attpool",
+     dict(channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, pool_loc=0)),
+    ("attpool_cifar_small", "HL_HGCNN_CIFAR10SP_dense_int3_attpool",
+     dict(channels=[1, 1], filters=[16, 32], mlp_channels=[32], K=3, keig=10, pool_loc=0,
+          l=0.5))])
+def test_head_state_dict_matches_reference(name, cls, kw):
+    """Every head's constructor builds the reference's module tree: the same
+    state_dict keys, in the same order, with the same shapes as the
+    reference's own instance stored in the golden fixture (make_golden_heads /
+    make_golden_attpool), so a reference checkpoint loads unchanged."""
+    import hlhgat
+    obj = hlhgat
+    for part in cls.split("."):
+        obj = getattr(obj, part)
+    g = load_golden(name)
+    ref = [(k[3:], tuple(g[k].shape)) for k in g if k.startswith("sd/")]
+    ours = [(k, tuple(v.shape)) for k, v in obj(**kw).state_dict().items()]
+    assert ours == ref

@@ -38,8 +38,7 @@ def set_variant(name, on):
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
     _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
-    _lib.LIB.hlhgat_set_bn_produced(1 if (on and name == "prodbn") else 0)
-    ops._ext.set_bn_fold(on and name == "bnfold")
+    _lib.LIB.hlhgat_set_bn_one_launch(0 if (on and name == "twolaunchbn") else 1)
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")

@@ -1,0 +1,68 @@
+#!/bin/bash
+# Round-5 GPU steps on one MI355X.  Usage: tools/gpu_r5.sh TAG step [step ...]
+#   bn      the BatchNorm barrier tests (hand-over, CU hog, bitwise)
+#   tests   the whole GPU suite
+#   smoke   __graft_entry__.smoke()
+#   bench   the default bench line (driver command)
+#   pmcstep the config-2 step under rocprofv3 --pmc (serialised dispatch)
+#   prof    rocprofv3 kernel stats + step census of the replayed bench
+#   pmc     FETCH / WRITE passes for the roofline traffic
+# Stops at the first crash / time-out.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=$1; shift
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/${TAG}_$name.log" 2>&1
+  local rc=$?; echo "=== $name rc=$rc"; tail -n 4 "gpurun_out/${TAG}_$name.log" | cut -c1-800
+  case $rc in
+    0|1) ;;
+    *) tail -n 40 "gpurun_out/${TAG}_$name.log"; exit $rc ;;
+  esac
+  return 0
+}
+PT="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method thread"
+for s in "$@"; do
+  case $s in
+    bn) step bn 600 $PT tests/test_gpu_parity.py -m gpu -v -s -k "bn_ or proj_bn or handover or hog" ;;
+    tests) step tests 1100 $PT tests -m gpu -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 900 python bench.py ;;
+    pmcstep) rm -rf gpurun_out/${TAG}_pmcstep_d
+             step pmcstep 200 timeout -s KILL 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/${TAG}_pmcstep_d -o p --output-format csv -- python3 tools/probes/poly_context.py --steps 3
+             rm -rf gpurun_out/${TAG}_pmcstep_d ;;
+    prof) rm -rf gpurun_out/prof_$TAG
+          B="python3 bench.py --steps 20 --warmup 6 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 3"
+          step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- $B
+          T=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
+          python tools/step_kernels.py "$T" --step -3 > gpurun_out/${TAG}_step_kernels.txt || true
+          python tools/step_gaps.py "$T" --step -3 --top 40 > gpurun_out/${TAG}_step_gaps.txt || true
+          S=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
+          cp "$S" gpurun_out/${TAG}_bench_kernel_stats.csv || true
+          rm -f "$T" ;;
+    pmc) rm -rf gpurun_out/pmcf gpurun_out/pmcw
+         E="python3 bench.py --eager --steps 2 --warmup 1 --prof-steps 1 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 1"
+         step pmc_fetch 200 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o f --output-format csv -- $E
+         step pmc_write 200 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o w --output-format csv -- $E
+         python tools/pmc_traffic.py $(find gpurun_out/pmcf -name '*counter_collection.csv' | head -1) $(find gpurun_out/pmcw -name '*counter_collection.csv' | head -1) --kernel k_poly_step --kernel k_proj_fwd --kernel k_edge_gather2 --kernel k_bn_fwd_grid --kernel k_bn_bwd_reduce --kernel k_proj_bwd_fused --kernel k_proj_bn_fwd --out gpurun_out/${TAG}_pmc_traffic.json --label "$TAG bench.py --eager cfg2 step" > /dev/null || true
+         rm -rf gpurun_out/pmcf gpurun_out/pmcw ;;
+    listctr) timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1; echo "=== listctr rc=$?" ;;
+    heads) step heads 600 $PT tests -m gpu -v -k "reference_golden or state_dict" ;;
+    pmcgemm) # SQ counters of k_proj_bwd_fused: isolated (kbench) and in the replayed step
+         L=gpurun_out/${TAG}_counters.txt
+         [ -s $L ] || timeout -k 10 120 rocprofv3 -L > $L 2>&1
+         C=$(python3 tools/pick_counters.py $L SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT)
+         echo "counters: $C"
+         rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step
+         step pmcgemm_iso 200 timeout -s KILL 180 rocprofv3 --pmc $C -d gpurun_out/${TAG}_pg_iso -o p --output-format csv -- python3 tools/kbench.py --only "proj_bwd_fused" --reps 5 --chain 5
+         python3 tools/pmc_kernel.py $(find gpurun_out/${TAG}_pg_iso -name '*counter_collection.csv' | head -1) --match k_proj_bwd_fused > gpurun_out/${TAG}_pmc_gemm_iso.txt 2>&1 || true
+         step pmcgemm_step 200 timeout -s KILL 180 rocprofv3 --pmc $C -d gpurun_out/${TAG}_pg_step -o p --output-format csv -- python3 tools/probes/poly_context.py --steps 3
+         python3 tools/pmc_kernel.py $(find gpurun_out/${TAG}_pg_step -name '*counter_collection.csv' | head -1) --match k_proj > gpurun_out/${TAG}_pmc_gemm_step.txt 2>&1 || true
+         rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
+    kbench) step kbench 300 python3 tools/kbench.py --only "proj" --reps 20 --chain 20 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "=== done"

@@ -205,10 +205,9 @@ def main():
         fl = 2.0 * M * N * sum(kbs)
         L.hlhgat_set_proj_bn_fused(1)
         run(f"proj_bn_fwd fused {tag}", pb, None, fl)
-        L.hlhgat_set_bn_poll_limit(0)
-        run(f"proj_bn_fwd fused NO-WAIT (timing probe, NaN rows) {tag}", pb, None, fl)
-        L.hlhgat_set_bn_poll_limit(1 << 22)
-        L.hlhgat_clear_device_errors()
+        L.hlhgat_set_bn_wait_us(0)
+        run(f"proj_bn_fwd fused, every tile handed to the finaliser {tag}", pb, None, fl)
+        L.hlhgat_set_bn_wait_us(1000)
         L.hlhgat_set_proj_bn_fused(0)
         run(f"proj_bn_fwd two-call {tag}", pb, None, fl)
         L.hlhgat_set_proj_bn_fused(1)

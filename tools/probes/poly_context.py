@@ -41,6 +41,7 @@ def main():
     torch.cuda.synchronize()
     ops.check_device_errors()
     print(st.stats)
+    print("bn give-ups", ops.bn_giveups())
 
 
 if __name__ == "__main__":
