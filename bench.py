@@ -111,54 +111,53 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16):
     for _ in range(2):
         pad_batch(collate(graphs, check_hodge=False), caps)
     out["python_collate_graphs_per_s_1core"] = round(2 * GRAPHS_PER_GPU / (time.perf_counter() - t0), 1)
-    # the loader-fed loop: GraphLoader(4 threads, pinned) -> TrainStep.stage (H2D
-    # on a copy stream straight into the static buffers of the graph that
-    # replays next, two graphs in turn) -> replayed step with no copy-in
+    # the loader-fed loop: GraphLoader(4 threads, pinned) -> StagedFeed (a
+    # feeder thread: TrainStep.stage, H2D on a copy stream straight into the
+    # static buffers of a captured graph, two batches ahead) -> the replayed
+    # step with no copy-in, launched from this thread alone
+    from hlhgat.loader import StagedFeed
     ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=4, prefetch=8, pin=True)
     cs = torch.cuda.Stream(device=device)
-
-    def upload(b):
-        return step.stage(b, cs)
+    depth = 2
+    step.stage_slots = max(step.stage_slots, depth + 1)
 
     def batches():
         while True:
             for b in ld:
                 yield b
 
-    src = batches()
-    nxt = upload(next(src))
-    host = {"wait_loader": 0.0, "upload": 0.0, "step_call": 0.0}
-    for i in range(steps + 2):
-        if i == 2:
+    feed = StagedFeed(batches(), step, depth=depth, stream=cs)
+    it = iter(feed)
+    host = {"wait_feed": 0.0, "step_call": 0.0}
+    warm = 4  # the first steps capture the shape's third graph
+    for i in range(steps + warm):
+        if i == warm:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             host = {k: 0.0 for k in host}
-        cur = nxt
         ta = time.perf_counter()
-        b_next = next(src)
+        st = next(it)
         tb = time.perf_counter()
-        nxt = upload(b_next)
+        step(st)
         tc = time.perf_counter()
-        step(cur)
-        td = time.perf_counter()
-        host["wait_loader"] += tb - ta
-        host["upload"] += tc - tb
-        host["step_call"] += td - tc
+        host["wait_feed"] += tb - ta
+        host["step_call"] += tc - tb
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    src.close()  # stop the loader's collation threads before the next leg
+    it.close()  # stops the feeder thread and the loader's collation threads
     torch.cuda.synchronize()
     ops_mod = __import__("hlhgat").ops
-    ops_mod.check_device_errors()  # a barrier timeout here is this leg's, not the next one's
+    ops_mod.check_device_errors()
     out["loader_fed"] = {"value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
                          "ms_per_step": round(dt * 1e3, 3), "workers": 4, "pinned": True,
-                         "steps": steps,
+                         "steps": steps, "stage_depth": depth,
                          "host_ms_per_step": {k: round(v / steps * 1e3, 3) for k, v in host.items()},
                          "what": "training steps fed by GraphLoader end to end: native collate "
-                                 "on 4 threads, H2D of the next batch on a copy stream during "
-                                 "the step straight into the static buffers of the graph that "
-                                 "replays next (TrainStep.stage, two graphs in turn), replayed "
-                                 "step with no copy-in"}
+                                 "on 4 threads, hlhgat.loader.StagedFeed's thread uploading "
+                                 "(TrainStep.stage: one H2D copy per batch on a copy stream, "
+                                 "straight into the static buffers of one of the shape's "
+                                 "captured graphs) two batches ahead, the replayed step (no "
+                                 "copy-in) launched from the training thread alone"}
     out["device_resident_ms_per_step"] = round(ms_step, 3)
     return out
 

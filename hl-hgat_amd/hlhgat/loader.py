@@ -16,15 +16,17 @@ TrainStep copies each into its captured step's static buffers.
 """
 from __future__ import annotations
 
+import queue
+import threading
 from collections import deque
 from concurrent.futures import ThreadPoolExecutor
-from typing import Dict, Iterator, List, Optional
+from typing import Dict, Iterable, Iterator, List, Optional
 
 import numpy as np
 
 from .hodge_dataset import Batch, PackedGraphs
 
-__all__ = ["GraphLoader"]
+__all__ = ["GraphLoader", "StagedFeed"]
 
 
 class GraphLoader:
@@ -92,3 +94,83 @@ class GraphLoader:
                 if nxt is not None:
                     pending.append(ex.submit(self.dataset.collate, nxt, caps, self.pin))
                 yield b
+
+
+class StagedFeed:
+    """The host side of the training loop off the thread that launches the
+    steps: a feeder thread takes collated batches from ``batches`` (e.g. a
+    GraphLoader, whose own threads collate ahead) and uploads each with
+    ``step.stage(batch, stream)`` -- on a copy stream, straight into the
+    static buffers of a captured graph of the batch's shape -- at most
+    ``depth`` batches ahead of the step; iterating yields the staged handles
+    in order, each to be passed to ``step(...)`` before the next is taken.
+
+        feed = StagedFeed(loader, step, depth=2)   # step = TrainStep(..., stage_slots=3)
+        for st in feed:
+            loss = step(st)
+
+    The replay call releases the GIL, so the feeder's Python work and the
+    copies' enqueueing overlap the launch thread's.  ``step.stage_slots``
+    should be >= depth + 1 (depth staged batches waiting + one replaying);
+    with fewer, a staged batch goes to fresh device tensors and is copied in
+    at its step (correct, one device copy more).  The reference loop this
+    serves: main_zinc_HL_HGCNN_dense_int3_pyr.py:151-162 (for data in
+    loader: data.to(device); step), with DataLoader(num_workers=4) (:223-225).
+    """
+
+    _END = object()
+
+    def __init__(self, batches: Iterable, step, depth: int = 2, stream=None):
+        import torch
+        if depth < 1:
+            raise ValueError("StagedFeed: depth must be >= 1")
+        self.batches = batches
+        self.step = step
+        self.depth = int(depth)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=step.device)
+        self._q: "queue.Queue" = queue.Queue()
+        self._room = threading.Semaphore(self.depth)
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+
+    def _run(self):
+        it = iter(self.batches)
+        try:
+            for b in it:
+                while not self._room.acquire(timeout=0.1):
+                    if self._stop.is_set():
+                        return
+                if self._stop.is_set():
+                    return
+                self._q.put(self.step.stage(b, self.stream))
+            self._q.put(self._END)
+        except BaseException as e:  # handed to the consumer
+            self._q.put(e)
+        finally:
+            close = getattr(it, "close", None)  # stop a generator source's own workers
+            if close is not None:
+                close()
+
+    def __iter__(self):
+        self._stop.clear()
+        self._thread = threading.Thread(target=self._run, name="hlhgat-stage", daemon=True)
+        self._thread.start()
+        try:
+            while True:
+                item = self._q.get()
+                if item is self._END:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+                self._room.release()  # the consumer has stepped it: room for one more
+        finally:
+            self.close()
+
+    def close(self):
+        self._stop.set()
+        t, self._thread = self._thread, None
+        if t is not None and t is not threading.current_thread():
+            # unblock a feeder waiting for room, then let it finish its batch
+            self._room.release()
+            t.join(timeout=30)

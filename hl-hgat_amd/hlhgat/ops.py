@@ -386,6 +386,12 @@ def set_hodge_factor(edge_index_s: torch.Tensor, edge_index: torch.Tensor, n_nod
     return edge_index_s
 
 
+def has_hodge_factor(edge_index_s: torch.Tensor) -> bool:
+    """Whether set_hodge_factor declared this L1 (its polynomial bases then
+    take the factored path when FACTOR_ENABLED)."""
+    return getattr(edge_index_s, "_hlhgat_factor", None) is not None
+
+
 def _build_factor(op: "HodgeOperator", ei_s: torch.Tensor, w: torch.Tensor, decl) -> None:
     """The device tensors of hlhgat_hodge_factor_t for op (no host sync)."""
     edge_index, n_nodes, node_order = decl

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import contextlib
 import gc
+import threading
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
@@ -202,7 +203,7 @@ class _Captured:
             ops.copy_words_batched([p[0] for p in pend], [p[1] for p in pend])
 
 
-STAGE_SLOTS = 2  # captured graphs per batch shape that TrainStep.stage fills in turn
+STAGE_SLOTS = 2  # default captured graphs per batch shape TrainStep.stage fills in turn
 STAGE_RING = 8   # staged batches that may be outstanding (uploaded, not yet stepped)
 
 
@@ -226,7 +227,7 @@ class TrainStep:
 
     def __init__(self, model: torch.nn.Module, loss_fn: Callable, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 graphs: bool = True, max_graphs: int = 32):
+                 graphs: bool = True, max_graphs: int = 32, stage_slots: int = STAGE_SLOTS):
         if isinstance(model, torch.nn.parallel.DistributedDataParallel):
             # DDP would all-reduce the gradients in its hooks and TrainStep again in
             # its bucket (two reductions, and DDP's gradient_as_bucket_view fights the
@@ -235,6 +236,15 @@ class TrainStep:
                              "wrapper -- TrainStep reduces the gradients itself (one bucket)")
         self.model = model
         self.loss_fn = loss_fn
+        # stage(): graphs per batch shape filled in turn (a feeder staging d
+        # batches ahead of the step needs d + 1), and the lock that lets a
+        # feeder thread stage while this thread replays (slot choice, pending
+        # counts and the slot lists are shared)
+        if not 1 <= stage_slots <= STAGE_RING:
+            raise ValueError(f"TrainStep: stage_slots must be in [1, {STAGE_RING}]")
+        self.stage_slots = int(stage_slots)
+        self._stage_lock = threading.RLock()
+        self._outstanding = 0
         params = [p for p in model.parameters() if p.requires_grad]
         if not params:
             raise ValueError("TrainStep: model has no trainable parameters")
@@ -429,7 +439,13 @@ class TrainStep:
                 self._ext.bn_workspace_reserve(int(h), idx, BN_RESERVE_CHANNELS)
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        with _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s):
+        # thread-local capture: the data loader's collation threads and a
+        # StagedFeed thread keep running beside it (pinned allocations, copies
+        # on other streams are legal there; a global-mode capture turns them
+        # into hipErrorStreamCaptureUnsupported); the stage lock keeps the
+        # feeder's uploads out of the capture window altogether
+        with self._stage_lock, _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s,
+                                                          capture_error_mode="thread_local"):
             prepared = self._prepare()
             loss = self._fwd_bwd(static, zeroed=True)
             if self._exchange_in_graph:
@@ -453,7 +469,8 @@ class TrainStep:
         ent = _Captured(g, static, loss)
         self.stats["captures"] += 1
         if slot_of is not None:
-            slot_of.slots.append(ent)
+            with self._stage_lock:
+                slot_of.slots.append(ent)
             return ent
         if len(self._graphs) >= self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
@@ -477,18 +494,45 @@ class TrainStep:
                 self._copy_stream = torch.cuda.Stream(device=self.device)
             stream = self._copy_stream
         key = batch_key(batch)
-        ent = self._graphs.get(key)
-        main = torch.cuda.current_stream(self.device)
+        # the stream the replays run on (stage may be called from a feeder
+        # thread, whose current stream is not the training loop's)
+        main = getattr(self, "_replay_stream", None) or torch.cuda.current_stream(self.device)
         self._staging = True
+        with self._stage_lock:  # whole body: never beside a capture (see _capture)
+            return self._stage_locked(batch, stream, key, main)
+
+    def _stage_locked(self, batch, stream, key, main) -> Staged:
         # a ring of events (kept for the process, see _EVENTS_KEEP): at most
-        # STAGE_RING staged batches may be outstanding
+        # STAGE_RING staged batches may be outstanding (a ring event is
+        # re-recorded only once its batch has been stepped)
+        if self._outstanding >= STAGE_RING:
+            raise RuntimeError(f"TrainStep.stage: more than {STAGE_RING} staged batches "
+                               f"outstanding (step them before staging more)")
         ring = getattr(self, "_stage_ring", None)
         if ring is None:
             ring = self._stage_ring = [_event() for _ in range(STAGE_RING)]
             self._stage_next = 0
         ev = ring[self._stage_next]
         self._stage_next = (self._stage_next + 1) % STAGE_RING
-        if ent is None or len(ent.slots) < STAGE_SLOTS:
+        self._outstanding += 1
+        ent = self._graphs.get(key)
+        slot = None
+        if ent is not None and len(ent.slots) >= self.stage_slots:
+            # the next graph of the shape in turn whose buffers no staged
+            # batch is waiting in (a slot with one pending would be
+            # overwritten before its batch is stepped)
+            n = len(ent.slots)
+            k0 = getattr(ent, "next_slot", 0)
+            for d in range(n):
+                cand = ent.slots[(k0 + d) % n]
+                if cand.pending == 0:
+                    slot = cand
+                    ent.next_slot = (k0 + d + 1) % n
+                    break
+        if slot is not None:
+            slot.pending += 1
+            free = slot.free
+        if slot is None:  # fresh device tensors (first steps of a shape, or every slot taken)
             with torch.cuda.stream(stream):
                 dev = [self._upload(b) for b in _parts(batch)]
                 if not isinstance(batch, (list, tuple)):
@@ -498,12 +542,8 @@ class TrainStep:
                 for _, v in _tensor_items(b):
                     v.record_stream(main)
             return Staged(dev, ev, None, key)
-        k = getattr(ent, "next_slot", 0)
-        ent.next_slot = (k + 1) % len(ent.slots)
-        slot = ent.slots[k]
-        slot.pending += 1
-        if slot.free is not None:
-            stream.wait_event(slot.free)
+        if free is not None:
+            stream.wait_event(free)
         else:  # replayed before staging began (no release event): after all of main
             stream.wait_stream(main)
         with torch.cuda.stream(stream):
@@ -553,6 +593,7 @@ class TrainStep:
         return out
 
     def _replay(self, ent: _Captured) -> torch.Tensor:
+        self._replay_stream = torch.cuda.current_stream(self.device)
         ent.graph.replay()
         if getattr(self, "_staging", False):  # stage() waits for the slot's release
             ent.released(torch.cuda.current_stream(self.device))
@@ -564,20 +605,32 @@ class TrainStep:
 
     def _call_staged(self, st: Staged) -> torch.Tensor:
         torch.cuda.current_stream(self.device).wait_event(st.event)
-        if st.slot is not None:
-            st.slot.pending -= 1
-            return self._replay(st.slot)
-        ent = self._graphs.get(st.key)
-        if ent is None:
-            return self(st.batch)
-        if len(ent.slots) >= STAGE_SLOTS:
-            free = [sl for sl in ent.slots if sl.pending == 0]
-            if free:  # copy-in into a graph no staged upload is waiting for
-                free[0].load(st.batch)
-                return self._replay(free[0])
-        # one more slot for this shape: the staged tensors are its static
-        # buffers; capturing does not run the step, the first replay does
-        return self._replay(self._capture(st.batch, st.key, slot_of=ent))
+        try:
+            if st.slot is not None:
+                loss = self._replay(st.slot)  # records the slot's release event
+                with self._stage_lock:  # only now may a feeder stage into it again
+                    st.slot.pending -= 1
+                return loss
+            ent = self._graphs.get(st.key)
+            if ent is None:
+                return self(st.batch)
+            if len(ent.slots) >= self.stage_slots:
+                with self._stage_lock:
+                    free = [sl for sl in ent.slots if sl.pending == 0]
+                    if free:  # taken, so a feeder does not stage into it meanwhile
+                        free[0].pending += 1
+                if free:  # copy-in into a graph no staged upload is waiting for
+                    free[0].load(st.batch)
+                    loss = self._replay(free[0])
+                    with self._stage_lock:
+                        free[0].pending -= 1
+                    return loss
+            # one more slot for this shape: the staged tensors are its static
+            # buffers; capturing does not run the step, the first replay does
+            return self._replay(self._capture(st.batch, st.key, slot_of=ent))
+        finally:
+            with self._stage_lock:
+                self._outstanding -= 1
 
     def __call__(self, batch) -> torch.Tensor:
         # a kernel of an earlier step that reported unusable results (the
@@ -594,11 +647,17 @@ class TrainStep:
             loss = self._eager(batch)
             self._capture(batch, key)
             return loss
-        free = [sl for sl in ent.slots if sl.pending == 0]
+        with self._stage_lock:
+            free = [sl for sl in ent.slots if sl.pending == 0]
+            if free:
+                free[0].pending += 1
         if not free:  # every graph of the shape awaits a staged batch: one more
             return self._replay(self._capture(self._upload(batch), key, slot_of=ent))
         free[0].load(batch)
-        return self._replay(free[0])
+        loss = self._replay(free[0])
+        with self._stage_lock:
+            free[0].pending -= 1
+        return loss
 
     def state_dict(self):
         return {"model": self.model.state_dict(), "opt": self.opt.state_dict()}
@@ -644,7 +703,8 @@ class InferStep:
         s = self._stream
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
-        with _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s):
+        with _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s,
+                                        capture_error_mode="thread_local"):
             out = self._forward(static)
             ops.join_capture_streams(self.device)
         left = ops.side_streams_capturing(self.device)

@@ -251,12 +251,21 @@ def _as_d(b, dtype):
 def _to_dev(b, cuda, factored):
     import copy
     from hlhgat import ops
-    bd = copy.copy(b).to(cuda)  # Batch.to moves in place: keep the host batch for the oracle
+    bd = copy.copy(b)  # Batch.to moves in place: keep the host batch for the oracle
+    # Batch.to declares the Hodge factor of L1 whenever collate set l1_factor:
+    # the CSR variant must not carry that flag (the _csr case had
+    # silently run the factored path)
+    bd.l1_factor = bool(factored) and bool(getattr(b, "l1_factor", False))
+    bd = bd.to(cuda)
     ops.mark_hodge(bd.edge_index_t)
     ops.mark_hodge(bd.edge_index_s)
     if factored:
         ops.set_hodge_factor(bd.edge_index_s, bd.edge_index, bd.x_t.shape[0])
+    assert ops.has_hodge_factor(bd.edge_index_s) == bool(factored)
     return bd
+
+
+_HIP_GRADS = {}  # case -> HIP parameter gradients (the CSR / factored pair compared)
 
 
 @pytest.mark.parametrize("name,kind,factored", [("cfg3_cifar_16", "cifar", True),
@@ -327,5 +336,12 @@ def test_frozen_mask_grads_heads_realistic_batches(cuda, name, kind, factored):
                     continue
                 sc = max(1.0, float(base[k].grad.abs().max()))
                 cond[k] = max(cond.get(k, 0.0), float((p.grad - base[k].grad).abs().max()) / sc)
+    _HIP_GRADS[name] = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()
+                        if p.grad is not None}
+    if name == "cfg5_tsp_4x2500_csr" and "cfg5_tsp_4x2500" in _HIP_GRADS:
+        # the two variants run different kernels (CSR SpMM vs the factored L1,
+        # not bitwise the same arithmetic): their gradients must differ
+        other = _HIP_GRADS["cfg5_tsp_4x2500"]
+        assert any(not torch.equal(v, other[k]) for k, v in _HIP_GRADS[name].items())
     _check(name, m, ref64, masked, ref32, cond)
     ops.check_device_errors()

@@ -760,3 +760,88 @@ def test_staged_arena_batches_single_copy_bitwise(cuda):
     for key in sd_ref:
         assert torch.equal(sd_ref[key], sd[key]), key
     assert step.stats["captures"] == 2 and single >= 4, (step.stats, single)
+
+
+@pytest.mark.gpu
+def test_staged_three_ahead_bitwise(cuda):
+    """Staging more batches ahead than a shape has captured graphs (three
+    ahead, two graphs): a graph whose buffers still hold a staged batch is
+    never picked again (the batch would be overwritten before its step and
+    never trained); the extra batch goes to fresh device tensors.  Losses and
+    parameters bitwise those of step(device batch) in the same order."""
+    import copy
+    import hlhgat
+    from hlhgat.synthetic import zinc_like_batch
+    from hlhgat.train import TrainStep
+    g = torch.Generator().manual_seed(5)
+    host = []
+    for k in range(4):  # one shape, four value sets
+        b = copy.copy(zinc_like_batch(36, seed=8))
+        b.x_t = b.x_t + 0.3 * k * torch.randn(b.x_t.shape, generator=g)
+        b.y = b.y + 0.1 * k
+        host.append(b)
+    order = [0, 1, 2, 3, 0, 2, 1, 3, 3, 0, 1, 2]
+    l_ref, sd_ref, _ = _run(True, True, [copy.copy(b).to(cuda) for b in host], order)
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
+    crit = torch.nn.L1Loss()
+    step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                     weight_decay=1e-3, graphs=True)
+    assert step.stage_slots == 2
+    cs = torch.cuda.Stream(device=cuda)
+    ahead = 3
+    queue = [step.stage(host[order[k]], cs) for k in range(ahead)]
+    losses = []
+    for k in range(len(order)):
+        cur = queue.pop(0)
+        if k + ahead < len(order):
+            queue.append(step.stage(host[order[k + ahead]], cs))
+        pend = [sl.pending for sl in step._graphs[cur.key].slots] if cur.key in step._graphs \
+            else []
+        assert all(p <= 1 for p in pend), pend  # never two batches waiting in one graph
+        losses.append(float(step(cur)))
+    torch.cuda.synchronize()
+    _check_errors()
+    assert step._outstanding == 0
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    assert losses == l_ref, (losses, l_ref)
+    for key in sd_ref:
+        assert torch.equal(sd_ref[key], sd[key]), key
+
+
+@pytest.mark.gpu
+def test_staged_feed_thread_bitwise(cuda):
+    """hlhgat.loader.StagedFeed: a feeder thread stages GraphLoader batches
+    (native collate on worker threads, pinned arenas) two ahead while this
+    thread replays, and a third graph of the shape is captured meanwhile
+    (the collation and feeder threads run beside a thread-local capture);
+    losses and parameters bitwise those of step(device batch) in order."""
+    import numpy as np
+    import hlhgat
+    from hlhgat.hodge_dataset import PackedGraphs
+    from hlhgat.loader import GraphLoader, StagedFeed
+    from hlhgat.synthetic import zinc_like_graph
+    from hlhgat.train import TrainStep
+    ds = PackedGraphs([zinc_like_graph(700 + i) for i in range(96)], check_hodge=False)
+    ld = GraphLoader(ds, 12, caps=None, workers=3, prefetch=6, pin=True)
+    idxs = ld.batch_indices(0)
+    caps = ld.epoch_caps(idxs)
+    ref_batches = [ds.collate(i, caps).to(cuda) for i in idxs]
+    l_ref, sd_ref, _ = _run(True, True, ref_batches, list(range(len(idxs))))
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
+    crit = torch.nn.L1Loss()
+    step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                     weight_decay=1e-3, graphs=True, stage_slots=3)
+    losses = []
+    for st in StagedFeed(ld, step, depth=2):
+        losses.append(float(step(st)))
+    torch.cuda.synchronize()
+    _check_errors()
+    assert len(losses) == len(idxs) and step._outstanding == 0
+    assert step.stats["captures"] == 3, step.stats
+    sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    assert losses == l_ref, (losses, l_ref)
+    for key in sd_ref:
+        assert torch.equal(sd_ref[key], sd[key]), key
+    assert np.isfinite(losses).all()

@@ -62,6 +62,13 @@ for s in "$@"; do
          python3 tools/pmc_kernel.py $(find gpurun_out/${TAG}_pg_step -name '*counter_collection.csv' | head -1) --match k_proj > gpurun_out/${TAG}_pmc_gemm_step.txt 2>&1 || true
          rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
     kbench) step kbench 300 python3 tools/kbench.py --only "proj" --reps 20 --chain 20 ;;
+    wsweep) # weight-item shape sweep of the fused Linear backward (kbench, isolated)
+         for wt in 1 2 3 4; do for it in 256 384 512; do
+           echo "=== WT=$wt WITEMS=$it" >> gpurun_out/${TAG}_wsweep.log
+           HLHGAT_WT=$wt HLHGAT_WITEMS=$it timeout -k 10 120 python3 tools/kbench.py --only "proj_bwd_fused" --reps 10 --chain 10 >> gpurun_out/${TAG}_wsweep.log 2>&1 || { echo "wsweep failed"; exit 3; }
+         done; done
+         echo "=== wsweep done" ;;
+    wtests) step wtests 600 env HLHGAT_WT=3 $PT tests/test_gpu_parity.py -m gpu -q -k "fused or proj or linear" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
