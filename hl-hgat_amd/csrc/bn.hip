@@ -1183,6 +1183,7 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
 struct ProjBnArgs {
   FwdArgs g;    // the projection: g.C = x (pre-BatchNorm), g.ldc
   StatsArgs s;  // the BatchNorm: s.out = y, partials / counters / error word
+  int stats_only;  // 1: no wait -- the finaliser writes the statistics, k_bn_apply follows
 };
 
 constexpr int kPbTN = 4;  // 64 columns per workgroup: one BatchNorm column tile
@@ -1274,6 +1275,19 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   float* sm = reinterpret_cast<float*>(sum1 + 64);  // [64]
   float* ss = sm + 64;                              // [64]
   unsigned long long* tile_slots = s.slots + (int64_t)by * gridDim.x;
+  if (a.stats_only) {  // x and the statistics only: nobody waits (k_bn_apply normalises)
+    if (!top) return;
+    reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
+    if (threadIdx.x < 64) {
+      const int cc = n_base + threadIdx.x;
+      float m, is;
+      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, true);
+      s.save_mean[cc] = m;
+      s.save_invstd[cc] = is;
+    }
+    if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
+    return;
+  }
   if (top) {
     reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
     if (threadIdx.x < 64) {
@@ -1368,6 +1382,14 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
 
 bool& proj_bn_fused_flag() {
   static bool v = true;
+  return v;
+}
+
+// hlhgat_set_proj_bn_split(1): the projection + statistics launch (no wait;
+// its last workgroup finalises) followed by k_bn_apply, instead of the one
+// launch whose workgroups wait for the statistics; bitwise the same y.
+bool& proj_bn_split_flag() {
+  static bool v = false;
   return v;
 }
 
@@ -1699,9 +1721,30 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   const double flops = 2.0 * (double)M * (double)N * (double)ktot;
   const double bytes = 4.0 * (double)M * ((double)ktot + 2.0 * (double)N);
   hipStream_t st = as_stream(stream);
-  ProfScope prof(HLHGAT_PROF_PROJ_BN, st, bytes, flops);
-  launch(k_proj_bn_fwd, dim3(gx, gy), dim3(kThreads), 0, st, &prof, a);
+  const bool split = proj_bn_split_flag();
+  a.stats_only = split ? 1 : 0;
+  {
+    ProfScope prof(HLHGAT_PROF_PROJ_BN, st, bytes, flops);
+    launch(k_proj_bn_fwd, dim3(gx, gy), dim3(kThreads), 0, st, &prof, a);
+  }
   HLH_CHECK_LAUNCH();
+  if (split) {
+    const bool vec2 = bn_vec_ok(N, {ldx, ldy}, {x, y});
+    const BnLayout L = bn_layout(M, N, vec2);
+    ApplyArgs p{n_valid, x, ldx, y, ldy, M, (int)N, save_mean, save_invstd, bn_weight, bn_bias,
+                relu, L.tpr, L.rp};
+    dim3 g2(apply_grid_x(M, L.rp), L.tiles);
+    if (vec2)
+      launch(k_bn_apply<4>, g2, dim3(kThreads), 0, st, nullptr, p);
+    else
+      launch(k_bn_apply<1>, g2, dim3(kThreads), 0, st, nullptr, p);
+    HLH_CHECK_LAUNCH();
+  }
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_set_proj_bn_split(int on) {
+  proj_bn_split_flag() = on != 0;
   return HLHGAT_OK;
 }
 

@@ -461,7 +461,6 @@ struct BwdWeightArgs {
   float* part;
   int64_t rows_per_split;
   int tiles_n;
-  int kt;       // 64-wide k tiles per weight item (k_proj_bwd_fused<.., WT>: WT == kt)
   int xcd_map;  // remap (tile, split) so each XCD walks one contiguous range of them
 };
 
@@ -615,14 +614,8 @@ __device__ __forceinline__ void weight_item(unsigned L, unsigned Y, unsigned tot
   bz = (int)(w / Y);
 }
 
-// WT 64-wide k tiles per item (§10.2 of DESIGN): the dC chunk of a split is
-// staged ONCE for all of them (at WT = 1 every k tile re-read it); each wave
-// keeps one 32x32 accumulator per k tile.  Same per-element MFMA sequence
-// for every WT: bitwise the same partials.
-template <int WT>
 __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by, int bz,
-                                                  float (*gl)[WR][64],
-                                                  float (*al)[WR][64 * WT]) {
+                                                  float (*gl)[WR][64], float (*al)[WR][64]) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int wn = wave >> 1, wk = wave & 1;
@@ -630,7 +623,7 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
   while (b + 1 < a.nb && by >= a.tile_start[b + 1]) ++b;
   const int t = by - a.tile_start[b];
   const int n_base = (t % a.tiles_n) * 64;
-  const int k_base = (t / a.tiles_n) * 64 * WT;
+  const int k_base = (t / a.tiles_n) * 64;
   const int kb = a.kb[b];
   const float* __restrict__ A = a.A[b];
   const int64_t lda = a.lda[b];
@@ -639,50 +632,39 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
   int64_t m_hi = m_lo + a.rows_per_split;
   if (m_hi > a.M) m_hi = a.M;
 
-  // staging: each 64-wide tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
+  // staging: each tile is 32 rows x 16 float4; thread -> (row = tid/16 + 16u, c4 = tid%16)
   const int sr = threadIdx.x >> 4, sc = (threadIdx.x & 15) * 4;
-  auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2][WT]) {
+  auto load = [&](int64_t m0, float4 (&g)[2], float4 (&x)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t m = m0 + sr + 16 * u;
       const bool mv = m < m_hi;
-      const int n = n_base + sc;
+      const int n = n_base + sc, k = k_base + sc;
       g[u] = (mv && n < a.N) ? *reinterpret_cast<const float4*>(a.G + m * a.ldg + n)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int w = 0; w < WT; ++w) {
-        const int k = k_base + 64 * w + sc;
-        x[u][w] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      x[u] = (mv && k < kb) ? *reinterpret_cast<const float4*>(A + m * lda + k)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store = [&](int buf, const float4 (&g)[2], const float4 (&x)[2][WT]) {
+  auto store = [&](int buf, const float4 (&g)[2], const float4 (&x)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       *reinterpret_cast<float4*>(&gl[buf][sr + 16 * u][sc]) = g[u];
-#pragma unroll
-      for (int w = 0; w < WT; ++w)
-        *reinterpret_cast<float4*>(&al[buf][sr + 16 * u][64 * w + sc]) = x[u][w];
+      *reinterpret_cast<float4*>(&al[buf][sr + 16 * u][sc]) = x[u];
     }
   };
 
-  floatx16 acc[WT];
+  floatx16 acc;
 #pragma unroll
-  for (int w = 0; w < WT; ++w)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[w][r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float bsum = 0.f;
   const int rl = lane >> 5, cl = lane & 31;
   auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < WR / 2; ++kk) {
       const float av = gl[buf][2 * kk + rl][32 * wn + cl];
-#pragma unroll
-      for (int w = 0; w < WT; ++w) {
-        const float bv = al[buf][2 * kk + rl][64 * w + 32 * wk + cl];
-        acc[w] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[w], 0, 0, 0);
-      }
+      const float bv = al[buf][2 * kk + rl][32 * wk + cl];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
       bsum = bsum + av;
     }
   };
@@ -691,7 +673,7 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
   // per chunk.  Chunk c goes register slot c % WDEPTH -> LDS buffer c & 1;
   // the one barrier per chunk also orders the buffer reuse (chunk c+2 is
   // stored after every wave passed chunk c+1's barrier, i.e. finished c).
-  float4 gr[WDEPTH][2], xr[WDEPTH][2][WT];
+  float4 gr[WDEPTH][2], xr[WDEPTH][2];
   const int64_t nchunk = m_hi > m_lo ? (m_hi - m_lo + WR - 1) / WR : 0;
 #pragma unroll
   for (int j = 0; j < WDEPTH; ++j)
@@ -710,14 +692,11 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
   }
 
   float* slab = a.part + (int64_t)bz * a.part_stride + a.part_off[b];
+  const int k = k_base + 32 * wk + cl;
 #pragma unroll
-  for (int w = 0; w < WT; ++w) {
-    const int k = k_base + 64 * w + 32 * wk + cl;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = n_base + 32 * wn + (r & 3) + 8 * (r >> 2) + 4 * rl;
-      if (n < a.N && k < kb) slab[(int64_t)n * kb + k] = acc[w][r];
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int n = n_base + 32 * wn + (r & 3) + 8 * (r >> 2) + 4 * rl;
+    if (n < a.N && k < kb) slab[(int64_t)n * kb + k] = acc[r];
   }
   if (do_bias && wk == 0) {
     // lanes l and l+32 hold partial column sums of n = n_base + 32wn + (l&31)
@@ -734,7 +713,7 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
   int by = (int)blockIdx.y, bz = (int)blockIdx.z;
   if (a.xcd_map)
     weight_item(blockIdx.y + blockIdx.z * gridDim.y, gridDim.y, gridDim.y * gridDim.z, by, bz);
-  bwd_weight32_body<1>(a, by, bz, gl, al);
+  bwd_weight32_body(a, by, bz, gl, al);
 }
 
 struct ReduceArgs {
@@ -827,7 +806,7 @@ struct BwdFusedArgs {
   ReduceArgs red;
 };
 
-template <int TND, bool ROWS, int WT>
+template <int TND, bool ROWS>
 __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
   const int L = (int)blk.x;
   if (L >= a.n_wpad + a.n_d) {
@@ -863,17 +842,17 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
   const int Y = a.w.tile_start[a.w.nb];
   int by = L % Y, bz = L / Y;
   if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
-  bwd_weight32_body<WT>(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
-                        reinterpret_cast<float (*)[WR][64 * WT]>(lds + 2 * WR * 64));
+  bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
+                    reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
-template <int TND, bool ROWS, int WT>
+template <int TND, bool ROWS>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   // ROWS: two W buffers + the epilogue scratch (bwd_data_rows_body)
-  constexpr int kW = 2 * WR * 64 * (1 + WT);
+  constexpr int kW = 2 * WR * 64 * 2;
   constexpr int kD = ROWS ? 2 * TND * 16 * KCP + 4 * 16 * (TND * 16 + 4) : 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
-  proj_bwd_fused_body<TND, ROWS, WT>(a, blk_hw(), lds);
+  proj_bwd_fused_body<TND, ROWS>(a, blk_hw(), lds);
 }
 
 // A/B hook (hlhgat_set_proj_bwd_rows): row-block data-gradient workgroups
@@ -885,7 +864,6 @@ bool& proj_bwd_rows_flag() {
 // --- planning ------------------------------------------------------------------
 struct WeightPlan {
   int tiles_n;
-  int kt;  // 64-wide k tiles per item
   int tiles_total;
   int splits;
   int64_t rows_per_split;
@@ -895,50 +873,16 @@ struct WeightPlan {
   int tile_start[MAXB + 1];
 };
 
-// Tunables of the fused Linear backward's weight items (read once; measured
-// defaults): HLHGAT_WT = 64-wide k tiles per item (1..4; 0 = by shape),
-// HLHGAT_WITEMS = target items, HLHGAT_WMINROWS = minimum rows per split.
-int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-int tune_wt() {
-  static const int v = env_int("HLHGAT_WT", 1);
-  return v;
-}
-int tune_witems() {
-  static const int v = env_int("HLHGAT_WITEMS", 384);
-  return v > 0 ? v : 384;
-}
-int tune_wminrows() {
-  static const int v = env_int("HLHGAT_WMINROWS", 128);
-  return v >= 32 ? v : 128;
-}
-
-// k tiles per weight item for these blocks (fused launch only)
-int pick_kt(int nb, const int64_t* kb) {
-  int kt = tune_wt();
-  if (kt < 0 || kt > 4) kt = 1;
-  if (kt == 0) {  // by shape: the widest block's tile count, up to 3
-    int64_t mx = 0;
-    for (int b = 0; b < nb; ++b) mx = std::max<int64_t>(mx, ceil_div(kb[b], WT_COLS));
-    kt = (int)std::min<int64_t>(3, mx);
-  }
-  return kt < 1 ? 1 : kt;
-}
-
 WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
-                       bool with_bias, int kt = 1) {
+                       bool with_bias) {
   WeightPlan p{};
   p.tiles_n = (int)ceil_div(N, WT_ROWS);
-  p.kt = kt;
   int64_t off = 0;
   p.tile_start[0] = 0;
   for (int b = 0; b < nb; ++b) {
     p.part_off[b] = off;
     off += N * kb[b];
-    p.tile_start[b + 1] =
-        p.tile_start[b] + p.tiles_n * (int)ceil_div(ceil_div(kb[b], WT_COLS), kt);
+    p.tile_start[b + 1] = p.tile_start[b] + p.tiles_n * (int)ceil_div(kb[b], WT_COLS);
   }
   p.bias_off = with_bias ? off : -1;
   if (with_bias) off += N;
@@ -947,14 +891,14 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   // aim for ~384 workgroups (1.5 per CU), each slice >= 128 rows: balances
   // MFMA parallelism against the split-slab traffic the reduce re-reads
   const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
-  int64_t splits = ceil_div(tune_witems(), tiles);
+  int64_t splits = ceil_div(384, tiles);
   // large M (config 3 / 5 heads, 1e5+ rows): up to ~1536 workgroups as long
   // as every slice keeps >= 4096 rows (the slab stays small against A);
   // measured 13-22 % faster on the TSP / CIFAR NEInt and conv shapes
   // (tools/kbench.py --big, profiles/r01_h_wsplit.log), ZINC shapes unchanged
   const int64_t big = std::min<int64_t>(ceil_div(1536, tiles), M / 4096);
   if (big > splits) splits = big;
-  int64_t max_splits = ceil_div(M, tune_wminrows());
+  int64_t max_splits = ceil_div(M, 128);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int64_t rps = ceil_div(M, splits);
@@ -1126,10 +1070,8 @@ extern "C" int64_t hlhgat_proj_bwd_weight_workspace_floats(int nblocks,
                                                            int64_t M, int64_t N,
                                                            int with_bias) {
   if (nblocks < 1 || nblocks > MAXB || N <= 0 || M < 0) return 0;
-  // the separate launches plan 1 k tile per item, the fused one pick_kt
   WeightPlan p = plan_weight(nblocks, kb, M, N, with_bias != 0);
-  WeightPlan q = plan_weight(nblocks, kb, M, N, with_bias != 0, pick_kt(nblocks, kb));
-  return (int64_t)std::max(p.splits, q.splits) * p.part_stride;
+  return (int64_t)p.splits * p.part_stride;
 }
 
 extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
@@ -1212,23 +1154,6 @@ namespace {
 static_assert(sizeof(ReduceArgs) + sizeof(int64_t) <= sizeof(hlhgat_reduce_desc_t),
               "hlhgat_reduce_desc_t too small");
 
-using FusedFn = void (*)(BwdFusedArgs);
-template <int TND, bool ROWS>
-FusedFn fused_by_wt(int wt) {
-  switch (wt) {
-    case 2: return k_proj_bwd_fused<TND, ROWS, 2>;
-    case 3: return k_proj_bwd_fused<TND, ROWS, 3>;
-    case 4: return k_proj_bwd_fused<TND, ROWS, 4>;
-    default: return k_proj_bwd_fused<TND, ROWS, 1>;
-  }
-}
-FusedFn fused_kernel(int tnd, bool rows, int wt) {
-  if (rows) return fused_by_wt<4, true>(wt);
-  if (tnd == 1) return fused_by_wt<1, false>(wt);
-  if (tnd == 2) return fused_by_wt<2, false>(wt);
-  return fused_by_wt<4, false>(wt);
-}
-
 int64_t reduce_blocks(const ReduceArgs& r) {
   const int64_t total = r.elem_start[r.nb] + (r.bias_off >= 0 ? r.N : 0);
   return ceil_div(total, 64);
@@ -1264,11 +1189,10 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   bool fuse = want_w && M > 0 && aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
   WeightPlan p{};
   if (want_w) {
-    for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
-    for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
-    p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr, fuse ? pick_kt(nb_w, kb_w) : 1);
+    p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr);
     HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
                   "proj_bwd: workspace too small");
+    for (int b = 0; b < nb_w && fuse; ++b) fuse = vec_ok(A[b], lda[b], kb_w[b]);
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
   if (prev && !fuse) {  // run the merged reduction on its own first
@@ -1317,7 +1241,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   a.part = workspace;
   a.rows_per_split = p.rows_per_split;
   a.tiles_n = p.tiles_n;
-  a.kt = p.kt;
   a.xcd_map = weight_xcd_map();
   f.n_w = p.tiles_total * p.splits;
 
@@ -1374,8 +1297,14 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   bytes += 4.0 * (double)p.splits * p.part_stride;
   ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-  launch(fused_kernel(rows ? 4 : tnd, rows, p.kt), dim3((unsigned)n_blocks), dim3(256), 0, s,
-         &prof, f);
+  if (rows)
+    launch(k_proj_bwd_fused<4, true>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else if (tnd == 1)
+    launch(k_proj_bwd_fused<1, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else if (tnd == 2)
+    launch(k_proj_bwd_fused<2, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else
+    launch(k_proj_bwd_fused<4, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;

@@ -90,6 +90,7 @@ SIGNATURES = {
                                    c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,
                                    c_f32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_set_proj_bn_fused": (c_i32, [c_i32]),
+    "hlhgat_set_proj_bn_split": (c_i32, [c_i32]),
     "hlhgat_set_proj_bwd_rows": (c_i32, [c_i32]),
     "hlhgat_proj_bn_fused_capacity": (c_i32, [P_i64]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),

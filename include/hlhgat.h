@@ -617,6 +617,10 @@ int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
 int hlhgat_set_proj_bwd_rows(int on);
 /* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
 int hlhgat_set_proj_bn_fused(int on);
+/* 1: hlhgat_proj_bn_fwd's fused path as two launches -- the projection with
+ * the statistics in its epilogue (its last workgroup finalises them; no
+ * workgroup waits), then the BatchNorm apply over x -- bitwise the same y. */
+int hlhgat_set_proj_bn_split(int on);
 /* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */
 int hlhgat_proj_bn_fused_capacity(int64_t* out);
 int hlhgat_set_bn_one_launch(int on);

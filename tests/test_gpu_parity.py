@@ -1686,3 +1686,31 @@ def test_proj_bn_handover_bitwise(cuda):
         assert torch.equal(a, b)
     gu = res[1][6]
     assert gu["count"] > 0 and all(r["kernel"] == 2 for r in gu["log"])
+
+
+@pytest.mark.parametrize("M,N,kb,pad", [(23157, 64, [64, 64, 64], 0), (25600, 64, [384, 384], 333),
+                                        (9728, 128, [128, 128], 0)])
+def test_proj_bn_split_bitwise(cuda, M, N, kb, pad):
+    """hlhgat_set_proj_bn_split(1): the projection with the BatchNorm
+    statistics in its epilogue (no workgroup waits), then k_bn_apply == the
+    one launch whose workgroups wait for the statistics: x, y, the batch and
+    running statistics bit for bit."""
+    from hlhgat import _lib
+    g = torch.Generator(device="cpu").manual_seed(M + 7)
+    As = [torch.randn(M, k, generator=g).to(cuda) for k in kb]
+    W = (torch.randn(N, sum(kb), generator=g) / sum(kb) ** 0.5).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    valid = torch.tensor([M - pad], dtype=torch.int32, device=cuda) if pad else None
+    res = []
+    for split in (0, 1):
+        torch.manual_seed(0)
+        bn = torch.nn.BatchNorm1d(N).to(cuda).train()
+        _lib.check(_lib.LIB.hlhgat_set_proj_bn_split(split), "set_proj_bn_split")
+        try:
+            out = _proj_bn_call(cuda, As, W, bias, bn, valid, True, True)
+        finally:
+            _lib.LIB.hlhgat_set_proj_bn_split(0)
+        res.append(list(out) + [bn.running_mean.clone(), bn.running_var.clone(),
+                                bn.num_batches_tracked.clone()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

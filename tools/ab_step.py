@@ -14,8 +14,10 @@ Variants (A/B hooks, not product settings):
   nomlp2      the readout MLP module by module (no two-layer fused node)
   noreadside  the edge readout mean on the main stream
   noreserve   BatchNorm workspaces not reserved before the capture
-  prodbn      NodeEdgeInt hidden-layer rows produced inside the BatchNorm (off by default)
-  bnfold      BatchNorm backward folded into the Linear backward (off by default)
+  twolaunchbn the BatchNorm forward as statistics + apply launches everywhere
+  splitbn     projection + BatchNorm as the projection with a statistics epilogue
+              (no wait) + the apply launch
+  nobarrier   twolaunchbn + splitbn: no kernel of the step waits for another workgroup
 """
 import argparse
 import json
@@ -38,7 +40,8 @@ def set_variant(name, on):
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
     _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
-    _lib.LIB.hlhgat_set_bn_one_launch(0 if (on and name == "twolaunchbn") else 1)
+    _lib.LIB.hlhgat_set_bn_one_launch(0 if (on and name in ("twolaunchbn", "nobarrier")) else 1)
+    _lib.LIB.hlhgat_set_proj_bn_split(1 if (on and name in ("splitbn", "nobarrier")) else 0)
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")

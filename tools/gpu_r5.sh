@@ -61,6 +61,9 @@ for s in "$@"; do
          step pmcgemm_step 200 timeout -s KILL 180 rocprofv3 --pmc $C -d gpurun_out/${TAG}_pg_step -o p --output-format csv -- python3 tools/probes/poly_context.py --steps 3
          python3 tools/pmc_kernel.py $(find gpurun_out/${TAG}_pg_step -name '*counter_collection.csv' | head -1) --match k_proj > gpurun_out/${TAG}_pmc_gemm_step.txt 2>&1 || true
          rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
+    hog) step hog 300 python3 tools/probes/hog_probe.py ;;
+    split) step split 300 $PT tests/test_gpu_parity.py -m gpu -q -k "proj_bn" ;;
+    ab) step ab 900 python3 tools/ab_step.py base1 splitbn twolaunchbn nobarrier base2 --rounds 5 ;;
     kbench) step kbench 300 python3 tools/kbench.py --only "proj" --reps 20 --chain 20 ;;
     wsweep) # weight-item shape sweep of the fused Linear backward (kbench, isolated)
          for wt in 1 2 3 4; do for it in 256 384 512; do
