@@ -1450,31 +1450,29 @@ def _sync_workspace(x: torch.Tensor, n: int, Cc: int) -> torch.Tensor:
     return ws
 
 
-def _all_gather_rows(t: torch.Tensor, group) -> torch.Tensor:
-    """[world, len(t)] gathered in rank order (RCCL all_gather_into_tensor;
-    gloo: list all_gather)."""
+def _sum_over_ranks(t: torch.Tensor, group) -> torch.Tensor:
+    """[1, len(t)]: the fp64 sums of every rank, added by an all-reduce (SUM)
+    -- RCCL under nccl, which a hipGraph capture records like the attention
+    max's all-reduce (an all_gather_into_tensor of the same vector did not
+    capture: hipStreamEndCapture segfaulted, ProcessGroupNCCL's watchdog then
+    queried an event of the capturing stream; round 4).  Every rank receives
+    the same bits; one rank (or no process group) returns t itself, so the
+    statistics are bitwise the single-process BatchNorm's."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return t.view(1, -1)
     from .distributed import collectives_on
-    world = dist.get_world_size(group)
     if not collectives_on(group):
         return t.view(1, -1)
-    out = torch.empty(world, t.numel(), dtype=t.dtype, device=t.device)
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, t, group=group)
-    else:
-        parts = list(out.unbind(0))
-        dist.all_gather(parts, t, group=group)
-        if parts[0].data_ptr() != out[0].data_ptr():
-            out = torch.stack(parts)
-    return out
+    out = t.clone()
+    dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+    return out.view(1, -1)
 
 
 class _SyncBatchNormFn(torch.autograd.Function):
     """BatchNorm1d (+ ReLU) with statistics over all ranks: local fp64 sums
-    (hlhgat_bn_sums_fwd) -> all-gather -> totals in rank order + apply
-    (hlhgat_bn_sync_fwd_apply).  Backward as torch.nn.SyncBatchNorm: global
+    (hlhgat_bn_sums_fwd) -> all-reduce (SUM) -> apply with the totals
+    (hlhgat_bn_sync_fwd_apply, one gathered row).  Backward as torch.nn.SyncBatchNorm: global
     sum g / sum g (x - mean) for dx, local dweight / dbias (DDP averages
     them)."""
 
@@ -1490,7 +1488,7 @@ class _SyncBatchNormFn(torch.autograd.Function):
         check(LIB.hlhgat_bn_sums_fwd(x.data_ptr(), _ld(x), y.data_ptr(), _ld(y), n, _ptr(valid),
                                      Cc, sums.data_ptr(), ws.data_ptr(), ws.numel(), _stream(x)),
               "bn_sums_fwd")
-        gathered = _all_gather_rows(sums, sg.group).contiguous()
+        gathered = _sum_over_ranks(sums, sg.group).contiguous()
         mean = torch.empty(Cc, device=x.device, dtype=x.dtype)
         invstd = torch.empty(Cc, device=x.device, dtype=x.dtype)
         check(LIB.hlhgat_bn_sync_fwd_apply(
@@ -1520,7 +1518,7 @@ class _SyncBatchNormFn(torch.autograd.Function):
             dx.data_ptr(), _ld(dx), n, _ptr(valid), Cc, mean.data_ptr(), invstd.data_ptr(),
             sums.data_ptr(), _ptr(dw), _ptr(db), ws.data_ptr(), ws.numel(), _stream(x)),
             "bn_sums_bwd")
-        gathered = _all_gather_rows(sums, ctx.sg.group).contiguous()
+        gathered = _sum_over_ranks(sums, ctx.sg.group).contiguous()
         check(LIB.hlhgat_bn_sync_bwd_apply(
             x.data_ptr(), _ld(x), _ptr(y), _ld(y) if y is not None else 0, gy.data_ptr(), _ld(gy),
             n, _ptr(valid), Cc, _ptr(weight), mean.data_ptr(), invstd.data_ptr(),

@@ -299,15 +299,10 @@ class TrainStep:
         self._exchange_in_graph = (self.graphs and self._exchange
                                    and dist.get_backend() == "nccl")
         self.graphs_off = None
-        sync_bn = any(ops.sync_bn_group(m) is not None for m in model.modules()
-                      if isinstance(m, torch.nn.modules.batchnorm._BatchNorm))
-        if self.graphs and self._exchange and dist.get_backend() == "nccl" and sync_bn:
-            # measured on MI355X (tests/test_rccl_capture.py): capturing the
-            # SyncBatchNorm all-gathers (RCCL) ends in a segfault inside
-            # hipStreamEndCapture; the all-reduce of the attpool heads captures
-            self.graphs = False
-            self.graphs_off = "SyncBatchNorm all-gathers under RCCL do not capture"
-        elif self.graphs and self._exchange and dist.get_backend() != "nccl" \
+        # (SyncBatchNorm's statistics exchange is an RCCL all-reduce, which
+        # captures; round 4's all-gather made hipStreamEndCapture segfault and
+        # ProcessGroupNCCL's watchdog query an event of the capturing stream)
+        if self.graphs and self._exchange and dist.get_backend() != "nccl" \
                 and forward_collectives(model):
             # a collective inside the forward (SyncBatchNorm statistics, the
             # attpool heads' batch-global max) runs on the host under gloo and

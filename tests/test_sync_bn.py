@@ -2,7 +2,7 @@
 statistics over every rank's rows, so a batch sharded by graph normalises as
 one process over the whole batch does (parity caveat 1).
 
-CPU: the module conversion and the rank-ordered all-gather of the fp64 sums
+CPU: the module conversion and the all-reduce (SUM) of the fp64 sums
 (2 gloo ranks).  GPU: one rank is bitwise the plain HIP BatchNorm; two gloo
 ranks sharing the card (HLHGAT_SHARE_GPU=1, the rehearsal mode of
 hlhgat.distributed.init_distributed) equal one process over the concatenated
@@ -80,21 +80,23 @@ def test_convert_and_revert_mark_every_batchnorm():
     assert all(ops.sync_bn_group(b) is None for b in bns)
 
 
-def _gather_worker(rank, world, port, q):
+def _sum_worker(rank, world, port, q):
     _env(rank, world, port)
-    from hlhgat.ops import _all_gather_rows
+    from hlhgat.ops import _sum_over_ranks
     dist.init_process_group("gloo")
-    t = torch.arange(5, dtype=torch.float64) + 100.0 * rank
-    g = _all_gather_rows(t, None)
+    t = torch.arange(5, dtype=torch.float64) * (1.0 + rank) + 0.1 * rank
+    g = _sum_over_ranks(t, None)
     q.put((rank, g.numpy()))
     dist.destroy_process_group()
 
 
-def test_all_gather_rows_rank_order_gloo():
-    res = _run_ranks(_gather_worker, 2)
-    want = np.stack([np.arange(5) + 100.0 * r for r in range(2)])
-    for r in range(2):
-        assert np.array_equal(res[r], want)
+def test_sum_over_ranks_gloo():
+    """SyncBatchNorm's exchange: the fp64 sums of both ranks added, the same
+    bits on every rank, one row (the apply kernels' gathered[1][2C+1])."""
+    res = _run_ranks(_sum_worker, 2)
+    want = (np.arange(5) * 1.0 + (np.arange(5) * 2.0 + 0.1)).reshape(1, -1)
+    assert np.array_equal(res[0], res[1])
+    assert res[0].shape == (1, 5) and np.allclose(res[0], want, rtol=0, atol=1e-12)
 
 
 # ---------------------------------------------------------------------------
