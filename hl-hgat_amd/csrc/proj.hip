@@ -675,6 +675,18 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
   // stored after every wave passed chunk c+1's barrier, i.e. finished c).
   float4 gr[WDEPTH][2], xr[WDEPTH][2];
   const int64_t nchunk = m_hi > m_lo ? (m_hi - m_lo + WR - 1) / WR : 0;
+  // Two-level fp32 accumulation: the MFMA accumulator chains at most
+  // kFlushChunks chunks (256 rows), then is added into `outer` and restarted.
+  // A split of 4096 rows (configs 3 / 5) otherwise sums 2048 MFMA steps in
+  // one chain -- twice the rounding error of the fp32 CPU GEMM, which blocks
+  // its reduction (the config-5 gradient gate).  Splits of at
+  // most kFlushChunks chunks (config 2) never flush: the same bits as before.
+  constexpr int kFlushChunks = 8;
+  floatx16 outer;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) outer[r] = 0.f;
+  float bouter = 0.f;
+  bool flushed = false;
 #pragma unroll
   for (int j = 0; j < WDEPTH; ++j)
     if (j < nchunk) load(m_lo + j * WR, gr[j], xr[j]);
@@ -688,7 +700,22 @@ __device__ __forceinline__ void bwd_weight32_body(const BwdWeightArgs& a, int by
       __syncthreads();
       if (c + WDEPTH < nchunk) load(m_lo + (c + WDEPTH) * WR, gr[j], xr[j]);
       compute(buf);
+      if ((c + 1) % kFlushChunks == 0 && c + 1 < nchunk) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          outer[r] = outer[r] + acc[r];
+          acc[r] = 0.f;
+        }
+        bouter = bouter + bsum;
+        bsum = 0.f;
+        flushed = true;
+      }
     }
+  }
+  if (flushed) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = outer[r] + acc[r];
+    bsum = bouter + bsum;
   }
 
   float* slab = a.part + (int64_t)bz * a.part_stride + a.part_off[b];
