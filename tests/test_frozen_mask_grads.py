@@ -345,3 +345,93 @@ def test_frozen_mask_grads_heads_realistic_batches(cuda, name, kind, factored):
         assert any(not torch.equal(v, other[k]) for k, v in _HIP_GRADS[name].items())
     _check(name, m, ref64, masked, ref32, cond)
     ops.check_device_errors()
+
+
+@pytest.mark.parametrize("factored", [True, False])
+def test_one_block_gate_cfg5_widths(cuda, factored):
+    """One dense HL block at config-5 widths (d=128, K=4; Laguerre conv on L0
+    and L1, BatchNorm, ReLU -- lib/Hodge_ST_Model.py:22-34 HL_block) on 4 TSP
+    graphs of 2500 nodes, against the fp64 oracle (oracle/hodge_ref.py
+    _ref_block) with the HIP forward's ReLU masks frozen.  One block has no
+    depth to amplify rounding, so this isolates the kernels' own error from the
+    12-block model's conditioning: every parameter and input
+    gradient within 1e-5 of fp64 (max|hip - fp64| <= 1e-5 * max(1, max|fp64|)),
+    the fp32 oracle's own error logged beside it."""
+    from hlhgat import ops
+    from hlhgat.hodge_st_model import _hl_block
+    tol = 1e-5
+    raw = _realistic("tsp")
+    n0, n1 = raw.x_t.shape[0], raw.x_s.shape[0]
+    d, K = 128, 4
+    gen = torch.Generator().manual_seed(7)
+    xt = torch.randn(n0, d, generator=gen)
+    xs = torch.randn(n1, d, generator=gen)
+    Rt = torch.randn(n0, d, generator=gen)
+    Rs = torch.randn(n1, d, generator=gen)
+    torch.manual_seed(3)
+    blk = _hl_block(d, d, d, K, 0.0)
+    for mod in blk.modules():  # non-trivial affine BatchNorm parameters
+        if isinstance(mod, tnn.BatchNorm1d):
+            with torch.no_grad():
+                mod.weight.uniform_(0.5, 1.5, generator=gen)
+                mod.bias.uniform_(-0.5, 0.5, generator=gen)
+    sd = blk.state_dict()
+    blk = blk.to(cuda).train()
+    ops.clear_caches()
+    bd = _to_dev(raw, cuda, factored)
+    xt_d = xt.to(cuda).requires_grad_(True)
+    xs_d = xs.to(cuda).requires_grad_(True)
+    (ot, os_), taps = _run_tapped(lambda: blk(xt_d, bd.edge_index_t, bd.edge_weight_t, xs_d,
+                                              bd.edge_index_s, bd.edge_weight_s))
+    ((ot * Rt.to(cuda)).sum() + (os_ * Rs.to(cuda)).sum()).backward()
+    torch.cuda.synchronize()
+    errs = {}
+    for dt in (torch.float64, torch.float32):
+        ref = R._ref_block(d, d, d, K, 0.0)
+        ref.load_state_dict({k: v.to(dt) if v.is_floating_point() else v for k, v in sd.items()})
+        ref = ref.to(dt).train()
+        _freeze(ref, blk, taps)
+        a = _as_d(raw, dt)
+        xr, sr = xt.to(dt).requires_grad_(True), xs.to(dt).requires_grad_(True)
+        rt, rs = ref(xr, a.edge_index_t, a.edge_weight_t, sr, a.edge_index_s, a.edge_weight_s)
+        ((rt * Rt.to(dt)).sum() + (rs * Rs.to(dt)).sum()).backward()
+        grads = {k: p.grad for k, p in ref.named_parameters()}
+        grads.update({"input.x_t": xr.grad, "input.x_s": sr.grad})
+        if dt == torch.float64:
+            g64, o64 = grads, (rt.detach(), rs.detach())
+            close(ot.detach().cpu(), o64[0], tol, "x_t out vs fp64")
+            close(os_.detach().cpu(), o64[1], tol, "x_s out vs fp64")
+        else:
+            g32 = grads
+    hip = {k: p.grad for k, p in blk.named_parameters()}
+    hip.update({"input.x_t": xt_d.grad, "input.x_s": xs_d.grad})
+    rows, bad = [], []
+    for k, e in g64.items():
+        h = hip[k]
+        scale = max(1.0, float(e.abs().max()))
+        err = float((h.detach().cpu().double() - e).abs().max()) / scale
+        err32 = float((g32[k].double() - e).abs().max()) / scale
+        if TB._bn_fed_bias(k):  # analytically zero (bias before a training BatchNorm):
+            # noise no larger than 3x the fp32 oracle's, as in _check
+            noise32 = float(g32[k].abs().max()) / scale
+            nb = max(1e-3, 3 * noise32)
+            rows.append({"param": k, "err": err, "bound": nb, "kind": "bn-fed bias (noise)"})
+            if err > nb:
+                bad.append((k, err, err32))
+            continue
+        rows.append({"param": k, "err": err, "err_fp32_oracle": err32, "bound": tol,
+                     "scale": scale})
+        if err > tol:
+            bad.append((k, err, err32))
+    case = f"one_block_cfg5_{'factored' if factored else 'csr'}"
+    out_dir = os.path.join(REPO, "gpurun_out", "grad_gates")
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, f"{case}.json"), "w") as f:
+        json.dump({"case": case, "tol": tol, "params": rows}, f, indent=1)
+    worst = max((r["err"], r["param"]) for r in rows if "err_fp32_oracle" in r)
+    worst32 = max(r["err_fp32_oracle"] for r in rows if "err_fp32_oracle" in r)
+    print(f"[one-block] {case}: worst HIP {worst[0]:.2e} ({worst[1]}), worst fp32 oracle "
+          f"{worst32:.2e}")
+    assert ops.has_hodge_factor(bd.edge_index_s) == factored
+    assert not bad, bad
+    ops.check_device_errors()
