@@ -197,7 +197,20 @@ struct BuildArgs {
   const int32_t* rp;       // output row pointer of this operator
   int32_t* col;
   float* val;
+  int64_t cap;             // entries col / val hold
+  unsigned* err;           // device error word (HLHGAT_DEVERR_HODGE_SIZE)
 };
+
+// A row whose end lies past the buffers (row sizes the caller supplied that
+// do not match the graph: duplicate edges, self-loops) writes nothing and
+// raises HLHGAT_DEVERR_HODGE_SIZE; rp is a prefix sum of non-negative sizes,
+// so rp[row + 1] <= cap puts the whole row in range.
+__device__ __forceinline__ bool row_fits(const BuildArgs& a, int64_t row) {
+  if ((int64_t)a.rp[row + 1] <= a.cap && a.rp[row] <= a.rp[row + 1]) return true;
+  if (a.err) __hip_atomic_store(a.err, (unsigned)HLHGAT_DEVERR_HODGE_SIZE, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
+  return false;
+}
 
 __device__ __forceinline__ float hodge_w(int v, float lam) {
   return (2.0f * (float)v) / lam;  // fl(fl(2 v) / lmax), the reference's float32 entry
@@ -211,6 +224,7 @@ __global__ __launch_bounds__(256) void k_hodge_l0_rows(BuildArgs a) {
   const int e0 = a.inc_rowptr[v], e1 = a.inc_rowptr[v + 1];
   const int deg = e1 - e0;
   if (deg == 0) return;  // isolated node: all-zero row, dropped as dense_to_sparse drops zeros
+  if (!row_fits(a, v)) return;
   const float lam = a.lam_node[v];
   int out = a.rp[v];
   int64_t last = -1;
@@ -234,6 +248,7 @@ __global__ __launch_bounds__(256) void k_hodge_l0_rows(BuildArgs a) {
 __global__ __launch_bounds__(256) void k_hodge_l1_rows(BuildArgs a) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= a.n_edges) return;
+  if (!row_fits(a, e)) return;
   const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
   const float lam = a.lam_node[i];
   int p = a.inc_rowptr[i], pe = a.inc_rowptr[i + 1];
@@ -335,14 +350,16 @@ extern "C" int hlhgat_hodge_row_sizes(const int32_t* inc_rowptr, const int64_t* 
 extern "C" int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_edge,
                                   const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
                                   const float* lam_node, const int32_t* rowptr_l0,
-                                  int32_t* col_l0, float* val_l0, const int32_t* rowptr_l1,
-                                  int32_t* col_l1, float* val_l1, void* stream) {
+                                  int32_t* col_l0, float* val_l0, int64_t cap_l0,
+                                  const int32_t* rowptr_l1, int32_t* col_l1, float* val_l1,
+                                  int64_t cap_l1, void* stream) {
   HLH_CHECK_ARG(n_edges >= 0 && n_nodes >= 0 && inc_rowptr && lam_node && rowptr_l0 &&
-                    rowptr_l1 && (n_edges == 0 || (inc_edge && edge_index && col_l0 && val_l0 &&
-                                                   col_l1 && val_l1)),
+                    rowptr_l1 && cap_l0 >= 0 && cap_l1 >= 0 &&
+                    (n_edges == 0 || (inc_edge && edge_index && col_l0 && val_l0 &&
+                                      col_l1 && val_l1)),
                 "hodge_build: bad arguments");
   BuildArgs a{inc_rowptr, inc_edge, edge_index, n_edges, n_nodes, lam_node, rowptr_l0, col_l0,
-              val_l0};
+              val_l0, cap_l0, device_error_word()};
   hipStream_t s = as_stream(stream);
   if (n_nodes > 0) {
     hipLaunchKernelGGL(k_hodge_l0_rows, dim3((unsigned)ceil_div(n_nodes, (int64_t)256)),
@@ -353,6 +370,7 @@ extern "C" int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_
     a.rp = rowptr_l1;
     a.col = col_l1;
     a.val = val_l1;
+    a.cap = cap_l1;
     hipLaunchKernelGGL(k_hodge_l1_rows, dim3((unsigned)ceil_div(n_edges, (int64_t)256)),
                        dim3(256), 0, s, a);
     HLH_CHECK_LAUNCH();

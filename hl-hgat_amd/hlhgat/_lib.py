@@ -70,8 +70,8 @@ SIGNATURES = {
     "hlhgat_eig_pe": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp,
                               c_i64, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_hodge_row_sizes": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
-    "hlhgat_hodge_build": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                   c_vp, c_vp, c_vp]),
+    "hlhgat_hodge_build": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64,
+                                   c_vp, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_proj_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                 c_vp, c_i64, c_i32, c_vp]),
     "hlhgat_proj_bwd_data": (c_i32, [c_i32, c_vp, c_i64, P_vp, P_i64, P_i64, c_i64, c_i64,
@@ -155,6 +155,7 @@ SIGNATURES = {
 POLY_LAGUERRE, POLY_CHEB, POLY_LAGUERRE_DEMO = 0, 1, 2
 SIGMA_SIGMOID, SIGMA_RELU = 0, 1
 DEVERR_BN_STATE = 1
+DEVERR_HODGE_SIZE = 2
 BN_LOG_MAX = 64
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
 PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD, PROF_PROJ_BN = 4, 5, 6, 7

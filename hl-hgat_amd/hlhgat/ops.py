@@ -458,7 +458,9 @@ def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tens
     sizes = (N, nnz(L0), nnz(L1)) when the caller knows them (nnz(L0) = the
     non-isolated nodes + 2 E, nnz(L1) = sum deg^2 - E): then nothing here
     waits on the device (HLHGAT_CHECK_SIZES=1 compares them with the device's
-    own row sizes)."""
+    own row sizes).  Sizes that do not fit the graph never write past the
+    buffers: the build kernels raise HLHGAT_DEVERR_HODGE_SIZE instead
+    (check_device_errors reports it)."""
     _req_dev(edge_index, "edge_index", torch.int64)
     dev = edge_index.device
     counts = torch.as_tensor(node_counts, dtype=torch.int64).to(dev)
@@ -501,12 +503,18 @@ def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tens
     v0 = torch.empty(max(nnz0, 1), dtype=torch.float32, device=dev)
     c1 = torch.empty(max(nnz1, 1), dtype=torch.int32, device=dev)
     v1 = torch.empty(max(nnz1, 1), dtype=torch.float32, device=dev)
+    # the kernels check every row against these capacities (a caller's sizes
+    # that do not fit the graph raise HLHGAT_DEVERR_HODGE_SIZE, nothing past
+    # the buffers is written)
     check(LIB.hlhgat_hodge_build(inc.rowptr.data_ptr(), inc.edge_ids.data_ptr() if E else None,
                                  _ptr(ei) if E else None, E, N, lam_node.data_ptr(), rp0.data_ptr(),
-                                 c0.data_ptr(), v0.data_ptr(), rp1.data_ptr(), c1.data_ptr(),
-                                 v1.data_ptr(), st), "hodge_build")
+                                 c0.data_ptr(), v0.data_ptr(), nnz0,
+                                 rp1.data_ptr(), c1.data_ptr(), v1.data_ptr(),
+                                 nnz1, st), "hodge_build")
 
     def coo(rp, c, v, n, nnz):
+        if sizes is not None:  # row pointers past a caller's nnz: clamped, never written past
+            rp = rp.clamp(max=nnz)
         rows = torch.repeat_interleave(torch.arange(n, device=dev), (rp[1:] - rp[:-1]).long(),
                                        output_size=nnz)
         return torch.stack([rows, c[:nnz].long()]), v[:nnz]
@@ -1602,6 +1610,9 @@ def l1_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
 # device error word (include/hlhgat.h: hlhgat_device_errors)
 # ----------------------------------------------------------------------------
 _DEVERR_TEXT = {
+    _lib.DEVERR_HODGE_SIZE: "hodge_build: a Laplacian row would end past the buffers sized "
+                            "from the caller's sizes= (duplicate edges or self-loops?); the "
+                            "row was not written",
     _lib.DEVERR_BN_STATE: "BatchNorm: an arrival counter was found beyond its total (the "
                           "workspace was written by something else or shared by concurrent "
                           "launches); that launch's statistics are not trusted",

@@ -310,6 +310,11 @@ class SuperpixelPipeline:
         nodes = self._segments(self.n_off[idx], ns)
 
         def nnz(e, n):
+            # the degree formulas (and the Laplacians themselves) assume a
+            # simple graph: unique edges with i < j
+            if e.shape[1] and ((e[0] >= e[1]).any() or
+                               np.unique(e[0] * n + e[1]).size != e.shape[1]):
+                raise ValueError("hlhgat: coarse edges are not unique i < j pairs")
             deg = np.bincount(e.reshape(-1), minlength=n)
             return int((deg > 0).sum()) + 2 * e.shape[1], int((deg * deg).sum()) - e.shape[1]
         ints = [ei_b.reshape(-1), ei1.reshape(-1), ns, E_g, n1, m1,

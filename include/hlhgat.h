@@ -411,12 +411,15 @@ int hlhgat_hodge_row_sizes(const int32_t* inc_rowptr, const int64_t* edge_index,
                            int32_t* sizes_l1, void* stream);
 /* L0 / L1 in CSR, columns ascending, entries fl(fl(2 v) / lam_node[row's
  * graph]) -- the reference's float32 arithmetic -- with v the integer entry
- * of B1 B1^T (deg, -1) / B1^T B1 (2, +1 same-end, -1 tail-to-head). */
+ * of B1 B1^T (deg, -1) / B1^T B1 (2, +1 same-end, -1 tail-to-head).
+ * cap_l0 / cap_l1 = the entries col_l* / val_l* hold: a row that would end
+ * past them (row pointers sized for a simple graph given a multigraph)
+ * writes nothing and raises HLHGAT_DEVERR_HODGE_SIZE. */
 int hlhgat_hodge_build(const int32_t* inc_rowptr, const int32_t* inc_edge,
                        const int64_t* edge_index, int64_t n_edges, int64_t n_nodes,
                        const float* lam_node, const int32_t* rowptr_l0, int32_t* col_l0,
-                       float* val_l0, const int32_t* rowptr_l1, int32_t* col_l1,
-                       float* val_l1, void* stream);
+                       float* val_l0, int64_t cap_l0, const int32_t* rowptr_l1,
+                       int32_t* col_l1, float* val_l1, int64_t cap_l1, void* stream);
 
 /* ---- dense per-simplex projections (fp32 MFMA) ------------------------ */
 #define HLHGAT_MAX_BLOCKS 16
@@ -764,6 +767,9 @@ int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
  * written by something else, or shared by concurrent launches): that launch's
  * statistics are not trusted */
 #define HLHGAT_DEVERR_BN_STATE 1u
+/* hlhgat_hodge_build: a row of L0 / L1 would end past the buffers the caller
+ * sized (the row pointers do not describe a simple graph's Laplacians) */
+#define HLHGAT_DEVERR_HODGE_SIZE 2u
 int hlhgat_device_errors(unsigned* out);
 int hlhgat_clear_device_errors(void);
 

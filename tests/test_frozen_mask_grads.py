@@ -116,10 +116,11 @@ def _check(case, m_hip, ref64, masked, ref32=None, cond=None):
                 bad.append((k, err, noise32))
             continue
         err32 = (float((p32[k].grad.double() - e).abs().max()) / scale) if k in p32 else 0.0
+        # the fp64 conditioning probe is logged, not gated: the
+        # bound is 1e-4 or 3x the fp32 oracle's own error with the same masks
         c = (cond or {}).get(k, 0.0)
-        bound = max(TOL, 3 * max(err32, c))
-        floor = "1e-4" if bound == TOL else ("3x fp32 (frozen)" if err32 >= c else
-                                              "3x fp64 conditioning (frozen)")
+        bound = max(TOL, 3 * err32)
+        floor = "1e-4" if bound == TOL else "3x fp32 (frozen)"
         rows.append({"param": k, "err": err, "bound": bound, "err_fp32_frozen": err32,
                      "cond_fp64_frozen": c, "scale": scale, "floor": floor})
         if err > bound:
@@ -128,13 +129,14 @@ def _check(case, m_hip, ref64, masked, ref32=None, cond=None):
     os.makedirs(out_dir, exist_ok=True)
     tight = [r for r in rows if "err_fp32_frozen" in r]
     n_floor = sum(r["floor"] != "1e-4" for r in tight)
-    n_cond = sum(r["floor"].startswith("3x fp64") for r in tight)
+    n_cond = sum(r["cond_fp64_frozen"] > r["err_fp32_frozen"] for r in tight)
     worst = max((r["err"], r["param"]) for r in tight)
     worst32 = max(r["err_fp32_frozen"] for r in tight)
     with open(os.path.join(out_dir, f"frozen_{case}.json"), "w") as f:
         json.dump({"case": case, "tol": TOL, "n_masks": sum(len(m.masks) for m in masked),
                    "worst_hip": worst[0], "worst_fp32_oracle_frozen": worst32,
-                   "params_at_fp32_floor": n_floor, "params_at_fp64_conditioning": n_cond,
+                   "params_at_fp32_floor": n_floor,
+                   "params_where_fp64_conditioning_exceeds_fp32_error": n_cond,
                    "params": rows}, f, indent=1)
     print(f"[frozen-mask] {case}: {len(tight)} params, worst HIP {worst[0]:.2e} ({worst[1]}), "
           f"worst fp32 oracle {worst32:.2e}; {n_floor} params bounded by the fp32 floor")
@@ -278,10 +280,10 @@ def test_frozen_mask_grads_heads_realistic_batches(cuda, name, kind, factored):
     or within 3x the fp32 oracle's own error where that is larger (each such
     parameter named in the gate log with its fp32 error).  TSP (12 blocks of
     batch-statistics BatchNorm over 10k nodes / 52k edges) is ill-conditioned
-    in fp32 itself (the fp32 oracle is up to ~1e-2 from fp64): there the bound
-    also admits 3x the fp64 gradient's own change under two 1e-6 relative
-    parameter perturbations WITH THE SAME frozen masks (a conditioning probe
-    with no mask flip), logged per parameter."""
+    in fp32 itself (the fp32 oracle is up to ~1e-2 from fp64); the fp64
+    gradient's own change under two 1e-6 relative parameter perturbations
+    WITH THE SAME frozen masks (a conditioning probe with no mask flip) is
+    logged per parameter for information, not used in the bound."""
     import hlhgat
     from hlhgat import ops
     torch.set_num_threads(min(16, os.cpu_count() or 1))

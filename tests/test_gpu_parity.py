@@ -1233,6 +1233,33 @@ def test_device_hodge_builder_matches_reference(cuda):
     close(lam_d.cpu(), torch.tensor(lams), 2e-6, "lanczos lmax")
 
 
+def test_hodge_build_undersized_raises(cuda):
+    """sizes= smaller than the graph's Laplacians (a caller's
+    simple-graph formula given other input): the build kernels write nothing
+    past the buffers and raise HLHGAT_DEVERR_HODGE_SIZE; exact sizes stay
+    clean and bitwise the sizes=None build."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import collate
+    from hlhgat.synthetic import zinc_like_graph
+    b = collate([zinc_like_graph(720 + i) for i in range(4)])
+    ei = dev(b.edge_index)
+    N = int(b.num_node1.sum())
+    lam = torch.ones(4)
+    ops.check_device_errors()
+    ref = ops.hodge_build(ei, b.num_node1.tolist(), lam)
+    nnz0, nnz1 = ref[0].shape[1], ref[2].shape[1]
+    got = ops.hodge_build(ei, b.num_node1.tolist(), lam, sizes=(N, nnz0, nnz1))
+    for x, y in zip(got[:4], ref[:4]):
+        assert torch.equal(x, y)
+    ops.check_device_errors()
+    for short in ((N, nnz0 - 5, nnz1), (N, nnz0, nnz1 - 7), (N, 0, 0)):
+        ops.hodge_build(ei, b.num_node1.tolist(), lam, sizes=short)
+        with pytest.raises(RuntimeError, match="hodge_build"):
+            ops.check_device_errors()
+        ops.clear_device_errors()
+    ops.check_device_errors()
+
+
 def _grads_with_fused_bwd(fused, run):
     from hlhgat import ops
     try:

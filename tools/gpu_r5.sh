@@ -63,6 +63,7 @@ for s in "$@"; do
          rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
+    grad) step grad 900 $PT tests/test_frozen_mask_grads.py -m gpu -v -s ;;
     split) step split 300 $PT tests/test_gpu_parity.py -m gpu -q -k "proj_bn" ;;
     ab) step ab 900 python3 tools/ab_step.py base1 splitbn twolaunchbn nobarrier base2 --rounds 5 ;;
     kbench) step kbench 300 python3 tools/kbench.py --only "proj" --reps 20 --chain 20 ;;
