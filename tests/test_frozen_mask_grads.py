@@ -151,11 +151,17 @@ def _d64(b):
     return d
 
 
-def test_frozen_mask_grads_cfg2_zinc_200(cuda):
-    """Config 2 (6 blocks K=3 d=64, mlp [256, 256]) on 200 ZINC-like graphs."""
+@pytest.mark.parametrize("case,kw", [
+    # config 1 at its exact hyperparameters (main_zinc_HL_HGCNN_dense_int3_pyr.py:151-177):
+    # one level of 2 blocks
+    ("cfg1_zinc_200", dict(channels=[2], filters=[64], mlp_channels=[256, 256], K=3, keig=15)),
+    ("cfg2_zinc_200", dict(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256],
+                           K=3, keig=15))])
+def test_frozen_mask_grads_zinc_200(cuda, case, kw):
+    """Configs 1 (2 blocks) and 2 (6 blocks), K=3 d=64, mlp [256, 256], on 200
+    ZINC-like graphs."""
     import hlhgat
     from hlhgat.synthetic import zinc_like_batch
-    kw = dict(channels=[2, 2, 2], filters=[64, 64, 64], mlp_channels=[256, 256], K=3, keig=15)
     b = zinc_like_batch(200, seed=21)
     torch.manual_seed(0)
     m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**kw)
@@ -175,7 +181,7 @@ def test_frozen_mask_grads_cfg2_zinc_200(cuda):
     (out64 * Rg.double()).sum().backward()
     _freeze(ref32, m, taps)
     (ref32.train()(b) * Rg).sum().backward()
-    _check("cfg2_zinc_200", m, ref64, masked, ref32)
+    _check(case, m, ref64, masked, ref32)
 
 
 @pytest.mark.parametrize("name,factored", [("baseline_cfg3_cifar", False),

@@ -42,6 +42,13 @@ for s in "$@"; do
           S=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
           cp "$S" gpurun_out/${TAG}_bench_kernel_stats.csv || true
           rm -f "$T" ;;
+    prof5) rm -rf gpurun_out/prof5_$TAG  # the config-5 head step (TSP 4x2500), replayed
+          step prof5 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5_$TAG -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+          S=$(find gpurun_out/prof5_$TAG -name '*kernel_stats.csv' | head -1)
+          cp "$S" gpurun_out/${TAG}_cfg5_kernel_stats.csv || true
+          T=$(find gpurun_out/prof5_$TAG -name '*kernel_trace.csv' | head -1)
+          python tools/step_kernels.py "$T" --step -3 > gpurun_out/${TAG}_cfg5_step_kernels.txt || true
+          rm -rf gpurun_out/prof5_$TAG ;;
     pmc) rm -rf gpurun_out/pmcf gpurun_out/pmcw
          E="python3 bench.py --eager --steps 2 --warmup 1 --prof-steps 1 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 1"
          step pmc_fetch 200 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o f --output-format csv -- $E
