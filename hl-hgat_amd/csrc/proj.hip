@@ -18,6 +18,7 @@
 // from L1/L2), 4 waves per workgroup stacked along M.
 #include "gemm_core.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
@@ -743,6 +744,10 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
   bwd_weight32_body(a, by, bz, gl, al);
 }
 
+}  // namespace
+#include "proj_big.h"
+namespace {
+
 struct ReduceArgs {
   int nb;
   int N;
@@ -890,6 +895,9 @@ bool& proj_bwd_rows_flag() {
 
 // --- planning ------------------------------------------------------------------
 struct WeightPlan {
+  int big;      // 0: the 64 x 64 items (bwd_weight32_body); else a BigCfg id
+  int tile_n;   // tile rows (n) and columns (k) of one item
+  int tile_k;
   int tiles_n;
   int tiles_total;
   int splits;
@@ -900,21 +908,105 @@ struct WeightPlan {
   int tile_start[MAXB + 1];
 };
 
+// --- the large-tile family (proj_big.h): when and which tile ------------------
+// HLHGAT_GEMM_BIG: unset = by shape (M >= big_min_m(), summed reduction width
+// >= 128), 0 = never, 1 = every vector-aligned shape (A/B and tests);
+// hlhgat_set_gemm_big overrides both at run time.
+std::atomic<int> g_big_mode{-2};  // -2: not read yet
+std::atomic<int64_t> g_big_min_m{-1};
+int big_mode() {
+  int v = g_big_mode.load(std::memory_order_relaxed);
+  if (v == -2) {
+    const char* e = std::getenv("HLHGAT_GEMM_BIG");
+    v = e ? std::atoi(e) : -1;
+    int expect = -2;
+    g_big_mode.compare_exchange_strong(expect, v);
+    v = g_big_mode.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+int64_t big_min_m() {
+  int64_t v = g_big_min_m.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("HLHGAT_GEMM_BIG_MIN_M");
+    // default above the fused projection + BatchNorm range (<= 512 row blocks)
+    v = e ? (int64_t)std::atoll(e) : (int64_t)32769;
+    int64_t expect = -1;
+    g_big_min_m.compare_exchange_strong(expect, v);
+    v = g_big_min_m.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+bool big_shape(int64_t M, int64_t ktot) {
+  const int m = big_mode();
+  if (m == 0) return false;
+  if (m == 1) return M > 0;
+  return M >= big_min_m() && ktot >= 128;
+}
+
+// tile configurations <WM, WN, TBM, TBN> (4 waves; tile (WM TBM 32) x (WN TBN 32))
+enum BigCfg { kBig128x128 = 1, kBig256x64, kBig256x32, kBig128x64, kBig64x128, kBig64x64,
+              kBig32x128 };
+inline void big_dims(int cfg, int& rows, int& cols) {
+  switch (cfg) {
+    case kBig128x128: rows = 128; cols = 128; return;
+    case kBig256x64: rows = 256; cols = 64; return;
+    case kBig256x32: rows = 256; cols = 32; return;
+    case kBig128x64: rows = 128; cols = 64; return;
+    case kBig64x128: rows = 64; cols = 128; return;
+    case kBig64x64: rows = 64; cols = 64; return;
+    default: rows = 32; cols = 128; return;
+  }
+}
+// forward: rows = M, cols = N
+int big_fwd_cfg(int64_t N) { return N > 64 ? kBig128x128 : (N > 32 ? kBig256x64 : kBig256x32); }
+// data gradient: rows = M, cols = the narrowest block's columns
+int big_data_cfg(int64_t min_kb) {
+  return min_kb >= 128 ? kBig128x128 : (min_kb > 32 ? kBig256x64 : kBig256x32);
+}
+// weight gradient: rows = N, cols = the narrowest block's columns
+int big_weight_cfg(int64_t N, int64_t min_kb) {
+  if (N > 64) return min_kb >= 128 ? kBig128x128 : kBig128x64;
+  if (N > 32) return min_kb >= 128 ? kBig64x128 : kBig64x64;
+  return kBig32x128;
+}
+
 WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
-                       bool with_bias) {
+                       bool with_bias, bool use_big = false) {
   WeightPlan p{};
-  p.tiles_n = (int)ceil_div(N, WT_ROWS);
+  int64_t min_kb = kb[0];
+  for (int b = 1; b < nb; ++b) min_kb = std::min<int64_t>(min_kb, kb[b]);
+  p.big = use_big ? big_weight_cfg(N, min_kb) : 0;
+  if (p.big) big_dims(p.big, p.tile_n, p.tile_k);
+  else {
+    p.tile_n = WT_ROWS;
+    p.tile_k = WT_COLS;
+  }
+  p.tiles_n = (int)ceil_div(N, p.tile_n);
   int64_t off = 0;
   p.tile_start[0] = 0;
   for (int b = 0; b < nb; ++b) {
     p.part_off[b] = off;
     off += N * kb[b];
-    p.tile_start[b + 1] = p.tile_start[b] + p.tiles_n * (int)ceil_div(kb[b], WT_COLS);
+    p.tile_start[b + 1] = p.tile_start[b] + p.tiles_n * (int)ceil_div(kb[b], p.tile_k);
   }
   p.bias_off = with_bias ? off : -1;
   if (with_bias) off += N;
   p.part_stride = off;
   p.tiles_total = p.tile_start[nb];
+  if (p.big) {
+    // two workgroups per CU over (tile, split) items; every split >= 512 rows
+    // (16 stages: the staging prologue stays small against the MFMAs)
+    const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
+    int64_t splits = ceil_div(512, tiles);
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, M / 512));
+    if (splits < 1) splits = 1;
+    int64_t rps = ceil_div(M > 0 ? M : 1, splits);
+    rps = ceil_div(rps, BKC) * BKC;
+    p.rows_per_split = rps;
+    p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
+    return p;
+  }
   // aim for ~384 workgroups (1.5 per CU), each slice >= 128 rows: balances
   // MFMA parallelism against the split-slab traffic the reduce re-reads
   const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
@@ -934,6 +1026,57 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   p.rows_per_split = rps;
   p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
   return p;
+}
+
+void launch_fwd_big(int cfg, unsigned nblk, hipStream_t s, const ProfScope* prof,
+                    const FwdArgs& a) {
+  if (cfg == kBig128x128) launch(k_proj_fwd_big<2, 2, 2, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+  else if (cfg == kBig256x64) launch(k_proj_fwd_big<4, 1, 2, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+  else launch(k_proj_fwd_big<4, 1, 2, 1>, dim3(nblk), dim3(256), 0, s, prof, a);
+}
+
+void launch_data_big(int cfg, unsigned nblk, hipStream_t s, const ProfScope* prof,
+                     const BwdDataArgs& a) {
+  if (cfg == kBig128x128)
+    launch(k_proj_bwd_data_big<2, 2, 2, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+  else if (cfg == kBig256x64)
+    launch(k_proj_bwd_data_big<4, 1, 2, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+  else
+    launch(k_proj_bwd_data_big<4, 1, 2, 1>, dim3(nblk), dim3(256), 0, s, prof, a);
+}
+
+void launch_weight_big(int cfg, unsigned nblk, hipStream_t s, const ProfScope* prof,
+                       const BwdWeightArgs& a) {
+  switch (cfg) {
+    case kBig128x128:
+      launch(k_proj_bwd_weight_big<2, 2, 2, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+      break;
+    case kBig128x64:
+      launch(k_proj_bwd_weight_big<4, 1, 1, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+      break;
+    case kBig64x128:
+      launch(k_proj_bwd_weight_big<2, 2, 1, 2>, dim3(nblk), dim3(256), 0, s, prof, a);
+      break;
+    case kBig64x64:
+      launch(k_proj_bwd_weight_big<2, 2, 1, 1>, dim3(nblk), dim3(256), 0, s, prof, a);
+      break;
+    default:
+      launch(k_proj_bwd_weight_big<1, 4, 1, 1>, dim3(nblk), dim3(256), 0, s, prof, a);
+  }
+}
+
+// The large-tile data gradient of all blocks: one launch (a.tile_start and the
+// grid in units of the configuration's column tile).  Returns the grid size.
+int64_t data_big_setup(BwdDataArgs& a, int& cfg) {
+  int64_t min_kb = a.kb[0];
+  for (int b = 1; b < a.nb; ++b) min_kb = std::min<int64_t>(min_kb, a.kb[b]);
+  cfg = big_data_cfg(min_kb);
+  int rows, cols;
+  big_dims(cfg, rows, cols);
+  a.tile_start[0] = 0;
+  for (int b = 0; b < a.nb; ++b)
+    a.tile_start[b + 1] = a.tile_start[b] + (int)ceil_div(a.kb[b], cols);
+  return ceil_div(a.M, rows) * a.tile_start[a.nb];
 }
 
 // XCD-aware work orders of the weight gradient's items and of the fused
@@ -1008,6 +1151,16 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   double bytes = 4.0 * (double)M * N;
   for (int b = 0; b < nblocks; ++b) bytes += 4.0 * (double)M * kb[b] + 4.0 * N * kb[b];
   ProfScope prof(HLHGAT_PROF_PROJ, s, bytes, flops);
+  if (vec && big_shape(M, ktot)) {
+    const int cfg = big_fwd_cfg(N);
+    int rows, cols;
+    big_dims(cfg, rows, cols);
+    const int64_t nblk = ceil_div(M, rows) * ceil_div(N, cols);
+    HLH_CHECK_ARG(nblk < (int64_t)INT32_MAX, "proj_fwd: grid too large");
+    launch_fwd_big(cfg, (unsigned)nblk, s, &prof, a);
+    HLH_CHECK_LAUNCH();
+    return HLHGAT_OK;
+  }
   if (vec) {
     dim3 g((unsigned)ceil_div(M, 64), (unsigned)ceil_div(N, tn * 16));
     if (tn == 1)
@@ -1069,6 +1222,14 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   for (int b = 0; b < nblocks; ++b)
     vec = vec && aligned16(W[b]) && (ldw[b] % 4) == 0 && (kb[b] % 4) == 0;
   hipStream_t s = as_stream(stream);
+  if (vec && big_shape(M, ktot)) {
+    int cfg;
+    const int64_t nblk = data_big_setup(a, cfg);
+    HLH_CHECK_ARG(nblk < (int64_t)INT32_MAX, "proj_bwd_data: grid too large");
+    launch_data_big(cfg, (unsigned)nblk, s, nullptr, a);
+    HLH_CHECK_LAUNCH();
+    return HLHGAT_OK;
+  }
   dim3 grid((unsigned)ceil_div(M, 4 * 16), (unsigned)a.tile_start[nblocks]);
   if (vec)
   {
@@ -1097,8 +1258,10 @@ extern "C" int64_t hlhgat_proj_bwd_weight_workspace_floats(int nblocks,
                                                            int64_t M, int64_t N,
                                                            int with_bias) {
   if (nblocks < 1 || nblocks > MAXB || N <= 0 || M < 0) return 0;
-  WeightPlan p = plan_weight(nblocks, kb, M, N, with_bias != 0);
-  return (int64_t)p.splits * p.part_stride;
+  // the larger of the two plans: the path is chosen by shape AND alignment
+  const WeightPlan p = plan_weight(nblocks, kb, M, N, with_bias != 0, false);
+  const WeightPlan q = plan_weight(nblocks, kb, M, N, with_bias != 0, true);
+  return std::max((int64_t)p.splits * p.part_stride, (int64_t)q.splits * q.part_stride);
 }
 
 extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc,
@@ -1111,7 +1274,13 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
   HLH_CHECK_ARG(nblocks >= 1 && nblocks <= MAXB, "proj_bwd_weight: nblocks=%d",
                 nblocks);
   HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd_weight: bad dC");
-  WeightPlan p = plan_weight(nblocks, kb, M, N, dbias != nullptr);
+  bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
+  int64_t ktot_w = 0;
+  for (int b = 0; b < nblocks; ++b) {
+    vec = vec && A[b] && aligned16(A[b]) && (lda[b] % 4) == 0 && (kb[b] % 4) == 0;
+    ktot_w += kb[b];
+  }
+  WeightPlan p = plan_weight(nblocks, kb, M, N, dbias != nullptr, vec && big_shape(M, ktot_w));
   HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
                 "proj_bwd_weight: workspace too small");
   BwdWeightArgs a{};
@@ -1157,10 +1326,9 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
     return HLHGAT_OK;
   }
   dim3 grid(1, (unsigned)p.tiles_total, (unsigned)p.splits);
-  bool vec = aligned16(dC) && (lddc % 4) == 0 && (N % 4) == 0;
-  for (int b = 0; b < nblocks; ++b)
-    vec = vec && aligned16(A[b]) && (lda[b] % 4) == 0 && (kb[b] % 4) == 0;
-  if (vec)
+  if (p.big)
+    launch_weight_big(p.big, (unsigned)(p.tiles_total * p.splits), s, nullptr, a);
+  else if (vec)
     launch(k_proj_bwd_weight32, dim3(grid), dim3(256), 0, s, nullptr, a);
   else
     launch(k_proj_bwd_weight, dim3(grid), dim3(256), 0, s, nullptr, a);
@@ -1193,6 +1361,111 @@ int run_reduce(const ReduceArgs& r, hipStream_t s) {
 }
 
 constexpr int64_t kDescMagic = 0x686c6872656431LL;  // "hlhred1"
+
+// The large-tile backward (proj_big.h): an earlier launch's deferred split
+// reduction first (if any), the weight-gradient partials, the data gradient,
+// then this launch's split reduction (or its descriptor, deferred).  Three
+// launches instead of the fused one: at these shapes each runs 100s of us.
+int proj_bwd_big(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
+                 const float* const* A, const int64_t* lda, const int64_t* kb_w,
+                 float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
+                 const float* const* W, const int64_t* ldw, const int64_t* kb_d,
+                 float* const* dA, const int64_t* ldda, int accumulate_d, float* workspace,
+                 int64_t workspace_floats, void* stream, const ReduceArgs* prev,
+                 hlhgat_reduce_desc_t* defer_out, int* deferred) {
+  hipStream_t s = as_stream(stream);
+  if (prev) {
+    const int rc = run_reduce(*prev, s);
+    if (rc != HLHGAT_OK) return rc;
+  }
+  ReduceArgs r{};
+  if (nb_w > 0) {
+    const WeightPlan p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr, true);
+    HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
+                  "proj_bwd: workspace too small");
+    BwdWeightArgs a{};
+    a.nb = nb_w;
+    a.M = M;
+    a.N = (int)N;
+    a.G = dC;
+    a.ldg = lddc;
+    r.nb = nb_w;
+    r.N = (int)N;
+    r.elem_start[0] = 0;
+    double flops = 0, bytes = 4.0 * (double)M * N;
+    for (int b = 0; b < nb_w; ++b) {
+      HLH_CHECK_ARG(A[b] && dW[b] && kb_w[b] > 0 && lda[b] >= kb_w[b] && lddw[b] >= kb_w[b],
+                    "proj_bwd: bad weight block %d", b);
+      a.A[b] = A[b];
+      a.lda[b] = lda[b];
+      a.kb[b] = (int)kb_w[b];
+      a.tile_start[b] = p.tile_start[b];
+      a.part_off[b] = p.part_off[b];
+      r.part_off[b] = p.part_off[b];
+      r.kb[b] = (int)kb_w[b];
+      r.dW[b] = dW[b];
+      r.lddw[b] = lddw[b];
+      r.elem_start[b + 1] = r.elem_start[b] + N * kb_w[b];
+      flops += 2.0 * (double)M * N * kb_w[b];
+      bytes += 4.0 * (double)M * kb_w[b];
+    }
+    a.tile_start[nb_w] = p.tile_start[nb_w];
+    a.bias_off = p.bias_off;
+    a.part_stride = p.part_stride;
+    a.part = workspace;
+    a.rows_per_split = p.rows_per_split;
+    a.tiles_n = p.tiles_n;
+    a.xcd_map = 1;
+    bytes += 4.0 * (double)p.splits * p.part_stride;
+    const int64_t nblk = (int64_t)p.tiles_total * p.splits;
+    HLH_CHECK_ARG(nblk < (int64_t)INT32_MAX, "proj_bwd: grid too large");
+    ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
+    launch_weight_big(p.big, (unsigned)nblk, s, &prof, a);
+    HLH_CHECK_LAUNCH();
+    r.splits = p.splits;
+    r.part = workspace;
+    r.part_stride = p.part_stride;
+    r.bias_off = p.bias_off;
+    r.dbias = dbias;
+    r.accumulate = 0;
+  }
+  if (nb_d > 0) {
+    BwdDataArgs d{};
+    d.nb = nb_d;
+    d.M = M;
+    d.N = (int)N;
+    d.G = dC;
+    d.ldg = lddc;
+    d.accumulate = accumulate_d;
+    double flops = 0, bytes = 4.0 * (double)M * N;
+    for (int b = 0; b < nb_d; ++b) {
+      HLH_CHECK_ARG(W[b] && dA[b] && kb_d[b] > 0 && ldw[b] >= kb_d[b] && ldda[b] >= kb_d[b],
+                    "proj_bwd: bad data block %d", b);
+      d.W[b] = W[b];
+      d.O[b] = dA[b];
+      d.ldw[b] = ldw[b];
+      d.ldo[b] = ldda[b];
+      d.kb[b] = (int)kb_d[b];
+      flops += 2.0 * (double)M * N * kb_d[b];
+      bytes += 4.0 * (double)M * kb_d[b] + 4.0 * N * kb_d[b];
+    }
+    int cfg;
+    const int64_t nblk = data_big_setup(d, cfg);
+    HLH_CHECK_ARG(nblk < (int64_t)INT32_MAX, "proj_bwd: grid too large");
+    ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
+    launch_data_big(cfg, (unsigned)nblk, s, &prof, d);
+    HLH_CHECK_LAUNCH();
+  }
+  if (nb_w == 0) return HLHGAT_OK;
+  if (defer_out) {
+    memset(defer_out, 0, sizeof(*defer_out));
+    defer_out->words[0] = kDescMagic;
+    memcpy(&defer_out->words[1], &r, sizeof(r));
+    if (deferred) *deferred = 1;
+    return HLHGAT_OK;
+  }
+  return run_reduce(r, s);
+}
 
 int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w, const float* const* A, const int64_t* lda,
                   const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
@@ -1237,6 +1510,13 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
                                             accumulate_d, stream);
     return HLHGAT_OK;
   }
+  int64_t ktot_w = 0, ktot_d = 0;
+  for (int b = 0; b < nb_w; ++b) ktot_w += kb_w[b];
+  for (int b = 0; b < nb_d; ++b) ktot_d += kb_d[b];
+  if (big_shape(M, want_w ? ktot_w : ktot_d))
+    return proj_bwd_big(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
+                        dA, ldda, accumulate_d, workspace, workspace_floats, stream, prev,
+                        defer_out, deferred);
   BwdFusedArgs f{};
   BwdWeightArgs& a = f.w;
   ReduceArgs r{};
@@ -1379,6 +1659,13 @@ extern "C" int hlhgat_proj_bwd(int64_t M, int64_t N, const float* dC, int64_t ld
   return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias,
                        nb_d, W, ldw, kb_d, dA, ldda, accumulate_d, workspace, workspace_floats,
                        stream);
+}
+
+extern "C" int hlhgat_set_gemm_big(int mode, int64_t min_m) {
+  HLH_CHECK_ARG(mode >= -1 && mode <= 1, "set_gemm_big: mode must be -1, 0 or 1");
+  g_big_mode.store(mode);
+  if (min_m > 0) g_big_min_m.store(min_m);
+  return HLHGAT_OK;
 }
 
 extern "C" int hlhgat_set_proj_bwd_rows(int on) {

@@ -73,6 +73,8 @@ for s in "$@"; do
     grad) step grad 900 $PT tests/test_frozen_mask_grads.py -m gpu -v -s ;;
     split) step split 300 $PT tests/test_gpu_parity.py -m gpu -q -k "proj_bn" ;;
     ab) step ab 900 python3 tools/ab_step.py base1 splitbn twolaunchbn nobarrier base2 --rounds 5 ;;
+    big) step bigtests 400 $PT tests/test_proj_big.py -m gpu -v -s
+         step bigbench 400 python3 tools/kbench.py --big --reps 10 --chain 5 ;;
     kbench) step kbench 300 python3 tools/kbench.py --only "proj" --reps 20 --chain 20 ;;
     wsweep) # weight-item shape sweep of the fused Linear backward (kbench, isolated)
          for wt in 1 2 3 4; do for it in 256 384 512; do

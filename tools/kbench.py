@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--big", action="store_true",
                     help="config 3 / 5 projection shapes only (CIFAR / TSP heads)")
+    ap.add_argument("--modes", default="0,1",
+                    help="--big: hlhgat_set_gemm_big modes to time (0 small tiles, 1 large)")
     args = ap.parse_args()
     from hlhgat import ops
     from hlhgat.synthetic import zinc_like_batch
@@ -93,11 +95,20 @@ def main():
         return torch.randn(*s, generator=g).to(dev)
 
     if args.big:  # projection shapes of the config-3 / config-5 heads (M rows, N, blocks)
-        for M, N, kbs, tag in [(206858, 128, [928, 928], "TSP NEInt L2 edge Linear(1856,128)"),
-                               (206858, 128, [128] * 4, "TSP conv K=4 d=128"),
-                               (206858, 64, [416, 416], "TSP NEInt L1 edge Linear(832,64)"),
-                               (143192, 256, [448, 448], "CIFAR NEInt L2 edge Linear(896,256)"),
-                               (143192, 64, [64] * 4, "CIFAR conv K=4 d=64")]:
+        # per-GPU config-5 batch: 4 TSP graphs of 2500 nodes -> 10000 nodes,
+        # 51698 edges; widths of the dense-concat NodeEdgeInt (2 d) and the
+        # K=4 convs; config 3: 256 CIFAR superpixel graphs
+        from hlhgat import _lib
+        shapes = [(51698, 128, [800, 800], "TSP edge NEInt L2 Linear(1600,128)"),
+                  (10000, 128, [800, 800], "TSP node NEInt L2 Linear(1600,128)"),
+                  (51698, 128, [128] * 4, "TSP edge conv K=4 d=128"),
+                  (51698, 64, [352, 352], "TSP edge NEInt L1 Linear(704,64)"),
+                  (51698, 64, [64] * 4, "TSP edge conv K=4 d=64"),
+                  (51698, 32, [128, 128], "TSP edge NEInt L0 Linear(256,32)"),
+                  (143192, 256, [448, 448], "CIFAR NEInt L2 edge Linear(896,256)"),
+                  (143192, 64, [64] * 4, "CIFAR conv K=4 d=64")]
+        modes = [int(m) for m in args.modes.split(",")]
+        for M, N, kbs, tag in shapes:
             As = [rnd(M, k) for k in kbs]
             W = rnd(N, sum(kbs))
             Ws, o = [], 0
@@ -107,18 +118,25 @@ def main():
             out = torch.empty(M, N, device=dev)
             fl = 2.0 * M * N * sum(kbs)
             by = 4.0 * M * (sum(kbs) + N)
-            run(f"proj_fwd {tag}", lambda: ops._proj_fwd(As, Ws, M, N, None, out), by, fl)
             G = rnd(M, N)
             dAs = [torch.empty(M, k, device=dev) for k in kbs]
-            run(f"proj_bwd_data {tag}", lambda: ops._proj_bwd_data(G, Ws, kbs, dAs), by, fl)
             dW = torch.empty_like(W)
             dWs, o = [], 0
             for k in kbs:
                 dWs.append(dW[:, o:o + k])
                 o += k
             db = torch.empty(N, device=dev)
-            run(f"proj_bwd_weight {tag}", lambda: ops._proj_bwd_weight(G, As, dWs, db), by, fl)
-            del As, G, dAs
+            for mode in modes:
+                _lib.check(_lib.LIB.hlhgat_set_gemm_big(mode, 0), "set_gemm_big")
+                tg = f"{tag} big={mode}"
+                run(f"proj_fwd {tg}", lambda: ops._proj_fwd(As, Ws, M, N, None, out), by, fl)
+                run(f"proj_bwd_data {tg}", lambda: ops._proj_bwd_data(G, Ws, kbs, dAs), by, fl)
+                run(f"proj_bwd_weight {tg}", lambda: ops._proj_bwd_weight(G, As, dWs, db), by, fl)
+            _lib.check(_lib.LIB.hlhgat_set_gemm_big(-1, 0), "set_gemm_big")
+            Acat = torch.cat(As, 1)
+            run(f"ref torch.mm fwd {tag}", lambda: torch.mm(Acat, W.t(), out=out), by, fl)
+            run(f"ref torch.mm wgrad {tag}", lambda: torch.mm(G.t(), Acat, out=dW), by, fl)
+            del As, G, dAs, Acat
         return
     zb = zinc_like_batch(1000, seed=1).to(dev)
     nt, ns = zb.x_t.shape[0], zb.x_s.shape[0]

@@ -29,10 +29,13 @@ print("hog done", flush=True)
 
 
 def timed(fn):
-    torch.cuda.synchronize()
+    # this stream only: a device-wide synchronize would also wait for the
+    # same-process hog on its own stream
+    cs = torch.cuda.current_stream()
+    cs.synchronize()
     t0 = time.perf_counter()
     fn()
-    torch.cuda.synchronize()
+    cs.synchronize()
     return (time.perf_counter() - t0) * 1e3
 
 
