@@ -16,7 +16,7 @@ from . import ops
 from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt, cluster_mean
 from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
-from .nn import BatchNorm, Sequential, run_mlp_stack
+from .nn import Abs, BatchNorm, Sequential, run_mlp_stack
 
 __all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_pepfunc_dense_int3_pyr",
            "HL_HGCNN_CIFAR10SP_dense_int3_pyr", "HL_HGCNN_zinc_dense_poolint3_pyr",
@@ -380,6 +380,7 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         self.out = Sequential("x_t, edge_index_t, edge_weight_t", [
             (HodgeLaguerreConv(mlp_insize, num_classes, K=1),
              "x_t, edge_index_t, edge_weight_t -> x_t")])
+        self.readout_abs = Abs()  # |B1^T x_t| (:848); a module so the gates can freeze its signs
 
     def forward(self, data, device="cuda:0"):
         dev = data.x_s.device
@@ -423,7 +424,7 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
                     x_t0 = torch.cat([x_t0, x_t], dim=-1)
                     x_s0 = torch.cat([x_s0, x_s], dim=-1)
         # readout (:846-851): x_t2s = |B1^T x_t| / 2 per edge
-        x_t2s = ops.boundary_t(x_t, par_1.incidence()).abs() / 2
+        x_t2s = self.readout_abs(ops.boundary_t(x_t, par_1.incidence())) / 2
         x_s = torch.cat([x_s, x_t2s], dim=-1)
         if len(self.mlp_channels) == 1:
             x_s = self.mlp(x_s, edge_index_s, edge_weight_s)

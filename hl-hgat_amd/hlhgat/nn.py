@@ -100,6 +100,16 @@ def tap(mod, y) -> None:
         TAP.setdefault(mod, []).append(y.detach().clone())
 
 
+class Abs(tnn.Module):
+    """x.abs() as a module (the TSP readout's |B1^T x_t|, lib/Hodge_ST_Model.py:
+    848): under TAP its input is recorded, so the gradient gates can freeze
+    the signs the HIP forward saw (tests/test_frozen_mask_grads.py)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        tap(self, x)
+        return x.abs()
+
+
 class L1Loss(tnn.L1Loss):
     """torch.nn.L1Loss (the ZINC training loss) whose mean reduction on ROCm
     tensors runs as one HIP launch each way (ops.l1_loss: the same input

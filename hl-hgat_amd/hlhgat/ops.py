@@ -86,7 +86,8 @@ def _arr(ctype, vals):
 # backward chains overlap too; captured into a hipGraph the fork/join becomes
 # two graph branches.
 _SIDE_STREAMS = {}
-_FORK_ENABLED = True
+# HLHGAT_STREAM_FORK=0: every chain on one stream (diagnosis / A-B)
+_FORK_ENABLED = os.environ.get("HLHGAT_STREAM_FORK", "1") != "0"
 
 
 def set_stream_fork(enabled: bool) -> None:

@@ -365,6 +365,14 @@ def _batch_vec(counts):
     return torch.cat([torch.full((int(c),), i, dtype=torch.long) for i, c in enumerate(counts)])
 
 
+class Abs(nn.Module):
+    """x.abs() as a module: the readout's |B1^T x_t| (:848), replaceable by a
+    frozen-sign multiplication in the gradient gates (like nn.ReLU's masks)."""
+
+    def forward(self, x):
+        return x.abs()
+
+
 class RefTSPModel(nn.Module):
     """lib/Hodge_ST_Model.py:756-855 (HL_HGCNN_TSP_dense_int3_pyr): no keig
     columns (:764-765), edge mask in x_s[:, 1:], readout |B1^T x_t| / 2 (:848),
@@ -396,6 +404,7 @@ class RefTSPModel(nn.Module):
             mlp_in = mlp_channels[0]
         self.out = RefSequential("x_t, edge_index_t, edge_weight_t", [
             (RefHodgeConv(mlp_in, num_classes, 1), "x_t, edge_index_t, edge_weight_t -> x_t")])
+        self.readout_abs = Abs()
 
     def forward(self, data):
         s_batch = _batch_vec(data.num_edge1)
@@ -413,7 +422,7 @@ class RefTSPModel(nn.Module):
                 x_t0 = torch.cat([x_t0, x_t], dim=-1)
                 x_s0 = torch.cat([x_s0, x_s], dim=-1)
         par_x = par_1 if par_1.dtype == x_t.dtype else par_1.to(x_t.dtype)  # (fp64 studies)
-        x_t2s = torch.sparse.mm(par_x.transpose(0, 1), x_t).abs() / 2            # :848
+        x_t2s = self.readout_abs(torch.sparse.mm(par_x.transpose(0, 1), x_t)) / 2  # :848
         x_s = torch.cat([x_s, x_t2s], dim=-1)
         if len(self.mlp_channels) == 1:
             x_s = self.mlp(x_s, ei_s, ew_s)

@@ -51,7 +51,8 @@ TOL = 1e-4
 
 
 class MaskedReLU(tnn.Module):
-    """ReLU with the mask of a recorded forward: x * [y_hip > 0], call by call."""
+    """ReLU (or Abs) with the mask (signs) of a recorded forward: x * [y_hip > 0]
+    (x * sign(x_hip)), call by call."""
 
     def __init__(self, masks):
         super().__init__()
@@ -78,16 +79,23 @@ def _run_tapped(fn):
 
 
 def _freeze(ref, m_hip, taps):
-    """Replace every nn.ReLU of the oracle `ref` by the HIP forward's masks."""
+    """Replace every nn.ReLU of the oracle `ref` by the HIP forward's masks,
+    and every Abs (the TSP readout's |B1^T x_t|, lib/Hodge_ST_Model.py:848) by
+    multiplication with the signs of the HIP forward's input: sign flips of
+    values within rounding of 0 are the same non-smooth points as ReLU's."""
     names = {id(mod): n for n, mod in m_hip.named_modules()}
-    by_name = {names[id(mod)]: [(y > 0).cpu() for y in ys] for mod, ys in taps.items()}
+    raw = {names[id(mod)]: ys for mod, ys in taps.items()}
     masked = []
     for name, mod in list(ref.named_modules()):
-        if not isinstance(mod, tnn.ReLU):
+        if isinstance(mod, tnn.ReLU):
+            assert name in raw, f"HIP forward recorded no ReLU output for {name}"
+            mm = MaskedReLU([(y > 0).cpu() for y in raw[name]])
+        elif isinstance(mod, R.Abs):
+            assert name in raw, f"HIP forward recorded no Abs input for {name}"
+            mm = MaskedReLU([torch.sign(y).cpu() for y in raw[name]])
+        else:
             continue
-        assert name in by_name, f"HIP forward recorded no ReLU output for {name}"
         parent = ref.get_submodule(name.rsplit(".", 1)[0]) if "." in name else ref
-        mm = MaskedReLU(by_name[name])
         setattr(parent, name.rsplit(".", 1)[-1], mm)
         masked.append(mm)
     return masked

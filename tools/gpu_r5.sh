@@ -47,8 +47,13 @@ for s in "$@"; do
           S=$(find gpurun_out/prof5_$TAG -name '*kernel_stats.csv' | head -1)
           cp "$S" gpurun_out/${TAG}_cfg5_kernel_stats.csv || true
           T=$(find gpurun_out/prof5_$TAG -name '*kernel_trace.csv' | head -1)
-          python tools/step_kernels.py "$T" --step -3 > gpurun_out/${TAG}_cfg5_step_kernels.txt || true
+          python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_cfg5_step_dispatches.csv > gpurun_out/${TAG}_cfg5_step_kernels.txt || true
           rm -rf gpurun_out/prof5_$TAG ;;
+    prof5s) rm -rf gpurun_out/prof5s_$TAG  # the same on ONE stream (HLHGAT_STREAM_FORK=0)
+          HLHGAT_STREAM_FORK=0 step prof5s 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5s_$TAG -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+          T=$(find gpurun_out/prof5s_$TAG -name '*kernel_trace.csv' | head -1)
+          python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_cfg5s_step_dispatches.csv > gpurun_out/${TAG}_cfg5s_step_kernels.txt || true
+          rm -rf gpurun_out/prof5s_$TAG ;;
     pmc) rm -rf gpurun_out/pmcf gpurun_out/pmcw
          E="python3 bench.py --eager --steps 2 --warmup 1 --prof-steps 1 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 1"
          step pmc_fetch 200 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o f --output-format csv -- $E
@@ -68,6 +73,7 @@ for s in "$@"; do
          step pmcgemm_step 200 timeout -s KILL 180 rocprofv3 --pmc $C -d gpurun_out/${TAG}_pg_step -o p --output-format csv -- python3 tools/probes/poly_context.py --steps 3
          python3 tools/pmc_kernel.py $(find gpurun_out/${TAG}_pg_step -name '*counter_collection.csv' | head -1) --match k_proj > gpurun_out/${TAG}_pmc_gemm_step.txt 2>&1 || true
          rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
+    syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
     grad) step grad 900 $PT tests/test_frozen_mask_grads.py -m gpu -v -s ;;
