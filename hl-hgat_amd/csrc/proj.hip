@@ -19,6 +19,7 @@
 #include "gemm_core.h"
 
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -937,6 +938,30 @@ int64_t big_min_m() {
   }
   return v;
 }
+// HLHGAT_LOG_PROJ=1: one stderr line per projection call (shape census)
+bool log_proj() {
+  static const bool v = [] {
+    const char* e = std::getenv("HLHGAT_LOG_PROJ");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+void log_call(const char* what, int64_t M, int64_t N, int nb, const int64_t* kb,
+              const int64_t* ld) {
+  if (!log_proj()) return;
+  char buf[512];
+  int o = snprintf(buf, sizeof(buf), "[hlhgat proj] %s M=%lld N=%lld kb=", what, (long long)M,
+                   (long long)N);
+  for (int b = 0; b < nb && o < 400; ++b)
+    o += snprintf(buf + o, sizeof(buf) - o, "%s%lld", b ? "," : "", (long long)kb[b]);
+  if (ld && o < 400) {
+    o += snprintf(buf + o, sizeof(buf) - o, " ld=");
+    for (int b = 0; b < nb && o < 480; ++b)
+      o += snprintf(buf + o, sizeof(buf) - o, "%s%lld", b ? "," : "", (long long)ld[b]);
+  }
+  fprintf(stderr, "%s\n", buf);
+}
+
 bool big_shape(int64_t M, int64_t ktot) {
   const int m = big_mode();
   if (m == 0) return false;
@@ -1139,6 +1164,7 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
     flops += 2.0 * (double)M * (double)N * (double)kb[b];
   }
   if (M == 0) return HLHGAT_OK;
+  log_call("fwd", M, N, nblocks, kb, lda);
   hipStream_t s = as_stream(stream);
   // 16-column tiles per wave: enough waves to cover the 1024 SIMDs several
   // times over (measured at the HL-HGAT shapes, tools/kbench.py): small M ->
@@ -1513,6 +1539,8 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   int64_t ktot_w = 0, ktot_d = 0;
   for (int b = 0; b < nb_w; ++b) ktot_w += kb_w[b];
   for (int b = 0; b < nb_d; ++b) ktot_d += kb_d[b];
+  log_call("bwd_w", M, N, nb_w, kb_w, lda);
+  log_call("bwd_d", M, N, nb_d, kb_d, nullptr);
   if (big_shape(M, want_w ? ktot_w : ktot_d))
     return proj_bwd_big(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
                         dA, ldda, accumulate_d, workspace, workspace_floats, stream, prev,

@@ -60,7 +60,7 @@ def child(variant):
 
 
 def main():
-    variants = sys.argv[1:] or ["nofork", "nochains", "fwdonly", "bwdonly", "base"]
+    variants = sys.argv[1:] or ["base", "nofork", "nochains"]
     for v in variants:
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0",
                    WORLD_SIZE="1", LOCAL_RANK="0")
