@@ -166,7 +166,12 @@ class _PyrHead(nn.Module):
         # kernels slow the two conv chains more than the overlap saves)
         # the node and edge chains of the block section on two streams with one
         # cross-stream exchange per block (ops.Chains) where the fused paths run
-        chains = ops.Chains(x_t.device) if dense else contextlib.nullcontext()
+        # (not in SyncBatchNorm mode: its statistics all-reduce inside the
+        # cross-block edge chain made hipStreamEndCapture segfault under RCCL,
+        # while per-block fork / join captured bitwise the same step,
+        # tools/probes/syncbn_capture_probe.py)
+        chains = (ops.Chains(x_t.device, enabled=not ops.has_sync_bn(self)) if dense
+                  else contextlib.nullcontext())
         with chains as ch:
             x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
                                          edge_weight_s)

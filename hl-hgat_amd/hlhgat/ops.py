@@ -155,9 +155,9 @@ class Chains:
     each stream).  A cross-stream hazard of a hipGraph capture is caught the
     same way as for ``fork``: the side stream is joined before capture end."""
 
-    def __init__(self, device):
+    def __init__(self, device, enabled: bool = True):
         self.device = device
-        self.on = (CHAINS_ENABLED and _FORK_ENABLED and device is not None
+        self.on = (enabled and CHAINS_ENABLED and _FORK_ENABLED and device is not None
                    and device.type == "cuda" and _ext is not None)
 
     def __enter__(self):
@@ -1439,6 +1439,13 @@ def sync_bn_group(bn) -> Optional[_SyncGroup]:
     if g is None or not _bn_uses_batch_stats(bn):
         return None
     return g
+
+
+def has_sync_bn(module: torch.nn.Module) -> bool:
+    """True when a BatchNorm1d of ``module`` normalises in SyncBatchNorm mode
+    now (hlhgat.distributed.convert_sync_batchnorm, training mode)."""
+    return any(isinstance(m, torch.nn.BatchNorm1d) and sync_bn_group(m) is not None
+               for m in module.modules())
 
 
 _SYNC_WS = {}

@@ -75,6 +75,7 @@ for s in "$@"; do
          rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
     census5) HLHGAT_LOG_PROJ=1 step census5 300 python3 bench.py --workload cfg5 --eager --steps 1 --warmup 0 --batches 1 --no-cpu-baseline
           grep "hlhgat proj" gpurun_out/${TAG}_census5.log | sort | uniq -c | sort -rn > gpurun_out/${TAG}_census5.txt || true ;;
+    kcensus) step kcensus 900 python3 tools/kbench_census.py profiles/r05_cfg5_proj_census.txt ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
