@@ -217,6 +217,26 @@ class Staged:
         self.batch, self.event, self.slot, self.key = batch, event, slot, key
 
 
+def _quiesce_collectives() -> None:
+    """Before a capture: every collective issued so far has completed and left
+    its process group's watchdog list (ProcessGroup._wait_for_pending_works),
+    so no watchdog query of an eager collective's events overlaps the capture
+    (the SyncBatchNorm step's capture_end segfaulted intermittently after eager
+    steps full of statistics all-reduces, round 5)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    torch.cuda.synchronize()
+    from torch.distributed import distributed_c10d as c10d
+    for pg in list(getattr(c10d._world, "pg_map", {}).keys()):
+        wait = getattr(pg, "_wait_for_pending_works", None)
+        if wait is not None:
+            try:
+                wait()
+            except (RuntimeError, NotImplementedError):  # a backend without it (gloo)
+                pass
+
+
 class TrainStep:
     """step(batch) -> loss: forward, loss_fn(out, batch), backward, gradient
     all-reduce (mean over ranks, as DDP) and Adam (L2 weight decay, as
@@ -434,6 +454,7 @@ class TrainStep:
                 self._ext.bn_workspace_reserve(int(h), idx, BN_RESERVE_CHANNELS)
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
+        _quiesce_collectives()
         # thread-local capture: the data loader's collation threads and a
         # StagedFeed thread keep running beside it (pinned allocations, copies
         # on other streams are legal there; a global-mode capture turns them
@@ -698,6 +719,7 @@ class InferStep:
         s = self._stream
         s.wait_stream(torch.cuda.current_stream(self.device))
         ops.clear_caches()
+        _quiesce_collectives()
         with _no_gc(), torch.cuda.graph(g, pool=self._pool, stream=s,
                                         capture_error_mode="thread_local"):
             out = self._forward(static)
