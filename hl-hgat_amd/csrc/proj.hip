@@ -962,11 +962,52 @@ void log_call(const char* what, int64_t M, int64_t N, int nb, const int64_t* kb,
   fprintf(stderr, "%s\n", buf);
 }
 
-bool big_shape(int64_t M, int64_t ktot) {
+// Per operation, by shape (mode -1), from the census-weighted A/B of the
+// config-5 step (tools/kbench_census.py, profiles/r05_kcensus_*.log): the
+// large tiles win where a launch fills the chip several times over and the
+// reduction is long enough to amortise the 128 x 128 staging prologue.
+bool big_mode_decides(int64_t M, bool& out) {
   const int m = big_mode();
-  if (m == 0) return false;
-  if (m == 1) return M > 0;
-  return M >= big_min_m() && ktot >= 128;
+  if (m == 0) { out = false; return true; }
+  if (m == 1) { out = M > 0; return true; }
+  if (M < big_min_m()) { out = false; return true; }
+  return false;
+}
+// forward C = A W^T: N output columns, ktot reduction
+bool big_fwd_ok(int64_t M, int64_t N, int64_t ktot) {
+  bool v;
+  if (big_mode_decides(M, v)) return v;
+  return M >= 2 * big_min_m() && N >= 128 && ktot >= 224;
+}
+// data gradient dA = dC W: reduction N, ktot output columns
+bool big_data_ok(int64_t M, int64_t N, int64_t ktot) {
+  bool v;
+  if (big_mode_decides(M, v)) return v;
+  if (N <= 32) return true;
+  return M >= 2 * big_min_m() && (N >= 256 || (N >= 128 && ktot >= 352));
+}
+// weight gradient dW = dC^T A: N rows, ktot columns, reduction M
+bool big_weight_ok(int64_t M, int64_t N, int64_t ktot) {
+  bool v;
+  if (big_mode_decides(M, v)) return v;
+  return M >= 2 * big_min_m() || (N >= 128 && ktot >= 288);
+}
+
+// compute units of the current device (cached; 256 on MI355X)
+int device_cus() {
+  static std::atomic<int> cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (v <= 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cache[dev].store(cus, std::memory_order_relaxed);
+    v = cus;
+  }
+  return v;
 }
 
 // tile configurations <WM, WN, TBM, TBN> (4 waves; tile (WM TBM 32) x (WN TBN 32))
@@ -1020,10 +1061,12 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   p.part_stride = off;
   p.tiles_total = p.tile_start[nb];
   if (p.big) {
-    // two workgroups per CU over (tile, split) items; every split >= 512 rows
-    // (16 stages: the staging prologue stays small against the MFMAs)
+    // at most one round of two workgroups per CU over (tile, split) items (a
+    // 513th item costs a whole second round: measured 1.2-1.3x at the
+    // config-5 shapes), every split >= 512 rows (16 stages: the staging
+    // prologue stays small against the MFMAs)
     const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
-    int64_t splits = ceil_div(512, tiles);
+    int64_t splits = std::max<int64_t>(1, (2 * (int64_t)device_cus()) / tiles);
     splits = std::min<int64_t>(splits, std::max<int64_t>(1, M / 512));
     if (splits < 1) splits = 1;
     int64_t rps = ceil_div(M > 0 ? M : 1, splits);
@@ -1177,7 +1220,7 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   double bytes = 4.0 * (double)M * N;
   for (int b = 0; b < nblocks; ++b) bytes += 4.0 * (double)M * kb[b] + 4.0 * N * kb[b];
   ProfScope prof(HLHGAT_PROF_PROJ, s, bytes, flops);
-  if (vec && big_shape(M, ktot)) {
+  if (vec && big_fwd_ok(M, N, ktot)) {
     const int cfg = big_fwd_cfg(N);
     int rows, cols;
     big_dims(cfg, rows, cols);
@@ -1248,7 +1291,7 @@ extern "C" int hlhgat_proj_bwd_data(int nblocks, const float* dC, int64_t lddc,
   for (int b = 0; b < nblocks; ++b)
     vec = vec && aligned16(W[b]) && (ldw[b] % 4) == 0 && (kb[b] % 4) == 0;
   hipStream_t s = as_stream(stream);
-  if (vec && big_shape(M, ktot)) {
+  if (vec && big_data_ok(M, N, ktot)) {
     int cfg;
     const int64_t nblk = data_big_setup(a, cfg);
     HLH_CHECK_ARG(nblk < (int64_t)INT32_MAX, "proj_bwd_data: grid too large");
@@ -1306,7 +1349,8 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
     vec = vec && A[b] && aligned16(A[b]) && (lda[b] % 4) == 0 && (kb[b] % 4) == 0;
     ktot_w += kb[b];
   }
-  WeightPlan p = plan_weight(nblocks, kb, M, N, dbias != nullptr, vec && big_shape(M, ktot_w));
+  WeightPlan p = plan_weight(nblocks, kb, M, N, dbias != nullptr,
+                             vec && big_weight_ok(M, N, ktot_w));
   HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
                 "proj_bwd_weight: workspace too small");
   BwdWeightArgs a{};
@@ -1392,7 +1436,8 @@ constexpr int64_t kDescMagic = 0x686c6872656431LL;  // "hlhred1"
 // reduction first (if any), the weight-gradient partials, the data gradient,
 // then this launch's split reduction (or its descriptor, deferred).  Three
 // launches instead of the fused one: at these shapes each runs 100s of us.
-int proj_bwd_big(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
+int proj_bwd_big(bool big_w, bool big_d, int64_t M, int64_t N, const float* dC, int64_t lddc,
+                 int nb_w,
                  const float* const* A, const int64_t* lda, const int64_t* kb_w,
                  float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
                  const float* const* W, const int64_t* ldw, const int64_t* kb_d,
@@ -1406,7 +1451,7 @@ int proj_bwd_big(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   ReduceArgs r{};
   if (nb_w > 0) {
-    const WeightPlan p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr, true);
+    const WeightPlan p = plan_weight(nb_w, kb_w, M, N, dbias != nullptr, big_w);
     HLH_CHECK_ARG(workspace && workspace_floats >= (int64_t)p.splits * p.part_stride,
                   "proj_bwd: workspace too small");
     BwdWeightArgs a{};
@@ -1441,12 +1486,16 @@ int proj_bwd_big(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     a.part = workspace;
     a.rows_per_split = p.rows_per_split;
     a.tiles_n = p.tiles_n;
-    a.xcd_map = 1;
+    a.xcd_map = p.big ? 1 : weight_xcd_map();
     bytes += 4.0 * (double)p.splits * p.part_stride;
     const int64_t nblk = (int64_t)p.tiles_total * p.splits;
     HLH_CHECK_ARG(nblk < (int64_t)INT32_MAX, "proj_bwd: grid too large");
     ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-    launch_weight_big(p.big, (unsigned)nblk, s, &prof, a);
+    if (p.big)
+      launch_weight_big(p.big, (unsigned)nblk, s, &prof, a);
+    else  // the 64 x 64 items (the same bits as the fused small launch's)
+      launch(k_proj_bwd_weight32, dim3(1, (unsigned)p.tiles_total, (unsigned)p.splits), dim3(256),
+             0, s, &prof, a);
     HLH_CHECK_LAUNCH();
     r.splits = p.splits;
     r.part = workspace;
@@ -1455,7 +1504,11 @@ int proj_bwd_big(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     r.dbias = dbias;
     r.accumulate = 0;
   }
-  if (nb_d > 0) {
+  if (nb_d > 0 && !big_d) {
+    const int rc = hlhgat_proj_bwd_data(nb_d, dC, lddc, W, ldw, kb_d, M, N, dA, ldda,
+                                        accumulate_d, stream);
+    if (rc != HLHGAT_OK) return rc;
+  } else if (nb_d > 0) {
     BwdDataArgs d{};
     d.nb = nb_d;
     d.M = M;
@@ -1541,8 +1594,10 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   for (int b = 0; b < nb_d; ++b) ktot_d += kb_d[b];
   log_call("bwd_w", M, N, nb_w, kb_w, lda);
   log_call("bwd_d", M, N, nb_d, kb_d, nullptr);
-  if (big_shape(M, want_w ? ktot_w : ktot_d))
-    return proj_bwd_big(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
+  const bool big_w = want_w && big_weight_ok(M, N, ktot_w);
+  const bool big_d = want_d && big_data_ok(M, N, ktot_d);
+  if (big_w || big_d)
+    return proj_bwd_big(big_w, big_d, M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
                         dA, ldda, accumulate_d, workspace, workspace_floats, stream, prev,
                         defer_out, deferred);
   BwdFusedArgs f{};

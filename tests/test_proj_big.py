@@ -124,10 +124,11 @@ def test_large_tiles_vs_fp64_and_small_tiles(cuda, M, N, kbs):
 
 
 def test_large_tiles_auto_by_shape(cuda):
-    """Mode -1 picks the large tiles at M >= 32769 (config-5 edge rows): the
-    result is bitwise the forced-large one, and differs from the small tiles."""
+    """Mode -1 picks the large-tile forward for config-5 edge rows (M >= 65538,
+    N >= 128, a reduction >= 224): the result is bitwise the forced-large one,
+    and differs from the small tiles."""
     from hlhgat import ops
-    M, N, kbs = 51698, 128, [128] * 4
+    M, N, kbs = 131072, 128, [128] * 4
     As, W, bias, G, C0 = _data(M, N, kbs, seed=5)
     Ad = [a.to(cuda) for a in As]
     Ws = _split(W.to(cuda), kbs)
