@@ -140,3 +140,31 @@ def test_large_tiles_auto_by_shape(cuda):
         outs[mode] = out.cpu()
     assert torch.equal(outs[-1], outs[1])
     assert not torch.equal(outs[1], outs[0])
+
+
+def test_mixed_large_weight_small_data_fused_equals_separate(cuda):
+    """Mode -1 at a config-5 conv shape where the rules differ per part (weight
+    gradient large tiles, data gradient small, M = 131072, N = 64, K = 4 x 64):
+    the fused backward (one hlhgat_proj_bwd call) gives the bits of the
+    separate weight / data calls."""
+    from hlhgat import ops
+    _mode(-1)
+    M, N, kbs = 131072, 64, [64] * 4
+    As, W, bias, G, _ = _data(M, N, kbs, seed=9)
+    Ad = [a.to(cuda) for a in As]
+    Wd = W.to(cuda)
+    Gd = G.to(cuda)
+    dAs = [torch.empty(M, k, device=cuda) for k in kbs]
+    ops._proj_bwd_data(Gd, _split(Wd, kbs), kbs, dAs)
+    dW = torch.empty_like(Wd)
+    db = torch.empty(N, device=cuda)
+    ops._proj_bwd_weight(Gd, Ad, _split(dW, kbs), db)
+    Ar = [a.clone().requires_grad_(True) for a in Ad]
+    Wr = Wd.clone().requires_grad_(True)
+    br = bias.to(cuda).clone().requires_grad_(True)
+    ops.linear_blocks(Ar, Wr, br).backward(Gd)
+    torch.cuda.synchronize()
+    assert torch.equal(Wr.grad, dW) and torch.equal(br.grad, db)
+    for x, y in zip(Ar, dAs):
+        assert torch.equal(x.grad, y)
+    ops.check_device_errors()
