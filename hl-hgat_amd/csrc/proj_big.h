@@ -109,30 +109,40 @@ __device__ __forceinline__ void rstage_store(float (*lds)[COLS], const RStage<CO
   }
 }
 
-// one stage of MFMAs with both operands k-contiguous in swizzled LDS rows
+// one stage of MFMAs with both operands k-contiguous in swizzled LDS rows.
+// The operand registers are double-buffered: group t + 1's ds_reads are issued
+// before group t's 4 TBM TBN MFMAs, so their latency hides behind the MFMAs
+// (with one set, the compiler issued each group's reads after the previous
+// group's MFMAs and waited on them: an exposed LDS round trip per group).
 template <int TBM, int TBN>
 __device__ __forceinline__ void mma_kk(const float (*as)[BKC], const float (*bs)[BKC], int arow0,
                                        int brow0, floatx16 (&acc)[TBM][TBN]) {
   const int lane = threadIdx.x & 63, li = lane & 31, lh = lane >> 5;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    float4 av[TBM], bv[TBN];
+  float4 av[2][TBM], bv[2][TBN];
+  auto fetch = [&](int t, int slot) {
 #pragma unroll
     for (int bm = 0; bm < TBM; ++bm) {
       const int r = arow0 + 32 * bm + li;
-      av[bm] = *reinterpret_cast<const float4*>(&as[r][4 * bslot(r, 4 * lh + t)]);
+      av[slot][bm] = *reinterpret_cast<const float4*>(&as[r][4 * bslot(r, 4 * lh + t)]);
     }
 #pragma unroll
     for (int bn = 0; bn < TBN; ++bn) {
       const int r = brow0 + 32 * bn + li;
-      bv[bn] = *reinterpret_cast<const float4*>(&bs[r][4 * bslot(r, 4 * lh + t)]);
+      bv[slot][bn] = *reinterpret_cast<const float4*>(&bs[r][4 * bslot(r, 4 * lh + t)]);
     }
+  };
+  fetch(0, 0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < 4) fetch(t + 1, cur ^ 1);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int bm = 0; bm < TBM; ++bm)
 #pragma unroll
-        for (int bn = 0; bn < TBN; ++bn) acc[bm][bn] = mfma32(av[bm][e], bv[bn][e], acc[bm][bn]);
+        for (int bn = 0; bn < TBN; ++bn)
+          acc[bm][bn] = mfma32(av[cur][bm][e], bv[cur][bn][e], acc[bm][bn]);
   }
 }
 
@@ -279,27 +289,34 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data_big(BwdDataArgs a) {
       kstage_load<BM>(sg, a.G, a.ldg, m0, a.M, n0 + BKC, a.N);
       rstage_load<BC>(sw, W, ldw, n0 + BKC, a.N, c0, kb);
     }
+    {  // operand registers double-buffered across the 4 groups (see mma_kk)
+      float4 av[2][TBM];
+      float bv[2][TBN][4];
+      auto fetch = [&](int t, int slot) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float4 av[TBM];
-      float bv[TBN][4];
+        for (int bm = 0; bm < TBM; ++bm) {
+          const int r = (wm * TBM + bm) * 32 + li;
+          av[slot][bm] = *reinterpret_cast<const float4*>(&Gs[buf][r][4 * bslot(r, 4 * lh + t)]);
+        }
 #pragma unroll
-      for (int bm = 0; bm < TBM; ++bm) {
-        const int r = (wm * TBM + bm) * 32 + li;
-        av[bm] = *reinterpret_cast<const float4*>(&Gs[buf][r][4 * bslot(r, 4 * lh + t)]);
-      }
+        for (int bn = 0; bn < TBN; ++bn)
 #pragma unroll
-      for (int bn = 0; bn < TBN; ++bn)
+          for (int e = 0; e < 4; ++e)
+            bv[slot][bn][e] = Ws[buf][16 * lh + 4 * t + e][(wn * TBN + bn) * 32 + li];
+      };
+      fetch(0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < 4) fetch(t + 1, cur ^ 1);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          bv[bn][e] = Ws[buf][16 * lh + 4 * t + e][(wn * TBN + bn) * 32 + li];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+          for (int bm = 0; bm < TBM; ++bm)
 #pragma unroll
-        for (int bm = 0; bm < TBM; ++bm)
-#pragma unroll
-          for (int bn = 0; bn < TBN; ++bn)
-            acc[bm][bn] = mfma32(av[bm][e], bv[bn][e], acc[bm][bn]);
+            for (int bn = 0; bn < TBN; ++bn)
+              acc[bm][bn] = mfma32(av[cur][bm][e], bv[cur][bn][e], acc[bm][bn]);
+      }
     }
     if (more) {
       kstage_store<BM>(Gs[buf ^ 1], sg);
@@ -383,25 +400,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       rstage_load<BNT>(sg, a.G, a.ldg, mn, m_hi, n0, a.N);
       rstage_load<BC>(sx, A, lda, mn, m_hi, c0, kb);
     }
+    {  // operand registers double-buffered across the 4 groups (see mma_kk)
+      float av[2][TBM][4], bv[2][TBN][4];
+      auto fetch = [&](int q, int slot) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float av[TBM][4], bv[TBN][4];
+        for (int e = 0; e < 4; ++e) {
+          const int m = 16 * lh + 4 * q + e;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = 16 * lh + 4 * q + e;
-#pragma unroll
-        for (int bm = 0; bm < TBM; ++bm) av[bm][e] = Gs[buf][m][(wm * TBM + bm) * 32 + li];
-#pragma unroll
-        for (int bn = 0; bn < TBN; ++bn) bv[bn][e] = Xs[buf][m][(wn * TBN + bn) * 32 + li];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int bm = 0; bm < TBM; ++bm) {
+          for (int bm = 0; bm < TBM; ++bm)
+            av[slot][bm][e] = Gs[buf][m][(wm * TBM + bm) * 32 + li];
 #pragma unroll
           for (int bn = 0; bn < TBN; ++bn)
-            acc[bm][bn] = mfma32(av[bm][e], bv[bn][e], acc[bm][bn]);
-          if (do_bias) bsum[bm] = bsum[bm] + av[bm][e];
+            bv[slot][bn][e] = Xs[buf][m][(wn * TBN + bn) * 32 + li];
+        }
+      };
+      fetch(0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cur = q & 1;
+        if (q + 1 < 4) fetch(q + 1, cur ^ 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int bm = 0; bm < TBM; ++bm) {
+#pragma unroll
+            for (int bn = 0; bn < TBN; ++bn)
+              acc[bm][bn] = mfma32(av[cur][bm][e], bv[cur][bn][e], acc[bm][bn]);
+            if (do_bias) bsum[bm] = bsum[bm] + av[cur][bm][e];
+          }
         }
       }
     }

@@ -98,8 +98,7 @@ def set_stream_fork(enabled: bool) -> None:
 
 def side_stream(device: torch.device, slot: int = 0) -> torch.cuda.Stream:
     """Side stream `slot` of the device (0: the edge chains; 1: batch
-    preparation that overlaps the first conv; 3: SyncBatchNorm's statistics
-    all-reduce)."""
+    preparation that overlaps the first conv)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE_STREAMS.get((idx, slot))
     if s is None:
@@ -1482,20 +1481,8 @@ def _sum_over_ranks(t: torch.Tensor, group) -> torch.Tensor:
     if not collectives_on(group):
         return t.view(1, -1)
     out = t.clone()
-    if t.is_cuda:
-        # issued from a torch-created stream forked off the current one: with
-        # the current stream the C++ fork's ExternalStream (the edge chain of
-        # ops.Chains), RCCL's capture made hipStreamEndCapture segfault
-        # (tools/probes/syncbn_capture_probe.py, round 5: per-block fork / join
-        # and one-stream runs captured fine)
-        cur = torch.cuda.current_stream(t.device)
-        cs = side_stream(t.device, slot=3)
-        cs.wait_stream(cur)
-        out.record_stream(cs)
-        with torch.cuda.stream(cs):
-            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
-        cur.wait_stream(cs)
-        return out.view(1, -1)
+    # on the current stream (a SyncBatchNorm model's block section runs with
+    # per-block fork / join, not ops.Chains: see _PyrHead.forward)
     dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
     return out.view(1, -1)
 

@@ -76,6 +76,10 @@ for s in "$@"; do
     census5) HLHGAT_LOG_PROJ=1 step census5 300 python3 bench.py --workload cfg5 --eager --steps 1 --warmup 0 --batches 1 --no-cpu-baseline
           grep "hlhgat proj" gpurun_out/${TAG}_census5.log | sort | uniq -c | sort -rn > gpurun_out/${TAG}_census5.txt || true ;;
     kcensus) step kcensus 900 python3 tools/kbench_census.py profiles/r05_cfg5_proj_census.txt ;;
+    ab5) for r in 1 2; do for m in 0 -1; do
+           HLHGAT_GEMM_BIG=$m step ab5_${m}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5_${m}_$r.log | sed "s/^/big=$m run $r /" >> gpurun_out/${TAG}_ab5.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
