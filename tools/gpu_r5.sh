@@ -75,6 +75,8 @@ for s in "$@"; do
          rm -rf gpurun_out/${TAG}_pg_iso gpurun_out/${TAG}_pg_step ;;
     census5) HLHGAT_LOG_PROJ=1 step census5 300 python3 bench.py --workload cfg5 --eager --steps 1 --warmup 0 --batches 1 --no-cpu-baseline
           grep "hlhgat proj" gpurun_out/${TAG}_census5.log | sort | uniq -c | sort -rn > gpurun_out/${TAG}_census5.txt || true ;;
+    census2) HLHGAT_LOG_PROJ=1 step census2 300 python3 bench.py --eager --steps 1 --warmup 0 --prof-steps 1 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 1
+          grep "hlhgat proj" gpurun_out/${TAG}_census2.log | sort | uniq -c | sort -rn > gpurun_out/${TAG}_census2.txt || true ;;
     kcensus) step kcensus 900 python3 tools/kbench_census.py profiles/r05_cfg5_proj_census.txt ;;
     ab5) for r in 1 2; do for m in 0 -1; do
            HLHGAT_GEMM_BIG=$m step ab5_${m}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
