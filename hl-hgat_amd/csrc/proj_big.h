@@ -172,6 +172,72 @@ __device__ __forceinline__ void flush_acc(floatx16 (&acc)[TBM][TBN],
       }
 }
 
+// Epilogue through LDS (the main loop's buffers, free after its last
+// barrier): every wave writes its accumulators (+ `outer`) into the tile
+// (ds_write_b32, 32 consecutive columns per lane group: conflict-free), then
+// the workgroup writes whole rows with float4 stores -- and float4 loads where
+// it accumulates -- instead of 4-byte stores, one per accumulator register,
+// into rows ld apart (the dense-slab outputs and gradient sinks, ld = the slab
+// width, accumulate = 1).  bias (per column) is added on the way.
+template <int WM, int WN, int TBM, int TBN>
+__device__ __forceinline__ void store_tile_lds(const floatx16 (&acc)[TBM][TBN],
+                                               const floatx16 (&outer)[TBM][TBN], bool with_outer,
+                                               float* lds, float* dst, int64_t ld, int64_t row0,
+                                               int64_t rows, int col0, int cols,
+                                               const float* bias, int accumulate) {
+  constexpr int BM = WM * TBM * 32, BN = WN * TBN * 32, C4 = BN / 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave % WM, wn = wave / WM, li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int bm = 0; bm < TBM; ++bm)
+#pragma unroll
+    for (int bn = 0; bn < TBN; ++bn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (wm * TBM + bm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const int cc = (wn * TBN + bn) * 32 + li;
+        lds[rr * BN + cc] = with_outer ? outer[bm][bn][r] + acc[bm][bn][r] : acc[bm][bn][r];
+      }
+  __syncthreads();
+  const bool vec = (reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (ld & 3) == 0 &&
+                   (cols & 3) == 0 && (col0 & 3) == 0 &&
+                   (!bias || (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
+  for (int idx = threadIdx.x; idx < BM * C4; idx += 256) {
+    const int r = idx / C4, c = 4 * (idx % C4);
+    const int64_t row = row0 + r;
+    const int col = col0 + c;
+    if (row >= rows || col >= cols) continue;
+    float4 v = *reinterpret_cast<const float4*>(&lds[r * BN + c]);
+    float* d = dst + row * ld + col;
+    if (vec) {
+      if (bias) {
+        const float4 bv = *reinterpret_cast<const float4*>(bias + col);
+        v.x = v.x + bv.x;
+        v.y = v.y + bv.y;
+        v.z = v.z + bv.z;
+        v.w = v.w + bv.w;
+      }
+      if (accumulate) {
+        const float4 o = *reinterpret_cast<const float4*>(d);
+        v.x = o.x + v.x;
+        v.y = o.y + v.y;
+        v.z = o.z + v.z;
+        v.w = o.w + v.w;
+      }
+      *reinterpret_cast<float4*>(d) = v;
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (col + j >= cols) break;
+        float x = vv[j];
+        if (bias) x = x + bias[col + j];
+        d[j] = accumulate ? d[j] + x : x;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // forward: C[M][N] (+)= sum_b A_b[M][kb] W_b[N][kb]^T + bias
 // Workgroup tile (WM * TBM * 32) x (WN * TBN * 32); grid = row blocks x
@@ -182,9 +248,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void k_proj_fwd_big(FwdArgs a) {
   constexpr int BM = WM * TBM * 32, BN = WN * TBN * 32;
   static_assert(WM * WN == 4, "4 waves");
-  __shared__ __attribute__((aligned(16))) float As[2][BM][BKC];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN][BKC];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  static_assert(2 * (BM + BN) * BKC >= BM * BN, "the epilogue tile fits the stage buffers");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * BKC];
+  float (*As)[BM][BKC] = reinterpret_cast<float (*)[BM][BKC]>(smem);
+  float (*Bs)[BN][BKC] = reinterpret_cast<float (*)[BN][BKC]>(smem + 2 * BM * BKC);
+  const int wave = threadIdx.x >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int ntile = (a.N + BN - 1) / BN;
   const int64_t m0 = (int64_t)(blockIdx.x / ntile) * BM;
@@ -228,24 +296,8 @@ void k_proj_fwd_big(FwdArgs a) {
     b = nbk;
     k0 = nk;
   }
-  const int li = lane & 31, lh = lane >> 5;
-#pragma unroll
-  for (int bn = 0; bn < TBN; ++bn) {
-    const int col = n0 + (wn * TBN + bn) * 32 + li;
-    if (col >= a.N) continue;
-    const float bv = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-    for (int bm = 0; bm < TBM; ++bm)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + (wm * TBM + bm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= a.M) continue;
-        float v = outer[bm][bn][r] + acc[bm][bn][r];
-        if (a.bias) v = v + bv;
-        float* dst = a.C + row * a.ldc + col;
-        *dst = a.accumulate ? *dst + v : v;
-      }
-  }
+  store_tile_lds<WM, WN, TBM, TBN>(acc, outer, true, smem, a.C, a.ldc, m0, a.M, n0, a.N, a.bias,
+                                   a.accumulate);
 }
 
 // ---------------------------------------------------------------------------
@@ -259,8 +311,10 @@ template <int WM, int WN, int TBM, int TBN>
 __global__ __launch_bounds__(256) void k_proj_bwd_data_big(BwdDataArgs a) {
   constexpr int BM = WM * TBM * 32, BC = WN * TBN * 32;
   static_assert(WM * WN == 4, "4 waves");
-  __shared__ __attribute__((aligned(16))) float Gs[2][BM][BKC];
-  __shared__ __attribute__((aligned(16))) float Ws[2][BKC][BC];
+  static_assert(2 * (BM + BC) * BKC >= BM * BC, "the epilogue tile fits the stage buffers");
+  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BC) * BKC];
+  float (*Gs)[BM][BKC] = reinterpret_cast<float (*)[BM][BKC]>(smem);
+  float (*Ws)[BKC][BC] = reinterpret_cast<float (*)[BKC][BC]>(smem + 2 * BM * BKC);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave % WM, wn = wave / WM;
   const int li = lane & 31, lh = lane >> 5;
@@ -325,23 +379,8 @@ __global__ __launch_bounds__(256) void k_proj_bwd_data_big(BwdDataArgs a) {
     __syncthreads();
     buf ^= 1;
   }
-  float* __restrict__ O = a.O[b];
-  const int64_t ldo = a.ldo[b];
-#pragma unroll
-  for (int bn = 0; bn < TBN; ++bn) {
-    const int col = c0 + (wn * TBN + bn) * 32 + li;
-    if (col >= kb) continue;
-#pragma unroll
-    for (int bm = 0; bm < TBM; ++bm)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + (wm * TBM + bm) * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (row >= a.M) continue;
-        float* dst = O + row * ldo + col;
-        const float v = acc[bm][bn][r];
-        *dst = a.accumulate ? *dst + v : v;
-      }
-  }
+  store_tile_lds<WM, WN, TBM, TBN>(acc, acc, false, smem, a.O[b], a.ldo[b], m0, a.M, c0, kb,
+                                   nullptr, a.accumulate);
 }
 
 // ---------------------------------------------------------------------------
