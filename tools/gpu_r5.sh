@@ -37,7 +37,7 @@ for s in "$@"; do
           B="python3 bench.py --steps 20 --warmup 6 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 3"
           step prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- $B
           T=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
-          python tools/step_kernels.py "$T" --step -3 > gpurun_out/${TAG}_step_kernels.txt || true
+          python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_step_dispatches.csv > gpurun_out/${TAG}_step_kernels.txt || true
           python tools/step_gaps.py "$T" --step -3 --top 40 > gpurun_out/${TAG}_step_gaps.txt || true
           S=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
           cp "$S" gpurun_out/${TAG}_bench_kernel_stats.csv || true
