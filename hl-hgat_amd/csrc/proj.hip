@@ -966,6 +966,19 @@ void log_call(const char* what, int64_t M, int64_t N, int nb, const int64_t* kb,
 // config-5 step (tools/kbench_census.py, profiles/r05_kcensus_*.log): the
 // large tiles win where a launch fills the chip several times over and the
 // reduction is long enough to amortise the 128 x 128 staging prologue.
+// HLHGAT_GEMM_BIG_OPS: which operations may take the large tiles in mode -1
+// ("f" forward, "d" data gradient, "w" weight gradient; default all)
+unsigned big_ops() {
+  static const unsigned v = [] {
+    const char* e = std::getenv("HLHGAT_GEMM_BIG_OPS");
+    if (!e) return 7u;
+    unsigned m = 0;
+    for (const char* c = e; *c; ++c) m |= *c == 'f' ? 1u : *c == 'd' ? 2u : *c == 'w' ? 4u : 0u;
+    return m;
+  }();
+  return v;
+}
+
 bool big_mode_decides(int64_t M, bool& out) {
   const int m = big_mode();
   if (m == 0) { out = false; return true; }
@@ -977,12 +990,14 @@ bool big_mode_decides(int64_t M, bool& out) {
 bool big_fwd_ok(int64_t M, int64_t N, int64_t ktot) {
   bool v;
   if (big_mode_decides(M, v)) return v;
+  if (!(big_ops() & 1u)) return false;
   return M >= 2 * big_min_m() && N >= 128 && ktot >= 224;
 }
 // data gradient dA = dC W: reduction N, ktot output columns
 bool big_data_ok(int64_t M, int64_t N, int64_t ktot) {
   bool v;
   if (big_mode_decides(M, v)) return v;
+  if (!(big_ops() & 2u)) return false;
   if (N <= 32) return true;
   return M >= 2 * big_min_m() && (N >= 256 || (N >= 128 && ktot >= 352));
 }
@@ -990,6 +1005,7 @@ bool big_data_ok(int64_t M, int64_t N, int64_t ktot) {
 bool big_weight_ok(int64_t M, int64_t N, int64_t ktot) {
   bool v;
   if (big_mode_decides(M, v)) return v;
+  if (!(big_ops() & 4u)) return false;
   return M >= 2 * big_min_m() || (N >= 128 && ktot >= 288);
 }
 

@@ -86,6 +86,14 @@ for s in "$@"; do
            HLHGAT_STREAM_FORK=$f HLHGAT_GEMM_BIG=$m step ab5f_${f}_${m} 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5f_${f}_${m}.log | sed "s/^/fork=$f big=$m /" >> gpurun_out/${TAG}_ab5f.txt || true
          done; done ;;
+    ab34) for w in cfg3 cfg4; do for m in 0 -1 0 -1; do
+           HLHGAT_GEMM_BIG=$m step ab34_${w}_${m} 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab34_${w}_${m}.log | sed "s/^/$w big=$m /" >> gpurun_out/${TAG}_ab34.txt || true
+         done; done ;;
+    abops) for w in cfg5 cfg3; do for o in x w fw dw; do
+           HLHGAT_GEMM_BIG_OPS=$o step abops_${w}_${o} 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abops_${w}_${o}.log | sed "s/^/$w ops=$o /" >> gpurun_out/${TAG}_abops.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
