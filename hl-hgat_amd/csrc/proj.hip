@@ -1009,6 +1009,18 @@ bool big_weight_ok(int64_t M, int64_t N, int64_t ktot) {
   return M >= 2 * big_min_m() || (N >= 128 && ktot >= 288);
 }
 
+// rounds of two workgroups per CU the large-tile weight gradient is planned
+// for (HLHGAT_BIG_W_ROUNDS; shorter items balance better beside the other
+// chain's kernels, at the cost of a larger split slab)
+int64_t big_w_rounds() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("HLHGAT_BIG_W_ROUNDS");
+    const int64_t r = e ? (int64_t)std::atoll(e) : 1;
+    return r < 1 ? (int64_t)1 : r;
+  }();
+  return v;
+}
+
 // compute units of the current device (cached; 256 on MI355X)
 int device_cus() {
   static std::atomic<int> cache[16];
@@ -1082,7 +1094,7 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
     // config-5 shapes), every split >= 512 rows (16 stages: the staging
     // prologue stays small against the MFMAs)
     const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
-    int64_t splits = std::max<int64_t>(1, (2 * (int64_t)device_cus()) / tiles);
+    int64_t splits = std::max<int64_t>(1, (big_w_rounds() * 2 * (int64_t)device_cus()) / tiles);
     splits = std::min<int64_t>(splits, std::max<int64_t>(1, M / 512));
     if (splits < 1) splits = 1;
     int64_t rps = ceil_div(M > 0 ? M : 1, splits);

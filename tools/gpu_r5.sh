@@ -94,6 +94,10 @@ for s in "$@"; do
            HLHGAT_GEMM_BIG_OPS=$o step abops_${w}_${o} 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abops_${w}_${o}.log | sed "s/^/$w ops=$o /" >> gpurun_out/${TAG}_abops.txt || true
          done; done ;;
+    abw) for w in cfg5 cfg3; do for v in x:1 dw:1 dw:4 dw:8 fdw:8; do o=${v%%:*}; r=${v##*:}
+           HLHGAT_GEMM_BIG_OPS=$o HLHGAT_BIG_W_ROUNDS=$r step abw_${w}_${o}_$r 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abw_${w}_${o}_$r.log | sed "s/^/$w ops=$o rounds=$r /" >> gpurun_out/${TAG}_abw.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
