@@ -910,16 +910,19 @@ struct WeightPlan {
 };
 
 // --- the large-tile family (proj_big.h): when and which tile ------------------
-// HLHGAT_GEMM_BIG: unset = by shape (M >= big_min_m(), summed reduction width
-// >= 128), 0 = never, 1 = every vector-aligned shape (A/B and tests);
-// hlhgat_set_gemm_big overrides both at run time.
+// HLHGAT_GEMM_BIG: 0 (default) = never, -1 = by shape (the rules below),
+// 1 = every vector-aligned shape (A/B and tests); hlhgat_set_gemm_big
+// overrides it at run time.
 std::atomic<int> g_big_mode{-2};  // -2: not read yet
 std::atomic<int64_t> g_big_min_m{-1};
 int big_mode() {
   int v = g_big_mode.load(std::memory_order_relaxed);
   if (v == -2) {
+    // default 0: in the measured training steps (configs 3 and 5, where the
+    // node and edge chains share the GPU) the large tiles lost 1-2 ms per
+    // step although they win shape by shape in isolation
     const char* e = std::getenv("HLHGAT_GEMM_BIG");
-    v = e ? std::atoi(e) : -1;
+    v = e ? std::atoi(e) : 0;
     int expect = -2;
     g_big_mode.compare_exchange_strong(expect, v);
     v = g_big_mode.load(std::memory_order_relaxed);
@@ -1015,7 +1018,7 @@ bool big_weight_ok(int64_t M, int64_t N, int64_t ktot) {
 int64_t big_w_rounds() {
   static const int64_t v = [] {
     const char* e = std::getenv("HLHGAT_BIG_W_ROUNDS");
-    const int64_t r = e ? (int64_t)std::atoll(e) : 1;
+    const int64_t r = e ? (int64_t)std::atoll(e) : 4;
     return r < 1 ? (int64_t)1 : r;
   }();
   return v;

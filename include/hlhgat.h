@@ -615,10 +615,12 @@ int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
                        float* save_mean, float* save_invstd, void* workspace,
                        int64_t workspace_bytes, void* stream);
 /* Large-tile projection kernels (128 x 128 workgroup tiles, 2 x 2 32x32x2
- * MFMA accumulators per wave; the config 3-5 shapes): mode -1 = by shape
- * (M >= min_m rows and a summed reduction width >= 128; default min_m 32769,
- * env HLHGAT_GEMM_BIG_MIN_M), 0 = never, 1 = every 16-B aligned shape (env
- * HLHGAT_GEMM_BIG).  min_m <= 0 keeps the current threshold.  Tests / A-B. */
+ * MFMA accumulators per wave; the config 3-5 shapes): mode 0 = never (the
+ * default: slower inside the measured two-chain steps),
+ * -1 = by shape (per-operation rules from the config-5 census; min_m rows at
+ * least, default 32769, env HLHGAT_GEMM_BIG_MIN_M), 1 = every 16-B aligned
+ * shape.  Env HLHGAT_GEMM_BIG sets the initial mode.  min_m <= 0 keeps the
+ * current threshold. */
 int hlhgat_set_gemm_big(int mode, int64_t min_m);
 /* 0: the fused Linear backward (hlhgat_proj_bwd / _defer) uses one
  * data-gradient workgroup per (row block, 64-column tile) instead of one per

@@ -59,7 +59,9 @@ for s in "$@"; do
          step pmc_fetch 200 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o f --output-format csv -- $E
          step pmc_write 200 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o w --output-format csv -- $E
          python tools/pmc_traffic.py $(find gpurun_out/pmcf -name '*counter_collection.csv' | head -1) $(find gpurun_out/pmcw -name '*counter_collection.csv' | head -1) --kernel k_poly_step --kernel k_proj_fwd --kernel k_edge_gather2 --kernel k_bn_fwd_grid --kernel k_bn_bwd_reduce --kernel k_proj_bwd_fused --kernel k_proj_bn_fwd --out gpurun_out/${TAG}_pmc_traffic.json --label "$TAG bench.py --eager cfg2 step" > /dev/null || true
-         rm -rf gpurun_out/pmcf gpurun_out/pmcw ;;
+         rm -rf gpurun_out/pmcf gpurun_out/pmcw
+         # the bench reads the newest profiles/*_pmc_traffic.json: this round's
+         cp gpurun_out/${TAG}_pmc_traffic.json profiles/r05_pmc_traffic.json || true ;;
     listctr) timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1; echo "=== listctr rc=$?" ;;
     heads) step heads 600 $PT tests -m gpu -v -k "reference_golden or state_dict" ;;
     pmcgemm) # SQ counters of k_proj_bwd_fused: isolated (kbench) and in the replayed step
