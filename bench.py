@@ -81,7 +81,7 @@ def make_batches(n_batches, rank, device, quantum=512, caps=None):
     return [ds.collate(i, caps).to(device) for i in idxs], caps, real, ds.collate(idxs[0]), ds
 
 
-def loader_leg(ds, step, caps, device, ms_step, steps=16):
+def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
     """The data loader beside the step (the reference feeds every step from a
     DataLoader with 4 workers and copies the batch in, main_zinc...:151-162,
     223-225).  Here: graphs/s of hlhgat.loader.GraphLoader (native collate +
@@ -118,7 +118,6 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16):
     from hlhgat.loader import StagedFeed
     ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=4, prefetch=8, pin=True)
     cs = torch.cuda.Stream(device=device)
-    depth = 2
     step.stage_slots = max(step.stage_slots, depth + 1)
 
     def batches():
@@ -990,6 +989,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loader-depth", type=int, default=2,
+                    help="batches StagedFeed uploads ahead of the step (loader leg)")
     ap.add_argument("--no-loader", action="store_true",
                     help="skip the data-loader leg (native collate rates, loader-fed steps)")
     ap.add_argument("--no-parity-check", action="store_true",
@@ -1200,7 +1201,8 @@ def main():
         result["eval"] = _guarded("eval", eval_leg, model, batches)
     if rank == 0 and world == 1 and not args.no_loader:
         log("[rank 0] loader leg")
-        result["loader"] = loader_leg(dataset, step, caps, device, ms_step)
+        result["loader"] = loader_leg(dataset, step, caps, device, ms_step,
+                                      depth=args.loader_depth)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
         result["cpu_baseline"] = cpu_baseline(raw0)

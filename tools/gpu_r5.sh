@@ -100,6 +100,10 @@ for s in "$@"; do
            HLHGAT_GEMM_BIG_OPS=$o HLHGAT_BIG_W_ROUNDS=$r step abw_${w}_${o}_$r 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abw_${w}_${o}_$r.log | sed "s/^/$w ops=$o rounds=$r /" >> gpurun_out/${TAG}_abw.txt || true
          done; done ;;
+    abload) for d in 2 3 4 2 3 4; do
+           step abload_$d 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --loader-depth $d
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']; print('depth', sys.argv[2], r['ms_per_step'], L['loader_fed']['ms_per_step'], round(r['ms_per_step']/L['loader_fed']['ms_per_step'],3), L['loader_fed']['host_ms_per_step'])" gpurun_out/${TAG}_abload_$d.log $d >> gpurun_out/${TAG}_abload.txt || true
+         done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
