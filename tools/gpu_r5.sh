@@ -80,6 +80,7 @@ for s in "$@"; do
     census2) HLHGAT_LOG_PROJ=1 step census2 300 python3 bench.py --eager --steps 1 --warmup 0 --prof-steps 1 --no-cpu-baseline --no-cfg5 --no-heads --no-loader --no-parity-check --no-replay-census --batches 1
           grep "hlhgat proj" gpurun_out/${TAG}_census2.log | sort | uniq -c | sort -rn > gpurun_out/${TAG}_census2.txt || true ;;
     kcensus) step kcensus 900 python3 tools/kbench_census.py profiles/r05_cfg5_proj_census.txt ;;
+    kcensus2) step kcensus2 600 python3 tools/kbench_census.py profiles/r05_cfg2_proj_census.txt --modes 0 --min-gflop 0.1 --reps 10 --chain 10 ;;
     ab5) for r in 1 2; do for m in 0 -1; do
            HLHGAT_GEMM_BIG=$m step ab5_${m}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5_${m}_$r.log | sed "s/^/big=$m run $r /" >> gpurun_out/${TAG}_ab5.txt || true
