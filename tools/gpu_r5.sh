@@ -105,6 +105,10 @@ for s in "$@"; do
            step abload_$d 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --loader-depth $d
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']; print('depth', sys.argv[2], r['ms_per_step'], L['loader_fed']['ms_per_step'], round(r['ms_per_step']/L['loader_fed']['ms_per_step'],3), L['loader_fed']['host_ms_per_step'])" gpurun_out/${TAG}_abload_$d.log $d >> gpurun_out/${TAG}_abload.txt || true
          done ;;
+    abfused) for r in 1 2; do for v in 384:0 384:1 360:0 360:1; do t=${v%%:*}; g=${v##*:}
+           HLHGAT_WSPLIT_TARGET=$t HLHGAT_MERGE_GUARD=$g step abfused_${t}_${g}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abfused_${t}_${g}_$r.log | sed "s/^/target=$t guard=$g run $r /" >> gpurun_out/${TAG}_abfused.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
