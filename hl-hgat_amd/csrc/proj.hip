@@ -1119,8 +1119,8 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
   // aim for ~360 workgroups (1.4 per CU), each slice >= 128 rows: balances
   // MFMA parallelism against the split-slab traffic the reduce re-reads.
   // (384 before round 5: beside the config-2 data-gradient rows (368 / 392
-  // row blocks) the fused launch had 752 / 776 workgroups for 768 slots --
-  // an 8-workgroup tail round at the 25088-row shape.)
+  // row blocks) the fused launch had 752 / 776 workgroups for 768 slots;
+  // 360 measured 2.709-2.711 vs 2.711-2.719 ms per config-2 step.)
   const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
   int64_t splits = ceil_div(wsplit_target(), tiles);
   // large M (config 3 / 5 heads, 1e5+ rows): up to ~1536 workgroups as long
@@ -1476,39 +1476,6 @@ int run_reduce(const ReduceArgs& r, hipStream_t s) {
 
 constexpr int64_t kDescMagic = 0x686c6872656431LL;  // "hlhred1"
 
-// HLHGAT_MERGE_GUARD=0: always merge a deferred reduction into the next
-// fused launch (the round-4 behaviour; A/B)
-bool merge_guard() {
-  static const bool v = [] {
-    const char* e = std::getenv("HLHGAT_MERGE_GUARD");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-// resident workgroups of a fused-backward variant on the whole device
-int64_t fused_slots(bool rows, int tnd) {
-  static std::atomic<int> occ[4];
-  const int idx = rows ? 3 : (tnd == 1 ? 0 : tnd == 2 ? 1 : 2);
-  int v = occ[idx].load(std::memory_order_relaxed);
-  if (v <= 0) {
-    int n = 0;
-    hipError_t e;
-    if (rows)
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_proj_bwd_fused<4, true>, 256, 0);
-    else if (tnd == 1)
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_proj_bwd_fused<1, false>, 256, 0);
-    else if (tnd == 2)
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_proj_bwd_fused<2, false>, 256, 0);
-    else
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_proj_bwd_fused<4, false>, 256, 0);
-    if (e != hipSuccess || n <= 0) n = 2;
-    occ[idx].store(n, std::memory_order_relaxed);
-    v = n;
-  }
-  return (int64_t)v * device_cus();
-}
-
 // The large-tile backward (proj_big.h): an earlier launch's deferred split
 // reduction first (if any), the weight-gradient partials, the data gradient,
 // then this launch's split reduction (or its descriptor, deferred).  Three
@@ -1744,20 +1711,10 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   f.n_d = rows ? f.d_gx : f.d_gx * d.tile_start[nb_d];
   f.d_xcd = data_xcd_map();
   if (prev) {
-    // the earlier launch's split reduction rides along as trailing workgroups
-    // only where it adds no round of workgroups to this launch (a tail of a
-    // few hundred reduce workgroups behind a full round cost more than the
-    // separate launch)
-    const int64_t base = (int64_t)f.n_wpad + (int64_t)f.n_d;
-    const int64_t red = reduce_blocks(*prev);
-    const int64_t slots = fused_slots(rows, tnd);
-    if (!merge_guard() || ceil_div(base + red, slots) == ceil_div(base, slots)) {
-      f.red = *prev;
-      f.n_red = (int)red;
-    } else {
-      const int rc = run_reduce(*prev, as_stream(stream));
-      if (rc != HLHGAT_OK) return rc;
-    }
+    // (merging it only where it adds no round of workgroups -- an extra
+    // launch otherwise -- measured 0.7-1.5 % slower at config 2, round 5)
+    f.red = *prev;
+    f.n_red = (int)reduce_blocks(*prev);
   }
   const int64_t n_blocks = (int64_t)f.n_wpad + (int64_t)f.n_d + (int64_t)f.n_red;
   HLH_CHECK_ARG(n_blocks < (int64_t)INT32_MAX, "proj_bwd: grid too large");
