@@ -80,15 +80,26 @@ bool bn_one_launch() { return bn_one_launch_flag(); }
 // 281.8k, 128 -> 287.2k, 256 -> 286.1k, 32 -> 265.8k graphs/s), one per 512
 // rows above (config 3 / 5 heads, 1.4e5-2e5 rows: 64 workgroups left most of
 // the 256 CUs idle).
-int64_t bn_parts(int64_t n) {
-  int64_t p = std::max<int64_t>(128, ceil_div(n, (int64_t)512));
+int64_t bn_parts(int64_t n, int64_t min_parts = 128) {
+  int64_t p = std::max<int64_t>(min_parts, ceil_div(n, (int64_t)512));
   // small batches (the readout MLP: one row per graph): >= 64 rows per
   // partition, so the finaliser's partial loads stay one batch deep
   p = std::min<int64_t>(p, std::max<int64_t>(1, ceil_div(n, (int64_t)64)));
   return p < 1 ? 1 : (p > kMaxParts ? kMaxParts : p);
 }
 
-BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
+// HLHGAT_BN_BWD_PARTS: minimum row partitions of the backward reduction
+// (default 128, the forward's; A/B)
+int64_t bn_bwd_min_parts() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("HLHGAT_BN_BWD_PARTS");
+    const int64_t p = e ? (int64_t)std::atoll(e) : 128;
+    return p < 1 ? (int64_t)1 : (p > kMaxParts ? (int64_t)kMaxParts : p);
+  }();
+  return v;
+}
+
+BnLayout bn_layout(int64_t n, int64_t C, bool vec, int64_t min_parts = 128) {
   BnLayout L;
   L.v = vec ? 4 : 1;
   int lanes = (int)ceil_div(C, L.v);
@@ -97,7 +108,7 @@ BnLayout bn_layout(int64_t n, int64_t C, bool vec) {
   L.rp = kThreads / L.tpr;
   L.tile_c = L.tpr * L.v;
   L.tiles = (int)ceil_div(C, L.tile_c);
-  int64_t parts = bn_parts(n);
+  int64_t parts = bn_parts(n, min_parts);
   int64_t max_parts = ceil_div(n, (int64_t)L.rp * 2);
   if (parts > max_parts) parts = max_parts;
   if (parts < 1) parts = 1;
@@ -1773,7 +1784,7 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   HLH_CHECK_ARG(workspace && workspace_bytes >= (int64_t)bn_ws_bytes(n, C),
                 "bn_bwd_train: workspace too small");
   const bool vec = bn_vec_ok(C, {ldx, lddy, lddx, y ? ldy : 4}, {x, y, dy, dx});
-  BnLayout L = bn_layout(n, C, vec);
+  BnLayout L = bn_layout(n, C, vec, bn_bwd_min_parts());
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
@@ -1821,7 +1832,7 @@ extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y,
                 "bn_bwd_reduce: workspace too small");
   // the layout hlhgat_bn_bwd_train picks for an aligned dx: the same bits
   const bool vec = bn_vec_ok(C, {ldx, lddy, y ? ldy : 4}, {x, y, dy});
-  BnLayout L = bn_layout(n, C, vec);
+  BnLayout L = bn_layout(n, C, vec, bn_bwd_min_parts());
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_reduce: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
