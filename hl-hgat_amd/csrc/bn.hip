@@ -99,6 +99,16 @@ int64_t bn_bwd_min_parts() {
   return v;
 }
 
+// HLHGAT_BN_BWD_FLAT_MAX: the backward reduction's flat / tree threshold
+int bn_bwd_flat_max() {
+  static const int v = [] {
+    const char* e = std::getenv("HLHGAT_BN_BWD_FLAT_MAX");
+    const int f = e ? std::atoi(e) : kFlatMax;
+    return f < 1 ? 1 : (f > kFlatMax ? kFlatMax : f);
+  }();
+  return v;
+}
+
 BnLayout bn_layout(int64_t n, int64_t C, bool vec, int64_t min_parts = 128) {
   BnLayout L;
   L.v = vec ? 4 : 1;
@@ -202,6 +212,9 @@ struct StatsArgs {
   // SyncBatchNorm (hlhgat_bn_sums_*): the finaliser writes this rank's fp64
   // column sums [S0[C], S1[C], n_eff] here instead of finishing the statistics
   double* sums_out;
+  // last_reduce: one flat pass over the partials up to this many, else the
+  // two-level tree (groups of kGroup); kFlatMax except in the backward
+  int flat_max;
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -550,7 +563,7 @@ template <int NT>
 __device__ __forceinline__ bool last_reduce(const StatsArgs& a, int c0, int tile_c,
                                             double* out0, double* out1, const Blk& blk) {
   const int tile = blk.y;
-  if (a.parts <= kFlatMax) {
+  if (a.parts <= a.flat_max) {
     if (!arrive_last(a.count + tile, (unsigned)a.parts, a.err)) return false;
     flat_reduce<NT>(a.part, a.parts, a, c0, tile_c, out0, out1);
     return true;
@@ -1438,6 +1451,7 @@ StatsArgs stats_args(const BnLayout& L, const BnWs& w, const float* x, int64_t l
   s.count = w.count;
   s.slots = w.slots;
   s.err = hlhgat::device_error_word();
+  s.flat_max = kFlatMax;
   return s;
 }
 
@@ -1788,6 +1802,7 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_train: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
+  s.flat_max = bn_bwd_flat_max();
   s.y = y;
   s.ldy = ldy;
   s.dy = dy;
@@ -1836,6 +1851,7 @@ extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y,
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_bwd_reduce: C too large");
   BnWs w = carve(workspace, n, C);
   StatsArgs s = stats_args(L, w, x, ldx, n, n_valid, C);
+  s.flat_max = bn_bwd_flat_max();
   s.y = y;
   s.ldy = ldy;
   s.dy = dy;

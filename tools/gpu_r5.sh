@@ -117,6 +117,10 @@ for s in "$@"; do
            HLHGAT_WSPLIT_TARGET=$v step abws_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abws_${v}_$r.log | sed "s/^/wsplit_target=$v run $r /" >> gpurun_out/${TAG}_abws.txt || true
          done; done ;;
+    abbn2) for r in 1 2; do for v in 128:256 128:16 512:256 256:16 512:16; do pp=${v%%:*}; fm=${v##*:}
+           HLHGAT_BN_BWD_PARTS=$pp HLHGAT_BN_BWD_FLAT_MAX=$fm step abbn2_${pp}_${fm}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abbn2_${pp}_${fm}_$r.log | sed "s/^/parts=$pp flat_max=$fm run $r /" >> gpurun_out/${TAG}_abbn2.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
