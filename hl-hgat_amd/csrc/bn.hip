@@ -99,11 +99,16 @@ int64_t bn_bwd_min_parts() {
   return v;
 }
 
-// HLHGAT_BN_BWD_FLAT_MAX: the backward reduction's flat / tree threshold
+// The backward reduction's partials go through the two-level tree (groups of
+// kGroup) from 16 partitions up: same-box A/B at config 2 (128 partitions,
+// profiles/r05/ab_cfg2_bn_bwd_tree.txt) 2.695 vs 2.710-2.718 ms with the flat
+// pass.  (The backward has one path, so no other launch's summation order has
+// to match it; the forward keeps the flat order its one- and two-launch paths
+// share.)  HLHGAT_BN_BWD_FLAT_MAX overrides (A/B).
 int bn_bwd_flat_max() {
   static const int v = [] {
     const char* e = std::getenv("HLHGAT_BN_BWD_FLAT_MAX");
-    const int f = e ? std::atoi(e) : kFlatMax;
+    const int f = e ? std::atoi(e) : kGroup;
     return f < 1 ? 1 : (f > kFlatMax ? kFlatMax : f);
   }();
   return v;

@@ -1016,7 +1016,7 @@ bool big_weight_ok(int64_t M, int64_t N, int64_t ktot) {
 int64_t wsplit_target() {
   static const int64_t v = [] {
     const char* e = std::getenv("HLHGAT_WSPLIT_TARGET");
-    const int64_t t = e ? (int64_t)std::atoll(e) : 360;
+    const int64_t t = e ? (int64_t)std::atoll(e) : 240;
     return t < 1 ? (int64_t)1 : t;
   }();
   return v;
@@ -1116,11 +1116,11 @@ WeightPlan plan_weight(int nb, const int64_t* kb, int64_t M, int64_t N,
     p.splits = (int)ceil_div(M > 0 ? M : 1, rps);
     return p;
   }
-  // aim for ~360 workgroups (1.4 per CU), each slice >= 128 rows: balances
-  // MFMA parallelism against the split-slab traffic the reduce re-reads.
-  // (384 before round 5: beside the config-2 data-gradient rows (368 / 392
-  // row blocks) the fused launch had 752 / 776 workgroups for 768 slots;
-  // 360 measured 2.709-2.711 vs 2.711-2.719 ms per config-2 step.)
+  // aim for ~240 workgroups, each slice >= 128 rows: balances MFMA
+  // parallelism against the split-slab traffic the reduce re-reads, beside
+  // the fused launch's data-gradient items (384 before round 5; same-box A/B
+  // of the config-2 step, profiles/r05/ab_cfg2_wsplit_target.txt: 180 2.72-2.73,
+  // 240 2.686-2.688, 360 2.694-2.709, 540 2.73-2.74 ms).
   const int64_t tiles = p.tiles_total > 0 ? p.tiles_total : 1;
   int64_t splits = ceil_div(wsplit_target(), tiles);
   // large M (config 3 / 5 heads, 1e5+ rows): up to ~1536 workgroups as long

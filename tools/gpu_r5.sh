@@ -121,6 +121,10 @@ for s in "$@"; do
            HLHGAT_BN_BWD_PARTS=$pp HLHGAT_BN_BWD_FLAT_MAX=$fm step abbn2_${pp}_${fm}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abbn2_${pp}_${fm}_$r.log | sed "s/^/parts=$pp flat_max=$fm run $r /" >> gpurun_out/${TAG}_abbn2.txt || true
          done; done ;;
+    abnew) for r in 1 2 3; do for v in 360:256 240:16; do t=${v%%:*}; fm=${v##*:}
+           HLHGAT_WSPLIT_TARGET=$t HLHGAT_BN_BWD_FLAT_MAX=$fm step abnew_${t}_${fm}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abnew_${t}_${fm}_$r.log | sed "s/^/wsplit=$t flat_max=$fm run $r /" >> gpurun_out/${TAG}_abnew.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
