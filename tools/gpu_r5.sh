@@ -125,6 +125,11 @@ for s in "$@"; do
            HLHGAT_WSPLIT_TARGET=$t HLHGAT_BN_BWD_FLAT_MAX=$fm step abnew_${t}_${fm}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abnew_${t}_${fm}_$r.log | sed "s/^/wsplit=$t flat_max=$fm run $r /" >> gpurun_out/${TAG}_abnew.txt || true
          done; done ;;
+    abload2) for r in 1 2; do for v in dflt sdma1 sdma0; do
+           case $v in dflt) E="";; sdma1) E="HSA_ENABLE_SDMA=1";; sdma0) E="HSA_ENABLE_SDMA=0";; esac
+           step abload2_${v}_$r 400 env $E python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --loader-depth 2
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']; print(sys.argv[2], r['ms_per_step'], L['loader_fed']['ms_per_step'], round(r['ms_per_step']/L['loader_fed']['ms_per_step'],3), L['loader_fed']['host_ms_per_step'], r['h2d'])" gpurun_out/${TAG}_abload2_${v}_$r.log $v >> gpurun_out/${TAG}_abload2.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
