@@ -111,7 +111,8 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
     for _ in range(2):
         pad_batch(collate(graphs, check_hodge=False), caps)
     out["python_collate_graphs_per_s_1core"] = round(2 * GRAPHS_PER_GPU / (time.perf_counter() - t0), 1)
-    # the loader-fed loop: GraphLoader(4 threads, pinned) -> StagedFeed (a
+    # the loader-fed loop: GraphLoader(4 threads, pinned; GraphLoader.stream:
+    # one collation pool prefetching across epochs) -> StagedFeed (a
     # feeder thread: TrainStep.stage, H2D on a copy stream straight into the
     # static buffers of a captured graph, two batches ahead) -> the replayed
     # step with no copy-in, launched from this thread alone
@@ -120,12 +121,7 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
     cs = torch.cuda.Stream(device=device)
     step.stage_slots = max(step.stage_slots, depth + 1)
 
-    def batches():
-        while True:
-            for b in ld:
-                yield b
-
-    feed = StagedFeed(batches(), step, depth=depth, stream=cs)
+    feed = StagedFeed(ld.stream(), step, depth=depth, stream=cs)
     it = iter(feed)
     host = {"wait_feed": 0.0, "step_call": 0.0}
     warm = 4  # the first steps capture the shape's third graph
@@ -134,6 +130,7 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             host = {k: 0.0 for k in host}
+            feed.timing.update(source=0.0, room=0.0, stage=0.0, n=0)
         ta = time.perf_counter()
         st = next(it)
         tb = time.perf_counter()
@@ -151,6 +148,8 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
                          "ms_per_step": round(dt * 1e3, 3), "workers": 4, "pinned": True,
                          "steps": steps, "stage_depth": depth,
                          "host_ms_per_step": {k: round(v / steps * 1e3, 3) for k, v in host.items()},
+                         "feeder_ms_per_batch": {k: round(feed.timing[k] / max(1, feed.timing["n"]) * 1e3, 3)
+                                                 for k in ("source", "room", "stage")},
                          "what": "training steps fed by GraphLoader end to end: native collate "
                                  "on 4 threads, hlhgat.loader.StagedFeed's thread uploading "
                                  "(TrainStep.stage: one H2D copy per batch on a copy stream, "

@@ -96,6 +96,37 @@ class GraphLoader:
                 yield b
 
 
+    def stream(self, epochs: Optional[int] = None) -> Iterator[Batch]:
+        """Batches of `epochs` consecutive epochs (None = without end) from ONE
+        pool of collation threads whose prefetch runs across epoch boundaries
+        -- iterating the loader once per epoch restarts the pipeline (a fresh
+        pool and an empty prefetch queue) every epoch, and the consumer then
+        waits for the first batch's collation.  Each epoch has its own order
+        and capacity bucket, as __iter__."""
+        def jobs():
+            e = 0
+            while epochs is None or e < epochs:
+                idxs = self.batch_indices(self.epoch)
+                caps = self.epoch_caps(idxs)
+                self.epoch += 1
+                e += 1
+                for i in idxs:
+                    yield i, caps
+        with ThreadPoolExecutor(self.workers, thread_name_prefix="hlhgat-collate") as ex:
+            pending = deque()
+            it = jobs()
+            for i, caps in it:
+                pending.append(ex.submit(self.dataset.collate, i, caps, self.pin))
+                if len(pending) >= self.prefetch:
+                    break
+            while pending:
+                b = pending.popleft().result()
+                nxt = next(it, None)
+                if nxt is not None:
+                    pending.append(ex.submit(self.dataset.collate, nxt[0], nxt[1], self.pin))
+                yield b
+
+
 class StagedFeed:
     """The host side of the training loop off the thread that launches the
     steps: a feeder thread takes collated batches from ``batches`` (e.g. a
@@ -132,17 +163,32 @@ class StagedFeed:
         self._room = threading.Semaphore(self.depth)
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
+        self.timing = {"source": 0.0, "room": 0.0, "stage": 0.0, "n": 0}
 
     def _run(self):
+        import time
         it = iter(self.batches)
+        clock = time.perf_counter
         try:
+            t0 = clock()
             for b in it:
+                t1 = clock()
                 while not self._room.acquire(timeout=0.1):
                     if self._stop.is_set():
                         return
                 if self._stop.is_set():
                     return
-                self._q.put(self.step.stage(b, self.stream))
+                t2 = clock()
+                st = self.step.stage(b, self.stream)
+                t3 = clock()
+                self._q.put(st)
+                # feeder time per batch: waiting for the source, for room
+                # (the consumer), in stage() (diagnostics, bench loader leg)
+                self.timing["source"] += t1 - t0
+                self.timing["room"] += t2 - t1
+                self.timing["stage"] += t3 - t2
+                self.timing["n"] += 1
+                t0 = clock()
             self._q.put(self._END)
         except BaseException as e:  # handed to the consumer
             self._q.put(e)

@@ -627,6 +627,27 @@ def test_graph_loader_batches_in_order_and_shuffled():
     _same_batch(b0, collate([gs[i] for i in sh.batch_indices(0)[0]], check_hodge=False))
 
 
+def test_graph_loader_stream_equals_epochs():
+    """GraphLoader.stream (one collation pool prefetching across epochs) yields
+    the batches of consecutive per-epoch iterations, bitwise, shuffled epochs
+    included; closing it mid-epoch stops its threads."""
+    from hlhgat.hodge_dataset import PackedGraphs
+    from hlhgat.loader import GraphLoader
+    from hlhgat.synthetic import zinc_like_graph
+    gs = [zinc_like_graph(7100 + i, keig=15) for i in range(50)]
+    ds = PackedGraphs(gs)
+    ref = GraphLoader(ds, 12, shuffle=True, seed=3, workers=2, prefetch=3)
+    want = [b for _ in range(3) for b in ref]
+    got = list(GraphLoader(ds, 12, shuffle=True, seed=3, workers=2, prefetch=3).stream(3))
+    assert len(got) == len(want) == 3 * 4
+    for a, b in zip(got, want):
+        _same_batch(a, b)
+    it = GraphLoader(ds, 12, workers=2, prefetch=3).stream()
+    for _ in range(6):  # past an epoch boundary of the endless stream
+        next(it)
+    it.close()
+
+
 def test_native_mlgc_batch_equals_per_graph():
     """hlhgat_mlgc_batch (one call, host threads) gives per graph exactly the
     per-graph graclus(both directions, unit weights, perm) + mlgc_map."""
