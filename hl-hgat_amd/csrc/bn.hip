@@ -1967,9 +1967,10 @@ extern "C" int hlhgat_bn_sums_bwd(const float* x, int64_t ldx, const float* y, i
   // the layout of hlhgat_bn_bwd_train over (x, y, dy, dx)
   const bool vec = bn_vec_ok(C, {ldx, lddy, dx_layout ? lddx : 4, y ? ldy : 4},
                              {x, y, dy, dx_layout});
-  const BnLayout L = bn_layout(n, C, vec);
+  const BnLayout L = bn_layout(n, C, vec, bn_bwd_min_parts());
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_sums_bwd: C too large");
   StatsArgs s = stats_args(L, carve(workspace, n, C), x, ldx, n, n_valid, C);
+  s.flat_max = bn_bwd_flat_max();  // the plain backward's partitions and order
   s.y = y;
   s.ldy = ldy;
   s.dy = dy;
