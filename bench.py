@@ -81,7 +81,7 @@ def make_batches(n_batches, rank, device, quantum=512, caps=None):
     return [ds.collate(i, caps).to(device) for i in idxs], caps, real, ds.collate(idxs[0]), ds
 
 
-def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
+def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2, workers=4, stream=True):
     """The data loader beside the step (the reference feeds every step from a
     DataLoader with 4 workers and copies the batch in, main_zinc...:151-162,
     223-225).  Here: graphs/s of hlhgat.loader.GraphLoader (native collate +
@@ -117,11 +117,17 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
     # static buffers of a captured graph, two batches ahead) -> the replayed
     # step with no copy-in, launched from this thread alone
     from hlhgat.loader import StagedFeed
-    ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=4, prefetch=8, pin=True)
+    ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=workers, prefetch=2 * workers,
+                     pin=True)
     cs = torch.cuda.Stream(device=device)
     step.stage_slots = max(step.stage_slots, depth + 1)
 
-    feed = StagedFeed(ld.stream(), step, depth=depth, stream=cs)
+    def per_epoch():
+        while True:
+            for b in ld:
+                yield b
+
+    feed = StagedFeed(ld.stream() if stream else per_epoch(), step, depth=depth, stream=cs)
     it = iter(feed)
     host = {"wait_feed": 0.0, "step_call": 0.0}
     warm = 4  # the first steps capture the shape's third graph
@@ -145,8 +151,8 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2):
     ops_mod = __import__("hlhgat").ops
     ops_mod.check_device_errors()
     out["loader_fed"] = {"value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
-                         "ms_per_step": round(dt * 1e3, 3), "workers": 4, "pinned": True,
-                         "steps": steps, "stage_depth": depth,
+                         "ms_per_step": round(dt * 1e3, 3), "workers": workers, "pinned": True,
+                         "across_epochs": bool(stream), "steps": steps, "stage_depth": depth,
                          "host_ms_per_step": {k: round(v / steps * 1e3, 3) for k, v in host.items()},
                          "feeder_ms_per_batch": {k: round(feed.timing[k] / max(1, feed.timing["n"]) * 1e3, 3)
                                                  for k in ("source", "room", "stage")},
@@ -988,6 +994,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loader-workers", type=int, default=4,
+                    help="GraphLoader collation threads (the reference's num_workers=4)")
+    ap.add_argument("--loader-per-epoch", action="store_true",
+                    help="iterate the loader epoch by epoch instead of GraphLoader.stream")
     ap.add_argument("--loader-depth", type=int, default=2,
                     help="batches StagedFeed uploads ahead of the step (loader leg)")
     ap.add_argument("--no-loader", action="store_true",
@@ -1201,7 +1211,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_loader:
         log("[rank 0] loader leg")
         result["loader"] = loader_leg(dataset, step, caps, device, ms_step,
-                                      depth=args.loader_depth)
+                                      depth=args.loader_depth, workers=args.loader_workers,
+                                      stream=not args.loader_per_epoch)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
         result["cpu_baseline"] = cpu_baseline(raw0)
