@@ -130,7 +130,7 @@ for s in "$@"; do
            step abload2_${v}_$r 400 env $E python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --loader-depth 2
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']; print(sys.argv[2], r['ms_per_step'], L['loader_fed']['ms_per_step'], round(r['ms_per_step']/L['loader_fed']['ms_per_step'],3), L['loader_fed']['host_ms_per_step'], r['h2d'])" gpurun_out/${TAG}_abload2_${v}_$r.log $v >> gpurun_out/${TAG}_abload2.txt || true
          done; done ;;
-    abload3) for r in 1 2; do for v in s4 s2 s1 e4 e2; do
+    abload3) for r in 1 2; do for v in s4 e4 s2; do
            case $v in s4) A="--loader-workers 4";; s2) A="--loader-workers 2";; s1) A="--loader-workers 1";; e4) A="--loader-workers 4 --loader-per-epoch";; e2) A="--loader-workers 2 --loader-per-epoch";; esac
            step abload3_${v}_$r 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census $A
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'))" gpurun_out/${TAG}_abload3_${v}_$r.log $v >> gpurun_out/${TAG}_abload3.txt || true
