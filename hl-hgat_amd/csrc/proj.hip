@@ -341,105 +341,6 @@ __device__ __forceinline__ void bwd_data_lds_body(const BwdDataArgs& a, int bx, 
                       a.accumulate, vec_ok);
 }
 
-// Data gradient for 64 < N <= 128 (the NodeEdgeInt first Linear, whose packed
-// output is 2 dl wide), one workgroup per 64-row block covering every column
-// tile: the wave's 16 dC rows x 128 n stay in registers (read once instead of
-// once per column tile), the W tile (128 n x 64 columns, transposed and
-// swizzled as bwd_data_lds_body's, two 64-n halves) goes through ONE LDS
-// buffer -- the next tile waits in registers, two barriers per tile -- so the
-// kernel keeps the LDS footprint of the N <= 64 rows variant.  Per element
-// the MFMA sequence of bwd_data_lds_body: bitwise the same dA.
-template <int TN>
-__device__ __forceinline__ void bwd_data_rows2_body(const BwdDataArgs& a, int bx, float* lds) {
-  float (*wl)[TN * 16][KCP] = reinterpret_cast<float (*)[TN * 16][KCP]>(lds);  // [2 halves]
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int q = lane >> 4, i = lane & 15;
-  float* scratch = lds + 2 * TN * 16 * KCP + wave * 16 * (TN * 16 + 4);
-  const int64_t m_base = ((int64_t)bx * 4 + wave) * 16;
-  const int64_t row = m_base + i;
-  const bool gval = row < a.M;
-  const float* grow = a.G + (gval ? row : 0) * a.ldg;
-  float4 gc[2][4];
-  load_a_chunk(grow, gval, 0, a.N, q, gc[0]);
-  load_a_chunk(grow, gval, KC, a.N, q, gc[1]);
-  const int ntiles = a.tile_start[a.nb];
-  auto tile_of = [&](int t, int& b, int& c_base) {
-    b = 0;
-    while (b + 1 < a.nb && t >= a.tile_start[b + 1]) ++b;
-    c_base = (t - a.tile_start[b]) * (TN * 16);
-  };
-  auto load_w = [&](int t, float4 (&st)[2][TN]) {
-    int b, c_base;
-    tile_of(t, b, c_base);
-    const float* __restrict__ W = a.W[b];
-    const int64_t ldw = a.ldw[b];
-    const int kb = a.kb[b];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int u = 0; u < TN; ++u) {
-        const int idx = threadIdx.x + 256 * u;
-        const int nl = idx & 63, c4 = idx >> 6;
-        const int n = KC * h + nl, c = c_base + 4 * c4;
-        st[h][u] = (n < a.N && c < kb) ? *reinterpret_cast<const float4*>(W + (int64_t)n * ldw + c)
-                                       : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-  };
-  auto store_w = [&](const float4 (&st)[2][TN]) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int u = 0; u < TN; ++u) {
-        const int idx = threadIdx.x + 256 * u;
-        const int nl = idx & 63, c4 = idx >> 6;
-        const int r0 = 4 * c4;
-        wl[h][r0 + 0][4 * wswz(r0 + 0, nl >> 2) + (nl & 3)] = st[h][u].x;
-        wl[h][r0 + 1][4 * wswz(r0 + 1, nl >> 2) + (nl & 3)] = st[h][u].y;
-        wl[h][r0 + 2][4 * wswz(r0 + 2, nl >> 2) + (nl & 3)] = st[h][u].z;
-        wl[h][r0 + 3][4 * wswz(r0 + 3, nl >> 2) + (nl & 3)] = st[h][u].w;
-      }
-  };
-  float4 wst[2][TN];
-  load_w(0, wst);
-  store_w(wst);
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const bool has_next = t + 1 < ntiles;
-    if (has_next) load_w(t + 1, wst);
-    floatx4 acc[TN];
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn) acc[tn] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float4 bf[TN];
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn)
-          bf[tn] = *reinterpret_cast<const float4*>(&wl[h][tn * 16 + i][4 * wswz(i, 4 * s + q)]);
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          acc[tn] = mfma16(gc[h][s].x, bf[tn].x, acc[tn]);
-          acc[tn] = mfma16(gc[h][s].y, bf[tn].y, acc[tn]);
-          acc[tn] = mfma16(gc[h][s].z, bf[tn].z, acc[tn]);
-          acc[tn] = mfma16(gc[h][s].w, bf[tn].w, acc[tn]);
-        }
-      }
-    int b, c_base;
-    tile_of(t, b, c_base);
-    const int ncols = a.kb[b] - c_base < TN * 16 ? a.kb[b] - c_base : TN * 16;
-    const bool vec_ok = (a.ldo[b] % 4) == 0 && (reinterpret_cast<uintptr_t>(a.O[b]) & 15) == 0;
-    store_tile_rows<TN>(acc, scratch, m_base, a.M, a.O[b] + c_base, a.ldo[b], ncols, nullptr,
-                        a.accumulate, vec_ok);
-    if (has_next) {
-      __syncthreads();  // every wave is done with this tile's W
-      store_w(wst);
-      __syncthreads();
-    }
-  }
-}
-
 // Data gradient, one workgroup per 64-row block covering EVERY column tile of
 // every block (N <= 64: the workgroup's whole dC chunk stays in registers), so
 // dC is read once per row block instead of once per column tile; the W tiles
@@ -938,7 +839,7 @@ struct BwdFusedArgs {
   ReduceArgs red;
 };
 
-template <int TND, bool ROWS, int NCH = 1>
+template <int TND, bool ROWS>
 __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
   const int L = (int)blk.x;
   if (L >= a.n_wpad + a.n_d) {
@@ -947,10 +848,7 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
     return;
   }
   if (ROWS && L >= a.n_wpad) {  // one workgroup per row block, every column tile
-    if (NCH == 2)
-      bwd_data_rows2_body<TND>(a.d, L - a.n_wpad, lds);
-    else
-      bwd_data_rows_body<TND>(a.d, L - a.n_wpad, lds);
+    bwd_data_rows_body<TND>(a.d, L - a.n_wpad, lds);
     return;
   }
   if (L >= a.n_wpad) {
@@ -981,24 +879,18 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
                     reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
-template <int TND, bool ROWS, int NCH = 1>
+template <int TND, bool ROWS>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
   // ROWS: two W buffers + the epilogue scratch (bwd_data_rows_body)
   constexpr int kW = 2 * WR * 64 * 2;
   constexpr int kD = ROWS ? 2 * TND * 16 * KCP + 4 * 16 * (TND * 16 + 4) : 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
-  proj_bwd_fused_body<TND, ROWS, NCH>(a, blk_hw(), lds);
+  proj_bwd_fused_body<TND, ROWS>(a, blk_hw(), lds);
 }
 
-// Row-block data-gradient workgroups in the fused Linear backward
-// (hlhgat_set_proj_bwd_rows): 0 = one per (row block, column tile), 1 = one per
-// row block for N <= 64 (bwd_data_rows_body), 2 = also for 64 < N <= 128
-// (bwd_data_rows2_body).  Initial mode: HLHGAT_PROJ_BWD_ROWS, else 1.
-int& proj_bwd_rows_mode() {
-  static int v = [] {
-    const char* e = std::getenv("HLHGAT_PROJ_BWD_ROWS");
-    return e ? std::atoi(e) : 1;
-  }();
+// A/B hook (hlhgat_set_proj_bwd_rows): row-block data-gradient workgroups
+bool& proj_bwd_rows_flag() {
+  static bool v = true;
   return v;
 }
 
@@ -1815,9 +1707,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   bool vec_d = aligned16(dC) && lddc % 4 == 0;
   for (int b = 0; b < nb_d; ++b)
     vec_d = vec_d && aligned16(W[b]) && ldw[b] % 4 == 0 && kb_d[b] % 4 == 0;
-  const int rmode = proj_bwd_rows_mode();
-  const bool rows2 = rmode >= 2 && tnd == 4 && N > KC && N <= 2 * KC && vec_d && want_d;
-  const bool rows = (rmode >= 1 && tnd == 4 && N <= KC && vec_d) || rows2;
+  const bool rows = proj_bwd_rows_flag() && tnd == 4 && N <= KC && vec_d;
   f.n_d = rows ? f.d_gx : f.d_gx * d.tile_start[nb_d];
   f.d_xcd = data_xcd_map();
   if (prev) {
@@ -1843,9 +1733,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   bytes += 4.0 * (double)p.splits * p.part_stride;
   ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-  if (rows2)
-    launch(k_proj_bwd_fused<4, true, 2>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
-  else if (rows)
+  if (rows)
     launch(k_proj_bwd_fused<4, true>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else if (tnd == 1)
     launch(k_proj_bwd_fused<1, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
@@ -1910,7 +1798,6 @@ extern "C" int hlhgat_set_gemm_big(int mode, int64_t min_m) {
 }
 
 extern "C" int hlhgat_set_proj_bwd_rows(int on) {
-  HLH_CHECK_ARG(on >= 0 && on <= 2, "set_proj_bwd_rows: mode must be 0, 1 or 2");
-  proj_bwd_rows_mode() = on;
+  proj_bwd_rows_flag() = on != 0;
   return HLHGAT_OK;
 }

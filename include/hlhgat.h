@@ -622,10 +622,9 @@ int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
  * shape.  Env HLHGAT_GEMM_BIG sets the initial mode.  min_m <= 0 keeps the
  * current threshold. */
 int hlhgat_set_gemm_big(int mode, int64_t min_m);
-/* Data-gradient workgroups of the fused Linear backward (hlhgat_proj_bwd /
- * _defer): 0 = one per (row block, 64-column tile); 1 (default) = one per row
- * block covering every column tile when N <= 64 (dC read once); 2 = also when
- * 64 < N <= 128.  Bitwise the same results in every mode (tests). */
+/* 0: the fused Linear backward (hlhgat_proj_bwd / _defer) uses one
+ * data-gradient workgroup per (row block, 64-column tile) instead of one per
+ * row block covering every column tile (N <= 64); bitwise the same (tests). */
 int hlhgat_set_proj_bwd_rows(int on);
 /* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
 int hlhgat_set_proj_bn_fused(int on);

@@ -135,11 +135,6 @@ for s in "$@"; do
            step abload3_${v}_$r 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census $A
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'))" gpurun_out/${TAG}_abload3_${v}_$r.log $v >> gpurun_out/${TAG}_abload3.txt || true
          done; done ;;
-    abrows) for r in 1 2; do for v in 1 2; do
-           HLHGAT_PROJ_BWD_ROWS=$v step abrows_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abrows_${v}_$r.log | sed "s/^/rows=$v run $r /" >> gpurun_out/${TAG}_abrows.txt || true
-         done; done
-         step rowstest 300 $PT tests/test_gpu_parity.py -m gpu -q -k "row_blocks_bitwise or fused_backward_zinc" ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
