@@ -81,7 +81,8 @@ def make_batches(n_batches, rank, device, quantum=512, caps=None):
     return [ds.collate(i, caps).to(device) for i in idxs], caps, real, ds.collate(idxs[0]), ds
 
 
-def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2, workers=4, stream=True):
+def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2, workers=4, stream=True,
+               priority=0, switch_ms=None, slots=None, thread=True):
     """The data loader beside the step (the reference feeds every step from a
     DataLoader with 4 workers and copies the batch in, main_zinc...:151-162,
     223-225).  Here: graphs/s of hlhgat.loader.GraphLoader (native collate +
@@ -119,24 +120,32 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2, workers=4, st
     from hlhgat.loader import StagedFeed
     ld = GraphLoader(ds, GRAPHS_PER_GPU, caps=caps, workers=workers, prefetch=2 * workers,
                      pin=True)
-    cs = torch.cuda.Stream(device=device)
-    step.stage_slots = max(step.stage_slots, depth + 1)
+    cs = torch.cuda.Stream(device=device, priority=priority)
+    # one captured graph more than depth + 1: the slot a batch is staged into
+    # was released a step earlier, so the feeder rarely waits for it
+    slots = slots or depth + 2
+    step.stage_slots = max(step.stage_slots, slots)
 
     def per_epoch():
         while True:
             for b in ld:
                 yield b
 
-    feed = StagedFeed(ld.stream() if stream else per_epoch(), step, depth=depth, stream=cs)
+    feed = StagedFeed(ld.stream() if stream else per_epoch(), step, depth=depth, stream=cs,
+                      thread=thread)
     it = iter(feed)
+    old_switch = sys.getswitchinterval()
+    if switch_ms:
+        sys.setswitchinterval(switch_ms * 1e-3)
     host = {"wait_feed": 0.0, "step_call": 0.0}
-    warm = 4  # the first steps capture the shape's third graph
+    warm = step.stage_slots + 1  # the first steps capture the shape's graphs (one per slot)
     for i in range(steps + warm):
         if i == warm:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             host = {k: 0.0 for k in host}
             feed.timing.update(source=0.0, room=0.0, stage=0.0, n=0)
+            step.stage_timing.update(dict.fromkeys(step.stage_timing, 0.0))
         ta = time.perf_counter()
         st = next(it)
         tb = time.perf_counter()
@@ -147,15 +156,21 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2, workers=4, st
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     it.close()  # stops the feeder thread and the loader's collation threads
+    sys.setswitchinterval(old_switch)
     torch.cuda.synchronize()
     ops_mod = __import__("hlhgat").ops
     ops_mod.check_device_errors()
     out["loader_fed"] = {"value": round(GRAPHS_PER_GPU / dt, 1), "unit": "graphs/s",
                          "ms_per_step": round(dt * 1e3, 3), "workers": workers, "pinned": True,
                          "across_epochs": bool(stream), "steps": steps, "stage_depth": depth,
+                         "copy_stream_priority": priority, "stage_slots": step.stage_slots,
+                         "feeder_thread": bool(thread),
+                         "gil_switch_ms": switch_ms if switch_ms else round(old_switch * 1e3, 3),
                          "host_ms_per_step": {k: round(v / steps * 1e3, 3) for k, v in host.items()},
                          "feeder_ms_per_batch": {k: round(feed.timing[k] / max(1, feed.timing["n"]) * 1e3, 3)
                                                  for k in ("source", "room", "stage")},
+                         "stage_ms_per_batch": {k: round(v / max(1, step.stage_timing["n"]) * 1e3, 3)
+                                                for k, v in step.stage_timing.items() if k != "n"},
                          "what": "training steps fed by GraphLoader end to end: native collate "
                                  "on 4 threads, hlhgat.loader.StagedFeed's thread uploading "
                                  "(TrainStep.stage: one H2D copy per batch on a copy stream, "
@@ -1000,6 +1015,14 @@ def main():
                     help="iterate the loader epoch by epoch instead of GraphLoader.stream")
     ap.add_argument("--loader-depth", type=int, default=2,
                     help="batches StagedFeed uploads ahead of the step (loader leg)")
+    ap.add_argument("--loader-slots", type=int, default=None,
+                    help="captured graphs per shape the loader leg stages into (default depth + 2)")
+    ap.add_argument("--loader-inline", action="store_true",
+                    help="stage the loader leg's batches from the training thread (no feeder thread)")
+    ap.add_argument("--loader-priority", type=int, default=0,
+                    help="priority of the loader leg's copy stream (torch: -1 = high)")
+    ap.add_argument("--loader-switch-ms", type=float, default=None,
+                    help="Python GIL switch interval during the loader-fed loop (ms)")
     ap.add_argument("--no-loader", action="store_true",
                     help="skip the data-loader leg (native collate rates, loader-fed steps)")
     ap.add_argument("--no-parity-check", action="store_true",
@@ -1212,7 +1235,11 @@ def main():
         log("[rank 0] loader leg")
         result["loader"] = loader_leg(dataset, step, caps, device, ms_step,
                                       depth=args.loader_depth, workers=args.loader_workers,
-                                      stream=not args.loader_per_epoch)
+                                      stream=not args.loader_per_epoch,
+                                      priority=args.loader_priority,
+                                      switch_ms=args.loader_switch_ms,
+                                      slots=args.loader_slots,
+                                      thread=not args.loader_inline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
         result["cpu_baseline"] = cpu_baseline(raw0)

@@ -136,22 +136,27 @@ class StagedFeed:
     ``depth`` batches ahead of the step; iterating yields the staged handles
     in order, each to be passed to ``step(...)`` before the next is taken.
 
-        feed = StagedFeed(loader, step, depth=2)   # step = TrainStep(..., stage_slots=3)
+        feed = StagedFeed(loader, step, depth=2)   # step = TrainStep(..., stage_slots=4)
         for st in feed:
             loss = step(st)
 
     The replay call releases the GIL, so the feeder's Python work and the
     copies' enqueueing overlap the launch thread's.  ``step.stage_slots``
-    should be >= depth + 1 (depth staged batches waiting + one replaying);
+    must be >= depth + 1 (depth staged batches waiting + one replaying);
     with fewer, a staged batch goes to fresh device tensors and is copied in
-    at its step (correct, one device copy more).  The reference loop this
+    at its step (correct, one device copy more).  depth + 2 is better: the
+    feeder waits on the host for the slot's previous replay to finish
+    (train.STAGE_WAIT), and one slot more makes that replay an older one.
+    ``thread=False`` stages from the consumer's own thread instead (no
+    feeder thread; it then also does those waits).  The reference loop this
     serves: main_zinc_HL_HGCNN_dense_int3_pyr.py:151-162 (for data in
     loader: data.to(device); step), with DataLoader(num_workers=4) (:223-225).
     """
 
     _END = object()
 
-    def __init__(self, batches: Iterable, step, depth: int = 2, stream=None):
+    def __init__(self, batches: Iterable, step, depth: int = 2, stream=None,
+                 thread: bool = True):
         import torch
         if depth < 1:
             raise ValueError("StagedFeed: depth must be >= 1")
@@ -163,6 +168,7 @@ class StagedFeed:
         self._room = threading.Semaphore(self.depth)
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
+        self.use_thread = bool(thread)
         self.timing = {"source": 0.0, "room": 0.0, "stage": 0.0, "n": 0}
 
     def _run(self):
@@ -197,7 +203,39 @@ class StagedFeed:
             if close is not None:
                 close()
 
+    def _inline(self):
+        # thread=False: the consumer's own thread stages `depth` batches ahead
+        # (between its step calls) -- no second Python thread contending for
+        # the GIL with the training loop
+        import time
+        clock = time.perf_counter
+        it = iter(self.batches)
+        ahead = deque()
+        try:
+            while True:
+                while len(ahead) < self.depth:
+                    t0 = clock()
+                    b = next(it, self._END)
+                    if b is self._END:
+                        break
+                    t1 = clock()
+                    ahead.append(self.step.stage(b, self.stream))
+                    t2 = clock()
+                    self.timing["source"] += t1 - t0
+                    self.timing["stage"] += t2 - t1
+                    self.timing["n"] += 1
+                if not ahead:
+                    return
+                yield ahead.popleft()
+        finally:
+            close = getattr(it, "close", None)
+            if close is not None:
+                close()
+
     def __iter__(self):
+        if not self.use_thread:
+            yield from self._inline()
+            return
         self._stop.clear()
         self._thread = threading.Thread(target=self._run, name="hlhgat-stage", daemon=True)
         self._thread.start()

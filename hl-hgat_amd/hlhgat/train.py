@@ -26,7 +26,9 @@ from __future__ import annotations
 
 import contextlib
 import gc
+import os
 import threading
+import time
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
@@ -205,6 +207,15 @@ class _Captured:
 
 STAGE_SLOTS = 2  # default captured graphs per batch shape TrainStep.stage fills in turn
 STAGE_RING = 8   # staged batches that may be outstanding (uploaded, not yet stepped)
+# how an upload into a captured graph's buffers waits for that graph's previous
+# replay to release them: "host" (the staging thread waits for the release
+# event, then enqueues the copy with no cross-stream dependency) or "device"
+# (the copy stream waits on the event).  "host" by default: with the
+# device-side wait the runtime blocks the enqueueing thread inside the copy
+# until the event has completed anyway (tools/probes/h2d_probe.py) and the
+# loader-fed loop measured 0.92 of device-resident steps; with the host-side
+# wait 0.96-0.98 (same-box A/B)
+STAGE_WAIT = os.environ.get("HLHGAT_STAGE_WAIT", "host")
 
 
 class Staged:
@@ -265,6 +276,7 @@ class TrainStep:
         self.stage_slots = int(stage_slots)
         self._stage_lock = threading.RLock()
         self._outstanding = 0
+        self.stage_timing = dict.fromkeys(("lock", "wait", "copy", "record", "total", "n"), 0.0)
         params = [p for p in model.parameters() if p.requires_grad]
         if not params:
             raise ValueError("TrainStep: model has no trainable parameters")
@@ -521,9 +533,18 @@ class TrainStep:
         # feeder's stage() into every step call).  A capture may then run
         # beside an upload: thread-local capture mode allows that, the copy is
         # on another stream and into a slot no capture touches.
+        clock = time.perf_counter
+        t0 = clock()
         with self._stage_lock:
+            t1 = clock()
             ev, slot, free = self._stage_plan(key)
-        return self._stage_copy(batch, stream, key, main, ev, slot, free)
+        st = self._stage_copy(batch, stream, key, main, ev, slot, free)
+        # host time per stage() part (diagnostics: bench.py's loader leg)
+        tm = self.stage_timing
+        tm["lock"] += t1 - t0
+        tm["total"] += clock() - t0
+        tm["n"] += 1
+        return st
 
     def _stage_plan(self, key):
         # a ring of events (kept for the process, see _EVENTS_KEEP): at most
@@ -570,10 +591,16 @@ class TrainStep:
                 for _, v in _tensor_items(b):
                     v.record_stream(main)
             return Staged(dev, ev, None, key)
+        clock = time.perf_counter
+        t0 = clock()
         if free is not None:
-            stream.wait_event(free)
+            if STAGE_WAIT == "host":
+                free.synchronize()
+            else:
+                stream.wait_event(free)
         else:  # replayed before staging began (no release event): after all of main
             stream.wait_stream(main)
+        t1 = clock()
         with torch.cuda.stream(stream):
             for b, sb in zip(_parts(batch), _parts(slot.batch)):
                 ha, da = getattr(b, "_arena", None), getattr(sb, "_arena", None)
@@ -583,7 +610,12 @@ class TrainStep:
                     continue
                 for name, v in _tensor_items(b):
                     getattr(sb, name).copy_(v, non_blocking=True)
+            t2 = clock()
             ev.record(stream)
+        tm = self.stage_timing
+        tm["wait"] += t1 - t0
+        tm["copy"] += t2 - t1
+        tm["record"] += clock() - t2
         return Staged(None, ev, slot, key)
 
     def _upload(self, b):

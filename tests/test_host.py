@@ -648,6 +648,47 @@ def test_graph_loader_stream_equals_epochs():
     it.close()
 
 
+@pytest.mark.parametrize("thread", [True, False])
+def test_staged_feed_order_and_depth(thread):
+    """StagedFeed's host logic (no device: a stand-in step records stage()
+    calls): every batch is staged once, in order, handed over in order, and
+    never more than `depth` staged batches wait beyond the one being stepped;
+    a source error reaches the consumer."""
+    import threading
+    from hlhgat.loader import StagedFeed
+
+    class FakeStep:
+        def __init__(self):
+            self.staged, self.stepped = [], []
+            self.lock = threading.Lock()
+
+        def stage(self, b, stream):
+            with self.lock:
+                self.staged.append(b)
+                assert len(self.staged) - len(self.stepped) <= 3, "staged too far ahead"
+            return ("st", b)
+
+        def __call__(self, st):
+            with self.lock:
+                self.stepped.append(st[1])
+
+    step = FakeStep()
+    feed = StagedFeed(iter(range(17)), step, depth=2, stream=object(), thread=thread)
+    for st in feed:
+        assert st == ("st", len(step.stepped))
+        step(st)
+    assert step.staged == step.stepped == list(range(17))
+
+    def bad():
+        yield 0
+        raise ValueError("source failed")
+
+    feed = StagedFeed(bad(), FakeStep(), depth=2, stream=object(), thread=thread)
+    with pytest.raises(ValueError, match="source failed"):
+        for st in feed:
+            pass
+
+
 def test_native_mlgc_batch_equals_per_graph():
     """hlhgat_mlgc_batch (one call, host threads) gives per graph exactly the
     per-graph graclus(both directions, unit weights, perm) + mlgc_map."""

@@ -810,12 +810,18 @@ def test_staged_three_ahead_bitwise(cuda):
 
 
 @pytest.mark.gpu
-def test_staged_feed_thread_bitwise(cuda):
-    """hlhgat.loader.StagedFeed: a feeder thread stages GraphLoader batches
-    (native collate on worker threads, pinned arenas) two ahead while this
-    thread replays, and a third graph of the shape is captured meanwhile
-    (the collation and feeder threads run beside a thread-local capture);
-    losses and parameters bitwise those of step(device batch) in order."""
+@pytest.mark.parametrize("wait,thread,slots", [("host", True, 4), ("device", True, 3),
+                                               ("host", False, 4)])
+def test_staged_feed_thread_bitwise(cuda, monkeypatch, wait, thread, slots):
+    """hlhgat.loader.StagedFeed: a feeder thread (or, thread=False, this
+    thread between its steps) stages GraphLoader batches (native collate on
+    worker threads, pinned arenas) two ahead while this thread replays, and
+    the shape's later graphs are captured meanwhile (the collation and feeder
+    threads run beside a thread-local capture); the slot's release waited for
+    on the host or by the copy stream (train.STAGE_WAIT); losses and
+    parameters bitwise those of step(device batch) in order."""
+    import hlhgat.train as train_mod
+    monkeypatch.setattr(train_mod, "STAGE_WAIT", wait)
     import numpy as np
     import hlhgat
     from hlhgat.hodge_dataset import PackedGraphs
@@ -832,14 +838,14 @@ def test_staged_feed_thread_bitwise(cuda):
     m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
     crit = torch.nn.L1Loss()
     step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
-                     weight_decay=1e-3, graphs=True, stage_slots=3)
+                     weight_decay=1e-3, graphs=True, stage_slots=slots)
     losses = []
-    for st in StagedFeed(ld, step, depth=2):
+    for st in StagedFeed(ld, step, depth=2, thread=thread):
         losses.append(float(step(st)))
     torch.cuda.synchronize()
     _check_errors()
     assert len(losses) == len(idxs) and step._outstanding == 0
-    assert step.stats["captures"] == 3, step.stats
+    assert step.stats["captures"] == slots, step.stats
     sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     assert losses == l_ref, (losses, l_ref)
     for key in sd_ref:

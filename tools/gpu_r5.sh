@@ -135,6 +135,36 @@ for s in "$@"; do
            step abload3_${v}_$r 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census $A
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'))" gpurun_out/${TAG}_abload3_${v}_$r.log $v >> gpurun_out/${TAG}_abload3.txt || true
          done; done ;;
+    abload4) for r in 1 2; do for v in base hi sw hisw; do
+           case $v in base) A="";; hi) A="--loader-priority -1";; sw) A="--loader-switch-ms 0.5";; hisw) A="--loader-priority -1 --loader-switch-ms 0.5";; esac
+           step abload4_${v}_$r 400 python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'))" gpurun_out/${TAG}_abload4_${v}_$r.log $v >> gpurun_out/${TAG}_abload4.txt || true
+         done; done ;;
+    abload5) for r in 1 2; do for v in base q8 q16 sw; do
+           case $v in base) E=""; A="";; q8) E="GPU_MAX_HW_QUEUES=8"; A="";; q16) E="GPU_MAX_HW_QUEUES=16"; A="";; sw) E=""; A="--loader-switch-ms 0.5";; esac
+           step abload5_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload5_${v}_$r.log $v >> gpurun_out/${TAG}_abload5.txt || true
+         done; done ;;
+    abload6) for r in 1 2; do for v in base sl4 sl5 d3sl5; do
+           case $v in base) A="";; sl4) A="--loader-slots 4";; sl5) A="--loader-slots 5";; d3sl5) A="--loader-depth 3 --loader-slots 5";; esac
+           step abload6_${v}_$r 400 python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload6_${v}_$r.log $v >> gpurun_out/${TAG}_abload6.txt || true
+         done; done ;;
+    abload7) for r in 1 2; do for v in base in1 in2 in2sw; do
+           case $v in base) A="";; in1) A="--loader-inline --loader-depth 1";; in2) A="--loader-inline";; in2sw) A="--loader-inline --loader-switch-ms 0.5";; esac
+           step abload7_${v}_$r 400 python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload7_${v}_$r.log $v >> gpurun_out/${TAG}_abload7.txt || true
+         done; done ;;
+    abload8) for r in 1 2; do for v in base raw rawin in2; do
+           case $v in base) E=""; A="";; raw) E="HLHGAT_STAGE_COPY=raw"; A="";; rawin) E="HLHGAT_STAGE_COPY=raw"; A="--loader-inline";; in2) E=""; A="--loader-inline";; esac
+           step abload8_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload8_${v}_$r.log $v >> gpurun_out/${TAG}_abload8.txt || true
+         done; done ;;
+    abload9) for r in 1 2; do for v in base host hostsl4 devsl4; do
+           case $v in base) E=""; A="";; host) E="HLHGAT_STAGE_WAIT=host"; A="";; hostsl4) E="HLHGAT_STAGE_WAIT=host"; A="--loader-slots 4";; devsl4) E=""; A="--loader-slots 4";; esac
+           step abload9_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
+           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload9_${v}_$r.log $v >> gpurun_out/${TAG}_abload9.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
