@@ -712,6 +712,7 @@ def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
     cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     for name, c in HEADS.items():
         kind, G = c["kind"], c["graphs"]
+        handovers0 = ops.bn_giveups()["count"]
         t0 = time.perf_counter()
         pool = _head_pool(kind, 2 * G)
         rng = np.random.RandomState(7)
@@ -803,6 +804,8 @@ def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
         if kind == "cifar":
             r["with_per_sample_work"] = _guarded("cifar pipeline", cifar_pipeline_leg,
                                                  device, c, G)
+        # one-launch BatchNorm workgroups that handed over in this head's legs
+        r["bn_handovers"] = ops.bn_giveups()["count"] - handovers0
         out[name] = r
         log(f"[heads] {name}: {r['value']} graphs/s replayed, {r['eager_value']} eager, "
             f"padding {overhead:.1%} (CPU oracle {r['cpu_baseline']['value']})")
@@ -1230,9 +1233,12 @@ def main():
         result["h2d"] = h
     if rank == 0 and world == 1:
         log("[rank 0] eval leg")
+        h0 = ops.bn_giveups()["count"]
         result["eval"] = _guarded("eval", eval_leg, model, batches)
+        result["eval"]["bn_handovers"] = ops.bn_giveups()["count"] - h0
     if rank == 0 and world == 1 and not args.no_loader:
         log("[rank 0] loader leg")
+        h0 = ops.bn_giveups()["count"]
         result["loader"] = loader_leg(dataset, step, caps, device, ms_step,
                                       depth=args.loader_depth, workers=args.loader_workers,
                                       stream=not args.loader_per_epoch,
@@ -1240,6 +1246,7 @@ def main():
                                       switch_ms=args.loader_switch_ms,
                                       slots=args.loader_slots,
                                       thread=not args.loader_inline)
+        result["loader"]["bn_handovers"] = ops.bn_giveups()["count"] - h0
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] timing the CPU oracle baseline")
         result["cpu_baseline"] = cpu_baseline(raw0)
