@@ -165,6 +165,19 @@ for s in "$@"; do
            step abload9_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload9_${v}_$r.log $v >> gpurun_out/${TAG}_abload9.txt || true
          done; done ;;
+    abskipw) for r in 1 2; do for v in 0 1; do
+           HLHGAT_DEBUG_SKIP_WEIGHT=$v step abskipw_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abskipw_${v}_$r.log | sed "s/^/skip_weight=$v run $r /" >> gpurun_out/${TAG}_abskipw.txt || true
+         done; done ;;
+    wstest) step wstest 400 $PT tests/test_train_step.py -m gpu -v -k "weight_stream or deferred or staged_feed" ;;
+    abws2) for r in 1 2 3; do for v in 0 1; do
+           HLHGAT_WEIGHT_STREAM=$v step abws2_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abws2_${v}_$r.log | sed "s/^/weight_stream=$v run $r /" >> gpurun_out/${TAG}_abws2.txt || true
+         done; done ;;
+    abws5) for r in 1 2; do for v in 0 1; do
+           HLHGAT_WEIGHT_STREAM=$v step abws5_${v}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abws5_${v}_$r.log | head -1 | sed "s/^/cfg5 weight_stream=$v run $r /" >> gpurun_out/${TAG}_abws5.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
