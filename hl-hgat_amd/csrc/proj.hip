@@ -1786,21 +1786,15 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     hipEvent_t ev = next_fork_event();
     HLH_CHECK_ARG(hipEventRecord(ev, s) == hipSuccess, "proj_bwd: hipEventRecord");
     HLH_CHECK_ARG(hipStreamWaitEvent(ws, ev, 0) == hipSuccess, "proj_bwd: hipStreamWaitEvent");
-    double fl_w = 0, by_w = 4.0 * (double)M * N + 4.0 * (double)p.splits * p.part_stride;
-    for (int b = 0; b < nb_w; ++b) {
-      fl_w += 2.0 * (double)M * N * kb_w[b];
-      by_w += 4.0 * (double)M * kb_w[b];
-    }
-    {
-      ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes - by_w + 4.0 * (double)M * N, flops - fl_w);
+    if (fd.n_d > 0) {
+      // (profiling stamps the data launch only; its figures are the whole
+      // backward's, as for the one launch; weight-only calls go unstamped)
+      ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
       fused_launch(fd, s, &prof);
       HLH_CHECK_LAUNCH();
     }
-    {
-      ProfScope prof(HLHGAT_PROF_PROJ_BWD, ws, by_w, fl_w);
-      fused_launch(fw, ws, &prof);
-      HLH_CHECK_LAUNCH();
-    }
+    fused_launch(fw, ws, nullptr);
+    HLH_CHECK_LAUNCH();
     if (on_wstream) *on_wstream = 1;
     s = ws;  // the split reduction belongs to the weight stream
   } else {
