@@ -178,6 +178,10 @@ for s in "$@"; do
            HLHGAT_WEIGHT_STREAM=$v step abws5_${v}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abws5_${v}_$r.log | head -1 | sed "s/^/cfg5 weight_stream=$v run $r /" >> gpurun_out/${TAG}_abws5.txt || true
          done; done ;;
+    abopsf) for r in 1 2; do for w in cfg5 cfg3; do for o in x f; do
+           HLHGAT_GEMM_BIG=-1 HLHGAT_GEMM_BIG_OPS=$o step abopsf_${w}_${o}_$r 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abopsf_${w}_${o}_$r.log | head -1 | sed "s/^/$w ops=$o run $r /" >> gpurun_out/${TAG}_abopsf.txt || true
+         done; done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
