@@ -182,6 +182,10 @@ for s in "$@"; do
            HLHGAT_GEMM_BIG=-1 HLHGAT_GEMM_BIG_OPS=$o step abopsf_${w}_${o}_$r 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abopsf_${w}_${o}_$r.log | head -1 | sed "s/^/$w ops=$o run $r /" >> gpurun_out/${TAG}_abopsf.txt || true
          done; done; done ;;
+    abwsf) for r in 1 2; do for v in 1:0 0:0 0:1; do f=${v%%:*}; w=${v##*:}
+           HLHGAT_STREAM_FORK=$f HLHGAT_WEIGHT_STREAM=$w step abwsf_${f}_${w}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abwsf_${f}_${w}_$r.log | sed "s/^/fork=$f weight_stream=$w run $r /" >> gpurun_out/${TAG}_abwsf.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
