@@ -312,9 +312,13 @@ void set_weight_stream(bool on) { weight_stream_flag() = on; }
 c10::hip::HIPStreamMasqueradingAsCUDA weight_stream_of(int dev) {
   static auto* streams = new std::unordered_map<int, c10::hip::HIPStreamMasqueradingAsCUDA>();
   auto it = streams->find(dev);
-  if (it == streams->end())
+  if (it == streams->end()) {
+    // HLHGAT_WEIGHT_STREAM_HI=1: a high-priority pool stream (A/B)
+    const char* e = std::getenv("HLHGAT_WEIGHT_STREAM_HI");
+    const bool hi = e && e[0] == '1';
     it = streams->emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
-                                   false, (c10::DeviceIndex)dev)).first;
+                                   hi, (c10::DeviceIndex)dev)).first;
+  }
   return it->second;
 }
 

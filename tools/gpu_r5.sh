@@ -186,6 +186,10 @@ for s in "$@"; do
            HLHGAT_STREAM_FORK=$f HLHGAT_WEIGHT_STREAM=$w step abwsf_${f}_${w}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abwsf_${f}_${w}_$r.log | sed "s/^/fork=$f weight_stream=$w run $r /" >> gpurun_out/${TAG}_abwsf.txt || true
          done; done ;;
+    abwshi) for r in 1 2; do for v in 0:0 1:0 1:1; do w=${v%%:*}; h=${v##*:}
+           HLHGAT_WEIGHT_STREAM=$w HLHGAT_WEIGHT_STREAM_HI=$h step abwshi_${w}_${h}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abwshi_${w}_${h}_$r.log | sed "s/^/weight_stream=$w high_prio=$h run $r /" >> gpurun_out/${TAG}_abwshi.txt || true
+         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
