@@ -1590,41 +1590,19 @@ int proj_bwd_big(bool big_w, bool big_d, int64_t M, int64_t N, const float* dC, 
   return run_reduce(r, s);
 }
 
-// events of the weight-stream mode (recorded and waited at once; a ring)
-hipEvent_t next_fork_event() {
-  static thread_local std::vector<hipEvent_t> pool;
-  static thread_local size_t k = 0;
-  if (pool.empty()) {
-    pool.resize(64);
-    for (auto& e : pool) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-  }
-  return pool[k++ % pool.size()];
-}
-
 int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w, const float* const* A, const int64_t* lda,
                   const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
                   int nb_d, const float* const* W, const int64_t* ldw, const int64_t* kb_d,
                   float* const* dA, const int64_t* ldda, int accumulate_d, float* workspace,
                   int64_t workspace_floats, void* stream,
                   const hlhgat_reduce_desc_t* merge = nullptr,
-                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr,
-                  void* wstream = nullptr, int* on_wstream = nullptr) {
+                  hlhgat_reduce_desc_t* defer_out = nullptr, int* deferred = nullptr) {
   if (deferred) *deferred = 0;
-  if (on_wstream) *on_wstream = 0;
   const ReduceArgs* prev = nullptr;
   if (merge) {
     HLH_CHECK_ARG(merge->words[0] == kDescMagic, "proj_bwd: merge is not a reduce descriptor");
     prev = reinterpret_cast<const ReduceArgs*>(&merge->words[1]);
   }
-  // weight-stream mode: `merge` was deferred on wstream; a call that cannot
-  // split runs it there first (after that stream's earlier work) and then
-  // proceeds on `stream` alone
-  auto settle_prev_on_w = [&]() -> int {
-    if (!wstream || !prev) return HLHGAT_OK;
-    const int rc = run_reduce(*prev, as_stream(wstream));
-    prev = nullptr;
-    return rc;
-  };
   HLH_CHECK_ARG(nb_w >= 0 && nb_w <= MAXB && nb_d >= 0 && nb_d <= MAXB,
                 "proj_bwd: nb_w=%d nb_d=%d", nb_w, nb_d);
   HLH_CHECK_ARG(M >= 0 && N > 0 && lddc >= N && dC, "proj_bwd: bad dC");
@@ -1641,7 +1619,7 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   for (int b = 0; b < nb_d && fuse; ++b) fuse = vec_ok(W[b], ldw[b], kb_d[b]);
   if (prev && !fuse) {  // run the merged reduction on its own first
-    const int rc = wstream ? settle_prev_on_w() : run_reduce(*prev, as_stream(stream));
+    const int rc = run_reduce(*prev, as_stream(stream));
     if (rc != HLHGAT_OK) return rc;
     prev = nullptr;
   }
@@ -1662,10 +1640,6 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   log_call("bwd_d", M, N, nb_d, kb_d, nullptr);
   const bool big_w = want_w && big_weight_ok(M, N, ktot_w);
   const bool big_d = want_d && big_data_ok(M, N, ktot_d);
-  if ((big_w || big_d) && wstream) {
-    const int rc = settle_prev_on_w();
-    if (rc != HLHGAT_OK) return rc;
-  }
   if (big_w || big_d)
     return proj_bwd_big(big_w, big_d, M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
                         dA, ldda, accumulate_d, workspace, workspace_floats, stream, prev,
@@ -1758,50 +1732,16 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
     bytes += 4.0 * (double)M * kb_d[b] + 4.0 * N * kb_d[b];
   }
   bytes += 4.0 * (double)p.splits * p.part_stride;
-  auto fused_launch = [&](const BwdFusedArgs& fa, hipStream_t st, ProfScope* pr) {
-    const int64_t nb = (int64_t)fa.n_wpad + (int64_t)fa.n_d + (int64_t)fa.n_red;
-    if (nb == 0) return;
-    if (rows)
-      launch(k_proj_bwd_fused<4, true>, dim3((unsigned)nb), dim3(256), 0, st, pr, fa);
-    else if (tnd == 1)
-      launch(k_proj_bwd_fused<1, false>, dim3((unsigned)nb), dim3(256), 0, st, pr, fa);
-    else if (tnd == 2)
-      launch(k_proj_bwd_fused<2, false>, dim3((unsigned)nb), dim3(256), 0, st, pr, fa);
-    else
-      launch(k_proj_bwd_fused<4, false>, dim3((unsigned)nb), dim3(256), 0, st, pr, fa);
-  };
-  if (wstream) {
-    // weight-stream mode: the data items on `stream` (the backward chain
-    // goes on as soon as they are done), the weight items -- with the merged
-    // reduction deferred earlier on the weight stream -- on `wstream` once it
-    // has seen this point of `stream`.  The same two kinds of workgroups as
-    // the one launch, so the same bits.
-    hipStream_t ws = as_stream(wstream);
-    BwdFusedArgs fd = f;
-    fd.n_w = 0;
-    fd.n_wpad = 0;
-    fd.n_red = 0;
-    BwdFusedArgs fw = f;
-    fw.n_d = 0;
-    hipEvent_t ev = next_fork_event();
-    HLH_CHECK_ARG(hipEventRecord(ev, s) == hipSuccess, "proj_bwd: hipEventRecord");
-    HLH_CHECK_ARG(hipStreamWaitEvent(ws, ev, 0) == hipSuccess, "proj_bwd: hipStreamWaitEvent");
-    if (fd.n_d > 0) {
-      // (profiling stamps the data launch only; its figures are the whole
-      // backward's, as for the one launch; weight-only calls go unstamped)
-      ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-      fused_launch(fd, s, &prof);
-      HLH_CHECK_LAUNCH();
-    }
-    fused_launch(fw, ws, nullptr);
-    HLH_CHECK_LAUNCH();
-    if (on_wstream) *on_wstream = 1;
-    s = ws;  // the split reduction belongs to the weight stream
-  } else {
-    ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-    fused_launch(f, s, &prof);
-    HLH_CHECK_LAUNCH();
-  }
+  ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
+  if (rows)
+    launch(k_proj_bwd_fused<4, true>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else if (tnd == 1)
+    launch(k_proj_bwd_fused<1, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else if (tnd == 2)
+    launch(k_proj_bwd_fused<2, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  else
+    launch(k_proj_bwd_fused<4, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
+  HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
   r.part_stride = p.part_stride;
@@ -1831,20 +1771,6 @@ extern "C" int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int6
   return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
                        dA, ldda, accumulate_d, workspace, workspace_floats, stream, merge,
                        defer_out, deferred);
-}
-
-extern "C" int hlhgat_proj_bwd_defer_split(
-    int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w, const float* const* A,
-    const int64_t* lda, const int64_t* kb_w, float* const* dW, const int64_t* lddw, float* dbias,
-    int nb_d, const float* const* W, const int64_t* ldw, const int64_t* kb_d, float* const* dA,
-    const int64_t* ldda, int accumulate_d, float* workspace, int64_t workspace_floats,
-    const hlhgat_reduce_desc_t* merge, hlhgat_reduce_desc_t* defer_out, int* deferred,
-    void* stream, void* weight_stream, int* on_weight_stream) {
-  HLH_CHECK_ARG(weight_stream && weight_stream != stream && on_weight_stream,
-                "proj_bwd_defer_split: needs a weight stream other than `stream`");
-  return proj_bwd_impl(M, N, dC, lddc, nb_w, A, lda, kb_w, dW, lddw, dbias, nb_d, W, ldw, kb_d,
-                       dA, ldda, accumulate_d, workspace, workspace_floats, stream, merge,
-                       defer_out, deferred, weight_stream, on_weight_stream);
 }
 
 extern "C" int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream) {

@@ -296,32 +296,6 @@ bool& fused_bwd_flag() {
 }
 void set_fused_bwd(bool on) { fused_bwd_flag() = on; }
 
-// Weight-gradient stream (hlhgat_proj_bwd_defer_split): under the deferred
-// reductions of TrainStep, a Linear backward's weight-gradient workgroups run
-// on this per-device stream while the data gradient -- the backward chain's
-// critical path -- continues on the chain's own stream; the bucket flush
-// waits for it.  HLHGAT_WEIGHT_STREAM=0/1 (set_weight_stream at run time).
-bool& weight_stream_flag() {
-  static bool on = [] {
-    const char* e = std::getenv("HLHGAT_WEIGHT_STREAM");
-    return e ? e[0] == '1' : false;
-  }();
-  return on;
-}
-void set_weight_stream(bool on) { weight_stream_flag() = on; }
-c10::hip::HIPStreamMasqueradingAsCUDA weight_stream_of(int dev) {
-  static auto* streams = new std::unordered_map<int, c10::hip::HIPStreamMasqueradingAsCUDA>();
-  auto it = streams->find(dev);
-  if (it == streams->end()) {
-    // HLHGAT_WEIGHT_STREAM_HI=1: a high-priority pool stream (A/B)
-    const char* e = std::getenv("HLHGAT_WEIGHT_STREAM_HI");
-    const bool hi = e && e[0] == '1';
-    it = streams->emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
-                                   hi, (c10::DeviceIndex)dev)).first;
-  }
-  return it->second;
-}
-
 
 // One launch for a set of strided rectangles (hlhgat_copy2d_batched);
 // src == nullptr zero-fills.
@@ -497,7 +471,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
                    const std::vector<const float*>& W, const std::vector<int64_t>& ldw,
                    const std::vector<int64_t>& kbd, std::vector<float*>& dA,
                    const std::vector<int64_t>& ldda, void* s, int acc_d = 0,
-                   bool force_defer = false, const std::vector<Tensor>& keep_a = {}) {
+                   bool force_defer = false) {
   const int nbw = (int)A.size(), nbd = (int)W.size();
   const int64_t M = G.size(0), N = G.size(1);
   const int64_t wsf =
@@ -509,22 +483,7 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
   // NodeEdgeInt unpack), which the flush runs after every reduction
   bool defer = d.on && nbw > 0 && (force_defer || deferred_ok(db));
   for (int b = 0; b < nbw && defer && !force_defer; ++b) defer = deferred_ok(dW[b]);
-  // weight-stream mode: only deferred work (every reader of dW waits for the
-  // flush) whose inputs are all held here (keep_a: the A blocks' tensors)
-  void* wst = nullptr;
-  if (defer && weight_stream_flag() && keep_a.size() > 0) {
-    wst = weight_stream_of(G.get_device()).stream();
-    if (wst == s) wst = nullptr;
-  }
-  if (wst) {  // a reduction this stream deferred outside weight-stream mode runs now
-    auto its = d.pending.find(s);
-    if (its != d.pending.end()) {
-      chk(hlhgat_reduce_run(&its->second.desc, s), "reduce_run");
-      d.pending.erase(its);  // its slab was allocated on s: freed in stream order
-    }
-  }
-  void* key = wst ? wst : s;
-  auto it = d.pending.find(key);
+  auto it = d.pending.find(s);
   PendingReduce prev;
   const bool merge = it != d.pending.end();
   if (merge) {
@@ -532,37 +491,16 @@ void proj_bwd_both(const Tensor& G, const std::vector<const float*>& A,
     d.pending.erase(it);
   }
   hlhgat_reduce_desc_t out;
-  int deferred = 0, on_w = 0;
-  if (wst) {
-    chk(hlhgat_proj_bwd_defer_split(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(),
-                                    lda.data(), kbw.data(), dW.data(), lddw.data(), db, nbd,
-                                    W.data(), ldw.data(), kbd.data(), dA.data(), ldda.data(),
-                                    acc_d, ws.data_ptr<float>(), wsf,
-                                    merge ? &prev.desc : nullptr, &out, &deferred, s, wst,
-                                    &on_w),
-        "proj_bwd_split");
-    // the weight stream read G and the A blocks, and (merged) the earlier slab
-    d.streams.insert(wst);
-    if (on_w) {
-      auto ts = weight_stream_of(G.get_device());
-      G.record_stream(ts);
-      for (const auto& t : keep_a)
-        if (t.defined()) t.record_stream(ts);
-      ws.record_stream(ts);
-    }
-    if (merge) prev.ws.record_stream(weight_stream_of(G.get_device()));
-  } else {
-    chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
+  int deferred = 0;
+  chk(hlhgat_proj_bwd_defer(M, N, G.data_ptr<float>(), ld_of(G), nbw, A.data(), lda.data(),
                               kbw.data(), dW.data(), lddw.data(), db, nbd, W.data(), ldw.data(),
                               kbd.data(), dA.data(), ldda.data(), acc_d, ws.data_ptr<float>(),
                               wsf, merge ? &prev.desc : nullptr, defer ? &out : nullptr,
                               &deferred, s),
-          "proj_bwd");
-  }
-  void* owner = on_w ? wst : s;
-  if (merge || deferred) d.streams.insert(owner);
+        "proj_bwd");
+  if (merge || deferred) d.streams.insert(s);
   if (deferred) {
-    d.pending[owner] = PendingReduce{out, ws, owner};
+    d.pending[s] = PendingReduce{out, ws, s};
     for (int b = 0; b < nbw; ++b) d.dests.insert(dW[b]);
     if (db) d.dests.insert(db);
   }
@@ -929,7 +867,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
       std::vector<int64_t> noL;
       std::vector<float*> noD;
       proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? db.data_ptr<float>() : nullptr, noW, noL,
-                    noL, noD, noL, s, 0, false, {x2, T});
+                    noL, noD, noL, s, 0, false);
     } else {
       for (auto& tt : dW) tt.zero_();
       if (need_b) db.zero_();
@@ -951,7 +889,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
       }
       if (!wdef.dWp.empty())
         proj_bwd_both(G, Ap, lda, kb, wdef.dWp, wdef.lddw, wdef.db, Wp, ldw, kb, dA, ldda, s, 0,
-                      false, {x2, T});
+                      false);
       else
         proj_bwd_data(G, Wp, ldw, kb, dA, ldda, s);
       if (K > 1 && !fac.empty()) {  // L1 symmetric: the adjoint uses the same factor
@@ -1214,7 +1152,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
         std::vector<int64_t> noL;
         std::vector<float*> noD;
         proj_bwd_both(G, Ap, lda, kb, dWp, lddw, need_b ? gb.data_ptr<float>() : nullptr, noW,
-                      noL, noL, noD, noL, s, 0, false, As);
+                      noL, noL, noD, noL, s, 0, false);
       }
     } else {
       gw.zero_();
@@ -1249,7 +1187,7 @@ void linear_backward(const Tensor& Gin, const std::vector<Tensor>& As, const Ten
       const int acc = into ? into_acc : 0;
       if (!wAp.empty())
         proj_bwd_both(G, wAp, wlda, kb, wdWp, wlddw, wdb, Wp, ldw, kbs, dA, ldda, s, acc,
-                      force_defer, As);
+                      force_defer);
       else
         proj_bwd_data(G, Wp, ldw, kbs, dA, ldda, s, acc);
     }
@@ -2440,7 +2378,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hlhgat C++ autograd nodes over the libhlhgat C-ABI";
   m.def("conv_bn", &conv_bn);
   m.def("set_fused_bwd", &set_fused_bwd);
-  m.def("set_weight_stream", &set_weight_stream);
   m.def("set_tap", &set_tap);
   m.def("take_tap", &take_tap);
   m.def("join_capture_streams", &join_capture_streams);

@@ -85,10 +85,6 @@ SIGNATURES = {
     "hlhgat_proj_bwd_defer": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_i32, P_vp, P_i64, P_i64,
                                       P_vp, P_i64, c_vp, c_i32, P_vp, P_i64, P_i64, P_vp, P_i64,
                                       c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
-    "hlhgat_proj_bwd_defer_split": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_i32, P_vp, P_i64,
-                                            P_i64, P_vp, P_i64, c_vp, c_i32, P_vp, P_i64, P_i64,
-                                            P_vp, P_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
-                                            c_vp, c_vp, c_vp]),
     "hlhgat_reduce_run": (c_i32, [c_vp, c_vp]),
     "hlhgat_proj_bn_fwd": (c_i32, [c_i32, P_vp, P_i64, P_vp, P_i64, P_i64, c_i64, c_i64, c_vp,
                                    c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32,

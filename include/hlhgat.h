@@ -500,26 +500,6 @@ int hlhgat_proj_bwd_defer(int64_t M, int64_t N, const float* dC, int64_t lddc, i
                           float* workspace, int64_t workspace_floats,
                           const hlhgat_reduce_desc_t* merge, hlhgat_reduce_desc_t* defer_out,
                           int* deferred, void* stream);
-/* hlhgat_proj_bwd_defer with the weight gradient off `stream`: where the
- * one-launch path applies, the data-gradient workgroups launch on `stream`
- * and the weight-gradient workgroups (with `merge`, which must have been
- * deferred on weight_stream) on weight_stream after it waits for `stream`;
- * *on_weight_stream = 1 and the split reduction (launched or deferred)
- * belongs to weight_stream.  Otherwise `merge` runs on weight_stream, the call
- * proceeds as hlhgat_proj_bwd_defer on `stream` and *on_weight_stream = 0.
- * Same workgroups, so the same bits as hlhgat_proj_bwd_defer.  The caller
- * orders every reader of dW / dbias after weight_stream and keeps dC and the
- * A blocks alive until weight_stream has run (hlhgat.train.TrainStep: the
- * bucket flush waits for it). */
-int hlhgat_proj_bwd_defer_split(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
-                                const float* const* A, const int64_t* lda, const int64_t* kb_w,
-                                float* const* dW, const int64_t* lddw, float* dbias, int nb_d,
-                                const float* const* W, const int64_t* ldw, const int64_t* kb_d,
-                                float* const* dA, const int64_t* ldda, int accumulate_d,
-                                float* workspace, int64_t workspace_floats,
-                                const hlhgat_reduce_desc_t* merge,
-                                hlhgat_reduce_desc_t* defer_out, int* deferred, void* stream,
-                                void* weight_stream, int* on_weight_stream);
 int hlhgat_reduce_run(const hlhgat_reduce_desc_t* desc, void* stream);
 
 /* ---- boundary-operator interaction ------------------------------------ */

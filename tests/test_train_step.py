@@ -218,30 +218,6 @@ def test_deferred_split_reductions_bitwise(cuda, graphs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("graphs,fork", [(False, True), (True, True), (True, False)])
-def test_weight_stream_bitwise(cuda, graphs, fork):
-    """The weight gradient's workgroups on their own stream
-    (hlhgat_proj_bwd_defer_split, set_weight_stream): losses and every
-    parameter / running statistic bitwise those of the one-launch Linear
-    backward, eager and graph-replayed steps, one or two chains."""
-    from hlhgat import ops
-    from hlhgat.synthetic import zinc_like_batch
-    batches = [zinc_like_batch(40, seed=7).to(cuda), zinc_like_batch(33, seed=8).to(cuda)]
-    order = [0, 1, 0, 1, 0]
-    res = []
-    try:
-        for on in (False, True):
-            ops._ext.set_weight_stream(on)
-            res.append(_run(graphs, fork, batches, order))
-    finally:
-        ops._ext.set_weight_stream(False)
-    (l0, sd0, _), (l1, sd1, _) = res
-    assert l0 == l1
-    for k in sd0:
-        assert torch.equal(sd0[k], sd1[k]), k
-
-
-@pytest.mark.gpu
 def test_prepacked_neint_weights_bitwise(cuda):
     """Every NodeEdgeInt's weight pack built in one launch per forward
     (ops.nei_prepack) and the gradient unpack deferred to the flush give the
