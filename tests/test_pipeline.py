@@ -217,14 +217,15 @@ def test_lanczos_lmax_matches_fp64_eigh_on_superpixel_batch(cuda):
 
 
 @pytest.mark.gpu
-def test_pipeline_producer_thread_beside_capture_bitwise(cuda):
-    """The config-3 loop of bench.py's cifar_pipeline_leg, small: a producer
+def test_pipeline_producer_thread_beside_replays_bitwise(cuda):
+    """The config-3 loop of bench.py's cifar_pipeline_leg, small: the eager
+    step and the capture of the bucket run first, serially; then a producer
     thread builds augmented superpixel batches on its own stream (device
-    Hodge builder, eig PE, batched MLGC) while this thread runs the training
-    step -- its eager step, the capture of the bucket (thread-local mode: the
-    producer's allocations and kernels on another stream go on beside it) and
-    replays.  Losses and parameters bitwise those of the same batches built
-    first and stepped serially (verdict r4 #8)."""
+    Hodge builder, eig PE, batched MLGC) while this thread replays the step.
+    Losses and parameters bitwise those of the same batches built first and
+    stepped serially (verdict r4 #8).  (A capture made WHILE the producer
+    runs is not supported: tried in round 5, a later test's graph replay in
+    the same process segfaulted)"""
     import queue
     import threading
     import hlhgat
@@ -254,6 +255,8 @@ def test_pipeline_producer_thread_beside_capture_bitwise(cuda):
             for b in range(nb):
                 losses.append(float(st(pad_levels(build(b), caps))))
         else:
+            for b in range(2):  # eager step + capture, serially (as the bench)
+                losses.append(float(st(pad_levels(build(b), caps))))
             main = torch.cuda.current_stream(cuda)
             q = queue.Queue(maxsize=2)
 
@@ -261,7 +264,7 @@ def test_pipeline_producer_thread_beside_capture_bitwise(cuda):
                 s = torch.cuda.Stream(device=cuda)
                 try:
                     with torch.cuda.stream(s):
-                        for b in range(nb):
+                        for b in range(2, nb):
                             datas = pad_levels(build(b), caps)
                             for lv in datas:
                                 for v in vars(lv).values():
