@@ -613,9 +613,18 @@ struct Fork {
   static TStream side_of(int dev) {
     auto& streams = registry();
     auto it = streams.find(dev);
-    if (it == streams.end())
-      it = streams.emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(
-                                    false, (c10::DeviceIndex)dev)).first;
+    if (it == streams.end()) {
+      // a stream of its own, not one of torch's round-robin pool: a pool
+      // stream is handed out again after 32 requests, e.g. as a user's copy
+      // stream, whose uploads would then land inside a capture this side
+      // stream has joined
+      c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)dev);
+      hipStream_t raw = nullptr;
+      TORCH_CHECK(hipStreamCreateWithFlags(&raw, hipStreamNonBlocking) == hipSuccess,
+                  "hlhgat: hipStreamCreateWithFlags");
+      it = streams.emplace(dev, c10::hip::getStreamFromExternalMasqueradingAsCUDA(
+                                    raw, (c10::DeviceIndex)dev)).first;
+    }
     return it->second;
   }
   static hipEvent_t next_event() {

@@ -163,7 +163,10 @@ class StagedFeed:
         self.batches = batches
         self.step = step
         self.depth = int(depth)
-        self.stream = stream if stream is not None else torch.cuda.Stream(device=step.device)
+        if stream is None:
+            from . import ops
+            stream = ops.own_stream(step.device, "copy")
+        self.stream = stream
         self._q: "queue.Queue" = queue.Queue()
         self._room = threading.Semaphore(self.depth)
         self._stop = threading.Event()

@@ -96,13 +96,45 @@ def set_stream_fork(enabled: bool) -> None:
     _FORK_ENABLED = bool(enabled)
 
 
+_OWN_STREAMS = {}
+_HIP_RT = None
+
+
+def own_stream(device, role: str) -> torch.cuda.Stream:
+    """A HIP stream of this library's own for `role` on `device` (created
+    once, non-blocking, never from torch's stream pool).  torch.cuda.Stream()
+    hands out its 32 pool streams round-robin, so two unrelated users can get
+    the same stream -- e.g. a user's copy stream and a side stream that has
+    joined a graph capture, whose uploads would then be captured.  The capture,
+    copy and side streams of TrainStep / StagedFeed / the chains are these."""
+    global _HIP_RT
+    idx = device.index if getattr(device, "index", None) is not None else (
+        device if isinstance(device, int) else torch.cuda.current_device())
+    s = _OWN_STREAMS.get((idx, role))
+    if s is None:
+        import ctypes
+        if _HIP_RT is None:
+            rt = ctypes.CDLL("libamdhip64.so")
+            rt.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            rt.hipSetDevice.argtypes = [ctypes.c_int]
+            _HIP_RT = rt
+        with torch.cuda.device(idx):
+            h = ctypes.c_void_p()
+            rc = _HIP_RT.hipStreamCreateWithFlags(ctypes.byref(h), 1)  # hipStreamNonBlocking
+            if rc != 0:
+                raise RuntimeError(f"hlhgat: hipStreamCreateWithFlags failed ({rc})")
+        s = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+        _OWN_STREAMS[(idx, role)] = s
+    return s
+
+
 def side_stream(device: torch.device, slot: int = 0) -> torch.cuda.Stream:
     """Side stream `slot` of the device (0: the edge chains; 1: batch
     preparation that overlaps the first conv)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE_STREAMS.get((idx, slot))
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        s = own_stream(idx, f"side{slot}")
         _SIDE_STREAMS[(idx, slot)] = s
     return s
 

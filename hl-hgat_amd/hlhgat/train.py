@@ -344,7 +344,7 @@ class TrainStep:
         self.max_graphs = max_graphs
         self._graphs: Dict[Tuple, _Captured] = {}
         self._pool = None
-        self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
+        self._stream = ops.own_stream(dev, "capture") if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
         self._fwd_bwd_calls = 0
         self._ones = {}
@@ -519,7 +519,7 @@ class TrainStep:
             raise RuntimeError("TrainStep.stage needs graphs=True (a ROCm device)")
         if stream is None:
             if getattr(self, "_copy_stream", None) is None:
-                self._copy_stream = torch.cuda.Stream(device=self.device)
+                self._copy_stream = ops.own_stream(self.device, "copy")
             stream = self._copy_stream
         key = batch_key(batch)
         # the stream the replays run on (stage may be called from a feeder
@@ -742,7 +742,7 @@ class InferStep:
         self.max_graphs = max_graphs
         self._graphs: Dict[Tuple, _Captured] = {}
         self._pool = None
-        self._stream = torch.cuda.Stream(device=dev) if self.graphs else None
+        self._stream = ops.own_stream(dev, "capture") if self.graphs else None
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
 
     def _forward(self, batch):

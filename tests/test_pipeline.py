@@ -215,3 +215,84 @@ def test_lanczos_lmax_matches_fp64_eigh_on_superpixel_batch(cuda):
         rel = np.abs(got - np.asarray(ref)) / np.asarray(ref)
         assert rel.max() <= 1e-7, (lv, rel.max(), int(rel.argmax()))
 
+
+@pytest.mark.gpu
+def test_pipeline_producer_thread_beside_replays_bitwise(cuda):
+    """The config-3 loop of bench.py's cifar_pipeline_leg, small: the eager
+    step and the capture of the bucket run first, serially; then a producer
+    thread builds augmented superpixel batches on its own stream (device
+    Hodge builder, eig PE, batched MLGC) while this thread replays the step.
+    Losses and parameters bitwise those of the same batches built first and
+    stepped serially (verdict r4 #8).  (Round 5: with this test in the
+    suite a later test's replay segfaulted while TrainStep, StagedFeed and the
+    chains took their streams from torch's round-robin pool; they now own
+    theirs, ops.own_stream.)"""
+    import queue
+    import threading
+    import hlhgat
+    from hlhgat.hodge_dataset import level_caps, pad_levels
+    from hlhgat.pipeline import SuperpixelPipeline, superpixel_raw
+    from hlhgat.train import TrainStep
+    G, nb = 6, 5
+    kw = dict(channels=[2, 2, 2], filters=[32, 32, 32], mlp_channels=[64], K=3, keig=10,
+              pool_loc=1, l=0.5)
+    raws = [superpixel_raw(9100 + i) for i in range(G * nb)]
+    for i, r in enumerate(raws):
+        r.y = torch.tensor([i % 10])
+    pipe = SuperpixelPipeline(raws, keig=kw["keig"] + 1, aug=True)
+
+    def build(b):
+        return pipe.batch(range(b * G, (b + 1) * G), seed=b, device=cuda)
+    caps = level_caps([build(b) for b in range(nb)], 512)
+    F = torch.nn.functional
+
+    def run(threaded):
+        torch.manual_seed(0)
+        m = hlhgat.HL_HGCNN_CIFAR10SP_dense_int3_attpool(**kw).to(cuda).train()
+        st = TrainStep(m, lambda o, d: F.cross_entropy(o, d[0].y.view(-1).long()), lr=1e-3,
+                       graphs=True)
+        losses = []
+        if not threaded:
+            for b in range(nb):
+                losses.append(float(st(pad_levels(build(b), caps))))
+        else:
+            for b in range(2):  # eager step + capture, serially (as the bench)
+                losses.append(float(st(pad_levels(build(b), caps))))
+            main = torch.cuda.current_stream(cuda)
+            q = queue.Queue(maxsize=2)
+
+            def produce():
+                s = torch.cuda.Stream(device=cuda)
+                try:
+                    with torch.cuda.stream(s):
+                        for b in range(2, nb):
+                            datas = pad_levels(build(b), caps)
+                            for lv in datas:
+                                for v in vars(lv).values():
+                                    if torch.is_tensor(v) and v.is_cuda:
+                                        v.record_stream(main)
+                            ev = torch.cuda.Event()
+                            ev.record(s)
+                            q.put((datas, ev))
+                finally:
+                    q.put(None)
+            th = threading.Thread(target=produce, daemon=True)
+            th.start()
+            while True:
+                it = q.get()
+                if it is None:
+                    break
+                datas, ev = it
+                main.wait_event(ev)
+                losses.append(float(st(datas)))
+            th.join()
+        torch.cuda.synchronize()
+        assert st.stats["captures"] == 1 and st.stats["replay"] == nb - 1, st.stats
+        return losses, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+
+    l0, sd0 = run(False)
+    l1, sd1 = run(True)
+    assert len(l1) == nb and l0 == l1, (l0, l1)
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+    assert np.isfinite(l0).all()
