@@ -361,8 +361,11 @@ __device__ __forceinline__ bool give_up(unsigned long long* word, unsigned long 
 }
 
 // The finaliser, after its generation bump: take every slot of [slots,
-// slots + n) left in this generation; taken[j] (LDS) = 1 for those.  Relaxed
-// loads issued after the bump returned; a match is taken with a seq_cst CAS.
+// slots + n) left in this generation; taken[j] (LDS) = 1 for those.  The bump
+// is a seq_cst RMW that thread 0 waits for (vmcnt(0)) and fences before the
+// workgroup barrier below, and the slot loads are seq_cst: with the waiter's
+// seq_cst (slot store, generation load) one of the two sides sees the other's
+// write.  A match is taken with a seq_cst CAS.
 // Returns (in every thread) whether any was taken.
 template <int NT>
 __device__ __forceinline__ bool take_left(unsigned long long* slots, int n, unsigned gen0,
@@ -374,7 +377,7 @@ __device__ __forceinline__ bool take_left(unsigned long long* slots, int n, unsi
   for (int j = threadIdx.x; j < n; j += NT) {
     unsigned char t = 0;
     const unsigned long long v =
-        __hip_atomic_load((gu64c_t*)(slots + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_load((gu64c_t*)(slots + j), __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
     if (v == mark) {
       unsigned long long exp = mark;
       if (__hip_atomic_compare_exchange_strong((gu64c_t*)(slots + j), &exp, mark + 1ull,
@@ -413,8 +416,13 @@ __device__ __forceinline__ unsigned bar_wait(unsigned long long* word, unsigned 
     unsigned role;
     if (arrived >= total) report_state_error(err);
     if (arrived == total - 1) {
+      // seq_cst bump, completed and fenced before the workgroup barrier that
+      // precedes take_left's slot loads (the finaliser's half of the
+      // store-load handshake with give_up)
       __hip_atomic_fetch_add((gu64c_t*)word, (1ull << 32) - (unsigned long long)total,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                             __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
       role = kFinal;
     } else if (poll_gen(word, gen0, wait_us)) {
       role = kOwn;
@@ -1333,9 +1341,12 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
     if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_fetch_add((gu64c_t*)word, 1ull << 32, __ATOMIC_RELAXED,
+    if (threadIdx.x == 0) {  // seq_cst, completed and fenced (see bar_wait)
+      __hip_atomic_fetch_add((gu64c_t*)word, 1ull << 32, __ATOMIC_SEQ_CST,
                              __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
   } else {
     if (threadIdx.x == 0) {
       unsigned ok = poll_gen(word, s_gen0, s.wait_us) ? 1u : 0u;

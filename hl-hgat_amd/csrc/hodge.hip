@@ -204,11 +204,17 @@ struct BuildArgs {
 // A row whose end lies past the buffers (row sizes the caller supplied that
 // do not match the graph: duplicate edges, self-loops) writes nothing and
 // raises HLHGAT_DEVERR_HODGE_SIZE; rp is a prefix sum of non-negative sizes,
-// so rp[row + 1] <= cap puts the whole row in range.
-__device__ __forceinline__ bool row_fits(const BuildArgs& a, int64_t row) {
-  if ((int64_t)a.rp[row + 1] <= a.cap && a.rp[row] <= a.rp[row + 1]) return true;
+// so rp[row + 1] <= cap puts the whole row in range.  The thread of the last
+// row also checks rp[n_rows] == cap: sizes whose total exceeds the device's
+// would otherwise leave the tail of col / val unwritten.
+__device__ __forceinline__ void hodge_size_error(const BuildArgs& a) {
   if (a.err) __hip_atomic_store(a.err, (unsigned)HLHGAT_DEVERR_HODGE_SIZE, __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool row_fits(const BuildArgs& a, int64_t row, int64_t n_rows) {
+  if (row == n_rows - 1 && (int64_t)a.rp[n_rows] != a.cap) hodge_size_error(a);
+  if ((int64_t)a.rp[row + 1] <= a.cap && a.rp[row] <= a.rp[row + 1]) return true;
+  hodge_size_error(a);
   return false;
 }
 
@@ -224,7 +230,7 @@ __global__ __launch_bounds__(256) void k_hodge_l0_rows(BuildArgs a) {
   const int e0 = a.inc_rowptr[v], e1 = a.inc_rowptr[v + 1];
   const int deg = e1 - e0;
   if (deg == 0) return;  // isolated node: all-zero row, dropped as dense_to_sparse drops zeros
-  if (!row_fits(a, v)) return;
+  if (!row_fits(a, v, a.n_nodes)) return;
   const float lam = a.lam_node[v];
   int out = a.rp[v];
   int64_t last = -1;
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(256) void k_hodge_l0_rows(BuildArgs a) {
 __global__ __launch_bounds__(256) void k_hodge_l1_rows(BuildArgs a) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= a.n_edges) return;
-  if (!row_fits(a, e)) return;
+  if (!row_fits(a, e, a.n_edges)) return;
   const int64_t i = a.ei[e], j = a.ei[a.n_edges + e];
   const float lam = a.lam_node[i];
   int p = a.inc_rowptr[i], pe = a.inc_rowptr[i + 1];

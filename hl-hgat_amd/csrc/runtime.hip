@@ -104,6 +104,43 @@ extern "C" int hlhgat_clear_device_errors(void) {
 
 extern "C" const char* hlhgat_last_error(void) { return g_last_error.c_str(); }
 
+extern "C" int hlhgat_stream_create(int device, unsigned flags, const uint32_t* cu_mask,
+                                    int cu_mask_words, void** out) {
+  HLH_CHECK_ARG(out && device >= 0 && cu_mask_words >= 0 && (cu_mask_words == 0 || cu_mask),
+                "stream_create: bad arguments");
+  int prev = 0;
+  HLH_CHECK_HIP(hipGetDevice(&prev));
+  HLH_CHECK_HIP(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  hipError_t e;
+  if (cu_mask_words > 0) {
+    int cus = 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    int on = 0;
+    for (int w = 0; w < cu_mask_words; ++w) on += __builtin_popcount(cu_mask[w]);
+    if (e == hipSuccess && (on == 0 || cu_mask_words * 32 < cus)) {
+      (void)hipSetDevice(prev);
+      HLH_CHECK_ARG(false, "stream_create: the CU mask must cover all %d CUs (%d words given) "
+                    "and enable at least one", cus, cu_mask_words);
+    }
+    if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&s, (uint32_t)cu_mask_words, cu_mask);
+    // (a CU-masked stream is blocking w.r.t. the null stream; the library's
+    // streams only ever synchronise through events)
+  } else {
+    e = hipStreamCreateWithFlags(&s, flags);
+  }
+  (void)hipSetDevice(prev);
+  HLH_CHECK_HIP(e);
+  *out = s;
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_stream_cu_mask(void* stream, uint32_t* cu_mask, int cu_mask_words) {
+  HLH_CHECK_ARG(stream && cu_mask && cu_mask_words > 0, "stream_cu_mask: bad arguments");
+  HLH_CHECK_HIP(hipExtStreamGetCUMask(as_stream(stream), (uint32_t)cu_mask_words, cu_mask));
+  return HLHGAT_OK;
+}
+
 extern "C" int hlhgat_prof_enable(int kernel_class, int enable) {
   HLH_CHECK_ARG(kernel_class >= 0 && kernel_class < HLHGAT_PROF_NCLASS,
                 "prof_enable: bad kernel class %d", kernel_class);

@@ -173,6 +173,7 @@ class StagedFeed:
         self._thread: Optional[threading.Thread] = None
         self.use_thread = bool(thread)
         self.timing = {"source": 0.0, "room": 0.0, "stage": 0.0, "n": 0}
+        self._last = None  # the handle last handed to the consumer (maybe not stepped)
 
     def _run(self):
         import time
@@ -229,8 +230,13 @@ class StagedFeed:
                     self.timing["n"] += 1
                 if not ahead:
                     return
-                yield ahead.popleft()
+                self._last = ahead.popleft()
+                yield self._last
         finally:
+            # a feed closed early: give back what was staged but not stepped
+            for st in ahead:
+                self.step.unstage(st)
+            self._unstage_last()
             close = getattr(it, "close", None)
             if close is not None:
                 close()
@@ -249,15 +255,34 @@ class StagedFeed:
                     return
                 if isinstance(item, BaseException):
                     raise item
+                self._last = item
                 yield item
                 self._room.release()  # the consumer has stepped it: room for one more
         finally:
             self.close()
 
+    def _unstage_last(self):
+        st, self._last = self._last, None
+        if st is not None:
+            self.step.unstage(st)  # a no-op when the consumer stepped it
+
     def close(self):
+        """Stop the feeder and give back every batch it staged that was not
+        stepped (TrainStep.unstage): the ones queued for the consumer, and the
+        one last handed out if the consumer left before stepping it."""
         self._stop.set()
         t, self._thread = self._thread, None
         if t is not None and t is not threading.current_thread():
             # unblock a feeder waiting for room, then let it finish its batch
             self._room.release()
             t.join(timeout=30)
+            if t.is_alive():
+                return  # still inside stage(): its handle cannot be reclaimed yet
+        while True:
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if item is not self._END and not isinstance(item, BaseException):
+                self.step.unstage(item)
+        self._unstage_last()

@@ -97,35 +97,41 @@ def set_stream_fork(enabled: bool) -> None:
 
 
 _OWN_STREAMS = {}
-_HIP_RT = None
 
 
-def own_stream(device, role: str) -> torch.cuda.Stream:
+def own_stream(device, role: str, cu_mask=None) -> torch.cuda.Stream:
     """A HIP stream of this library's own for `role` on `device` (created
     once, non-blocking, never from torch's stream pool).  torch.cuda.Stream()
     hands out its 32 pool streams round-robin, so two unrelated users can get
     the same stream -- e.g. a user's copy stream and a side stream that has
     joined a graph capture, whose uploads would then be captured.  The capture,
-    copy and side streams of TrainStep / StagedFeed / the chains are these."""
-    global _HIP_RT
+    copy and side streams of TrainStep / StagedFeed / the chains are these.
+    Created by libhlhgat (hlhgat_stream_create), i.e. by the HIP runtime torch
+    loaded.  cu_mask (a list of 32-bit words, bit c = CU c): the stream runs on
+    those CUs only (the first call for a role fixes its mask)."""
     idx = device.index if getattr(device, "index", None) is not None else (
         device if isinstance(device, int) else torch.cuda.current_device())
     s = _OWN_STREAMS.get((idx, role))
     if s is None:
         import ctypes
-        if _HIP_RT is None:
-            rt = ctypes.CDLL("libamdhip64.so")
-            rt.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
-            rt.hipSetDevice.argtypes = [ctypes.c_int]
-            _HIP_RT = rt
-        with torch.cuda.device(idx):
-            h = ctypes.c_void_p()
-            rc = _HIP_RT.hipStreamCreateWithFlags(ctypes.byref(h), 1)  # hipStreamNonBlocking
-            if rc != 0:
-                raise RuntimeError(f"hlhgat: hipStreamCreateWithFlags failed ({rc})")
+        h = ctypes.c_void_p()
+        if cu_mask:
+            words = (ctypes.c_uint32 * len(cu_mask))(*[int(w) & 0xffffffff for w in cu_mask])
+            check(LIB.hlhgat_stream_create(idx, 1, words, len(cu_mask), ctypes.byref(h)),
+                  "stream_create")
+        else:
+            check(LIB.hlhgat_stream_create(idx, 1, None, 0, ctypes.byref(h)), "stream_create")
         s = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
         _OWN_STREAMS[(idx, role)] = s
     return s
+
+
+def stream_cu_mask(stream, words: int = 8):
+    """The CU mask `stream` runs on (a list of 32-bit words)."""
+    import ctypes
+    buf = (ctypes.c_uint32 * words)()
+    check(LIB.hlhgat_stream_cu_mask(stream.cuda_stream, buf, words), "stream_cu_mask")
+    return list(buf)
 
 
 def side_stream(device: torch.device, slot: int = 0) -> torch.cuda.Stream:

@@ -222,10 +222,11 @@ class Staged:
     """A batch uploaded for a coming step by TrainStep.stage: either already
     in the static buffers of the captured graph `slot`, or in fresh device
     tensors (`batch`); `event` marks the end of the upload."""
-    __slots__ = ("batch", "event", "slot", "key")
+    __slots__ = ("batch", "event", "slot", "key", "done")
 
     def __init__(self, batch, event, slot, key):
         self.batch, self.event, self.slot, self.key = batch, event, slot, key
+        self.done = False  # stepped, or given back by TrainStep.unstage
 
 
 def _quiesce_collectives() -> None:
@@ -538,7 +539,11 @@ class TrainStep:
         with self._stage_lock:
             t1 = clock()
             ev, slot, free = self._stage_plan(key)
-        st = self._stage_copy(batch, stream, key, main, ev, slot, free)
+        try:
+            st = self._stage_copy(batch, stream, key, main, ev, slot, free)
+        except BaseException:
+            self._release(slot)  # the plan counted this batch: give the counts back
+            raise
         # host time per stage() part (diagnostics: bench.py's loader leg)
         tm = self.stage_timing
         tm["lock"] += t1 - t0
@@ -579,6 +584,25 @@ class TrainStep:
             slot.pending += 1
             free = slot.free
         return ev, slot, free
+
+    def _release(self, slot) -> None:
+        """Undo one staged batch's bookkeeping: its slot's pending count (the
+        slot may be staged into again) and the outstanding count."""
+        with self._stage_lock:
+            if slot is not None:
+                slot.pending -= 1
+            self._outstanding -= 1
+
+    def unstage(self, st: Staged) -> None:
+        """Give back a staged batch that will not be stepped (a feed closed
+        early: a break, an exception, StagedFeed.close()).  Its upload may
+        still be in flight; a later stage() into the same slot waits for the
+        slot's release as always, and the copy stream is in order.  A handle
+        already stepped or given back is ignored."""
+        if st.done:
+            return
+        st.done = True
+        self._release(st.slot)
 
     def _stage_copy(self, batch, stream, key, main, ev, slot, free) -> Staged:
         if slot is None:  # fresh device tensors (first steps of a shape, or every slot taken)
@@ -664,13 +688,17 @@ class TrainStep:
         return ent.loss
 
     def _call_staged(self, st: Staged) -> torch.Tensor:
+        if st.done:
+            raise RuntimeError("TrainStep: this staged batch was already stepped or unstaged")
+        st.done = True
         torch.cuda.current_stream(self.device).wait_event(st.event)
         try:
             if st.slot is not None:
-                loss = self._replay(st.slot)  # records the slot's release event
-                with self._stage_lock:  # only now may a feeder stage into it again
-                    st.slot.pending -= 1
-                return loss
+                try:
+                    return self._replay(st.slot)  # records the slot's release event
+                finally:
+                    with self._stage_lock:  # only now may a feeder stage into it again
+                        st.slot.pending -= 1
             ent = self._graphs.get(st.key)
             if ent is None:
                 return self(st.batch)
@@ -680,11 +708,12 @@ class TrainStep:
                     if free:  # taken, so a feeder does not stage into it meanwhile
                         free[0].pending += 1
                 if free:  # copy-in into a graph no staged upload is waiting for
-                    free[0].load(st.batch)
-                    loss = self._replay(free[0])
-                    with self._stage_lock:
-                        free[0].pending -= 1
-                    return loss
+                    try:
+                        free[0].load(st.batch)
+                        return self._replay(free[0])
+                    finally:
+                        with self._stage_lock:
+                            free[0].pending -= 1
             # one more slot for this shape: the staged tensors are its static
             # buffers; capturing does not run the step, the first replay does
             return self._replay(self._capture(st.batch, st.key, slot_of=ent))
@@ -713,11 +742,12 @@ class TrainStep:
                 free[0].pending += 1
         if not free:  # every graph of the shape awaits a staged batch: one more
             return self._replay(self._capture(self._upload(batch), key, slot_of=ent))
-        free[0].load(batch)
-        loss = self._replay(free[0])
-        with self._stage_lock:
-            free[0].pending -= 1
-        return loss
+        try:
+            free[0].load(batch)
+            return self._replay(free[0])
+        finally:
+            with self._stage_lock:
+                free[0].pending -= 1
 
     def state_dict(self):
         return {"model": self.model.state_dict(), "opt": self.opt.state_dict()}

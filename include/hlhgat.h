@@ -781,6 +781,25 @@ int hlhgat_copy2d_batched(int n, const float* const* src, const int64_t* lds,
 int hlhgat_device_errors(unsigned* out);
 int hlhgat_clear_device_errors(void);
 
+/* ---- streams ------------------------------------------------------------ */
+/* A HIP stream of the library's own on `device` (the capture, copy and side
+ * streams of hlhgat.train.TrainStep / hlhgat.loader.StagedFeed / the node and
+ * edge chains: never one of torch's round-robin pool streams, which two
+ * unrelated users can be handed at once).  Created by the HIP runtime this
+ * library is linked against -- the one torch loaded (same SONAME), so the
+ * handle is valid in torch.cuda.ExternalStream.  cu_mask_words > 0: the stream
+ * runs only on the CUs whose bits are set (hipExtStreamCreateWithCUMask; bit
+ * c of word c/32 = CU c; the words must cover every CU of the device) -- the
+ * config-3 per-sample producer's stream (hlhgat.pipeline), so the replayed
+ * step keeps the other CUs.  flags: hipStreamNonBlocking (1) etc., unmasked
+ * streams only.  The reference has no streams (one implicit CUDA stream,
+ * main_*.py); these are plumbing of the drop-in's own training loop. */
+int hlhgat_stream_create(int device, unsigned flags, const uint32_t* cu_mask, int cu_mask_words,
+                         void** out);
+/* The CU mask a stream runs on (hipExtStreamGetCUMask): all ones for an
+ * unmasked stream. */
+int hlhgat_stream_cu_mask(void* stream, uint32_t* cu_mask, int cu_mask_words);
+
 /* Test hook: `workgroups` workgroups of 64 threads with lds_bytes of LDS
  * each; the first `hold` of them stay resident for `usec` microseconds (time
  * bounded), the others exit at once -- a kernel that holds most CUs while

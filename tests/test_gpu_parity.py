@@ -1234,9 +1234,10 @@ def test_device_hodge_builder_matches_reference(cuda):
 
 
 def test_hodge_build_undersized_raises(cuda):
-    """sizes= smaller than the graph's Laplacians (a caller's
-    simple-graph formula given other input): the build kernels write nothing
-    past the buffers and raise HLHGAT_DEVERR_HODGE_SIZE; exact sizes stay
+    """sizes= smaller (a caller's simple-graph formula given other
+    input) or larger than the graph's Laplacians: the build
+    kernels write nothing past the buffers and raise HLHGAT_DEVERR_HODGE_SIZE;
+    exact sizes stay
     clean and bitwise the sizes=None build."""
     from hlhgat import ops
     from hlhgat.hodge_dataset import collate
@@ -1252,7 +1253,10 @@ def test_hodge_build_undersized_raises(cuda):
     for x, y in zip(got[:4], ref[:4]):
         assert torch.equal(x, y)
     ops.check_device_errors()
-    for short in ((N, nnz0 - 5, nnz1), (N, nnz0, nnz1 - 7), (N, 0, 0)):
+    # undersized, and oversized: a total past the device's rows
+    # would leave the tail of col / val unwritten
+    for short in ((N, nnz0 - 5, nnz1), (N, nnz0, nnz1 - 7), (N, 0, 0),
+                  (N, nnz0 + 5, nnz1), (N, nnz0, nnz1 + 7)):
         ops.hodge_build(ei, b.num_node1.tolist(), lam, sizes=short)
         with pytest.raises(RuntimeError, match="hodge_build"):
             ops.check_device_errors()

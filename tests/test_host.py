@@ -648,45 +648,98 @@ def test_graph_loader_stream_equals_epochs():
     it.close()
 
 
+class _FakeStaged:
+    def __init__(self, b):
+        self.b, self.done = b, False
+
+    def __eq__(self, other):
+        return other == ("st", self.b)
+
+
+class _FakeStep:
+    """Stand-in for TrainStep's staging interface (stage / __call__ /
+    unstage), recording the calls."""
+
+    def __init__(self, limit=3):
+        import threading
+        self.staged, self.stepped, self.unstaged = [], [], []
+        self.lock = threading.Lock()
+        self.limit = limit
+
+    def stage(self, b, stream):
+        with self.lock:
+            self.staged.append(b)
+            out = len(self.staged) - len(self.stepped) - len(self.unstaged)
+            assert out <= self.limit, "staged too far ahead"
+        return _FakeStaged(b)
+
+    def __call__(self, st):
+        assert not st.done
+        st.done = True
+        with self.lock:
+            self.stepped.append(st.b)
+
+    def unstage(self, st):
+        if st.done:
+            return
+        st.done = True
+        with self.lock:
+            self.unstaged.append(st.b)
+
+
 @pytest.mark.parametrize("thread", [True, False])
 def test_staged_feed_order_and_depth(thread):
     """StagedFeed's host logic (no device: a stand-in step records stage()
     calls): every batch is staged once, in order, handed over in order, and
     never more than `depth` staged batches wait beyond the one being stepped;
     a source error reaches the consumer."""
-    import threading
     from hlhgat.loader import StagedFeed
 
-    class FakeStep:
-        def __init__(self):
-            self.staged, self.stepped = [], []
-            self.lock = threading.Lock()
-
-        def stage(self, b, stream):
-            with self.lock:
-                self.staged.append(b)
-                assert len(self.staged) - len(self.stepped) <= 3, "staged too far ahead"
-            return ("st", b)
-
-        def __call__(self, st):
-            with self.lock:
-                self.stepped.append(st[1])
-
-    step = FakeStep()
+    step = _FakeStep()
     feed = StagedFeed(iter(range(17)), step, depth=2, stream=object(), thread=thread)
     for st in feed:
         assert st == ("st", len(step.stepped))
         step(st)
     assert step.staged == step.stepped == list(range(17))
+    assert step.unstaged == []
 
     def bad():
         yield 0
         raise ValueError("source failed")
 
-    feed = StagedFeed(bad(), FakeStep(), depth=2, stream=object(), thread=thread)
+    step = _FakeStep()
+    feed = StagedFeed(bad(), step, depth=2, stream=object(), thread=thread)
     with pytest.raises(ValueError, match="source failed"):
         for st in feed:
             pass
+    assert step.unstaged == [0]  # handed out, never stepped: given back
+
+
+@pytest.mark.parametrize("thread", [True, False])
+@pytest.mark.parametrize("before_step", [False, True])
+def test_staged_feed_early_close_unstages(thread, before_step):
+    """a feed left early (break; the endless GraphLoader.stream()
+    is only ever left that way) gives back every batch it staged and nobody
+    stepped -- the queued ones and, when the consumer broke before stepping
+    it, the one last handed out -- so the step's outstanding / pending counts
+    return to what was stepped, and staging can go on (repeatedly)."""
+    import itertools
+    from hlhgat.loader import StagedFeed
+
+    step = _FakeStep()
+    for rnd in range(4):
+        feed = StagedFeed(itertools.count(100 * rnd), step, depth=2, stream=object(),
+                          thread=thread)
+        for k, st in enumerate(feed):
+            if before_step and k == 3:
+                break
+            step(st)
+            if k == 3:
+                break
+        assert sorted(step.stepped + step.unstaged) == sorted(step.staged), rnd
+    assert len(step.stepped) == (12 if before_step else 16)
+    if not thread:  # the inline feed stages `depth` ahead deterministically
+        assert len(step.unstaged) >= 4, step.unstaged
 
 
 def test_native_mlgc_batch_equals_per_graph():

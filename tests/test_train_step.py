@@ -851,3 +851,93 @@ def test_staged_feed_thread_bitwise(cuda, monkeypatch, wait, thread, slots):
     for key in sd_ref:
         assert torch.equal(sd_ref[key], sd[key]), key
     assert np.isfinite(losses).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thread", [True, False])
+def test_staged_feed_early_close_then_stage_again(cuda, thread):
+    """leaving StagedFeed(GraphLoader.stream(), ...) early gives
+    back the batches it staged and nobody stepped (TrainStep.unstage): after
+    several early exits the step's outstanding count is 0, every slot's
+    pending count is 0, and staging / stepping goes on (it would raise
+    'more than 8 staged batches outstanding' with the handles leaked)."""
+    import hlhgat
+    from hlhgat.hodge_dataset import PackedGraphs
+    from hlhgat.loader import GraphLoader, StagedFeed
+    from hlhgat.synthetic import zinc_like_graph
+    from hlhgat.train import TrainStep
+    ds = PackedGraphs([zinc_like_graph(900 + i) for i in range(48)], check_hodge=False)
+    ld = GraphLoader(ds, 12, caps=None, workers=2, prefetch=4, pin=True)
+    torch.manual_seed(0)
+    m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**KW).to(cuda).train()
+    crit = torch.nn.L1Loss()
+    step = TrainStep(m, lambda o, b: crit(o.view(-1, 1), b.y.view(-1, 1)), lr=1e-3,
+                     graphs=True, stage_slots=4)
+    n = 0
+    for rnd in range(5):
+        it = ld.stream()
+        try:
+            for k, st in enumerate(StagedFeed(it, step, depth=3, thread=thread)):
+                if k == 2 and rnd % 2:
+                    break  # left before stepping the handle
+                step(st)
+                n += 1
+                if k == 2:
+                    break
+        finally:
+            it.close()
+        assert step._outstanding == 0, (rnd, step._outstanding)
+        for ent in step._graphs.values():
+            assert all(sl.pending == 0 for sl in ent.slots), rnd
+    torch.cuda.synchronize()
+    _check_errors()
+    assert n == 3 * 3 + 2 * 2
+    assert step.stats["replay"] >= 8
+
+
+@pytest.mark.gpu
+def test_own_streams_never_from_torch_pool(cuda):
+    """Round 5's host segfault: torch's 32-stream round-robin pool handed a
+    test's copy stream out again as a capture-joined side stream.  The
+    library's capture, copy and side streams (Python roles and the C++
+    fork's side stream) are its own: none of them is among 64 consecutive
+    torch.cuda.Stream() handles, and each role keeps one stream."""
+    from hlhgat import ops
+    idx = cuda.index if cuda.index is not None else torch.cuda.current_device()
+    ours = {ops.own_stream(cuda, r).cuda_stream for r in ("capture", "copy")}
+    ours |= {ops.side_stream(cuda, k).cuda_stream for k in (0, 1)}
+    ours.add(int(ops._ext.fork_side_stream(idx)))
+    assert len(ours) == 5
+    pool = {torch.cuda.Stream(device=cuda).cuda_stream for _ in range(64)}
+    assert not (ours & pool), "a library stream came from torch's pool"
+    assert ops.own_stream(cuda, "copy").cuda_stream in ours  # cached per role
+    # unmasked streams run on every CU
+    n_cu = torch.cuda.get_device_properties(cuda).multi_processor_count
+    mask = ops.stream_cu_mask(ops.own_stream(cuda, "capture"), words=(n_cu + 31) // 32)
+    assert sum(bin(w).count("1") for w in mask) == n_cu
+
+
+@pytest.mark.gpu
+def test_cu_masked_stream_runs_kernels(cuda):
+    """hlhgat_stream_create with a CU mask (the config-3 producer's stream):
+    the mask reads back as set, and library kernels launched on the stream
+    give the same results as on the default stream."""
+    from hlhgat import ops
+    n_cu = torch.cuda.get_device_properties(cuda).multi_processor_count
+    words = (n_cu + 31) // 32
+    mask = [0] * words
+    for c in range(0, n_cu, 8):  # one CU in eight: every XCD keeps some
+        mask[c // 32] |= 1 << (c % 32)
+    s = ops.own_stream(cuda, "test-masked", cu_mask=mask)
+    got = ops.stream_cu_mask(s, words=words)
+    assert got == mask, (got, mask)
+    x = torch.randn(5000, 64, device=cuda)
+    w = torch.randn(32, 64, device=cuda)
+    ref = ops.linear_blocks([x], w, None)
+    torch.cuda.synchronize()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out = ops.linear_blocks([x], w, None)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -1,5 +1,8 @@
 #!/bin/bash
-# Round-5 GPU steps on one MI355X.  Usage: tools/gpu_r5.sh TAG step [step ...]
+# GPU steps on one MI355X (every round's measurements go through this one script).
+# Usage: tools/gpu_steps.sh TAG step [step ...]
+#   sel     the GPU tests matching $SEL (pytest -k)
+#   quick   the config-2 bench line alone (no heads, loader, census, CPU leg)
 #   bn      the BatchNorm barrier tests (hand-over, CU hog, bitwise)
 #   tests   the whole GPU suite
 #   smoke   __graft_entry__.smoke()
@@ -26,6 +29,8 @@ step() {  # name timeout cmd...
 PT="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method thread"
 for s in "$@"; do
   case $s in
+    sel) step sel 600 $PT tests -m gpu -v -k "$SEL" ;;  # SEL="expr" tools/gpu_steps.sh TAG sel
+    quick) step quick 300 python bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-replay-census --no-loader --steps 30 ;;
     bn) step bn 600 $PT tests/test_gpu_parity.py -m gpu -v -s -k "bn_ or proj_bn or handover or hog" ;;
     tests) step tests 1100 $PT tests -m gpu -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

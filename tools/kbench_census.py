@@ -1,5 +1,5 @@
 """Projection kernels at the exact shapes of a step (a HLHGAT_LOG_PROJ census,
-tools/gpu_r5.sh census5): each distinct (call, M, N, blocks, ld) timed in
+tools/gpu_steps.sh census5): each distinct (call, M, N, blocks, ld) timed in
 isolation per hlhgat_set_gemm_big mode, and the census-weighted sum -- the
 step's GEMM time if every launch ran as fast as alone.
 
