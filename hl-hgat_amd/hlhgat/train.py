@@ -44,6 +44,17 @@ HIP_ADAM = True
 # DEFER_REDUCE = False (tests): every Linear backward launches its own split
 # reduction instead of handing it to the next one on its stream (same bits)
 DEFER_REDUCE = True
+# Gradient exchange for world > 1 (DDP's job in the reference-side drop-in,
+# SURVEY §8e; the reference itself is single-GPU): the flat gradient buffer is
+# cut into buckets of about BUCKET_MB, last parameters first (the order the
+# backward finishes them), and each bucket's all-reduce is issued from a
+# post-accumulate-grad hook as soon as its last gradient has landed, so it
+# runs beside the rest of the backward.  OVERLAP: "auto" (default) = only when
+# that makes at least two buckets (configs 3-5: 10-16 MB of gradients; config
+# 2's 2.6 MB stays one all-reduce after the backward), "1" = always (tests),
+# "0" = never.
+BUCKET_MB = float(os.environ.get("HLHGAT_BUCKET_MB", "4"))
+OVERLAP = os.environ.get("HLHGAT_OVERLAP", "auto")
 # KEEP_GRAPHS = True (tests, introspection): captures keep their hipGraph_t
 # (torch.cuda.CUDAGraph(keep_graph=True), then instantiate), so
 # ops.graph_kernel_count can inspect a captured step
@@ -259,7 +270,8 @@ class TrainStep:
 
     def __init__(self, model: torch.nn.Module, loss_fn: Callable, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 graphs: bool = True, max_graphs: int = 32, stage_slots: int = STAGE_SLOTS):
+                 graphs: bool = True, max_graphs: int = 32, stage_slots: int = STAGE_SLOTS,
+                 overlap: Optional[bool] = None, bucket_mb: Optional[float] = None):
         if isinstance(model, torch.nn.parallel.DistributedDataParallel):
             # DDP would all-reduce the gradients in its hooks and TrainStep again in
             # its bucket (two reductions, and DDP's gradient_as_bucket_view fights the
@@ -346,6 +358,7 @@ class TrainStep:
         self._graphs: Dict[Tuple, _Captured] = {}
         self._pool = None
         self._stream = ops.own_stream(dev, "capture") if self.graphs else None
+        self._setup_buckets(overlap, bucket_mb)
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
         self._fwd_bwd_calls = 0
         self._ones = {}
@@ -375,6 +388,7 @@ class TrainStep:
         dests = []
         if defer:
             self._ext.reduce_defer(True)
+        ov = self._overlap_begin(defer)
         try:
             out = self.model(batch)
             loss = self.loss_fn(out, batch)
@@ -385,23 +399,156 @@ class TrainStep:
                 one = self._ones[key] = torch.ones((), dtype=loss.dtype, device=loss.device)
             loss.backward(one if loss.dim() == 0 else None)
         finally:
+            if ov is not None:
+                self._ov = None  # hooks idle again (also after an exception)
             if self._ext is not None and self._fwd_bwd_calls == 1:
                 # first step: only a parameter whose .grad IS its bucket view
                 # (ONE contribution, a HIP node's view that AccumulateGrad
                 # adopted unread) may have its reduction deferred; a summed,
-                # cloned or torch-produced gradient is never deferred
+                # cloned or torch-produced gradient is never deferred (with the
+                # overlap, a bucket's launch re-points .grad at its view: the
+                # hook recorded what AccumulateGrad had left there)
                 base = self.flat_grad.data_ptr()
                 self._ext.grad_bucket_no_defer(
-                    [p for p, off in zip(self.params, self._offsets)
-                     if p.grad is None or p.grad.data_ptr() != base + 4 * off])
+                    [p for i, (p, off) in enumerate(zip(self.params, self._offsets))
+                     if (ov is not None and i in ov["not_adopted"]) or p.grad is None
+                     or p.grad.data_ptr() != base + 4 * off])
             if defer:
                 # the last reduction of each stream, before anything reads the bucket
-                dests = self._ext.reduce_flush(self.device.index if self.device.index is not None
-                                               else torch.cuda.current_device())
+                dests = self._ext.reduce_flush(self._dev_index())
                 self._ext.reduce_defer(False)
+        if ov is not None:
+            dests = list(dests) + ov["dests"]
         if self._ext is not None:
             self._adopt_grads(set(dests))
+        if ov is not None:
+            # buckets whose hooks did not all fire (unused parameters; a
+            # gradient that never reached AccumulateGrad): now, after the flush
+            late = 0
+            for b in range(len(self._buckets)):
+                if not ov["launched"][b]:
+                    self._launch_bucket(ov, b, flush=False)
+                    late += 1
+            self._ov_works = ov["works"]
+            self.overlap_stats["in_backward"] += len(self._buckets) - late
+            self.overlap_stats["after_backward"] += late
         return loss.detach()
+
+    # -- the gradient exchange, bucketed and overlapped with the backward --
+    def _dev_index(self) -> int:
+        return self.device.index if self.device.index is not None else torch.cuda.current_device()
+
+    def _setup_buckets(self, overlap: Optional[bool], bucket_mb: Optional[float]) -> None:
+        """Buckets of the flat gradient buffer (contiguous ranges, last
+        parameters first, each >= bucket_mb unless it is the first) and a
+        post-accumulate-grad hook per parameter that counts its bucket down."""
+        self._ov = None
+        self._ov_works = []
+        self._buckets = []
+        self.overlap = False
+        # bucket all-reduces issued from the backward's hooks / after it
+        self.overlap_stats = {"in_backward": 0, "after_backward": 0}
+        if not self._exchange:
+            return
+        mb = BUCKET_MB if bucket_mb is None else float(bucket_mb)
+        lim = max(1, int(mb * (1 << 20) / 4))
+        cur, size = [], 0
+        for i in reversed(range(len(self.params))):
+            cur.append(i)
+            size += self.params[i].numel()
+            if size >= lim:
+                self._buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self._buckets.append(cur)
+        want = OVERLAP if overlap is None else ("1" if overlap else "0")
+        on = want == "1" or (want == "auto" and len(self._buckets) >= 2)
+        # replayed gloo steps exchange after the replay (host collectives are
+        # not captured): nothing to overlap with there
+        on = on and (not self.graphs or self._exchange_in_graph)
+        if not on:
+            self._buckets = []
+            return
+        self.overlap = True
+        self._bucket_of = {}
+        for b, idx in enumerate(self._buckets):
+            for i in idx:
+                self._bucket_of[i] = b
+        self._ranges = []
+        for idx in self._buckets:
+            lo = min(self._offsets[i] for i in idx)
+            hi = max(self._offsets[i] + self.params[i].numel() for i in idx)
+            self._ranges.append((lo, hi))
+        for i, p in enumerate(self.params):
+            p.register_post_accumulate_grad_hook(self._grad_hook(i))
+
+    def _grad_hook(self, i: int):
+        def hook(p):
+            ov = self._ov
+            if ov is None:
+                return
+            off = self._offsets[i]
+            if p.grad is None or p.grad.data_ptr() != self.flat_grad.data_ptr() + 4 * off:
+                ov["not_adopted"].add(i)
+            b = self._bucket_of[i]
+            ov["left"][b] -= 1
+            if ov["left"][b] == 0 and not ov["launched"][b]:
+                self._launch_bucket(ov, b, flush=True)
+        return hook
+
+    def _overlap_begin(self, defer: bool):
+        if not self.overlap:
+            return None
+        self._ov_works = []
+        self._ov = {"left": [len(idx) for idx in self._buckets],
+                    "launched": [False] * len(self._buckets), "works": [], "dests": [],
+                    "not_adopted": set(), "defer": defer,
+                    "main": torch.cuda.current_stream(self.device)
+                    if self.device.type == "cuda" else None}
+        return self._ov
+
+    def _launch_bucket(self, ov, b: int, flush: bool) -> None:
+        """All-reduce bucket b now: on the step's main stream, after every
+        stream that produced gradients so far (the chains' and fork's side
+        streams that are part of the step), after the deferred split
+        reductions pending so far (hlhgat reduce_flush: a deferred gradient is
+        written by a later launch on its stream), with each gradient
+        AccumulateGrad did not adopt copied into the bucket view first."""
+        ov["launched"][b] = True
+        main = ov["main"]
+        ctx = torch.cuda.stream(main) if main is not None else contextlib.nullcontext()
+        with ctx:
+            if main is not None and self._ext is not None:
+                self._ext.join_capture_streams(self._dev_index(), self._side_handles()) \
+                    if torch.cuda.is_current_stream_capturing() else self._join_sides(main)
+            if flush and ov["defer"]:
+                ov["dests"].extend(self._ext.reduce_flush(self._dev_index()))
+            deferred = set(ov["dests"])
+            base = self.flat_grad.data_ptr()
+            for i in self._buckets[b]:
+                p, off = self.params[i], self._offsets[i]
+                view = self.flat_grad[off:off + p.numel()].view_as(p)
+                g = p.grad
+                if g is not None and g.data_ptr() != base + 4 * off:
+                    if base + 4 * off not in deferred:
+                        view.copy_(g)
+                    p.grad = view
+            lo, hi = self._ranges[b]
+            ov["works"].append(dist.all_reduce(self.flat_grad[lo:hi], async_op=True))
+
+    def _side_handles(self):
+        idx = self._dev_index()
+        return [ops.side_stream(self.device, k).cuda_stream for k in (0, 1)] + \
+            [int(self._ext.fork_side_stream(idx))]
+
+    def _join_sides(self, main) -> None:
+        # eager: the main stream waits for every side stream and for the
+        # stream this hook runs on (autograd's, for the node that finished)
+        cur = torch.cuda.current_stream(self.device)
+        for h in self._side_handles():
+            main.wait_stream(torch.cuda.ExternalStream(h, device=self.device))
+        if cur.cuda_stream != main.cuda_stream:
+            main.wait_stream(cur)
 
     def _adopt_grads(self, deferred=frozenset()) -> None:
         """Every p.grad must be its flat_grad view: gradients produced outside
@@ -430,9 +577,14 @@ class TrainStep:
 
     def _exchange_and_update(self, prepared: bool = False) -> None:
         if self._exchange:
-            # one contiguous bucket; mean over ranks as DDP
-            dist.all_reduce(self.flat_grad)
-            self.flat_grad.div_(self.world)
+            if self.overlap and self._ov_works:
+                # the buckets' all-reduces were issued during the backward
+                works, self._ov_works = self._ov_works, []
+                for w in works:
+                    w.wait()
+            else:
+                dist.all_reduce(self.flat_grad)  # one contiguous bucket
+            self.flat_grad.div_(self.world)  # mean over ranks, as DDP
         self._opt_step(prepared)
 
     def _eager(self, batch) -> torch.Tensor:
@@ -773,6 +925,7 @@ class InferStep:
         self._graphs: Dict[Tuple, _Captured] = {}
         self._pool = None
         self._stream = ops.own_stream(dev, "capture") if self.graphs else None
+        self._setup_buckets(overlap, bucket_mb)
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
 
     def _forward(self, batch):

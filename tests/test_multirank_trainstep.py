@@ -73,7 +73,7 @@ def _head_shards(kind, world=2):
 
 def _loss(kind):
     F = torch.nn.functional
-    if kind == "zinc":
+    if kind.startswith("zinc"):
         import hlhgat
         crit = hlhgat.nn.L1Loss()
         return lambda out, b: crit(out.view(-1, 1), b.y.view(-1, 1))
@@ -85,7 +85,7 @@ def _loss(kind):
 def _model(kind, dev):
     import hlhgat
     torch.manual_seed(0)
-    if kind == "zinc":
+    if kind.startswith("zinc"):
         return hlhgat.HL_HGCNN_zinc_dense_int3_pyr(**ZKW).to(dev).train()
     return getattr(hlhgat, HEADCLS[kind])(**HEADKW[kind]).to(dev).train()
 
@@ -133,13 +133,18 @@ def _rank_worker(rank, world, port, q, kind, path):
     r, w, dev = init_distributed()
     shards = _load_shards(path)  # the parent's exact inputs
     model = _model(kind, dev)
-    st = TrainStep(model, _loss(kind), lr=1e-3, weight_decay=1e-3, graphs=True)
+    # zinc_overlap: eager steps (gloo's exchange cannot be captured) with the
+    # gradient all-reduce in small buckets issued from the backward's hooks
+    kw = dict(graphs=False, overlap=True, bucket_mb=0.02) if kind.endswith("_overlap") else \
+        dict(graphs=True)
+    st = TrainStep(model, _loss(kind), lr=1e-3, weight_decay=1e-3, **kw)
     losses = []
     for s in range(STEPS):
         losses.append(float(st(_to(shards[s][r], dev))))
     torch.cuda.synchronize()
     q.put((r, dict(flat=st.flat.cpu().numpy(), stats=dict(st.stats), graphs=st.graphs,
-                   graphs_off=st.graphs_off, losses=losses)))
+                   graphs_off=st.graphs_off, losses=losses, overlap=st.overlap,
+                   overlap_stats=dict(st.overlap_stats))))
     dist.destroy_process_group()
 
 
@@ -236,9 +241,9 @@ class _EmuMax(torch.autograd.Function):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["zinc", "peptides", "peptides_cfg4", "cifar"])
+@pytest.mark.parametrize("kind", ["zinc", "peptides", "peptides_cfg4", "cifar", "zinc_overlap"])
 def test_trainstep_two_ranks_bitwise_one_process(cuda, kind, tmp_path):
-    shards = _zinc_shards(2) if kind == "zinc" else _head_shards(kind, 2)
+    shards = _zinc_shards(2) if kind.startswith("zinc") else _head_shards(kind, 2)
     path = str(tmp_path / "shards.pt")
     _save_shards(shards, path)
     res = _run_ranks(_rank_worker, 2, kind, path, timeout=200)
@@ -246,6 +251,9 @@ def test_trainstep_two_ranks_bitwise_one_process(cuda, kind, tmp_path):
         st = res[r]["stats"]
         if kind == "cifar":
             assert res[r]["graphs_off"] and st["eager"] == STEPS, st
+        elif kind.endswith("_overlap"):
+            assert res[r]["overlap"] and st["eager"] == STEPS, st
+            assert res[r]["overlap_stats"]["in_backward"] >= 3 * STEPS, res[r]["overlap_stats"]
         else:
             assert res[r]["graphs"] and st["replay"] >= 2, st
     assert np.array_equal(res[0]["flat"], res[1]["flat"]), "ranks hold different parameters"

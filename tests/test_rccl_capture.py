@@ -31,7 +31,8 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["cifar_global_max", "zinc_sync_bn"])
+@pytest.mark.parametrize("case", ["cifar_global_max", "zinc_sync_bn", "zinc_overlap",
+                                  "pepfunc_overlap"])
 def test_rccl_collectives_captured_replay_equals_eager(cuda, case):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
                WORLD_SIZE="1", LOCAL_RANK="0")
@@ -48,6 +49,13 @@ def test_rccl_collectives_captured_replay_equals_eager(cuda, case):
     assert res["exchange_in_graph"] is True
     # RCCL's kernels inside the graphs (names resolved: ours are found by name)
     assert res["own_kernels_in_graphs"] > 0 and res["foreign_kernels_in_graphs"] > 0, res
+    if case.endswith("_overlap"):
+        # the gradient all-reduce in buckets issued from the backward's hooks
+        # (deferred split reductions flushed per bucket, the chains' side
+        # streams joined), captured; the same bits as the one-bucket step
+        assert res["overlap"] and res["buckets"] >= 3, res
+        assert res["overlap_stats"]["in_backward"] > 0, res
+        assert res["one_bucket_equal"], res
 
 
 def _child(case):
@@ -79,6 +87,16 @@ def _child(case):
 
         def loss(o, d):
             return F.cross_entropy(o, d[0].y.view(-1).long())
+    elif case == "pepfunc_overlap":
+        from hlhgat.synthetic import two_level_batch
+        batches = [[x.to(dev) for x in two_level_batch("peptides", 6, seed=s)] for s in (1, 2)]
+
+        def mk():
+            return hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool(
+                channels=[1, 1], filters=[32, 64], mlp_channels=[64], K=3, pool_loc=0)
+
+        def loss(o, d):
+            return F.binary_cross_entropy_with_logits(o, d[0].y.view(o.shape).float())
     else:
         from hlhgat.synthetic import zinc_like_batch
         batches = [zinc_like_batch(40, seed=3).to(dev), zinc_like_batch(33, seed=4).to(dev)]
@@ -86,25 +104,32 @@ def _child(case):
         def mk():
             m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[1, 1], filters=[32, 32],
                                                     mlp_channels=[64], K=3, keig=15)
-            return hd.convert_sync_batchnorm(m)
+            return m if case == "zinc_overlap" else hd.convert_sync_batchnorm(m)
 
         crit = torch.nn.L1Loss()
 
         def loss(o, d):
             return crit(o.view(-1, 1), d.y.view(-1, 1))
     order = [0, 1, 0, 1, 1, 0]
+    ov = case.endswith("_overlap")
+    # small buckets: several per step at these widths
+    kw = dict(overlap=True, bucket_mb=0.02) if ov else {}
     res = []
-    for graphs in (False, True):
+    for graphs, kwr in ((False, kw), (True, kw)) + (((True, dict(overlap=False)),) if ov else ()):
         torch.manual_seed(0)
         m = mk().to(dev).train()
-        st = TrainStep(m, loss, lr=1e-3, weight_decay=1e-3, graphs=graphs)
+        st = TrainStep(m, loss, lr=1e-3, weight_decay=1e-3, graphs=graphs, **kwr)
         ls = []
         for k, i in enumerate(order):
             ls.append(float(st(batches[i]).detach()))
-            note(f"graphs={graphs} step {k}: {st.stats}")
+            note(f"graphs={graphs} {kwr} step {k}: {st.stats} {st.overlap_stats}")
         torch.cuda.synchronize()
         res.append((ls, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, st))
-    (l_e, sd_e, _), (l_g, sd_g, st) = res
+    (l_e, sd_e, _), (l_g, sd_g, st) = res[:2]
+    one_equal = None
+    if ov:
+        l_1, sd_1, _ = res[2]
+        one_equal = l_1 == l_g and all(torch.equal(sd_1[k], sd_g[k]) for k in sd_g)
     # kernels in the captured step graphs that are not this library's (k_*):
     # RCCL's (and torch's few elementwise ones, which the eager step has too)
     n_coll, n_ours = 0, 0
@@ -116,7 +141,9 @@ def _child(case):
     print(json.dumps({"captures": st.stats["captures"], "replay": st.stats["replay"],
                       "exchange_in_graph": st._exchange_in_graph,
                       "foreign_kernels_in_graphs": n_coll, "own_kernels_in_graphs": n_ours,
-                      "graphs_off": st.graphs_off,
+                      "graphs_off": st.graphs_off, "overlap": st.overlap,
+                      "buckets": len(st._buckets), "overlap_stats": st.overlap_stats,
+                      "one_bucket_equal": one_equal,
                       "losses_equal": l_e == l_g, "losses": [l_e, l_g],
                       "param_diffs": [k for k in sd_e if not torch.equal(sd_e[k], sd_g[k])]}))
     dist.destroy_process_group()
