@@ -599,7 +599,12 @@ def _guarded(name, fn, *a):
         return {"error": repr(e)[:400]}
 
 
-def cifar_pipeline_leg(device, c, G, n_batches=8):
+# CUs the config-3 producer's stream may use (hipExtStreamCreateWithCUMask via
+# hlhgat_stream_create); 0 = an unmasked stream of its own
+PRODUCER_CUS = int(os.environ.get("HLHGAT_PRODUCER_CUS", "64"))
+
+
+def cifar_pipeline_leg(device, c, G, n_batches=8, producer_cus=None):
     """Config 3 WITH the reference's per-sample work (its Dataset.get() runs
     every epoch in num_workers DataLoader processes beside training,
     main_cifar10SP...:67-125,214): hlhgat.pipeline.SuperpixelPipeline builds
@@ -609,7 +614,11 @@ def cifar_pipeline_leg(device, c, G, n_batches=8):
     stream, pads both levels to one capacity bucket (pad_levels on the
     device), and hands it over; the training step replays ONE captured graph
     for every batch (TrainStep) while the next batch is built.
-    Reported: the overlapped rate, and the pipeline alone / the serial sum."""
+    Reported: the overlapped rate, and the pipeline alone / the serial sum.
+    The producer's stream runs on `producer_cus` CUs only (a CU-masked stream,
+    the highest-numbered CUs), so the step's kernels keep the rest of the chip
+    and its one-launch BatchNorm grids (<= half the chip's capacity) fit
+    beside it; 0 = unmasked."""
     import queue
     import threading
     import hlhgat
@@ -635,8 +644,15 @@ def cifar_pipeline_leg(device, c, G, n_batches=8):
     st = TrainStep(m, lambda o, d: _head_loss("cifar", o, d), lr=1e-3, graphs=True)
     main = torch.cuda.current_stream(device)
 
+    from hlhgat import ops
+    cus = PRODUCER_CUS if producer_cus is None else int(producer_cus)
+    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
+    cus = min(max(cus, 0), n_cu)
+    mask = ops.cu_mask_high(cus, n_cu) if 0 < cus < n_cu else None
+    # a stream of the library's own (never one of torch's round-robin pool)
+    s = ops.own_stream(device, f"producer{cus if mask else ''}", cu_mask=mask)
+
     def produce(q, seeds):
-        s = torch.cuda.Stream(device=device)
         with torch.cuda.stream(s):
             for k, b in enumerate(seeds):
                 datas = fit(pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device))
@@ -668,11 +684,22 @@ def cifar_pipeline_leg(device, c, G, n_batches=8):
         st(fit(pipe.batch(range(b * G, (b + 1) * G), seed=b, device=device)))
     torch.cuda.synchronize()
     n_cap = st.stats["captures"]
+    h0 = ops.bn_giveups()["count"]
     t0 = time.perf_counter()
     nb = run(list(range(n_batches)))
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    handovers = ops.bn_giveups()["count"] - h0
     assert st.stats["captures"] == n_cap, "a timed batch left the capacity bucket"
+    # the replayed step alone, same graph and batch buffers (no producer)
+    last = fit(pipe.batch(range(0, G), seed=0, device=device))
+    st(last)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for _ in range(n_batches):
+        st(last)
+    torch.cuda.synchronize()
+    t_step = (time.perf_counter() - t2) / n_batches
     # the pipeline alone (same producer, no training)
     t1 = time.perf_counter()
     for b in range(n_batches):
@@ -681,6 +708,9 @@ def cifar_pipeline_leg(device, c, G, n_batches=8):
     t_pipe = time.perf_counter() - t1
     return {"value": round(nb * G / dt, 1), "unit": "graphs/s",
             "ms_per_batch": round(dt / nb * 1e3, 2),
+            "step_alone_ms": round(t_step * 1e3, 2),
+            "ratio_to_step": round((dt / nb) / t_step, 3),
+            "producer_cus": cus if mask else n_cu, "bn_handovers": handovers,
             "pipeline_graphs_per_s": round(n_batches * G / t_pipe, 1),
             "pipeline_ms_per_batch": round(t_pipe / n_batches * 1e3, 1),
             "captures": st.stats["captures"], "replays": st.stats["replay"],

@@ -126,6 +126,16 @@ def own_stream(device, role: str, cu_mask=None) -> torch.cuda.Stream:
     return s
 
 
+def cu_mask_high(n_on: int, n_cu: int):
+    """A CU mask (32-bit words covering n_cu CUs) with the n_on
+    highest-numbered CUs set."""
+    words = (n_cu + 31) // 32
+    mask = [0] * words
+    for c in range(n_cu - n_on, n_cu):
+        mask[c // 32] |= 1 << (c % 32)
+    return mask
+
+
 def stream_cu_mask(stream, words: int = 8):
     """The CU mask `stream` runs on (a list of 32-bit words)."""
     import ctypes

@@ -1,7 +1,10 @@
 """The config-3 overlapped pipeline leg of bench.py on its own
 (bench.cifar_pipeline_leg), with the replayed step alone beside it.
 
-    python tools/probes/cfg3_pipe.py [--batches 8]
+    python tools/probes/cfg3_pipe.py [--batches 8] [--cus 0,32,64,128]
+
+One leg per CU count of the producer's stream (0 = unmasked), interleaved
+--rounds times.
 """
 import argparse
 import json
@@ -20,16 +23,23 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=8)
+    ap.add_argument("--cus", default="")
+    ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
     c = bench.HEADS["cfg3_cifar_attpool"]
-    t = time.perf_counter()
-    r = bench.cifar_pipeline_leg(dev, c, c["graphs"], n_batches=args.batches)
-    r.pop("caps", None)
-    r.pop("what", None)
-    r["wall_s"] = round(time.perf_counter() - t, 1)
-    print(json.dumps(r))
+    cus = [int(v) for v in args.cus.split(",")] if args.cus else [None]
+    for rnd in range(args.rounds):
+        for n in cus:
+            t = time.perf_counter()
+            r = bench.cifar_pipeline_leg(dev, c, c["graphs"], n_batches=args.batches,
+                                         producer_cus=n)
+            r.pop("caps", None)
+            r.pop("what", None)
+            r["wall_s"] = round(time.perf_counter() - t, 1)
+            r["round"] = rnd
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
