@@ -548,10 +548,13 @@ def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tens
                 raise RuntimeError(f"hlhgat: hodge_build sizes {tuple(sizes)} != device {got}")
     else:
         nnz0, nnz1 = int(rp0[-1].item()), int(rp1[-1].item())
-    c0 = torch.empty(max(nnz0, 1), dtype=torch.int32, device=dev)
-    v0 = torch.empty(max(nnz0, 1), dtype=torch.float32, device=dev)
-    c1 = torch.empty(max(nnz1, 1), dtype=torch.int32, device=dev)
-    v1 = torch.empty(max(nnz1, 1), dtype=torch.float32, device=dev)
+    # caller's sizes: zero-filled, so entries past the device's rows (sizes
+    # too large: HLHGAT_DEVERR_HODGE_SIZE) hold in-range column 0, never garbage
+    alloc = torch.empty if sizes is None else torch.zeros
+    c0 = alloc(max(nnz0, 1), dtype=torch.int32, device=dev)
+    v0 = alloc(max(nnz0, 1), dtype=torch.float32, device=dev)
+    c1 = alloc(max(nnz1, 1), dtype=torch.int32, device=dev)
+    v1 = alloc(max(nnz1, 1), dtype=torch.float32, device=dev)
     # the kernels check every row against these capacities (a caller's sizes
     # that do not fit the graph raise HLHGAT_DEVERR_HODGE_SIZE, nothing past
     # the buffers is written)
@@ -562,10 +565,18 @@ def hodge_build(edge_index: torch.Tensor, node_counts, lmax: Optional[torch.Tens
                                  nnz1, st), "hodge_build")
 
     def coo(rp, c, v, n, nnz):
-        if sizes is not None:  # row pointers past a caller's nnz: clamped, never written past
+        if sizes is not None:
+            # a caller's nnz may not match the device's rows (then the build
+            # raised HLHGAT_DEVERR_HODGE_SIZE): the row of entry k by binary
+            # search over the clamped row pointers -- repeat_interleave with an
+            # output_size other than the sum of the repeats trips torch's
+            # device-side assert, a GPU exception that ends the process's context
             rp = rp.clamp(max=nnz)
-        rows = torch.repeat_interleave(torch.arange(n, device=dev), (rp[1:] - rp[:-1]).long(),
-                                       output_size=nnz)
+            k = torch.arange(nnz, device=dev, dtype=torch.int32)
+            rows = torch.searchsorted(rp[1:], k, right=True).clamp_(max=max(n - 1, 0))
+        else:
+            rows = torch.repeat_interleave(torch.arange(n, device=dev), (rp[1:] - rp[:-1]).long(),
+                                           output_size=nnz)
         return torch.stack([rows, c[:nnz].long()]), v[:nnz]
 
     ei_t, w_t = coo(rp0, c0, v0, N, nnz0)

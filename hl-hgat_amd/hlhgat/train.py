@@ -925,7 +925,6 @@ class InferStep:
         self._graphs: Dict[Tuple, _Captured] = {}
         self._pool = None
         self._stream = ops.own_stream(dev, "capture") if self.graphs else None
-        self._setup_buckets(overlap, bucket_mb)
         self.stats = {"eager": 0, "replay": 0, "captures": 0}
 
     def _forward(self, batch):
