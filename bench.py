@@ -601,10 +601,13 @@ def _guarded(name, fn, *a):
 
 # CUs the config-3 producer's stream may use (hipExtStreamCreateWithCUMask via
 # hlhgat_stream_create); 0 = an unmasked stream of its own
-PRODUCER_CUS = int(os.environ.get("HLHGAT_PRODUCER_CUS", "64"))
+PRODUCER_CUS = int(os.environ.get("HLHGAT_PRODUCER_CUS", "0"))
+# the producer stream's HIP priority: "low" (the device's least priority),
+# "high", or "0" (default)
+PRODUCER_PRIO = os.environ.get("HLHGAT_PRODUCER_PRIO", "0")
 
 
-def cifar_pipeline_leg(device, c, G, n_batches=8, producer_cus=None):
+def cifar_pipeline_leg(device, c, G, n_batches=8, producer_cus=None, producer_prio=None):
     """Config 3 WITH the reference's per-sample work (its Dataset.get() runs
     every epoch in num_workers DataLoader processes beside training,
     main_cifar10SP...:67-125,214): hlhgat.pipeline.SuperpixelPipeline builds
@@ -649,8 +652,12 @@ def cifar_pipeline_leg(device, c, G, n_batches=8, producer_cus=None):
     n_cu = torch.cuda.get_device_properties(device).multi_processor_count
     cus = min(max(cus, 0), n_cu)
     mask = ops.cu_mask_high(cus, n_cu) if 0 < cus < n_cu else None
+    pr = PRODUCER_PRIO if producer_prio is None else str(producer_prio)
+    least, greatest = torch.cuda.Stream.priority_range()
+    prio = {"low": least, "high": greatest}.get(pr, 0) if mask is None else 0
     # a stream of the library's own (never one of torch's round-robin pool)
-    s = ops.own_stream(device, f"producer{cus if mask else ''}", cu_mask=mask)
+    s = ops.own_stream(device, f"producer{cus if mask else ''}p{prio}", cu_mask=mask,
+                       priority=prio)
 
     def produce(q, seeds):
         with torch.cuda.stream(s):
@@ -710,7 +717,8 @@ def cifar_pipeline_leg(device, c, G, n_batches=8, producer_cus=None):
             "ms_per_batch": round(dt / nb * 1e3, 2),
             "step_alone_ms": round(t_step * 1e3, 2),
             "ratio_to_step": round((dt / nb) / t_step, 3),
-            "producer_cus": cus if mask else n_cu, "bn_handovers": handovers,
+            "producer_cus": cus if mask else n_cu, "producer_priority": prio,
+            "bn_handovers": handovers,
             "pipeline_graphs_per_s": round(n_batches * G / t_pipe, 1),
             "pipeline_ms_per_batch": round(t_pipe / n_batches * 1e3, 1),
             "captures": st.stats["captures"], "replays": st.stats["replay"],

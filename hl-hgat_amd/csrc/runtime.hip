@@ -104,10 +104,11 @@ extern "C" int hlhgat_clear_device_errors(void) {
 
 extern "C" const char* hlhgat_last_error(void) { return g_last_error.c_str(); }
 
-extern "C" int hlhgat_stream_create(int device, unsigned flags, const uint32_t* cu_mask,
-                                    int cu_mask_words, void** out) {
-  HLH_CHECK_ARG(out && device >= 0 && cu_mask_words >= 0 && (cu_mask_words == 0 || cu_mask),
-                "stream_create: bad arguments");
+extern "C" int hlhgat_stream_create(int device, unsigned flags, int priority,
+                                    const uint32_t* cu_mask, int cu_mask_words, void** out) {
+  HLH_CHECK_ARG(out && device >= 0 && cu_mask_words >= 0 && (cu_mask_words == 0 || cu_mask) &&
+                    (cu_mask_words == 0 || priority == 0),
+                "stream_create: bad arguments (a CU-masked stream has the default priority)");
   int prev = 0;
   HLH_CHECK_HIP(hipGetDevice(&prev));
   HLH_CHECK_HIP(hipSetDevice(device));
@@ -126,6 +127,8 @@ extern "C" int hlhgat_stream_create(int device, unsigned flags, const uint32_t* 
     if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&s, (uint32_t)cu_mask_words, cu_mask);
     // (a CU-masked stream is blocking w.r.t. the null stream; the library's
     // streams only ever synchronise through events)
+  } else if (priority != 0) {
+    e = hipStreamCreateWithPriority(&s, flags, priority);
   } else {
     e = hipStreamCreateWithFlags(&s, flags);
   }

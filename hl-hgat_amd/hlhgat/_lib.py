@@ -101,7 +101,7 @@ SIGNATURES = {
     "hlhgat_bn_giveup_reset": (c_i32, []),
     "hlhgat_test_occupy": (c_i32, [c_i32, c_i32, c_i32, C.c_uint32, c_vp]),
     "hlhgat_device_errors": (c_i32, [c_vp]),
-    "hlhgat_stream_create": (c_i32, [c_i32, C.c_uint32, c_vp, c_i32, c_vp]),
+    "hlhgat_stream_create": (c_i32, [c_i32, C.c_uint32, c_i32, c_vp, c_i32, c_vp]),
     "hlhgat_stream_cu_mask": (c_i32, [c_vp, c_vp, c_i32]),
     "hlhgat_clear_device_errors": (c_i32, []),
     "hlhgat_bn_wait_timeouts": (c_i32, [c_vp]),

@@ -99,7 +99,7 @@ def set_stream_fork(enabled: bool) -> None:
 _OWN_STREAMS = {}
 
 
-def own_stream(device, role: str, cu_mask=None) -> torch.cuda.Stream:
+def own_stream(device, role: str, cu_mask=None, priority: int = 0) -> torch.cuda.Stream:
     """A HIP stream of this library's own for `role` on `device` (created
     once, non-blocking, never from torch's stream pool).  torch.cuda.Stream()
     hands out its 32 pool streams round-robin, so two unrelated users can get
@@ -108,7 +108,8 @@ def own_stream(device, role: str, cu_mask=None) -> torch.cuda.Stream:
     copy and side streams of TrainStep / StagedFeed / the chains are these.
     Created by libhlhgat (hlhgat_stream_create), i.e. by the HIP runtime torch
     loaded.  cu_mask (a list of 32-bit words, bit c = CU c): the stream runs on
-    those CUs only (the first call for a role fixes its mask)."""
+    those CUs only (the first call for a role fixes its mask); priority: HIP
+    stream priority (lower = higher; 0 = default)."""
     idx = device.index if getattr(device, "index", None) is not None else (
         device if isinstance(device, int) else torch.cuda.current_device())
     s = _OWN_STREAMS.get((idx, role))
@@ -117,10 +118,11 @@ def own_stream(device, role: str, cu_mask=None) -> torch.cuda.Stream:
         h = ctypes.c_void_p()
         if cu_mask:
             words = (ctypes.c_uint32 * len(cu_mask))(*[int(w) & 0xffffffff for w in cu_mask])
-            check(LIB.hlhgat_stream_create(idx, 1, words, len(cu_mask), ctypes.byref(h)),
+            check(LIB.hlhgat_stream_create(idx, 1, 0, words, len(cu_mask), ctypes.byref(h)),
                   "stream_create")
         else:
-            check(LIB.hlhgat_stream_create(idx, 1, None, 0, ctypes.byref(h)), "stream_create")
+            check(LIB.hlhgat_stream_create(idx, 1, int(priority), None, 0, ctypes.byref(h)),
+                  "stream_create")
         s = torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
         _OWN_STREAMS[(idx, role)] = s
     return s

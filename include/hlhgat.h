@@ -792,10 +792,11 @@ int hlhgat_clear_device_errors(void);
  * c of word c/32 = CU c; the words must cover every CU of the device) -- the
  * config-3 per-sample producer's stream (hlhgat.pipeline), so the replayed
  * step keeps the other CUs.  flags: hipStreamNonBlocking (1) etc., unmasked
- * streams only.  The reference has no streams (one implicit CUDA stream,
+ * streams only; priority != 0: hipStreamCreateWithPriority (lower = higher
+ * priority, hipDeviceGetStreamPriorityRange), unmasked streams only.  The reference has no streams (one implicit CUDA stream,
  * main_*.py); these are plumbing of the drop-in's own training loop. */
-int hlhgat_stream_create(int device, unsigned flags, const uint32_t* cu_mask, int cu_mask_words,
-                         void** out);
+int hlhgat_stream_create(int device, unsigned flags, int priority, const uint32_t* cu_mask,
+                         int cu_mask_words, void** out);
 /* The CU mask a stream runs on (hipExtStreamGetCUMask): all ones for an
  * unmasked stream. */
 int hlhgat_stream_cu_mask(void* stream, uint32_t* cu_mask, int cu_mask_words);

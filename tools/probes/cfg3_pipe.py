@@ -25,16 +25,18 @@ def main():
     ap.add_argument("--batches", type=int, default=8)
     ap.add_argument("--cus", default="")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--prio", default="", help="comma list of low / high / 0 (unmasked only)")
     args = ap.parse_args()
     import bench
     dev = torch.device("cuda:0")
     c = bench.HEADS["cfg3_cifar_attpool"]
-    cus = [int(v) for v in args.cus.split(",")] if args.cus else [None]
+    legs = [(int(v), None) for v in args.cus.split(",")] if args.cus else []
+    legs += [(0, p) for p in args.prio.split(",")] if args.prio else []
     for rnd in range(args.rounds):
-        for n in cus:
+        for n, pr in legs or [(None, None)]:
             t = time.perf_counter()
             r = bench.cifar_pipeline_leg(dev, c, c["graphs"], n_batches=args.batches,
-                                         producer_cus=n)
+                                         producer_cus=n, producer_prio=pr)
             r.pop("caps", None)
             r.pop("what", None)
             r["wall_s"] = round(time.perf_counter() - t, 1)
