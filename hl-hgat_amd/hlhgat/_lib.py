@@ -92,6 +92,7 @@ SIGNATURES = {
     "hlhgat_set_proj_bn_fused": (c_i32, [c_i32]),
     "hlhgat_set_proj_bn_split": (c_i32, [c_i32]),
     "hlhgat_set_proj_bwd_rows": (c_i32, [c_i32]),
+    "hlhgat_set_wgrad_stages": (c_i32, [c_i32]),
     "hlhgat_set_gemm_big": (c_i32, [c_i32, c_i64]),
     "hlhgat_proj_bn_fused_capacity": (c_i32, [P_i64]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),

@@ -626,6 +626,12 @@ int hlhgat_set_gemm_big(int mode, int64_t min_m);
  * data-gradient workgroup per (row block, 64-column tile) instead of one per
  * row block covering every column tile (N <= 64); bitwise the same (tests). */
 int hlhgat_set_proj_bwd_rows(int on);
+/* Weight-gradient items of the Linear backward (hlhgat_proj_bwd*,
+ * hlhgat_proj_bwd_weight): 0 = chunks staged through a two-deep register
+ * ring, 3..6 = staged by LDS-DMA (buffer_load ... lds) into a ring of that
+ * many chunks.  Bitwise the same gradients either way.  Env
+ * HLHGAT_WGRAD_STAGES sets the process default. */
+int hlhgat_set_wgrad_stages(int stages);
 /* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
 int hlhgat_set_proj_bn_fused(int on);
 /* 1: hlhgat_proj_bn_fwd's fused path as two launches -- the projection with

@@ -1753,3 +1753,49 @@ def test_proj_bn_split_bitwise(cuda, M, N, kb, pad):
                                 bn.num_batches_tracked.clone()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M", [37, 5000, 70000])
+@pytest.mark.parametrize("widths,N", [([64, 128, 8], 96), ([64, 64, 64], 64), ([36, 36], 32),
+                                      ([200], 256)])
+def test_wgrad_dma_ring_bitwise(cuda, M, widths, N):
+    """The weight-gradient items staged by LDS-DMA into a 3..6-deep ring
+    (hlhgat_set_wgrad_stages) give the bits of the register ring: the fused
+    Linear backward (weight, bias and data gradients) and the standalone
+    weight gradient, ragged M (rows past a slice read as zeros through the
+    buffer descriptor), widths not a multiple of the 64-column tile, one to
+    three input blocks; both against torch."""
+    from hlhgat import _lib, ops
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    blocks = [torch.randn(M, k, generator=g).to(cuda) for k in widths]
+    W = torch.randn(N, sum(widths), generator=g).to(cuda) * 0.1
+    b = torch.randn(N, generator=g).to(cuda)
+    R = torch.randn(M, N, generator=g).to(cuda)
+
+    def run():
+        xs = [t.clone().requires_grad_(True) for t in blocks]
+        Wv, bv = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        (ops.linear_blocks(xs, Wv, bv) * R).sum().backward()
+        dW = torch.empty_like(W)
+        dWs, o = [], 0
+        for k in widths:
+            dWs.append(dW[:, o:o + k])
+            o += k
+        db = torch.empty(N, device=cuda)
+        ops._proj_bwd_weight(R, blocks, dWs, db)
+        return [Wv.grad, bv.grad] + [x.grad for x in xs] + [dW, db]
+    res = {}
+    for st in (0, 3, 4, 6):
+        _lib.check(_lib.LIB.hlhgat_set_wgrad_stages(st), "set_wgrad_stages")
+        try:
+            res[st] = run()
+        finally:
+            _lib.LIB.hlhgat_set_wgrad_stages(0)
+    torch.cuda.synchronize()
+    for st in (3, 4, 6):
+        for i, (u, v) in enumerate(zip(res[0], res[st])):
+            assert torch.equal(u, v), (st, i)
+    ref = [R.t() @ torch.cat(blocks, 1), R.sum(0)]
+    close(res[0][0].cpu(), ref[0].cpu(), 1e-4, "dW vs torch")
+    close(res[0][1].cpu(), ref[1].cpu(), 1e-4, "db vs torch")
+    close(res[0][-2].cpu(), ref[0].cpu(), 1e-4, "standalone dW vs torch")

@@ -31,6 +31,7 @@ for s in "$@"; do
   case $s in
     sel) step sel 600 $PT tests -m gpu -v -k "$SEL" ;;  # SEL="expr" tools/gpu_steps.sh TAG sel
     cfg3pipe) step cfg3pipe 600 python tools/probes/cfg3_pipe.py --cus "${CUS-0,32,64,128}" --prio "${PRIO-}" --rounds 2 ;;
+    wgrad) step wgrad 600 python tools/wgrad_bench.py --stages "${STAGES:-0,3,4,5,6}" ;;
     quick) step quick 300 python bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-replay-census --no-loader --steps 30 ;;
     bn) step bn 600 $PT tests/test_gpu_parity.py -m gpu -v -s -k "bn_ or proj_bn or handover or hog" ;;
     tests) step tests 1100 $PT tests -m gpu -q ;;
