@@ -51,6 +51,10 @@ SIGNATURES = {
                                  c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                       c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
+    "hlhgat_poly_basis_fwd_local": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                            c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
+    "hlhgat_poly_basis_bwd_local": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                            c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                       c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_hodge_factor_work_floats": (c_i64, [c_i64, c_i64]),
