@@ -279,8 +279,35 @@ struct LocalArgs {
   LocalStep st[kLocalMaxSteps];
 };
 
+// One step's row whose CSR entries (<= LPR of them) are already in the row
+// group's lanes (cm, wm: entry e0 + sub): the gathers of k_poly_step's first
+// staged chunk, without its rowptr / col / val loads -- the operator is the
+// same for every step, so k_poly_local loads them once.  Same sums (CSR
+// order from 0) and epilogue as poly_row_body: the same bits.
 template <int V, int LPR>
-__global__ __launch_bounds__(256) void k_poly_local(LocalArgs a) {
+__device__ __forceinline__ void local_row_cached(const PolyArgs& a, int64_t row, bool live,
+                                                 int sub, int cnt, int cm, float wm) {
+  using vt = typename VecT<V>::type;
+  for (int f0 = 0; f0 < a.d; f0 += LPR * V) {
+    const int f = f0 + sub * V;
+    const bool fok = live && f < a.d;
+    vt acc;
+#pragma unroll
+    for (int i = 0; i < V; ++i) vget(acc, i) = 0.f;
+    if (cnt <= 8) {
+      gather_batch<V, 8, LPR>(a.X, a.ldx, f, fok, cm, wm, 0, cnt, acc);
+    } else {
+      int j = 0;
+      for (; j + 3 < cnt; j += 4) gather_batch<V, 4, LPR>(a.X, a.ldx, f, fok, cm, wm, j, 4, acc);
+      if (j < cnt) gather_batch<V, 3, LPR>(a.X, a.ldx, f, fok, cm, wm, j, cnt - j, acc);
+    }
+    if (!fok) continue;
+    poly_epilogue<V>(a, row, f, acc, 1.f);
+  }
+}
+
+template <int V, int LPR, int NT>
+__global__ __launch_bounds__(NT) void k_poly_local(LocalArgs a) {
   const int64_t wg = blockIdx.x;
   int64_t r0, r1;
   if (wg < a.n_seg) {
@@ -293,8 +320,18 @@ __global__ __launch_bounds__(256) void k_poly_local(LocalArgs a) {
   }
   if (r1 > a.n_rows) r1 = a.n_rows;
   if (r0 > r1) r0 = r1;
-  constexpr int RG = 256 / LPR;
+  constexpr int RG = NT / LPR;
   const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+  // a graph that fits one pass with rows of <= LPR entries (every ZINC row):
+  // its CSR row is loaded once, into the row group's lanes, for all steps
+  const int64_t crow = r0 + grp;
+  const bool one_pass = r1 - r0 <= RG;
+  const bool clive = one_pass && crow < r1;
+  const int ce0 = clive ? a.rowptr[crow] : 0;
+  const int ccnt = clive ? a.rowptr[crow + 1] - ce0 : 0;
+  const bool cached = ccnt <= LPR;  // uniform in the row group
+  const int cm = (clive && sub < ccnt) ? a.col[ce0 + sub] : 0;
+  const float wm = (clive && sub < ccnt) ? (a.val ? a.val[ce0 + sub] : 1.f) : 0.f;
   PolyArgs p{};
   p.rowptr = a.rowptr;
   p.col = a.col;
@@ -321,10 +358,14 @@ __global__ __launch_bounds__(256) void k_poly_local(LocalArgs a) {
     p.div = t.div;
     p.p = t.p;
     p.q = t.q;
-    for (int64_t rb = r0; rb < r1; rb += RG) {
-      const int64_t row = rb + grp;
-      const bool live = row < r1;
-      poly_row_body<V, LPR, 4>(p, live ? row : 0, live, sub);
+    if (one_pass && cached) {
+      local_row_cached<V, LPR>(p, clive ? crow : 0, clive, sub, ccnt, cm, wm);
+    } else {
+      for (int64_t rb = r0; rb < r1; rb += RG) {
+        const int64_t row = rb + grp;
+        const bool live = row < r1;
+        poly_row_body<V, LPR, 4>(p, live ? row : 0, live, sub);
+      }
     }
     __syncthreads();  // this step's rows are the next step's gathered operand
   }
@@ -1112,9 +1153,11 @@ int launch_local(LocalArgs& L, int64_t nnz, hipStream_t s) {
   }
   const int v = pick_vec_of(L.d, lds, ptrs);
   const int l = pick_lpr(L.d, v);
-  // padding rows: ~ one tenth of the rows in workgroups of 4 row passes (the
-  // last one takes whatever is left)
-  L.tail_rows = 4 * (256 / l);
+  // workgroup: 64 rows per pass (a ZINC graph in one pass), 256..1024 threads
+  const int nt = l * 64 <= 256 ? 256 : (l * 64 >= 1024 ? 1024 : l * 64);
+  // padding rows: ~ one tenth of the rows in workgroups of one row pass each
+  // (the last one takes whatever is left)
+  L.tail_rows = nt / l;
   L.tail_wgs = (int)std::max<int64_t>(1, ceil_div(std::max<int64_t>(L.n_rows / 10, 1), L.tail_rows));
   const int64_t grid = L.n_seg + L.tail_wgs;
   HLH_CHECK_ARG(grid < (int64_t)INT32_MAX, "poly_basis_local: too many graphs");
@@ -1132,8 +1175,15 @@ int launch_local(LocalArgs& L, int64_t nnz, hipStream_t s) {
   ProfScope prof(HLHGAT_PROF_POLY, s, b, 2.0 * (double)nnz * L.d * L.n_steps);
   const unsigned g = (unsigned)grid;
   switch (v * 100 + l) {
-#define HLH_LOCAL_CASE(VV, LL) \
-  case VV * 100 + LL: launch(k_poly_local<VV, LL>, g, 256, 0, s, &prof, L); break;
+#define HLH_LOCAL_CASE(VV, LL)                                                          \
+  case VV * 100 + LL:                                                                   \
+    if (nt == 256)                                                                      \
+      launch(k_poly_local<VV, LL, 256>, g, 256, 0, s, &prof, L);                        \
+    else if (nt == 512)                                                                 \
+      launch(k_poly_local<VV, LL, 512>, g, 512, 0, s, &prof, L);                        \
+    else                                                                                \
+      launch(k_poly_local<VV, LL, 1024>, g, 1024, 0, s, &prof, L);                      \
+    break;
     HLH_LOCAL_CASE(1, 1) HLH_LOCAL_CASE(1, 2) HLH_LOCAL_CASE(1, 4) HLH_LOCAL_CASE(1, 8)
     HLH_LOCAL_CASE(1, 16) HLH_LOCAL_CASE(1, 32) HLH_LOCAL_CASE(1, 64)
     HLH_LOCAL_CASE(2, 1) HLH_LOCAL_CASE(2, 2) HLH_LOCAL_CASE(2, 4) HLH_LOCAL_CASE(2, 8)
