@@ -1154,7 +1154,11 @@ int launch_local(LocalArgs& L, int64_t nnz, hipStream_t s) {
   const int v = pick_vec_of(L.d, lds, ptrs);
   const int l = pick_lpr(L.d, v);
   // workgroup: 64 rows per pass (a ZINC graph in one pass), 256..1024 threads
-  const int nt = l * 64 <= 256 ? 256 : (l * 64 >= 1024 ? 1024 : l * 64);
+  int nt = l * 64 <= 256 ? 256 : (l * 64 >= 1024 ? 1024 : l * 64);
+  if (const char* e = std::getenv("HLHGAT_LOCAL_NT")) {  // A/B: 256 / 512 / 1024
+    const int v_nt = std::atoi(e);
+    if (v_nt == 256 || v_nt == 512 || v_nt == 1024) nt = v_nt;
+  }
   // padding rows: ~ one tenth of the rows in workgroups of one row pass each
   // (the last one takes whatever is left)
   L.tail_rows = nt / l;
