@@ -170,8 +170,8 @@ class _PyrHead(nn.Module):
         # cross-block edge chain made hipStreamEndCapture segfault under RCCL,
         # while per-block fork / join captured bitwise the same step,
         # tools/probes/syncbn_capture_probe.py)
-        chains = (ops.Chains(x_t.device, enabled=not ops.has_sync_bn(self)) if dense
-                  else contextlib.nullcontext())
+        chains = (ops.Chains(x_t.device, enabled=not ops.has_sync_bn(self) or ops.SYNCBN_CHAINS)
+                  if dense else contextlib.nullcontext())
         with chains as ch:
             x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
                                          edge_weight_s)

@@ -203,7 +203,7 @@ for s in "$@"; do
            HLHGAT_WEIGHT_STREAM=$w HLHGAT_WEIGHT_STREAM_HI=$h step abwshi_${w}_${h}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abwshi_${w}_${h}_$r.log | sed "s/^/weight_stream=$w high_prio=$h run $r /" >> gpurun_out/${TAG}_abwshi.txt || true
          done; done ;;
-    syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ;;
+    syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ${PROBE:-} ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
     grad) step grad 900 $PT tests/test_frozen_mask_grads.py -m gpu -v -s ;;

@@ -9,6 +9,11 @@ one-rank nccl group, collectives executed) with one thing changed:
   fwdonly     the backward's statistics all-reduce skipped (one rank: the
               same sums), so only the forward's collectives are captured
   bwdonly     the forward's skipped instead
+  chains      the persistent chains forced on (ops.SYNCBN_CHAINS), all-reduce
+              on the layer's stream (the round-5 crash)
+  chains_own  chains forced on, every statistics all-reduce issued from one
+              dedicated collective stream (ops.SYNC_BN_STREAM = "own")
+  nochains_own  per-block fork / join, the dedicated collective stream
 
     python tools/probes/syncbn_capture_probe.py [variant ...]
 """
@@ -31,6 +36,10 @@ def _port():
 def child(variant):
     sys.path[:0] = [os.path.join(REPO, "tests"), REPO, os.path.join(REPO, "hl-hgat_amd")]
     from hlhgat import ops
+    if variant.startswith("chains"):
+        ops.SYNCBN_CHAINS = True
+    if variant.endswith("_own"):
+        ops.SYNC_BN_STREAM = "own"
     if variant == "nofork":
         ops.set_stream_fork(False)
     elif variant == "nochains":
