@@ -14,7 +14,6 @@
 #include "common.h"
 
 #include <cstdlib>
-#include <vector>
 
 using namespace hlhgat;
 
@@ -143,12 +142,17 @@ __device__ __forceinline__ void gather_batch(const float* __restrict__ X, int64_
 // row) and the < 4 entries after the 4-batches go as one gather_batch
 // (same-process A/B at the cfg2 step: +0.3-0.6 %; the L0 Laguerre step
 // 5.95 -> 5.6 us in a chain, profiles/r03_l_ab_poly_batch.txt).
-// One output row per group of LPR lanes (`live` false: the group only takes
-// part in its shuffles).  Shared by k_poly_step and k_poly_local.
 template <int V, int LPR, int DEPTH>
-__device__ __forceinline__ void poly_row_body(const PolyArgs& a, int64_t row, bool live,
-                                              int sub) {
+__device__ __forceinline__ void poly_step_body(const PolyArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
+  // XCD-aware slots: blocks are dealt round-robin over the 8 XCDs, so block b
+  // takes slot range xcd_slot(b): each XCD walks ONE contiguous range of the
+  // (optionally locality-ordered) row schedule and its L2 sees the neighbours
+  // of the rows it is working on.
+  const int64_t slot = ((int64_t)xcd_slot(blk.x, blk.gx) * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  const bool live = slot < a.n_rows;
+  const int64_t row = live ? (a.order ? (int64_t)a.order[slot] : slot) : 0;
   const int64_t rr = row;
   const int e0 = live ? a.rowptr[rr] : 0;
   const int e1 = live ? a.rowptr[rr + 1] : 0;
@@ -221,19 +225,6 @@ __device__ __forceinline__ void poly_row_body(const PolyArgs& a, int64_t row, bo
   }
 }
 
-template <int V, int LPR, int DEPTH>
-__device__ __forceinline__ void poly_step_body(const PolyArgs& a, Blk blk) {
-  // XCD-aware slots: blocks are dealt round-robin over the 8 XCDs, so block b
-  // takes slot range xcd_slot(b): each XCD walks ONE contiguous range of the
-  // (optionally locality-ordered) row schedule and its L2 sees the neighbours
-  // of the rows it is working on.
-  const int64_t slot = ((int64_t)xcd_slot(blk.x, blk.gx) * 256 + threadIdx.x) / LPR;
-  const int sub = threadIdx.x % LPR;
-  const bool live = slot < a.n_rows;
-  const int64_t row = live ? (a.order ? (int64_t)a.order[slot] : slot) : 0;
-  poly_row_body<V, LPR, DEPTH>(a, row, live, sub);
-}
-
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
   poly_step_body<V, LPR, 4>(a, blk_hw());
@@ -242,133 +233,6 @@ __global__ __launch_bounds__(256) void k_poly_step(PolyArgs a) {
 template <int V, int LPR>
 __global__ __launch_bounds__(256) void k_poly_step_deep(PolyArgs a) {
   poly_step_body<V, LPR, 8>(a, blk_hw());
-}
-
-// ---------------------------------------------------------------------------
-// The whole polynomial basis (or its adjoint) of a block-diagonal operator in
-// ONE launch: one workgroup per graph (PairData batching keeps a graph's rows
-// contiguous and its Laplacian entries inside them, lib/Hodge_Dataset.py:
-// 40-48), which runs the K-1 recurrence steps over its own rows with a
-// workgroup barrier between steps -- step k+1 only gathers rows of step k's
-// output that the same workgroup wrote.  Rows past the last graph (static-
-// shape padding: isolated rows) go to `tail_wgs` extra workgroups.  Each
-// row of each step is poly_row_body, the per-row code of k_poly_step: the
-// results are bitwise those of the K-1 chained launches.  At the ZINC shape
-// a Laguerre step is ~18 MB and ~6.8 us, launch-bound; this removes K-2
-// dependent launches per basis (forward and adjoint) and the intermediate
-// terms are re-read from L2 while still resident.
-// ---------------------------------------------------------------------------
-struct LocalStep {
-  const float* X;
-  const float* B;
-  const float* Z;
-  const float* P;
-  const float* Q;
-  float* Y;
-  int64_t ldx, ldb, ldz, ldp, ldq, ldy;
-  float alpha, beta, gamma, div, p, q;
-};
-constexpr int kLocalMaxSteps = 5;  // K <= 6 (the configs' largest K)
-struct LocalArgs {
-  const int32_t* rowptr;
-  const int32_t* col;
-  const float* val;
-  const int32_t* seg;  // [n_seg + 1] graph row offsets
-  int64_t n_seg, n_rows, tail_rows;
-  int tail_wgs, d, n_steps;
-  LocalStep st[kLocalMaxSteps];
-};
-
-// One step's row whose CSR entries (<= LPR of them) are already in the row
-// group's lanes (cm, wm: entry e0 + sub): the gathers of k_poly_step's first
-// staged chunk, without its rowptr / col / val loads -- the operator is the
-// same for every step, so k_poly_local loads them once.  Same sums (CSR
-// order from 0) and epilogue as poly_row_body: the same bits.
-template <int V, int LPR>
-__device__ __forceinline__ void local_row_cached(const PolyArgs& a, int64_t row, bool live,
-                                                 int sub, int cnt, int cm, float wm) {
-  using vt = typename VecT<V>::type;
-  for (int f0 = 0; f0 < a.d; f0 += LPR * V) {
-    const int f = f0 + sub * V;
-    const bool fok = live && f < a.d;
-    vt acc;
-#pragma unroll
-    for (int i = 0; i < V; ++i) vget(acc, i) = 0.f;
-    if (cnt <= 8) {
-      gather_batch<V, 8, LPR>(a.X, a.ldx, f, fok, cm, wm, 0, cnt, acc);
-    } else {
-      int j = 0;
-      for (; j + 3 < cnt; j += 4) gather_batch<V, 4, LPR>(a.X, a.ldx, f, fok, cm, wm, j, 4, acc);
-      if (j < cnt) gather_batch<V, 3, LPR>(a.X, a.ldx, f, fok, cm, wm, j, cnt - j, acc);
-    }
-    if (!fok) continue;
-    poly_epilogue<V>(a, row, f, acc, 1.f);
-  }
-}
-
-template <int V, int LPR, int NT>
-__global__ __launch_bounds__(NT) void k_poly_local(LocalArgs a) {
-  const int64_t wg = blockIdx.x;
-  int64_t r0, r1;
-  if (wg < a.n_seg) {
-    r0 = a.seg[wg];
-    r1 = a.seg[wg + 1];
-  } else {  // padding rows past the last graph, tail_rows per workgroup
-    const int64_t j = wg - a.n_seg;
-    r0 = (int64_t)a.seg[a.n_seg] + j * a.tail_rows;
-    r1 = j + 1 == a.tail_wgs ? a.n_rows : r0 + a.tail_rows;
-  }
-  if (r1 > a.n_rows) r1 = a.n_rows;
-  if (r0 > r1) r0 = r1;
-  constexpr int RG = NT / LPR;
-  const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
-  // a graph that fits one pass with rows of <= LPR entries (every ZINC row):
-  // its CSR row is loaded once, into the row group's lanes, for all steps
-  const int64_t crow = r0 + grp;
-  const bool one_pass = r1 - r0 <= RG;
-  const bool clive = one_pass && crow < r1;
-  const int ce0 = clive ? a.rowptr[crow] : 0;
-  const int ccnt = clive ? a.rowptr[crow + 1] - ce0 : 0;
-  const bool cached = ccnt <= LPR;  // uniform in the row group
-  const int cm = (clive && sub < ccnt) ? a.col[ce0 + sub] : 0;
-  const float wm = (clive && sub < ccnt) ? (a.val ? a.val[ce0 + sub] : 1.f) : 0.f;
-  PolyArgs p{};
-  p.rowptr = a.rowptr;
-  p.col = a.col;
-  p.val = a.val;
-  p.n_rows = a.n_rows;
-  p.d = a.d;
-  for (int s = 0; s < a.n_steps; ++s) {
-    const LocalStep& t = a.st[s];
-    p.X = t.X;
-    p.B = t.B;
-    p.Z = t.Z;
-    p.P = t.P;
-    p.Q = t.Q;
-    p.Y = t.Y;
-    p.ldx = t.ldx;
-    p.ldb = t.ldb;
-    p.ldz = t.ldz;
-    p.ldp = t.ldp;
-    p.ldq = t.ldq;
-    p.ldy = t.ldy;
-    p.alpha = t.alpha;
-    p.beta = t.beta;
-    p.gamma = t.gamma;
-    p.div = t.div;
-    p.p = t.p;
-    p.q = t.q;
-    if (one_pass && cached) {
-      local_row_cached<V, LPR>(p, clive ? crow : 0, clive, sub, ccnt, cm, wm);
-    } else {
-      for (int64_t rb = r0; rb < r1; rb += RG) {
-        const int64_t row = rb + grp;
-        const bool live = row < r1;
-        poly_row_body<V, LPR, 4>(p, live ? row : 0, live, sub);
-      }
-    }
-    __syncthreads();  // this step's rows are the next step's gathered operand
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -689,8 +553,8 @@ __global__ __launch_bounds__(256) void k_segment_mean_bwd(SegArgs a) {
 // --- host-side dispatch ------------------------------------------------------
 // Widest vector width V in {4,2,1} that divides d and every row stride and
 // keeps every base pointer aligned; lanes per row = next pow2 of d/V (<= 64).
-template <class LDS, class PTRS>
-int pick_vec_of(int64_t d, const LDS& lds, const PTRS& ptrs) {
+int pick_vec(int64_t d, std::initializer_list<int64_t> lds,
+             std::initializer_list<const void*> ptrs) {
   for (int v : {4, 2}) {
     bool ok = (d % v) == 0;
     for (int64_t ld : lds) ok = ok && (ld % v) == 0;
@@ -700,10 +564,6 @@ int pick_vec_of(int64_t d, const LDS& lds, const PTRS& ptrs) {
     if (ok) return v;
   }
   return 1;
-}
-int pick_vec(int64_t d, std::initializer_list<int64_t> lds,
-             std::initializer_list<const void*> ptrs) {
-  return pick_vec_of(d, lds, ptrs);
 }
 
 int pick_lpr(int64_t d, int v) {
@@ -1116,188 +976,7 @@ int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
   return HLHGAT_OK;
 }
 
-// The steps basis_fwd_core / basis_bwd_core launch, as LocalStep records
-// (the same operands and coefficients), and one k_poly_local launch.
-LocalStep local_step(const PolyArgs& a) {
-  LocalStep t{};
-  t.X = a.X;
-  t.B = a.B;
-  t.Z = a.Z;
-  t.P = a.P;
-  t.Q = a.Q;
-  t.Y = a.Y;
-  t.ldx = a.ldx;
-  t.ldb = a.ldb;
-  t.ldz = a.ldz;
-  t.ldp = a.ldp;
-  t.ldq = a.ldq;
-  t.ldy = a.ldy;
-  t.alpha = a.alpha;
-  t.beta = a.beta;
-  t.gamma = a.gamma;
-  t.div = a.div;
-  t.p = a.p;
-  t.q = a.q;
-  return t;
-}
-
-int launch_local(LocalArgs& L, int64_t nnz, hipStream_t s) {
-  if (L.n_steps == 0 || L.n_rows == 0) return HLHGAT_OK;
-  std::vector<int64_t> lds;
-  std::vector<const void*> ptrs;
-  for (int i = 0; i < L.n_steps; ++i) {
-    const LocalStep& t = L.st[i];
-    lds.insert(lds.end(), {t.ldx, t.ldy, t.B ? t.ldb : 4, t.Z ? t.ldz : 4, t.P ? t.ldp : 4,
-                           t.Q ? t.ldq : 4});
-    ptrs.insert(ptrs.end(), {t.X, t.Y, t.B, t.Z, t.P, t.Q});
-  }
-  const int v = pick_vec_of(L.d, lds, ptrs);
-  const int l = pick_lpr(L.d, v);
-  // workgroup: 64 rows per pass (a ZINC graph in one pass), 256..1024 threads
-  int nt = l * 64 <= 256 ? 256 : (l * 64 >= 1024 ? 1024 : l * 64);
-  if (const char* e = std::getenv("HLHGAT_LOCAL_NT")) {  // A/B: 256 / 512 / 1024
-    const int v_nt = std::atoi(e);
-    if (v_nt == 256 || v_nt == 512 || v_nt == 1024) nt = v_nt;
-  }
-  // padding rows: ~ one tenth of the rows in workgroups of one row pass each
-  // (the last one takes whatever is left)
-  L.tail_rows = nt / l;
-  L.tail_wgs = (int)std::max<int64_t>(1, ceil_div(std::max<int64_t>(L.n_rows / 10, 1), L.tail_rows));
-  const int64_t grid = L.n_seg + L.tail_wgs;
-  HLH_CHECK_ARG(grid < (int64_t)INT32_MAX, "poly_basis_local: too many graphs");
-  PolyArgs bytes_of{};
-  bytes_of.n_rows = L.n_rows;
-  bytes_of.d = L.d;
-  // algorithmic bytes of the fused basis: the CSR once, the input operand
-  // read once, each step's output written once and its dense epilogue
-  // operands other than the terms this launch wrote itself read once
-  double b = (double)nnz * (L.val ? 8.0 : 4.0) + 4.0 * (double)(L.n_rows + 1) +
-             4.0 * (double)(L.n_seg + 1);
-  const double row = 4.0 * (double)L.n_rows * L.d;
-  b += row;  // the first step's gathered operand
-  for (int i = 0; i < L.n_steps; ++i) b += row;  // every term written
-  ProfScope prof(HLHGAT_PROF_POLY, s, b, 2.0 * (double)nnz * L.d * L.n_steps);
-  const unsigned g = (unsigned)grid;
-  switch (v * 100 + l) {
-#define HLH_LOCAL_CASE(VV, LL)                                                          \
-  case VV * 100 + LL:                                                                   \
-    if (nt == 256)                                                                      \
-      launch(k_poly_local<VV, LL, 256>, g, 256, 0, s, &prof, L);                        \
-    else if (nt == 512)                                                                 \
-      launch(k_poly_local<VV, LL, 512>, g, 512, 0, s, &prof, L);                        \
-    else                                                                                \
-      launch(k_poly_local<VV, LL, 1024>, g, 1024, 0, s, &prof, L);                      \
-    break;
-    HLH_LOCAL_CASE(1, 1) HLH_LOCAL_CASE(1, 2) HLH_LOCAL_CASE(1, 4) HLH_LOCAL_CASE(1, 8)
-    HLH_LOCAL_CASE(1, 16) HLH_LOCAL_CASE(1, 32) HLH_LOCAL_CASE(1, 64)
-    HLH_LOCAL_CASE(2, 1) HLH_LOCAL_CASE(2, 2) HLH_LOCAL_CASE(2, 4) HLH_LOCAL_CASE(2, 8)
-    HLH_LOCAL_CASE(2, 16) HLH_LOCAL_CASE(2, 32) HLH_LOCAL_CASE(2, 64)
-    HLH_LOCAL_CASE(4, 1) HLH_LOCAL_CASE(4, 2) HLH_LOCAL_CASE(4, 4) HLH_LOCAL_CASE(4, 8)
-    HLH_LOCAL_CASE(4, 16) HLH_LOCAL_CASE(4, 32) HLH_LOCAL_CASE(4, 64)
-#undef HLH_LOCAL_CASE
-    default: break;
-  }
-  HLH_CHECK_LAUNCH();
-  return HLHGAT_OK;
-}
-
-LocalArgs local_args(const int32_t* rowptr, const int32_t* col, const float* val, int64_t n,
-                     const int32_t* seg, int64_t n_seg, int64_t F) {
-  LocalArgs L{};
-  L.rowptr = rowptr;
-  L.col = col;
-  L.val = val;
-  L.seg = seg;
-  L.n_seg = n_seg;
-  L.n_rows = n;
-  L.d = (int)F;
-  return L;
-}
 }  // namespace
-
-extern "C" int hlhgat_poly_basis_fwd_local(int kind, const int32_t* rowptr, const int32_t* col,
-                                           const float* val, int64_t n, int64_t nnz,
-                                           const int32_t* seg_ptr, int64_t n_seg,
-                                           const float* X, int64_t ldx, int64_t F, int K,
-                                           float* T, void* stream) {
-  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
-                "poly_basis_fwd_local: kind %d (Laguerre or Chebyshev)", kind);
-  HLH_CHECK_ARG(K >= 1 && K - 1 <= kLocalMaxSteps, "poly_basis_fwd_local: K=%d not in [1, %d]",
-                K, kLocalMaxSteps + 1);
-  HLH_CHECK_ARG(n >= 0 && F > 0 && ldx >= F && n_seg >= 0 && (n == 0 || (rowptr && seg_ptr)) &&
-                    (nnz == 0 || col),
-                "poly_basis_fwd_local: bad arguments");
-  if (K == 1 || n == 0) return HLHGAT_OK;
-  HLH_CHECK_ARG(X && T, "poly_basis_fwd_local: NULL operand");
-  const int64_t blk = n * F;
-  auto Tk = [&](int k) -> float* { return T + (int64_t)(k - 1) * blk; };
-  LocalArgs L = local_args(rowptr, col, val, n, seg_ptr, n_seg, F);
-  {  // T_1, as basis_fwd_core
-    PolyArgs a = make_args(rowptr, col, val, n, X, ldx, F, Tk(1), F);
-    if (kind != HLHGAT_POLY_CHEB) {
-      a.alpha = -1.f;
-      a.beta = 1.f;
-    }
-    L.st[L.n_steps++] = local_step(a);
-  }
-  for (int k = 1; k + 1 < K; ++k) {
-    const float* prev = (k == 1) ? X : Tk(k - 1);
-    const int64_t ldprev = (k == 1) ? ldx : F;
-    PolyArgs a = make_args(rowptr, col, val, n, Tk(k), F, F, Tk(k + 1), F);
-    a.Z = prev;
-    a.ldz = ldprev;
-    if (kind == HLHGAT_POLY_LAGUERRE) {
-      a.alpha = -1.f;
-      a.beta = (float)(2 * k + 1);
-      a.gamma = -(float)k;
-      a.div = (float)(k + 1);
-    } else {
-      a.alpha = 2.f;
-      a.gamma = -1.f;
-    }
-    L.st[L.n_steps++] = local_step(a);
-  }
-  return launch_local(L, nnz, as_stream(stream));
-}
-
-extern "C" int hlhgat_poly_basis_bwd_local(int kind, const int32_t* rowptr_t,
-                                           const int32_t* col_t, const float* val_t, int64_t n,
-                                           int64_t nnz, const int32_t* seg_ptr, int64_t n_seg,
-                                           int64_t F, int K, float* G, void* stream) {
-  HLH_CHECK_ARG(kind == HLHGAT_POLY_LAGUERRE || kind == HLHGAT_POLY_CHEB,
-                "poly_basis_bwd_local: kind %d (Laguerre or Chebyshev)", kind);
-  HLH_CHECK_ARG(K >= 1 && K - 1 <= kLocalMaxSteps, "poly_basis_bwd_local: K=%d not in [1, %d]",
-                K, kLocalMaxSteps + 1);
-  HLH_CHECK_ARG(n >= 0 && F > 0 && n_seg >= 0 && (n == 0 || (rowptr_t && seg_ptr)) &&
-                    (nnz == 0 || col_t),
-                "poly_basis_bwd_local: bad arguments");
-  if (K == 1 || n == 0) return HLHGAT_OK;
-  HLH_CHECK_ARG(G, "poly_basis_bwd_local: G is NULL");
-  const int64_t blk = n * F;
-  auto Gk = [&](int k) -> float* { return G + (int64_t)k * blk; };
-  LocalArgs L = local_args(rowptr_t, col_t, val_t, n, seg_ptr, n_seg, F);
-  for (int k = K - 1; k >= 1; --k) {  // as basis_bwd_core
-    PolyArgs a = make_args(rowptr_t, col_t, val_t, n, Gk(k), F, F, Gk(k - 1), F);
-    a.P = Gk(k - 1);
-    a.ldp = F;
-    a.p = 1.f;
-    if (k + 1 <= K - 1) {
-      a.Q = Gk(k + 1);
-      a.ldq = F;
-    }
-    if (kind == HLHGAT_POLY_LAGUERRE) {
-      a.alpha = -1.f;
-      a.beta = (float)(2 * k - 1);
-      a.div = (float)k;
-      a.q = -(float)k / (float)(k + 1);
-    } else {
-      a.alpha = (k == 1) ? 1.f : 2.f;
-      a.q = -1.f;
-    }
-    L.st[L.n_steps++] = local_step(a);
-  }
-  return launch_local(L, nnz, as_stream(stream));
-}
 
 extern "C" int hlhgat_poly_basis_fwd(int kind, const int32_t* rowptr, const int32_t* col,
                                      const float* val, int64_t n, int64_t nnz,

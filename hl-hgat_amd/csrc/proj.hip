@@ -745,171 +745,6 @@ __global__ __launch_bounds__(256) void k_proj_bwd_weight32(BwdWeightArgs a) {
   bwd_weight32_body(a, by, bz, gl, al);
 }
 
-// ---------------------------------------------------------------------------
-// The same weight-gradient item with its chunks staged by LDS-DMA
-// (buffer_load_dwordx4 ... lds) into an NS-deep ring: NS-1 chunks in flight
-// while one is consumed, no staging registers, one raw barrier per chunk.
-// At ~1 resident workgroup per CU (the split plan aims at ~240 items) the
-// register ring above keeps two chunks in flight -- about one HBM round trip
-// against a chunk's ~1k MFMA cycles per wave, so 44 % of wave time sat in
-// s_waitcnt (profiles/r05/pmc_gemm_in_step.txt).  Rows past the
-// item's slice come back as zeros from the buffer descriptor's range check
-// (no tail code); columns past N / kb load whatever the row holds, which only
-// reaches output rows / columns that are never stored.  Per element the same
-// MFMA chain, chunk order and two-level flush as bwd_weight32_body: bitwise
-// the same partials.
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, float* lds_row, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_row, 16, voff, 0, 0, 0);
-}
-
-// wait until at most n of this wave's DMA instructions are outstanding
-__device__ __forceinline__ void vm_wait(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-  }
-}
-
-template <int NS>
-__device__ __forceinline__ void bwd_weight_dma_body(const BwdWeightArgs& a, int by, int bz,
-                                                    float* lds) {
-  static_assert(NS >= 2 && NS <= 7, "ring depth");
-  // stage s: dC rows [s][0][32][64], A rows [s][1][32][64]
-  float (*ring)[2][WR][64] = reinterpret_cast<float (*)[2][WR][64]>(lds);
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int wn = wave >> 1, wk = wave & 1;
-  int b = 0;
-  while (b + 1 < a.nb && by >= a.tile_start[b + 1]) ++b;
-  const int t = by - a.tile_start[b];
-  const int n_base = (t % a.tiles_n) * 64;
-  const int k_base = (t / a.tiles_n) * 64;
-  const int kb = a.kb[b];
-  const int64_t lda = a.lda[b];
-  const bool do_bias = a.bias_off >= 0 && b == 0 && k_base == 0;
-  const int64_t m_lo = (int64_t)bz * a.rows_per_split;
-  int64_t m_hi = m_lo + a.rows_per_split;
-  if (m_hi > a.M) m_hi = a.M;
-  const int64_t nchunk = m_hi > m_lo ? (m_hi - m_lo + WR - 1) / WR : 0;
-  // descriptors over this slice's rows only: rows >= m_hi read as 0
-  const unsigned rows = (unsigned)(m_hi > m_lo ? m_hi - m_lo : 0);
-  __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.G + m_lo * a.ldg), 0, (int)(rows * (unsigned)a.ldg * 4u), 0x00020000);
-  __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.A[b] + m_lo * lda), 0, (int)(rows * (unsigned)lda * 4u), 0x00020000);
-  // DMA piece j (0..1) of this wave: rows (2 wave + j) * 4 + lane / 16, float4 lane % 16
-  const int pr = lane >> 4, pc = (lane & 15) * 4;
-  auto issue = [&](int64_t c, int st) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r0 = (2 * wave + j) * 4;
-      const unsigned r = (unsigned)(c * WR + r0 + pr);
-      dma16(rg, &ring[st][0][r0][0], (r * (unsigned)a.ldg + (unsigned)(n_base + pc)) * 4u);
-      dma16(ra, &ring[st][1][r0][0], (r * (unsigned)lda + (unsigned)(k_base + pc)) * 4u);
-    }
-  };
-
-  floatx16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  float bsum = 0.f;
-  const int rl = lane >> 5, cl = lane & 31;
-  constexpr int kFlushChunks = 8;  // as bwd_weight32_body (same bits)
-  floatx16 outer;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) outer[r] = 0.f;
-  float bouter = 0.f;
-  bool flushed = false;
-#pragma unroll
-  for (int j = 0; j < NS - 1; ++j)
-    if (j < nchunk) issue(j, j);
-  for (int64_t c = 0; c < nchunk; ++c) {
-    // chunk c landed (this wave's pieces; later chunks may stay in flight),
-    // this wave's reads of the stage about to be refilled retired, then every
-    // wave past the barrier: chunk c is whole in LDS, stage (c-1) % NS free
-    const int64_t later = nchunk - 1 - c;
-    vm_wait(4 * (int)(later < NS - 2 ? later : NS - 2));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (c + NS - 1 < nchunk) issue(c + NS - 1, (int)((c + NS - 1) % NS));
-    const int st = (int)(c % NS);
-#pragma unroll
-    for (int kk = 0; kk < WR / 2; ++kk) {
-      const float av = ring[st][0][2 * kk + rl][32 * wn + cl];
-      const float bv = ring[st][1][2 * kk + rl][32 * wk + cl];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-      bsum = bsum + av;
-    }
-    if ((c + 1) % kFlushChunks == 0 && c + 1 < nchunk) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        outer[r] = outer[r] + acc[r];
-        acc[r] = 0.f;
-      }
-      bouter = bouter + bsum;
-      bsum = 0.f;
-      flushed = true;
-    }
-  }
-  if (flushed) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = outer[r] + acc[r];
-    bsum = bouter + bsum;
-  }
-  float* slab = a.part + (int64_t)bz * a.part_stride + a.part_off[b];
-  const int k = k_base + 32 * wk + cl;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int n = n_base + 32 * wn + (r & 3) + 8 * (r >> 2) + 4 * rl;
-    if (n < a.N && k < kb) slab[(int64_t)n * kb + k] = acc[r];
-  }
-  if (do_bias && wk == 0) {
-    const float tot = bsum + __shfl_xor(bsum, 32, 64);
-    const int n = n_base + 32 * wn + cl;
-    if (rl == 0 && n < a.N) a.part[(int64_t)bz * a.part_stride + a.bias_off + n] = tot;
-  }
-}
-
-template <int NS>
-__global__ __launch_bounds__(256) void k_proj_bwd_weight_dma(BwdWeightArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[NS * 2 * WR * 64];
-  int by = (int)blockIdx.y, bz = (int)blockIdx.z;
-  if (a.xcd_map)
-    weight_item(blockIdx.y + blockIdx.z * gridDim.y, gridDim.y, gridDim.y * gridDim.z, by, bz);
-  bwd_weight_dma_body<NS>(a, by, bz, lds);
-}
-
-// the DMA ring addresses a slice through 32-bit buffer offsets: every row
-// of a slice of every operand must lie within 2^31 bytes of the slice start
-bool wgrad_dma_fits(int64_t rows_per_split, int64_t lddc, int nb, const int64_t* lda) {
-  int64_t ld = lddc;
-  for (int b = 0; b < nb; ++b) ld = std::max<int64_t>(ld, lda[b]);
-  return (rows_per_split + 1) * ld * 4 < ((int64_t)1 << 31);
-}
-
-// HLHGAT_WGRAD_STAGES / hlhgat_set_wgrad_stages: 0 = the register ring
-// (bwd_weight32_body), 3..6 = the LDS-DMA ring of that depth
-std::atomic<int> g_wgrad_stages{-1};
-int wgrad_stages() {
-  int v = g_wgrad_stages.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = std::getenv("HLHGAT_WGRAD_STAGES");
-    v = e ? std::atoi(e) : 0;
-    if (v != 0 && (v < 3 || v > 6)) v = 0;
-    int expect = -1;
-    g_wgrad_stages.compare_exchange_strong(expect, v);
-    v = g_wgrad_stages.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-
 }  // namespace
 #include "proj_big.h"
 namespace {
@@ -1004,7 +839,7 @@ struct BwdFusedArgs {
   ReduceArgs red;
 };
 
-template <int TND, bool ROWS, int WNS>
+template <int TND, bool ROWS>
 __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk blk, float* lds) {
   const int L = (int)blk.x;
   if (L >= a.n_wpad + a.n_d) {
@@ -1040,21 +875,17 @@ __device__ __forceinline__ void proj_bwd_fused_body(const BwdFusedArgs& a, Blk b
   const int Y = a.w.tile_start[a.w.nb];
   int by = L % Y, bz = L / Y;
   if (a.w.xcd_map) weight_item((unsigned)L, (unsigned)Y, (unsigned)a.n_w, by, bz);
-  if (WNS > 0)
-    bwd_weight_dma_body<(WNS > 0 ? WNS : 2)>(a.w, by, bz, lds);
-  else
-    bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
-                      reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
+  bwd_weight32_body(a.w, by, bz, reinterpret_cast<float (*)[WR][64]>(lds),
+                    reinterpret_cast<float (*)[WR][64]>(lds + 2 * WR * 64));
 }
 
-template <int TND, bool ROWS, int WNS = 0>
+template <int TND, bool ROWS>
 __global__ __launch_bounds__(256) void k_proj_bwd_fused(BwdFusedArgs a) {
-  // ROWS: two W buffers + the epilogue scratch (bwd_data_rows_body);
-  // WNS > 0: the weight items' LDS-DMA ring of WNS stages
-  constexpr int kW = (WNS > 0 ? WNS : 2) * WR * 64 * 2;
+  // ROWS: two W buffers + the epilogue scratch (bwd_data_rows_body)
+  constexpr int kW = 2 * WR * 64 * 2;
   constexpr int kD = ROWS ? 2 * TND * 16 * KCP + 4 * 16 * (TND * 16 + 4) : 2 * TND * 16 * KCP;
   __shared__ __attribute__((aligned(16))) float lds[kW > kD ? kW : kD];
-  proj_bwd_fused_body<TND, ROWS, WNS>(a, blk_hw(), lds);
+  proj_bwd_fused_body<TND, ROWS>(a, blk_hw(), lds);
 }
 
 // A/B hook (hlhgat_set_proj_bwd_rows): row-block data-gradient workgroups
@@ -1609,17 +1440,8 @@ extern "C" int hlhgat_proj_bwd_weight(int nblocks, const float* dC, int64_t lddc
     return HLHGAT_OK;
   }
   dim3 grid(1, (unsigned)p.tiles_total, (unsigned)p.splits);
-  const int wns = wgrad_dma_fits(p.rows_per_split, lddc, nblocks, lda) ? wgrad_stages() : 0;
   if (p.big)
     launch_weight_big(p.big, (unsigned)(p.tiles_total * p.splits), s, nullptr, a);
-  else if (vec && wns == 3)
-    launch(k_proj_bwd_weight_dma<3>, dim3(grid), dim3(256), 0, s, nullptr, a);
-  else if (vec && wns == 4)
-    launch(k_proj_bwd_weight_dma<4>, dim3(grid), dim3(256), 0, s, nullptr, a);
-  else if (vec && wns == 5)
-    launch(k_proj_bwd_weight_dma<5>, dim3(grid), dim3(256), 0, s, nullptr, a);
-  else if (vec && wns == 6)
-    launch(k_proj_bwd_weight_dma<6>, dim3(grid), dim3(256), 0, s, nullptr, a);
   else if (vec)
     launch(k_proj_bwd_weight32, dim3(grid), dim3(256), 0, s, nullptr, a);
   else
@@ -1911,27 +1733,14 @@ int proj_bwd_impl(int64_t M, int64_t N, const float* dC, int64_t lddc, int nb_w,
   }
   bytes += 4.0 * (double)p.splits * p.part_stride;
   ProfScope prof(HLHGAT_PROF_PROJ_BWD, s, bytes, flops);
-  const int wns = want_w && wgrad_dma_fits(p.rows_per_split, lddc, nb_w, lda) ? wgrad_stages() : 0;
-  const dim3 g((unsigned)n_blocks);
-#define HLH_FUSED(TND_, ROWS_)                                                       \
-  do {                                                                               \
-    switch (wns) {                                                                   \
-      case 3: launch(k_proj_bwd_fused<TND_, ROWS_, 3>, g, dim3(256), 0, s, &prof, f); break; \
-      case 4: launch(k_proj_bwd_fused<TND_, ROWS_, 4>, g, dim3(256), 0, s, &prof, f); break; \
-      case 5: launch(k_proj_bwd_fused<TND_, ROWS_, 5>, g, dim3(256), 0, s, &prof, f); break; \
-      case 6: launch(k_proj_bwd_fused<TND_, ROWS_, 6>, g, dim3(256), 0, s, &prof, f); break; \
-      default: launch(k_proj_bwd_fused<TND_, ROWS_>, g, dim3(256), 0, s, &prof, f);        \
-    }                                                                                \
-  } while (0)
   if (rows)
-    HLH_FUSED(4, true);
+    launch(k_proj_bwd_fused<4, true>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else if (tnd == 1)
-    HLH_FUSED(1, false);
+    launch(k_proj_bwd_fused<1, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else if (tnd == 2)
-    HLH_FUSED(2, false);
+    launch(k_proj_bwd_fused<2, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   else
-    HLH_FUSED(4, false);
-#undef HLH_FUSED
+    launch(k_proj_bwd_fused<4, false>, dim3((unsigned)n_blocks), dim3(256), 0, s, &prof, f);
   HLH_CHECK_LAUNCH();
   r.splits = p.splits;
   r.part = workspace;
@@ -1985,13 +1794,6 @@ extern "C" int hlhgat_set_gemm_big(int mode, int64_t min_m) {
   HLH_CHECK_ARG(mode >= -1 && mode <= 1, "set_gemm_big: mode must be -1, 0 or 1");
   g_big_mode.store(mode);
   if (min_m > 0) g_big_min_m.store(min_m);
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_set_wgrad_stages(int stages) {
-  HLH_CHECK_ARG(stages == 0 || (stages >= 3 && stages <= 6),
-                "set_wgrad_stages: 0 (register ring) or 3..6 (LDS-DMA ring depth)");
-  g_wgrad_stages.store(stages);
   return HLHGAT_OK;
 }
 

@@ -669,12 +669,11 @@ struct ConvArgs {
   OptT h_hdr;
   std::vector<Tensor> fac;
   int64_t fac_nodes = 0;
-  OptT seg;  // graph row offsets: the basis in one launch (hlhgat_poly_basis_*_local)
 };
 
 // What one side's backward needs: the tensors (kSavedFixed, then W[0..K),
 // then the factor) and the sizes.
-constexpr size_t kSavedFixed = 22;
+constexpr size_t kSavedFixed = 21;
 struct ConvSaved {
   std::vector<Tensor> t;
   std::vector<int64_t> dims;  // N, Cin, F, M, dout, K, kind, nnz, bn_mode, has_bias
@@ -731,19 +730,7 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv) {
                            has(c.h_sval) ? *c.h_sval : Tensor(), c.h_bounds, *c.h_hdr)
                : hlhgat_halo_t{};
   const bool factored = !c.fac.empty();
-  // graph-local basis: block-diagonal L with the batch's graph offsets, no
-  // row schedule / halo tiles (small graphs: ZINC), Laguerre or Chebyshev
-  const bool local = has(c.seg) && !factored && !use_halo && !has(c.a_order) &&
-                     (c.kind == HLHGAT_POLY_LAGUERRE || c.kind == HLHGAT_POLY_CHEB) && K <= 6;
-  if (local && K > 1 && N > 0) {
-    chk(hlhgat_poly_basis_fwd_local((int)c.kind, c.a_rowptr.data_ptr<int>(),
-                                    c.nnz ? c.a_col.data_ptr<int>() : nullptr,
-                                    c.nnz ? fptr(c.a_val) : nullptr, N, c.nnz,
-                                    c.seg->data_ptr<int>(), c.seg->numel() - 1,
-                                    x2.data_ptr<float>(), ld_of(x2), F, (int)K,
-                                    T.data_ptr<float>(), s),
-        "poly_basis_fwd_local");
-  } else if (factored && K > 1 && N > 0) {
+  if (factored && K > 1 && N > 0) {
     const hlhgat_hodge_factor_t hf = make_factor(c.fac, c.fac_nodes, N);
     Tensor work = at::empty({hlhgat_hodge_factor_work_floats(c.fac_nodes, F)}, x.options());
     chk(hlhgat_poly_basis_fwd_factored((int)c.kind, &hf, x2.data_ptr<float>(), ld_of(x2), F,
@@ -819,10 +806,7 @@ Tensor conv_forward(const ConvArgs& c, ConvSaved& sv) {
           halo_bwd ? *c.h_srp : Tensor(),
           halo_bwd ? *c.h_lcol : Tensor(),
           (halo_bwd && has(c.h_sval)) ? *c.h_sval : Tensor(),
-          halo_bwd ? *c.h_hdr : Tensor(),
-          // the adjoint's graph-local launch: L^T is L (one CSR) and no schedule
-          (local && c.t_rowptr.data_ptr() == c.a_rowptr.data_ptr() && !has(c.t_order))
-              ? *c.seg : Tensor()};
+          halo_bwd ? *c.h_hdr : Tensor()};
   for (const auto& w : c.W) sv.t.push_back(w);
   for (const auto& t : c.fac) sv.t.push_back(t);
   std::vector<int64_t> oshape = x.sizes().vec();
@@ -839,7 +823,7 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
   Tensor x2 = t[0], T = t[1], t_order = t[2], valid = t[3], t_rowptr = t[4], t_col = t[5],
          t_val = t[6], pre = t[7], yout = t[8], mean = t[9], invstd = t[10], bn_w = t[11],
          bias_p = t[12], bn_b = t[13], h_tile = t[14], h_ptr = t[15], h_cols = t[16],
-         h_srp = t[17], h_lcol = t[18], h_sval = t[19], h_hdr = t[20], seg = t[21];
+         h_srp = t[17], h_lcol = t[18], h_sval = t[19], h_hdr = t[20];
   std::vector<Tensor> W(t.begin() + kSavedFixed, t.begin() + kSavedFixed + K);
   std::vector<Tensor> fac(t.begin() + kSavedFixed + K, t.end());
   const bool use_halo = h_lcol.defined();
@@ -923,13 +907,6 @@ ConvGrads conv_backward(const ConvSaved& sv, const Tensor& grad, const ConvNeeds
         chk(hlhgat_poly_basis_bwd_factored((int)kind, &hf, F, (int)K, Gs.data_ptr<float>(),
                                            work.data_ptr<float>(), s),
             "poly_basis_bwd_factored");
-      } else if (K > 1 && seg.defined() && !use_halo) {
-        chk(hlhgat_poly_basis_bwd_local((int)kind, t_rowptr.data_ptr<int>(),
-                                        nnz ? t_col.data_ptr<int>() : nullptr,
-                                        (nnz && t_val.defined()) ? t_val.data_ptr<float>() : nullptr,
-                                        N, nnz, seg.data_ptr<int>(), seg.numel() - 1, F, (int)K,
-                                        Gs.data_ptr<float>(), s),
-            "poly_basis_bwd_local");
       } else if (K > 1) {
         chk(hlhgat_poly_basis_bwd((int)kind, t_rowptr.data_ptr<int>(),
                                   nnz ? t_col.data_ptr<int>() : nullptr,
@@ -994,9 +971,8 @@ void edge_map_conv(EdgeMap& em, const ConvArgs& c) {
   em.opt(c.h_hdr);
   em.list(c.fac);
   em.other();
-  em.opt(c.seg);
 }
-constexpr int64_t conv_positions(int64_t K, int64_t n_fac) { return 30 + K + n_fac + 2; }
+constexpr int64_t conv_positions(int64_t K, int64_t n_fac) { return 30 + K + n_fac + 1; }
 
 void put_grads(variable_list& out, int64_t base, int64_t K, const ConvGrads& g) {
   out[base] = g.dx;
@@ -1016,11 +992,11 @@ class ConvBNFn : public torch::autograd::Function<ConvBNFn> {
                         int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT valid,
                         OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol,
                         OptT h_sval, std::vector<int64_t> h_bounds, OptT h_hdr,
-                        at::TensorList fac, int64_t fac_nodes, OptT seg) {
+                        at::TensorList fac, int64_t fac_nodes) {
     ConvArgs c{x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind, W.vec(), bias,
                bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps, bn_mode, out_buf, a_order,
                t_order, valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds, h_hdr,
-               fac.vec(), fac_nodes, seg};
+               fac.vec(), fac_nodes};
     ConvSaved sv;
     Tensor y = conv_forward(c, sv);
     EdgeMap em;
@@ -1927,11 +1903,11 @@ Tensor conv_bn(Tensor x, Tensor a_rowptr, Tensor a_col, OptT a_val, Tensor t_row
                int64_t bn_mode, OptT out_buf, OptT a_order, OptT t_order, OptT valid,
                OptT h_tile, OptT h_ptr, OptT h_cols, OptT h_srp, OptT h_lcol, OptT h_sval,
                std::vector<int64_t> h_bounds, OptT h_hdr, std::vector<Tensor> fac,
-               int64_t fac_nodes, OptT seg) {
+               int64_t fac_nodes) {
   return ConvBNFn::apply(x, a_rowptr, a_col, a_val, t_rowptr, t_col, t_val, nnz, kind,
                          at::TensorList(W), bias, bn_w, bn_b, bn_rm, bn_rv, bn_nbt, momentum, eps,
                          bn_mode, out_buf, a_order, t_order, valid, h_tile, h_ptr, h_cols, h_srp, h_lcol, h_sval, h_bounds,
-                         h_hdr, at::TensorList(fac), fac_nodes, seg);
+                         h_hdr, at::TensorList(fac), fac_nodes);
 }
 
 Tensor bn_act(Tensor x, OptT w, OptT b, OptT rm, OptT rv, OptT nbt, double momentum, double eps,

@@ -51,10 +51,6 @@ SIGNATURES = {
                                  c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                       c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
-    "hlhgat_poly_basis_fwd_local": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                            c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
-    "hlhgat_poly_basis_bwd_local": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                            c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                       c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_hodge_factor_work_floats": (c_i64, [c_i64, c_i64]),
@@ -96,7 +92,6 @@ SIGNATURES = {
     "hlhgat_set_proj_bn_fused": (c_i32, [c_i32]),
     "hlhgat_set_proj_bn_split": (c_i32, [c_i32]),
     "hlhgat_set_proj_bwd_rows": (c_i32, [c_i32]),
-    "hlhgat_set_wgrad_stages": (c_i32, [c_i32]),
     "hlhgat_set_gemm_big": (c_i32, [c_i32, c_i64]),
     "hlhgat_proj_bn_fused_capacity": (c_i32, [P_i64]),
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),

@@ -138,15 +138,6 @@ class Batch(PairData):
             if (torch.is_tensor(t) and t.is_cuda and torch.is_tensor(rp) and torch.is_tensor(col)
                     and self.hodge_sorted.get(k, False)):
                 ops.set_csr(t, rp, col)
-        for side in ("t", "s"):  # graph offsets: one-launch polynomial bases
-            k = "edge_index_" + side
-            t, seg = getattr(self, k, None), getattr(self, "seg_ptr_" + side, None)
-            mr = getattr(self, "max_rows_" + side, None)
-            if (torch.is_tensor(t) and t.is_cuda and torch.is_tensor(seg) and seg.is_cuda
-                    and self.hodge_sorted.get(k, False) and mr is not None
-                    and mr <= LOCAL_MAX_ROWS
-                    and getattr(self, "num_graphs", 0) >= LOCAL_MIN_GRAPHS):
-                ops.set_segments(t, seg)
         ip, ie = getattr(self, "inc_rowptr", None), getattr(self, "inc_eids", None)
         if torch.is_tensor(ei) and ei.is_cuda and torch.is_tensor(ip) and torch.is_tensor(ie):
             ops.set_incidence(ei, ip, ie)
@@ -408,18 +399,10 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
             ptr = torch.zeros(c.numel() + 1, dtype=torch.int32)
             ptr[1:] = torch.cumsum(c, 0).to(torch.int32)
             setattr(b, key, ptr)
-            setattr(b, "max_rows_" + key[-1], int(c.max()) if c.numel() else 0)
     return b
 
 
 FACTOR_MIN_ROW = 8.0  # L1 entries per row from which the factored L1 pays (hlhgat.h)
-# batches of at least LOCAL_MIN_GRAPHS graphs of at most LOCAL_MAX_ROWS rows
-# (per Laplacian) get their polynomial bases in one launch, a workgroup per
-# graph (ops.set_segments: ZINC, 1000 graphs of ~25 rows); bigger graphs or
-# fewer of them (configs 3-5: 4-256 graphs of 10^2-10^5 rows) keep the
-# per-step launches spread over all rows of the chip
-LOCAL_MAX_ROWS = 64
-LOCAL_MIN_GRAPHS = 512
 
 
 def hodge_factor_ok(edge_index, n_nodes: int, edge_index_s, edge_weight_s) -> bool:
@@ -808,8 +791,6 @@ class PackedGraphs:
         if self.y_dim:
             b.y = t["y"]
         b.num_node1, b.num_edge1 = t["num_node1"], t["num_edge1"]
-        b.max_rows_t = int(b.num_node1.max()) if B else 0  # host arena: no device read
-        b.max_rows_s = int(b.num_edge1.max()) if B else 0
         b.num_nodes = Rt
         b.hodge_sorted = dict(self.hodge_sorted)
         # factored L1 as collate decides it (never for padded batches: pad_batch)

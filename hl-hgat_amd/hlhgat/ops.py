@@ -296,10 +296,6 @@ class SparseCSR:
     # halo tiles (tile_ptr, halo_ptr, halo, lcol, max_halo) for the LDS-staged
     # SpMM of large Laplacians (hodge_dataset.halo_tiles; hlhgat_halo_t)
     halo: Optional[tuple] = None
-    # int32 [B+1] row offsets of the operator's diagonal blocks (the graphs of a
-    # collated batch): the polynomial bases run in one launch
-    # (hlhgat_poly_basis_*_local, set_segments)
-    segments: Optional[torch.Tensor] = None
 
 
 @dataclass
@@ -406,24 +402,6 @@ def set_valid(edge_index: torch.Tensor, n_valid: torch.Tensor, attr: str = "_hlh
     from edge_index as static-shape padding (hodge_dataset.pad_batch): the
     BatchNorm statistics of its layers use the valid rows only."""
     setattr(edge_index, attr, n_valid.to(device=edge_index.device, dtype=torch.int32).view(1))
-    return edge_index
-
-
-# LOCAL_BASIS = False (A/B, tests): the polynomial bases of operators with
-# graph segments as K-1 chained launches (the same bits)
-LOCAL_BASIS = os.environ.get("HLHGAT_LOCAL_BASIS", "1") != "0"
-
-
-def set_segments(edge_index: torch.Tensor, seg_ptr: torch.Tensor) -> torch.Tensor:
-    """Declare the graph row offsets of a sorted symmetric Laplacian's
-    block-diagonal batch (collate's seg_ptr_t for L0, seg_ptr_s for L1; rows
-    past the last offset must be isolated, as pad_batch's padding rows are):
-    the operator's polynomial bases and their adjoints then run as ONE launch
-    with a workgroup per graph (hlhgat_poly_basis_fwd_local; bitwise the K-1
-    chained steps).  Meant for small graphs (collate attaches it up to
-    hodge_dataset.LOCAL_MAX_ROWS rows per graph)."""
-    edge_index._hlhgat_segments = seg_ptr.to(  # type: ignore[attr-defined]
-        device=edge_index.device, dtype=torch.int32).contiguous()
     return edge_index
 
 
@@ -774,9 +752,6 @@ def hodge_operator(edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor]
             a = _csr_sorted(ei[0], ei[1], w, n, n)
         a.order = order
         a.valid = valid
-        seg = getattr(edge_index, "_hlhgat_segments", None)
-        if seg is not None and seg.device == ei.device and int(seg.numel()) >= 1:
-            a.segments = seg
         halo = getattr(edge_index, "_hlhgat_halo", None)
         if halo is not None:  # built for the COO order = this CSR's entry order
             _attach_halo(a, halo)
@@ -948,11 +923,6 @@ def _bn_uses_batch_stats(bn) -> bool:
     return bn.training or not bn.track_running_stats
 
 
-def _segments(A: SparseCSR) -> Optional[torch.Tensor]:
-    """The conv node's graph offsets (one-launch bases), or None."""
-    return A.segments if LOCAL_BASIS else None
-
-
 def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.Tensor],
                     bias: Optional[torch.Tensor], kind: int = POLY_LAGUERRE,
                     bn: Optional[torch.nn.BatchNorm1d] = None, relu: bool = False,
@@ -975,11 +945,11 @@ def hodge_poly_conv(x: torch.Tensor, op: HodgeOperator, weights: Sequence[torch.
             raise ValueError("Expected more than 1 value per channel when training")
         return _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind,
                             ws, bias, *_bn_args(bn), 2 if relu else 1, out, A.order, At.order,
-                            A.valid, *_halo_args(A), *_factor_args(op), _segments(A))
+                            A.valid, *_halo_args(A), *_factor_args(op))
     sink = out if (bn is None and not relu and x.dim() == 2) else None
     y = _ext.conv_bn(x, A.rowptr, A.col, A.val, At.rowptr, At.col, At.val, A.nnz, kind, ws,
                      bias, None, None, None, None, None, 0.0, 0.0, 0, sink, A.order, At.order,
-                     A.valid, *_halo_args(A), *_factor_args(op), _segments(A))
+                     A.valid, *_halo_args(A), *_factor_args(op))
     if bn is not None:
         y = batch_norm_act(y, bn, relu, valid=A.valid)
     elif relu:

@@ -310,25 +310,6 @@ int hlhgat_poly_basis_bwd(int kind, const int32_t* rowptr_t,
                           const hlhgat_halo_t* halo, int64_t F,
                           int K, float* G, void* stream);
 
-/* The same basis (forward) / adjoint recurrence (backward) of a block-
- * diagonal operator in ONE launch: seg_ptr[n_seg + 1] are the row offsets of
- * its diagonal blocks -- the graphs of a PairData batch, whose Laplacian
- * entries never leave their graph's rows (lib/Hodge_Dataset.py:40-48) -- and
- * rows past seg_ptr[n_seg] (static-shape padding) must be isolated (entries
- * on their own row only).  One workgroup per graph runs the K-1 steps over
- * its rows with a barrier between them.  Same arguments and bitwise the same
- * results as hlhgat_poly_basis_fwd / _bwd without row schedule or halo tiles;
- * Laguerre and Chebyshev, K <= 6.  Replaces the K-1 chained propagate calls
- * of lib/Hodge_Cheb_Conv.py:494-507 (:412-432) for small graphs (ZINC). */
-int hlhgat_poly_basis_fwd_local(int kind, const int32_t* rowptr, const int32_t* col,
-                                const float* val, int64_t n, int64_t nnz,
-                                const int32_t* seg_ptr, int64_t n_seg, const float* X,
-                                int64_t ldx, int64_t F, int K, float* T, void* stream);
-int hlhgat_poly_basis_bwd_local(int kind, const int32_t* rowptr_t, const int32_t* col_t,
-                                const float* val_t, int64_t n, int64_t nnz,
-                                const int32_t* seg_ptr, int64_t n_seg, int64_t F, int K,
-                                float* G, void* stream);
-
 /* ---- Hodge-factored L1 (large, high-degree edge Laplacians) ------------ */
 /* Every L1 the reference builds is 2 B1^T B1 / lmax in fp32
  * (lib/Hodge_Dataset.py:451-456, :780-799; MLGC :283-287): its entries are
@@ -645,12 +626,6 @@ int hlhgat_set_gemm_big(int mode, int64_t min_m);
  * data-gradient workgroup per (row block, 64-column tile) instead of one per
  * row block covering every column tile (N <= 64); bitwise the same (tests). */
 int hlhgat_set_proj_bwd_rows(int on);
-/* Weight-gradient items of the Linear backward (hlhgat_proj_bwd*,
- * hlhgat_proj_bwd_weight): 0 = chunks staged through a two-deep register
- * ring, 3..6 = staged by LDS-DMA (buffer_load ... lds) into a ring of that
- * many chunks.  Bitwise the same gradients either way.  Env
- * HLHGAT_WGRAD_STAGES sets the process default. */
-int hlhgat_set_wgrad_stages(int stages);
 /* 0: hlhgat_proj_bn_fwd always takes the two-call path (tests). */
 int hlhgat_set_proj_bn_fused(int on);
 /* 1: hlhgat_proj_bn_fwd's fused path as two launches -- the projection with

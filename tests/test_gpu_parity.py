@@ -1753,134 +1753,3 @@ def test_proj_bn_split_bitwise(cuda, M, N, kb, pad):
                                 bn.num_batches_tracked.clone()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("M", [37, 5000, 70000])
-@pytest.mark.parametrize("widths,N", [([64, 128, 8], 96), ([64, 64, 64], 64), ([36, 36], 32),
-                                      ([200], 256)])
-def test_wgrad_dma_ring_bitwise(cuda, M, widths, N):
-    """The weight-gradient items staged by LDS-DMA into a 3..6-deep ring
-    (hlhgat_set_wgrad_stages) give the bits of the register ring: the fused
-    Linear backward (weight, bias and data gradients) and the standalone
-    weight gradient, ragged M (rows past a slice read as zeros through the
-    buffer descriptor), widths not a multiple of the 64-column tile, one to
-    three input blocks; both against torch."""
-    from hlhgat import _lib, ops
-    g = torch.Generator(device="cpu").manual_seed(M + N)
-    blocks = [torch.randn(M, k, generator=g).to(cuda) for k in widths]
-    W = torch.randn(N, sum(widths), generator=g).to(cuda) * 0.1
-    b = torch.randn(N, generator=g).to(cuda)
-    R = torch.randn(M, N, generator=g).to(cuda)
-
-    def run():
-        xs = [t.clone().requires_grad_(True) for t in blocks]
-        Wv, bv = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
-        (ops.linear_blocks(xs, Wv, bv) * R).sum().backward()
-        dW = torch.empty_like(W)
-        dWs, o = [], 0
-        for k in widths:
-            dWs.append(dW[:, o:o + k])
-            o += k
-        db = torch.empty(N, device=cuda)
-        ops._proj_bwd_weight(R, blocks, dWs, db)
-        return [Wv.grad, bv.grad] + [x.grad for x in xs] + [dW, db]
-    res = {}
-    for st in (0, 3, 4, 6):
-        _lib.check(_lib.LIB.hlhgat_set_wgrad_stages(st), "set_wgrad_stages")
-        try:
-            res[st] = run()
-        finally:
-            _lib.LIB.hlhgat_set_wgrad_stages(0)
-    torch.cuda.synchronize()
-    for st in (3, 4, 6):
-        for i, (u, v) in enumerate(zip(res[0], res[st])):
-            assert torch.equal(u, v), (st, i)
-    ref = [R.t() @ torch.cat(blocks, 1), R.sum(0)]
-    close(res[0][0].cpu(), ref[0].cpu(), 1e-4, "dW vs torch")
-    close(res[0][1].cpu(), ref[1].cpu(), 1e-4, "db vs torch")
-    close(res[0][-2].cpu(), ref[0].cpu(), 1e-4, "standalone dW vs torch")
-
-
-def _local_basis_case(cuda, n_graphs, seed, pad):
-    from hlhgat import ops
-    from hlhgat.hodge_dataset import collate, pad_batch
-    from hlhgat.synthetic import zinc_like_graph
-    b = collate([zinc_like_graph(seed + i) for i in range(n_graphs)])
-    if pad:
-        nt, ns = b.x_t.size(0), b.x_s.size(0)
-        b = pad_batch(b, {"rows_t": nt + 77, "rows_s": ns + 64,
-                          "nnz_t": b.edge_index_t.size(1) + 300,
-                          "nnz_s": b.edge_index_s.size(1) + 200})
-    return b.to(cuda)
-
-
-@pytest.mark.parametrize("pad", [False, True])
-@pytest.mark.parametrize("kind", [0, 1])  # Laguerre, Chebyshev
-def test_local_basis_bitwise_chained(cuda, pad, kind):
-    """hlhgat_poly_basis_fwd_local / _bwd_local (one launch, a workgroup per
-    graph, barrier between steps) == hlhgat_poly_basis_fwd / _bwd (K-1
-    chained k_poly_step launches), bit for bit, on L0 and L1 of a ZINC batch
-    (and its static-shape padding rows, isolated, in the tail workgroups),
-    K = 2..6, widths 18 / 36 / 64 / 128 (the configs' conv widths)."""
-    from hlhgat import _lib, ops
-    L = _lib.LIB
-    b = _local_basis_case(cuda, 37, 300, pad)
-    st = torch.cuda.current_stream().cuda_stream
-    g = torch.Generator(device="cpu").manual_seed(7 + kind)
-    for side, seg in (("t", b.seg_ptr_t), ("s", b.seg_ptr_s)):
-        ei = getattr(b, "edge_index_" + side)
-        w = getattr(b, "edge_weight_" + side)
-        n = getattr(b, "x_" + side).size(0)
-        A = ops.hodge_operator(ei, w, n).fwd
-        for F in (18, 36, 64, 128):
-            X = torch.randn(n, F, generator=g).to(cuda)
-            for K in (2, 3, 4, 6):
-                T0 = torch.full((K - 1, n, F), float("nan"), device=cuda)
-                T1 = torch.full((K - 1, n, F), float("nan"), device=cuda)
-                args = (kind, A.rowptr.data_ptr(), A.col.data_ptr(), A.val.data_ptr(), n, A.nnz)
-                _lib.check(L.hlhgat_poly_basis_fwd(*args, None, None, X.data_ptr(), F, F, K,
-                                                   T0.data_ptr(), st), "fwd")
-                _lib.check(L.hlhgat_poly_basis_fwd_local(*args, seg.data_ptr(), seg.numel() - 1,
-                                                         X.data_ptr(), F, F, K, T1.data_ptr(),
-                                                         st), "fwd_local")
-                G0 = torch.randn(K, n, F, generator=g).to(cuda)
-                G1 = G0.clone()
-                _lib.check(L.hlhgat_poly_basis_bwd(*args, None, None, F, K, G0.data_ptr(), st),
-                           "bwd")
-                _lib.check(L.hlhgat_poly_basis_bwd_local(*args, seg.data_ptr(), seg.numel() - 1,
-                                                         F, K, G1.data_ptr(), st), "bwd_local")
-                torch.cuda.synchronize()
-                assert torch.isfinite(T0).all(), (side, F, K)
-                assert torch.equal(T0, T1), (side, F, K, (T0 - T1).abs().max().item())
-                assert torch.equal(G0[0], G1[0]), (side, F, K)
-
-
-def test_local_basis_model_step_bitwise(cuda, monkeypatch):
-    """The ZINC model's training step with its convs' bases in one launch
-    (segments attached to the batch's Laplacians) == the chained launches:
-    loss, every parameter gradient and the running statistics, bitwise."""
-    import hlhgat
-    from hlhgat import hodge_dataset as HD, ops
-    monkeypatch.setattr(HD, "LOCAL_MIN_GRAPHS", 1)
-    res = []
-    for local in (True, False):
-        monkeypatch.setattr(ops, "LOCAL_BASIS", local)
-        b = _local_basis_case(cuda, 50, 900, True)
-        assert getattr(b.edge_index_t, "_hlhgat_segments", None) is not None
-        torch.manual_seed(0)
-        m = hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[1, 1], filters=[32, 32],
-                                                mlp_channels=[64], K=3, keig=15).to(cuda).train()
-        out = m(b)
-        loss = torch.nn.functional.l1_loss(out.view(-1), b.y.view(-1))
-        loss.backward()
-        torch.cuda.synchronize()
-        res.append((loss.detach().clone(), {k: p.grad.detach().clone()
-                                            for k, p in m.named_parameters()},
-                    {k: v.detach().clone() for k, v in m.state_dict().items()}))
-        ops.clear_caches()
-    (l1, g1, s1), (l0, g0, s0) = res
-    assert torch.equal(l1, l0)
-    for k in g0:
-        assert torch.equal(g1[k], g0[k]), k
-    for k in s0:
-        assert torch.equal(s1[k], s0[k]), k

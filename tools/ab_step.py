@@ -18,10 +18,6 @@ Variants (A/B hooks, not product settings):
   splitbn     projection + BatchNorm as the projection with a statistics epilogue
               (no wait) + the apply launch
   nobarrier   twolaunchbn + splitbn: no kernel of the step waits for another workgroup
-  nolocal     the polynomial bases as K-1 chained launches (ops.LOCAL_BASIS
-              = False) instead of one launch with a workgroup per graph
-  wdma3/4/0   the Linear backward's weight items staged by LDS-DMA into a 3 / 4
-              deep ring (hlhgat_set_wgrad_stages), or the register ring (0)
 """
 import argparse
 import json
@@ -39,13 +35,8 @@ import torch  # noqa: E402
 
 def set_variant(name, on):
     from hlhgat import ops, _lib
-    if name.startswith("wdma"):
-        _lib.LIB.hlhgat_set_wgrad_stages(int(name[4]) if on else int(
-            os.environ.get("HLHGAT_WGRAD_STAGES", "0")))
-        name = "wdma"
     name = name.rstrip("0123456789")  # base1, base2: repeats of one variant
     ops.CHAINS_ENABLED = not (on and name == "nochain")
-    ops.LOCAL_BASIS = not (on and name == "nolocal")
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
     _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)

@@ -31,13 +31,7 @@ for s in "$@"; do
   case $s in
     sel) step sel 600 $PT tests -m gpu -v -k "$SEL" ;;  # SEL="expr" tools/gpu_steps.sh TAG sel
     cfg3pipe) step cfg3pipe 600 python tools/probes/cfg3_pipe.py --cus "${CUS-0,32,64,128}" --prio "${PRIO-}" --rounds 2 ;;
-    abw5) for r in 1 2; do for v in 0 3 4; do
-           HLHGAT_WGRAD_STAGES=$v step abw5_${v}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abw5_${v}_$r.log | head -1 | sed "s/^/cfg5 wgrad_stages=$v run $r /" >> gpurun_out/${TAG}_abw5.txt || true
-         done; done ;;
-    abstep) step abstep 900 python3 tools/ab_step.py ${AB:-base1 wdma3 wdma4 base2} --rounds 5 ;;
-    localb) for nt in 256 512 1024; do HLHGAT_LOCAL_NT=$nt step localb_$nt 300 python tools/local_bench.py; done ;;
-    wgrad) step wgrad 600 python tools/wgrad_bench.py --stages "${STAGES:-0,3,4,5,6}" ;;
+    abstep) step abstep 900 python3 tools/ab_step.py ${AB:-base1 base2} --rounds 5 ;;
     quick) step quick 300 python bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-replay-census --no-loader --steps 30 ;;
     bn) step bn 600 $PT tests/test_gpu_parity.py -m gpu -v -s -k "bn_ or proj_bn or handover or hog" ;;
     tests) step tests 1100 $PT tests -m gpu -q ;;
