@@ -1510,12 +1510,11 @@ def has_sync_bn(module: torch.nn.Module) -> bool:
 
 _SYNC_WS = {}
 _SYNC_WS_RETIRED = []
-# SyncBatchNorm's statistics all-reduce: "current" = issued on the layer's
-# stream; "own" = from a dedicated collective stream, event-ordered with it.
-# SYNCBN_CHAINS: run SyncBatchNorm models with the persistent node / edge
-# chains (ops.Chains) instead of a fork / join per block (A/B: the
-# round-5 capture segfault, tools/probes/syncbn_capture_probe.py)
-SYNC_BN_STREAM = os.environ.get("HLHGAT_SYNC_BN_STREAM", "current")
+# SYNCBN_CHAINS (probe only): run SyncBatchNorm models with the persistent
+# node / edge chains (ops.Chains) instead of a fork / join per block -- their
+# capture under RCCL segfaults in hipStreamEndCapture (round 5; issuing the
+# statistics all-reduces from one dedicated stream does not change that,
+# round 6: tools/probes/syncbn_capture_probe.py, profiles/r06/)
 SYNCBN_CHAINS = os.environ.get("HLHGAT_SYNCBN_CHAINS", "0") == "1"
 
 
@@ -1549,18 +1548,6 @@ def _sum_over_ranks(t: torch.Tensor, group) -> torch.Tensor:
     if not collectives_on(group):
         return t.view(1, -1)
     out = t.clone()
-    if SYNC_BN_STREAM == "own" and out.is_cuda:
-        # issued from one dedicated stream of the library's own, ordered by
-        # events with the stream the layer runs on (a chain's side stream or
-        # the main one): RCCL's stream then only ever waits on that one stream
-        cur = torch.cuda.current_stream(out.device)
-        cs = own_stream(out.device, "collective")
-        cs.wait_stream(cur)
-        with torch.cuda.stream(cs):
-            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
-        cur.wait_stream(cs)
-        out.record_stream(cur)
-        return out.view(1, -1)
     # on the current stream (a SyncBatchNorm model's block section runs with
     # per-block fork / join, not ops.Chains: see _PyrHead.forward)
     dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)

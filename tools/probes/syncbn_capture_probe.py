@@ -11,9 +11,9 @@ one-rank nccl group, collectives executed) with one thing changed:
   bwdonly     the forward's skipped instead
   chains      the persistent chains forced on (ops.SYNCBN_CHAINS), all-reduce
               on the layer's stream (the round-5 crash)
-  chains_own  chains forced on, every statistics all-reduce issued from one
-              dedicated collective stream (ops.SYNC_BN_STREAM = "own")
-  nochains_own  per-block fork / join, the dedicated collective stream
+  (round 6 also tried every statistics all-reduce issued from one dedicated
+   collective stream, event-ordered with the layer's stream: the chains
+   capture crashed the same way, profiles/r06/syncbn_capture_probe.log)
 
     python tools/probes/syncbn_capture_probe.py [variant ...]
 """
@@ -38,8 +38,6 @@ def child(variant):
     from hlhgat import ops
     if variant.startswith("chains"):
         ops.SYNCBN_CHAINS = True
-    if variant.endswith("_own"):
-        ops.SYNC_BN_STREAM = "own"
     if variant == "nofork":
         ops.set_stream_fork(False)
     elif variant == "nochains":
