@@ -566,7 +566,10 @@ Tensor proj_bn_forward(const std::vector<const float*>& A, const std::vector<int
 // set_bn_relu_x(false) (tests, A/B): the BatchNorm + ReLU backward reads the
 // mask from y instead of recomputing it from x (bitwise the same)
 bool& bn_relu_x_flag() {
-  static bool on = true;
+  static bool on = [] {
+    const char* e = std::getenv("HLHGAT_BN_RELU_X");
+    return !(e && e[0] == '0');
+  }();
   return on;
 }
 void set_bn_relu_x(bool on) { bn_relu_x_flag() = on; }

@@ -31,6 +31,10 @@ for s in "$@"; do
   case $s in
     sel) step sel 600 $PT tests -m gpu -v -k "$SEL" ;;  # SEL="expr" tools/gpu_steps.sh TAG sel
     cfg3pipe) step cfg3pipe 600 python tools/probes/cfg3_pipe.py --cus "${CUS-0,32,64,128}" --prio "${PRIO-}" --rounds 2 ;;
+    ab5env) for r in 1 2; do for v in ${AB5:-0 1}; do  # AB5ENV=NAME: cfg5 step with NAME=v
+           env $AB5ENV=$v timeout -k 10 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline > gpurun_out/${TAG}_ab5env_${v}_$r.log 2>&1
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5env_${v}_$r.log | head -1 | sed "s/^/cfg5 $AB5ENV=$v run $r /" >> gpurun_out/${TAG}_ab5env.txt || true
+         done; done; cat gpurun_out/${TAG}_ab5env.txt ;;
     abstep) step abstep 900 python3 tools/ab_step.py ${AB:-base1 base2} --rounds 5 ;;
     quick) step quick 300 python bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-replay-census --no-loader --steps 30 ;;
     bn) step bn 600 $PT tests/test_gpu_parity.py -m gpu -v -s -k "bn_ or proj_bn or handover or hog" ;;
