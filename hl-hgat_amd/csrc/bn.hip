@@ -220,10 +220,6 @@ struct StatsArgs {
   // last_reduce: one flat pass over the partials up to this many, else the
   // two-level tree (groups of kGroup); kFlatMax except in the backward
   int flat_max;
-  // backward: the ReLU mask recomputed from x and the forward's statistics
-  // ((x - mean) * (w invstd) + bias > 0, the forward's own fp32 operations)
-  // instead of read from y
-  int relu_x;
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -797,20 +793,7 @@ struct BwdApplyArgs {
   const float* coef;
   const float* mean;
   int tpr, rp;
-  // relu_x: the mask from x (see StatsArgs::relu_x), y not read
-  int relu_x;
-  const float* weight;
-  const float* invstd;
-  const float* bias;
 };
-
-// The forward's normalisation of one element, (x - mean) * (w invstd) + b,
-// with the operations every forward path uses (k_bn_apply, k_bn_fwd_grid,
-// k_proj_bn_fwd): its sign is the ReLU mask y > 0 of that forward.
-__device__ __forceinline__ bool relu_open(float x, float mean, float scale, float shift) {
-  const float z = (x - mean) * scale + shift;
-  return z > 0.f;
-}
 
 // Backward statistics (two-launch path): partials of sum(g), sum(g (x - mean));
 // the finalising workgroup of a column tile forms dweight, dbias and dx's
@@ -827,39 +810,31 @@ __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
   if (r_hi > n_eff) r_hi = n_eff;
   double s0[V], s1[V];
-  float mu[V], ms[V], mt[V];
+  float mu[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     s0[v] = s1[v] = 0.0;
-    const bool in = c + v < a.C;
-    mu[v] = in ? a.save_mean[c + v] : 0.f;
-    ms[v] = (in && a.relu_x) ? (a.weight ? a.weight[c + v] : 1.f) * a.save_invstd[c + v] : 0.f;
-    mt[v] = (in && a.relu_x && a.bias) ? a.bias[c + v] : 0.f;
+    mu[v] = (c + v < a.C) ? a.save_mean[c + v] : 0.f;
   }
-  const bool read_y = a.y && !a.relu_x;
   if (c < a.C) {
     auto acc = [&](vt xv, vt gv, vt yv) {
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         float g = vget(gv, v);
-        if (a.relu_x) {
-          if (!relu_open(vget(xv, v), mu[v], ms[v], mt[v])) g = 0.f;
-        } else if (a.y && !(vget(yv, v) > 0.f)) {
-          g = 0.f;
-        }
+        if (a.y && !(vget(yv, v) > 0.f)) g = 0.f;
         s0[v] += (double)g;
         s1[v] += (double)g * (double)(vget(xv, v) - mu[v]);
       }
     };
     int64_t r = r_lo + rg;
-    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows (8-12 loads) in flight
+    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows (12 loads) in flight
       vt xv[4], gv[4], yv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t rr = r + u * a.rp;
         xv[u] = vload<V>(a.x + rr * a.ldx + c);
         gv[u] = vload<V>(a.dy + rr * a.lddy + c);
-        yv[u] = read_y ? vload<V>(a.y + rr * a.ldy + c) : gv[u];
+        if (a.y) yv[u] = vload<V>(a.y + rr * a.ldy + c);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc(xv[u], gv[u], yv[u]);
@@ -868,7 +843,7 @@ __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk
       vt xv = vload<V>(a.x + r * a.ldx + c);
       vt gv = vload<V>(a.dy + r * a.lddy + c);
       vt yv = gv;
-      if (read_y) yv = vload<V>(a.y + r * a.ldy + c);
+      if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
       acc(xv, gv, yv);
     }
   }
@@ -912,17 +887,14 @@ __device__ __forceinline__ void k_bn_bwd_apply_body(const BwdApplyArgs& a, Blk b
   const int rg = threadIdx.x / a.tpr;
   const int c = blk.y * a.tpr * V + cl * V;
   if (c >= a.C) return;
-  float A[V], B[V], Cc[V], mu[V], ms[V], mt[V];
+  float A[V], B[V], Cc[V], mu[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     A[v] = a.coef[c + v];
     B[v] = a.coef[a.C + c + v];
     Cc[v] = a.coef[2 * a.C + c + v];
     mu[v] = a.mean[c + v];
-    ms[v] = a.relu_x ? (a.weight ? a.weight[c + v] : 1.f) * a.invstd[c + v] : 0.f;
-    mt[v] = (a.relu_x && a.bias) ? a.bias[c + v] : 0.f;
   }
-  const bool read_y = a.y && !a.relu_x;
   const int64_t n_eff = eff_rows(a.n, a.nvalid);
   const int64_t r0 = (int64_t)blk.x * a.rp * APPLY_RPT + rg;
   vt xv[APPLY_RPT], gv[APPLY_RPT], yv[APPLY_RPT];
@@ -932,7 +904,7 @@ __device__ __forceinline__ void k_bn_bwd_apply_body(const BwdApplyArgs& a, Blk b
     if (r < n_eff) {
       xv[u] = vload<V>(a.x + r * a.ldx + c);
       gv[u] = vload<V>(a.dy + r * a.lddy + c);
-      if (read_y) yv[u] = vload<V>(a.y + r * a.ldy + c);
+      if (a.y) yv[u] = vload<V>(a.y + r * a.ldy + c);
     }
   }
 #pragma unroll
@@ -943,11 +915,7 @@ __device__ __forceinline__ void k_bn_bwd_apply_body(const BwdApplyArgs& a, Blk b
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float g = vget(gv[u], v);
-      if (a.relu_x) {
-        if (!relu_open(vget(xv[u], v), mu[v], ms[v], mt[v])) g = 0.f;
-      } else if (a.y && !(vget(yv[u], v) > 0.f)) {
-        g = 0.f;
-      }
+      if (a.y && !(vget(yv[u], v) > 0.f)) g = 0.f;
       vget(o, v) = r >= n_eff ? 0.f : A[v] * g + (B[v] * (vget(xv[u], v) - mu[v]) + Cc[v]);
     }
     vstore<V>(a.dx + r * a.lddx + c, o);
@@ -1832,13 +1800,14 @@ extern "C" int hlhgat_proj_bn_fused_capacity(int64_t* out) {
   return HLHGAT_OK;
 }
 
-namespace {
-int bn_bwd_train_impl(const float* x, int64_t ldx, const float* y, int64_t ldy, const float* dy,
-                      int64_t lddy, int64_t n, const int32_t* n_valid, int64_t C,
-                      const float* weight, const float* bias, int relu_x,
-                      const float* save_mean, const float* save_invstd, float* dx, int64_t lddx,
-                      float* dweight, float* dbias, void* workspace, int64_t workspace_bytes,
-                      void* stream) {
+extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
+                                   int64_t ldy, const float* dy, int64_t lddy,
+                                   int64_t n, const int32_t* n_valid, int64_t C,
+                                   const float* weight,
+                                   const float* save_mean, const float* save_invstd,
+                                   float* dx, int64_t lddx, float* dweight,
+                                   float* dbias, void* workspace,
+                                   int64_t workspace_bytes, void* stream) {
   HLH_CHECK_ARG(n >= 1 && C >= 1 && ldx >= C && lddy >= C && lddx >= C && (!y || ldy >= C),
                 "bn_bwd_train: bad sizes");
   HLH_CHECK_ARG(x && dy && dx && save_mean && save_invstd, "bn_bwd_train: NULL pointer");
@@ -1860,12 +1829,10 @@ int bn_bwd_train_impl(const float* x, int64_t ldx, const float* y, int64_t ldy, 
   s.coef = w.coef;
   s.dweight = dweight;
   s.dbias = dbias;
-  s.bias = bias;
-  s.relu_x = relu_x;
   hipStream_t st = as_stream(stream);
   dim3 g1(L.parts, L.tiles);
   {  // algorithmic bytes of the reduction: x, dy (and y for the ReLU mask) read once
-    ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y && !relu_x ? 12.0 : 8.0) * (double)n * C, 0.0);
+    ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
     if (vec)
       launch(k_bn_bwd_reduce<4>, g1, dim3(kThreads), 0, st, &prof, s);
     else
@@ -1873,7 +1840,7 @@ int bn_bwd_train_impl(const float* x, int64_t ldx, const float* y, int64_t ldy, 
   }
   HLH_CHECK_LAUNCH();
   BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, save_mean,
-                 L.tpr, L.rp, relu_x, weight, save_invstd, bias};
+                 L.tpr, L.rp};
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)
     launch(k_bn_bwd_apply<4>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
@@ -1881,33 +1848,6 @@ int bn_bwd_train_impl(const float* x, int64_t ldx, const float* y, int64_t ldy, 
     launch(k_bn_bwd_apply<1>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
-}
-}  // namespace
-
-extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
-                                   int64_t ldy, const float* dy, int64_t lddy,
-                                   int64_t n, const int32_t* n_valid, int64_t C,
-                                   const float* weight,
-                                   const float* save_mean, const float* save_invstd,
-                                   float* dx, int64_t lddx, float* dweight,
-                                   float* dbias, void* workspace,
-                                   int64_t workspace_bytes, void* stream) {
-  return bn_bwd_train_impl(x, ldx, y, ldy, dy, lddy, n, n_valid, C, weight, nullptr, 0,
-                           save_mean, save_invstd, dx, lddx, dweight, dbias, workspace,
-                           workspace_bytes, stream);
-}
-
-extern "C" int hlhgat_bn_bwd_train_relu(const float* x, int64_t ldx, const float* y,
-                                        int64_t ldy, const float* dy, int64_t lddy, int64_t n,
-                                        const int32_t* n_valid, int64_t C, const float* weight,
-                                        const float* bias, const float* save_mean,
-                                        const float* save_invstd, float* dx, int64_t lddx,
-                                        float* dweight, float* dbias, void* workspace,
-                                        int64_t workspace_bytes, void* stream) {
-  HLH_CHECK_ARG(y, "bn_bwd_train_relu: y (the ReLU forward's output) is NULL");
-  return bn_bwd_train_impl(x, ldx, y, ldy, dy, lddy, n, n_valid, C, weight, bias, 1, save_mean,
-                           save_invstd, dx, lddx, dweight, dbias, workspace, workspace_bytes,
-                           stream);
 }
 
 extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y, int64_t ldy,

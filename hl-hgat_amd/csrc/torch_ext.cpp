@@ -563,17 +563,6 @@ Tensor proj_bn_forward(const std::vector<const float*>& A, const std::vector<int
   return y;
 }
 
-// set_bn_relu_x(false) (tests, A/B): the BatchNorm + ReLU backward reads the
-// mask from y instead of recomputing it from x (bitwise the same)
-bool& bn_relu_x_flag() {
-  static bool on = [] {
-    const char* e = std::getenv("HLHGAT_BN_RELU_X");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-void set_bn_relu_x(bool on) { bn_relu_x_flag() = on; }
-
 // returns dx; fills dw/db when requested
 // dx_into: optional [n, C] row-strided destination (e.g. a column slice)
 Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT& w,
@@ -589,19 +578,6 @@ Tensor bn_backward(const Tensor& x, const OptT& y, const Tensor& dy, const OptT&
                                                  : at::empty({C}, x.options()))
               : Tensor();
   Tensor ws = bn_workspace(x, n, C);
-  if (has(y) && bn_relu_x_flag()) {
-    // ReLU mask from x and the statistics (the forward's operations), not y
-    const float* bias = (b_param && b_param->defined()) ? b_param->data_ptr<float>() : nullptr;
-    chk(hlhgat_bn_bwd_train_relu(
-            x.data_ptr<float>(), ld_of(x), fptr(y), ld_of(*y), dyc.data_ptr<float>(), ld_of(dyc),
-            n, valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w), bias,
-            mean.data_ptr<float>(), invstd.data_ptr<float>(), dx.data_ptr<float>(), ld_of(dx),
-            dw.defined() ? dw.data_ptr<float>() : nullptr,
-            db.defined() ? db.data_ptr<float>() : nullptr, ws.data_ptr(), ws.numel(),
-            stream_of(x)),
-        "bn_bwd_train_relu");
-    return dx;
-  }
   chk(hlhgat_bn_bwd_train(x.data_ptr<float>(), ld_of(x), fptr(y), has(y) ? ld_of(*y) : 0,
                           dyc.data_ptr<float>(), ld_of(dyc), n,
                           valid.defined() ? valid.data_ptr<int32_t>() : nullptr, C, fptr(w),
@@ -2430,7 +2406,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_bucket_no_defer", &grad_bucket_no_defer);
   m.def("reduce_defer", &reduce_defer);
   m.def("reduce_flush", &reduce_flush);
-  m.def("set_bn_relu_x", &set_bn_relu_x);
   m.def("node_from_edges", &node_from_edges);
   m.def("edge_from_nodes", &edge_from_nodes);
   m.def("version", []() { return hlhgat_version(); });

@@ -120,9 +120,6 @@ SIGNATURES = {
     "hlhgat_bn_fwd_train": (c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                     c_vp, c_f32, c_f32, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp,
                                     c_i64, c_vp]),
-    "hlhgat_bn_bwd_train_relu": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
-                                         c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
-                                         c_vp, c_i64, c_vp]),
     "hlhgat_bn_bwd_train": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                     c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                     c_vp]),

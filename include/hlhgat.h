@@ -680,20 +680,6 @@ int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y, int64_t ldy
                         const float* save_invstd, float* dx, int64_t lddx,
                         float* dweight, float* dbias, void* workspace,
                         int64_t workspace_bytes, void* stream);
-/* hlhgat_bn_bwd_train after a BatchNorm + ReLU forward, with the ReLU mask
- * recomputed from x and the forward's statistics -- (x - mean) * (weight *
- * invstd) + bias > 0, the forward's fp32 operations, so the same mask as
- * y > 0 -- instead of read from y: 8 instead of 12 bytes per element in the
- * reduction, 12 instead of 16 in the apply (the mask is the backward of
- * lib/Hodge_ST_Model.py:556-566's ReLU).  y must be that forward's output
- * (it fixes the layout, so the results are bitwise hlhgat_bn_bwd_train's);
- * bias NULL = no BatchNorm bias. */
-int hlhgat_bn_bwd_train_relu(const float* x, int64_t ldx, const float* y, int64_t ldy,
-                             const float* dy, int64_t lddy, int64_t n, const int32_t* n_valid,
-                             int64_t C, const float* weight, const float* bias,
-                             const float* save_mean, const float* save_invstd, float* dx,
-                             int64_t lddx, float* dweight, float* dbias, void* workspace,
-                             int64_t workspace_bytes, void* stream);
 
 /* ---- SyncBatchNorm (batch statistics over every data-parallel rank) ----- */
 /* torch.nn.SyncBatchNorm semantics for the BatchNorm1d layers of the path

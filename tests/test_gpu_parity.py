@@ -1753,65 +1753,3 @@ def test_proj_bn_split_bitwise(cuda, M, N, kb, pad):
                                 bn.num_batches_tracked.clone()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("head", ["zinc_padded", "tsp", "pepfunc"])
-def test_bn_relu_mask_from_x_bitwise(cuda, head):
-    """The BatchNorm + ReLU backward with the ReLU mask recomputed from x and
-    the forward's statistics (hlhgat_bn_bwd_train_relu: (x - mean) * (w
-    invstd) + b > 0, the forward's fp32 operations) == the mask read from y,
-    bit for bit: every parameter gradient of a ZINC step on a padded batch
-    (one-launch BatchNorm and projection + BatchNorm, padding rows), the TSP
-    head (two-launch BatchNorm at 10^4 rows) and the peptides attpool head
-    (NodeEdgeInt MLP BatchNorms)."""
-    import hlhgat
-    from hlhgat import ops
-    from hlhgat.synthetic import two_level_batch, tsp_like_graph, zinc_like_batch
-    from hlhgat.hodge_dataset import collate, pad_batch
-    F = torch.nn.functional
-    if head == "zinc_padded":
-        b = zinc_like_batch(60, seed=11)
-        b = pad_batch(b, {"rows_t": b.x_t.size(0) + 100, "rows_s": b.x_s.size(0) + 90,
-                          "nnz_t": b.edge_index_t.size(1) + 400,
-                          "nnz_s": b.edge_index_s.size(1) + 300}).to(cuda)
-
-        def mk():
-            return hlhgat.HL_HGCNN_zinc_dense_int3_pyr(channels=[2, 1], filters=[32, 32],
-                                                       mlp_channels=[64], K=3, keig=15)
-
-        def loss(o):
-            return F.l1_loss(o.view(-1), b.y.view(-1))
-    elif head == "tsp":
-        b = collate([tsp_like_graph(91, n=2500, k=9)], check_hodge=False).to(cuda)
-
-        def mk():
-            return hlhgat.HL_HGCNN_TSP_dense_int3_pyr(channels=[1, 1], filters=[16, 32],
-                                                      mlp_channels=[32], K=3)
-
-        def loss(o):
-            return o[0].float().square().mean()
-    else:
-        b = [x.to(cuda) for x in two_level_batch("peptides", 6, seed=2)]
-
-        def mk():
-            return hlhgat.HL_HGCNN_pepfunc_dense_int3_attpool(
-                channels=[1, 1], filters=[32, 64], mlp_channels=[64], K=3, pool_loc=0)
-
-        def loss(o):
-            return F.binary_cross_entropy_with_logits(o, b[0].y.view(o.shape).float())
-    res = []
-    for flag in (True, False):
-        ops._ext.set_bn_relu_x(flag)
-        try:
-            torch.manual_seed(0)
-            m = mk().to(cuda).train()
-            loss(m(b)).backward()
-            torch.cuda.synchronize()
-            res.append({k: p.grad.detach().clone() for k, p in m.named_parameters()
-                        if p.grad is not None})
-        finally:
-            ops._ext.set_bn_relu_x(True)
-        ops.clear_caches()
-    assert res[0].keys() == res[1].keys() and len(res[0]) > 10
-    for k in res[0]:
-        assert torch.equal(res[0][k], res[1][k]), k

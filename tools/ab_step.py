@@ -18,8 +18,6 @@ Variants (A/B hooks, not product settings):
   splitbn     projection + BatchNorm as the projection with a statistics epilogue
               (no wait) + the apply launch
   nobarrier   twolaunchbn + splitbn: no kernel of the step waits for another workgroup
-  ymask       the BatchNorm + ReLU backward reads the ReLU mask from y (round 5)
-              instead of recomputing it from x
 """
 import argparse
 import json
@@ -39,7 +37,6 @@ def set_variant(name, on):
     from hlhgat import ops, _lib
     name = name.rstrip("0123456789")  # base1, base2: repeats of one variant
     ops.CHAINS_ENABLED = not (on and name == "nochain")
-    ops._ext.set_bn_relu_x(not (on and name == "ymask"))
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
     _lib.LIB.hlhgat_set_proj_bn_fused(0 if (on and name == "nofusedbn") else 1)
     _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
