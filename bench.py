@@ -183,8 +183,36 @@ def loader_leg(ds, step, caps, device, ms_step, steps=16, depth=2, workers=4, st
 
 # kernel classes of the replayed step whose rooflines the bench reports
 # (name regex in the rocprofv3 trace, hlhgat_prof class, bound)
+# k_poly_step's call sites, one hlhgat_prof class each (per-call-site census
+# below); the kernel's roofline sums them, like the rocprof average does
+POLY_SITES = (("Laplacian basis (L0 / L1 Laguerre steps, fwd)", "PROF_POLY"),
+              ("adjoint recurrence (basis backward)", "PROF_POLY_ADJ"),
+              ("|B1| incidence gather (NodeEdgeInt node rows)", "PROF_INCIDENCE"))
+POLY_CLASSES = tuple(c for _, c in POLY_SITES)
+
+
+def prof_sum(L, names):
+    """hlhgat_prof_read summed over the classes `names` (one name or a tuple)"""
+    from hlhgat import ops
+    names = (names,) if isinstance(names, str) else names
+    tot = {"launches": 0, "ms": 0.0, "bytes": 0.0, "flops": 0.0}
+    for nm in names:
+        p = ops.prof_read(getattr(L, nm))
+        for k in tot:
+            tot[k] += p[k]
+    return tot
+
+
+def prof_enable_all(L, names, on):
+    from hlhgat import ops
+    for nm in names:
+        for c in ((nm,) if isinstance(nm, str) else nm):
+            ops.prof_enable(getattr(L, c), on)
+
+
 REPLAY_CLASSES = {
-    "k_poly_step": (r"k_poly_step<", "PROF_POLY", "hbm"),
+    "k_poly_step": (r"k_poly_step<", POLY_CLASSES, "hbm"),
+    "k_edge_gather2": (r"k_edge_gather2<", "PROF_GATHER2", "hbm"),
     "k_proj_bwd_fused": (r"k_proj_bwd_fused<", "PROF_PROJ_BWD", "mfma"),
     "k_proj_fwd": (r"k_proj_fwd", "PROF_PROJ", "mfma"),
     "k_proj_bn_fwd": (r"k_proj_bn_fwd", "PROF_PROJ_BN", "mfma"),
@@ -510,6 +538,16 @@ def isolated_poly_step(device, batch, reps=20, chain=20):
                         "and L1, replayed 20x, events around the replays"}
 
 
+def _site(p, steps):
+    """one call site's census entry: per step launches, time and bytes"""
+    n = max(p["launches"], 1)
+    return {"launches_per_step": round(p["launches"] / steps, 1),
+            "us_per_step": round(p["ms"] * 1e3 / steps, 1),
+            "bytes_per_step": round(p["bytes"] / steps),
+            "avg_launch_us": round(p["ms"] * 1e3 / n, 2),
+            "gbs": round(p["bytes"] / (p["ms"] * 1e-3) / 1e9, 1) if p["ms"] > 0 else None}
+
+
 def kernel_roofline(p, bound, note):
     """roofline entry of one event-stamped kernel class (hlhgat_prof_read)"""
     if not p["launches"] or p["ms"] <= 0:
@@ -578,7 +616,10 @@ def _head_loss(kind, out, datas):
     return F.binary_cross_entropy_with_logits(out, y.view(out.shape).float())  # pepfunc
 
 
-HEAD_PROF = (("k_poly_step", "PROF_POLY", "hbm"), ("hodge_node (factored L1, B1 X)",
+HEAD_PROF = (("k_poly_step (all call sites)", POLY_CLASSES, "hbm"),
+             *((f"k_poly_step: {nm}", c, "hbm") for nm, c in POLY_SITES),
+             ("k_edge_gather2 (edge rows gathering their two node rows)", "PROF_GATHER2", "hbm"),
+             ("hodge_node (factored L1, B1 X)",
              "PROF_HODGE_NODE", "hbm"), ("hodge_edge (factored L1 edge step)", "PROF_HODGE_EDGE",
              "hbm"), ("k_proj_fwd", "PROF_PROJ", "mfma"), ("k_proj_bn_fwd", "PROF_PROJ_BN", "mfma"),
              ("k_proj_bwd_fused", "PROF_PROJ_BWD",
@@ -788,18 +829,16 @@ def heads_leg(device, steps=8, warmup=2, n_batches=8, cpu_budget_s=8.0):
                     st.stats["replay"] == steps + warmup - 1, st.stats
                 # kernel breakdown: one event-stamped eager step of the same model
                 ops.prof_reset()
-                for _, cls, _ in HEAD_PROF:
-                    ops.prof_enable(getattr(L, cls), True)
+                prof_enable_all(L, [cls for _, cls, _ in HEAD_PROF], True)
                 torch.cuda.synchronize()
                 t2 = time.perf_counter()
                 st._eager(batches[0])
                 torch.cuda.synchronize()
                 eager_ms = (time.perf_counter() - t2) * 1e3
-                for _, cls, _ in HEAD_PROF:
-                    ops.prof_enable(getattr(L, cls), False)
+                prof_enable_all(L, [cls for _, cls, _ in HEAD_PROF], False)
                 brk = {}
                 for nm, cls, bound in HEAD_PROF:
-                    kr = kernel_roofline(ops.prof_read(getattr(L, cls)), bound, "")
+                    kr = kernel_roofline(prof_sum(L, cls), bound, "")
                     if kr:
                         kr.pop("what")
                         kr["ms_per_step"] = round(kr["avg_launch_us"] * kr["launches"] / 1e3, 3)
@@ -1145,19 +1184,17 @@ def main():
 
     # roofline pass: eager steps, SpMM / projection / BatchNorm launches event-stamped
     L = hlhgat._lib
-    classes = (L.PROF_POLY, L.PROF_PROJ, L.PROF_PROJ_BWD, L.PROF_PROJ_BN, L.PROF_BN_FWD,
-               L.PROF_BN_BWD)
+    classes = (*POLY_CLASSES, "PROF_GATHER2", "PROF_PROJ", "PROF_PROJ_BWD", "PROF_PROJ_BN",
+               "PROF_BN_FWD", "PROF_BN_BWD")
     ops.prof_reset()
-    for c in classes:
-        ops.prof_enable(c, True)
+    prof_enable_all(L, classes, True)
     for i in range(args.prof_steps):
         step._eager(batches[i % len(batches)])
     torch.cuda.synchronize()
-    for c in classes:
-        ops.prof_enable(c, False)
+    prof_enable_all(L, classes, False)
     ops.check_device_errors()
 
-    poly = ops.prof_read(L.PROF_POLY)
+    poly = prof_sum(L, POLY_CLASSES)
     proj = ops.prof_read(L.PROF_PROJ)
     ms_step = elapsed / args.steps * 1e3
     value = world * GRAPHS_PER_GPU * args.steps / elapsed
@@ -1178,6 +1215,8 @@ def main():
         "launches": poly["launches"],
         "avg_launch_us": round(poly["ms"] * 1e3 / max(poly["launches"], 1), 2),
         "algorithmic_bytes_per_launch": round(poly["bytes"] / max(poly["launches"], 1)),
+        # per call site, per eager step: launches, time, algorithmic bytes
+        "call_sites": {nm: _site(prof_sum(L, c), args.prof_steps) for nm, c in POLY_SITES},
     }
     result = {
         "metric": METRIC,
@@ -1214,7 +1253,10 @@ def main():
             ("k_bn_fwd_grid", L.PROF_BN_FWD, "hbm",
              "BatchNorm forward (statistics + normalise, one launch); bytes 8 n C"),
             ("k_bn_bwd_reduce", L.PROF_BN_BWD, "hbm",
-             "BatchNorm backward statistics; bytes 12 n C (x, dy, y)"))},
+             "BatchNorm backward statistics; bytes 12 n C (x, dy, y)"),
+            ("k_edge_gather2", L.PROF_GATHER2, "hbm",
+             "edge rows gathering their two node rows (NodeEdgeInt x_t2s and the adjoint of "
+             "x_s2t); bytes 16 E + 4 E d (2 gathered + out [+ z] [+ out read])"))},
         "spmm_cfg5": None,
         "heads": None,
         "eval": None,
@@ -1229,7 +1271,7 @@ def main():
         # trace of the replayed workload, work per step from the stamped pass
         eager_work = {}
         for k, (_, cls, _) in REPLAY_CLASSES.items():
-            p = ops.prof_read(getattr(L, cls))
+            p = prof_sum(L, cls)
             if p["launches"]:
                 eager_work[k] = {"bytes": p["bytes"] / args.prof_steps,
                                  "flops": p["flops"] / args.prof_steps,

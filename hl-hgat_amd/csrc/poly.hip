@@ -816,8 +816,9 @@ struct StepRunner {
   const hlhgat_hodge_factor_t* fac;
   float* work;
   hipStream_t s;
+  int prof_class = HLHGAT_PROF_POLY;  // the adjoint recurrence: HLHGAT_PROF_POLY_ADJ
   int operator()(PolyArgs& a) const {
-    return fac ? launch_factored(a, *fac, work, s) : launch_poly(a, nnz, s);
+    return fac ? launch_factored(a, *fac, work, s) : launch_poly(a, nnz, s, prof_class);
   }
 };
 
@@ -859,6 +860,27 @@ extern "C" int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
   a.p = p;
   a.q = q;
   return launch_poly(a, nnz, as_stream(stream));
+}
+
+extern "C" int hlhgat_incidence_step(const int32_t* rowptr, const int32_t* col,
+                                     const float* val, const float* rs, int64_t n_rows,
+                                     int64_t nnz, int64_t n_src, const float* X, int64_t ldx,
+                                     int64_t d, const float* Z, int64_t ldz, float alpha,
+                                     float gamma, float* Y, int64_t ldy, void* stream) {
+  HLH_CHECK_ARG(n_src >= 0, "incidence_step: n_src < 0");
+  PolyArgs a = make_args(rowptr, col, val, n_rows, X, ldx, d, Y, ldy);
+  a.rs = rs;
+  a.Z = Z;
+  a.ldz = ldz;
+  a.alpha = alpha;
+  a.gamma = gamma;
+  a.div = 1.f;
+  // algorithmic bytes: the incidence CSR once, the n_src gathered rows once,
+  // Y written, Z / rs read once
+  const double bytes = (double)nnz * (val ? 8.0 : 4.0) + 4.0 * (double)(n_rows + 1) +
+                       4.0 * (double)n_src * d + 4.0 * (double)n_rows * d * (Z ? 2.0 : 1.0) +
+                       (rs ? 4.0 * (double)n_rows : 0.0);
+  return launch_poly(a, nnz, as_stream(stream), HLHGAT_PROF_INCIDENCE, bytes);
 }
 
 namespace {
@@ -932,7 +954,7 @@ int basis_bwd_core(int kind, const int32_t* rowptr_t, const int32_t* col_t,
   if (K == 1 || n == 0) return HLHGAT_OK;
   HLH_CHECK_ARG(G, "poly_basis_bwd: G is NULL");
   hipStream_t s = as_stream(stream);
-  const StepRunner run{nnz, fac, work, s};
+  const StepRunner run{nnz, fac, work, s, HLHGAT_PROF_POLY_ADJ};
   const int64_t blk = n * F;
   auto Gk = [&](int k) -> float* { return G + (int64_t)k * blk; };
   if (kind == HLHGAT_POLY_LAGUERRE_DEMO) {
@@ -1063,7 +1085,14 @@ extern "C" int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
   const int v = pick_vec(d, {ldx, ldo, z ? ldz : 4}, {x, out, z});
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
-  HLH_DISPATCH_VL(v, l, k_edge_gather2, n_edges, s, a, nullptr);
+  // algorithmic bytes: the edge list, the two gathered rows per
+  // edge, the out rows written (and read when accumulating), z and the scales
+  const double gb = 16.0 * (double)n_edges +
+                    4.0 * (double)n_edges * d * (2.0 + 1.0 + (accumulate ? 1.0 : 0.0) +
+                                                 (z ? 1.0 : 0.0)) +
+                    ((sa ? 4.0 : 0.0) + (sb ? 4.0 : 0.0)) * (double)n_edges;
+  ProfScope prof(HLHGAT_PROF_GATHER2, s, gb, 4.0 * (double)n_edges * d);
+  HLH_DISPATCH_VL(v, l, k_edge_gather2, n_edges, s, a, &prof);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -1363,12 +1363,11 @@ Tensor node_segment(const Tensor& rowptr, const Tensor& eids, int64_t n_nodes, i
                     const Tensor& x, const float* rs, float alpha) {
   Tensor out = at::empty({n_nodes, x.size(1)}, x.options());
   if (n_nodes > 0) {
-    chk(hlhgat_poly_step(rowptr.data_ptr<int>(), n_edges ? eids.data_ptr<int>() : nullptr,
-                         nullptr, rs, n_nodes, 2 * n_edges, nullptr, nullptr, x.data_ptr<float>(),
-                         ld_of(x),
-                         x.size(1), nullptr, 0, nullptr, 0, nullptr, 0, alpha, 0.f, 0.f, 1.f,
-                         0.f, 0.f, out.data_ptr<float>(), ld_of(out), stream_of(x)),
-        "poly_step(incidence)");
+    chk(hlhgat_incidence_step(rowptr.data_ptr<int>(), n_edges ? eids.data_ptr<int>() : nullptr,
+                              nullptr, rs, n_nodes, 2 * n_edges, n_edges, x.data_ptr<float>(),
+                              ld_of(x), x.size(1), nullptr, 0, alpha, 0.f,
+                              out.data_ptr<float>(), ld_of(out), stream_of(x)),
+        "incidence_step");
   }
   return out;
 }
@@ -1662,12 +1661,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
                                   ld_of(h1), 0, stream_of(h1)),
               "edge_gather2");
         else
-          chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr,
-                               nullptr, rD.data_ptr<float>(), n, 2 * E, nullptr, nullptr, pr->p,
-                               pr->ldp, (int)C, pr->z, pr->ldz, nullptr, 0, nullptr, 0, 1.f, 0.f,
-                               1.f, 1.f, 0.f, 0.f, h1.data_ptr<float>(), ld_of(h1),
-                               stream_of(h1)),
-              "poly_step");
+          chk(hlhgat_incidence_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr,
+                                    nullptr, rD.data_ptr<float>(), n, 2 * E, E, pr->p, pr->ldp,
+                                    (int)C, pr->z, pr->ldz, 1.f, 1.f, h1.data_ptr<float>(),
+                                    ld_of(h1), stream_of(h1)),
+              "incidence_step");
       }
       o.a1 = bn_forward(h1, bst, true, o.m1, o.i1);
       Tensor W3 = p[7].stride(1) == 1 ? p[7] : p[7].contiguous();
@@ -1826,13 +1824,11 @@ class NEIntValueFn : public torch::autograd::Function<NEIntValueFn> {
     }
     // dP2[v] = 1/2 sum_{e ni v} dh1_s[e]  -> dYt[:, dn:]
     if (N > 0) {
-      chk(hlhgat_poly_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr, nullptr,
-                           nullptr, N, 2 * E, nullptr, nullptr, dYs.data_ptr<float>(), de + dn,
-                           de,
-                           nullptr, 0,
-                           nullptr, 0, nullptr, 0, 0.5f, 0.f, 0.f, 1.f, 0.f, 0.f,
-                           dYt.data_ptr<float>() + dn, dn + de, fk.main.stream()),
-          "poly_step(nei node bwd)");
+      chk(hlhgat_incidence_step(rowptr.data_ptr<int>(), E ? eids.data_ptr<int>() : nullptr,
+                                nullptr, nullptr, N, 2 * E, E, dYs.data_ptr<float>(), de + dn, de,
+                                nullptr, 0, 0.5f, 0.f, dYt.data_ptr<float>() + dn, dn + de,
+                                fk.main.stream()),
+          "incidence_step(nei node bwd)");
     }
     Tensor dWt, dbt, dWs, dbs;
     std::vector<Tensor> dxt, dxs;

@@ -49,6 +49,8 @@ SIGNATURES = {
     "hlhgat_poly_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp,
                                  c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_f32,
                                  c_f32, c_f32, c_f32, c_f32, c_f32, c_vp, c_i64, c_vp]),
+    "hlhgat_incidence_step": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
+                                      c_i64, c_vp, c_i64, c_f32, c_f32, c_vp, c_i64, c_vp]),
     "hlhgat_poly_basis_fwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
                                       c_vp, c_i64, c_i64, c_i32, c_vp, c_vp]),
     "hlhgat_poly_basis_bwd": (c_i32, [c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp,
@@ -162,6 +164,7 @@ DEVERR_HODGE_SIZE = 2
 BN_LOG_MAX = 64
 PROF_POLY, PROF_PROJ, PROF_HODGE_NODE, PROF_HODGE_EDGE = 0, 1, 2, 3
 PROF_PROJ_BWD, PROF_BN_FWD, PROF_BN_BWD, PROF_PROJ_BN = 4, 5, 6, 7
+PROF_POLY_ADJ, PROF_INCIDENCE, PROF_GATHER2 = 8, 9, 10
 MAX_BLOCKS = 16
 
 

@@ -283,6 +283,16 @@ int hlhgat_poly_step(const int32_t* rowptr, const int32_t* col,
                      float gamma, float div, float p, float q, float* Y,
                      int64_t ldy, void* stream);
 
+/* hlhgat_poly_step over a rectangular incidence operator (rows: n_rows nodes;
+ * columns: the n_src edges, each referenced by exactly two rows): the same
+ * kernel, timed as HLHGAT_PROF_INCIDENCE with the gathered operand counted as
+ * n_src rows (what it reads), not n_rows.  Y = alpha rs (A X) + gamma Z.  Replaces the torch.sparse.mm(|B1|, .) of
+ * lib/Hodge_Cheb_Conv.py:294 (and the node-side adjoint of :295). */
+int hlhgat_incidence_step(const int32_t* rowptr, const int32_t* col, const float* val,
+                          const float* rs, int64_t n_rows, int64_t nnz, int64_t n_src,
+                          const float* X, int64_t ldx, int64_t d, const float* Z, int64_t ldz,
+                          float alpha, float gamma, float* Y, int64_t ldy, void* stream);
+
 /* Polynomial basis T_1..T_{K-1} of X over A (K >= 1; K==1 is a no-op).
  * kind = HLHGAT_POLY_LAGUERRE: T_1 = X - A X,
  *        T_{k+1} = (-A T_k + (2k+1) T_k - k T_{k-1}) / (k+1)
@@ -816,7 +826,16 @@ int hlhgat_test_occupy(int workgroups, int hold, int lds_bytes, unsigned usec, v
 #define HLHGAT_PROF_BN_FWD 5 /* BatchNorm forward: k_bn_fwd_grid / k_bn_stats + k_bn_apply */
 #define HLHGAT_PROF_BN_BWD 6 /* BatchNorm backward: k_bn_bwd_reduce + k_bn_bwd_apply */
 #define HLHGAT_PROF_PROJ_BN 7 /* projection + BatchNorm forward in one launch: k_proj_bn_fwd */
-#define HLHGAT_PROF_NCLASS 8
+/* call sites of k_poly_step beside the Laplacian basis (HLHGAT_PROF_POLY):
+ * the adjoint recurrence of the basis backward (hlhgat_poly_basis_bwd*), and
+ * the |B1| incidence gathers of NodeEdgeInt (hlhgat_incidence_step: node
+ * rows gathering edge rows, x_s2t of lib/Hodge_Cheb_Conv.py:294 and the
+ * node-side adjoint of x_t2s, :295); k_edge_gather2 (edge rows gathering
+ * their two node rows: x_t2s and the adjoint of x_s2t) */
+#define HLHGAT_PROF_POLY_ADJ 8
+#define HLHGAT_PROF_INCIDENCE 9
+#define HLHGAT_PROF_GATHER2 10
+#define HLHGAT_PROF_NCLASS 11
 /* Enable (1) / disable (0) event timing of the given kernel class. */
 int hlhgat_prof_enable(int kernel_class, int enable);
 int hlhgat_prof_reset(void);

@@ -330,6 +330,57 @@ def test_node_edge_int_vs_reference_golden(cuda, name):
         close(p.grad.cpu(), g["grad/" + k], 1e-4, "grad " + k)
 
 
+def test_poly_step_call_site_census(cuda):
+    """Each k_poly_step call site is stamped under its own hlhgat_prof class
+    (the bench's per-call-site census): a Laguerre conv's forward basis under
+    PROF_POLY and its backward under PROF_POLY_ADJ; NodeEdgeInt's |B1| node
+    gathers under PROF_INCIDENCE (counted with the n_src rows they read) and
+    its edge gathers under PROF_GATHER2, none under PROF_POLY."""
+    import hlhgat
+    from hlhgat import _lib, ops
+    classes = (_lib.PROF_POLY, _lib.PROF_POLY_ADJ, _lib.PROF_INCIDENCE, _lib.PROF_GATHER2)
+
+    def census(fn):
+        torch.cuda.synchronize()
+        ops.prof_reset()
+        for c in classes:
+            ops.prof_enable(c, True)
+        fn()
+        torch.cuda.synchronize()
+        for c in classes:
+            ops.prof_enable(c, False)
+        return {c: ops.prof_read(c) for c in classes}
+
+    ei, w = rand_graph(300, 2000, seed=5, sort=True)
+    conv = hlhgat.HodgeLaguerreConv(24, 32, K=4).to(cuda)
+    xd = torch.randn(300, 24, device=cuda, requires_grad=True)
+    got = census(lambda: conv(xd, dev(ei), dev(w)).sum().backward())
+    assert got[_lib.PROF_POLY]["launches"] > 0 and got[_lib.PROF_POLY_ADJ]["launches"] > 0, got
+    assert got[_lib.PROF_INCIDENCE]["launches"] == 0 and got[_lib.PROF_GATHER2]["launches"] == 0
+
+    g = load_golden("nei_value")
+    sd = {k[3:]: T(v) for k, v in g.items() if k.startswith("sd/")}
+    m = hlhgat.NodeEdgeInt(d=sd["WV_Node.0.weight"].shape[1] // 2,
+                           dv=sd["WV_Node.3.weight"].shape[0])
+    m.load_state_dict(sd)
+    m = m.to(cuda).train()
+    x_t = dev(g["x_t"]).requires_grad_(True)
+    x_s = dev(g["x_s"]).requires_grad_(True)
+    par = hlhgat.adj2par1(dev(g["edge_index"]), x_t.shape[0], x_s.shape[0])
+
+    def nei():
+        a, c = m(x_t, x_s, par, dev(g["D"]))
+        (a.sum() + c.sum()).backward()
+    got = census(nei)
+    inc = got[_lib.PROF_INCIDENCE]
+    assert inc["launches"] >= 2 and got[_lib.PROF_GATHER2]["launches"] >= 1, got
+    assert got[_lib.PROF_POLY]["launches"] == 0 and got[_lib.PROF_POLY_ADJ]["launches"] == 0
+    # the gathered operand is the edge side: at least 4 n_edges d bytes a launch
+    E = x_s.shape[0]
+    assert inc["bytes"] / inc["launches"] >= 4.0 * E * 1, inc
+    ops.check_device_errors()
+
+
 def test_incidence_gathers_bitexact(cuda):
     from hlhgat import ops
     from hlhgat.synthetic import zinc_like_batch

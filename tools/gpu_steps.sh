@@ -10,6 +10,7 @@
 #   pmcstep the config-2 step under rocprofv3 --pmc (serialised dispatch)
 #   prof    rocprofv3 kernel stats + step census of the replayed bench
 #   pmc     FETCH / WRITE passes for the roofline traffic
+#   census  bench line with heads: k_poly_step per call site (tools/poly_census.py)
 # Stops at the first crash / time-out.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -72,7 +73,15 @@ for s in "$@"; do
          python tools/pmc_traffic.py $(find gpurun_out/pmcf -name '*counter_collection.csv' | head -1) $(find gpurun_out/pmcw -name '*counter_collection.csv' | head -1) --kernel k_poly_step --kernel k_proj_fwd --kernel k_edge_gather2 --kernel k_bn_fwd_grid --kernel k_bn_bwd_reduce --kernel k_proj_bwd_fused --kernel k_proj_bn_fwd --out gpurun_out/${TAG}_pmc_traffic.json --label "$TAG bench.py --eager cfg2 step" > /dev/null || true
          rm -rf gpurun_out/pmcf gpurun_out/pmcw
          # the bench reads the newest profiles/*_pmc_traffic.json: this round's
-         cp gpurun_out/${TAG}_pmc_traffic.json profiles/r05_pmc_traffic.json || true ;;
+         cp gpurun_out/${TAG}_pmc_traffic.json profiles/r06_pmc_traffic.json || true ;;
+    census) step census 900 python3 bench.py --no-cpu-baseline --no-loader --no-parity-check --steps 20
+          python3 tools/poly_census.py gpurun_out/${TAG}_census.log > gpurun_out/${TAG}_poly_census.txt || true ;;
+    census1) HLHGAT_STREAM_FORK=0 step census1 900 python3 bench.py --no-cpu-baseline --no-loader --no-parity-check --no-replay-census --steps 10
+          python3 tools/poly_census.py gpurun_out/${TAG}_census1.log > gpurun_out/${TAG}_poly_census_1stream.txt || true ;;
+    fcalib) rm -rf gpurun_out/${TAG}_fc
+          step fcalib 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fc -o f --output-format csv -- python3 tools/probes/fetch_calib.py run --meta gpurun_out/${TAG}_fc_meta.json
+          python3 tools/probes/fetch_calib.py parse $(find gpurun_out/${TAG}_fc -name '*counter_collection.csv' | head -1) --meta gpurun_out/${TAG}_fc_meta.json > gpurun_out/${TAG}_fetch_calib.json || true
+          rm -rf gpurun_out/${TAG}_fc ;;
     listctr) timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1; echo "=== listctr rc=$?" ;;
     heads) step heads 600 $PT tests -m gpu -v -k "reference_golden or state_dict" ;;
     pmcgemm) # SQ counters of k_proj_bwd_fused: isolated (kbench) and in the replayed step
