@@ -38,6 +38,7 @@
 // ticket; readers use agent-scope atomic loads.
 #include "gemm_core.h"
 
+#include <atomic>
 #include <cstdlib>
 
 using namespace hlhgat;
@@ -798,7 +799,7 @@ struct BwdApplyArgs {
 // Backward statistics (two-launch path): partials of sum(g), sum(g (x - mean));
 // the finalising workgroup of a column tile forms dweight, dbias and dx's
 // coefficients.
-template <int V>
+template <int V, int RB>
 __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
@@ -826,25 +827,23 @@ __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk
         s1[v] += (double)g * (double)(vget(xv, v) - mu[v]);
       }
     };
-    int64_t r = r_lo + rg;
-    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows (12 loads) in flight
-      vt xv[4], gv[4], yv[4];
+    // RB rows (3 RB loads) in flight per batch, the batch's tail rows
+    // predicated in the same batch (one memory round trip per batch; the
+    // rows are still summed in ascending order, so any RB gives the same bits)
+    for (int64_t r = r_lo + rg; r < r_hi; r += RB * a.rp) {
+      vt xv[RB], gv[RB], yv[RB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RB; ++u) {
         const int64_t rr = r + u * a.rp;
-        xv[u] = vload<V>(a.x + rr * a.ldx + c);
-        gv[u] = vload<V>(a.dy + rr * a.lddy + c);
-        if (a.y) yv[u] = vload<V>(a.y + rr * a.ldy + c);
+        if (rr < r_hi) {
+          xv[u] = vload<V>(a.x + rr * a.ldx + c);
+          gv[u] = vload<V>(a.dy + rr * a.lddy + c);
+          yv[u] = a.y ? vload<V>(a.y + rr * a.ldy + c) : gv[u];
+        }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc(xv[u], gv[u], yv[u]);
-    }
-    for (; r < r_hi; r += a.rp) {
-      vt xv = vload<V>(a.x + r * a.ldx + c);
-      vt gv = vload<V>(a.dy + r * a.lddy + c);
-      vt yv = gv;
-      if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
-      acc(xv, gv, yv);
+      for (int u = 0; u < RB; ++u)
+        if (r + u * a.rp < r_hi) acc(xv[u], gv[u], yv[u]);
     }
   }
   write_partials<V, kThreads>(s0, s1, a, c0, blk);
@@ -875,9 +874,38 @@ __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk
   }
 }
 
-template <int V>
+template <int V, int RB>
 __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
-  k_bn_bwd_reduce_body<V>(a, blk_hw());
+  k_bn_bwd_reduce_body<V, RB>(a, blk_hw());
+}
+
+// rows per batch of the backward reduction: 4, or 8 (HLHGAT_BN_BWD_RB=8 /
+// hlhgat_set_bn_bwd_rows; bitwise the same results).  Same-box A/B, round 6
+// (profiles/r06/ab_bn_bwd_rows.txt): config 2 2.757 (8) vs 2.748-2.755 ms,
+// config 5 36.75-36.80 (8) vs 36.56-36.61 ms -- 4 stays.
+std::atomic<int> g_bn_bwd_rb{0};
+int bn_bwd_rb() {
+  int v = g_bn_bwd_rb.load(std::memory_order_relaxed);
+  if (v == 0) {
+    const char* e = std::getenv("HLHGAT_BN_BWD_RB");
+    v = (e && std::atoi(e) == 8) ? 8 : 4;
+    int expect = 0;
+    g_bn_bwd_rb.compare_exchange_strong(expect, v);
+    v = g_bn_bwd_rb.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+
+void launch_bwd_reduce(bool vec, dim3 grid, hipStream_t st, ProfScope* prof, const StatsArgs& s) {
+  const int rb = bn_bwd_rb();
+  if (vec && rb == 8)
+    launch(k_bn_bwd_reduce<4, 8>, grid, dim3(kThreads), 0, st, prof, s);
+  else if (vec)
+    launch(k_bn_bwd_reduce<4, 4>, grid, dim3(kThreads), 0, st, prof, s);
+  else if (rb == 8)
+    launch(k_bn_bwd_reduce<1, 8>, grid, dim3(kThreads), 0, st, prof, s);
+  else
+    launch(k_bn_bwd_reduce<1, 4>, grid, dim3(kThreads), 0, st, prof, s);
 }
 
 template <int V>
@@ -1834,9 +1862,9 @@ extern "C" int hlhgat_bn_bwd_train(const float* x, int64_t ldx, const float* y,
   {  // algorithmic bytes of the reduction: x, dy (and y for the ReLU mask) read once
     ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
     if (vec)
-      launch(k_bn_bwd_reduce<4>, g1, dim3(kThreads), 0, st, &prof, s);
+      launch_bwd_reduce(true, g1, st, &prof, s);
     else
-      launch(k_bn_bwd_reduce<1>, g1, dim3(kThreads), 0, st, &prof, s);
+      launch_bwd_reduce(false, g1, st, &prof, s);
   }
   HLH_CHECK_LAUNCH();
   BwdApplyArgs p{n_valid, x, ldx, y, ldy, dy, lddy, dx, lddx, n, (int)C, w.coef, save_mean,
@@ -1881,9 +1909,9 @@ extern "C" int hlhgat_bn_bwd_reduce(const float* x, int64_t ldx, const float* y,
   hipStream_t st = as_stream(stream);
   ProfScope prof(HLHGAT_PROF_BN_BWD, st, (y ? 12.0 : 8.0) * (double)n * C, 0.0);
   if (vec)
-    launch(k_bn_bwd_reduce<4>, dim3(L.parts, L.tiles), dim3(kThreads), 0, st, &prof, s);
+    launch_bwd_reduce(true, dim3(L.parts, L.tiles), st, &prof, s);
   else
-    launch(k_bn_bwd_reduce<1>, dim3(L.parts, L.tiles), dim3(kThreads), 0, st, &prof, s);
+    launch_bwd_reduce(false, dim3(L.parts, L.tiles), st, &prof, s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -1993,9 +2021,9 @@ extern "C" int hlhgat_bn_sums_bwd(const float* x, int64_t ldx, const float* y, i
   s.sums_out = sums;
   dim3 g1(L.parts, L.tiles);
   if (vec)
-    launch(k_bn_bwd_reduce<4>, dim3(g1), dim3(kThreads), 0, as_stream(stream), nullptr, s);
+    launch_bwd_reduce(true, dim3(g1), as_stream(stream), nullptr, s);
   else
-    launch(k_bn_bwd_reduce<1>, dim3(g1), dim3(kThreads), 0, as_stream(stream), nullptr, s);
+    launch_bwd_reduce(false, dim3(g1), as_stream(stream), nullptr, s);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }
@@ -2047,6 +2075,12 @@ extern "C" int hlhgat_set_bn_one_launch(int on) {
 }
 
 extern "C" int hlhgat_get_bn_one_launch(void) { return bn_one_launch_flag() ? 1 : 0; }
+
+extern "C" int hlhgat_set_bn_bwd_rows(int rows) {
+  HLH_CHECK_ARG(rows == 4 || rows == 8, "set_bn_bwd_rows: rows must be 4 or 8");
+  g_bn_bwd_rb.store(rows, std::memory_order_relaxed);
+  return HLHGAT_OK;
+}
 
 extern "C" int hlhgat_set_bn_wait_us(unsigned wait_us) {
   g_wait_us = wait_us;

@@ -125,10 +125,6 @@ for s in "$@"; do
            step abload_$d 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --loader-depth $d
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']; print('depth', sys.argv[2], r['ms_per_step'], L['loader_fed']['ms_per_step'], round(r['ms_per_step']/L['loader_fed']['ms_per_step'],3), L['loader_fed']['host_ms_per_step'])" gpurun_out/${TAG}_abload_$d.log $d >> gpurun_out/${TAG}_abload.txt || true
          done ;;
-    abfused) for r in 1 2; do for v in 384:0 384:1 360:0 360:1; do t=${v%%:*}; g=${v##*:}
-           HLHGAT_WSPLIT_TARGET=$t HLHGAT_MERGE_GUARD=$g step abfused_${t}_${g}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abfused_${t}_${g}_$r.log | sed "s/^/target=$t guard=$g run $r /" >> gpurun_out/${TAG}_abfused.txt || true
-         done; done ;;
     abbn) for r in 1 2; do for v in 128 64 256 512; do
            HLHGAT_BN_BWD_PARTS=$v step abbn_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abbn_${v}_$r.log | sed "s/^/bwd_parts=$v run $r /" >> gpurun_out/${TAG}_abbn.txt || true
@@ -145,71 +141,15 @@ for s in "$@"; do
            HLHGAT_WSPLIT_TARGET=$t HLHGAT_BN_BWD_FLAT_MAX=$fm step abnew_${t}_${fm}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abnew_${t}_${fm}_$r.log | sed "s/^/wsplit=$t flat_max=$fm run $r /" >> gpurun_out/${TAG}_abnew.txt || true
          done; done ;;
-    abload2) for r in 1 2; do for v in dflt sdma1 sdma0; do
-           case $v in dflt) E="";; sdma1) E="HSA_ENABLE_SDMA=1";; sdma0) E="HSA_ENABLE_SDMA=0";; esac
-           step abload2_${v}_$r 400 env $E python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --loader-depth 2
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']; print(sys.argv[2], r['ms_per_step'], L['loader_fed']['ms_per_step'], round(r['ms_per_step']/L['loader_fed']['ms_per_step'],3), L['loader_fed']['host_ms_per_step'], r['h2d'])" gpurun_out/${TAG}_abload2_${v}_$r.log $v >> gpurun_out/${TAG}_abload2.txt || true
-         done; done ;;
-    abload3) for r in 1 2; do for v in s4 e4 s2; do
-           case $v in s4) A="--loader-workers 4";; s2) A="--loader-workers 2";; s1) A="--loader-workers 1";; e4) A="--loader-workers 4 --loader-per-epoch";; e2) A="--loader-workers 2 --loader-per-epoch";; esac
-           step abload3_${v}_$r 400 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census $A
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'))" gpurun_out/${TAG}_abload3_${v}_$r.log $v >> gpurun_out/${TAG}_abload3.txt || true
-         done; done ;;
-    abload4) for r in 1 2; do for v in base hi sw hisw; do
-           case $v in base) A="";; hi) A="--loader-priority -1";; sw) A="--loader-switch-ms 0.5";; hisw) A="--loader-priority -1 --loader-switch-ms 0.5";; esac
-           step abload4_${v}_$r 400 python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'))" gpurun_out/${TAG}_abload4_${v}_$r.log $v >> gpurun_out/${TAG}_abload4.txt || true
-         done; done ;;
-    abload5) for r in 1 2; do for v in base q8 q16 sw; do
-           case $v in base) E=""; A="";; q8) E="GPU_MAX_HW_QUEUES=8"; A="";; q16) E="GPU_MAX_HW_QUEUES=16"; A="";; sw) E=""; A="--loader-switch-ms 0.5";; esac
-           step abload5_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload5_${v}_$r.log $v >> gpurun_out/${TAG}_abload5.txt || true
-         done; done ;;
-    abload6) for r in 1 2; do for v in base sl4 sl5 d3sl5; do
-           case $v in base) A="";; sl4) A="--loader-slots 4";; sl5) A="--loader-slots 5";; d3sl5) A="--loader-depth 3 --loader-slots 5";; esac
-           step abload6_${v}_$r 400 python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload6_${v}_$r.log $v >> gpurun_out/${TAG}_abload6.txt || true
-         done; done ;;
-    abload7) for r in 1 2; do for v in base in1 in2 in2sw; do
-           case $v in base) A="";; in1) A="--loader-inline --loader-depth 1";; in2) A="--loader-inline";; in2sw) A="--loader-inline --loader-switch-ms 0.5";; esac
-           step abload7_${v}_$r 400 python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload7_${v}_$r.log $v >> gpurun_out/${TAG}_abload7.txt || true
-         done; done ;;
-    abload8) for r in 1 2; do for v in base raw rawin in2; do
-           case $v in base) E=""; A="";; raw) E="HLHGAT_STAGE_COPY=raw"; A="";; rawin) E="HLHGAT_STAGE_COPY=raw"; A="--loader-inline";; in2) E=""; A="--loader-inline";; esac
-           step abload8_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
-           python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload8_${v}_$r.log $v >> gpurun_out/${TAG}_abload8.txt || true
-         done; done ;;
     abload9) for r in 1 2; do for v in base host hostsl4 devsl4; do
            case $v in base) E=""; A="";; host) E="HLHGAT_STAGE_WAIT=host"; A="";; hostsl4) E="HLHGAT_STAGE_WAIT=host"; A="--loader-slots 4";; devsl4) E=""; A="--loader-slots 4";; esac
            step abload9_${v}_$r 400 env $E python3 bench.py --no-heads --no-cpu-baseline --no-replay-census $A
            python3 -c "import json,sys; r=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]; L=r['loader']['loader_fed']; print(sys.argv[2], r['ms_per_step'], L['ms_per_step'], round(r['ms_per_step']/L['ms_per_step'],3), L['host_ms_per_step'], L.get('feeder_ms_per_batch'), L.get('stage_ms_per_batch'))" gpurun_out/${TAG}_abload9_${v}_$r.log $v >> gpurun_out/${TAG}_abload9.txt || true
          done; done ;;
-    abskipw) for r in 1 2; do for v in 0 1; do
-           HLHGAT_DEBUG_SKIP_WEIGHT=$v step abskipw_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abskipw_${v}_$r.log | sed "s/^/skip_weight=$v run $r /" >> gpurun_out/${TAG}_abskipw.txt || true
-         done; done ;;
-    wstest) step wstest 400 $PT tests/test_train_step.py -m gpu -v -k "weight_stream or deferred or staged_feed" ;;
-    abws2) for r in 1 2 3; do for v in 0 1; do
-           HLHGAT_WEIGHT_STREAM=$v step abws2_${v}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abws2_${v}_$r.log | sed "s/^/weight_stream=$v run $r /" >> gpurun_out/${TAG}_abws2.txt || true
-         done; done ;;
-    abws5) for r in 1 2; do for v in 0 1; do
-           HLHGAT_WEIGHT_STREAM=$v step abws5_${v}_$r 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abws5_${v}_$r.log | head -1 | sed "s/^/cfg5 weight_stream=$v run $r /" >> gpurun_out/${TAG}_abws5.txt || true
-         done; done ;;
     abopsf) for r in 1 2; do for w in cfg5 cfg3; do for o in x f; do
            HLHGAT_GEMM_BIG=-1 HLHGAT_GEMM_BIG_OPS=$o step abopsf_${w}_${o}_$r 400 python3 bench.py --workload $w --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abopsf_${w}_${o}_$r.log | head -1 | sed "s/^/$w ops=$o run $r /" >> gpurun_out/${TAG}_abopsf.txt || true
          done; done; done ;;
-    abwsf) for r in 1 2; do for v in 1:0 0:0 0:1; do f=${v%%:*}; w=${v##*:}
-           HLHGAT_STREAM_FORK=$f HLHGAT_WEIGHT_STREAM=$w step abwsf_${f}_${w}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abwsf_${f}_${w}_$r.log | sed "s/^/fork=$f weight_stream=$w run $r /" >> gpurun_out/${TAG}_abwsf.txt || true
-         done; done ;;
-    abwshi) for r in 1 2; do for v in 0:0 1:0 1:1; do w=${v%%:*}; h=${v##*:}
-           HLHGAT_WEIGHT_STREAM=$w HLHGAT_WEIGHT_STREAM_HI=$h step abwshi_${w}_${h}_$r 300 python3 bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-parity-check --no-replay-census --no-loader --steps 30
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_abwshi_${w}_${h}_$r.log | sed "s/^/weight_stream=$w high_prio=$h run $r /" >> gpurun_out/${TAG}_abwshi.txt || true
-         done; done ;;
     syncprobe) step syncprobe 900 python3 tools/probes/syncbn_capture_probe.py ${PROBE:-} ;;
     hog) step hog 300 python3 tools/probes/hog_probe.py ;;
     rccl) step rccl 600 $PT tests/test_rccl_capture.py tests/test_sync_bn.py tests/test_train_step.py -m gpu -v -k "rccl or sync or staged" ;;
@@ -219,13 +159,6 @@ for s in "$@"; do
     big) step bigtests 400 $PT tests/test_proj_big.py -m gpu -v -s
          step bigbench 400 python3 tools/kbench.py --big --reps 10 --chain 5 ;;
     kbench) step kbench 300 python3 tools/kbench.py --only "proj" --reps 20 --chain 20 ;;
-    wsweep) # weight-item shape sweep of the fused Linear backward (kbench, isolated)
-         for wt in 1 2 3 4; do for it in 256 384 512; do
-           echo "=== WT=$wt WITEMS=$it" >> gpurun_out/${TAG}_wsweep.log
-           HLHGAT_WT=$wt HLHGAT_WITEMS=$it timeout -k 10 120 python3 tools/kbench.py --only "proj_bwd_fused" --reps 10 --chain 10 >> gpurun_out/${TAG}_wsweep.log 2>&1 || { echo "wsweep failed"; exit 3; }
-         done; done
-         echo "=== wsweep done" ;;
-    wtests) step wtests 600 env HLHGAT_WT=3 $PT tests/test_gpu_parity.py -m gpu -q -k "fused or proj or linear" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -14,7 +14,12 @@ def main(path):
         rows.append(("cfg2", nm, e["launches_per_step"], e["us_per_step"],
                      e["bytes_per_step"], e["gbs"]))
     g2 = (r.get("rooflines") or {}).get("k_edge_gather2")
-    if g2:  # the replayed step's entry (per step)
+    if g2 and "launches_per_step" not in g2:  # eager stamps (--no-replay-census)
+        n = 3  # the bench's --prof-steps default
+        rows.append(("cfg2", "k_edge_gather2 (eager)", round(g2["launches"] / n, 1),
+                     round(g2["avg_launch_us"] * g2["launches"] / n, 1),
+                     round(g2["per_launch"] * g2["launches"] / n), g2["achieved"]))
+    elif g2:  # the replayed step's entry (per step)
         rows.append(("cfg2", "k_edge_gather2 (replayed)", g2["launches_per_step"],
                      g2["time_per_step_us"], g2["work_per_step"], g2["achieved"]))
     for head, h in (r.get("heads") or {}).items():
