@@ -1249,7 +1249,20 @@ struct ProjBnArgs {
   FwdArgs g;    // the projection: g.C = x (pre-BatchNorm), g.ldc
   StatsArgs s;  // the BatchNorm: s.out = y, partials / counters / error word
   int stats_only;  // 1: no wait -- the finaliser writes the statistics, k_bn_apply follows
+  // diagnostics (hlhgat_set_proj_bn_stamps): 8 words per workgroup, thread 0
+  // stamps s_memrealtime (100 MHz) at each phase boundary; NULL = off
+  unsigned long long* stamps;
 };
+
+// one phase stamp of k_proj_bn_fwd (a plain vector store from one lane); a
+// separate instantiation (STAMPS), so the product kernel keeps its registers
+// (the stamps cost the 4th resident workgroup per CU)
+template <bool STAMPS>
+__device__ __forceinline__ void pb_stamp(const ProjBnArgs& a, int k, unsigned long long v) {
+  if (STAMPS && a.stamps && threadIdx.x == 0)
+    a.stamps[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + k] = v;
+}
+__device__ __forceinline__ unsigned long long pb_now() { return __builtin_amdgcn_s_memrealtime(); }
 
 constexpr int kPbTN = 4;  // 64 columns per workgroup: one BatchNorm column tile
 
@@ -1257,6 +1270,7 @@ __device__ __forceinline__ unsigned long long* gen_word(const StatsArgs& a, int 
   return reinterpret_cast<unsigned long long*>(a.count + kGridBase) + tile;
 }
 
+template <bool STAMPS>
 __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   __shared__ __attribute__((aligned(16))) float wl[2][kPbTN * 16][KCP];
   __shared__ unsigned s_gen0, s_ok;
@@ -1268,7 +1282,9 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   const int64_t m_base = ((int64_t)bx * 4 + wave) * 16;
   const int n_base = by * (kPbTN * 16);
   floatx4 acc[kPbTN];
+  pb_stamp<STAMPS>(a, 0, pb_now());
   proj_fwd_lds_mainloop<kPbTN>(g, bx, by, wl, acc);
+  pb_stamp<STAMPS>(a, 1, pb_now());
   // x = acc + bias, as store_tile_rows adds it
   if (g.bias) {
 #pragma unroll
@@ -1285,8 +1301,11 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   double* sum0 = red + 2 * 4 * 64;  // [64]
   double* sum1 = sum0 + 64;         // [64]
   const bool vx = (g.ldc % 4) == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0;
-  store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr, 0,
-                         vx);
+  // x is stored AFTER the partials are in (below): the statistics chain does
+  // not wait for the x stores to drain (arrive_last waits for every store).
+  // Round 6: bitwise the round-5 order (x first, running statistics before
+  // the bump), ~1 us less per launch alone, neutral in the config-2 step
+  // (profiles/r06/ab_proj_bn_order.txt, proj_bn_phases.log)
   const int64_t n_eff = eff_rows(s.n, s.nvalid);
 #pragma unroll
   for (int tn = 0; tn < kPbTN; ++tn) {
@@ -1328,7 +1347,10 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   const int first = grp * kGroup;
   const int cnt = parts - first < kGroup ? parts - first : kGroup;
   bool top = false;
-  if (arrive_last(s.count + kMaxTiles + by * kMaxGroups + grp, (unsigned)cnt, s.err)) {
+  pb_stamp<STAMPS>(a, 2, pb_now());
+  const bool grp_last = arrive_last(s.count + kMaxTiles + by * kMaxGroups + grp, (unsigned)cnt,
+                                    s.err);
+  if (grp_last) {
     reduce_range<kThreads>(s.part, first, cnt, s, n_base, 64, sum0, sum1);
     if (threadIdx.x < 64) {
       double* dst = s.gpart + ((int64_t)grp * s.C + n_base + threadIdx.x) * 2;
@@ -1337,9 +1359,19 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
     }
     top = arrive_last(s.count + by, (unsigned)ng, s.err);
   }
+  pb_stamp<STAMPS>(a, 3, pb_now());
+  pb_stamp<STAMPS>(a, 6, (grp_last ? 1ull : 0ull) | (top ? 2ull : 0ull));
   float* sm = reinterpret_cast<float*>(sum1 + 64);  // [64]
   float* ss = sm + 64;                              // [64]
   unsigned long long* tile_slots = s.slots + (int64_t)by * gridDim.x;
+  if (!top) {
+    // x, drained before a possible give-up: the finaliser normalises a
+    // given-up tile from it (give_up's release is thread 0's)
+    store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr,
+                           0, vx);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   if (a.stats_only) {  // x and the statistics only: nobody waits (k_bn_apply normalises)
     if (!top) return;
     reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
@@ -1351,6 +1383,8 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
       s.save_invstd[cc] = is;
     }
     if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
+    store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr,
+                           0, vx);
     return;
   }
   if (top) {
@@ -1358,7 +1392,7 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
     if (threadIdx.x < 64) {
       const int cc = n_base + threadIdx.x;
       float m, is;
-      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, true);
+      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, false);
       __hip_atomic_store(reinterpret_cast<unsigned*>(s.save_mean + cc), __float_as_uint(m),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(reinterpret_cast<unsigned*>(s.save_invstd + cc), __float_as_uint(is),
@@ -1366,7 +1400,6 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
       sm[threadIdx.x] = m;
       ss[threadIdx.x] = is;
     }
-    if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {  // seq_cst, completed and fenced (see bar_wait)
@@ -1375,9 +1408,22 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     }
+    pb_stamp<STAMPS>(a, 4, pb_now());
+    // off the waiting workgroups' path: the running statistics (the same
+    // finalisation arithmetic, now with the update), the batch counter, and
+    // the finaliser's own x
+    if (threadIdx.x < 64) {
+      float m, is;
+      fwd_finalize(s, n_base + threadIdx.x, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is,
+                   true);
+    }
+    if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
+    store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr,
+                           0, vx);
   } else {
     if (threadIdx.x == 0) {
       unsigned ok = poll_gen(word, s_gen0, s.wait_us) ? 1u : 0u;
+      pb_stamp<STAMPS>(a, 4, pb_now());
       if (!ok)
         ok = give_up(word, tile_slots + bx, s_gen0, kKidProjBn, s.count + by, false,
                      (unsigned)ng, s.wait_us)
@@ -1413,6 +1459,7 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   const bool vy = (s.ldo % 4) == 0 && (reinterpret_cast<uintptr_t>(s.out) & 15) == 0;
   store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, s.out + n_base, s.ldo, kPbTN * 16, nullptr,
                          0, vy);
+  pb_stamp<STAMPS>(a, 5, pb_now());
   if (!top) return;
   // row blocks whose owners gave up: y from the x they stored, same operations
   __shared__ unsigned char taken[kMaxParts];
@@ -1708,6 +1755,16 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
 // Projection + BatchNorm (+ ReLU) forward (see k_proj_bn_fwd): one launch where
 // the projection's grid fits co-resident, else hlhgat_proj_fwd then
 // hlhgat_bn_fwd_train on x.
+unsigned long long* g_pb_stamps = nullptr;
+int64_t g_pb_stamps_words = 0;
+
+extern "C" int hlhgat_set_proj_bn_stamps(void* buf, int64_t words) {
+  HLH_CHECK_ARG(words >= 0 && (buf != nullptr || words == 0), "set_proj_bn_stamps: bad buffer");
+  g_pb_stamps = reinterpret_cast<unsigned long long*>(buf);
+  g_pb_stamps_words = words;
+  return HLHGAT_OK;
+}
+
 extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int64_t* lda,
                                   const float* const* W, const int64_t* ldw, const int64_t* kb,
                                   int64_t M, int64_t N, const float* bias, float* x, int64_t ldx,
@@ -1738,7 +1795,7 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   bool fused = proj_bn_fused_flag() && vec && N % 64 == 0 && gy <= (unsigned)kMaxTiles &&
                gx <= (unsigned)kMaxParts && (int64_t)gx * gy <= kMaxSlots;
   if (fused) {
-    const int64_t cap = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd));
+    const int64_t cap = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd<false>));
     fused = (int64_t)gx * gy <= cap;
   }
   if (!fused) {
@@ -1792,9 +1849,13 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   hipStream_t st = as_stream(stream);
   const bool split = proj_bn_split_flag();
   a.stats_only = split ? 1 : 0;
+  if (g_pb_stamps && g_pb_stamps_words >= (int64_t)gx * gy * 8) a.stamps = g_pb_stamps;
   {
     ProfScope prof(HLHGAT_PROF_PROJ_BN, st, bytes, flops);
-    launch(k_proj_bn_fwd, dim3(gx, gy), dim3(kThreads), 0, st, &prof, a);
+    if (a.stamps)
+      launch(k_proj_bn_fwd<true>, dim3(gx, gy), dim3(kThreads), 0, st, &prof, a);
+    else
+      launch(k_proj_bn_fwd<false>, dim3(gx, gy), dim3(kThreads), 0, st, &prof, a);
   }
   HLH_CHECK_LAUNCH();
   if (split) {
@@ -1824,7 +1885,7 @@ extern "C" int hlhgat_set_proj_bn_fused(int on) {
 
 extern "C" int hlhgat_proj_bn_fused_capacity(int64_t* out) {
   HLH_CHECK_ARG(out, "proj_bn_fused_capacity: NULL pointer");
-  *out = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd));
+  *out = capacity_of(reinterpret_cast<const void*>(k_proj_bn_fwd<false>));
   return HLHGAT_OK;
 }
 

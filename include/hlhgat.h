@@ -642,6 +642,13 @@ int hlhgat_set_proj_bn_fused(int on);
  * the statistics in its epilogue (its last workgroup finalises them; no
  * workgroup waits), then the BatchNorm apply over x -- bitwise the same y. */
 int hlhgat_set_proj_bn_split(int on);
+/* Diagnostics: k_proj_bn_fwd stamps s_memrealtime (100 MHz) into buf, 8
+ * words per workgroup (blockIdx.y * gridDim.x + blockIdx.x): start, main loop
+ * done, partials written, group level done, statistics known (finaliser:
+ * generation bumped; others: poll returned), y stored, flags (1: last of its
+ * group, 2: finaliser); launches whose grid needs more than `words` words
+ * stamp nothing.  buf = NULL, words = 0: off (default). */
+int hlhgat_set_proj_bn_stamps(void* buf, int64_t words);
 /* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */
 int hlhgat_proj_bn_fused_capacity(int64_t* out);
 int hlhgat_set_bn_one_launch(int on);

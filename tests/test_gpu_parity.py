@@ -1816,6 +1816,38 @@ def test_proj_bn_handover_bitwise(cuda):
     assert gu["count"] > 0 and all(r["kernel"] == 2 for r in gu["log"])
 
 
+def test_proj_bn_phase_stamps(cuda):
+    """hlhgat_set_proj_bn_stamps (diagnostics, tools/probes/proj_bn_phases.py):
+    the stamped instantiation of k_proj_bn_fwd gives the same x / y as the
+    product one, and every workgroup's phases are in order, with exactly one
+    finaliser; the stamps are off again afterwards."""
+    from hlhgat import _lib
+    M, kb = 23157, [64, 64, 64]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    As = [torch.randn(M, k, generator=g).to(cuda) for k in kb]
+    W = (torch.randn(64, 192, generator=g) / 192 ** 0.5).to(cuda)
+    bias = torch.randn(64, generator=g).to(cuda)
+    gx = (M + 63) // 64
+    st = torch.zeros(gx * 8, dtype=torch.int64, device=cuda)
+    res = []
+    for stamps in (False, True):
+        torch.manual_seed(0)
+        bn = torch.nn.BatchNorm1d(64).to(cuda).train()
+        if stamps:
+            _lib.check(_lib.LIB.hlhgat_set_proj_bn_stamps(st.data_ptr(), st.numel()), "stamps")
+        try:
+            res.append(_proj_bn_call(cuda, As, W, bias, bn, None, True, True))
+        finally:
+            _lib.LIB.hlhgat_set_proj_bn_stamps(None, 0)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    t = st.view(gx, 8).cpu()
+    assert int(((t[:, 6] & 2) != 0).sum()) == 1
+    for k in range(5):
+        assert bool((t[:, k + 1] >= t[:, k]).all()), k
+    assert bool((t[:, 0] > 0).all())
+
+
 @pytest.mark.parametrize("M,N,kb,pad", [(23157, 64, [64, 64, 64], 0), (25600, 64, [384, 384], 333),
                                         (9728, 128, [128, 128], 0)])
 def test_proj_bn_split_bitwise(cuda, M, N, kb, pad):

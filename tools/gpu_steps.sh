@@ -82,6 +82,7 @@ for s in "$@"; do
           step fcalib 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fc -o f --output-format csv -- python3 tools/probes/fetch_calib.py run --meta gpurun_out/${TAG}_fc_meta.json
           python3 tools/probes/fetch_calib.py parse $(find gpurun_out/${TAG}_fc -name '*counter_collection.csv' | head -1) --meta gpurun_out/${TAG}_fc_meta.json > gpurun_out/${TAG}_fetch_calib.json || true
           rm -rf gpurun_out/${TAG}_fc ;;
+    pbphase) step pbphase 300 python3 tools/probes/proj_bn_phases.py --reps 20 ;;
     listctr) timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1; echo "=== listctr rc=$?" ;;
     heads) step heads 600 $PT tests -m gpu -v -k "reference_golden or state_dict" ;;
     pmcgemm) # SQ counters of k_proj_bwd_fused: isolated (kbench) and in the replayed step
