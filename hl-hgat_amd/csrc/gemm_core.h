@@ -31,6 +31,7 @@ struct FwdArgs {
   float* C;
   int64_t ldc;
   int accumulate;
+  int xcd_map;  // k_proj_fwd_lds: the column tiles of one row block on one XCD
 };
 
 // ---------------------------------------------------------------------------

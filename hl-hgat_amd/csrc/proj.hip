@@ -148,10 +148,26 @@ __device__ __forceinline__ void proj_fwd_lds_body(const FwdArgs& a, Blk blk,
                       a.bias ? a.bias + n_base : nullptr, a.accumulate, vec_ok);
 }
 
+// XCD-aware order (a.xcd_map): workgroups are dealt round-robin over the 8
+// XCDs, so linear id L goes to XCD L % 8; w = that XCD's (L / 8)-th item of
+// ONE contiguous range of the (row block, column tile) items, column tile
+// fastest: the gridDim.y column tiles of a row block run at about the same
+// time on one XCD and read its A rows from HBM once (the others hit that
+// XCD's L2).  With blockIdx.x fastest, a row block's A rows were read once
+// per column tile, far apart in time (config 5's N = 256 Linears: 4x A).
+__device__ __forceinline__ Blk fwd_item(const FwdArgs& a) {
+  if (!a.xcd_map || gridDim.y == 1) return blk_hw();
+  const unsigned total = gridDim.x * gridDim.y;
+  const unsigned L = blockIdx.x + blockIdx.y * gridDim.x;
+  const unsigned x = L & 7u, k = L >> 3, per = total >> 3, extra = total & 7u;
+  const unsigned w = x * per + (x < extra ? x : extra) + k;
+  return Blk{w / gridDim.y, w % gridDim.y, gridDim.x, gridDim.y};
+}
+
 template <int TN>
 __global__ __launch_bounds__(256) void k_proj_fwd_lds(FwdArgs a) {
   __shared__ float wl[2][TN * 16][KCP];
-  proj_fwd_lds_body<TN>(a, blk_hw(), wl);
+  proj_fwd_lds_body<TN>(a, fwd_item(a), wl);
 }
 
 // ---------------------------------------------------------------------------
@@ -1220,6 +1236,15 @@ int fwd_tn(int64_t M, int64_t N, int64_t ktot) {
 
 using namespace hlhgat;
 
+// HLHGAT_FWD_XCD=0: k_proj_fwd_lds in blockIdx.x-fastest order (A/B)
+int fwd_xcd_map() {
+  static const int v = [] {
+    const char* e = std::getenv("HLHGAT_FWD_XCD");
+    return (e && std::atoi(e) == 0) ? 0 : 1;
+  }();
+  return v;
+}
+
 extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
                                const int64_t* lda, const float* const* W,
                                const int64_t* ldw, const int64_t* kb, int64_t M,
@@ -1276,6 +1301,7 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   }
   if (vec) {
     dim3 g((unsigned)ceil_div(M, 64), (unsigned)ceil_div(N, tn * 16));
+    a.xcd_map = fwd_xcd_map();
     if (tn == 1)
       launch(k_proj_fwd_lds<1>, g, 256, 0, s, &prof, a);
     else if (tn == 2)

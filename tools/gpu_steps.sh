@@ -83,6 +83,9 @@ for s in "$@"; do
           python3 tools/probes/fetch_calib.py parse $(find gpurun_out/${TAG}_fc -name '*counter_collection.csv' | head -1) --meta gpurun_out/${TAG}_fc_meta.json > gpurun_out/${TAG}_fetch_calib.json || true
           rm -rf gpurun_out/${TAG}_fc ;;
     pbphase) step pbphase 300 python3 tools/probes/proj_bn_phases.py --reps 20 ;;
+    bnshapes) step bnshapes 300 python3 tools/probes/bn_shapes.py ;;
+    fwdxcd) for v in 1 0; do HLHGAT_FWD_XCD=$v timeout -k 10 300 python3 tools/kbench.py --big --modes 0 --only "proj_fwd" --reps 10 --chain 5 > gpurun_out/${TAG}_fwdxcd_$v.log 2>&1 || exit 3; done
+          grep -h '^{' gpurun_out/${TAG}_fwdxcd_1.log gpurun_out/${TAG}_fwdxcd_0.log ;;
     listctr) timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1; echo "=== listctr rc=$?" ;;
     heads) step heads 600 $PT tests -m gpu -v -k "reference_golden or state_dict" ;;
     pmcgemm) # SQ counters of k_proj_bwd_fused: isolated (kbench) and in the replayed step
