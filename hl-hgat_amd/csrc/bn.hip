@@ -1227,13 +1227,16 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
 // 556-566, lib/Hodge_Cheb_Conv.py:276-289).  Here the projection's workgroups
 // (64 rows x 64 columns each, proj_fwd_lds_mainloop) keep their output tile
 // in registers and finish the BatchNorm themselves:
-//   1. x = A W^T + bias is stored (the backward needs it) and the tile's fp64
-//      column sums over its valid rows are formed in a fixed order (rows of a
-//      lane, lanes q by xor 16 then 32, waves 0..3) and written through;
+//   1. the tile's fp64 column sums of x = A W^T + bias over its valid rows
+//      are formed in a fixed order (rows of a lane, lanes q by xor 16 then
+//      32, waves 0..3) and written through; x itself (the backward needs it)
+//      is stored after this workgroup's arrival is counted (the finaliser's:
+//      after its bump), so the statistics chain never waits for x stores;
 //   2. a two-level last-arriver tree per 64-column tile: the last workgroup of
 //      each group of kGroup partials sums them (reduce_range, fixed order),
-//      the last group sums the group partials, finalises mean / invstd and the
-//      running statistics, and bumps the tile's generation word;
+//      the last group sums the group partials, finalises mean / invstd,
+//      bumps the tile's generation word, and only then updates the running
+//      statistics;
 //   3. every other workgroup polls that word, reads the statistics and
 //      normalises its tile from the registers: y = relu?((x - mean) *
 //      (w invstd) + b), rows >= n_valid written as 0.  The wait is bounded
