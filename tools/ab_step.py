@@ -19,6 +19,8 @@ Variants (A/B hooks, not product settings):
               (no wait) + the apply launch
   nobarrier   twolaunchbn + splitbn: no kernel of the step waits for another workgroup
   rb8         the BatchNorm backward reduction with 8 rows per batch
+  pblate      k_proj_bn_fwd's finaliser sums the statistics before it releases the
+              waiting workgroups (round-5 protocol)
 """
 import argparse
 import json
@@ -44,6 +46,7 @@ def set_variant(name, on):
     _lib.LIB.hlhgat_set_bn_one_launch(0 if (on and name in ("twolaunchbn", "nobarrier")) else 1)
     _lib.LIB.hlhgat_set_proj_bn_split(1 if (on and name in ("splitbn", "nobarrier")) else 0)
     _lib.LIB.hlhgat_set_bn_bwd_rows(8 if (on and name == "rb8") else 4)
+    _lib.LIB.hlhgat_set_proj_bn_early(0 if (on and name == "pblate") else 1)
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")
