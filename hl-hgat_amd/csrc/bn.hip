@@ -1809,6 +1809,8 @@ extern "C" int hlhgat_set_proj_bn_early(int on) {
   return HLHGAT_OK;
 }
 
+extern "C" int hlhgat_get_proj_bn_early(void) { return g_pb_early; }
+
 extern "C" int hlhgat_set_proj_bn_stamps(void* buf, int64_t words) {
   HLH_CHECK_ARG(words >= 0 && (buf != nullptr || words == 0), "set_proj_bn_stamps: bad buffer");
   g_pb_stamps = reinterpret_cast<unsigned long long*>(buf);

@@ -654,6 +654,7 @@ int hlhgat_set_proj_bn_stamps(void* buf, int64_t words);
  * workgroup sums them itself; 0 = the finaliser sums them, publishes mean /
  * invstd, then releases the waiting workgroups. */
 int hlhgat_set_proj_bn_early(int on);
+int hlhgat_get_proj_bn_early(void);
 /* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */
 int hlhgat_proj_bn_fused_capacity(int64_t* out);
 int hlhgat_set_bn_one_launch(int on);

@@ -1833,6 +1833,7 @@ def test_proj_bn_early_publish_bitwise(cuda, M, N, kb, pad, wait):
     bias = torch.randn(N, generator=g).to(cuda)
     valid = torch.tensor([M - pad], dtype=torch.int32, device=cuda) if pad else None
     res = []
+    prior = int(_lib.LIB.hlhgat_get_proj_bn_early())
     for early in (0, 1):
         torch.manual_seed(0)
         bn = torch.nn.BatchNorm1d(N).to(cuda).train()
@@ -1842,7 +1843,7 @@ def test_proj_bn_early_publish_bitwise(cuda, M, N, kb, pad, wait):
             with _BnWait(wait):
                 out = _proj_bn_call(cuda, As, W, bias, bn, valid, True, True)
         finally:
-            _lib.LIB.hlhgat_set_proj_bn_early(1)
+            _lib.LIB.hlhgat_set_proj_bn_early(prior)
         res.append(list(out) + [bn.running_mean.clone(), bn.running_var.clone(),
                                 bn.num_batches_tracked.clone()])
     ops.check_device_errors()
