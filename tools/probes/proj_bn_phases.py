@@ -43,6 +43,7 @@ def main():
     nt, ns = zb.x_t.shape[0], zb.x_s.shape[0]
     g = torch.Generator(device="cpu").manual_seed(0)
     out = []
+    prior = int(L.hlhgat_get_proj_bn_early())
     for M, kbs, tag in [(nt, [64, 64, 64], "conv K=3 d=64 (nodes)"),
                         (ns, [64, 64, 64], "conv K=3 d=64 (edges)"),
                         (ns, [384, 384], "Linear(768,64) (edges)")]:
@@ -74,53 +75,63 @@ def main():
                 y.data_ptr(), N, mean.data_ptr(), inv.data_ptr(), ws.data_ptr(), ws.numel(),
                 torch.cuda.current_stream().cuda_stream), "proj_bn_fwd")
 
-        for _ in range(5):
-            pb()
+        for early in (0, 1):
+            _lib.check(L.hlhgat_set_proj_bn_early(early), "set_proj_bn_early")
+            res = measure(pb, st, gx, args.reps)
+            res.update({"shape": tag, "M": M, "K": sum(kbs), "workgroups": gx, "early": early})
+            out.append(res)
+            print(json.dumps(res), flush=True)
+        _lib.check(L.hlhgat_set_proj_bn_early(prior), "restore")
+
+
+def measure(pb, st, gx, reps):
+    from hlhgat import _lib
+    L = _lib.LIB
+    for _ in range(5):
+        pb()
+    torch.cuda.synchronize()
+    ev = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        pb()
+        b.record()
+        b.synchronize()
+        ev.append(a.elapsed_time(b) * 1e3)
+    runs = []
+    for _ in range(reps):
+        st.zero_()
+        _lib.check(L.hlhgat_set_proj_bn_stamps(st.data_ptr(), st.numel()), "stamps")
+        pb()
         torch.cuda.synchronize()
-        ev = []
-        for _ in range(args.reps):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            pb()
-            b.record()
-            b.synchronize()
-            ev.append(a.elapsed_time(b) * 1e3)
-        runs = []
-        for _ in range(args.reps):
-            st.zero_()
-            _lib.check(L.hlhgat_set_proj_bn_stamps(st.data_ptr(), st.numel()), "stamps")
-            pb()
-            torch.cuda.synchronize()
-            _lib.check(L.hlhgat_set_proj_bn_stamps(None, 0), "stamps off")
-            runs.append(st.view(gx, 8).cpu().numpy().astype(np.float64))
-        from hlhgat import ops
-        ops.check_device_errors()
-        res = {"shape": tag, "M": M, "K": sum(kbs), "workgroups": gx,
-               "event_us": q(ev)}
-        keys = ["start_skew", "gemm", "partials", "last_partials", "group_level",
-                "finaliser_bump", "poll_lag", "y_store", "last_y_store"]
-        agg = {k: [] for k in keys}
-        for s in runs:
-            t = (s[:, :6] - s[:, 0].min()) / 100.0  # µs
-            flags = s[:, 6].astype(np.int64)
-            top = np.nonzero(flags & 2)[0]
-            if len(top) != 1:
-                continue
-            tp = top[0]
-            others = np.nonzero((flags & 2) == 0)[0]
-            agg["start_skew"].append(t[:, 0].max())
-            agg["gemm"].append(np.median(t[:, 1] - t[:, 0]))
-            agg["partials"].append(np.median(t[:, 2] - t[:, 1]))
-            agg["last_partials"].append(t[:, 2].max())
-            agg["group_level"].append(t[tp, 3] - t[:, 2].max())
-            agg["finaliser_bump"].append(t[tp, 4])
-            agg["poll_lag"].append(np.median(t[others, 4]) - t[tp, 4])
-            agg["y_store"].append(np.median(t[:, 5] - t[:, 4]))
-            agg["last_y_store"].append(t[:, 5].max())
-        res["phases_us"] = {k: q(v) for k, v in agg.items() if v}
-        res["stamped_runs"] = len(agg["gemm"])
-        out.append(res)
-        print(json.dumps(res), flush=True)
+        _lib.check(L.hlhgat_set_proj_bn_stamps(None, 0), "stamps off")
+        runs.append(st.view(gx, 8).cpu().numpy().astype(np.float64))
+    from hlhgat import ops
+    ops.check_device_errors()
+    res = {"event_us": q(ev)}
+    keys = ["start_skew", "gemm", "partials", "last_partials", "group_level",
+            "finaliser_bump", "poll_lag", "y_store", "last_y_store"]
+    agg = {k: [] for k in keys}
+    for s in runs:
+        t = (s[:, :6] - s[:, 0].min()) / 100.0  # µs
+        flags = s[:, 6].astype(np.int64)
+        top = np.nonzero(flags & 2)[0]
+        if len(top) != 1:
+            continue
+        tp = top[0]
+        others = np.nonzero((flags & 2) == 0)[0]
+        agg["start_skew"].append(t[:, 0].max())
+        agg["gemm"].append(np.median(t[:, 1] - t[:, 0]))
+        agg["partials"].append(np.median(t[:, 2] - t[:, 1]))
+        agg["last_partials"].append(t[:, 2].max())
+        agg["group_level"].append(t[tp, 3] - t[:, 2].max())
+        agg["finaliser_bump"].append(t[tp, 4])
+        agg["poll_lag"].append(np.median(t[others, 4]) - t[tp, 4])
+        agg["y_store"].append(np.median(t[:, 5] - t[:, 4]))
+        agg["last_y_store"].append(t[:, 5].max())
+    res["phases_us"] = {k: q(v) for k, v in agg.items() if v}
+    res["stamped_runs"] = len(agg["gemm"])
+    return res
 
 
 if __name__ == "__main__":
