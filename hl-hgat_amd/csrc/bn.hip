@@ -1255,11 +1255,6 @@ struct ProjBnArgs {
   // diagnostics (hlhgat_set_proj_bn_stamps): 8 words per workgroup, thread 0
   // stamps s_memrealtime (100 MHz) at each phase boundary; NULL = off
   unsigned long long* stamps;
-  // 1 (default): the finaliser bumps the generation as soon as the group
-  // partials are complete and every workgroup sums them itself; 0: the
-  // finaliser sums them, publishes mean / invstd, then bumps (A/B hook,
-  // hlhgat_set_proj_bn_early; the same bits)
-  int early;
 };
 
 // one phase stamp of k_proj_bn_fwd (a plain vector store from one lane); a
@@ -1395,21 +1390,11 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
                            0, vx);
     return;
   }
-  const bool early = a.early != 0;
-  if (top && early) {
-    // every group's last workgroup wrote its group partial (drained) before
-    // arriving on the top counter, so the group partials are complete now:
-    // publish at once (the statistics are formed below by every workgroup)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {  // seq_cst, completed and fenced (see bar_wait)
-      __hip_atomic_fetch_add((gu64c_t*)word, 1ull << 32, __ATOMIC_SEQ_CST,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    }
-    pb_stamp<STAMPS>(a, 4, pb_now());
-  } else if (top) {
+  // (Round 6: releasing the waiting workgroups as soon as the group partials
+  // were complete, each summing them itself, moved the bump 1.6 us earlier
+  // but their own sum cost the same: end of launch unchanged, step neutral --
+  // profiles/r06/proj_bn_phases_early.log, ab_proj_bn_early.txt.)
+  if (top) {
     reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
     if (threadIdx.x < 64) {
       const int cc = n_base + threadIdx.x;
@@ -1455,36 +1440,13 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
     }
     __syncthreads();
     if (!s_ok) return;  // the finaliser normalises this tile from the stored x
-    if (!early && threadIdx.x < 64) {
+    if (threadIdx.x < 64) {
       const int cc = n_base + threadIdx.x;
       sm[threadIdx.x] = __uint_as_float(__hip_atomic_load(
           reinterpret_cast<unsigned*>(s.save_mean + cc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       ss[threadIdx.x] = __uint_as_float(__hip_atomic_load(
           reinterpret_cast<unsigned*>(s.save_invstd + cc), __ATOMIC_RELAXED,
           __HIP_MEMORY_SCOPE_AGENT));
-    }
-  }
-  if (early) {
-    // every workgroup that normalises its own rows: the statistics from the
-    // group partials, in the finaliser's order (bitwise the same everywhere);
-    // the finaliser alone writes the saved / running statistics and the
-    // batch counter, then its x
-    reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
-    if (threadIdx.x < 64) {
-      const int cc = n_base + threadIdx.x;
-      float m, is;
-      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, top);
-      sm[threadIdx.x] = m;
-      ss[threadIdx.x] = is;
-      if (top) {
-        s.save_mean[cc] = m;
-        s.save_invstd[cc] = is;
-      }
-    }
-    if (top) {
-      if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
-      store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16,
-                             nullptr, 0, vx);
     }
   }
   __syncthreads();
@@ -1802,14 +1764,6 @@ extern "C" int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
 // hlhgat_bn_fwd_train on x.
 unsigned long long* g_pb_stamps = nullptr;
 int64_t g_pb_stamps_words = 0;
-int g_pb_early = 0;  // flipped to 1 once measured (see hlhgat_set_proj_bn_early)
-
-extern "C" int hlhgat_set_proj_bn_early(int on) {
-  g_pb_early = on != 0 ? 1 : 0;
-  return HLHGAT_OK;
-}
-
-extern "C" int hlhgat_get_proj_bn_early(void) { return g_pb_early; }
 
 extern "C" int hlhgat_set_proj_bn_stamps(void* buf, int64_t words) {
   HLH_CHECK_ARG(words >= 0 && (buf != nullptr || words == 0), "set_proj_bn_stamps: bad buffer");
@@ -1903,7 +1857,6 @@ extern "C" int hlhgat_proj_bn_fwd(int nblocks, const float* const* A, const int6
   const bool split = proj_bn_split_flag();
   a.stats_only = split ? 1 : 0;
   if (g_pb_stamps && g_pb_stamps_words >= (int64_t)gx * gy * 8) a.stamps = g_pb_stamps;
-  a.early = g_pb_early;
   {
     ProfScope prof(HLHGAT_PROF_PROJ_BN, st, bytes, flops);
     if (a.stamps)

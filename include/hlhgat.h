@@ -649,12 +649,6 @@ int hlhgat_set_proj_bn_split(int on);
  * group, 2: finaliser); launches whose grid needs more than `words` words
  * stamp nothing.  buf = NULL, words = 0: off (default). */
 int hlhgat_set_proj_bn_stamps(void* buf, int64_t words);
-/* A/B hook (the same bits either way): 1 (default) = k_proj_bn_fwd's
- * finaliser publishes as soon as the group partials are complete and every
- * workgroup sums them itself; 0 = the finaliser sums them, publishes mean /
- * invstd, then releases the waiting workgroups. */
-int hlhgat_set_proj_bn_early(int on);
-int hlhgat_get_proj_bn_early(void);
 /* Workgroups k_proj_bn_fwd may use (half of the resident capacity). */
 int hlhgat_proj_bn_fused_capacity(int64_t* out);
 int hlhgat_set_bn_one_launch(int on);

@@ -1816,41 +1816,6 @@ def test_proj_bn_handover_bitwise(cuda):
     assert gu["count"] > 0 and all(r["kernel"] == 2 for r in gu["log"])
 
 
-@pytest.mark.parametrize("wait", [1000, 0])
-@pytest.mark.parametrize("M,N,kb,pad", [(23157, 64, [64, 64, 64], 0), (25600, 64, [384, 384], 333),
-                                        (9728, 128, [128, 128], 0), (700, 256, [256], 0)])
-def test_proj_bn_early_publish_bitwise(cuda, M, N, kb, pad, wait):
-    """k_proj_bn_fwd publishing as soon as the group partials are complete,
-    every workgroup summing them itself (default) == the finaliser summing
-    them and publishing mean / invstd before it releases the others
-    (hlhgat_set_proj_bn_early(0)): x, y, the batch and running statistics
-    and the batch counter bit for bit, with waiting workgroups and with every
-    waiting workgroup handing its tile over (wait bound 0)."""
-    from hlhgat import _lib, ops
-    g = torch.Generator(device="cpu").manual_seed(M + 13)
-    As = [torch.randn(M, k, generator=g).to(cuda) for k in kb]
-    W = (torch.randn(N, sum(kb), generator=g) / sum(kb) ** 0.5).to(cuda)
-    bias = torch.randn(N, generator=g).to(cuda)
-    valid = torch.tensor([M - pad], dtype=torch.int32, device=cuda) if pad else None
-    res = []
-    prior = int(_lib.LIB.hlhgat_get_proj_bn_early())
-    for early in (0, 1):
-        torch.manual_seed(0)
-        bn = torch.nn.BatchNorm1d(N).to(cuda).train()
-        ops.bn_giveups_reset()
-        _lib.check(_lib.LIB.hlhgat_set_proj_bn_early(early), "set_proj_bn_early")
-        try:
-            with _BnWait(wait):
-                out = _proj_bn_call(cuda, As, W, bias, bn, valid, True, True)
-        finally:
-            _lib.LIB.hlhgat_set_proj_bn_early(prior)
-        res.append(list(out) + [bn.running_mean.clone(), bn.running_var.clone(),
-                                bn.num_batches_tracked.clone()])
-    ops.check_device_errors()
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
-
-
 def test_proj_bn_phase_stamps(cuda):
     """hlhgat_set_proj_bn_stamps (diagnostics, tools/probes/proj_bn_phases.py):
     the stamped instantiation of k_proj_bn_fwd gives the same x / y as the

@@ -19,9 +19,6 @@ Variants (A/B hooks, not product settings):
               (no wait) + the apply launch
   nobarrier   twolaunchbn + splitbn: no kernel of the step waits for another workgroup
   rb8         the BatchNorm backward reduction with 8 rows per batch
-  pblate      k_proj_bn_fwd's finaliser sums the statistics before it releases the
-              waiting workgroups (round-5 protocol)
-  pbearly     k_proj_bn_fwd publishes as soon as the group partials are complete
 """
 import argparse
 import json
@@ -37,14 +34,8 @@ for p in (REPO, os.path.join(REPO, "hl-hgat_amd")):
 import torch  # noqa: E402
 
 
-PB_EARLY0 = None  # the library's default, read before any variant is set
-
-
 def set_variant(name, on):
     from hlhgat import ops, _lib
-    global PB_EARLY0
-    if PB_EARLY0 is None:
-        PB_EARLY0 = int(_lib.LIB.hlhgat_get_proj_bn_early())
     name = name.rstrip("0123456789")  # base1, base2: repeats of one variant
     ops.CHAINS_ENABLED = not (on and name == "nochain")
     ops._ext.set_chain_bwd(not (on and name == "nochainbwd"))
@@ -53,8 +44,6 @@ def set_variant(name, on):
     _lib.LIB.hlhgat_set_bn_one_launch(0 if (on and name in ("twolaunchbn", "nobarrier")) else 1)
     _lib.LIB.hlhgat_set_proj_bn_split(1 if (on and name in ("splitbn", "nobarrier")) else 0)
     _lib.LIB.hlhgat_set_bn_bwd_rows(8 if (on and name == "rb8") else 4)
-    _lib.LIB.hlhgat_set_proj_bn_early(0 if (on and name == "pblate") else
-                                      1 if (on and name == "pbearly") else PB_EARLY0)
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")

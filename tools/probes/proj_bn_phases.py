@@ -43,7 +43,6 @@ def main():
     nt, ns = zb.x_t.shape[0], zb.x_s.shape[0]
     g = torch.Generator(device="cpu").manual_seed(0)
     out = []
-    prior = int(L.hlhgat_get_proj_bn_early())
     for M, kbs, tag in [(nt, [64, 64, 64], "conv K=3 d=64 (nodes)"),
                         (ns, [64, 64, 64], "conv K=3 d=64 (edges)"),
                         (ns, [384, 384], "Linear(768,64) (edges)")]:
@@ -75,13 +74,10 @@ def main():
                 y.data_ptr(), N, mean.data_ptr(), inv.data_ptr(), ws.data_ptr(), ws.numel(),
                 torch.cuda.current_stream().cuda_stream), "proj_bn_fwd")
 
-        for early in (0, 1):
-            _lib.check(L.hlhgat_set_proj_bn_early(early), "set_proj_bn_early")
-            res = measure(pb, st, gx, args.reps)
-            res.update({"shape": tag, "M": M, "K": sum(kbs), "workgroups": gx, "early": early})
-            out.append(res)
-            print(json.dumps(res), flush=True)
-        _lib.check(L.hlhgat_set_proj_bn_early(prior), "restore")
+        res = measure(pb, st, gx, args.reps)
+        res.update({"shape": tag, "M": M, "K": sum(kbs), "workgroups": gx})
+        out.append(res)
+        print(json.dumps(res), flush=True)
 
 
 def measure(pb, st, gx, reps):
