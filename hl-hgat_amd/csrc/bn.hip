@@ -734,6 +734,10 @@ struct ApplyArgs {
   const float* bias;
   int relu;
   int tpr, rp;
+  // eval mode (hlhgat_bn_apply_running): invstd = 1 / sqrt(var + eps) per
+  // column from the running variance instead of `invstd`
+  const float* var;
+  float eps;
 };
 
 template <int V>
@@ -747,7 +751,8 @@ __device__ __forceinline__ void k_bn_apply_body(const ApplyArgs& a, Blk blk) {
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const float w = a.weight ? a.weight[c + v] : 1.f;
-    s[v] = w * a.invstd[c + v];
+    const float is = a.var ? 1.f / sqrtf(a.var[c + v] + a.eps) : a.invstd[c + v];
+    s[v] = w * is;
     m[v] = a.mean[c + v];
     t[v] = a.bias ? a.bias[c + v] : 0.f;
   }
@@ -1679,6 +1684,28 @@ extern "C" int hlhgat_bn_apply(const float* x, int64_t ldx, int64_t n, const int
   HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_apply: C too large");
   ApplyArgs p{n_valid, x, ldx, y, ldy, n, (int)C, save_mean, save_invstd, weight, bias, relu,
               L.tpr, L.rp};
+  hipStream_t st = as_stream(stream);
+  dim3 g2(apply_grid_x(n, L.rp), L.tiles);
+  if (vec)
+    launch(k_bn_apply<4>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
+  else
+    launch(k_bn_apply<1>, dim3(g2), dim3(kThreads), 0, st, nullptr, p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bn_apply_running(const float* x, int64_t ldx, int64_t n, int64_t C,
+                                       const float* weight, const float* bias,
+                                       const float* running_mean, const float* running_var,
+                                       float eps, int relu, float* y, int64_t ldy, void* stream) {
+  HLH_CHECK_ARG(n >= 1 && C >= 1 && C < (1 << 20) && ldx >= C && ldy >= C,
+                "bn_apply_running: bad sizes n=%lld C=%lld", (long long)n, (long long)C);
+  HLH_CHECK_ARG(x && y && running_mean && running_var, "bn_apply_running: NULL pointer");
+  const bool vec = bn_vec_ok(C, {ldx, ldy}, {x, y});
+  BnLayout L = bn_layout(n, C, vec);
+  HLH_CHECK_ARG(L.tiles <= kMaxTiles, "bn_apply_running: C too large");
+  ApplyArgs p{nullptr, x, ldx, y, ldy, n, (int)C, running_mean, nullptr, weight, bias, relu,
+              L.tpr, L.rp, running_var, eps};
   hipStream_t st = as_stream(stream);
   dim3 g2(apply_grid_x(n, L.rp), L.tiles);
   if (vec)

@@ -1460,13 +1460,26 @@ def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,
 def batch_norm_act(x: torch.Tensor, bn: torch.nn.BatchNorm1d, relu: bool = False,
                    valid: Optional[torch.Tensor] = None) -> torch.Tensor:
     """bn(x) followed by ReLU when ``relu``; training mode (or no running
-    stats) uses the HIP batch-statistics kernels, eval mode the running
-    statistics (ATen's fused eval kernel)."""
+    stats) uses the HIP batch-statistics kernels; eval mode the running
+    statistics: inference (nothing to differentiate) in one HIP launch
+    (hlhgat_bn_apply_running, the ReLU fused), an eval-mode BatchNorm inside
+    a differentiated graph through ATen's eval kernel (its autograd)."""
     _req_dev(x, "x")
     if x.dim() != 2:
         raise RuntimeError("hlhgat: batch_norm_act expects [N, C] input")
     use_batch = bn.training or not bn.track_running_stats
     if not use_batch:
+        grads = torch.is_grad_enabled() and (
+            x.requires_grad or any(t is not None and t.requires_grad
+                                   for t in (bn.weight, bn.bias)))
+        if not grads and x.size(0) > 0:
+            x = _rows2d(x, "x")
+            y = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+            check(LIB.hlhgat_bn_apply_running(
+                x.data_ptr(), _ld(x), x.size(0), x.size(1), _ptr(bn.weight), _ptr(bn.bias),
+                bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(bn.eps),
+                1 if relu else 0, y.data_ptr(), _ld(y), _stream(x)), "bn_apply_running")
+            return y
         y = torch.nn.functional.batch_norm(x, bn.running_mean, bn.running_var, bn.weight,
                                            bn.bias, False, 0.0, bn.eps)
         return torch.relu(y) if relu else y

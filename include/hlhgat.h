@@ -570,6 +570,15 @@ int64_t hlhgat_bn_workspace_bytes(int64_t n, int64_t C);
 /* n_valid (optional, device int32 scalar): rows >= *n_valid are capacity
  * padding of a static-shape batch: excluded from the statistics, their
  * outputs (and, backward, input gradients) written as 0.  NULL = all n. */
+/* Eval-mode BatchNorm1d (+ ReLU) from the running statistics, one launch:
+ * y = relu?((x - running_mean) * (w / sqrt(running_var + eps)) + b).  Replaces
+ * torch's eval-mode batch_norm (+ relu) in the reference's test() loops
+ * (lib/Hodge_ST_Model.py:556-566 under model.eval(); main_zinc...:165-177).
+ * weight / bias may be NULL (1 / 0). */
+int hlhgat_bn_apply_running(const float* x, int64_t ldx, int64_t n, int64_t C,
+                            const float* weight, const float* bias, const float* running_mean,
+                            const float* running_var, float eps, int relu, float* y,
+                            int64_t ldy, void* stream);
 int hlhgat_bn_fwd_train(const float* x, int64_t ldx, int64_t n,
                         const int32_t* n_valid, int64_t C,
                         const float* weight, const float* bias,

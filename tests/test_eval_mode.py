@@ -236,3 +236,39 @@ def test_infer_step_padded_batch_equals_unpadded(cuda):
     for o in outs:
         assert o.shape == ref.shape
         close(o, ref.numpy(), 1e-5, "padded eval vs unpadded")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,C,relu,affine", [(23157, 64, True, True), (4097, 6, False, True),
+                                             (1000, 256, True, False), (700, 128, False, False)])
+def test_eval_batch_norm_hip_matches_torch(cuda, n, C, relu, affine):
+    """Eval-mode BatchNorm (+ ReLU) in inference runs in one HIP launch from
+    the running statistics (hlhgat_bn_apply_running; unaligned C takes the
+    scalar path) and equals torch's eval batch_norm (+ relu) to 1e-6; with
+    gradients wanted it stays on ATen's autograd (same values)."""
+    from hlhgat import ops
+    torch.manual_seed(n + C)
+    bn = torch.nn.BatchNorm1d(C, affine=affine).to(cuda)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.2, 3.0)
+        if affine:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+    bn.eval()
+    x = torch.randn(n, C, device=cuda) * 2 + 0.3
+    with torch.no_grad():
+        ref = torch.nn.functional.batch_norm(x, bn.running_mean, bn.running_var, bn.weight,
+                                             bn.bias, False, 0.0, bn.eps)
+        if relu:
+            ref = torch.relu(ref)
+    with torch.no_grad():
+        y = ops.batch_norm_act(x, bn, relu=relu)
+    torch.cuda.synchronize()
+    ops.check_device_errors()
+    close(y.cpu(), ref.cpu(), 1e-6, "eval bn")
+    xg = x.clone().requires_grad_(True)
+    yg = ops.batch_norm_act(xg, bn, relu=relu)  # differentiated: ATen's path
+    yg.sum().backward()
+    close(yg.detach().cpu(), ref.cpu(), 1e-6, "eval bn (autograd path)")
+    assert xg.grad is not None
