@@ -130,7 +130,10 @@ class Batch(PairData):
         eis = getattr(self, "edge_index_s", None)
         if (getattr(self, "l1_factor", False) and torch.is_tensor(ei) and ei.is_cuda
                 and torch.is_tensor(eis) and eis.is_cuda):
-            ops.set_hodge_factor(eis, ei, self.x_t.size(0), getattr(self, "row_order_t", None))
+            tabs = tuple(getattr(self, k, None) for k in ("fac_alpha", "fac_sign", "fac_ends"))
+            tabs = tabs if all(torch.is_tensor(t) and t.is_cuda for t in tabs) else None
+            ops.set_hodge_factor(eis, ei, self.x_t.size(0), getattr(self, "row_order_t", None),
+                                 tables=tabs)
         for side in ("t", "s"):
             k = "edge_index_" + side
             t = getattr(self, k, None)
@@ -323,6 +326,35 @@ def _attach_csr(b, sides=("t", "s")) -> None:
             setattr(b, "csr_col_" + side, col)
 
 
+# HLHGAT_FACTOR_TABLES=0: leave the factored L1's tables to the device build
+# inside the step (A/B)
+FACTOR_TABLES = os.environ.get("HLHGAT_FACTOR_TABLES", "1") != "0"
+
+
+def factor_tables(b) -> None:
+    """The factored L1's per-batch tables (hlhgat_hodge_factor_t), built on
+    the host at collate time so the training step does not rebuild them on
+    the device (in a captured step: every replay): alpha_e = L1[e, e] / 2
+    (fp32, the diagonal's weight times 0.5), the signed B1 values in
+    incidence-CSR order (-1 tail, +1 head: adj2par1, lib/Hodge_Dataset.py:
+    169-191) and the edge ends as int32 [E, 2].  The same values as
+    ops._build_factor's device build (tests/test_host.py)."""
+    ei_s = np.asarray(b.edge_index_s, dtype=np.int64)
+    w = np.asarray(b.edge_weight_s, dtype=np.float32)
+    E = int(b.x_s.shape[0])
+    diag = ei_s[0] == ei_s[1]
+    alpha = np.zeros(E, dtype=np.float32)
+    np.add.at(alpha, ei_s[0][diag], w[diag] * np.float32(0.5))
+    rp = np.asarray(b.inc_rowptr, dtype=np.int64)
+    eids = np.asarray(b.inc_eids, dtype=np.int64)
+    ei = np.asarray(b.edge_index, dtype=np.int64).reshape(2, -1)
+    node = np.repeat(np.arange(rp.size - 1, dtype=np.int64), np.diff(rp))
+    sign = np.where(ei[1][eids] == node, np.float32(1.0), np.float32(-1.0)).astype(np.float32)
+    b.fac_alpha = torch.from_numpy(alpha)
+    b.fac_sign = torch.from_numpy(np.ascontiguousarray(sign))
+    b.fac_ends = torch.from_numpy(np.ascontiguousarray(ei.T.astype(np.int32)))
+
+
 def node_degree(inc_rowptr: torch.Tensor, valid: Optional[int] = None
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """degree(edge_index.view(-1), N_t) (lib/Hodge_Cheb_Conv.py:359, the D of
@@ -390,6 +422,8 @@ def collate(graphs: Sequence[PairData], check_hodge: bool = True) -> Batch:
     if torch.is_tensor(ei) and torch.is_tensor(getattr(b, "x_t", None)):
         b.inc_rowptr, b.inc_eids = incidence_csr(ei, b.x_t.size(0))
         b.deg_t, b.inv_deg_t = node_degree(b.inc_rowptr)
+        if b.l1_factor and FACTOR_TABLES:
+            factor_tables(b)
     # graph segment offsets of the readout (global_mean_pool over the
     # graph-contiguous rows, lib/Hodge_ST_Model.py:636), built here once
     # instead of by four small device ops per pool in every step
@@ -594,6 +628,8 @@ def pad_batch(b: "Batch", caps: Dict[str, int]) -> "Batch":
             out.inc_rowptr, out.inc_eids = incidence_csr(out.edge_index, Rt)
             # padding nodes: unit degree (the model's masked_fill, no 1/0)
             out.deg_t, out.inv_deg_t = node_degree(out.inc_rowptr, valid=nt)
+            if out.l1_factor and getattr(b, "fac_alpha", None) is not None:
+                factor_tables(out)  # padding edges: alpha 0, self-edge signs +1
     for side, n, R in (("t", nt, Rt), ("s", ns, Rs)):
         o = getattr(b, "row_order_" + side, None)
         if o is not None:

@@ -408,7 +408,7 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
             ds.append(x_s)
         x_s0, x_t0 = x_s, x_t
         par_1 = adj2par1(data.edge_index, x_t.shape[0], x_s.shape[0])
-        D = degree(data.edge_index.view(-1), num_nodes=x_t.shape[0]) + 1e-6  # (:823)
+        D = _node_degree(data, x_t.shape[0], x_t.device) + 1e-6  # (:823)
         for i, _ in enumerate(self.channels):
             for j in range(self.channels[i]):
                 neint = getattr(self, "NEInt{}{}".format(i, j))
@@ -434,6 +434,17 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         if len(self.mlp_channels) == 1:
             x_s = self.mlp(x_s, edge_index_s, edge_weight_s)
         return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch
+
+
+def _node_degree(data, n: int, device) -> torch.Tensor:
+    """degree(edge_index.view(-1), n) (lib/Hodge_Cheb_Conv.py:359): the
+    collate-time deg_t when the batch carries it (no device work in the step;
+    static-shape padding nodes get 1 there instead of 0 -- they belong to no
+    edge of a real simplex, so no real row changes), else computed here."""
+    d = getattr(data, "deg_t", None)
+    if torch.is_tensor(d) and d.device == device and d.numel() == n:
+        return d
+    return degree(data.edge_index.view(-1), num_nodes=n)
 
 
 def _per_row(vals: torch.Tensor, counts: torch.Tensor, rows: int, fill=0) -> torch.Tensor:
@@ -548,7 +559,7 @@ class _AttPoolHead(nn.Module):
         x_t0, x_s0 = x_t, x_s
         k = 0
         par_1 = adj2par1(d0.edge_index, x_t0.shape[0], x_s0.shape[0])
-        D = degree(d0.edge_index.view(-1), num_nodes=x_t0.shape[0]) + self._deg_eps
+        D = _node_degree(d0, x_t0.shape[0], x_t0.device) + self._deg_eps
         att_t = att_s = None
         dense = x_t.is_cuda and ops.DENSE_SLAB
         for i, _ in enumerate(self.channels):
@@ -603,7 +614,7 @@ class _AttPoolHead(nn.Module):
                 edge_index_t, edge_weight_t = d1.edge_index_t, d1.edge_weight_t
                 k = 1
                 par_1 = adj2par1(d1.edge_index, x_t0.shape[0], x_s0.shape[0])
-                D = degree(d1.edge_index.view(-1), num_nodes=x_t0.shape[0]) + self._deg_eps
+                D = _node_degree(d1, x_t0.shape[0], x_t0.device) + self._deg_eps
         dr = datas[min(len(self.channels) - 1, 1)]
         if x_t.size(0) != dr.x_t.size(0) or x_s.size(0) != dr.x_s.size(0):
             # the reference's readout (lib/Hodge_ST_Model.py:1076-1080) pools the

@@ -426,14 +426,20 @@ FACTOR_ENABLED = os.environ.get("HLHGAT_FACTOR", "1") != "0"
 
 
 def set_hodge_factor(edge_index_s: torch.Tensor, edge_index: torch.Tensor, n_nodes: int,
-                     node_order: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     node_order: Optional[torch.Tensor] = None,
+                     tables: Optional[tuple] = None) -> torch.Tensor:
     """Declare that the L1 built from (edge_index_s, edge_weight_s) equals
     alpha_e * B1^T B1 with B1 the boundary of ``edge_index`` ([2, E], i < j,
     adj2par1 lib/Hodge_Dataset.py:169-191) on n_nodes nodes -- exactly, as
     every L1 of the Hodge builder is (lib/Hodge_Dataset.py:451-456); the
     caller has checked it (hodge_dataset.hodge_factor_ok).  Polynomial bases
-    over it then gather ~4 rows per edge instead of nnz/E (hlhgat.h)."""
-    edge_index_s._hlhgat_factor = (edge_index, int(n_nodes), node_order)  # type: ignore
+    over it then gather ~4 rows per edge instead of nnz/E (hlhgat.h).
+    ``tables`` = (alpha [E] f32, signs [2E] f32 in incidence-CSR order,
+    ends [E, 2] int32) built at collate time (hodge_dataset.factor_tables):
+    the operator then takes them instead of building them on the device (in
+    a captured step, every replay)."""
+    edge_index_s._hlhgat_factor = (edge_index, int(n_nodes), node_order,  # type: ignore
+                                   tables)
     return edge_index_s
 
 
@@ -445,22 +451,30 @@ def has_hodge_factor(edge_index_s: torch.Tensor) -> bool:
 
 def _build_factor(op: "HodgeOperator", ei_s: torch.Tensor, w: torch.Tensor, decl) -> None:
     """The device tensors of hlhgat_hodge_factor_t for op (no host sync)."""
-    edge_index, n_nodes, node_order = decl
+    edge_index, n_nodes, node_order, tables = decl
     E = op.fwd.n_rows
     if edge_index.size(1) != E:
         raise RuntimeError(f"hlhgat: hodge factor: B1 has {edge_index.size(1)} edges, "
                            f"L1 has {E} rows")
     inc = incidence(edge_index, n_nodes)
     dev = ei_s.device
-    diag = ei_s[0] == ei_s[1]
-    alpha = torch.zeros(E, device=dev, dtype=torch.float32)
-    alpha.index_put_((ei_s[0],), torch.where(diag, w * 0.5, torch.zeros_like(w)),
-                     accumulate=True)
+    if tables is not None:  # collate-time tables: no device work here
+        alpha, signs, ends = tables
+        if (alpha.numel() != E or signs.numel() != 2 * E or tuple(ends.shape) != (E, 2)
+                or alpha.device != dev or signs.device != dev or ends.device != dev):
+            raise RuntimeError("hlhgat: hodge factor tables do not match the operator "
+                               f"({alpha.numel()}, {signs.numel()}, {tuple(ends.shape)}; E={E})")
+    else:
+        diag = ei_s[0] == ei_s[1]
+        alpha = torch.zeros(E, device=dev, dtype=torch.float32)
+        alpha.index_put_((ei_s[0],), torch.where(diag, w * 0.5, torch.zeros_like(w)),
+                         accumulate=True)
+        signs = _incidence_signs(inc)
+        ends = edge_index.t().to(torch.int32).contiguous()
     none_i = torch.empty(0, dtype=torch.int32, device=dev)
     no = (node_order.to(dev, torch.int32).contiguous() if node_order is not None else none_i)
     eo = op.fwd.order if op.fwd.order is not None else none_i
-    op.factor = (inc.rowptr, inc.edge_ids, _incidence_signs(inc), no,
-                 edge_index.t().to(torch.int32).contiguous(), alpha, eo)
+    op.factor = (inc.rowptr, inc.edge_ids, signs, no, ends, alpha, eo)
     op.factor_nodes = int(n_nodes)
 
 

@@ -1874,3 +1874,37 @@ def test_proj_bn_split_bitwise(cuda, M, N, kb, pad):
                                 bn.num_batches_tracked.clone()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_factor_tables_from_collate_bitwise_device_build(cuda):
+    """A factored L1 whose batch carries the collate-time tables
+    (hodge_dataset.factor_tables: alpha, signs, ends) builds the same
+    hlhgat_hodge_factor_t as the device build without them, and the factored
+    SpMM and a Laguerre conv over it give the same bits -- padded batch."""
+    import hlhgat
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import collate, pad_batch, static_caps
+    from hlhgat.synthetic import cifar_like_graphs
+    cb = collate([cifar_like_graphs(s)[0] for s in range(3)])
+    pb = pad_batch(cb, static_caps(cb))
+    assert pb.l1_factor and pb.fac_alpha is not None
+    torch.manual_seed(0)
+    conv = hlhgat.HodgeLaguerreConv(16, 24, K=4).to(cuda)
+    X = torch.randn(pb.x_s.shape[0], 16, device=cuda)
+    res = []
+    for keep in (True, False):
+        b = pb.__class__.__new__(pb.__class__)
+        for k, v in vars(pb).items():
+            if keep or not k.startswith("fac_"):
+                setattr(b, k, v)
+        d = b.to(cuda)
+        op = ops.hodge_operator(d.edge_index_s, d.edge_weight_s, d.x_s.shape[0])
+        assert op.factor is not None and ops.has_hodge_factor(d.edge_index_s)
+        xr = X.clone().requires_grad_(True)
+        y = conv(xr, d.edge_index_s, d.edge_weight_s)
+        y.square().sum().backward()
+        res.append([t.clone() for t in op.factor] + [ops.hodge_spmm(op, X), y.detach(),
+                                                     xr.grad])
+    ops.check_device_errors()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

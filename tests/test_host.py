@@ -801,3 +801,32 @@ def test_head_state_dict_matches_reference(name, cls, kw):
     ref = [(k[3:], tuple(g[k].shape)) for k in g if k.startswith("sd/")]
     ours = [(k, tuple(v.shape)) for k, v in obj(**kw).state_dict().items()]
     assert ours == ref
+
+
+def test_factor_tables_equal_the_device_build_restated():
+    """hodge_dataset.factor_tables (collate time, numpy) == what
+    ops._build_factor computes on the device when the batch carries no
+    tables, restated with the same torch ops on the CPU: alpha by an
+    accumulating index_put of the L1 diagonal / 2, the signed incidence in
+    CSR order, the int32 edge ends -- bit for bit, for a collated batch and
+    its padded copy (padding edges: alpha 0, self-edge signs +1)."""
+    from hlhgat.hodge_dataset import collate, pad_batch, static_caps
+    from hlhgat.synthetic import cifar_like_graphs
+    cb = collate([cifar_like_graphs(s)[0] for s in range(3)])
+    assert cb.l1_factor and cb.fac_alpha is not None
+    for b in (cb, pad_batch(cb, static_caps(cb))):
+        ei_s, w = b.edge_index_s, b.edge_weight_s
+        E = b.x_s.shape[0]
+        diag = ei_s[0] == ei_s[1]
+        alpha = torch.zeros(E, dtype=torch.float32)
+        alpha.index_put_((ei_s[0],), torch.where(diag, w * 0.5, torch.zeros_like(w)),
+                         accumulate=True)
+        rp, eids = b.inc_rowptr.long(), b.inc_eids.long()
+        node = torch.repeat_interleave(torch.arange(rp.numel() - 1), rp[1:] - rp[:-1])
+        head = b.edge_index[1][eids]
+        sign = torch.where(head == node, 1.0, -1.0).to(torch.float32)
+        ends = b.edge_index.t().to(torch.int32).contiguous()
+        assert torch.equal(b.fac_alpha, alpha)
+        assert torch.equal(b.fac_sign, sign)
+        assert torch.equal(b.fac_ends, ends)
+        assert b.fac_alpha.dtype == torch.float32 and b.fac_ends.dtype == torch.int32
