@@ -592,11 +592,14 @@ def _head_pool(kind, n, seed=0):
 
 
 def _head_collate(kind, items):
-    from hlhgat.hodge_dataset import collate
+    from hlhgat.hodge_dataset import collate, pool_tables
     if kind == "tsp":
         return collate(items, check_hodge=False)
-    return [collate([p[0] for p in items], check_hodge=False),
-            collate([p[1] for p in items], check_hodge=False)]
+    datas = [collate([p[0] for p in items], check_hodge=False),
+             collate([p[1] for p in items], check_hodge=False)]
+    if os.environ.get("HLHGAT_POOL_TABLES", "1") != "0":  # A/B: 0 = sorted in the step
+        pool_tables(datas)  # the MLGC cluster CSR, once per batch (not in every step)
+    return datas
 
 
 def _head_batch(kind, graphs, seed):

@@ -520,6 +520,38 @@ def static_caps(b: "Batch", quantum: int = 512) -> Dict[str, int]:
     return caps
 
 
+def pool_tables(datas: Sequence["Batch"]) -> None:
+    """The attpool heads' MLGC cluster CSR per side, built on the host once
+    per level list instead of inside every step (lib/Hodge_ST_Model.py:
+    1029-1038, 1067-1069): fine row r of datas[0] belongs to coarse cluster
+    x[r, 0] + (first coarse row of its graph); rows whose cluster is inf
+    (edges MLGC dropped, static-shape padding) go to a trailing bucket that
+    the mean leaves out.  datas[0].pool_rowptr_{t,s} (int32 [n_coarse + 2])
+    and pool_rows_{t,s} (int32 [n_fine], the fine rows grouped by cluster,
+    ascending within one) are the CSR hodge_cheb_conv.cluster_mean sorts on
+    the device -- the same members in the same order."""
+    d0, d1 = datas[0], datas[1]
+    for side, cnt in (("t", "num_node1"), ("s", "num_edge1")):
+        x0 = np.asarray(getattr(d0, "x_" + side)[:, 0], dtype=np.float32)
+        n = x0.size
+        n_seg = int(getattr(d1, "x_" + side).shape[0])
+        counts = np.asarray(getattr(d0, cnt), dtype=np.int64)
+        ahead = np.zeros(counts.size, dtype=np.float32)
+        ahead[1:] = np.cumsum(np.asarray(getattr(d1, cnt), dtype=np.int64))[:-1]
+        per_row = np.zeros(n, dtype=np.float32)
+        k = min(int(counts.sum()), n)
+        per_row[:k] = np.repeat(ahead, counts)[:k]
+        pos = x0 + per_row  # float32, as the device forward adds them
+        idx = np.where(np.isinf(pos), n_seg, pos).astype(np.int64)
+        if idx.size and (idx.min() < 0 or idx.max() > n_seg):
+            raise ValueError(f"pool_tables: cluster ids outside [0, {n_seg}] on side {side}")
+        order = np.argsort(idx, kind="stable")
+        rowptr = np.zeros(n_seg + 2, dtype=np.int32)
+        rowptr[1:] = np.cumsum(np.bincount(idx, minlength=n_seg + 1)).astype(np.int32)
+        setattr(d0, "pool_rowptr_" + side, torch.from_numpy(rowptr))
+        setattr(d0, "pool_rows_" + side, torch.from_numpy(order.astype(np.int32)))
+
+
 def level_caps(levels: Sequence[Sequence["Batch"]], quantum: int = 512) -> List[Dict[str, int]]:
     """static_caps per MLGC level, the max over several level-batch lists
     (the attpool heads' `datas`): one capacity bucket for all of them."""
@@ -548,6 +580,12 @@ def pad_levels(datas: Sequence["Batch"], caps: Sequence[Dict[str, int]]) -> List
         x = getattr(p0, key).clone()
         x[getattr(b0, key).size(0):, 0] = float("inf")
         setattr(p0, key, x)
+    if getattr(b0, "pool_rowptr_t", None) is not None and p0.x_t.device.type == "cpu":
+        pool_tables(out)  # the padded rows (inf) in the dropped bucket
+    else:
+        for k in ("pool_rowptr_t", "pool_rows_t", "pool_rowptr_s", "pool_rows_s"):
+            if hasattr(p0, k):
+                delattr(p0, k)
     return out
 
 

@@ -436,6 +436,25 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch
 
 
+def _has_pool_tables(d0, device) -> bool:
+    return all(torch.is_tensor(getattr(d0, k, None)) and getattr(d0, k).device == device
+               for k in ("pool_rowptr_t", "pool_rows_t", "pool_rowptr_s", "pool_rows_s"))
+
+
+def _pool(x: torch.Tensor, pos, d0, side: str, n_seg: int) -> torch.Tensor:
+    """cluster_mean(x, pos, n_seg) -- from the level list's collate-time
+    cluster CSR when it carries one (hodge_dataset.pool_tables: the CSR
+    cluster_mean would sort on the device, so the same bits), else on the
+    device from pos."""
+    if pos is None:
+        rp, rows = getattr(d0, "pool_rowptr_" + side), getattr(d0, "pool_rows_" + side)
+        if rp.numel() != n_seg + 2 or rows.numel() != x.size(0):
+            raise RuntimeError(f"hlhgat: pool tables ({rp.numel() - 2} clusters, {rows.numel()} "
+                               f"rows) do not match ({n_seg}, {x.size(0)})")
+        return ops.segment_mean(x, rp, n_seg, rows)
+    return cluster_mean(x, pos, n_seg)
+
+
 def _node_degree(data, n: int, device) -> torch.Tensor:
     """degree(edge_index.view(-1), n) (lib/Hodge_Cheb_Conv.py:359): the
     collate-time deg_t when the batch carries it (no device work in the step;
@@ -547,11 +566,14 @@ class _AttPoolHead(nn.Module):
     def forward(self, datas, device="cuda:0", if_final_layer=False, if_att=False):
         d0 = datas[0]
         dev = d0.x_t.device
-        # global coarse index of every fine node / edge (pos_ts / pos_ss)
-        pos_t = d0.x_t[:, 0] + _level_offsets(datas[1].num_node1, d0.num_node1, dev,
-                                                 d0.x_t.size(0))
-        pos_s = d0.x_s[:, 0] + _level_offsets(datas[1].num_edge1, d0.num_edge1, dev,
-                                                 d0.x_s.size(0))
+        # global coarse index of every fine node / edge (pos_ts / pos_ss);
+        # not needed when the level list carries its cluster CSR (pool_tables)
+        pos_t = pos_s = None
+        if not _has_pool_tables(d0, dev):
+            pos_t = d0.x_t[:, 0] + _level_offsets(datas[1].num_node1, d0.num_node1, dev,
+                                                     d0.x_t.size(0))
+            pos_s = d0.x_s[:, 0] + _level_offsets(datas[1].num_edge1, d0.num_edge1, dev,
+                                                     d0.x_s.size(0))
         x_s, edge_index_s, edge_weight_s = d0.x_s[:, 1:], d0.edge_index_s, d0.edge_weight_s
         x_t, edge_index_t, edge_weight_t = d0.x_t[:, 1:], d0.edge_index_t, d0.edge_weight_t
         x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
@@ -608,8 +630,8 @@ class _AttPoolHead(nn.Module):
                     x_t = x_t * att_t
                     x_s = x_s * att_s
                 d1 = datas[k + 1]
-                x_t0 = cluster_mean(x_t0, pos_t, d1.x_t.shape[0])
-                x_s0 = cluster_mean(x_s0, pos_s, d1.x_s.shape[0])  # inf members dropped
+                x_t0 = _pool(x_t0, pos_t, d0, "t", d1.x_t.shape[0])
+                x_s0 = _pool(x_s0, pos_s, d0, "s", d1.x_s.shape[0])  # inf members dropped
                 edge_index_s, edge_weight_s = d1.edge_index_s, d1.edge_weight_s
                 edge_index_t, edge_weight_t = d1.edge_index_t, d1.edge_weight_t
                 k = 1

@@ -830,3 +830,34 @@ def test_factor_tables_equal_the_device_build_restated():
         assert torch.equal(b.fac_sign, sign)
         assert torch.equal(b.fac_ends, ends)
         assert b.fac_alpha.dtype == torch.float32 and b.fac_ends.dtype == torch.int32
+
+
+def test_pool_tables_equal_the_device_cluster_csr_restated():
+    """hodge_dataset.pool_tables == the cluster CSR hodge_cheb_conv.cluster_mean
+    builds on the device from pos = x[:, 0] + level offsets (inf -> the
+    dropped bucket), restated with torch ops on the CPU (stable sort of the
+    members by cluster), for a two-level list and its padded copy."""
+    from hlhgat.hodge_dataset import level_caps, pad_levels, pool_tables
+    from hlhgat.synthetic import two_level_batch
+    raw = two_level_batch("cifar", 5, seed=3)
+    pool_tables(raw)
+    padded = pad_levels(raw, level_caps([raw], 128))
+    for datas in (raw, padded):
+        d0, d1 = datas
+        for side, cnt in (("t", "num_node1"), ("s", "num_edge1")):
+            x0 = getattr(d0, "x_" + side)[:, 0]
+            n_seg = getattr(d1, "x_" + side).shape[0]
+            counts = getattr(d0, cnt).long()
+            ahead = torch.zeros(counts.numel(), dtype=torch.float32)
+            ahead[1:] = torch.cumsum(getattr(d1, cnt).long(), 0)[:-1].float()
+            n = x0.numel()
+            tail = max(n - int(counts.sum()), 0)
+            per = torch.repeat_interleave(torch.cat([ahead, torch.zeros(1)]),
+                                          torch.cat([counts, torch.tensor([tail])]))[:n]
+            pos = x0 + per
+            idx = torch.where(torch.isinf(pos), torch.full_like(pos, float(n_seg)), pos).long()
+            order = torch.sort(idx, stable=True).indices
+            rowptr = torch.zeros(n_seg + 2, dtype=torch.int64)
+            rowptr[1:] = torch.cumsum(torch.bincount(idx, minlength=n_seg + 1), 0)
+            assert torch.equal(getattr(d0, "pool_rows_" + side), order.to(torch.int32)), side
+            assert torch.equal(getattr(d0, "pool_rowptr_" + side), rowptr.to(torch.int32)), side

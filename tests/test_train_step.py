@@ -941,3 +941,40 @@ def test_cu_masked_stream_runs_kernels(cuda):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["peptides", "cifar"])
+@pytest.mark.parametrize("padded", [False, True])
+def test_pool_tables_bitwise_device_cluster_csr(cuda, kind, padded):
+    """An attpool level list carrying its collate-time MLGC cluster CSR
+    (hodge_dataset.pool_tables) gives the same outputs, gradients and running
+    statistics, bit for bit, as the same list without it (the cluster CSR
+    sorted on the device inside the step), padded or not."""
+    from hlhgat.hodge_dataset import pool_tables
+    raw, mk, loss = _head_case(kind)
+    base = _pad_all(kind, raw)[0] if padded else raw[0]
+    res = []
+    for tables in (False, True):
+        datas = []
+        for b in base:
+            c = b.__class__.__new__(b.__class__)
+            for k, v in vars(b).items():
+                if not k.startswith("pool_"):
+                    setattr(c, k, v)
+            datas.append(c)
+        if tables:
+            pool_tables(datas)
+            assert datas[0].pool_rowptr_t is not None
+        torch.manual_seed(0)
+        m = mk().to(cuda).train()
+        d = _dev(datas, cuda)
+        out = m(d)
+        loss(out, d).backward()
+        res.append((out.detach().cpu(), {k: p.grad.detach().cpu().clone()
+                                         for k, p in m.named_parameters() if p.grad is not None},
+                    {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}))
+    (o0, g0, s0), (o1, g1, s1) = res
+    assert torch.equal(o0, o1)
+    assert set(g0) == set(g1) and all(torch.equal(g0[k], g1[k]) for k in g0)
+    assert all(torch.equal(s0[k], s1[k]) for k in s0)

@@ -33,8 +33,8 @@ for s in "$@"; do
     sel) step sel 600 $PT tests -m gpu -v -k "$SEL" ;;  # SEL="expr" tools/gpu_steps.sh TAG sel
     cfg3pipe) step cfg3pipe 600 python tools/probes/cfg3_pipe.py --cus "${CUS-0,32,64,128}" --prio "${PRIO-}" --rounds 2 ;;
     ab5env) for r in 1 2; do for v in ${AB5:-0 1}; do  # AB5ENV=NAME: cfg5 step with NAME=v
-           env $AB5ENV=$v timeout -k 10 400 python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline > gpurun_out/${TAG}_ab5env_${v}_$r.log 2>&1
-           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5env_${v}_$r.log | head -1 | sed "s/^/cfg5 $AB5ENV=$v run $r /" >> gpurun_out/${TAG}_ab5env.txt || true
+           env $AB5ENV=$v timeout -k 10 400 python3 bench.py --workload ${WL:-cfg5} --steps 10 --warmup 3 --batches 2 --no-cpu-baseline > gpurun_out/${TAG}_ab5env_${v}_$r.log 2>&1
+           grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5env_${v}_$r.log | head -1 | sed "s/^/${WL:-cfg5} $AB5ENV=$v run $r /" >> gpurun_out/${TAG}_ab5env.txt || true
          done; done; cat gpurun_out/${TAG}_ab5env.txt ;;
     abstep) step abstep 900 python3 tools/ab_step.py ${AB:-base1 base2} --rounds 5 ;;
     quick) step quick 300 python bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-replay-census --no-loader --steps 30 ;;
@@ -61,6 +61,11 @@ for s in "$@"; do
           T=$(find gpurun_out/prof5_$TAG -name '*kernel_trace.csv' | head -1)
           python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_cfg5_step_dispatches.csv > gpurun_out/${TAG}_cfg5_step_kernels.txt || true
           rm -rf gpurun_out/prof5_$TAG ;;
+    prof3) rm -rf gpurun_out/prof3_$TAG  # the config-3 head step (CIFAR attpool), replayed
+          step prof3 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3_$TAG -o run --output-format csv -- python3 bench.py --workload cfg3 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+          T=$(find gpurun_out/prof3_$TAG -name '*kernel_trace.csv' | head -1)
+          python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_cfg3_step_dispatches.csv > gpurun_out/${TAG}_cfg3_step_kernels.txt || true
+          rm -rf gpurun_out/prof3_$TAG ;;
     prof5s) rm -rf gpurun_out/prof5s_$TAG  # the same on ONE stream (HLHGAT_STREAM_FORK=0)
           HLHGAT_STREAM_FORK=0 step prof5s 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5s_$TAG -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
           T=$(find gpurun_out/prof5s_$TAG -name '*kernel_trace.csv' | head -1)
