@@ -361,13 +361,27 @@ __device__ __forceinline__ bool give_up(unsigned long long* word, unsigned long 
   return mine;
 }
 
-// The finaliser, after its generation bump: take every slot of [slots,
-// slots + n) left in this generation; taken[j] (LDS) = 1 for those.  The bump
-// is a seq_cst RMW that thread 0 waits for (vmcnt(0)) and fences before the
-// workgroup barrier below, and the slot loads are seq_cst: with the waiter's
-// seq_cst (slot store, generation load) one of the two sides sees the other's
-// write.  A match is taken with a seq_cst CAS.
-// Returns (in every thread) whether any was taken.
+// The finaliser's generation bump (thread 0): a RETURNING agent-scope RMW,
+// performed at the coherence point, that thread 0 waits for (vmcnt(0))
+// before the workgroup barrier preceding take_left's slot loads -- so every
+// slot load is issued after the bump is visible to every workgroup.  With the
+// waiter's seq_cst slot store then generation load (give_up), one of the two
+// sides sees the other's write.  No agent-scope fence: what the
+// waiting workgroups read after the bump (partials, mean / invstd) was
+// written through with atomic stores and drained before it, and the fence's
+// L2 write-back cost ~2 us on every launch's critical path (round 6: the
+// config-2 step 2.73 vs 2.64 ms with it, profiles/r06/ab_bn_bump.txt).
+__device__ __forceinline__ void publish_gen(unsigned long long* word, unsigned long long inc) {
+  const unsigned long long old =
+      __hip_atomic_fetch_add((gu64c_t*)word, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("" ::"v"(old));  // the returning form: its completion is what vmcnt waits for
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The finaliser, after publish_gen: take every slot of [slots, slots + n)
+// left in this generation; taken[j] (LDS) = 1 for those (agent-scope atomic
+// loads, issued after the bump completed; a match is taken with a seq_cst
+// CAS).  Returns (in every thread) whether any was taken.
 template <int NT>
 __device__ __forceinline__ bool take_left(unsigned long long* slots, int n, unsigned gen0,
                                           unsigned char* taken) {
@@ -378,7 +392,7 @@ __device__ __forceinline__ bool take_left(unsigned long long* slots, int n, unsi
   for (int j = threadIdx.x; j < n; j += NT) {
     unsigned char t = 0;
     const unsigned long long v =
-        __hip_atomic_load((gu64c_t*)(slots + j), __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_load((gu64c_t*)(slots + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v == mark) {
       unsigned long long exp = mark;
       if (__hip_atomic_compare_exchange_strong((gu64c_t*)(slots + j), &exp, mark + 1ull,
@@ -417,13 +431,10 @@ __device__ __forceinline__ unsigned bar_wait(unsigned long long* word, unsigned 
     unsigned role;
     if (arrived >= total) report_state_error(err);
     if (arrived == total - 1) {
-      // seq_cst bump, completed and fenced before the workgroup barrier that
-      // precedes take_left's slot loads (the finaliser's half of the
-      // store-load handshake with give_up; ADVICE r5)
-      __hip_atomic_fetch_add((gu64c_t*)word, (1ull << 32) - (unsigned long long)total,
-                             __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+      // the bump, completed before the workgroup barrier that precedes
+      // take_left's slot loads (publish_gen: the finaliser's half of the
+      // store-load handshake with give_up)
+      publish_gen(word, (1ull << 32) - (unsigned long long)total);
       role = kFinal;
     } else if (poll_gen(word, gen0, wait_us)) {
       role = kOwn;
@@ -804,7 +815,7 @@ struct BwdApplyArgs {
 // Backward statistics (two-launch path): partials of sum(g), sum(g (x - mean));
 // the finalising workgroup of a column tile forms dweight, dbias and dx's
 // coefficients.
-template <int V, int RB>
+template <int V>
 __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk) {
   using vt = typename VecT<V>::type;
   const int cl = threadIdx.x % a.tpr;
@@ -832,23 +843,25 @@ __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk
         s1[v] += (double)g * (double)(vget(xv, v) - mu[v]);
       }
     };
-    // RB rows (3 RB loads) in flight per batch, the batch's tail rows
-    // predicated in the same batch (one memory round trip per batch; the
-    // rows are still summed in ascending order, so any RB gives the same bits)
-    for (int64_t r = r_lo + rg; r < r_hi; r += RB * a.rp) {
-      vt xv[RB], gv[RB], yv[RB];
+    int64_t r = r_lo + rg;
+    for (; r + 3 * a.rp < r_hi; r += 4 * a.rp) {  // 4 rows (12 loads) in flight
+      vt xv[4], gv[4], yv[4];
 #pragma unroll
-      for (int u = 0; u < RB; ++u) {
+      for (int u = 0; u < 4; ++u) {
         const int64_t rr = r + u * a.rp;
-        if (rr < r_hi) {
-          xv[u] = vload<V>(a.x + rr * a.ldx + c);
-          gv[u] = vload<V>(a.dy + rr * a.lddy + c);
-          yv[u] = a.y ? vload<V>(a.y + rr * a.ldy + c) : gv[u];
-        }
+        xv[u] = vload<V>(a.x + rr * a.ldx + c);
+        gv[u] = vload<V>(a.dy + rr * a.lddy + c);
+        if (a.y) yv[u] = vload<V>(a.y + rr * a.ldy + c);
       }
 #pragma unroll
-      for (int u = 0; u < RB; ++u)
-        if (r + u * a.rp < r_hi) acc(xv[u], gv[u], yv[u]);
+      for (int u = 0; u < 4; ++u) acc(xv[u], gv[u], yv[u]);
+    }
+    for (; r < r_hi; r += a.rp) {
+      vt xv = vload<V>(a.x + r * a.ldx + c);
+      vt gv = vload<V>(a.dy + r * a.lddy + c);
+      vt yv = gv;
+      if (a.y) yv = vload<V>(a.y + r * a.ldy + c);
+      acc(xv, gv, yv);
     }
   }
   write_partials<V, kThreads>(s0, s1, a, c0, blk);
@@ -879,38 +892,16 @@ __device__ __forceinline__ void k_bn_bwd_reduce_body(const StatsArgs& a, Blk blk
   }
 }
 
-template <int V, int RB>
+template <int V>
 __global__ __launch_bounds__(kThreads) void k_bn_bwd_reduce(StatsArgs a) {
-  k_bn_bwd_reduce_body<V, RB>(a, blk_hw());
-}
-
-// rows per batch of the backward reduction: 4, or 8 (HLHGAT_BN_BWD_RB=8 /
-// hlhgat_set_bn_bwd_rows; bitwise the same results).  Same-box A/B, round 6
-// (profiles/r06/ab_bn_bwd_rows.txt): config 2 2.757 (8) vs 2.748-2.755 ms,
-// config 5 36.75-36.80 (8) vs 36.56-36.61 ms -- 4 stays.
-std::atomic<int> g_bn_bwd_rb{0};
-int bn_bwd_rb() {
-  int v = g_bn_bwd_rb.load(std::memory_order_relaxed);
-  if (v == 0) {
-    const char* e = std::getenv("HLHGAT_BN_BWD_RB");
-    v = (e && std::atoi(e) == 8) ? 8 : 4;
-    int expect = 0;
-    g_bn_bwd_rb.compare_exchange_strong(expect, v);
-    v = g_bn_bwd_rb.load(std::memory_order_relaxed);
-  }
-  return v;
+  k_bn_bwd_reduce_body<V>(a, blk_hw());
 }
 
 void launch_bwd_reduce(bool vec, dim3 grid, hipStream_t st, ProfScope* prof, const StatsArgs& s) {
-  const int rb = bn_bwd_rb();
-  if (vec && rb == 8)
-    launch(k_bn_bwd_reduce<4, 8>, grid, dim3(kThreads), 0, st, prof, s);
-  else if (vec)
-    launch(k_bn_bwd_reduce<4, 4>, grid, dim3(kThreads), 0, st, prof, s);
-  else if (rb == 8)
-    launch(k_bn_bwd_reduce<1, 8>, grid, dim3(kThreads), 0, st, prof, s);
+  if (vec)
+    launch(k_bn_bwd_reduce<4>, grid, dim3(kThreads), 0, st, prof, s);
   else
-    launch(k_bn_bwd_reduce<1, 4>, grid, dim3(kThreads), 0, st, prof, s);
+    launch(k_bn_bwd_reduce<1>, grid, dim3(kThreads), 0, st, prof, s);
 }
 
 template <int V>
@@ -1232,16 +1223,13 @@ __global__ __launch_bounds__(kThreads) void k_bn_fwd_grid(StatsArgs a) {
 // 556-566, lib/Hodge_Cheb_Conv.py:276-289).  Here the projection's workgroups
 // (64 rows x 64 columns each, proj_fwd_lds_mainloop) keep their output tile
 // in registers and finish the BatchNorm themselves:
-//   1. the tile's fp64 column sums of x = A W^T + bias over its valid rows
-//      are formed in a fixed order (rows of a lane, lanes q by xor 16 then
-//      32, waves 0..3) and written through; x itself (the backward needs it)
-//      is stored after this workgroup's arrival is counted (the finaliser's:
-//      after its bump), so the statistics chain never waits for x stores;
+//   1. x = A W^T + bias is stored (the backward needs it) and the tile's fp64
+//      column sums over its valid rows are formed in a fixed order (rows of a
+//      lane, lanes q by xor 16 then 32, waves 0..3) and written through;
 //   2. a two-level last-arriver tree per 64-column tile: the last workgroup of
 //      each group of kGroup partials sums them (reduce_range, fixed order),
-//      the last group sums the group partials, finalises mean / invstd,
-//      bumps the tile's generation word, and only then updates the running
-//      statistics;
+//      the last group sums the group partials, finalises mean / invstd and the
+//      running statistics, and bumps the tile's generation word;
 //   3. every other workgroup polls that word, reads the statistics and
 //      normalises its tile from the registers: y = relu?((x - mean) *
 //      (w invstd) + b), rows >= n_valid written as 0.  The wait is bounded
@@ -1309,11 +1297,11 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   double* sum0 = red + 2 * 4 * 64;  // [64]
   double* sum1 = sum0 + 64;         // [64]
   const bool vx = (g.ldc % 4) == 0 && (reinterpret_cast<uintptr_t>(g.C) & 15) == 0;
-  // x is stored AFTER the partials are in (below): the statistics chain does
-  // not wait for the x stores to drain (arrive_last waits for every store).
-  // Round 6: bitwise the round-5 order (x first, running statistics before
-  // the bump), ~1 us less per launch alone, neutral in the config-2 step
-  // (profiles/r06/ab_proj_bn_order.txt, proj_bn_phases.log)
+  store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr, 0,
+                         vx);
+  // (Round 6: storing x after the partials and the running statistics after
+  // the bump was bitwise and ~1 us shorter alone, but not faster in the
+  // config-2 step -- profiles/r06/ab_proj_bn_order.txt; not kept.)
   const int64_t n_eff = eff_rows(s.n, s.nvalid);
 #pragma unroll
   for (int tn = 0; tn < kPbTN; ++tn) {
@@ -1372,14 +1360,6 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
   float* sm = reinterpret_cast<float*>(sum1 + 64);  // [64]
   float* ss = sm + 64;                              // [64]
   unsigned long long* tile_slots = s.slots + (int64_t)by * gridDim.x;
-  if (!top) {
-    // x, drained before a possible give-up: the finaliser normalises a
-    // given-up tile from it (give_up's release is thread 0's)
-    store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr,
-                           0, vx);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
   if (a.stats_only) {  // x and the statistics only: nobody waits (k_bn_apply normalises)
     if (!top) return;
     reduce_range<kThreads>(s.gpart, 0, ng, s, n_base, 64, sum0, sum1);
@@ -1391,8 +1371,6 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
       s.save_invstd[cc] = is;
     }
     if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
-    store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr,
-                           0, vx);
     return;
   }
   // (Round 6: releasing the waiting workgroups as soon as the group partials
@@ -1404,7 +1382,7 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
     if (threadIdx.x < 64) {
       const int cc = n_base + threadIdx.x;
       float m, is;
-      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, false);
+      fwd_finalize(s, cc, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is, true);
       __hip_atomic_store(reinterpret_cast<unsigned*>(s.save_mean + cc), __float_as_uint(m),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(reinterpret_cast<unsigned*>(s.save_invstd + cc), __float_as_uint(is),
@@ -1412,26 +1390,11 @@ __global__ __launch_bounds__(kThreads) void k_proj_bn_fwd(ProjBnArgs a) {
       sm[threadIdx.x] = m;
       ss[threadIdx.x] = is;
     }
+    if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {  // seq_cst, completed and fenced (see bar_wait)
-      __hip_atomic_fetch_add((gu64c_t*)word, 1ull << 32, __ATOMIC_SEQ_CST,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    }
+    if (threadIdx.x == 0) publish_gen(word, 1ull << 32);  // completed (see take_left)
     pb_stamp<STAMPS>(a, 4, pb_now());
-    // off the waiting workgroups' path: the running statistics (the same
-    // finalisation arithmetic, now with the update), the batch counter, and
-    // the finaliser's own x
-    if (threadIdx.x < 64) {
-      float m, is;
-      fwd_finalize(s, n_base + threadIdx.x, sum0[threadIdx.x], sum1[threadIdx.x], n_eff, m, is,
-                   true);
-    }
-    if (s.nbt && by == 0 && threadIdx.x == 0) s.nbt[0] += 1;
-    store_tile_rows<kPbTN>(acc, scratch, m_base, g.M, g.C + n_base, g.ldc, kPbTN * 16, nullptr,
-                           0, vx);
   } else {
     if (threadIdx.x == 0) {
       unsigned ok = poll_gen(word, s_gen0, s.wait_us) ? 1u : 0u;
@@ -2170,12 +2133,6 @@ extern "C" int hlhgat_set_bn_one_launch(int on) {
 }
 
 extern "C" int hlhgat_get_bn_one_launch(void) { return bn_one_launch_flag() ? 1 : 0; }
-
-extern "C" int hlhgat_set_bn_bwd_rows(int rows) {
-  HLH_CHECK_ARG(rows == 4 || rows == 8, "set_bn_bwd_rows: rows must be 4 or 8");
-  g_bn_bwd_rb.store(rows, std::memory_order_relaxed);
-  return HLHGAT_OK;
-}
 
 extern "C" int hlhgat_set_bn_wait_us(unsigned wait_us) {
   g_wait_us = wait_us;

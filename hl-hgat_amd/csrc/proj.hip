@@ -1301,7 +1301,9 @@ extern "C" int hlhgat_proj_fwd(int nblocks, const float* const* A,
   }
   if (vec) {
     dim3 g((unsigned)ceil_div(M, 64), (unsigned)ceil_div(N, tn * 16));
-    a.xcd_map = fwd_xcd_map();
+    // large slabs only (configs 3 / 5: 1.4e5-2e5 rows); the config-2 shapes
+    // (2.3e4 rows, their A in L2 anyway) keep the blockIdx order
+    a.xcd_map = M >= 65536 ? fwd_xcd_map() : 0;
     if (tn == 1)
       launch(k_proj_fwd_lds<1>, g, 256, 0, s, &prof, a);
     else if (tn == 2)

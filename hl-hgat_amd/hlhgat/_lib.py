@@ -99,7 +99,6 @@ SIGNATURES = {
     "hlhgat_set_bn_one_launch": (c_i32, [c_i32]),
     "hlhgat_get_bn_one_launch": (c_i32, []),
     "hlhgat_set_bn_wait_us": (c_i32, [C.c_uint32]),
-    "hlhgat_set_bn_bwd_rows": (c_i32, [c_i32]),
     "hlhgat_set_proj_bn_stamps": (c_i32, [c_vp, c_i64]),
     "hlhgat_bn_giveup_log": (c_i32, [c_vp, c_i32, c_vp]),
     "hlhgat_bn_giveup_reset": (c_i32, []),

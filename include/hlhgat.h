@@ -667,10 +667,6 @@ int hlhgat_get_bn_one_launch(void);
  * hand over at once unless already final: a test hook that forces the
  * hand-over path, bitwise the same results). */
 int hlhgat_set_bn_wait_us(unsigned wait_us);
-/* Rows each thread of the BatchNorm backward reduction keeps in flight per
- * batch: 4 (default) or 8 (env HLHGAT_BN_BWD_RB=8).  Rows are summed in the
- * same order either way: bitwise the same results (A/B hook). */
-int hlhgat_set_bn_bwd_rows(int rows);
 
 /* Times a one-launch BatchNorm workgroup gave up waiting for its tile's
  * statistics (and handed its rows over): reads the device counter

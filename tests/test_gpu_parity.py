@@ -1500,44 +1500,6 @@ def test_bn_one_launch_bitwise(cuda, n, C, relu, pad):
     assert not outs[0][0][nv:].any()
 
 
-@pytest.mark.parametrize("n,C,pad", [(700, 64, 0), (23501, 64, 17), (207360, 128, 0),
-                                     (4097, 6, 5), (1000, 256, 0)])
-def test_bn_bwd_rows_in_flight_bitwise(cuda, n, C, pad):
-    """The BatchNorm backward reduction with 8 rows per batch == 4 rows per
-    batch (default), the batch's tail rows predicated in the same batch, bit
-    for bit: dx, dweight, dbias (rows summed in the same order); ragged
-    partitions, padded rows and an unaligned C (the scalar path) included."""
-    from hlhgat import _lib, ops
-    g = torch.Generator(device="cpu").manual_seed(n * 7 + C)
-    x0 = (torch.randn(n, C, generator=g) * 2 - 0.5).to(cuda)
-    R = torch.randn(n, C, generator=g).to(cuda)
-    valid = torch.tensor([n - pad], dtype=torch.int32, device=cuda) if pad else None
-    outs = []
-    try:
-        for rows in (4, 8):
-            _lib.check(_lib.LIB.hlhgat_set_bn_bwd_rows(rows), "set_bn_bwd_rows")
-            torch.manual_seed(0)
-            bn = torch.nn.BatchNorm1d(C).to(cuda).train()
-            with torch.no_grad():
-                bn.weight.uniform_(0.5, 1.5)
-                bn.bias.uniform_(-0.5, 0.5)
-            x = x0.clone().requires_grad_(True)
-            y = ops.batch_norm_act(x, bn, relu=True, valid=valid)
-            (y * R).sum().backward()
-            outs.append([x.grad, bn.weight.grad, bn.bias.grad])
-    finally:
-        _lib.LIB.hlhgat_set_bn_bwd_rows(4)
-    ops.check_device_errors()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-    nv = n - pad
-    xr = x0[:nv].double().requires_grad_(True)
-    yr = torch.nn.functional.batch_norm(xr, None, None, bn.weight.detach().double(),
-                                        bn.bias.detach().double(), training=True, eps=1e-5)
-    (yr.clamp_min(0) * R[:nv].double()).sum().backward()
-    close(outs[1][0][:nv].cpu(), xr.grad.float().cpu(), 1e-5, "bn backward vs fp64")
-
-
 def test_bn_one_launch_handover_bitwise(cuda):
     """A one-launch BatchNorm (k_bn_fwd_grid) whose waiting workgroups all
     give up at once (wait bound 0) hands their rows to the finalising

@@ -18,7 +18,6 @@ Variants (A/B hooks, not product settings):
   splitbn     projection + BatchNorm as the projection with a statistics epilogue
               (no wait) + the apply launch
   nobarrier   twolaunchbn + splitbn: no kernel of the step waits for another workgroup
-  rb8         the BatchNorm backward reduction with 8 rows per batch
 """
 import argparse
 import json
@@ -43,7 +42,6 @@ def set_variant(name, on):
     _lib.LIB.hlhgat_set_proj_bwd_rows(0 if (on and name == "norows") else 1)
     _lib.LIB.hlhgat_set_bn_one_launch(0 if (on and name in ("twolaunchbn", "nobarrier")) else 1)
     _lib.LIB.hlhgat_set_proj_bn_split(1 if (on and name in ("splitbn", "nobarrier")) else 0)
-    _lib.LIB.hlhgat_set_bn_bwd_rows(8 if (on and name == "rb8") else 4)
     from hlhgat import nn as hnn, hodge_st_model, train
     hnn.MLP_PAIRS = not (on and name == "nomlp2")
     hodge_st_model.READOUT_ON_CHAIN = not (on and name == "noreadside")

@@ -66,6 +66,11 @@ for s in "$@"; do
           T=$(find gpurun_out/prof3_$TAG -name '*kernel_trace.csv' | head -1)
           python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_cfg3_step_dispatches.csv > gpurun_out/${TAG}_cfg3_step_kernels.txt || true
           rm -rf gpurun_out/prof3_$TAG ;;
+    prof4) rm -rf gpurun_out/prof4_$TAG  # the config-4 head step (peptides attpool), replayed
+          step prof4 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4_$TAG -o run --output-format csv -- python3 bench.py --workload cfg4 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
+          T=$(find gpurun_out/prof4_$TAG -name '*kernel_trace.csv' | head -1)
+          python tools/step_kernels.py "$T" --step -3 --dump gpurun_out/${TAG}_cfg4_step_dispatches.csv > gpurun_out/${TAG}_cfg4_step_kernels.txt || true
+          rm -rf gpurun_out/prof4_$TAG ;;
     prof5s) rm -rf gpurun_out/prof5s_$TAG  # the same on ONE stream (HLHGAT_STREAM_FORK=0)
           HLHGAT_STREAM_FORK=0 step prof5s 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5s_$TAG -o run --output-format csv -- python3 bench.py --workload cfg5 --steps 10 --warmup 3 --batches 2 --no-cpu-baseline
           T=$(find gpurun_out/prof5s_$TAG -name '*kernel_trace.csv' | head -1)
