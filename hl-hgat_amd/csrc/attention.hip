@@ -107,6 +107,74 @@ __global__ __launch_bounds__(256) void k_att_bwd(AttArgs a) {
   }
 }
 
+// Row scaling by the attention score (the NEAtt product x0 * att,
+// main_pepfunc_HL_HGCNN_dense_int3_attpool.py:134-136, lib/Hodge_ST_Model.py:
+// 276-280): y[r] = x[r] * a[r]; backward dx[r] = dy[r] * a[r] and
+// da[r] = <dy[r], x[r]> in ONE pass over dy and x (ATen: a broadcast multiply,
+// a full-size product and a row reduction).  One LPR-lane group per row.
+struct ScaleArgs {
+  int64_t n;
+  int d;
+  const float* x;
+  int64_t ldx;
+  const float* a;
+  const float* dy;
+  int64_t lddy;
+  float* y;  // fwd: y; bwd: dx
+  int64_t ldy;
+  float* da;
+};
+
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_row_scale_fwd(ScaleArgs p) {
+  using vt = typename VecT<V>::type;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  if (row >= p.n) return;
+  const float s = p.a[row];
+  for (int f = sub * V; f < p.d; f += LPR * V) {
+    vt v = vload<V>(p.x + row * p.ldx + f);
+#pragma unroll
+    for (int c = 0; c < V; ++c) vget(v, c) = vget(v, c) * s;
+    vstore<V>(p.y + row * p.ldy + f, v);
+  }
+}
+
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_row_scale_bwd(ScaleArgs p) {
+  using vt = typename VecT<V>::type;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  const bool live = row < p.n;
+  float acc = 0.f;
+  if (live) {
+    const float s = p.a[row];
+    for (int f = sub * V; f < p.d; f += LPR * V) {
+      vt g = vload<V>(p.dy + row * p.lddy + f);
+      vt x = vload<V>(p.x + row * p.ldx + f);
+      vt o;
+#pragma unroll
+      for (int c = 0; c < V; ++c) {
+        vget(o, c) = vget(g, c) * s;
+        acc += vget(g, c) * vget(x, c);
+      }
+      vstore<V>(p.y + row * p.ldy + f, o);
+    }
+  }
+  acc = group_sum<LPR>(acc);  // every lane of the wave takes part
+  if (live && sub == 0) p.da[row] = acc;
+}
+
+int pick_v_scale(const ScaleArgs& p) {
+  for (int v : {4, 2}) {
+    bool ok = p.d % v == 0 && p.ldx % v == 0 && p.ldy % v == 0 &&
+              ((uintptr_t)p.x % (4 * v)) == 0 && ((uintptr_t)p.y % (4 * v)) == 0;
+    if (p.dy) ok = ok && p.lddy % v == 0 && ((uintptr_t)p.dy % (4 * v)) == 0;
+    if (ok) return v;
+  }
+  return 1;
+}
+
 int pick_v(const AttArgs& a, bool bwd) {
   for (int v : {4, 2}) {
     bool ok = a.dk % v == 0 && a.ldqc % v == 0 && a.ldqs % v == 0 && a.ldk % v == 0;
@@ -227,6 +295,38 @@ extern "C" int hlhgat_att_score_bwd(int64_t n, int64_t dk, const float* Qc,
   const unsigned grid = (unsigned)ceil_div(n, 256 / l);
   hipStream_t s = as_stream(stream);
   HLH_ATT_DISPATCH(k_att_bwd, v, l, grid, s, a);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_row_scale_fwd(int64_t n, int64_t d, const float* x, int64_t ldx,
+                                    const float* a, float* y, int64_t ldy, void* stream) {
+  HLH_CHECK_ARG(n >= 0 && d > 0 && ldx >= d && ldy >= d, "row_scale_fwd: bad sizes");
+  if (n == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(x && a && y, "row_scale_fwd: NULL pointer");
+  ScaleArgs p{n, (int)d, x, ldx, a, nullptr, 0, y, ldy, nullptr};
+  const int v = pick_v_scale(p);
+  int l = next_pow2((int)ceil_div(d, v));
+  if (l > 64) l = 64;
+  const unsigned grid = (unsigned)ceil_div(n, 256 / l);
+  HLH_ATT_DISPATCH(k_row_scale_fwd, v, l, grid, as_stream(stream), p);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_row_scale_bwd(int64_t n, int64_t d, const float* x, int64_t ldx,
+                                    const float* a, const float* dy, int64_t lddy, float* dx,
+                                    int64_t lddx, float* da, void* stream) {
+  HLH_CHECK_ARG(n >= 0 && d > 0 && ldx >= d && lddy >= d && lddx >= d,
+                "row_scale_bwd: bad sizes");
+  if (n == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(x && a && dy && dx && da, "row_scale_bwd: NULL pointer");
+  ScaleArgs p{n, (int)d, x, ldx, a, dy, lddy, dx, lddx, da};
+  const int v = pick_v_scale(p);
+  int l = next_pow2((int)ceil_div(d, v));
+  if (l > 64) l = 64;
+  const unsigned grid = (unsigned)ceil_div(n, 256 / l);
+  HLH_ATT_DISPATCH(k_row_scale_bwd, v, l, grid, as_stream(stream), p);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -523,10 +523,19 @@ __global__ __launch_bounds__(256) void k_segment_mean_bwd(SegArgs a) {
   if (s >= a.n_seg) {
     const int64_t z = s - a.n_seg;
     if (z >= a.n_fill) return;
-    const int64_t lo = a.ptr[0], hi = a.ptr[a.n_seg];
     vt zero;
 #pragma unroll
     for (int c = 0; c < V; ++c) vget(zero, c) = 0.f;
+    if (a.rows) {
+      // listed members covering every row (hlhgat_pool_mean_bwd): the
+      // trailing bucket n_seg lists the rows in no segment, zeroed here
+      for (int64_t t = a.ptr[a.n_seg] + z; t < a.ptr[a.n_seg + 1]; t += a.n_fill) {
+        const int64_t r = a.rows[t];
+        for (int f = sub * V; f < a.d; f += LPR * V) vstore<V>(a.out + r * a.ldo + f, zero);
+      }
+      return;
+    }
+    const int64_t lo = a.ptr[0], hi = a.ptr[a.n_seg];
     for (int64_t r = z; r < a.n_rows; r += a.n_fill) {
       if (r >= lo && r < hi) {
         r = hi - 1 - ((hi - 1 - z) % a.n_fill);  // next stride point >= hi
@@ -1110,6 +1119,25 @@ extern "C" int hlhgat_segment_mean_fwd(const int32_t* seg_ptr,
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
   HLH_DISPATCH_VL(v, l, k_segment_mean_fwd, n_seg, s, a, nullptr);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_pool_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
+                                    int64_t n_seg, const float* dout, int64_t ldo, int64_t d,
+                                    float* dx, int64_t ldx, int64_t n_rows, void* stream) {
+  HLH_CHECK_ARG(n_seg >= 0 && d > 0 && ldx >= d && ldo >= d && n_rows >= 0,
+                "pool_mean_bwd: bad sizes");
+  if (n_rows == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(seg_ptr && seg_rows && dx && (n_seg == 0 || dout),
+                "pool_mean_bwd: NULL pointer");
+  // lane groups after the segment groups stride over the zero bucket
+  const int64_t n_fill = n_rows < 1024 ? n_rows : 1024;
+  SegArgs a{seg_ptr, seg_rows, n_seg, dout, ldo, (int)d, dx, ldx, n_rows, n_fill};
+  const int v = pick_vec(d, {ldx, ldo}, {dout, dx});
+  const int l = pick_lpr(d, v);
+  hipStream_t s = as_stream(stream);
+  HLH_DISPATCH_VL(v, l, k_segment_mean_bwd, n_seg + n_fill, s, a, nullptr);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

@@ -119,6 +119,11 @@ SIGNATURES = {
                                         c_vp]),
     "hlhgat_segment_mean_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                         c_i64, c_vp]),
+    "hlhgat_row_scale_fwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
+    "hlhgat_row_scale_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                     c_vp, c_vp]),
+    "hlhgat_pool_mean_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                     c_i64, c_vp]),
     "hlhgat_bn_workspace_bytes": (c_i64, [c_i64, c_i64]),
     "hlhgat_bn_apply_running": (c_i32, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_f32,
                                         c_i32, c_vp, c_i64, c_vp]),

@@ -262,14 +262,12 @@ class NodeEdgeInt(nn.Module):
             b_t = torch.cat([self.WK_Node.bias, self.WQ_Node.bias], 0)
             kq_t = ops.linear_blocks([x_t], w_t, b_t)
             qc_t = ops.linear_blocks([x_s2t], self.WQ_Edge.weight, self.WQ_Edge.bias)
-            a_t = ops.att_score(qc_t, kq_t[:, dk:], kq_t[:, :dk], 1 - self.lambda_Node,
-                                self.lambda_Node, sq, code)
+            a_t = ops.att_score_kq(qc_t, kq_t, 1 - self.lambda_Node, self.lambda_Node, sq, code)
             w_s = torch.cat([self.WK_Edge.weight, self.WQ_Edge.weight], 0)
             b_s = torch.cat([self.WK_Edge.bias, self.WQ_Edge.bias], 0)
             kq_s = ops.linear_blocks([x_s], w_s, b_s)
             qc_s = ops.linear_blocks([x_t2s], self.WQ_Node.weight, self.WQ_Node.bias)
-            a_s = ops.att_score(qc_s, kq_s[:, dk:], kq_s[:, :dk], 1 - self.lambda_Edge,
-                                self.lambda_Edge, sq, code)
+            a_s = ops.att_score_kq(qc_s, kq_s, 1 - self.lambda_Edge, self.lambda_Edge, sq, code)
             if isinstance(self.sigma, nn.ReLU):
                 _nn.tap(self.sigma, a_t)
                 _nn.tap(self.sigma, a_s)

@@ -441,17 +441,19 @@ def _has_pool_tables(d0, device) -> bool:
                for k in ("pool_rowptr_t", "pool_rows_t", "pool_rowptr_s", "pool_rows_s"))
 
 
-def _pool(x: torch.Tensor, pos, d0, side: str, n_seg: int) -> torch.Tensor:
+def _pool(x: torch.Tensor, pos, d0, side: str, n_seg: int, out=None, gsink=None) -> torch.Tensor:
     """cluster_mean(x, pos, n_seg) -- from the level list's collate-time
     cluster CSR when it carries one (hodge_dataset.pool_tables: the CSR
-    cluster_mean would sort on the device, so the same bits), else on the
-    device from pos."""
+    cluster_mean would sort on the device, so the same bits; written into
+    ``out``, a DenseConcat sink, when given; x's gradient into ``gsink``, the
+    gradient slab of x = DenseConcat.view(), when given), else on the device
+    from pos."""
     if pos is None:
         rp, rows = getattr(d0, "pool_rowptr_" + side), getattr(d0, "pool_rows_" + side)
         if rp.numel() != n_seg + 2 or rows.numel() != x.size(0):
             raise RuntimeError(f"hlhgat: pool tables ({rp.numel() - 2} clusters, {rows.numel()} "
                                f"rows) do not match ({n_seg}, {x.size(0)})")
-        return ops.segment_mean(x, rp, n_seg, rows)
+        return ops.segment_mean(x, rp, n_seg, rows, out=out, covering=True, gsink=gsink)
     return cluster_mean(x, pos, n_seg)
 
 
@@ -563,6 +565,21 @@ class _AttPoolHead(nn.Module):
             mlp_insize = mlp_outsize
         self.out = Linear(mlp_insize, num_classes)
 
+    def _slab_ends(self, i: int) -> bool:
+        """Level i ends by scaling (att) or pooling x0: the next level starts
+        a new dense slab."""
+        return (self.att_mode == "every" or i == self.pool_loc
+                or i == len(self.channels) - 1)
+
+    def _run_width(self, i: int) -> int:
+        """Columns the blocks of levels i..(the end of i's slab run) add."""
+        w = 0
+        for q in range(i, len(self.channels)):
+            w += self.channels[q] * self.filters[q]
+            if self._slab_ends(q):
+                break
+        return w
+
     def forward(self, datas, device="cuda:0", if_final_layer=False, if_att=False):
         d0 = datas[0]
         dev = d0.x_t.device
@@ -584,14 +601,22 @@ class _AttPoolHead(nn.Module):
         D = _node_degree(d0, x_t0.shape[0], x_t0.device) + self._deg_eps
         att_t = att_s = None
         dense = x_t.is_cuda and ops.DENSE_SLAB
+        nxt = None  # the next run's slabs, already holding the pooled x0
+        last = len(self.channels) - 1
         for i, _ in enumerate(self.channels):
-            # one dense slab per level: x0 (scaled / pooled) then the level's blocks
-            if dense:
-                w = x_t0.size(1) + self.channels[i] * self.filters[i]
-                dt = ops.DenseConcat(x_t0.size(0), w, x_t0)
-                ds = ops.DenseConcat(x_s0.size(0), w, x_s0)
-                dt.append(x_t0)
-                ds.append(x_s0)
+            # one dense slab per run of levels: x0 (scaled / pooled) then the
+            # blocks of every level up to the next scale or pool of x0 (levels
+            # whose x0 passes unchanged continue the same slab: no re-copy)
+            if dense and (i == 0 or self._slab_ends(i - 1)):
+                if nxt is not None:
+                    dt, ds = nxt
+                    nxt = None
+                else:
+                    w = x_t0.size(1) + self._run_width(i)
+                    dt = ops.DenseConcat(x_t0.size(0), w, x_t0)
+                    ds = ops.DenseConcat(x_s0.size(0), w, x_s0)
+                    dt.append(x_t0)
+                    ds.append(x_s0)
             for j in range(self.channels[i]):
                 neint = getattr(self, "NEInt{}{}".format(i, j))
                 if dense:
@@ -610,12 +635,34 @@ class _AttPoolHead(nn.Module):
                 else:
                     x_t0 = torch.cat([x_t0, x_t], dim=-1)
                     x_s0 = torch.cat([x_s0, x_s], dim=-1)
-            if dense:
+            if dense and self._slab_ends(i):
+                # (a continuing slab takes no view here: the first view taken
+                # after a part is appended hands that part its gradient, so it
+                # must be one the next level's NodeEdgeInt consumes)
                 x_t0, x_s0 = dt.view(), ds.view()
             if self.att_mode == "every" or (self.att_mode == "concat" and i == self.pool_loc):
                 att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t0, x_s0, par_1, D)
-                x_t0 = x_t0 * att_t
-                x_s0 = x_s0 * att_s
+                if i == last:
+                    pass  # x0 is not part of the readout: the product is never read
+                elif dense:
+                    out_t = out_s = None
+                    if i != self.pool_loc:
+                        # the scaled x0 lands in the first columns of the next slabs
+                        w = x_t0.size(1) + self._run_width(i + 1)
+                        nt = ops.DenseConcat(x_t0.size(0), w, x_t0)
+                        ns = ops.DenseConcat(x_s0.size(0), w, x_s0)
+                        out_t, out_s = nt.sink(x_t0.size(1)), ns.sink(x_s0.size(1))
+                    # fresh views, consumed by the product alone: its input
+                    # gradient is written into the slab's gradient in place
+                    x_t0 = ops.row_scale(dt.view(), att_t, out_t, dt.grad_sink())
+                    x_s0 = ops.row_scale(ds.view(), att_s, out_s, ds.grad_sink())
+                    if out_t is not None:
+                        nt.append(x_t0)
+                        ns.append(x_s0)
+                        nxt = (nt, ns)
+                else:
+                    x_t0 = x_t0 * att_t
+                    x_s0 = x_s0 * att_s
             if i == self.pool_loc:
                 if self.att_mode == "block":
                     att_t, att_s = getattr(self, "NEAtt%d" % i)(x_t, x_s, par_1, D)
@@ -627,11 +674,31 @@ class _AttPoolHead(nn.Module):
                                                                getattr(dk, "n_valid_t", None)))
                         att_s = att_s / global_max(_valid_rows(att_s,
                                                                getattr(dk, "n_valid_s", None)))
-                    x_t = x_t * att_t
-                    x_s = x_s * att_s
+                    if i == last:
+                        # below the last level the scaled block output is never
+                        # read (the next level's first NEConv replaces x_t): the
+                        # reference's product is dead there, att is still returned
+                        x_t = x_t * att_t
+                        x_s = x_s * att_s
                 d1 = datas[k + 1]
-                x_t0 = _pool(x_t0, pos_t, d0, "t", d1.x_t.shape[0])
-                x_s0 = _pool(x_s0, pos_s, d0, "s", d1.x_s.shape[0])  # inf members dropped
+                out_t = out_s = None
+                if dense and i < last and pos_t is None:
+                    # the pooled x0 lands in the first columns of the next run's slabs
+                    w = x_t0.size(1) + self._run_width(i + 1)
+                    nt = ops.DenseConcat(d1.x_t.shape[0], w, x_t0)
+                    ns = ops.DenseConcat(d1.x_s.shape[0], w, x_s0)
+                    out_t, out_s = nt.sink(x_t0.size(1)), ns.sink(x_s0.size(1))
+                # block mode pools the slab view itself: its gradient goes
+                # straight into the slab's gradient
+                gk_t = gk_s = None
+                if dense and self.att_mode == "block":
+                    gk_t, gk_s = dt.grad_sink(), ds.grad_sink()
+                x_t0 = _pool(x_t0, pos_t, d0, "t", d1.x_t.shape[0], out_t, gk_t)
+                x_s0 = _pool(x_s0, pos_s, d0, "s", d1.x_s.shape[0], out_s, gk_s)  # inf dropped
+                if out_t is not None:
+                    nt.append(x_t0)
+                    ns.append(x_s0)
+                    nxt = (nt, ns)
                 edge_index_s, edge_weight_s = d1.edge_index_s, d1.edge_weight_s
                 edge_index_t, edge_weight_t = d1.edge_index_t, d1.edge_weight_t
                 k = 1

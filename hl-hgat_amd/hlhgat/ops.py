@@ -1350,6 +1350,101 @@ class _AttScoreFn(torch.autograd.Function):
         return g[0], g[1], g[2], None, None, None, None
 
 
+class _AttScoreKQFn(torch.autograd.Function):
+    """_AttScoreFn with K = kq[:, :dk] and Qs = kq[:, dk:2dk] (one GEMM's
+    output): the backward returns kq's gradient as ONE [n, 2dk] block, no
+    per-slice zero fill + copy + add."""
+
+    @staticmethod
+    def forward(ctx, Qc, kq, w_cross, w_self, sqrt_dk, sigma):
+        n, dk = kq.size(0), Qc.size(1)
+        a = torch.empty(n, 1, device=kq.device, dtype=kq.dtype)
+        check(LIB.hlhgat_att_score_fwd(n, dk, Qc.data_ptr(), _ld(Qc), kq.data_ptr() + 4 * dk,
+                                       _ld(kq), kq.data_ptr(), _ld(kq), w_cross, w_self, sqrt_dk,
+                                       sigma, a.data_ptr(), _stream(kq)), "att_score_fwd")
+        ctx.consts = (w_cross, w_self, sqrt_dk, sigma)
+        ctx.save_for_backward(Qc, kq, a)
+        return a
+
+    @staticmethod
+    def backward(ctx, ga):
+        Qc, kq, a = ctx.saved_tensors
+        w_cross, w_self, sqrt_dk, sigma = ctx.consts
+        n, dk = kq.size(0), Qc.size(1)
+        ga = ga.contiguous()
+        # columns [0, dk) dK, [dk, 2dk) dQs (= d kq), [2dk, 3dk) dQc
+        g = torch.empty(n, 3 * dk, device=kq.device, dtype=kq.dtype)
+        p = g.data_ptr()
+        check(LIB.hlhgat_att_score_bwd(n, dk, Qc.data_ptr(), _ld(Qc), kq.data_ptr() + 4 * dk,
+                                       _ld(kq), kq.data_ptr(), _ld(kq), w_cross, w_self, sqrt_dk,
+                                       sigma, a.data_ptr(), ga.data_ptr(), p + 8 * dk,
+                                       p + 4 * dk, p, 3 * dk, _stream(kq)), "att_score_bwd")
+        return g[:, 2 * dk:], g[:, :2 * dk], None, None, None, None
+
+
+def att_score_kq(Qc, kq, w_cross: float, w_self: float, sqrt_dk: float,
+                 sigma: int) -> torch.Tensor:
+    """att_score(Qc, kq[:, dk:], kq[:, :dk], ...) with dk = Qc.size(1): the
+    key and the self query as the two column halves of one [n, 2dk] GEMM
+    output (lib/Hodge_Cheb_Conv.py:299-304)."""
+    _req_dev(Qc, "Qc")
+    _req_dev(kq, "kq")
+    Qc, kq = _rows2d(Qc, "Qc"), _rows2d(kq, "kq")
+    if kq.size(1) != 2 * Qc.size(1) or kq.size(0) != Qc.size(0):
+        raise RuntimeError(f"hlhgat: att_score_kq: kq {tuple(kq.shape)} vs Qc {tuple(Qc.shape)}")
+    return _AttScoreKQFn.apply(Qc, kq, float(w_cross), float(w_self), float(sqrt_dk), int(sigma))
+
+
+class _RowScaleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a, out, gsink):
+        n, d = x.size(0), x.size(1)
+        y = out if out is not None else torch.empty(n, d, device=x.device, dtype=x.dtype)
+        check(LIB.hlhgat_row_scale_fwd(n, d, x.data_ptr(), _ld(x), a.data_ptr(), y.data_ptr(),
+                                       _ld(y), _stream(x)), "row_scale_fwd")
+        ctx.gsink = gsink
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, a = ctx.saved_tensors
+        n, d = x.size(0), x.size(1)
+        g = _rows2d(g, "grad")
+        sink, flag = ctx.gsink if ctx.gsink is not None else (None, None)
+        if sink is not None and int(flag[0]) == 0:
+            gx = sink  # the first gradient into x's slab: written in place
+            flag[0] = 1
+        else:
+            gx = torch.empty(n, d, device=x.device, dtype=x.dtype)
+        ga = torch.empty(n, 1, device=x.device, dtype=x.dtype)
+        check(LIB.hlhgat_row_scale_bwd(n, d, x.data_ptr(), _ld(x), a.data_ptr(), g.data_ptr(),
+                                       _ld(g), gx.data_ptr(), _ld(gx), ga.data_ptr(),
+                                       _stream(x)), "row_scale_bwd")
+        return gx, ga, None, None
+
+
+def row_scale(x: torch.Tensor, a: torch.Tensor, out: Optional[torch.Tensor] = None,
+              gsink=None) -> torch.Tensor:
+    """x * a for a per-row score a [n, 1] (the NEAtt product, main_pepfunc...:
+    134-136): bitwise ATen's product; the backward's da = rowsum(dy * x) is
+    one fused pass (fp32, its own summation order).  out: a DenseConcat sink
+    for y; gsink: DenseConcat.grad_sink() of x = view(), written in place
+    when x's gradient lands there first -- x must then have no other
+    consumer (take a fresh view())."""
+    _req_dev(x, "x")
+    _req_dev(a, "a")
+    x = _rows2d(x, "x")
+    if a.numel() != x.size(0):
+        raise RuntimeError(f"hlhgat: row_scale: a has {a.numel()} entries for {x.size(0)} rows")
+    a = a.contiguous()
+    if out is not None and (tuple(out.shape) != tuple(x.shape) or out.stride(1) != 1):
+        raise RuntimeError(f"hlhgat: row_scale out {tuple(out.shape)} vs x {tuple(x.shape)}")
+    if gsink is not None and (gsink[0] is None or gsink[0].shape != x.shape):
+        gsink = None
+    return _RowScaleFn.apply(x, a, out, gsink)
+
+
 def att_score(Qc, Qs, Kr, w_cross: float, w_self: float, sqrt_dk: float,
               sigma: int) -> torch.Tensor:
     """sigma((w_cross<Qc,K> + w_self<Qs,K>)/sqrt_dk) per row -> [n, 1]
@@ -1365,27 +1460,43 @@ def att_score(Qc, Qs, Kr, w_cross: float, w_self: float, sqrt_dk: float,
 # ----------------------------------------------------------------------------
 class _SegmentMeanFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, seg_ptr, seg_rows, n_seg):
+    def forward(ctx, x, seg_ptr, seg_rows, n_seg, out, covering, gsink):
         d = x.size(1)
-        out = torch.empty(n_seg, d, device=x.device, dtype=x.dtype)
+        if out is None:
+            out = torch.empty(n_seg, d, device=x.device, dtype=x.dtype)
         check(LIB.hlhgat_segment_mean_fwd(seg_ptr.data_ptr(), _ptr(seg_rows), n_seg,
                                           x.data_ptr(), _ld(x), d, out.data_ptr(), _ld(out),
                                           _stream(x)), "segment_mean_fwd")
-        ctx.meta = (x.size(0), n_seg, seg_rows is not None)
+        ctx.meta = (x.size(0), n_seg, seg_rows is not None, covering)
+        ctx.gsink = gsink
         ctx.save_for_backward(seg_ptr, seg_rows if seg_rows is not None else seg_ptr)
         return out
 
     @staticmethod
     def backward(ctx, g):
         seg_ptr, seg_rows = ctx.saved_tensors
-        n_rows, n_seg, listed = ctx.meta
+        n_rows, n_seg, listed, covering = ctx.meta
         g = _rows2d(g, "grad")
+        if covering:
+            # every row is listed (the trailing bucket: rows in no cluster,
+            # written as zeros): no zero fill; into the slab's gradient when
+            # this is the first gradient to land there (DenseConcat.grad_sink)
+            sink, flag = ctx.gsink if ctx.gsink is not None else (None, None)
+            if sink is not None and int(flag[0]) == 0 and sink.shape == (n_rows, g.size(1)):
+                gx = sink
+                flag[0] = 1
+            else:
+                gx = torch.empty(n_rows, g.size(1), device=g.device, dtype=g.dtype)
+            check(LIB.hlhgat_pool_mean_bwd(seg_ptr.data_ptr(), seg_rows.data_ptr(), n_seg,
+                                           g.data_ptr(), _ld(g), g.size(1), gx.data_ptr(),
+                                           _ld(gx), n_rows, _stream(g)), "pool_mean_bwd")
+            return gx, None, None, None, None, None, None
         gx = (torch.zeros if listed else torch.empty)(n_rows, g.size(1), device=g.device,
                                                       dtype=g.dtype)
         check(LIB.hlhgat_segment_mean_bwd(seg_ptr.data_ptr(), _ptr(seg_rows) if listed else None,
                                           n_seg, g.data_ptr(), _ld(g), g.size(1), gx.data_ptr(),
                                           _ld(gx), n_rows, _stream(g)), "segment_mean_bwd")
-        return gx, None, None, None
+        return gx, None, None, None, None, None, None
 
 
 class _SegmentMeanCatFn(torch.autograd.Function):
@@ -1457,15 +1568,33 @@ def segment_mean_cat(xs: Sequence[torch.Tensor], seg_ptrs: Sequence[torch.Tensor
 
 
 def segment_mean(x: torch.Tensor, seg_ptr: torch.Tensor, n_seg: int,
-                 seg_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 seg_rows: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                 covering: bool = False, gsink=None) -> torch.Tensor:
     """Mean of x rows per segment.  seg_ptr int32 [n_seg+1]; members are the
     contiguous rows seg_ptr[s]..seg_ptr[s+1] (global_mean_pool over a sorted
-    batch vector) or seg_rows[seg_ptr[s]:seg_ptr[s+1]] (scatter_mean)."""
+    batch vector) or seg_rows[seg_ptr[s]:seg_ptr[s+1]] (scatter_mean).
+    covering: seg_ptr has n_seg+2 entries and the extra segment lists the
+    rows in no segment, so seg_rows is a permutation of x's rows (the pool
+    tables of hodge_dataset.pool_tables); the backward then writes every row
+    (zeros for that bucket) without a zero fill, into ``gsink`` (a
+    DenseConcat.grad_sink of x) when it is the first gradient there.  out: a
+    [n_seg, d] destination (a DenseConcat sink) instead of a new tensor."""
     _req_dev(x, "x")
     _req_dev(seg_ptr, "seg_ptr", torch.int32)
     if seg_rows is not None:
         _req_dev(seg_rows, "seg_rows", torch.int32)
-    return _SegmentMeanFn.apply(_rows2d(x, "x"), seg_ptr, seg_rows, int(n_seg))
+    x = _rows2d(x, "x")
+    if covering and (seg_rows is None or seg_ptr.numel() != n_seg + 2
+                     or seg_rows.numel() != x.size(0)):
+        raise RuntimeError("hlhgat: segment_mean(covering=True) needs seg_ptr [n_seg+2] and "
+                           "seg_rows listing every row of x")
+    if out is not None and (tuple(out.shape) != (n_seg, x.size(1)) or out.stride(1) != 1
+                            or out.device != x.device or out.dtype != x.dtype):
+        raise RuntimeError(f"hlhgat: segment_mean out {tuple(out.shape)} does not match "
+                           f"({n_seg}, {x.size(1)})")
+    if gsink is not None and (gsink[0] is None or gsink[0].shape != x.shape):
+        gsink = None
+    return _SegmentMeanFn.apply(x, seg_ptr, seg_rows, int(n_seg), out, bool(covering), gsink)
 
 
 # ----------------------------------------------------------------------------

@@ -540,6 +540,18 @@ int hlhgat_att_score_bwd(int64_t n, int64_t dk, const float* Qc, int64_t ldqc,
                          const float* da, float* dQc, float* dQs, float* dK,
                          int64_t ldg, void* stream);
 
+/* The NEAtt product x0 * att of the attention-pooling heads
+ * (main_pepfunc_HL_HGCNN_dense_int3_attpool.py:134-136, lib/Hodge_ST_Model.py:
+ * 276-280): y[r][:] = x[r][:] * a[r] over n rows of d features (y may be a
+ * column block of a wider slab, ldy). */
+int hlhgat_row_scale_fwd(int64_t n, int64_t d, const float* x, int64_t ldx,
+                         const float* a, float* y, int64_t ldy, void* stream);
+/* Its backward in one pass: dx[r][:] = dy[r][:] * a[r] and
+ * da[r] = sum_j dy[r][j] * x[r][j]. */
+int hlhgat_row_scale_bwd(int64_t n, int64_t d, const float* x, int64_t ldx,
+                         const float* a, const float* dy, int64_t lddy, float* dx,
+                         int64_t lddx, float* da, void* stream);
+
 /* ---- segment mean (scatter_mean / global_mean_pool) -------------------- */
 /* out[s] = mean over rows r of CSR segment s of x[r] (rows listed in
  * seg_rows, or contiguous when seg_rows == NULL); empty segments give 0. */
@@ -556,6 +568,19 @@ int hlhgat_segment_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
                             int64_t n_seg, const float* dout, int64_t ldo,
                             int64_t d, float* dx, int64_t ldx, int64_t n_rows,
                             void* stream);
+
+/* Backward of the MLGC cluster pooling (scatter_mean over pos_ts / pos_ss,
+ * lib/Hodge_ST_Model.py:1066-1069) from the pool tables
+ * (hlhgat.hodge_dataset.pool_tables): seg_ptr has n_seg + 2 entries and its
+ * extra segment n_seg lists the rows in no cluster (inf cluster id: padding
+ * rows, edges between clusters), so seg_rows[0 .. seg_ptr[n_seg+1]) is a
+ * permutation of the n_rows rows.  dx[r] = dout[s] / |s| for a member of
+ * cluster s, exact zeros for the extra segment's rows: every row of dx is
+ * written (no caller zero fill). */
+int hlhgat_pool_mean_bwd(const int32_t* seg_ptr, const int32_t* seg_rows,
+                         int64_t n_seg, const float* dout, int64_t ldo,
+                         int64_t d, float* dx, int64_t ldx, int64_t n_rows,
+                         void* stream);
 
 /* ---- BatchNorm1d (training) + optional fused ReLU ---------------------- */
 /* gnn.BatchNorm / nn.BatchNorm1d in training mode over x [n][C] (batch

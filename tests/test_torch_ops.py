@@ -192,3 +192,73 @@ def test_opcheck(cuda):
     torch.library.opcheck(h.att_score.default, (*q, 0.1, 0.9, 8 ** 0.5, 1), test_utils=tests)
     ptr = torch.tensor([0, n // 2, n], dtype=torch.int32, device=cuda)
     torch.library.opcheck(h.segment_mean.default, (x, ptr, None, 2), test_utils=tests)
+
+
+@pytest.mark.gpu
+def test_row_scale_att_kq_pool_bwd_match_torch(cuda):
+    """The attention-pooling heads' glue kernels: ops.row_scale (x0 * att,
+    main_pepfunc...:134-136) against ATen's broadcast product (forward and dx
+    bitwise, da to fp32 rounding); att_score_kq against att_score on the two
+    column halves (bitwise); segment_mean(covering=True) (the pool tables'
+    backward, zero bucket written by the kernel) against the zero-filled
+    scatter_mean backward (bitwise), also into a strided slab column block."""
+    from hlhgat import ops
+    g = torch.Generator().manual_seed(11)
+    for n, d in ((517, 448), (300, 192), (64, 3)):
+        x = torch.randn(n, d + 5, generator=g)[:, :d].to(cuda)  # strided rows
+        a = torch.rand(n, 1, generator=g).to(cuda)
+        xd, ad = x.clone().requires_grad_(True), a.clone().requires_grad_(True)
+        y = ops.row_scale(xd, ad)
+        xr, ar = x.clone().requires_grad_(True), a.clone().requires_grad_(True)
+        yr = xr * ar
+        assert torch.equal(y, yr)
+        R_ = torch.randn(n, d, generator=g).to(cuda)
+        (y * R_).sum().backward()
+        (yr * R_).sum().backward()
+        assert torch.equal(xd.grad, xr.grad)
+        close(ad.grad.cpu(), ar.grad.cpu(), 1e-5, "row_scale da")
+        slab = torch.zeros(n, d + 64, device=cuda)
+        y2 = ops.row_scale(x, a, out=slab[:, :d])
+        assert y2.data_ptr() == slab.data_ptr() and torch.equal(slab[:, :d], yr.detach())
+        assert not slab[:, d:].any()
+    dk = 32
+    qc = torch.randn(200, dk, generator=g).to(cuda)
+    kq = torch.randn(200, 2 * dk, generator=g).to(cuda)
+    q1, k1 = qc.clone().requires_grad_(True), kq.clone().requires_grad_(True)
+    q2, k2 = qc.clone().requires_grad_(True), kq.clone().requires_grad_(True)
+    for code in (ops.SIGMA_SIGMOID, ops.SIGMA_RELU):
+        a1 = ops.att_score_kq(q1, k1, 0.1, 0.9, float(np.sqrt(dk)), code)
+        a2 = ops.att_score(q2, k2[:, dk:], k2[:, :dk], 0.1, 0.9, float(np.sqrt(dk)), code)
+        assert torch.equal(a1, a2)
+        w = torch.randn(200, 1, generator=g).to(cuda)
+        (a1 * w).sum().backward()
+        (a2 * w).sum().backward()
+        assert torch.equal(q1.grad, q2.grad) and torch.equal(k1.grad, k2.grad)
+    # covering pool tables: 4 clusters, rows 3, 7, 11 in no cluster (bucket 4)
+    n, d, n_seg = 13, 24, 4
+    assign = torch.tensor([0, 1, 1, -1, 2, 0, 3, -1, 2, 2, 1, -1, 0])
+    order = torch.argsort(torch.where(assign < 0, n_seg, assign), stable=True)
+    counts = torch.bincount(torch.where(assign < 0, n_seg, assign), minlength=n_seg + 1)
+    rp = torch.zeros(n_seg + 2, dtype=torch.int32)
+    rp[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    rows = order.to(torch.int32)
+    x = torch.randn(n, d, generator=g).to(cuda)
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    s1 = ops.segment_mean(x1, rp.to(cuda), n_seg, rows.to(cuda), covering=True)
+    s2 = ops.segment_mean(x2, rp[:n_seg + 1].to(cuda), n_seg, rows[:int(rp[n_seg])].to(cuda))
+    assert torch.equal(s1, s2)
+    gr = torch.randn(n_seg, d, generator=g).to(cuda)
+    (s1 * gr).sum().backward()
+    (s2 * gr).sum().backward()
+    assert torch.equal(x1.grad, x2.grad) and not x1.grad[assign < 0].any()
+    # into a strided destination + the gradient sink of a DenseConcat-style slab
+    G = torch.full((n, d + 8), float("nan"), device=cuda)
+    flag = torch.zeros(1, dtype=torch.int32)
+    out = torch.zeros(n_seg, d + 4, device=cuda)
+    x3 = x.clone().requires_grad_(True)
+    s3 = ops.segment_mean(x3, rp.to(cuda), n_seg, rows.to(cuda), out=out[:, :d], covering=True,
+                          gsink=(G[:, :d], flag))
+    assert s3.data_ptr() == out.data_ptr() and torch.equal(out[:, :d], s2.detach())
+    (s3 * gr).sum().backward()
+    assert int(flag[0]) == 1 and torch.equal(G[:, :d], x2.grad)
+    assert torch.isnan(G[:, d:]).all()
