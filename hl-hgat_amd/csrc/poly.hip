@@ -457,6 +457,49 @@ __global__ __launch_bounds__(256) void k_edge_gather2(Gather2Args a) {
   }
 }
 
+// The TSP readout's x_t2s = |B1^T x_t| / 2 per edge (lib/Hodge_ST_Model.py:
+// 846-848: sparse.mm(par_1^T, x_t), .abs(), / 2) in one pass, and its
+// backward's edge factor (g / 2) * sgn(x_j - x_i) (DivBackward, AbsBackward)
+// before the B1 product: the arithmetic of the unfused ops, bit for bit.
+// BWD: a.z holds g; out = the edge factor.
+template <bool BWD, int V, int LPR>
+__device__ __forceinline__ void edge_absdiff_body(const Gather2Args& a) {
+  using vt = typename VecT<V>::type;
+  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPR;
+  const int sub = threadIdx.x % LPR;
+  if (e >= a.n_edges) return;
+  const int64_t i = a.ei[e];
+  const int64_t j = a.ei[a.n_edges + e];
+  for (int f = sub * V; f < a.d; f += LPR * V) {
+    vt xi = vload<V>(a.x + i * a.ldx + f);
+    vt xj = vload<V>(a.x + j * a.ldx + f);
+    vt o;
+    if (BWD) {
+      vt g = vload<V>(a.z + e * a.ldz + f);
+#pragma unroll
+      for (int c = 0; c < V; ++c) {
+        const float dd = -vget(xi, c) + vget(xj, c);
+        const float sg = dd > 0.f ? 1.f : (dd < 0.f ? -1.f : 0.f);  // torch.sgn
+        vget(o, c) = (vget(g, c) * 0.5f) * sg;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < V; ++c) vget(o, c) = fabsf(-vget(xi, c) + vget(xj, c)) * 0.5f;
+    }
+    vstore<V>(a.out + e * a.ldo + f, o);
+  }
+}
+
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_edge_absdiff_fwd(Gather2Args a) {
+  edge_absdiff_body<false, V, LPR>(a);
+}
+
+template <int V, int LPR>
+__global__ __launch_bounds__(256) void k_edge_absdiff_bwd(Gather2Args a) {
+  edge_absdiff_body<true, V, LPR>(a);
+}
+
 // Segment mean: out[s] = (sum_{r in seg s} x[r]) / max(|seg|, 1)
 // (torch_scatter.scatter_mean semantics: sum divided by clamped count).
 struct SegArgs {
@@ -1119,6 +1162,26 @@ extern "C" int hlhgat_segment_mean_fwd(const int32_t* seg_ptr,
   const int l = pick_lpr(d, v);
   hipStream_t s = as_stream(stream);
   HLH_DISPATCH_VL(v, l, k_segment_mean_fwd, n_seg, s, a, nullptr);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_edge_absdiff(const int64_t* edge_index, int64_t n_edges, const float* x,
+                                   int64_t ldx, int64_t d, const float* g, int64_t ldg,
+                                   float* out, int64_t ldo, void* stream) {
+  HLH_CHECK_ARG(n_edges >= 0 && d > 0 && ldx >= d && ldo >= d && (!g || ldg >= d),
+                "edge_absdiff: bad sizes");
+  if (n_edges == 0) return HLHGAT_OK;
+  HLH_CHECK_ARG(edge_index && x && out, "edge_absdiff: NULL pointer");
+  Gather2Args a{edge_index, n_edges, x, ldx, (int)d, nullptr, nullptr, -1.f, 1.f, g,
+                g ? ldg : 0, out, ldo, 0};
+  const int v = pick_vec(d, {ldx, ldo, g ? ldg : 4}, {x, out, g});
+  const int l = pick_lpr(d, v);
+  hipStream_t s = as_stream(stream);
+  if (g)
+    HLH_DISPATCH_VL(v, l, k_edge_absdiff_bwd, n_edges, s, a, nullptr);
+  else
+    HLH_DISPATCH_VL(v, l, k_edge_absdiff_fwd, n_edges, s, a, nullptr);
   HLH_CHECK_LAUNCH();
   return HLHGAT_OK;
 }

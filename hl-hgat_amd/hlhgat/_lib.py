@@ -122,6 +122,8 @@ SIGNATURES = {
     "hlhgat_row_scale_fwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp]),
     "hlhgat_row_scale_bwd": (c_i32, [c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_i64,
                                      c_vp, c_vp]),
+    "hlhgat_edge_absdiff": (c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64,
+                                    c_vp]),
     "hlhgat_pool_mean_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
                                      c_i64, c_vp]),
     "hlhgat_bn_workspace_bytes": (c_i64, [c_i64, c_i64]),

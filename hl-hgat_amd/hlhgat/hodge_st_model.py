@@ -16,6 +16,7 @@ from . import ops
 from .hodge_cheb_conv import HodgeLaguerreConv, NodeEdgeInt, cluster_mean
 from .distributed import global_max
 from .hodge_dataset import adj2par1, degree
+from . import nn as _nn
 from .nn import Abs, BatchNorm, Sequential, run_mlp_stack
 
 __all__ = ["HL_HGCNN_zinc_dense_int3_pyr", "HL_HGCNN_pepfunc_dense_int3_pyr",
@@ -397,9 +398,14 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
         x_t, edge_index_t, edge_weight_t = data.x_t, data.edge_index_t, data.edge_weight_t
         width = self.initial_channel + sum(c * f for c, f in zip(self.channels, self.filters))
         dense = x_t.is_cuda and x_t.dim() == 2 and ops.DENSE_SLAB
+        # the readout's |B1^T x_t| / 2 in the edge slab's last columns, right
+        # after the last block's x_s: cat([x_s, x_t2s]) is a window of the slab
+        # (unless the Abs is observed: a tap or hooks see the unfused path)
+        fused_ro = dense and _nn.TAP is None and not (self.readout_abs._forward_hooks or
+                                                       self.readout_abs._forward_pre_hooks)
         if dense:
             dt = ops.DenseConcat(x_t.size(0), width, x_t)
-            ds = ops.DenseConcat(x_s.size(0), width, x_s)
+            ds = ops.DenseConcat(x_s.size(0), width + (self.filters[-1] if fused_ro else 0), x_s)
             _sink(self.HL_init_conv, dt, ds, self.initial_channel)
         x_t, x_s = self.HL_init_conv(x_t, edge_index_t, edge_weight_t, x_s, edge_index_s,
                                      edge_weight_s)
@@ -429,8 +435,12 @@ class HL_HGCNN_TSP_dense_int3_pyr(nn.Module):
                     x_t0 = torch.cat([x_t0, x_t], dim=-1)
                     x_s0 = torch.cat([x_s0, x_s], dim=-1)
         # readout (:846-851): x_t2s = |B1^T x_t| / 2 per edge
-        x_t2s = self.readout_abs(ops.boundary_t(x_t, par_1.incidence())) / 2
-        x_s = torch.cat([x_s, x_t2s], dim=-1)
+        if fused_ro:
+            c0, c1 = ds.cols[-1]
+            x_s = ops.tsp_readout(x_s, x_t, par_1.incidence(), ds.S[:, c0:c1 + x_t.size(1)])
+        else:
+            x_t2s = self.readout_abs(ops.boundary_t(x_t, par_1.incidence())) / 2
+            x_s = torch.cat([x_s, x_t2s], dim=-1)
         if len(self.mlp_channels) == 1:
             x_s = self.mlp(x_s, edge_index_s, edge_weight_s)
         return self.out(x_s, edge_index_s, edge_weight_s) * edge_mask, s_batch

@@ -1253,6 +1253,57 @@ class _BoundaryTFn(torch.autograd.Function):
         return dx, None
 
 
+class _TspReadoutFn(torch.autograd.Function):
+    """R = cat([x_s, |B1^T x_t| / 2], -1) where R is a column window of a
+    dense slab whose first columns already hold x_s (its last part): only the
+    x_t2s half is computed, in one pass; the backward hands x_s its half of
+    dR as a view and x_t B1 ((dR2 / 2) * sgn(B1^T x_t))."""
+
+    @staticmethod
+    def forward(ctx, x_s, x_t, inc, R):
+        cs, E, d = x_s.size(1), inc.n_edges, x_t.size(1)
+        ctx.inc, ctx.cs = inc, cs
+        ctx.save_for_backward(x_t)
+        check(LIB.hlhgat_edge_absdiff(inc.edge_index.data_ptr(), E, x_t.data_ptr(), _ld(x_t), d,
+                                      None, 0, R.data_ptr() + 4 * cs, _ld(R), _stream(x_t)),
+              "edge_absdiff")
+        return R
+
+    @staticmethod
+    def backward(ctx, g):
+        (x_t,) = ctx.saved_tensors
+        inc, cs = ctx.inc, ctx.cs
+        g = _rows2d(g, "grad")
+        E, d = inc.n_edges, x_t.size(1)
+        ge = torch.empty(E, d, device=g.device, dtype=g.dtype)
+        check(LIB.hlhgat_edge_absdiff(inc.edge_index.data_ptr(), E, x_t.data_ptr(), _ld(x_t), d,
+                                      g.data_ptr() + 4 * cs, _ld(g), ge.data_ptr(), d,
+                                      _stream(g)), "edge_absdiff backward")
+        A = SparseCSR(inc.rowptr, inc.edge_ids, _incidence_signs(inc), inc.n_nodes,
+                      inc.n_edges, 2 * inc.n_edges)
+        dx = torch.empty(inc.n_nodes, d, device=g.device, dtype=g.dtype)
+        if inc.n_nodes:
+            _poly_step(A, ge, dx)
+        return g[:, :cs], dx, None, None
+
+
+def tsp_readout(x_s: torch.Tensor, x_t: torch.Tensor, inc: Incidence,
+                R: torch.Tensor) -> torch.Tensor:
+    """The TSP head's readout input cat([x_s, |B1^T x_t| / 2], -1)
+    (lib/Hodge_ST_Model.py:846-849) into R, a [n_edges, C_s + C_t] window of
+    the edge slab whose first C_s columns hold x_s already: bitwise the
+    unfused boundary_t / abs / div / cat and their gradients."""
+    _req_dev(x_t, "x_t")
+    x_t = _rows2d(x_t, "x_t")
+    E = inc.n_edges
+    if x_t.size(0) != inc.n_nodes or x_s.size(0) != E:
+        raise RuntimeError(f"hlhgat: tsp_readout rows ({x_t.size(0)}, {x_s.size(0)}) vs |B1| "
+                           f"({inc.n_nodes}, {E})")
+    if tuple(R.shape) != (E, x_s.size(1) + x_t.size(1)) or R.stride(1) != 1:
+        raise RuntimeError(f"hlhgat: tsp_readout window {tuple(R.shape)} does not fit")
+    return _TspReadoutFn.apply(x_s, x_t, inc, R)
+
+
 def boundary_t(x_t: torch.Tensor, inc: Incidence) -> torch.Tensor:
     """torch.sparse.mm(par_1.transpose(0, 1), x_t) for par_1 = adj2par1(...)
     (lib/Hodge_ST_Model.py:846): per edge (i, j), x_t[j] - x_t[i], summed in

@@ -523,6 +523,16 @@ int hlhgat_edge_gather2(const int64_t* edge_index, int64_t n_edges,
                         int64_t ldz, float* out, int64_t ldo, int accumulate,
                         void* stream);
 
+/* The TSP edge readout x_t2s = |B1^T x_t| / 2 (lib/Hodge_ST_Model.py:846-848)
+ * with g == NULL: out[e] = |x[j] - x[i]| / 2 for edge e = (i, j)
+ * (edge_index [2][n_edges]); with g: its backward's edge factor
+ * out[e] = (g[e] / 2) * sgn(x[j] - x[i]) (then B1 out, hlhgat_poly_step on
+ * the signed incidence CSR, gives dx).  Bitwise the unfused
+ * sparse.mm / abs / div and their backwards. */
+int hlhgat_edge_absdiff(const int64_t* edge_index, int64_t n_edges, const float* x,
+                        int64_t ldx, int64_t d, const float* g, int64_t ldg, float* out,
+                        int64_t ldo, void* stream);
+
 /* ---- attention score (NodeEdgeInt only_att) ---------------------------- */
 /* a[r] = sigma((w_cross*<Qc[r],Kr[r]> + w_self*<Qs[r],Kr[r]>) / sqrt_dk)
  * with w_cross = (1-lambda), w_self = lambda (lib/Hodge_Cheb_Conv.py:299-304).

@@ -262,3 +262,33 @@ def test_row_scale_att_kq_pool_bwd_match_torch(cuda):
     (s3 * gr).sum().backward()
     assert int(flag[0]) == 1 and torch.equal(G[:, :d], x2.grad)
     assert torch.isnan(G[:, d:]).all()
+
+
+@pytest.mark.gpu
+def test_tsp_readout_bitwise_unfused(cuda):
+    """ops.tsp_readout (cat([x_s, |B1^T x_t| / 2]) in a slab window, one pass
+    each way) against boundary_t / abs / div / cat: bitwise values and
+    gradients (lib/Hodge_ST_Model.py:846-849)."""
+    from hlhgat import ops
+    from hlhgat.hodge_dataset import adj2par1
+    from hlhgat.synthetic import tsp_like_graph
+    from hlhgat.hodge_dataset import collate
+    b = collate([tsp_like_graph(1), tsp_like_graph(2)], check_hodge=False).to(cuda)
+    nt, ne = b.x_t.size(0), b.x_s.size(0)
+    inc = adj2par1(b.edge_index, nt, ne).incidence()
+    g = torch.Generator().manual_seed(4)
+    ct, cs = 64, 48
+    xt = torch.randn(nt, ct, generator=g).to(cuda)
+    xt[:5] = 0.0  # zero differences: sgn 0 in the backward
+    xs = torch.randn(ne, cs, generator=g).to(cuda)
+    S = torch.full((ne, 16 + cs + ct), float("nan"), device=cuda)
+    S[:, 16:16 + cs] = xs
+    x1, s1 = xt.clone().requires_grad_(True), xs.clone().requires_grad_(True)
+    R = ops.tsp_readout(s1, x1, inc, S[:, 16:])
+    x2, s2 = xt.clone().requires_grad_(True), xs.clone().requires_grad_(True)
+    R2 = torch.cat([s2, ops.boundary_t(x2, inc).abs() / 2], dim=-1)
+    assert R.data_ptr() == S.data_ptr() + 4 * 16 and torch.equal(R, R2)
+    W = torch.randn(ne, cs + ct, generator=g).to(cuda)
+    (R * W).sum().backward()
+    (R2 * W).sum().backward()
+    assert torch.equal(x1.grad, x2.grad) and torch.equal(s1.grad, s2.grad)

@@ -37,7 +37,8 @@ for s in "$@"; do
            grep -o '"ms_per_step": [0-9.]*' gpurun_out/${TAG}_ab5env_${v}_$r.log | head -1 | sed "s/^/${WL:-cfg5} $AB5ENV=$v run $r /" >> gpurun_out/${TAG}_ab5env.txt || true
          done; done; cat gpurun_out/${TAG}_ab5env.txt ;;
     glue) step glue3 300 python3 tools/probes/glue_ops.py --head cfg3_cifar_attpool &&
-          step glue4 300 python3 tools/probes/glue_ops.py --head cfg4_pepfunc_attpool ;;
+          step glue4 300 python3 tools/probes/glue_ops.py --head cfg4_pepfunc_attpool &&
+          step glue5 300 python3 tools/probes/glue_ops.py --head cfg5_tsp_pyr ;;
     abstep) step abstep 900 python3 tools/ab_step.py ${AB:-base1 base2} --rounds 5 ;;
     quick) step quick 300 python bench.py --no-cfg5 --no-heads --no-cpu-baseline --no-replay-census --no-loader --steps 30 ;;
     bn) step bn 600 $PT tests/test_gpu_parity.py -m gpu -v -s -k "bn_ or proj_bn or handover or hog" ;;
