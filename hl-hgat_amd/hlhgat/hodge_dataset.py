@@ -134,6 +134,10 @@ class Batch(PairData):
             tabs = tabs if all(torch.is_tensor(t) and t.is_cuda for t in tabs) else None
             ops.set_hodge_factor(eis, ei, self.x_t.size(0), getattr(self, "row_order_t", None),
                                  tables=tabs)
+            if tabs is not None:
+                # the factor's signed B1 values are the incidence CSR's signs
+                # (ops._incidence_signs) -- not rebuilt on the device per step
+                ei._hlhgat_inc_signs = tabs[1]
         for side in ("t", "s"):
             k = "edge_index_" + side
             t = getattr(self, k, None)

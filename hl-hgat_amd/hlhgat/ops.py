@@ -821,7 +821,11 @@ def incidence(edge_index: torch.Tensor, n_nodes: int) -> Incidence:
         if rowptr.numel() != n_nodes + 1 or eids.numel() != 2 * E:
             raise RuntimeError(f"hlhgat: attached incidence CSR has {rowptr.numel() - 1} rows / "
                                f"{eids.numel()} entries, expected {n_nodes} / {2 * E}")
-        return _INC_CACHE.put([edge_index], n_nodes, Incidence(rowptr, eids, ei, n_nodes, E))
+        inc = Incidence(rowptr, eids, ei, n_nodes, E)
+        signs = getattr(edge_index, "_hlhgat_inc_signs", None)  # collate-time (factor tables)
+        if torch.is_tensor(signs) and signs.numel() == 2 * E and signs.device == dev:
+            inc._signs = signs  # type: ignore[attr-defined]
+        return _INC_CACHE.put([edge_index], n_nodes, inc)
     rowptr = torch.empty(n_nodes + 1, dtype=torch.int32, device=dev)
     eids = torch.empty(max(2 * E, 1), dtype=torch.int32, device=dev)[:2 * E]
     ws_bytes = int(LIB.hlhgat_csr_workspace_bytes(2 * E))
