@@ -608,6 +608,7 @@ def _head_batch(kind, graphs, seed):
 
 
 def _head_loss(kind, out, datas):
+    import hlhgat
     F = torch.nn.functional
     if kind == "tsp":  # main_TSP...:316-321 (BCE on the masked edge logits), mean over
         # the batch's real edges (padding edges carry a zero mask and label)
@@ -616,7 +617,8 @@ def _head_loss(kind, out, datas):
     y = datas[0].y
     if kind == "cifar":  # main_cifar10SP: cross entropy
         return F.cross_entropy(out, y.view(-1).long())
-    return F.binary_cross_entropy_with_logits(out, y.view(out.shape).float())  # pepfunc
+    # pepfunc; hlhgat.nn.BCEWithLogitsLoss: torch's module, one HIP launch each way
+    return hlhgat.nn.BCEWithLogitsLoss()(out, y.view(out.shape).float())
 
 
 HEAD_PROF = (("k_poly_step (all call sites)", POLY_CLASSES, "hbm"),

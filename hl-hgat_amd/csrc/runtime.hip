@@ -430,6 +430,72 @@ __global__ __launch_bounds__(256) void k_l1_loss_bwd(const float* __restrict__ x
 }
 }  // namespace
 
+// --- BCE with logits (torch.nn.BCEWithLogitsLoss, no weights) ---------------
+// The multi-label loss of the peptides-func loop and the TSP edge loss
+// (main_pepfunc...:181-183, main_TSP...:316-321): ATen composes it of
+// log_sigmoid / rsub / mul / sub / mean and ~8 backward launches.  One each:
+//   forward  loss = (sum_i (1 - t_i) x_i - log_sigmoid(x_i)) / div
+//            (div = n for "mean", 1 for "sum"; one workgroup, fixed order);
+//   backward dx = gm (1 - t) + (-gm) (m - s z / (1 + z)), gm = g / div,
+//            z = exp(-|x|), (m, s) = (1, 1) for x < 0 else (0, -1): the
+//            arithmetic of MulBackward + LogSigmoidBackward summed.
+__global__ __launch_bounds__(256) void k_bce_logits_fwd(const float* __restrict__ x,
+                                                        const float* __restrict__ y, int64_t n,
+                                                        float div, float* __restrict__ loss) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const float v = x[i];
+    const float ls = fminf(v, 0.f) - log1pf(expf(-fabsf(v)));  // log_sigmoid
+    s += (1.f - y[i]) * v - ls;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = red[0] / div;
+}
+
+__global__ __launch_bounds__(256) void k_bce_logits_bwd(const float* __restrict__ x,
+                                                        const float* __restrict__ y, int64_t n,
+                                                        float div,
+                                                        const float* __restrict__ gout,
+                                                        float* __restrict__ dx) {
+  const float gm = gout[0] / div;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const float v = x[i];
+    const bool neg = v < 0.f;
+    const float m = neg ? 1.f : 0.f, sg = neg ? 1.f : -1.f;
+    const float z = expf(-fabsf(v));
+    dx[i] = gm * (1.f - y[i]) + (-gm) * (m - sg * (z / (1.f + z)));
+  }
+}
+
+extern "C" int hlhgat_bce_logits_fwd(const float* x, const float* y, int64_t n, float div,
+                                     float* loss, void* stream) {
+  HLH_CHECK_ARG(n > 0 && x && y && loss && div > 0.f,
+                "bce_logits_fwd: NULL pointer, n <= 0 or div <= 0");
+  launch(k_bce_logits_fwd, dim3(1), dim3(256), 0, as_stream(stream), nullptr, x, y, n, div,
+         loss);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
+extern "C" int hlhgat_bce_logits_bwd(const float* x, const float* y, int64_t n, float div,
+                                     const float* gout, float* dx, void* stream) {
+  HLH_CHECK_ARG(n > 0 && x && y && gout && dx && div > 0.f,
+                "bce_logits_bwd: NULL pointer, n <= 0 or div <= 0");
+  int64_t g = ceil_div(n, 256);
+  if (g > 1024) g = 1024;
+  launch(k_bce_logits_bwd, dim3((unsigned)g), dim3(256), 0, as_stream(stream), nullptr, x, y,
+         n, div, gout, dx);
+  HLH_CHECK_LAUNCH();
+  return HLHGAT_OK;
+}
+
 extern "C" int hlhgat_l1_loss_fwd(const float* x, const float* y, int64_t n, float* loss,
                                   void* stream) {
   HLH_CHECK_ARG(n > 0 && x && y && loss, "l1_loss_fwd: NULL pointer or n <= 0");

@@ -140,6 +140,8 @@ SIGNATURES = {
                                           c_f64, c_f64, c_f64, c_vp]),
     "hlhgat_adam_flat": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_f64, c_f64, c_f64,
                                  c_f64, c_f64, c_vp]),
+    "hlhgat_bce_logits_fwd": (c_i32, [c_vp, c_vp, c_i64, c_f32, c_vp, c_vp]),
+    "hlhgat_bce_logits_bwd": (c_i32, [c_vp, c_vp, c_i64, c_f32, c_vp, c_vp, c_vp]),
     "hlhgat_l1_loss_fwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlhgat_l1_loss_bwd": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "hlhgat_bn_sums_len": (c_i64, [c_i64]),

@@ -16,7 +16,8 @@ from typing import Callable, List, Sequence, Tuple, Union
 import torch
 import torch.nn as tnn
 
-__all__ = ["Sequential", "BatchNorm", "Linear", "L1Loss", "glorot", "global_mean_pool"]
+__all__ = ["Sequential", "BatchNorm", "Linear", "L1Loss", "BCEWithLogitsLoss", "glorot",
+           "global_mean_pool"]
 
 
 def glorot(t: torch.Tensor) -> None:
@@ -121,6 +122,28 @@ class L1Loss(tnn.L1Loss):
                 and input.numel() > 0):
             from . import ops
             return ops.l1_loss(input, target)
+        return super().forward(input, target)
+
+
+class BCEWithLogitsLoss(tnn.BCEWithLogitsLoss):
+    """torch.nn.BCEWithLogitsLoss (the peptides-func and TSP training losses)
+    whose unweighted "mean" / "sum" reductions on ROCm fp32 tensors run as one
+    HIP launch each way (ops.bce_with_logits; the input gradient in ATen's
+    arithmetic) up to FUSED_MAX elements: the forward's fixed-order sum is one
+    workgroup, which for a per-edge loss (config 5: 207k logits) waits on
+    ~800 dependent loads per lane and loses to ATen's grid reduction
+    (measured +0.3 ms per config-5 step).  Weights, pos_weight, CPU tensors,
+    "none" and larger inputs go to torch."""
+
+    FUSED_MAX = 16384
+
+    def forward(self, input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        if (self.weight is None and self.pos_weight is None
+                and self.reduction in ("mean", "sum") and input.is_cuda
+                and input.dtype == torch.float32 and input.shape == target.shape
+                and not target.requires_grad and 0 < input.numel() <= self.FUSED_MAX):
+            from . import ops
+            return ops.bce_with_logits(input, target, self.reduction)
         return super().forward(input, target)
 
 

@@ -1894,6 +1894,47 @@ def l1_loss(input: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     return _L1LossFn.apply(x, target.to(torch.float32).contiguous())
 
 
+class _BCELogitsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, div):
+        loss = torch.empty((), device=x.device, dtype=torch.float32)
+        check(LIB.hlhgat_bce_logits_fwd(x.data_ptr(), y.data_ptr(), x.numel(), div,
+                                        loss.data_ptr(), _stream(x)), "bce_logits_fwd")
+        ctx.div = div
+        ctx.save_for_backward(x, y)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        g = g.contiguous()
+        dx = torch.empty_like(x)
+        check(LIB.hlhgat_bce_logits_bwd(x.data_ptr(), y.data_ptr(), x.numel(), ctx.div,
+                                        g.data_ptr(), dx.data_ptr(), _stream(x)),
+              "bce_logits_bwd")
+        return dx, None, None
+
+
+def bce_with_logits(input: torch.Tensor, target: torch.Tensor,
+                    reduction: str = "mean") -> torch.Tensor:
+    """F.binary_cross_entropy_with_logits(input, target, reduction=...) for
+    "mean" / "sum" without weights, one launch each way
+    (hlhgat_bce_logits_fwd / _bwd); the loss value is the fp32 sum in a fixed
+    order.  No gradient flows into target (the labels)."""
+    _req_dev(input, "input")
+    if input.shape != target.shape:
+        raise RuntimeError(f"hlhgat: bce_with_logits shapes differ: {tuple(input.shape)} vs "
+                           f"{tuple(target.shape)}")
+    if target.requires_grad:
+        raise RuntimeError("hlhgat: bce_with_logits: target must not require grad")
+    if input.numel() == 0:
+        raise RuntimeError("hlhgat: bce_with_logits of an empty tensor")
+    if reduction not in ("mean", "sum"):
+        raise ValueError(f"hlhgat: bce_with_logits reduction {reduction!r}")
+    div = float(input.numel()) if reduction == "mean" else 1.0
+    return _BCELogitsFn.apply(input.contiguous(), target.to(torch.float32).contiguous(), div)
+
+
 # ----------------------------------------------------------------------------
 # device error word (include/hlhgat.h: hlhgat_device_errors)
 # ----------------------------------------------------------------------------

@@ -812,6 +812,17 @@ int hlhgat_l1_loss_fwd(const float* x, const float* y, int64_t n, float* loss, v
 int hlhgat_l1_loss_bwd(const float* x, const float* y, int64_t n, const float* gout, float* dx,
                        void* stream);
 
+/* BCE with logits, torch.nn.BCEWithLogitsLoss (no weight / pos_weight) of the
+ * peptides-func and TSP loops (main_pepfunc...:181-183, main_TSP...:316-321):
+ * loss = sum_i ((1 - y_i) x_i - log_sigmoid(x_i)) / div (div = n: "mean",
+ * 1: "sum"), one workgroup, fixed summation order; backward
+ * dx = (g / div) (sigmoid(x) - y) in ATen's MulBackward + LogSigmoidBackward
+ * arithmetic.  One launch each way. */
+int hlhgat_bce_logits_fwd(const float* x, const float* y, int64_t n, float div, float* loss,
+                          void* stream);
+int hlhgat_bce_logits_bwd(const float* x, const float* y, int64_t n, float div,
+                          const float* gout, float* dx, void* stream);
+
 /* ---- workspaces --------------------------------------------------------- */
 /* Zero `bytes` (a multiple of 4) at p with a kernel on `stream` (graph-capture
  * safe; used to initialise the BatchNorm workspace counters). */

@@ -292,3 +292,28 @@ def test_tsp_readout_bitwise_unfused(cuda):
     (R * W).sum().backward()
     (R2 * W).sum().backward()
     assert torch.equal(x1.grad, x2.grad) and torch.equal(s1.grad, s2.grad)
+
+
+@pytest.mark.gpu
+def test_bce_with_logits_matches_torch(cuda):
+    """hlhgat.nn.BCEWithLogitsLoss (one HIP launch each way) against torch's:
+    loss to fp32 summation order, input gradient to 1 ulp-scale tolerance;
+    weighted, CPU and large inputs go to torch."""
+    import hlhgat
+    g = torch.Generator().manual_seed(8)
+    for shape, red in (((64, 10), "mean"), ((16001,), "sum"), ((3, 5), "mean")):
+        x = (torch.randn(shape, generator=g) * 6).to(cuda)
+        x.view(-1)[:3] = torch.tensor([0.0, -0.0, 30.0])
+        t = (torch.rand(shape, generator=g) > 0.5).float().to(cuda)
+        x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        l1 = hlhgat.nn.BCEWithLogitsLoss(reduction=red)(x1, t)
+        l2 = torch.nn.BCEWithLogitsLoss(reduction=red)(x2, t)
+        close(l1.detach().cpu(), l2.detach().cpu(), 1e-5, f"bce {red} loss")
+        (l1 * 1.7).backward()
+        (l2 * 1.7).backward()
+        close(x1.grad.cpu(), x2.grad.cpu(), 1e-6, f"bce {red} grad")
+    w = torch.rand(4, 3).to(cuda)
+    x = torch.randn(4, 3).to(cuda)
+    t = torch.ones(4, 3).to(cuda)
+    assert torch.equal(hlhgat.nn.BCEWithLogitsLoss(weight=w)(x, t),
+                       torch.nn.BCEWithLogitsLoss(weight=w)(x, t))
