@@ -258,13 +258,18 @@ class NodeEdgeInt(nn.Module):
             dk = self.dk
             sq = float(np.sqrt(dk))
             # node side: K = WK_Node(x_t), Q_self = WQ_Node(x_t) in one GEMM
-            w_t = torch.cat([self.WK_Node.weight, self.WQ_Node.weight], 0)
-            b_t = torch.cat([self.WK_Node.bias, self.WQ_Node.bias], 0)
+            # (the K|Q packs of the whole forward: ops.att_prepack, one launch)
+            pk = ops.take_att_pack(self) if x_t.is_cuda else None
+            if pk is not None:
+                w_t, b_t, w_s, b_s = pk
+            else:
+                w_t = torch.cat([self.WK_Node.weight, self.WQ_Node.weight], 0)
+                b_t = torch.cat([self.WK_Node.bias, self.WQ_Node.bias], 0)
+                w_s = torch.cat([self.WK_Edge.weight, self.WQ_Edge.weight], 0)
+                b_s = torch.cat([self.WK_Edge.bias, self.WQ_Edge.bias], 0)
             kq_t = ops.linear_blocks([x_t], w_t, b_t)
             qc_t = ops.linear_blocks([x_s2t], self.WQ_Edge.weight, self.WQ_Edge.bias)
             a_t = ops.att_score_kq(qc_t, kq_t, 1 - self.lambda_Node, self.lambda_Node, sq, code)
-            w_s = torch.cat([self.WK_Edge.weight, self.WQ_Edge.weight], 0)
-            b_s = torch.cat([self.WK_Edge.bias, self.WQ_Edge.bias], 0)
             kq_s = ops.linear_blocks([x_s], w_s, b_s)
             qc_s = ops.linear_blocks([x_t2s], self.WQ_Node.weight, self.WQ_Node.bias)
             a_s = ops.att_score_kq(qc_s, kq_s, 1 - self.lambda_Edge, self.lambda_Edge, sq, code)

@@ -613,6 +613,15 @@ class _AttPoolHead(nn.Module):
         dense = x_t.is_cuda and ops.DENSE_SLAB
         nxt = None  # the next run's slabs, already holding the pooled x0
         last = len(self.channels) - 1
+        if x_t.is_cuda:
+            # every NodeEdgeInt's first-Linear pack and the K|Q packs of the
+            # NEAtts this forward uses: one launch each
+            ops.nei_prepack([getattr(self, "NEInt{}{}".format(i, j))
+                             for i, _ in enumerate(self.channels)
+                             for j in range(self.channels[i])])
+            ops.att_prepack([getattr(self, "NEAtt%d" % i) for i in range(len(self.channels))
+                             if hasattr(self, "NEAtt%d" % i)
+                             and (self.att_mode == "every" or i == self.pool_loc)])
         for i, _ in enumerate(self.channels):
             # one dense slab per run of levels: x0 (scaled / pooled) then the
             # blocks of every level up to the next scale or pool of x0 (levels

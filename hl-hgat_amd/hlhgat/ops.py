@@ -1160,8 +1160,88 @@ def nei_prepack(neints) -> None:
 
 
 _PACK_EPOCH = 0  # a pack is only used by the forward that built it
-# PREPACK = False (tests): each NodeEdgeInt packs its own weights (same results)
-PREPACK = True
+# PREPACK = False (tests; HLHGAT_PREPACK=0 for A/B): each NodeEdgeInt packs its
+# own weights, each only_att NodeEdgeInt concatenates its K|Q (same results)
+PREPACK = os.environ.get("HLHGAT_PREPACK", "1") != "0"
+
+
+class _AttPackFn(torch.autograd.Function):
+    """The only_att NodeEdgeInts' concatenated projections
+    (cat[WK_Node; WQ_Node] and cat[WK_Edge; WQ_Edge], weights and biases) of
+    a whole forward in ONE batched copy instead of four torch.cat launches
+    per module; the backward hands each parameter its rows of the packed
+    gradients (views, as torch.cat's backward does)."""
+
+    @staticmethod
+    def forward(ctx, n_mod, *params):
+        outs, srcs, dsts = [], [], []
+        for i in range(n_mod):
+            wkn, wqn, bkn, bqn, wke, wqe, bke, bqe = params[8 * i:8 * i + 8]
+            for a, b in ((wkn, wqn), (bkn, bqn), (wke, wqe), (bke, bqe)):
+                o = torch.empty((a.size(0) + b.size(0),) + tuple(a.shape[1:]), device=a.device,
+                                dtype=a.dtype)
+                srcs += [a.detach(), b.detach()]
+                dsts += [o[:a.size(0)], o[a.size(0):]]
+                outs.append(o)
+        copy_words_batched(srcs, dsts)
+        ctx.n_mod = n_mod
+        ctx.rows = [p.size(0) for p in params]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        out = [None]
+        for i in range(ctx.n_mod):
+            r = ctx.rows[8 * i:8 * i + 8]
+            for q, g in enumerate(grads[4 * i:4 * i + 4]):
+                k = r[2 * q]  # rows of the pair's first parameter
+                if g is None:
+                    out += [None, None]
+                else:
+                    out += [g[:k], g[k:]]
+        # params order: wkn, wqn, bkn, bqn, wke, wqe, bke, bqe per module
+        return tuple(out)
+
+
+def att_prepack(neatts) -> None:
+    """Pack the K|Q projections of every only_att NodeEdgeInt in `neatts`
+    in one launch at the start of the forward (NodeEdgeInt._unfused takes
+    its pack once, take_pack's epoch rule)."""
+    mods = [m for m in (neatts if PREPACK else [])
+            if m.only_att and m.WK_Node.weight.is_cuda and m.WK_Node.bias is not None]
+    if not mods:
+        return
+    params = []
+    for m in mods:
+        params += [m.WK_Node.weight, m.WQ_Node.weight, m.WK_Node.bias, m.WQ_Node.bias,
+                   m.WK_Edge.weight, m.WQ_Edge.weight, m.WK_Edge.bias, m.WQ_Edge.bias]
+    global _ATT_EPOCH
+    _ATT_EPOCH += 1
+    outs = _AttPackFn.apply(len(mods), *params)
+    for i, m in enumerate(mods):
+        m._hlhgat_att_packed = (outs[4 * i:4 * i + 4], _att_versions(m), _ATT_EPOCH)
+
+
+_ATT_EPOCH = 0  # the latest att_prepack (a pack is only used until the next one)
+
+
+def _att_versions(m):
+    return tuple(t._version for t in (m.WK_Node.weight, m.WQ_Node.weight, m.WK_Node.bias,
+                                      m.WQ_Node.bias, m.WK_Edge.weight, m.WQ_Edge.weight,
+                                      m.WK_Edge.bias, m.WQ_Edge.bias))
+
+
+def take_att_pack(m):
+    """The module's (w_t, b_t, w_s, b_s) from the latest att_prepack,
+    consumed; None when there is none, a later att_prepack ran, or a
+    parameter's version counter moved since (an in-place update)."""
+    p, m._hlhgat_att_packed = getattr(m, "_hlhgat_att_packed", None), None
+    if p is None or p[2] != _ATT_EPOCH or p[1] != _att_versions(m):
+        return None
+    if (torch.is_grad_enabled() and m.WK_Node.weight.requires_grad
+            and not p[0][0].requires_grad):
+        return None  # packed under no_grad, used with gradients
+    return p[0]
 
 
 def take_pack(m) -> Optional[torch.Tensor]:

@@ -291,6 +291,49 @@ def test_deferred_reductions_heads_bitwise(cuda, kind):
         assert torch.equal(res[0][1][k], res[1][1][k]), k
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["peptides", "cifar"])
+@pytest.mark.parametrize("graphs", [False, True])
+def test_prepacked_attpool_weights_bitwise(cuda, kind, graphs):
+    """The attention-pooling heads with their NodeEdgeInt packs and NEAtt K|Q
+    packs built in one launch each per forward (ops.nei_prepack,
+    ops.att_prepack) equal the per-module packs / torch.cat: losses and every
+    parameter after eager or graph-replayed steps, bit for bit."""
+    import hlhgat
+    from hlhgat import ops, train
+    from hlhgat.synthetic import two_level_batch
+    F = torch.nn.functional
+    raw = [two_level_batch(kind, 6, seed=s) for s in (0, 1)]
+    batches = [[x.to(cuda) for x in b] for b in raw]
+    kw = dict(channels=[1, 1, 1], filters=[16, 32, 32], mlp_channels=[32], pool_loc=1, K=3)
+    if kind == "cifar":
+        cls = "HL_HGCNN_CIFAR10SP_dense_int3_attpool"
+        kw.update(keig=10, l=0.5)
+
+        def loss_fn(o, d):
+            return F.cross_entropy(o, d[0].y.view(-1).long())
+    else:
+        cls = "HL_HGCNN_pepfunc_dense_int3_attpool"
+
+        def loss_fn(o, d):
+            return F.binary_cross_entropy_with_logits(o, d[0].y.view(o.shape).float())
+    res = []
+    prev = ops.PREPACK
+    for pre in (False, True):
+        ops.PREPACK = pre
+        try:
+            torch.manual_seed(0)
+            m = getattr(hlhgat, cls)(**kw).to(cuda).train()
+            st = train.TrainStep(m, loss_fn, lr=1e-3, graphs=graphs)
+            losses = [float(st(batches[i % 2])) for i in range(4)]
+            res.append((losses, {k: v.detach().clone() for k, v in m.state_dict().items()}))
+        finally:
+            ops.PREPACK = prev
+    assert res[0][0] == res[1][0], (res[0][0], res[1][0])
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
 class _Twice(torch.nn.Module):
     """One HIP Linear applied twice: its weight gets two gradients per step."""
 
